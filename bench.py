@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""Headline benchmark: p50 Allocate->ContainerReady latency at N advertised MI355X GPUs.
+
+Metric and config come from BASELINE.json ("p50 Allocate→ContainerReady latency;
+GPUs advertised at 1/2/4/8 MI355X"). One timed step is one pod admission:
+
+  1. (rank 0) the fake kubelet runs kubelet's devicemanager sequence against
+     the real device plugin over UDS gRPC: GetPreferredAllocation for a pod
+     requesting amd.com/gpu=N out of the N advertised devices, then Allocate;
+  2. the DeviceSpecs in the Allocate response are turned into a "container":
+     one fresh process per allocated GPU (one rank per GPU, like the pod's own
+     torchrun would start) restricted to its render node via
+     ROCR_VISIBLE_DEVICES;
+  3. each container initialises HIP and runs the gfx950 MFMA liveness kernel
+     on its GPU; it is "ready" when the tile verifies bit-exactly;
+  4. latency = (last container ready) - (kubelet starts GetPreferredAllocation),
+     both on CLOCK_MONOTONIC.
+
+The plugin is the real one (real /sys discovery, real C++ allocator, real
+gRPC servicer); only kubelet and the CRI runtime are stand-ins (see
+rocm_k8s_device_plugin_amd/testing/fake_kubelet.py, container_runtime.py).
+
+  python bench.py --gpus N --steps K --warmup W
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "p50 Allocate→ContainerReady latency; GPUs advertised at 1/2/4/8 MI355X"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sysfs-root", default="/sys")
+    ap.add_argument("--dev-root", default="/dev")
+    ap.add_argument("--fixture", action="store_true",
+                    help="CPU-only: synthetic 8x MI355X sysfs, containers are no-op processes")
+    ap.add_argument("--container-timeout", type=float, default=120.0)
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args()
+
+
+def pct(xs, q):
+    s = sorted(xs)
+    if not s:
+        return float("nan")
+    return s[min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))]
+
+
+class Dist:
+    """torch.distributed when launched by torchrun, else a 1-rank stub."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        self.cuda = False
+        self.gloo = None
+        try:
+            import torch
+            self.torch = torch
+            self.cuda = torch.cuda.is_available()
+        except Exception:
+            self.torch = None
+        if self.world > 1:
+            import torch.distributed as dist
+            self.dist = dist
+            if self.cuda:
+                self.torch.cuda.set_device(self.local_rank)
+                dist.init_process_group("nccl", device_id=self.torch.device("cuda", self.local_rank))
+                self.gloo = dist.new_group(backend="gloo")
+            else:
+                dist.init_process_group("gloo")
+                self.gloo = None
+
+    def sync(self):
+        if self.world > 1:
+            self.dist.barrier()
+        if self.cuda:
+            self.torch.cuda.synchronize()
+
+    def bcast(self, obj):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0, group=self.gloo)
+        return box[0]
+
+    def gather(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.gloo)
+        return out
+
+    def max(self, x: float) -> float:
+        return max(self.gather(x))
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    d = Dist()
+    n = args.gpus
+    if d.world > 1 and d.world != n:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE {d.world}: launch one rank per GPU")
+
+    from rocm_k8s_device_plugin_amd import _build
+    if d.rank == 0:
+        _build.ensure_built(hip=not args.fixture)
+    d.sync()
+
+    from rocm_k8s_device_plugin_amd.container_runtime import render_minors_from_specs, start_container
+
+    step_payload = None
+    loop = None
+    kubelet = mgr = mgr_task = impl = None
+    minor_to_ord = {}
+    tmp = None
+    if d.rank == 0:
+        from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+        from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+        from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
+        from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+        from rocm_k8s_device_plugin_amd.topology import Inventory, discover, hip_ordinals
+        from rocm_k8s_device_plugin_amd.utils import log as ulog
+        ulog.setup(0)
+        import logging
+        logging.getLogger("mi355x").setLevel(logging.WARNING)
+
+        tmp = tempfile.mkdtemp(prefix="mi355x-bench-")
+        sysfs, devroot = args.sysfs_root, args.dev_root
+        if args.fixture:
+            from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+            fi = make_mi355x_node(os.path.join(tmp, "node"))
+            sysfs, devroot = str(fi.sysfs), str(fi.dev)
+        full = discover(sysfs)
+        ords = hip_ordinals(full, devroot, check_access=not args.fixture)
+        usable = sorted((dv for dv in full.devices if dv.id in ords), key=lambda dv: ords[dv.id])
+        if len(usable) < n:
+            raise SystemExit(f"only {len(usable)} accessible GPU devices on this node, need {n}")
+        adv = tuple(usable[:n])     # "GPUs advertised at N"
+        inv = Inventory(sysfs_root=sysfs, devices=adv, topology=full.topology, driver_loaded=full.driver_loaded,
+                        kfd_present=full.kfd_present)
+        minor_to_ord = {dv.render_minor: ords[dv.id] for dv in adv}
+        impl = ContainerImpl("single", sysfs, HealthConfig(exporter_socket=None), inventory=inv)
+        pdir = os.path.join(tmp, "device-plugins")
+        loop = asyncio.new_event_loop()
+        kubelet = FakeKubelet(pdir)
+        loop.run_until_complete(kubelet.start())
+        mgr = PluginManager(impl, ManagerConfig(pulse_s=0, plugin_dir=pdir, handle_signals=False))
+        mgr_task = loop.create_task(mgr.run())
+        loop.run_until_complete(kubelet.wait_for_resource("amd.com/gpu", n, timeout=30))
+        gpu_info = {"ids": [dv.id for dv in adv], "gfx_target_version": sorted({dv.gfx_target_version for dv in adv}),
+                    "hive_ids": sorted({str(dv.hive_id) for dv in adv}),
+                    "partition": sorted({dv.partition_type for dv in adv})}
+    else:
+        gpu_info = None
+
+    rpc_ms, alloc_rpc_ms, lat_ms, ready_ms, kern_us = [], [], [], [], []
+
+    def one_step(record: bool):
+        nonlocal step_payload
+        if d.rank == 0:
+            t0 = time.monotonic_ns()
+            adm = loop.run_until_complete(kubelet.admit("amd.com/gpu", n))
+            minors = render_minors_from_specs(adm.response.container_responses[0])
+            ordl = [minor_to_ord[m] for m in minors]
+            payload = (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids))
+        else:
+            payload = None
+        payload = d.bcast(payload)
+        t0, ordl, tot, amsl, ids = payload
+        if args.fixture:
+            import subprocess
+            ts = time.monotonic_ns()
+            subprocess.run(["/bin/true"])
+            mine = (True, time.monotonic_ns(), 0.0, "")
+        else:
+            mine_ord = [ordl[d.rank]] if d.world > 1 else ordl
+            r = start_container(mine_ord, timeout_s=args.container_timeout)
+            kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
+            mine = (r.ok, r.t_ready_ns, kus, r.error)
+        allr = d.gather(mine)
+        bad = [e for ok, _, _, e in allr if not ok]
+        if bad:
+            raise SystemExit(f"container failed to become ready: {bad[0]}")
+        t_ready = max(t for _, t, _, _ in allr)
+        if d.rank == 0:
+            kubelet.release("amd.com/gpu", ids)
+        if record:
+            lat_ms.append((t_ready - t0) / 1e6)
+            rpc_ms.append(tot)
+            alloc_rpc_ms.append(amsl)
+            ready_ms.append((t_ready - t0) / 1e6 - tot)
+            kern_us.append(max(k for _, _, k, _ in allr))
+
+    for _ in range(args.warmup):
+        one_step(False)
+    d.sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        one_step(True)
+    d.sync()
+    elapsed = time.perf_counter() - t_start
+    elapsed = d.max(elapsed)
+
+    extra = {}
+    if d.rank == 0:
+        # allocator microbenchmark on the same request (ours vs the reference's ordered BFS)
+        pol = mgr.plugins["gpu"].ctx.allocator
+        avail = [dv.id for dv in impl.devices("gpu")]
+        t = time.perf_counter()
+        for _ in range(200):
+            pol.allocate(avail, [], n)
+        ours = (time.perf_counter() - t) / 200 * 1e6
+        t = time.perf_counter()
+        for _ in range(20):
+            ref = pol.reference_allocate(avail, [], n)
+        refu = (time.perf_counter() - t) / 20 * 1e6
+        extra = {"plugin_rpc_p50_ms": round(pct(rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rpc_ms, .99), 4),
+                 "allocate_rpc_p50_ms": round(pct(alloc_rpc_ms, .5), 4),
+                 "container_start_to_ready_p50_ms": round(pct(ready_ms, .5), 3),
+                 "latency_p99_ms": round(pct(lat_ms, .99), 3), "latency_mean_ms": round(statistics.mean(lat_ms), 3),
+                 "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
+                 "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
+                 "reference_algorithm_candidates": ref["candidates"], "gpus": gpu_info}
+        loop.run_until_complete(kubelet.stop())
+        mgr.request_stop()
+        loop.run_until_complete(mgr_task)
+        loop.close()
+        out = {
+            "metric": METRIC,
+            "value": round(pct(lat_ms, .5), 3),
+            "unit": "ms",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 3),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": ("synthetic pod specs requesting amd.com/gpu=N; real /sys discovery, fake kubelet over UDS, "
+                     "container = fresh process restricted to its render node running the MFMA liveness kernel"
+                     if not args.fixture else "synthetic 8xMI355X sysfs fixture; no-op containers (CPU only)"),
+            "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
+                       "global_batch": n, "seq_len": None,
+                       "parallelism": f"{n} GPUs advertised, 1 pod requesting {n}, 1 container process per GPU"},
+            "extra": extra,
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,72 @@
+// pybind11 bindings for the in-process liveness probe (_hip). Compiled with
+// hipcc and linked against the gfx950 kernel object; importing it loads the
+// HIP runtime, so the control plane never imports it — only GPU tests and
+// smoke() do. The plugin itself runs the probe executable in a child process.
+#include <pybind11/pybind11.h>
+
+#include "mi355x/liveness_probe.h"
+
+namespace py = pybind11;
+
+namespace {
+
+py::dict to_dict(const mi355x_probe_result& r) {
+  py::dict d;
+  d["ordinal"] = r.ordinal;
+  d["ok"] = static_cast<bool>(r.ok);
+  d["hip_error"] = r.hip_error;
+  d["mismatches"] = r.mismatches;
+  d["nonce"] = r.nonce;
+  d["xcc_id"] = r.xcc_id;
+  d["hw_id"] = r.hw_id;
+  d["iters"] = r.iters;
+  d["kernel_us"] = r.kernel_us;
+  d["total_us"] = r.total_us;
+  d["pci_bus_id"] = std::string(r.pci_bus_id);
+  d["arch"] = std::string(r.arch);
+  d["name"] = std::string(r.name);
+  d["uuid"] = std::string(r.uuid);
+  d["pci_domain"] = r.pci_domain;
+  d["pci_bus"] = r.pci_bus;
+  d["pci_device"] = r.pci_device;
+  d["cu_count"] = r.cu_count;
+  d["total_mem"] = r.total_mem;
+  d["error"] = std::string(r.error);
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "gfx950 MFMA liveness probe (in-process)";
+  m.def("device_count", [] {
+    int n;
+    {
+      py::gil_scoped_release nogil;
+      n = mi355x_probe_device_count();
+    }
+    return n;
+  });
+  m.def(
+      "probe",
+      [](int ordinal, uint32_t nonce, int iters) {
+        mi355x_probe_result r;
+        {
+          py::gil_scoped_release nogil;
+          mi355x_probe_device(ordinal, nonce, iters, &r);
+        }
+        return to_dict(r);
+      },
+      py::arg("ordinal") = 0, py::arg("nonce") = 12345u, py::arg("iters") = 4);
+  m.def(
+      "identify",
+      [](int ordinal) {
+        mi355x_probe_result r;
+        {
+          py::gil_scoped_release nogil;
+          mi355x_probe_identify(ordinal, &r);
+        }
+        return to_dict(r);
+      },
+      py::arg("ordinal") = 0);
+}

@@ -1,0 +1,407 @@
+#include <algorithm>
+#include <deque>
+#include <limits>
+#include <unordered_set>
+
+#include "mi355x/allocator.h"
+#include "mi355x/constants.h"
+
+namespace mi355x {
+
+namespace {
+
+// Error strings are part of the drop-in surface: kubelet logs them verbatim
+// (reference besteffort_policy.go:36-43).
+constexpr const char* kInvalidSize = "allocation size can not be negative";
+constexpr const char* kInvalidAvailable = "available devices count less than allocation size";
+constexpr const char* kInvalidRequired = "must_include devices size is more than allocation size";
+constexpr const char* kInvalidReqAvailable =
+    "must_include length should be less than or equal to avilable device size";
+constexpr const char* kInvalidInit = "Init method must be called before Allocate";
+constexpr const char* kNoCandidate = "No candidate subset found with matching criteria";
+
+int link_rank(int type) {
+  // lower is better: xGMI, then PCIe, then anything else
+  if (type == kLinkXgmi) return 0;
+  if (type == kLinkPcie) return 1;
+  return 2;
+}
+
+bool is_xcp_id(const std::string& id) { return id.find("amdgpu_xcp") != std::string::npos; }
+
+}  // namespace
+
+int pair_weight_formula(bool same_gpu, int link_type, bool same_numa, bool cross_hive,
+                        const AllocatorOptions& opt, bool has_link) {
+  if (!has_link && !opt.missing_pair_is_worst) return 0;  // reference quirk (device.go:266)
+  int w = same_gpu ? kSameDevIdWeight : kDifferentDevIdWeight;
+  if (!has_link) {
+    // Partitions of one package talk over the on-die fabric; anything else
+    // without a reported link is treated as the worst link.
+    w += same_gpu ? kXgmiLinkWeight : kOtherLinkWeight;
+  } else if (link_type == kLinkXgmi) {
+    w += kXgmiLinkWeight;
+  } else if (link_type == kLinkPcie) {
+    w += kPcieLinkWeight;
+  } else {
+    w += kOtherLinkWeight;
+  }
+  w += same_numa ? kSameNumaWeight : kDifferentNumaWeight;
+  if (cross_hive) w += opt.cross_hive_penalty;
+  return w;
+}
+
+std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdTopology& topo,
+                                const AllocatorOptions& opt) {
+  devs_.clear();
+  index_.clear();
+  groups_.clear();
+  dev_group_.clear();
+  w_.clear();
+  link_.clear();
+  linked_pairs_ = from_keys_ = 0;
+  opt_ = opt;
+  if (devs.empty()) return "Devices list is empty. Unable to calculate pair wise weights";
+
+  devs_ = devs;
+  const int n = static_cast<int>(devs_.size());
+  std::unordered_map<int, int> node2dev;
+  for (int i = 0; i < n; ++i) {
+    index_.emplace(devs_[i].id, i);
+    node2dev.emplace(devs_[i].node_id, i);
+    if (devs_[i].hive_id == 0)
+      if (const KfdNode* kn = topo.node(devs_[i].node_id)) devs_[i].hive_id = kn->hive_id();
+  }
+
+  link_.assign(static_cast<size_t>(n) * n, 0);
+  for (const KfdLink& l : topo.all_gpu_links()) {
+    auto a = node2dev.find(l.node_from), b = node2dev.find(l.node_to);
+    if (a == node2dev.end() || b == node2dev.end() || a->second == b->second) continue;
+    int i = a->second, j = b->second;
+    int& cur = link_[static_cast<size_t>(i) * n + j];
+    int t = l.type <= 0 ? kLinkOther : l.type;
+    if (cur == 0 || link_rank(t) < link_rank(cur)) {
+      cur = t;
+      link_[static_cast<size_t>(j) * n + i] = t;
+    }
+  }
+  std::unordered_set<int> froms;
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j)
+      if (link_[static_cast<size_t>(i) * n + j]) {
+        ++linked_pairs_;
+        froms.insert(std::min(devs_[i].node_id, devs_[j].node_id));
+      }
+  from_keys_ = froms.size();
+
+  w_.assign(static_cast<size_t>(n) * n, 0);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (i == j) continue;
+      const auto& a = devs_[i];
+      const auto& b = devs_[j];
+      int lt = link_[static_cast<size_t>(i) * n + j];
+      bool cross_hive = a.hive_id != 0 && b.hive_id != 0 && a.hive_id != b.hive_id;
+      w_[static_cast<size_t>(i) * n + j] =
+          pair_weight_formula(a.unique_id == b.unique_id, lt, a.numa_node == b.numa_node, cross_hive, opt_, lt != 0);
+    }
+
+  // group by physical GPU, in first-seen order; members by kfd node id
+  std::unordered_map<std::string, int> gidx;
+  dev_group_.assign(n, -1);
+  for (int i = 0; i < n; ++i) {
+    auto it = gidx.find(devs_[i].unique_id);
+    int g;
+    if (it == gidx.end()) {
+      g = static_cast<int>(groups_.size());
+      gidx.emplace(devs_[i].unique_id, g);
+      groups_.push_back(Group{devs_[i].unique_id, "", {}});
+    } else {
+      g = it->second;
+    }
+    if (!is_xcp_id(devs_[i].id)) groups_[g].parent_id = devs_[i].id;
+    groups_[g].members.push_back(i);
+    dev_group_[i] = g;
+  }
+  for (auto& g : groups_)
+    std::sort(g.members.begin(), g.members.end(),
+              [&](int a, int b) { return devs_[a].node_id < devs_[b].node_id; });
+  return "";
+}
+
+int HiveAllocator::pair_weight(const std::string& a, const std::string& b) const {
+  auto ia = index_.find(a), ib = index_.find(b);
+  if (ia == index_.end() || ib == index_.end()) return -1;
+  return w_[static_cast<size_t>(ia->second) * devs_.size() + ib->second];
+}
+
+int HiveAllocator::link_type(const std::string& a, const std::string& b) const {
+  auto ia = index_.find(a), ib = index_.find(b);
+  if (ia == index_.end() || ib == index_.end()) return -1;
+  return link_[static_cast<size_t>(ia->second) * devs_.size() + ib->second];
+}
+
+std::string HiveAllocator::validate(const std::vector<std::string>& available,
+                                    const std::vector<std::string>& required, int size, AllocResult* out,
+                                    std::vector<int>* avail_idx, std::vector<int>* req_idx) const {
+  if (size <= 0) return kInvalidSize;
+  if (static_cast<int>(available.size()) < size) return kInvalidAvailable;
+  if (static_cast<int>(required.size()) > size) return kInvalidRequired;
+  if (required.size() > available.size()) return kInvalidReqAvailable;
+  if (devs_.empty()) return kInvalidInit;
+  if (static_cast<int>(available.size()) == size) {
+    out->ids = available;
+    out->short_circuit = true;
+    return "";
+  }
+  if (static_cast<int>(required.size()) == size) {
+    out->ids = required;
+    out->short_circuit = true;
+    return "";
+  }
+  std::unordered_set<std::string> av(available.begin(), available.end());
+  for (auto& r : required)
+    if (!av.count(r)) return kNoCandidate;
+  std::unordered_set<int> seen;
+  for (auto& a : available) {
+    auto it = index_.find(a);
+    if (it == index_.end()) return "unknown device ID: " + a;
+    if (seen.insert(it->second).second) avail_idx->push_back(it->second);
+  }
+  std::unordered_set<int> rseen;
+  for (auto& r : required) {
+    auto it = index_.find(r);
+    if (it == index_.end()) return "unknown device ID: " + r;
+    if (rseen.insert(it->second).second) req_idx->push_back(it->second);
+  }
+  return "";
+}
+
+std::vector<std::vector<int>> HiveAllocator::filtered_groups(const std::vector<int>& avail_idx,
+                                                             const std::vector<int>& req_idx) const {
+  std::vector<char> is_av(devs_.size(), 0), is_req(devs_.size(), 0);
+  for (int i : avail_idx) is_av[i] = 1;
+  for (int i : req_idx) is_req[i] = 1;
+  struct FG {
+    const Group* g;
+    std::vector<int> m;
+  };
+  std::vector<FG> fgs;
+  for (auto& g : groups_) {
+    FG f{&g, {}};
+    for (int m : g.members)
+      if (is_av[m] && !is_req[m]) f.m.push_back(m);
+    if (!f.m.empty()) fgs.push_back(std::move(f));
+  }
+  // anti-fragmentation order: fewest free partitions first, then parent ID
+  // (reference filterPartitions, device.go:339-349); unique_id breaks the
+  // remaining ties deterministically.
+  std::stable_sort(fgs.begin(), fgs.end(), [](const FG& a, const FG& b) {
+    if (a.m.size() != b.m.size()) return a.m.size() < b.m.size();
+    if (a.g->parent_id != b.g->parent_id) return a.g->parent_id < b.g->parent_id;
+    return a.g->key < b.g->key;
+  });
+  std::vector<std::vector<int>> out;
+  out.reserve(fgs.size());
+  for (auto& f : fgs) out.push_back(std::move(f.m));
+  return out;
+}
+
+AllocResult HiveAllocator::allocate(const std::vector<std::string>& available,
+                                    const std::vector<std::string>& required, int size) const {
+  AllocResult res;
+  std::vector<int> avail_idx, req_idx;
+  res.error = validate(available, required, size, &res, &avail_idx, &req_idx);
+  if (!res.error.empty() || res.short_circuit) return res;
+
+  const size_t n = devs_.size();
+  auto W = [&](int a, int b) { return static_cast<int64_t>(w_[static_cast<size_t>(a) * n + b]); };
+  const auto fg = filtered_groups(avail_idx, req_idx);
+  const int G = static_cast<int>(fg.size());
+  const int need = size - static_cast<int>(req_idx.size());
+  int maxc = 0;
+  for (auto& g : fg) maxc = std::max(maxc, static_cast<int>(g.size()));
+  const int R = maxc + 1;
+
+  // Aggregates. P[g][r]: internal weight of the first r members of g.
+  // C[(p*G+g)*R + r]: weight between the first r members of p and all of g.
+  // Q[p][r]: weight between the first r members of p and the required set.
+  std::vector<int64_t> P(static_cast<size_t>(G) * R, 0), Q(static_cast<size_t>(G) * R, 0);
+  std::vector<int64_t> C(static_cast<size_t>(G) * G * R, 0);
+  for (int p = 0; p < G; ++p) {
+    const auto& mp = fg[p];
+    for (int r = 1; r <= static_cast<int>(mp.size()); ++r) {
+      int64_t add = 0, radd = 0;
+      for (int i = 0; i < r - 1; ++i) add += W(mp[i], mp[r - 1]);
+      for (int q : req_idx) radd += W(mp[r - 1], q);
+      P[p * R + r] = P[p * R + r - 1] + add;
+      Q[p * R + r] = Q[p * R + r - 1] + radd;
+      for (int g = 0; g < G; ++g) {
+        if (g == p) continue;
+        int64_t c = 0;
+        for (int m : fg[g]) c += W(mp[r - 1], m);
+        C[(static_cast<size_t>(p) * G + g) * R + r] = C[(static_cast<size_t>(p) * G + g) * R + r - 1] + c;
+      }
+    }
+  }
+  int64_t RR = 0;
+  for (size_t i = 0; i < req_idx.size(); ++i)
+    for (size_t j = i + 1; j < req_idx.size(); ++j) RR += W(req_idx[i], req_idx[j]);
+
+  struct Best {
+    bool found = false;
+    int64_t w = std::numeric_limits<int64_t>::max();
+    int level = 0;
+    std::vector<int> seq;
+    int partial = -1;  // group whose prefix is taken, -1 = all full
+    int take = 0;
+  } best;
+
+  std::vector<int> S;
+  std::vector<int> seq;
+  std::vector<char> inS(G, 0);
+  uint64_t cands = 0;
+
+  // depth-first over sets of whole GPUs (strictly increasing group index)
+  auto dfs = [&](auto&& self, int start, int64_t fw, int cnt) -> void {
+    if (best.found && fw + RR > best.w) return;  // all weights are >= 0
+    const int r = need - cnt;
+    for (int p = 0; p < G; ++p) {
+      const int cp = static_cast<int>(fg[p].size());
+      if (inS[p] || cp < r) continue;
+      int64_t w = fw + RR + P[p * R + r] + Q[p * R + r];
+      for (int g : S) w += C[(static_cast<size_t>(p) * G + g) * R + r];
+      ++cands;
+      if (best.found && w > best.w) continue;
+      const int level = static_cast<int>(S.size()) + 1;
+      seq.assign(S.begin(), S.end());
+      bool exact = (cp == r);
+      if (exact) {
+        seq.insert(std::upper_bound(seq.begin(), seq.end(), p), p);
+      } else {
+        seq.push_back(p);
+      }
+      bool better = !best.found || w < best.w || (w == best.w && level < best.level) ||
+                    (w == best.w && level == best.level && seq < best.seq);
+      if (better) {
+        best.found = true;
+        best.w = w;
+        best.level = level;
+        best.seq = seq;
+        best.partial = exact ? -1 : p;
+        best.take = r;
+      }
+    }
+    for (int g = start; g < G; ++g) {
+      const int cg = static_cast<int>(fg[g].size());
+      if (cnt + cg >= need) continue;
+      int64_t nfw = fw + P[g * R + cg] + Q[g * R + cg];
+      for (int h : S) nfw += C[(static_cast<size_t>(g) * G + h) * R + cg];
+      S.push_back(g);
+      inS[g] = 1;
+      self(self, g + 1, nfw, cnt + cg);
+      inS[g] = 0;
+      S.pop_back();
+    }
+  };
+  dfs(dfs, 0, 0, 0);
+  res.candidates = cands;
+  if (!best.found) {
+    res.error = kNoCandidate;
+    return res;
+  }
+  res.weight = best.w;
+  for (int g : best.seq) {
+    int take = (g == best.partial) ? best.take : static_cast<int>(fg[g].size());
+    for (int i = 0; i < take; ++i) res.ids.push_back(devs_[fg[g][i]].id);
+  }
+  for (int q : req_idx) res.ids.push_back(devs_[q].id);
+  return res;
+}
+
+AllocResult HiveAllocator::reference_allocate(const std::vector<std::string>& available,
+                                              const std::vector<std::string>& required, int size) const {
+  AllocResult res;
+  std::vector<int> avail_idx, req_idx;
+  res.error = validate(available, required, size, &res, &avail_idx, &req_idx);
+  if (!res.error.empty() || res.short_circuit) return res;
+
+  const size_t n = devs_.size();
+  const auto fg = filtered_groups(avail_idx, req_idx);
+  const int G = static_cast<int>(fg.size());
+  const int need = size - static_cast<int>(req_idx.size());
+
+  struct Cand {
+    std::vector<int> ids;
+    std::vector<int> parents;
+    int64_t w = 0;
+  };
+  auto add = [&](Cand& c, int dev) {
+    for (int d : c.ids) c.w += w_[static_cast<size_t>(d) * n + dev];
+    c.ids.push_back(dev);
+  };
+  auto finish = [&](Cand& c) {
+    for (int q : req_idx) add(c, q);
+  };
+
+  std::vector<Cand> finals;
+  std::deque<Cand> temp;
+  for (int idx = 0; idx < G; ++idx) {
+    Cand c;
+    c.parents = {idx};
+    add(c, fg[idx][0]);
+    if (need == 1) {
+      finish(c);
+      finals.push_back(std::move(c));
+      continue;
+    }
+    bool done = false;
+    for (size_t i = 1; i < fg[idx].size(); ++i) {
+      add(c, fg[idx][i]);
+      if (static_cast<int>(i) == need - 1) {
+        done = true;
+        break;
+      }
+    }
+    if (done) {
+      finish(c);
+      finals.push_back(std::move(c));
+    } else {
+      temp.push_back(std::move(c));
+    }
+  }
+  while (!temp.empty()) {
+    Cand cur = std::move(temp.front());
+    temp.pop_front();
+    if (static_cast<int>(cur.parents.size()) == G) continue;
+    for (int idx = 0; idx < G; ++idx) {
+      if (std::find(cur.parents.begin(), cur.parents.end(), idx) != cur.parents.end()) continue;
+      Cand c = cur;
+      c.parents.push_back(idx);
+      bool done = false;
+      for (int d : fg[idx]) {
+        add(c, d);
+        if (static_cast<int>(c.ids.size()) == need) {
+          finish(c);
+          finals.push_back(c);
+          done = true;
+          break;
+        }
+      }
+      if (!done && static_cast<int>(c.ids.size()) < need) temp.push_back(std::move(c));
+    }
+  }
+  res.candidates = finals.size();
+  const Cand* best = nullptr;
+  for (auto& c : finals)
+    if (!best || c.w < best->w) best = &c;
+  if (!best) {
+    res.error = kNoCandidate;
+    return res;
+  }
+  res.weight = best->w;
+  for (int d : best->ids) res.ids.push_back(devs_[d].id);
+  return res;
+}
+
+}  // namespace mi355x

@@ -1,0 +1,129 @@
+"""Build driver for the native core (CMake + Ninja, in-tree outputs).
+
+Outputs land inside the package so they travel with the repo snapshot:
+
+* ``_native*.so``                 host core (kfd/sysfs, allocator, PCI, drm, amd-smi)
+* ``_hip*.so``                    in-process gfx950 liveness probe
+* ``bin/mi355x-liveness-probe``   probe executable (plugin health loop, bench "container")
+* ``kernels/liveness_gfx950.hsaco``
+
+``ensure_built()`` is cheap when everything is up to date (one ninja no-op).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+NATIVE_DIR = REPO_DIR / "native"
+BUILD_DIR = REPO_DIR / "build" / "native"
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+NATIVE_SO = PKG_DIR / f"_native{EXT_SUFFIX}"
+HIP_SO = PKG_DIR / f"_hip{EXT_SUFFIX}"
+PROBE_EXE = PKG_DIR / "bin" / "mi355x-liveness-probe"
+HSACO = PKG_DIR / "kernels" / "liveness_gfx950.hsaco"
+
+
+def hipcc_available() -> bool:
+    return shutil.which("hipcc") is not None or Path("/opt/rocm/bin/hipcc").exists()
+
+
+def _sources_newer_than(target: Path) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    for p in NATIVE_DIR.rglob("*"):
+        if p.is_file() and p.suffix in {".cpp", ".h", ".hip", ".txt"} and p.stat().st_mtime > t:
+            return True
+    return False
+
+
+def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = None,
+          jobs: int | None = None, quiet: bool = True) -> None:
+    """Configure + build. ``hip=None`` builds the HIP probe when hipcc exists."""
+    if hip is None:
+        hip = hipcc_available()
+    bdir = build_dir or (BUILD_DIR if not sanitize else REPO_DIR / "build" / f"native-{sanitize.replace(',', '-')}")
+    bdir.mkdir(parents=True, exist_ok=True)
+    gen = ["-G", "Ninja"] if shutil.which("ninja") else []
+    cfg = [
+        "cmake", "-S", str(NATIVE_DIR), "-B", str(bdir), *gen,
+        f"-DPython3_EXECUTABLE={sys.executable}",
+        f"-DMI355X_BUILD_HIP={'ON' if hip else 'OFF'}",
+        f"-DMI355X_SANITIZE={sanitize}",
+        "-DCMAKE_BUILD_TYPE=Release",
+    ]
+    if sanitize:
+        # sanitizer builds are for ctest only; keep the package outputs untouched
+        cfg.append(f"-DMI355X_PKG_DIR={bdir / 'pkg'}")
+    out = subprocess.DEVNULL if quiet else None
+    if not (bdir / "CMakeCache.txt").exists() or sanitize:
+        subprocess.run(cfg, check=True, stdout=out)
+    else:
+        # re-run configure only if the HIP option flipped
+        cache = (bdir / "CMakeCache.txt").read_text()
+        want = f"MI355X_BUILD_HIP:BOOL={'ON' if hip else 'OFF'}"
+        if want not in cache:
+            subprocess.run(cfg, check=True, stdout=out)
+    j = jobs or min(8, os.cpu_count() or 4)
+    res = subprocess.run(["cmake", "--build", str(bdir), "-j", str(j)], stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout)
+        raise RuntimeError("native build failed")
+    if not quiet:
+        sys.stdout.write(res.stdout)
+
+
+def ensure_built(hip: bool | None = None) -> None:
+    """Build if any output is missing or older than the native sources.
+
+    Serialised across processes with a lock file, so ranks or pytest workers
+    that start together do not run two builds into the same tree.
+    """
+    import fcntl
+
+    if hip is None:
+        hip = hipcc_available()
+    targets = [NATIVE_SO] + ([HIP_SO, PROBE_EXE, HSACO] if hip else [])
+    if not any(_sources_newer_than(t) for t in targets):
+        return
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    with open(BUILD_DIR.parent / ".build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if any(_sources_newer_than(t) for t in targets):
+                build(hip=hip)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def run_ctest(sanitize: str = "") -> subprocess.CompletedProcess:
+    bdir = BUILD_DIR if not sanitize else REPO_DIR / "build" / f"native-{sanitize.replace(',', '-')}"
+    build(hip=False if sanitize else None, sanitize=sanitize)
+    env = dict(os.environ)
+    if "thread" in sanitize:
+        env.setdefault("TSAN_OPTIONS", "halt_on_error=1")
+    return subprocess.run(["ctest", "--test-dir", str(bdir), "--output-on-failure"],
+                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+
+
+if __name__ == "__main__":
+    import argparse
+
+    ap = argparse.ArgumentParser(description="build the native core")
+    ap.add_argument("--no-hip", action="store_true")
+    ap.add_argument("--sanitize", default="")
+    ap.add_argument("--ctest", action="store_true")
+    a = ap.parse_args()
+    if a.ctest:
+        r = run_ctest(a.sanitize)
+        print(r.stdout)
+        sys.exit(r.returncode)
+    build(hip=False if a.no_hip else None, sanitize=a.sanitize, quiet=False)

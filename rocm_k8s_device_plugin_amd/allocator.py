@@ -1,0 +1,94 @@
+"""Allocation policy facade (reference: internal/pkg/allocator/allocator.go:21-30
+``Policy{Init, Allocate}`` and BestEffortPolicy, besteffort_policy.go:45-151).
+
+The search itself is native (C++ ``HiveAllocator``, native/src/alloc/hive_allocator.cpp).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence
+
+from .ops.native import core
+
+
+class AllocationError(Exception):
+    pass
+
+
+@dataclass
+class AllocStats:
+    calls: int = 0
+    total_us: float = 0.0
+    last_us: float = 0.0
+    last_candidates: int = 0
+    last_weight: int = -1
+
+
+class Policy:
+    """Interface kept for parity with the reference Policy."""
+
+    def init(self, devices, topology) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def allocate(self, available: Sequence[str], required: Sequence[str], size: int) -> List[str]:
+        raise NotImplementedError  # pragma: no cover
+
+
+class BestEffortPolicy(Policy):
+    """Hive-aware optimal subset selection with the reference's tie-breaks."""
+
+    def __init__(self, missing_pair_is_worst: bool = True, cross_hive_penalty: int = 100):
+        n = core()
+        self._opts = n.AllocatorOptions(missing_pair_is_worst=missing_pair_is_worst,
+                                        cross_hive_penalty=cross_hive_penalty)
+        self._alloc = n.HiveAllocator()
+        self.stats = AllocStats()
+
+    @staticmethod
+    def to_alloc_devices(devices: Iterable) -> list:
+        """Accepts topology.Gpu objects or (id, node_id, numa, unique_id[, hive]) tuples."""
+        n = core()
+        out = []
+        for d in devices:
+            if isinstance(d, tuple):
+                out.append(n.AllocDevice(*d))
+            else:
+                out.append(n.AllocDevice(d.id, d.node_id, d.numa_node, d.unique_id, int(getattr(d, "hive_id", 0))))
+        return out
+
+    def init(self, devices, topology) -> None:
+        err = self._alloc.init(self.to_alloc_devices(devices), topology, self._opts)
+        if err:
+            raise AllocationError(err)
+
+    @property
+    def native(self):
+        return self._alloc
+
+    def allocate(self, available: Sequence[str], required: Sequence[str], size: int) -> List[str]:
+        t0 = time.perf_counter()
+        r = self._alloc.allocate(list(available), list(required or ()), int(size))
+        dt = (time.perf_counter() - t0) * 1e6
+        self.stats.calls += 1
+        self.stats.total_us += dt
+        self.stats.last_us = dt
+        self.stats.last_candidates = r["candidates"]
+        self.stats.last_weight = r["weight"]
+        if r["error"]:
+            raise AllocationError(r["error"])
+        return list(r["ids"])
+
+    def reference_allocate(self, available: Sequence[str], required: Sequence[str], size: int) -> dict:
+        """The reference's ordered-BFS enumeration on the same weights (benchmarks/parity)."""
+        return self._alloc.reference_allocate(list(available), list(required or ()), int(size))
+
+    def explain(self, available: Sequence[str], required: Sequence[str], size: int) -> dict:
+        return self._alloc.allocate(list(available), list(required or ()), int(size))
+
+
+def load_topology(nodes_dir: Optional[str] = None, sysfs_root: Optional[str] = None):
+    n = core()
+    if nodes_dir:
+        return n.KfdTopology.load(nodes_dir)
+    return n.KfdTopology.load_sysfs(sysfs_root or "/sys")

@@ -1,0 +1,139 @@
+"""``k8s-device-plugin`` entry point.
+
+Reference: cmd/k8s-device-plugin/main.go:34-120. Same flag names and
+semantics (``-pulse``, ``-driver_type``, ``-resource_naming_strategy`` plus
+glog flags), same validation messages and exit codes, same implementation
+auto-selection order (container -> vf-passthrough -> pf-passthrough; an
+explicit type that fails exits 1; if every strategy fails the manager still
+starts and idles).
+
+Additions (documented by the reference but never implemented there, or new):
+``AMD_GPU_DEVICE_COUNT`` / ``CONFIG_FILE_PATH`` (``gpu.device_count``),
+``--kubelet-url`` (accepted; registration is always over the UDS),
+``-sysfs_root`` / ``-dev_root`` / ``-kubelet_dir`` for fixture-driven runs,
+the MFMA liveness probe (``-liveness``), ``-metrics_port`` and JSON logs.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import sys
+from typing import List, Optional
+
+import yaml
+
+from .. import __version__
+from .. import constants as C
+from ..health.monitor import HealthConfig
+from ..plugin.base import DeviceImpl, DeviceImplError
+from ..plugin.manager import ManagerConfig, PluginManager
+from ..proto import deviceplugin as pb
+from ..topology import device_count_limit_from_env
+from ..utils import flags, log
+
+BANNER = ["AMD GPU device plugin for Kubernetes (MI355X-native)",
+          f"{os.path.basename(sys.argv[0] if sys.argv else 'k8s-device-plugin')} version {__version__}"]
+
+
+def build_parser() -> flags.GoFlagParser:
+    p = flags.GoFlagParser(prog="k8s-device-plugin", description="\n".join(BANNER))
+    p.add_int(C.FLAG_PULSE, 0, "time between health check polling in seconds.  Set to 0 to disable.")
+    p.add_str(C.FLAG_DRIVER_TYPE, "", "Driver type to use: container, vf-passthrough, or pf-passthrough")
+    p.add_str(C.FLAG_RESOURCE_NAMING_STRATEGY, C.STRATEGY_SINGLE, "Resource strategy to be used: single or mixed")
+    flags.add_glog_flags(p)
+    p.add_str("kubelet-url", "http://localhost:10250", "accepted for compatibility; registration uses the UDS")
+    p.add_str("kubelet_dir", pb.DEVICE_PLUGIN_PATH, "kubelet device-plugin socket directory")
+    p.add_str("sysfs_root", "/sys", "sysfs mount to read (fixtures: a generated tree)")
+    p.add_str("dev_root", "/dev", "device node directory")
+    p.add_str("exporter_socket", pb_exporter_socket(), "AMD metrics-exporter health socket ('' disables)")
+    p.add_bool("liveness", False, "run the gfx950 MFMA liveness probe on every device each pulse")
+    p.add_float("liveness_timeout", 10.0, "per-device liveness probe deadline (s)")
+    p.add_int("liveness_fail_threshold", 2, "consecutive probe failures before a device turns Unhealthy")
+    p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
+    p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
+    p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
+    p.add_str("log_format", "glog", "glog | json")
+    p.add_str("config", os.environ.get("CONFIG_FILE_PATH", ""), "YAML config file (gpu.device_count, ...)")
+    return p
+
+
+def pb_exporter_socket() -> str:
+    from ..proto.metricssvc import DEFAULT_SOCKET
+    return DEFAULT_SOCKET
+
+
+def validate(ns) -> Optional[str]:
+    if ns.pulse < 0:
+        return f"pulse must be a non-negative integer, got {ns.pulse}"
+    if ns.driver_type not in ("",) + C.DRIVER_TYPES:
+        return (f"invalid driver_type provided: {ns.driver_type}, supported values are container, "
+                "vf-passthrough, or pf-passthrough")
+    if ns.resource_naming_strategy not in (C.STRATEGY_SINGLE, C.STRATEGY_MIXED):
+        return (f"invalid resource_naming_strategy provided: {ns.resource_naming_strategy}, supported values "
+                "are single or mixed")
+    return None
+
+
+def load_config(path: str) -> dict:
+    if not path:
+        return {}
+    with open(path) as f:
+        return yaml.safe_load(f) or {}
+
+
+def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
+    if name == C.CONTAINER:
+        from ..plugin.container import ContainerImpl
+        hc = HealthConfig(exporter_socket=ns.exporter_socket or None, liveness=ns.liveness,
+                          liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
+                          smi_ecc=ns.smi_ecc, dev_root=ns.dev_root)
+        return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count)
+    if name == C.VF_PASSTHROUGH:
+        from ..plugin.passthrough import VfImpl
+        return VfImpl(ns.resource_naming_strategy, ns.sysfs_root, ns.exporter_socket or None)
+    if name == C.PF_PASSTHROUGH:
+        from ..plugin.passthrough import PfImpl
+        return PfImpl(ns.resource_naming_strategy, ns.sysfs_root)
+    raise DeviceImplError(f"unknown driver type {name}")
+
+
+def select_impl(ns, device_count: Optional[int], logger) -> Optional[DeviceImpl]:
+    if ns.driver_type:
+        try:
+            return create_impl(ns.driver_type, ns, device_count)
+        except Exception as e:
+            logger.error("Error instantiating driver type %s: %s", ns.driver_type, e)
+            raise SystemExit(1)
+    for name in C.DRIVER_TYPES:
+        try:
+            return create_impl(name, ns, device_count)
+        except Exception as e:
+            logger.warning("%s implementation failed: %s. Trying next...", name, e)
+    return None
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    p = build_parser()
+    ns = p.parse_args(argv)
+    logger = log.setup(ns.v, json_format=ns.log_format == "json", stderr_threshold=ns.stderrthreshold,
+                       logtostderr=ns.logtostderr)
+    err = validate(ns)
+    if err:
+        logger.error("%s", err)
+        return 1
+    for line in BANNER:
+        logger.info("%s", line)
+    cfg = load_config(ns.config)
+    device_count = device_count_limit_from_env()
+    if device_count is None:
+        dc = (cfg.get("gpu") or {}).get("device_count")
+        device_count = int(dc) if dc is not None else None
+    impl = select_impl(ns, device_count, logger)
+    mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
+                       metrics_port=ns.metrics_port)
+    asyncio.run(PluginManager(impl, mc).run())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,71 @@
+"""A minimal stand-in for the CRI runtime step of pod admission.
+
+Real admission: kubelet -> GetPreferredAllocation -> Allocate -> CRI creates
+the container with the returned DeviceSpecs -> ROCr in the container sees
+exactly the injected render nodes -> the app starts. We cannot create real
+containers here, so the runtime step is emulated faithfully where it matters
+for latency: a fresh process is started whose GPU visibility is restricted to
+the allocated devices (``ROCR_VISIBLE_DEVICES`` = the ROCr ordinals of the
+render nodes in the DeviceSpecs), and "ready" is the moment that process has
+initialised HIP and executed the MFMA liveness kernel on its device(s).
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import subprocess
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Mapping, Optional, Sequence
+
+from .health.liveness import _VISIBILITY_VARS
+from .ops.native import probe_executable
+
+_RENDER_RE = re.compile(r"/dev/dri/renderD(\d+)$")
+
+
+def render_minors_from_specs(container_response) -> List[int]:
+    """renderD minors named in a ContainerAllocateResponse's device specs, in order."""
+    out = []
+    for d in container_response.devices:
+        m = _RENDER_RE.search(d.host_path)
+        if m:
+            out.append(int(m.group(1)))
+    return out
+
+
+@dataclass
+class ContainerResult:
+    ok: bool
+    t_start_ns: int          # parent-side spawn time (CLOCK_MONOTONIC)
+    t_ready_ns: int          # child-reported ready time (CLOCK_MONOTONIC)
+    wall_ms: float
+    doc: dict
+    error: str = ""
+
+
+def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int = 4,
+                    exe: Optional[str] = None) -> ContainerResult:
+    """Run the container entrypoint restricted to `ordinals`; block until ready/exit."""
+    env = {k: v for k, v in os.environ.items() if k not in _VISIBILITY_VARS}
+    env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
+    argv = [exe or str(probe_executable()), "--devices", ",".join(str(i) for i in range(len(ordinals))),
+            "--iters", str(iters)]
+    t0 = time.monotonic_ns()
+    try:
+        p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return ContainerResult(False, t0, 0, (time.monotonic_ns() - t0) / 1e6, {}, "container start timed out")
+    wall = (time.monotonic_ns() - t0) / 1e6
+    try:
+        doc = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return ContainerResult(False, t0, 0, wall, {}, f"bad output rc={p.returncode}: {p.stderr.decode()[-300:]}")
+    ok = p.returncode == 0 and bool(doc.get("ok"))
+    err = "" if ok else "; ".join(d.get("error", "") for d in doc.get("devices", [])) or doc.get("error", "")
+    return ContainerResult(ok, t0, int(doc.get("t_ready_ns", 0)), wall, doc, err)
+
+
+def ordinals_for_minors(minors: Sequence[int], minor_to_ordinal: Mapping[int, int]) -> List[int]:
+    return [minor_to_ordinal[m] for m in minors]

@@ -1,0 +1,196 @@
+"""Per-device health aggregation for the container (KFD) mode.
+
+Reference behaviour (internal/pkg/amdgpu/amdgpu.go:322-345,865-974): one
+node-global verdict — "Healthy" if *any* kfd node is a live GPU — copied onto
+every device, then overridden per PCI BDF by the metrics exporter. Partitions
+never get their own verdict and the verdict objects are mutated in place while
+RPCs read them.
+
+Here each device gets its own verdict from up to four sources, and a device is
+Healthy only if every *available* source agrees:
+
+1. kfd: the device's own kfd node still exists and is a live GPU node;
+2. exporter: per-BDF verdict, applied to every partition of that BDF;
+3. liveness: the gfx950 MFMA probe on that exact HIP device, with hysteresis
+   (``fail_threshold`` consecutive failures to go Unhealthy,
+   ``recover_threshold`` successes to come back);
+4. amd-smi: a rise in uncorrectable ECC errors since the last sweep.
+
+Verdicts are published as immutable snapshots with a version number, so
+ListAndWatch streams can send on change without locks.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Mapping, Optional, Tuple
+
+from ..ops.native import core
+from ..proto import deviceplugin as dp
+from ..topology import Inventory, hip_ordinals
+from ..utils import log
+from . import exporter
+from .liveness import LivenessProber
+
+_log = log.get("health")
+
+
+@dataclass(frozen=True)
+class Verdict:
+    health: str
+    reasons: Tuple[str, ...] = ()
+
+
+@dataclass
+class HealthConfig:
+    exporter_socket: Optional[str] = exporter.DEFAULT_SOCKET
+    exporter_timeout_s: float = 10.0
+    liveness: bool = False
+    liveness_timeout_s: float = 10.0
+    liveness_iters: int = 4
+    liveness_parallel: int = 8
+    fail_threshold: int = 2
+    recover_threshold: int = 1
+    smi_ecc: bool = False
+    dev_root: str = "/dev"
+
+
+@dataclass
+class _Track:
+    fails: int = 0
+    oks: int = 0
+    live: bool = True
+    last_reason: str = ""
+
+
+class HealthMonitor:
+    def __init__(self, inventory: Inventory, cfg: Optional[HealthConfig] = None,
+                 prober: Optional[LivenessProber] = None,
+                 ordinal_map: Optional[Mapping[str, int]] = None,
+                 exporter_fn: Optional[Callable] = None):
+        self.inv = inventory
+        self.cfg = cfg or HealthConfig()
+        self.prober = prober
+        if self.cfg.liveness and self.prober is None:
+            self.prober = LivenessProber(timeout_s=self.cfg.liveness_timeout_s, iters=self.cfg.liveness_iters,
+                                         max_parallel=self.cfg.liveness_parallel)
+        self._ordinals = dict(ordinal_map) if ordinal_map is not None else None
+        self._exporter_fn = exporter_fn or exporter.get_gpu_health
+        self._track: Dict[str, _Track] = {d.id: _Track() for d in inventory.devices}
+        self._ecc: Dict[str, int] = {}
+        self._snapshot: Dict[str, Verdict] = {d.id: Verdict(dp.HEALTHY) for d in inventory.devices}
+        self.version = 0
+        self.sweeps = 0
+        self.last_sweep_ms = 0.0
+
+    # ------------------------------------------------------------------ views
+    def snapshot(self) -> Dict[str, Verdict]:
+        return self._snapshot
+
+    def health(self, dev_id: str) -> str:
+        v = self._snapshot.get(dev_id)
+        return v.health if v else dp.UNHEALTHY
+
+    def ordinals(self) -> Dict[str, int]:
+        if self._ordinals is None:
+            self._ordinals = hip_ordinals(self.inv, self.cfg.dev_root)
+        return self._ordinals
+
+    # ---------------------------------------------------------------- sources
+    def _kfd_verdicts(self) -> Dict[str, Optional[str]]:
+        n = core()
+        nodes_dir = os.path.join(self.inv.sysfs_root, "class/kfd/kfd/topology/nodes")
+        out: Dict[str, Optional[str]] = {}
+        if not os.path.isdir(nodes_dir):
+            return {d.id: "kfd topology unavailable" for d in self.inv.devices}
+        for d in self.inv.devices:
+            if d.node_id < 0:
+                out[d.id] = None
+                continue
+            kv = n.parse_kv_file(os.path.join(nodes_dir, str(d.node_id), "properties"))
+            if kv is None:
+                out[d.id] = f"kfd node {d.node_id} missing"
+                continue
+            try:
+                cores = int(kv.get("cpu_cores_count", "0"), 0)
+                gfx = int(kv.get("gfx_target_version", "0"), 0)
+            except ValueError:
+                out[d.id] = f"kfd node {d.node_id} unparseable"
+                continue
+            out[d.id] = None if (cores == 0 and gfx > 0) else f"kfd node {d.node_id} not a live GPU"
+        return out
+
+    def _smi_ecc(self) -> Dict[str, str]:
+        n = core()
+        if not n.smi_available():
+            return {}
+        snap = n.smi_snapshot()
+        if not snap["ok"]:
+            return {}
+        bad: Dict[str, str] = {}
+        by_bdf = {g["bdf"]: g for g in snap["gpus"] if g["ecc_ok"]}
+        for d in self.inv.devices:
+            g = by_bdf.get(d.bdf)
+            if not g:
+                continue
+            prev = self._ecc.get(d.id)
+            cur = int(g["ecc_uncorrectable"])
+            self._ecc[d.id] = cur
+            if prev is not None and cur > prev:
+                bad[d.id] = f"uncorrectable ECC errors rose {prev}->{cur}"
+        return bad
+
+    # ------------------------------------------------------------------ sweep
+    async def check_once(self) -> bool:
+        """Run one sweep; returns True if any verdict changed."""
+        t0 = time.perf_counter()
+        reasons: Dict[str, list] = {d.id: [] for d in self.inv.devices}
+        for dev, r in self._kfd_verdicts().items():
+            if r:
+                reasons[dev].append(r)
+
+        if self.cfg.exporter_socket:
+            hmap = await self._exporter_fn(self.cfg.exporter_socket, self.cfg.exporter_timeout_s)
+            if hmap:
+                for d in self.inv.devices:
+                    if hmap.get(d.bdf) == dp.UNHEALTHY:
+                        reasons[d.id].append(f"exporter reports {d.bdf} unhealthy")
+
+        if self.cfg.liveness and self.prober is not None:
+            ords = {k: v for k, v in self.ordinals().items() if k in reasons}
+            outcomes = await self.prober.probe(ords)
+            for dev_id, o in outcomes.items():
+                tr = self._track[dev_id]
+                if o.ok:
+                    tr.fails, tr.oks = 0, tr.oks + 1
+                    if not tr.live and tr.oks >= self.cfg.recover_threshold:
+                        tr.live = True
+                else:
+                    tr.oks, tr.fails = 0, tr.fails + 1
+                    tr.last_reason = o.reason
+                    if tr.live and tr.fails >= self.cfg.fail_threshold:
+                        tr.live = False
+                if not tr.live:
+                    reasons[dev_id].append(f"liveness probe: {tr.last_reason}")
+            for dev_id in reasons:
+                if dev_id not in ords:
+                    reasons[dev_id].append("no HIP device for this ID (render node inaccessible?)")
+
+        if self.cfg.smi_ecc:
+            for dev_id, r in self._smi_ecc().items():
+                reasons[dev_id].append(r)
+
+        new = {dev: Verdict(dp.UNHEALTHY if rs else dp.HEALTHY, tuple(rs)) for dev, rs in reasons.items()}
+        changed = any(new[k].health != self._snapshot.get(k, Verdict("")).health for k in new)
+        if changed:
+            for k, v in new.items():
+                old = self._snapshot.get(k)
+                if old is None or old.health != v.health:
+                    _log.warning("device %s: %s -> %s %s", k, old.health if old else "?", v.health,
+                                 "; ".join(v.reasons))
+            self.version += 1
+        self._snapshot = new
+        self.sweeps += 1
+        self.last_sweep_ms = (time.perf_counter() - t0) * 1e3
+        return changed

@@ -1,0 +1,143 @@
+"""Container (ROCm/KFD) device strategy.
+
+Reference: AMDGPUKFDImpl, internal/pkg/amdgpu/amdgpu.go:47-345.
+
+Kept identical (drop-in): device IDs (BDF / amdgpu_xcp_N), resource names
+(``gpu`` | ``<compute>_<memory>``), the heterogeneous+single init error, the
+``/dev/kfd`` + ``/dev/dri/card<N>`` + ``/dev/dri/renderD<N>`` spec list with
+``rw`` permissions, GetPreferredAllocationAvailable unless allocator init
+failed, NUMA topology hints.
+
+Changed: per-device health (health.monitor), immutable device snapshots,
+deterministic device-node order, an error (not silently empty specs) for an
+unknown device ID, and a hive-aware exact allocator.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+from .. import constants as C
+from ..allocator import AllocationError
+from ..health.monitor import HealthConfig, HealthMonitor
+from ..proto import deviceplugin as pb
+from ..topology import Gpu, Inventory, discover
+from ..utils import log
+from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto
+
+_log = log.get("container")
+
+
+class ContainerImpl(DeviceImpl):
+    name = C.CONTAINER
+
+    def __init__(self, naming_strategy: str = C.STRATEGY_SINGLE, sysfs_root: str = "/sys",
+                 health_cfg: Optional[HealthConfig] = None, device_count_limit: Optional[int] = None,
+                 inventory: Optional[Inventory] = None, monitor: Optional[HealthMonitor] = None):
+        self.strategy = naming_strategy
+        self.sysfs_root = sysfs_root
+        if not os.path.exists(os.path.join(sysfs_root, C.KFD_CLASS_REL)):
+            raise DeviceImplError("No amd gpu driver loaded")
+        self.inv = inventory or discover(sysfs_root, device_count_limit)
+        for w in self.inv.warnings:
+            _log.warning("%s", w)
+        self.homogeneous = self.inv.homogeneous
+        if not self.homogeneous and self.strategy == C.STRATEGY_SINGLE:
+            raise DeviceImplError(
+                "Partitions of different styles across GPUs in a node is not supported with single strategy. "
+                "Please start device plugin with mixed strategy")
+        self.monitor = monitor or HealthMonitor(self.inv, health_cfg or HealthConfig())
+        self._resources = self._compute_resource_names()
+        self._members: Dict[str, List[Gpu]] = {r: self._devices_for(r) for r in self._resources}
+        _log.info("Found %d AMDGPUs (%s)", len(self.inv), ", ".join(
+            f"{r}={len(v)}" for r, v in self._members.items()))
+
+    # ------------------------------------------------------------- resources
+    def _compute_resource_names(self) -> List[str]:
+        if len(self.inv) == 0:
+            return []
+        counts = self.inv.partition_counts()
+        if self.homogeneous:
+            if self.strategy == C.STRATEGY_SINGLE or not counts:
+                return [C.DEVICE_TYPE_GPU]
+            return sorted(t for t, c in counts.items() if c > 0)
+        return sorted(t for t, c in counts.items() if c > 0)
+
+    def _devices_for(self, resource: str) -> List[Gpu]:
+        if self.homogeneous:
+            return list(self.inv.devices)
+        return [d for d in self.inv.devices if d.partition_type == resource]
+
+    def resource_names(self) -> List[str]:
+        return list(self._resources)
+
+    def devices(self, resource: str) -> List[Gpu]:
+        return list(self._members.get(resource, []))
+
+    # ------------------------------------------------------------- lifecycle
+    def start(self, ctx: PluginContext) -> None:
+        devs = self._members.get(ctx.resource, list(self.inv.devices))
+        if ctx.allocator is None:
+            ctx.allocator_error = True
+            return
+        try:
+            ctx.allocator.init(devs, self.inv.topology)
+        except AllocationError as e:
+            _log.error("allocator init failed for plugin %s. Falling back to kubelet default allocation. "
+                       "Error %s", ctx.resource, e)
+            ctx.allocator_error = True
+
+    def options(self, ctx: PluginContext) -> pb.DevicePluginOptions:
+        if ctx.allocator_error:
+            return pb.DevicePluginOptions()
+        return pb.DevicePluginOptions(get_preferred_allocation_available=True)
+
+    # ---------------------------------------------------------------- device lists
+    def _device_list(self, resource: str) -> List[pb.Device]:
+        snap = self.monitor.snapshot()
+        out = []
+        for d in self._members.get(resource, []):
+            v = snap.get(d.id)
+            out.append(device_proto(d.id, v.health if v else pb.HEALTHY, d.numa_node))
+        return out
+
+    def enumerate(self, ctx: PluginContext) -> List[pb.Device]:
+        return self._device_list(ctx.resource)
+
+    def update_health(self, ctx: PluginContext) -> List[pb.Device]:
+        return self._device_list(ctx.resource)
+
+    async def refresh_health(self) -> bool:
+        return await self.monitor.check_once()
+
+    def health_version(self) -> int:
+        return self.monitor.version
+
+    # ---------------------------------------------------------------- allocation
+    def allocate(self, ctx: PluginContext, req: pb.AllocateRequest) -> pb.AllocateResponse:
+        resp = pb.AllocateResponse()
+        for creq in req.container_requests:
+            car = resp.container_responses.add()
+            # one /dev/kfd per container regardless of the number of GPUs
+            car.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
+            for dev_id in creq.devices_ids:
+                d = self.inv.by_id.get(dev_id)
+                if d is None:
+                    raise DeviceImplError(f"unknown device ID {dev_id!r} for resource {ctx.resource}")
+                for p in d.dev_paths():
+                    car.devices.add(container_path=p, host_path=p, permissions="rw")
+        return resp
+
+    def preferred_allocation(self, ctx: PluginContext,
+                             req: pb.PreferredAllocationRequest) -> pb.PreferredAllocationResponse:
+        resp = pb.PreferredAllocationResponse()
+        if ctx.allocator is None or ctx.allocator_error:
+            raise DeviceImplError("allocator unavailable")
+        for creq in req.container_requests:
+            try:
+                ids = ctx.allocator.allocate(list(creq.available_deviceIDs), list(creq.must_include_deviceIDs),
+                                             creq.allocation_size)
+            except AllocationError as e:
+                raise DeviceImplError(f"unable to get preferred allocation list. Error:{e}") from e
+            resp.container_responses.add(deviceIDs=ids)
+        return resp

@@ -1,0 +1,259 @@
+"""Device-plugin lifecycle manager.
+
+Reference: internal/pkg/manager/manager.go:31-104 (lister, heartbeat) and the
+vendored kubevirt device-plugin-manager (vendor/github.com/kubevirt/
+device-plugin-manager/pkg/dpm/{manager,plugin}.go). Same externally visible
+behaviour:
+
+* one gRPC server per resource on ``<plugin_dir>/amd.com_<resource>``;
+* stale socket removed before listening;
+* ``Register{Version: v1beta1, Endpoint: <socket basename>,
+  ResourceName: amd.com/<resource>, Options}`` against ``kubelet.sock``;
+* server start retried 3 times, 3 s apart;
+* kubelet restart (``kubelet.sock`` re-created) -> re-serve and re-register,
+  ``kubelet.sock`` removed -> stop servers;
+* SIGTERM/SIGINT/SIGQUIT -> stop everything and remove sockets;
+* no DeviceImpl (every strategy failed) -> idle until signalled.
+
+Re-designed: asyncio instead of goroutines; the kubelet socket is watched by
+inode polling (works on any filesystem, catches delete+recreate between
+polls); the heartbeat is a broadcast health sweep (one sweep per pulse for the
+whole node, every resource's ListAndWatch woken).
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import signal
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import grpc
+
+from .. import constants as C
+from ..proto import deviceplugin as pb
+from ..utils import log
+from ..utils.broadcast import Broadcast
+from ..utils.metrics import REGISTRY, serve_metrics
+from .base import DeviceImpl, PluginContext, new_context
+from .servicer import DevicePluginServicer
+
+_log = log.get("manager")
+
+
+@dataclass
+class ManagerConfig:
+    pulse_s: float = 0.0
+    plugin_dir: str = pb.DEVICE_PLUGIN_PATH
+    kubelet_socket: Optional[str] = None   # default: <plugin_dir>/kubelet.sock
+    namespace: str = C.RESOURCE_NAMESPACE
+    start_retries: int = 3
+    retry_wait_s: float = 3.0
+    register_timeout_s: float = 10.0
+    watch_interval_s: float = 0.5
+    send_every_pulse: bool = False
+    metrics_port: int = 0
+    handle_signals: bool = True
+
+
+class ResourcePlugin:
+    def __init__(self, mgr: "PluginManager", name: str):
+        self.mgr = mgr
+        self.name = name
+        cfg = mgr.cfg
+        self.resource_name = f"{cfg.namespace}/{name}"
+        self.socket = os.path.join(cfg.plugin_dir, f"{cfg.namespace}_{name}")
+        self.ctx: PluginContext = new_context(name)
+        self.stop_bc = Broadcast()
+        self.servicer: Optional[DevicePluginServicer] = None
+        self.server: Optional[grpc.aio.Server] = None
+        self.running = False
+        self.started = False
+        self.registrations = 0
+        self._lock = asyncio.Lock()
+
+    def start(self) -> bool:
+        try:
+            self.mgr.impl.start(self.ctx)
+            self.started = True
+        except Exception as e:  # reference: log and do not start the server
+            _log.error('Failed to start plugin "%s": %s', self.name, e)
+            self.started = False
+        return self.started
+
+    def _cleanup(self) -> None:
+        try:
+            os.unlink(self.socket)
+        except FileNotFoundError:
+            pass
+
+    async def _serve(self) -> None:
+        self._cleanup()
+        os.makedirs(os.path.dirname(self.socket), exist_ok=True)
+        self.stop_bc = Broadcast()
+        self.servicer = DevicePluginServicer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
+                                             self.mgr.cfg.send_every_pulse)
+        server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
+        server.add_generic_rpc_handlers((pb.device_plugin_handler(self.servicer),))
+        server.add_insecure_port(f"unix:{self.socket}")
+        await server.start()
+        self.server = server
+
+    async def _register(self) -> None:
+        sock = self.mgr.kubelet_socket
+        opts = self.mgr.impl.options(self.ctx)
+        req = pb.RegisterRequest(version=pb.VERSION, endpoint=os.path.basename(self.socket),
+                                 resource_name=self.resource_name, options=opts)
+        _log.info("%s: Registration for endpoint %s", self.name, req.endpoint)
+        async with grpc.aio.insecure_channel(f"unix:{sock}") as ch:
+            await pb.RegistrationStub(ch).Register(req, timeout=self.mgr.cfg.register_timeout_s)
+        self.registrations += 1
+        REGISTRY.inc("mi355x_dp_registrations_total", resource=self.name)
+
+    async def start_server(self) -> bool:
+        async with self._lock:
+            if self.running:
+                return True
+            cfg = self.mgr.cfg
+            for attempt in range(1, cfg.start_retries + 1):
+                try:
+                    t0 = time.perf_counter()
+                    await self._serve()
+                    await self._register()
+                    self.running = True
+                    log.info_fields(_log, "plugin server started", resource=self.resource_name,
+                                    socket=self.socket, startup_ms=f"{(time.perf_counter() - t0) * 1e3:.2f}")
+                    return True
+                except Exception as e:
+                    await self._stop_locked()
+                    if attempt == cfg.start_retries:
+                        _log.error('Failed to start plugin\'s "%s" server, within given %d tries: %s', self.name,
+                                   cfg.start_retries, e)
+                    else:
+                        _log.error('Failed to start plugin\'s "%s" server, attempt %d out of %d, waiting %.1fs '
+                                   'before next try: %s', self.name, attempt, cfg.start_retries, cfg.retry_wait_s, e)
+                        await asyncio.sleep(cfg.retry_wait_s)
+            return False
+
+    async def _stop_locked(self) -> None:
+        self.stop_bc.close()
+        if self.server is not None:
+            await self.server.stop(grace=0.5)
+            self.server = None
+        self.running = False
+        self._cleanup()
+
+    async def stop_server(self) -> None:
+        async with self._lock:
+            await self._stop_locked()
+
+
+class PluginManager:
+    def __init__(self, impl: Optional[DeviceImpl], cfg: Optional[ManagerConfig] = None):
+        self.impl = impl
+        self.cfg = cfg or ManagerConfig()
+        self.kubelet_socket = self.cfg.kubelet_socket or os.path.join(self.cfg.plugin_dir, "kubelet.sock")
+        self.plugins: Dict[str, ResourcePlugin] = {}
+        self.pulse = Broadcast()
+        self.stopped = asyncio.Event()
+        self.ready = asyncio.Event()
+        self._tasks: List[asyncio.Task] = []
+        self._metrics_server = None
+
+    # ------------------------------------------------------------- control
+    def request_stop(self) -> None:
+        self.stopped.set()
+
+    def resources(self) -> List[str]:
+        return list(self.plugins)
+
+    async def _start_all(self) -> None:
+        await asyncio.gather(*(p.start_server() for p in self.plugins.values() if p.started))
+
+    async def _stop_servers(self) -> None:
+        await asyncio.gather(*(p.stop_server() for p in self.plugins.values()))
+
+    async def _health_loop(self) -> None:
+        while not self.stopped.is_set():
+            try:
+                await asyncio.wait_for(self.stopped.wait(), self.cfg.pulse_s)
+                return
+            except asyncio.TimeoutError:
+                pass
+            t0 = time.perf_counter()
+            try:
+                changed = await self.impl.refresh_health()
+            except Exception as e:  # health must never take the plugin down
+                _log.error("health sweep failed: %s", e)
+                changed = False
+            REGISTRY.histogram("mi355x_dp_health_sweep_seconds", "health sweep latency").observe(
+                (time.perf_counter() - t0) * 1e3)
+            if changed:
+                REGISTRY.inc("mi355x_dp_health_changes_total")
+            self.pulse.fire()
+
+    def _sock_id(self) -> Optional[Tuple[int, int, int]]:
+        # inode numbers are recycled by delete+create; ctime tells them apart
+        try:
+            st = os.stat(self.kubelet_socket)
+            return (st.st_ino, st.st_dev, st.st_ctime_ns)
+        except FileNotFoundError:
+            return None
+
+    async def _watch_kubelet(self) -> None:
+        last = self._sock_id()
+        while not self.stopped.is_set():
+            try:
+                await asyncio.wait_for(self.stopped.wait(), self.cfg.watch_interval_s)
+                return
+            except asyncio.TimeoutError:
+                pass
+            cur = self._sock_id()
+            if cur == last:
+                continue
+            if cur is None:
+                _log.info("kubelet socket removed; stopping plugin servers")
+                await self._stop_servers()
+            else:
+                _log.info("kubelet socket (re)created; restarting plugin servers and re-registering")
+                await self._stop_servers()
+                await self._start_all()
+            last = cur
+
+    async def run(self) -> None:
+        loop = asyncio.get_running_loop()
+        if self.cfg.handle_signals:
+            for s in (signal.SIGTERM, signal.SIGINT, signal.SIGQUIT):
+                try:
+                    loop.add_signal_handler(s, self.request_stop)
+                except (NotImplementedError, RuntimeError):
+                    pass
+        if self.cfg.metrics_port:
+            self._metrics_server = await serve_metrics(self.cfg.metrics_port)
+        names = self.impl.resource_names() if self.impl is not None else []
+        if not names:
+            _log.warning("no device implementation/resources available; idling")
+        for n in names:
+            p = ResourcePlugin(self, n)
+            self.plugins[n] = p
+            p.start()
+        await self._start_all()
+        if self.impl is not None and self.cfg.pulse_s > 0:
+            self._tasks.append(asyncio.create_task(self._health_loop()))
+        self._tasks.append(asyncio.create_task(self._watch_kubelet()))
+        self.ready.set()
+        await self.stopped.wait()
+        await self.shutdown()
+
+    async def shutdown(self) -> None:
+        self.pulse.close()
+        for t in self._tasks:
+            t.cancel()
+        await asyncio.gather(*self._tasks, return_exceptions=True)
+        self._tasks.clear()
+        await self._stop_servers()
+        if self._metrics_server is not None:
+            self._metrics_server.close()
+            await self._metrics_server.wait_closed()
+        _log.info("device plugin manager stopped")

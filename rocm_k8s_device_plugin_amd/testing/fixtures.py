@@ -1,0 +1,294 @@
+"""Synthetic MI355X node fixtures (sysfs + /dev trees).
+
+The reference only has captured trees of older parts (MI210, MI300X CPX,
+MI308X) and its discovery cannot even read them because its
+paths are hard-coded. This generator writes a complete, self-consistent
+8x MI355X (gfx950, gfx_target_version 90500, 288 GiB HBM3E, 256 CUs / 8 XCDs
+per GPU) node in any compute partition mode (SPX/DPX/QPX/CPX: 1/2/4/8
+partitions per GPU) and memory mode (NPS1/NPS2), with:
+
+* kfd topology: CPU nodes + one GPU node per partition, properties,
+  io_links (xGMI inside a hive, PCIe to the CPU), p2p_links (PCIe across hives),
+  mem_banks;
+* amdgpu PCI functions (``module/amdgpu/drivers/pci:amdgpu/<BDF>`` symlinks
+  into ``devices/pci0000:00``) with partition files, numa_node and drm nodes;
+* ``devices/platform/amdgpu_xcp_<N>`` for the partitions beyond the first;
+* ``class/drm/card<N>/device`` links with vendor/device/product_name and
+  driver module version;
+* optional SR-IOV (gim + virtfn) or vfio-pci passthrough PCI trees;
+* a matching ``dev`` tree (kfd, dri/card*, dri/renderD*, vfio/*).
+
+Everything here is synthetic; exact MI355X sysfs strings should be confirmed
+on hardware (the GPU tests compare this layout with the real box).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence
+
+PARTITIONS = {"spx": 1, "dpx": 2, "qpx": 4, "cpx": 8}
+MI355X_DEVICE_ID = 0x75A3
+MI355X_VF_DEVICE_ID = 0x75B3
+MI355X_PRODUCT = "AMD Instinct MI355X"
+MI355X_VRAM = 288 * 1024 ** 3
+MI355X_CUS = 256
+MI355X_XCDS = 8
+DEFAULT_BUSES = [0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xE5, 0xF5]
+
+
+@dataclass
+class FixtureSpec:
+    num_gpus: int = 8
+    compute_partition: str = "spx"
+    memory_partition: str = "nps1"
+    numa_nodes: int = 2
+    hive_size: int = 8                  # GPUs per xGMI hive (8 = one hive)
+    gfx_target_version: int = 90500
+    device_id: int = MI355X_DEVICE_ID
+    product_name: str = MI355X_PRODUCT
+    driver_version: str = "6.12.12"
+    driver_srcversion: str = "A1B2C3D4E5F60718293A4B5"
+    mode: str = "container"             # container | vf | pf
+    vfs_per_gpu: int = 1                # SR-IOV VFs per PF (mode="vf")
+    partition_support: bool = True      # write available_*_partition files
+    per_gpu_compute: Optional[List[str]] = None  # heterogeneous nodes
+
+
+@dataclass
+class FixtureInfo:
+    root: Path
+    sysfs: Path
+    dev: Path
+    device_ids: List[str] = field(default_factory=list)
+    bdfs: List[str] = field(default_factory=list)
+    unique_ids: List[str] = field(default_factory=list)
+    hive_ids: List[int] = field(default_factory=list)
+    render_minors: Dict[str, int] = field(default_factory=dict)
+    node_ids: Dict[str, int] = field(default_factory=dict)
+
+
+def _w(path: Path, content: str) -> None:
+    path.parent.mkdir(parents=True, exist_ok=True)
+    path.write_text(content if content.endswith("\n") else content + "\n")
+
+
+def _link(target: Path, link: Path) -> None:
+    link.parent.mkdir(parents=True, exist_ok=True)
+    if link.is_symlink() or link.exists():
+        link.unlink()
+    os.symlink(os.path.relpath(target, link.parent), link)
+
+
+def _props(kv: Sequence) -> str:
+    return "\n".join(f"{k} {v}" for k, v in kv)
+
+
+def _unique_id(g: int) -> str:
+    # stable 64-bit-ish ids, like kfd's (decimal)
+    return str((0x9E3779B97F4A7C15 * (g + 1)) % (2 ** 64))
+
+
+def _hive_id(h: int) -> int:
+    return (0xC2B2AE3D27D4EB4F * (h + 7)) % (2 ** 64)
+
+
+def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw) -> FixtureInfo:
+    spec = spec or FixtureSpec(**kw)
+    root = Path(root)
+    sysfs = root / "sys"
+    dev = root / "dev"
+    info = FixtureInfo(root=root, sysfs=sysfs, dev=dev)
+    nodes_dir = sysfs / "class/kfd/kfd/topology/nodes"
+    pci_root = sysfs / "devices/pci0000:00"
+    drv_amdgpu = sysfs / "bus/pci/drivers/amdgpu"
+    _w(sysfs / "module/amdgpu/version", spec.driver_version)
+    _w(sysfs / "module/amdgpu/srcversion", spec.driver_srcversion)
+    (sysfs / "module/amdgpu/drivers").mkdir(parents=True, exist_ok=True)
+    drv_amdgpu.mkdir(parents=True, exist_ok=True)
+    _link(sysfs / "module/amdgpu", drv_amdgpu / "module")
+    _link(drv_amdgpu, sysfs / "module/amdgpu/drivers/pci:amdgpu")
+    dev.mkdir(parents=True, exist_ok=True)
+    (dev / "dri").mkdir(exist_ok=True)
+    _w(dev / "kfd", "")
+    _w(sysfs / "class/kfd/kfd/topology/generation_id", "1")
+
+    numa = max(1, spec.numa_nodes)
+    # CPU nodes 0..numa-1
+    for c in range(numa):
+        nd = nodes_dir / str(c)
+        _w(nd / "properties", _props([
+            ("cpu_cores_count", 64), ("simd_count", 0), ("mem_banks_count", 1), ("caches_count", 0),
+            ("io_links_count", 0), ("p2p_links_count", 0), ("cpu_core_id_base", 64 * c), ("simd_id_base", 0),
+            ("max_waves_per_simd", 0), ("lds_size_in_kb", 0), ("gds_size_in_kb", 0), ("num_gws", 0),
+            ("wave_front_size", 0), ("array_count", 0), ("simd_arrays_per_engine", 0), ("cu_per_simd_array", 0),
+            ("simd_per_cu", 0), ("max_slots_scratch_cu", 0), ("gfx_target_version", 0), ("vendor_id", 0),
+            ("device_id", 0), ("location_id", 0), ("domain", 0), ("drm_render_minor", 0), ("hive_id", 0),
+            ("num_sdma_engines", 0), ("num_sdma_xgmi_engines", 0), ("num_sdma_queues_per_engine", 0),
+            ("num_cp_queues", 0), ("max_engine_clk_ccompute", 3700), ("local_mem_size", 0)]))
+        _w(nd / "name", "")
+        _w(nd / "gpu_id", "0")
+
+    gpu_compute = spec.per_gpu_compute or [spec.compute_partition] * spec.num_gpus
+    gpu_nodes: List[dict] = []
+    node_id = numa
+    render = 128
+    card = 1
+    xcp_counter = 0
+    for g in range(spec.num_gpus):
+        cp = gpu_compute[g].lower()
+        parts = PARTITIONS[cp]
+        bus = DEFAULT_BUSES[g] if g < len(DEFAULT_BUSES) else (0x10 + 8 * g) & 0xFF
+        bdf = f"0000:{bus:02x}:00.0"
+        uid = _unique_id(g)
+        hive = _hive_id(g // max(1, spec.hive_size)) if spec.hive_size > 0 else 0
+        numa_node = g * numa // spec.num_gpus
+        info.bdfs.append(bdf)
+        info.unique_ids.append(uid)
+        info.hive_ids.append(hive)
+        dev_dir = pci_root / bdf
+        _w(dev_dir / "vendor", "0x1002")
+        _w(dev_dir / "device", f"0x{spec.device_id:04x}")
+        _w(dev_dir / "numa_node", str(numa_node))
+        _w(dev_dir / "product_name", spec.product_name)
+        if spec.partition_support:
+            _w(dev_dir / "current_compute_partition", cp.upper())
+            _w(dev_dir / "current_memory_partition", spec.memory_partition.upper())
+            _w(dev_dir / "available_compute_partition", "SPX, DPX, QPX, CPX")
+            _w(dev_dir / "available_memory_partition", "NPS1, NPS2")
+        iommu = sysfs / "kernel/iommu_groups" / str(10 + g)
+        iommu.mkdir(parents=True, exist_ok=True)
+        _link(iommu, dev_dir / "iommu_group")
+        if spec.mode == "container":
+            _link(drv_amdgpu, dev_dir / "driver")
+            _link(dev_dir, drv_amdgpu / bdf)
+        _link(dev_dir, sysfs / "bus/pci/devices" / bdf)
+        for p in range(parts):
+            if spec.mode != "container":
+                break
+            if p == 0:
+                owner = dev_dir
+                dev_name = bdf
+            else:
+                xcp_idx = 8 * g + p
+                owner = sysfs / "devices/platform" / f"amdgpu_xcp_{xcp_idx}"
+                dev_name = f"amdgpu_xcp_{xcp_idx}"
+                xcp_counter += 1
+            (owner / "drm" / f"card{card}").mkdir(parents=True, exist_ok=True)
+            (owner / "drm" / f"renderD{render}").mkdir(parents=True, exist_ok=True)
+            _link(owner, sysfs / "class/drm" / f"card{card}" / "device")
+            _link(owner, sysfs / "class/drm" / f"renderD{render}" / "device")
+            if p > 0:
+                # the platform device is not a PCI function; labeller reads through it
+                _w(owner / "vendor", "0x1002")
+                _w(owner / "device", f"0x{spec.device_id:04x}")
+                _w(owner / "product_name", spec.product_name)
+                _link(drv_amdgpu, owner / "driver")
+            _w(dev / "dri" / f"card{card}", "")
+            _w(dev / "dri" / f"renderD{render}", "")
+            info.device_ids.append(dev_name)
+            info.render_minors[dev_name] = render
+            info.node_ids[dev_name] = node_id
+            gpu_nodes.append(dict(node=node_id, gpu=g, part=p, parts=parts, bus=bus, uid=uid, hive=hive,
+                                  numa=numa_node, render=render))
+            node_id += 1
+            render += 1
+            card += 1
+
+    # kfd GPU nodes
+    by_node = {n["node"]: n for n in gpu_nodes}
+    for n in gpu_nodes:
+        nd = nodes_dir / str(n["node"])
+        parts = n["parts"]
+        xcc = MI355X_XCDS // parts
+        io_links = [dict(type=2, to=n["numa"], weight=20, bw_min=0, bw_max=64000)]
+        p2p_links = []
+        for m in gpu_nodes:
+            if m["node"] == n["node"]:
+                continue
+            if m["gpu"] == n["gpu"]:
+                io_links.append(dict(type=11, to=m["node"], weight=13, bw_min=819200, bw_max=819200))
+            elif m["hive"] == n["hive"] and n["hive"] != 0:
+                io_links.append(dict(type=11, to=m["node"], weight=15, bw_min=153600, bw_max=153600))
+            else:
+                p2p_links.append(dict(type=2, to=m["node"], weight=72, bw_min=0, bw_max=0))
+        vram = MI355X_VRAM // parts
+        if spec.memory_partition.lower() == "nps2" and parts == 1:
+            vram = MI355X_VRAM
+        props = [
+            ("cpu_cores_count", 0), ("simd_count", MI355X_CUS * 4 // parts), ("mem_banks_count", 1),
+            ("caches_count", 0), ("io_links_count", len(io_links)), ("p2p_links_count", len(p2p_links)),
+            ("cpu_core_id_base", 0), ("simd_id_base", 2147487744 + 8 * n["node"]), ("max_waves_per_simd", 8),
+            ("lds_size_in_kb", 160), ("gds_size_in_kb", 0), ("num_gws", 64), ("wave_front_size", 64),
+            ("array_count", 4 * xcc), ("simd_arrays_per_engine", 1), ("cu_per_simd_array", 8),
+            ("simd_per_cu", 4), ("max_slots_scratch_cu", 32), ("gfx_target_version", spec.gfx_target_version),
+            ("vendor_id", 4098), ("device_id", spec.device_id), ("location_id", (n["bus"] << 8) | n["part"]),
+            ("domain", 0), ("drm_render_minor", n["render"]), ("hive_id", n["hive"]),
+            ("num_sdma_engines", 2), ("num_sdma_xgmi_engines", 6 if n["hive"] else 0),
+            ("num_sdma_queues_per_engine", 8), ("num_cp_queues", 24), ("max_engine_clk_fcompute", 2400),
+            ("local_mem_size", 0), ("fw_version", 200), ("capability", 2893521536), ("debug_prop", 1511),
+            ("sdma_fw_version", 24), ("unique_id", n["uid"]), ("num_xcc", xcc), ("max_engine_clk_ccompute", 3700)]
+        _w(nd / "properties", _props(props))
+        _w(nd / "name", "gfx950")
+        _w(nd / "gpu_id", str(40000 + n["node"]))
+        for i, l in enumerate(io_links):
+            _w(nd / "io_links" / str(i) / "properties", _props([
+                ("type", l["type"]), ("version_major", 0), ("version_minor", 0), ("node_from", n["node"]),
+                ("node_to", l["to"]), ("weight", l["weight"]), ("min_latency", 0), ("max_latency", 0),
+                ("min_bandwidth", l["bw_min"]), ("max_bandwidth", l["bw_max"]), ("recommended_transfer_size", 0),
+                ("recommended_sdma_engine_id_mask", 3), ("flags", 1)]))
+        for i, l in enumerate(p2p_links):
+            _w(nd / "p2p_links" / str(i) / "properties", _props([
+                ("type", l["type"]), ("version_major", 0), ("version_minor", 0), ("node_from", n["node"]),
+                ("node_to", l["to"]), ("weight", l["weight"]), ("min_latency", 0), ("max_latency", 0),
+                ("min_bandwidth", 0), ("max_bandwidth", 0), ("recommended_transfer_size", 0),
+                ("recommended_sdma_engine_id_mask", 0), ("flags", 3)]))
+        _w(nd / "mem_banks/0/properties", _props([
+            ("heap_type", 1), ("size_in_bytes", vram), ("flags", 0), ("width", 8192), ("mem_clk_max", 1900)]))
+    del by_node
+
+    if spec.mode == "vf":
+        drv_gim = sysfs / "bus/pci/drivers/gim"
+        drv_gim.mkdir(parents=True, exist_ok=True)
+        _w(sysfs / "module/gim/version", "8.1.0.K+ddfa1e2")
+        _w(sysfs / "module/gim/srcversion", "F00DFACE0123456789ABCDE")
+        dev_vfio = dev / "vfio"
+        dev_vfio.mkdir(parents=True, exist_ok=True)
+        _w(dev_vfio / "vfio", "")
+        info.device_ids = []
+        for g, bdf in enumerate(info.bdfs):
+            pf_dir = pci_root / bdf
+            _link(drv_gim, pf_dir / "driver")
+            for v in range(spec.vfs_per_gpu):
+                bus = int(bdf.split(":")[1], 16)
+                vf_bdf = f"0000:{bus:02x}:02.{v}"
+                vf_dir = pci_root / vf_bdf
+                _w(vf_dir / "vendor", "0x1002")
+                _w(vf_dir / "device", f"0x{MI355X_VF_DEVICE_ID:04x}")
+                grp = 100 + g * spec.vfs_per_gpu + v
+                iommu = sysfs / "kernel/iommu_groups" / str(grp)
+                iommu.mkdir(parents=True, exist_ok=True)
+                _link(iommu, vf_dir / "iommu_group")
+                _link(vf_dir, pf_dir / f"virtfn{v}")
+                _link(vf_dir, sysfs / "bus/pci/devices" / vf_bdf)
+                _w(dev_vfio / str(grp), "")
+                info.device_ids.append(str(grp))
+    elif spec.mode == "pf":
+        drv_vfio = sysfs / "bus/pci/drivers/vfio-pci"
+        drv_vfio.mkdir(parents=True, exist_ok=True)
+        dev_vfio = dev / "vfio"
+        dev_vfio.mkdir(parents=True, exist_ok=True)
+        _w(dev_vfio / "vfio", "")
+        info.device_ids = []
+        for g, bdf in enumerate(info.bdfs):
+            _link(drv_vfio, pci_root / bdf / "driver")
+            _w(dev_vfio / str(10 + g), "")
+            info.device_ids.append(str(10 + g))
+    return info
+
+
+def make_single_gpu_node(root: os.PathLike, **kw) -> FixtureInfo:
+    kw.setdefault("num_gpus", 1)
+    kw.setdefault("numa_nodes", 1)
+    return make_mi355x_node(root, **kw)

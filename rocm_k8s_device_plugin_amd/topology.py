@@ -1,0 +1,184 @@
+"""Node GPU inventory: immutable snapshots over the native discovery.
+
+``discover()`` is the Python face of the C++ ``discover_gpus`` (reference
+GetAMDGPUs, internal/pkg/amdgpu/amdgpu.go:448-568). Snapshots are frozen
+dataclasses: health updates build new device lists instead of mutating shared
+objects, which removes the reference's data race between UpdateHealth and
+concurrent RPCs.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from .ops.native import core
+
+
+@dataclass(frozen=True)
+class Gpu:
+    id: str
+    bdf: str
+    is_partition: bool
+    xcp_index: int
+    card: int
+    render_minor: int
+    unique_id: str
+    compute_partition: str
+    memory_partition: str
+    numa_node: int
+    node_id: int
+    gfx_target_version: int = 0
+    simd_count: int = 0
+    simd_per_cu: int = 0
+    num_xcc: int = 0
+    pci_device_id: int = 0
+    location_id: int = 0
+    domain: int = 0
+    hive_id: int = 0
+    vram_bytes: int = 0
+
+    @property
+    def partition_type(self) -> str:
+        if not self.compute_partition or not self.memory_partition:
+            return ""
+        return f"{self.compute_partition}_{self.memory_partition}"
+
+    @property
+    def cu_count(self) -> int:
+        return self.simd_count // self.simd_per_cu if self.simd_per_cu else 0
+
+    @property
+    def is_gfx950(self) -> bool:
+        return self.gfx_target_version == 90500
+
+    def dev_paths(self) -> List[str]:
+        """/dev nodes a container needs for this device: card then renderD
+        (fixed order; the reference's order depended on Go map iteration,
+        SURVEY Appendix B #13)."""
+        out = []
+        if self.card >= 0:
+            out.append(f"/dev/dri/card{self.card}")
+        if self.render_minor >= 0:
+            out.append(f"/dev/dri/renderD{self.render_minor}")
+        return out
+
+    @classmethod
+    def from_native(cls, g) -> "Gpu":
+        return cls(id=g.id, bdf=g.bdf, is_partition=g.is_partition, xcp_index=g.xcp_index, card=g.card,
+                   render_minor=g.render_minor, unique_id=g.unique_id, compute_partition=g.compute_partition,
+                   memory_partition=g.memory_partition, numa_node=g.numa_node, node_id=g.node_id,
+                   gfx_target_version=g.gfx_target_version, simd_count=g.simd_count, simd_per_cu=g.simd_per_cu,
+                   num_xcc=g.num_xcc, pci_device_id=g.pci_device_id, location_id=g.location_id, domain=g.domain,
+                   hive_id=g.hive_id, vram_bytes=g.vram_bytes)
+
+
+@dataclass
+class Inventory:
+    sysfs_root: str
+    devices: Tuple[Gpu, ...]
+    topology: object  # native KfdTopology
+    driver_loaded: bool
+    kfd_present: bool
+    warnings: List[str] = field(default_factory=list)
+
+    def __post_init__(self):
+        self.by_id: Dict[str, Gpu] = {d.id: d for d in self.devices}
+
+    def __len__(self) -> int:
+        return len(self.devices)
+
+    def partition_counts(self) -> Dict[str, int]:
+        out: Dict[str, int] = {}
+        for d in self.devices:
+            t = d.partition_type
+            if t:
+                out[t] = out.get(t, 0) + 1
+        return out
+
+    @property
+    def homogeneous(self) -> bool:
+        return len(self.partition_counts()) <= 1
+
+    def physical_gpus(self) -> Dict[str, List[Gpu]]:
+        """unique_id -> devices (partitions) of that physical GPU, in device order."""
+        out: Dict[str, List[Gpu]] = {}
+        for d in self.devices:
+            out.setdefault(d.unique_id, []).append(d)
+        return out
+
+    def hives(self) -> Dict[int, List[str]]:
+        out: Dict[int, List[str]] = {}
+        for d in self.devices:
+            out.setdefault(d.hive_id, []).append(d.id)
+        return out
+
+    def compute_partition_supported(self) -> bool:
+        return core().compute_partition_supported(self.sysfs_root)
+
+    def memory_partition_supported(self) -> bool:
+        return core().memory_partition_supported(self.sysfs_root)
+
+
+def _limit_physical(devs: List[Gpu], limit: Optional[int]) -> List[Gpu]:
+    """Keep the devices of the first `limit` physical GPUs (BDF order)."""
+    if limit is None or limit < 0:
+        return devs
+    keep = []
+    seen: List[str] = []
+    for d in devs:
+        if d.unique_id not in seen:
+            seen.append(d.unique_id)
+    allowed = set(seen[:limit])
+    for d in devs:
+        if d.unique_id in allowed:
+            keep.append(d)
+    return keep
+
+
+def device_count_limit_from_env(env=None) -> Optional[int]:
+    """AMD_GPU_DEVICE_COUNT: documented by the reference
+    (docs/user-guide/configuration.md:11) but never implemented there; here it
+    caps the number of advertised physical GPUs."""
+    env = os.environ if env is None else env
+    v = env.get("AMD_GPU_DEVICE_COUNT", "").strip()
+    if not v:
+        return None
+    try:
+        n = int(v)
+    except ValueError:
+        return None
+    return n if n >= 0 else None
+
+
+def discover(sysfs_root: str = "/sys", device_count_limit: Optional[int] = None) -> Inventory:
+    n = core()
+    topo = n.KfdTopology.load_sysfs(sysfs_root)
+    res = n.discover_gpus_with(sysfs_root, topo)
+    devs = [Gpu.from_native(g) for g in res.devices]
+    devs = _limit_physical(devs, device_count_limit)
+    return Inventory(sysfs_root=sysfs_root, devices=tuple(devs), topology=topo, driver_loaded=res.driver_loaded,
+                     kfd_present=res.kfd_present, warnings=list(res.warnings))
+
+
+def hip_ordinals(inv: Inventory, dev_root: str = "/dev", check_access: bool = True) -> Dict[str, int]:
+    """kubelet device ID -> ROCr/HIP ordinal on this host (all devices visible).
+
+    ROCr enumerates GPU agents in kfd node order and skips render nodes it
+    cannot open, so the ordinal of a device is its position among accessible
+    GPU nodes sorted by kfd node id. In CPX mode every partition is its own
+    agent and gets its own ordinal.
+    """
+    gpu_nodes = []
+    for nid in inv.topology.gpu_node_ids():
+        node = inv.topology.node(nid)
+        minor = node.drm_render_minor
+        if minor <= 0:
+            continue
+        if check_access and os.path.isdir(os.path.join(dev_root, "dri")):
+            p = os.path.join(dev_root, "dri", f"renderD{minor}")
+            if not os.access(p, os.R_OK | os.W_OK):
+                continue
+        gpu_nodes.append(nid)
+    pos = {nid: i for i, nid in enumerate(gpu_nodes)}
+    return {d.id: pos[d.node_id] for d in inv.devices if d.node_id in pos}

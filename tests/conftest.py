@@ -1,0 +1,51 @@
+import asyncio
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+if str(REPO) not in sys.path:
+    sys.path.insert(0, str(REPO))
+
+REF_TESTDATA = Path("/root/reference/testdata")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
+    config.addinivalue_line("markers", "slow: takes more than a few seconds")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _native_built():
+    """Build the native core once per session (no-op when up to date)."""
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=None)
+    yield
+
+
+@pytest.fixture
+def ref_testdata():
+    if not REF_TESTDATA.exists():
+        pytest.skip("reference testdata not mounted")
+    return REF_TESTDATA
+
+
+@pytest.fixture
+def mi355x_node(tmp_path):
+    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+    return make_mi355x_node(tmp_path / "node")
+
+
+def run(coro, timeout=60):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+@pytest.fixture
+def arun():
+    return run
+
+
+def has_gpu() -> bool:
+    return os.path.exists("/dev/kfd")

@@ -1,0 +1,213 @@
+"""Allocator behavioural contract.
+
+Every expectation of the reference's TestBestPolicyAllocator
+(internal/pkg/allocator/besteffort_policy_test.go:25-216) on its own kfd
+fixtures, plus: exact search == the reference's ordered BFS (same set, same
+order, same weight) on every size, optimality against brute force, hive
+packing, determinism, and the error strings.
+"""
+import itertools
+import random
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.allocator import AllocationError, BestEffortPolicy, load_topology
+
+
+def synthetic_devices(dev_count, parts, numa_count, start, end):
+    """Same shape as the reference's getTestDevices (device_test.go:43-67)."""
+    out = []
+    node = start
+    per_numa = dev_count // numa_count
+    for i in range(dev_count):
+        for j in range(parts):
+            if node > end:
+                break
+            dev_id = f"test{i + 1}" if j == 0 else f"amdgpu_xcp_{i * 8 + j}"
+            out.append((dev_id, node, i // per_numa, str(i)))
+            node += 1
+    return out
+
+
+TOPOS = {
+    "mi308": dict(dev_count=4, parts=8, numa=2, start=2, end=33, path="topology-parsing-mi308/topology/nodes"),
+    "mi210": dict(dev_count=8, parts=1, numa=2, start=2, end=9, path="topo-mi210-xgmi-pcie/nodes"),
+    "mi300cpx": dict(dev_count=8, parts=8, numa=2, start=2, end=64, path="topo-mi300-cpx/topology/nodes"),
+}
+
+# (topology, size, available or None, required, filtered-out, expected or None) — besteffort_policy_test.go:54-159
+CASES = [
+    ("mi308", 1, None, [], [], None),
+    ("mi308", 3, None, [], [], None),
+    ("mi308", 12, None, [], [], None),
+    ("mi210", 1, None, [], [], ["test1"]),
+    ("mi210", 3, None, [], [], ["test1", "test2", "test3"]),
+    ("mi210", 5, None, [], [], ["test1", "test2", "test3", "test4", "test5"]),
+    ("mi210", 3, ["test3", "test4", "test5", "test6", "test7", "test8"], [], [], ["test5", "test6", "test7"]),
+    ("mi300cpx", 1, None, [], [], ["test8"]),
+    ("mi300cpx", 3, None, [], [], ["test8", "amdgpu_xcp_57", "amdgpu_xcp_58"]),
+    ("mi300cpx", 5, None, [], [], ["test8", "amdgpu_xcp_57", "amdgpu_xcp_58", "amdgpu_xcp_59", "amdgpu_xcp_60"]),
+    ("mi300cpx", 3, ["test3", "test4", "test5", "test6", "test7", "test8"], [], [], ["test5", "test6", "test7"]),
+    ("mi300cpx", 3, ["test3", "test4", "test5", "test6", "test7", "test8"], ["test5"], [],
+     ["test5", "test6", "test7"]),
+    ("mi300cpx", 30, None, [], [], None),
+    ("mi300cpx", 8, None, [], [], ["test1"] + [f"amdgpu_xcp_{i}" for i in range(1, 8)]),
+    ("mi300cpx", 7, None, [], [], ["test8"] + [f"amdgpu_xcp_{i}" for i in range(57, 63)]),
+    ("mi300cpx", 4, None, [], ["test8", "amdgpu_xcp_57", "amdgpu_xcp_58"],
+     [f"amdgpu_xcp_{i}" for i in range(59, 63)]),
+    ("mi300cpx", 10, None, [], ["test1", "test2", "test3", "test4", "test8", "amdgpu_xcp_57"],
+     ["test5"] + [f"amdgpu_xcp_{i}" for i in range(33, 40)] + ["amdgpu_xcp_58", "amdgpu_xcp_59"]),
+]
+
+
+def make_policy(ref, name, **opts):
+    t = TOPOS[name]
+    devs = synthetic_devices(t["dev_count"], t["parts"], t["numa"], t["start"], t["end"])
+    pol = BestEffortPolicy(**opts)
+    pol.init(devs, load_topology(nodes_dir=str(ref / t["path"])))
+    return pol, [d[0] for d in devs]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-k{c[1]}")
+@pytest.mark.parametrize("reference_weights", [False, True], ids=["hive-aware", "reference-weights"])
+def test_reference_contract(ref_testdata, case, reference_weights):
+    name, size, avail, req, filt, expected = case
+    opts = dict(missing_pair_is_worst=False, cross_hive_penalty=0) if reference_weights else {}
+    pol, all_ids = make_policy(ref_testdata, name, **opts)
+    av = list(avail) if avail else list(all_ids)
+    av = [a for a in av if a not in filt]
+    res = pol.allocate(av, req, size)
+    assert len(res) == size
+    for r in req:
+        assert r in res
+    if expected:
+        assert sorted(res) == sorted(expected)
+
+
+@pytest.mark.parametrize("name", list(TOPOS))
+def test_exact_search_matches_reference_bfs(ref_testdata, name):
+    """Same chosen set, order and weight as the reference's ordered BFS on the same weights."""
+    pol, ids = make_policy(ref_testdata, name)
+    maxk = len(ids)
+    ks = range(1, maxk) if name != "mi210" else range(1, 8)
+    for k in ks:
+        if name == "mi300cpx" and k > 40:
+            break
+        ours = pol.explain(ids, [], k)
+        ref = pol.reference_allocate(ids, [], k)
+        assert ours["error"] == ref["error"] == ""
+        assert ours["weight"] == ref["weight"], k
+        assert ours["ids"] == ref["ids"], k
+        # the set search scores far fewer candidates than the ordered enumeration
+        assert ours["candidates"] <= max(ref["candidates"], 64)
+
+
+def test_candidate_counts_reference_bfs(ref_testdata):
+    """Reference enumeration counts from the survey (§6.2): 8!/(8-k)! on MI210."""
+    pol, ids = make_policy(ref_testdata, "mi210")
+    for k, n in [(1, 8), (2, 56), (3, 336), (4, 1680), (5, 6720)]:
+        assert pol.reference_allocate(ids, [], k)["candidates"] == n
+
+
+def test_pair_weights_from_kfd(ref_testdata):
+    pol, ids = make_policy(ref_testdata, "mi308")
+    nat = pol.native
+    # reference TestPairWeightsCalculation expects 31 'from' keys
+    assert nat.num_from_keys == 31
+    assert nat.num_groups == 4  # TestGroupPartitionsByDevId
+    pol2, _ = make_policy(ref_testdata, "mi210")
+    # same hive xGMI pair: 20 (diff GPU) + 10 (xgmi) + 10 (same numa)
+    assert pol2.native.link_type("test1", "test2") == 11
+    assert pol2.native.pair_weight("test1", "test2") == 40
+    # cross hive pcie + different numa + hive penalty
+    assert pol2.native.link_type("test1", "test5") == 2
+    assert pol2.native.pair_weight("test1", "test5") == 20 + 40 + 20 + 100
+
+
+def test_errors(ref_testdata):
+    pol, ids = make_policy(ref_testdata, "mi210")
+    with pytest.raises(AllocationError, match="allocation size can not be negative"):
+        pol.allocate(ids, [], 0)
+    with pytest.raises(AllocationError, match="available devices count less than allocation size"):
+        pol.allocate(ids[:2], [], 3)
+    with pytest.raises(AllocationError, match="must_include devices size is more than allocation size"):
+        pol.allocate(ids, ids[:3], 2)
+    with pytest.raises(AllocationError, match="No candidate subset found"):
+        pol.allocate(ids[:4], ["test8"], 2)
+    with pytest.raises(AllocationError, match="unknown device ID"):
+        pol.allocate(ids + ["bogus"], [], 2)
+    # short-circuits
+    assert pol.allocate(ids[:3], [], 3) == ids[:3]
+    assert pol.allocate(ids, ["test2", "test7"], 2) == ["test2", "test7"]
+    fresh = BestEffortPolicy()
+    with pytest.raises(AllocationError):
+        fresh.init([], load_topology(nodes_dir=str(ref_testdata / TOPOS["mi210"]["path"])))
+    with pytest.raises(AllocationError, match="Init method must be called"):
+        fresh.allocate(["a", "b"], [], 1)
+
+
+def _brute_force(pol, ids, required, k):
+    nat = pol.native
+    best = None
+    rest = [i for i in ids if i not in required]
+    for combo in itertools.combinations(rest, k - len(required)):
+        s = list(combo) + list(required)
+        w = sum(nat.pair_weight(a, b) for a, b in itertools.combinations(s, 2))
+        if best is None or w < best:
+            best = w
+    return best
+
+
+def test_never_worse_than_any_whole_gpu_subset_mi210(ref_testdata):
+    """On whole GPUs the candidate family covers every subset: result is the global optimum."""
+    pol, ids = make_policy(ref_testdata, "mi210")
+    rng = random.Random(7)
+    for _ in range(40):
+        av = rng.sample(ids, rng.randint(2, 8))
+        k = rng.randint(1, len(av))
+        req = rng.sample(av, rng.randint(0, min(2, k)))
+        r = pol.explain(av, req, k)
+        if r["short_circuit"]:
+            continue
+        assert r["weight"] == _brute_force(pol, av, req, k)
+
+
+def test_hive_packing_mi210(ref_testdata):
+    """A request that fits in one xGMI hive never straddles both."""
+    pol, ids = make_policy(ref_testdata, "mi210")
+    hive_a, hive_b = set(ids[:4]), set(ids[4:])
+    rng = random.Random(3)
+    for _ in range(50):
+        av = rng.sample(ids, rng.randint(3, 8))
+        k = rng.randint(2, 4)
+        if len(av) <= k:
+            continue
+        fits = len(hive_a & set(av)) >= k or len(hive_b & set(av)) >= k
+        res = set(pol.allocate(av, [], k))
+        if fits:
+            assert res <= hive_a or res <= hive_b, (av, k, res)
+
+
+def test_deterministic(ref_testdata):
+    pol, ids = make_policy(ref_testdata, "mi300cpx")
+    first = [pol.allocate(ids, [], k) for k in (1, 5, 9, 17)]
+    for _ in range(3):
+        pol2, _ = make_policy(ref_testdata, "mi300cpx")
+        assert [pol2.allocate(ids, [], k) for k in (1, 5, 9, 17)] == first
+
+
+def test_mi355x_fixture_cpx(tmp_path):
+    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+    from rocm_k8s_device_plugin_amd.topology import discover
+    fi = make_mi355x_node(tmp_path, compute_partition="cpx")
+    inv = discover(str(fi.sysfs))
+    pol = BestEffortPolicy()
+    pol.init(inv.devices, inv.topology)
+    ids = [d.id for d in inv.devices]
+    # 8 partitions = one whole physical GPU
+    r = pol.allocate(ids, [], 8)
+    assert len({inv.by_id[i].unique_id for i in r}) == 1
+    # 12 = one GPU + 4 partitions of a second on the same NUMA node
+    r = pol.allocate(ids, [], 12)
+    assert len({inv.by_id[i].unique_id for i in r}) == 2
+    assert len({inv.by_id[i].numa_node for i in r}) == 1
