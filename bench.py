@@ -50,6 +50,10 @@ def parse_args():
     ap.add_argument("--fixture", action="store_true",
                     help="CPU-only: synthetic 8x MI355X sysfs, containers are no-op processes")
     ap.add_argument("--container-timeout", type=float, default=120.0)
+    ap.add_argument("--container-runtime", default="hsa", choices=["hsa", "hip"],
+                    help="how the container entrypoint reaches the GPU: ROCr-direct or the HIP runtime")
+    ap.add_argument("--hip-compare", type=int, default=5,
+                    help="extra untimed admissions with HIP-runtime containers, reported for comparison")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -177,8 +181,9 @@ def main():
         gpu_info = None
 
     rpc_ms, alloc_rpc_ms, lat_ms, ready_ms, kern_us = [], [], [], [], []
+    exec_ms, rt_ms, dev_ms = [], [], []
 
-    def one_step(record: bool):
+    def one_step(record: bool, runtime: str = args.container_runtime, sink=None):
         nonlocal step_payload
         if d.rank == 0:
             t0 = time.monotonic_ns()
@@ -194,25 +199,34 @@ def main():
             import subprocess
             ts = time.monotonic_ns()
             subprocess.run(["/bin/true"])
-            mine = (True, time.monotonic_ns(), 0.0, "")
+            tr = time.monotonic_ns()
+            mine = (True, tr, 0.0, "", (ts, ts, tr))
         else:
             mine_ord = [ordl[d.rank]] if d.world > 1 else ordl
-            r = start_container(mine_ord, timeout_s=args.container_timeout)
+            r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
-            mine = (r.ok, r.t_ready_ns, kus, r.error)
+            phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
+            mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
         allr = d.gather(mine)
-        bad = [e for ok, _, _, e in allr if not ok]
+        bad = [m[3] for m in allr if not m[0]]
         if bad:
             raise SystemExit(f"container failed to become ready: {bad[0]}")
-        t_ready = max(t for _, t, _, _ in allr)
+        slowest = max(allr, key=lambda m: m[1])
+        t_ready = slowest[1]
         if d.rank == 0:
             kubelet.release("amd.com/gpu", ids)
+        if sink is not None:
+            sink.append((t_ready - t0) / 1e6)
         if record:
             lat_ms.append((t_ready - t0) / 1e6)
             rpc_ms.append(tot)
             alloc_rpc_ms.append(amsl)
             ready_ms.append((t_ready - t0) / 1e6 - tot)
-            kern_us.append(max(k for _, _, k, _ in allr))
+            kern_us.append(max(m[2] for m in allr))
+            sp, tm, trt = slowest[4]
+            exec_ms.append((tm - sp) / 1e6)
+            rt_ms.append((trt - tm) / 1e6)
+            dev_ms.append((t_ready - trt) / 1e6)
 
     for _ in range(args.warmup):
         one_step(False)
@@ -223,6 +237,10 @@ def main():
     d.sync()
     elapsed = time.perf_counter() - t_start
     elapsed = d.max(elapsed)
+    hip_lat = []
+    if not args.fixture and args.container_runtime == "hsa":
+        for _ in range(args.hip_compare):
+            one_step(False, runtime="hip", sink=hip_lat)
 
     extra = {}
     if d.rank == 0:
@@ -241,7 +259,12 @@ def main():
                  "allocate_rpc_p50_ms": round(pct(alloc_rpc_ms, .5), 4),
                  "container_start_to_ready_p50_ms": round(pct(ready_ms, .5), 3),
                  "latency_p99_ms": round(pct(lat_ms, .99), 3), "latency_mean_ms": round(statistics.mean(lat_ms), 3),
+                 "container_runtime": args.container_runtime,
+                 "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
                  "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
+                 "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
+                                             "hip_runtime_init": round(pct(rt_ms, .5), 3),
+                                             "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
                  "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
                  "reference_algorithm_candidates": ref["candidates"], "gpus": gpu_info}
         loop.run_until_complete(kubelet.stop())

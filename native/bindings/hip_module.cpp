@@ -1,6 +1,6 @@
-// pybind11 bindings for the in-process liveness probe (_hip). Compiled with
-// hipcc and linked against the gfx950 kernel object; importing it loads the
-// HIP runtime, so the control plane never imports it — only GPU tests and
+// pybind11 bindings for the in-process liveness probe (_hip): the HIP launch
+// path and the HSA-direct path over the same gfx950 kernel. Importing it loads
+// the GPU runtimes, so the control plane never imports it — only GPU tests and
 // smoke() do. The plugin itself runs the probe executable in a child process.
 #include <pybind11/pybind11.h>
 
@@ -20,6 +20,10 @@ py::dict to_dict(const mi355x_probe_result& r) {
   d["xcc_id"] = r.xcc_id;
   d["hw_id"] = r.hw_id;
   d["iters"] = r.iters;
+  d["dispatches"] = r.dispatches;
+  d["kfd_node_id"] = r.kfd_node_id;
+  d["runtime"] = std::string(r.runtime);
+  d["setup_us"] = r.setup_us;
   d["kernel_us"] = r.kernel_us;
   d["total_us"] = r.total_us;
   d["pci_bus_id"] = std::string(r.pci_bus_id);
@@ -65,6 +69,37 @@ PYBIND11_MODULE(_hip, m) {
         {
           py::gil_scoped_release nogil;
           mi355x_probe_identify(ordinal, &r);
+        }
+        return to_dict(r);
+      },
+      py::arg("ordinal") = 0);
+  // HSA-direct path (same code object, one AQL dispatch, no HIP runtime involvement)
+  m.def("hsa_device_count", [] {
+    int n;
+    {
+      py::gil_scoped_release nogil;
+      n = mi355x_hsa_probe_init();
+    }
+    return n;
+  });
+  m.def(
+      "hsa_probe",
+      [](int ordinal, uint32_t nonce, int iters, double timeout_s) {
+        mi355x_probe_result r;
+        {
+          py::gil_scoped_release nogil;
+          mi355x_hsa_probe_device(ordinal, nonce, iters, timeout_s, &r);
+        }
+        return to_dict(r);
+      },
+      py::arg("ordinal") = 0, py::arg("nonce") = 12345u, py::arg("iters") = 4, py::arg("timeout_s") = 5.0);
+  m.def(
+      "hsa_identify",
+      [](int ordinal) {
+        mi355x_probe_result r;
+        {
+          py::gil_scoped_release nogil;
+          mi355x_hsa_probe_identify(ordinal, &r);
         }
         return to_dict(r);
       },

@@ -1,13 +1,13 @@
 // Host side of the per-device MFMA liveness probe.
 //
-// Used three ways:
-//   * `mi355x-liveness-probe` executable — what the device plugin's health
-//     loop runs in a child process per sweep, under a hard deadline, so a
-//     wedged GPU can never block ListAndWatch and no HIP context is held on
-//     devices that pods own;
-//   * the same executable is the "container entrypoint" of the
-//     Allocate->ContainerReady benchmark;
-//   * the `_hip` Python extension, for in-process GPU tests and smoke().
+// Two launch paths for the same gfx950 code object:
+//   * HSA-direct (mi355x_hsa_*): ROCr only, code object loaded from the
+//     embedded .hsaco, one AQL kernel-dispatch packet on a private queue,
+//     output in fine-grained host memory — exactly one dispatch per probe and
+//     no HIP runtime start-up cost. This is what the plugin's health loop and
+//     the benchmark's container entrypoint run by default.
+//   * HIP (mi355x_probe_*): the same kernel through the HIP runtime, for the
+//     in-process `_hip` extension and as a cross-check.
 #pragma once
 
 #include <stdint.h>
@@ -17,33 +17,42 @@ extern "C" {
 #endif
 
 typedef struct {
-  int ordinal;            // HIP device ordinal probed
-  int ok;                 // 1 = tile bit-exact, nonce echoed, no HIP error
-  int hip_error;          // first hipError_t seen (0 = none)
+  int ordinal;            // HIP / HSA GPU agent ordinal probed
+  int ok;                 // 1 = tile bit-exact, nonce echoed, no runtime error
+  int hip_error;          // first hipError_t / hsa_status_t seen (0 = none)
   int mismatches;         // elements differing from the host reference
   uint32_t nonce;
   uint32_t xcc_id;        // HW_REG_XCC_ID of the wave that ran
   uint32_t hw_id;
   int iters;
-  double kernel_us;       // hipEvent-timed dispatch
-  double total_us;        // set-device + alloc + launch + copy-back + verify
-  char pci_bus_id[32];    // hipDeviceGetPCIBusId
-  char arch[64];          // gcnArchName, e.g. "gfx950:sramecc+:xnack-"
+  int dispatches;         // GPU dispatches issued by this probe
+  int kfd_node_id;        // kfd topology node of the agent (-1 if unknown)
+  double kernel_us;       // dispatch start->end (HSA profiling) or hipEvent time
+  double setup_us;        // code object load + queue/stream + buffers
+  double total_us;        // everything for this device, including verify
+  char runtime[8];        // "hsa" | "hip"
+  char pci_bus_id[32];    // dddd:bb:dd.f
+  char arch[64];          // e.g. "gfx950" / "gfx950:sramecc+:xnack-"
   char name[128];
-  char uuid[40];          // hex of hipDeviceProp_t.uuid
+  char uuid[40];
   int pci_domain, pci_bus, pci_device;
   int cu_count;
   uint64_t total_mem;
   char error[160];
 } mi355x_probe_result;
 
-// Number of HIP devices, or -hipError on failure.
+// ---- HIP path -------------------------------------------------------------
 int mi355x_probe_device_count(void);
-// Probe one device. Returns 0 if the device is live, non-zero otherwise
-// (details in *out).
 int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355x_probe_result* out);
-// Fill only the identity fields (bus id, uuid, arch) without launching.
 int mi355x_probe_identify(int ordinal, mi355x_probe_result* out);
+
+// ---- HSA-direct path ------------------------------------------------------
+// hsa_init + GPU agent enumeration; returns the number of GPU agents or
+// -hsa_status_t. Idempotent.
+int mi355x_hsa_probe_init(void);
+int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, double timeout_s, mi355x_probe_result* out);
+int mi355x_hsa_probe_identify(int ordinal, mi355x_probe_result* out);
+void mi355x_hsa_probe_shutdown(void);
 
 #ifdef __cplusplus
 }

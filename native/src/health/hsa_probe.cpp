@@ -1,0 +1,348 @@
+// HSA-direct launcher for the gfx950 MFMA liveness kernel.
+//
+// The HIP runtime costs ~170 ms of start-up before the first kernel can run
+// (measured on MI355X, profiles/round1_container_ready.md), which is pure
+// overhead for a 2.4 us liveness dispatch that the plugin runs on every
+// device every pulse. This path talks to ROCr directly:
+//
+//   hsa_init -> GPU agents (ROCR_VISIBLE_DEVICES honoured)
+//   code object: the embedded liveness_gfx950.hsaco -> executable -> kernel object
+//   AQL kernel-dispatch packet on a private queue, completion signal,
+//   dispatch timestamps from hsa_amd_profiling
+//   outputs in fine-grained system memory (host reads them directly),
+//   scratch in the device's coarse-grained HBM pool.
+//
+// Exactly one dispatch per probe; the agent's kfd node id comes from
+// HSA_AMD_AGENT_INFO_DRIVER_NODE_ID, so the verdict maps to the kubelet
+// device ID without guessing.
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "liveness_kernel.h"
+#include "mi355x/liveness_probe.h"
+#include "probe_verify.h"
+
+// The gfx950 code object, embedded at build time.
+extern "C" const unsigned char mi355x_hsaco_start[];
+extern "C" const unsigned char mi355x_hsaco_end[];
+#ifndef MI355X_HSACO_PATH
+#error "MI355X_HSACO_PATH must name the gfx950 code object to embed"
+#endif
+asm(".section .rodata.mi355x_hsaco,\"a\",@progbits\n"
+    ".p2align 12\n"
+    ".globl mi355x_hsaco_start\n"
+    "mi355x_hsaco_start:\n"
+    ".incbin \"" MI355X_HSACO_PATH "\"\n"
+    ".globl mi355x_hsaco_end\n"
+    "mi355x_hsaco_end:\n"
+    ".byte 0\n"
+    ".previous\n");
+
+namespace {
+
+struct Agent {
+  hsa_agent_t agent{};
+  hsa_amd_memory_pool_t coarse{};  // device HBM
+  bool has_coarse = false;
+};
+
+struct Runtime {
+  std::mutex mu;
+  bool inited = false;
+  hsa_status_t init_status = HSA_STATUS_SUCCESS;
+  std::vector<Agent> gpus;
+  hsa_agent_t cpu{};
+  hsa_amd_memory_pool_t kernarg{};
+  hsa_amd_memory_pool_t fine{};
+  bool has_kernarg = false, has_fine = false;
+  uint64_t ts_freq = 0;
+} g_rt;
+
+hsa_status_t collect_agent(hsa_agent_t a, void*) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_GPU) {
+    Agent ag;
+    ag.agent = a;
+    g_rt.gpus.push_back(ag);
+  } else if (t == HSA_DEVICE_TYPE_CPU && g_rt.cpu.handle == 0) {
+    g_rt.cpu = a;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t cpu_pool(hsa_amd_memory_pool_t p, void*) {
+  hsa_amd_segment_t seg;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT) && !g_rt.has_kernarg) {
+    g_rt.kernarg = p;
+    g_rt.has_kernarg = true;
+  }
+  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) && !g_rt.has_fine) {
+    g_rt.fine = p;
+    g_rt.has_fine = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t gpu_pool(hsa_amd_memory_pool_t p, void* data) {
+  auto* ag = static_cast<Agent*>(data);
+  hsa_amd_segment_t seg;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  bool alloc_ok = false;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc_ok);
+  if (alloc_ok && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && !ag->has_coarse) {
+    ag->coarse = p;
+    ag->has_coarse = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+void set_status(mi355x_probe_result* r, hsa_status_t s, const char* what) {
+  if (r->hip_error == 0) r->hip_error = static_cast<int>(s);
+  const char* msg = nullptr;
+  hsa_status_string(s, &msg);
+  std::snprintf(r->error, sizeof(r->error), "%s: %s", what, msg ? msg : "hsa error");
+}
+
+void fill_identity(const Agent& ag, int ordinal, mi355x_probe_result* out) {
+  out->ordinal = ordinal;
+  std::snprintf(out->runtime, sizeof(out->runtime), "hsa");
+  char name[64] = {0};
+  hsa_agent_get_info(ag.agent, HSA_AGENT_INFO_NAME, name);
+  std::snprintf(out->arch, sizeof(out->arch), "%s", name);
+  char product[64] = {0};
+  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_PRODUCT_NAME), product);
+  std::snprintf(out->name, sizeof(out->name), "%s", product);
+  uint32_t node = 0, bdf = 0, domain = 0, cus = 0;
+  if (hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DRIVER_NODE_ID), &node) ==
+      HSA_STATUS_SUCCESS)
+    out->kfd_node_id = static_cast<int>(node);
+  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &domain);
+  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cus);
+  out->pci_domain = static_cast<int>(domain);
+  out->pci_bus = static_cast<int>((bdf >> 8) & 0xFF);
+  out->pci_device = static_cast<int>((bdf >> 3) & 0x1F);
+  out->cu_count = static_cast<int>(cus);
+  std::snprintf(out->pci_bus_id, sizeof(out->pci_bus_id), "%04x:%02x:%02x.%x", domain, (bdf >> 8) & 0xFF,
+                (bdf >> 3) & 0x1F, bdf & 0x7);
+  char uuid[24] = {0};
+  if (hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_UUID), uuid) ==
+      HSA_STATUS_SUCCESS)
+    std::snprintf(out->uuid, sizeof(out->uuid), "%s", uuid);
+  if (ag.has_coarse) {
+    size_t sz = 0;
+    hsa_amd_memory_pool_get_info(ag.coarse, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz);
+    out->total_mem = sz;
+  }
+}
+
+}  // namespace
+
+extern "C" int mi355x_hsa_probe_init(void) {
+  std::lock_guard<std::mutex> lk(g_rt.mu);
+  if (g_rt.inited) return g_rt.init_status == HSA_STATUS_SUCCESS ? static_cast<int>(g_rt.gpus.size())
+                                                                  : -static_cast<int>(g_rt.init_status);
+  g_rt.inited = true;
+  hsa_status_t s = hsa_init();
+  if (s != HSA_STATUS_SUCCESS) {
+    g_rt.init_status = s;
+    return -static_cast<int>(s);
+  }
+  hsa_iterate_agents(collect_agent, nullptr);
+  if (g_rt.cpu.handle) hsa_amd_agent_iterate_memory_pools(g_rt.cpu, cpu_pool, nullptr);
+  for (auto& ag : g_rt.gpus) hsa_amd_agent_iterate_memory_pools(ag.agent, gpu_pool, &ag);
+  hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_rt.ts_freq);
+  return static_cast<int>(g_rt.gpus.size());
+}
+
+extern "C" void mi355x_hsa_probe_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_rt.mu);
+  if (g_rt.inited && g_rt.init_status == HSA_STATUS_SUCCESS) hsa_shut_down();
+  g_rt.inited = false;
+  g_rt.gpus.clear();
+  g_rt.has_kernarg = g_rt.has_fine = false;
+  g_rt.cpu = hsa_agent_t{};
+}
+
+extern "C" int mi355x_hsa_probe_identify(int ordinal, mi355x_probe_result* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->kfd_node_id = -1;
+  int n = mi355x_hsa_probe_init();
+  if (n < 0) {
+    set_status(out, static_cast<hsa_status_t>(-n), "hsa_init");
+    return 1;
+  }
+  if (ordinal < 0 || ordinal >= n) {
+    std::snprintf(out->error, sizeof(out->error), "no such GPU agent (count=%d)", n);
+    return 1;
+  }
+  fill_identity(g_rt.gpus[ordinal], ordinal, out);
+  return 0;
+}
+
+extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, double timeout_s,
+                                       mi355x_probe_result* out) {
+  using clk = std::chrono::steady_clock;
+  std::memset(out, 0, sizeof(*out));
+  out->kfd_node_id = -1;
+  out->nonce = nonce;
+  out->iters = iters < 1 ? 1 : iters;
+  const auto t0 = clk::now();
+  auto t_setup = t0;
+  int n = mi355x_hsa_probe_init();
+  if (n < 0) {
+    set_status(out, static_cast<hsa_status_t>(-n), "hsa_init");
+    return 1;
+  }
+  if (ordinal < 0 || ordinal >= n) {
+    out->ordinal = ordinal;
+    std::snprintf(out->error, sizeof(out->error), "no such GPU agent (count=%d)", n);
+    return 1;
+  }
+  const Agent& ag = g_rt.gpus[ordinal];
+  fill_identity(ag, ordinal, out);
+  if (!g_rt.has_kernarg || !g_rt.has_fine || !ag.has_coarse) {
+    std::snprintf(out->error, sizeof(out->error), "missing memory pool (kernarg=%d fine=%d coarse=%d)",
+                  g_rt.has_kernarg, g_rt.has_fine, ag.has_coarse);
+    return 1;
+  }
+
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t sig{};
+  float* h_out = nullptr;
+  uint32_t* h_meta = nullptr;
+  float* d_scratch = nullptr;
+  mi355x_liveness_args* kargs = nullptr;
+  uint64_t kobj = 0;
+  uint32_t kseg = 0, gseg = 0, pseg = 0;
+  hsa_executable_symbol_t sym{};
+  hsa_status_t s;
+  const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
+
+#define HSA_CHECK(expr, what)   \
+  do {                          \
+    s = (expr);                 \
+    if (s != HSA_STATUS_SUCCESS) { \
+      set_status(out, s, what); \
+      goto done;                \
+    }                           \
+  } while (0)
+
+  HSA_CHECK(hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader), "code object reader");
+  HSA_CHECK(hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe),
+            "executable create");
+  HSA_CHECK(hsa_executable_load_agent_code_object(exe, ag.agent, reader, nullptr, nullptr), "load code object");
+  HSA_CHECK(hsa_executable_freeze(exe, nullptr), "executable freeze");
+  HSA_CHECK(hsa_executable_get_symbol_by_name(exe, "mi355x_mfma_liveness.kd", &ag.agent, &sym), "kernel symbol");
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &kobj);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kseg);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &gseg);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &pseg);
+  if (kseg < sizeof(mi355x_liveness_args)) {
+    std::snprintf(out->error, sizeof(out->error), "kernarg segment %u < %zu: code object / host ABI mismatch",
+                  kseg, sizeof(mi355x_liveness_args));
+    goto done;
+  }
+
+  HSA_CHECK(hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &queue),
+            "queue create");
+  hsa_amd_profiling_set_profiler_enabled(queue, 1);
+  HSA_CHECK(hsa_signal_create(1, 0, nullptr, &sig), "signal create");
+  HSA_CHECK(hsa_amd_memory_pool_allocate(g_rt.fine, MI355X_PROBE_OUT * sizeof(float), 0,
+                                         reinterpret_cast<void**>(&h_out)),
+            "alloc out");
+  HSA_CHECK(hsa_amd_memory_pool_allocate(g_rt.fine, 64, 0, reinterpret_cast<void**>(&h_meta)), "alloc meta");
+  HSA_CHECK(hsa_amd_memory_pool_allocate(ag.coarse, MI355X_SCRATCH_FLOATS * sizeof(float), 0,
+                                         reinterpret_cast<void**>(&d_scratch)),
+            "alloc scratch");
+  HSA_CHECK(hsa_amd_memory_pool_allocate(g_rt.kernarg, kseg < 64 ? 64 : kseg, 0, reinterpret_cast<void**>(&kargs)),
+            "alloc kernarg");
+  HSA_CHECK(hsa_amd_agents_allow_access(1, &ag.agent, nullptr, h_out), "allow out");
+  HSA_CHECK(hsa_amd_agents_allow_access(1, &ag.agent, nullptr, h_meta), "allow meta");
+  HSA_CHECK(hsa_amd_agents_allow_access(1, &ag.agent, nullptr, kargs), "allow kernarg");
+  std::memset(h_out, 0xFF, MI355X_PROBE_OUT * sizeof(float));
+  std::memset(h_meta, 0, 64);
+  std::memset(kargs, 0, kseg);
+  kargs->out = h_out;
+  kargs->meta = h_meta;
+  kargs->scratch = d_scratch;
+  kargs->nonce = nonce;
+  kargs->iters = out->iters;
+  t_setup = clk::now();
+
+  {
+    const uint64_t idx = hsa_queue_add_write_index_screlease(queue, 1);
+    auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address) + (idx & (queue->size - 1));
+    std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
+    pkt->workgroup_size_x = 64;
+    pkt->workgroup_size_y = 1;
+    pkt->workgroup_size_z = 1;
+    pkt->grid_size_x = 64;
+    pkt->grid_size_y = 1;
+    pkt->grid_size_z = 1;
+    pkt->private_segment_size = pseg;
+    pkt->group_segment_size = gseg;
+    pkt->kernel_object = kobj;
+    pkt->kernarg_address = kargs;
+    pkt->completion_signal = sig;
+    const uint16_t header = static_cast<uint16_t>(
+        (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
+                     __ATOMIC_RELEASE);
+    hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+    out->dispatches = 1;
+  }
+  {
+    // bounded wait: a wedged device must come back as a verdict, not a hang
+    const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
+    hsa_signal_value_t v = 1;
+    while ((v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
+                                          HSA_WAIT_STATE_BLOCKED)) >= 1) {
+      if (clk::now() > deadline) break;
+    }
+    if (v >= 1) {
+      std::snprintf(out->error, sizeof(out->error), "dispatch did not complete within %.1fs", timeout_s);
+      out->hip_error = -1;
+      goto done;
+    }
+  }
+  {
+    hsa_amd_profiling_dispatch_time_t dt{};
+    if (hsa_amd_profiling_get_dispatch_time(ag.agent, sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
+      out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
+  }
+  mi355x::verify_tile(h_out, h_meta, nonce, out->iters, out);
+
+done:
+  out->setup_us = std::chrono::duration<double, std::micro>(t_setup - t0).count();
+  if (kargs) hsa_amd_memory_pool_free(kargs);
+  if (d_scratch) hsa_amd_memory_pool_free(d_scratch);
+  if (h_meta) hsa_amd_memory_pool_free(h_meta);
+  if (h_out) hsa_amd_memory_pool_free(h_out);
+  if (sig.handle) hsa_signal_destroy(sig);
+  if (queue) hsa_queue_destroy(queue);
+  if (exe.handle) hsa_executable_destroy(exe);
+  if (reader.handle) hsa_code_object_reader_destroy(reader);
+  out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+#undef HSA_CHECK
+  return out->ok ? 0 : 1;
+}

@@ -1,16 +1,20 @@
-// Host launcher + bit-exact verification for the MFMA liveness kernel.
+// HIP launcher for the MFMA liveness kernel.
+//
+// Output and meta live in coherent pinned host memory and are poisoned by the
+// CPU, so the probe issues exactly ONE GPU dispatch (no memset/blit kernels —
+// the first version issued five, see profiles/round1_probe_rocprof.md).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
-#include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <vector>
 
 #include "liveness_kernel.h"
 #include "mi355x/liveness_probe.h"
+#include "probe_verify.h"
 
-extern "C" __global__ void mi355x_mfma_liveness(float* out, uint32_t* meta, uint32_t nonce, int iters);
+extern "C" __global__ void mi355x_mfma_liveness(float* out, uint32_t* meta, float* scratch, uint32_t nonce,
+                                                int iters);
 
 namespace {
 
@@ -42,7 +46,9 @@ void fill_identity(int ordinal, mi355x_probe_result* out) {
     for (int i = 0; i < 16 && i * 2 + 2 < static_cast<int>(sizeof(out->uuid)); ++i)
       std::snprintf(u + 2 * i, 3, "%02x", static_cast<unsigned char>(p.uuid.bytes[i]));
   }
-  hipDeviceGetPCIBusId(out->pci_bus_id, sizeof(out->pci_bus_id), ordinal);
+  (void)hipDeviceGetPCIBusId(out->pci_bus_id, sizeof(out->pci_bus_id), ordinal);
+  out->kfd_node_id = -1;
+  std::snprintf(out->runtime, sizeof(out->runtime), "hip");
 }
 
 }  // namespace
@@ -72,63 +78,50 @@ extern "C" int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355
   out->nonce = nonce;
   out->iters = iters < 1 ? 1 : iters;
   const auto t0 = std::chrono::steady_clock::now();
-  float* d_out = nullptr;
-  uint32_t* d_meta = nullptr;
+  auto t_setup = t0;
+  float* h_out = nullptr;
+  uint32_t* h_meta = nullptr;
+  float* d_scratch = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipStream_t stream = nullptr;
-  std::vector<float> h(MI355X_PROBE_OUT, 0.f);
-  uint32_t meta[MI355X_META_WORDS] = {0, 0, 0, 0};
-  int mism = 0;
   float ms = 0.f;
 
   PROBE_CHECK(hipSetDevice(ordinal), "hipSetDevice");
   fill_identity(ordinal, out);
   PROBE_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
-  PROBE_CHECK(hipMalloc(&d_out, MI355X_PROBE_OUT * sizeof(float)), "hipMalloc(out)");
-  PROBE_CHECK(hipMalloc(&d_meta, MI355X_META_WORDS * sizeof(uint32_t)), "hipMalloc(meta)");
-  // poison so a kernel that never runs cannot pass
-  PROBE_CHECK(hipMemsetAsync(d_out, 0xFF, MI355X_PROBE_OUT * sizeof(float), stream), "hipMemset(out)");
-  PROBE_CHECK(hipMemsetAsync(d_meta, 0, MI355X_META_WORDS * sizeof(uint32_t), stream), "hipMemset(meta)");
+  PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_out), MI355X_PROBE_OUT * sizeof(float),
+                            hipHostMallocCoherent),
+              "hipHostMalloc(out)");
+  PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_meta), MI355X_META_WORDS * sizeof(uint32_t),
+                            hipHostMallocCoherent),
+              "hipHostMalloc(meta)");
+  PROBE_CHECK(hipMalloc(reinterpret_cast<void**>(&d_scratch), MI355X_SCRATCH_FLOATS * sizeof(float)),
+              "hipMalloc(scratch)");
+  // poison from the CPU so a kernel that never ran cannot pass
+  std::memset(h_out, 0xFF, MI355X_PROBE_OUT * sizeof(float));
+  std::memset(h_meta, 0, MI355X_META_WORDS * sizeof(uint32_t));
   PROBE_CHECK(hipEventCreate(&ev0), "hipEventCreate");
   PROBE_CHECK(hipEventCreate(&ev1), "hipEventCreate");
+  t_setup = std::chrono::steady_clock::now();
   PROBE_CHECK(hipEventRecord(ev0, stream), "hipEventRecord");
-  hipLaunchKernelGGL(mi355x_mfma_liveness, dim3(1), dim3(64), 0, stream, d_out, d_meta, nonce, out->iters);
+  hipLaunchKernelGGL(mi355x_mfma_liveness, dim3(1), dim3(64), 0, stream, h_out, h_meta, d_scratch, nonce,
+                     out->iters);
+  out->dispatches = 1;
   PROBE_CHECK(hipGetLastError(), "launch");
   PROBE_CHECK(hipEventRecord(ev1, stream), "hipEventRecord");
-  PROBE_CHECK(hipMemcpyAsync(h.data(), d_out, MI355X_PROBE_OUT * sizeof(float), hipMemcpyDeviceToHost, stream),
-              "hipMemcpy(out)");
-  PROBE_CHECK(hipMemcpyAsync(meta, d_meta, sizeof(meta), hipMemcpyDeviceToHost, stream), "hipMemcpy(meta)");
   PROBE_CHECK(hipStreamSynchronize(stream), "hipStreamSynchronize");
   PROBE_CHECK(hipEventElapsedTime(&ms, ev0, ev1), "hipEventElapsedTime");
   out->kernel_us = ms * 1000.0;
-
-  // host reference: D = C + iters * A·B, exact in f32 for these magnitudes
-  for (int i = 0; i < MI355X_PROBE_M; ++i)
-    for (int j = 0; j < MI355X_PROBE_N; ++j) {
-      float ab = 0.f;
-      for (int k = 0; k < MI355X_PROBE_K; ++k) ab += probe_a(i, k, nonce) * probe_b(k, j, nonce);
-      float want = probe_c(i, j, nonce) + static_cast<float>(out->iters) * ab;
-      if (h[i * MI355X_PROBE_N + j] != want) ++mism;
-    }
-  out->mismatches = mism;
-  out->xcc_id = meta[MI355X_META_XCC];
-  out->hw_id = meta[MI355X_META_HWID];
-  if (meta[MI355X_META_MAGIC] != MI355X_PROBE_MAGIC || meta[MI355X_META_NONCE] != nonce) {
-    std::snprintf(out->error, sizeof(out->error), "meta mismatch: magic=%08x nonce=%u", meta[MI355X_META_MAGIC],
-                  meta[MI355X_META_NONCE]);
-  } else if (mism) {
-    std::snprintf(out->error, sizeof(out->error), "%d/%d MFMA results differ from host reference", mism,
-                  MI355X_PROBE_OUT);
-  } else {
-    out->ok = 1;
-  }
+  mi355x::verify_tile(h_out, h_meta, nonce, out->iters, out);
 
 done:
-  if (ev0) hipEventDestroy(ev0);
-  if (ev1) hipEventDestroy(ev1);
-  if (d_out) hipFree(d_out);
-  if (d_meta) hipFree(d_meta);
-  if (stream) hipStreamDestroy(stream);
+  out->setup_us = std::chrono::duration<double, std::micro>(t_setup - t0).count();
+  if (ev0) (void)hipEventDestroy(ev0);
+  if (ev1) (void)hipEventDestroy(ev1);
+  if (h_out) (void)hipHostFree(h_out);
+  if (h_meta) (void)hipHostFree(h_meta);
+  if (d_scratch) (void)hipFree(d_scratch);
+  if (stream) (void)hipStreamDestroy(stream);
   out->total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   return out->ok ? 0 : 1;
 }

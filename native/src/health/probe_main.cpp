@@ -1,7 +1,11 @@
-// mi355x-liveness-probe: run the gfx950 MFMA liveness kernel on HIP devices
+// mi355x-liveness-probe: run the gfx950 MFMA liveness kernel on GPU agents
 // and print one JSON document.
 //
-//   mi355x-liveness-probe [--devices all|0,2,..] [--nonce N] [--iters N] [--identify]
+//   mi355x-liveness-probe [--devices all|0,2,..] [--nonce N] [--iters N] [--identify] [--timeout S]
+//
+// Built twice from this file: `mi355x-liveness-probe` launches through ROCr
+// directly (MI355X_PROBE_HSA; links only libhsa-runtime64, one AQL dispatch),
+// `mi355x-liveness-probe-hip` through the HIP runtime.
 //
 // Exit status: 0 all probed devices live, 1 at least one failed, 2 usage or
 // HIP runtime unavailable. The parent (the plugin's health loop, or the
@@ -45,14 +49,29 @@ std::string json_escape(const char* s) {
 void print_device(const mi355x_probe_result& r, bool last) {
   std::printf(
       "{\"ordinal\":%d,\"ok\":%s,\"hip_error\":%d,\"mismatches\":%d,\"nonce\":%u,\"xcc_id\":%u,"
-      "\"hw_id\":%u,\"iters\":%d,\"kernel_us\":%.3f,\"total_us\":%.3f,\"pci_bus_id\":\"%s\","
+      "\"hw_id\":%u,\"iters\":%d,\"dispatches\":%d,\"kfd_node_id\":%d,\"runtime\":\"%s\","
+      "\"kernel_us\":%.3f,\"setup_us\":%.3f,\"total_us\":%.3f,\"pci_bus_id\":\"%s\","
       "\"arch\":\"%s\",\"name\":\"%s\",\"uuid\":\"%s\",\"pci_domain\":%d,\"pci_bus\":%d,"
       "\"pci_device\":%d,\"cu_count\":%d,\"total_mem\":%llu,\"error\":\"%s\"}%s",
       r.ordinal, r.ok ? "true" : "false", r.hip_error, r.mismatches, r.nonce, r.xcc_id, r.hw_id, r.iters,
-      r.kernel_us, r.total_us, json_escape(r.pci_bus_id).c_str(), json_escape(r.arch).c_str(),
+      r.dispatches, r.kfd_node_id, r.runtime, r.kernel_us, r.setup_us, r.total_us, json_escape(r.pci_bus_id).c_str(), json_escape(r.arch).c_str(),
       json_escape(r.name).c_str(), json_escape(r.uuid).c_str(), r.pci_domain, r.pci_bus, r.pci_device,
       r.cu_count, static_cast<unsigned long long>(r.total_mem), json_escape(r.error).c_str(), last ? "" : ",");
 }
+
+#ifdef MI355X_PROBE_HSA
+int device_count() { return mi355x_hsa_probe_init(); }
+int probe(int o, uint32_t nonce, int iters, double timeout_s, mi355x_probe_result* r) {
+  return mi355x_hsa_probe_device(o, nonce, iters, timeout_s, r);
+}
+int identify_dev(int o, mi355x_probe_result* r) { return mi355x_hsa_probe_identify(o, r); }
+#else
+int device_count() { return mi355x_probe_device_count(); }
+int probe(int o, uint32_t nonce, int iters, double, mi355x_probe_result* r) {
+  return mi355x_probe_device(o, nonce, iters, r);
+}
+int identify_dev(int o, mi355x_probe_result* r) { return mi355x_probe_identify(o, r); }
+#endif
 
 }  // namespace
 
@@ -61,6 +80,7 @@ int main(int argc, char** argv) {
   std::string devices = "all";
   uint32_t nonce = static_cast<uint32_t>(t_start ^ (t_start >> 32));
   int iters = 4;
+  double timeout_s = 5.0;
   bool identify = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -77,10 +97,13 @@ int main(int argc, char** argv) {
       nonce = static_cast<uint32_t>(std::strtoul(next("--nonce"), nullptr, 0));
     } else if (a == "--iters") {
       iters = std::atoi(next("--iters"));
+    } else if (a == "--timeout") {
+      timeout_s = std::atof(next("--timeout"));
     } else if (a == "--identify") {
       identify = true;
     } else if (a == "-h" || a == "--help") {
-      std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify]\n", argv[0]);
+      std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S]\n",
+                  argv[0]);
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -88,9 +111,10 @@ int main(int argc, char** argv) {
     }
   }
 
-  const int n = mi355x_probe_device_count();
+  const int n = device_count();
+  const uint64_t t_runtime = mono_ns();  // HIP runtime + ROCr initialised
   if (n < 0) {
-    std::printf("{\"ok\":false,\"hip_device_count\":0,\"error\":\"hipGetDeviceCount failed (%d)\",\"devices\":[],"
+    std::printf("{\"ok\":false,\"hip_device_count\":0,\"error\":\"GPU runtime init failed (%d)\",\"devices\":[],"
                 "\"t_start_ns\":%llu,\"t_ready_ns\":0}\n",
                 -n, static_cast<unsigned long long>(t_start));
     return 2;
@@ -119,15 +143,16 @@ int main(int argc, char** argv) {
       all_ok = false;
       continue;
     }
-    int rc = identify ? mi355x_probe_identify(ords[i], &results[i])
-                      : mi355x_probe_device(ords[i], nonce + static_cast<uint32_t>(i), iters, &results[i]);
+    int rc = identify ? identify_dev(ords[i], &results[i])
+                      : probe(ords[i], nonce + static_cast<uint32_t>(i), iters, timeout_s, &results[i]);
     if (identify && rc == 0) results[i].ok = 1;
     if (rc != 0) all_ok = false;
   }
   const uint64_t t_ready = mono_ns();
-  std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_ready_ns\":%llu,\"devices\":[",
+  std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
+              "\"t_ready_ns\":%llu,\"devices\":[",
               all_ok ? "true" : "false", n, identify ? "true" : "false", static_cast<unsigned long long>(t_start),
-              static_cast<unsigned long long>(t_ready));
+              static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(t_ready));
   for (size_t i = 0; i < results.size(); ++i) print_device(results[i], i + 1 == results.size());
   std::printf("]}\n");
   std::fflush(stdout);

@@ -4,7 +4,8 @@ Outputs land inside the package so they travel with the repo snapshot:
 
 * ``_native*.so``                 host core (kfd/sysfs, allocator, PCI, drm, amd-smi)
 * ``_hip*.so``                    in-process gfx950 liveness probe
-* ``bin/mi355x-liveness-probe``   probe executable (plugin health loop, bench "container")
+* ``bin/mi355x-liveness-probe``   HSA-direct probe executable (health loop, bench "container")
+* ``bin/mi355x-liveness-probe-hip`` the same probe through the HIP runtime
 * ``kernels/liveness_gfx950.hsaco``
 
 ``ensure_built()`` is cheap when everything is up to date (one ninja no-op).
@@ -27,6 +28,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 NATIVE_SO = PKG_DIR / f"_native{EXT_SUFFIX}"
 HIP_SO = PKG_DIR / f"_hip{EXT_SUFFIX}"
 PROBE_EXE = PKG_DIR / "bin" / "mi355x-liveness-probe"
+PROBE_EXE_HIP = PKG_DIR / "bin" / "mi355x-liveness-probe-hip"
 HSACO = PKG_DIR / "kernels" / "liveness_gfx950.hsaco"
 
 
@@ -34,14 +36,28 @@ def hipcc_available() -> bool:
     return shutil.which("hipcc") is not None or Path("/opt/rocm/bin/hipcc").exists()
 
 
-def _sources_newer_than(target: Path) -> bool:
-    if not target.exists():
-        return True
-    t = target.stat().st_mtime
+STAMP = REPO_DIR / "build" / ".native.stamp"
+_checked: set = set()
+
+
+def _newest_source_mtime() -> float:
+    newest = 0.0
     for p in NATIVE_DIR.rglob("*"):
-        if p.is_file() and p.suffix in {".cpp", ".h", ".hip", ".txt"} and p.stat().st_mtime > t:
-            return True
-    return False
+        if p.is_file() and p.suffix in {".cpp", ".h", ".hip", ".txt"}:
+            newest = max(newest, p.stat().st_mtime)
+    return newest
+
+
+def _up_to_date(targets) -> bool:
+    # Compare against a stamp written after each successful build, not against
+    # the targets: a no-op ninja run does not touch the targets, so after a
+    # copy that leaves sources "newer" (e.g. the gpurun snapshot) a target-based
+    # check would re-run the build on every call.
+    if not all(t.exists() for t in targets):
+        return False
+    if not STAMP.exists():
+        return False
+    return _newest_source_mtime() <= STAMP.stat().st_mtime
 
 
 def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = None,
@@ -77,6 +93,9 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
     if res.returncode != 0:
         sys.stderr.write(res.stdout)
         raise RuntimeError("native build failed")
+    if not sanitize and build_dir is None:
+        STAMP.parent.mkdir(parents=True, exist_ok=True)
+        STAMP.write_text(f"hip={hip}\n")
     if not quiet:
         sys.stdout.write(res.stdout)
 
@@ -91,17 +110,19 @@ def ensure_built(hip: bool | None = None) -> None:
 
     if hip is None:
         hip = hipcc_available()
-    targets = [NATIVE_SO] + ([HIP_SO, PROBE_EXE, HSACO] if hip else [])
-    if not any(_sources_newer_than(t) for t in targets):
+    if hip in _checked:
         return
-    BUILD_DIR.mkdir(parents=True, exist_ok=True)
-    with open(BUILD_DIR.parent / ".build.lock", "w") as lk:
-        fcntl.flock(lk, fcntl.LOCK_EX)
-        try:
-            if any(_sources_newer_than(t) for t in targets):
-                build(hip=hip)
-        finally:
-            fcntl.flock(lk, fcntl.LOCK_UN)
+    targets = [NATIVE_SO] + ([HIP_SO, PROBE_EXE, PROBE_EXE_HIP, HSACO] if hip else [])
+    if not _up_to_date(targets):
+        BUILD_DIR.mkdir(parents=True, exist_ok=True)
+        with open(BUILD_DIR.parent / ".build.lock", "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            try:
+                if not _up_to_date(targets):
+                    build(hip=hip)
+            finally:
+                fcntl.flock(lk, fcntl.LOCK_UN)
+    _checked.add(hip)
 
 
 def run_ctest(sanitize: str = "") -> subprocess.CompletedProcess:

@@ -54,7 +54,10 @@ class BestEffortPolicy(Policy):
             if isinstance(d, tuple):
                 out.append(n.AllocDevice(*d))
             else:
-                out.append(n.AllocDevice(d.id, d.node_id, d.numa_node, d.unique_id, int(getattr(d, "hive_id", 0))))
+                # a device whose kfd node is unreadable (e.g. cgroup-denied inside a
+                # container) has no unique_id: group it by its own PCI function
+                key = d.unique_id or f"bdf:{getattr(d, 'bdf', '') or d.id}"
+                out.append(n.AllocDevice(d.id, d.node_id, d.numa_node, key, int(getattr(d, "hive_id", 0))))
         return out
 
     def init(self, devices, topology) -> None:

@@ -46,12 +46,17 @@ class ContainerResult:
 
 
 def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int = 4,
-                    exe: Optional[str] = None) -> ContainerResult:
-    """Run the container entrypoint restricted to `ordinals`; block until ready/exit."""
+                    exe: Optional[str] = None, runtime: str = "hsa") -> ContainerResult:
+    """Run the container entrypoint restricted to `ordinals`; block until ready/exit.
+
+    runtime "hsa": the entrypoint launches the MFMA kernel straight through ROCr
+    (one AQL dispatch); "hip": the same kernel through the HIP runtime, i.e. what a
+    typical HIP/PyTorch application pays before its first kernel.
+    """
     env = {k: v for k, v in os.environ.items() if k not in _VISIBILITY_VARS}
     env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
-    argv = [exe or str(probe_executable()), "--devices", ",".join(str(i) for i in range(len(ordinals))),
-            "--iters", str(iters)]
+    argv = [exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
+            "--iters", str(iters), "--timeout", str(min(timeout_s, 30.0))]
     t0 = time.monotonic_ns()
     try:
         p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=timeout_s)

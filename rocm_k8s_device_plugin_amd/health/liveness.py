@@ -60,7 +60,8 @@ class LivenessProber:
 
     async def probe_ordinal(self, ordinal: int, nonce: Optional[int] = None) -> ProbeOutcome:
         nonce = (int(time.monotonic_ns()) ^ (ordinal * 0x9E3779B1)) & 0xFFFFFFFF if nonce is None else nonce
-        argv = [*self.argv_prefix, self._exe(), "--devices", "0", "--iters", str(self.iters), "--nonce", str(nonce)]
+        argv = [*self.argv_prefix, self._exe(), "--devices", "0", "--iters", str(self.iters), "--nonce", str(nonce),
+                "--timeout", f"{max(0.5, self.timeout_s - 0.5):.2f}"]
         t0 = time.perf_counter()
         try:
             proc = await asyncio.create_subprocess_exec(

@@ -20,6 +20,7 @@ _hip = None
 
 PKG_DIR = Path(__file__).resolve().parent.parent
 PROBE_EXE = PKG_DIR / "bin" / "mi355x-liveness-probe"
+PROBE_EXE_HIP = PKG_DIR / "bin" / "mi355x-liveness-probe-hip"
 HSACO = PKG_DIR / "kernels" / "liveness_gfx950.hsaco"
 
 
@@ -61,10 +62,12 @@ def hip():
     return _hip
 
 
-def probe_executable() -> Path:
-    if not PROBE_EXE.exists() and _auto_build_allowed():
+def probe_executable(runtime: str = "hsa") -> Path:
+    """The liveness probe: "hsa" (ROCr-direct, default) or "hip"."""
+    exe = PROBE_EXE if runtime == "hsa" else PROBE_EXE_HIP
+    if _auto_build_allowed():
         from .. import _build
         _build.ensure_built(hip=True)
-    if not PROBE_EXE.exists():
-        raise FileNotFoundError(f"liveness probe executable missing: {PROBE_EXE}")
-    return PROBE_EXE
+    if not exe.exists():
+        raise FileNotFoundError(f"liveness probe executable missing: {exe}")
+    return exe

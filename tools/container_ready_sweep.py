@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Where does "container ready" time go? Run the container entrypoint (the
+liveness probe) repeatedly under different runtime environments and report
+p50 of each phase: spawn->main (exec + dynamic loading), main->HIP runtime
+ready (ROCr/HIP init), runtime->ready (device setup + MFMA kernel + verify).
+
+  python tools/container_ready_sweep.py --reps 15 --out gpurun_out/container_sweep.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from rocm_k8s_device_plugin_amd.ops.native import probe_executable  # noqa: E402
+
+VIS = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+
+VARIANTS = {
+    "rocr_visible": {"ROCR_VISIBLE_DEVICES": "0"},
+    "hip_visible": {"HIP_VISIBLE_DEVICES": "0"},
+    "no_visibility_env": {},
+    "rocr_visible+hw_queues_1": {"ROCR_VISIBLE_DEVICES": "0", "GPU_MAX_HW_QUEUES": "1"},
+    "rocr_visible+sdma_off": {"ROCR_VISIBLE_DEVICES": "0", "HSA_ENABLE_SDMA": "0"},
+    "rocr_visible+no_interrupt": {"ROCR_VISIBLE_DEVICES": "0", "HSA_ENABLE_INTERRUPT": "0"},
+    "rocr_visible+no_scratch_reclaim": {"ROCR_VISIBLE_DEVICES": "0", "HSA_NO_SCRATCH_RECLAIM": "1"},
+}
+
+
+def run_once(env_extra, args, runtime="hsa"):
+    env = {k: v for k, v in os.environ.items() if k not in VIS}
+    env.update(env_extra)
+    argv = [str(probe_executable(runtime)), "--devices", "0", "--iters", "4"] + args
+    t0 = time.monotonic_ns()
+    p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=120)
+    t1 = time.monotonic_ns()
+    doc = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    return {
+        "ok": p.returncode == 0 and doc["ok"],
+        "spawn_to_main_ms": (doc["t_start_ns"] - t0) / 1e6,
+        "hip_init_ms": (doc["t_runtime_ns"] - doc["t_start_ns"]) / 1e6,
+        "device_ms": (doc["t_ready_ns"] - doc["t_runtime_ns"]) / 1e6,
+        "ready_ms": (doc["t_ready_ns"] - t0) / 1e6,
+        "exit_ms": (t1 - t0) / 1e6,
+        "kernel_us": doc["devices"][0]["kernel_us"] if doc["devices"] else 0.0,
+        "setup_us": doc["devices"][0].get("setup_us", 0.0) if doc["devices"] else 0.0,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    table = {}
+    plan = [(f"{rt}:{name}", env, rt) for rt in ("hsa", "hip") for name, env in VARIANTS.items()]
+    plan += [(f"{rt}:rocr_visible+identify_only", {"ROCR_VISIBLE_DEVICES": "0"}, rt) for rt in ("hsa", "hip")]
+    for name, env, rt in plan:
+        extra = ["--identify"] if name.endswith("identify_only") else []
+        runs = [run_once(env, extra, rt) for _ in range(a.reps)]
+        row = {k: round(statistics.median(r[k] for r in runs), 3) for k in runs[0] if k != "ok"}
+        row["all_ok"] = all(r["ok"] for r in runs)
+        row["ready_ms_min"] = round(min(r["ready_ms"] for r in runs), 3)
+        table[name] = row
+        print(f"{name:40s} {json.dumps(row)}", flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(table, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
