@@ -57,10 +57,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--out", default="")
+    ap.add_argument("--only", default="", help="comma list of variant names (default: all)")
+    ap.add_argument("--parent-gpu", action="store_true",
+                    help="initialise HIP in this (parent) process first, like a torch-based harness would")
     a = ap.parse_args()
+    if a.parent_gpu:
+        import torch
+        torch.cuda.synchronize() if torch.cuda.is_available() else None
+        print("parent holds a HIP context:", torch.cuda.is_available(), flush=True)
     table = {}
     plan = [(f"{rt}:{name}", env, rt) for rt in ("hsa", "hip") for name, env in VARIANTS.items()]
     plan += [(f"{rt}:rocr_visible+identify_only", {"ROCR_VISIBLE_DEVICES": "0"}, rt) for rt in ("hsa", "hip")]
+    if a.only:
+        keep = set(a.only.split(","))
+        plan = [p for p in plan if p[0] in keep]
     for name, env, rt in plan:
         extra = ["--identify"] if name.endswith("identify_only") else []
         runs = [run_once(env, extra, rt) for _ in range(a.reps)]
