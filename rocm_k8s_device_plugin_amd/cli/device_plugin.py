@@ -106,9 +106,15 @@ def select_impl(ns, device_count: Optional[int], logger) -> Optional[DeviceImpl]
             raise SystemExit(1)
     for name in C.DRIVER_TYPES:
         try:
-            return create_impl(name, ns, device_count)
+            impl = create_impl(name, ns, device_count)
         except Exception as e:
             logger.warning("%s implementation failed: %s. Trying next...", name, e)
+            continue
+        if not impl.resource_names():
+            # e.g. kfd present but no GPU behind it: let VF/PF detection run
+            logger.warning("%s implementation found no devices. Trying next...", name)
+            continue
+        return impl
     return None
 
 

@@ -1,0 +1,77 @@
+"""``k8s-node-labeller`` entry point.
+
+Reference: cmd/k8s-node-labeller/main.go:507-590 — one boolean flag per
+label kind (``-vram``, ``-cu-count``, ...), ``-driver_type``, ``-kubeconfig``,
+node name from ``$DS_NODE_NAME``. Same flags here; additions: ``-resync``
+(periodic re-assert; 0 = apply once like the reference), ``-dry_run`` (print
+the labels as JSON and exit), ``-sysfs_root`` / ``-dev_root``, and the opt-in
+extra kinds ``-gfx-target`` / ``-xgmi-hive-count``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import sys
+from typing import List, Optional
+
+from .. import __version__
+from .. import constants as C
+from ..labeller.controller import NodeLabeller
+from ..labeller.kube import KubeClient, get_config
+from ..labeller.labels import EXTRA_LABELS, generate_labels
+from ..utils import flags, log
+
+
+def build_parser() -> flags.GoFlagParser:
+    p = flags.GoFlagParser(prog="k8s-node-labeller",
+                           description=f"AMD GPU Node Labeller for Kubernetes (MI355X-native) version {__version__}")
+    p.add_str("driver_type", "", "Driver type to use: container, vf-passthrough, or pf-passthrough")
+    for k in C.SUPPORTED_LABELS + EXTRA_LABELS:
+        p.add_bool(k, False, f"Set this to label nodes with {k} properties", dest=f"label_{k}")
+    p.add_str("kubeconfig", "", "Paths to a kubeconfig. Only required if out-of-cluster.")
+    flags.add_glog_flags(p)
+    p.add_str("node_name", os.environ.get("DS_NODE_NAME", ""), "node to label (default $DS_NODE_NAME)")
+    p.add_float("resync", 300.0, "seconds between label re-asserts (0 = apply once and exit)")
+    p.add_bool("dry_run", False, "print the generated labels as JSON and exit")
+    p.add_str("sysfs_root", "/sys", "sysfs mount to read")
+    p.add_str("dev_root", "/dev", "device node directory")
+    p.add_str("log_format", "glog", "glog | json")
+    return p
+
+
+def enabled_labels(ns) -> dict:
+    return {k: bool(getattr(ns, f"label_{k}")) for k in C.SUPPORTED_LABELS + EXTRA_LABELS}
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ns = build_parser().parse_args(argv)
+    logger = log.setup(ns.v, json_format=ns.log_format == "json")
+    if ns.driver_type not in ("",) + C.DRIVER_TYPES:
+        logger.error("invalid driver_type %s", ns.driver_type)
+        return 1
+    enabled = enabled_labels(ns)
+
+    def gen():
+        return generate_labels(enabled, ns.driver_type, ns.sysfs_root, ns.dev_root)
+
+    if ns.dry_run:
+        print(json.dumps(gen(), indent=1, sort_keys=True))
+        return 0
+    if not ns.node_name:
+        logger.error("node name unknown: set DS_NODE_NAME or -node_name")
+        return 1
+    try:
+        client = KubeClient(get_config(ns.kubeconfig))
+    except Exception as e:
+        logger.error("unable to set up kubernetes client: %s", e)
+        return 1
+    lab = NodeLabeller(client, ns.node_name, gen, resync_s=ns.resync)
+    for s in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(s, lambda *_: lab.stop())
+    lab.run(once=ns.resync <= 0)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

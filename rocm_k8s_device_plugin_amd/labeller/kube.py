@@ -1,0 +1,148 @@
+"""Minimal Kubernetes API client for the node labeller (no client library).
+
+The reference uses controller-runtime (cmd/k8s-node-labeller/main.go:529-586,
+controller.go:23-58): GET the Node, strip old labels, overlay new ones, full
+``Update`` of the object. Here: GET + a JSON merge patch of
+``metadata.labels`` (``null`` deletes a key), which cannot lose concurrent
+changes to other fields and needs no resourceVersion retry loop.
+
+Config sources, in order: ``--kubeconfig`` (token or client-certificate auth,
+embedded or file CA), ``$KUBECONFIG``, in-cluster service account
+(KUBERNETES_SERVICE_HOST/PORT + /var/run/secrets/kubernetes.io/serviceaccount).
+"""
+from __future__ import annotations
+
+import base64
+import json
+import os
+import ssl
+import tempfile
+import urllib.error
+import urllib.request
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import yaml
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class KubeError(Exception):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"HTTP {status}: {msg}")
+        self.status = status
+
+
+@dataclass
+class KubeConfig:
+    server: str
+    token: Optional[str] = None
+    ca_file: Optional[str] = None
+    cert_file: Optional[str] = None
+    key_file: Optional[str] = None
+    insecure: bool = False
+
+    def ssl_context(self) -> Optional[ssl.SSLContext]:
+        if not self.server.startswith("https"):
+            return None
+        ctx = ssl.create_default_context(cafile=self.ca_file) if self.ca_file else ssl.create_default_context()
+        if self.insecure:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        if self.cert_file and self.key_file:
+            ctx.load_cert_chain(self.cert_file, self.key_file)
+        return ctx
+
+
+def _materialise(data_b64: Optional[str], suffix: str) -> Optional[str]:
+    if not data_b64:
+        return None
+    f = tempfile.NamedTemporaryFile(prefix="labeller-", suffix=suffix, delete=False)
+    f.write(base64.b64decode(data_b64))
+    f.close()
+    os.chmod(f.name, 0o600)
+    return f.name
+
+
+def load_kubeconfig(path: str) -> KubeConfig:
+    with open(path) as f:
+        doc = yaml.safe_load(f) or {}
+    ctx_name = doc.get("current-context")
+    contexts = {c["name"]: c.get("context", {}) for c in doc.get("contexts", [])}
+    ctx = contexts.get(ctx_name) or (next(iter(contexts.values())) if contexts else {})
+    clusters = {c["name"]: c.get("cluster", {}) for c in doc.get("clusters", [])}
+    users = {u["name"]: u.get("user", {}) for u in doc.get("users", [])}
+    cluster = clusters.get(ctx.get("cluster")) or (next(iter(clusters.values())) if clusters else {})
+    user = users.get(ctx.get("user")) or (next(iter(users.values())) if users else {})
+    base = os.path.dirname(os.path.abspath(path))
+
+    def rel(p):
+        return p if not p or os.path.isabs(p) else os.path.join(base, p)
+
+    token = user.get("token")
+    if not token and user.get("tokenFile"):
+        with open(rel(user["tokenFile"])) as f:
+            token = f.read().strip()
+    return KubeConfig(
+        server=cluster.get("server", "").rstrip("/"),
+        token=token,
+        ca_file=rel(cluster.get("certificate-authority")) or _materialise(cluster.get("certificate-authority-data"),
+                                                                          ".crt"),
+        cert_file=rel(user.get("client-certificate")) or _materialise(user.get("client-certificate-data"), ".crt"),
+        key_file=rel(user.get("client-key")) or _materialise(user.get("client-key-data"), ".key"),
+        insecure=bool(cluster.get("insecure-skip-tls-verify")),
+    )
+
+
+def in_cluster_config(sa_dir: str = SA_DIR) -> KubeConfig:
+    host = os.environ.get("KUBERNETES_SERVICE_HOST")
+    port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+    if not host:
+        raise KubeError(0, "not running in a cluster (KUBERNETES_SERVICE_HOST unset) and no kubeconfig given")
+    if ":" in host and not host.startswith("["):
+        host = f"[{host}]"
+    with open(os.path.join(sa_dir, "token")) as f:
+        token = f.read().strip()
+    ca = os.path.join(sa_dir, "ca.crt")
+    return KubeConfig(server=f"https://{host}:{port}", token=token, ca_file=ca if os.path.exists(ca) else None)
+
+
+def get_config(kubeconfig: str = "") -> KubeConfig:
+    """controller-runtime GetConfigOrDie order: flag, $KUBECONFIG, in-cluster."""
+    path = kubeconfig or os.environ.get("KUBECONFIG", "")
+    if path:
+        return load_kubeconfig(path)
+    return in_cluster_config()
+
+
+class KubeClient:
+    def __init__(self, cfg: KubeConfig, timeout_s: float = 15.0):
+        self.cfg = cfg
+        self.timeout_s = timeout_s
+        self._ssl = cfg.ssl_context()
+
+    def _request(self, method: str, path: str, body: Optional[dict] = None,
+                 content_type: str = "application/json") -> dict:
+        data = json.dumps(body).encode() if body is not None else None
+        req = urllib.request.Request(self.cfg.server + path, data=data, method=method)
+        req.add_header("Accept", "application/json")
+        req.add_header("User-Agent", "mi355x-node-labeller")
+        if data is not None:
+            req.add_header("Content-Type", content_type)
+        if self.cfg.token:
+            req.add_header("Authorization", f"Bearer {self.cfg.token}")
+        try:
+            with urllib.request.urlopen(req, timeout=self.timeout_s, context=self._ssl) as resp:
+                raw = resp.read()
+        except urllib.error.HTTPError as e:
+            raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from e
+        except urllib.error.URLError as e:
+            raise KubeError(0, str(e.reason)) from e
+        return json.loads(raw) if raw else {}
+
+    def get_node(self, name: str) -> dict:
+        return self._request("GET", f"/api/v1/nodes/{name}")
+
+    def patch_node_labels(self, name: str, labels: Dict[str, Optional[str]]) -> dict:
+        return self._request("PATCH", f"/api/v1/nodes/{name}", {"metadata": {"labels": labels}},
+                             "application/merge-patch+json")

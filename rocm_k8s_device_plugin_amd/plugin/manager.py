@@ -203,6 +203,7 @@ class PluginManager:
 
     async def _watch_kubelet(self) -> None:
         last = self._sock_id()
+        next_retry = 0.0
         while not self.stopped.is_set():
             try:
                 await asyncio.wait_for(self.stopped.wait(), self.cfg.watch_interval_s)
@@ -211,6 +212,13 @@ class PluginManager:
                 pass
             cur = self._sock_id()
             if cur == last:
+                # kubelet is up but a plugin never got registered (e.g. the socket
+                # appeared before kubelet was serving): keep retrying, rate-limited
+                now = time.monotonic()
+                pending = [p for p in self.plugins.values() if p.started and not p.running]
+                if cur is not None and pending and now >= next_retry:
+                    next_retry = now + max(self.cfg.retry_wait_s, self.cfg.watch_interval_s)
+                    await asyncio.gather(*(p.start_server() for p in pending))
                 continue
             if cur is None:
                 _log.info("kubelet socket removed; stopping plugin servers")

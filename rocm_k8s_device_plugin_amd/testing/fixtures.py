@@ -112,11 +112,12 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
     dev.mkdir(parents=True, exist_ok=True)
     (dev / "dri").mkdir(exist_ok=True)
     _w(dev / "kfd", "")
-    _w(sysfs / "class/kfd/kfd/topology/generation_id", "1")
+    if spec.mode == "container":
+        _w(sysfs / "class/kfd/kfd/topology/generation_id", "1")
 
     numa = max(1, spec.numa_nodes)
-    # CPU nodes 0..numa-1
-    for c in range(numa):
+    # CPU nodes 0..numa-1 (passthrough hosts run gim/vfio-pci, not amdgpu+kfd)
+    for c in range(numa if spec.mode == "container" else 0):
         nd = nodes_dir / str(c)
         _w(nd / "properties", _props([
             ("cpu_cores_count", 64), ("simd_count", 0), ("mem_banks_count", 1), ("caches_count", 0),
@@ -197,7 +198,6 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
             card += 1
 
     # kfd GPU nodes
-    by_node = {n["node"]: n for n in gpu_nodes}
     for n in gpu_nodes:
         nd = nodes_dir / str(n["node"])
         parts = n["parts"]
@@ -246,7 +246,6 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
                 ("recommended_sdma_engine_id_mask", 0), ("flags", 3)]))
         _w(nd / "mem_banks/0/properties", _props([
             ("heap_type", 1), ("size_in_bytes", vram), ("flags", 0), ("width", 8192), ("mem_clk_max", 1900)]))
-    del by_node
 
     if spec.mode == "vf":
         drv_gim = sysfs / "bus/pci/drivers/gim"

@@ -1,0 +1,237 @@
+"""Node labeller: schema parity with cmd/k8s-node-labeller/main.go and the
+reconcile loop against a fake apiserver."""
+import json
+import os
+
+import pytest
+
+from rocm_k8s_device_plugin_amd import constants as C
+from rocm_k8s_device_plugin_amd.labeller import labels as L
+from rocm_k8s_device_plugin_amd.labeller.controller import NodeLabeller, label_patch
+from rocm_k8s_device_plugin_amd.labeller.kube import KubeClient, KubeConfig, KubeError, load_kubeconfig
+from rocm_k8s_device_plugin_amd.testing.fake_apiserver import FakeApiServer
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+from rocm_k8s_device_plugin_amd.topology import discover
+
+ALL = {k: True for k in C.SUPPORTED_LABELS}
+
+
+def test_create_labels_single_and_multi():
+    one = L.create_labels("family", {"AI": 8})
+    assert one == {"beta.amd.com/gpu.family.AI": "8", "beta.amd.com/gpu.family": "AI",
+                   "amd.com/gpu.family.AI": "8", "amd.com/gpu.family": "AI"}
+    two = L.create_labels("vram", {"288G": 4, "144G": 4})
+    assert "amd.com/gpu.vram" not in two and two["amd.com/gpu.vram.288G"] == "4"
+    assert L.create_labels("x", {}) == {}
+
+
+def test_all_label_keys_reference_lists():
+    keys = set(L.all_label_keys())
+    # every generator of the reference + the three un-prefixed legacy keys (main.go:50-62)
+    for k in C.SUPPORTED_LABELS:
+        assert f"amd.com/gpu.{k}" in keys
+    for k in ("amd.com/compute-partitioning-supported", "amd.com/memory-partitioning-supported",
+              "amd.com/compute-memory-partition"):
+        assert k in keys
+    exp = set(L.all_experimental_label_keys())
+    assert "beta.amd.com/gpu.family" in exp and "beta.amd.com/gpu.mode" in exp
+
+
+def test_remove_old_node_labels_reference_cases():
+    """The two cases of TestRemoveOldNodeLabels (main_test.go:59-125)."""
+    labels = {
+        "amd.com/gpu.cu-count": "104", "amd.com/gpu.device-id": "740f", "amd.com/gpu.driver-version": "6.10.5",
+        "amd.com/gpu.family": "AI", "amd.com/gpu.product-name": "Instinct_MI210", "amd.com/gpu.simd-count": "416",
+        "amd.com/gpu.vram": "64G", "beta.amd.com/gpu.cu-count": "104", "beta.amd.com/gpu.cu-count.104": "1",
+        "beta.amd.com/gpu.device-id": "740f", "beta.amd.com/gpu.device-id.740f": "1",
+        "beta.amd.com/gpu.family": "HPC", "beta.amd.com/gpu.family.HPC": "1",
+        "beta.amd.com/gpu.product-name": "Instinct_MI300X", "beta.amd.com/gpu.product-name.Instinct_MI300X": "1",
+        "beta.amd.com/gpu.simd-count": "416", "beta.amd.com/gpu.simd-count.416": "1",
+        "beta.amd.com/gpu.vram": "64G", "beta.amd.com/gpu.vram.64G": "1", "dummyLabel1": "1", "dummyLabel2": "2",
+    }
+    assert L.remove_old_node_labels(labels) == {"dummyLabel1": "1", "dummyLabel2": "2"}
+    keep = {"amd.com/cpu": "true", "amd.com/gpu": "true", "amd.com/mi300x": "true", "dummyLabel1": "1",
+            "dummyLabel2": "2"}
+    assert L.remove_old_node_labels(keep) == keep
+    # improvement: orphaned beta counters are removed too
+    assert L.remove_old_node_labels({"beta.amd.com/gpu.family.AI": "8"}) == {}
+    assert L.remove_old_node_labels(None) == {}
+
+
+@pytest.mark.parametrize("mode,parts", [("spx", 1), ("cpx", 8), ("qpx", 4)])
+def test_container_labels_mi355x(tmp_path, mode, parts):
+    fi = make_mi355x_node(tmp_path, compute_partition=mode)
+    lab = L.generate_labels({**ALL, "firmware": False, "family": False}, "container", str(fi.sysfs), str(fi.dev))
+    n = 8 * parts
+    assert lab["amd.com/gpu.device-id"] == "75a3"
+    assert lab["amd.com/gpu.device-id.75a3"] == str(n)
+    assert lab["amd.com/gpu.product-name"] == "AMD_Instinct_MI355X"
+    assert lab["amd.com/gpu.cu-count"] == str(256 // parts)
+    assert lab["amd.com/gpu.simd-count"] == str(1024 // parts)
+    assert lab["amd.com/gpu.vram"] == f"{288 // parts}G"
+    assert lab["amd.com/gpu.compute-memory-partition"] == f"{mode}_nps1"
+    assert lab["amd.com/gpu.compute-partitioning-supported"] == "true"
+    assert lab["amd.com/gpu.memory-partitioning-supported"] == "true"
+    assert lab["amd.com/gpu.mode"] == "container" and lab["beta.amd.com/gpu.mode"] == "container"
+    assert lab["amd.com/gpu.driver-version"] == "6.12.12"
+    assert lab["amd.com/gpu.driver-src-version"] == "A1B2C3D4E5F60718293A4B5"
+    # beta + amd.com for counted kinds only; driver versions are amd.com only
+    assert "beta.amd.com/gpu.driver-version" not in lab
+    # firmware/family need a real GPU (libdrm ioctl); off here
+    assert not any("firmware" in k or "family" in k for k in lab)
+    # the opt-in additions stay off unless enabled
+    assert not any("gfx-target" in k for k in lab)
+
+
+def test_extra_labels(tmp_path):
+    fi = make_mi355x_node(tmp_path, hive_size=4)
+    lab = L.generate_labels({"gfx-target": True, "xgmi-hive-count": True}, "container", str(fi.sysfs),
+                            str(fi.dev))
+    assert lab["amd.com/gpu.gfx-target"] == "gfx950"
+    assert lab["amd.com/gpu.xgmi-hive-count"] == "2"
+    assert L.gfx_name(90402) == "gfx942" and L.gfx_name(90010) == "gfx90a" and L.gfx_name(90500) == "gfx950"
+
+
+def test_heterogeneous_no_partition_label(tmp_path):
+    fi = make_mi355x_node(tmp_path, per_gpu_compute=["spx"] * 4 + ["cpx"] * 4)
+    lab = L.generate_labels({"compute-memory-partition": True}, "container", str(fi.sysfs), str(fi.dev))
+    assert lab == {}
+
+
+def test_no_partition_support(tmp_path):
+    fi = make_mi355x_node(tmp_path, partition_support=False)
+    lab = L.generate_labels({"compute-partitioning-supported": True, "memory-partitioning-supported": True},
+                            "container", str(fi.sysfs), str(fi.dev))
+    assert lab == {"amd.com/gpu.compute-partitioning-supported": "false",
+                   "amd.com/gpu.memory-partitioning-supported": "false"}
+
+
+def test_vf_labels(tmp_path):
+    fi = make_mi355x_node(tmp_path, mode="vf", vfs_per_gpu=2)
+    lab = L.generate_labels(ALL, "", str(fi.sysfs), str(fi.dev))
+    assert lab["amd.com/gpu.mode"] == "vf-passthrough" and lab["beta.amd.com/gpu.mode"] == "vf-passthrough"
+    assert lab["amd.com/gpu.driver-version"] == "8.1.0.K"      # cut at '+'
+    assert lab["amd.com/gpu.driver-src-version"] == "F00DFACE0123456789ABCDE"
+    assert lab["amd.com/gpu.device-id.0x75b3"] == "16"         # raw VF ids, as the reference emits them
+
+
+def test_pf_labels(tmp_path):
+    fi = make_mi355x_node(tmp_path, mode="pf")
+    lab = L.generate_labels(ALL, "", str(fi.sysfs), str(fi.dev))
+    assert lab["amd.com/gpu.mode"] == "pf-passthrough"
+    assert "beta.amd.com/gpu.mode" not in lab
+    assert lab["amd.com/gpu.device-id.0x75a3"] == "8"
+
+
+def test_no_gpus_no_labels(tmp_path):
+    (tmp_path / "sys").mkdir()
+    assert L.generate_labels(ALL, "", str(tmp_path / "sys"), str(tmp_path / "dev")) == {}
+
+
+def test_label_patch_minimal():
+    cur = {"amd.com/gpu.vram": "64G", "beta.amd.com/gpu.vram": "64G", "beta.amd.com/gpu.vram.64G": "1",
+           "other": "x"}
+    want = {"amd.com/gpu.vram": "288G"}
+    p = label_patch(cur, want)
+    assert p == {"beta.amd.com/gpu.vram": None, "beta.amd.com/gpu.vram.64G": None, "amd.com/gpu.vram": "288G"}
+    assert label_patch({"amd.com/gpu.vram": "288G"}, want) == {}
+
+
+def test_reconcile_against_fake_apiserver(tmp_path):
+    fi = make_mi355x_node(tmp_path)
+    srv = FakeApiServer(token="tok").start()
+    try:
+        srv.add_node("node-a", {"amd.com/gpu.family": "stale", "beta.amd.com/gpu.family": "stale",
+                                "beta.amd.com/gpu.family.stale": "8", "kubernetes.io/hostname": "node-a"})
+        client = KubeClient(KubeConfig(server=srv.url, token="tok"))
+        enabled = {**ALL, "firmware": False, "family": False}
+        lab = NodeLabeller(client, "node-a",
+                           lambda: L.generate_labels(enabled, "container", str(fi.sysfs), str(fi.dev)), resync_s=0)
+        lab.run(once=True)
+        got = srv.labels("node-a")
+        assert got["kubernetes.io/hostname"] == "node-a"
+        assert "amd.com/gpu.family" not in got and "beta.amd.com/gpu.family.stale" not in got
+        assert got["amd.com/gpu.vram"] == "288G"
+        patches = [r for r in srv.requests if r[0] == "PATCH"]
+        assert len(patches) == 1
+        # second pass: nothing to change -> no PATCH
+        assert lab.reconcile_once()
+        assert len([r for r in srv.requests if r[0] == "PATCH"]) == 1
+        # someone deletes a label -> re-asserted
+        srv.nodes["node-a"]["metadata"]["labels"].pop("amd.com/gpu.vram")
+        assert lab.reconcile_once()
+        assert srv.labels("node-a")["amd.com/gpu.vram"] == "288G"
+        # apiserver errors are retried, not fatal
+        srv.fail_next = 1
+        assert not lab.reconcile_once()
+        assert lab.stats.errors == 1
+        assert lab.reconcile_once()
+    finally:
+        srv.stop()
+
+
+def test_unauthorized_and_missing_node():
+    srv = FakeApiServer(token="tok").start()
+    try:
+        srv.add_node("n")
+        with pytest.raises(KubeError) as e:
+            KubeClient(KubeConfig(server=srv.url, token="bad")).get_node("n")
+        assert e.value.status == 401
+        with pytest.raises(KubeError) as e:
+            KubeClient(KubeConfig(server=srv.url, token="tok")).get_node("missing")
+        assert e.value.status == 404
+    finally:
+        srv.stop()
+
+
+def test_kubeconfig_parsing(tmp_path):
+    import base64
+    ca = base64.b64encode(b"-----BEGIN CERTIFICATE-----\nx\n-----END CERTIFICATE-----\n").decode()
+    kc = tmp_path / "kubeconfig"
+    kc.write_text(f"""
+apiVersion: v1
+kind: Config
+current-context: c1
+clusters:
+- name: k1
+  cluster: {{server: "https://10.0.0.1:6443/", certificate-authority-data: "{ca}"}}
+contexts:
+- name: c1
+  context: {{cluster: k1, user: u1}}
+users:
+- name: u1
+  user: {{token: abc}}
+""")
+    cfg = load_kubeconfig(str(kc))
+    assert cfg.server == "https://10.0.0.1:6443" and cfg.token == "abc"
+    assert cfg.ca_file and os.path.exists(cfg.ca_file)
+
+
+def test_labeller_cli_dry_run(tmp_path, capsys):
+    from rocm_k8s_device_plugin_amd.cli import node_labeller
+    fi = make_mi355x_node(tmp_path)
+    rc = node_labeller.main(["-dry_run", "-vram", "-cu-count=true", "-simd-count=false",
+                             "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)])
+    assert rc == 0
+    out = json.loads(capsys.readouterr().out)
+    assert out["amd.com/gpu.vram"] == "288G" and out["amd.com/gpu.cu-count"] == "256"
+    assert not any("simd" in k for k in out)
+
+
+def test_labeller_cli_against_fake_apiserver(tmp_path):
+    from rocm_k8s_device_plugin_amd.cli import node_labeller
+    fi = make_mi355x_node(tmp_path)
+    srv = FakeApiServer(token=None).start()
+    try:
+        srv.add_node("worker-7")
+        kc = tmp_path / "kc"
+        kc.write_text(f"clusters: [{{name: a, cluster: {{server: '{srv.url}'}}}}]\n"
+                      "contexts: [{name: a, context: {cluster: a, user: a}}]\ncurrent-context: a\n"
+                      "users: [{name: a, user: {}}]\n")
+        rc = node_labeller.main(["-kubeconfig", str(kc), "-node_name", "worker-7", "-resync", "0",
+                                 "-mode", "-vram", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)])
+        assert rc == 0
+        got = srv.labels("worker-7")
+        assert got["amd.com/gpu.mode"] == "container" and got["amd.com/gpu.vram"] == "288G"
+    finally:
+        srv.stop()

@@ -1,0 +1,468 @@
+"""Device plugin end to end over real gRPC/UDS against the fake kubelet.
+
+Covers what the reference never tested: registration,
+ListAndWatch streaming, Allocate / GetPreferredAllocation responses, kubelet
+restart re-registration, late kubelet start, shutdown cleanup, health flips
+from the exporter, liveness fault injection, kfd node loss, the mixed
+strategy on heterogeneous nodes and passthrough modes.
+"""
+import asyncio
+import json
+import os
+import sys
+from contextlib import asynccontextmanager
+
+import grpc
+import pytest
+
+from rocm_k8s_device_plugin_amd import constants as C
+from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig, HealthMonitor
+from rocm_k8s_device_plugin_amd.plugin.base import DeviceImplError
+from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
+from rocm_k8s_device_plugin_amd.plugin.passthrough import PfImpl, VfImpl
+from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+from rocm_k8s_device_plugin_amd.testing.fake_exporter import FakeExporter
+from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+from rocm_k8s_device_plugin_amd.topology import discover
+
+STUB = os.path.join(os.path.dirname(__file__), "..", "rocm_k8s_device_plugin_amd", "testing", "stub_probe.py")
+
+
+def run(coro, timeout=60):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+@asynccontextmanager
+async def plugin_env(tmp_path, impl, pulse=0.0, start_kubelet=True, **mcfg):
+    pdir = str(tmp_path / "dp")
+    k = FakeKubelet(pdir)
+    if start_kubelet:
+        await k.start()
+    cfg = ManagerConfig(pulse_s=pulse, plugin_dir=pdir, handle_signals=False, retry_wait_s=0.05,
+                        watch_interval_s=0.05, **mcfg)
+    mgr = PluginManager(impl, cfg)
+    task = asyncio.create_task(mgr.run())
+    try:
+        yield k, mgr
+    finally:
+        mgr.request_stop()
+        await asyncio.wait_for(task, 20)
+        await k.stop()
+
+
+def container(fi, strategy="single", **hc):
+    hc.setdefault("exporter_socket", None)
+    return ContainerImpl(strategy, str(fi.sysfs), HealthConfig(**hc))
+
+
+# ------------------------------------------------------------------ basics
+
+def test_register_list_allocate(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = container(fi)
+
+    async def go():
+        async with plugin_env(tmp_path, impl) as (k, mgr):
+            st = await k.wait_for_resource("amd.com/gpu", 8)
+            reg = k.registrations[0]
+            assert reg.version == "v1beta1" and reg.endpoint == "amd.com_gpu"
+            assert reg.resource_name == "amd.com/gpu"
+            assert reg.options.get_preferred_allocation_available and not reg.options.pre_start_required
+            assert set(st.devices) == set(fi.bdfs)
+            assert all(h == "Healthy" for h in st.devices.values())
+            assert st.numa["0000:05:00.0"] == [0] and st.numa["0000:f5:00.0"] == [1]
+            adm = await k.admit("amd.com/gpu", 2)
+            specs = [(d.container_path, d.host_path, d.permissions) for d in adm.response.container_responses[0].devices]
+            assert specs[0] == ("/dev/kfd", "/dev/kfd", "rw")
+            for dev in adm.device_ids:
+                g = impl.inv.by_id[dev]
+                assert (f"/dev/dri/card{g.card}", f"/dev/dri/card{g.card}", "rw") in specs
+                assert (f"/dev/dri/renderD{g.render_minor}", f"/dev/dri/renderD{g.render_minor}", "rw") in specs
+            assert len(specs) == 1 + 2 * 2
+            assert not adm.response.container_responses[0].envs
+            # PreStartContainer is a no-op
+            r = await st.stub.PreStartContainer(pb.PreStartContainerRequest(devices_ids=adm.device_ids))
+            assert r == pb.PreStartContainerResponse()
+            # unknown device -> INVALID_ARGUMENT, not a silent empty spec list
+            req = pb.AllocateRequest()
+            req.container_requests.add(devices_ids=["0000:ff:00.0"])
+            with pytest.raises(grpc.aio.AioRpcError) as e:
+                await st.stub.Allocate(req)
+            assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+            # multi-container pod: one /dev/kfd per container
+            req = pb.AllocateRequest()
+            req.container_requests.add(devices_ids=[fi.bdfs[0]])
+            req.container_requests.add(devices_ids=[fi.bdfs[1]])
+            resp = await st.stub.Allocate(req)
+            assert [sum(d.host_path == "/dev/kfd" for d in c.devices) for c in resp.container_responses] == [1, 1]
+        assert not os.path.exists(tmp_path / "dp" / "amd.com_gpu"), "socket not cleaned up"
+
+    run(go())
+
+
+def test_preferred_allocation_packs_one_hive(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", hive_size=4)   # two xGMI hives of 4 GPUs
+    impl = container(fi)
+    hive = {d.id: d.hive_id for d in impl.inv.devices}
+
+    async def go():
+        async with plugin_env(tmp_path, impl) as (k, mgr):
+            await k.wait_for_resource("amd.com/gpu", 8)
+            for n in (2, 3, 4):
+                adm = await k.admit("amd.com/gpu", n)
+                assert adm.preferred_used
+                assert len({hive[d] for d in adm.device_ids}) == 1, adm.device_ids
+                k.release("amd.com/gpu", adm.device_ids)
+            # fragment hive A: 2 free there, 4 free in B -> a 3-GPU pod goes to B
+            first = await k.admit("amd.com/gpu", 2, available=fi.bdfs[:4])
+            adm = await k.admit("amd.com/gpu", 3)
+            assert {hive[d] for d in adm.device_ids} == {hive[fi.bdfs[4]]}
+            # must_include is honoured
+            k.release("amd.com/gpu", adm.device_ids + first.device_ids)
+            adm = await k.admit("amd.com/gpu", 2, must_include=[fi.bdfs[6]])
+            assert fi.bdfs[6] in adm.device_ids and len({hive[d] for d in adm.device_ids}) == 1
+            # an impossible request surfaces the allocator's error string
+            st = k.resources["amd.com/gpu"]
+            req = pb.PreferredAllocationRequest()
+            req.container_requests.add(available_deviceIDs=fi.bdfs[:2], must_include_deviceIDs=[],
+                                       allocation_size=3)
+            with pytest.raises(grpc.aio.AioRpcError) as e:
+                await st.stub.GetPreferredAllocation(req)
+            assert "available devices count less than allocation size" in e.value.details()
+
+    run(go())
+
+
+def test_cpx_partitions_prefer_same_gpu(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="cpx")
+    impl = container(fi)
+    uid = {d.id: d.unique_id for d in impl.inv.devices}
+
+    async def go():
+        async with plugin_env(tmp_path, impl) as (k, mgr):
+            st = await k.wait_for_resource("amd.com/gpu", 64)
+            assert any(d.startswith("amdgpu_xcp_") for d in st.devices)
+            adm = await k.admit("amd.com/gpu", 4)
+            assert len({uid[d] for d in adm.device_ids}) == 1
+            adm2 = await k.admit("amd.com/gpu", 4)
+            # anti-fragmentation: the second 4 fills the same, already-opened GPU
+            assert {uid[d] for d in adm2.device_ids} == {uid[d] for d in adm.device_ids}
+
+    run(go())
+
+
+# ------------------------------------------------------------ strategies
+
+def test_mixed_strategy_heterogeneous(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", per_gpu_compute=["spx"] * 4 + ["cpx"] * 4)
+    with pytest.raises(DeviceImplError, match="not supported with single strategy"):
+        container(fi, "single")
+    impl = container(fi, "mixed")
+    assert impl.resource_names() == ["cpx_nps1", "spx_nps1"]
+
+    async def go():
+        async with plugin_env(tmp_path, impl, pulse=0.1, send_every_pulse=True) as (k, mgr):
+            a = await k.wait_for_resource("amd.com/spx_nps1", 4)
+            b = await k.wait_for_resource("amd.com/cpx_nps1", 32)
+            assert len(a.devices) == 4 and len(b.devices) == 32
+            ua, ub = a.updates, b.updates
+            # every pulse reaches EVERY resource's stream (reference Appendix B #1)
+            await k.wait_for_update("amd.com/spx_nps1", ua + 2, timeout=10)
+            await k.wait_for_update("amd.com/cpx_nps1", ub + 2, timeout=10)
+            adm = await k.admit("amd.com/cpx_nps1", 3)
+            assert all(impl.inv.by_id[d].partition_type == "cpx_nps1" for d in adm.device_ids)
+
+    run(go())
+
+
+def test_mixed_strategy_homogeneous_partition_name(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="dpx", memory_partition="nps2")
+    assert container(fi, "mixed").resource_names() == ["dpx_nps2"]
+    assert container(fi, "single").resource_names() == ["gpu"]
+    fi2 = make_mi355x_node(tmp_path / "m", partition_support=False)
+    assert container(fi2, "mixed").resource_names() == ["gpu"]
+
+
+def test_device_count_limit(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="qpx")
+    impl = ContainerImpl("single", str(fi.sysfs), HealthConfig(exporter_socket=None), device_count_limit=2)
+    assert len(impl.devices("gpu")) == 8  # 2 physical GPUs x 4 partitions
+    assert len({d.unique_id for d in impl.devices("gpu")}) == 2
+
+
+def test_no_kfd_is_an_init_error(tmp_path):
+    with pytest.raises(DeviceImplError, match="No amd gpu driver loaded"):
+        ContainerImpl("single", str(tmp_path), HealthConfig(exporter_socket=None))
+
+
+# ----------------------------------------------------------- lifecycle
+
+def test_kubelet_restart_reregisters(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = container(fi)
+
+    async def go():
+        async with plugin_env(tmp_path, impl) as (k, mgr):
+            await k.wait_for_resource("amd.com/gpu", 8)
+            assert len(k.registrations) == 1
+            await k.restart(downtime_s=0.2)
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=10)
+            assert len(k.registrations) == 2
+            adm = await k.admit("amd.com/gpu", 1)
+            assert len(adm.device_ids) == 1
+            # quick delete+recreate (inode reuse) is also detected
+            await k.restart()
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=10)
+            assert len(k.registrations) == 3
+            assert mgr.plugins["gpu"].registrations == 3
+
+    run(go())
+
+
+def test_late_kubelet(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = container(fi)
+
+    async def go():
+        async with plugin_env(tmp_path, impl, start_kubelet=False, start_retries=2) as (k, mgr):
+            await asyncio.wait_for(mgr.ready.wait(), 10)
+            assert not mgr.plugins["gpu"].running          # registration failed, retries exhausted
+            await k.start()                                  # kubelet comes up later
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=10)
+            assert mgr.plugins["gpu"].running
+
+    run(go())
+
+
+def test_no_impl_idles(tmp_path):
+    async def go():
+        async with plugin_env(tmp_path, None) as (k, mgr):
+            await asyncio.wait_for(mgr.ready.wait(), 5)
+            assert mgr.resources() == []
+            await asyncio.sleep(0.2)
+            assert k.registrations == []
+
+    run(go())
+
+
+# -------------------------------------------------------------- health
+
+def test_exporter_health_flip_reaches_partitions(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="dpx")
+    sock = str(tmp_path / "exp" / "exporter.sock")
+    impl = container(fi, exporter_socket=sock)
+    bad_bdf = fi.bdfs[3]
+
+    async def go():
+        exp = FakeExporter(sock, {b: "healthy" for b in fi.bdfs})
+        await exp.start()
+        try:
+            async with plugin_env(tmp_path, impl, pulse=0.1) as (k, mgr):
+                st = await k.wait_for_resource("amd.com/gpu", 16)
+                u = st.updates
+                exp.states[bad_bdf] = "unhealthy"
+                st = await k.wait_for_update("amd.com/gpu", u, timeout=10)
+                bad = sorted(d for d, h in st.devices.items() if h == "Unhealthy")
+                # the BDF verdict applies to the GPU's xcp partition too (reference Appendix B #4)
+                want = sorted(d.id for d in impl.inv.devices if d.bdf == bad_bdf)
+                assert bad == want and len(want) == 2
+                # kubelet must not hand out unhealthy devices
+                assert not set(bad) & set(k.healthy_free("amd.com/gpu"))
+                u = st.updates
+                exp.states[bad_bdf] = "healthy"
+                st = await k.wait_for_update("amd.com/gpu", u, timeout=10)
+                assert all(h == "Healthy" for h in st.devices.values())
+                assert exp.calls >= 2
+        finally:
+            await exp.stop()
+
+    run(go())
+
+
+def _stub_prober(tmp_path, control, timeout=2.0):
+    ctl = tmp_path / "probe_ctl.json"
+    ctl.write_text(json.dumps(control))
+    return ctl, LivenessProber(exe=STUB, argv_prefix=[sys.executable], timeout_s=timeout,
+                               extra_env={"MI355X_STUB_PROBE_CONTROL": str(ctl)})
+
+
+def test_liveness_fault_injection_hysteresis(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ords = {d.id: i for i, d in enumerate(inv.devices)}
+    ctl, prober = _stub_prober(tmp_path, {"2": "fail", "5": "hang", "6": "stale", "7": "garbage"}, timeout=1.5)
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=2,
+                                          recover_threshold=1), prober=prober, ordinal_map=ords)
+
+    async def go():
+        changed = await mon.check_once()          # 1st failure: below threshold
+        assert not changed and all(v.health == "Healthy" for v in mon.snapshot().values())
+        changed = await mon.check_once()          # 2nd consecutive failure
+        assert changed
+        snap = mon.snapshot()
+        bad = {d for d, v in snap.items() if v.health == "Unhealthy"}
+        assert bad == {fi.bdfs[2], fi.bdfs[5], fi.bdfs[6], fi.bdfs[7]}
+        assert "differ" in snap[fi.bdfs[2]].reasons[0]
+        assert "deadline" in snap[fi.bdfs[5]].reasons[0]
+        assert "stale" in snap[fi.bdfs[6]].reasons[0]
+        assert "unparseable" in snap[fi.bdfs[7]].reasons[0]
+        ctl.write_text("{}")                        # everything recovers
+        assert await mon.check_once()
+        assert all(v.health == "Healthy" for v in mon.snapshot().values())
+
+    run(go(), timeout=60)
+
+
+def test_liveness_through_listandwatch(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl, prober = _stub_prober(tmp_path, {})
+    inv = discover(str(fi.sysfs))
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=1), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+    impl = ContainerImpl("single", str(fi.sysfs), inventory=inv, monitor=mon)
+
+    async def go():
+        async with plugin_env(tmp_path, impl, pulse=0.1) as (k, mgr):
+            st = await k.wait_for_resource("amd.com/gpu", 8)
+            u = st.updates
+            ctl.write_text(json.dumps({"4": "fail"}))
+            st = await k.wait_for_update("amd.com/gpu", u, timeout=15)
+            assert st.devices[fi.bdfs[4]] == "Unhealthy"
+            assert sum(h == "Unhealthy" for h in st.devices.values()) == 1
+
+    run(go())
+
+
+def test_kfd_node_loss_marks_device_unhealthy(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = container(fi)
+    victim = impl.inv.by_id[fi.bdfs[1]]
+
+    async def go():
+        async with plugin_env(tmp_path, impl, pulse=0.1) as (k, mgr):
+            st = await k.wait_for_resource("amd.com/gpu", 8)
+            u = st.updates
+            os.remove(fi.sysfs / "class/kfd/kfd/topology/nodes" / str(victim.node_id) / "properties")
+            st = await k.wait_for_update("amd.com/gpu", u, timeout=10)
+            assert st.devices[victim.id] == "Unhealthy"
+            assert sum(h == "Unhealthy" for h in st.devices.values()) == 1
+
+    run(go())
+
+
+# ---------------------------------------------------------- passthrough
+
+def test_vf_passthrough(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", mode="vf", vfs_per_gpu=2)
+    sock = str(tmp_path / "exp.sock")
+    impl = VfImpl("mixed", str(fi.sysfs), exporter_socket=sock)
+    assert impl.resource_names() == ["gpu_vf"]
+    assert VfImpl("single", str(fi.sysfs)).resource_names() == ["gpu"]
+
+    async def go():
+        exp = FakeExporter(sock, {b: "healthy" for b in fi.bdfs})
+        await exp.start()
+        try:
+            async with plugin_env(tmp_path, impl, pulse=0.1) as (k, mgr):
+                st = await k.wait_for_resource("amd.com/gpu_vf", 16)
+                assert not k.registrations[0].options.get_preferred_allocation_available
+                groups = sorted(st.devices, key=int)[:3]
+                adm = await k.admit("amd.com/gpu_vf", 3, available=groups)
+                car = adm.response.container_responses[0]
+                paths = [d.host_path for d in car.devices]
+                assert [d.permissions for d in car.devices] == ["mrw"] * len(paths)
+                assert paths.count("/dev/vfio/vfio") == 1           # once per container (Appendix B #9)
+                for g in groups:
+                    assert f"/dev/vfio/{g}" in paths
+                env = car.envs["PCI_RESOURCE_AMD_COM_GPU_VF"].split(",")
+                assert len(env) == 3                               # all groups, not only the last
+                # PF unhealthy -> its VF groups unhealthy
+                u = st.updates
+                exp.states[fi.bdfs[0]] = "unhealthy"
+                st = await k.wait_for_update("amd.com/gpu_vf", u, timeout=10)
+                bad = sorted((d for d, h in st.devices.items() if h == "Unhealthy"), key=int)
+                assert bad == ["100", "101"]
+        finally:
+            await exp.stop()
+
+    run(go())
+
+
+def test_vf_driver_removed(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", mode="vf")
+    impl = VfImpl("single", str(fi.sysfs), exporter_socket=None)
+    os.rmdir(fi.sysfs / "bus/pci/drivers/gim")
+    assert run(impl.refresh_health())
+    assert all(d.health == "Unhealthy" for d in impl.enumerate(None))
+
+
+def test_pf_passthrough(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", mode="pf")
+    impl = PfImpl("mixed", str(fi.sysfs))
+    assert impl.resource_names() == ["gpu_pf"]
+    devs = impl.enumerate(None)
+    assert [d.ID for d in devs] == [str(10 + i) for i in range(8)]
+    from rocm_k8s_device_plugin_amd.plugin.base import PluginContext
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["10", "13"])
+    resp = impl.allocate(PluginContext("gpu_pf"), req)
+    assert resp.container_responses[0].envs["PCI_RESOURCE_AMD_COM_GPU_PF"] == f"{fi.bdfs[0]},{fi.bdfs[3]}"
+    with pytest.raises(DeviceImplError, match="not found"):
+        bad = pb.AllocateRequest()
+        bad.container_requests.add(devices_ids=["99"])
+        impl.allocate(PluginContext("gpu_pf"), bad)
+    os.rmdir(fi.sysfs / "bus/pci/drivers/vfio-pci")
+    assert run(impl.refresh_health())
+    assert all(d.health == "Unhealthy" for d in impl.enumerate(None))
+    with pytest.raises(DeviceImplError, match="vfio-pci"):
+        PfImpl("single", str(fi.sysfs))
+
+
+# ----------------------------------------------------------------- CLI
+
+def test_cli_validation(tmp_path):
+    from rocm_k8s_device_plugin_amd.cli import device_plugin as cli
+    assert cli.main(["-pulse=-1"]) == 1
+    assert cli.main(["-driver_type", "bogus"]) == 1
+    assert cli.main(["--resource_naming_strategy=weird"]) == 1
+    with pytest.raises(SystemExit) as e:
+        cli.main(["-driver_type=container", "-sysfs_root", str(tmp_path)])
+    assert e.value.code == 1
+
+
+def test_cli_flag_spellings():
+    from rocm_k8s_device_plugin_amd.cli import device_plugin as cli
+    ns = cli.build_parser().parse_args(["-logtostderr=true", "-stderrthreshold=INFO", "-v=5", "-pulse=2",
+                                        "--resource_naming_strategy", "mixed", "-liveness"])
+    assert ns.pulse == 2 and ns.v == 5 and ns.logtostderr is True and ns.liveness is True
+    assert ns.resource_naming_strategy == "mixed"
+
+
+def test_cli_autoselect_order(tmp_path):
+    from rocm_k8s_device_plugin_amd.cli import device_plugin as cli
+    from rocm_k8s_device_plugin_amd.utils import log
+    lg = log.setup(0)
+    p = cli.build_parser()
+    fi = make_mi355x_node(tmp_path / "vf", mode="vf")
+    ns = p.parse_args(["-sysfs_root", str(fi.sysfs), "-exporter_socket", ""])
+    impl = cli.select_impl(ns, None, lg)
+    assert impl.name == C.VF_PASSTHROUGH           # no kfd -> container fails -> VF
+    fi2 = make_mi355x_node(tmp_path / "c")
+    ns = p.parse_args(["-sysfs_root", str(fi2.sysfs), "-exporter_socket", ""])
+    assert cli.select_impl(ns, None, lg).name == C.CONTAINER
+    ns = p.parse_args(["-sysfs_root", str(tmp_path / "empty")])
+    assert cli.select_impl(ns, None, lg) is None
+
+
+def test_cli_config_file_device_count(tmp_path, monkeypatch):
+    from rocm_k8s_device_plugin_amd.cli import device_plugin as cli
+    cfgf = tmp_path / "config.yaml"
+    cfgf.write_text("gpu:\n  device_count: 3\n")
+    assert cli.load_config(str(cfgf))["gpu"]["device_count"] == 3
+    from rocm_k8s_device_plugin_amd.topology import device_count_limit_from_env
+    assert device_count_limit_from_env({"AMD_GPU_DEVICE_COUNT": "2"}) == 2
+    assert device_count_limit_from_env({"AMD_GPU_DEVICE_COUNT": "x"}) is None
+    assert device_count_limit_from_env({}) is None
