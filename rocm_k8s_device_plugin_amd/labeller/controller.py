@@ -42,6 +42,7 @@ def label_patch(current: Dict[str, str], desired: Dict[str, str]) -> Dict[str, O
 class ReconcileStats:
     passes: int = 0
     patches: int = 0
+    updates: int = 0
     errors: int = 0
     last_error: str = ""
     last_patch: Dict[str, Optional[str]] = field(default_factory=dict)
@@ -67,7 +68,14 @@ class NodeLabeller:
             current = (node.get("metadata") or {}).get("labels") or {}
             patch = label_patch(current, desired)
             if patch:
-                self.client.patch_node_labels(self.node, patch)
+                try:
+                    self.client.patch_node_labels(self.node, patch)
+                except KubeError as e:
+                    if e.status != 403:
+                        raise
+                    # RBAC from the upstream manifests grants "update" but not
+                    # "patch": fall back to the reference's GET + Update
+                    self._update_with_retry(desired)
                 self.stats.patches += 1
                 self.stats.last_patch = patch
                 log.info_fields(_log, "node labels updated", node=self.node, changed=len(patch))
@@ -77,6 +85,21 @@ class NodeLabeller:
             self.stats.last_error = str(e)
             _log.error("reconcile of node %s failed: %s", self.node, e)
             return False
+
+    def _update_with_retry(self, desired: Dict[str, str], attempts: int = 5) -> None:
+        for i in range(attempts):
+            node = self.client.get_node(self.node)
+            meta = node.setdefault("metadata", {})
+            labels = remove_old_node_labels(meta.get("labels") or {})
+            labels.update(desired)
+            meta["labels"] = labels
+            try:
+                self.client.update_node(self.node, node)
+                self.stats.updates += 1
+                return
+            except KubeError as e:
+                if e.status != 409 or i == attempts - 1:
+                    raise
 
     def stop(self) -> None:
         self._stop.set()

@@ -146,3 +146,7 @@ class KubeClient:
     def patch_node_labels(self, name: str, labels: Dict[str, Optional[str]]) -> dict:
         return self._request("PATCH", f"/api/v1/nodes/{name}", {"metadata": {"labels": labels}},
                              "application/merge-patch+json")
+
+    def update_node(self, name: str, node: dict) -> dict:
+        """Full-object update (PUT); fails with 409 if resourceVersion is stale."""
+        return self._request("PUT", f"/api/v1/nodes/{name}", node)

@@ -28,6 +28,7 @@ class FakeApiServer:
         self.nodes: Dict[str, dict] = {}
         self.requests: List[Tuple[str, str, Optional[dict]]] = []
         self.fail_next: int = 0          # respond 500 to the next N requests
+        self.forbid: set = set()         # HTTP methods answered with 403 (RBAC without that verb)
         self._lock = threading.Lock()
         srv = self
 
@@ -65,6 +66,8 @@ class FakeApiServer:
                         return self._send(500, {"kind": "Status", "message": "injected failure"})
                 if not self._auth():
                     return
+                if method in srv.forbid:
+                    return self._send(403, {"kind": "Status", "message": f"{method} forbidden"})
                 name = self._node()
                 with srv._lock:
                     node = srv.nodes.get(name) if name else None
@@ -77,6 +80,8 @@ class FakeApiServer:
                             return self._send(415, {"message": "unsupported patch type"})
                         node = merge_patch(node, body)
                     elif method == "PUT":
+                        if body["metadata"].get("resourceVersion") != node["metadata"].get("resourceVersion"):
+                            return self._send(409, {"kind": "Status", "message": "conflict"})
                         node = body
                     rv = int(node["metadata"].get("resourceVersion", "1")) + 1
                     node["metadata"]["resourceVersion"] = str(rv)

@@ -235,3 +235,22 @@ def test_labeller_cli_against_fake_apiserver(tmp_path):
         assert got["amd.com/gpu.mode"] == "container" and got["amd.com/gpu.vram"] == "288G"
     finally:
         srv.stop()
+
+
+def test_reconcile_falls_back_to_update_without_patch_verb(tmp_path):
+    """Upstream RBAC (get/list/watch/update, no patch) keeps working."""
+    fi = make_mi355x_node(tmp_path)
+    srv = FakeApiServer(token=None).start()
+    try:
+        srv.add_node("n1", {"beta.amd.com/gpu.vram": "64G", "beta.amd.com/gpu.vram.64G": "1", "x": "y"})
+        srv.forbid = {"PATCH"}
+        client = KubeClient(KubeConfig(server=srv.url))
+        lab = NodeLabeller(client, "n1", lambda: L.generate_labels({"vram": True}, "container", str(fi.sysfs),
+                                                                   str(fi.dev)), resync_s=0)
+        assert lab.reconcile_once()
+        assert lab.stats.updates == 1
+        got = srv.labels("n1")
+        assert got["amd.com/gpu.vram"] == "288G" and got["x"] == "y"
+        assert "beta.amd.com/gpu.vram.64G" not in got
+    finally:
+        srv.stop()

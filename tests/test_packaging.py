@@ -1,0 +1,111 @@
+"""Drop-in packaging checks: DaemonSet manifests, Helm values, images, examples."""
+import os
+import re
+from pathlib import Path
+
+import pytest
+import yaml
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _docs(name):
+    return [d for d in yaml.safe_load_all((REPO / name).read_text()) if d]
+
+
+def _ds(doc):
+    return doc["spec"]["template"]["spec"]
+
+
+def test_device_plugin_manifests():
+    for name, cname in [("k8s-ds-amdgpu-dp.yaml", "amdgpu-dp-cntr"),
+                        ("k8s-ds-amdgpu-dp-health.yaml", "amdgpu-dp-cntr-health")]:
+        (ds,) = _docs(name)
+        assert ds["kind"] == "DaemonSet" and ds["metadata"]["name"] == "amdgpu-device-plugin-daemonset"
+        assert ds["metadata"]["namespace"] == "kube-system"
+        assert ds["spec"]["selector"]["matchLabels"] == {"name": "amdgpu-dp-ds"}
+        spec = _ds(ds)
+        assert spec["priorityClassName"] == "system-node-critical"
+        assert {"key": "CriticalAddonsOnly", "operator": "Exists"} in spec["tolerations"]
+        c = spec["containers"][0]
+        assert c["name"] == cname
+        mounts = {m["mountPath"] for m in c["volumeMounts"]}
+        assert {"/var/lib/kubelet/device-plugins", "/sys"} <= mounts
+    (health,) = _docs("k8s-ds-amdgpu-dp-health.yaml")
+    c = _ds(health)["containers"][0]
+    assert c["command"] == ["./k8s-device-plugin"]
+    assert "-pulse=2" in c["args"] and "-liveness=true" in c["args"]
+    assert "/dev" in {m["mountPath"] for m in c["volumeMounts"]}
+
+
+def test_labeller_manifest():
+    docs = {d["kind"]: d for d in _docs("k8s-ds-amdgpu-labeller.yaml")}
+    assert docs["ClusterRole"]["metadata"]["name"] == "cr-node-labeller"
+    verbs = set(docs["ClusterRole"]["rules"][0]["verbs"])
+    assert {"get", "list", "watch", "update", "patch"} <= verbs
+    assert docs["ServiceAccount"]["metadata"]["name"] == "node-labeller-sa"
+    ds = docs["DaemonSet"]
+    assert ds["metadata"]["name"] == "amdgpu-labeller-daemonset"
+    c = _ds(ds)["containers"][0]
+    assert c["command"] == ["./k8s-node-labeller"]
+    assert c["args"] == ["-vram", "-cu-count", "-simd-count", "-device-id", "-family"]
+    assert c["env"][0]["name"] == "DS_NODE_NAME"
+    # every labeller arg is a real flag
+    from rocm_k8s_device_plugin_amd.cli.node_labeller import build_parser
+    build_parser().parse_args(c["args"])
+
+
+def _keys(d, prefix=""):
+    out = set()
+    for k, v in d.items():
+        out.add(prefix + k)
+        if isinstance(v, dict):
+            out |= _keys(v, prefix + k + ".")
+    return out
+
+
+def test_helm_values_superset_of_upstream(ref_testdata):
+    ours = yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())
+    ref = yaml.safe_load((ref_testdata.parent / "helm/amd-gpu/values.yaml").read_text())
+    missing = _keys(ref) - _keys(ours)
+    assert not missing, missing
+    chart = yaml.safe_load((REPO / "helm/amd-gpu/Chart.yaml").read_text())
+    assert chart["name"] == "amd-gpu"
+
+
+def test_helm_object_names():
+    t = (REPO / "helm/amd-gpu/templates")
+    assert "{{ .Chart.Name }}-device-plugin-daemonset" in (t / "deviceplugin-daemonset.yaml").read_text()
+    assert "{{ .Chart.Name }}-labeller-daemonset" in (t / "labeller.yaml").read_text()
+    assert "cr-{{ .Chart.Name }}-node-labeller" in (t / "rbac.yaml").read_text()
+    assert "{{ .Chart.Name }}-node-labeller-sa" in (t / "serviceaccount.yaml").read_text()
+    # Helm template braces balance (cheap syntax sanity without a helm binary)
+    for f in t.iterdir():
+        s = f.read_text()
+        assert s.count("{{") == s.count("}}"), f
+        opens = len(re.findall(r"\{\{-?\s*(if|with|range|define)\b", s))
+        ends = len(re.findall(r"\{\{-?\s*end\s*-?\}\}", s))
+        assert opens == ends, f
+
+
+def test_images_entrypoints():
+    for f, exe in [("Dockerfile", "k8s-device-plugin"), ("labeller.Dockerfile", "k8s-node-labeller"),
+                   ("ubi-dp.Dockerfile", "k8s-device-plugin"), ("ubi-labeller.Dockerfile", "k8s-node-labeller")]:
+        s = (REPO / f).read_text()
+        assert f"CMD [\"./{exe}\"" in s, f
+        assert "WORKDIR /root" in s
+    assert "-pulse=30" in (REPO / "ubi-dp.Dockerfile").read_text()
+    for exe in ("k8s-device-plugin", "k8s-node-labeller"):
+        p = REPO / "scripts" / exe
+        assert os.access(p, os.X_OK)
+
+
+def test_examples_parse_and_request_gpus():
+    n = 0
+    for f in (REPO / "example").rglob("*.yaml"):
+        for d in yaml.safe_load_all(f.read_text()):
+            n += 1
+            assert "kind" in d
+    assert n >= 7
+    pod = _docs("example/pod/alexnet-gpu.yaml")[0]
+    assert pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == 1
