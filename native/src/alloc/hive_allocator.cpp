@@ -224,10 +224,11 @@ AllocResult HiveAllocator::allocate(const std::vector<std::string>& available,
   const int R = maxc + 1;
 
   // Aggregates. P[g][r]: internal weight of the first r members of g.
-  // C[(p*G+g)*R + r]: weight between the first r members of p and all of g.
   // Q[p][r]: weight between the first r members of p and the required set.
+  // C[(p*G+g)*R + r]: weight between the first r members of p and all of g,
+  // filled lazily per (p, g) row: requests that fit inside one GPU never
+  // touch it, which keeps small CPX requests at O(partitions^2).
   std::vector<int64_t> P(static_cast<size_t>(G) * R, 0), Q(static_cast<size_t>(G) * R, 0);
-  std::vector<int64_t> C(static_cast<size_t>(G) * G * R, 0);
   for (int p = 0; p < G; ++p) {
     const auto& mp = fg[p];
     for (int r = 1; r <= static_cast<int>(mp.size()); ++r) {
@@ -236,14 +237,27 @@ AllocResult HiveAllocator::allocate(const std::vector<std::string>& available,
       for (int q : req_idx) radd += W(mp[r - 1], q);
       P[p * R + r] = P[p * R + r - 1] + add;
       Q[p * R + r] = Q[p * R + r - 1] + radd;
-      for (int g = 0; g < G; ++g) {
-        if (g == p) continue;
-        int64_t c = 0;
-        for (int m : fg[g]) c += W(mp[r - 1], m);
-        C[(static_cast<size_t>(p) * G + g) * R + r] = C[(static_cast<size_t>(p) * G + g) * R + r - 1] + c;
-      }
     }
   }
+  std::vector<int64_t> C;
+  std::vector<char> c_ready;
+  auto cross = [&](int p, int g, int r) -> int64_t {
+    if (C.empty()) {
+      C.assign(static_cast<size_t>(G) * G * R, 0);
+      c_ready.assign(static_cast<size_t>(G) * G, 0);
+    }
+    const size_t row = static_cast<size_t>(p) * G + g;
+    if (!c_ready[row]) {
+      const auto& mp = fg[p];
+      for (int rr = 1; rr <= static_cast<int>(mp.size()); ++rr) {
+        int64_t c = 0;
+        for (int m : fg[g]) c += W(mp[rr - 1], m);
+        C[row * R + rr] = C[row * R + rr - 1] + c;
+      }
+      c_ready[row] = 1;
+    }
+    return C[row * R + r];
+  };
   int64_t RR = 0;
   for (size_t i = 0; i < req_idx.size(); ++i)
     for (size_t j = i + 1; j < req_idx.size(); ++j) RR += W(req_idx[i], req_idx[j]);
@@ -270,7 +284,7 @@ AllocResult HiveAllocator::allocate(const std::vector<std::string>& available,
       const int cp = static_cast<int>(fg[p].size());
       if (inS[p] || cp < r) continue;
       int64_t w = fw + RR + P[p * R + r] + Q[p * R + r];
-      for (int g : S) w += C[(static_cast<size_t>(p) * G + g) * R + r];
+      for (int g : S) w += cross(p, g, r);
       ++cands;
       if (best.found && w > best.w) continue;
       const int level = static_cast<int>(S.size()) + 1;
@@ -296,7 +310,7 @@ AllocResult HiveAllocator::allocate(const std::vector<std::string>& available,
       const int cg = static_cast<int>(fg[g].size());
       if (cnt + cg >= need) continue;
       int64_t nfw = fw + P[g * R + cg] + Q[g * R + cg];
-      for (int h : S) nfw += C[(static_cast<size_t>(g) * G + h) * R + cg];
+      for (int h : S) nfw += cross(g, h, cg);
       S.push_back(g);
       inS[g] = 1;
       self(self, g + 1, nfw, cnt + cg);
