@@ -10,6 +10,7 @@ from dataclasses import dataclass
 from typing import Iterable, List, Optional, Sequence
 
 from .ops.native import core
+from .utils.trace import TRACER
 
 
 class AllocationError(Exception):
@@ -71,7 +72,8 @@ class BestEffortPolicy(Policy):
 
     def allocate(self, available: Sequence[str], required: Sequence[str], size: int) -> List[str]:
         t0 = time.perf_counter()
-        r = self._alloc.allocate(list(available), list(required or ()), int(size))
+        with TRACER.span("allocator.allocate", "alloc", size=size, available=len(available)):
+            r = self._alloc.allocate(list(available), list(required or ()), int(size))
         dt = (time.perf_counter() - t0) * 1e6
         self.stats.calls += 1
         self.stats.total_us += dt

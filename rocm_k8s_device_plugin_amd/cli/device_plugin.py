@@ -53,6 +53,7 @@ def build_parser() -> flags.GoFlagParser:
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
     p.add_str("log_format", "glog", "glog | json")
+    p.add_str("trace_file", "", "write a Chrome trace of RPC / allocator / health spans to this file on exit")
     p.add_str("config", os.environ.get("CONFIG_FILE_PATH", ""), "YAML config file (gpu.device_count, ...)")
     return p
 
@@ -137,7 +138,12 @@ def main(argv: Optional[List[str]] = None) -> int:
     impl = select_impl(ns, device_count, logger)
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
                        metrics_port=ns.metrics_port)
-    asyncio.run(PluginManager(impl, mc).run())
+    from ..utils.trace import TRACER
+    TRACER.configure(ns.trace_file or None)
+    try:
+        asyncio.run(PluginManager(impl, mc).run())
+    finally:
+        TRACER.flush()
     return 0
 
 

@@ -22,6 +22,7 @@ from typing import Dict, Mapping, Optional, Sequence
 
 from ..ops.native import probe_executable
 from ..utils import log
+from ..utils.trace import TRACER
 
 _log = log.get("liveness")
 
@@ -101,7 +102,8 @@ class LivenessProber:
 
         async def one(o: int):
             async with sem:
-                return o, await self.probe_ordinal(o)
+                with TRACER.span("liveness.probe", "health", ordinal=o):
+                    return o, await self.probe_ordinal(o)
 
         results = dict(await asyncio.gather(*(one(o) for o in uniq)))
         self.sweeps += 1

@@ -30,6 +30,7 @@ from ..ops.native import core
 from ..proto import deviceplugin as dp
 from ..topology import Inventory, hip_ordinals
 from ..utils import log
+from ..utils.trace import TRACER
 from . import exporter
 from .liveness import LivenessProber
 
@@ -144,6 +145,10 @@ class HealthMonitor:
     # ------------------------------------------------------------------ sweep
     async def check_once(self) -> bool:
         """Run one sweep; returns True if any verdict changed."""
+        with TRACER.span("health.sweep", "health", devices=len(self.inv.devices)):
+            return await self._check_once()
+
+    async def _check_once(self) -> bool:
         t0 = time.perf_counter()
         reasons: Dict[str, list] = {d.id: [] for d in self.inv.devices}
         for dev, r in self._kfd_verdicts().items():

@@ -22,6 +22,7 @@ from ..proto import deviceplugin as pb
 from ..utils import log
 from ..utils.broadcast import Broadcast
 from ..utils.metrics import REGISTRY
+from ..utils.trace import TRACER
 from .base import DeviceImpl, DeviceImplError, PluginContext
 
 _log = log.get("plugin")
@@ -59,7 +60,9 @@ class DevicePluginServicer:
     async def GetPreferredAllocation(self, request, context):  # noqa: N802
         t0 = time.perf_counter()
         try:
-            return self.impl.preferred_allocation(self.ctx, request)
+            with TRACER.span("GetPreferredAllocation", "rpc", resource=self.ctx.resource,
+                             sizes=[c.allocation_size for c in request.container_requests]):
+                return self.impl.preferred_allocation(self.ctx, request)
         except DeviceImplError as e:
             _log.error("%s", e)
             REGISTRY.inc("mi355x_dp_rpc_errors_total", rpc="GetPreferredAllocation", resource=self.ctx.resource)
@@ -70,7 +73,8 @@ class DevicePluginServicer:
     async def Allocate(self, request, context):  # noqa: N802
         t0 = time.perf_counter()
         try:
-            resp = self.impl.allocate(self.ctx, request)
+            with TRACER.span("Allocate", "rpc", resource=self.ctx.resource):
+                resp = self.impl.allocate(self.ctx, request)
             for creq in request.container_requests:
                 _log.info("Allocating device IDs: %s", ",".join(creq.devices_ids))
             return resp
@@ -98,6 +102,7 @@ class DevicePluginServicer:
                 if not self.send_every_pulse and hv == last_health:
                     continue
                 last_health = hv
+                TRACER.instant("ListAndWatch.send", "rpc", resource=self.ctx.resource, health_version=hv)
                 yield pb.ListAndWatchResponse(devices=self.impl.update_health(self.ctx))
                 self.sent += 1
         finally:

@@ -466,3 +466,22 @@ def test_cli_config_file_device_count(tmp_path, monkeypatch):
     assert device_count_limit_from_env({"AMD_GPU_DEVICE_COUNT": "2"}) == 2
     assert device_count_limit_from_env({"AMD_GPU_DEVICE_COUNT": "x"}) is None
     assert device_count_limit_from_env({}) is None
+
+
+def test_trace_spans(tmp_path):
+    from rocm_k8s_device_plugin_amd.utils.trace import TRACER
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = container(fi)
+    TRACER.configure(str(tmp_path / "trace.json"))
+    try:
+        async def go():
+            async with plugin_env(tmp_path, impl) as (k, mgr):
+                await k.wait_for_resource("amd.com/gpu", 8)
+                await k.admit("amd.com/gpu", 3)
+        run(go())
+        TRACER.flush()
+        doc = json.loads((tmp_path / "trace.json").read_text())
+        names = {e["name"] for e in doc["traceEvents"]}
+        assert {"GetPreferredAllocation", "Allocate", "allocator.allocate"} <= names
+    finally:
+        TRACER.configure(None)
