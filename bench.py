@@ -85,6 +85,8 @@ class Dist:
             import torch.distributed as dist
             self.dist = dist
             if self.cuda:
+                # one rank per GPU over RCCL for the step barriers; object exchange
+                # (allocation -> ranks, ready timestamps -> rank 0) over a gloo group
                 self.torch.cuda.set_device(self.local_rank)
                 dist.init_process_group("nccl", device_id=self.torch.device("cuda", self.local_rank))
                 self.gloo = dist.new_group(backend="gloo")

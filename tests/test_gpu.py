@@ -211,3 +211,28 @@ def test_end_to_end_admission_container_ready(inv, ordinals):
     import tempfile
     with tempfile.TemporaryDirectory() as tmp:
         asyncio.run(asyncio.wait_for(go(tmp), 120))
+
+
+@pytest.mark.parametrize("runtime", ["hsa", "hip"])
+def test_rocprof_exactly_one_dispatch_per_probe(tmp_path, runtime):
+    """SURVEY §2.5 H1 verification: rocprofv3 sees exactly one kernel dispatch per device per probe."""
+    import csv
+    import shutil
+    if not shutil.which("rocprofv3"):
+        pytest.skip("rocprofv3 not available")
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    out = tmp_path / "prof"
+    env = dict(os.environ, TMPDIR="/tmp")
+    p = subprocess.run(["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", str(out), "-o", "probe",
+                        "--", str(probe_executable(runtime)), "--devices", "all"], capture_output=True,
+                       timeout=300, env=env, cwd="/tmp")
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    traces = list(out.rglob("*kernel_trace.csv"))
+    assert traces, list(out.rglob("*"))
+    rows = list(csv.DictReader(open(traces[0])))
+    names = [r["Kernel_Name"] for r in rows]
+    doc = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    assert names == ["mi355x_mfma_liveness"] * len(doc["devices"]), names
+    r = rows[0]
+    assert (r["Workgroup_Size_X"], r["Grid_Size_X"]) == ("64", "64")
+    assert int(r["LDS_Block_Size"]) == 0 and int(r["Scratch_Size"]) == 0
