@@ -52,6 +52,8 @@ def build_parser() -> flags.GoFlagParser:
     p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
+    p.add_bool("topology_view", False, "experimental: bind-mount a kfd topology filtered to the allocated "
+                                       "GPUs into each container (faster ROCr start-up, GPU isolation)")
     p.add_str("log_format", "glog", "glog | json")
     p.add_str("trace_file", "", "write a Chrome trace of RPC / allocator / health spans to this file on exit")
     p.add_str("config", os.environ.get("CONFIG_FILE_PATH", ""), "YAML config file (gpu.device_count, ...)")
@@ -88,7 +90,9 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
         hc = HealthConfig(exporter_socket=ns.exporter_socket or None, liveness=ns.liveness,
                           liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
                           smi_ecc=ns.smi_ecc, dev_root=ns.dev_root)
-        return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count)
+        view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
+        return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count,
+                             topology_view_dir=view_dir)
     if name == C.VF_PASSTHROUGH:
         from ..plugin.passthrough import VfImpl
         return VfImpl(ns.resource_naming_strategy, ns.sysfs_root, ns.exporter_socket or None)

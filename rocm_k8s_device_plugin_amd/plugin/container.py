@@ -22,6 +22,7 @@ from ..allocator import AllocationError
 from ..health.monitor import HealthConfig, HealthMonitor
 from ..proto import deviceplugin as pb
 from ..topology import Gpu, Inventory, discover
+from ..topology_view import KFD_TOPOLOGY_CONTAINER_PATH, TopologyViews
 from ..utils import log
 from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto
 
@@ -33,9 +34,13 @@ class ContainerImpl(DeviceImpl):
 
     def __init__(self, naming_strategy: str = C.STRATEGY_SINGLE, sysfs_root: str = "/sys",
                  health_cfg: Optional[HealthConfig] = None, device_count_limit: Optional[int] = None,
-                 inventory: Optional[Inventory] = None, monitor: Optional[HealthMonitor] = None):
+                 inventory: Optional[Inventory] = None, monitor: Optional[HealthMonitor] = None,
+                 topology_view_dir: Optional[str] = None):
         self.strategy = naming_strategy
         self.sysfs_root = sysfs_root
+        # opt-in: per-allocation filtered kfd topology bind-mounted into the container
+        self.topology_views = (TopologyViews(topology_view_dir, os.path.join(sysfs_root, "class/kfd/kfd/topology"))
+                               if topology_view_dir else None)
         if not os.path.exists(os.path.join(sysfs_root, C.KFD_CLASS_REL)):
             raise DeviceImplError("No amd gpu driver loaded")
         self.inv = inventory or discover(sysfs_root, device_count_limit)
@@ -120,12 +125,20 @@ class ContainerImpl(DeviceImpl):
             car = resp.container_responses.add()
             # one /dev/kfd per container regardless of the number of GPUs
             car.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
+            nodes = []
             for dev_id in creq.devices_ids:
                 d = self.inv.by_id.get(dev_id)
                 if d is None:
                     raise DeviceImplError(f"unknown device ID {dev_id!r} for resource {ctx.resource}")
                 for p in d.dev_paths():
                     car.devices.add(container_path=p, host_path=p, permissions="rw")
+                nodes.append(d.node_id)
+            if self.topology_views is not None and creq.devices_ids and all(n >= 0 for n in nodes):
+                try:
+                    view = self.topology_views.get(nodes)
+                    car.mounts.add(container_path=KFD_TOPOLOGY_CONTAINER_PATH, host_path=view, read_only=True)
+                except OSError as e:  # never fail an admission over an optimisation
+                    _log.warning("topology view for %s unavailable: %s", list(creq.devices_ids), e)
         return resp
 
     def preferred_allocation(self, ctx: PluginContext,
