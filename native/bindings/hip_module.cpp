@@ -26,6 +26,12 @@ py::dict to_dict(const mi355x_probe_result& r) {
   d["setup_us"] = r.setup_us;
   d["kernel_us"] = r.kernel_us;
   d["total_us"] = r.total_us;
+  py::dict ph;
+  ph["code_object"] = r.phase_us[0];
+  ph["queue"] = r.phase_us[1];
+  ph["buffers"] = r.phase_us[2];
+  ph["dispatch_wait"] = r.phase_us[3];
+  d["phase_us"] = ph;
   d["pci_bus_id"] = std::string(r.pci_bus_id);
   d["arch"] = std::string(r.arch);
   d["name"] = std::string(r.name);

@@ -62,6 +62,7 @@ struct Runtime {
   hsa_amd_memory_pool_t fine{};
   bool has_kernarg = false, has_fine = false;
   uint64_t ts_freq = 0;
+  double init_us[3] = {0, 0, 0};
 } g_rt;
 
 hsa_status_t collect_agent(hsa_agent_t a, void*) {
@@ -157,16 +158,30 @@ extern "C" int mi355x_hsa_probe_init(void) {
   if (g_rt.inited) return g_rt.init_status == HSA_STATUS_SUCCESS ? static_cast<int>(g_rt.gpus.size())
                                                                   : -static_cast<int>(g_rt.init_status);
   g_rt.inited = true;
+  using clk = std::chrono::steady_clock;
+  auto us = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double, std::micro>(b - a).count();
+  };
+  const auto t0 = clk::now();
   hsa_status_t s = hsa_init();
+  const auto t1 = clk::now();
+  g_rt.init_us[0] = us(t0, t1);
   if (s != HSA_STATUS_SUCCESS) {
     g_rt.init_status = s;
     return -static_cast<int>(s);
   }
   hsa_iterate_agents(collect_agent, nullptr);
+  const auto t2 = clk::now();
   if (g_rt.cpu.handle) hsa_amd_agent_iterate_memory_pools(g_rt.cpu, cpu_pool, nullptr);
   for (auto& ag : g_rt.gpus) hsa_amd_agent_iterate_memory_pools(ag.agent, gpu_pool, &ag);
   hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_rt.ts_freq);
+  g_rt.init_us[1] = us(t1, t2);
+  g_rt.init_us[2] = us(t2, clk::now());
   return static_cast<int>(g_rt.gpus.size());
+}
+
+extern "C" void mi355x_hsa_init_phases(double out_us[3]) {
+  for (int i = 0; i < 3; ++i) out_us[i] = g_rt.init_us[i];
 }
 
 extern "C" void mi355x_hsa_probe_shutdown(void) {
@@ -244,6 +259,12 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     }                           \
   } while (0)
 
+  auto t_phase = clk::now();
+  auto mark = [&](int i) {
+    const auto now = clk::now();
+    out->phase_us[i] = std::chrono::duration<double, std::micro>(now - t_phase).count();
+    t_phase = now;
+  };
   HSA_CHECK(hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader), "code object reader");
   HSA_CHECK(hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe),
             "executable create");
@@ -260,10 +281,12 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     goto done;
   }
 
+  mark(0);
   HSA_CHECK(hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &queue),
             "queue create");
   hsa_amd_profiling_set_profiler_enabled(queue, 1);
   HSA_CHECK(hsa_signal_create(1, 0, nullptr, &sig), "signal create");
+  mark(1);
   HSA_CHECK(hsa_amd_memory_pool_allocate(g_rt.fine, MI355X_PROBE_OUT * sizeof(float), 0,
                                          reinterpret_cast<void**>(&h_out)),
             "alloc out");
@@ -284,6 +307,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
   kargs->scratch = d_scratch;
   kargs->nonce = nonce;
   kargs->iters = out->iters;
+  mark(2);
   t_setup = clk::now();
 
   {
@@ -324,6 +348,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
       out->hip_error = -1;
       goto done;
     }
+    mark(3);
   }
   {
     hsa_amd_profiling_dispatch_time_t dt{};

@@ -10,6 +10,7 @@
 // Exit status: 0 all probed devices live, 1 at least one failed, 2 usage or
 // HIP runtime unavailable. The parent (the plugin's health loop, or the
 // benchmark's fake container runtime) enforces the deadline by killing us.
+#include <sys/resource.h>
 #include <time.h>
 
 #include <cstdio>
@@ -21,6 +22,12 @@
 #include "mi355x/liveness_probe.h"
 
 namespace {
+
+double cpu_ms() {
+  rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  return (ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e3 + (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) / 1e3;
+}
 
 uint64_t mono_ns() {
   timespec ts;
@@ -50,11 +57,14 @@ void print_device(const mi355x_probe_result& r, bool last) {
   std::printf(
       "{\"ordinal\":%d,\"ok\":%s,\"hip_error\":%d,\"mismatches\":%d,\"nonce\":%u,\"xcc_id\":%u,"
       "\"hw_id\":%u,\"iters\":%d,\"dispatches\":%d,\"kfd_node_id\":%d,\"runtime\":\"%s\","
-      "\"kernel_us\":%.3f,\"setup_us\":%.3f,\"total_us\":%.3f,\"pci_bus_id\":\"%s\","
+      "\"kernel_us\":%.3f,\"setup_us\":%.3f,\"total_us\":%.3f,"
+      "\"phase_us\":{\"code_object\":%.1f,\"queue\":%.1f,\"buffers\":%.1f,\"dispatch_wait\":%.1f},"
+      "\"pci_bus_id\":\"%s\","
       "\"arch\":\"%s\",\"name\":\"%s\",\"uuid\":\"%s\",\"pci_domain\":%d,\"pci_bus\":%d,"
       "\"pci_device\":%d,\"cu_count\":%d,\"total_mem\":%llu,\"error\":\"%s\"}%s",
       r.ordinal, r.ok ? "true" : "false", r.hip_error, r.mismatches, r.nonce, r.xcc_id, r.hw_id, r.iters,
-      r.dispatches, r.kfd_node_id, r.runtime, r.kernel_us, r.setup_us, r.total_us, json_escape(r.pci_bus_id).c_str(), json_escape(r.arch).c_str(),
+      r.dispatches, r.kfd_node_id, r.runtime, r.kernel_us, r.setup_us, r.total_us, r.phase_us[0], r.phase_us[1],
+      r.phase_us[2], r.phase_us[3], json_escape(r.pci_bus_id).c_str(), json_escape(r.arch).c_str(),
       json_escape(r.name).c_str(), json_escape(r.uuid).c_str(), r.pci_domain, r.pci_bus, r.pci_device,
       r.cu_count, static_cast<unsigned long long>(r.total_mem), json_escape(r.error).c_str(), last ? "" : ",");
 }
@@ -65,7 +75,9 @@ int probe(int o, uint32_t nonce, int iters, double timeout_s, mi355x_probe_resul
   return mi355x_hsa_probe_device(o, nonce, iters, timeout_s, r);
 }
 int identify_dev(int o, mi355x_probe_result* r) { return mi355x_hsa_probe_identify(o, r); }
+void init_phases(double out[3]) { mi355x_hsa_init_phases(out); }
 #else
+void init_phases(double out[3]) { out[0] = out[1] = out[2] = 0; }
 int device_count() { return mi355x_probe_device_count(); }
 int probe(int o, uint32_t nonce, int iters, double, mi355x_probe_result* r) {
   return mi355x_probe_device(o, nonce, iters, r);
@@ -113,6 +125,9 @@ int main(int argc, char** argv) {
 
   const int n = device_count();
   const uint64_t t_runtime = mono_ns();  // HIP runtime + ROCr initialised
+  const double cpu_runtime = cpu_ms();
+  double iph[3];
+  init_phases(iph);
   if (n < 0) {
     std::printf("{\"ok\":false,\"hip_device_count\":0,\"error\":\"GPU runtime init failed (%d)\",\"devices\":[],"
                 "\"t_start_ns\":%llu,\"t_ready_ns\":0}\n",
@@ -149,10 +164,13 @@ int main(int argc, char** argv) {
     if (rc != 0) all_ok = false;
   }
   const uint64_t t_ready = mono_ns();
+  const double cpu_ready = cpu_ms();
   std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
-              "\"t_ready_ns\":%llu,\"devices\":[",
+              "\"t_ready_ns\":%llu,\"cpu_ms_runtime\":%.2f,\"cpu_ms_ready\":%.2f,"
+              "\"init_us\":{\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"devices\":[",
               all_ok ? "true" : "false", n, identify ? "true" : "false", static_cast<unsigned long long>(t_start),
-              static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(t_ready));
+              static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(t_ready), cpu_runtime,
+              cpu_ready, iph[0], iph[1], iph[2]);
   for (size_t i = 0; i < results.size(); ++i) print_device(results[i], i + 1 == results.size());
   std::printf("]}\n");
   std::fflush(stdout);

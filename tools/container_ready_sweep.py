@@ -50,6 +50,11 @@ def run_once(env_extra, args, runtime="hsa"):
         "exit_ms": (t1 - t0) / 1e6,
         "kernel_us": doc["devices"][0]["kernel_us"] if doc["devices"] else 0.0,
         "setup_us": doc["devices"][0].get("setup_us", 0.0) if doc["devices"] else 0.0,
+        # ROCr start-up split (HSA build) and the process' CPU time up to each point
+        "init_us": doc.get("init_us", {}),
+        "phase_us": doc["devices"][0].get("phase_us", {}) if doc["devices"] else {},
+        "cpu_ms_runtime": doc.get("cpu_ms_runtime", 0.0),
+        "cpu_ms_ready": doc.get("cpu_ms_ready", 0.0),
     }
 
 
@@ -74,7 +79,14 @@ def main():
     for name, env, rt in plan:
         extra = ["--identify"] if name.endswith("identify_only") else []
         runs = [run_once(env, extra, rt) for _ in range(a.reps)]
-        row = {k: round(statistics.median(r[k] for r in runs), 3) for k in runs[0] if k != "ok"}
+        row = {}
+        for k, v in runs[0].items():
+            if k == "ok":
+                continue
+            if isinstance(v, dict):
+                row[k] = {kk: round(statistics.median(r[k].get(kk, 0.0) for r in runs), 1) for kk in v}
+            else:
+                row[k] = round(statistics.median(r[k] for r in runs), 3)
         row["all_ok"] = all(r["ok"] for r in runs)
         row["ready_ms_min"] = round(min(r["ready_ms"] for r in runs), 3)
         table[name] = row
