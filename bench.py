@@ -14,7 +14,13 @@ GPUs advertised at 1/2/4/8 MI355X"). One timed step is one pod admission:
   3. each container initialises HIP and runs the gfx950 MFMA liveness kernel
      on its GPU; it is "ready" when the tile verifies bit-exactly;
   4. latency = (last container ready) - (kubelet starts GetPreferredAllocation),
-     both on CLOCK_MONOTONIC.
+     both on CLOCK_MONOTONIC;
+  5. (untimed in the latency, inside the timed loop) the pod terminates: its
+     processes exit and the driver tears down their kfd processes. The next
+     admission starts once /sys/class/kfd/kfd/proc no longer lists them
+     (--settle kfd); with --settle none it would start inside that teardown and
+     block ~100-150 ms in open("/dev/kfd") (profiles/README.md §3c) — reported
+     as latency_p50_ms_back_to_back.
 
 The plugin is the real one (real /sys discovery, real C++ allocator, real
 gRPC servicer); only kubelet and the CRI runtime are stand-ins (see
@@ -54,6 +60,11 @@ def parse_args():
                     help="how the container entrypoint reaches the GPU: ROCr-direct or the HIP runtime")
     ap.add_argument("--hip-compare", type=int, default=5,
                     help="extra untimed admissions with HIP-runtime containers, reported for comparison")
+    ap.add_argument("--settle", default="kfd", choices=["kfd", "none"],
+                    help="between admissions wait until the previous containers' kfd processes are torn down "
+                         "(the previous pod has terminated) or start the next one immediately")
+    ap.add_argument("--b2b-compare", type=int, default=5,
+                    help="extra untimed admissions with --settle none, reported for comparison")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -183,9 +194,10 @@ def main():
         gpu_info = None
 
     rpc_ms, alloc_rpc_ms, lat_ms, ready_ms, kern_us = [], [], [], [], []
-    exec_ms, rt_ms, dev_ms = [], [], []
+    exec_ms, rt_ms, dev_ms, settle_ms = [], [], [], []
+    from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
 
-    def one_step(record: bool, runtime: str = args.container_runtime, sink=None):
+    def one_step(record: bool, runtime: str = args.container_runtime, sink=None, settle: str = args.settle):
         nonlocal step_payload
         if d.rank == 0:
             t0 = time.monotonic_ns()
@@ -203,12 +215,14 @@ def main():
             subprocess.run(["/bin/true"])
             tr = time.monotonic_ns()
             mine = (True, tr, 0.0, "", (ts, ts, tr))
+            lingering = frozenset()
         else:
             mine_ord = [ordl[d.rank]] if d.world > 1 else ordl
             r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
             phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
+            lingering = r.kfd_lingering
         allr = d.gather(mine)
         bad = [m[3] for m in allr if not m[0]]
         if bad:
@@ -217,6 +231,11 @@ def main():
         t_ready = slowest[1]
         if d.rank == 0:
             kubelet.release("amd.com/gpu", ids)
+        # pod termination: the driver finishes tearing down each container's
+        # kfd process ~150 ms after it exits (bench latency excludes this wait)
+        waited = wait_kfd_released(lingering) if settle == "kfd" else 0.0
+        if record:
+            settle_ms.append(waited)
         if sink is not None:
             sink.append((t_ready - t0) / 1e6)
         if record:
@@ -239,10 +258,13 @@ def main():
     d.sync()
     elapsed = time.perf_counter() - t_start
     elapsed = d.max(elapsed)
-    hip_lat = []
+    hip_lat, b2b_lat = [], []
     if not args.fixture and args.container_runtime == "hsa":
         for _ in range(args.hip_compare):
             one_step(False, runtime="hip", sink=hip_lat)
+    if not args.fixture and args.settle == "kfd":
+        for _ in range(args.b2b_compare):
+            one_step(False, sink=b2b_lat, settle="none")
 
     extra = {}
     if d.rank == 0:
@@ -263,6 +285,8 @@ def main():
                  "latency_p99_ms": round(pct(lat_ms, .99), 3), "latency_mean_ms": round(statistics.mean(lat_ms), 3),
                  "container_runtime": args.container_runtime,
                  "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
+                 "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
+                 "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
                  "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
                  "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
                                              "hip_runtime_init": round(pct(rt_ms, .5), 3),
@@ -290,7 +314,9 @@ def main():
                      if not args.fixture else "synthetic 8xMI355X sysfs fixture; no-op containers (CPU only)"),
             "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
                        "global_batch": n, "seq_len": None,
-                       "parallelism": f"{n} GPUs advertised, 1 pod requesting {n}, 1 container process per GPU"},
+                       "parallelism": f"{n} GPUs advertised, 1 pod requesting {n}, 1 container process per GPU",
+                       "between_admissions": ("previous pod's kfd teardown complete" if args.settle == "kfd"
+                                              else "back-to-back")},
             "extra": extra,
         }
         line = json.dumps(out)

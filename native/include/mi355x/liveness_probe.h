@@ -30,8 +30,9 @@ typedef struct {
   double kernel_us;       // dispatch start->end (HSA profiling) or hipEvent time
   double setup_us;        // code object load + queue/stream + buffers
   double total_us;        // everything for this device, including verify
-  // HSA path phases (us): 0 code object load+freeze, 1 queue+signal, 2 buffers,
-  // 3 doorbell -> completion signal observed on the host
+  // HSA path phases (us): 0 code object load+freeze, 1 queue+signal+buffers
+  // (on a helper thread, overlapped with 0), 2 unused, 3 doorbell -> completion
+  // signal observed on the host
   double phase_us[4];
   char runtime[8];        // "hsa" | "hip"
   char pci_bus_id[32];    // dddd:bb:dd.f
@@ -56,6 +57,11 @@ int mi355x_hsa_probe_init(void);
 int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, double timeout_s, mi355x_probe_result* out);
 int mi355x_hsa_probe_identify(int ordinal, mi355x_probe_result* out);
 void mi355x_hsa_probe_shutdown(void);
+// With defer on, probe resources (queue, executable, buffers) outlive the
+// verdict until mi355x_hsa_probe_release(): a caller that reports readiness
+// takes teardown off its critical path.
+void mi355x_hsa_probe_defer_release(int on);
+void mi355x_hsa_probe_release(void);
 // Runtime start-up split of the last mi355x_hsa_probe_init (us): hsa_init,
 // agent enumeration, memory-pool discovery.
 void mi355x_hsa_init_phases(double out_us[3]);

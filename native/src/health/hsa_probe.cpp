@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "liveness_kernel.h"
@@ -185,6 +186,7 @@ extern "C" void mi355x_hsa_init_phases(double out_us[3]) {
 }
 
 extern "C" void mi355x_hsa_probe_shutdown(void) {
+  mi355x_hsa_probe_release();
   std::lock_guard<std::mutex> lk(g_rt.mu);
   if (g_rt.inited && g_rt.init_status == HSA_STATUS_SUCCESS) hsa_shut_down();
   g_rt.inited = false;
@@ -209,15 +211,126 @@ extern "C" int mi355x_hsa_probe_identify(int ordinal, mi355x_probe_result* out) 
   return 0;
 }
 
+namespace {
+
+// Everything one probe allocates. Released right after the verdict, or — for
+// the container entrypoint, which reports "ready" as soon as the verdict is
+// known — after the JSON line is out (mi355x_hsa_probe_defer_release).
+struct ProbeResources {
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t sig{};
+  float* h_out = nullptr;
+  uint32_t* h_meta = nullptr;
+  float* d_scratch = nullptr;
+  mi355x_liveness_args* kargs = nullptr;
+
+  void release() {
+    if (kargs) hsa_amd_memory_pool_free(kargs);
+    if (d_scratch) hsa_amd_memory_pool_free(d_scratch);
+    if (h_meta) hsa_amd_memory_pool_free(h_meta);
+    if (h_out) hsa_amd_memory_pool_free(h_out);
+    if (sig.handle) hsa_signal_destroy(sig);
+    if (queue) hsa_queue_destroy(queue);
+    if (exe.handle) hsa_executable_destroy(exe);
+    if (reader.handle) hsa_code_object_reader_destroy(reader);
+    *this = ProbeResources{};
+  }
+};
+
+std::mutex g_deferred_mu;
+bool g_defer_release = false;
+std::vector<ProbeResources> g_deferred;
+
+// kernarg buffer size; the code object's segment size is checked against it
+constexpr uint32_t kKernargBytes = 256;
+
+struct Step {
+  hsa_status_t s = HSA_STATUS_SUCCESS;
+  const char* what = nullptr;
+  bool ok() const { return s == HSA_STATUS_SUCCESS; }
+};
+
+#define STEP(st, expr, label)         \
+  do {                                \
+    (st).s = (expr);                  \
+    if ((st).s != HSA_STATUS_SUCCESS) { \
+      (st).what = (label);            \
+      return st;                      \
+    }                                 \
+  } while (0)
+
+// Queue, completion signal and buffers: independent of the code object, so it
+// runs on a helper thread while the main thread loads the executable (both are
+// a few ms of driver work each on MI355X).
+Step make_queue_and_buffers(const Agent& ag, ProbeResources& r) {
+  Step st;
+  STEP(st, hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &r.queue),
+       "queue create");
+  hsa_amd_profiling_set_profiler_enabled(r.queue, 1);
+  STEP(st, hsa_signal_create(1, 0, nullptr, &r.sig), "signal create");
+  STEP(st, hsa_amd_memory_pool_allocate(g_rt.fine, MI355X_PROBE_OUT * sizeof(float), 0,
+                                        reinterpret_cast<void**>(&r.h_out)), "alloc out");
+  STEP(st, hsa_amd_memory_pool_allocate(g_rt.fine, 64, 0, reinterpret_cast<void**>(&r.h_meta)), "alloc meta");
+  STEP(st, hsa_amd_memory_pool_allocate(ag.coarse, MI355X_SCRATCH_FLOATS * sizeof(float), 0,
+                                        reinterpret_cast<void**>(&r.d_scratch)), "alloc scratch");
+  STEP(st, hsa_amd_memory_pool_allocate(g_rt.kernarg, kKernargBytes, 0, reinterpret_cast<void**>(&r.kargs)),
+       "alloc kernarg");
+  STEP(st, hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.h_out), "allow out");
+  STEP(st, hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.h_meta), "allow meta");
+  STEP(st, hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.kargs), "allow kernarg");
+  return st;
+}
+
+struct KernelInfo {
+  uint64_t kobj = 0;
+  uint32_t kseg = 0, gseg = 0, pseg = 0;
+};
+
+Step load_kernel(const Agent& ag, ProbeResources& r, KernelInfo& k) {
+  Step st;
+  const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
+  STEP(st, hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &r.reader), "code object reader");
+  STEP(st, hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &r.exe),
+       "executable create");
+  STEP(st, hsa_executable_load_agent_code_object(r.exe, ag.agent, r.reader, nullptr, nullptr), "load code object");
+  STEP(st, hsa_executable_freeze(r.exe, nullptr), "executable freeze");
+  hsa_executable_symbol_t sym{};
+  STEP(st, hsa_executable_get_symbol_by_name(r.exe, "mi355x_mfma_liveness.kd", &ag.agent, &sym), "kernel symbol");
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.kobj);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kseg);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.gseg);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.pseg);
+  return st;
+}
+#undef STEP
+
+}  // namespace
+
+extern "C" void mi355x_hsa_probe_defer_release(int on) {
+  std::lock_guard<std::mutex> lk(g_deferred_mu);
+  g_defer_release = on != 0;
+}
+
+extern "C" void mi355x_hsa_probe_release(void) {
+  std::vector<ProbeResources> todo;
+  {
+    std::lock_guard<std::mutex> lk(g_deferred_mu);
+    todo.swap(g_deferred);
+  }
+  for (auto& r : todo) r.release();
+}
+
 extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, double timeout_s,
                                        mi355x_probe_result* out) {
   using clk = std::chrono::steady_clock;
+  auto us_since = [](clk::time_point a) { return std::chrono::duration<double, std::micro>(clk::now() - a).count(); };
   std::memset(out, 0, sizeof(*out));
   out->kfd_node_id = -1;
   out->nonce = nonce;
   out->iters = iters < 1 ? 1 : iters;
   const auto t0 = clk::now();
-  auto t_setup = t0;
   int n = mi355x_hsa_probe_init();
   if (n < 0) {
     set_status(out, static_cast<hsa_status_t>(-n), "hsa_init");
@@ -236,83 +349,40 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     return 1;
   }
 
-  hsa_code_object_reader_t reader{};
-  hsa_executable_t exe{};
-  hsa_queue_t* queue = nullptr;
-  hsa_signal_t sig{};
-  float* h_out = nullptr;
-  uint32_t* h_meta = nullptr;
-  float* d_scratch = nullptr;
-  mi355x_liveness_args* kargs = nullptr;
-  uint64_t kobj = 0;
-  uint32_t kseg = 0, gseg = 0, pseg = 0;
-  hsa_executable_symbol_t sym{};
-  hsa_status_t s;
-  const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
+  ProbeResources r;
+  KernelInfo k;
+  Step qst, kst;
+  double queue_us = 0;
+  std::thread qthread([&] {
+    const auto tq = clk::now();
+    qst = make_queue_and_buffers(ag, r);
+    queue_us = us_since(tq);
+  });
+  kst = load_kernel(ag, r, k);
+  out->phase_us[0] = us_since(t0);  // code object load + freeze
+  qthread.join();
+  out->phase_us[1] = queue_us;      // queue + signal + buffers (overlapped with phase 0)
+  const auto t_setup = clk::now();
+  out->setup_us = std::chrono::duration<double, std::micro>(t_setup - t0).count();
+  out->phase_us[2] = 0;
+  if (!kst.ok() || !qst.ok()) {
+    const Step& bad = !kst.ok() ? kst : qst;
+    set_status(out, bad.s, bad.what);
+  } else if (k.kseg < sizeof(mi355x_liveness_args) || k.kseg > kKernargBytes) {
+    std::snprintf(out->error, sizeof(out->error), "kernarg segment %u outside [%zu, %u]: code object / host ABI mismatch",
+                  k.kseg, sizeof(mi355x_liveness_args), kKernargBytes);
+  } else {
+    std::memset(r.h_out, 0xFF, MI355X_PROBE_OUT * sizeof(float));
+    std::memset(r.h_meta, 0, 64);
+    std::memset(r.kargs, 0, kKernargBytes);
+    r.kargs->out = r.h_out;
+    r.kargs->meta = r.h_meta;
+    r.kargs->scratch = r.d_scratch;
+    r.kargs->nonce = nonce;
+    r.kargs->iters = out->iters;
 
-#define HSA_CHECK(expr, what)   \
-  do {                          \
-    s = (expr);                 \
-    if (s != HSA_STATUS_SUCCESS) { \
-      set_status(out, s, what); \
-      goto done;                \
-    }                           \
-  } while (0)
-
-  auto t_phase = clk::now();
-  auto mark = [&](int i) {
-    const auto now = clk::now();
-    out->phase_us[i] = std::chrono::duration<double, std::micro>(now - t_phase).count();
-    t_phase = now;
-  };
-  HSA_CHECK(hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader), "code object reader");
-  HSA_CHECK(hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe),
-            "executable create");
-  HSA_CHECK(hsa_executable_load_agent_code_object(exe, ag.agent, reader, nullptr, nullptr), "load code object");
-  HSA_CHECK(hsa_executable_freeze(exe, nullptr), "executable freeze");
-  HSA_CHECK(hsa_executable_get_symbol_by_name(exe, "mi355x_mfma_liveness.kd", &ag.agent, &sym), "kernel symbol");
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &kobj);
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kseg);
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &gseg);
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &pseg);
-  if (kseg < sizeof(mi355x_liveness_args)) {
-    std::snprintf(out->error, sizeof(out->error), "kernarg segment %u < %zu: code object / host ABI mismatch",
-                  kseg, sizeof(mi355x_liveness_args));
-    goto done;
-  }
-
-  mark(0);
-  HSA_CHECK(hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &queue),
-            "queue create");
-  hsa_amd_profiling_set_profiler_enabled(queue, 1);
-  HSA_CHECK(hsa_signal_create(1, 0, nullptr, &sig), "signal create");
-  mark(1);
-  HSA_CHECK(hsa_amd_memory_pool_allocate(g_rt.fine, MI355X_PROBE_OUT * sizeof(float), 0,
-                                         reinterpret_cast<void**>(&h_out)),
-            "alloc out");
-  HSA_CHECK(hsa_amd_memory_pool_allocate(g_rt.fine, 64, 0, reinterpret_cast<void**>(&h_meta)), "alloc meta");
-  HSA_CHECK(hsa_amd_memory_pool_allocate(ag.coarse, MI355X_SCRATCH_FLOATS * sizeof(float), 0,
-                                         reinterpret_cast<void**>(&d_scratch)),
-            "alloc scratch");
-  HSA_CHECK(hsa_amd_memory_pool_allocate(g_rt.kernarg, kseg < 64 ? 64 : kseg, 0, reinterpret_cast<void**>(&kargs)),
-            "alloc kernarg");
-  HSA_CHECK(hsa_amd_agents_allow_access(1, &ag.agent, nullptr, h_out), "allow out");
-  HSA_CHECK(hsa_amd_agents_allow_access(1, &ag.agent, nullptr, h_meta), "allow meta");
-  HSA_CHECK(hsa_amd_agents_allow_access(1, &ag.agent, nullptr, kargs), "allow kernarg");
-  std::memset(h_out, 0xFF, MI355X_PROBE_OUT * sizeof(float));
-  std::memset(h_meta, 0, 64);
-  std::memset(kargs, 0, kseg);
-  kargs->out = h_out;
-  kargs->meta = h_meta;
-  kargs->scratch = d_scratch;
-  kargs->nonce = nonce;
-  kargs->iters = out->iters;
-  mark(2);
-  t_setup = clk::now();
-
-  {
-    const uint64_t idx = hsa_queue_add_write_index_screlease(queue, 1);
-    auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address) + (idx & (queue->size - 1));
+    const uint64_t idx = hsa_queue_add_write_index_screlease(r.queue, 1);
+    auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(r.queue->base_address) + (idx & (r.queue->size - 1));
     std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
     pkt->workgroup_size_x = 64;
     pkt->workgroup_size_y = 1;
@@ -320,11 +390,11 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     pkt->grid_size_x = 64;
     pkt->grid_size_y = 1;
     pkt->grid_size_z = 1;
-    pkt->private_segment_size = pseg;
-    pkt->group_segment_size = gseg;
-    pkt->kernel_object = kobj;
-    pkt->kernarg_address = kargs;
-    pkt->completion_signal = sig;
+    pkt->private_segment_size = k.pseg;
+    pkt->group_segment_size = k.gseg;
+    pkt->kernel_object = k.kobj;
+    pkt->kernarg_address = r.kargs;
+    pkt->completion_signal = r.sig;
     const uint16_t header = static_cast<uint16_t>(
         (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
         (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
@@ -332,42 +402,36 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
                      __ATOMIC_RELEASE);
-    hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+    hsa_signal_store_screlease(r.queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
     out->dispatches = 1;
-  }
-  {
+
     // bounded wait: a wedged device must come back as a verdict, not a hang
     const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
     hsa_signal_value_t v = 1;
-    while ((v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
+    while ((v = hsa_signal_wait_scacquire(r.sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
                                           HSA_WAIT_STATE_BLOCKED)) >= 1) {
       if (clk::now() > deadline) break;
     }
+    out->phase_us[3] = us_since(t_setup);
     if (v >= 1) {
       std::snprintf(out->error, sizeof(out->error), "dispatch did not complete within %.1fs", timeout_s);
       out->hip_error = -1;
-      goto done;
+    } else {
+      hsa_amd_profiling_dispatch_time_t dt{};
+      if (hsa_amd_profiling_get_dispatch_time(ag.agent, r.sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
+        out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
+      mi355x::verify_tile(r.h_out, r.h_meta, nonce, out->iters, out);
     }
-    mark(3);
   }
-  {
-    hsa_amd_profiling_dispatch_time_t dt{};
-    if (hsa_amd_profiling_get_dispatch_time(ag.agent, sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
-      out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
-  }
-  mi355x::verify_tile(h_out, h_meta, nonce, out->iters, out);
-
-done:
-  out->setup_us = std::chrono::duration<double, std::micro>(t_setup - t0).count();
-  if (kargs) hsa_amd_memory_pool_free(kargs);
-  if (d_scratch) hsa_amd_memory_pool_free(d_scratch);
-  if (h_meta) hsa_amd_memory_pool_free(h_meta);
-  if (h_out) hsa_amd_memory_pool_free(h_out);
-  if (sig.handle) hsa_signal_destroy(sig);
-  if (queue) hsa_queue_destroy(queue);
-  if (exe.handle) hsa_executable_destroy(exe);
-  if (reader.handle) hsa_code_object_reader_destroy(reader);
   out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
-#undef HSA_CHECK
+  {
+    std::unique_lock<std::mutex> lk(g_deferred_mu);
+    // a timed-out dispatch may still be running: never free what it can write
+    if (g_defer_release || out->hip_error == -1) {
+      if (out->hip_error != -1) g_deferred.push_back(r);
+      return out->ok ? 0 : 1;
+    }
+  }
+  r.release();
   return out->ok ? 0 : 1;
 }

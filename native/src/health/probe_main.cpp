@@ -2,6 +2,7 @@
 // and print one JSON document.
 //
 //   mi355x-liveness-probe [--devices all|0,2,..] [--nonce N] [--iters N] [--identify] [--timeout S]
+//   mi355x-liveness-probe --serve      (long-lived; requests on stdin, see serve())
 //
 // Built twice from this file: `mi355x-liveness-probe` launches through ROCr
 // directly (MI355X_PROBE_HSA; links only libhsa-runtime64, one AQL dispatch),
@@ -10,15 +11,20 @@
 // Exit status: 0 all probed devices live, 1 at least one failed, 2 usage or
 // HIP runtime unavailable. The parent (the plugin's health loop, or the
 // benchmark's fake container runtime) enforces the deadline by killing us.
+#include <signal.h>
+#include <sys/prctl.h>
 #include <sys/resource.h>
+#include <unistd.h>
 #include <time.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
+#include "init_sampler.h"
 #include "mi355x/liveness_probe.h"
 
 namespace {
@@ -27,6 +33,19 @@ double cpu_ms() {
   rusage ru;
   getrusage(RUSAGE_SELF, &ru);
   return (ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e3 + (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) / 1e3;
+}
+
+// read syscalls issued so far (/proc/self/io "syscr"): ROCr's start-up is
+// dominated by walking the kfd topology in sysfs, this makes that visible.
+long long read_syscalls() {
+  FILE* f = std::fopen("/proc/self/io", "r");
+  if (!f) return -1;
+  char line[128];
+  long long v = -1;
+  while (std::fgets(line, sizeof(line), f))
+    if (std::sscanf(line, "syscr: %lld", &v) == 1) break;
+  std::fclose(f);
+  return v;
 }
 
 uint64_t mono_ns() {
@@ -53,20 +72,23 @@ std::string json_escape(const char* s) {
   return o;
 }
 
-void print_device(const mi355x_probe_result& r, bool last) {
-  std::printf(
+std::string device_json(const mi355x_probe_result& r) {
+  char buf[2048];
+  std::snprintf(
+      buf, sizeof(buf),
       "{\"ordinal\":%d,\"ok\":%s,\"hip_error\":%d,\"mismatches\":%d,\"nonce\":%u,\"xcc_id\":%u,"
       "\"hw_id\":%u,\"iters\":%d,\"dispatches\":%d,\"kfd_node_id\":%d,\"runtime\":\"%s\","
       "\"kernel_us\":%.3f,\"setup_us\":%.3f,\"total_us\":%.3f,"
       "\"phase_us\":{\"code_object\":%.1f,\"queue\":%.1f,\"buffers\":%.1f,\"dispatch_wait\":%.1f},"
       "\"pci_bus_id\":\"%s\","
       "\"arch\":\"%s\",\"name\":\"%s\",\"uuid\":\"%s\",\"pci_domain\":%d,\"pci_bus\":%d,"
-      "\"pci_device\":%d,\"cu_count\":%d,\"total_mem\":%llu,\"error\":\"%s\"}%s",
+      "\"pci_device\":%d,\"cu_count\":%d,\"total_mem\":%llu,\"error\":\"%s\"}",
       r.ordinal, r.ok ? "true" : "false", r.hip_error, r.mismatches, r.nonce, r.xcc_id, r.hw_id, r.iters,
       r.dispatches, r.kfd_node_id, r.runtime, r.kernel_us, r.setup_us, r.total_us, r.phase_us[0], r.phase_us[1],
       r.phase_us[2], r.phase_us[3], json_escape(r.pci_bus_id).c_str(), json_escape(r.arch).c_str(),
       json_escape(r.name).c_str(), json_escape(r.uuid).c_str(), r.pci_domain, r.pci_bus, r.pci_device,
-      r.cu_count, static_cast<unsigned long long>(r.total_mem), json_escape(r.error).c_str(), last ? "" : ",");
+      r.cu_count, static_cast<unsigned long long>(r.total_mem), json_escape(r.error).c_str());
+  return buf;
 }
 
 #ifdef MI355X_PROBE_HSA
@@ -76,14 +98,115 @@ int probe(int o, uint32_t nonce, int iters, double timeout_s, mi355x_probe_resul
 }
 int identify_dev(int o, mi355x_probe_result* r) { return mi355x_hsa_probe_identify(o, r); }
 void init_phases(double out[3]) { mi355x_hsa_init_phases(out); }
+void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
+void teardown() { mi355x_hsa_probe_release(); }
+void runtime_shutdown() { mi355x_hsa_probe_shutdown(); }
 #else
 void init_phases(double out[3]) { out[0] = out[1] = out[2] = 0; }
+void defer_teardown() {}
+void teardown() {}
+void runtime_shutdown() {}
 int device_count() { return mi355x_probe_device_count(); }
 int probe(int o, uint32_t nonce, int iters, double, mi355x_probe_result* r) {
   return mi355x_probe_device(o, nonce, iters, r);
 }
 int identify_dev(int o, mi355x_probe_result* r) { return mi355x_probe_identify(o, r); }
 #endif
+
+// Probe (or identify) a set of ordinals, one host thread per GPU so an 8-GPU
+// request pays one device setup, not eight. Returns true when all are live.
+bool run_batch(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, int iters, double timeout_s,
+               bool identify, int n, std::vector<mi355x_probe_result>& results) {
+  results.assign(ords.size(), mi355x_probe_result{});
+  std::vector<int> rcs(ords.size(), 1);
+  auto run_one = [&](size_t i) {
+    if (ords[i] < 0 || ords[i] >= n) {
+      results[i].ordinal = ords[i];
+      std::snprintf(results[i].error, sizeof(results[i].error), "no such GPU (count=%d)", n);
+      return;
+    }
+    rcs[i] = identify ? identify_dev(ords[i], &results[i]) : probe(ords[i], nonces[i], iters, timeout_s, &results[i]);
+    if (identify && rcs[i] == 0) results[i].ok = 1;
+  };
+  if (ords.size() > 1) {
+    std::vector<std::thread> ths;
+    for (size_t i = 0; i < ords.size(); ++i) ths.emplace_back(run_one, i);
+    for (auto& t : ths) t.join();
+  } else if (!ords.empty()) {
+    run_one(0);
+  }
+  bool all_ok = !ords.empty();
+  for (int rc : rcs) all_ok = all_ok && rc == 0;
+  return all_ok;
+}
+
+std::string devices_json(const std::vector<mi355x_probe_result>& results) {
+  std::string o = "[";
+  for (size_t i = 0; i < results.size(); ++i) {
+    if (i) o += ",";
+    o += device_json(results[i]);
+  }
+  return o + "]";
+}
+
+// --serve: a long-lived prober for the plugin's health loop. The runtime is
+// initialised once; every request line
+//     probe <iters> <timeout_s> <ordinal>:<nonce> [<ordinal>:<nonce> ...]
+// is answered with one JSON line {"ok":..,"t_ready_ns":..,"devices":[..]}.
+// "quit" or EOF on stdin ends the server, and so does the parent's death
+// (PR_SET_PDEATHSIG). Spawning a fresh probe process per pulse would create
+// and tear down a kfd process each time, and a GPU process that starts while
+// such a teardown is in flight blocks in open("/dev/kfd") for up to ~150 ms
+// (profiles/README.md §3c): a pod admitted during a health sweep would pay it.
+int serve(int n, uint64_t t_start, uint64_t t_runtime) {
+  prctl(PR_SET_PDEATHSIG, SIGKILL);
+  if (getppid() == 1) return 0;  // parent already gone
+  std::printf("{\"serve\":true,\"ok\":%s,\"hip_device_count\":%d,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu}\n",
+              n >= 0 ? "true" : "false", n < 0 ? 0 : n, static_cast<unsigned long long>(t_start),
+              static_cast<unsigned long long>(t_runtime));
+  std::fflush(stdout);
+  if (n < 0) return 2;
+  std::string line;
+  char buf[4096];
+  while (std::fgets(buf, sizeof(buf), stdin)) {
+    line = buf;
+    while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
+    if (line.empty()) continue;
+    if (line == "quit") break;
+    int iters = 0;
+    double timeout_s = 0;
+    int consumed = 0;
+    if (std::sscanf(line.c_str(), "probe %d %lf %n", &iters, &timeout_s, &consumed) < 2 || consumed == 0) {
+      std::printf("{\"ok\":false,\"error\":\"bad request\",\"devices\":[]}\n");
+      std::fflush(stdout);
+      continue;
+    }
+    std::vector<int> ords;
+    std::vector<uint32_t> nonces;
+    const char* p = line.c_str() + consumed;
+    while (*p) {
+      char* end = nullptr;
+      const long o = std::strtol(p, &end, 10);
+      if (end == p || *end != ':') break;
+      p = end + 1;
+      const unsigned long nc = std::strtoul(p, &end, 0);
+      if (end == p) break;
+      ords.push_back(static_cast<int>(o));
+      nonces.push_back(static_cast<uint32_t>(nc));
+      p = end;
+      while (*p == ' ') ++p;
+    }
+    std::vector<mi355x_probe_result> results;
+    defer_teardown();
+    const bool ok = run_batch(ords, nonces, iters, timeout_s, false, n, results);
+    std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"t_ready_ns\":%llu,\"devices\":%s}\n", ok ? "true" : "false",
+                n, static_cast<unsigned long long>(mono_ns()), devices_json(results).c_str());
+    std::fflush(stdout);
+    teardown();  // queues/executables go, the runtime (and the kfd process) stays
+  }
+  runtime_shutdown();
+  return 0;
+}
 
 }  // namespace
 
@@ -94,6 +217,9 @@ int main(int argc, char** argv) {
   int iters = 4;
   double timeout_s = 5.0;
   bool identify = false;
+  int sample_us = 0;
+  std::string exit_mode = "shutdown";
+  bool serve_mode = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&](const char* what) -> const char* {
@@ -111,10 +237,21 @@ int main(int argc, char** argv) {
       iters = std::atoi(next("--iters"));
     } else if (a == "--timeout") {
       timeout_s = std::atof(next("--timeout"));
+    } else if (a == "--sample-init") {
+      sample_us = std::atoi(next("--sample-init"));
+    } else if (a == "--exit") {
+      exit_mode = next("--exit");
+      if (exit_mode != "shutdown" && exit_mode != "release" && exit_mode != "fast") {
+        std::fprintf(stderr, "--exit must be shutdown|release|fast\n");
+        return 2;
+      }
     } else if (a == "--identify") {
       identify = true;
+    } else if (a == "--serve") {
+      serve_mode = true;
     } else if (a == "-h" || a == "--help") {
-      std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S]\n",
+      std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
+                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve]\n",
                   argv[0]);
       return 0;
     } else {
@@ -123,15 +260,21 @@ int main(int argc, char** argv) {
     }
   }
 
+  mi355x::InitSampler sampler(sample_us > 0 ? sample_us : 1);
+  if (sample_us > 0) sampler.start();
   const int n = device_count();
+  if (sample_us > 0) sampler.stop();
+  const std::string init_profile = sample_us > 0 ? sampler.json() : "null";
   const uint64_t t_runtime = mono_ns();  // HIP runtime + ROCr initialised
   const double cpu_runtime = cpu_ms();
+  const long long syscr_runtime = read_syscalls();
   double iph[3];
   init_phases(iph);
+  if (serve_mode) return serve(n, t_start, t_runtime);
   if (n < 0) {
     std::printf("{\"ok\":false,\"hip_device_count\":0,\"error\":\"GPU runtime init failed (%d)\",\"devices\":[],"
-                "\"t_start_ns\":%llu,\"t_ready_ns\":0}\n",
-                -n, static_cast<unsigned long long>(t_start));
+                "\"t_start_ns\":%llu,\"t_ready_ns\":0,\"init_profile\":%s}\n",
+                -n, static_cast<unsigned long long>(t_start), init_profile.c_str());
     return 2;
   }
   std::vector<int> ords;
@@ -148,31 +291,29 @@ int main(int argc, char** argv) {
     }
   }
 
-  std::vector<mi355x_probe_result> results(ords.size());
-  bool all_ok = !ords.empty();
-  for (size_t i = 0; i < ords.size(); ++i) {
-    if (ords[i] < 0 || ords[i] >= n) {
-      std::memset(&results[i], 0, sizeof(results[i]));
-      results[i].ordinal = ords[i];
-      std::snprintf(results[i].error, sizeof(results[i].error), "no such HIP device (count=%d)", n);
-      all_ok = false;
-      continue;
-    }
-    int rc = identify ? identify_dev(ords[i], &results[i])
-                      : probe(ords[i], nonce + static_cast<uint32_t>(i), iters, timeout_s, &results[i]);
-    if (identify && rc == 0) results[i].ok = 1;
-    if (rc != 0) all_ok = false;
-  }
+  std::vector<uint32_t> nonces;
+  for (size_t i = 0; i < ords.size(); ++i) nonces.push_back(nonce + static_cast<uint32_t>(i));
+  std::vector<mi355x_probe_result> results;
+  // Queues/executables are torn down after the verdict is printed: the caller
+  // (container runtime, health loop) only waits for the JSON line.
+  defer_teardown();
+  const bool all_ok = run_batch(ords, nonces, iters, timeout_s, identify, n, results);
   const uint64_t t_ready = mono_ns();
   const double cpu_ready = cpu_ms();
   std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
-              "\"t_ready_ns\":%llu,\"cpu_ms_runtime\":%.2f,\"cpu_ms_ready\":%.2f,"
-              "\"init_us\":{\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"devices\":[",
+              "\"t_ready_ns\":%llu,\"cpu_ms_runtime\":%.2f,\"cpu_ms_ready\":%.2f,\"read_syscalls_runtime\":%lld,"
+              "\"init_us\":{\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"init_profile\":%s,\"devices\":%s}\n",
               all_ok ? "true" : "false", n, identify ? "true" : "false", static_cast<unsigned long long>(t_start),
               static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(t_ready), cpu_runtime,
-              cpu_ready, iph[0], iph[1], iph[2]);
-  for (size_t i = 0; i < results.size(); ++i) print_device(results[i], i + 1 == results.size());
-  std::printf("]}\n");
+              cpu_ready, syscr_runtime, iph[0], iph[1], iph[2], init_profile.c_str(),
+              devices_json(results).c_str());
   std::fflush(stdout);
-  return all_ok ? 0 : 1;
+  // After the verdict. The exit mode was an experiment: the kernel's kfd
+  // process teardown after we are gone costs the same either way
+  // (profiles/README.md §3c).
+  const int code = all_ok ? 0 : 1;
+  if (exit_mode == "fast") std::_Exit(code);
+  teardown();
+  if (exit_mode == "shutdown") runtime_shutdown();
+  return code;
 }

@@ -47,6 +47,8 @@ def build_parser() -> flags.GoFlagParser:
     p.add_str("dev_root", "/dev", "device node directory")
     p.add_str("exporter_socket", pb_exporter_socket(), "AMD metrics-exporter health socket ('' disables)")
     p.add_bool("liveness", False, "run the gfx950 MFMA liveness probe on every device each pulse")
+    p.add_str("liveness_mode", "persistent", "persistent: one long-lived probe server per node; spawn: a fresh "
+                                             "probe process per device per pulse")
     p.add_float("liveness_timeout", 10.0, "per-device liveness probe deadline (s)")
     p.add_int("liveness_fail_threshold", 2, "consecutive probe failures before a device turns Unhealthy")
     p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
@@ -74,6 +76,8 @@ def validate(ns) -> Optional[str]:
     if ns.resource_naming_strategy not in (C.STRATEGY_SINGLE, C.STRATEGY_MIXED):
         return (f"invalid resource_naming_strategy provided: {ns.resource_naming_strategy}, supported values "
                 "are single or mixed")
+    if ns.liveness_mode not in ("persistent", "spawn"):
+        return f"invalid liveness_mode provided: {ns.liveness_mode}, supported values are persistent or spawn"
     return None
 
 
@@ -89,7 +93,7 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
         from ..plugin.container import ContainerImpl
         hc = HealthConfig(exporter_socket=ns.exporter_socket or None, liveness=ns.liveness,
                           liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
-                          smi_ecc=ns.smi_ecc, dev_root=ns.dev_root)
+                          smi_ecc=ns.smi_ecc, dev_root=ns.dev_root, liveness_mode=ns.liveness_mode)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count,
                              topology_view_dir=view_dir)

@@ -17,7 +17,7 @@ import re
 import subprocess
 import time
 from dataclasses import dataclass
-from typing import Dict, List, Mapping, Optional, Sequence
+from typing import Dict, FrozenSet, Iterable, List, Mapping, Optional, Sequence, Set
 
 from .health.liveness import _VISIBILITY_VARS
 from .ops.native import probe_executable
@@ -43,6 +43,38 @@ class ContainerResult:
     wall_ms: float
     doc: dict
     error: str = ""
+    # kfd processes that appeared while the container ran and were still being
+    # torn down by the driver when it exited (see wait_kfd_released)
+    kfd_lingering: FrozenSet[str] = frozenset()
+
+
+KFD_PROC_DIR = "/sys/class/kfd/kfd/proc"
+
+
+def kfd_processes(proc_dir: str = KFD_PROC_DIR) -> Set[str]:
+    """Host PIDs that currently own a kfd process (one directory each)."""
+    try:
+        return set(os.listdir(proc_dir))
+    except OSError:
+        return set()
+
+
+def wait_kfd_released(entries: Iterable[str], timeout_s: float = 2.0, proc_dir: str = KFD_PROC_DIR) -> float:
+    """Block until the driver has finished tearing down `entries`; returns ms waited.
+
+    A GPU process's kfd teardown continues for ~150 ms after the process has
+    exited, and any GPU process that starts meanwhile blocks in
+    open("/dev/kfd") until it is done (measured on MI355X,
+    profiles/README.md §3c). The procfs entry disappears exactly when the
+    teardown completes, so this is the point at which the previous pod has
+    really terminated — what kubelet waits for before reusing its devices.
+    """
+    left = set(entries)
+    t0 = time.monotonic()
+    while left and time.monotonic() - t0 < timeout_s:
+        time.sleep(0.002)
+        left &= kfd_processes(proc_dir)
+    return (time.monotonic() - t0) * 1e3
 
 
 def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int = 4,
@@ -57,6 +89,7 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
     env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
     argv = [exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
             "--iters", str(iters), "--timeout", str(min(timeout_s, 30.0))]
+    before = kfd_processes()
     t0 = time.monotonic_ns()
     try:
         p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=timeout_s)
@@ -69,7 +102,8 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
         return ContainerResult(False, t0, 0, wall, {}, f"bad output rc={p.returncode}: {p.stderr.decode()[-300:]}")
     ok = p.returncode == 0 and bool(doc.get("ok"))
     err = "" if ok else "; ".join(d.get("error", "") for d in doc.get("devices", [])) or doc.get("error", "")
-    return ContainerResult(ok, t0, int(doc.get("t_ready_ns", 0)), wall, doc, err)
+    return ContainerResult(ok, t0, int(doc.get("t_ready_ns", 0)), wall, doc, err,
+                           frozenset(kfd_processes() - before))
 
 
 def ordinals_for_minors(minors: Sequence[int], minor_to_ordinal: Mapping[int, int]) -> List[int]:

@@ -1,14 +1,25 @@
-"""Per-device MFMA liveness probing in isolated child processes.
+"""Per-device MFMA liveness probing out of process.
 
-Each device is probed by its own ``mi355x-liveness-probe`` child with
-``ROCR_VISIBLE_DEVICES`` narrowed to that device, under a hard deadline:
+Two modes, both under a hard deadline enforced from here:
 
-* a wedged GPU can only stall its own child, which is killed at the deadline
-  and reported Unhealthy — ListAndWatch never blocks on the GPU;
-* the plugin process itself never initialises HIP, so it holds no context on
-  devices that pods own exclusively;
-* the verdict lands on the exact kubelet device ID (partition-accurate in CPX),
-  unlike the reference's node-global sysfs check (amdgpu.go:865-910).
+``persistent`` (default): one long-lived ``mi355x-liveness-probe --serve``
+child keeps the GPU runtime initialised and answers one request per sweep,
+probing every device in parallel. Measured on MI355X (profiles/README.md §3c):
+each GPU process that exits leaves ~150 ms of kfd teardown in the kernel, and a
+GPU process that starts meanwhile (a pod's runtime init) blocks in
+``open("/dev/kfd")`` for it. A prober that spawned a process per device per
+pulse would inject exactly that stall into pod start-up; the server creates
+its kfd process once. Per-sweep cost drops from ~150 ms to ~10 ms.
+
+``spawn``: each device probed by its own child with ``ROCR_VISIBLE_DEVICES``
+narrowed to that device. Used for isolation whenever the server misses its
+deadline or dies: the sweep is re-run per device so that one wedged GPU is
+reported Unhealthy on its own rather than taking the whole node with it.
+
+Either way ListAndWatch never blocks on a GPU, the plugin process itself never
+initialises a GPU runtime, and the verdict lands on the exact kubelet device
+ID (partition-accurate in CPX), unlike the reference's node-global sysfs check
+(amdgpu.go:865-910).
 """
 from __future__ import annotations
 
@@ -37,30 +48,114 @@ class ProbeOutcome:
     detail: dict = field(default_factory=dict)
 
 
+class ProbeServerError(RuntimeError):
+    pass
+
+
+class _ProbeServer:
+    """One ``--serve`` child: JSON lines on stdout, requests on stdin."""
+
+    def __init__(self, proc: asyncio.subprocess.Process, hello: dict):
+        self.proc = proc
+        self.hello = hello
+        self.requests = 0
+
+    @classmethod
+    async def start(cls, argv, env, timeout_s: float) -> "_ProbeServer":
+        proc = await asyncio.create_subprocess_exec(
+            *argv, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
+            stderr=asyncio.subprocess.DEVNULL, env=env, start_new_session=True)
+        srv = cls(proc, {})
+        try:
+            srv.hello = await srv._read(timeout_s)
+        except BaseException:
+            await srv.kill()
+            raise
+        if not srv.hello.get("serve") or not srv.hello.get("ok"):
+            await srv.kill()
+            raise ProbeServerError(f"probe server failed to start: {srv.hello}")
+        return srv
+
+    async def _read(self, timeout_s: float) -> dict:
+        line = await asyncio.wait_for(self.proc.stdout.readline(), timeout=timeout_s)
+        if not line:
+            raise ProbeServerError(f"probe server exited (rc={self.proc.returncode})")
+        try:
+            return json.loads(line)
+        except ValueError as e:
+            raise ProbeServerError(f"unparseable probe server output: {line[-200:]!r}") from e
+
+    async def request(self, line: str, timeout_s: float) -> dict:
+        try:
+            self.proc.stdin.write(line.encode() + b"\n")
+            await self.proc.stdin.drain()
+        except (BrokenPipeError, ConnectionResetError) as e:
+            raise ProbeServerError(f"probe server gone: {e}") from e
+        self.requests += 1
+        return await self._read(timeout_s)
+
+    @property
+    def alive(self) -> bool:
+        return self.proc.returncode is None
+
+    async def kill(self) -> None:
+        if self.proc.returncode is None:
+            try:
+                os.killpg(self.proc.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+        await self.proc.wait()
+
+
 class LivenessProber:
+    MODES = ("persistent", "spawn")
+    SERVER_BACKOFF_SWEEPS = 4
+
     def __init__(self, exe: Optional[str] = None, timeout_s: float = 10.0, iters: int = 4, max_parallel: int = 8,
-                 extra_env: Optional[Mapping[str, str]] = None, argv_prefix: Sequence[str] = ()):
+                 extra_env: Optional[Mapping[str, str]] = None, argv_prefix: Sequence[str] = (),
+                 mode: str = "persistent"):
+        if mode not in self.MODES:
+            raise ValueError(f"liveness mode must be one of {self.MODES}, got {mode!r}")
         self.exe = str(exe) if exe else None
         self.timeout_s = timeout_s
         self.iters = iters
         self.max_parallel = max(1, max_parallel)
         self.extra_env = dict(extra_env or {})
         self.argv_prefix = list(argv_prefix)
+        self.mode = mode
         self.sweeps = 0
+        self.server_starts = 0
+        self.fallbacks = 0
+        self._server: Optional[_ProbeServer] = None
+        self._server_backoff = 0  # sweeps to run in spawn mode after a server failure
 
     def _exe(self) -> str:
         if self.exe is None:
             self.exe = str(probe_executable())
         return self.exe
 
-    def _env(self, ordinal: int) -> Dict[str, str]:
+    def _env(self, ordinal: Optional[int]) -> Dict[str, str]:
         env = {k: v for k, v in os.environ.items() if k not in _VISIBILITY_VARS}
         env.update(self.extra_env)
-        env["ROCR_VISIBLE_DEVICES"] = str(ordinal)
+        if ordinal is not None:  # the server sees every device: its ordinals are host ROCr ordinals
+            env["ROCR_VISIBLE_DEVICES"] = str(ordinal)
         return env
 
+    @staticmethod
+    def _nonce(ordinal: int) -> int:
+        return (int(time.monotonic_ns()) ^ (ordinal * 0x9E3779B1)) & 0xFFFFFFFF
+
+    @staticmethod
+    def _judge(doc_ok: bool, d: dict, nonce: int, dt: float, rc: int = 0) -> ProbeOutcome:
+        if rc != 0 or not doc_ok or not d.get("ok"):
+            reason = d.get("error") or f"probe exit {rc}"
+            return ProbeOutcome(False, reason, dt, d)
+        if d.get("nonce") != nonce:
+            return ProbeOutcome(False, f"stale probe result (nonce {d.get('nonce')} != {nonce})", dt, d)
+        return ProbeOutcome(True, "", dt, d)
+
     async def probe_ordinal(self, ordinal: int, nonce: Optional[int] = None) -> ProbeOutcome:
-        nonce = (int(time.monotonic_ns()) ^ (ordinal * 0x9E3779B1)) & 0xFFFFFFFF if nonce is None else nonce
+        nonce = self._nonce(ordinal) if nonce is None else nonce
         argv = [*self.argv_prefix, self._exe(), "--devices", "0", "--iters", str(self.iters), "--nonce", str(nonce),
                 "--timeout", f"{max(0.5, self.timeout_s - 0.5):.2f}"]
         t0 = time.perf_counter()
@@ -88,17 +183,54 @@ class LivenessProber:
                                        f"{(err or out).decode(errors='replace')[-200:]}", dt)
         devs = doc.get("devices") or []
         d = devs[0] if devs else {}
-        if proc.returncode != 0 or not doc.get("ok") or not d.get("ok"):
-            reason = d.get("error") or doc.get("error") or f"probe exit {proc.returncode}"
-            return ProbeOutcome(False, reason, dt, d)
-        if d.get("nonce") != nonce:
-            return ProbeOutcome(False, f"stale probe result (nonce {d.get('nonce')} != {nonce})", dt, d)
-        return ProbeOutcome(True, "", dt, d)
+        if not d and doc.get("error"):
+            d = {"error": doc["error"]}
+        return self._judge(bool(doc.get("ok")), d, nonce, dt, proc.returncode)
+
+    # ------------------------------------------------------------ persistent
+    async def _probe_server(self, uniq) -> Dict[int, ProbeOutcome]:
+        t0 = time.perf_counter()
+        if self._server is None or not self._server.alive:
+            argv = [*self.argv_prefix, self._exe(), "--serve"]
+            self._server = await _ProbeServer.start(argv, self._env(None), self.timeout_s)
+            self.server_starts += 1
+        nonces = {o: self._nonce(o) for o in uniq}
+        inner = max(0.5, self.timeout_s - 0.5)
+        line = f"probe {self.iters} {inner:.2f} " + " ".join(f"{o}:{nonces[o]}" for o in uniq)
+        doc = await self._server.request(line, self.timeout_s)
+        dt = (time.perf_counter() - t0) * 1e3
+        by_ord = {d.get("ordinal"): d for d in doc.get("devices") or []}
+        out = {}
+        for o in uniq:
+            d = by_ord.get(o)
+            out[o] = (self._judge(bool(d.get("ok")), d, nonces[o], dt) if d is not None
+                      else ProbeOutcome(False, "device missing from probe server reply", dt))
+        return out
+
+    async def close(self) -> None:
+        if self._server is not None:
+            await self._server.kill()
+            self._server = None
 
     async def probe(self, ordinals: Mapping[str, int]) -> Dict[str, ProbeOutcome]:
         """device ID -> outcome; devices sharing an ordinal are probed once."""
-        sem = asyncio.Semaphore(self.max_parallel)
         uniq = sorted(set(ordinals.values()))
+        use_server = self.mode == "persistent" and uniq and self._server_backoff == 0
+        self._server_backoff = max(0, self._server_backoff - 1)
+        if use_server:
+            try:
+                with TRACER.span("liveness.request", "health", ordinals=len(uniq)):
+                    results = await self._probe_server(uniq)
+                self.sweeps += 1
+                return {dev: results[o] for dev, o in ordinals.items()}
+            except (asyncio.TimeoutError, ProbeServerError, OSError) as e:
+                # a wedged device stalls the whole server: drop it and isolate per device
+                _log.warning("probe server failed (%s); re-probing each device in its own process",
+                             e if str(e) else type(e).__name__)
+                self.fallbacks += 1
+                self._server_backoff = self.SERVER_BACKOFF_SWEEPS
+                await self.close()
+        sem = asyncio.Semaphore(self.max_parallel)
 
         async def one(o: int):
             async with sem:

@@ -51,6 +51,7 @@ class HealthConfig:
     liveness_timeout_s: float = 10.0
     liveness_iters: int = 4
     liveness_parallel: int = 8
+    liveness_mode: str = "persistent"  # persistent probe server | spawn per device per sweep
     fail_threshold: int = 2
     recover_threshold: int = 1
     smi_ecc: bool = False
@@ -75,7 +76,7 @@ class HealthMonitor:
         self.prober = prober
         if self.cfg.liveness and self.prober is None:
             self.prober = LivenessProber(timeout_s=self.cfg.liveness_timeout_s, iters=self.cfg.liveness_iters,
-                                         max_parallel=self.cfg.liveness_parallel)
+                                         max_parallel=self.cfg.liveness_parallel, mode=self.cfg.liveness_mode)
         self._ordinals = dict(ordinal_map) if ordinal_map is not None else None
         self._exporter_fn = exporter_fn or exporter.get_gpu_health
         self._track: Dict[str, _Track] = {d.id: _Track() for d in inventory.devices}
@@ -143,6 +144,10 @@ class HealthMonitor:
         return bad
 
     # ------------------------------------------------------------------ sweep
+    async def close(self) -> None:
+        if self.prober is not None:
+            await self.prober.close()
+
     async def check_once(self) -> bool:
         """Run one sweep; returns True if any verdict changed."""
         with TRACER.span("health.sweep", "health", devices=len(self.inv.devices)):

@@ -89,6 +89,9 @@ class DeviceImpl(abc.ABC):
     def health_version(self) -> int:
         return 0
 
+    async def close(self) -> None:
+        """Release helper processes (e.g. the liveness probe server) at shutdown."""
+
 
 def device_proto(dev_id: str, health: str, numa: Optional[int] = None) -> pb.Device:
     d = pb.Device(ID=dev_id, health=health)

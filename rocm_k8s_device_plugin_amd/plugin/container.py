@@ -118,6 +118,9 @@ class ContainerImpl(DeviceImpl):
     def health_version(self) -> int:
         return self.monitor.version
 
+    async def close(self) -> None:
+        await self.monitor.close()
+
     # ---------------------------------------------------------------- allocation
     def allocate(self, ctx: PluginContext, req: pb.AllocateRequest) -> pb.AllocateResponse:
         resp = pb.AllocateResponse()

@@ -261,6 +261,8 @@ class PluginManager:
         await asyncio.gather(*self._tasks, return_exceptions=True)
         self._tasks.clear()
         await self._stop_servers()
+        if self.impl is not None:
+            await self.impl.close()
         if self._metrics_server is not None:
             self._metrics_server.close()
             await self._metrics_server.wait_closed()

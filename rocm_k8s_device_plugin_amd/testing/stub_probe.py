@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """Fault-injection stand-in for ``mi355x-liveness-probe`` (CPU tests).
 
-Speaks the same CLI and JSON contract. Behaviour per ROCr ordinal comes from
-the JSON file named by $MI355X_STUB_PROBE_CONTROL, e.g.
+Speaks the same CLI and JSON contract, one-shot and ``--serve``. Behaviour
+per ROCr ordinal comes from the JSON file named by $MI355X_STUB_PROBE_CONTROL
+(re-read on every request), e.g.
 ``{"0": "ok", "3": "fail", "5": "hang", "6": "stale", "7": "garbage"}``
-(missing ordinals are "ok"). Exercises the real LivenessProber code path:
-process spawn, deadline kill, output parsing, nonce check, hysteresis.
+(missing ordinals are "ok"; "serve": "broken" makes --serve fail to start).
+Exercises the real LivenessProber code path: process spawn, server protocol,
+deadline kill, fallback to per-device isolation, output parsing, nonce check,
+hysteresis. Each start appends a line to $MI355X_STUB_PROBE_LOG if set.
 """
 import json
 import os
@@ -13,31 +16,72 @@ import sys
 import time
 
 
+def _control():
+    path = os.environ.get("MI355X_STUB_PROBE_CONTROL")
+    if path and os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return {}
+
+
+def _device(ordinal_reported, mode, nonce):
+    ok = mode == "ok"
+    return {"ordinal": ordinal_reported, "ok": ok or mode == "stale", "hip_error": 0, "mismatches": 0 if ok else 17,
+           "nonce": nonce if mode != "stale" else (nonce + 1) & 0xFFFFFFFF, "xcc_id": 0, "hw_id": 0, "iters": 4,
+           "dispatches": 1, "kfd_node_id": -1, "runtime": "stub", "kernel_us": 3.0, "setup_us": 1.0,
+           "total_us": 5.0, "pci_bus_id": "", "arch": "gfx950", "name": "", "uuid": "", "pci_domain": 0,
+           "pci_bus": 0, "pci_device": 0, "cu_count": 256, "total_mem": 0,
+           "error": "" if ok or mode == "stale" else "17/1024 MFMA results differ from host reference"}
+
+
+def serve():
+    ctl = _control()
+    if ctl.get("serve") == "broken":
+        print(json.dumps({"serve": True, "ok": False, "hip_device_count": 0}), flush=True)
+        return 2
+    t = time.monotonic_ns()
+    print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "t_start_ns": t, "t_runtime_ns": t}),
+          flush=True)
+    for line in sys.stdin:
+        parts = line.split()
+        if not parts or parts[0] == "quit":
+            break
+        ctl = _control()
+        devs = []
+        for tok in parts[3:]:
+            o, n = tok.split(":")
+            mode = ctl.get(o, "ok")
+            if mode == "hang":
+                time.sleep(3600)
+            if mode == "garbage":
+                print("segfault-ish noise", flush=True)
+                return 139
+            devs.append(_device(int(o), mode, int(n, 0)))
+        print(json.dumps({"ok": all(d["ok"] for d in devs), "hip_device_count": 8, "t_ready_ns": time.monotonic_ns(),
+                          "devices": devs}), flush=True)
+    return 0
+
+
 def main(argv):
+    log = os.environ.get("MI355X_STUB_PROBE_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(("serve" if "--serve" in argv else os.environ.get("ROCR_VISIBLE_DEVICES", "0")) + "\n")
+    if "--serve" in argv:
+        return serve()
     nonce = 0
     for i, a in enumerate(argv):
         if a == "--nonce":
             nonce = int(argv[i + 1], 0)
     ordinal = os.environ.get("ROCR_VISIBLE_DEVICES", "0").split(",")[0]
-    ctl = {}
-    path = os.environ.get("MI355X_STUB_PROBE_CONTROL")
-    if path and os.path.exists(path):
-        with open(path) as f:
-            ctl = json.load(f)
-    mode = ctl.get(ordinal, "ok")
+    mode = _control().get(ordinal, "ok")
     if mode == "hang":
         time.sleep(3600)
     if mode == "garbage":
         print("segfault-ish noise")
         return 139
     t = time.monotonic_ns()
-    ok = mode == "ok"
-    dev = {"ordinal": 0, "ok": ok or mode == "stale", "hip_error": 0, "mismatches": 0 if ok else 17,
-           "nonce": nonce if mode != "stale" else (nonce + 1) & 0xFFFFFFFF, "xcc_id": 0, "hw_id": 0, "iters": 4,
-           "dispatches": 1, "kfd_node_id": -1, "runtime": "stub", "kernel_us": 3.0, "setup_us": 1.0,
-           "total_us": 5.0, "pci_bus_id": "", "arch": "gfx950", "name": "", "uuid": "", "pci_domain": 0,
-           "pci_bus": 0, "pci_device": 0, "cu_count": 256, "total_mem": 0,
-           "error": "" if ok or mode == "stale" else "17/1024 MFMA results differ from host reference"}
+    dev = _device(0, mode, nonce)
     doc = {"ok": dev["ok"], "hip_device_count": 1, "identify": False, "t_start_ns": t, "t_runtime_ns": t,
            "t_ready_ns": t, "devices": [dev]}
     print(json.dumps(doc))

@@ -141,6 +141,28 @@ def test_liveness_monitor_marks_live_devices_healthy(inv, ordinals):
     assert all(v.health == "Healthy" for v in snap.values()), snap
 
 
+def test_persistent_probe_server(ordinals):
+    """One --serve process answers several sweeps; per-sweep cost is device work only."""
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    prober = LivenessProber(timeout_s=60, mode="persistent")
+    ords = dict(ordinals)
+
+    async def go():
+        lat = []
+        for _ in range(4):
+            res = await prober.probe(ords)
+            assert all(r.ok for r in res.values()), res
+            assert all(r.detail["runtime"] == "hsa" and r.detail["dispatches"] == 1 for r in res.values())
+            lat.append(max(r.latency_ms for r in res.values()))
+        assert prober.server_starts == 1 and prober.fallbacks == 0
+        await prober.close()
+        return lat
+
+    lat = asyncio.run(go())
+    # the first sweep includes ROCr start-up; later sweeps only code object + queue + dispatch
+    assert min(lat[1:]) < 100.0, lat
+
+
 def test_smi_cross_check(inv):
     from rocm_k8s_device_plugin_amd.ops.native import core
     n = core()

@@ -428,6 +428,7 @@ def test_cli_validation(tmp_path):
     assert cli.main(["-pulse=-1"]) == 1
     assert cli.main(["-driver_type", "bogus"]) == 1
     assert cli.main(["--resource_naming_strategy=weird"]) == 1
+    assert cli.main(["-liveness_mode=sometimes"]) == 1
     with pytest.raises(SystemExit) as e:
         cli.main(["-driver_type=container", "-sysfs_root", str(tmp_path)])
     assert e.value.code == 1
@@ -439,6 +440,8 @@ def test_cli_flag_spellings():
                                         "--resource_naming_strategy", "mixed", "-liveness"])
     assert ns.pulse == 2 and ns.v == 5 and ns.logtostderr is True and ns.liveness is True
     assert ns.resource_naming_strategy == "mixed"
+    assert ns.liveness_mode == "persistent"
+    assert cli.build_parser().parse_args(["-liveness_mode=spawn"]).liveness_mode == "spawn"
 
 
 def test_cli_autoselect_order(tmp_path):
@@ -485,3 +488,76 @@ def test_trace_spans(tmp_path):
         assert {"GetPreferredAllocation", "Allocate", "allocator.allocate"} <= names
     finally:
         TRACER.configure(None)
+
+
+def test_liveness_persistent_server_reused(tmp_path):
+    """Healthy sweeps go through ONE long-lived probe server, no per-device spawns."""
+    log_path = tmp_path / "starts.log"
+    ctl, prober = _stub_prober(tmp_path, {"3": "fail"})
+    prober.extra_env["MI355X_STUB_PROBE_LOG"] = str(log_path)
+    ords = {f"dev{i}": i for i in range(8)}
+
+    async def go():
+        for _ in range(3):
+            res = await prober.probe(ords)
+            assert {d for d, r in res.items() if not r.ok} == {"dev3"}
+            assert "differ" in res["dev3"].reason
+        assert prober.server_starts == 1 and prober.fallbacks == 0 and prober._server.requests == 3
+        await prober.close()
+        assert prober._server is None
+
+    run(go())
+    assert log_path.read_text().split() == ["serve"]
+
+
+def test_liveness_server_failure_isolates_per_device(tmp_path):
+    """A hanging server is killed and the sweep re-run one process per device."""
+    log_path = tmp_path / "starts.log"
+    ctl, prober = _stub_prober(tmp_path, {"5": "hang"}, timeout=1.0)
+    prober.extra_env["MI355X_STUB_PROBE_LOG"] = str(log_path)
+    ords = {f"dev{i}": i for i in range(8)}
+
+    async def go():
+        res = await prober.probe(ords)
+        assert {d for d, r in res.items() if not r.ok} == {"dev5"}
+        assert "deadline" in res["dev5"].reason
+        assert prober.fallbacks == 1 and prober._server is None
+        # backoff: the next sweeps stay in spawn mode, then the server is retried
+        ctl.write_text("{}")
+        for _ in range(LivenessProber.SERVER_BACKOFF_SWEEPS):
+            assert all(r.ok for r in (await prober.probe(ords)).values())
+            assert prober._server is None
+        assert all(r.ok for r in (await prober.probe(ords)).values())
+        assert prober._server is not None and prober.server_starts == 2
+        await prober.close()
+
+    run(go(), timeout=60)
+    starts = log_path.read_text().split()
+    assert starts[0] == "serve" and sorted(starts[1:9]) == [str(i) for i in range(8)] and starts[-1] == "serve"
+
+
+def test_liveness_server_start_failure_falls_back(tmp_path):
+    ctl, prober = _stub_prober(tmp_path, {"serve": "broken", "1": "stale"})
+    ords = {f"dev{i}": i for i in range(4)}
+
+    async def go():
+        res = await prober.probe(ords)
+        assert prober.fallbacks == 1
+        assert {d for d, r in res.items() if not r.ok} == {"dev1"} and "stale" in res["dev1"].reason
+
+    run(go())
+
+
+def test_liveness_spawn_mode_never_starts_server(tmp_path):
+    ctl = tmp_path / "probe_ctl.json"
+    ctl.write_text("{}")
+    prober = LivenessProber(exe=STUB, argv_prefix=[sys.executable], timeout_s=2.0, mode="spawn",
+                            extra_env={"MI355X_STUB_PROBE_CONTROL": str(ctl)})
+
+    async def go():
+        assert all(r.ok for r in (await prober.probe({"a": 0, "b": 1})).values())
+        assert prober.server_starts == 0
+
+    run(go())
+    with pytest.raises(ValueError):
+        LivenessProber(mode="bogus")

@@ -30,13 +30,28 @@ VARIANTS = {
     "rocr_visible+sdma_off": {"ROCR_VISIBLE_DEVICES": "0", "HSA_ENABLE_SDMA": "0"},
     "rocr_visible+no_interrupt": {"ROCR_VISIBLE_DEVICES": "0", "HSA_ENABLE_INTERRUPT": "0"},
     "rocr_visible+no_scratch_reclaim": {"ROCR_VISIBLE_DEVICES": "0", "HSA_NO_SCRATCH_RECLAIM": "1"},
+    # ROCr start-up knobs (names from libhsa-runtime64's own getenv table)
+    "rocr_visible+disable_image": {"ROCR_VISIBLE_DEVICES": "0", "HSA_DISABLE_IMAGE": "1"},
+    "rocr_visible+tools_disable_register": {"ROCR_VISIBLE_DEVICES": "0", "HSA_TOOLS_DISABLE_REGISTER": "1"},
+    "rocr_visible+cu_mask_skip_init": {"ROCR_VISIBLE_DEVICES": "0", "HSA_CU_MASK_SKIP_INIT": "1"},
+    "rocr_visible+no_pc_sampling": {"ROCR_VISIBLE_DEVICES": "0", "HSA_DISABLE_PC_SAMPLING": "1"},
+    "rocr_visible+lean": {"ROCR_VISIBLE_DEVICES": "0", "HSA_DISABLE_IMAGE": "1", "HSA_TOOLS_DISABLE_REGISTER": "1",
+                          "HSA_CU_MASK_SKIP_INIT": "1", "HSA_DISABLE_PC_SAMPLING": "1"},
 }
+SAMPLE_ARGS: list = []
+
+
+def kfd_procs():
+    try:
+        return set(os.listdir("/sys/class/kfd/kfd/proc"))
+    except OSError:
+        return set()
 
 
 def run_once(env_extra, args, runtime="hsa"):
     env = {k: v for k, v in os.environ.items() if k not in VIS}
     env.update(env_extra)
-    argv = [str(probe_executable(runtime)), "--devices", "0", "--iters", "4"] + args
+    argv = [str(probe_executable(runtime)), "--devices", "0", "--iters", "4"] + args + SAMPLE_ARGS
     t0 = time.monotonic_ns()
     p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=120)
     t1 = time.monotonic_ns()
@@ -55,6 +70,8 @@ def run_once(env_extra, args, runtime="hsa"):
         "phase_us": doc["devices"][0].get("phase_us", {}) if doc["devices"] else {},
         "cpu_ms_runtime": doc.get("cpu_ms_runtime", 0.0),
         "cpu_ms_ready": doc.get("cpu_ms_ready", 0.0),
+        "read_syscalls_runtime": doc.get("read_syscalls_runtime", -1),
+        "init_profile": doc.get("init_profile"),
     }
 
 
@@ -63,9 +80,20 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--out", default="")
     ap.add_argument("--only", default="", help="comma list of variant names (default: all)")
+    ap.add_argument("--sample-init", type=int, default=0,
+                    help="probe samples its own threads every N us during runtime init (see init_sampler.h)")
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="idle time between runs (lets the previous process' kfd teardown finish)")
+    ap.add_argument("--probe-args", default="", help="extra probe arguments, e.g. '--exit fast'")
+    ap.add_argument("--wait-kfd", action="store_true",
+                    help="after each run wait until its /sys/class/kfd/kfd/proc entry is gone (<= 2 s)")
+    ap.add_argument("--tag", default="", help="suffix for the row names")
     ap.add_argument("--parent-gpu", action="store_true",
                     help="initialise HIP in this (parent) process first, like a torch-based harness would")
     a = ap.parse_args()
+    if a.sample_init:
+        SAMPLE_ARGS[:] = ["--sample-init", str(a.sample_init)]
+    SAMPLE_ARGS.extend(a.probe_args.split())
     if a.parent_gpu:
         import torch
         torch.cuda.synchronize() if torch.cuda.is_available() else None
@@ -78,10 +106,31 @@ def main():
         plan = [p for p in plan if p[0] in keep]
     for name, env, rt in plan:
         extra = ["--identify"] if name.endswith("identify_only") else []
-        runs = [run_once(env, extra, rt) for _ in range(a.reps)]
+        runs = []
+        for _ in range(a.reps):
+            before = kfd_procs()
+            runs.append(run_once(env, extra, rt))
+            if a.wait_kfd:
+                t = time.monotonic()
+                left = kfd_procs() - before
+                while left and time.monotonic() - t < 2.0:
+                    time.sleep(0.002)
+                    left = kfd_procs() & left
+                runs[-1]["kfd_linger_ms"] = (time.monotonic() - t) * 1e3
+            if a.gap_ms:
+                time.sleep(a.gap_ms / 1e3)
         row = {}
         for k, v in runs[0].items():
             if k == "ok":
+                continue
+            if k == "init_profile":
+                if v:  # pooled histogram over all runs, in ms of wall time per run
+                    agg = {}
+                    for r in runs:
+                        for b, c in r[k]["buckets"].items():
+                            agg[b] = agg.get(b, 0) + c
+                    per = v["period_us"] / 1e3 / len(runs)
+                    row[k] = dict(sorted(((b, round(c * per, 2)) for b, c in agg.items()), key=lambda x: -x[1]))
                 continue
             if isinstance(v, dict):
                 row[k] = {kk: round(statistics.median(r[k].get(kk, 0.0) for r in runs), 1) for kk in v}
@@ -89,6 +138,7 @@ def main():
                 row[k] = round(statistics.median(r[k] for r in runs), 3)
         row["all_ok"] = all(r["ok"] for r in runs)
         row["ready_ms_min"] = round(min(r["ready_ms"] for r in runs), 3)
+        name = name + a.tag
         table[name] = row
         print(f"{name:40s} {json.dumps(row)}", flush=True)
     if a.out:

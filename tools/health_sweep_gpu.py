@@ -35,18 +35,19 @@ async def main_async(a):
     acc = Inventory(sysfs_root=a.sysfs_root, devices=tuple(inv.by_id[i] for i in ords), topology=inv.topology,
                     driver_loaded=True, kfd_present=True)
     mon = HealthMonitor(acc, HealthConfig(exporter_socket=None, liveness=True, liveness_timeout_s=30,
-                                          dev_root=a.dev_root), ordinal_map=ords)
+                                          dev_root=a.dev_root, liveness_mode=a.liveness_mode), ordinal_map=ords)
     impl = ContainerImpl("single", a.sysfs_root, inventory=acc, monitor=mon)
     sweep_ms, probe_ms, kernel_us = [], [], []
-    orig = mon.prober.probe_ordinal
+    orig = mon.prober.probe
 
-    async def timed(o, nonce=None):
-        r = await orig(o, nonce)
-        probe_ms.append(r.latency_ms)
-        kernel_us.append(float(r.detail.get("kernel_us", 0.0)))
-        return r
+    async def timed(ordinals):
+        res = await orig(ordinals)
+        for r in res.values():
+            probe_ms.append(r.latency_ms)
+            kernel_us.append(float(r.detail.get("kernel_us", 0.0)))
+        return res
 
-    mon.prober.probe_ordinal = timed
+    mon.prober.probe = timed
     with tempfile.TemporaryDirectory() as d:
         k = FakeKubelet(d)
         await k.start()
@@ -72,6 +73,8 @@ async def main_async(a):
         "probe_ms_p50": round(statistics.median(probe_ms), 2) if probe_ms else None,
         "probe_ms_max": round(max(probe_ms), 2) if probe_ms else None,
         "kernel_us_p50": round(statistics.median(kernel_us), 2) if kernel_us else None,
+        "liveness_mode": a.liveness_mode, "probe_server_starts": mon.prober.server_starts,
+        "probe_fallbacks": mon.prober.fallbacks,
     }
     return res
 
@@ -84,6 +87,7 @@ def main():
     ap.add_argument("--dev-root", default="/dev")
     ap.add_argument("--out", default="")
     ap.add_argument("--trace", default="")
+    ap.add_argument("--liveness-mode", default="persistent", choices=("persistent", "spawn"))
     a = ap.parse_args()
     log.setup(0)
     TRACER.configure(a.trace or None)
