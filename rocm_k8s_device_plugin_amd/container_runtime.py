@@ -59,7 +59,7 @@ def kfd_processes(proc_dir: str = KFD_PROC_DIR) -> Set[str]:
         return set()
 
 
-def wait_kfd_released(entries: Iterable[str], timeout_s: float = 2.0, proc_dir: str = KFD_PROC_DIR) -> float:
+def wait_kfd_released(entries: Iterable[str], timeout_s: float = 0.5, proc_dir: str = KFD_PROC_DIR) -> float:
     """Block until the driver has finished tearing down `entries`; returns ms waited.
 
     A GPU process's kfd teardown continues for ~150 ms after the process has
@@ -68,6 +68,9 @@ def wait_kfd_released(entries: Iterable[str], timeout_s: float = 2.0, proc_dir: 
     profiles/README.md §3c). The procfs entry disappears exactly when the
     teardown completes, so this is the point at which the previous pod has
     really terminated — what kubelet waits for before reusing its devices.
+    The entries are host PIDs that appeared while our container ran, so another
+    tenant's GPU process started meanwhile can be among them: the wait is
+    capped (default 0.5 s, ~3x a teardown) rather than unbounded.
     """
     left = set(entries)
     t0 = time.monotonic()
