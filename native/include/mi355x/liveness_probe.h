@@ -62,9 +62,10 @@ void mi355x_hsa_probe_shutdown(void);
 // takes teardown off its critical path.
 void mi355x_hsa_probe_defer_release(int on);
 void mi355x_hsa_probe_release(void);
-// Runtime start-up split of the last mi355x_hsa_probe_init (us): hsa_init,
-// agent enumeration, memory-pool discovery.
-void mi355x_hsa_init_phases(double out_us[3]);
+// Runtime start-up split of the last mi355x_hsa_probe_init (us): dlopen of
+// ROCr (its constructors), pre-open of /dev/kfd (on a second thread,
+// overlapped with the dlopen), hsa_init, agent enumeration, pool discovery.
+void mi355x_hsa_init_phases(double out_us[5]);
 
 #ifdef __cplusplus
 }

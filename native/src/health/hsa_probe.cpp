@@ -15,6 +15,9 @@
 // Exactly one dispatch per probe; the agent's kfd node id comes from
 // HSA_AMD_AGENT_INFO_DRIVER_NODE_ID, so the verdict maps to the kubelet
 // device ID without guessing.
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <unistd.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
@@ -25,6 +28,7 @@
 #include <thread>
 #include <vector>
 
+#include "hsa_api.h"
 #include "liveness_kernel.h"
 #include "mi355x/liveness_probe.h"
 #include "probe_verify.h"
@@ -45,7 +49,41 @@ asm(".section .rodata.mi355x_hsaco,\"a\",@progbits\n"
     ".byte 0\n"
     ".previous\n");
 
+namespace mi355x {
+
+const HsaApi& hsa_api() {
+  static HsaApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const auto t0 = std::chrono::steady_clock::now();
+    // RTLD_NOLOAD first: in a process that already has ROCr (torch, the HIP
+    // runtime) reuse that copy rather than loading a second one
+    void* h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+    if (!h) h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/libhsa-runtime64.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      std::snprintf(api.error, sizeof(api.error), "dlopen libhsa-runtime64.so.1: %s", dlerror());
+      return;
+    }
+#define MI355X_HSA_SYM(name)                                                                  \
+  api.name = reinterpret_cast<decltype(&::name)>(dlsym(h, #name));                            \
+  if (!api.name) {                                                                            \
+    std::snprintf(api.error, sizeof(api.error), "libhsa-runtime64.so.1 lacks %s", #name);     \
+    return;                                                                                   \
+  }
+    MI355X_HSA_FUNCS(MI355X_HSA_SYM)
+#undef MI355X_HSA_SYM
+    api.loaded = true;
+    api.load_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  });
+  return api;
+}
+
+}  // namespace mi355x
+
 namespace {
+
+inline const mi355x::HsaApi& H() { return mi355x::hsa_api(); }
 
 struct Agent {
   hsa_agent_t agent{};
@@ -63,12 +101,15 @@ struct Runtime {
   hsa_amd_memory_pool_t fine{};
   bool has_kernarg = false, has_fine = false;
   uint64_t ts_freq = 0;
-  double init_us[3] = {0, 0, 0};
+  // dlopen(ROCr), pre-open of /dev/kfd (overlapped with dlopen), hsa_init,
+  // agent enumeration, pool discovery
+  double init_us[5] = {0, 0, 0, 0, 0};
+  int kfd_fd = -1;
 } g_rt;
 
 hsa_status_t collect_agent(hsa_agent_t a, void*) {
   hsa_device_type_t t;
-  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (H().hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
   if (t == HSA_DEVICE_TYPE_GPU) {
     Agent ag;
     ag.agent = a;
@@ -81,10 +122,10 @@ hsa_status_t collect_agent(hsa_agent_t a, void*) {
 
 hsa_status_t cpu_pool(hsa_amd_memory_pool_t p, void*) {
   hsa_amd_segment_t seg;
-  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  H().hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
   if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
   uint32_t flags = 0;
-  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  H().hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
   if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT) && !g_rt.has_kernarg) {
     g_rt.kernarg = p;
     g_rt.has_kernarg = true;
@@ -99,12 +140,12 @@ hsa_status_t cpu_pool(hsa_amd_memory_pool_t p, void*) {
 hsa_status_t gpu_pool(hsa_amd_memory_pool_t p, void* data) {
   auto* ag = static_cast<Agent*>(data);
   hsa_amd_segment_t seg;
-  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  H().hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
   if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
   uint32_t flags = 0;
-  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  H().hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
   bool alloc_ok = false;
-  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc_ok);
+  H().hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc_ok);
   if (alloc_ok && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && !ag->has_coarse) {
     ag->coarse = p;
     ag->has_coarse = true;
@@ -115,7 +156,11 @@ hsa_status_t gpu_pool(hsa_amd_memory_pool_t p, void* data) {
 void set_status(mi355x_probe_result* r, hsa_status_t s, const char* what) {
   if (r->hip_error == 0) r->hip_error = static_cast<int>(s);
   const char* msg = nullptr;
-  hsa_status_string(s, &msg);
+  if (!H().loaded) {
+    std::snprintf(r->error, sizeof(r->error), "%s: %.120s", what, H().error);
+    return;
+  }
+  H().hsa_status_string(s, &msg);
   std::snprintf(r->error, sizeof(r->error), "%s: %s", what, msg ? msg : "hsa error");
 }
 
@@ -123,18 +168,18 @@ void fill_identity(const Agent& ag, int ordinal, mi355x_probe_result* out) {
   out->ordinal = ordinal;
   std::snprintf(out->runtime, sizeof(out->runtime), "hsa");
   char name[64] = {0};
-  hsa_agent_get_info(ag.agent, HSA_AGENT_INFO_NAME, name);
+  H().hsa_agent_get_info(ag.agent, HSA_AGENT_INFO_NAME, name);
   std::snprintf(out->arch, sizeof(out->arch), "%s", name);
   char product[64] = {0};
-  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_PRODUCT_NAME), product);
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_PRODUCT_NAME), product);
   std::snprintf(out->name, sizeof(out->name), "%s", product);
   uint32_t node = 0, bdf = 0, domain = 0, cus = 0;
-  if (hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DRIVER_NODE_ID), &node) ==
+  if (H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DRIVER_NODE_ID), &node) ==
       HSA_STATUS_SUCCESS)
     out->kfd_node_id = static_cast<int>(node);
-  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
-  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &domain);
-  hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cus);
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &domain);
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cus);
   out->pci_domain = static_cast<int>(domain);
   out->pci_bus = static_cast<int>((bdf >> 8) & 0xFF);
   out->pci_device = static_cast<int>((bdf >> 3) & 0x1F);
@@ -142,12 +187,12 @@ void fill_identity(const Agent& ag, int ordinal, mi355x_probe_result* out) {
   std::snprintf(out->pci_bus_id, sizeof(out->pci_bus_id), "%04x:%02x:%02x.%x", domain, (bdf >> 8) & 0xFF,
                 (bdf >> 3) & 0x1F, bdf & 0x7);
   char uuid[24] = {0};
-  if (hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_UUID), uuid) ==
+  if (H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_UUID), uuid) ==
       HSA_STATUS_SUCCESS)
     std::snprintf(out->uuid, sizeof(out->uuid), "%s", uuid);
   if (ag.has_coarse) {
     size_t sz = 0;
-    hsa_amd_memory_pool_get_info(ag.coarse, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz);
+    H().hsa_amd_memory_pool_get_info(ag.coarse, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz);
     out->total_mem = sz;
   }
 }
@@ -163,32 +208,48 @@ extern "C" int mi355x_hsa_probe_init(void) {
   auto us = [](clk::time_point a, clk::time_point b) {
     return std::chrono::duration<double, std::micro>(b - a).count();
   };
+  // Create this process' kfd process (kernel side) while ROCr's constructors
+  // run on this thread; hsa_init's own open() then finds it (hsa_api.h).
+  const auto tk = clk::now();
+  std::thread preopen([tk] {
+    g_rt.kfd_fd = open("/dev/kfd", O_RDWR | O_CLOEXEC);
+    g_rt.init_us[1] = std::chrono::duration<double, std::micro>(clk::now() - tk).count();
+  });
+  const mi355x::HsaApi& api = H();
+  preopen.join();
+  g_rt.init_us[0] = api.load_us;
+  if (!api.loaded) {
+    g_rt.init_status = HSA_STATUS_ERROR;
+    return -static_cast<int>(HSA_STATUS_ERROR);
+  }
   const auto t0 = clk::now();
-  hsa_status_t s = hsa_init();
+  hsa_status_t s = H().hsa_init();
   const auto t1 = clk::now();
-  g_rt.init_us[0] = us(t0, t1);
+  g_rt.init_us[2] = us(t0, t1);
   if (s != HSA_STATUS_SUCCESS) {
     g_rt.init_status = s;
     return -static_cast<int>(s);
   }
-  hsa_iterate_agents(collect_agent, nullptr);
+  H().hsa_iterate_agents(collect_agent, nullptr);
   const auto t2 = clk::now();
-  if (g_rt.cpu.handle) hsa_amd_agent_iterate_memory_pools(g_rt.cpu, cpu_pool, nullptr);
-  for (auto& ag : g_rt.gpus) hsa_amd_agent_iterate_memory_pools(ag.agent, gpu_pool, &ag);
-  hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_rt.ts_freq);
-  g_rt.init_us[1] = us(t1, t2);
-  g_rt.init_us[2] = us(t2, clk::now());
+  if (g_rt.cpu.handle) H().hsa_amd_agent_iterate_memory_pools(g_rt.cpu, cpu_pool, nullptr);
+  for (auto& ag : g_rt.gpus) H().hsa_amd_agent_iterate_memory_pools(ag.agent, gpu_pool, &ag);
+  H().hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_rt.ts_freq);
+  g_rt.init_us[3] = us(t1, t2);
+  g_rt.init_us[4] = us(t2, clk::now());
   return static_cast<int>(g_rt.gpus.size());
 }
 
-extern "C" void mi355x_hsa_init_phases(double out_us[3]) {
-  for (int i = 0; i < 3; ++i) out_us[i] = g_rt.init_us[i];
+extern "C" void mi355x_hsa_init_phases(double out_us[5]) {
+  for (int i = 0; i < 5; ++i) out_us[i] = g_rt.init_us[i];
 }
 
 extern "C" void mi355x_hsa_probe_shutdown(void) {
   mi355x_hsa_probe_release();
   std::lock_guard<std::mutex> lk(g_rt.mu);
-  if (g_rt.inited && g_rt.init_status == HSA_STATUS_SUCCESS) hsa_shut_down();
+  if (g_rt.inited && g_rt.init_status == HSA_STATUS_SUCCESS) H().hsa_shut_down();
+  if (g_rt.kfd_fd >= 0) close(g_rt.kfd_fd);
+  g_rt.kfd_fd = -1;
   g_rt.inited = false;
   g_rt.gpus.clear();
   g_rt.has_kernarg = g_rt.has_fine = false;
@@ -227,14 +288,14 @@ struct ProbeResources {
   mi355x_liveness_args* kargs = nullptr;
 
   void release() {
-    if (kargs) hsa_amd_memory_pool_free(kargs);
-    if (d_scratch) hsa_amd_memory_pool_free(d_scratch);
-    if (h_meta) hsa_amd_memory_pool_free(h_meta);
-    if (h_out) hsa_amd_memory_pool_free(h_out);
-    if (sig.handle) hsa_signal_destroy(sig);
-    if (queue) hsa_queue_destroy(queue);
-    if (exe.handle) hsa_executable_destroy(exe);
-    if (reader.handle) hsa_code_object_reader_destroy(reader);
+    if (kargs) H().hsa_amd_memory_pool_free(kargs);
+    if (d_scratch) H().hsa_amd_memory_pool_free(d_scratch);
+    if (h_meta) H().hsa_amd_memory_pool_free(h_meta);
+    if (h_out) H().hsa_amd_memory_pool_free(h_out);
+    if (sig.handle) H().hsa_signal_destroy(sig);
+    if (queue) H().hsa_queue_destroy(queue);
+    if (exe.handle) H().hsa_executable_destroy(exe);
+    if (reader.handle) H().hsa_code_object_reader_destroy(reader);
     *this = ProbeResources{};
   }
 };
@@ -266,20 +327,20 @@ struct Step {
 // a few ms of driver work each on MI355X).
 Step make_queue_and_buffers(const Agent& ag, ProbeResources& r) {
   Step st;
-  STEP(st, hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &r.queue),
+  STEP(st, H().hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &r.queue),
        "queue create");
-  hsa_amd_profiling_set_profiler_enabled(r.queue, 1);
-  STEP(st, hsa_signal_create(1, 0, nullptr, &r.sig), "signal create");
-  STEP(st, hsa_amd_memory_pool_allocate(g_rt.fine, MI355X_PROBE_OUT * sizeof(float), 0,
+  H().hsa_amd_profiling_set_profiler_enabled(r.queue, 1);
+  STEP(st, H().hsa_signal_create(1, 0, nullptr, &r.sig), "signal create");
+  STEP(st, H().hsa_amd_memory_pool_allocate(g_rt.fine, MI355X_PROBE_OUT * sizeof(float), 0,
                                         reinterpret_cast<void**>(&r.h_out)), "alloc out");
-  STEP(st, hsa_amd_memory_pool_allocate(g_rt.fine, 64, 0, reinterpret_cast<void**>(&r.h_meta)), "alloc meta");
-  STEP(st, hsa_amd_memory_pool_allocate(ag.coarse, MI355X_SCRATCH_FLOATS * sizeof(float), 0,
+  STEP(st, H().hsa_amd_memory_pool_allocate(g_rt.fine, 64, 0, reinterpret_cast<void**>(&r.h_meta)), "alloc meta");
+  STEP(st, H().hsa_amd_memory_pool_allocate(ag.coarse, MI355X_SCRATCH_FLOATS * sizeof(float), 0,
                                         reinterpret_cast<void**>(&r.d_scratch)), "alloc scratch");
-  STEP(st, hsa_amd_memory_pool_allocate(g_rt.kernarg, kKernargBytes, 0, reinterpret_cast<void**>(&r.kargs)),
+  STEP(st, H().hsa_amd_memory_pool_allocate(g_rt.kernarg, kKernargBytes, 0, reinterpret_cast<void**>(&r.kargs)),
        "alloc kernarg");
-  STEP(st, hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.h_out), "allow out");
-  STEP(st, hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.h_meta), "allow meta");
-  STEP(st, hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.kargs), "allow kernarg");
+  STEP(st, H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.h_out), "allow out");
+  STEP(st, H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.h_meta), "allow meta");
+  STEP(st, H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, r.kargs), "allow kernarg");
   return st;
 }
 
@@ -291,17 +352,17 @@ struct KernelInfo {
 Step load_kernel(const Agent& ag, ProbeResources& r, KernelInfo& k) {
   Step st;
   const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
-  STEP(st, hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &r.reader), "code object reader");
-  STEP(st, hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &r.exe),
+  STEP(st, H().hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &r.reader), "code object reader");
+  STEP(st, H().hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &r.exe),
        "executable create");
-  STEP(st, hsa_executable_load_agent_code_object(r.exe, ag.agent, r.reader, nullptr, nullptr), "load code object");
-  STEP(st, hsa_executable_freeze(r.exe, nullptr), "executable freeze");
+  STEP(st, H().hsa_executable_load_agent_code_object(r.exe, ag.agent, r.reader, nullptr, nullptr), "load code object");
+  STEP(st, H().hsa_executable_freeze(r.exe, nullptr), "executable freeze");
   hsa_executable_symbol_t sym{};
-  STEP(st, hsa_executable_get_symbol_by_name(r.exe, "mi355x_mfma_liveness.kd", &ag.agent, &sym), "kernel symbol");
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.kobj);
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kseg);
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.gseg);
-  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.pseg);
+  STEP(st, H().hsa_executable_get_symbol_by_name(r.exe, "mi355x_mfma_liveness.kd", &ag.agent, &sym), "kernel symbol");
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.kobj);
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kseg);
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.gseg);
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.pseg);
   return st;
 }
 #undef STEP
@@ -381,7 +442,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     r.kargs->nonce = nonce;
     r.kargs->iters = out->iters;
 
-    const uint64_t idx = hsa_queue_add_write_index_screlease(r.queue, 1);
+    const uint64_t idx = H().hsa_queue_add_write_index_screlease(r.queue, 1);
     auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(r.queue->base_address) + (idx & (r.queue->size - 1));
     std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
     pkt->workgroup_size_x = 64;
@@ -402,13 +463,13 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
                      __ATOMIC_RELEASE);
-    hsa_signal_store_screlease(r.queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+    H().hsa_signal_store_screlease(r.queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
     out->dispatches = 1;
 
     // bounded wait: a wedged device must come back as a verdict, not a hang
     const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
     hsa_signal_value_t v = 1;
-    while ((v = hsa_signal_wait_scacquire(r.sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
+    while ((v = H().hsa_signal_wait_scacquire(r.sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
                                           HSA_WAIT_STATE_BLOCKED)) >= 1) {
       if (clk::now() > deadline) break;
     }
@@ -418,7 +479,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
       out->hip_error = -1;
     } else {
       hsa_amd_profiling_dispatch_time_t dt{};
-      if (hsa_amd_profiling_get_dispatch_time(ag.agent, r.sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
+      if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, r.sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
         out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
       mi355x::verify_tile(r.h_out, r.h_meta, nonce, out->iters, out);
     }

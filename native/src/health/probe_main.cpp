@@ -97,12 +97,12 @@ int probe(int o, uint32_t nonce, int iters, double timeout_s, mi355x_probe_resul
   return mi355x_hsa_probe_device(o, nonce, iters, timeout_s, r);
 }
 int identify_dev(int o, mi355x_probe_result* r) { return mi355x_hsa_probe_identify(o, r); }
-void init_phases(double out[3]) { mi355x_hsa_init_phases(out); }
+void init_phases(double out[5]) { mi355x_hsa_init_phases(out); }
 void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
 void teardown() { mi355x_hsa_probe_release(); }
 void runtime_shutdown() { mi355x_hsa_probe_shutdown(); }
 #else
-void init_phases(double out[3]) { out[0] = out[1] = out[2] = 0; }
+void init_phases(double out[5]) { out[0] = out[1] = out[2] = out[3] = out[4] = 0; }
 void defer_teardown() {}
 void teardown() {}
 void runtime_shutdown() {}
@@ -268,7 +268,7 @@ int main(int argc, char** argv) {
   const uint64_t t_runtime = mono_ns();  // HIP runtime + ROCr initialised
   const double cpu_runtime = cpu_ms();
   const long long syscr_runtime = read_syscalls();
-  double iph[3];
+  double iph[5];
   init_phases(iph);
   if (serve_mode) return serve(n, t_start, t_runtime);
   if (n < 0) {
@@ -302,10 +302,10 @@ int main(int argc, char** argv) {
   const double cpu_ready = cpu_ms();
   std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
               "\"t_ready_ns\":%llu,\"cpu_ms_runtime\":%.2f,\"cpu_ms_ready\":%.2f,\"read_syscalls_runtime\":%lld,"
-              "\"init_us\":{\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"init_profile\":%s,\"devices\":%s}\n",
+              "\"init_us\":{\"dlopen\":%.1f,\"kfd_open\":%.1f,\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"init_profile\":%s,\"devices\":%s}\n",
               all_ok ? "true" : "false", n, identify ? "true" : "false", static_cast<unsigned long long>(t_start),
               static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(t_ready), cpu_runtime,
-              cpu_ready, syscr_runtime, iph[0], iph[1], iph[2], init_profile.c_str(),
+              cpu_ready, syscr_runtime, iph[0], iph[1], iph[2], iph[3], iph[4], init_profile.c_str(),
               devices_json(results).c_str());
   std::fflush(stdout);
   // After the verdict. The exit mode was an experiment: the kernel's kfd
