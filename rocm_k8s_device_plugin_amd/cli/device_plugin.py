@@ -136,7 +136,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     if err:
         logger.error("%s", err)
         return 1
-    for line in BANNER:
+    from ..utils.versions import banner_line
+    for line in BANNER + [banner_line(ns.sysfs_root)]:
         logger.info("%s", line)
     cfg = load_config(ns.config)
     device_count = device_count_limit_from_env()

@@ -44,6 +44,7 @@ class FixtureSpec:
     compute_partition: str = "spx"
     memory_partition: str = "nps1"
     numa_nodes: int = 2
+    cpus_per_numa: int = 64
     hive_size: int = 8                  # GPUs per xGMI hive (8 = one hive)
     gfx_target_version: int = 90500
     device_id: int = MI355X_DEVICE_ID
@@ -152,6 +153,8 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
         _w(dev_dir / "vendor", "0x1002")
         _w(dev_dir / "device", f"0x{spec.device_id:04x}")
         _w(dev_dir / "numa_node", str(numa_node))
+        per = max(1, spec.cpus_per_numa)
+        _w(dev_dir / "local_cpulist", f"{numa_node * per}-{numa_node * per + per - 1}")
         _w(dev_dir / "product_name", spec.product_name)
         if spec.partition_support:
             _w(dev_dir / "current_compute_partition", cp.upper())
