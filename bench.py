@@ -65,6 +65,9 @@ def parse_args():
                          "(the previous pod has terminated) or start the next one immediately")
     ap.add_argument("--b2b-compare", type=int, default=5,
                     help="extra untimed admissions with --settle none, reported for comparison")
+    ap.add_argument("--peer-check", type=int, default=1,
+                    help="after the timed loop, DMA-copy + verify over every pair of the N GPUs' links (H2); "
+                         "reported in extra.peer_probe, never part of the metric")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -179,6 +182,7 @@ def main():
         inv = Inventory(sysfs_root=sysfs, devices=adv, topology=full.topology, driver_loaded=full.driver_loaded,
                         kfd_present=full.kfd_present)
         minor_to_ord = {dv.render_minor: ords[dv.id] for dv in adv}
+        adv_ordinals = [ords[dv.id] for dv in adv]
         impl = ContainerImpl("single", sysfs, HealthConfig(exporter_socket=None), inventory=inv)
         pdir = os.path.join(tmp, "device-plugins")
         loop = asyncio.new_event_loop()
@@ -293,6 +297,10 @@ def main():
                                              "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
                  "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
                  "reference_algorithm_candidates": ref["candidates"], "gpus": gpu_info}
+        if args.peer_check and not args.fixture:
+            from rocm_k8s_device_plugin_amd.health.peer import probe_peers
+            rep = probe_peers(adv_ordinals, nbytes=64 << 20, reps=3, timeout_s=120)
+            extra["peer_probe"] = dict(rep.summary(), wall_ms=round(rep.wall_ms, 1))
         loop.run_until_complete(kubelet.stop())
         mgr.request_stop()
         loop.run_until_complete(mgr_task)

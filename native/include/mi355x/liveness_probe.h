@@ -67,6 +67,36 @@ void mi355x_hsa_probe_release(void);
 // overlapped with the dlopen), hsa_init, agent enumeration, pool discovery.
 void mi355x_hsa_init_phases(double out_us[5]);
 
+// ---- xGMI / PCIe peer probe ------------------------------
+// `bytes` of a nonce-derived pattern filled in src's HBM, copied src -> dst
+// HBM by the DMA engines over the link between them (`reps` times, best time
+// kept), then dst -> host and verified word by word. Link properties are ROCr's
+// view of dst's HBM pool from src. src == dst exercises the same path on one
+// device (single-GPU boxes).
+typedef struct {
+  int src, dst;              // HSA GPU agent ordinals
+  int ok;
+  int hsa_error;
+  uint32_t value;            // fill pattern
+  int access;                // hsa_amd_memory_pool_access_t of dst HBM from src
+  int link_type;             // hsa_amd_link_info_type_t of the first hop (4 = xGMI, 2 = PCIe)
+  uint32_t hops;
+  uint32_t numa_distance;
+  uint32_t link_max_bw_mbps; // ROCr's link bandwidth figure for the first hop
+  int reps;
+  uint64_t bytes;
+  uint64_t mismatches;
+  double copy_us_best;
+  double gbps_best;
+  double total_us;
+  char src_bus_id[32];
+  char dst_bus_id[32];
+  char error[160];
+} mi355x_peer_result;
+
+int mi355x_hsa_peer_probe(int src, int dst, uint32_t nonce, uint64_t bytes, int reps, double timeout_s,
+                          mi355x_peer_result* out);
+
 #ifdef __cplusplus
 }
 #endif

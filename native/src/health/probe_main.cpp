@@ -3,6 +3,8 @@
 //
 //   mi355x-liveness-probe [--devices all|0,2,..] [--nonce N] [--iters N] [--identify] [--timeout S]
 //   mi355x-liveness-probe --serve      (long-lived; requests on stdin, see serve())
+//   mi355x-liveness-probe --peer [--devices ..] [--peer-bytes B] [--peer-reps R]
+//                                      (DMA copy over every GPU pair's link, verified)
 //
 // Built twice from this file: `mi355x-liveness-probe` launches through ROCr
 // directly (MI355X_PROBE_HSA; links only libhsa-runtime64, one AQL dispatch),
@@ -97,6 +99,9 @@ int probe(int o, uint32_t nonce, int iters, double timeout_s, mi355x_probe_resul
   return mi355x_hsa_probe_device(o, nonce, iters, timeout_s, r);
 }
 int identify_dev(int o, mi355x_probe_result* r) { return mi355x_hsa_probe_identify(o, r); }
+int peer(int a, int b, uint32_t nonce, uint64_t bytes, int reps, double timeout_s, mi355x_peer_result* r) {
+  return mi355x_hsa_peer_probe(a, b, nonce, bytes, reps, timeout_s, r);
+}
 void init_phases(double out[5]) { mi355x_hsa_init_phases(out); }
 void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
 void teardown() { mi355x_hsa_probe_release(); }
@@ -111,6 +116,15 @@ int probe(int o, uint32_t nonce, int iters, double, mi355x_probe_result* r) {
   return mi355x_probe_device(o, nonce, iters, r);
 }
 int identify_dev(int o, mi355x_probe_result* r) { return mi355x_probe_identify(o, r); }
+int peer(int a, int b, uint32_t, uint64_t bytes, int reps, double, mi355x_peer_result* r) {
+  std::memset(r, 0, sizeof(*r));
+  r->src = a;
+  r->dst = b;
+  r->bytes = bytes;
+  r->reps = reps;
+  std::snprintf(r->error, sizeof(r->error), "--peer needs the HSA-direct build (mi355x-liveness-probe)");
+  return 1;
+}
 #endif
 
 // Probe (or identify) a set of ordinals, one host thread per GPU so an 8-GPU
@@ -138,6 +152,48 @@ bool run_batch(const std::vector<int>& ords, const std::vector<uint32_t>& nonces
   bool all_ok = !ords.empty();
   for (int rc : rcs) all_ok = all_ok && rc == 0;
   return all_ok;
+}
+
+std::string peer_json(const mi355x_peer_result& r) {
+  char buf[1024];
+  std::snprintf(buf, sizeof(buf),
+                "{\"src\":%d,\"dst\":%d,\"src_bus_id\":\"%s\",\"dst_bus_id\":\"%s\",\"ok\":%s,\"hsa_error\":%d,"
+                "\"access\":%d,\"link_type\":%d,\"hops\":%u,\"numa_distance\":%u,\"link_max_bw_mbps\":%u,"
+                "\"bytes\":%llu,\"reps\":%d,\"mismatches\":%llu,\"copy_us_best\":%.2f,\"gbps_best\":%.2f,"
+                "\"total_us\":%.1f,\"error\":\"%s\"}",
+                r.src, r.dst, json_escape(r.src_bus_id).c_str(), json_escape(r.dst_bus_id).c_str(),
+                r.ok ? "true" : "false", r.hsa_error, r.access, r.link_type, r.hops, r.numa_distance,
+                r.link_max_bw_mbps, static_cast<unsigned long long>(r.bytes), r.reps,
+                static_cast<unsigned long long>(r.mismatches), r.copy_us_best, r.gbps_best, r.total_us,
+                json_escape(r.error).c_str());
+  return buf;
+}
+
+// --peer: every ordered pair of the selected GPUs (or the one GPU with itself),
+// one pair at a time so each copy has its link to itself.
+int run_peer(const std::vector<int>& ords, uint32_t nonce, uint64_t bytes, int reps, double timeout_s, int n) {
+  std::vector<std::pair<int, int>> pairs;
+  if (ords.size() == 1) {
+    pairs.emplace_back(ords[0], ords[0]);
+  } else {
+    for (int a : ords)
+      for (int b : ords)
+        if (a != b) pairs.emplace_back(a, b);
+  }
+  bool all_ok = !pairs.empty();
+  std::string o = "[";
+  for (size_t i = 0; i < pairs.size(); ++i) {
+    mi355x_peer_result r;
+    const int rc = peer(pairs[i].first, pairs[i].second, nonce + static_cast<uint32_t>(i), bytes, reps, timeout_s, &r);
+    all_ok = all_ok && rc == 0;
+    if (i) o += ",";
+    o += peer_json(r);
+    if (r.hsa_error == -1) break;  // a copy is still in flight: stop touching the devices
+  }
+  std::printf("{\"peer\":true,\"ok\":%s,\"hip_device_count\":%d,\"t_ready_ns\":%llu,\"pairs\":%s]}\n",
+              all_ok ? "true" : "false", n, static_cast<unsigned long long>(mono_ns()), o.c_str());
+  std::fflush(stdout);
+  return all_ok ? 0 : 1;
 }
 
 std::string devices_json(const std::vector<mi355x_probe_result>& results) {
@@ -220,6 +276,9 @@ int main(int argc, char** argv) {
   int sample_us = 0;
   std::string exit_mode = "shutdown";
   bool serve_mode = false;
+  bool peer_mode = false;
+  uint64_t peer_bytes = 64ull << 20;
+  int peer_reps = 3;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&](const char* what) -> const char* {
@@ -249,9 +308,15 @@ int main(int argc, char** argv) {
       identify = true;
     } else if (a == "--serve") {
       serve_mode = true;
+    } else if (a == "--peer") {
+      peer_mode = true;
+    } else if (a == "--peer-bytes") {
+      peer_bytes = std::strtoull(next("--peer-bytes"), nullptr, 0);
+    } else if (a == "--peer-reps") {
+      peer_reps = std::atoi(next("--peer-reps"));
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
-                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve]\n",
+                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve] [--peer [--peer-bytes B] [--peer-reps R]]\n",
                   argv[0]);
       return 0;
     } else {
@@ -291,6 +356,7 @@ int main(int argc, char** argv) {
     }
   }
 
+  if (peer_mode) return run_peer(ords, nonce, peer_bytes, peer_reps, timeout_s, n);
   std::vector<uint32_t> nonces;
   for (size_t i = 0; i < ords.size(); ++i) nonces.push_back(nonce + static_cast<uint32_t>(i));
   std::vector<mi355x_probe_result> results;

@@ -163,6 +163,18 @@ def test_persistent_probe_server(ordinals):
     assert min(lat[1:]) < 100.0, lat
 
 
+def test_peer_probe_self_copy(ordinals):
+    """H2 path on one GPU: HBM -> HBM DMA copy, readback, word-exact verify."""
+    from rocm_k8s_device_plugin_amd.health.peer import probe_peers
+    o = sorted(ordinals.values())[0]
+    rep = probe_peers([o], nbytes=32 << 20, reps=3, timeout_s=120)
+    assert rep.ok, rep
+    (p,) = rep.pairs
+    assert p["src"] == p["dst"] == o and p["mismatches"] == 0 and p["bytes"] == 32 << 20
+    assert p["gbps_best"] > 10.0, p           # an HBM-local DMA copy on MI355X
+    assert rep.summary()["pairs_ok"] == 1
+
+
 def test_smi_cross_check(inv):
     from rocm_k8s_device_plugin_amd.ops.native import core
     n = core()
