@@ -109,3 +109,14 @@ def test_examples_parse_and_request_gpus():
     assert n >= 7
     pod = _docs("example/pod/alexnet-gpu.yaml")[0]
     assert pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == 1
+
+
+def test_ci_workflows_parse_and_run_real_entry_points():
+    import yaml
+    root = os.path.join(os.path.dirname(__file__), "..", ".github", "workflows")
+    docs = {f: yaml.safe_load(open(os.path.join(root, f))) for f in os.listdir(root)}
+    assert set(docs) == {"ci.yaml", "helm-chart-release.yaml"}
+    steps = " ".join(s.get("run", "") for j in docs["ci.yaml"]["jobs"].values() for s in j["steps"])
+    for cmd in ("rocm_k8s_device_plugin_amd._build", '-m "not gpu"', "-m gpu", "bench.py"):
+        assert cmd in steps
+    assert docs["helm-chart-release.yaml"]["jobs"]["release"]["steps"][-1]["with"]["charts_dir"] == "helm"
