@@ -109,6 +109,25 @@ class InitSampler {
     return o;
   }
 
+  static std::string fd_path(long fd) {
+    char link[64], target[256];
+    std::snprintf(link, sizeof(link), "/proc/self/fd/%ld", fd);
+    const ssize_t k = readlink(link, target, sizeof(target) - 1);
+    if (k <= 0) return "?";
+    target[k] = 0;
+    std::string o;
+    for (const char* c = target; *c && o.size() < 120; ++c) {
+      if (*c >= '0' && *c <= '9') {
+        if (o.empty() || o.back() != 'N') o += 'N';
+      } else if (*c == '"' || *c == '\\') {
+        o += '_';
+      } else {
+        o += *c;
+      }
+    }
+    return o;
+  }
+
   static bool read_small(const char* path, char* buf, size_t n) {
     FILE* f = std::fopen(path, "r");
     if (!f) return false;
@@ -139,6 +158,9 @@ class InitSampler {
           unsigned long a0 = std::strtoul(p, &p, 16);
           unsigned long a1 = std::strtoul(p, &p, 16);
           what += " " + open_path(nr == 2 ? a0 : a1);
+        } else if (nr == 0 || nr == 17 || nr == 16 || nr == 3) {  // read/pread64/ioctl/close(fd, ..)
+          const long fd = static_cast<long>(std::strtoul(p, &p, 16));
+          what += " " + fd_path(fd);
         }
       }
     } else {

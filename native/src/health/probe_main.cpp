@@ -31,9 +31,10 @@
 
 namespace {
 
-double cpu_ms() {
+double cpu_ms(double* user_ms = nullptr) {
   rusage ru;
   getrusage(RUSAGE_SELF, &ru);
+  if (user_ms) *user_ms = ru.ru_utime.tv_sec * 1e3 + ru.ru_utime.tv_usec / 1e3;
   return (ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e3 + (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) / 1e3;
 }
 
@@ -331,7 +332,8 @@ int main(int argc, char** argv) {
   if (sample_us > 0) sampler.stop();
   const std::string init_profile = sample_us > 0 ? sampler.json() : "null";
   const uint64_t t_runtime = mono_ns();  // HIP runtime + ROCr initialised
-  const double cpu_runtime = cpu_ms();
+  double cpu_user_runtime = 0;
+  const double cpu_runtime = cpu_ms(&cpu_user_runtime);
   const long long syscr_runtime = read_syscalls();
   double iph[5];
   init_phases(iph);
@@ -367,11 +369,11 @@ int main(int argc, char** argv) {
   const uint64_t t_ready = mono_ns();
   const double cpu_ready = cpu_ms();
   std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
-              "\"t_ready_ns\":%llu,\"cpu_ms_runtime\":%.2f,\"cpu_ms_ready\":%.2f,\"read_syscalls_runtime\":%lld,"
+              "\"t_ready_ns\":%llu,\"cpu_ms_runtime\":%.2f,\"cpu_user_ms_runtime\":%.2f,\"cpu_ms_ready\":%.2f,\"read_syscalls_runtime\":%lld,"
               "\"init_us\":{\"dlopen\":%.1f,\"kfd_open\":%.1f,\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"init_profile\":%s,\"devices\":%s}\n",
               all_ok ? "true" : "false", n, identify ? "true" : "false", static_cast<unsigned long long>(t_start),
               static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(t_ready), cpu_runtime,
-              cpu_ready, syscr_runtime, iph[0], iph[1], iph[2], iph[3], iph[4], init_profile.c_str(),
+              cpu_user_runtime, cpu_ready, syscr_runtime, iph[0], iph[1], iph[2], iph[3], iph[4], init_profile.c_str(),
               devices_json(results).c_str());
   std::fflush(stdout);
   // After the verdict. The exit mode was an experiment: the kernel's kfd

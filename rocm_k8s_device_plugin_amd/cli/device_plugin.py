@@ -56,6 +56,8 @@ def build_parser() -> flags.GoFlagParser:
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
     p.add_bool("topology_view", False, "experimental: bind-mount a kfd topology filtered to the allocated "
                                        "GPUs into each container (faster ROCr start-up, GPU isolation)")
+    p.add_bool("node_view", False, "experimental: bind-mount /sys/devices/system/node without the per-CPU cache "
+                                   "descriptors ROCr walks at start-up (3x faster hsa_init on 256-CPU hosts)")
     p.add_str("log_format", "glog", "glog | json")
     p.add_str("trace_file", "", "write a Chrome trace of RPC / allocator / health spans to this file on exit")
     p.add_str("config", os.environ.get("CONFIG_FILE_PATH", ""), "YAML config file (gpu.device_count, ...)")
@@ -95,8 +97,9 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
                           liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
                           smi_ecc=ns.smi_ecc, dev_root=ns.dev_root, liveness_mode=ns.liveness_mode)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
+        node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count,
-                             topology_view_dir=view_dir)
+                             topology_view_dir=view_dir, node_view_dir=node_dir)
     if name == C.VF_PASSTHROUGH:
         from ..plugin.passthrough import VfImpl
         return VfImpl(ns.resource_naming_strategy, ns.sysfs_root, ns.exporter_socket or None)

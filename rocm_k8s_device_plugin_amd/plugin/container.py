@@ -22,6 +22,7 @@ from ..allocator import AllocationError
 from ..health.monitor import HealthConfig, HealthMonitor
 from ..proto import deviceplugin as pb
 from ..topology import Gpu, Inventory, discover
+from ..node_view import NodeView
 from ..topology_view import KFD_TOPOLOGY_CONTAINER_PATH, TopologyViews
 from ..utils import log
 from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto
@@ -35,12 +36,14 @@ class ContainerImpl(DeviceImpl):
     def __init__(self, naming_strategy: str = C.STRATEGY_SINGLE, sysfs_root: str = "/sys",
                  health_cfg: Optional[HealthConfig] = None, device_count_limit: Optional[int] = None,
                  inventory: Optional[Inventory] = None, monitor: Optional[HealthMonitor] = None,
-                 topology_view_dir: Optional[str] = None):
+                 topology_view_dir: Optional[str] = None, node_view_dir: Optional[str] = None):
         self.strategy = naming_strategy
         self.sysfs_root = sysfs_root
         # opt-in: per-allocation filtered kfd topology bind-mounted into the container
         self.topology_views = (TopologyViews(topology_view_dir, os.path.join(sysfs_root, "class/kfd/kfd/topology"))
                                if topology_view_dir else None)
+        # opt-in: NUMA-node sysfs without the per-CPU cache walk ROCr does at start-up
+        self.node_view = NodeView(node_view_dir, sysfs_root) if node_view_dir else None
         if not os.path.exists(os.path.join(sysfs_root, C.KFD_CLASS_REL)):
             raise DeviceImplError("No amd gpu driver loaded")
         self.inv = inventory or discover(sysfs_root, device_count_limit)
@@ -142,6 +145,12 @@ class ContainerImpl(DeviceImpl):
                     car.mounts.add(container_path=KFD_TOPOLOGY_CONTAINER_PATH, host_path=view, read_only=True)
                 except OSError as e:  # never fail an admission over an optimisation
                     _log.warning("topology view for %s unavailable: %s", list(creq.devices_ids), e)
+            if self.node_view is not None and creq.devices_ids:
+                try:
+                    for host, ctr in self.node_view.mounts():
+                        car.mounts.add(container_path=ctr, host_path=host, read_only=True)
+                except OSError as e:
+                    _log.warning("node view unavailable: %s", e)
         return resp
 
     def preferred_allocation(self, ctx: PluginContext,

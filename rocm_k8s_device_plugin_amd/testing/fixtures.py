@@ -45,6 +45,7 @@ class FixtureSpec:
     memory_partition: str = "nps1"
     numa_nodes: int = 2
     cpus_per_numa: int = 64
+    cpu_dirs_per_numa: int = 2  # CPUs materialised under devices/system/{node,cpu} (keeps fixtures small)
     hive_size: int = 8                  # GPUs per xGMI hive (8 = one hive)
     gfx_target_version: int = 90500
     device_id: int = MI355X_DEVICE_ID
@@ -117,6 +118,23 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
         _w(sysfs / "class/kfd/kfd/topology/generation_id", "1")
 
     numa = max(1, spec.numa_nodes)
+    # host NUMA/CPU sysfs (a few CPUs per node, each with cache descriptors)
+    for c in range(numa):
+        nd = sysfs / f"devices/system/node/node{c}"
+        _w(nd / "meminfo", f"Node {c} MemTotal:       1048576 kB\n")
+        _w(nd / "distance", " ".join("10" if i == c else "32" for i in range(numa)) + "\n")
+        _w(nd / "cpulist", f"{c * spec.cpus_per_numa}-{(c + 1) * spec.cpus_per_numa - 1}\n")
+        for k in range(spec.cpu_dirs_per_numa):
+            cpu = c * spec.cpus_per_numa + k
+            cd = sysfs / f"devices/system/cpu/cpu{cpu}"
+            _w(cd / "online", "1\n")
+            for idx, (lvl, typ, size) in enumerate([(1, "Data", "48K"), (1, "Instruction", "32K"), (2, "Unified", "1024K"),
+                                                    (3, "Unified", "32768K")]):
+                _w(cd / f"cache/index{idx}/level", f"{lvl}\n")
+                _w(cd / f"cache/index{idx}/type", f"{typ}\n")
+                _w(cd / f"cache/index{idx}/size", f"{size}\n")
+            _link(sysfs / f"devices/system/cpu/cpu{cpu}", nd / f"cpu{cpu}")
+    _w(sysfs / "devices/system/node/online", f"0-{numa - 1}\n")
     # CPU nodes 0..numa-1 (passthrough hosts run gim/vfio-pci, not amdgpu+kfd)
     for c in range(numa if spec.mode == "container" else 0):
         nd = nodes_dir / str(c)

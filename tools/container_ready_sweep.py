@@ -70,6 +70,7 @@ def run_once(env_extra, args, runtime="hsa"):
         "phase_us": doc["devices"][0].get("phase_us", {}) if doc["devices"] else {},
         "cpu_ms_runtime": doc.get("cpu_ms_runtime", 0.0),
         "cpu_ms_ready": doc.get("cpu_ms_ready", 0.0),
+        "cpu_user_ms_runtime": doc.get("cpu_user_ms_runtime", 0.0),
         "read_syscalls_runtime": doc.get("read_syscalls_runtime", -1),
         "init_profile": doc.get("init_profile"),
     }

@@ -1,11 +1,9 @@
 #!/bin/bash
-# dlopen(ROCr) overlapped with the /dev/kfd open: start-up split + bench.
+# ROCr start-up CPU split (user vs kernel) and blocking-syscall attribution.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests/test_gpu.py -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python tools/container_ready_sweep.py --reps 15 --sample-init 250 --wait-kfd --tag "@wait_kfd" \
-    --only hsa:rocr_visible,hip:rocr_visible --out gpurun_out/container_dlopen.json > gpurun_out/container_dlopen.log 2>&1 || { cat gpurun_out/container_dlopen.log; exit 1; }
-cat gpurun_out/container_dlopen.log
-timeout -k 10 400 python bench.py --gpus 1 --steps 40 --warmup 3 --hip-compare 10 --b2b-compare 10 > gpurun_out/bench1.json 2> gpurun_out/bench1.err || { tail gpurun_out/bench1.err; exit 1; }
-cat gpurun_out/bench1.json; cat /proc/loadavg
+timeout -k 10 300 python tools/container_ready_sweep.py --reps 15 --sample-init 100 --wait-kfd --tag "@wait_kfd" \
+    --only hsa:rocr_visible,hsa:rocr_visible+identify_only --out gpurun_out/container_cpusplit.json > gpurun_out/container_cpusplit.log 2>&1 || { cat gpurun_out/container_cpusplit.log; exit 1; }
+python -c "
+import json;d=json.load(open('gpurun_out/container_cpusplit.json'))
+for k,v in d.items(): print(k, 'init',v['hip_init_ms'],'ready',v['ready_ms'],'cpu',v['cpu_ms_runtime'],'user',v['cpu_user_ms_runtime'],'reads',v['read_syscalls_runtime'],v['init_us'],v['init_profile'])"
