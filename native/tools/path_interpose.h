@@ -1,0 +1,229 @@
+#pragma once
+// Path interposition for measurement builds (never linked into shipped binaries).
+//
+// The executable exports its own open/openat/fopen/opendir (-rdynamic). ROCr
+// (dlopen()ed below) resolves those symbols against the executable first, so
+// every path its thunk opens passes through here: counted per path template
+// (digit runs folded to N) and, if it matches a prefix in
+// $MI355X_INITPROF_HIDE (colon separated, 'N' stands for a digit run), refused with ENOENT — an in-process
+// stand-in for a container view that lacks those files (bind mounts need root).
+//
+// Include in exactly ONE translation unit of an executable linked with
+// -rdynamic; call path_interpose_configure() at the top of main().
+#include <dirent.h>
+#include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <time.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+std::mutex g_mu;
+std::map<std::string, long>* g_counts = nullptr;  // allocated lazily (interposers run before main)
+std::vector<std::string>* g_hide = nullptr;
+// $MI355X_INITPROF_REDIRECT="<from>=<to>[;<from>=<to>...]": path prefix rewrites
+std::vector<std::pair<std::string, std::string>>* g_redir = nullptr;
+std::atomic<long> g_redirected{0};
+thread_local std::string t_path;
+std::atomic<long> g_hidden{0};
+thread_local bool t_in_hook = false;
+
+double now_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+
+std::string fold(const char* p) {
+  std::string o;
+  for (; p && *p && o.size() < 160; ++p) {
+    if (*p >= '0' && *p <= '9') {
+      if (o.empty() || o.back() != 'N') o += 'N';
+    } else {
+      o += *p;
+    }
+  }
+  return o;
+}
+
+// redirect `path` if it starts with the configured prefix (emulates a bind mount)
+const char* map_path(const char* path) {
+  if (!path || !g_redir) return path;
+  for (const auto& r : *g_redir) {
+    if (std::strncmp(path, r.first.c_str(), r.first.size()) == 0) {
+      t_path = r.second + (path + r.first.size());
+      g_redirected.fetch_add(1);
+      return t_path.c_str();
+    }
+  }
+  return path;
+}
+
+// true -> refuse this path
+bool note(const char* path) {
+  if (!path || t_in_hook) return false;
+  t_in_hook = true;
+  bool hide = false;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_counts) g_counts = new std::map<std::string, long>();
+    const std::string f = fold(path);
+    ++(*g_counts)[f];
+    if (g_hide)  // prefixes are matched against the folded path ('N' = any digits)
+      for (const auto& h : *g_hide)
+        if (!h.empty() && f.compare(0, h.size(), h) == 0) hide = true;
+  }
+  t_in_hook = false;
+  if (hide) g_hidden.fetch_add(1);
+  return hide;
+}
+
+template <typename F>
+F real(const char* name) {
+  return reinterpret_cast<F>(dlsym(RTLD_NEXT, name));
+}
+
+}  // namespace
+
+extern "C" {
+
+int open(const char* path, int flags, ...) {
+  static auto fn = real<int (*)(const char*, int, ...)>("open");
+  mode_t mode = 0;
+  if (flags & (O_CREAT | O_TMPFILE)) {
+    va_list ap;
+    va_start(ap, flags);
+    mode = va_arg(ap, mode_t);
+    va_end(ap);
+  }
+  if (note(path)) {
+    errno = ENOENT;
+    return -1;
+  }
+  return fn(map_path(path), flags, mode);
+}
+
+int open64(const char* path, int flags, ...) {
+  static auto fn = real<int (*)(const char*, int, ...)>("open64");
+  mode_t mode = 0;
+  if (flags & (O_CREAT | O_TMPFILE)) {
+    va_list ap;
+    va_start(ap, flags);
+    mode = va_arg(ap, mode_t);
+    va_end(ap);
+  }
+  if (note(path)) {
+    errno = ENOENT;
+    return -1;
+  }
+  return fn(map_path(path), flags, mode);
+}
+
+int openat(int dirfd, const char* path, int flags, ...) {
+  static auto fn = real<int (*)(int, const char*, int, ...)>("openat");
+  mode_t mode = 0;
+  if (flags & (O_CREAT | O_TMPFILE)) {
+    va_list ap;
+    va_start(ap, flags);
+    mode = va_arg(ap, mode_t);
+    va_end(ap);
+  }
+  if (note(path)) {
+    errno = ENOENT;
+    return -1;
+  }
+  return fn(dirfd, map_path(path), flags, mode);
+}
+
+FILE* fopen(const char* path, const char* mode) {
+  static auto fn = real<FILE* (*)(const char*, const char*)>("fopen");
+  if (note(path)) {
+    errno = ENOENT;
+    return nullptr;
+  }
+  return fn(map_path(path), mode);
+}
+
+FILE* fopen64(const char* path, const char* mode) {
+  static auto fn = real<FILE* (*)(const char*, const char*)>("fopen64");
+  if (note(path)) {
+    errno = ENOENT;
+    return nullptr;
+  }
+  return fn(map_path(path), mode);
+}
+
+DIR* opendir(const char* path) {
+  static auto fn = real<DIR* (*)(const char*)>("opendir");
+  if (note(path)) {
+    errno = ENOENT;
+    return nullptr;
+  }
+  return fn(map_path(path));
+}
+
+}  // extern "C"
+
+
+// Reads $MI355X_INITPROF_HIDE / $MI355X_INITPROF_REDIRECT and resets the counters.
+inline void path_interpose_configure() {
+  if (const char* h = std::getenv("MI355X_INITPROF_HIDE")) {
+    g_hide = new std::vector<std::string>();
+    std::string s = h;
+    size_t pos = 0;
+    while (pos <= s.size()) {
+      size_t c = s.find(':', pos);
+      if (c == std::string::npos) c = s.size();
+      g_hide->push_back(s.substr(pos, c - pos));
+      pos = c + 1;
+    }
+  }
+  if (const char* r = std::getenv("MI355X_INITPROF_REDIRECT")) {
+    g_redir = new std::vector<std::pair<std::string, std::string>>();
+    std::string s = r;
+    size_t pos = 0;
+    while (pos < s.size()) {
+      size_t c = s.find(';', pos);
+      if (c == std::string::npos) c = s.size();
+      const std::string item = s.substr(pos, c - pos);
+      const size_t eq = item.find('=');
+      if (eq != std::string::npos) g_redir->emplace_back(item.substr(0, eq), item.substr(eq + 1));
+      pos = c + 1;
+    }
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_counts) g_counts->clear();  // ignore the dynamic loader's own opens
+  }
+}
+
+// {"opens":N,"hidden":N,"redirected":N,"by_template":{...top 40...}}
+inline std::string path_interpose_json() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  long total = 0;
+  std::vector<std::pair<long, std::string>> top;
+  if (g_counts)
+    for (const auto& kv : *g_counts) {
+      total += kv.second;
+      top.emplace_back(kv.second, kv.first);
+    }
+  std::sort(top.rbegin(), top.rend());
+  std::string o;
+  for (size_t i = 0; i < top.size() && i < 40; ++i) {
+    if (i) o += ",";
+    o += "\"" + top[i].second + "\":" + std::to_string(top[i].first);
+  }
+  return "{\"opens\":" + std::to_string(total) + ",\"hidden\":" + std::to_string(g_hidden.load()) +
+         ",\"redirected\":" + std::to_string(g_redirected.load()) + ",\"by_template\":{" + o + "}}";
+}

@@ -1,210 +1,13 @@
 // mi355x-rocr-initprof: which files does ROCr's hsa_init() walk, and what does
-// hiding some of them save? (measurement tool, not shipped in the image)
+// hiding or redirecting some of them save? (measurement tool, not shipped)
 //
-// The executable exports its own open/openat/fopen/opendir (-rdynamic). ROCr
-// (dlopen()ed below) resolves those symbols against the executable first, so
-// every path its thunk opens passes through here: counted per path template
-// (digit runs folded to N) and, if it matches a prefix in
-// $MI355X_INITPROF_HIDE (colon separated, 'N' stands for a digit run), refused with ENOENT — an in-process
-// stand-in for a container view that lacks those files (bind mounts need root).
-//
-//   mi355x-rocr-initprof [--reps N]    -> one JSON line
-#include <dirent.h>
-#include <dlfcn.h>
-#include <errno.h>
-#include <fcntl.h>
-#include <stdarg.h>
-#include <stdio.h>
-#include <time.h>
-
+//   [MI355X_INITPROF_HIDE=...] [MI355X_INITPROF_REDIRECT=...] mi355x-rocr-initprof  -> one JSON line
 #include <hsa/hsa.h>
 
-#include <algorithm>
-#include <atomic>
-#include <cstdlib>
-#include <cstring>
-#include <map>
-#include <mutex>
-#include <string>
-#include <vector>
-
-namespace {
-
-std::mutex g_mu;
-std::map<std::string, long>* g_counts = nullptr;  // allocated lazily (interposers run before main)
-std::vector<std::string>* g_hide = nullptr;
-// $MI355X_INITPROF_REDIRECT="<from>=<to>[;<from>=<to>...]": path prefix rewrites
-std::vector<std::pair<std::string, std::string>>* g_redir = nullptr;
-std::atomic<long> g_redirected{0};
-thread_local std::string t_path;
-std::atomic<long> g_hidden{0};
-thread_local bool t_in_hook = false;
-
-double now_ms() {
-  timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
-}
-
-std::string fold(const char* p) {
-  std::string o;
-  for (; p && *p && o.size() < 160; ++p) {
-    if (*p >= '0' && *p <= '9') {
-      if (o.empty() || o.back() != 'N') o += 'N';
-    } else {
-      o += *p;
-    }
-  }
-  return o;
-}
-
-// redirect `path` if it starts with the configured prefix (emulates a bind mount)
-const char* map_path(const char* path) {
-  if (!path || !g_redir) return path;
-  for (const auto& r : *g_redir) {
-    if (std::strncmp(path, r.first.c_str(), r.first.size()) == 0) {
-      t_path = r.second + (path + r.first.size());
-      g_redirected.fetch_add(1);
-      return t_path.c_str();
-    }
-  }
-  return path;
-}
-
-// true -> refuse this path
-bool note(const char* path) {
-  if (!path || t_in_hook) return false;
-  t_in_hook = true;
-  bool hide = false;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_counts) g_counts = new std::map<std::string, long>();
-    const std::string f = fold(path);
-    ++(*g_counts)[f];
-    if (g_hide)  // prefixes are matched against the folded path ('N' = any digits)
-      for (const auto& h : *g_hide)
-        if (!h.empty() && f.compare(0, h.size(), h) == 0) hide = true;
-  }
-  t_in_hook = false;
-  if (hide) g_hidden.fetch_add(1);
-  return hide;
-}
-
-template <typename F>
-F real(const char* name) {
-  return reinterpret_cast<F>(dlsym(RTLD_NEXT, name));
-}
-
-}  // namespace
-
-extern "C" {
-
-int open(const char* path, int flags, ...) {
-  static auto fn = real<int (*)(const char*, int, ...)>("open");
-  mode_t mode = 0;
-  if (flags & (O_CREAT | O_TMPFILE)) {
-    va_list ap;
-    va_start(ap, flags);
-    mode = va_arg(ap, mode_t);
-    va_end(ap);
-  }
-  if (note(path)) {
-    errno = ENOENT;
-    return -1;
-  }
-  return fn(map_path(path), flags, mode);
-}
-
-int open64(const char* path, int flags, ...) {
-  static auto fn = real<int (*)(const char*, int, ...)>("open64");
-  mode_t mode = 0;
-  if (flags & (O_CREAT | O_TMPFILE)) {
-    va_list ap;
-    va_start(ap, flags);
-    mode = va_arg(ap, mode_t);
-    va_end(ap);
-  }
-  if (note(path)) {
-    errno = ENOENT;
-    return -1;
-  }
-  return fn(map_path(path), flags, mode);
-}
-
-int openat(int dirfd, const char* path, int flags, ...) {
-  static auto fn = real<int (*)(int, const char*, int, ...)>("openat");
-  mode_t mode = 0;
-  if (flags & (O_CREAT | O_TMPFILE)) {
-    va_list ap;
-    va_start(ap, flags);
-    mode = va_arg(ap, mode_t);
-    va_end(ap);
-  }
-  if (note(path)) {
-    errno = ENOENT;
-    return -1;
-  }
-  return fn(dirfd, map_path(path), flags, mode);
-}
-
-FILE* fopen(const char* path, const char* mode) {
-  static auto fn = real<FILE* (*)(const char*, const char*)>("fopen");
-  if (note(path)) {
-    errno = ENOENT;
-    return nullptr;
-  }
-  return fn(map_path(path), mode);
-}
-
-FILE* fopen64(const char* path, const char* mode) {
-  static auto fn = real<FILE* (*)(const char*, const char*)>("fopen64");
-  if (note(path)) {
-    errno = ENOENT;
-    return nullptr;
-  }
-  return fn(map_path(path), mode);
-}
-
-DIR* opendir(const char* path) {
-  static auto fn = real<DIR* (*)(const char*)>("opendir");
-  if (note(path)) {
-    errno = ENOENT;
-    return nullptr;
-  }
-  return fn(map_path(path));
-}
-
-}  // extern "C"
+#include "path_interpose.h"
 
 int main(int argc, char** argv) {
-  if (const char* h = std::getenv("MI355X_INITPROF_HIDE")) {
-    g_hide = new std::vector<std::string>();
-    std::string s = h;
-    size_t pos = 0;
-    while (pos <= s.size()) {
-      size_t c = s.find(':', pos);
-      if (c == std::string::npos) c = s.size();
-      g_hide->push_back(s.substr(pos, c - pos));
-      pos = c + 1;
-    }
-  }
-  if (const char* r = std::getenv("MI355X_INITPROF_REDIRECT")) {
-    g_redir = new std::vector<std::pair<std::string, std::string>>();
-    std::string s = r;
-    size_t pos = 0;
-    while (pos < s.size()) {
-      size_t c = s.find(';', pos);
-      if (c == std::string::npos) c = s.size();
-      const std::string item = s.substr(pos, c - pos);
-      const size_t eq = item.find('=');
-      if (eq != std::string::npos) g_redir->emplace_back(item.substr(0, eq), item.substr(eq + 1));
-      pos = c + 1;
-    }
-  }
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (g_counts) g_counts->clear();  // ignore the dynamic loader's own opens
-  }
+  path_interpose_configure();
   const double t0 = now_ms();
   void* lib = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_GLOBAL);
   if (!lib) lib = dlopen("/opt/rocm/lib/libhsa-runtime64.so.1", RTLD_NOW | RTLD_GLOBAL);
@@ -221,25 +24,9 @@ int main(int argc, char** argv) {
   int agents = 0;
   if (s == HSA_STATUS_SUCCESS)
     iterate([](hsa_agent_t, void* n) { ++*static_cast<int*>(n); return HSA_STATUS_SUCCESS; }, &agents);
-  std::lock_guard<std::mutex> lk(g_mu);
-  long total = 0;
-  std::string o;
-  std::vector<std::pair<long, std::string>> top;
-  if (g_counts)
-    for (const auto& kv : *g_counts) {
-      total += kv.second;
-      top.emplace_back(kv.second, kv.first);
-    }
-  std::sort(top.rbegin(), top.rend());
-  for (size_t i = 0; i < top.size() && i < 40; ++i) {
-    if (i) o += ",";
-    o += "\"" + top[i].second + "\":" + std::to_string(top[i].first);
-  }
-  std::printf("{\"ok\":%s,\"hsa_status\":%d,\"agents\":%d,\"dlopen_ms\":%.2f,\"hsa_init_ms\":%.2f,"
-              "\"opens\":%ld,\"hidden\":%ld,\"redirected\":%ld,\"hide\":\"%s\",\"templates\":%zu,\"by_template\":{%s}}\n",
-              s == HSA_STATUS_SUCCESS ? "true" : "false", static_cast<int>(s), agents, t1 - t0, t2 - t1, total,
-              g_hidden.load(), g_redirected.load(), std::getenv("MI355X_INITPROF_HIDE") ? std::getenv("MI355X_INITPROF_HIDE") : "",
-              top.size(), o.c_str());
+  std::printf("{\"ok\":%s,\"hsa_status\":%d,\"agents\":%d,\"dlopen_ms\":%.2f,\"hsa_init_ms\":%.2f,\"walk\":%s}\n",
+              s == HSA_STATUS_SUCCESS ? "true" : "false", static_cast<int>(s), agents, t1 - t0, t2 - t1,
+              path_interpose_json().c_str());
   (void)argc;
   (void)argv;
   return s == HSA_STATUS_SUCCESS ? 0 : 1;

@@ -39,6 +39,8 @@ VARIANTS = {
                           "HSA_CU_MASK_SKIP_INIT": "1", "HSA_DISABLE_PC_SAMPLING": "1"},
 }
 SAMPLE_ARGS: list = []
+EXE_OVERRIDE: list = []   # --exe: e.g. the path-interposing measurement build
+EXTRA_ENV: dict = {}      # --env K=V
 
 
 def kfd_procs():
@@ -51,7 +53,9 @@ def kfd_procs():
 def run_once(env_extra, args, runtime="hsa"):
     env = {k: v for k, v in os.environ.items() if k not in VIS}
     env.update(env_extra)
-    argv = [str(probe_executable(runtime)), "--devices", "0", "--iters", "4"] + args + SAMPLE_ARGS
+    env.update(EXTRA_ENV)
+    argv = [EXE_OVERRIDE[0] if EXE_OVERRIDE else str(probe_executable(runtime)), "--devices", "0", "--iters", "4"] \
+        + args + SAMPLE_ARGS
     t0 = time.monotonic_ns()
     p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=120)
     t1 = time.monotonic_ns()
@@ -88,6 +92,8 @@ def main():
     ap.add_argument("--probe-args", default="", help="extra probe arguments, e.g. '--exit fast'")
     ap.add_argument("--wait-kfd", action="store_true",
                     help="after each run wait until its /sys/class/kfd/kfd/proc entry is gone (<= 2 s)")
+    ap.add_argument("--exe", default="", help="entrypoint binary instead of the built probe")
+    ap.add_argument("--env", action="append", default=[], help="K=V added to every run's environment")
     ap.add_argument("--tag", default="", help="suffix for the row names")
     ap.add_argument("--parent-gpu", action="store_true",
                     help="initialise HIP in this (parent) process first, like a torch-based harness would")
@@ -95,6 +101,11 @@ def main():
     if a.sample_init:
         SAMPLE_ARGS[:] = ["--sample-init", str(a.sample_init)]
     SAMPLE_ARGS.extend(a.probe_args.split())
+    if a.exe:
+        EXE_OVERRIDE.append(a.exe)
+    for kv in a.env:
+        k, v = kv.split("=", 1)
+        EXTRA_ENV[k] = v
     if a.parent_gpu:
         import torch
         torch.cuda.synchronize() if torch.cuda.is_available() else None
