@@ -271,6 +271,36 @@ PYBIND11_MODULE(_native, m) {
   });
 
   m.def("smi_available", &smi_available);
+  m.def("smi_event_name", [](int t) { return std::string(smi_event_name(t)); });
+  py::class_<SmiEventWatcher>(m, "SmiEventWatcher")
+      .def(py::init<>())
+      .def("start", [](SmiEventWatcher& w, uint64_t mask) {
+        py::gil_scoped_release nogil;
+        return w.start(mask);
+      }, py::arg("mask"))
+      .def("poll", [](SmiEventWatcher& w, int timeout_ms) {
+        std::vector<SmiEvent> ev;
+        {
+          py::gil_scoped_release nogil;
+          ev = w.poll(timeout_ms);
+        }
+        py::list out;
+        for (auto& e : ev) {
+          py::dict d;
+          d["bdf"] = e.bdf;
+          d["type"] = e.type;
+          d["name"] = e.name;
+          d["message"] = e.message;
+          out.append(d);
+        }
+        return out;
+      }, py::arg("timeout_ms") = 0)
+      .def("stop", [](SmiEventWatcher& w) {
+        py::gil_scoped_release nogil;
+        w.stop();
+      })
+      .def_property_readonly("running", &SmiEventWatcher::running)
+      .def_property_readonly("devices", &SmiEventWatcher::devices);
   m.def("smi_snapshot", [] {
     SmiSnapshot s;
     {

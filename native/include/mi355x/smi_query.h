@@ -45,7 +45,41 @@ struct SmiSnapshot {
 };
 
 bool smi_available();
-// amdsmi_init(AMD_GPUS) -> enumerate every GPU processor -> amdsmi_shut_down.
+// amdsmi_init(AMD_GPUS) -> enumerate every GPU processor -> amdsmi_shut_down
+// (init/shut_down are reference-counted across this file's users).
 SmiSnapshot smi_snapshot();
+
+// Push-style GPU events from the driver (amdsmi_*_gpu_event_notification):
+// resets, VM faults, thermal throttling, queue evictions. SURVEY §5 "failure
+// detection": the health loop drains them every pulse instead of waiting for
+// a probe to fail.
+struct SmiEvent {
+  std::string bdf;
+  int type = 0;            // amdsmi_evt_notification_type_t
+  std::string name;        // "gpu_pre_reset", ...
+  std::string message;
+};
+
+class SmiEventWatcher {
+ public:
+  SmiEventWatcher() = default;
+  ~SmiEventWatcher();
+  SmiEventWatcher(const SmiEventWatcher&) = delete;
+  SmiEventWatcher& operator=(const SmiEventWatcher&) = delete;
+  // Subscribe every GPU to `mask` (bit i-1 = event type i). Returns "" or an error.
+  std::string start(uint64_t mask);
+  // Events that arrived within `timeout_ms` (0 = just drain what is queued).
+  std::vector<SmiEvent> poll(int timeout_ms);
+  void stop();
+  bool running() const { return running_; }
+  size_t devices() const { return handles_.size(); }
+
+ private:
+  bool running_ = false;
+  std::vector<void*> handles_;
+  std::vector<std::string> bdfs_;
+};
+
+const char* smi_event_name(int type);
 
 }  // namespace mi355x

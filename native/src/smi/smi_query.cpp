@@ -35,6 +35,10 @@ struct SmiLib {
   decltype(&amdsmi_get_gpu_vram_info) vram = nullptr;
   decltype(&amdsmi_get_gpu_total_ecc_count) ecc = nullptr;
   decltype(&amdsmi_get_gpu_enumeration_info) enumeration = nullptr;
+  decltype(&amdsmi_init_gpu_event_notification) evt_init = nullptr;
+  decltype(&amdsmi_set_gpu_event_notification_mask) evt_mask = nullptr;
+  decltype(&amdsmi_get_gpu_event_notification) evt_get = nullptr;
+  decltype(&amdsmi_stop_gpu_event_notification) evt_stop = nullptr;
 };
 
 template <typename T>
@@ -65,8 +69,54 @@ const SmiLib& smi() {
     bind(l.h, "amdsmi_get_gpu_vram_info", &l.vram);
     bind(l.h, "amdsmi_get_gpu_total_ecc_count", &l.ecc);
     bind(l.h, "amdsmi_get_gpu_enumeration_info", &l.enumeration);
+    bind(l.h, "amdsmi_init_gpu_event_notification", &l.evt_init);
+    bind(l.h, "amdsmi_set_gpu_event_notification_mask", &l.evt_mask);
+    bind(l.h, "amdsmi_get_gpu_event_notification", &l.evt_get);
+    bind(l.h, "amdsmi_stop_gpu_event_notification", &l.evt_stop);
   });
   return l;
+}
+
+// amdsmi_init / amdsmi_shut_down shared by snapshots and the event watcher
+std::mutex g_init_mu;
+int g_init_refs = 0;
+
+bool acquire() {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_init_refs == 0 && smi().init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return false;
+  ++g_init_refs;
+  return true;
+}
+
+void release() {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_init_refs > 0 && --g_init_refs == 0 && smi().shut_down) smi().shut_down();
+}
+
+std::string bdf_of(amdsmi_processor_handle h) {
+  amdsmi_bdf_t bdf{};
+  if (!smi().bdf || smi().bdf(h, &bdf) != AMDSMI_STATUS_SUCCESS) return "";
+  char buf[64];
+  std::snprintf(buf, sizeof(buf), "%04llx:%02llx:%02llx.%llx", static_cast<unsigned long long>(bdf.domain_number),
+                static_cast<unsigned long long>(bdf.bus_number), static_cast<unsigned long long>(bdf.device_number),
+                static_cast<unsigned long long>(bdf.function_number));
+  return buf;
+}
+
+std::vector<amdsmi_processor_handle> all_gpus() {
+  std::vector<amdsmi_processor_handle> out;
+  uint32_t nsock = 0;
+  if (smi().sockets(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS || nsock == 0) return out;
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  smi().sockets(&nsock, socks.data());
+  for (uint32_t s = 0; s < nsock; ++s) {
+    uint32_t nproc = 0;
+    if (smi().processors(socks[s], &nproc, nullptr) != AMDSMI_STATUS_SUCCESS || nproc == 0) continue;
+    std::vector<amdsmi_processor_handle> procs(nproc);
+    smi().processors(socks[s], &nproc, procs.data());
+    out.insert(out.end(), procs.begin(), procs.end());
+  }
+  return out;
 }
 
 std::string lower(const char* s) {
@@ -89,7 +139,7 @@ SmiSnapshot smi_snapshot() {
     snap.error = "libamd_smi unavailable";
     return snap;
   }
-  if (L.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) {
+  if (!acquire()) {
     snap.error = "amdsmi_init failed";
     return snap;
   }
@@ -159,9 +209,86 @@ SmiSnapshot smi_snapshot() {
       }
     }
   }
-  if (L.shut_down) L.shut_down();
+  release();
   snap.ok = true;
   return snap;
+}
+
+const char* smi_event_name(int type) {
+  switch (type) {
+    case AMDSMI_EVT_NOTIF_VMFAULT: return "vmfault";
+    case AMDSMI_EVT_NOTIF_THERMAL_THROTTLE: return "thermal_throttle";
+    case AMDSMI_EVT_NOTIF_GPU_PRE_RESET: return "gpu_pre_reset";
+    case AMDSMI_EVT_NOTIF_GPU_POST_RESET: return "gpu_post_reset";
+    case AMDSMI_EVT_NOTIF_MIGRATE_START: return "migrate_start";
+    case AMDSMI_EVT_NOTIF_MIGRATE_END: return "migrate_end";
+    case AMDSMI_EVT_NOTIF_PAGE_FAULT_START: return "page_fault_start";
+    case AMDSMI_EVT_NOTIF_PAGE_FAULT_END: return "page_fault_end";
+    case AMDSMI_EVT_NOTIF_QUEUE_EVICTION: return "queue_eviction";
+    case AMDSMI_EVT_NOTIF_QUEUE_RESTORE: return "queue_restore";
+    case AMDSMI_EVT_NOTIF_UNMAP_FROM_GPU: return "unmap_from_gpu";
+    case AMDSMI_EVT_NOTIF_PROCESS_START: return "process_start";
+    case AMDSMI_EVT_NOTIF_PROCESS_END: return "process_end";
+    default: return "unknown";
+  }
+}
+
+SmiEventWatcher::~SmiEventWatcher() { stop(); }
+
+std::string SmiEventWatcher::start(uint64_t mask) {
+  stop();
+  const auto& L = smi();
+  if (!smi_available() || !L.evt_init || !L.evt_mask || !L.evt_get || !L.evt_stop)
+    return "libamd_smi event notification unavailable";
+  if (!acquire()) return "amdsmi_init failed";
+  for (auto h : all_gpus()) {
+    if (L.evt_init(h) != AMDSMI_STATUS_SUCCESS) continue;
+    if (L.evt_mask(h, mask) != AMDSMI_STATUS_SUCCESS) {
+      L.evt_stop(h);
+      continue;
+    }
+    handles_.push_back(h);
+    bdfs_.push_back(bdf_of(h));
+  }
+  if (handles_.empty()) {
+    release();
+    return "no GPU accepted event notification";
+  }
+  running_ = true;
+  return "";
+}
+
+std::vector<SmiEvent> SmiEventWatcher::poll(int timeout_ms) {
+  std::vector<SmiEvent> out;
+  if (!running_) return out;
+  for (;;) {
+    amdsmi_evt_notification_data_t data[32];
+    uint32_t n = 32;
+    const amdsmi_status_t st = smi().evt_get(timeout_ms, &n, data);
+    if (st != AMDSMI_STATUS_SUCCESS || n == 0) break;
+    for (uint32_t i = 0; i < n; ++i) {
+      SmiEvent e;
+      for (size_t k = 0; k < handles_.size(); ++k)
+        if (handles_[k] == data[i].processor_handle) e.bdf = bdfs_[k];
+      if (e.bdf.empty()) e.bdf = bdf_of(data[i].processor_handle);
+      e.type = static_cast<int>(data[i].event);
+      e.name = smi_event_name(e.type);
+      e.message = data[i].message;
+      out.push_back(std::move(e));
+    }
+    if (n < 32) break;
+    timeout_ms = 0;  // drain the rest without waiting again
+  }
+  return out;
+}
+
+void SmiEventWatcher::stop() {
+  if (!running_) return;
+  for (auto h : handles_) smi().evt_stop(h);
+  handles_.clear();
+  bdfs_.clear();
+  running_ = false;
+  release();
 }
 
 #else  // no amd-smi header at build time
@@ -172,6 +299,11 @@ SmiSnapshot smi_snapshot() {
   s.error = "built without amd_smi/amdsmi.h";
   return s;
 }
+const char* smi_event_name(int) { return "unknown"; }
+SmiEventWatcher::~SmiEventWatcher() = default;
+std::string SmiEventWatcher::start(uint64_t) { return "built without amd_smi/amdsmi.h"; }
+std::vector<SmiEvent> SmiEventWatcher::poll(int) { return {}; }
+void SmiEventWatcher::stop() {}
 
 #endif
 

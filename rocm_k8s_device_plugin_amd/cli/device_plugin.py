@@ -52,6 +52,8 @@ def build_parser() -> flags.GoFlagParser:
     p.add_float("liveness_timeout", 10.0, "per-device liveness probe deadline (s)")
     p.add_int("liveness_fail_threshold", 2, "consecutive probe failures before a device turns Unhealthy")
     p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
+    p.add_bool("smi_events", False, "subscribe to amd-smi GPU events; a device is Unhealthy between a "
+                                    "gpu_pre_reset and its gpu_post_reset, other events are counted")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
     p.add_bool("topology_view", False, "experimental: bind-mount a kfd topology filtered to the allocated "
@@ -95,7 +97,8 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
         from ..plugin.container import ContainerImpl
         hc = HealthConfig(exporter_socket=ns.exporter_socket or None, liveness=ns.liveness,
                           liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
-                          smi_ecc=ns.smi_ecc, dev_root=ns.dev_root, liveness_mode=ns.liveness_mode)
+                          smi_ecc=ns.smi_ecc, smi_events=ns.smi_events, dev_root=ns.dev_root,
+                          liveness_mode=ns.liveness_mode)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count,

@@ -14,7 +14,11 @@ Healthy only if every *available* source agrees:
 3. liveness: the gfx950 MFMA probe on that exact HIP device, with hysteresis
    (``fail_threshold`` consecutive failures to go Unhealthy,
    ``recover_threshold`` successes to come back);
-4. amd-smi: a rise in uncorrectable ECC errors since the last sweep.
+4. amd-smi: a rise in uncorrectable ECC errors since the last sweep;
+5. amd-smi events (push-style, drained every sweep): a ``gpu_pre_reset`` keeps
+   the device Unhealthy until its ``gpu_post_reset``; VM faults, thermal
+   throttling and queue evictions are counted
+   (``mi355x_dp_gpu_events_total``) and logged.
 
 Verdicts are published as immutable snapshots with a version number, so
 ListAndWatch streams can send on change without locks.
@@ -55,6 +59,7 @@ class HealthConfig:
     fail_threshold: int = 2
     recover_threshold: int = 1
     smi_ecc: bool = False
+    smi_events: bool = False
     dev_root: str = "/dev"
 
 
@@ -70,7 +75,7 @@ class HealthMonitor:
     def __init__(self, inventory: Inventory, cfg: Optional[HealthConfig] = None,
                  prober: Optional[LivenessProber] = None,
                  ordinal_map: Optional[Mapping[str, int]] = None,
-                 exporter_fn: Optional[Callable] = None):
+                 exporter_fn: Optional[Callable] = None, event_source=None):
         self.inv = inventory
         self.cfg = cfg or HealthConfig()
         self.prober = prober
@@ -78,6 +83,11 @@ class HealthMonitor:
             self.prober = LivenessProber(timeout_s=self.cfg.liveness_timeout_s, iters=self.cfg.liveness_iters,
                                          max_parallel=self.cfg.liveness_parallel, mode=self.cfg.liveness_mode)
         self._ordinals = dict(ordinal_map) if ordinal_map is not None else None
+        # amd-smi event watcher (or a test double with start/poll/stop)
+        self._events = event_source
+        self._events_started = False
+        self._resetting: Dict[str, str] = {}   # bdf -> message of the pending pre-reset
+        self.event_counts: Dict[Tuple[str, str], int] = {}
         self._exporter_fn = exporter_fn or exporter.get_gpu_health
         self._track: Dict[str, _Track] = {d.id: _Track() for d in inventory.devices}
         self._ecc: Dict[str, int] = {}
@@ -143,10 +153,46 @@ class HealthMonitor:
                 bad[d.id] = f"uncorrectable ECC errors rose {prev}->{cur}"
         return bad
 
+    EVENT_MASK_NAMES = ("vmfault", "thermal_throttle", "gpu_pre_reset", "gpu_post_reset", "queue_eviction")
+    _EVENT_TYPES = {"vmfault": 1, "thermal_throttle": 2, "gpu_pre_reset": 3, "gpu_post_reset": 4,
+                    "queue_eviction": 9}
+
+    def _drain_events(self) -> None:
+        if self._events is None:
+            self._events = core().SmiEventWatcher()
+        if not self._events_started:
+            mask = 0
+            for nm in self.EVENT_MASK_NAMES:
+                mask |= 1 << (self._EVENT_TYPES[nm] - 1)
+            err = self._events.start(mask)
+            self._events_started = True
+            if err:
+                _log.warning("amd-smi event notification unavailable: %s", err)
+                return
+        if not getattr(self._events, "running", True):
+            return
+        from ..utils.metrics import REGISTRY
+        for ev in self._events.poll(0):
+            bdf, name = ev.get("bdf", ""), ev.get("name", "unknown")
+            key = (bdf, name)
+            self.event_counts[key] = self.event_counts.get(key, 0) + 1
+            REGISTRY.inc("mi355x_dp_gpu_events_total", help="amd-smi GPU events", bdf=bdf, event=name)
+            if name == "gpu_pre_reset":
+                self._resetting[bdf] = ev.get("message", "")
+                _log.warning("GPU %s: reset starting (%s)", bdf, ev.get("message", ""))
+            elif name == "gpu_post_reset":
+                self._resetting.pop(bdf, None)
+                _log.warning("GPU %s: reset finished", bdf)
+            else:
+                _log.info("GPU %s: %s %s", bdf, name, ev.get("message", ""))
+
     # ------------------------------------------------------------------ sweep
     async def close(self) -> None:
         if self.prober is not None:
             await self.prober.close()
+        if self._events is not None and self._events_started:
+            self._events.stop()
+            self._events_started = False
 
     async def check_once(self) -> bool:
         """Run one sweep; returns True if any verdict changed."""
@@ -190,6 +236,12 @@ class HealthMonitor:
         if self.cfg.smi_ecc:
             for dev_id, r in self._smi_ecc().items():
                 reasons[dev_id].append(r)
+
+        if self.cfg.smi_events:
+            self._drain_events()
+            for d in self.inv.devices:
+                if d.bdf in self._resetting:
+                    reasons[d.id].append("GPU reset in progress (amd-smi gpu_pre_reset, no post_reset yet)")
 
         new = {dev: Verdict(dp.UNHEALTHY if rs else dp.HEALTHY, tuple(rs)) for dev, rs in reasons.items()}
         changed = any(new[k].health != self._snapshot.get(k, Verdict("")).health for k in new)

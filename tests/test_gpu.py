@@ -175,6 +175,25 @@ def test_peer_probe_self_copy(ordinals):
     assert rep.summary()["pairs_ok"] == 1
 
 
+def test_smi_event_watcher_subscribes(inv):
+    """amd-smi event notification starts on the real GPU and drains without error.
+
+    A liveness probe run while subscribed makes kfd emit nothing we subscribe
+    to (no reset/fault), so the expectation is an empty or benign list."""
+    from rocm_k8s_device_plugin_amd.ops.native import core
+    w = core().SmiEventWatcher()
+    mask = (1 << 0) | (1 << 1) | (1 << 2) | (1 << 3) | (1 << 8)
+    err = w.start(mask)
+    assert err == "", err
+    assert w.running and w.devices >= 1
+    ev = w.poll(50)
+    assert all(e["name"] in ("vmfault", "thermal_throttle", "gpu_pre_reset", "gpu_post_reset", "queue_eviction")
+               for e in ev), ev
+    w.stop()
+    assert not w.running
+    assert w.poll(0) == []
+
+
 def test_smi_cross_check(inv):
     from rocm_k8s_device_plugin_amd.ops.native import core
     n = core()

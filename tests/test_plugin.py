@@ -561,3 +561,62 @@ def test_liveness_spawn_mode_never_starts_server(tmp_path):
     run(go())
     with pytest.raises(ValueError):
         LivenessProber(mode="bogus")
+
+
+class _FakeEvents:
+    def __init__(self):
+        self.queue, self.mask, self.running, self.stopped = [], None, False, False
+
+    def start(self, mask):
+        self.mask, self.running = mask, True
+        return ""
+
+    def poll(self, timeout_ms=0):
+        out, self.queue = self.queue, []
+        return out
+
+    def stop(self):
+        self.stopped, self.running = True, False
+
+
+def test_smi_events_reset_window_marks_device_unhealthy(tmp_path):
+    from rocm_k8s_device_plugin_amd.utils.metrics import REGISTRY
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ev = _FakeEvents()
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, smi_events=True), event_source=ev)
+    victim = inv.by_id[fi.bdfs[3]]
+
+    async def go():
+        assert not await mon.check_once()
+        assert ev.mask == (1 << 0) | (1 << 1) | (1 << 2) | (1 << 3) | (1 << 8)
+        ev.queue = [{"bdf": victim.bdf, "type": 3, "name": "gpu_pre_reset", "message": "RAS"},
+                    {"bdf": fi.bdfs[5], "type": 1, "name": "vmfault", "message": "pasid 7"}]
+        assert await mon.check_once()
+        snap = mon.snapshot()
+        assert {d for d, v in snap.items() if v.health == "Unhealthy"} == {victim.id}
+        assert "reset in progress" in snap[victim.id].reasons[0]
+        assert not await mon.check_once()          # still resetting, nothing new
+        ev.queue = [{"bdf": victim.bdf, "type": 4, "name": "gpu_post_reset", "message": ""}]
+        assert await mon.check_once()
+        assert all(v.health == "Healthy" for v in mon.snapshot().values())
+        assert mon.event_counts[(fi.bdfs[5], "vmfault")] == 1
+        await mon.close()
+        assert ev.stopped
+
+    run(go())
+    assert 'mi355x_dp_gpu_events_total{bdf="%s",event="vmfault"}' % fi.bdfs[5] in REGISTRY.render()
+
+
+def test_smi_events_unavailable_is_not_fatal(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, smi_events=True))   # real watcher, no GPU here
+
+    async def go():
+        await mon.check_once()
+        await mon.check_once()
+        assert all(v.health == "Healthy" for v in mon.snapshot().values())
+        await mon.close()
+
+    run(go())
