@@ -237,7 +237,10 @@ def main():
             kubelet.release("amd.com/gpu", ids)
         # pod termination: the driver finishes tearing down each container's
         # kfd process ~150 ms after it exits (bench latency excludes this wait)
-        waited = wait_kfd_released(lingering) if settle == "kfd" else 0.0
+        # N containers exiting together may be torn down one after another: allow
+        # ~0.25 s each (measured ~0.15 s), capped so a stuck entry cannot stall the run
+        cap = min(3.0, 0.25 + 0.25 * len(lingering))
+        waited = wait_kfd_released(lingering, timeout_s=cap) if settle == "kfd" else 0.0
         if record:
             settle_ms.append(waited)
         if sink is not None:
