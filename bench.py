@@ -63,6 +63,9 @@ def parse_args():
     ap.add_argument("--settle", default="kfd", choices=["kfd", "none"],
                     help="between admissions wait until the previous containers' kfd processes are torn down "
                          "(the previous pod has terminated) or start the next one immediately")
+    ap.add_argument("--node-view-compare", type=int, default=5,
+                    help="extra untimed admissions with the plugin's -node_view mounts applied to the containers "
+                         "(by path redirection: no root for bind mounts), reported for comparison")
     ap.add_argument("--b2b-compare", type=int, default=5,
                     help="extra untimed admissions with --settle none, reported for comparison")
     ap.add_argument("--peer-check", type=int, default=1,
@@ -208,11 +211,12 @@ def main():
             adm = loop.run_until_complete(kubelet.admit("amd.com/gpu", n))
             minors = render_minors_from_specs(adm.response.container_responses[0])
             ordl = [minor_to_ord[m] for m in minors]
-            payload = (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids))
+            mounts = [(m.container_path, m.host_path) for m in adm.response.container_responses[0].mounts]
+            payload = (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids), mounts)
         else:
             payload = None
         payload = d.bcast(payload)
-        t0, ordl, tot, amsl, ids = payload
+        t0, ordl, tot, amsl, ids, mounts = payload
         if args.fixture:
             import subprocess
             ts = time.monotonic_ns()
@@ -222,7 +226,7 @@ def main():
             lingering = frozenset()
         else:
             mine_ord = [ordl[d.rank]] if d.world > 1 else ordl
-            r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime)
+            r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime, mounts=mounts)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
             phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
@@ -265,7 +269,18 @@ def main():
     d.sync()
     elapsed = time.perf_counter() - t_start
     elapsed = d.max(elapsed)
-    hip_lat, b2b_lat = [], []
+    hip_lat, b2b_lat, nv_lat = [], [], []
+    if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
+        # the plugin returns -node_view mounts from now on (alias = host path: the
+        # fake runtime applies mounts by redirection and cannot add the alias mount)
+        if d.rank == 0:
+            from rocm_k8s_device_plugin_amd.node_view import NodeView
+            impl.node_view = NodeView(os.path.join(tmp, "node-view"), sysfs,
+                                      alias=os.path.join(sysfs, "devices/system/node"))
+        for _ in range(args.node_view_compare):
+            one_step(False, sink=nv_lat)
+        if d.rank == 0:
+            impl.node_view = None
     if not args.fixture and args.container_runtime == "hsa":
         for _ in range(args.hip_compare):
             one_step(False, runtime="hip", sink=hip_lat)
@@ -294,6 +309,7 @@ def main():
                  "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
                  "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
                  "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
+                 "latency_p50_ms_node_view_emulated": round(pct(nv_lat, .5), 3) if nv_lat else None,
                  "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
                  "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
                                              "hip_runtime_init": round(pct(rt_ms, .5), 3),

@@ -39,11 +39,6 @@ thread_local std::string t_path;
 std::atomic<long> g_hidden{0};
 thread_local bool t_in_hook = false;
 
-double now_ms() {
-  timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
-}
 
 std::string fold(const char* p) {
   std::string o;

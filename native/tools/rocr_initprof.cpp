@@ -6,6 +6,14 @@
 
 #include "path_interpose.h"
 
+namespace {
+double now_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+}  // namespace
+
 int main(int argc, char** argv) {
   path_interpose_configure();
   const double t0 = now_ms();

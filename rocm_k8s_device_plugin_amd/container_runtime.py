@@ -80,8 +80,23 @@ def wait_kfd_released(entries: Iterable[str], timeout_s: float = 0.5, proc_dir: 
     return (time.monotonic() - t0) * 1e3
 
 
+def mount_redirects(mounts: Iterable) -> str:
+    """Allocate-response mounts -> MI355X_INITPROF_REDIRECT spec (container_path=host_path;...).
+
+    A real runtime bind-mounts these; without root the fake runtime runs the
+    path-interposing probe build, which rewrites opens under container_path to
+    host_path (native/tools/path_interpose.h). Identity mounts are dropped.
+    """
+    out = []
+    for m in mounts:
+        cp, hp = (m.container_path, m.host_path) if hasattr(m, "container_path") else m
+        if os.path.abspath(cp) != os.path.abspath(hp):
+            out.append(f"{cp}={hp}")
+    return ";".join(out)
+
+
 def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int = 4,
-                    exe: Optional[str] = None, runtime: str = "hsa") -> ContainerResult:
+                    exe: Optional[str] = None, runtime: str = "hsa", mounts: Iterable = ()) -> ContainerResult:
     """Run the container entrypoint restricted to `ordinals`; block until ready/exit.
 
     runtime "hsa": the entrypoint launches the MFMA kernel straight through ROCr
@@ -90,6 +105,12 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
     """
     env = {k: v for k, v in os.environ.items() if k not in _VISIBILITY_VARS}
     env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
+    redirect = mount_redirects(mounts)
+    if redirect:
+        if runtime != "hsa":
+            raise ValueError("mounts can only be applied to the HSA entrypoint (mount emulation build)")
+        runtime = "mountemu"
+        env["MI355X_INITPROF_REDIRECT"] = redirect
     argv = [exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
             "--iters", str(iters), "--timeout", str(min(timeout_s, 30.0))]
     before = kfd_processes()

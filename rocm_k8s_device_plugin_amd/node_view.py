@@ -85,8 +85,12 @@ def build_node_view(src: str, dst: str, alias: str = NODE_ALIAS, cpu_root: str =
 class NodeView:
     """Builds the view once (lazily) and hands out the Allocate mounts."""
 
-    def __init__(self, root: str, sysfs_root: str = "/sys"):
+    def __init__(self, root: str, sysfs_root: str = "/sys", alias: str = NODE_ALIAS):
+        """`alias`: where the real node directory is visible in the container. A
+        runtime that cannot mount (bench.py's fake one) passes the host path
+        itself, and the view's symlinks then resolve without the alias mount."""
         self.root = root
+        self.alias = alias
         self.src = os.path.join(sysfs_root, "devices/system/node")
         self.src_cpu = os.path.join(sysfs_root, "devices/system/cpu")
         self._lock = threading.Lock()
@@ -101,7 +105,7 @@ class NodeView:
                 tmp = tempfile.mkdtemp(prefix=".node-", dir=self.root)
                 try:
                     self.links, self.hidden = build_node_view(self.src, os.path.join(tmp, "node"),
-                                                              src_cpu_root=self.src_cpu)
+                                                              alias=self.alias, src_cpu_root=self.src_cpu)
                     if os.path.exists(final):
                         shutil.rmtree(final)
                     os.rename(os.path.join(tmp, "node"), final)
@@ -112,4 +116,6 @@ class NodeView:
 
     def mounts(self) -> List[Tuple[str, str]]:
         """(host_path, container_path) pairs, in mount order."""
-        return [(self.src, NODE_ALIAS), (self.path(), NODE_CONTAINER_PATH)]
+        view = self.path()
+        alias = [] if os.path.abspath(self.alias) == os.path.abspath(self.src) else [(self.src, self.alias)]
+        return alias + [(view, NODE_CONTAINER_PATH)]

@@ -21,6 +21,7 @@ _hip = None
 PKG_DIR = Path(__file__).resolve().parent.parent
 PROBE_EXE = PKG_DIR / "bin" / "mi355x-liveness-probe"
 PROBE_EXE_HIP = PKG_DIR / "bin" / "mi355x-liveness-probe-hip"
+MOUNTEMU_EXE = PKG_DIR / "bin" / "mi355x-probe-mountemu"
 HSACO = PKG_DIR / "kernels" / "liveness_gfx950.hsaco"
 
 
@@ -63,8 +64,10 @@ def hip():
 
 
 def probe_executable(runtime: str = "hsa") -> Path:
-    """The liveness probe: "hsa" (ROCr-direct, default) or "hip"."""
-    exe = PROBE_EXE if runtime == "hsa" else PROBE_EXE_HIP
+    """The liveness probe: "hsa" (ROCr-direct, default), "hip", or "mountemu" (the
+    HSA probe built with path interposition, used by the fake container runtime
+    to apply Allocate mounts without root)."""
+    exe = {"hsa": PROBE_EXE, "hip": PROBE_EXE_HIP, "mountemu": MOUNTEMU_EXE}[runtime]
     if _auto_build_allowed():
         from .. import _build
         _build.ensure_built(hip=True)

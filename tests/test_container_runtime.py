@@ -28,3 +28,13 @@ def test_wait_kfd_released_tracks_procfs(tmp_path):
     assert wait_kfd_released(set(), proc_dir=str(proc)) < 5
     # a process that never goes away costs at most the timeout
     assert 90 <= wait_kfd_released({"100"}, timeout_s=0.1, proc_dir=str(proc)) < 1000
+
+
+def test_mount_redirects():
+    from rocm_k8s_device_plugin_amd.container_runtime import mount_redirects
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    ms = [pb.Mount(container_path="/sys/devices/system/node", host_path="/var/lib/x/node", read_only=True),
+          pb.Mount(container_path="/sys/devices/system/node", host_path="/sys/devices/system/node")]
+    assert mount_redirects(ms) == "/sys/devices/system/node=/var/lib/x/node"
+    assert mount_redirects([("/a", "/b"), ("/c", "/d")]) == "/a=/b;/c=/d"
+    assert mount_redirects([]) == ""

@@ -194,6 +194,24 @@ def test_smi_event_watcher_subscribes(inv):
     assert w.poll(0) == []
 
 
+def test_container_with_node_view_mounts(tmp_path, ordinals):
+    """The fake runtime applies -node_view mounts (by redirection) and ROCr in the
+    container skips the host CPU-cache walk: fewer opens, same MFMA verdict."""
+    from rocm_k8s_device_plugin_amd.container_runtime import start_container, wait_kfd_released
+    from rocm_k8s_device_plugin_amd.node_view import NodeView
+    o = sorted(ordinals.values())[0]
+    nv = NodeView(str(tmp_path / "nv"), "/sys", alias="/sys/devices/system/node")
+    plain = start_container([o], timeout_s=120)
+    assert plain.ok, plain.error
+    wait_kfd_released(plain.kfd_lingering)
+    viewed = start_container([o], timeout_s=120, mounts=nv.mounts())
+    assert viewed.ok, viewed.error
+    assert viewed.doc["devices"][0]["mismatches"] == 0
+    assert nv.hidden > 0
+    init = lambda r: r.doc["init_us"]["hsa_init"]
+    assert init(viewed) < init(plain), (init(viewed), init(plain))
+
+
 def test_smi_cross_check(inv):
     from rocm_k8s_device_plugin_amd.ops.native import core
     n = core()

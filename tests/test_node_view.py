@@ -80,3 +80,13 @@ def test_allocate_returns_node_view_mounts(tmp_path):
     mounts = list(impl.allocate(PluginContext("gpu"), req).container_responses[0].mounts)
     assert [(m.container_path, m.read_only) for m in mounts] == [(NODE_ALIAS, True), (NODE_CONTAINER_PATH, True)]
     assert os.path.isdir(mounts[1].host_path)
+
+
+def test_nodeview_alias_equal_to_host_path_needs_one_mount(tmp_path):
+    root = _sysfs(tmp_path)
+    src = str(root / "devices/system/node")
+    nv = NodeView(str(tmp_path / "views"), sysfs_root=str(root), alias=src)
+    (m,) = nv.mounts()
+    assert m[1] == NODE_CONTAINER_PATH
+    # symlinks resolve directly on the host
+    assert open(os.path.join(m[0], "node0/meminfo")).read().startswith("Node 0")
