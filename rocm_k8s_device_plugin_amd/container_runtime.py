@@ -81,7 +81,8 @@ def wait_kfd_released(entries: Iterable[str], timeout_s: float = 0.5, proc_dir: 
 
 
 def mount_redirects(mounts: Iterable) -> str:
-    """Allocate-response mounts -> MI355X_INITPROF_REDIRECT spec (container_path=host_path;...).
+    """Allocate-response mounts (pb.Mount or (container_path, host_path) tuples)
+    -> MI355X_INITPROF_REDIRECT spec (container_path=host_path;...).
 
     A real runtime bind-mounts these; without root the fake runtime runs the
     path-interposing probe build, which rewrites opens under container_path to

@@ -204,7 +204,7 @@ def test_container_with_node_view_mounts(tmp_path, ordinals):
     plain = start_container([o], timeout_s=120)
     assert plain.ok, plain.error
     wait_kfd_released(plain.kfd_lingering)
-    viewed = start_container([o], timeout_s=120, mounts=nv.mounts())
+    viewed = start_container([o], timeout_s=120, mounts=[(ctr, host) for host, ctr in nv.mounts()])
     assert viewed.ok, viewed.error
     assert viewed.doc["devices"][0]["mismatches"] == 0
     assert nv.hidden > 0
