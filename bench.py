@@ -204,7 +204,8 @@ def main():
     exec_ms, rt_ms, dev_ms, settle_ms = [], [], [], []
     from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
 
-    def one_step(record: bool, runtime: str = args.container_runtime, sink=None, settle: str = args.settle):
+    def one_step(record: bool, runtime: str = args.container_runtime, sink=None, settle: str = args.settle,
+                 init_sink=None):
         nonlocal step_payload
         if d.rank == 0:
             t0 = time.monotonic_ns()
@@ -249,6 +250,9 @@ def main():
             settle_ms.append(waited)
         if sink is not None:
             sink.append((t_ready - t0) / 1e6)
+        if init_sink is not None:
+            sp, tm, trt = slowest[4]
+            init_sink.append((trt - tm) / 1e6)
         if record:
             lat_ms.append((t_ready - t0) / 1e6)
             rpc_ms.append(tot)
@@ -269,7 +273,7 @@ def main():
     d.sync()
     elapsed = time.perf_counter() - t_start
     elapsed = d.max(elapsed)
-    hip_lat, b2b_lat, nv_lat = [], [], []
+    hip_lat, b2b_lat, nv_lat, nv_init = [], [], [], []
     if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
         # the plugin returns -node_view mounts from now on (alias = host path: the
         # fake runtime applies mounts by redirection and cannot add the alias mount)
@@ -277,8 +281,9 @@ def main():
             from rocm_k8s_device_plugin_amd.node_view import NodeView
             impl.node_view = NodeView(os.path.join(tmp, "node-view"), sysfs,
                                       alias=os.path.join(sysfs, "devices/system/node"))
+            impl.node_view.path()  # built at plugin start-up in a real deployment
         for _ in range(args.node_view_compare):
-            one_step(False, sink=nv_lat)
+            one_step(False, sink=nv_lat, init_sink=nv_init)
         if d.rank == 0:
             impl.node_view = None
     if not args.fixture and args.container_runtime == "hsa":
@@ -310,6 +315,7 @@ def main():
                  "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
                  "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
                  "latency_p50_ms_node_view_emulated": round(pct(nv_lat, .5), 3) if nv_lat else None,
+                 "node_view_emulated_runtime_init_p50_ms": round(pct(nv_init, .5), 3) if nv_init else None,
                  "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
                  "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
                                              "hip_runtime_init": round(pct(rt_ms, .5), 3),

@@ -44,6 +44,11 @@ class ContainerImpl(DeviceImpl):
                                if topology_view_dir else None)
         # opt-in: NUMA-node sysfs without the per-CPU cache walk ROCr does at start-up
         self.node_view = NodeView(node_view_dir, sysfs_root) if node_view_dir else None
+        if self.node_view is not None:  # build at start-up, not inside the first Allocate
+            try:
+                self.node_view.path()
+            except OSError as e:
+                _log.warning("node view unavailable: %s", e)
         if not os.path.exists(os.path.join(sysfs_root, C.KFD_CLASS_REL)):
             raise DeviceImplError("No amd gpu driver loaded")
         self.inv = inventory or discover(sysfs_root, device_count_limit)
