@@ -58,11 +58,13 @@ class FakeKubelet:
         self.server: Optional[grpc.aio.Server] = None
         self.resources: Dict[str, ResourceState] = {}
         self.registrations: List[object] = []
+        self.register_times: Dict[str, float] = {}   # resource -> time.monotonic() of its last Register
         self._registered = asyncio.Event()
 
     # -------------------------------------------------------------- server side
     async def Register(self, request, context):  # noqa: N802
         self.registrations.append(request)
+        self.register_times[request.resource_name] = time.monotonic()
         if request.version != pb.VERSION:
             await context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unsupported version {request.version}")
         old = self.resources.get(request.resource_name)

@@ -8,3 +8,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -2 gpurun_out/smoke.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
 cat gpurun_out/bench_default.json; cat /proc/loadavg
+timeout -k 10 200 python tools/plugin_startup.py --reps 5 --out gpurun_out/plugin_startup.json > gpurun_out/plugin_startup.log 2>&1 || { tail -20 gpurun_out/plugin_startup.log; exit 1; }
+cat gpurun_out/plugin_startup.log
