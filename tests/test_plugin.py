@@ -620,3 +620,19 @@ def test_smi_events_unavailable_is_not_fatal(tmp_path):
         await mon.close()
 
     run(go())
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only: exercises the failure path of the real probe")
+def test_real_probe_binary_without_gpu_reports_unhealthy():
+    """The real mi355x-liveness-probe (server and one-shot) on a machine without a
+    GPU: the server refuses to start, the prober falls back per device, and the
+    verdict carries the runtime error instead of hanging or crashing."""
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    prober = LivenessProber(exe=str(probe_executable("hsa")), timeout_s=20)
+
+    async def go():
+        res = await prober.probe({"a": 0})
+        assert not res["a"].ok and "runtime init failed" in res["a"].reason
+        assert prober.fallbacks == 1 and prober._server is None
+
+    run(go())
