@@ -8,11 +8,13 @@ GetPreferredAllocation, UpdateHealth}`` and
 from __future__ import annotations
 
 import abc
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
 from ..allocator import BestEffortPolicy, Policy
 from ..proto import deviceplugin as pb
+from ..utils import log
 
 
 class DeviceImplError(Exception):
@@ -91,6 +93,15 @@ class DeviceImpl(abc.ABC):
 
     async def close(self) -> None:
         """Release helper processes (e.g. the liveness probe server) at shutdown."""
+
+
+def driver_present(path: str) -> bool:
+    """Is the driver behind `path` loaded? (reference: checkDriver,
+    internal/pkg/amdgpu/utils.go:24-31 — stat plus a log line on absence)."""
+    if os.path.exists(path):
+        return True
+    log.get("plugin").info("driver path %s not present", path)
+    return False
 
 
 def device_proto(dev_id: str, health: str, numa: Optional[int] = None) -> pb.Device:

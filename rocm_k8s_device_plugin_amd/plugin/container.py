@@ -25,7 +25,7 @@ from ..topology import Gpu, Inventory, discover
 from ..node_view import NodeView
 from ..topology_view import KFD_TOPOLOGY_CONTAINER_PATH, TopologyViews
 from ..utils import log
-from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto
+from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto, driver_present
 
 _log = log.get("container")
 
@@ -49,7 +49,7 @@ class ContainerImpl(DeviceImpl):
                 self.node_view.path()
             except OSError as e:
                 _log.warning("node view unavailable: %s", e)
-        if not os.path.exists(os.path.join(sysfs_root, C.KFD_CLASS_REL)):
+        if not driver_present(os.path.join(sysfs_root, C.KFD_CLASS_REL)):
             raise DeviceImplError("No amd gpu driver loaded")
         self.inv = inventory or discover(sysfs_root, device_count_limit)
         for w in self.inv.warnings:

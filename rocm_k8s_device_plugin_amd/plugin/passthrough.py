@@ -20,7 +20,7 @@ from ..health import exporter
 from ..ops.native import core
 from ..proto import deviceplugin as pb
 from ..utils import log
-from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto
+from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto, driver_present
 
 _log = log.get("passthrough")
 
@@ -41,7 +41,7 @@ class _PassthroughBase(DeviceImpl):
         self.sysfs_root = sysfs_root
         self.exporter_socket = exporter_socket
         self._exporter_fn = exporter_fn or exporter.get_gpu_health
-        if not os.path.exists(os.path.join(sysfs_root, self.driver_rel)):
+        if not driver_present(os.path.join(sysfs_root, self.driver_rel)):
             raise DeviceImplError(self.driver_missing_msg)
         res = self._scan()
         if not res.ok:
@@ -122,7 +122,7 @@ class VfImpl(_PassthroughBase):
     async def refresh_health(self) -> bool:
         """gim driver gone -> all Unhealthy; else a group is Unhealthy iff any
         parent PF is Unhealthy per the exporter (amdgpu_sriov.go:217-308)."""
-        if not os.path.exists(os.path.join(self.sysfs_root, C.GIM_DRIVER_REL)):
+        if not driver_present(os.path.join(self.sysfs_root, C.GIM_DRIVER_REL)):
             return self._set_health({g: pb.UNHEALTHY for g in self._order})
         pf_health = None
         if self.exporter_socket:
@@ -152,5 +152,5 @@ class PfImpl(_PassthroughBase):
 
     async def refresh_health(self) -> bool:
         """vfio-pci driver present -> Healthy (amdgpu_pf.go:210-229)."""
-        ok = os.path.exists(os.path.join(self.sysfs_root, C.VFIO_DRIVER_REL))
+        ok = driver_present(os.path.join(self.sysfs_root, C.VFIO_DRIVER_REL))
         return self._set_health({g: pb.HEALTHY if ok else pb.UNHEALTHY for g in self._order})
