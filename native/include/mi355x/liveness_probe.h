@@ -97,6 +97,37 @@ typedef struct {
 int mi355x_hsa_peer_probe(int src, int dst, uint32_t nonce, uint64_t bytes, int reps, double timeout_s,
                           mi355x_peer_result* out);
 
+// ---- full-chip sweep (every CU of every XCD) --------------------------------
+// One workgroup per CU (each holds the CU's whole 160 KiB LDS), all resident
+// at once (bounded wait), each checks 4 MFMA tiles against the VALU, writes
+// and cross-reads the whole LDS, and reports its XCC / CU ids; the host
+// verifies records and wave 0's tiles bit-exactly and counts the distinct
+// CUs and XCDs that ran.
+typedef struct {
+  int ordinal;
+  int ok;                 // every record present and correct, every tile exact, all XCDs seen
+  int hsa_error;
+  uint32_t nonce;
+  int iters;
+  int grid;               // workgroups launched (= agent CU count)
+  int cu_count;           // HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT
+  int num_xcc;            // HSA_AMD_AGENT_INFO_NUM_XCC
+  int records_ok;         // workgroups whose record is present, echoed the nonce and found no fault
+  uint32_t mfma_bad;      // MFMA elements differing from the VALU recomputation (all waves)
+  uint32_t lds_bad;       // LDS words read back wrong
+  uint32_t tile_bad;      // wave-0 tile elements differing from the host reference
+  int cus_covered;        // distinct (XCC, SE, SH, CU) that ran a workgroup
+  int xccs_covered;
+  int all_resident;       // every workgroup saw the whole grid resident before working
+  int wgs_per_xcc[16];
+  double kernel_us;       // dispatch start -> end (HSA profiling)
+  double arrival_spread_us;  // first to last workgroup arrival (s_memrealtime)
+  double total_us;
+  char error[160];
+} mi355x_sweep_result;
+
+int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, double timeout_s, mi355x_sweep_result* out);
+
 #ifdef __cplusplus
 }
 #endif

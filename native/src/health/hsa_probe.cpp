@@ -21,6 +21,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -637,6 +638,200 @@ done:
     if (a_buf) H().hsa_amd_memory_pool_free(a_buf);
   }
   if (out->copy_us_best >= 1e29) out->copy_us_best = 0;
+  out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+  return out->ok ? 0 : 1;
+}
+
+extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, double timeout_s,
+                                     mi355x_sweep_result* out) {
+  using clk = std::chrono::steady_clock;
+  std::memset(out, 0, sizeof(*out));
+  out->ordinal = ordinal;
+  out->nonce = nonce;
+  out->iters = iters < 1 ? 1 : (iters > 64 ? 64 : iters);
+  const auto t0 = clk::now();
+  const int n = mi355x_hsa_probe_init();
+  if (n < 0) {
+    out->hsa_error = n;
+    std::snprintf(out->error, sizeof(out->error), "hsa_init: %.140s", H().loaded ? "runtime init failed" : H().error);
+    return 1;
+  }
+  if (ordinal < 0 || ordinal >= n) {
+    std::snprintf(out->error, sizeof(out->error), "no such GPU agent (count=%d)", n);
+    return 1;
+  }
+  const Agent& ag = g_rt.gpus[ordinal];
+  uint32_t cus = 0, xcc = 0;
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cus);
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_NUM_XCC), &xcc);
+  out->cu_count = static_cast<int>(cus);
+  out->num_xcc = static_cast<int>(xcc);
+  if (cus == 0 || cus > 1024 || !g_rt.has_fine || !g_rt.has_kernarg || !ag.has_coarse) {
+    std::snprintf(out->error, sizeof(out->error), "unexpected agent (cus=%u) or missing memory pool", cus);
+    return 1;
+  }
+  const uint32_t grid = cus;
+  out->grid = static_cast<int>(grid);
+
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t sig{};
+  uint32_t* records = nullptr;
+  float* tiles = nullptr;
+  uint32_t* arrive = nullptr;
+  mi355x_sweep_args* kargs = nullptr;
+  bool in_flight = false;
+  hsa_status_t s = HSA_STATUS_SUCCESS;
+  uint64_t kobj = 0;
+  uint32_t kseg = 0, gseg = 0, pseg = 0;
+  hsa_executable_symbol_t sym{};
+  const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
+  const size_t rec_bytes = static_cast<size_t>(grid) * MI355X_SWEEP_REC_WORDS * sizeof(uint32_t);
+  const size_t tile_bytes = static_cast<size_t>(grid) * MI355X_PROBE_OUT * sizeof(float);
+  auto fail = [&](hsa_status_t st, const char* what) {
+    out->hsa_error = static_cast<int>(st);
+    const char* msg = nullptr;
+    H().hsa_status_string(st, &msg);
+    std::snprintf(out->error, sizeof(out->error), "%s: %s", what, msg ? msg : "hsa error");
+  };
+#define SWEEP_CHECK(expr, what) \
+  if ((s = (expr)) != HSA_STATUS_SUCCESS) { fail(s, what); goto done; }
+
+  SWEEP_CHECK(H().hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader), "code object");
+  SWEEP_CHECK(H().hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe),
+              "executable create");
+  SWEEP_CHECK(H().hsa_executable_load_agent_code_object(exe, ag.agent, reader, nullptr, nullptr), "load code object");
+  SWEEP_CHECK(H().hsa_executable_freeze(exe, nullptr), "freeze");
+  SWEEP_CHECK(H().hsa_executable_get_symbol_by_name(exe, "mi355x_chip_sweep.kd", &ag.agent, &sym), "kernel symbol");
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &kobj);
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kseg);
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &gseg);
+  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &pseg);
+  if (kseg < sizeof(mi355x_sweep_args) || kseg > kKernargBytes) {
+    std::snprintf(out->error, sizeof(out->error), "sweep kernarg segment %u: code object / host ABI mismatch", kseg);
+    goto done;
+  }
+  SWEEP_CHECK(H().hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX,
+                                   &queue), "queue create");
+  H().hsa_amd_profiling_set_profiler_enabled(queue, 1);
+  SWEEP_CHECK(H().hsa_signal_create(1, 0, nullptr, &sig), "signal create");
+  SWEEP_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.fine, rec_bytes, 0, reinterpret_cast<void**>(&records)),
+              "alloc records");
+  SWEEP_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.fine, tile_bytes, 0, reinterpret_cast<void**>(&tiles)),
+              "alloc tiles");
+  SWEEP_CHECK(H().hsa_amd_memory_pool_allocate(ag.coarse, 4096, 0, reinterpret_cast<void**>(&arrive)), "alloc arrive");
+  SWEEP_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.kernarg, kKernargBytes, 0, reinterpret_cast<void**>(&kargs)),
+              "alloc kernarg");
+  SWEEP_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, records), "allow records");
+  SWEEP_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, tiles), "allow tiles");
+  SWEEP_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, kargs), "allow kernarg");
+  SWEEP_CHECK(H().hsa_amd_memory_fill(arrive, 0u, 4096 / 4), "zero arrive");
+  std::memset(records, 0, rec_bytes);
+  std::memset(tiles, 0xFF, tile_bytes);
+  std::memset(kargs, 0, kKernargBytes);
+  kargs->records = records;
+  kargs->tiles = tiles;
+  kargs->arrive = arrive;
+  kargs->nonce = nonce;
+  kargs->iters = out->iters;
+  kargs->grid = grid;
+  kargs->wait_ticks = 2000000;  // 20 ms at the 100 MHz s_memrealtime clock
+  {
+    const uint64_t idx = H().hsa_queue_add_write_index_screlease(queue, 1);
+    auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address) + (idx & (queue->size - 1));
+    std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
+    pkt->workgroup_size_x = MI355X_SWEEP_THREADS;
+    pkt->workgroup_size_y = 1;
+    pkt->workgroup_size_z = 1;
+    pkt->grid_size_x = grid * MI355X_SWEEP_THREADS;
+    pkt->grid_size_y = 1;
+    pkt->grid_size_z = 1;
+    pkt->private_segment_size = pseg;
+    pkt->group_segment_size = gseg;
+    pkt->kernel_object = kobj;
+    pkt->kernarg_address = kargs;
+    pkt->completion_signal = sig;
+    const uint16_t header = static_cast<uint16_t>(
+        (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
+                     __ATOMIC_RELEASE);
+    H().hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+  }
+  if (!wait_signal(sig, timeout_s)) {
+    in_flight = true;
+    std::snprintf(out->error, sizeof(out->error), "chip sweep did not complete within %.1fs", timeout_s);
+    out->hsa_error = -1;
+    goto done;
+  }
+  {
+    hsa_amd_profiling_dispatch_time_t dt{};
+    if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
+      out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
+  }
+  {
+    std::vector<uint32_t> keys;
+    keys.reserve(grid);
+    uint64_t tmin = UINT64_MAX, tmax = 0;
+    uint32_t xmask = 0;
+    bool all_res = true;
+    std::vector<float> want(MI355X_PROBE_OUT);
+    for (uint32_t w = 0; w < grid; ++w) {
+      const uint32_t* r = records + static_cast<size_t>(w) * MI355X_SWEEP_REC_WORDS;
+      const bool present = r[MI355X_REC_MAGIC] == MI355X_SWEEP_MAGIC && r[MI355X_REC_WG] == w &&
+                           r[MI355X_REC_NONCE] == (nonce ^ w);
+      if (!present) continue;
+      out->mfma_bad += r[MI355X_REC_MFMA_BAD];
+      out->lds_bad += r[MI355X_REC_LDS_BAD];
+      const uint32_t x = r[MI355X_REC_XCC] & 0xF;
+      xmask |= 1u << x;
+      ++out->wgs_per_xcc[x];
+      keys.push_back((x << 16) | ((r[MI355X_REC_HWID] >> 8) & 0xFF));
+      all_res = all_res && r[MI355X_REC_ARRIVED] >= grid;
+      const uint64_t t = (static_cast<uint64_t>(r[MI355X_REC_T0_HI]) << 32) | r[MI355X_REC_T0_LO];
+      tmin = t < tmin ? t : tmin;
+      tmax = t > tmax ? t : tmax;
+      // wave 0's tile against the host reference
+      const uint32_t nw = sweep_nonce(nonce, w, 0);
+      uint32_t tb = 0;
+      const float* tile = tiles + static_cast<size_t>(w) * MI355X_PROBE_OUT;
+      for (int i = 0; i < MI355X_PROBE_M; ++i)
+        for (int j = 0; j < MI355X_PROBE_N; ++j) {
+          float dot = 0.f;
+          for (int k = 0; k < MI355X_PROBE_K; ++k) dot += probe_a(i, k, nw) * probe_b(k, j, nw);
+          const float e = probe_c(i, j, nw) + static_cast<float>(out->iters) * dot;
+          tb += tile[i * MI355X_PROBE_N + j] != e;
+        }
+      out->tile_bad += tb;
+      if (r[MI355X_REC_MFMA_BAD] == 0 && r[MI355X_REC_LDS_BAD] == 0 && tb == 0) ++out->records_ok;
+    }
+    std::sort(keys.begin(), keys.end());
+    out->cus_covered = static_cast<int>(std::unique(keys.begin(), keys.end()) - keys.begin());
+    out->xccs_covered = __builtin_popcount(xmask);
+    out->all_resident = all_res && out->records_ok == static_cast<int>(grid);
+    if (tmax >= tmin && tmin != UINT64_MAX) out->arrival_spread_us = static_cast<double>(tmax - tmin) / 100.0;
+    out->ok = out->records_ok == static_cast<int>(grid) &&
+              (out->num_xcc <= 0 || out->xccs_covered == out->num_xcc);
+    if (!out->ok)
+      std::snprintf(out->error, sizeof(out->error),
+                    "%d/%d workgroups correct (mfma_bad=%u lds_bad=%u tile_bad=%u), %d/%d XCDs ran", out->records_ok,
+                    grid, out->mfma_bad, out->lds_bad, out->tile_bad, out->xccs_covered, out->num_xcc);
+  }
+#undef SWEEP_CHECK
+done:
+  if (!in_flight) {
+    if (kargs) H().hsa_amd_memory_pool_free(kargs);
+    if (arrive) H().hsa_amd_memory_pool_free(arrive);
+    if (tiles) H().hsa_amd_memory_pool_free(tiles);
+    if (records) H().hsa_amd_memory_pool_free(records);
+    if (sig.handle) H().hsa_signal_destroy(sig);
+    if (queue) H().hsa_queue_destroy(queue);
+    if (exe.handle) H().hsa_executable_destroy(exe);
+    if (reader.handle) H().hsa_code_object_reader_destroy(reader);
+  }
   out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
   return out->ok ? 0 : 1;
 }

@@ -41,3 +41,43 @@ struct mi355x_liveness_args {
 MI355X_HD float probe_a(int i, int k, uint32_t nonce) { return (float)((int)((i * 3u + k * 5u + nonce) % 7u) - 3); }
 MI355X_HD float probe_b(int k, int j, uint32_t nonce) { return (float)((int)((j * 11u + k * 2u + nonce) % 5u) - 2); }
 MI355X_HD float probe_c(int i, int j, uint32_t nonce) { return (float)((int)((i + 2u * j + nonce) % 4u)); }
+
+// ---- full-chip sweep (mi355x_chip_sweep) --------------------------------------
+// One 256-lane workgroup per CU: each holds all 160 KiB of its CU's LDS, so no
+// two workgroups can share a CU, and they wait (bounded) until the whole grid
+// is resident before working — every CU of every XCD runs exactly one. Each of
+// the 4 waves runs the MFMA tile (operands vary per workgroup and wave) and
+// checks it against a VALU recomputation; the whole LDS is written and read
+// back across waves; wave 0's tile also goes to the host for a bit-exact check.
+#define MI355X_SWEEP_THREADS 256
+#define MI355X_SWEEP_LDS_WORDS (40960 - 16)  // + 16 counter words = 160 KiB
+#define MI355X_SWEEP_REC_WORDS 16
+#define MI355X_SWEEP_MAGIC 0x43484950u /* "CHIP" */
+// record words (one record per workgroup)
+#define MI355X_REC_MAGIC 0
+#define MI355X_REC_NONCE 1
+#define MI355X_REC_XCC 2
+#define MI355X_REC_HWID 3        // wave 0; waves 1-3 in 12..14
+#define MI355X_REC_MFMA_BAD 4
+#define MI355X_REC_LDS_BAD 5
+#define MI355X_REC_ARRIVED 6     // workgroups resident when this one started work
+#define MI355X_REC_T0_LO 7       // s_memrealtime (100 MHz) at arrival
+#define MI355X_REC_T0_HI 8
+#define MI355X_REC_T1_LO 9       // at completion
+#define MI355X_REC_T1_HI 10
+#define MI355X_REC_WG 11
+
+struct mi355x_sweep_args {
+  uint32_t* records;   // host-visible, grid * MI355X_SWEEP_REC_WORDS
+  float* tiles;        // host-visible, grid * MI355X_PROBE_OUT (wave 0's tile per workgroup)
+  uint32_t* arrive;    // device memory, 1 word, zero before launch
+  uint32_t nonce;
+  int32_t iters;
+  uint32_t grid;       // workgroups launched (= CUs of the agent)
+  uint32_t wait_ticks; // max residency wait, s_memrealtime ticks
+};
+
+MI355X_HD uint32_t sweep_nonce(uint32_t nonce, uint32_t wg, uint32_t wave) { return nonce + wg * 4u + wave; }
+MI355X_HD uint32_t sweep_lds_pattern(uint32_t i, uint32_t nonce, uint32_t wg) {
+  return (i * 2654435761u) ^ (nonce + wg * 0x9E3779B1u);
+}

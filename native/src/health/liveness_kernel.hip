@@ -62,3 +62,87 @@ extern "C" __global__ __launch_bounds__(64) void mi355x_mfma_liveness(float* __r
     meta[MI355X_META_HWID] = __builtin_amdgcn_s_getreg(MI355X_HWREG_HW_ID);
   }
 }
+
+// Full-chip sweep: see liveness_kernel.h. Every path out of the residency wait
+// is bounded (wait_ticks), so the grid drains even when some CUs are held by
+// other work or disabled; coverage is then reported, not assumed.
+extern "C" __global__ __launch_bounds__(MI355X_SWEEP_THREADS) void mi355x_chip_sweep(mi355x_sweep_args args) {
+  __shared__ uint32_t lds[MI355X_SWEEP_LDS_WORDS];
+  __shared__ uint32_t ctr[16];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = tid >> 6;
+  const int lane = tid & 63;
+  const uint32_t wg = blockIdx.x;
+  if (tid < 16) ctr[tid] = 0;
+  if (tid == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_fetch_add(args.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t seen;
+    while ((seen = __hip_atomic_load(args.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < args.grid) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > args.wait_ticks) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    ctr[8] = seen;
+    ctr[9] = static_cast<uint32_t>(t0);
+    ctr[10] = static_cast<uint32_t>(t0 >> 32);
+  }
+  __syncthreads();
+
+  // MFMA tile per wave, checked lane by lane against the VALU
+  const uint32_t n = sweep_nonce(args.nonce, wg, wave);
+  const int row = lane & 31;
+  const int kk = lane >> 5;
+  const float a = probe_a(row, kk, n);
+  const float b = probe_b(kk, row, n);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = probe_c((r & 3) + 8 * (r >> 2) + 4 * kk, row, n);
+  for (int it = 0; it < args.iters; ++it) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+  uint32_t bad = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = (r & 3) + 8 * (r >> 2) + 4 * kk;
+    float dot = 0.f;
+    for (int k = 0; k < MI355X_PROBE_K; ++k) dot += probe_a(i, k, n) * probe_b(k, row, n);
+    const float want = probe_c(i, row, n) + static_cast<float>(args.iters) * dot;
+    bad += acc[r] != want;
+  }
+  if (bad) atomicAdd(&ctr[0], bad);
+  if (wave == 0) {
+    float* tile = args.tiles + static_cast<size_t>(wg) * MI355X_PROBE_OUT;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[((r & 3) + 8 * (r >> 2) + 4 * kk) * MI355X_PROBE_N + row] = acc[r];
+  }
+
+  // whole-LDS pattern, read back from another wave's writes
+  for (uint32_t i = tid; i < MI355X_SWEEP_LDS_WORDS; i += MI355X_SWEEP_THREADS)
+    lds[i] = sweep_lds_pattern(i, args.nonce, wg);
+  __syncthreads();
+  uint32_t lbad = 0;
+  const uint32_t other = (tid + 64) & (MI355X_SWEEP_THREADS - 1);
+  for (uint32_t i = other; i < MI355X_SWEEP_LDS_WORDS; i += MI355X_SWEEP_THREADS)
+    lbad += lds[i] != sweep_lds_pattern(i, args.nonce, wg);
+  if (lbad) atomicAdd(&ctr[1], lbad);
+  if (lane == 0) ctr[12 + wave] = __builtin_amdgcn_s_getreg(MI355X_HWREG_HW_ID);
+  __syncthreads();
+
+  if (tid == 0) {
+    uint32_t* rec = args.records + static_cast<size_t>(wg) * MI355X_SWEEP_REC_WORDS;
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    rec[MI355X_REC_NONCE] = args.nonce ^ wg;
+    rec[MI355X_REC_XCC] = __builtin_amdgcn_s_getreg(MI355X_HWREG_XCC_ID) & 0xF;
+    rec[MI355X_REC_HWID] = ctr[12];
+    rec[MI355X_REC_MFMA_BAD] = ctr[0];
+    rec[MI355X_REC_LDS_BAD] = ctr[1];
+    rec[MI355X_REC_ARRIVED] = ctr[8];
+    rec[MI355X_REC_T0_LO] = ctr[9];
+    rec[MI355X_REC_T0_HI] = ctr[10];
+    rec[MI355X_REC_T1_LO] = static_cast<uint32_t>(t1);
+    rec[MI355X_REC_T1_HI] = static_cast<uint32_t>(t1 >> 32);
+    rec[MI355X_REC_WG] = wg;
+    rec[12] = ctr[13];
+    rec[13] = ctr[14];
+    rec[14] = ctr[15];
+    rec[MI355X_REC_MAGIC] = MI355X_SWEEP_MAGIC;
+  }
+}

@@ -3,6 +3,7 @@
 //
 //   mi355x-liveness-probe [--devices all|0,2,..] [--nonce N] [--iters N] [--identify] [--timeout S]
 //   mi355x-liveness-probe --serve      (long-lived; requests on stdin, see serve())
+//   mi355x-liveness-probe --sweep [--devices ..]   (every CU of every XCD, see mi355x_chip_sweep)
 //   mi355x-liveness-probe --peer [--devices ..] [--peer-bytes B] [--peer-reps R]
 //                                      (DMA copy over every GPU pair's link, verified)
 //
@@ -103,6 +104,9 @@ int identify_dev(int o, mi355x_probe_result* r) { return mi355x_hsa_probe_identi
 int peer(int a, int b, uint32_t nonce, uint64_t bytes, int reps, double timeout_s, mi355x_peer_result* r) {
   return mi355x_hsa_peer_probe(a, b, nonce, bytes, reps, timeout_s, r);
 }
+int chip_sweep(int o, uint32_t nonce, int iters, double timeout_s, mi355x_sweep_result* r) {
+  return mi355x_hsa_chip_sweep(o, nonce, iters, timeout_s, r);
+}
 void init_phases(double out[5]) { mi355x_hsa_init_phases(out); }
 void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
 void teardown() { mi355x_hsa_probe_release(); }
@@ -117,6 +121,14 @@ int probe(int o, uint32_t nonce, int iters, double, mi355x_probe_result* r) {
   return mi355x_probe_device(o, nonce, iters, r);
 }
 int identify_dev(int o, mi355x_probe_result* r) { return mi355x_probe_identify(o, r); }
+int chip_sweep(int o, uint32_t nonce, int iters, double, mi355x_sweep_result* r) {
+  std::memset(r, 0, sizeof(*r));
+  r->ordinal = o;
+  r->nonce = nonce;
+  r->iters = iters;
+  std::snprintf(r->error, sizeof(r->error), "--sweep needs the HSA-direct build (mi355x-liveness-probe)");
+  return 1;
+}
 int peer(int a, int b, uint32_t, uint64_t bytes, int reps, double, mi355x_peer_result* r) {
   std::memset(r, 0, sizeof(*r));
   r->src = a;
@@ -197,6 +209,55 @@ int run_peer(const std::vector<int>& ords, uint32_t nonce, uint64_t bytes, int r
   return all_ok ? 0 : 1;
 }
 
+std::string sweep_json(const mi355x_sweep_result& r) {
+  std::string per = "[";
+  for (int i = 0; i < 16 && i < (r.num_xcc > 0 ? r.num_xcc : 8); ++i) {
+    if (i) per += ",";
+    per += std::to_string(r.wgs_per_xcc[i]);
+  }
+  per += "]";
+  char buf[1024];
+  std::snprintf(buf, sizeof(buf),
+                "{\"ordinal\":%d,\"ok\":%s,\"hsa_error\":%d,\"nonce\":%u,\"iters\":%d,\"grid\":%d,"
+                "\"cu_count\":%d,\"num_xcc\":%d,\"records_ok\":%d,\"mfma_bad\":%u,\"lds_bad\":%u,"
+                "\"tile_bad\":%u,\"cus_covered\":%d,\"xccs_covered\":%d,\"all_resident\":%s,"
+                "\"wgs_per_xcc\":%s,\"kernel_us\":%.2f,\"arrival_spread_us\":%.2f,\"total_us\":%.1f,"
+                "\"error\":\"%s\"}",
+                r.ordinal, r.ok ? "true" : "false", r.hsa_error, r.nonce, r.iters, r.grid, r.cu_count, r.num_xcc,
+                r.records_ok, r.mfma_bad, r.lds_bad, r.tile_bad, r.cus_covered, r.xccs_covered,
+                r.all_resident ? "true" : "false", per.c_str(), r.kernel_us, r.arrival_spread_us, r.total_us,
+                json_escape(r.error).c_str());
+  return buf;
+}
+
+// --sweep: the full-chip sweep on each selected GPU (parallel host threads).
+bool run_sweeps(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, int iters, double timeout_s,
+                int n, std::string& json) {
+  std::vector<mi355x_sweep_result> res(ords.size());
+  std::vector<int> rcs(ords.size(), 1);
+  auto one = [&](size_t i) {
+    if (ords[i] < 0 || ords[i] >= n) {
+      std::memset(&res[i], 0, sizeof(res[i]));
+      res[i].ordinal = ords[i];
+      std::snprintf(res[i].error, sizeof(res[i].error), "no such GPU (count=%d)", n);
+      return;
+    }
+    rcs[i] = chip_sweep(ords[i], nonces[i], iters, timeout_s, &res[i]);
+  };
+  std::vector<std::thread> ths;
+  for (size_t i = 0; i < ords.size(); ++i) ths.emplace_back(one, i);
+  for (auto& t : ths) t.join();
+  bool ok = !ords.empty();
+  json = "[";
+  for (size_t i = 0; i < res.size(); ++i) {
+    ok = ok && rcs[i] == 0;
+    if (i) json += ",";
+    json += sweep_json(res[i]);
+  }
+  json += "]";
+  return ok;
+}
+
 std::string devices_json(const std::vector<mi355x_probe_result>& results) {
   std::string o = "[";
   for (size_t i = 0; i < results.size(); ++i) {
@@ -233,7 +294,9 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
     int iters = 0;
     double timeout_s = 0;
     int consumed = 0;
-    if (std::sscanf(line.c_str(), "probe %d %lf %n", &iters, &timeout_s, &consumed) < 2 || consumed == 0) {
+    const bool sweep_req = line.compare(0, 6, "sweep ") == 0;
+    const char* fmt = sweep_req ? "sweep %d %lf %n" : "probe %d %lf %n";
+    if (std::sscanf(line.c_str(), fmt, &iters, &timeout_s, &consumed) < 2 || consumed == 0) {
       std::printf("{\"ok\":false,\"error\":\"bad request\",\"devices\":[]}\n");
       std::fflush(stdout);
       continue;
@@ -255,9 +318,17 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
     }
     std::vector<mi355x_probe_result> results;
     defer_teardown();
-    const bool ok = run_batch(ords, nonces, iters, timeout_s, false, n, results);
-    std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"t_ready_ns\":%llu,\"devices\":%s}\n", ok ? "true" : "false",
-                n, static_cast<unsigned long long>(mono_ns()), devices_json(results).c_str());
+    std::string body;
+    bool ok;
+    if (sweep_req) {
+      ok = run_sweeps(ords, nonces, iters, timeout_s, n, body);
+    } else {
+      ok = run_batch(ords, nonces, iters, timeout_s, false, n, results);
+      body = devices_json(results);
+    }
+    std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"sweep\":%s,\"t_ready_ns\":%llu,\"devices\":%s}\n",
+                ok ? "true" : "false", n, sweep_req ? "true" : "false", static_cast<unsigned long long>(mono_ns()),
+                body.c_str());
     std::fflush(stdout);
     teardown();  // queues/executables go, the runtime (and the kfd process) stays
   }
@@ -278,6 +349,7 @@ int main(int argc, char** argv) {
   std::string exit_mode = "shutdown";
   bool serve_mode = false;
   bool peer_mode = false;
+  bool sweep_mode = false;
   uint64_t peer_bytes = 64ull << 20;
   int peer_reps = 3;
   for (int i = 1; i < argc; ++i) {
@@ -311,13 +383,15 @@ int main(int argc, char** argv) {
       serve_mode = true;
     } else if (a == "--peer") {
       peer_mode = true;
+    } else if (a == "--sweep") {
+      sweep_mode = true;
     } else if (a == "--peer-bytes") {
       peer_bytes = std::strtoull(next("--peer-bytes"), nullptr, 0);
     } else if (a == "--peer-reps") {
       peer_reps = std::atoi(next("--peer-reps"));
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
-                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve] [--peer [--peer-bytes B] [--peer-reps R]]\n",
+                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep]\n",
                   argv[0]);
       return 0;
     } else {
@@ -361,6 +435,16 @@ int main(int argc, char** argv) {
   if (peer_mode) return run_peer(ords, nonce, peer_bytes, peer_reps, timeout_s, n);
   std::vector<uint32_t> nonces;
   for (size_t i = 0; i < ords.size(); ++i) nonces.push_back(nonce + static_cast<uint32_t>(i));
+  if (sweep_mode) {
+    std::string body;
+    const bool ok = run_sweeps(ords, nonces, iters, timeout_s, n, body);
+    std::printf("{\"ok\":%s,\"sweep\":true,\"hip_device_count\":%d,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
+                "\"t_ready_ns\":%llu,\"devices\":%s}\n",
+                ok ? "true" : "false", n, static_cast<unsigned long long>(t_start),
+                static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(mono_ns()), body.c_str());
+    std::fflush(stdout);
+    return ok ? 0 : 1;
+  }
   std::vector<mi355x_probe_result> results;
   // Queues/executables are torn down after the verdict is printed: the caller
   // (container runtime, health loop) only waits for the JSON line.

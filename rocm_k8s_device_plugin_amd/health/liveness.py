@@ -154,10 +154,10 @@ class LivenessProber:
             return ProbeOutcome(False, f"stale probe result (nonce {d.get('nonce')} != {nonce})", dt, d)
         return ProbeOutcome(True, "", dt, d)
 
-    async def probe_ordinal(self, ordinal: int, nonce: Optional[int] = None) -> ProbeOutcome:
+    async def probe_ordinal(self, ordinal: int, nonce: Optional[int] = None, kind: str = "probe") -> ProbeOutcome:
         nonce = self._nonce(ordinal) if nonce is None else nonce
         argv = [*self.argv_prefix, self._exe(), "--devices", "0", "--iters", str(self.iters), "--nonce", str(nonce),
-                "--timeout", f"{max(0.5, self.timeout_s - 0.5):.2f}"]
+                "--timeout", f"{max(0.5, self.timeout_s - 0.5):.2f}"] + (["--sweep"] if kind == "sweep" else [])
         t0 = time.perf_counter()
         try:
             proc = await asyncio.create_subprocess_exec(
@@ -188,7 +188,7 @@ class LivenessProber:
         return self._judge(bool(doc.get("ok")), d, nonce, dt, proc.returncode)
 
     # ------------------------------------------------------------ persistent
-    async def _probe_server(self, uniq) -> Dict[int, ProbeOutcome]:
+    async def _probe_server(self, uniq, kind: str = "probe") -> Dict[int, ProbeOutcome]:
         t0 = time.perf_counter()
         if self._server is None or not self._server.alive:
             argv = [*self.argv_prefix, self._exe(), "--serve"]
@@ -196,7 +196,7 @@ class LivenessProber:
             self.server_starts += 1
         nonces = {o: self._nonce(o) for o in uniq}
         inner = max(0.5, self.timeout_s - 0.5)
-        line = f"probe {self.iters} {inner:.2f} " + " ".join(f"{o}:{nonces[o]}" for o in uniq)
+        line = f"{kind} {self.iters} {inner:.2f} " + " ".join(f"{o}:{nonces[o]}" for o in uniq)
         doc = await self._server.request(line, self.timeout_s)
         dt = (time.perf_counter() - t0) * 1e3
         by_ord = {d.get("ordinal"): d for d in doc.get("devices") or []}
@@ -212,15 +212,22 @@ class LivenessProber:
             await self._server.kill()
             self._server = None
 
-    async def probe(self, ordinals: Mapping[str, int]) -> Dict[str, ProbeOutcome]:
+    async def sweep(self, ordinals: Mapping[str, int]) -> Dict[str, ProbeOutcome]:
+        """The full-chip sweep (every CU of every XCD) instead of the one-wave probe.
+
+        It holds each CU's whole LDS for ~50 us and waits for the entire grid to
+        be resident, so callers run it only on GPUs without foreign work."""
+        return await self.probe(ordinals, kind="sweep")
+
+    async def probe(self, ordinals: Mapping[str, int], kind: str = "probe") -> Dict[str, ProbeOutcome]:
         """device ID -> outcome; devices sharing an ordinal are probed once."""
         uniq = sorted(set(ordinals.values()))
         use_server = self.mode == "persistent" and uniq and self._server_backoff == 0
         self._server_backoff = max(0, self._server_backoff - 1)
         if use_server:
             try:
-                with TRACER.span("liveness.request", "health", ordinals=len(uniq)):
-                    results = await self._probe_server(uniq)
+                with TRACER.span("liveness.request", "health", ordinals=len(uniq), kind=kind):
+                    results = await self._probe_server(uniq, kind)
                 self.sweeps += 1
                 return {dev: results[o] for dev, o in ordinals.items()}
             except (asyncio.TimeoutError, ProbeServerError, OSError) as e:
@@ -234,8 +241,8 @@ class LivenessProber:
 
         async def one(o: int):
             async with sem:
-                with TRACER.span("liveness.probe", "health", ordinal=o):
-                    return o, await self.probe_ordinal(o)
+                with TRACER.span("liveness.probe", "health", ordinal=o, kind=kind):
+                    return o, await self.probe_ordinal(o, kind=kind)
 
         results = dict(await asyncio.gather(*(one(o) for o in uniq)))
         self.sweeps += 1

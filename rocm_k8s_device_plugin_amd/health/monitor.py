@@ -32,7 +32,7 @@ from typing import Callable, Dict, Mapping, Optional, Tuple
 
 from ..ops.native import core
 from ..proto import deviceplugin as dp
-from ..topology import Inventory, hip_ordinals
+from ..topology import Inventory, hip_ordinals, kfd_busy_gpu_ids
 from ..utils import log
 from ..utils.trace import TRACER
 from . import exporter
@@ -56,6 +56,9 @@ class HealthConfig:
     liveness_iters: int = 4
     liveness_parallel: int = 8
     liveness_mode: str = "persistent"  # persistent probe server | spawn per device per sweep
+    # every N-th sweep (and the first), GPUs with no user queues from any process
+    # get the full-chip sweep (every CU of every XCD) instead of the one-wave probe
+    chip_sweep_every: int = 0
     fail_threshold: int = 2
     recover_threshold: int = 1
     smi_ecc: bool = False
@@ -88,6 +91,7 @@ class HealthMonitor:
         self._events_started = False
         self._resetting: Dict[str, str] = {}   # bdf -> message of the pending pre-reset
         self.event_counts: Dict[Tuple[str, str], int] = {}
+        self.chip_sweeps = 0
         self._exporter_fn = exporter_fn or exporter.get_gpu_health
         self._track: Dict[str, _Track] = {d.id: _Track() for d in inventory.devices}
         self._ecc: Dict[str, int] = {}
@@ -186,6 +190,33 @@ class HealthMonitor:
             else:
                 _log.info("GPU %s: %s %s", bdf, name, ev.get("message", ""))
 
+    def _idle_devices(self, dev_ids) -> set:
+        """Devices whose kfd gpu_id has no user queue in any process right now."""
+        busy = kfd_busy_gpu_ids(self.inv.sysfs_root)
+        idle = set()
+        for dev_id in dev_ids:
+            d = self.inv.by_id.get(dev_id)
+            node = self.inv.topology.node(d.node_id) if d is not None and d.node_id >= 0 else None
+            gid = int(getattr(node, "gpu_id", 0) or 0) if node is not None else 0
+            if gid and gid not in busy:
+                idle.add(dev_id)
+        return idle
+
+    async def _liveness(self, ords: Dict[str, int]):
+        every = self.cfg.chip_sweep_every
+        if every <= 0 or self.sweeps % every != 0:
+            return await self.prober.probe(ords)
+        idle = self._idle_devices(ords)
+        out = {}
+        if idle:
+            swept = await self.prober.sweep({k: v for k, v in ords.items() if k in idle})
+            out.update(swept)
+            self.chip_sweeps += 1
+        rest = {k: v for k, v in ords.items() if k not in idle}
+        if rest:
+            out.update(await self.prober.probe(rest))
+        return out
+
     # ------------------------------------------------------------------ sweep
     async def close(self) -> None:
         if self.prober is not None:
@@ -215,7 +246,7 @@ class HealthMonitor:
 
         if self.cfg.liveness and self.prober is not None:
             ords = {k: v for k, v in self.ordinals().items() if k in reasons}
-            outcomes = await self.prober.probe(ords)
+            outcomes = await self._liveness(ords)
             for dev_id, o in outcomes.items():
                 tr = self._track[dev_id]
                 if o.ok:

@@ -46,6 +46,7 @@ def serve():
         parts = line.split()
         if not parts or parts[0] == "quit":
             break
+        kind = parts[0]
         ctl = _control()
         devs = []
         for tok in parts[3:]:
@@ -57,8 +58,8 @@ def serve():
                 print("segfault-ish noise", flush=True)
                 return 139
             devs.append(_device(int(o), mode, int(n, 0)))
-        print(json.dumps({"ok": all(d["ok"] for d in devs), "hip_device_count": 8, "t_ready_ns": time.monotonic_ns(),
-                          "devices": devs}), flush=True)
+        print(json.dumps({"ok": all(d["ok"] for d in devs), "hip_device_count": 8, "sweep": kind == "sweep",
+                          "t_ready_ns": time.monotonic_ns(), "devices": devs}), flush=True)
     return 0
 
 

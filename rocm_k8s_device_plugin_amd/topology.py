@@ -182,3 +182,28 @@ def hip_ordinals(inv: Inventory, dev_root: str = "/dev", check_access: bool = Tr
         gpu_nodes.append(nid)
     pos = {nid: i for i, nid in enumerate(gpu_nodes)}
     return {d.id: pos[d.node_id] for d in inv.devices if d.node_id in pos}
+
+
+def kfd_busy_gpu_ids(sysfs_root: str = "/sys") -> set:
+    """kfd gpu_ids that currently have user queues, from any process on the host
+    (``/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/gpuid``). A GPU without queues
+    runs no work; the liveness loop runs its full-chip sweep only on those."""
+    busy = set()
+    root = os.path.join(sysfs_root, "class/kfd/kfd/proc")
+    try:
+        pids = os.listdir(root)
+    except OSError:
+        return busy
+    for pid in pids:
+        qdir = os.path.join(root, pid, "queues")
+        try:
+            qids = os.listdir(qdir)
+        except OSError:
+            continue
+        for q in qids:
+            try:
+                with open(os.path.join(qdir, q, "gpuid")) as f:
+                    busy.add(int(f.read().strip() or 0))
+            except (OSError, ValueError):
+                continue
+    return busy

@@ -212,6 +212,33 @@ def test_container_with_node_view_mounts(tmp_path, ordinals):
     assert init(viewed) < init(plain), (init(viewed), init(plain))
 
 
+def test_chip_sweep_covers_every_cu_and_xcd(ordinals):
+    """Full-chip sweep: one workgroup per CU, all resident together, every XCD runs
+    and every MFMA tile / LDS word is exact (one-shot and through the server)."""
+    import json
+    import subprocess
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    o = sorted(ordinals.values())[0]
+    env = dict(os.environ, ROCR_VISIBLE_DEVICES=str(o))
+    p = subprocess.run([str(probe_executable("hsa")), "--sweep", "--devices", "0", "--timeout", "20"],
+                       stdout=subprocess.PIPE, env=env, timeout=120)
+    d = json.loads(p.stdout.decode().strip().splitlines()[-1])["devices"][0]
+    assert p.returncode == 0 and d["ok"], d
+    assert d["grid"] == d["cu_count"] == d["cus_covered"], d
+    assert d["num_xcc"] == d["xccs_covered"] == 8 and len(set(d["wgs_per_xcc"])) == 1, d
+    assert d["mfma_bad"] == d["lds_bad"] == d["tile_bad"] == 0 and d["all_resident"], d
+    prober = LivenessProber(timeout_s=60)
+
+    async def go():
+        res = await prober.sweep({"gpu": o})
+        await prober.close()
+        return res["gpu"]
+
+    r = asyncio.run(go())
+    assert r.ok and r.detail["cus_covered"] == r.detail["cu_count"], r
+
+
 def test_smi_cross_check(inv):
     from rocm_k8s_device_plugin_amd.ops.native import core
     n = core()

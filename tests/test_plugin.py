@@ -636,3 +636,41 @@ def test_real_probe_binary_without_gpu_reports_unhealthy():
         assert prober.fallbacks == 1 and prober._server is None
 
     run(go())
+
+
+def test_chip_sweep_runs_on_idle_gpus_only(tmp_path):
+    """Every N-th pulse, GPUs without user queues get the full-chip sweep; a GPU
+    with another process' queues keeps the one-wave probe."""
+    from rocm_k8s_device_plugin_amd.topology import kfd_busy_gpu_ids
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    busy_dev = inv.by_id[fi.bdfs[2]]
+    busy_gid = inv.topology.node(busy_dev.node_id).gpu_id
+    q = fi.sysfs / "class/kfd/kfd/proc/4242/queues/0"
+    q.mkdir(parents=True)
+    (q / "gpuid").write_text(f"{busy_gid}\n")
+    assert kfd_busy_gpu_ids(str(fi.sysfs)) == {busy_gid}
+    ctl, prober = _stub_prober(tmp_path, {})
+    kinds = []
+    orig = prober.probe
+
+    async def spy(ordinals, kind="probe"):
+        kinds.append((kind, sorted(ordinals)))
+        return await orig(ordinals, kind)
+
+    prober.probe = spy
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, chip_sweep_every=2), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+
+    async def go():
+        for _ in range(3):
+            await mon.check_once()
+        assert all(v.health == "Healthy" for v in mon.snapshot().values())
+        await mon.close()
+
+    run(go())
+    everyone = sorted(d.id for d in inv.devices)
+    idle = sorted(set(everyone) - {busy_dev.id})
+    assert kinds == [("sweep", idle), ("probe", [busy_dev.id]), ("probe", everyone),
+                     ("sweep", idle), ("probe", [busy_dev.id])]
+    assert mon.chip_sweeps == 2
