@@ -8,11 +8,14 @@ GPUs advertised at 1/2/4/8 MI355X"). One timed step is one pod admission:
      the real device plugin over UDS gRPC: GetPreferredAllocation for a pod
      requesting amd.com/gpu=N out of the N advertised devices, then Allocate;
   2. the DeviceSpecs in the Allocate response are turned into a "container":
-     one fresh process per allocated GPU (one rank per GPU, like the pod's own
-     torchrun would start) restricted to its render node via
-     ROCR_VISIBLE_DEVICES;
-  3. each container initialises HIP and runs the gfx950 MFMA liveness kernel
-     on its GPU; it is "ready" when the tile verifies bit-exactly;
+     one fresh process (rank 0) restricted to the allocated render nodes via
+     ROCR_VISIBLE_DEVICES (--container-mode pod, what kubelet starts for a
+     pod), or one process per allocated GPU, one per rank, like a torchrun
+     workload inside the pod would start (--container-mode per-gpu; reported
+     as a comparison at N > 1);
+  3. the container initialises the GPU runtime and runs the gfx950 MFMA
+     liveness kernel on each of its GPUs (parallel host threads); it is
+     "ready" when every tile verifies bit-exactly;
   4. latency = (last container ready) - (kubelet starts GetPreferredAllocation),
      both on CLOCK_MONOTONIC;
   5. (untimed in the latency, inside the timed loop) the pod terminates: its
@@ -63,6 +66,11 @@ def parse_args():
     ap.add_argument("--settle", default="kfd", choices=["kfd", "none"],
                     help="between admissions wait until the previous containers' kfd processes are torn down "
                          "(the previous pod has terminated) or start the next one immediately")
+    ap.add_argument("--container-mode", default="pod", choices=["pod", "per-gpu"],
+                    help="pod: ONE container process gets all N allocated GPUs (rank 0 starts it; what kubelet "
+                         "does for a pod); per-gpu: each rank starts a process for its GPU (torchrun-style workload)")
+    ap.add_argument("--mode-compare", type=int, default=5,
+                    help="for N > 1: extra untimed admissions in the other --container-mode, reported for comparison")
     ap.add_argument("--node-view-compare", type=int, default=5,
                     help="extra untimed admissions with the plugin's -node_view mounts applied to the containers "
                          "(by path redirection: no root for bind mounts), reported for comparison")
@@ -204,7 +212,7 @@ def main():
     from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
 
     def one_step(record: bool, runtime: str = args.container_runtime, sink=None, settle: str = args.settle,
-                 init_sink=None):
+                 init_sink=None, mode: str = args.container_mode):
         if d.rank == 0:
             t0 = time.monotonic_ns()
             adm = loop.run_until_complete(kubelet.admit("amd.com/gpu", n))
@@ -223,8 +231,12 @@ def main():
             tr = time.monotonic_ns()
             mine = (True, tr, 0.0, "", (ts, ts, tr))
             lingering = frozenset()
+        elif mode == "pod" and d.rank != 0:
+            # the pod's single container runs on rank 0; other ranks only keep step
+            mine = (True, 0, 0.0, "", (0, 0, 0))
+            lingering = frozenset()
         else:
-            mine_ord = [ordl[d.rank]] if d.world > 1 else ordl
+            mine_ord = ordl if mode == "pod" or d.world == 1 else [ordl[d.rank]]
             r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime, mounts=mounts)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
             phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
@@ -270,7 +282,11 @@ def main():
     d.sync()
     elapsed = time.perf_counter() - t_start
     elapsed = d.max(elapsed)
-    hip_lat, b2b_lat, nv_lat, nv_init = [], [], [], []
+    hip_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
+    other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
+    if not args.fixture and n > 1:
+        for _ in range(args.mode_compare):
+            one_step(False, sink=other_mode_lat, mode=other_mode)
     if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
         # the plugin returns -node_view mounts from now on (alias = host path: the
         # fake runtime applies mounts by redirection and cannot add the alias mount)
@@ -311,6 +327,9 @@ def main():
                  "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
                  "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
                  "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
+                 "container_mode": args.container_mode,
+                 f"latency_p50_ms_container_mode_{other_mode}": round(pct(other_mode_lat, .5), 3) if other_mode_lat
+                 else None,
                  "latency_p50_ms_node_view_emulated": round(pct(nv_lat, .5), 3) if nv_lat else None,
                  "node_view_emulated_runtime_init_p50_ms": round(pct(nv_init, .5), 3) if nv_init else None,
                  "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
@@ -344,7 +363,9 @@ def main():
                      if not args.fixture else "synthetic 8xMI355X sysfs fixture; no-op containers (CPU only)"),
             "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
                        "global_batch": n, "seq_len": None,
-                       "parallelism": f"{n} GPUs advertised, 1 pod requesting {n}, 1 container process per GPU",
+                       "parallelism": (f"{n} GPUs advertised, 1 pod requesting {n}, " +
+                                       ("1 container process with all N GPUs" if args.container_mode == "pod"
+                                        else "1 container process per GPU")),
                        "between_admissions": ("previous pod's kfd teardown complete" if args.settle == "kfd"
                                               else "back-to-back")},
             "extra": extra,
