@@ -254,7 +254,7 @@ def main():
         # kfd process ~150 ms after it exits (bench latency excludes this wait)
         # N containers exiting together may be torn down one after another: allow
         # ~0.25 s each (measured ~0.15 s), capped so a stuck entry cannot stall the run
-        cap = min(3.0, 0.25 + 0.25 * len(lingering))
+        cap = min(3.0, 0.25 + 0.25 * max(len(lingering), n))  # one process with N GPUs tears down N VMs
         waited = wait_kfd_released(lingering, timeout_s=cap) if settle == "kfd" else 0.0
         if record:
             settle_ms.append(waited)
