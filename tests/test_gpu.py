@@ -239,6 +239,22 @@ def test_chip_sweep_covers_every_cu_and_xcd(ordinals):
     assert r.ok and r.detail["cus_covered"] == r.detail["cu_count"], r
 
 
+def test_node_labeller_on_real_mi355x():
+    """All label kinds on the real node: schema keys present and MI355X values."""
+    from rocm_k8s_device_plugin_amd import constants as C
+    from rocm_k8s_device_plugin_amd.labeller import labels as L
+    lab = L.generate_labels({k: True for k in C.SUPPORTED_LABELS}, "container")
+    flat = dict(lab)
+    keys = {k.split("/", 1)[1] for k in flat}
+    for k in ("gpu.family", "gpu.device-id", "gpu.cu-count", "gpu.vram", "gpu.simd-count",
+              "gpu.compute-partitioning-supported", "gpu.memory-partitioning-supported", "gpu.mode"):
+        assert any(x.startswith(k) for x in keys), (k, sorted(keys))
+    vals = {k.split("/", 1)[1]: v for k, v in flat.items() if k.startswith("amd.com/")}
+    assert vals.get("gpu.family") == "AI", vals
+    assert vals.get("gpu.device-id") == "75a3" and vals.get("gpu.cu-count") == "256", vals
+    assert vals.get("gpu.mode") == "container"
+
+
 def test_smi_cross_check(inv):
     from rocm_k8s_device_plugin_amd.ops.native import core
     n = core()

@@ -10,3 +10,5 @@ timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/
 cat gpurun_out/bench_default.json; cat /proc/loadavg
 timeout -k 10 200 python tools/plugin_startup.py --reps 5 --out gpurun_out/plugin_startup.json > gpurun_out/plugin_startup.log 2>&1 || { tail -20 gpurun_out/plugin_startup.log; exit 1; }
 cat gpurun_out/plugin_startup.log
+timeout -k 10 60 python -m rocm_k8s_device_plugin_amd.cli.node_labeller -dry_run -vram -cu-count -family -device-id -product-name -simd-count -driver-version -firmware -compute-memory-partition -compute-partitioning-supported -memory-partitioning-supported > gpurun_out/labels_box.json 2> gpurun_out/labels_box.err || { tail gpurun_out/labels_box.err; exit 1; }
+echo "labels: $(grep -c '"' gpurun_out/labels_box.json)"
