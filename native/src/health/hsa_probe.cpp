@@ -205,6 +205,7 @@ extern "C" int mi355x_hsa_probe_init(void) {
   if (g_rt.inited) return g_rt.init_status == HSA_STATUS_SUCCESS ? static_cast<int>(g_rt.gpus.size())
                                                                   : -static_cast<int>(g_rt.init_status);
   g_rt.inited = true;
+  g_rt.init_status = HSA_STATUS_SUCCESS;  // a shut-down runtime may be initialised again
   using clk = std::chrono::steady_clock;
   auto us = [](clk::time_point a, clk::time_point b) {
     return std::chrono::duration<double, std::micro>(b - a).count();
