@@ -79,6 +79,12 @@ def parse_args():
     ap.add_argument("--peer-check", type=int, default=1,
                     help="after the timed loop, DMA-copy + verify over every pair of the N GPUs' links (H2); "
                          "reported in extra.peer_probe, never part of the metric")
+    ap.add_argument("--collectives", type=int, default=1,
+                    help="for N > 1: after the timed loop, verify + time RCCL all-reduce / all-gather / "
+                         "reduce-scatter / all-to-all on the N ranks' GPUs (parallel/collectives.py); "
+                         "reported in extra.rccl next to the allocated set's xGMI fabric bound, never part of the metric")
+    ap.add_argument("--collective-sizes", default="",
+                    help="per-rank bytes for --collectives (default 1M,64M,256M on GPUs, 64K on CPU)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -306,6 +312,21 @@ def main():
         for _ in range(args.b2b_compare):
             one_step(False, sink=b2b_lat, settle="none")
 
+    rccl = None
+    if args.collectives and d.world > 1:
+        # the pod's GPUs as a torchrun workload sees them: one rank per GPU, RCCL over xGMI
+        from rocm_k8s_device_plugin_amd.parallel import collectives as coll
+        if d.cuda:
+            sizes = args.collective_sizes or "1M,64M,256M"
+            ops, iters, dtype = coll.DEFAULT_OPS, 20, d.torch.bfloat16
+        else:
+            sizes = args.collective_sizes or "64K"
+            ops, iters, dtype = ("all_reduce", "all_gather"), 3, d.torch.float32
+        rows = coll.run([coll.parse_size(x) for x in sizes.split(",") if x], ops, iters=iters, warmup=3,
+                        dtype=dtype)
+        rccl = coll.summary(rows)
+        rccl["backend"] = d.dist.get_backend()
+
     extra = {}
     if d.rank == 0:
         # allocator microbenchmark on the same request (ours vs the reference's ordered BFS)
@@ -338,6 +359,9 @@ def main():
                                              "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
                  "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
                  "reference_algorithm_candidates": ref["candidates"], "gpus": gpu_info}
+        from rocm_k8s_device_plugin_amd.parallel.fabric import Fabric
+        extra["fabric"] = Fabric(inv).report([dv.id for dv in adv]).as_dict()
+        extra["rccl"] = rccl
         if args.peer_check and not args.fixture:
             from rocm_k8s_device_plugin_amd.health.peer import probe_peers
             rep = probe_peers(adv_ordinals, nbytes=64 << 20, reps=3, timeout_s=120)

@@ -161,6 +161,12 @@ class InitSampler {
         } else if (nr == 0 || nr == 17 || nr == 16 || nr == 3) {  // read/pread64/ioctl/close(fd, ..)
           const long fd = static_cast<long>(std::strtoul(p, &p, 16));
           what += " " + fd_path(fd);
+          if (nr == 16) {  // ioctl(fd, cmd): the command's number byte names the kfd/drm call
+            const unsigned long cmd = std::strtoul(p, &p, 16);
+            char c[16];
+            std::snprintf(c, sizeof(c), " #%02lx", cmd & 0xFF);
+            what += c;
+          }
         }
       }
     } else {

@@ -28,13 +28,15 @@ from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence
 
-PARTITIONS = {"spx": 1, "dpx": 2, "qpx": 4, "cpx": 8}
-MI355X_DEVICE_ID = 0x75A3
-MI355X_VF_DEVICE_ID = 0x75B3
-MI355X_PRODUCT = "AMD Instinct MI355X"
-MI355X_VRAM = 288 * 1024 ** 3
-MI355X_CUS = 256
-MI355X_XCDS = 8
+from ..models import MI355X
+
+PARTITIONS = {cp: MI355X.partitions_per_gpu(cp) for cp in MI355X.compute_partitions}
+MI355X_DEVICE_ID = MI355X.device_ids[0]
+MI355X_VF_DEVICE_ID = MI355X.vf_device_ids[0]
+MI355X_PRODUCT = MI355X.name
+MI355X_VRAM = MI355X.vram_bytes
+MI355X_CUS = MI355X.cus
+MI355X_XCDS = MI355X.xcds
 DEFAULT_BUSES = [0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xE5, 0xF5]
 
 
@@ -231,7 +233,8 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
             if m["gpu"] == n["gpu"]:
                 io_links.append(dict(type=11, to=m["node"], weight=13, bw_min=819200, bw_max=819200))
             elif m["hive"] == n["hive"] and n["hive"] != 0:
-                io_links.append(dict(type=11, to=m["node"], weight=15, bw_min=153600, bw_max=153600))
+                io_links.append(dict(type=11, to=m["node"], weight=15, bw_min=MI355X.xgmi_link_mbps,
+                                     bw_max=MI355X.xgmi_link_mbps))
             else:
                 p2p_links.append(dict(type=2, to=m["node"], weight=72, bw_min=0, bw_max=0))
         vram = MI355X_VRAM // parts

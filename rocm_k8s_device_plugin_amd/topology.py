@@ -157,8 +157,9 @@ def discover(sysfs_root: str = "/sys", device_count_limit: Optional[int] = None)
     res = n.discover_gpus_with(sysfs_root, topo)
     devs = [Gpu.from_native(g) for g in res.devices]
     devs = _limit_physical(devs, device_count_limit)
+    from .models import check_inventory
     return Inventory(sysfs_root=sysfs_root, devices=tuple(devs), topology=topo, driver_loaded=res.driver_loaded,
-                     kfd_present=res.kfd_present, warnings=list(res.warnings))
+                     kfd_present=res.kfd_present, warnings=list(res.warnings) + check_inventory(devs))
 
 
 def hip_ordinals(inv: Inventory, dev_root: str = "/dev", check_access: bool = True) -> Dict[str, int]:

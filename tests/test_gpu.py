@@ -350,3 +350,50 @@ def test_rocprof_exactly_one_dispatch_per_probe(tmp_path, runtime):
     r = rows[0]
     assert (r["Workgroup_Size_X"], r["Grid_Size_X"]) == ("64", "64")
     assert int(r["LDS_Block_Size"]) == 0 and int(r["Scratch_Size"]) == 0
+
+
+def test_real_box_matches_mi355x_model(inv):
+    """The registry's MI355X numbers against the real part; consistent partitions."""
+    from rocm_k8s_device_plugin_amd.models import MI355X, check_inventory, model_for
+    readable = [d for d in inv.devices if d.unique_id]
+    for d in readable:
+        assert model_for(d.pci_device_id, d.gfx_target_version) is MI355X, hex(d.pci_device_id)
+        assert d.cu_count == MI355X.cus_per_partition(d.compute_partition)
+        assert abs(d.vram_bytes * MI355X.partitions_per_gpu(d.compute_partition) - MI355X.vram_bytes) \
+            < 0.01 * MI355X.vram_bytes
+    assert check_inventory(readable) == []
+
+
+def test_real_fabric_links(inv):
+    """Record the kfd io_links of the readable GPU nodes (xGMI type/bandwidth as the driver reports them)."""
+    from rocm_k8s_device_plugin_amd.parallel import Fabric
+    fab = Fabric(inv)
+    links = []
+    for nid in inv.topology.gpu_node_ids():
+        n = inv.topology.node(nid)
+        links += [dict(l, src=nid) for l in n.io_links] + [dict(l, src=nid) for l in n.p2p_links]
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/real_fabric_links.json", "w") as f:
+        json.dump({"links": links, "report": fab.report([d.id for d in inv.devices]).as_dict()}, f, indent=1)
+    readable = [d for d in inv.devices if d.unique_id]
+    assert readable
+    rep = fab.report([readable[0].id])
+    assert rep.physical_gpus == 1
+
+
+def test_collectives_cli_on_rccl():
+    """The pod-side collective check on RCCL (one rank: the box has one GPU; the 8-rank run is the driver's)."""
+    import socket
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), "-m", "rocm_k8s_device_plugin_amd.parallel.collectives",
+           "--sizes", "1M,64M", "--iters", "5", "--warmup", "2"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert {r["op"] for r in rows} == {"all_reduce", "all_gather", "reduce_scatter", "all_to_all"}
+    for r in rows:
+        assert r["ok"] is True and r["ranks"] == 1 and r["dtype"] == "bfloat16"

@@ -1,0 +1,103 @@
+"""Fabric model of allocated sets and the RCCL/gloo collective check (CPU)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.models import MI355X
+from rocm_k8s_device_plugin_amd.parallel import Fabric
+from rocm_k8s_device_plugin_amd.parallel.collectives import BUS_FACTOR, parse_size, summary
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+from rocm_k8s_device_plugin_amd.topology import discover
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_full_hive_bound(tmp_path):
+    inv = discover(str(make_mi355x_node(tmp_path / "n").sysfs))
+    fab = Fabric(inv)
+    ids = [d.id for d in inv.devices]
+    for k in (2, 4, 8):
+        r = fab.report(ids[:k])
+        assert r.one_hive and r.physical_gpus == k
+        assert r.pairs["xgmi"] == k * (k - 1) // 2 and r.pairs["pcie"] == 0
+        assert r.min_xgmi_degree == k - 1
+        # k-1 links per GPU carry a ring each: the bound grows with the set
+        assert r.allreduce_bound_gbs == pytest.approx((k - 1) * MI355X.xgmi_link_mbps / 1000)
+    assert fab.report(ids[:1]).allreduce_bound_gbs is None
+
+
+def test_split_hive_is_bounded_by_pcie(tmp_path):
+    inv = discover(str(make_mi355x_node(tmp_path / "n", hive_size=4).sysfs))
+    fab = Fabric(inv)
+    ids = [d.id for d in inv.devices]
+    same = fab.report(ids[:4])
+    split = fab.report(ids[2:6])          # 2 GPUs from each hive
+    assert same.one_hive and not split.one_hive
+    assert split.pairs["pcie"] == 4 and split.pairs["xgmi"] == 2
+    assert "crosses PCIe" in split.note
+    assert same.allreduce_bound_gbs == pytest.approx(3 * MI355X.xgmi_link_mbps / 1000)
+    assert split.allreduce_bound_gbs is None or split.allreduce_bound_gbs < same.allreduce_bound_gbs
+
+
+def test_partitions_share_their_gpu(tmp_path):
+    inv = discover(str(make_mi355x_node(tmp_path / "n", compute_partition="cpx").sysfs))
+    fab = Fabric(inv)
+    gpus = list(inv.physical_gpus().values())
+    one = fab.report([d.id for d in gpus[0][:4]])
+    assert one.physical_gpus == 1 and one.pairs["same_gpu"] == 6
+    two = fab.report([d.id for d in gpus[0][:2] + gpus[1][:2]])
+    assert two.physical_gpus == 2 and two.pairs["same_gpu"] == 2 and two.pairs["xgmi"] == 4
+    assert two.allreduce_bound_gbs == pytest.approx(MI355X.xgmi_link_mbps / 1000)
+
+
+def test_bus_factors_and_sizes():
+    assert BUS_FACTOR["all_reduce"](8) == pytest.approx(1.75)
+    assert BUS_FACTOR["all_gather"](8) == pytest.approx(0.875)
+    assert parse_size("64K") == 65536 and parse_size("1M") == 1 << 20 and parse_size("123") == 123
+    s = summary([{"op": "all_reduce", "bytes": 1, "busbw_gbs": 1.0, "ok": True},
+                 {"op": "all_reduce", "bytes": 4, "busbw_gbs": 3.0, "ok": True},
+                 {"op": "reduce_scatter", "bytes": 4, "ok": None, "unsupported": "gloo"}])
+    assert s["ok"] and s["busbw_gbs"] == {"all_reduce": 3.0}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_collectives_gloo_two_ranks():
+    """The pod-side CLI, launched the way a pod would (torchrun, one rank per device), on gloo."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), "-m", "rocm_k8s_device_plugin_amd.parallel.collectives",
+           "--sizes", "4K,64K", "--iters", "2", "--warmup", "1", "--dtype", "float32"]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    ops = {r["op"] for r in rows}
+    assert {"all_reduce", "all_gather", "all_to_all"} <= ops
+    for r in rows:
+        assert r["ranks"] == 2
+        if not r.get("unsupported"):
+            assert r["ok"] is True and r["algbw_gbs"] > 0
+
+
+def test_bench_fixture_reports_fabric_and_collectives():
+    """bench.py at N=2 on the fixture: the timed admissions, then collectives on the 2 ranks."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--fixture", "--steps", "2",
+           "--warmup", "1"]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["higher_is_better"] is False
+    fab, rccl = d["extra"]["fabric"], d["extra"]["rccl"]
+    assert fab["one_hive"] and fab["pairs"]["xgmi"] == 1
+    assert rccl["ok"] and rccl["backend"] == "gloo" and rccl["busbw_gbs"]["all_reduce"] > 0
