@@ -8,10 +8,12 @@
 // 0x18 MAP_MEMORY_TO_GPU, ...).
 //
 //   mi355x-rocr-devsetup HSACO [--order queue-first|alloc-first|code-first] -> one JSON line
+#include <dirent.h>
 #include <dlfcn.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstring>
@@ -39,7 +41,35 @@ struct Step {
   double ms = 0;
   hsa_status_t status = HSA_STATUS_SUCCESS;
   std::string profile;
+  std::string queues;
 };
+
+// This process' kfd queues (/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/type):
+// the queues ROCr created behind the API, e.g. {"ComputeAQL":2,"SDMA":1}.
+std::string kfd_queues() {
+  char dir[96];
+  std::snprintf(dir, sizeof(dir), "/sys/class/kfd/kfd/proc/%d/queues", static_cast<int>(getpid()));
+  DIR* d = opendir(dir);
+  if (!d) return "null";
+  std::vector<std::pair<std::string, int>> counts;
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] == '.') continue;
+    std::string p = std::string(dir) + "/" + e->d_name + "/type";
+    std::ifstream f(p);
+    std::string t;
+    std::getline(f, t);
+    if (t.empty()) t = "?";
+    bool found = false;
+    for (auto& kv : counts)
+      if (kv.first == t) ++kv.second, found = true;
+    if (!found) counts.emplace_back(t, 1);
+  }
+  closedir(d);
+  std::string o = "{";
+  for (size_t i = 0; i < counts.size(); ++i)
+    o += (i ? ",\"" : "\"") + counts[i].first + "\":" + std::to_string(counts[i].second);
+  return o + "}";
+}
 
 }  // namespace
 
@@ -247,7 +277,7 @@ int main(int argc, char** argv) {
     const hsa_status_t st = fn();
     const double b = now_ms();
     smp.stop();
-    steps.push_back({name, b - a, st, smp.json()});
+    steps.push_back({name, b - a, st, smp.json(), kfd_queues()});
     if (st != HSA_STATUS_SUCCESS) {
       ok = false;
       break;
@@ -260,7 +290,8 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < steps.size(); ++i) {
     if (i) o += ",";
     o += "{\"name\":\"" + steps[i].name + "\",\"ms\":" + std::to_string(steps[i].ms) +
-         ",\"status\":" + std::to_string(static_cast<int>(steps[i].status)) + ",\"profile\":" + steps[i].profile + "}";
+         ",\"status\":" + std::to_string(static_cast<int>(steps[i].status)) + ",\"profile\":" + steps[i].profile +
+         ",\"kfd_queues\":" + steps[i].queues + "}";
   }
   o += "]}";
   std::printf("%s\n", o.c_str());
