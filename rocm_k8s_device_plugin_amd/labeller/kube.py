@@ -22,7 +22,6 @@ import urllib.request
 from dataclasses import dataclass
 from typing import Dict, Optional
 
-import yaml
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
@@ -65,6 +64,7 @@ def _materialise(data_b64: Optional[str], suffix: str) -> Optional[str]:
 
 
 def load_kubeconfig(path: str) -> KubeConfig:
+    import yaml  # out-of-cluster only
     with open(path) as f:
         doc = yaml.safe_load(f) or {}
     ctx_name = doc.get("current-context")
