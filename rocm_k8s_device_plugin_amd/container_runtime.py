@@ -17,7 +17,7 @@ import re
 import subprocess
 import time
 from dataclasses import dataclass
-from typing import Dict, FrozenSet, Iterable, List, Mapping, Optional, Sequence, Set
+from typing import FrozenSet, Iterable, List, Mapping, Optional, Sequence, Set
 
 from .health.liveness import _VISIBILITY_VARS
 from .ops.native import probe_executable

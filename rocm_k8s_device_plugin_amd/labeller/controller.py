@@ -13,7 +13,6 @@ partition mode can change under a running DaemonSet) and re-asserted every
 from __future__ import annotations
 
 import threading
-import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Optional
 

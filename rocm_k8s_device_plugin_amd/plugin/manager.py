@@ -26,7 +26,7 @@ import asyncio
 import os
 import signal
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import grpc

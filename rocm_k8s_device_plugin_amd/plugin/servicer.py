@@ -14,7 +14,6 @@ adapter delegating to the DeviceImpl. Differences:
 from __future__ import annotations
 
 import time
-from typing import Optional
 
 import grpc
 
