@@ -340,6 +340,21 @@ def main():
         for _ in range(20):
             ref = pol.reference_allocate(avail, [], n)
         refu = (time.perf_counter() - t) / 20 * 1e6
+        # every smaller request on the same N advertised GPUs (the allocations a
+        # shared node serves): our set search vs the reference's ordered BFS,
+        # both in C++ on the same weights, same chosen set required
+        sweep = {}
+        for k in range(1, n):
+            t = time.perf_counter()
+            for _ in range(50):
+                mine = pol.native.allocate(avail, [], k)
+            mine_us = (time.perf_counter() - t) / 50 * 1e6
+            t = time.perf_counter()
+            for _ in range(3):
+                refk = pol.reference_allocate(avail, [], k)
+            sweep[str(k)] = {"ours_us": round(mine_us, 2), "reference_us": round((time.perf_counter() - t) / 3 * 1e6, 2),
+                             "reference_candidates": refk["candidates"], "ours_candidates": mine["candidates"],
+                             "same_set": sorted(mine["ids"]) == sorted(refk["ids"])}
         extra = {"plugin_rpc_p50_ms": round(pct(rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rpc_ms, .99), 4),
                  "allocate_rpc_p50_ms": round(pct(alloc_rpc_ms, .5), 4),
                  "container_start_to_ready_p50_ms": round(pct(ready_ms, .5), 3),
@@ -358,7 +373,7 @@ def main():
                                              "gpu_runtime_init": round(pct(rt_ms, .5), 3),
                                              "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
                  "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
-                 "reference_algorithm_candidates": ref["candidates"], "gpus": gpu_info}
+                 "reference_algorithm_candidates": ref["candidates"], "allocator_sweep": sweep, "gpus": gpu_info}
         from rocm_k8s_device_plugin_amd.parallel.fabric import Fabric
         extra["fabric"] = Fabric(inv).report([dv.id for dv in adv]).as_dict()
         extra["rccl"] = rccl
