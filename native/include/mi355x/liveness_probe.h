@@ -62,6 +62,11 @@ void mi355x_hsa_probe_shutdown(void);
 // takes teardown off its critical path.
 void mi355x_hsa_probe_defer_release(int on);
 void mi355x_hsa_probe_release(void);
+// With keep on, each device's queue, executable and buffers are created by its
+// first probe and reused by every later one (released by shutdown, or dropped
+// after a failed probe). A kept probe is one AQL packet: no kfd ioctl, so no
+// HWS runlist update that would preempt the queues of the pods on that GPU.
+void mi355x_hsa_probe_keep(int on);
 // Runtime start-up split of the last mi355x_hsa_probe_init (us): dlopen of
 // ROCr (its constructors), pre-open of /dev/kfd (on a second thread,
 // overlapped with the dlopen), hsa_init, agent enumeration, pool discovery.

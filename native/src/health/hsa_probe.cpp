@@ -25,6 +25,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -246,8 +247,13 @@ extern "C" void mi355x_hsa_init_phases(double out_us[5]) {
   for (int i = 0; i < 5; ++i) out_us[i] = g_rt.init_us[i];
 }
 
+namespace {
+void release_residents();
+}  // namespace
+
 extern "C" void mi355x_hsa_probe_shutdown(void) {
   mi355x_hsa_probe_release();
+  release_residents();
   std::lock_guard<std::mutex> lk(g_rt.mu);
   if (g_rt.inited && g_rt.init_status == HSA_STATUS_SUCCESS) H().hsa_shut_down();
   if (g_rt.kfd_fd >= 0) close(g_rt.kfd_fd);
@@ -385,15 +391,153 @@ extern "C" void mi355x_hsa_probe_release(void) {
   for (auto& r : todo) r.release();
 }
 
+namespace {
+
+// Queue + buffers (helper thread) and the executable (this thread), overlapped.
+// Fills out->phase_us[0..1] and out->setup_us; false with out->error on failure.
+bool setup_resources(const Agent& ag, ProbeResources& r, KernelInfo& k, mi355x_probe_result* out) {
+  using clk = std::chrono::steady_clock;
+  auto us_since = [](clk::time_point a) { return std::chrono::duration<double, std::micro>(clk::now() - a).count(); };
+  const auto t0 = clk::now();
+  Step qst, kst;
+  double queue_us = 0;
+  std::thread qthread([&] {
+    const auto tq = clk::now();
+    qst = make_queue_and_buffers(ag, r);
+    queue_us = us_since(tq);
+  });
+  kst = load_kernel(ag, r, k);
+  out->phase_us[0] = us_since(t0);  // code object load + freeze
+  qthread.join();
+  out->phase_us[1] = queue_us;      // queue + signal + buffers (overlapped with phase 0)
+  out->setup_us = us_since(t0);
+  if (!kst.ok() || !qst.ok()) {
+    const Step& bad = !kst.ok() ? kst : qst;
+    set_status(out, bad.s, bad.what);
+    return false;
+  }
+  if (k.kseg < sizeof(mi355x_liveness_args) || k.kseg > kKernargBytes) {
+    std::snprintf(out->error, sizeof(out->error), "kernarg segment %u outside [%zu, %u]: code object / host ABI mismatch",
+                  k.kseg, sizeof(mi355x_liveness_args), kKernargBytes);
+    return false;
+  }
+  return true;
+}
+
+// One AQL dispatch of the liveness kernel on r's queue, bounded wait, verdict.
+// Sets out->hip_error = -1 when the dispatch did not complete: r must then
+// never be freed (the kernel may still write to it).
+void dispatch_and_verify(const Agent& ag, ProbeResources& r, const KernelInfo& k, uint32_t nonce, double timeout_s,
+                         mi355x_probe_result* out) {
+  using clk = std::chrono::steady_clock;
+  const auto t_disp = clk::now();
+  std::memset(r.h_out, 0xFF, MI355X_PROBE_OUT * sizeof(float));
+  std::memset(r.h_meta, 0, 64);
+  std::memset(r.kargs, 0, kKernargBytes);
+  r.kargs->out = r.h_out;
+  r.kargs->meta = r.h_meta;
+  r.kargs->scratch = r.d_scratch;
+  r.kargs->nonce = nonce;
+  r.kargs->iters = out->iters;
+  H().hsa_signal_store_screlease(r.sig, 1);  // a kept signal was left at 0 by the previous dispatch
+
+  const uint64_t idx = H().hsa_queue_add_write_index_screlease(r.queue, 1);
+  auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(r.queue->base_address) + (idx & (r.queue->size - 1));
+  std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
+  pkt->workgroup_size_x = 64;
+  pkt->workgroup_size_y = 1;
+  pkt->workgroup_size_z = 1;
+  pkt->grid_size_x = 64;
+  pkt->grid_size_y = 1;
+  pkt->grid_size_z = 1;
+  pkt->private_segment_size = k.pseg;
+  pkt->group_segment_size = k.gseg;
+  pkt->kernel_object = k.kobj;
+  pkt->kernarg_address = r.kargs;
+  pkt->completion_signal = r.sig;
+  const uint16_t header = static_cast<uint16_t>(
+      (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
+                   __ATOMIC_RELEASE);
+  H().hsa_signal_store_screlease(r.queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+  out->dispatches = 1;
+
+  // bounded wait: a wedged device must come back as a verdict, not a hang
+  const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
+  hsa_signal_value_t v = 1;
+  while ((v = H().hsa_signal_wait_scacquire(r.sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
+                                        HSA_WAIT_STATE_BLOCKED)) >= 1) {
+    if (clk::now() > deadline) break;
+  }
+  out->phase_us[3] = std::chrono::duration<double, std::micro>(clk::now() - t_disp).count();
+  if (v >= 1) {
+    std::snprintf(out->error, sizeof(out->error), "dispatch did not complete within %.1fs", timeout_s);
+    out->hip_error = -1;
+    return;
+  }
+  hsa_amd_profiling_dispatch_time_t dt{};
+  if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, r.sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
+    out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
+  mi355x::verify_tile(r.h_out, r.h_meta, nonce, out->iters, out);
+}
+
+// Kept ("resident") per-device resources for mi355x_hsa_probe_keep(1).
+struct Resident {
+  std::mutex mu;  // one probe at a time per device
+  bool ready = false;
+  ProbeResources r;
+  KernelInfo k;
+};
+std::mutex g_resident_mu;
+bool g_keep = false;
+std::vector<std::pair<int, std::unique_ptr<Resident>>> g_resident;
+// resources of timed-out dispatches: the kernel may still write to them, so
+// they are never freed (bounded by one per device per hang)
+std::vector<ProbeResources> g_abandoned;
+
+// Frees every kept device's resources (runtime shutdown); abandoned ones go
+// with the runtime itself.
+void release_residents() {
+  std::lock_guard<std::mutex> lk(g_resident_mu);
+  for (auto& e : g_resident) {
+    std::lock_guard<std::mutex> lk2(e.second->mu);
+    if (e.second->ready) e.second->r.release();
+    e.second->ready = false;
+  }
+  g_resident.clear();
+  g_abandoned.clear();
+}
+
+Resident* resident_slot(int ordinal) {
+  std::lock_guard<std::mutex> lk(g_resident_mu);
+  for (auto& e : g_resident)
+    if (e.first == ordinal) return e.second.get();
+  g_resident.emplace_back(ordinal, std::make_unique<Resident>());
+  return g_resident.back().second.get();
+}
+
+}  // namespace
+
+extern "C" void mi355x_hsa_probe_keep(int on) {
+  std::lock_guard<std::mutex> lk(g_resident_mu);
+  g_keep = on != 0;
+}
+
 extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, double timeout_s,
                                        mi355x_probe_result* out) {
   using clk = std::chrono::steady_clock;
-  auto us_since = [](clk::time_point a) { return std::chrono::duration<double, std::micro>(clk::now() - a).count(); };
   std::memset(out, 0, sizeof(*out));
   out->kfd_node_id = -1;
   out->nonce = nonce;
   out->iters = iters < 1 ? 1 : iters;
   const auto t0 = clk::now();
+  auto finish = [&] {
+    out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+    return out->ok ? 0 : 1;
+  };
   int n = mi355x_hsa_probe_init();
   if (n < 0) {
     set_status(out, static_cast<hsa_status_t>(-n), "hsa_init");
@@ -411,92 +555,49 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
                   g_rt.has_kernarg, g_rt.has_fine, ag.has_coarse);
     return 1;
   }
+  bool keep;
+  {
+    std::lock_guard<std::mutex> lk(g_resident_mu);
+    keep = g_keep;
+  }
+
+  if (keep) {
+    Resident* slot = resident_slot(ordinal);
+    std::lock_guard<std::mutex> lk(slot->mu);
+    if (!slot->ready) {
+      if (!setup_resources(ag, slot->r, slot->k, out)) {
+        slot->r.release();
+        return finish();
+      }
+      slot->ready = true;
+    }
+    dispatch_and_verify(ag, slot->r, slot->k, nonce, timeout_s, out);
+    if (out->hip_error == -1) {  // still running: abandon, never free
+      std::lock_guard<std::mutex> lk2(g_resident_mu);
+      g_abandoned.push_back(slot->r);
+      slot->r = ProbeResources{};
+      slot->ready = false;
+    } else if (!out->ok) {       // wrong tile or error: start from fresh resources next time
+      slot->r.release();
+      slot->ready = false;
+    }
+    return finish();
+  }
 
   ProbeResources r;
   KernelInfo k;
-  Step qst, kst;
-  double queue_us = 0;
-  std::thread qthread([&] {
-    const auto tq = clk::now();
-    qst = make_queue_and_buffers(ag, r);
-    queue_us = us_since(tq);
-  });
-  kst = load_kernel(ag, r, k);
-  out->phase_us[0] = us_since(t0);  // code object load + freeze
-  qthread.join();
-  out->phase_us[1] = queue_us;      // queue + signal + buffers (overlapped with phase 0)
-  const auto t_setup = clk::now();
-  out->setup_us = std::chrono::duration<double, std::micro>(t_setup - t0).count();
-  out->phase_us[2] = 0;
-  if (!kst.ok() || !qst.ok()) {
-    const Step& bad = !kst.ok() ? kst : qst;
-    set_status(out, bad.s, bad.what);
-  } else if (k.kseg < sizeof(mi355x_liveness_args) || k.kseg > kKernargBytes) {
-    std::snprintf(out->error, sizeof(out->error), "kernarg segment %u outside [%zu, %u]: code object / host ABI mismatch",
-                  k.kseg, sizeof(mi355x_liveness_args), kKernargBytes);
-  } else {
-    std::memset(r.h_out, 0xFF, MI355X_PROBE_OUT * sizeof(float));
-    std::memset(r.h_meta, 0, 64);
-    std::memset(r.kargs, 0, kKernargBytes);
-    r.kargs->out = r.h_out;
-    r.kargs->meta = r.h_meta;
-    r.kargs->scratch = r.d_scratch;
-    r.kargs->nonce = nonce;
-    r.kargs->iters = out->iters;
-
-    const uint64_t idx = H().hsa_queue_add_write_index_screlease(r.queue, 1);
-    auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(r.queue->base_address) + (idx & (r.queue->size - 1));
-    std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
-    pkt->workgroup_size_x = 64;
-    pkt->workgroup_size_y = 1;
-    pkt->workgroup_size_z = 1;
-    pkt->grid_size_x = 64;
-    pkt->grid_size_y = 1;
-    pkt->grid_size_z = 1;
-    pkt->private_segment_size = k.pseg;
-    pkt->group_segment_size = k.gseg;
-    pkt->kernel_object = k.kobj;
-    pkt->kernarg_address = r.kargs;
-    pkt->completion_signal = r.sig;
-    const uint16_t header = static_cast<uint16_t>(
-        (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
-        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
-                     __ATOMIC_RELEASE);
-    H().hsa_signal_store_screlease(r.queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
-    out->dispatches = 1;
-
-    // bounded wait: a wedged device must come back as a verdict, not a hang
-    const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
-    hsa_signal_value_t v = 1;
-    while ((v = H().hsa_signal_wait_scacquire(r.sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
-                                          HSA_WAIT_STATE_BLOCKED)) >= 1) {
-      if (clk::now() > deadline) break;
-    }
-    out->phase_us[3] = us_since(t_setup);
-    if (v >= 1) {
-      std::snprintf(out->error, sizeof(out->error), "dispatch did not complete within %.1fs", timeout_s);
-      out->hip_error = -1;
-    } else {
-      hsa_amd_profiling_dispatch_time_t dt{};
-      if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, r.sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
-        out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
-      mi355x::verify_tile(r.h_out, r.h_meta, nonce, out->iters, out);
-    }
-  }
-  out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+  if (setup_resources(ag, r, k, out)) dispatch_and_verify(ag, r, k, nonce, timeout_s, out);
+  const int rc = finish();
   {
     std::unique_lock<std::mutex> lk(g_deferred_mu);
     // a timed-out dispatch may still be running: never free what it can write
     if (g_defer_release || out->hip_error == -1) {
       if (out->hip_error != -1) g_deferred.push_back(r);
-      return out->ok ? 0 : 1;
+      return rc;
     }
   }
   r.release();
-  return out->ok ? 0 : 1;
+  return rc;
 }
 
 namespace {

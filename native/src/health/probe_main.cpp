@@ -2,7 +2,7 @@
 // and print one JSON document.
 //
 //   mi355x-liveness-probe [--devices all|0,2,..] [--nonce N] [--iters N] [--identify] [--timeout S]
-//   mi355x-liveness-probe --serve      (long-lived; requests on stdin, see serve())
+//   mi355x-liveness-probe --serve [--keep]  (long-lived; requests on stdin, see serve())
 //   mi355x-liveness-probe --sweep [--devices ..]   (every CU of every XCD, see mi355x_chip_sweep)
 //   mi355x-liveness-probe --peer [--devices ..] [--peer-bytes B] [--peer-reps R]
 //                                      (DMA copy over every GPU pair's link, verified)
@@ -111,7 +111,9 @@ void init_phases(double out[5]) { mi355x_hsa_init_phases(out); }
 void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
 void teardown() { mi355x_hsa_probe_release(); }
 void runtime_shutdown() { mi355x_hsa_probe_shutdown(); }
+void keep_resources(bool on) { mi355x_hsa_probe_keep(on ? 1 : 0); }
 #else
+void keep_resources(bool) {}  // the HIP build reuses its runtime's queues anyway
 void init_phases(double out[5]) { out[0] = out[1] = out[2] = out[3] = out[4] = 0; }
 void defer_teardown() {}
 void teardown() {}
@@ -276,6 +278,9 @@ std::string devices_json(const std::vector<mi355x_probe_result>& results) {
 // and tear down a kfd process each time, and a GPU process that starts while
 // such a teardown is in flight blocks in open("/dev/kfd") for up to ~150 ms
 // (profiles/README.md §3c): a pod admitted during a health sweep would pay it.
+// With --keep the per-device queue, executable and buffers also stay: a probe
+// is then one AQL packet, with no queue creation (an HWS runlist update that
+// preempts every queue on that GPU, ~5 ms, profiles/README.md §3f) per pulse.
 int serve(int n, uint64_t t_start, uint64_t t_runtime) {
   prctl(PR_SET_PDEATHSIG, SIGKILL);
   if (getppid() == 1) return 0;  // parent already gone
@@ -348,6 +353,7 @@ int main(int argc, char** argv) {
   int sample_us = 0;
   std::string exit_mode = "shutdown";
   bool serve_mode = false;
+  bool keep = false;  // --serve --keep: per-device queue/executable/buffers live across requests
   bool peer_mode = false;
   bool sweep_mode = false;
   uint64_t peer_bytes = 64ull << 20;
@@ -381,6 +387,8 @@ int main(int argc, char** argv) {
       identify = true;
     } else if (a == "--serve") {
       serve_mode = true;
+    } else if (a == "--keep") {
+      keep = true;
     } else if (a == "--peer") {
       peer_mode = true;
     } else if (a == "--sweep") {
@@ -391,7 +399,7 @@ int main(int argc, char** argv) {
       peer_reps = std::atoi(next("--peer-reps"));
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
-                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep]\n",
+                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve [--keep]] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep]\n",
                   argv[0]);
       return 0;
     } else {
@@ -411,7 +419,10 @@ int main(int argc, char** argv) {
   const long long syscr_runtime = read_syscalls();
   double iph[5];
   init_phases(iph);
-  if (serve_mode) return serve(n, t_start, t_runtime);
+  if (serve_mode) {
+    keep_resources(keep);
+    return serve(n, t_start, t_runtime);
+  }
   if (n < 0) {
     std::printf("{\"ok\":false,\"hip_device_count\":0,\"error\":\"GPU runtime init failed (%d)\",\"devices\":[],"
                 "\"t_start_ns\":%llu,\"t_ready_ns\":0,\"init_profile\":%s}\n",

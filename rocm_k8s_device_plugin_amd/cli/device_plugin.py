@@ -48,6 +48,9 @@ def build_parser() -> flags.GoFlagParser:
     p.add_bool("liveness", False, "run the gfx950 MFMA liveness probe on every device each pulse")
     p.add_str("liveness_mode", "persistent", "persistent: one long-lived probe server per node; spawn: a fresh "
                                              "probe process per device per pulse")
+    p.add_bool("liveness_keep_queues", True, "persistent mode: keep each device's probe queue between pulses, so a "
+                                             "pulse creates no kfd queue (no HWS runlist update that preempts the "
+                                             "pods on that GPU); false: create and destroy it every pulse")
     p.add_int("liveness_chip_sweep_every", 0, "every N-th pulse (and the first) run the full-chip MFMA/LDS sweep "
                                              "(every CU of every XCD) on GPUs with no running work; 0 = off")
     p.add_float("liveness_timeout", 10.0, "per-device liveness probe deadline (s)")
@@ -100,7 +103,8 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
         hc = HealthConfig(exporter_socket=ns.exporter_socket or None, liveness=ns.liveness,
                           liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
                           smi_ecc=ns.smi_ecc, smi_events=ns.smi_events, dev_root=ns.dev_root,
-                          liveness_mode=ns.liveness_mode, chip_sweep_every=ns.liveness_chip_sweep_every)
+                          liveness_mode=ns.liveness_mode, chip_sweep_every=ns.liveness_chip_sweep_every,
+                          liveness_keep_queues=ns.liveness_keep_queues)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count,

@@ -113,7 +113,7 @@ class LivenessProber:
 
     def __init__(self, exe: Optional[str] = None, timeout_s: float = 10.0, iters: int = 4, max_parallel: int = 8,
                  extra_env: Optional[Mapping[str, str]] = None, argv_prefix: Sequence[str] = (),
-                 mode: str = "persistent"):
+                 mode: str = "persistent", keep_queues: bool = True):
         if mode not in self.MODES:
             raise ValueError(f"liveness mode must be one of {self.MODES}, got {mode!r}")
         self.exe = str(exe) if exe else None
@@ -123,6 +123,10 @@ class LivenessProber:
         self.extra_env = dict(extra_env or {})
         self.argv_prefix = list(argv_prefix)
         self.mode = mode
+        # persistent mode only: the server keeps each device's queue, executable
+        # and buffers between sweeps (`--serve --keep`), so a sweep creates no
+        # kfd queue and causes no HWS runlist update on the tenants' GPUs
+        self.keep_queues = keep_queues
         self.sweeps = 0
         self.server_starts = 0
         self.fallbacks = 0
@@ -191,7 +195,7 @@ class LivenessProber:
     async def _probe_server(self, uniq, kind: str = "probe") -> Dict[int, ProbeOutcome]:
         t0 = time.perf_counter()
         if self._server is None or not self._server.alive:
-            argv = [*self.argv_prefix, self._exe(), "--serve"]
+            argv = [*self.argv_prefix, self._exe(), "--serve", *(["--keep"] if self.keep_queues else [])]
             self._server = await _ProbeServer.start(argv, self._env(None), self.timeout_s)
             self.server_starts += 1
         nonces = {o: self._nonce(o) for o in uniq}

@@ -56,6 +56,7 @@ class HealthConfig:
     liveness_iters: int = 4
     liveness_parallel: int = 8
     liveness_mode: str = "persistent"  # persistent probe server | spawn per device per sweep
+    liveness_keep_queues: bool = True  # persistent server keeps per-device queues between sweeps
     # every N-th sweep (and the first), GPUs with no user queues from any process
     # get the full-chip sweep (every CU of every XCD) instead of the one-wave probe
     chip_sweep_every: int = 0
@@ -84,7 +85,8 @@ class HealthMonitor:
         self.prober = prober
         if self.cfg.liveness and self.prober is None:
             self.prober = LivenessProber(timeout_s=self.cfg.liveness_timeout_s, iters=self.cfg.liveness_iters,
-                                         max_parallel=self.cfg.liveness_parallel, mode=self.cfg.liveness_mode)
+                                         max_parallel=self.cfg.liveness_parallel, mode=self.cfg.liveness_mode,
+                                         keep_queues=self.cfg.liveness_keep_queues)
         self._ordinals = dict(ordinal_map) if ordinal_map is not None else None
         # amd-smi event watcher (or a test double with start/poll/stop)
         self._events = event_source

@@ -67,7 +67,8 @@ def main(argv):
     log = os.environ.get("MI355X_STUB_PROBE_LOG")
     if log:
         with open(log, "a") as f:
-            f.write(("serve" if "--serve" in argv else os.environ.get("ROCR_VISIBLE_DEVICES", "0")) + "\n")
+            f.write(("serve" + ("+keep" if "--keep" in argv else "") if "--serve" in argv
+                     else os.environ.get("ROCR_VISIBLE_DEVICES", "0")) + "\n")
     if "--serve" in argv:
         return serve()
     nonce = 0

@@ -163,6 +163,32 @@ def test_persistent_probe_server(ordinals):
     assert min(lat[1:]) < 100.0, lat
 
 
+def test_persistent_probe_server_keeps_queues(ordinals):
+    """--serve --keep: the first sweep sets the device up, later sweeps are one packet each (no set-up, fresh
+    nonce verified every time); a kept device survives many sweeps."""
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    prober = LivenessProber(timeout_s=60, mode="persistent", keep_queues=True)
+    ords = dict(ordinals)
+
+    async def go():
+        docs = []
+        for _ in range(12):
+            res = await prober.probe(ords)
+            assert all(r.ok for r in res.values()), res
+            docs.append([r.detail for r in res.values()])
+        assert prober.server_starts == 1 and prober.fallbacks == 0
+        await prober.close()
+        return docs
+
+    docs = asyncio.run(go())
+    assert all(d["setup_us"] > 1000 for d in docs[0])        # queue + executable on the first sweep
+    for sweep in docs[1:]:
+        for d in sweep:
+            assert d["setup_us"] == 0 and d["dispatches"] == 1 and d["mismatches"] == 0
+            assert d["total_us"] < 5000, d                    # one AQL packet + wait, no kfd ioctls
+    assert len({d["nonce"] for sweep in docs for d in sweep}) == sum(len(s) for s in docs)
+
+
 def test_peer_probe_self_copy(ordinals):
     """H2 path on one GPU: HBM -> HBM DMA copy, readback, word-exact verify."""
     from rocm_k8s_device_plugin_amd.health.peer import probe_peers

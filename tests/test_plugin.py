@@ -507,7 +507,27 @@ def test_liveness_persistent_server_reused(tmp_path):
         assert prober._server is None
 
     run(go())
-    assert log_path.read_text().split() == ["serve"]
+    assert log_path.read_text().split() == ["serve+keep"]
+
+
+def test_liveness_keep_queues_flag_reaches_server(tmp_path):
+    """-liveness_keep_queues (default on) starts the server as `--serve --keep` (resources kept between sweeps)."""
+    from rocm_k8s_device_plugin_amd.cli import device_plugin as cli
+    assert cli.build_parser().parse_args([]).liveness_keep_queues is True
+    assert cli.build_parser().parse_args(["-liveness_keep_queues=false"]).liveness_keep_queues is False
+    log_path = tmp_path / "starts.log"
+    ctl, prober = _stub_prober(tmp_path, {})
+    prober.keep_queues = True
+    prober.extra_env["MI355X_STUB_PROBE_LOG"] = str(log_path)
+
+    async def go():
+        for _ in range(2):
+            res = await prober.probe({"dev0": 0, "dev1": 1})
+            assert all(r.ok for r in res.values())
+        await prober.close()
+
+    run(go())
+    assert log_path.read_text().split() == ["serve+keep"]
 
 
 def test_liveness_server_failure_isolates_per_device(tmp_path):
@@ -533,7 +553,7 @@ def test_liveness_server_failure_isolates_per_device(tmp_path):
 
     run(go(), timeout=60)
     starts = log_path.read_text().split()
-    assert starts[0] == "serve" and sorted(starts[1:9]) == [str(i) for i in range(8)] and starts[-1] == "serve"
+    assert starts[0] == "serve+keep" and sorted(starts[1:9]) == [str(i) for i in range(8)] and starts[-1] == "serve+keep"
 
 
 def test_liveness_server_start_failure_falls_back(tmp_path):

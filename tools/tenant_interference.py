@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""Does the plugin's liveness loop disturb a pod that is computing on the GPU?
+
+A "tenant" process runs back-to-back bf16 GEMMs (torch, hipBLASLt) on GPU 0
+and times every one with HIP events, while the plugin's LivenessProber probes
+the same GPU every --pulse seconds in one of these modes:
+
+  none        no health loop (reference point)
+  per_sweep   persistent probe server, queue/executable created and destroyed
+              every sweep (two kfd queue operations = two HWS runlist updates
+              per pulse, each of which preempts every queue on the GPU)
+  keep        persistent probe server with --keep: the queue lives across
+              sweeps, a sweep is one AQL packet
+
+Reports, per mode, the tenant's GEMM time distribution (p50/p99/p99.9/max),
+GEMMs slower than 1.5x the median ("stalls"), throughput, and the sweep
+latency.
+
+  python tools/tenant_interference.py --seconds 6 --pulse 0.05 --out gpurun_out/tenant_interference.json
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+TENANT = r"""
+import json, sys, time, torch
+n, seconds = int(sys.argv[1]), float(sys.argv[2])
+a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+for _ in range(20):
+    torch.matmul(a, b, out=c)
+torch.cuda.synchronize()
+print("READY", flush=True)
+sys.stdin.readline()                      # go
+evs, t_end = [], time.perf_counter() + seconds
+while time.perf_counter() < t_end:        # batches of 50 GEMMs, each bracketed by events
+    batch = [torch.cuda.Event(enable_timing=True) for _ in range(51)]
+    batch[0].record()
+    for i in range(50):
+        torch.matmul(a, b, out=c)
+        batch[i + 1].record()
+    evs.append(batch)
+    if len(evs) > 2:
+        evs[-3][-1].synchronize()        # keep at most ~2 batches queued ahead
+torch.cuda.synchronize()
+ms = [batch[i].elapsed_time(batch[i + 1]) for batch in evs for i in range(50)]
+print(json.dumps({"n": n, "gemms": len(ms), "ms": ms}), flush=True)
+"""
+
+
+def stats(ms, n):
+    s = sorted(ms)
+    med = statistics.median(s)
+    q = lambda p: s[min(len(s) - 1, int(p * (len(s) - 1)))]  # noqa: E731
+    flops = 2.0 * n ** 3
+    return {"gemms": len(s), "p50_ms": round(med, 4), "p99_ms": round(q(0.99), 4), "p999_ms": round(q(0.999), 4),
+            "max_ms": round(s[-1], 4), "stalls_over_1p5x": sum(1 for x in s if x > 1.5 * med),
+            "stall_ms_total": round(sum(x - med for x in s if x > 1.5 * med), 3),
+            "tflops_mean": round(flops * len(s) / (sum(s) * 1e-3) / 1e12, 1)}
+
+
+async def run_mode(mode: str, a) -> dict:
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    prober = None
+    if mode != "none":
+        prober = LivenessProber(timeout_s=30, mode="persistent", keep_queues=(mode == "keep"))
+        res = await prober.probe({"gpu0": 0})          # server up before the tenant starts timing
+        assert all(r.ok for r in res.values()), res
+    tenant = subprocess.Popen([sys.executable, "-c", TENANT, str(a.n), str(a.seconds)], stdin=subprocess.PIPE,
+                              stdout=subprocess.PIPE, text=True, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    line = await asyncio.to_thread(tenant.stdout.readline)
+    assert line.strip() == "READY", line
+    stop = asyncio.Event()
+    sweep_ms = []
+
+    async def health_loop():
+        while not stop.is_set():
+            t0 = time.perf_counter()
+            res = await prober.probe({"gpu0": 0})
+            assert all(r.ok for r in res.values()), res
+            sweep_ms.append((time.perf_counter() - t0) * 1e3)
+            try:
+                await asyncio.wait_for(stop.wait(), a.pulse)
+            except asyncio.TimeoutError:
+                pass
+
+    tenant.stdin.write("go\n")
+    tenant.stdin.flush()
+    task = asyncio.create_task(health_loop()) if prober else None
+    out = await asyncio.to_thread(tenant.stdout.readline)
+    stop.set()
+    if task:
+        await task
+        await prober.close()
+    rc = await asyncio.to_thread(tenant.wait)
+    assert rc == 0, rc
+    doc = json.loads(out)
+    r = {"mode": mode, "pulse_s": a.pulse if prober else None, "gemm_n": a.n, **stats(doc["ms"], a.n),
+         "health_sweeps": len(sweep_ms),
+         "health_sweep_ms_p50": round(statistics.median(sweep_ms), 3) if sweep_ms else None}
+    print(json.dumps(r), flush=True)
+    return r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=6.0)
+    ap.add_argument("--pulse", type=float, default=0.05)
+    ap.add_argument("--n", type=int, default=8192, help="GEMM size (n x n x n, bf16)")
+    ap.add_argument("--modes", default="none,per_sweep,keep,none")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+
+    async def go():
+        return [await run_mode(m, a) for m in a.modes.split(",")]
+
+    res = asyncio.run(go())
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"runs": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
