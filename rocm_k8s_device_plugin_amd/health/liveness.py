@@ -113,7 +113,8 @@ class LivenessProber:
 
     def __init__(self, exe: Optional[str] = None, timeout_s: float = 10.0, iters: int = 4, max_parallel: int = 8,
                  extra_env: Optional[Mapping[str, str]] = None, argv_prefix: Sequence[str] = (),
-                 mode: str = "persistent", keep_queues: bool = True):
+                 mode: str = "persistent", keep_queues: bool = True,
+                 kfd_proc_dir: str = "/sys/class/kfd/kfd/proc"):
         if mode not in self.MODES:
             raise ValueError(f"liveness mode must be one of {self.MODES}, got {mode!r}")
         self.exe = str(exe) if exe else None
@@ -127,11 +128,38 @@ class LivenessProber:
         # and buffers between sweeps (`--serve --keep`), so a sweep creates no
         # kfd queue and causes no HWS runlist update on the tenants' GPUs
         self.keep_queues = keep_queues
+        # the server's own kfd process entry (its queues must not make a GPU
+        # look busy to the chip-sweep scheduler); found by listing
+        # <kfd_proc_dir> around the server's start-up, since the entry is
+        # named by the host PID, which a containerised plugin cannot see
+        self.kfd_proc_dir = kfd_proc_dir
+        self._own_kfd: frozenset = frozenset()
         self.sweeps = 0
         self.server_starts = 0
         self.fallbacks = 0
         self._server: Optional[_ProbeServer] = None
         self._server_backoff = 0  # sweeps to run in spawn mode after a server failure
+
+    def _kfd_entries(self) -> set:
+        try:
+            return set(os.listdir(self.kfd_proc_dir))
+        except OSError:
+            return set()
+
+    @property
+    def own_kfd_entries(self) -> frozenset:
+        """kfd proc entries of the running probe server (empty when unknown).
+
+        Several entries can appear while the server starts if another GPU
+        process starts at the same moment; the ambiguity resolves once the
+        others have exited (the server's entry lives as long as it does).
+        Unresolved, nothing is claimed, so GPUs look busy: the safe side.
+        """
+        if self._server is None or not self._server.alive:
+            return frozenset()
+        if len(self._own_kfd) > 1:
+            self._own_kfd = frozenset(self._own_kfd & self._kfd_entries())
+        return self._own_kfd if len(self._own_kfd) == 1 else frozenset()
 
     def _exe(self) -> str:
         if self.exe is None:
@@ -196,7 +224,9 @@ class LivenessProber:
         t0 = time.perf_counter()
         if self._server is None or not self._server.alive:
             argv = [*self.argv_prefix, self._exe(), "--serve", *(["--keep"] if self.keep_queues else [])]
+            before = self._kfd_entries()
             self._server = await _ProbeServer.start(argv, self._env(None), self.timeout_s)
+            self._own_kfd = frozenset(self._kfd_entries() - before)
             self.server_starts += 1
         nonces = {o: self._nonce(o) for o in uniq}
         inner = max(0.5, self.timeout_s - 0.5)

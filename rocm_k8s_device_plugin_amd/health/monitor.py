@@ -86,7 +86,8 @@ class HealthMonitor:
         if self.cfg.liveness and self.prober is None:
             self.prober = LivenessProber(timeout_s=self.cfg.liveness_timeout_s, iters=self.cfg.liveness_iters,
                                          max_parallel=self.cfg.liveness_parallel, mode=self.cfg.liveness_mode,
-                                         keep_queues=self.cfg.liveness_keep_queues)
+                                         keep_queues=self.cfg.liveness_keep_queues,
+                                         kfd_proc_dir=os.path.join(self.inv.sysfs_root, "class/kfd/kfd/proc"))
         self._ordinals = dict(ordinal_map) if ordinal_map is not None else None
         # amd-smi event watcher (or a test double with start/poll/stop)
         self._events = event_source
@@ -194,7 +195,8 @@ class HealthMonitor:
 
     def _idle_devices(self, dev_ids) -> set:
         """Devices whose kfd gpu_id has no user queue in any process right now."""
-        busy = kfd_busy_gpu_ids(self.inv.sysfs_root)
+        own = self.prober.own_kfd_entries if self.prober is not None else ()
+        busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
         idle = set()
         for dev_id in dev_ids:
             d = self.inv.by_id.get(dev_id)

@@ -34,11 +34,29 @@ def _device(ordinal_reported, mode, nonce):
            "error": "" if ok or mode == "stale" else "17/1024 MFMA results differ from host reference"}
 
 
+def _kfd_entry():
+    """Like a kept-queue server: a kfd proc entry with one queue per GPU id
+    (MI355X_STUB_KFD_PROC / MI355X_STUB_KFD_GPUIDS), removed on exit."""
+    root, gids = os.environ.get("MI355X_STUB_KFD_PROC"), os.environ.get("MI355X_STUB_KFD_GPUIDS", "")
+    if not root:
+        return None
+    import shutil
+    entry = os.path.join(root, str(os.getpid()))
+    for i, g in enumerate(x for x in gids.split(",") if x):
+        os.makedirs(os.path.join(entry, "queues", str(i)), exist_ok=True)
+        with open(os.path.join(entry, "queues", str(i), "gpuid"), "w") as f:
+            f.write(g + "\n")
+    import atexit
+    atexit.register(shutil.rmtree, entry, True)
+    return entry
+
+
 def serve():
     ctl = _control()
     if ctl.get("serve") == "broken":
         print(json.dumps({"serve": True, "ok": False, "hip_device_count": 0}), flush=True)
         return 2
+    _kfd_entry()
     t = time.monotonic_ns()
     print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "t_start_ns": t, "t_runtime_ns": t}),
           flush=True)

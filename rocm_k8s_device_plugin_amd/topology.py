@@ -185,17 +185,21 @@ def hip_ordinals(inv: Inventory, dev_root: str = "/dev", check_access: bool = Tr
     return {d.id: pos[d.node_id] for d in inv.devices if d.node_id in pos}
 
 
-def kfd_busy_gpu_ids(sysfs_root: str = "/sys") -> set:
+def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
     """kfd gpu_ids that currently have user queues, from any process on the host
-    (``/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/gpuid``). A GPU without queues
-    runs no work; the liveness loop runs its full-chip sweep only on those."""
+    (``/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/gpuid``) except the ``exclude``d
+    entries (the plugin's own probe server). A GPU without queues runs no work;
+    the liveness loop runs its full-chip sweep only on those."""
     busy = set()
     root = os.path.join(sysfs_root, "class/kfd/kfd/proc")
     try:
         pids = os.listdir(root)
     except OSError:
         return busy
+    skip = set(exclude)
     for pid in pids:
+        if pid in skip:
+            continue
         qdir = os.path.join(root, pid, "queues")
         try:
             qids = os.listdir(qdir)

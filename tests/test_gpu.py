@@ -189,6 +189,29 @@ def test_persistent_probe_server_keeps_queues(ordinals):
     assert len({d["nonce"] for sweep in docs for d in sweep}) == sum(len(s) for s in docs)
 
 
+def test_kept_queue_server_is_not_a_tenant(inv, ordinals):
+    """The kept-queue server's own kfd entry is found and excluded: its queue does not make the GPU look busy."""
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    from rocm_k8s_device_plugin_amd.topology import kfd_busy_gpu_ids
+    dev_id, o = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
+    gid = inv.topology.node(inv.by_id[dev_id].node_id).gpu_id
+    prober = LivenessProber(timeout_s=60, mode="persistent", keep_queues=True)
+
+    async def go():
+        before = kfd_busy_gpu_ids("/sys")     # this test process may hold HIP queues of its own
+        res = await prober.probe({dev_id: o})
+        assert all(r.ok for r in res.values()), res
+        own = prober.own_kfd_entries
+        assert len(own) == 1, own
+        qdir = os.path.join("/sys/class/kfd/kfd/proc", next(iter(own)), "queues")
+        gids = {int(open(os.path.join(qdir, q, "gpuid")).read()) for q in os.listdir(qdir)}
+        assert gid in gids                                          # the server's kept queue
+        assert kfd_busy_gpu_ids("/sys", exclude=own) == before      # ... is not counted as a tenant
+        await prober.close()
+
+    asyncio.run(go())
+
+
 def test_peer_probe_self_copy(ordinals):
     """H2 path on one GPU: HBM -> HBM DMA copy, readback, word-exact verify."""
     from rocm_k8s_device_plugin_amd.health.peer import probe_peers

@@ -658,6 +658,51 @@ def test_real_probe_binary_without_gpu_reports_unhealthy():
     run(go())
 
 
+def test_chip_sweep_ignores_the_probe_servers_own_queues(tmp_path):
+    """A kept-queue probe server has a queue on every GPU; those must not make the GPUs look busy."""
+    from rocm_k8s_device_plugin_amd.topology import kfd_busy_gpu_ids
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    proc = fi.sysfs / "class/kfd/kfd/proc"
+    gids = [inv.topology.node(d.node_id).gpu_id for d in inv.devices]
+    busy_dev = inv.by_id[fi.bdfs[5]]
+    q = proc / "777/queues/0"          # a pod's process on GPU 5
+    q.mkdir(parents=True)
+    (q / "gpuid").write_text(f"{gids[5]}\n")
+    ctl, prober = _stub_prober(tmp_path, {})
+    prober.kfd_proc_dir = str(proc)
+    prober.extra_env.update({"MI355X_STUB_KFD_PROC": str(proc),
+                             "MI355X_STUB_KFD_GPUIDS": ",".join(str(g) for g in gids)})
+    kinds = []
+    orig = prober.probe
+
+    async def spy(ordinals, kind="probe"):
+        kinds.append((kind, sorted(ordinals)))
+        return await orig(ordinals, kind)
+
+    prober.probe = spy
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, chip_sweep_every=2), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+
+    async def go():
+        for _ in range(3):
+            await mon.check_once()
+        own = prober.own_kfd_entries
+        assert own == {str(prober._server.proc.pid)}
+        assert kfd_busy_gpu_ids(str(fi.sysfs)) == set(gids)                 # everyone, counting the server
+        assert kfd_busy_gpu_ids(str(fi.sysfs), exclude=own) == {gids[5]}    # only the pod's GPU
+        await mon.close()
+        assert prober.own_kfd_entries == frozenset()
+
+    run(go())
+    everyone = sorted(d.id for d in inv.devices)
+    idle = sorted(set(everyone) - {busy_dev.id})
+    # pulse 2 runs while the server holds queues on all 8 GPUs: still swept as idle
+    assert kinds == [("sweep", idle), ("probe", [busy_dev.id]), ("probe", everyone),
+                     ("sweep", idle), ("probe", [busy_dev.id])]
+    assert mon.chip_sweeps == 2
+
+
 def test_chip_sweep_runs_on_idle_gpus_only(tmp_path):
     """Every N-th pulse, GPUs without user queues get the full-chip sweep; a GPU
     with another process' queues keeps the one-wave probe."""
