@@ -206,7 +206,8 @@ def test_kept_queue_server_is_not_a_tenant(inv, ordinals):
         qdir = os.path.join("/sys/class/kfd/kfd/proc", next(iter(own)), "queues")
         gids = {int(open(os.path.join(qdir, q, "gpuid")).read()) for q in os.listdir(qdir)}
         assert gid in gids                                          # the server's kept queue
-        assert kfd_busy_gpu_ids("/sys", exclude=own) == before      # ... is not counted as a tenant
+        # ... is not counted as a tenant (other GPUs of the shared host come and go: look at ours only)
+        assert (gid in kfd_busy_gpu_ids("/sys", exclude=own)) == (gid in before)
         await prober.close()
 
     asyncio.run(go())
