@@ -211,3 +211,51 @@ def test_mi355x_fixture_cpx(tmp_path):
     r = pol.allocate(ids, [], 12)
     assert len({inv.by_id[i].unique_id for i in r}) == 2
     assert len({inv.by_id[i].numa_node for i in r}) == 1
+
+
+# ---- property: fragmented nodes ------------------------------------------------
+# kubelet's real requests come from partly used nodes: random availability and
+# must-include sets. Ours must pick exactly what the reference's ordered BFS
+# picks (same set, same weight) on the same weights, whatever the state.
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+_POLS = {}
+
+
+def _pol(ref, name):
+    if name not in _POLS:
+        _POLS[name] = make_policy(ref, name)
+    return _POLS[name]
+
+
+@st.composite
+def _fragmented(draw, n_ids):
+    avail_mask = draw(st.lists(st.booleans(), min_size=n_ids, max_size=n_ids).filter(lambda m: sum(m) >= 1))
+    avail = [i for i, m in enumerate(avail_mask) if m]
+    k = draw(st.integers(min_value=1, max_value=min(len(avail), 12)))
+    nreq = draw(st.integers(min_value=0, max_value=min(2, k)))
+    req = draw(st.lists(st.sampled_from(avail), min_size=nreq, max_size=nreq, unique=True)) if nreq else []
+    return avail, req, k
+
+
+@pytest.mark.parametrize("name", ["mi300cpx", "mi308", "mi210"])
+def test_fragmented_nodes_match_reference_bfs(ref_testdata, name):
+    pol, ids = _pol(ref_testdata, name)
+
+    @settings(max_examples=120, deadline=None, derandomize=True,
+              suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+    @given(_fragmented(len(ids)))
+    def check(state):
+        avail_i, req_i, k = state
+        av = [ids[i] for i in avail_i]
+        req = [ids[i] for i in req_i]
+        ours = pol.explain(av, req, k)
+        ref = pol.reference_allocate(av, req, k)
+        assert ours["error"] == ref["error"]
+        if ours["error"]:
+            return
+        assert set(req) <= set(ours["ids"]) and len(ours["ids"]) == k
+        assert ours["weight"] == ref["weight"], (av, req, k)
+        assert sorted(ours["ids"]) == sorted(ref["ids"]), (av, req, k)
+
+    check()
