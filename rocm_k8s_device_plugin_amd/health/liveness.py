@@ -136,6 +136,7 @@ class LivenessProber:
         self._own_kfd: frozenset = frozenset()
         self.sweeps = 0
         self.server_starts = 0
+        self.server_restarts = 0   # restarted after failing a device a fresh process found healthy
         self.fallbacks = 0
         self._server: Optional[_ProbeServer] = None
         self._server_backoff = 0  # sweeps to run in spawn mode after a server failure
@@ -253,6 +254,37 @@ class LivenessProber:
         be resident, so callers run it only on GPUs without foreign work."""
         return await self.probe(ordinals, kind="sweep")
 
+    async def _confirm_failures(self, failed, results, kind: str) -> Dict[int, ProbeOutcome]:
+        """Re-probe the devices the server failed, each in a fresh process.
+
+        The server's runtime lives across sweeps (and with kept queues so do its
+        queues): after a GPU reset, or anything else that leaves that runtime
+        stale, it could keep failing a device that a fresh process finds
+        healthy. A failure is therefore only reported when a fresh process
+        confirms it; if one does not, the server is restarted for the next sweep.
+        """
+        sem = asyncio.Semaphore(self.max_parallel)
+
+        async def one(o: int):
+            async with sem:
+                return o, await self.probe_ordinal(o, kind=kind)
+
+        fresh = dict(await asyncio.gather(*(one(o) for o in failed)))
+        out = {}
+        stale = False
+        for o, r in fresh.items():
+            if r.ok:
+                stale = True
+                out[o] = r
+            else:
+                out[o] = ProbeOutcome(False, f"{r.reason} (server: {results[o].reason})", r.latency_ms, r.detail)
+        if stale:
+            self.server_restarts += 1
+            _log.warning("probe server failed ordinals %s that a fresh process found healthy; restarting it",
+                         sorted(o for o, r in fresh.items() if r.ok))
+            await self.close()
+        return out
+
     async def probe(self, ordinals: Mapping[str, int], kind: str = "probe") -> Dict[str, ProbeOutcome]:
         """device ID -> outcome; devices sharing an ordinal are probed once."""
         uniq = sorted(set(ordinals.values()))
@@ -262,6 +294,9 @@ class LivenessProber:
             try:
                 with TRACER.span("liveness.request", "health", ordinals=len(uniq), kind=kind):
                     results = await self._probe_server(uniq, kind)
+                failed = [o for o in uniq if not results[o].ok]
+                if failed:
+                    results.update(await self._confirm_failures(failed, results, kind))
                 self.sweeps += 1
                 return {dev: results[o] for dev, o in ordinals.items()}
             except (asyncio.TimeoutError, ProbeServerError, OSError) as e:

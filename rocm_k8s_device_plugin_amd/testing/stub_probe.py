@@ -5,7 +5,8 @@ Speaks the same CLI and JSON contract, one-shot and ``--serve``. Behaviour
 per ROCr ordinal comes from the JSON file named by $MI355X_STUB_PROBE_CONTROL
 (re-read on every request), e.g.
 ``{"0": "ok", "3": "fail", "5": "hang", "6": "stale", "7": "garbage"}``
-(missing ordinals are "ok"; "serve": "broken" makes --serve fail to start).
+(missing ordinals are "ok"; "serve": "broken" makes --serve fail to start;
+"server_fail" fails only inside --serve: a stale server runtime).
 Exercises the real LivenessProber code path: process spawn, server protocol,
 deadline kill, fallback to per-device isolation, output parsing, nonce check,
 hysteresis. Each start appends a line to $MI355X_STUB_PROBE_LOG if set.
@@ -70,6 +71,8 @@ def serve():
         for tok in parts[3:]:
             o, n = tok.split(":")
             mode = ctl.get(o, "ok")
+            if mode == "server_fail":
+                mode = "fail"
             if mode == "hang":
                 time.sleep(3600)
             if mode == "garbage":
@@ -95,6 +98,8 @@ def main(argv):
             nonce = int(argv[i + 1], 0)
     ordinal = os.environ.get("ROCR_VISIBLE_DEVICES", "0").split(",")[0]
     mode = _control().get(ordinal, "ok")
+    if mode == "server_fail":
+        mode = "ok"
     if mode == "hang":
         time.sleep(3600)
     if mode == "garbage":

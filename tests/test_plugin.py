@@ -501,13 +501,35 @@ def test_liveness_persistent_server_reused(tmp_path):
         for _ in range(3):
             res = await prober.probe(ords)
             assert {d for d, r in res.items() if not r.ok} == {"dev3"}
-            assert "differ" in res["dev3"].reason
+            assert "differ" in res["dev3"].reason and "(server: " in res["dev3"].reason
         assert prober.server_starts == 1 and prober.fallbacks == 0 and prober._server.requests == 3
         await prober.close()
         assert prober._server is None
 
     run(go())
-    assert log_path.read_text().split() == ["serve+keep"]
+    # each sweep's failure is confirmed by a fresh process for that device only
+    assert log_path.read_text().split() == ["serve+keep", "3", "3", "3"]
+
+
+def test_liveness_stale_server_failure_is_not_reported(tmp_path):
+    """A device the server fails but a fresh process finds healthy is Healthy, and the server is restarted."""
+    log_path = tmp_path / "starts.log"
+    ctl, prober = _stub_prober(tmp_path, {"4": "server_fail"})
+    prober.extra_env["MI355X_STUB_PROBE_LOG"] = str(log_path)
+    ords = {f"dev{i}": i for i in range(8)}
+
+    async def go():
+        res = await prober.probe(ords)
+        assert all(r.ok for r in res.values()), {d: r.reason for d, r in res.items() if not r.ok}
+        assert prober.server_restarts == 1 and prober._server is None
+        ctl.write_text("{}")                       # the fresh server is fine
+        res = await prober.probe(ords)
+        assert all(r.ok for r in res.values())
+        assert prober.server_starts == 2 and prober.server_restarts == 1
+        await prober.close()
+
+    run(go())
+    assert log_path.read_text().split() == ["serve+keep", "4", "serve+keep"]
 
 
 def test_liveness_keep_queues_flag_reaches_server(tmp_path):
