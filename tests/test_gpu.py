@@ -402,6 +402,33 @@ def test_rocprof_exactly_one_dispatch_per_probe(tmp_path, runtime):
     assert int(r["LDS_Block_Size"]) == 0 and int(r["Scratch_Size"]) == 0
 
 
+def test_rocprof_kept_queue_server_one_dispatch_per_sweep(tmp_path):
+    """--serve --keep under rocprofv3: K sweeps are exactly K liveness dispatches, no runtime blit/fill kernels."""
+    import csv
+    import shutil
+    if not shutil.which("rocprofv3"):
+        pytest.skip("rocprofv3 not available")
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    out = tmp_path / "prof"
+    sweeps = 16
+    reqs = "".join(f"probe 4 5.0 0:{1000 + i}\n" for i in range(sweeps)) + "quit\n"
+    env = dict(os.environ, TMPDIR="/tmp")
+    p = subprocess.run(["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", str(out), "-o", "serve",
+                        "--", str(probe_executable("hsa")), "--serve", "--keep"], input=reqs.encode(),
+                       capture_output=True, timeout=300, env=env, cwd="/tmp")
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    lines = [json.loads(l) for l in p.stdout.decode().splitlines() if l.startswith("{")]
+    replies = [d for d in lines if "devices" in d]
+    assert len(replies) == sweeps and all(d["ok"] for d in replies)
+    assert [d["devices"][0]["setup_us"] > 0 for d in replies] == [True] + [False] * (sweeps - 1)
+    traces = list(out.rglob("*kernel_trace.csv"))
+    assert traces, list(out.rglob("*"))
+    names = [r["Kernel_Name"] for r in csv.DictReader(open(traces[0]))]
+    assert names == ["mi355x_mfma_liveness"] * sweeps, names
+    os.makedirs("gpurun_out", exist_ok=True)
+    shutil.copy(traces[0], "gpurun_out/rocprof_kept_server_kernel_trace.csv")
+
+
 def test_real_box_matches_mi355x_model(inv):
     """The registry's MI355X numbers against the real part; consistent partitions."""
     from rocm_k8s_device_plugin_amd.models import MI355X, check_inventory, model_for
