@@ -60,6 +60,9 @@ def build_parser() -> flags.GoFlagParser:
                                     "gpu_pre_reset and its gpu_post_reset, other events are counted")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
+    p.add_float("topology_watch", 5.0, "seconds between checks for a GPU topology change (kfd generation, "
+                                       "partition modes); on a change the devices are re-discovered and "
+                                       "re-advertised (0 = off: devices fixed at start-up, as upstream)")
     p.add_bool("topology_view", False, "experimental: bind-mount a kfd topology filtered to the allocated "
                                        "GPUs into each container (faster ROCr start-up, GPU isolation)")
     p.add_bool("node_view", False, "experimental: bind-mount /sys/devices/system/node without the per-CPU cache "
@@ -158,7 +161,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         device_count = int(dc) if dc is not None else None
     impl = select_impl(ns, device_count, logger)
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
-                       metrics_port=ns.metrics_port)
+                       metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch)
     from ..utils.trace import TRACER
     TRACER.configure(ns.trace_file or None)
     try:

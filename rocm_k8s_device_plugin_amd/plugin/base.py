@@ -91,6 +91,11 @@ class DeviceImpl(abc.ABC):
     def health_version(self) -> int:
         return 0
 
+    async def reload_topology(self) -> Optional[dict]:
+        """Re-discover devices if the node's GPU topology changed; None if the
+        advertised devices are unchanged (see ContainerImpl.reload_topology)."""
+        return None
+
     async def close(self) -> None:
         """Release helper processes (e.g. the liveness probe server) at shutdown."""
 

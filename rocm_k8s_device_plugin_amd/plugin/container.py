@@ -10,7 +10,11 @@ failed, NUMA topology hints.
 
 Changed: per-device health (health.monitor), immutable device snapshots,
 deterministic device-node order, an error (not silently empty specs) for an
-unknown device ID, and a hive-aware exact allocator.
+unknown device ID, and a hive-aware exact allocator. New: the node is
+re-discovered when its GPU topology changes (``reload_topology``: a compute /
+memory partition switch done with amd-smi while the plugin runs); the
+reference computes its device list once at start-up and keeps advertising
+devices that no longer exist until it is restarted.
 """
 from __future__ import annotations
 
@@ -28,6 +32,9 @@ from ..utils import log
 from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto, driver_present
 
 _log = log.get("container")
+
+_HETERO_SINGLE = ("Partitions of different styles across GPUs in a node is not supported with single strategy. "
+                  "Please start device plugin with mixed strategy")
 
 
 class ContainerImpl(DeviceImpl):
@@ -51,15 +58,18 @@ class ContainerImpl(DeviceImpl):
                 _log.warning("node view unavailable: %s", e)
         if not driver_present(os.path.join(sysfs_root, C.KFD_CLASS_REL)):
             raise DeviceImplError("No amd gpu driver loaded")
+        self.device_count_limit = device_count_limit
+        self.health_cfg = health_cfg or HealthConfig()
+        self._epoch = 0            # bumped by every topology reload (part of health_version)
+        self._sig = self._signature()
+        self._pinned = inventory is not None
         self.inv = inventory or discover(sysfs_root, device_count_limit)
         for w in self.inv.warnings:
             _log.warning("%s", w)
         self.homogeneous = self.inv.homogeneous
         if not self.homogeneous and self.strategy == C.STRATEGY_SINGLE:
-            raise DeviceImplError(
-                "Partitions of different styles across GPUs in a node is not supported with single strategy. "
-                "Please start device plugin with mixed strategy")
-        self.monitor = monitor or HealthMonitor(self.inv, health_cfg or HealthConfig())
+            raise DeviceImplError(_HETERO_SINGLE)
+        self.monitor = monitor or HealthMonitor(self.inv, self.health_cfg)
         self._resources = self._compute_resource_names()
         self._members: Dict[str, List[Gpu]] = {r: self._devices_for(r) for r in self._resources}
         _log.info("Found %d AMDGPUs (%s)", len(self.inv), ", ".join(
@@ -124,7 +134,72 @@ class ContainerImpl(DeviceImpl):
         return await self.monitor.check_once()
 
     def health_version(self) -> int:
-        return self.monitor.version
+        # a reload replaces the monitor (its version restarts): the epoch keeps
+        # the combined value moving so every ListAndWatch stream re-sends
+        return self._epoch * 1_000_000_000 + self.monitor.version
+
+    # ---------------------------------------------------------------- topology reload
+    def _signature(self) -> tuple:
+        """Cheap fingerprint of the GPU topology: kfd's generation_id (bumped
+        by the driver when kfd nodes come or go) and every amdgpu PCI
+        function's current partition modes (~17 small reads on 8 GPUs)."""
+        def rd(path):
+            try:
+                with open(path) as f:
+                    return f.read().strip()
+            except OSError:
+                return None
+        root = self.sysfs_root
+        gen = rd(os.path.join(root, "class/kfd/kfd/topology/generation_id"))
+        drv = os.path.join(root, "module/amdgpu/drivers/pci:amdgpu")
+        try:
+            bdfs = sorted(e for e in os.listdir(drv) if ":" in e)
+        except OSError:
+            bdfs = []
+        parts = tuple((b, rd(os.path.join(drv, b, "current_compute_partition")),
+                       rd(os.path.join(drv, b, "current_memory_partition"))) for b in bdfs)
+        return gen, parts
+
+    async def reload_topology(self) -> Optional[dict]:
+        """Re-discover when the topology fingerprint changed.
+
+        Returns None when the advertised devices did not change, else
+        ``{"resources_changed": bool, "added": [...], "removed": [...],
+        "resources": [...]}``. RPC handlers see the old or the new snapshots,
+        never a mix (they are swapped in one step between awaits). The health
+        monitor is rebuilt: a probe server's GPU agents were enumerated at its
+        start and no longer match.
+        """
+        if self._pinned:  # the caller chose the devices (benchmarks, tests): keep them
+            return None
+        sig = self._signature()
+        if sig == self._sig:
+            return None
+        inv = discover(self.sysfs_root, self.device_count_limit)
+        self._sig = sig
+        old_ids, new_ids = set(self.inv.by_id), set(inv.by_id)
+        if old_ids == new_ids and all(self.inv.by_id[i].partition_type == inv.by_id[i].partition_type
+                                      for i in new_ids):
+            return None
+        for w in inv.warnings:
+            _log.warning("%s", w)
+        old_resources = list(self._resources)
+        monitor = HealthMonitor(inv, self.health_cfg)
+        await self.monitor.close()
+        self.inv, self.homogeneous, self.monitor = inv, inv.homogeneous, monitor
+        if not self.homogeneous and self.strategy == C.STRATEGY_SINGLE:
+            _log.error("GPU topology changed: %s. Advertising no devices until then.", _HETERO_SINGLE)
+            self._members = {r: [] for r in old_resources}
+        else:
+            self._resources = self._compute_resource_names()
+            self._members = {r: self._devices_for(r) for r in self._resources}
+        self._epoch += 1
+        _log.warning("GPU topology changed (kfd generation %s): %d devices (%s); resources %s -> %s",
+                     sig[0], len(inv), ", ".join(f"{r}={len(v)}" for r, v in self._members.items()),
+                     old_resources, self._resources)
+        return {"resources_changed": sorted(self._resources) != sorted(old_resources),
+                "added": sorted(new_ids - old_ids), "removed": sorted(old_ids - new_ids),
+                "resources": list(self._resources)}
 
     async def close(self) -> None:
         await self.monitor.close()

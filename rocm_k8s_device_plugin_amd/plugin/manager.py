@@ -18,7 +18,9 @@ behaviour:
 Re-designed: asyncio instead of goroutines; the kubelet socket is watched by
 inode polling (works on any filesystem, catches delete+recreate between
 polls); the heartbeat is a broadcast health sweep (one sweep per pulse for the
-whole node, every resource's ListAndWatch woken).
+whole node, every resource's ListAndWatch woken). New: a topology watch
+re-discovers the node when its GPU topology changes (partition switch) and
+starts / stops per-resource servers to match.
 """
 from __future__ import annotations
 
@@ -55,6 +57,7 @@ class ManagerConfig:
     send_every_pulse: bool = False
     metrics_port: int = 0
     handle_signals: bool = True
+    topology_watch_s: float = 5.0   # re-discovery check period (partition switches); 0 = off
 
 
 class ResourcePlugin:
@@ -160,6 +163,8 @@ class PluginManager:
         self.ready = asyncio.Event()
         self._tasks: List[asyncio.Task] = []
         self._metrics_server = None
+        self._impl_lock: Optional[asyncio.Lock] = None   # health sweep vs topology reload
+        self.topology_reloads = 0
 
     # ------------------------------------------------------------- control
     def request_stop(self) -> None:
@@ -183,7 +188,8 @@ class PluginManager:
                 pass
             t0 = time.perf_counter()
             try:
-                changed = await self.impl.refresh_health()
+                async with self._impl_lock:
+                    changed = await self.impl.refresh_health()
             except Exception as e:  # health must never take the plugin down
                 _log.error("health sweep failed: %s", e)
                 changed = False
@@ -192,6 +198,46 @@ class PluginManager:
             if changed:
                 REGISTRY.inc("mi355x_dp_health_changes_total")
             self.pulse.fire()
+
+    async def _topology_loop(self) -> None:
+        """Every topology_watch_s: has the node's GPU topology changed (e.g. an
+        amd-smi partition switch)? Then advertise what is there now."""
+        while not self.stopped.is_set():
+            try:
+                await asyncio.wait_for(self.stopped.wait(), self.cfg.topology_watch_s)
+                return
+            except asyncio.TimeoutError:
+                pass
+            try:
+                async with self._impl_lock:
+                    change = await self.impl.reload_topology()
+                if change:
+                    await self._apply_topology_change(change)
+            except Exception as e:  # never take the plugin down over a re-discovery
+                _log.error("topology reload failed: %s", e)
+
+    async def _apply_topology_change(self, change: dict) -> None:
+        """Plugins of vanished resources stop (kubelet drops the resource when
+        the stream ends); kept ones get their allocator re-initialised on the
+        new devices and re-send their list; new resources register."""
+        self.topology_reloads += 1
+        REGISTRY.inc("mi355x_dp_topology_reloads_total")
+        names = list(self.impl.resource_names())
+        for n in [n for n in self.plugins if n not in names]:
+            _log.warning("resource %s no longer exists: stopping its plugin server", n)
+            await self.plugins.pop(n).stop_server()
+        for n, p in self.plugins.items():
+            p.start()
+        new = [n for n in names if n not in self.plugins]
+        for n in new:
+            p = ResourcePlugin(self, n)
+            self.plugins[n] = p
+            p.start()
+        if new:
+            await asyncio.gather(*(self.plugins[n].start_server() for n in new if self.plugins[n].started))
+        log.info_fields(_log, "topology reloaded", resources=",".join(names), added=len(change.get("added", [])),
+                        removed=len(change.get("removed", [])))
+        self.pulse.fire()
 
     def _sock_id(self) -> Optional[Tuple[int, int, int]]:
         # inode numbers are recycled by delete+create; ctime tells them apart
@@ -247,8 +293,11 @@ class PluginManager:
             self.plugins[n] = p
             p.start()
         await self._start_all()
+        self._impl_lock = asyncio.Lock()
         if self.impl is not None and self.cfg.pulse_s > 0:
             self._tasks.append(asyncio.create_task(self._health_loop()))
+        if self.impl is not None and self.cfg.topology_watch_s > 0:
+            self._tasks.append(asyncio.create_task(self._topology_loop()))
         self._tasks.append(asyncio.create_task(self._watch_kubelet()))
         self.ready.set()
         await self.stopped.wait()

@@ -58,6 +58,7 @@ class FixtureSpec:
     vfs_per_gpu: int = 1                # SR-IOV VFs per PF (mode="vf")
     partition_support: bool = True      # write available_*_partition files
     per_gpu_compute: Optional[List[str]] = None  # heterogeneous nodes
+    generation: int = 1                 # kfd topology generation_id (bump to emulate a reconfiguration)
 
 
 @dataclass
@@ -117,7 +118,7 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
     (dev / "dri").mkdir(exist_ok=True)
     _w(dev / "kfd", "")
     if spec.mode == "container":
-        _w(sysfs / "class/kfd/kfd/topology/generation_id", "1")
+        _w(sysfs / "class/kfd/kfd/topology/generation_id", str(spec.generation))
 
     numa = max(1, spec.numa_nodes)
     # host NUMA/CPU sysfs (a few CPUs per node, each with cache descriptors)
