@@ -474,3 +474,15 @@ def test_collectives_cli_on_rccl():
     assert {r["op"] for r in rows} == {"all_reduce", "all_gather", "reduce_scatter", "all_to_all"}
     for r in rows:
         assert r["ok"] is True and r["ranks"] == 1 and r["dtype"] == "bfloat16"
+
+
+def test_topology_watch_signature_on_real_sysfs():
+    """The reload fingerprint reads on the real box (kfd generation_id + partition modes) and is stable."""
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+    from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+    impl = ContainerImpl("single", "/sys", HealthConfig(exporter_socket=None))
+    gen, parts = impl._signature()
+    assert gen is not None and gen.isdigit(), gen
+    assert parts and all(cp for _, cp, _ in parts), parts
+    assert asyncio.run(impl.reload_topology()) is None
+    asyncio.run(impl.close())
