@@ -292,6 +292,14 @@ class PluginManager:
             p = ResourcePlugin(self, n)
             self.plugins[n] = p
             p.start()
+        if self.impl is not None and self.cfg.pulse_s > 0 and names:
+            # one sweep before registering, so the first ListAndWatch already
+            # carries real verdicts (the reference advertises everything Healthy
+            # until its first pulse)
+            try:
+                await self.impl.refresh_health()
+            except Exception as e:
+                _log.error("initial health sweep failed: %s", e)
         await self._start_all()
         self._impl_lock = asyncio.Lock()
         if self.impl is not None and self.cfg.pulse_s > 0:

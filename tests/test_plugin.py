@@ -336,6 +336,24 @@ def test_liveness_through_listandwatch(tmp_path):
     run(go())
 
 
+def test_first_listandwatch_already_carries_health(tmp_path):
+    """With a pulse, one sweep runs before registration: a dead GPU is never advertised Healthy."""
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl, prober = _stub_prober(tmp_path, {"3": "fail"})
+    inv = discover(str(fi.sysfs))
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=1), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+    impl = ContainerImpl("single", str(fi.sysfs), inventory=inv, monitor=mon)
+
+    async def go():
+        async with plugin_env(tmp_path, impl, pulse=30) as (k, mgr):
+            st = await k.wait_for_resource("amd.com/gpu", 8)
+            assert st.updates == 1                                  # the initial list, no pulse yet
+            assert {d for d, h in st.devices.items() if h == "Unhealthy"} == {fi.bdfs[3]}
+
+    run(go())
+
+
 def test_kfd_node_loss_marks_device_unhealthy(tmp_path):
     fi = make_mi355x_node(tmp_path / "n")
     impl = container(fi)
