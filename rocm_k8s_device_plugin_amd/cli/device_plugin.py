@@ -60,6 +60,8 @@ def build_parser() -> flags.GoFlagParser:
                                     "gpu_pre_reset and its gpu_post_reset, other events are counted")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
+    p.add_bool("dry_run", False, "print what this node would advertise (implementation, resources, devices, "
+                                 "health after one sweep, preferred allocations per size) as JSON and exit")
     p.add_float("topology_watch", 5.0, "seconds between checks for a GPU topology change (kfd generation, "
                                        "partition modes); on a change the devices are re-discovered and "
                                        "re-advertised (0 = off: devices fixed at start-up, as upstream)")
@@ -142,6 +144,40 @@ def select_impl(ns, device_count: Optional[int], logger) -> Optional[DeviceImpl]
     return None
 
 
+async def dry_run_report(impl: Optional[DeviceImpl], sweep: bool) -> dict:
+    """What the plugin would tell kubelet on this node, without registering."""
+    from ..plugin.base import new_context
+    if impl is None:
+        return {"implementation": None, "resources": {}}
+    if sweep:
+        await impl.refresh_health()
+    out = {"implementation": impl.name, "resources": {}}
+    for r in impl.resource_names():
+        ctx = new_context(r)
+        impl.start(ctx)
+        devs = impl.enumerate(ctx)
+        ids = [d.ID for d in devs]
+        res = {"devices": [{"id": d.ID, "health": d.health, "numa": [n.ID for n in d.topology.nodes]}
+                           for d in devs],
+               "preferred_allocation": not ctx.allocator_error}
+        if not ctx.allocator_error and ids:
+            from ..parallel.fabric import Fabric
+            fab = Fabric(impl.inv) if hasattr(impl, "inv") else None
+            prefs = {}
+            for k in sorted({1, 2, 4, 8, len(ids)} & set(range(1, len(ids) + 1))):
+                chosen = ctx.allocator.allocate(ids, [], k)
+                prefs[str(k)] = {"ids": chosen}
+                if fab is not None:
+                    rep = fab.report(chosen)
+                    prefs[str(k)].update(one_hive=rep.one_hive, allreduce_bound_gbs=rep.allreduce_bound_gbs)
+            res["allocations"] = prefs
+        out["resources"][f"{C.RESOURCE_NAMESPACE}/{r}"] = res
+    if hasattr(impl, "inv"):
+        out["warnings"] = list(impl.inv.warnings)
+    await impl.close()
+    return out
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     p = build_parser()
     ns = p.parse_args(argv)
@@ -160,6 +196,10 @@ def main(argv: Optional[List[str]] = None) -> int:
         dc = (cfg.get("gpu") or {}).get("device_count")
         device_count = int(dc) if dc is not None else None
     impl = select_impl(ns, device_count, logger)
+    if ns.dry_run:
+        import json
+        print(json.dumps(asyncio.run(dry_run_report(impl, sweep=ns.pulse > 0)), indent=1))
+        return 0
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
                        metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch)
     from ..utils.trace import TRACER

@@ -779,3 +779,22 @@ def test_chip_sweep_runs_on_idle_gpus_only(tmp_path):
     assert kinds == [("sweep", idle), ("probe", [busy_dev.id]), ("probe", everyone),
                      ("sweep", idle), ("probe", [busy_dev.id])]
     assert mon.chip_sweeps == 2
+
+
+def test_cli_dry_run_reports_node(tmp_path):
+    """-dry_run: implementation, resources, devices and preferred allocations as JSON, no registration."""
+    import subprocess
+    fi = make_mi355x_node(tmp_path / "n", hive_size=4)
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    p = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.device_plugin", "-dry_run",
+                        "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket", "",
+                        "-kubelet_dir", str(tmp_path / "dp")], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    doc = json.loads(p.stdout)
+    assert doc["implementation"] == "container" and list(doc["resources"]) == ["amd.com/gpu"]
+    r = doc["resources"]["amd.com/gpu"]
+    assert [d["id"] for d in r["devices"]] == fi.bdfs and r["preferred_allocation"]
+    four = r["allocations"]["4"]
+    assert four["one_hive"] and four["allreduce_bound_gbs"] > 0     # a whole hive of 4
+    assert not r["allocations"]["8"]["one_hive"]                    # 8 spans both hives
+    assert not os.path.exists(tmp_path / "dp" / "amd.com_gpu")      # nothing served
