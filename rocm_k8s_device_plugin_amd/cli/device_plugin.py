@@ -69,6 +69,12 @@ def build_parser() -> flags.GoFlagParser:
                                        "GPUs into each container (faster ROCr start-up, GPU isolation)")
     p.add_bool("node_view", False, "experimental: bind-mount /sys/devices/system/node without the per-CPU cache "
                                    "descriptors ROCr walks at start-up (3x faster hsa_init on 256-CPU hosts)")
+    p.add_str("device_list_strategy", "device-specs", "what Allocate returns: device-specs (the /dev nodes, as "
+                                                       "upstream), cdi-cri (CDI device names, the runtime applies "
+                                                       "the specs in -cdi_spec_dir), cdi-annotations; comma-separated "
+                                                       "to combine")
+    p.add_str("cdi_spec_dir", "/var/run/cdi", "where the CDI specs of the advertised devices are written "
+                                              "(cdi-* device list strategies)")
     p.add_str("log_format", "glog", "glog | json")
     p.add_str("trace_file", "", "write a Chrome trace of RPC / allocator / health spans to this file on exit")
     p.add_str("config", os.environ.get("CONFIG_FILE_PATH", ""), "YAML config file (gpu.device_count, ...)")
@@ -89,6 +95,11 @@ def validate(ns) -> Optional[str]:
     if ns.resource_naming_strategy not in (C.STRATEGY_SINGLE, C.STRATEGY_MIXED):
         return (f"invalid resource_naming_strategy provided: {ns.resource_naming_strategy}, supported values "
                 "are single or mixed")
+    try:
+        from .. import cdi
+        cdi.parse_strategies(ns.device_list_strategy)
+    except ValueError as e:
+        return str(e)
     if ns.liveness_mode not in ("persistent", "spawn"):
         return f"invalid liveness_mode provided: {ns.liveness_mode}, supported values are persistent or spawn"
     return None
@@ -112,8 +123,11 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
                           liveness_keep_queues=ns.liveness_keep_queues)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
+        from .. import cdi
         return ContainerImpl(ns.resource_naming_strategy, ns.sysfs_root, hc, device_count,
-                             topology_view_dir=view_dir, node_view_dir=node_dir)
+                             topology_view_dir=view_dir, node_view_dir=node_dir,
+                             device_list_strategy=cdi.parse_strategies(ns.device_list_strategy),
+                             cdi_spec_dir=ns.cdi_spec_dir)
     if name == C.VF_PASSTHROUGH:
         from ..plugin.passthrough import VfImpl
         return VfImpl(ns.resource_naming_strategy, ns.sysfs_root, ns.exporter_socket or None)

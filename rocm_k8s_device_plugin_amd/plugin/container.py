@@ -19,8 +19,9 @@ devices that no longer exist until it is restarted.
 from __future__ import annotations
 
 import os
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
+from .. import cdi
 from .. import constants as C
 from ..allocator import AllocationError
 from ..health.monitor import HealthConfig, HealthMonitor
@@ -43,8 +44,13 @@ class ContainerImpl(DeviceImpl):
     def __init__(self, naming_strategy: str = C.STRATEGY_SINGLE, sysfs_root: str = "/sys",
                  health_cfg: Optional[HealthConfig] = None, device_count_limit: Optional[int] = None,
                  inventory: Optional[Inventory] = None, monitor: Optional[HealthMonitor] = None,
-                 topology_view_dir: Optional[str] = None, node_view_dir: Optional[str] = None):
+                 topology_view_dir: Optional[str] = None, node_view_dir: Optional[str] = None,
+                 device_list_strategy: Sequence[str] = (cdi.DEVICE_SPECS,), cdi_spec_dir: str = cdi.DEFAULT_SPEC_DIR):
         self.strategy = naming_strategy
+        # what Allocate returns: DeviceSpecs (reference) and/or CDI device names
+        self.list_strategies = tuple(device_list_strategy) or (cdi.DEVICE_SPECS,)
+        self.cdi_spec_dir = cdi_spec_dir
+        self._cdi = any(s != cdi.DEVICE_SPECS for s in self.list_strategies)
         self.sysfs_root = sysfs_root
         # opt-in: per-allocation filtered kfd topology bind-mounted into the container
         self.topology_views = (TopologyViews(topology_view_dir, os.path.join(sysfs_root, "class/kfd/kfd/topology"))
@@ -74,6 +80,14 @@ class ContainerImpl(DeviceImpl):
         self._members: Dict[str, List[Gpu]] = {r: self._devices_for(r) for r in self._resources}
         _log.info("Found %d AMDGPUs (%s)", len(self.inv), ", ".join(
             f"{r}={len(v)}" for r, v in self._members.items()))
+        if self._cdi:
+            self._write_cdi_specs()
+
+    def _write_cdi_specs(self, stale=()) -> None:
+        # before registration: kubelet may hand a CDI name to the runtime as
+        # soon as the first Allocate returns, the spec must already be there
+        paths = cdi.write_specs(self.cdi_spec_dir, self._members, stale)
+        _log.info("CDI specs written: %s", ", ".join(paths))
 
     # ------------------------------------------------------------- resources
     def _compute_resource_names(self) -> List[str]:
@@ -194,6 +208,11 @@ class ContainerImpl(DeviceImpl):
             self._resources = self._compute_resource_names()
             self._members = {r: self._devices_for(r) for r in self._resources}
         self._epoch += 1
+        if self._cdi:
+            try:
+                self._write_cdi_specs(stale=old_resources)
+            except (OSError, ValueError) as e:
+                _log.error("CDI specs not updated after the topology change: %s", e)
         _log.warning("GPU topology changed (kfd generation %s): %d devices (%s); resources %s -> %s",
                      sig[0], len(inv), ", ".join(f"{r}={len(v)}" for r, v in self._members.items()),
                      old_resources, self._resources)
@@ -207,18 +226,28 @@ class ContainerImpl(DeviceImpl):
     # ---------------------------------------------------------------- allocation
     def allocate(self, ctx: PluginContext, req: pb.AllocateRequest) -> pb.AllocateResponse:
         resp = pb.AllocateResponse()
+        specs = cdi.DEVICE_SPECS in self.list_strategies
         for creq in req.container_requests:
             car = resp.container_responses.add()
             # one /dev/kfd per container regardless of the number of GPUs
-            car.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
+            if specs:
+                car.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
             nodes = []
             for dev_id in creq.devices_ids:
                 d = self.inv.by_id.get(dev_id)
                 if d is None:
                     raise DeviceImplError(f"unknown device ID {dev_id!r} for resource {ctx.resource}")
-                for p in d.dev_paths():
-                    car.devices.add(container_path=p, host_path=p, permissions="rw")
+                if specs:
+                    for p in d.dev_paths():
+                        car.devices.add(container_path=p, host_path=p, permissions="rw")
                 nodes.append(d.node_id)
+            if self._cdi and creq.devices_ids:
+                ids = list(creq.devices_ids)
+                if cdi.CDI_CRI in self.list_strategies:
+                    for i in ids:
+                        car.cdi_devices.add(name=cdi.qualified_name(ctx.resource, i))
+                if cdi.CDI_ANNOTATIONS in self.list_strategies:
+                    car.annotations[cdi.annotation_key(ctx.resource)] = cdi.annotation_value(ctx.resource, ids)
             if self.topology_views is not None and creq.devices_ids and all(n >= 0 for n in nodes):
                 try:
                     view = self.topology_views.get(nodes)
