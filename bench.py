@@ -8,8 +8,10 @@ GPUs advertised at 1/2/4/8 MI355X"). One timed step is one pod admission:
      the real device plugin over UDS gRPC: GetPreferredAllocation for a pod
      requesting amd.com/gpu=N out of the N advertised devices, then Allocate;
   2. the DeviceSpecs in the Allocate response are turned into a "container":
-     one fresh process (rank 0) restricted to the allocated render nodes via
-     ROCR_VISIBLE_DEVICES (--container-mode pod, what kubelet starts for a
+     one fresh process (rank 0) whose /dev/dri holds exactly the allocated
+     nodes (--dev-view specs: opens of any other render node fail as in a
+     container, so ROCr initialises only the pod's GPUs; container_runtime.py)
+     (--container-mode pod, what kubelet starts for a
      pod), or one process per allocated GPU, one per rank, like a torchrun
      workload inside the pod would start (--container-mode per-gpu; reported
      as a comparison at N > 1);
@@ -74,6 +76,12 @@ def parse_args():
     ap.add_argument("--node-view-compare", type=int, default=5,
                     help="extra untimed admissions with the plugin's -node_view mounts applied to the containers "
                          "(by path redirection: no root for bind mounts), reported for comparison")
+    ap.add_argument("--dev-view", default="specs", choices=["specs", "visible-devices"],
+                    help="container GPU visibility: specs = the container's /dev holds exactly the Allocate "
+                         "DeviceSpecs (ROCr skips the other GPUs' render nodes, as in a real container); "
+                         "visible-devices = every host GPU openable, restricted with ROCR_VISIBLE_DEVICES")
+    ap.add_argument("--visibility-compare", type=int, default=5,
+                    help="extra untimed admissions with the other --dev-view, reported for comparison")
     ap.add_argument("--b2b-compare", type=int, default=5,
                     help="extra untimed admissions with --settle none, reported for comparison")
     ap.add_argument("--peer-check", type=int, default=1,
@@ -198,6 +206,7 @@ def main():
         inv = Inventory(sysfs_root=sysfs, devices=adv, topology=full.topology, driver_loaded=full.driver_loaded,
                         kfd_present=full.kfd_present)
         minor_to_ord = {dv.render_minor: ords[dv.id] for dv in adv}
+        minor_to_paths = {dv.render_minor: dv.dev_paths() for dv in adv}
         adv_ordinals = [ords[dv.id] for dv in adv]
         impl = ContainerImpl("single", sysfs, HealthConfig(exporter_socket=None), inventory=inv)
         pdir = os.path.join(tmp, "device-plugins")
@@ -218,18 +227,22 @@ def main():
     from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
 
     def one_step(record: bool, runtime: str = args.container_runtime, sink=None, settle: str = args.settle,
-                 init_sink=None, mode: str = args.container_mode):
+                 init_sink=None, mode: str = args.container_mode, dev_view: str = args.dev_view):
         if d.rank == 0:
             t0 = time.monotonic_ns()
             adm = loop.run_until_complete(kubelet.admit("amd.com/gpu", n))
-            minors = render_minors_from_specs(adm.response.container_responses[0])
+            car = adm.response.container_responses[0]
+            minors = render_minors_from_specs(car)
             ordl = [minor_to_ord[m] for m in minors]
-            mounts = [(m.container_path, m.host_path) for m in adm.response.container_responses[0].mounts]
-            payload = (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids), mounts)
+            mounts = [(m.container_path, m.host_path) for m in car.mounts]
+            # the container's /dev: the DeviceSpecs, per allocated GPU (card + render node)
+            spec_paths = {ds.host_path for ds in car.devices}
+            groups = [[p for p in minor_to_paths[m] if p in spec_paths] for m in minors]
+            payload = (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids), mounts, groups)
         else:
             payload = None
         payload = d.bcast(payload)
-        t0, ordl, tot, amsl, ids, mounts = payload
+        t0, ordl, tot, amsl, ids, mounts, groups = payload
         if args.fixture:
             import subprocess
             ts = time.monotonic_ns()
@@ -242,8 +255,13 @@ def main():
             mine = (True, 0, 0.0, "", (0, 0, 0))
             lingering = frozenset()
         else:
-            mine_ord = ordl if mode == "pod" or d.world == 1 else [ordl[d.rank]]
-            r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime, mounts=mounts)
+            pod = mode == "pod" or d.world == 1
+            mine_ord = ordl if pod else [ordl[d.rank]]
+            paths = None
+            if dev_view == "specs":
+                paths = ["/dev/kfd"] + [p for g in (groups if pod else [groups[d.rank]]) for p in g]
+            r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime, mounts=mounts,
+                                device_paths=paths)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
             phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
@@ -305,6 +323,11 @@ def main():
             one_step(False, sink=nv_lat, init_sink=nv_init)
         if d.rank == 0:
             impl.node_view = None
+    vis_lat = []
+    other_view = "visible-devices" if args.dev_view == "specs" else "specs"
+    if not args.fixture and args.container_runtime == "hsa":
+        for _ in range(args.visibility_compare):
+            one_step(False, sink=vis_lat, dev_view=other_view)
     if not args.fixture and args.container_runtime == "hsa":
         for _ in range(args.hip_compare):
             one_step(False, runtime="hip", sink=hip_lat)
@@ -364,6 +387,8 @@ def main():
                  "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
                  "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
                  "container_mode": args.container_mode,
+                 "container_dev_view": args.dev_view,
+                 f"latency_p50_ms_dev_view_{other_view}": round(pct(vis_lat, .5), 3) if vis_lat else None,
                  f"latency_p50_ms_container_mode_{other_mode}": round(pct(other_mode_lat, .5), 3) if other_mode_lat
                  else None,
                  "latency_p50_ms_node_view_emulated": round(pct(nv_lat, .5), 3) if nv_lat else None,
@@ -398,7 +423,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": ("synthetic pod specs requesting amd.com/gpu=N; real /sys discovery, fake kubelet over UDS, "
-                     "container = fresh process restricted to its render node running the MFMA liveness kernel"
+                     "container = fresh process whose /dev is the Allocate DeviceSpecs running the MFMA liveness kernel"
                      if not args.fixture else "synthetic 8xMI355X sysfs fixture; no-op containers (CPU only)"),
             "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
                        "global_batch": n, "seq_len": None,

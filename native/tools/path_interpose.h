@@ -8,6 +8,13 @@
 // $MI355X_INITPROF_HIDE (colon separated, 'N' stands for a digit run), refused with ENOENT — an in-process
 // stand-in for a container view that lacks those files (bind mounts need root).
 //
+// $MI355X_DEV_ALLOW (';'-separated exact paths) emulates the container's /dev
+// as the Allocate DeviceSpecs build it: under /dev/dri/ only the listed nodes
+// exist, every other open there fails with ENOENT — so ROCr's thunk skips the
+// GPUs the pod was not given, as it does for render nodes a container lacks.
+// $MI355X_INITPROF_COUNT=0 turns the per-path counting off (no lock, no map:
+// the container entrypoint build pays two string compares per open).
+//
 // Include in exactly ONE translation unit of an executable linked with
 // -rdynamic; call path_interpose_configure() at the top of main().
 #include <dirent.h>
@@ -35,6 +42,8 @@ std::vector<std::string>* g_hide = nullptr;
 // $MI355X_INITPROF_REDIRECT="<from>=<to>[;<from>=<to>...]": path prefix rewrites
 std::vector<std::pair<std::string, std::string>>* g_redir = nullptr;
 std::atomic<long> g_redirected{0};
+std::vector<std::string>* g_dev_allow = nullptr;   // $MI355X_DEV_ALLOW
+bool g_count = true;                               // $MI355X_INITPROF_COUNT != 0
 thread_local std::string t_path;
 std::atomic<long> g_hidden{0};
 thread_local bool t_in_hook = false;
@@ -66,15 +75,27 @@ const char* map_path(const char* path) {
 }
 
 // true -> refuse this path
+bool dev_hidden(const char* path) {
+  if (!g_dev_allow || std::strncmp(path, "/dev/dri/", 9) != 0) return false;
+  for (const auto& a : *g_dev_allow)
+    if (a == path) return false;
+  return true;
+}
+
 bool note(const char* path) {
   if (!path || t_in_hook) return false;
+  if (dev_hidden(path)) {
+    g_hidden.fetch_add(1);
+    return true;
+  }
+  if (!g_count && !g_hide) return false;
   t_in_hook = true;
   bool hide = false;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_counts) g_counts = new std::map<std::string, long>();
     const std::string f = fold(path);
-    ++(*g_counts)[f];
+    if (g_count) ++(*g_counts)[f];
     if (g_hide)  // prefixes are matched against the folded path ('N' = any digits)
       for (const auto& h : *g_hide)
         if (!h.empty() && f.compare(0, h.size(), h) == 0) hide = true;
@@ -184,6 +205,18 @@ inline void path_interpose_configure() {
       pos = c + 1;
     }
   }
+  if (const char* a = std::getenv("MI355X_DEV_ALLOW")) {
+    g_dev_allow = new std::vector<std::string>();
+    std::string s = a;
+    size_t pos = 0;
+    while (pos < s.size()) {
+      size_t c = s.find(';', pos);
+      if (c == std::string::npos) c = s.size();
+      if (c > pos) g_dev_allow->push_back(s.substr(pos, c - pos));
+      pos = c + 1;
+    }
+  }
+  if (const char* c = std::getenv("MI355X_INITPROF_COUNT")) g_count = std::strcmp(c, "0") != 0;
   if (const char* r = std::getenv("MI355X_INITPROF_REDIRECT")) {
     g_redir = new std::vector<std::pair<std::string, std::string>>();
     std::string s = r;

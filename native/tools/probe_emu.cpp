@@ -1,7 +1,10 @@
-// Measurement build of the liveness probe: probe_main + the HSA-direct path
-// with path interposition, so the whole container entrypoint (ROCr init, code
-// object, queue, MFMA dispatch, verify) can run against an emulated container
-// sysfs view (MI355X_INITPROF_REDIRECT, see path_interpose.h). Not shipped.
+// Container-entrypoint build of the liveness probe for the fake CRI runtime
+// (container_runtime.py): probe_main + the HSA-direct path with path
+// interposition, so the whole entrypoint (ROCr init, code object, queue, MFMA
+// dispatch, verify) runs against the container's view without root: its /dev
+// as the Allocate DeviceSpecs build it (MI355X_DEV_ALLOW) and the Allocate
+// mounts (MI355X_INITPROF_REDIRECT), see path_interpose.h. Not shipped in the
+// plugin image.
 #include "path_interpose.h"
 
 namespace {

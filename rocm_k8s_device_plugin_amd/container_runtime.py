@@ -5,9 +5,21 @@ the container with the returned DeviceSpecs -> ROCr in the container sees
 exactly the injected render nodes -> the app starts. We cannot create real
 containers here, so the runtime step is emulated faithfully where it matters
 for latency: a fresh process is started whose GPU visibility is restricted to
-the allocated devices (``ROCR_VISIBLE_DEVICES`` = the ROCr ordinals of the
-render nodes in the DeviceSpecs), and "ready" is the moment that process has
-initialised HIP and executed the MFMA liveness kernel on its device(s).
+the allocated devices, and "ready" is the moment that process has
+initialised the GPU runtime and executed the MFMA liveness kernel on its
+device(s).
+
+Visibility: a real container's /dev holds exactly the DeviceSpecs (``/dev/kfd``
+and each allocated GPU's card / render node), and ROCr's thunk skips every
+GPU whose render node it cannot open. Given the specs (``device_paths``), the
+HSA entrypoint runs in its path-interposing build with the same view: opens
+under ``/dev/dri/`` outside the specs fail with ENOENT (native/tools/
+path_interpose.h, ``MI355X_DEV_ALLOW``), so ROCr initialises only the pod's
+GPUs, numbered 0..N-1 as inside the container. Without the specs (or with
+the HIP entrypoint) the process sees every GPU the host lets it open and is
+restricted with ``ROCR_VISIBLE_DEVICES`` = the host ROCr ordinals instead —
+on a node whose GPUs are all accessible that still initialises (and later
+tears down) a VM on every GPU, which a container never does.
 """
 from __future__ import annotations
 
@@ -97,18 +109,30 @@ def mount_redirects(mounts: Iterable) -> str:
 
 
 def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int = 4,
-                    exe: Optional[str] = None, runtime: str = "hsa", mounts: Iterable = ()) -> ContainerResult:
+                    exe: Optional[str] = None, runtime: str = "hsa", mounts: Iterable = (),
+                    device_paths: Optional[Sequence[str]] = None) -> ContainerResult:
     """Run the container entrypoint restricted to `ordinals`; block until ready/exit.
 
     runtime "hsa": the entrypoint launches the MFMA kernel straight through ROCr
     (one AQL dispatch); "hip": the same kernel through the HIP runtime, i.e. what a
     typical HIP/PyTorch application pays before its first kernel.
+    device_paths: the container's device nodes from the Allocate DeviceSpecs;
+    with "hsa" the process then sees only those GPUs (module docstring).
     """
     env = {k: v for k, v in os.environ.items() if k not in _VISIBILITY_VARS}
-    env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
+    dev_view = device_paths is not None and runtime == "hsa"
+    if dev_view:
+        dri = [p for p in device_paths if p.startswith("/dev/dri/")]
+        if not dri:
+            raise ValueError("device_paths name no /dev/dri node")
+        env["MI355X_DEV_ALLOW"] = ";".join(dri)
+        env["MI355X_INITPROF_COUNT"] = "0"
+        runtime = "mountemu"
+    else:
+        env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
     redirect = mount_redirects(mounts)
     if redirect:
-        if runtime != "hsa":
+        if runtime not in ("hsa", "mountemu"):
             raise ValueError("mounts can only be applied to the HSA entrypoint (mount emulation build)")
         runtime = "mountemu"
         env["MI355X_INITPROF_REDIRECT"] = redirect
@@ -127,6 +151,9 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
         return ContainerResult(False, t0, 0, wall, {}, f"bad output rc={p.returncode}: {p.stderr.decode()[-300:]}")
     ok = p.returncode == 0 and bool(doc.get("ok"))
     err = "" if ok else "; ".join(d.get("error", "") for d in doc.get("devices", [])) or doc.get("error", "")
+    if ok and dev_view and doc.get("hip_device_count") != len(ordinals):
+        ok, err = False, (f"container /dev view: ROCr saw {doc.get('hip_device_count')} GPUs, "
+                          f"the pod was given {len(ordinals)}")
     return ContainerResult(ok, t0, int(doc.get("t_ready_ns", 0)), wall, doc, err,
                            frozenset(kfd_processes() - before))
 

@@ -262,6 +262,27 @@ def test_container_with_node_view_mounts(tmp_path, ordinals):
     assert init(viewed) < init(plain), (init(viewed), init(plain))
 
 
+def test_container_dev_view_hides_unallocated_gpus(inv, ordinals):
+    """The fake runtime's /dev view is what ROCr sees: with the GPU's render node
+    in the DeviceSpecs the container runs on it; with a render node that is not
+    this GPU's, ROCr's thunk finds no GPU at all (ENOENT, as in a container
+    without the node) and the container does not become ready."""
+    from rocm_k8s_device_plugin_amd.container_runtime import start_container, wait_kfd_released
+    dev_id, o = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
+    g = inv.by_id[dev_id]
+    ok = start_container([o], timeout_s=120, device_paths=["/dev/kfd"] + g.dev_paths())
+    assert ok.ok, ok.error
+    assert ok.doc["hip_device_count"] == 1
+    assert ok.doc["devices"][0]["pci_bus_id"].lower() == dev_id.lower()
+    wait_kfd_released(ok.kfd_lingering)
+    other = [d for d in inv.devices if d.render_minor >= 0 and d.render_minor != g.render_minor]
+    wrong = ["/dev/kfd"] + (other[0].dev_paths() if other else ["/dev/dri/renderD1"])
+    bad = start_container([o], timeout_s=120, device_paths=wrong)
+    wait_kfd_released(bad.kfd_lingering)
+    assert not bad.ok
+    assert bad.doc.get("hip_device_count", 0) == 0, bad.doc
+
+
 def test_chip_sweep_covers_every_cu_and_xcd(ordinals):
     """Full-chip sweep: one workgroup per CU, all resident together, every XCD runs
     and every MFMA tile / LDS word is exact (one-shot and through the server)."""
@@ -359,11 +380,15 @@ def test_end_to_end_admission_container_ready(inv, ordinals):
         try:
             await k.wait_for_resource("amd.com/gpu", len(acc), timeout=30)
             adm = await k.admit("amd.com/gpu", 1)
-            minors = render_minors_from_specs(adm.response.container_responses[0])
+            car = adm.response.container_responses[0]
+            minors = render_minors_from_specs(car)
             m2o = {acc.by_id[i].render_minor: o for i, o in ordinals.items()}
-            r = start_container([m2o[m] for m in minors])
+            # the container's /dev holds exactly the DeviceSpecs: ROCr sees the pod's GPU only
+            r = start_container([m2o[m] for m in minors], device_paths=[ds.host_path for ds in car.devices])
             assert r.ok, r.error
             assert r.t_ready_ns > r.t_start_ns
+            assert r.doc["hip_device_count"] == 1
+            assert r.doc["devices"][0]["pci_bus_id"].lower() == adm.device_ids[0].lower()
             # the health loop (with liveness) must keep every device Healthy
             st = k.resources["amd.com/gpu"]
             assert all(h == "Healthy" for h in st.devices.values())
