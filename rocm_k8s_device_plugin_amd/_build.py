@@ -30,6 +30,7 @@ HIP_SO = PKG_DIR / f"_hip{EXT_SUFFIX}"
 PROBE_EXE = PKG_DIR / "bin" / "mi355x-liveness-probe"
 PROBE_EXE_HIP = PKG_DIR / "bin" / "mi355x-liveness-probe-hip"
 MOUNTEMU_EXE = PKG_DIR / "bin" / "mi355x-probe-mountemu"
+HIP_DEVEMU_EXE = PKG_DIR / "bin" / "mi355x-probe-hip-devemu"
 HSACO = PKG_DIR / "kernels" / "liveness_gfx950.hsaco"
 
 
@@ -113,7 +114,7 @@ def ensure_built(hip: bool | None = None) -> None:
         hip = hipcc_available()
     if hip in _checked:
         return
-    targets = [NATIVE_SO] + ([HIP_SO, PROBE_EXE, PROBE_EXE_HIP, MOUNTEMU_EXE, HSACO] if hip else [])
+    targets = [NATIVE_SO] + ([HIP_SO, PROBE_EXE, PROBE_EXE_HIP, MOUNTEMU_EXE, HIP_DEVEMU_EXE, HSACO] if hip else [])
     if not _up_to_date(targets):
         BUILD_DIR.mkdir(parents=True, exist_ok=True)
         with open(BUILD_DIR.parent / ".build.lock", "w") as lk:

@@ -15,8 +15,8 @@ GPU whose render node it cannot open. Given the specs (``device_paths``), the
 HSA entrypoint runs in its path-interposing build with the same view: opens
 under ``/dev/dri/`` outside the specs fail with ENOENT (native/tools/
 path_interpose.h, ``MI355X_DEV_ALLOW``), so ROCr initialises only the pod's
-GPUs, numbered 0..N-1 as inside the container. Without the specs (or with
-the HIP entrypoint) the process sees every GPU the host lets it open and is
+GPUs, numbered 0..N-1 as inside the container (the HIP entrypoint has the
+same build). Without the specs the process sees every GPU the host lets it open and is
 restricted with ``ROCR_VISIBLE_DEVICES`` = the host ROCr ordinals instead —
 on a node whose GPUs are all accessible that still initialises (and later
 tears down) a VM on every GPU, which a container never does.
@@ -117,17 +117,17 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
     (one AQL dispatch); "hip": the same kernel through the HIP runtime, i.e. what a
     typical HIP/PyTorch application pays before its first kernel.
     device_paths: the container's device nodes from the Allocate DeviceSpecs;
-    with "hsa" the process then sees only those GPUs (module docstring).
+    the process then sees only those GPUs (module docstring).
     """
     env = {k: v for k, v in os.environ.items() if k not in _VISIBILITY_VARS}
-    dev_view = device_paths is not None and runtime == "hsa"
+    dev_view = device_paths is not None and runtime in ("hsa", "hip")
     if dev_view:
         dri = [p for p in device_paths if p.startswith("/dev/dri/")]
         if not dri:
             raise ValueError("device_paths name no /dev/dri node")
         env["MI355X_DEV_ALLOW"] = ";".join(dri)
         env["MI355X_INITPROF_COUNT"] = "0"
-        runtime = "mountemu"
+        runtime = "mountemu" if runtime == "hsa" else "hip-devemu"
     else:
         env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
     redirect = mount_redirects(mounts)

@@ -22,6 +22,7 @@ PKG_DIR = Path(__file__).resolve().parent.parent
 PROBE_EXE = PKG_DIR / "bin" / "mi355x-liveness-probe"
 PROBE_EXE_HIP = PKG_DIR / "bin" / "mi355x-liveness-probe-hip"
 MOUNTEMU_EXE = PKG_DIR / "bin" / "mi355x-probe-mountemu"
+HIP_DEVEMU_EXE = PKG_DIR / "bin" / "mi355x-probe-hip-devemu"
 HSACO = PKG_DIR / "kernels" / "liveness_gfx950.hsaco"
 
 
@@ -64,10 +65,11 @@ def hip():
 
 
 def probe_executable(runtime: str = "hsa") -> Path:
-    """The liveness probe: "hsa" (ROCr-direct, default), "hip", or "mountemu" (the
-    HSA probe built with path interposition, used by the fake container runtime
-    to apply Allocate mounts without root)."""
-    exe = {"hsa": PROBE_EXE, "hip": PROBE_EXE_HIP, "mountemu": MOUNTEMU_EXE}[runtime]
+    """The liveness probe: "hsa" (ROCr-direct, default), "hip", or the container
+    entrypoint builds with path interposition that the fake container runtime
+    uses to give a process the container's view without root (its /dev and the
+    Allocate mounts): "mountemu" (HSA) and "hip-devemu" (HIP runtime)."""
+    exe = {"hsa": PROBE_EXE, "hip": PROBE_EXE_HIP, "mountemu": MOUNTEMU_EXE, "hip-devemu": HIP_DEVEMU_EXE}[runtime]
     if _auto_build_allowed():
         from .. import _build
         _build.ensure_built(hip=True)

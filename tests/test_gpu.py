@@ -262,7 +262,8 @@ def test_container_with_node_view_mounts(tmp_path, ordinals):
     assert init(viewed) < init(plain), (init(viewed), init(plain))
 
 
-def test_container_dev_view_hides_unallocated_gpus(inv, ordinals):
+@pytest.mark.parametrize("runtime", ["hsa", "hip"])
+def test_container_dev_view_hides_unallocated_gpus(inv, ordinals, runtime):
     """The fake runtime's /dev view is what ROCr sees: with the GPU's render node
     in the DeviceSpecs the container runs on it; with a render node that is not
     this GPU's, ROCr's thunk finds no GPU at all (ENOENT, as in a container
@@ -270,14 +271,14 @@ def test_container_dev_view_hides_unallocated_gpus(inv, ordinals):
     from rocm_k8s_device_plugin_amd.container_runtime import start_container, wait_kfd_released
     dev_id, o = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
     g = inv.by_id[dev_id]
-    ok = start_container([o], timeout_s=120, device_paths=["/dev/kfd"] + g.dev_paths())
+    ok = start_container([o], timeout_s=120, device_paths=["/dev/kfd"] + g.dev_paths(), runtime=runtime)
     assert ok.ok, ok.error
     assert ok.doc["hip_device_count"] == 1
     assert ok.doc["devices"][0]["pci_bus_id"].lower() == dev_id.lower()
     wait_kfd_released(ok.kfd_lingering)
     other = [d for d in inv.devices if d.render_minor >= 0 and d.render_minor != g.render_minor]
     wrong = ["/dev/kfd"] + (other[0].dev_paths() if other else ["/dev/dri/renderD1"])
-    bad = start_container([o], timeout_s=120, device_paths=wrong)
+    bad = start_container([o], timeout_s=120, device_paths=wrong, runtime=runtime)
     wait_kfd_released(bad.kfd_lingering)
     assert not bad.ok
     assert bad.doc.get("hip_device_count", 0) == 0, bad.doc
