@@ -25,6 +25,9 @@
 
 #include "../src/health/init_sampler.h"
 #include "../src/health/liveness_kernel.h"
+#ifdef MI355X_IOCTL_TRACE
+#include "ioctl_trace.h"  // build with -DMI355X_IOCTL_TRACE -rdynamic: per-step ioctl wall times
+#endif
 
 namespace {
 
@@ -42,6 +45,7 @@ struct Step {
   hsa_status_t status = HSA_STATUS_SUCCESS;
   std::string profile;
   std::string queues;
+  std::string ioctls = "null";
 };
 
 // This process' kfd queues (/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/type):
@@ -114,9 +118,17 @@ int main(int argc, char** argv) {
   FN(hsa_executable_symbol_get_info);
   FN(hsa_amd_profiling_set_profiler_enabled);
 
+#ifdef MI355X_IOCTL_TRACE
+  const size_t io_init = ioctl_trace_mark();
+#endif
   const double t0 = now_ms();
   hsa_status_t s = hsa_init();
   const double t_init = now_ms() - t0;
+#ifdef MI355X_IOCTL_TRACE
+  const std::string init_ioctls = ioctl_trace_json(io_init);
+#else
+  const std::string init_ioctls = "null";
+#endif
   if (s != HSA_STATUS_SUCCESS) {
     std::printf("{\"ok\":false,\"error\":\"hsa_init %d\"}\n", static_cast<int>(s));
     return 1;
@@ -273,11 +285,17 @@ int main(int argc, char** argv) {
   for (auto& [name, fn] : plan) {
     mi355x::InitSampler smp(100);
     smp.start();
+#ifdef MI355X_IOCTL_TRACE
+    const size_t io0 = ioctl_trace_mark();
+#endif
     const double a = now_ms();
     const hsa_status_t st = fn();
     const double b = now_ms();
     smp.stop();
     steps.push_back({name, b - a, st, smp.json(), kfd_queues()});
+#ifdef MI355X_IOCTL_TRACE
+    steps.back().ioctls = ioctl_trace_json(io0);
+#endif
     if (st != HSA_STATUS_SUCCESS) {
       ok = false;
       break;
@@ -285,13 +303,13 @@ int main(int argc, char** argv) {
   }
   const double t_dev = now_ms() - t_dev0;
   std::string o = "{\"ok\":" + std::string(ok ? "true" : "false") + ",\"order\":\"" + order +
-                  "\",\"hsa_init_ms\":" + std::to_string(t_init) + ",\"device_setup_ms\":" + std::to_string(t_dev) +
+                  "\",\"hsa_init_ms\":" + std::to_string(t_init) + ",\"hsa_init_ioctls\":" + init_ioctls + ",\"device_setup_ms\":" + std::to_string(t_dev) +
                   ",\"steps\":[";
   for (size_t i = 0; i < steps.size(); ++i) {
     if (i) o += ",";
     o += "{\"name\":\"" + steps[i].name + "\",\"ms\":" + std::to_string(steps[i].ms) +
          ",\"status\":" + std::to_string(static_cast<int>(steps[i].status)) + ",\"profile\":" + steps[i].profile +
-         ",\"kfd_queues\":" + steps[i].queues + "}";
+         ",\"kfd_queues\":" + steps[i].queues + ",\"ioctls\":" + steps[i].ioctls + "}";
   }
   o += "]}";
   std::printf("%s\n", o.c_str());
