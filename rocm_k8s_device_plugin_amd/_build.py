@@ -42,24 +42,26 @@ STAMP = REPO_DIR / "build" / ".native.stamp"
 _checked: set = set()
 
 
-def _newest_source_mtime() -> float:
-    newest = 0.0
-    for p in NATIVE_DIR.rglob("*"):
+def _source_digest() -> str:
+    """Content hash of every native source (paths + bytes)."""
+    import hashlib
+    h = hashlib.sha1()
+    for p in sorted(NATIVE_DIR.rglob("*")):
         if p.is_file() and p.suffix in {".cpp", ".h", ".hip", ".txt"}:
-            newest = max(newest, p.stat().st_mtime)
-    return newest
+            h.update(str(p.relative_to(NATIVE_DIR)).encode())
+            h.update(p.read_bytes())
+    return h.hexdigest()
 
 
 def _up_to_date(targets) -> bool:
-    # Compare against a stamp written after each successful build, not against
-    # the targets: a no-op ninja run does not touch the targets, so after a
-    # copy that leaves sources "newer" (e.g. the gpurun snapshot) a target-based
-    # check would re-run the build on every call.
+    # Compare the sources' content hash with the one recorded after the last
+    # successful build, not mtimes: a copy of the tree (the gpurun snapshot, a
+    # container image layer) changes mtimes without changing what was built.
     if not all(t.exists() for t in targets):
         return False
     if not STAMP.exists():
         return False
-    return _newest_source_mtime() <= STAMP.stat().st_mtime
+    return f"digest={_source_digest()}" in STAMP.read_text().split()
 
 
 def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = None,
@@ -97,7 +99,7 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
         raise RuntimeError("native build failed")
     if not sanitize and build_dir is None:
         STAMP.parent.mkdir(parents=True, exist_ok=True)
-        STAMP.write_text(f"hip={hip}\n")
+        STAMP.write_text(f"hip={hip}\ndigest={_source_digest()}\n")
     if not quiet:
         sys.stdout.write(res.stdout)
 
@@ -121,7 +123,17 @@ def ensure_built(hip: bool | None = None) -> None:
             fcntl.flock(lk, fcntl.LOCK_EX)
             try:
                 if not _up_to_date(targets):
-                    build(hip=hip)
+                    try:
+                        build(hip=hip)
+                    except (RuntimeError, OSError, subprocess.CalledProcessError) as e:
+                        # a tree shipped with its outputs (e.g. to a GPU box without
+                        # the build directory) keeps working on what was built; the
+                        # warning names the sources that no longer match them
+                        if not all(t.exists() for t in targets):
+                            raise
+                        import warnings
+                        warnings.warn(f"native sources changed since the last build and the rebuild failed "
+                                      f"({e}); using the existing build outputs")
             finally:
                 fcntl.flock(lk, fcntl.LOCK_UN)
     _checked.add(hip)

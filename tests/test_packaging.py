@@ -120,3 +120,26 @@ def test_ci_workflows_parse_and_run_real_entry_points():
     for cmd in ("rocm_k8s_device_plugin_amd._build", '-m "not gpu"', "-m gpu", "bench.py"):
         assert cmd in steps
     assert docs["helm-chart-release.yaml"]["jobs"]["release"]["steps"][-1]["with"]["charts_dir"] == "helm"
+
+
+def test_build_stamp_follows_content_not_mtime(tmp_path, monkeypatch):
+    """A copied tree (gpurun snapshot, image layer) gets new mtimes: that must not
+    trigger a rebuild on a box without the build directory; an edit must."""
+    import os
+    from rocm_k8s_device_plugin_amd import _build
+    src = tmp_path / "native"
+    (src / "src").mkdir(parents=True)
+    f = src / "src" / "a.cpp"
+    f.write_text("int a;\n")
+    out = tmp_path / "out.so"
+    out.write_text("")
+    monkeypatch.setattr(_build, "NATIVE_DIR", src)
+    monkeypatch.setattr(_build, "STAMP", tmp_path / "stamp")
+    assert not _build._up_to_date([out])
+    _build.STAMP.write_text(f"hip=True\ndigest={_build._source_digest()}\n")
+    assert _build._up_to_date([out])
+    os.utime(f, (1e10, 1e10))                      # touched, same content
+    assert _build._up_to_date([out])
+    f.write_text("int a = 1;\n")                   # edited
+    assert not _build._up_to_date([out])
+    assert not _build._up_to_date([tmp_path / "missing.so"])
