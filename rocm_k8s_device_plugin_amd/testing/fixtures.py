@@ -316,3 +316,68 @@ def make_single_gpu_node(root: os.PathLike, **kw) -> FixtureInfo:
     kw.setdefault("num_gpus", 1)
     kw.setdefault("numa_nodes", 1)
     return make_mi355x_node(root, **kw)
+
+
+def wrap_kfd_topology(topology_dir: os.PathLike, root: os.PathLike) -> FixtureInfo:
+    """A node sysfs around a captured kfd topology (e.g. the reference's
+    ``testdata/topology-parsing/topology``, which holds only
+    ``class/kfd/kfd/topology``): the topology is copied as is and every GPU
+    node gets the PCI function, drm card/render nodes and /dev entries that the
+    plugin's discovery joins it with (through ``drm_render_minor``, as
+    ``GetDevIdsFromTopology`` does, amdgpu.go:406-445). The BDF comes from the
+    node's ``domain`` / ``location_id``; a node that repeats another's
+    location (the reference fixture's node 2 "is a cp of 1") gets the next
+    free bus number, since two PCI functions cannot share one."""
+    import shutil
+    src = Path(topology_dir)
+    root = Path(root)
+    sysfs, dev = root / "sys", root / "dev"
+    info = FixtureInfo(root=root, sysfs=sysfs, dev=dev)
+    topo = sysfs / "class/kfd/kfd/topology"
+    shutil.copytree(src, topo)
+    if not (topo / "generation_id").exists():
+        _w(topo / "generation_id", "1")
+    pci_root = sysfs / "devices/pci0000:00"
+    drv = sysfs / "bus/pci/drivers/amdgpu"
+    drv.mkdir(parents=True, exist_ok=True)
+    _w(sysfs / "module/amdgpu/version", "capture")
+    (sysfs / "module/amdgpu/drivers").mkdir(parents=True, exist_ok=True)
+    _link(sysfs / "module/amdgpu", drv / "module")
+    _link(drv, sysfs / "module/amdgpu/drivers/pci:amdgpu")
+    (dev / "dri").mkdir(parents=True, exist_ok=True)
+    _w(dev / "kfd", "")
+    used = set()
+    nodes = sorted((p for p in (topo / "nodes").iterdir() if p.name.isdigit()), key=lambda p: int(p.name))
+    for nd in nodes:
+        props = {}
+        for line in (nd / "properties").read_text().splitlines():
+            k, _, v = line.partition(" ")
+            props[k] = v.strip()
+        if int(props.get("simd_count", "0")) == 0:
+            continue
+        loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+        bus, devfn = (loc >> 8) & 0xFF, loc & 0xFF
+        while (dom, bus, devfn) in used:
+            bus = (bus + 1) & 0xFF
+        used.add((dom, bus, devfn))
+        bdf = f"{dom:04x}:{bus:02x}:{devfn >> 3:02x}.{devfn & 7:x}"
+        minor = int(props.get("drm_render_minor", "0"))
+        card = minor - 128
+        dev_dir = pci_root / bdf
+        _w(dev_dir / "vendor", f"0x{int(props.get('vendor_id', '4098')):04x}")
+        _w(dev_dir / "device", f"0x{int(props.get('device_id', '0')):04x}")
+        _w(dev_dir / "numa_node", "0")
+        _link(drv, dev_dir / "driver")
+        _link(dev_dir, drv / bdf)
+        _link(dev_dir, sysfs / "bus/pci/devices" / bdf)
+        (dev_dir / "drm" / f"card{card}").mkdir(parents=True, exist_ok=True)
+        (dev_dir / "drm" / f"renderD{minor}").mkdir(parents=True, exist_ok=True)
+        _link(dev_dir, sysfs / "class/drm" / f"card{card}" / "device")
+        _link(dev_dir, sysfs / "class/drm" / f"renderD{minor}" / "device")
+        _w(dev / "dri" / f"card{card}", "")
+        _w(dev / "dri" / f"renderD{minor}", "")
+        info.bdfs.append(bdf)
+        info.device_ids.append(bdf)
+        info.render_minors[bdf] = minor
+        info.node_ids[bdf] = int(nd.name)
+    return info
