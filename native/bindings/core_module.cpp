@@ -183,7 +183,8 @@ PYBIND11_MODULE(_native, m) {
            }),
            py::arg("missing_pair_is_worst") = true, py::arg("cross_hive_penalty") = 100)
       .def_readwrite("missing_pair_is_worst", &AllocatorOptions::missing_pair_is_worst)
-      .def_readwrite("cross_hive_penalty", &AllocatorOptions::cross_hive_penalty);
+      .def_readwrite("cross_hive_penalty", &AllocatorOptions::cross_hive_penalty)
+      .def_readwrite("degraded_links", &AllocatorOptions::degraded_links);
 
   py::class_<HiveAllocator>(m, "HiveAllocator")
       .def(py::init<>())
@@ -301,6 +302,40 @@ PYBIND11_MODULE(_native, m) {
       })
       .def_property_readonly("running", &SmiEventWatcher::running)
       .def_property_readonly("devices", &SmiEventWatcher::devices);
+  m.def("smi_xgmi_links", [] {
+    SmiXgmiSnapshot s;
+    {
+      py::gil_scoped_release nogil;
+      s = smi_xgmi_links();
+    }
+    py::dict out;
+    out["ok"] = s.ok;
+    out["error"] = s.error;
+    py::list gpus;
+    for (auto& g : s.gpus) {
+      py::dict d;
+      d["bdf"] = g.bdf;
+      d["status_ok"] = g.status_ok;
+      d["status"] = g.status;
+      d["metrics_ok"] = g.metrics_ok;
+      py::list peers;
+      for (auto& p : g.peers) {
+        py::dict pd;
+        pd["peer_bdf"] = p.peer_bdf;
+        pd["link_type"] = p.link_type;
+        pd["bit_rate_gbps"] = p.bit_rate_gbps;
+        pd["max_bandwidth_gbps"] = p.max_bandwidth_gbps;
+        pd["read_kb"] = p.read_kb;
+        pd["write_kb"] = p.write_kb;
+        peers.append(pd);
+      }
+      d["peers"] = peers;
+      d["error"] = g.error;
+      gpus.append(d);
+    }
+    out["gpus"] = gpus;
+    return out;
+  });
   m.def("smi_snapshot", [] {
     SmiSnapshot s;
     {

@@ -50,6 +50,11 @@ struct AllocatorOptions {
   bool missing_pair_is_worst = true;
   // extra weight for a pair whose endpoints sit in different (known) xGMI hives
   int cross_hive_penalty = 100;
+  // physical-GPU pairs (AllocDevice::unique_id keys) whose direct xGMI link is
+  // down at run time (amd-smi link state, health/fabric.py): their kfd link
+  // still reads xGMI, but traffic between them now takes another path, so the
+  // pair scores as the worst link ("other") and packing avoids it
+  std::vector<std::pair<std::string, std::string>> degraded_links;
 };
 
 struct AllocResult {

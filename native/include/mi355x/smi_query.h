@@ -49,6 +49,36 @@ bool smi_available();
 // (init/shut_down are reference-counted across this file's users).
 SmiSnapshot smi_snapshot();
 
+// xGMI link state of one GPU (amdsmi_get_gpu_xgmi_link_status: up / down /
+// disabled per link) and the per-link peers it is wired to
+// (amdsmi_get_link_metrics: destination BDF, bit rate, max bandwidth, type,
+// traffic counters). The health loop watches for links that go down; the
+// allocator then stops treating that GPU pair as xGMI-connected.
+struct SmiLinkPeer {
+  std::string peer_bdf;
+  int link_type = -1;          // amdsmi_link_type_t: 1 PCIe, 2 xGMI
+  uint32_t bit_rate_gbps = 0;  // current
+  uint32_t max_bandwidth_gbps = 0;
+  uint64_t read_kb = 0, write_kb = 0;
+};
+
+struct SmiXgmiLinks {
+  std::string bdf;
+  bool status_ok = false;       // link status query answered
+  std::vector<int> status;      // per link: 0 down, 1 up, 2 disabled
+  bool metrics_ok = false;
+  std::vector<SmiLinkPeer> peers;
+  std::string error;
+};
+
+struct SmiXgmiSnapshot {
+  bool ok = false;
+  std::string error;
+  std::vector<SmiXgmiLinks> gpus;
+};
+
+SmiXgmiSnapshot smi_xgmi_links();
+
 // Push-style GPU events from the driver (amdsmi_*_gpu_event_notification):
 // resets, VM faults, thermal throttling, queue evictions. SURVEY §5 "failure
 // detection": the health loop drains them every pulse instead of waiting for

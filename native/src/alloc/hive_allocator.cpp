@@ -1,9 +1,12 @@
 #include <algorithm>
 #include <deque>
 #include <limits>
+#include <set>
 #include <unordered_set>
 
 #include "mi355x/allocator.h"
+
+#include <set>
 #include "mi355x/constants.h"
 
 namespace mi355x {
@@ -94,6 +97,9 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
       }
   from_keys_ = froms.size();
 
+  std::set<std::pair<std::string, std::string>> degraded;
+  for (const auto& p : opt.degraded_links)
+    degraded.insert(p.first < p.second ? p : std::make_pair(p.second, p.first));
   w_.assign(static_cast<size_t>(n) * n, 0);
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) {
@@ -101,6 +107,10 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
       const auto& a = devs_[i];
       const auto& b = devs_[j];
       int lt = link_[static_cast<size_t>(i) * n + j];
+      if (lt != 0 && !degraded.empty() && a.unique_id != b.unique_id &&
+          degraded.count(a.unique_id < b.unique_id ? std::make_pair(a.unique_id, b.unique_id)
+                                                   : std::make_pair(b.unique_id, a.unique_id)))
+        lt = kLinkOther;
       bool cross_hive = a.hive_id != 0 && b.hive_id != 0 && a.hive_id != b.hive_id;
       w_[static_cast<size_t>(i) * n + j] =
           pair_weight_formula(a.unique_id == b.unique_id, lt, a.numa_node == b.numa_node, cross_hive, opt_, lt != 0);

@@ -39,6 +39,8 @@ struct SmiLib {
   decltype(&amdsmi_set_gpu_event_notification_mask) evt_mask = nullptr;
   decltype(&amdsmi_get_gpu_event_notification) evt_get = nullptr;
   decltype(&amdsmi_stop_gpu_event_notification) evt_stop = nullptr;
+  decltype(&amdsmi_get_gpu_xgmi_link_status) link_status = nullptr;
+  decltype(&amdsmi_get_link_metrics) link_metrics = nullptr;
 };
 
 template <typename T>
@@ -73,6 +75,8 @@ const SmiLib& smi() {
     bind(l.h, "amdsmi_set_gpu_event_notification_mask", &l.evt_mask);
     bind(l.h, "amdsmi_get_gpu_event_notification", &l.evt_get);
     bind(l.h, "amdsmi_stop_gpu_event_notification", &l.evt_stop);
+    bind(l.h, "amdsmi_get_gpu_xgmi_link_status", &l.link_status);
+    bind(l.h, "amdsmi_get_link_metrics", &l.link_metrics);
   });
   return l;
 }
@@ -214,6 +218,70 @@ SmiSnapshot smi_snapshot() {
   return snap;
 }
 
+SmiXgmiSnapshot smi_xgmi_links() {
+  SmiXgmiSnapshot snap;
+  const auto& L = smi();
+  if (!smi_available()) {
+    snap.error = "libamd_smi unavailable";
+    return snap;
+  }
+  if (!L.link_status && !L.link_metrics) {
+    snap.error = "libamd_smi has no xGMI link queries";
+    return snap;
+  }
+  if (!acquire()) {
+    snap.error = "amdsmi_init failed";
+    return snap;
+  }
+  for (auto h : all_gpus()) {
+    SmiXgmiLinks g;
+    g.bdf = bdf_of(h);
+    if (L.link_status) {
+      amdsmi_xgmi_link_status_t st{};
+      const amdsmi_status_t rc = L.link_status(h, &st);
+      if (rc == AMDSMI_STATUS_SUCCESS) {
+        g.status_ok = true;
+        const uint32_t n = st.total_links < AMDSMI_MAX_NUM_XGMI_LINKS ? st.total_links : AMDSMI_MAX_NUM_XGMI_LINKS;
+        for (uint32_t i = 0; i < n; ++i) g.status.push_back(static_cast<int>(st.status[i]));
+      } else {
+        g.error = "xgmi_link_status rc=" + std::to_string(static_cast<int>(rc));
+      }
+    }
+    if (L.link_metrics) {
+      amdsmi_link_metrics_t lm{};
+      const amdsmi_status_t rc = L.link_metrics(h, &lm);
+      if (rc == AMDSMI_STATUS_SUCCESS) {
+        g.metrics_ok = true;
+        const uint32_t n =
+            lm.num_links < AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK ? lm.num_links : AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK;
+        for (uint32_t i = 0; i < n; ++i) {
+          const auto& l = lm.links[i];
+          SmiLinkPeer p;
+          char buf[64];
+          std::snprintf(buf, sizeof(buf), "%04llx:%02llx:%02llx.%llx",
+                        static_cast<unsigned long long>(l.bdf.domain_number),
+                        static_cast<unsigned long long>(l.bdf.bus_number),
+                        static_cast<unsigned long long>(l.bdf.device_number),
+                        static_cast<unsigned long long>(l.bdf.function_number));
+          p.peer_bdf = buf;
+          p.link_type = static_cast<int>(l.link_type);
+          p.bit_rate_gbps = l.bit_rate;
+          p.max_bandwidth_gbps = l.max_bandwidth;
+          p.read_kb = l.read;
+          p.write_kb = l.write;
+          g.peers.push_back(p);
+        }
+      } else if (g.error.empty()) {
+        g.error = "link_metrics rc=" + std::to_string(static_cast<int>(rc));
+      }
+    }
+    snap.gpus.push_back(std::move(g));
+  }
+  release();
+  snap.ok = true;
+  return snap;
+}
+
 const char* smi_event_name(int type) {
   switch (type) {
     case AMDSMI_EVT_NOTIF_VMFAULT: return "vmfault";
@@ -296,6 +364,11 @@ void SmiEventWatcher::stop() {
 bool smi_available() { return false; }
 SmiSnapshot smi_snapshot() {
   SmiSnapshot s;
+  s.error = "built without amd_smi/amdsmi.h";
+  return s;
+}
+SmiXgmiSnapshot smi_xgmi_links() {
+  SmiXgmiSnapshot s;
   s.error = "built without amd_smi/amdsmi.h";
   return s;
 }

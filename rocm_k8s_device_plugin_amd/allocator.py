@@ -29,11 +29,18 @@ class AllocStats:
 class Policy:
     """Interface kept for parity with the reference Policy."""
 
-    def init(self, devices, topology) -> None:  # pragma: no cover - interface
+    def init(self, devices, topology, degraded_links: Iterable = ()) -> None:  # pragma: no cover - interface
         raise NotImplementedError
 
     def allocate(self, available: Sequence[str], required: Sequence[str], size: int) -> List[str]:
         raise NotImplementedError  # pragma: no cover
+
+
+def group_key(d) -> str:
+    """Physical-GPU identity the allocator groups partitions by: kfd's
+    unique_id, or — for a device whose kfd node is unreadable (e.g.
+    cgroup-denied inside a container) — its own PCI function."""
+    return d.unique_id or f"bdf:{getattr(d, 'bdf', '') or d.id}"
 
 
 class BestEffortPolicy(Policy):
@@ -57,11 +64,14 @@ class BestEffortPolicy(Policy):
             else:
                 # a device whose kfd node is unreadable (e.g. cgroup-denied inside a
                 # container) has no unique_id: group it by its own PCI function
-                key = d.unique_id or f"bdf:{getattr(d, 'bdf', '') or d.id}"
-                out.append(n.AllocDevice(d.id, d.node_id, d.numa_node, key, int(getattr(d, "hive_id", 0))))
+                out.append(n.AllocDevice(d.id, d.node_id, d.numa_node, group_key(d), int(getattr(d, "hive_id", 0))))
         return out
 
-    def init(self, devices, topology) -> None:
+    def init(self, devices, topology, degraded_links: Iterable = ()) -> None:
+        """``degraded_links``: pairs of physical-GPU keys (``group_key``) whose
+        direct xGMI link is down (health/fabric.py); they score as the worst
+        link until the next init without them."""
+        self._opts.degraded_links = sorted(tuple(sorted(p)) for p in degraded_links)
         err = self._alloc.init(self.to_alloc_devices(devices), topology, self._opts)
         if err:
             raise AllocationError(err)

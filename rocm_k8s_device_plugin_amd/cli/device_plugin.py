@@ -58,6 +58,8 @@ def build_parser() -> flags.GoFlagParser:
     p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
     p.add_bool("smi_events", False, "subscribe to amd-smi GPU events; a device is Unhealthy between a "
                                     "gpu_pre_reset and its gpu_post_reset, other events are counted")
+    p.add_bool("smi_xgmi", False, "watch amd-smi xGMI link state every pulse; a GPU pair whose link goes down "
+                                  "stops counting as xGMI-connected in preferred allocation (devices stay Healthy)")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
     p.add_bool("dry_run", False, "print what this node would advertise (implementation, resources, devices, "
@@ -118,7 +120,7 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
         from ..plugin.container import ContainerImpl
         hc = HealthConfig(exporter_socket=ns.exporter_socket or None, liveness=ns.liveness,
                           liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
-                          smi_ecc=ns.smi_ecc, smi_events=ns.smi_events, dev_root=ns.dev_root,
+                          smi_ecc=ns.smi_ecc, smi_events=ns.smi_events, smi_xgmi=ns.smi_xgmi, dev_root=ns.dev_root,
                           liveness_mode=ns.liveness_mode, chip_sweep_every=ns.liveness_chip_sweep_every,
                           liveness_keep_queues=ns.liveness_keep_queues)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None

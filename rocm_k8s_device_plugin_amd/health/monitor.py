@@ -20,6 +20,10 @@ Healthy only if every *available* source agrees:
    throttling and queue evictions are counted
    (``mi355x_dp_gpu_events_total``) and logged.
 
+Not a verdict but read in the same sweep: the xGMI link state (``smi_xgmi``,
+health/fabric.py). A GPU pair whose link went down stays Healthy; the
+allocator stops treating it as xGMI-connected (``degraded_links``).
+
 Verdicts are published as immutable snapshots with a version number, so
 ListAndWatch streams can send on change without locks.
 """
@@ -36,6 +40,7 @@ from ..topology import Inventory, hip_ordinals, kfd_busy_gpu_ids
 from ..utils import log
 from ..utils.trace import TRACER
 from . import exporter
+from .fabric import FabricWatcher
 from .liveness import LivenessProber
 
 _log = log.get("health")
@@ -64,6 +69,7 @@ class HealthConfig:
     recover_threshold: int = 1
     smi_ecc: bool = False
     smi_events: bool = False
+    smi_xgmi: bool = False             # watch xGMI link state (placement input, health/fabric.py)
     dev_root: str = "/dev"
 
 
@@ -79,7 +85,8 @@ class HealthMonitor:
     def __init__(self, inventory: Inventory, cfg: Optional[HealthConfig] = None,
                  prober: Optional[LivenessProber] = None,
                  ordinal_map: Optional[Mapping[str, int]] = None,
-                 exporter_fn: Optional[Callable] = None, event_source=None):
+                 exporter_fn: Optional[Callable] = None, event_source=None,
+                 fabric_source: Optional[Callable[[], dict]] = None):
         self.inv = inventory
         self.cfg = cfg or HealthConfig()
         self.prober = prober
@@ -102,6 +109,16 @@ class HealthMonitor:
         self.version = 0
         self.sweeps = 0
         self.last_sweep_ms = 0.0
+        self.fabric = FabricWatcher(inventory, fabric_source) if self.cfg.smi_xgmi else None
+
+    # ------------------------------------------------------------------ fabric
+    def degraded_links(self):
+        """Physical-GPU pairs (allocator group keys) whose xGMI link is down."""
+        return self.fabric.degraded if self.fabric is not None else frozenset()
+
+    @property
+    def fabric_version(self) -> int:
+        return self.fabric.version if self.fabric is not None else 0
 
     # ------------------------------------------------------------------ views
     def snapshot(self) -> Dict[str, Verdict]:
@@ -277,6 +294,10 @@ class HealthMonitor:
             for d in self.inv.devices:
                 if d.bdf in self._resetting:
                     reasons[d.id].append("GPU reset in progress (amd-smi gpu_pre_reset, no post_reset yet)")
+
+        if self.fabric is not None:
+            import asyncio
+            await asyncio.to_thread(self.fabric.check)   # amd-smi queries run off the event loop
 
         new = {dev: Verdict(dp.UNHEALTHY if rs else dp.HEALTHY, tuple(rs)) for dev, rs in reasons.items()}
         changed = any(new[k].health != self._snapshot.get(k, Verdict("")).health for k in new)

@@ -91,6 +91,11 @@ class DeviceImpl(abc.ABC):
     def health_version(self) -> int:
         return 0
 
+    def fabric_version(self) -> int:
+        """Bumped when the live xGMI link state changes the pair weights; the
+        manager then re-initialises every resource's allocator."""
+        return 0
+
     async def reload_topology(self) -> Optional[dict]:
         """Re-discover devices if the node's GPU topology changed; None if the
         advertised devices are unchanged (see ContainerImpl.reload_topology)."""

@@ -118,7 +118,7 @@ class ContainerImpl(DeviceImpl):
             ctx.allocator_error = True
             return
         try:
-            ctx.allocator.init(devs, self.inv.topology)
+            ctx.allocator.init(devs, self.inv.topology, degraded_links=self.monitor.degraded_links())
         except AllocationError as e:
             _log.error("allocator init failed for plugin %s. Falling back to kubelet default allocation. "
                        "Error %s", ctx.resource, e)
@@ -151,6 +151,9 @@ class ContainerImpl(DeviceImpl):
         # a reload replaces the monitor (its version restarts): the epoch keeps
         # the combined value moving so every ListAndWatch stream re-sends
         return self._epoch * 1_000_000_000 + self.monitor.version
+
+    def fabric_version(self) -> int:
+        return self._epoch * 1_000_000_000 + self.monitor.fabric_version
 
     # ---------------------------------------------------------------- topology reload
     def _signature(self) -> tuple:

@@ -165,6 +165,7 @@ class PluginManager:
         self._metrics_server = None
         self._impl_lock: Optional[asyncio.Lock] = None   # health sweep vs topology reload
         self.topology_reloads = 0
+        self._fabric_seen = 0
 
     # ------------------------------------------------------------- control
     def request_stop(self) -> None:
@@ -197,6 +198,16 @@ class PluginManager:
                 (time.perf_counter() - t0) * 1e3)
             if changed:
                 REGISTRY.inc("mi355x_dp_health_changes_total")
+            fv = self.impl.fabric_version()
+            if fv != self._fabric_seen:
+                # xGMI link state changed the pair weights: re-initialise every
+                # resource's allocator (devices and their health are unchanged)
+                self._fabric_seen = fv
+                async with self._impl_lock:
+                    for p in self.plugins.values():
+                        p.start()
+                REGISTRY.inc("mi355x_dp_fabric_reweights_total")
+                _log.warning("xGMI link state changed: preferred allocation re-weighted")
             self.pulse.fire()
 
     async def _topology_loop(self) -> None:

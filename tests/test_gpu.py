@@ -512,3 +512,24 @@ def test_topology_watch_signature_on_real_sysfs():
     assert parts and all(cp for _, cp, _ in parts), parts
     assert asyncio.run(impl.reload_topology()) is None
     asyncio.run(impl.close())
+
+
+def test_xgmi_link_state_on_real_mi355x(inv):
+    """amd-smi's live xGMI link state for this GPU: link slots with 7 up on an
+    8-GPU MI355X node, peers named by BDF; the watcher's first reading is the
+    baseline and degrades nothing."""
+    from rocm_k8s_device_plugin_amd.health.fabric import LINK_UP, FabricWatcher
+    from rocm_k8s_device_plugin_amd.ops.native import core
+    snap = core().smi_xgmi_links()
+    assert snap["ok"], snap
+    mine = {d.bdf.lower() for d in inv.devices}
+    gpus = [g for g in snap["gpus"] if g["bdf"].lower() in mine]
+    assert gpus, snap
+    for g in gpus:
+        assert g["status_ok"], g
+        assert sum(s == LINK_UP for s in g["status"]) >= 1, g
+        if g["metrics_ok"]:
+            assert any(p["peer_bdf"].lower() in mine and p["link_type"] == 2 for p in g["peers"]), g
+    w = FabricWatcher(inv)
+    w.check()
+    assert not w.check() and w.degraded == frozenset()
