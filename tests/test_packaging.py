@@ -34,7 +34,8 @@ def test_device_plugin_manifests():
     (health,) = _docs("k8s-ds-amdgpu-dp-health.yaml")
     c = _ds(health)["containers"][0]
     assert c["command"] == ["./k8s-device-plugin"]
-    assert "-pulse=2" in c["args"] and "-liveness=true" in c["args"]
+    assert "-pulse=2" in c["args"] and "-liveness=true" in c["args"] and "-smi_xgmi=true" in c["args"]
+    assert c["resources"]["requests"]["memory"] == "3Gi"
     assert "/dev" in {m["mountPath"] for m in c["volumeMounts"]}
 
 
