@@ -81,7 +81,10 @@ class ContainerImpl(DeviceImpl):
         _log.info("Found %d AMDGPUs (%s)", len(self.inv), ", ".join(
             f"{r}={len(v)}" for r, v in self._members.items()))
         if self._cdi:
-            self._write_cdi_specs()
+            try:
+                self._write_cdi_specs()
+            except (OSError, ValueError) as e:
+                raise DeviceImplError(f"cannot write CDI specs to {self.cdi_spec_dir}: {e}") from e
 
     def _write_cdi_specs(self, stale=()) -> None:
         # before registration: kubelet may hand a CDI name to the runtime as

@@ -152,3 +152,13 @@ def test_cli_dry_run_with_cdi(tmp_path, capsys):
                    "-kubelet_dir", str(tmp_path / "dp")])
     assert rc == 0
     assert (tmp_path / "cdi" / "amd.com-gpu.json").exists()
+
+
+def test_unwritable_spec_dir_is_an_init_error(tmp_path):
+    from rocm_k8s_device_plugin_amd.plugin.base import DeviceImplError
+    fi = make_mi355x_node(tmp_path / "n")
+    blocker = tmp_path / "file"
+    blocker.write_text("")
+    with pytest.raises(DeviceImplError, match="CDI specs"):
+        ContainerImpl("single", str(fi.sysfs), HealthConfig(exporter_socket=None), device_list_strategy=["cdi-cri"],
+                      cdi_spec_dir=str(blocker / "cdi"))
