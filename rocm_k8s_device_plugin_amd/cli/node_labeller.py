@@ -5,7 +5,7 @@ label kind (``-vram``, ``-cu-count``, ...), ``-driver_type``, ``-kubeconfig``,
 node name from ``$DS_NODE_NAME``. Same flags here; additions: ``-resync``
 (periodic re-assert; 0 = apply once like the reference), ``-dry_run`` (print
 the labels as JSON and exit), ``-sysfs_root`` / ``-dev_root``, and the opt-in
-extra kinds ``-gfx-target`` / ``-xgmi-hive-count``.
+extra kinds ``-gfx-target`` / ``-xgmi-hive-count`` / ``-xgmi-links-down``.
 """
 from __future__ import annotations
 

@@ -20,7 +20,10 @@ via the card node or — inside containers that only get render nodes — the
 render node).
 
 Additions (off by default, never emitted unless enabled):
-``amd.com/gpu.gfx-target`` (e.g. ``gfx950``) and ``amd.com/gpu.xgmi-hive-count``.
+``amd.com/gpu.gfx-target`` (e.g. ``gfx950``), ``amd.com/gpu.xgmi-hive-count`` and
+``amd.com/gpu.xgmi-links-down`` (xGMI links amd-smi reports down across the
+node's GPUs, disabled slots not counted: a scheduler can keep multi-GPU jobs
+off a node whose fabric is degraded; re-asserted every ``-resync``).
 """
 from __future__ import annotations
 
@@ -36,7 +39,7 @@ from ..utils import log
 
 _log = log.get("labeller")
 
-EXTRA_LABELS = ["gfx-target", "xgmi-hive-count"]
+EXTRA_LABELS = ["gfx-target", "xgmi-hive-count", "xgmi-links-down"]
 
 
 def create_label_prefix(name: str, experimental: bool) -> str:
@@ -61,6 +64,7 @@ class LabelContext:
     inventory: Optional[Inventory] = None
     _fw_cache: dict = field(default_factory=dict)
     _drm_cache: dict = field(default_factory=dict)
+    xgmi_source: Optional[Callable[[], dict]] = None   # amd-smi link state (tests inject a fake)
 
     @property
     def gpus(self) -> List[Gpu]:
@@ -264,6 +268,18 @@ def _xgmi_hive_count(ctx: LabelContext) -> Dict[str, str]:
     return {create_label_prefix("xgmi-hive-count", False): str(len(hives))}
 
 
+def _xgmi_links_down(ctx: LabelContext) -> Dict[str, str]:
+    snap = ctx.xgmi_source() if ctx.xgmi_source is not None else core().smi_xgmi_links()
+    if not snap.get("ok") or not ctx.gpus:
+        return {}
+    mine = {g.bdf.lower() for g in ctx.gpus}
+    seen = [g for g in snap.get("gpus", []) if g.get("bdf", "").lower() in mine and g.get("status_ok")]
+    if not seen:
+        return {}
+    down = sum(1 for g in seen for st in g.get("status", []) if st == 0)
+    return {create_label_prefix("xgmi-links-down", False): str(down)}
+
+
 LABEL_GENERATORS: Dict[str, Callable[[LabelContext], Dict[str, str]]] = {
     "firmware": _firmware,
     "family": _family,
@@ -280,6 +296,7 @@ LABEL_GENERATORS: Dict[str, Callable[[LabelContext], Dict[str, str]]] = {
     "mode": _mode,
     "gfx-target": _gfx_target,
     "xgmi-hive-count": _xgmi_hive_count,
+    "xgmi-links-down": _xgmi_links_down,
 }
 
 
@@ -373,7 +390,8 @@ def generate_pf_labels(enabled: Dict[str, bool], sysfs_root: str) -> Dict[str, s
 
 
 def generate_labels(enabled: Dict[str, bool], driver_type: str = "", sysfs_root: str = "/sys",
-                    dev_root: str = "/dev", inventory: Optional[Inventory] = None) -> Dict[str, str]:
+                    dev_root: str = "/dev", inventory: Optional[Inventory] = None,
+                    xgmi_source: Optional[Callable[[], dict]] = None) -> Dict[str, str]:
     """Reference generateLabels (main.go:389-408): explicit mode, else container -> VF -> PF."""
 
     def container():
@@ -381,7 +399,7 @@ def generate_labels(enabled: Dict[str, bool], driver_type: str = "", sysfs_root:
         if inv is None:
             inv = discover(sysfs_root) if os.path.exists(os.path.join(sysfs_root, "module/amdgpu/drivers")) \
                 else None
-        return generate_container_labels(enabled, LabelContext(sysfs_root, dev_root, inv))
+        return generate_container_labels(enabled, LabelContext(sysfs_root, dev_root, inv, xgmi_source=xgmi_source))
 
     if driver_type == C.CONTAINER:
         return container()

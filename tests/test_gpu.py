@@ -325,6 +325,10 @@ def test_node_labeller_on_real_mi355x():
     assert vals.get("gpu.family") == "AI", vals
     assert vals.get("gpu.device-id") == "75a3" and vals.get("gpu.cu-count") == "256", vals
     assert vals.get("gpu.mode") == "container"
+    # additions: gfx950 target, one hive, no xGMI link down on a healthy node
+    extra = L.generate_labels({"gfx-target": True, "xgmi-hive-count": True, "xgmi-links-down": True}, "container")
+    assert extra.get("amd.com/gpu.gfx-target") == "gfx950", extra
+    assert extra.get("amd.com/gpu.xgmi-links-down") == "0", extra
 
 
 def test_smi_cross_check(inv):

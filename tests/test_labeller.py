@@ -92,6 +92,29 @@ def test_extra_labels(tmp_path):
     assert L.gfx_name(90402) == "gfx942" and L.gfx_name(90010) == "gfx90a" and L.gfx_name(90500) == "gfx950"
 
 
+def test_xgmi_links_down_label(tmp_path):
+    """Counts links amd-smi reports down (status 0) on this node's GPUs; disabled
+    slots (2) and other nodes' GPUs do not count; no label without amd-smi."""
+    fi = make_mi355x_node(tmp_path)
+
+    def reading(down_on_first=0):
+        gpus = [{"bdf": b, "status_ok": True, "status": [2] + [1] * 7, "peers": [], "metrics_ok": False}
+                for b in fi.bdfs]
+        gpus[0]["status"] = [2] + [0] * down_on_first + [1] * (7 - down_on_first)
+        gpus.append({"bdf": "0000:ee:00.0", "status_ok": True, "status": [0] * 8})    # not ours
+        return {"ok": True, "error": "", "gpus": gpus}
+
+    on = {"xgmi-links-down": True}
+    lab = L.generate_labels(on, "container", str(fi.sysfs), str(fi.dev), xgmi_source=lambda: reading(0))
+    assert lab == {"amd.com/gpu.xgmi-links-down": "0"}
+    lab = L.generate_labels(on, "container", str(fi.sysfs), str(fi.dev), xgmi_source=lambda: reading(2))
+    assert lab == {"amd.com/gpu.xgmi-links-down": "2"}
+    lab = L.generate_labels(on, "container", str(fi.sysfs), str(fi.dev),
+                            xgmi_source=lambda: {"ok": False, "error": "no amd-smi", "gpus": []})
+    assert lab == {}
+    assert "amd.com/gpu.xgmi-links-down" in L.all_label_keys()
+
+
 def test_heterogeneous_no_partition_label(tmp_path):
     fi = make_mi355x_node(tmp_path, per_gpu_compute=["spx"] * 4 + ["cpx"] * 4)
     lab = L.generate_labels({"compute-memory-partition": True}, "container", str(fi.sysfs), str(fi.dev))
