@@ -272,6 +272,14 @@ PYBIND11_MODULE(_native, m) {
   });
 
   m.def("smi_available", &smi_available);
+  m.def("smi_hold", [] {
+    py::gil_scoped_release nogil;
+    return smi_hold();
+  });
+  m.def("smi_unhold", [] {
+    py::gil_scoped_release nogil;
+    smi_unhold();
+  });
   m.def("smi_event_name", [](int t) { return std::string(smi_event_name(t)); });
   py::class_<SmiEventWatcher>(m, "SmiEventWatcher")
       .def(py::init<>())

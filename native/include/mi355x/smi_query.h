@@ -45,6 +45,11 @@ struct SmiSnapshot {
 };
 
 bool smi_available();
+// Keep amd-smi initialised between queries (a reference on the shared
+// amdsmi_init): each query otherwise pays a full init/shut_down cycle, ~26 ms
+// on an MI355X node. The health loop holds one while amd-smi sources are on.
+bool smi_hold();
+void smi_unhold();
 // amdsmi_init(AMD_GPUS) -> enumerate every GPU processor -> amdsmi_shut_down
 // (init/shut_down are reference-counted across this file's users).
 SmiSnapshot smi_snapshot();

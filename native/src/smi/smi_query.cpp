@@ -136,6 +136,11 @@ bool smi_available() {
   return L.init && L.sockets && L.processors;
 }
 
+bool smi_hold() { return smi_available() && acquire(); }
+void smi_unhold() {
+  if (smi_available()) release();
+}
+
 SmiSnapshot smi_snapshot() {
   SmiSnapshot snap;
   const auto& L = smi();
@@ -362,6 +367,8 @@ void SmiEventWatcher::stop() {
 #else  // no amd-smi header at build time
 
 bool smi_available() { return false; }
+bool smi_hold() { return false; }
+void smi_unhold() {}
 SmiSnapshot smi_snapshot() {
   SmiSnapshot s;
   s.error = "built without amd_smi/amdsmi.h";

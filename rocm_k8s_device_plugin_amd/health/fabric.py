@@ -59,6 +59,10 @@ class FabricWatcher:
         self.error = ""
         self.readings = 0
 
+    @property
+    def reads_amd_smi(self) -> bool:
+        return self._source is None
+
     def _read(self) -> dict:
         if self._source is not None:
             return self._source()

@@ -29,6 +29,7 @@ ListAndWatch streams can send on change without locks.
 """
 from __future__ import annotations
 
+import asyncio
 import os
 import time
 from dataclasses import dataclass
@@ -110,6 +111,7 @@ class HealthMonitor:
         self.sweeps = 0
         self.last_sweep_ms = 0.0
         self.fabric = FabricWatcher(inventory, fabric_source) if self.cfg.smi_xgmi else None
+        self._smi_held = False   # amd-smi kept initialised while its sources are on (smi_hold)
 
     # ------------------------------------------------------------------ fabric
     def degraded_links(self):
@@ -157,10 +159,18 @@ class HealthMonitor:
             out[d.id] = None if (cores == 0 and gfx > 0) else f"kfd node {d.node_id} not a live GPU"
         return out
 
+    def _smi_hold(self) -> None:
+        # one amdsmi_init for the monitor's lifetime instead of one per query
+        # (~26 ms each on MI355X, tools/smi_timing.py)
+        if not self._smi_held:
+            n = core()
+            self._smi_held = bool(n.smi_available() and n.smi_hold())
+
     def _smi_ecc(self) -> Dict[str, str]:
         n = core()
         if not n.smi_available():
             return {}
+        self._smi_hold()
         snap = n.smi_snapshot()
         if not snap["ok"]:
             return {}
@@ -245,6 +255,9 @@ class HealthMonitor:
         if self._events is not None and self._events_started:
             self._events.stop()
             self._events_started = False
+        if self._smi_held:
+            core().smi_unhold()
+            self._smi_held = False
 
     async def check_once(self) -> bool:
         """Run one sweep; returns True if any verdict changed."""
@@ -286,7 +299,7 @@ class HealthMonitor:
                     reasons[dev_id].append("no HIP device for this ID (render node inaccessible?)")
 
         if self.cfg.smi_ecc:
-            for dev_id, r in self._smi_ecc().items():
+            for dev_id, r in (await asyncio.to_thread(self._smi_ecc)).items():   # amd-smi off the event loop
                 reasons[dev_id].append(r)
 
         if self.cfg.smi_events:
@@ -296,7 +309,8 @@ class HealthMonitor:
                     reasons[d.id].append("GPU reset in progress (amd-smi gpu_pre_reset, no post_reset yet)")
 
         if self.fabric is not None:
-            import asyncio
+            if self.fabric.reads_amd_smi:
+                self._smi_hold()
             await asyncio.to_thread(self.fabric.check)   # amd-smi queries run off the event loop
 
         new = {dev: Verdict(dp.UNHEALTHY if rs else dp.HEALTHY, tuple(rs)) for dev, rs in reasons.items()}
