@@ -377,6 +377,8 @@ PYBIND11_MODULE(_native, m) {
       d["hsa_id"] = g.hsa_id;
       d["hip_id"] = g.hip_id;
       d["hip_uuid"] = g.hip_uuid;
+      d["driver_name"] = g.driver_name;
+      d["driver_version"] = g.driver_version;
       gpus.append(d);
     }
     out["gpus"] = gpus;

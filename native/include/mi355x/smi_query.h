@@ -36,6 +36,8 @@ struct SmiGpu {
   int hsa_id = -1;
   int hip_id = -1;
   std::string hip_uuid;
+  std::string driver_name;      // amdsmi_get_gpu_driver_info
+  std::string driver_version;
 };
 
 struct SmiSnapshot {

@@ -41,6 +41,7 @@ struct SmiLib {
   decltype(&amdsmi_stop_gpu_event_notification) evt_stop = nullptr;
   decltype(&amdsmi_get_gpu_xgmi_link_status) link_status = nullptr;
   decltype(&amdsmi_get_link_metrics) link_metrics = nullptr;
+  decltype(&amdsmi_get_gpu_driver_info) driver = nullptr;
 };
 
 template <typename T>
@@ -77,6 +78,7 @@ const SmiLib& smi() {
     bind(l.h, "amdsmi_stop_gpu_event_notification", &l.evt_stop);
     bind(l.h, "amdsmi_get_gpu_xgmi_link_status", &l.link_status);
     bind(l.h, "amdsmi_get_link_metrics", &l.link_metrics);
+    bind(l.h, "amdsmi_get_gpu_driver_info", &l.driver);
   });
   return l;
 }
@@ -213,6 +215,11 @@ SmiSnapshot smi_snapshot() {
           g.hsa_id = static_cast<int>(en.hsa_id);
           g.hip_id = static_cast<int>(en.hip_id);
           g.hip_uuid = en.hip_uuid;
+        }
+        amdsmi_driver_info_t di{};
+        if (L.driver && L.driver(h, &di) == AMDSMI_STATUS_SUCCESS) {
+          g.driver_name = di.driver_name;
+          g.driver_version = di.driver_version;
         }
         snap.gpus.push_back(std::move(g));
       }

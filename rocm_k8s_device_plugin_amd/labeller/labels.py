@@ -148,8 +148,31 @@ def _module_attr(ctx: LabelContext, attr: str) -> str:
     return ""
 
 
+def _amdgpu_version_fallback(ctx: LabelContext) -> str:
+    """The card's ``driver/module/version`` is absent when amdgpu is built into
+    the kernel or loaded without a version string (the MI355X test host): the
+    reference then labels an empty string (main.go:166-181). Fall back to
+    ``/sys/module/amdgpu/version``, then to amd-smi's driver info."""
+    try:
+        with open(os.path.join(ctx.sysfs_root, "module/amdgpu/version")) as f:
+            v = f.read().strip()
+            if v:
+                return v
+    except OSError:
+        pass
+    n = core()
+    if ctx.gpus and n.smi_available():
+        snap = n.smi_snapshot()
+        mine = {g.bdf.lower() for g in ctx.gpus}
+        for g in snap.get("gpus", []) if snap.get("ok") else []:
+            if g["bdf"].lower() in mine and g.get("driver_version"):
+                return g["driver_version"]
+    return ""
+
+
 def _driver_version(ctx: LabelContext) -> Dict[str, str]:
-    return {create_label_prefix("driver-version", False): _module_attr(ctx, "version")}
+    v = _module_attr(ctx, "version") or _amdgpu_version_fallback(ctx)
+    return {create_label_prefix("driver-version", False): v}
 
 
 def _driver_src_version(ctx: LabelContext) -> Dict[str, str]:

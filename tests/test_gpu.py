@@ -329,6 +329,11 @@ def test_node_labeller_on_real_mi355x():
     extra = L.generate_labels({"gfx-target": True, "xgmi-hive-count": True, "xgmi-links-down": True}, "container")
     assert extra.get("amd.com/gpu.gfx-target") == "gfx950", extra
     assert extra.get("amd.com/gpu.xgmi-links-down") == "0", extra
+    # driver version: the card's module/version, /sys/module/amdgpu/version or amd-smi
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/labels_gpu_test.json", "w") as f:
+        json.dump({"labels": lab, "extra": extra}, f, indent=1)
+    assert vals.get("gpu.driver-version"), vals
 
 
 def test_smi_cross_check(inv):

@@ -277,3 +277,16 @@ def test_reconcile_falls_back_to_update_without_patch_verb(tmp_path):
         assert "beta.amd.com/gpu.vram.64G" not in got
     finally:
         srv.stop()
+
+
+def test_driver_version_fallback_when_card_has_no_module_version(tmp_path):
+    """amdgpu built in / without a version under the card's driver/module: the
+    reference labels "" (main.go:166-181); here /sys/module/amdgpu/version."""
+    import os
+    fi = make_mi355x_node(tmp_path)
+    os.unlink(fi.sysfs / "bus/pci/drivers/amdgpu/module")
+    lab = L.generate_labels({"driver-version": True}, "container", str(fi.sysfs), str(fi.dev))
+    assert lab["amd.com/gpu.driver-version"] == "6.12.12"
+    (fi.sysfs / "module/amdgpu/version").unlink()
+    lab = L.generate_labels({"driver-version": True}, "container", str(fi.sysfs), str(fi.dev))
+    assert lab["amd.com/gpu.driver-version"] == ""      # nothing left to read (no amd-smi here)
