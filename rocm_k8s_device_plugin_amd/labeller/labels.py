@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import math
 import os
+import re
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
@@ -148,6 +149,27 @@ def _module_attr(ctx: LabelContext, attr: str) -> str:
     return ""
 
 
+# Kubernetes label values: <= 63 chars, [A-Za-z0-9] at both ends, [-_.A-Za-z0-9]
+# between (apimachinery validation.IsValidLabelValue). The apiserver rejects a
+# whole patch with one bad value, which would leave the node with no labels.
+_LABEL_VALUE_RE = re.compile(r"^(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?$")
+
+
+def sanitize_label_value(v: str) -> str:
+    if len(v) <= 63 and _LABEL_VALUE_RE.match(v):
+        return v
+    out = re.sub(r"[^-A-Za-z0-9_.]", "_", v)[:63]
+    return re.sub(r"^[^A-Za-z0-9]+|[^A-Za-z0-9]+$", "", out)
+
+
+def _driver_version_value(raw: str) -> str:
+    # amd-smi reports an in-tree amdgpu's version as the kernel banner with the
+    # spaces removed ("Linuxversion6.18.54-ant.1(nixbld@...)..." on the MI355X
+    # host): the kernel release is the driver version then
+    m = re.match(r"^Linux\s*version\s*([0-9][^\s(]*)", raw)
+    return m.group(1) if m else raw
+
+
 def _amdgpu_version_fallback(ctx: LabelContext) -> str:
     """The card's ``driver/module/version`` is absent when amdgpu is built into
     the kernel or loaded without a version string (the MI355X test host): the
@@ -166,7 +188,7 @@ def _amdgpu_version_fallback(ctx: LabelContext) -> str:
         mine = {g.bdf.lower() for g in ctx.gpus}
         for g in snap.get("gpus", []) if snap.get("ok") else []:
             if g["bdf"].lower() in mine and g.get("driver_version"):
-                return g["driver_version"]
+                return _driver_version_value(g["driver_version"])
     return ""
 
 
@@ -366,7 +388,7 @@ def generate_container_labels(enabled: Dict[str, bool], ctx: LabelContext) -> Di
         if not enabled.get(name):
             continue
         results.update(gen(ctx))
-    return results
+    return {k: sanitize_label_value(v) for k, v in results.items()}
 
 
 def generate_vf_labels(enabled: Dict[str, bool], sysfs_root: str) -> Dict[str, str]:
@@ -426,13 +448,16 @@ def generate_labels(enabled: Dict[str, bool], driver_type: str = "", sysfs_root:
 
     if driver_type == C.CONTAINER:
         return container()
+    def clean(labels):
+        return {k: sanitize_label_value(v) for k, v in labels.items()}
+
     if driver_type == C.VF_PASSTHROUGH:
-        return generate_vf_labels(enabled, sysfs_root)
+        return clean(generate_vf_labels(enabled, sysfs_root))
     if driver_type == C.PF_PASSTHROUGH:
-        return generate_pf_labels(enabled, sysfs_root)
+        return clean(generate_pf_labels(enabled, sysfs_root))
     labels = container()
     if not labels:
         labels = generate_vf_labels(enabled, sysfs_root)
     if not labels:
         labels = generate_pf_labels(enabled, sysfs_root)
-    return labels
+    return clean(labels)

@@ -334,6 +334,7 @@ def test_node_labeller_on_real_mi355x():
     with open("gpurun_out/labels_gpu_test.json", "w") as f:
         json.dump({"labels": lab, "extra": extra}, f, indent=1)
     assert vals.get("gpu.driver-version"), vals
+    assert "(" not in vals["gpu.driver-version"] and len(vals["gpu.driver-version"]) <= 63, vals
 
 
 def test_smi_cross_check(inv):

@@ -290,3 +290,16 @@ def test_driver_version_fallback_when_card_has_no_module_version(tmp_path):
     (fi.sysfs / "module/amdgpu/version").unlink()
     lab = L.generate_labels({"driver-version": True}, "container", str(fi.sysfs), str(fi.dev))
     assert lab["amd.com/gpu.driver-version"] == ""      # nothing left to read (no amd-smi here)
+
+
+def test_label_values_are_valid_kubernetes_values():
+    """One invalid value makes the apiserver reject the whole node patch."""
+    import re
+    ok = re.compile(r"^(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?$")
+    banner = "Linuxversion6.18.54-ant.1(nixbld@localhost)(gcc(GCC)15.3.0,GNUld(GNUBinutils)2.46)#1-ant-ociSMP"
+    assert L._driver_version_value(banner) == "6.18.54-ant.1"
+    assert L._driver_version_value("6.12.12") == "6.12.12"
+    for v in (banner, "a b", "(x)", "-lead", "trail-", "x" * 80, "", "6.12.12", "AMD_Instinct_MI355_OAM"):
+        s = L.sanitize_label_value(v)
+        assert len(s) <= 63 and ok.match(s), (v, s)
+    assert L.sanitize_label_value("6.12.12") == "6.12.12"
