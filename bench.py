@@ -93,6 +93,10 @@ def parse_args():
                          "reported in extra.rccl next to the allocated set's xGMI fabric bound, never part of the metric")
     ap.add_argument("--collective-sizes", default="",
                     help="per-rank bytes for --collectives (default 1M,64M,256M on GPUs, 64K on CPU)")
+    ap.add_argument("--health-pulse", type=float, default=0.0,
+                    help="> 0: run the plugin as the health DaemonSet does (MFMA liveness via the kept-queue probe "
+                         "server, amd-smi ECC / events / xGMI link state) with this pulse in seconds, while pods "
+                         "are admitted (BASELINE config: health-check DaemonSet enabled)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -208,12 +212,15 @@ def main():
         minor_to_ord = {dv.render_minor: ords[dv.id] for dv in adv}
         minor_to_paths = {dv.render_minor: dv.dev_paths() for dv in adv}
         adv_ordinals = [ords[dv.id] for dv in adv]
-        impl = ContainerImpl("single", sysfs, HealthConfig(exporter_socket=None), inventory=inv)
+        hp = args.health_pulse if not args.fixture else 0.0
+        hcfg = (HealthConfig(exporter_socket=None, liveness=True, smi_ecc=True, smi_events=True, smi_xgmi=True)
+                if hp > 0 else HealthConfig(exporter_socket=None))
+        impl = ContainerImpl("single", sysfs, hcfg, inventory=inv)
         pdir = os.path.join(tmp, "device-plugins")
         loop = asyncio.new_event_loop()
         kubelet = FakeKubelet(pdir)
         loop.run_until_complete(kubelet.start())
-        mgr = PluginManager(impl, ManagerConfig(pulse_s=0, plugin_dir=pdir, handle_signals=False))
+        mgr = PluginManager(impl, ManagerConfig(pulse_s=hp, plugin_dir=pdir, handle_signals=False))
         mgr_task = loop.create_task(mgr.run())
         loop.run_until_complete(kubelet.wait_for_resource("amd.com/gpu", n, timeout=30))
         gpu_info = {"ids": [dv.id for dv in adv], "gfx_target_version": sorted({dv.gfx_target_version for dv in adv}),
@@ -225,6 +232,14 @@ def main():
     rpc_ms, alloc_rpc_ms, lat_ms, ready_ms, kern_us = [], [], [], [], []
     exec_ms, rt_ms, dev_ms, settle_ms = [], [], [], []
     from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
+
+    def blocking(fn, *a, **kw):
+        """Run fn; with the health loop on, on a worker thread while rank 0's
+        event loop keeps sweeping (so sweeps overlap the container start)."""
+        if loop is not None and args.health_pulse > 0 and not args.fixture:
+            import functools
+            return loop.run_until_complete(asyncio.to_thread(functools.partial(fn, *a, **kw)))
+        return fn(*a, **kw)
 
     def one_step(record: bool, runtime: str = args.container_runtime, sink=None, settle: str = args.settle,
                  init_sink=None, mode: str = args.container_mode, dev_view: str = args.dev_view):
@@ -260,8 +275,8 @@ def main():
             paths = None
             if dev_view == "specs":
                 paths = ["/dev/kfd"] + [p for g in (groups if pod else [groups[d.rank]]) for p in g]
-            r = start_container(mine_ord, timeout_s=args.container_timeout, runtime=runtime, mounts=mounts,
-                                device_paths=paths)
+            r = blocking(start_container, mine_ord, timeout_s=args.container_timeout, runtime=runtime, mounts=mounts,
+                         device_paths=paths)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
             phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
@@ -279,7 +294,7 @@ def main():
         # N containers exiting together may be torn down one after another: allow
         # ~0.25 s each (measured ~0.15 s), capped so a stuck entry cannot stall the run
         cap = min(3.0, 0.25 + 0.25 * max(len(lingering), n))  # one process with N GPUs tears down N VMs
-        waited = wait_kfd_released(lingering, timeout_s=cap) if settle == "kfd" else 0.0
+        waited = blocking(wait_kfd_released, lingering, timeout_s=cap) if settle == "kfd" else 0.0
         if record:
             settle_ms.append(waited)
         sp, tm, trt = slowest[4]   # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC)
@@ -388,6 +403,11 @@ def main():
                  "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
                  "container_mode": args.container_mode,
                  "container_dev_view": args.dev_view,
+                 "health_loop": ({"pulse_s": args.health_pulse, "sweeps": impl.monitor.sweeps,
+                                  "sweep_ms_last": round(impl.monitor.last_sweep_ms, 3),
+                                  "unhealthy": sorted(k for k, v in impl.monitor.snapshot().items()
+                                                      if v.health != "Healthy")}
+                                 if args.health_pulse > 0 and not args.fixture else None),
                  f"latency_p50_ms_dev_view_{other_view}": round(pct(vis_lat, .5), 3) if vis_lat else None,
                  f"latency_p50_ms_container_mode_{other_mode}": round(pct(other_mode_lat, .5), 3) if other_mode_lat
                  else None,
