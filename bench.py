@@ -414,6 +414,8 @@ def main():
                  "latency_p50_ms_node_view_emulated": round(pct(nv_lat, .5), 3) if nv_lat else None,
                  "node_view_emulated_runtime_init_p50_ms": round(pct(nv_init, .5), 3) if nv_init else None,
                  "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
+                 # per timed step, for tail analysis: latency, ROCr init, settle wait before the next step
+                 "steps_ms": [[round(a, 2), round(b, 2), round(c, 1)] for a, b, c in zip(lat_ms, rt_ms, settle_ms)],
                  "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
                                              "gpu_runtime_init": round(pct(rt_ms, .5), 3),
                                              "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
