@@ -133,6 +133,42 @@ static void test_errors() {
   CHECK(r.short_circuit && r.ids.size() == 2);
 }
 
+// xGMI link down at run time (AllocatorOptions::degraded_links): the pair
+// scores as the worst link, so packing avoids it; the search and the
+// reference BFS still agree on the re-weighted matrix.
+static void test_degraded_links(const std::string& ref) {
+  auto topo = KfdTopology::load(ref + "/topo-mi210-xgmi-pcie/nodes");
+  if (topo.nodes().empty()) {
+    ++g_skip;
+    return;
+  }
+  auto devs = synthetic_devices(8, 1, 2, 1, 8);
+  HiveAllocator a;
+  CHECK(a.init(devs, topo).empty());
+  auto all = ids_of(devs);
+  auto before = a.allocate(all, {}, 2);
+  CHECK(before.error.empty() && before.ids.size() == 2);
+  // degrade the chosen pair (physical GPU keys = unique_id = GPU index here)
+  AllocatorOptions opt;
+  std::string ka, kb;
+  for (auto& d : devs) {
+    if (d.id == before.ids[0]) ka = d.unique_id;
+    if (d.id == before.ids[1]) kb = d.unique_id;
+  }
+  opt.degraded_links = {{kb, ka}};  // order does not matter
+  CHECK(a.init(devs, topo, opt).empty());
+  auto after = a.allocate(all, {}, 2);
+  CHECK(after.error.empty() && as_set(after.ids) != as_set(before.ids));
+  CHECK(after.weight <= before.weight);  // another same-hive pair is as good
+  auto forced = a.allocate(before.ids, {}, 2);  // only the degraded pair available
+  CHECK(forced.short_circuit && as_set(forced.ids) == as_set(before.ids));
+  for (int k = 2; k <= 7; ++k) {
+    auto e = a.allocate(all, {}, k);
+    auto b = a.reference_allocate(all, {}, k);
+    CHECK(e.weight == b.weight);
+  }
+}
+
 int main(int argc, char** argv) {
   std::string repo = argc > 1 ? argv[1] : "testdata";
   std::string ref = argc > 2 ? argv[2] : "/root/reference/testdata";
@@ -140,6 +176,7 @@ int main(int argc, char** argv) {
   test_parsers(ref);
   test_allocator_reference_contract(ref);
   test_errors();
+  test_degraded_links(ref);
   std::printf("test_core: %d passed, %d failed, %d skipped\n", g_pass, g_fail, g_skip);
   return g_fail ? 1 : 0;
 }
