@@ -385,7 +385,9 @@ def test_end_to_end_admission_container_ready(inv, ordinals):
     async def go(tmp):
         k = FakeKubelet(tmp)
         await k.start()
-        impl = ContainerImpl("single", "/sys", HealthConfig(exporter_socket=None, liveness=True), inventory=acc)
+        # the health DaemonSet's sources: liveness + amd-smi ECC, events and xGMI link state
+        impl = ContainerImpl("single", "/sys", HealthConfig(exporter_socket=None, liveness=True, smi_ecc=True,
+                                                            smi_events=True, smi_xgmi=True), inventory=acc)
         mgr = PluginManager(impl, ManagerConfig(pulse_s=0.5, plugin_dir=tmp, handle_signals=False))
         t = asyncio.create_task(mgr.run())
         try:
@@ -403,6 +405,9 @@ def test_end_to_end_admission_container_ready(inv, ordinals):
             # the health loop (with liveness) must keep every device Healthy
             st = k.resources["amd.com/gpu"]
             assert all(h == "Healthy" for h in st.devices.values())
+            mon = impl.monitor
+            assert mon.sweeps >= 1 and mon.fabric is not None and not mon.fabric.error, mon.fabric.error
+            assert mon.degraded_links() == frozenset()
         finally:
             mgr.request_stop()
             await t
