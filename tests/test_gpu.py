@@ -265,9 +265,10 @@ def test_container_with_node_view_mounts(tmp_path, ordinals):
 @pytest.mark.parametrize("runtime", ["hsa", "hip"])
 def test_container_dev_view_hides_unallocated_gpus(inv, ordinals, runtime):
     """The fake runtime's /dev view is what ROCr sees: with the GPU's render node
-    in the DeviceSpecs the container runs on it; with a render node that is not
-    this GPU's, ROCr's thunk finds no GPU at all (ENOENT, as in a container
-    without the node) and the container does not become ready."""
+    in the DeviceSpecs the container runs on it; handed a node the test process
+    cannot open (another tenant's GPU on a 1-GPU box) the thunk finds no GPU
+    and the container does not become ready; handed another GPU the process can
+    open (a multi-GPU box) it runs on exactly that one."""
     from rocm_k8s_device_plugin_amd.container_runtime import start_container, wait_kfd_released
     dev_id, o = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
     g = inv.by_id[dev_id]
@@ -276,12 +277,21 @@ def test_container_dev_view_hides_unallocated_gpus(inv, ordinals, runtime):
     assert ok.doc["hip_device_count"] == 1
     assert ok.doc["devices"][0]["pci_bus_id"].lower() == dev_id.lower()
     wait_kfd_released(ok.kfd_lingering)
-    other = [d for d in inv.devices if d.render_minor >= 0 and d.render_minor != g.render_minor]
-    wrong = ["/dev/kfd"] + (other[0].dev_paths() if other else ["/dev/dri/renderD1"])
+    others = [d for d in inv.devices if d.render_minor >= 0 and d.render_minor != g.render_minor]
+    hidden = [d for d in others if d.id not in ordinals]       # render node not openable here
+    wrong = ["/dev/kfd"] + (hidden[0].dev_paths() if hidden else ["/dev/dri/renderD1"])
     bad = start_container([o], timeout_s=120, device_paths=wrong, runtime=runtime)
     wait_kfd_released(bad.kfd_lingering)
     assert not bad.ok
     assert bad.doc.get("hip_device_count", 0) == 0, bad.doc
+    reachable = [d for d in others if d.id in ordinals]
+    if reachable:
+        h = reachable[0]
+        r = start_container([ordinals[h.id]], timeout_s=120, device_paths=["/dev/kfd"] + h.dev_paths(),
+                            runtime=runtime)
+        wait_kfd_released(r.kfd_lingering)
+        assert r.ok and r.doc["hip_device_count"] == 1, r.error
+        assert r.doc["devices"][0]["pci_bus_id"].lower() == h.id.lower()
 
 
 def test_chip_sweep_covers_every_cu_and_xcd(ordinals):
