@@ -225,6 +225,21 @@ def test_peer_probe_self_copy(ordinals):
     assert rep.summary()["pairs_ok"] == 1
 
 
+def test_peer_probe_xgmi_pair(ordinals):
+    """H2 over a real link: on a box with 2+ accessible MI355X GPUs (the 1-GPU
+    test box has one: skipped), every ordered pair is copied and verified over
+    xGMI, one hop."""
+    from rocm_k8s_device_plugin_amd.health.peer import probe_peers
+    ords = sorted(ordinals.values())
+    if len(ords) < 2:
+        pytest.skip("one accessible GPU")
+    rep = probe_peers(ords[:2], nbytes=32 << 20, reps=3, timeout_s=120)
+    assert rep.ok, rep
+    cross = [p for p in rep.pairs if p["src"] != p["dst"]]
+    assert len(cross) == 2 and all(p["mismatches"] == 0 for p in cross), cross
+    assert rep.summary()["link_types"] == ["xgmi"], rep.summary()
+
+
 def test_smi_event_watcher_subscribes(inv):
     """amd-smi event notification starts on the real GPU and drains without error.
 
