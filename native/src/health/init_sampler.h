@@ -172,6 +172,15 @@ class InitSampler {
     } else {
       what = "?";
     }
+    if (state == 'D') {
+      // uninterruptible sleep: name the kernel function it waits in
+      // (/proc/self/task/<tid>/wchan is readable by the task's owner)
+      std::snprintf(path, sizeof(path), "/proc/self/task/%d/wchan", tid);
+      if (read_small(path, buf, sizeof(buf)) && buf[0] && std::strcmp(buf, "0") != 0) {
+        what += " @";
+        for (const char* c = buf; *c && *c != '\n' && what.size() < 200; ++c) what += *c;
+      }
+    }
     std::string key = tid == main_tid_ ? "main " : "aux ";
     key += state;
     key += ' ';
