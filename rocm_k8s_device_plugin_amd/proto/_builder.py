@@ -9,24 +9,24 @@ each module — and materialised through ``descriptor_pool`` +
 """
 from __future__ import annotations
 
+import hashlib
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
-from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+from google.protobuf import descriptor_pool, message_factory
 
-F = descriptor_pb2.FieldDescriptorProto
-
+# FieldDescriptorProto.Type / .Label values (descriptor.proto); spelled out so
+# that a plugin start with a warm cache never imports descriptor_pb2 (~18 ms)
 _SCALARS = {
-    "string": F.TYPE_STRING,
-    "bool": F.TYPE_BOOL,
-    "int32": F.TYPE_INT32,
-    "int64": F.TYPE_INT64,
-    "uint32": F.TYPE_UINT32,
-    "uint64": F.TYPE_UINT64,
-    "bytes": F.TYPE_BYTES,
-    "double": F.TYPE_DOUBLE,
-    "float": F.TYPE_FLOAT,
+    "double": 1, "float": 2, "int64": 3, "uint64": 4, "int32": 5, "bool": 8, "string": 9, "bytes": 12,
+    "uint32": 13,
 }
+_TYPE_MESSAGE, _TYPE_ENUM = 11, 14
+_LABEL_OPTIONAL, _LABEL_REPEATED = 1, 3
+
+# serialized FileDescriptorProtos keyed by a hash of the declarations above
+_CACHE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_fdcache")
 
 
 @dataclass
@@ -73,6 +73,38 @@ def build_file(package: str, filename: str, messages: Sequence[Message], service
                pool: Optional[descriptor_pool.DescriptorPool] = None):
     """Register the file in `pool` and return {message name: class}."""
     pool = pool or descriptor_pool.Default()
+    try:
+        fd_desc = pool.FindFileByName(filename)
+    except KeyError:
+        fd_desc = None
+    if fd_desc is None:
+        key = hashlib.sha1(repr((package, filename, list(messages), list(services), list(enums), list(deps)))
+                           .encode()).hexdigest()[:16]
+        cached = os.path.join(_CACHE_DIR, f"{filename.replace('/', '_')}.{key}.pb")
+        try:
+            with open(cached, "rb") as f:
+                pool.AddSerializedFile(f.read())
+        except OSError:
+            blob = _file_proto(package, filename, messages, services, enums, deps).SerializeToString()
+            pool.AddSerializedFile(blob)
+            try:  # best effort: a read-only install just builds every time
+                os.makedirs(_CACHE_DIR, exist_ok=True)
+                tmp = f"{cached}.{os.getpid()}.tmp"
+                with open(tmp, "wb") as f:
+                    f.write(blob)
+                os.replace(tmp, cached)
+            except OSError:
+                pass
+        fd_desc = pool.FindFileByName(filename)
+    classes: Dict[str, type] = {}
+    for m in messages:
+        classes[m.name] = message_factory.GetMessageClass(pool.FindMessageTypeByName(f"{package}.{m.name}"))
+    return classes, fd_desc
+
+
+def _file_proto(package: str, filename: str, messages: Sequence[Message], services: Sequence[Service],
+                enums: Sequence[EnumDef], deps: Sequence[str]):
+    from google.protobuf import descriptor_pb2
     fdp = descriptor_pb2.FileDescriptorProto(name=filename, package=package, syntax="proto3")
     fdp.dependency.extend(deps)
     for e in enums:
@@ -89,22 +121,22 @@ def build_file(package: str, filename: str, messages: Sequence[Message], service
                 k, v = f.type[4:-1].split(",")
                 entry = md.nested_type.add(name=_camel(f.name) + "Entry")
                 entry.options.map_entry = True
-                entry.field.add(name="key", number=1, label=F.LABEL_OPTIONAL, type=_SCALARS[k.strip()],
+                entry.field.add(name="key", number=1, label=_LABEL_OPTIONAL, type=_SCALARS[k.strip()],
                                 json_name="key")
-                entry.field.add(name="value", number=2, label=F.LABEL_OPTIONAL, type=_SCALARS[v.strip()],
+                entry.field.add(name="value", number=2, label=_LABEL_OPTIONAL, type=_SCALARS[v.strip()],
                                 json_name="value")
-                fd.label = F.LABEL_REPEATED
-                fd.type = F.TYPE_MESSAGE
+                fd.label = _LABEL_REPEATED
+                fd.type = _TYPE_MESSAGE
                 fd.type_name = f".{package}.{m.name}.{entry.name}"
                 continue
-            fd.label = F.LABEL_REPEATED if f.repeated else F.LABEL_OPTIONAL
+            fd.label = _LABEL_REPEATED if f.repeated else _LABEL_OPTIONAL
             if f.type in _SCALARS:
                 fd.type = _SCALARS[f.type]
             elif f.type in enum_names:
-                fd.type = F.TYPE_ENUM
+                fd.type = _TYPE_ENUM
                 fd.type_name = f".{package}.{f.type}"
             else:
-                fd.type = F.TYPE_MESSAGE
+                fd.type = _TYPE_MESSAGE
                 fd.type_name = f.type if f.type.startswith(".") else f".{package}.{f.type}"
     for s in services:
         sd = fdp.service.add(name=s.name)
@@ -113,16 +145,7 @@ def build_file(package: str, filename: str, messages: Sequence[Message], service
                           input_type=mt.input if mt.input.startswith(".") else f".{package}.{mt.input}",
                           output_type=mt.output if mt.output.startswith(".") else f".{package}.{mt.output}",
                           server_streaming=mt.server_streaming)
-    try:
-        fd_desc = pool.FindFileByName(filename)
-    except KeyError:
-        fd_desc = pool.Add(fdp)
-        if not hasattr(fd_desc, "message_types_by_name"):
-            fd_desc = pool.FindFileByName(filename)
-    classes: Dict[str, type] = {}
-    for m in messages:
-        classes[m.name] = message_factory.GetMessageClass(pool.FindMessageTypeByName(f"{package}.{m.name}"))
-    return classes, fd_desc
+    return fdp
 
 
 def _lower_camel(s: str) -> str:
