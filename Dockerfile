@@ -10,7 +10,8 @@ WORKDIR /src
 COPY native native
 COPY rocm_k8s_device_plugin_amd rocm_k8s_device_plugin_amd
 RUN python3 rocm_k8s_device_plugin_amd/_build.py && \
-    rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe --help >/dev/null
+    rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe --help >/dev/null && \
+    python3 -c "import rocm_k8s_device_plugin_amd.proto.deviceplugin, rocm_k8s_device_plugin_amd.proto.metricssvc"
 
 FROM ${ROCM_IMAGE}
 ARG GIT_DESCRIBE=dev
