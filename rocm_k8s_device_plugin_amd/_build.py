@@ -42,11 +42,18 @@ STAMP = REPO_DIR / "build" / ".native.stamp"
 _checked: set = set()
 
 
+# native/tools/ holds measurement programs compiled ad hoc on the GPU box; only
+# these two are part of the CMake build (the container-entrypoint emulation)
+_CMAKE_TOOLS = {"probe_emu.cpp", "path_interpose.h"}
+
+
 def _source_digest() -> str:
-    """Content hash of every native source (paths + bytes)."""
+    """Content hash of every native source the CMake build uses (paths + bytes)."""
     import hashlib
     h = hashlib.sha1()
     for p in sorted(NATIVE_DIR.rglob("*")):
+        if p.parent.name == "tools" and p.parent.parent == NATIVE_DIR and p.name not in _CMAKE_TOOLS:
+            continue
         if p.is_file() and p.suffix in {".cpp", ".h", ".hip", ".txt"}:
             h.update(str(p.relative_to(NATIVE_DIR)).encode())
             h.update(p.read_bytes())

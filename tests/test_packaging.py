@@ -141,6 +141,9 @@ def test_build_stamp_follows_content_not_mtime(tmp_path, monkeypatch):
     assert _build._up_to_date([out])
     os.utime(f, (1e10, 1e10))                      # touched, same content
     assert _build._up_to_date([out])
+    (src / "tools").mkdir()
+    (src / "tools" / "adhoc_measurement.cpp").write_text("int m;\n")   # compiled on the box, not by CMake
+    assert _build._up_to_date([out])
     f.write_text("int a = 1;\n")                   # edited
     assert not _build._up_to_date([out])
     assert not _build._up_to_date([tmp_path / "missing.so"])
