@@ -37,7 +37,7 @@ from typing import Callable, Dict, Mapping, Optional, Tuple
 
 from ..ops.native import core
 from ..proto import deviceplugin as dp
-from ..topology import Inventory, hip_ordinals, kfd_busy_gpu_ids
+from ..topology import Inventory, KfdBusyUnknown, hip_ordinals, kfd_busy_gpu_ids
 from ..utils import log
 from ..utils.trace import TRACER
 from . import exporter
@@ -223,7 +223,12 @@ class HealthMonitor:
     def _idle_devices(self, dev_ids) -> set:
         """Devices whose kfd gpu_id has no user queue in any process right now."""
         own = self.prober.own_kfd_entries if self.prober is not None else ()
-        busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
+        try:
+            busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
+        except KfdBusyUnknown as e:
+            # cannot tell which GPUs run work: sweep none (the sweep holds every CU)
+            _log.warning("full-chip sweep skipped: %s", e)
+            return set()
         idle = set()
         for dev_id in dev_ids:
             d = self.inv.by_id.get(dev_id)

@@ -185,11 +185,18 @@ def hip_ordinals(inv: Inventory, dev_root: str = "/dev", check_access: bool = Tr
     return {d.id: pos[d.node_id] for d in inv.devices if d.node_id in pos}
 
 
+class KfdBusyUnknown(Exception):
+    """Another process' kfd queues could not be read (permissions): which GPUs
+    are busy is unknown, so callers must treat every GPU as busy."""
+
+
 def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
     """kfd gpu_ids that currently have user queues, from any process on the host
     (``/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/gpuid``) except the ``exclude``d
     entries (the plugin's own probe server). A GPU without queues runs no work;
-    the liveness loop runs its full-chip sweep only on those."""
+    the liveness loop runs its full-chip sweep only on those. Raises
+    KfdBusyUnknown when a process' queues are unreadable (not when it merely
+    exited meanwhile)."""
     busy = set()
     root = os.path.join(sysfs_root, "class/kfd/kfd/proc")
     try:
@@ -203,12 +210,16 @@ def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
         qdir = os.path.join(root, pid, "queues")
         try:
             qids = os.listdir(qdir)
+        except PermissionError as e:
+            raise KfdBusyUnknown(f"{qdir}: {e}") from e
         except OSError:
-            continue
+            continue            # the process exited meanwhile
         for q in qids:
             try:
                 with open(os.path.join(qdir, q, "gpuid")) as f:
                     busy.add(int(f.read().strip() or 0))
+            except PermissionError as e:
+                raise KfdBusyUnknown(f"{qdir}/{q}: {e}") from e
             except (OSError, ValueError):
                 continue
     return busy

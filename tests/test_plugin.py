@@ -798,3 +798,25 @@ def test_cli_dry_run_reports_node(tmp_path):
     assert four["one_hive"] and four["allreduce_bound_gbs"] > 0     # a whole hive of 4
     assert not r["allocations"]["8"]["one_hive"]                    # 8 spans both hives
     assert not os.path.exists(tmp_path / "dp" / "amd.com_gpu")      # nothing served
+
+
+def test_chip_sweep_skipped_when_kfd_queues_unreadable(tmp_path, monkeypatch):
+    """Without permission to read another process' kfd queues the plugin cannot
+    tell idle GPUs from busy ones: no device is treated as idle."""
+    from rocm_k8s_device_plugin_amd import topology as T
+    fi = make_mi355x_node(tmp_path / "n")
+    proc = fi.sysfs / "class/kfd/kfd/proc/4242/queues"
+    proc.mkdir(parents=True)
+    real_listdir = os.listdir
+
+    def listdir(p):
+        if str(p).endswith("4242/queues"):
+            raise PermissionError(13, "Permission denied")
+        return real_listdir(p)
+
+    monkeypatch.setattr(T.os, "listdir", listdir)
+    with pytest.raises(T.KfdBusyUnknown):
+        T.kfd_busy_gpu_ids(str(fi.sysfs))
+    inv = discover(str(fi.sysfs))
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None))
+    assert mon._idle_devices([d.id for d in inv.devices]) == set()
