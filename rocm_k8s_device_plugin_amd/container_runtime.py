@@ -29,7 +29,7 @@ import re
 import subprocess
 import time
 from dataclasses import dataclass
-from typing import FrozenSet, Iterable, List, Mapping, Optional, Sequence, Set
+from typing import FrozenSet, Iterable, List, Optional, Sequence, Set
 
 from .health.liveness import _VISIBILITY_VARS
 from .ops.native import probe_executable
@@ -157,6 +157,3 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
     return ContainerResult(ok, t0, int(doc.get("t_ready_ns", 0)), wall, doc, err,
                            frozenset(kfd_processes() - before))
 
-
-def ordinals_for_minors(minors: Sequence[int], minor_to_ordinal: Mapping[int, int]) -> List[int]:
-    return [minor_to_ordinal[m] for m in minors]

@@ -312,11 +312,6 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
     return info
 
 
-def make_single_gpu_node(root: os.PathLike, **kw) -> FixtureInfo:
-    kw.setdefault("num_gpus", 1)
-    kw.setdefault("numa_nodes", 1)
-    return make_mi355x_node(root, **kw)
-
 
 def wrap_kfd_topology(topology_dir: os.PathLike, root: os.PathLike) -> FixtureInfo:
     """A node sysfs around a captured kfd topology (e.g. the reference's
