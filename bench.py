@@ -49,6 +49,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "p50 Allocate→ContainerReady latency; GPUs advertised at 1/2/4/8 MI355X"
+STUB_PROBE = os.path.join(REPO, "rocm_k8s_device_plugin_amd", "testing", "stub_probe.py")
 
 
 def parse_args():
@@ -258,14 +259,7 @@ def main():
             payload = None
         payload = d.bcast(payload)
         t0, ordl, tot, amsl, ids, mounts, groups = payload
-        if args.fixture:
-            import subprocess
-            ts = time.monotonic_ns()
-            subprocess.run(["/bin/true"])
-            tr = time.monotonic_ns()
-            mine = (True, tr, 0.0, "", (ts, ts, tr))
-            lingering = frozenset()
-        elif mode == "pod" and d.rank != 0:
+        if mode == "pod" and d.rank != 0:
             # the pod's single container runs on rank 0; other ranks only keep step
             mine = (True, 0, 0.0, "", (0, 0, 0))
             lingering = frozenset()
@@ -275,8 +269,11 @@ def main():
             paths = None
             if dev_view == "specs":
                 paths = ["/dev/kfd"] + [p for g in (groups if pod else [groups[d.rank]]) for p in g]
-            r = blocking(start_container, mine_ord, timeout_s=args.container_timeout, runtime=runtime, mounts=mounts,
-                         device_paths=paths)
+            # CPU rehearsal (--fixture): the stub probe stands in for the GPU entrypoint,
+            # through the same runtime path (/dev view, per-GPU split, result parsing)
+            stub = dict(exe=STUB_PROBE, argv_prefix=[sys.executable]) if args.fixture else {}
+            r = blocking(start_container, mine_ord, timeout_s=args.container_timeout, runtime=runtime,
+                         mounts=mounts if not args.fixture else (), device_paths=paths, **stub)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
             phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
@@ -323,7 +320,7 @@ def main():
     elapsed = d.max(elapsed)
     hip_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
     other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
-    if not args.fixture and n > 1:
+    if n > 1:
         for _ in range(args.mode_compare):
             one_step(False, sink=other_mode_lat, mode=other_mode)
     if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
@@ -446,7 +443,7 @@ def main():
             "dtype": "fp32",
             "data": ("synthetic pod specs requesting amd.com/gpu=N; real /sys discovery, fake kubelet over UDS, "
                      "container = fresh process whose /dev is the Allocate DeviceSpecs running the MFMA liveness kernel"
-                     if not args.fixture else "synthetic 8xMI355X sysfs fixture; no-op containers (CPU only)"),
+                     if not args.fixture else "synthetic 8xMI355X sysfs fixture; stub-probe containers (CPU only)"),
             "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
                        "global_batch": n, "seq_len": None,
                        "parallelism": (f"{n} GPUs advertised, 1 pod requesting {n}, " +

@@ -110,7 +110,8 @@ def mount_redirects(mounts: Iterable) -> str:
 
 def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int = 4,
                     exe: Optional[str] = None, runtime: str = "hsa", mounts: Iterable = (),
-                    device_paths: Optional[Sequence[str]] = None) -> ContainerResult:
+                    device_paths: Optional[Sequence[str]] = None,
+                    argv_prefix: Sequence[str] = ()) -> ContainerResult:
     """Run the container entrypoint restricted to `ordinals`; block until ready/exit.
 
     runtime "hsa": the entrypoint launches the MFMA kernel straight through ROCr
@@ -118,6 +119,7 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
     typical HIP/PyTorch application pays before its first kernel.
     device_paths: the container's device nodes from the Allocate DeviceSpecs;
     the process then sees only those GPUs (module docstring).
+    exe / argv_prefix: another entrypoint (CPU rehearsals run the stub probe).
     """
     env = {k: v for k, v in os.environ.items() if k not in _VISIBILITY_VARS}
     dev_view = device_paths is not None and runtime in ("hsa", "hip")
@@ -136,7 +138,7 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
             raise ValueError("mounts can only be applied to the HSA entrypoint (mount emulation build)")
         runtime = "mountemu"
         env["MI355X_INITPROF_REDIRECT"] = redirect
-    argv = [exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
+    argv = [*argv_prefix, exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
             "--iters", str(iters), "--timeout", str(min(timeout_s, 30.0))]
     before = kfd_processes()
     t0 = time.monotonic_ns()

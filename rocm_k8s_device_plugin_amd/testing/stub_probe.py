@@ -106,11 +106,21 @@ def main(argv):
         print("segfault-ish noise")
         return 139
     t = time.monotonic_ns()
-    dev = _device(0, mode, nonce)
-    doc = {"ok": dev["ok"], "hip_device_count": 1, "identify": False, "t_start_ns": t, "t_runtime_ns": t,
-           "t_ready_ns": t, "devices": [dev]}
+    # as a container entrypoint (bench.py --fixture): one result per --devices
+    # entry; with the fake runtime's /dev view the visible GPU count is the
+    # number of render nodes it allows (what ROCr's thunk would find)
+    wanted = ["0"]
+    if "--devices" in argv:
+        wanted = [x for x in argv[argv.index("--devices") + 1].split(",") if x]
+    allow = os.environ.get("MI355X_DEV_ALLOW")
+    count = (sum(1 for p in allow.split(";") if "/renderD" in p) if allow is not None
+             else max(1, len(wanted)))
+    devs = [_device(int(o), mode, nonce + i) for i, o in enumerate(wanted)]
+    ok = all(d["ok"] for d in devs)
+    doc = {"ok": ok, "hip_device_count": count, "identify": False, "t_start_ns": t, "t_runtime_ns": t,
+           "t_ready_ns": time.monotonic_ns(), "devices": devs}
     print(json.dumps(doc))
-    return 0 if dev["ok"] else 1
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":
