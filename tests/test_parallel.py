@@ -101,3 +101,8 @@ def test_bench_fixture_reports_fabric_and_collectives():
     fab, rccl = d["extra"]["fabric"], d["extra"]["rccl"]
     assert fab["one_hive"] and fab["pairs"]["xgmi"] == 1
     assert rccl["ok"] and rccl["backend"] == "gloo" and rccl["busbw_gbs"]["all_reduce"] > 0
+    # the containers went through the runtime path: the pod's process saw both GPUs'
+    # render nodes, and the per-GPU comparison split them one per rank
+    e = d["extra"]
+    assert e["container_dev_view"] == "specs" and e["latency_p50_ms_container_mode_per-gpu"] > 0
+    assert len(e["steps_ms"]) == 2
