@@ -40,6 +40,22 @@ def build_parser() -> flags.GoFlagParser:
     return p
 
 
+HOSTNAME_FILE = "/labeller/hostname"
+
+
+def node_name_from(ns, hostname_file: str = HOSTNAME_FILE) -> str:
+    """-node_name / $DS_NODE_NAME (what the reference's code reads,
+    cmd/k8s-node-labeller/main.go:551), else the file its README documents
+    (cmd/k8s-node-labeller/README.md:10) but the code never read."""
+    if ns.node_name:
+        return ns.node_name
+    try:
+        with open(hostname_file) as f:
+            return f.read().strip()
+    except OSError:
+        return ""
+
+
 def enabled_labels(ns) -> dict:
     return {k: bool(getattr(ns, f"label_{k}")) for k in C.SUPPORTED_LABELS + EXTRA_LABELS}
 
@@ -58,15 +74,16 @@ def main(argv: Optional[List[str]] = None) -> int:
     if ns.dry_run:
         print(json.dumps(gen(), indent=1, sort_keys=True))
         return 0
-    if not ns.node_name:
-        logger.error("node name unknown: set DS_NODE_NAME or -node_name")
+    node = node_name_from(ns)
+    if not node:
+        logger.error("node name unknown: set DS_NODE_NAME or -node_name (or mount %s)", HOSTNAME_FILE)
         return 1
     try:
         client = KubeClient(get_config(ns.kubeconfig))
     except Exception as e:
         logger.error("unable to set up kubernetes client: %s", e)
         return 1
-    lab = NodeLabeller(client, ns.node_name, gen, resync_s=ns.resync)
+    lab = NodeLabeller(client, node, gen, resync_s=ns.resync)
     for s in (signal.SIGTERM, signal.SIGINT):
         signal.signal(s, lambda *_: lab.stop())
     lab.run(once=ns.resync <= 0)

@@ -303,3 +303,17 @@ def test_label_values_are_valid_kubernetes_values():
         s = L.sanitize_label_value(v)
         assert len(s) <= 63 and ok.match(s), (v, s)
     assert L.sanitize_label_value("6.12.12") == "6.12.12"
+
+
+def test_node_name_sources(tmp_path, monkeypatch):
+    """-node_name / $DS_NODE_NAME first, else the hostname file the reference's
+    README documents (cmd/k8s-node-labeller/README.md:10)."""
+    from rocm_k8s_device_plugin_amd.cli import node_labeller as cli
+    monkeypatch.delenv("DS_NODE_NAME", raising=False)
+    ns = cli.build_parser().parse_args([])
+    f = tmp_path / "hostname"
+    assert cli.node_name_from(ns, str(f)) == ""
+    f.write_text("gpu-node-7\n")
+    assert cli.node_name_from(ns, str(f)) == "gpu-node-7"
+    ns = cli.build_parser().parse_args(["-node_name", "n1"])
+    assert cli.node_name_from(ns, str(f)) == "n1"
