@@ -286,7 +286,10 @@ class HealthMonitor:
         if self.cfg.liveness and self.prober is not None:
             ords = {k: v for k, v in self.ordinals().items() if k in reasons}
             outcomes = await self._liveness(ords)
+            from ..utils.metrics import REGISTRY
             for dev_id, o in outcomes.items():
+                REGISTRY.set("mi355x_dp_liveness_probe_ms", float(o.latency_ms),
+                             help="last liveness probe round trip", device=dev_id)
                 tr = self._track[dev_id]
                 if o.ok:
                     tr.fails, tr.oks = 0, tr.oks + 1
@@ -328,6 +331,10 @@ class HealthMonitor:
                                  "; ".join(v.reasons))
             self.version += 1
         self._snapshot = new
+        from ..utils.metrics import REGISTRY
+        for dev, v in new.items():
+            REGISTRY.set("mi355x_dp_device_healthy", 1.0 if v.health == dp.HEALTHY else 0.0,
+                         help="1 if the device is advertised Healthy", device=dev)
         self.sweeps += 1
         self.last_sweep_ms = (time.perf_counter() - t0) * 1e3
         return changed

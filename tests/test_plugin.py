@@ -820,3 +820,26 @@ def test_chip_sweep_skipped_when_kfd_queues_unreadable(tmp_path, monkeypatch):
     inv = discover(str(fi.sysfs))
     mon = HealthMonitor(inv, HealthConfig(exporter_socket=None))
     assert mon._idle_devices([d.id for d in inv.devices]) == set()
+
+
+def test_health_metrics_per_device(tmp_path):
+    """After a sweep every device has a health gauge (and a probe latency with liveness)."""
+    from rocm_k8s_device_plugin_amd.utils.metrics import REGISTRY
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ctl, prober = _stub_prober(tmp_path, {"2": "fail"})
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=1), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+
+    async def go():
+        try:
+            await mon.check_once()
+        finally:
+            await mon.close()
+
+    run(go())
+    text = REGISTRY.render()
+    bad = inv.devices[2].id
+    assert f'mi355x_dp_device_healthy{{device="{bad}"}} 0' in text
+    assert f'mi355x_dp_device_healthy{{device="{inv.devices[0].id}"}} 1' in text
+    assert f'mi355x_dp_liveness_probe_ms{{device="{bad}"}}' in text
