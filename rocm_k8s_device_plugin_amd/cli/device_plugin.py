@@ -190,6 +190,15 @@ async def dry_run_report(impl: Optional[DeviceImpl], sweep: bool) -> dict:
         out["resources"][f"{C.RESOURCE_NAMESPACE}/{r}"] = res
     if hasattr(impl, "inv"):
         out["warnings"] = list(impl.inv.warnings)
+    if hasattr(impl, "list_strategies"):
+        out["device_list_strategy"] = list(impl.list_strategies)
+        if getattr(impl, "_cdi", False):
+            out["cdi_spec_dir"] = impl.cdi_spec_dir
+    mon = getattr(impl, "monitor", None)
+    if mon is not None and getattr(mon, "fabric", None) is not None:
+        fab = mon.fabric
+        out["xgmi"] = {"readings": fab.readings, "error": fab.error,
+                       "degraded_pairs": [list(p) for p in sorted(fab.degraded)], "links_down": fab.links_down}
     await impl.close()
     return out
 
