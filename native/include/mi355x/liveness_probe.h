@@ -42,6 +42,10 @@ typedef struct {
   int pci_domain, pci_bus, pci_device;
   int cu_count;
   uint64_t total_mem;
+  // kept-queue path: the verdict belongs to a dispatch submitted by an earlier
+  // probe (1), and how long the current outstanding dispatch has been pending
+  int late;
+  double pending_s;
   char error[160];
 } mi355x_probe_result;
 

@@ -424,13 +424,8 @@ bool setup_resources(const Agent& ag, ProbeResources& r, KernelInfo& k, mi355x_p
   return true;
 }
 
-// One AQL dispatch of the liveness kernel on r's queue, bounded wait, verdict.
-// Sets out->hip_error = -1 when the dispatch did not complete: r must then
-// never be freed (the kernel may still write to it).
-void dispatch_and_verify(const Agent& ag, ProbeResources& r, const KernelInfo& k, uint32_t nonce, double timeout_s,
-                         mi355x_probe_result* out) {
-  using clk = std::chrono::steady_clock;
-  const auto t_disp = clk::now();
+// Submits one AQL dispatch of the liveness kernel on r's queue (no wait).
+void submit_dispatch(ProbeResources& r, const KernelInfo& k, uint32_t nonce, int iters, mi355x_probe_result* out) {
   std::memset(r.h_out, 0xFF, MI355X_PROBE_OUT * sizeof(float));
   std::memset(r.h_meta, 0, 64);
   std::memset(r.kargs, 0, kKernargBytes);
@@ -438,7 +433,7 @@ void dispatch_and_verify(const Agent& ag, ProbeResources& r, const KernelInfo& k
   r.kargs->meta = r.h_meta;
   r.kargs->scratch = r.d_scratch;
   r.kargs->nonce = nonce;
-  r.kargs->iters = out->iters;
+  r.kargs->iters = iters;
   H().hsa_signal_store_screlease(r.sig, 1);  // a kept signal was left at 0 by the previous dispatch
 
   const uint64_t idx = H().hsa_queue_add_write_index_screlease(r.queue, 1);
@@ -463,25 +458,42 @@ void dispatch_and_verify(const Agent& ag, ProbeResources& r, const KernelInfo& k
   __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
                    __ATOMIC_RELEASE);
   H().hsa_signal_store_screlease(r.queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
-  out->dispatches = 1;
+  out->dispatches += 1;
+}
 
-  // bounded wait: a wedged device must come back as a verdict, not a hang
-  const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
+// Bounded wait for the dispatch submitted on r (nonce / iters as submitted),
+// then the verdict. Returns false, with out->hip_error = -1, if it has not
+// completed yet: r must then never be freed (the kernel may still write to it).
+bool wait_and_verify(const Agent& ag, ProbeResources& r, uint32_t nonce, int iters, double timeout_s,
+                     mi355x_probe_result* out) {
+  using clk = std::chrono::steady_clock;
+  const auto t_wait = clk::now();
+  const auto deadline = t_wait + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
   hsa_signal_value_t v = 1;
   while ((v = H().hsa_signal_wait_scacquire(r.sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
                                         HSA_WAIT_STATE_BLOCKED)) >= 1) {
     if (clk::now() > deadline) break;
   }
-  out->phase_us[3] = std::chrono::duration<double, std::micro>(clk::now() - t_disp).count();
+  out->phase_us[3] = std::chrono::duration<double, std::micro>(clk::now() - t_wait).count();
   if (v >= 1) {
     std::snprintf(out->error, sizeof(out->error), "dispatch did not complete within %.1fs", timeout_s);
     out->hip_error = -1;
-    return;
+    return false;
   }
   hsa_amd_profiling_dispatch_time_t dt{};
   if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, r.sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
     out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
-  mi355x::verify_tile(r.h_out, r.h_meta, nonce, out->iters, out);
+  out->nonce = nonce;
+  out->iters = iters;
+  mi355x::verify_tile(r.h_out, r.h_meta, nonce, iters, out);
+  return true;
+}
+
+// One dispatch, bounded wait, verdict (out->hip_error = -1 when it did not complete).
+void dispatch_and_verify(const Agent& ag, ProbeResources& r, const KernelInfo& k, uint32_t nonce, double timeout_s,
+                         mi355x_probe_result* out) {
+  submit_dispatch(r, k, nonce, out->iters, out);
+  wait_and_verify(ag, r, nonce, out->iters, timeout_s, out);
 }
 
 // Kept ("resident") per-device resources for mi355x_hsa_probe_keep(1).
@@ -490,25 +502,28 @@ struct Resident {
   bool ready = false;
   ProbeResources r;
   KernelInfo k;
+  // a dispatch that has not completed yet (a tenant's long kernel holds every
+  // CU, or the device hangs): the next probe waits for it instead of
+  // submitting another or abandoning the queue with its 181 MB save area
+  bool pending = false;
+  uint32_t pending_nonce = 0;
+  int pending_iters = 1;
+  std::chrono::steady_clock::time_point pending_since{};
 };
 std::mutex g_resident_mu;
 bool g_keep = false;
 std::vector<std::pair<int, std::unique_ptr<Resident>>> g_resident;
-// resources of timed-out dispatches: the kernel may still write to them, so
-// they are never freed (bounded by one per device per hang)
-std::vector<ProbeResources> g_abandoned;
 
-// Frees every kept device's resources (runtime shutdown); abandoned ones go
-// with the runtime itself.
+// Frees every kept device's resources (runtime shutdown); a slot whose
+// dispatch is still pending goes with the runtime itself.
 void release_residents() {
   std::lock_guard<std::mutex> lk(g_resident_mu);
   for (auto& e : g_resident) {
     std::lock_guard<std::mutex> lk2(e.second->mu);
-    if (e.second->ready) e.second->r.release();
+    if (e.second->ready && !e.second->pending) e.second->r.release();
     e.second->ready = false;
   }
   g_resident.clear();
-  g_abandoned.clear();
 }
 
 Resident* resident_slot(int ordinal) {
@@ -571,13 +586,29 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
       }
       slot->ready = true;
     }
-    dispatch_and_verify(ag, slot->r, slot->k, nonce, timeout_s, out);
-    if (out->hip_error == -1) {  // still running: abandon, never free
-      std::lock_guard<std::mutex> lk2(g_resident_mu);
-      g_abandoned.push_back(slot->r);
-      slot->r = ProbeResources{};
-      slot->ready = false;
-    } else if (!out->ok) {       // wrong tile or error: start from fresh resources next time
+    if (slot->pending) {
+      // the previous probe's dispatch is still outstanding: wait for it (it
+      // carries its own nonce), never stack a second one behind it
+      if (!wait_and_verify(ag, slot->r, slot->pending_nonce, slot->pending_iters, timeout_s, out)) {
+        const double s_out = std::chrono::duration<double>(clk::now() - slot->pending_since).count();
+        std::snprintf(out->error, sizeof(out->error), "dispatch pending for %.1fs (not completed)", s_out);
+        out->pending_s = s_out;
+        return finish();
+      }
+      slot->pending = false;
+      out->late = 1;  // verdict of the dispatch submitted by an earlier probe
+    } else {
+      submit_dispatch(slot->r, slot->k, nonce, out->iters, out);
+      if (!wait_and_verify(ag, slot->r, nonce, out->iters, timeout_s, out)) {
+        slot->pending = true;
+        slot->pending_nonce = nonce;
+        slot->pending_iters = out->iters;
+        slot->pending_since = t0;
+        out->pending_s = std::chrono::duration<double>(clk::now() - t0).count();
+        return finish();
+      }
+    }
+    if (!out->ok) {  // wrong tile or error: start from fresh resources next time
       slot->r.release();
       slot->ready = false;
     }

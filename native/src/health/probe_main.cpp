@@ -86,12 +86,13 @@ std::string device_json(const mi355x_probe_result& r) {
       "\"phase_us\":{\"code_object\":%.1f,\"queue\":%.1f,\"buffers\":%.1f,\"dispatch_wait\":%.1f},"
       "\"pci_bus_id\":\"%s\","
       "\"arch\":\"%s\",\"name\":\"%s\",\"uuid\":\"%s\",\"pci_domain\":%d,\"pci_bus\":%d,"
-      "\"pci_device\":%d,\"cu_count\":%d,\"total_mem\":%llu,\"error\":\"%s\"}",
+      "\"pci_device\":%d,\"cu_count\":%d,\"total_mem\":%llu,\"late\":%s,\"pending_s\":%.3f,\"error\":\"%s\"}",
       r.ordinal, r.ok ? "true" : "false", r.hip_error, r.mismatches, r.nonce, r.xcc_id, r.hw_id, r.iters,
       r.dispatches, r.kfd_node_id, r.runtime, r.kernel_us, r.setup_us, r.total_us, r.phase_us[0], r.phase_us[1],
       r.phase_us[2], r.phase_us[3], json_escape(r.pci_bus_id).c_str(), json_escape(r.arch).c_str(),
       json_escape(r.name).c_str(), json_escape(r.uuid).c_str(), r.pci_domain, r.pci_bus, r.pci_device,
-      r.cu_count, static_cast<unsigned long long>(r.total_mem), json_escape(r.error).c_str());
+      r.cu_count, static_cast<unsigned long long>(r.total_mem), r.late ? "true" : "false", r.pending_s,
+      json_escape(r.error).c_str());
   return buf;
 }
 

@@ -55,6 +55,9 @@ def build_parser() -> flags.GoFlagParser:
                                              "(every CU of every XCD) on GPUs with no running work; 0 = off")
     p.add_float("liveness_timeout", 10.0, "per-device liveness probe deadline (s)")
     p.add_int("liveness_fail_threshold", 2, "consecutive probe failures before a device turns Unhealthy")
+    p.add_float("liveness_busy_grace", 300.0, "seconds a probe may stay queued behind other processes' work on "
+                                              "its GPU (a tenant kernel holding every CU) before it counts as a "
+                                              "failure")
     p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
     p.add_bool("smi_events", False, "subscribe to amd-smi GPU events; a device is Unhealthy between a "
                                     "gpu_pre_reset and its gpu_post_reset, other events are counted")
@@ -122,7 +125,8 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
                           liveness_timeout_s=ns.liveness_timeout, fail_threshold=ns.liveness_fail_threshold,
                           smi_ecc=ns.smi_ecc, smi_events=ns.smi_events, smi_xgmi=ns.smi_xgmi, dev_root=ns.dev_root,
                           liveness_mode=ns.liveness_mode, chip_sweep_every=ns.liveness_chip_sweep_every,
-                          liveness_keep_queues=ns.liveness_keep_queues)
+                          liveness_keep_queues=ns.liveness_keep_queues,
+                          liveness_busy_grace_s=ns.liveness_busy_grace)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         from .. import cdi

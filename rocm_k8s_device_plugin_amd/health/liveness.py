@@ -29,7 +29,7 @@ import os
 import signal
 import time
 from dataclasses import dataclass, field
-from typing import Dict, Mapping, Optional, Sequence
+from typing import Collection, Dict, Mapping, Optional, Sequence
 
 from ..ops.native import probe_executable
 from ..utils import log
@@ -46,6 +46,10 @@ class ProbeOutcome:
     reason: str = ""
     latency_ms: float = 0.0
     detail: dict = field(default_factory=dict)
+    # kept-queue server: the dispatch has not completed yet and stays queued
+    # (e.g. behind a tenant kernel that holds every CU); the next probe waits
+    # for it instead of submitting another
+    pending: bool = False
 
 
 class ProbeServerError(RuntimeError):
@@ -140,6 +144,7 @@ class LivenessProber:
         self.fallbacks = 0
         self._server: Optional[_ProbeServer] = None
         self._server_backoff = 0  # sweeps to run in spawn mode after a server failure
+        self._pending_nonce: Dict[int, int] = {}   # ordinal -> nonce of the server's outstanding dispatch
 
     def _kfd_entries(self) -> set:
         try:
@@ -230,7 +235,8 @@ class LivenessProber:
             self._own_kfd = frozenset(self._kfd_entries() - before)
             self.server_starts += 1
         nonces = {o: self._nonce(o) for o in uniq}
-        inner = max(0.5, self.timeout_s - 0.5)
+        # the server's own dispatch wait ends before our deadline for the reply
+        inner = self.timeout_s - min(0.5, 0.25 * self.timeout_s)
         line = f"{kind} {self.iters} {inner:.2f} " + " ".join(f"{o}:{nonces[o]}" for o in uniq)
         doc = await self._server.request(line, self.timeout_s)
         dt = (time.perf_counter() - t0) * 1e3
@@ -238,11 +244,22 @@ class LivenessProber:
         out = {}
         for o in uniq:
             d = by_ord.get(o)
-            out[o] = (self._judge(bool(d.get("ok")), d, nonces[o], dt) if d is not None
-                      else ProbeOutcome(False, "device missing from probe server reply", dt))
+            if d is None:
+                out[o] = ProbeOutcome(False, "device missing from probe server reply", dt)
+                continue
+            # a late verdict answers the dispatch (and nonce) of the probe that left it pending
+            expect = self._pending_nonce.pop(o, nonces[o]) if d.get("late") else nonces[o]
+            r = self._judge(bool(d.get("ok")), d, expect, dt)
+            if not r.ok and float(d.get("pending_s") or 0) > 0:
+                r.pending = True
+                self._pending_nonce.setdefault(o, nonces[o])
+            elif not d.get("late"):
+                self._pending_nonce.pop(o, None)
+            out[o] = r
         return out
 
     async def close(self) -> None:
+        self._pending_nonce.clear()   # a new server starts without outstanding dispatches
         if self._server is not None:
             await self._server.kill()
             self._server = None
@@ -285,8 +302,13 @@ class LivenessProber:
             await self.close()
         return out
 
-    async def probe(self, ordinals: Mapping[str, int], kind: str = "probe") -> Dict[str, ProbeOutcome]:
-        """device ID -> outcome; devices sharing an ordinal are probed once."""
+    async def probe(self, ordinals: Mapping[str, int], kind: str = "probe",
+                    busy: Collection[int] = ()) -> Dict[str, ProbeOutcome]:
+        """device ID -> outcome; devices sharing an ordinal are probed once.
+
+        `busy`: ordinals whose GPU runs other processes' queues. A pending
+        dispatch there is a tenant holding the GPU, not evidence of a fault, so
+        it is not re-probed in a fresh process (which would only wait too)."""
         uniq = sorted(set(ordinals.values()))
         use_server = self.mode == "persistent" and uniq and self._server_backoff == 0
         self._server_backoff = max(0, self._server_backoff - 1)
@@ -294,7 +316,7 @@ class LivenessProber:
             try:
                 with TRACER.span("liveness.request", "health", ordinals=len(uniq), kind=kind):
                     results = await self._probe_server(uniq, kind)
-                failed = [o for o in uniq if not results[o].ok]
+                failed = [o for o in uniq if not results[o].ok and not (results[o].pending and o in busy)]
                 if failed:
                     results.update(await self._confirm_failures(failed, results, kind))
                 self.sweeps += 1

@@ -67,6 +67,10 @@ class HealthConfig:
     # get the full-chip sweep (every CU of every XCD) instead of the one-wave probe
     chip_sweep_every: int = 0
     fail_threshold: int = 2
+    # a probe whose dispatch stays queued behind other processes' work on the
+    # GPU (a tenant kernel holding every CU) is inconclusive for this long
+    # before it counts as a failure
+    liveness_busy_grace_s: float = 300.0
     recover_threshold: int = 1
     smi_ecc: bool = False
     smi_events: bool = False
@@ -80,6 +84,7 @@ class _Track:
     oks: int = 0
     live: bool = True
     last_reason: str = ""
+    pending_since: Optional[float] = None   # first inconclusive (busy GPU) probe
 
 
 class HealthMonitor:
@@ -238,10 +243,27 @@ class HealthMonitor:
                 idle.add(dev_id)
         return idle
 
-    async def _liveness(self, ords: Dict[str, int]):
+    def _busy_devices(self, dev_ids) -> set:
+        """Devices whose GPU runs other processes' queues (unknown -> all)."""
+        own = self.prober.own_kfd_entries if self.prober is not None else ()
+        try:
+            busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
+        except KfdBusyUnknown:
+            return set(dev_ids)
+        out = set()
+        for dev_id in dev_ids:
+            d = self.inv.by_id.get(dev_id)
+            node = self.inv.topology.node(d.node_id) if d is not None and d.node_id >= 0 else None
+            gid = int(getattr(node, "gpu_id", 0) or 0) if node is not None else 0
+            if gid and gid in busy:
+                out.add(dev_id)
+        return out
+
+    async def _liveness(self, ords: Dict[str, int], busy_devs=frozenset()):
         every = self.cfg.chip_sweep_every
+        busy = {o for d, o in ords.items() if d in busy_devs}
         if every <= 0 or self.sweeps % every != 0:
-            return await self.prober.probe(ords)
+            return await self.prober.probe(ords, busy=busy)
         idle = self._idle_devices(ords)
         out = {}
         if idle:
@@ -250,7 +272,7 @@ class HealthMonitor:
             self.chip_sweeps += 1
         rest = {k: v for k, v in ords.items() if k not in idle}
         if rest:
-            out.update(await self.prober.probe(rest))
+            out.update(await self.prober.probe(rest, busy=busy))
         return out
 
     # ------------------------------------------------------------------ sweep
@@ -285,19 +307,30 @@ class HealthMonitor:
 
         if self.cfg.liveness and self.prober is not None:
             ords = {k: v for k, v in self.ordinals().items() if k in reasons}
-            outcomes = await self._liveness(ords)
+            busy_devs = self._busy_devices(ords)
+            outcomes = await self._liveness(ords, busy_devs)
             from ..utils.metrics import REGISTRY
+            now = time.monotonic()
             for dev_id, o in outcomes.items():
                 REGISTRY.set("mi355x_dp_liveness_probe_ms", float(o.latency_ms),
                              help="last liveness probe round trip", device=dev_id)
                 tr = self._track[dev_id]
                 if o.ok:
                     tr.fails, tr.oks = 0, tr.oks + 1
+                    tr.pending_since = None
                     if not tr.live and tr.oks >= self.cfg.recover_threshold:
                         tr.live = True
+                elif o.pending and dev_id in busy_devs and \
+                        now - (tr.pending_since or now) < self.cfg.liveness_busy_grace_s:
+                    # queued behind a tenant's kernel: neither a pass nor a failure yet
+                    tr.pending_since = tr.pending_since or now
+                    REGISTRY.inc("mi355x_dp_liveness_inconclusive_total", help="probes queued behind a busy GPU",
+                                 device=dev_id)
                 else:
                     tr.oks, tr.fails = 0, tr.fails + 1
                     tr.last_reason = o.reason
+                    if not o.pending:
+                        tr.pending_since = None
                     if tr.live and tr.fails >= self.cfg.fail_threshold:
                         tr.live = False
                 if not tr.live:

@@ -78,6 +78,11 @@ def serve():
             if mode == "garbage":
                 print("segfault-ish noise", flush=True)
                 return 139
+            if mode == "pending":   # kept-queue server: dispatch still queued behind other work
+                d = _device(int(o), "fail", int(n, 0))
+                d.update(hip_error=-1, mismatches=0, pending_s=1.0, error="dispatch pending for 1.0s (not completed)")
+                devs.append(d)
+                continue
             devs.append(_device(int(o), mode, int(n, 0)))
         print(json.dumps({"ok": all(d["ok"] for d in devs), "hip_device_count": 8, "sweep": kind == "sweep",
                           "t_ready_ns": time.monotonic_ns(), "devices": devs}), flush=True)
@@ -100,6 +105,8 @@ def main(argv):
     mode = _control().get(ordinal, "ok")
     if mode == "server_fail":
         mode = "ok"
+    if mode == "pending":   # a fresh process waits too, then gives up
+        mode = "fail"
     if mode == "hang":
         time.sleep(3600)
     if mode == "garbage":
