@@ -317,6 +317,10 @@ class LivenessProber:
                 with TRACER.span("liveness.request", "health", ordinals=len(uniq), kind=kind):
                     results = await self._probe_server(uniq, kind)
                 failed = [o for o in uniq if not results[o].ok and not (results[o].pending and o in busy)]
+                if not self.keep_queues and any(r.detail.get("hip_error") == -1 for r in results.values()):
+                    # without kept queues a timed-out dispatch's queue (and its 181 MB
+                    # save area) can never be freed by the server: restart it
+                    await self.close()
                 if failed:
                     results.update(await self._confirm_failures(failed, results, kind))
                 self.sweeps += 1

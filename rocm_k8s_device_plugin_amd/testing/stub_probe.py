@@ -78,6 +78,11 @@ def serve():
             if mode == "garbage":
                 print("segfault-ish noise", flush=True)
                 return 139
+            if mode == "timeout":   # server without kept queues: the dispatch did not complete
+                d = _device(int(o), "fail", int(n, 0))
+                d.update(hip_error=-1, mismatches=0, error="dispatch did not complete within 1.0s")
+                devs.append(d)
+                continue
             if mode == "pending":   # kept-queue server: dispatch still queued behind other work
                 d = _device(int(o), "fail", int(n, 0))
                 d.update(hip_error=-1, mismatches=0, pending_s=1.0, error="dispatch pending for 1.0s (not completed)")
@@ -105,7 +110,7 @@ def main(argv):
     mode = _control().get(ordinal, "ok")
     if mode == "server_fail":
         mode = "ok"
-    if mode == "pending":   # a fresh process waits too, then gives up
+    if mode in ("pending", "timeout"):   # a fresh process waits too, then gives up
         mode = "fail"
     if mode == "hang":
         time.sleep(3600)

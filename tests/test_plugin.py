@@ -892,3 +892,22 @@ def test_liveness_pending_behind_tenant(tmp_path, busy, grace, unhealthy_after):
         if not busy:
             assert spawned                          # idle GPU: confirmed in a fresh process
     assert all(mon.health(d.id) == "Healthy" for d in inv.devices if d.id != dev)
+
+
+def test_server_without_kept_queues_restarts_after_a_timeout(tmp_path):
+    """Without kept queues the server cannot free a timed-out dispatch's queue
+    (181 MB save area on MI355X): the prober restarts it to reclaim the memory."""
+    ctl, prober = _stub_prober(tmp_path, {"1": "timeout"})
+    prober.keep_queues = False
+    ords = {f"dev{i}": i for i in range(4)}
+
+    async def go():
+        res = await prober.probe(ords)
+        assert not res["dev1"].ok and all(res[f"dev{i}"].ok for i in (0, 2, 3))
+        assert prober._server is None            # killed after the sweep
+        ctl.write_text("{}")
+        assert all(r.ok for r in (await prober.probe(ords)).values())
+        assert prober.server_starts == 2
+        await prober.close()
+
+    run(go())
