@@ -167,6 +167,32 @@ class LivenessProber:
             self._own_kfd = frozenset(self._own_kfd & self._kfd_entries())
         return self._own_kfd if len(self._own_kfd) == 1 else frozenset()
 
+    def own_kfd_entries_for(self, gpu_ids) -> frozenset:
+        """own_kfd_entries, resolving a start-up ambiguity by queue coverage: a
+        kept-queue server holds a queue on every GPU it probed, while a pod's
+        process only sees (and queues on) the pod's GPUs. The one candidate
+        whose queues cover all of `gpu_ids` is the server."""
+        own = self.own_kfd_entries
+        want = {int(g) for g in gpu_ids if g}
+        if own or len(self._own_kfd) <= 1 or not want or not self.keep_queues:
+            return own
+        match = []
+        for e in sorted(self._own_kfd):
+            qdir = os.path.join(self.kfd_proc_dir, e, "queues")
+            have = set()
+            try:
+                for q in os.listdir(qdir):
+                    with open(os.path.join(qdir, q, "gpuid")) as f:
+                        have.add(int(f.read().strip() or 0))
+            except (OSError, ValueError):
+                continue
+            if want <= have:
+                match.append(e)
+        if len(match) == 1:
+            self._own_kfd = frozenset(match)
+            return self._own_kfd
+        return frozenset()
+
     def _exe(self) -> str:
         if self.exe is None:
             self.exe = str(probe_executable())

@@ -227,7 +227,7 @@ class HealthMonitor:
 
     def _idle_devices(self, dev_ids) -> set:
         """Devices whose kfd gpu_id has no user queue in any process right now."""
-        own = self.prober.own_kfd_entries if self.prober is not None else ()
+        own = self._own_entries()
         try:
             busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
         except KfdBusyUnknown as e:
@@ -243,9 +243,21 @@ class HealthMonitor:
                 idle.add(dev_id)
         return idle
 
+    def _gpu_id(self, dev_id: str) -> int:
+        d = self.inv.by_id.get(dev_id)
+        node = self.inv.topology.node(d.node_id) if d is not None and d.node_id >= 0 else None
+        return int(getattr(node, "gpu_id", 0) or 0) if node is not None else 0
+
+    def _own_entries(self):
+        """The probe server's kfd proc entries (see LivenessProber.own_kfd_entries_for)."""
+        if self.prober is None:
+            return ()
+        probed = self._ordinals.keys() if self._ordinals else ()
+        return self.prober.own_kfd_entries_for({self._gpu_id(d) for d in probed})
+
     def _busy_devices(self, dev_ids) -> set:
         """Devices whose GPU runs other processes' queues (unknown -> all)."""
-        own = self.prober.own_kfd_entries if self.prober is not None else ()
+        own = self._own_entries()
         try:
             busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
         except KfdBusyUnknown:

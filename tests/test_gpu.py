@@ -201,15 +201,15 @@ def test_kept_queue_server_is_not_a_tenant(inv, ordinals):
         before = kfd_busy_gpu_ids("/sys")     # this test process may hold HIP queues of its own
         res = await prober.probe({dev_id: o})
         assert all(r.ok for r in res.values()), res
-        own = prober.own_kfd_entries
         # on the shared host another tenant's GPU process may have started in the
-        # same instant as the server: the claim stays empty (the safe side) until
-        # the other one exits
+        # same instant as the server: queue coverage of our GPU resolves it, else
+        # the claim stays empty (the safe side) until the other one exits
+        own = prober.own_kfd_entries_for({gid})
         for _ in range(100):
             if own:
                 break
             await asyncio.sleep(0.1)
-            own = prober.own_kfd_entries
+            own = prober.own_kfd_entries_for({gid})
         if not own:
             await prober.close()
             pytest.skip(f"another GPU process started with the probe server and is still running: "

@@ -911,3 +911,40 @@ def test_server_without_kept_queues_restarts_after_a_timeout(tmp_path):
         await prober.close()
 
     run(go())
+
+
+def test_server_kfd_entry_ambiguity_resolved_by_queue_coverage(tmp_path):
+    """Another GPU process starting in the same instant as the probe server
+    leaves two candidate kfd entries; the server's is the one with a queue on
+    every probed GPU (a pod's process only queues on its own GPUs)."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    proc = fi.sysfs / "class/kfd/kfd/proc"
+    gids = [inv.topology.node(d.node_id).gpu_id for d in inv.devices]
+
+    def entry(pid, gpu_ids):
+        for i, g in enumerate(gpu_ids):
+            q = proc / pid / "queues" / str(i)
+            q.mkdir(parents=True, exist_ok=True)
+            (q / "gpuid").write_text(f"{g}\n")
+
+    entry("1001", gids)            # the server: one kept queue per GPU
+    entry("1002", gids[2:4])       # a pod that started at the same moment, 2 GPUs
+    ctl, prober = _stub_prober(tmp_path, {})
+    prober.kfd_proc_dir = str(proc)
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+
+    async def go():
+        try:
+            await prober.probe({"dev0": 0})          # server up
+            prober._own_kfd = frozenset({"1001", "1002"})
+            assert prober.own_kfd_entries == frozenset()          # ambiguous on its own
+            assert mon._own_entries() == frozenset({"1001"})     # resolved by coverage
+            # the pod's two GPUs are busy, the rest are idle
+            busy = mon._busy_devices([d.id for d in inv.devices])
+            assert busy == {inv.devices[2].id, inv.devices[3].id}
+        finally:
+            await prober.close()
+
+    run(go())
