@@ -113,6 +113,7 @@ PYBIND11_MODULE(_native, m) {
         return ids;
       })
       .def("count_gpu_nodes", &KfdTopology::count_gpu_nodes)
+      .def("unreadable_node_ids", &KfdTopology::unreadable_node_ids)
       .def("any_live_gpu", &KfdTopology::any_live_gpu)
       .def("all_gpu_links", [](const KfdTopology& t) {
         py::list l;
@@ -142,6 +143,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("domain", &GpuDevice::domain)
       .def_readwrite("hive_id", &GpuDevice::hive_id)
       .def_readwrite("vram_bytes", &GpuDevice::vram_bytes)
+      .def_readwrite("identity", &GpuDevice::identity)
       .def_property_readonly("partition_type", &GpuDevice::partition_type)
       .def_property_readonly("cu_count", &GpuDevice::cu_count);
 
@@ -149,7 +151,12 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("devices", &DiscoveryResult::devices)
       .def_readonly("driver_loaded", &DiscoveryResult::driver_loaded)
       .def_readonly("kfd_present", &DiscoveryResult::kfd_present)
-      .def_readonly("warnings", &DiscoveryResult::warnings);
+      .def_readonly("warnings", &DiscoveryResult::warnings)
+      .def_readonly("kfd_unreadable_nodes", &DiscoveryResult::kfd_unreadable_nodes)
+      .def_readonly("recovered_devices", &DiscoveryResult::recovered_devices)
+      .def_readonly("unresolved", &DiscoveryResult::unresolved);
+  m.def("partitions_for_mode", &partitions_for_mode, py::arg("mode"), py::arg("total_xcc"));
+  m.def("xcc_count_for_device_id", &xcc_count_for_device_id, py::arg("pci_device_id"));
 
   m.def("discover_gpus", py::overload_cast<const std::string&>(&discover_gpus), py::arg("sysfs_root") = "/sys");
   m.def("discover_gpus_with", py::overload_cast<const std::string&, const KfdTopology&>(&discover_gpus),
@@ -164,10 +171,13 @@ PYBIND11_MODULE(_native, m) {
   });
 
   py::class_<AllocDevice>(m, "AllocDevice")
-      .def(py::init([](std::string id, int node_id, int numa_node, std::string unique_id, uint64_t hive_id) {
-             return AllocDevice{std::move(id), node_id, numa_node, std::move(unique_id), hive_id};
+      .def(py::init([](std::string id, int node_id, int numa_node, std::string unique_id, uint64_t hive_id,
+                       bool inferred_links) {
+             return AllocDevice{std::move(id), node_id, numa_node, std::move(unique_id), hive_id, inferred_links};
            }),
-           py::arg("id"), py::arg("node_id"), py::arg("numa_node"), py::arg("unique_id"), py::arg("hive_id") = 0)
+           py::arg("id"), py::arg("node_id"), py::arg("numa_node"), py::arg("unique_id"), py::arg("hive_id") = 0,
+           py::arg("inferred_links") = false)
+      .def_readwrite("inferred_links", &AllocDevice::inferred_links)
       .def_readwrite("id", &AllocDevice::id)
       .def_readwrite("node_id", &AllocDevice::node_id)
       .def_readwrite("numa_node", &AllocDevice::numa_node)
@@ -219,6 +229,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("num_groups", &HiveAllocator::num_groups)
       .def_property_readonly("num_linked_pairs", &HiveAllocator::num_linked_pairs)
       .def_property_readonly("num_from_keys", &HiveAllocator::num_from_keys)
+      .def_property_readonly("num_inferred_pairs", &HiveAllocator::num_inferred_pairs)
       .def("pair_weight", &HiveAllocator::pair_weight)
       .def("link_type", &HiveAllocator::link_type);
 

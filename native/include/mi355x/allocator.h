@@ -43,6 +43,10 @@ struct AllocDevice {
   int numa_node = -1;
   std::string unique_id;  // physical GPU identity ("DevId" in the reference)
   uint64_t hive_id = 0;   // 0 = unknown; filled from kfd when possible
+  // The device's kfd node is unreadable (EPERM) but its identity was
+  // recovered from PCI sysfs (GpuDevice::identity == "sysfs"): links to it are
+  // inferred from unique_id / hive_id instead of kfd io_links.
+  bool inferred_links = false;
 };
 
 struct AllocatorOptions {
@@ -93,6 +97,8 @@ class HiveAllocator {
   // number of (from<to) node pairs that had a kfd link (reference len(p2pWeights) counts 'from' keys)
   size_t num_linked_pairs() const { return linked_pairs_; }
   size_t num_from_keys() const { return from_keys_; }
+  // number of (i<j) device pairs whose link was inferred from sysfs identity
+  size_t num_inferred_pairs() const { return inferred_pairs_; }
   int pair_weight(const std::string& a, const std::string& b) const;
   int link_type(const std::string& a, const std::string& b) const;
   const AllocatorOptions& options() const { return opt_; }
@@ -119,6 +125,7 @@ class HiveAllocator {
   std::vector<int> dev_group_;  // device index -> group index
   size_t linked_pairs_ = 0;
   size_t from_keys_ = 0;
+  size_t inferred_pairs_ = 0;
 };
 
 // Reference pair-weight formula (device.go:135-157) plus the hive term.

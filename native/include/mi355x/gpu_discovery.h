@@ -46,6 +46,13 @@ struct GpuDevice {
   int domain = 0;
   uint64_t hive_id = 0;        // xGMI hive; 0 = not in a hive
   uint64_t vram_bytes = 0;
+  // Where the identity (unique_id / hive / partition membership) came from:
+  //   "kfd"   - the device's kfd topology node (reference behaviour);
+  //   "sysfs" - kfd denied the read (EPERM under a device cgroup), recovered
+  //             from PCI sysfs: <dev>/unique_id, xgmi_hive_info/xgmi_hive_id,
+  //             and for partitions the amdgpu_xcp_* drm-minor block layout;
+  //   ""      - unknown: no kfd node and no recoverable sysfs identity.
+  std::string identity;
 
   std::string partition_type() const {
     if (compute_partition.empty() || memory_partition.empty()) return "";
@@ -59,7 +66,17 @@ struct DiscoveryResult {
   bool driver_loaded = false;      // <sysfs>/module/amdgpu/drivers exists
   bool kfd_present = false;        // <sysfs>/class/kfd exists
   std::vector<std::string> warnings;
+  std::vector<int> kfd_unreadable_nodes;  // kfd node dirs whose properties could not be read
+  int recovered_devices = 0;              // devices whose identity came from sysfs instead of kfd
+  std::vector<std::string> unresolved;    // device IDs with no identity (placement must not trust them)
 };
+
+// Logical devices one physical GPU splits into in compute mode `mode`
+// (lower-case); CPX = one per XCC. 0 = unknown mode or XCC count.
+int partitions_for_mode(const std::string& mode, int total_xcc);
+// XCCs per physical GPU by PCI device id (MI355X 0x75a3, MI300X 0x74a1: 8;
+// MI308X 0x74a2: 4); 0 = unknown. Mirrors rocm_k8s_device_plugin_amd/models.
+int xcc_count_for_device_id(int pci_device_id);
 
 DiscoveryResult discover_gpus(const std::string& sysfs_root, const KfdTopology& topo);
 DiscoveryResult discover_gpus(const std::string& sysfs_root);

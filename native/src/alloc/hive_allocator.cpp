@@ -62,7 +62,7 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
   dev_group_.clear();
   w_.clear();
   link_.clear();
-  linked_pairs_ = from_keys_ = 0;
+  linked_pairs_ = from_keys_ = inferred_pairs_ = 0;
   opt_ = opt;
   if (devs.empty()) return "Devices list is empty. Unable to calculate pair wise weights";
 
@@ -96,6 +96,31 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
         froms.insert(std::min(devs_[i].node_id, devs_[j].node_id));
       }
   from_keys_ = froms.size();
+
+  // Pairs with an endpoint whose kfd node is unreadable have no kfd link.
+  // With a recovered identity the link type still follows from the fabric:
+  // partitions of one package talk on-die (kfd reports them as xGMI), GPUs of
+  // one xGMI hive are one xGMI hop apart (8x MI355X: fully connected), and
+  // GPUs outside a common hive go through PCIe.
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const auto& a = devs_[i];
+      const auto& b = devs_[j];
+      if (!(a.inferred_links || b.inferred_links)) continue;
+      if (link_[static_cast<size_t>(i) * n + j]) continue;
+      bool a_known = a.inferred_links || a.node_id >= 0;
+      bool b_known = b.inferred_links || b.node_id >= 0;
+      if (!a_known || !b_known) continue;
+      int t;
+      if (!a.unique_id.empty() && a.unique_id == b.unique_id)
+        t = kLinkXgmi;
+      else if (a.hive_id != 0 && a.hive_id == b.hive_id)
+        t = kLinkXgmi;
+      else
+        t = kLinkPcie;
+      link_[static_cast<size_t>(i) * n + j] = link_[static_cast<size_t>(j) * n + i] = t;
+      ++inferred_pairs_;
+    }
 
   std::set<std::pair<std::string, std::string>> degraded;
   for (const auto& p : opt.degraded_links)
@@ -133,9 +158,14 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
     groups_[g].members.push_back(i);
     dev_group_[i] = g;
   }
+  // members by kfd node id; devices without a readable kfd node keep their
+  // input order (the discovery order: the PCI function, then xcp by index)
   for (auto& g : groups_)
-    std::sort(g.members.begin(), g.members.end(),
-              [&](int a, int b) { return devs_[a].node_id < devs_[b].node_id; });
+    std::stable_sort(g.members.begin(), g.members.end(), [&](int a, int b) {
+      int na = devs_[a].node_id < 0 ? std::numeric_limits<int>::max() : devs_[a].node_id;
+      int nb = devs_[b].node_id < 0 ? std::numeric_limits<int>::max() : devs_[b].node_id;
+      return na < nb;
+    });
   return "";
 }
 

@@ -47,8 +47,12 @@ KfdTopology KfdTopology::load(const std::string& nodes_dir) {
   std::sort(ids.begin(), ids.end());
   for (int id : ids) {
     std::string dir = path_join(nodes_dir, std::to_string(id));
-    auto kv = parse_kv_file(path_join(dir, "properties"));
-    if (!kv) continue;
+    const std::string props = path_join(dir, "properties");
+    auto kv = parse_kv_file(props);
+    if (!kv) {
+      if (path_exists(props)) t.unreadable_.push_back(id);
+      continue;
+    }
     KfdNode n;
     n.id = id;
     n.props = std::move(*kv);

@@ -63,8 +63,11 @@ class BestEffortPolicy(Policy):
                 out.append(n.AllocDevice(*d))
             else:
                 # a device whose kfd node is unreadable (e.g. cgroup-denied inside a
-                # container) has no unique_id: group it by its own PCI function
-                out.append(n.AllocDevice(d.id, d.node_id, d.numa_node, group_key(d), int(getattr(d, "hive_id", 0))))
+                # container) is grouped by its sysfs unique_id, else by its own PCI
+                # function; with a sysfs identity its links are inferred from the hive
+                inferred = d.node_id < 0 and getattr(d, "identity", "") == "sysfs"
+                out.append(n.AllocDevice(d.id, d.node_id, d.numa_node, group_key(d), int(getattr(d, "hive_id", 0)),
+                                         inferred))
         return out
 
     def init(self, devices, topology, degraded_links: Iterable = ()) -> None:

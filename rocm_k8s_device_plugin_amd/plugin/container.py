@@ -30,6 +30,7 @@ from ..topology import Gpu, Inventory, discover
 from ..node_view import NodeView
 from ..topology_view import KFD_TOPOLOGY_CONTAINER_PATH, TopologyViews
 from ..utils import log
+from ..utils.metrics import REGISTRY
 from .base import DeviceImpl, DeviceImplError, PluginContext, device_proto, driver_present
 
 _log = log.get("container")
@@ -72,6 +73,7 @@ class ContainerImpl(DeviceImpl):
         self.inv = inventory or discover(sysfs_root, device_count_limit)
         for w in self.inv.warnings:
             _log.warning("%s", w)
+        self._report_kfd_access(self.inv)
         self.homogeneous = self.inv.homogeneous
         if not self.homogeneous and self.strategy == C.STRATEGY_SINGLE:
             raise DeviceImplError(_HETERO_SINGLE)
@@ -85,6 +87,27 @@ class ContainerImpl(DeviceImpl):
                 self._write_cdi_specs()
             except (OSError, ValueError) as e:
                 raise DeviceImplError(f"cannot write CDI specs to {self.cdi_spec_dir}: {e}") from e
+
+    @staticmethod
+    def _report_kfd_access(inv: Inventory) -> None:
+        """kfd answers EPERM for the topology nodes of GPUs the plugin's device
+        cgroup denies (a non-privileged pod without /dev: the drop-in Helm
+        chart's default). Say so loudly: identity then comes from PCI sysfs,
+        or — when even that fails — placement cannot be topology-aware."""
+        REGISTRY.set("mi355x_dp_kfd_unreadable_nodes", float(len(inv.kfd_unreadable_nodes)),
+                     help="kfd topology nodes whose properties the plugin cannot read (EPERM)")
+        REGISTRY.set("mi355x_dp_devices_identity_from_sysfs", float(len(inv.recovered)),
+                     help="devices identified from PCI sysfs because their kfd node is unreadable")
+        REGISTRY.set("mi355x_dp_devices_identity_unknown", float(len(inv.unresolved)),
+                     help="devices without a known physical GPU / xGMI hive (placement not topology-aware)")
+        if inv.kfd_unreadable_nodes:
+            _log.warning("kfd denies %d topology node(s) %s to this process; %d device(s) identified from "
+                         "PCI sysfs (unique_id, xgmi_hive_id, amdgpu_xcp block layout). Run the plugin with /dev "
+                         "mounted or privileged for kfd-exact topology.", len(inv.kfd_unreadable_nodes),
+                         list(inv.kfd_unreadable_nodes), len(inv.recovered))
+        if not inv.placement_trusted:
+            _log.warning("physical-GPU identity unknown for %s: GetPreferredAllocation disabled (kubelet picks "
+                         "devices itself) rather than placing by an incomplete topology", list(inv.unresolved))
 
     def _write_cdi_specs(self, stale=()) -> None:
         # before registration: kubelet may hand a CDI name to the runtime as
@@ -117,7 +140,14 @@ class ContainerImpl(DeviceImpl):
     # ------------------------------------------------------------- lifecycle
     def start(self, ctx: PluginContext) -> None:
         devs = self._members.get(ctx.resource, list(self.inv.devices))
+        ctx.allocator_error = False  # re-evaluated on every (re)start, e.g. after a topology reload
         if ctx.allocator is None:
+            ctx.allocator_error = True
+            return
+        unknown = set(self.inv.unresolved) & {d.id for d in devs}
+        if unknown:
+            _log.error("allocator disabled for plugin %s: no physical-GPU identity for %s (kfd unreadable, no "
+                       "sysfs unique_id). Falling back to kubelet default allocation.", ctx.resource, sorted(unknown))
             ctx.allocator_error = True
             return
         try:
@@ -203,6 +233,7 @@ class ContainerImpl(DeviceImpl):
             return None
         for w in inv.warnings:
             _log.warning("%s", w)
+        self._report_kfd_access(inv)
         old_resources = list(self._resources)
         monitor = HealthMonitor(inv, self.health_cfg)
         await self.monitor.close()

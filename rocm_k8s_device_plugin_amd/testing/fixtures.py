@@ -59,6 +59,14 @@ class FixtureSpec:
     partition_support: bool = True      # write available_*_partition files
     per_gpu_compute: Optional[List[str]] = None  # heterogeneous nodes
     generation: int = 1                 # kfd topology generation_id (bump to emulate a reconfiguration)
+    # "compact": one amdgpu_xcp_<8g+p> per extra partition, drm minors numbered
+    # over active partitions only (the reference test-ID scheme).
+    # "kernel": what amdgpu does (amdgpu_xcp_dev_alloc; measured on the MI355X
+    # box, profiles/sysfs_access_box.json): every GPU owns a block of 8 drm
+    # minors in probe order (its own + 7 amdgpu_xcp_* devices, present even in
+    # SPX), xcp index 7*rank + slot - 1; inactive slots have no kfd node.
+    xcp_layout: str = "compact"
+    probe_order: Optional[List[int]] = None  # kernel layout: GPU indices in driver probe order
 
 
 @dataclass
@@ -72,6 +80,7 @@ class FixtureInfo:
     hive_ids: List[int] = field(default_factory=list)
     render_minors: Dict[str, int] = field(default_factory=dict)
     node_ids: Dict[str, int] = field(default_factory=dict)
+    gpu_of: Dict[str, int] = field(default_factory=dict)   # device ID -> GPU index
 
 
 def _w(path: Path, content: str) -> None:
@@ -177,6 +186,13 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
         per = max(1, spec.cpus_per_numa)
         _w(dev_dir / "local_cpulist", f"{numa_node * per}-{numa_node * per + per - 1}")
         _w(dev_dir / "product_name", spec.product_name)
+        # identity attributes amdgpu exposes on the PCI device (readable without
+        # device-cgroup access, unlike kfd nodes): unique_id in hex, the hive id
+        # in decimal, as on the MI355X box
+        _w(dev_dir / "unique_id", f"{int(uid):016x}")
+        _w(dev_dir / "mem_info_vram_total", str(MI355X_VRAM))
+        if hive:
+            _w(dev_dir / "xgmi_hive_info" / "xgmi_hive_id", str(hive))
         if spec.partition_support:
             _w(dev_dir / "current_compute_partition", cp.upper())
             _w(dev_dir / "current_memory_partition", spec.memory_partition.upper())
@@ -189,14 +205,19 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
             _link(drv_amdgpu, dev_dir / "driver")
             _link(dev_dir, drv_amdgpu / bdf)
         _link(dev_dir, sysfs / "bus/pci/devices" / bdf)
-        for p in range(parts):
+        kernel = spec.xcp_layout == "kernel"
+        slots = 8 if kernel else parts
+        if kernel:
+            rank = (spec.probe_order or list(range(spec.num_gpus))).index(g)
+            card, render = 8 * rank, 128 + 8 * rank
+        for p in range(slots):
             if spec.mode != "container":
                 break
             if p == 0:
                 owner = dev_dir
                 dev_name = bdf
             else:
-                xcp_idx = 8 * g + p
+                xcp_idx = 7 * rank + p - 1 if kernel else 8 * g + p
                 owner = sysfs / "devices/platform" / f"amdgpu_xcp_{xcp_idx}"
                 dev_name = f"amdgpu_xcp_{xcp_idx}"
                 xcp_counter += 1
@@ -212,12 +233,14 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
                 _link(drv_amdgpu, owner / "driver")
             _w(dev / "dri" / f"card{card}", "")
             _w(dev / "dri" / f"renderD{render}", "")
-            info.device_ids.append(dev_name)
-            info.render_minors[dev_name] = render
-            info.node_ids[dev_name] = node_id
-            gpu_nodes.append(dict(node=node_id, gpu=g, part=p, parts=parts, bus=bus, uid=uid, hive=hive,
-                                  numa=numa_node, render=render))
-            node_id += 1
+            if p < parts:  # an active partition: a kubelet device with a kfd node
+                info.device_ids.append(dev_name)
+                info.render_minors[dev_name] = render
+                info.node_ids[dev_name] = node_id
+                info.gpu_of[dev_name] = g
+                gpu_nodes.append(dict(node=node_id, gpu=g, part=p, parts=parts, bus=bus, uid=uid, hive=hive,
+                                      numa=numa_node, render=render))
+                node_id += 1
             render += 1
             card += 1
 
@@ -311,6 +334,23 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
             info.device_ids.append(str(10 + g))
     return info
 
+
+
+def deny_kfd_nodes(fi: FixtureInfo, node_ids) -> None:
+    """Make kfd GPU nodes unreadable the way a device cgroup does: kfd then
+    answers EPERM for every file under the node (properties, gpu_id, name,
+    io_links, p2p_links, mem_banks; profiles/sysfs_access_box.json). Tests run
+    as root, which ignores permission bits, so each file becomes a directory:
+    it still exists but cannot be read as a file."""
+    nodes = fi.sysfs / "class/kfd/kfd/topology/nodes"
+    for nid in node_ids:
+        nd = nodes / str(nid)
+        for f in list(nd.rglob("*")):
+            if f.is_file() and not f.is_symlink():
+                f.unlink()
+                f.mkdir()
+        if not (nd / "properties").exists():
+            (nd / "properties").mkdir(parents=True)
 
 
 def wrap_kfd_topology(topology_dir: os.PathLike, root: os.PathLike) -> FixtureInfo:

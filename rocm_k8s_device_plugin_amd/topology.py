@@ -37,6 +37,8 @@ class Gpu:
     domain: int = 0
     hive_id: int = 0
     vram_bytes: int = 0
+    # "kfd" | "sysfs" (kfd node unreadable, identity from PCI sysfs) | "" (unknown)
+    identity: str = ""
 
     @property
     def partition_type(self) -> str:
@@ -70,7 +72,7 @@ class Gpu:
                    memory_partition=g.memory_partition, numa_node=g.numa_node, node_id=g.node_id,
                    gfx_target_version=g.gfx_target_version, simd_count=g.simd_count, simd_per_cu=g.simd_per_cu,
                    num_xcc=g.num_xcc, pci_device_id=g.pci_device_id, location_id=g.location_id, domain=g.domain,
-                   hive_id=g.hive_id, vram_bytes=g.vram_bytes)
+                   hive_id=g.hive_id, vram_bytes=g.vram_bytes, identity=g.identity)
 
 
 @dataclass
@@ -81,6 +83,10 @@ class Inventory:
     driver_loaded: bool
     kfd_present: bool
     warnings: List[str] = field(default_factory=list)
+    # kfd node dirs whose properties this process cannot read (EPERM: the device
+    # cgroup denies those GPUs) and devices whose identity could not be recovered
+    kfd_unreadable_nodes: Tuple[int, ...] = ()
+    unresolved: Tuple[str, ...] = ()
 
     def __post_init__(self):
         self.by_id: Dict[str, Gpu] = {d.id: d for d in self.devices}
@@ -99,6 +105,18 @@ class Inventory:
     @property
     def homogeneous(self) -> bool:
         return len(self.partition_counts()) <= 1
+
+    @property
+    def recovered(self) -> List[str]:
+        """Devices identified from PCI sysfs because kfd denied their nodes."""
+        return [d.id for d in self.devices if d.identity == "sysfs"]
+
+    @property
+    def placement_trusted(self) -> bool:
+        """Every device has a known physical-GPU identity and fabric position
+        (from kfd or recovered from sysfs): topology-aware placement is sound."""
+        ids = set(self.by_id)
+        return not any(u in ids for u in self.unresolved)
 
     def physical_gpus(self) -> Dict[str, List[Gpu]]:
         """unique_id -> devices (partitions) of that physical GPU, in device order."""
@@ -127,11 +145,11 @@ def _limit_physical(devs: List[Gpu], limit: Optional[int]) -> List[Gpu]:
     keep = []
     seen: List[str] = []
     for d in devs:
-        if d.unique_id not in seen:
-            seen.append(d.unique_id)
+        if (d.unique_id or d.bdf) not in seen:
+            seen.append(d.unique_id or d.bdf)
     allowed = set(seen[:limit])
     for d in devs:
-        if d.unique_id in allowed:
+        if (d.unique_id or d.bdf) in allowed:
             keep.append(d)
     return keep
 
@@ -159,7 +177,8 @@ def discover(sysfs_root: str = "/sys", device_count_limit: Optional[int] = None)
     devs = _limit_physical(devs, device_count_limit)
     from .models import check_inventory
     return Inventory(sysfs_root=sysfs_root, devices=tuple(devs), topology=topo, driver_loaded=res.driver_loaded,
-                     kfd_present=res.kfd_present, warnings=list(res.warnings) + check_inventory(devs))
+                     kfd_present=res.kfd_present, warnings=list(res.warnings) + check_inventory(devs),
+                     kfd_unreadable_nodes=tuple(res.kfd_unreadable_nodes), unresolved=tuple(res.unresolved))
 
 
 def hip_ordinals(inv: Inventory, dev_root: str = "/dev", check_access: bool = True) -> Dict[str, int]:

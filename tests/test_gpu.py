@@ -64,7 +64,7 @@ def test_inprocess_hsa_direct_probe(hip, inv):
         # DRIVER_NODE_ID is the thunk's node index, which is renumbered when the
         # container's device cgroup hides GPUs; match the agent by PCI location
         assert r["kfd_node_id"] >= 0
-        devs = [d for d in inv.devices if d.unique_id and (d.location_id >> 8) & 0xFF == r["pci_bus"]]
+        devs = [d for d in inv.devices if d.identity == "kfd" and (d.location_id >> 8) & 0xFF == r["pci_bus"]]
         assert len(devs) == 1, (r, inv.devices)
         assert r["pci_domain"] == devs[0].domain
 
@@ -105,7 +105,7 @@ def test_real_sysfs_discovery(inv):
                    "kfd_nodes_readable": [n.id for n in inv.topology.nodes]}, f, indent=1, default=str)
     # kfd hides the properties of GPUs this container's device cgroup denies
     # (kfd_topology.c permission check), so only accessible GPUs carry kfd data
-    readable = [d for d in inv.devices if d.unique_id]
+    readable = [d for d in inv.devices if d.identity == "kfd"]
     assert readable, "no GPU with readable kfd properties"
     gfx = {d.gfx_target_version for d in readable}
     assert gfx == {90500}, gfx
@@ -116,6 +116,48 @@ def test_real_sysfs_discovery(inv):
         assert d.cu_count == 32 * d.num_xcc  # 32 CUs per XCD; SPX = 8 XCDs = 256 CUs
     assert {d.partition_type for d in inv.devices} <= {"spx_nps1", "spx_nps2", "dpx_nps1", "dpx_nps2",
                                                      "qpx_nps1", "qpx_nps2", "cpx_nps1", "cpx_nps2"}
+
+
+def test_kfd_denied_gpus_identified_from_sysfs(inv, caplog):
+    """The box's device cgroup denies all but the job's GPU: kfd answers EPERM
+    for their topology nodes. Discovery says so (warning + metric) and still
+    knows every GPU's identity and hive from PCI sysfs; for the readable GPU
+    the sysfs-derived values must equal kfd's (hex unique_id -> kfd decimal)."""
+    import logging
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+    from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+    from rocm_k8s_device_plugin_amd.topology import discover
+    from rocm_k8s_device_plugin_amd.utils.metrics import REGISTRY
+    kfd = [d for d in inv.devices if d.identity == "kfd"]
+    assert kfd
+    for d in kfd:
+        dev_dir = f"/sys/bus/pci/devices/{d.bdf}"
+        with open(f"{dev_dir}/unique_id") as f:
+            assert str(int(f.read().strip(), 16)) == d.unique_id
+        if os.path.exists(f"{dev_dir}/xgmi_hive_info/xgmi_hive_id"):
+            with open(f"{dev_dir}/xgmi_hive_info/xgmi_hive_id") as f:
+                assert int(f.read().strip()) == d.hive_id
+    assert all(d.unique_id for d in inv.devices) and inv.placement_trusted
+    if not inv.kfd_unreadable_nodes:
+        pytest.skip("this box's device cgroup hides no GPU")
+    assert sorted(inv.recovered) == sorted(d.id for d in inv.devices if d.identity != "kfd")
+    assert any("unreadable" in w for w in inv.warnings)
+    assert len({d.hive_id for d in inv.devices}) == 1      # one 8-GPU xGMI hive
+    with caplog.at_level(logging.WARNING):
+        impl = ContainerImpl("single", "/sys", HealthConfig(exporter_socket=None), inventory=discover("/sys"))
+    assert any("kfd denies" in r.getMessage() for r in caplog.records)
+    assert f"mi355x_dp_kfd_unreadable_nodes {float(len(inv.kfd_unreadable_nodes))}" in REGISTRY.render()
+    from rocm_k8s_device_plugin_amd.plugin.base import new_context
+    ctx = new_context("gpu")
+    impl.start(ctx)
+    assert impl.options(ctx).get_preferred_allocation_available
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/kfd_denied_recovery_box.json", "w") as f:
+        json.dump({"kfd_unreadable_nodes": list(inv.kfd_unreadable_nodes), "recovered": inv.recovered,
+                   "devices": {d.id: {"identity": d.identity, "unique_id": d.unique_id, "hive_id": str(d.hive_id),
+                                      "location_id": d.location_id, "card": d.card, "render": d.render_minor}
+                               for d in inv.devices},
+                   "warnings": inv.warnings}, f, indent=1)
 
 
 def test_hip_ordinal_mapping_matches_pci_bus(inv, ordinals, hip):
@@ -510,7 +552,7 @@ def test_rocprof_kept_queue_server_one_dispatch_per_sweep(tmp_path):
 def test_real_box_matches_mi355x_model(inv):
     """The registry's MI355X numbers against the real part; consistent partitions."""
     from rocm_k8s_device_plugin_amd.models import MI355X, check_inventory, model_for
-    readable = [d for d in inv.devices if d.unique_id]
+    readable = [d for d in inv.devices if d.identity == "kfd"]
     for d in readable:
         assert model_for(d.pci_device_id, d.gfx_target_version) is MI355X, hex(d.pci_device_id)
         assert d.cu_count == MI355X.cus_per_partition(d.compute_partition)
@@ -530,7 +572,7 @@ def test_real_fabric_links(inv):
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/real_fabric_links.json", "w") as f:
         json.dump({"links": links, "report": fab.report([d.id for d in inv.devices]).as_dict()}, f, indent=1)
-    readable = [d for d in inv.devices if d.unique_id]
+    readable = [d for d in inv.devices if d.identity == "kfd"]
     assert readable
     rep = fab.report([readable[0].id])
     assert rep.physical_gpus == 1

@@ -113,19 +113,22 @@ def test_real_box_layout_quirks(tmp_path):
 
 def test_unreadable_kfd_nodes(tmp_path):
     """kfd EPERMs the properties of cgroup-denied GPUs inside containers: the device
-    stays (from PCI sysfs) but carries no kfd data and no HIP ordinal."""
+    stays (from PCI sysfs) with its identity recovered from sysfs, but carries no
+    kfd node and no HIP ordinal (tests/test_kfd_denied.py covers whole nodes)."""
     fi = make_mi355x_node(tmp_path)
     victim = fi.node_ids[fi.bdfs[2]]
     os.remove(fi.sysfs / "class/kfd/kfd/topology/nodes" / str(victim) / "properties")
     inv = discover(str(fi.sysfs))
     d = inv.by_id[fi.bdfs[2]]
-    assert d.unique_id == "" and d.node_id == -1 and d.gfx_target_version == 0
+    assert d.node_id == -1 and d.identity == "sysfs"
+    assert d.unique_id == fi.unique_ids[2] and d.hive_id == fi.hive_ids[2]
+    assert d.gfx_target_version == 90500       # from a readable sibling of the same part
     assert fi.bdfs[2] not in hip_ordinals(inv, str(fi.dev))
-    # the allocator groups it by BDF instead of lumping all such devices together
     from rocm_k8s_device_plugin_amd.allocator import BestEffortPolicy
     pol = BestEffortPolicy()
     pol.init(inv.devices, inv.topology)
     assert pol.native.num_groups == 8
+    assert pol.native.link_type(fi.bdfs[2], fi.bdfs[3]) == 11   # same hive -> xGMI, inferred
 
 
 def test_device_without_drm_does_not_inherit(tmp_path):
@@ -135,7 +138,8 @@ def test_device_without_drm_does_not_inherit(tmp_path):
     shutil.rmtree(drm)
     inv = discover(str(fi.sysfs))
     d = inv.by_id[fi.bdfs[3]]
-    assert d.card == -1 and d.render_minor == -1 and d.unique_id == ""
+    # no drm node: nothing kfd-side; the identity is its own (sysfs), not its neighbour's
+    assert d.card == -1 and d.render_minor == -1 and d.unique_id == fi.unique_ids[3]
     assert inv.by_id[fi.bdfs[2]].card != -1
 
 
