@@ -52,7 +52,7 @@ METRIC = "p50 Allocate→ContainerReady latency; GPUs advertised at 1/2/4/8 MI35
 STUB_PROBE = os.path.join(REPO, "rocm_k8s_device_plugin_amd", "testing", "stub_probe.py")
 
 
-def parse_args():
+def make_parser():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -99,7 +99,11 @@ def parse_args():
                          "server, amd-smi ECC / events / xGMI link state) with this pulse in seconds, while pods "
                          "are admitted (BASELINE config: health-check DaemonSet enabled)")
     ap.add_argument("--json-out", default="")
-    return ap.parse_args()
+    return ap
+
+
+def parse_args(argv=None):
+    return make_parser().parse_args(argv)
 
 
 def pct(xs, q):

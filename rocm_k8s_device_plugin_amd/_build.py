@@ -156,16 +156,26 @@ def run_ctest(sanitize: str = "") -> subprocess.CompletedProcess:
                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
 
 
-if __name__ == "__main__":
+def make_parser():
     import argparse
-
-    ap = argparse.ArgumentParser(description="build the native core")
+    ap = argparse.ArgumentParser(prog="python -m rocm_k8s_device_plugin_amd._build",
+                                 description="build the native core")
     ap.add_argument("--no-hip", action="store_true")
-    ap.add_argument("--sanitize", default="")
+    ap.add_argument("--sanitize", default="",
+                    help="comma-separated -fsanitize= list for a ctest-only build, e.g. address,undefined or thread")
     ap.add_argument("--ctest", action="store_true")
-    a = ap.parse_args()
+    return ap
+
+
+def main(argv=None) -> int:
+    a = make_parser().parse_args(argv)
     if a.ctest:
         r = run_ctest(a.sanitize)
         print(r.stdout)
-        sys.exit(r.returncode)
+        return r.returncode
     build(hip=False if a.no_hip else None, sanitize=a.sanitize, quiet=False)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -112,15 +112,71 @@ def test_examples_parse_and_request_gpus():
     assert pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == 1
 
 
+def _workflow_commands():
+    """(workflow, step name, argv) for every command line of every run: step."""
+    import shlex
+    root = REPO / ".github" / "workflows"
+    for f in sorted(root.iterdir()):
+        doc = yaml.safe_load(f.read_text())
+        for job in doc["jobs"].values():
+            for step in job["steps"]:
+                for line in step.get("run", "").splitlines():
+                    for part in line.split("&&"):
+                        if part.strip():
+                            yield f.name, step.get("name", ""), shlex.split(part)
+
+
 def test_ci_workflows_parse_and_run_real_entry_points():
-    import yaml
-    root = os.path.join(os.path.dirname(__file__), "..", ".github", "workflows")
-    docs = {f: yaml.safe_load(open(os.path.join(root, f))) for f in os.listdir(root)}
+    docs = {f.name: yaml.safe_load(f.read_text()) for f in (REPO / ".github" / "workflows").iterdir()}
     assert set(docs) == {"ci.yaml", "helm-chart-release.yaml"}
     steps = " ".join(s.get("run", "") for j in docs["ci.yaml"]["jobs"].values() for s in j["steps"])
     for cmd in ("rocm_k8s_device_plugin_amd._build", '-m "not gpu"', "-m gpu", "bench.py"):
         assert cmd in steps
+    assert "--sanitize address,undefined" in steps and "--sanitize thread" in steps
     assert docs["helm-chart-release.yaml"]["jobs"]["release"]["steps"][-1]["with"]["charts_dir"] == "helm"
+
+
+def test_ci_command_lines_pass_the_real_argument_parsers():
+    """Every workflow command goes through the argparse parser of the entry
+    point it calls (a wrong flag fails here, not on the CI runner). pytest
+    lines run pytest's own option parsing and collection; unknown commands
+    fail so new steps must be added to this check."""
+    import importlib.util
+    import subprocess
+    import sys
+    from rocm_k8s_device_plugin_amd import _build
+    spec = importlib.util.spec_from_file_location("bench_under_test", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    checked = 0
+    for wf, name, argv in _workflow_commands():
+        where = f"{wf}: {name}: {' '.join(argv)}"
+        if argv[0] in ("git", "helm"):
+            continue
+        assert argv[0] in ("python3", "python"), where
+        if argv[1:4] == ["-m", "pip", "install"]:
+            continue
+        try:
+            if argv[1:3] == ["-m", "rocm_k8s_device_plugin_amd._build"]:
+                _build.make_parser().parse_args(argv[3:])
+            elif argv[1] == "bench.py":
+                bench.make_parser().parse_args(argv[2:])
+            elif argv[1:3] == ["-m", "pytest"]:
+                r = subprocess.run([sys.executable, "-m", "pytest", *argv[3:], "--collect-only", "-q",
+                                    "-p", "no:cacheprovider"], cwd=REPO, capture_output=True, text=True, timeout=300)
+                assert r.returncode == 0, f"{where}\n{r.stdout[-2000:]}{r.stderr[-2000:]}"
+            else:
+                raise AssertionError(f"unchecked workflow command: {where}")
+        except SystemExit as e:   # argparse error
+            raise AssertionError(f"argument error in {where}") from e
+        checked += 1
+    assert checked >= 7
+
+
+def test_ci_check_catches_a_bad_flag():
+    from rocm_k8s_device_plugin_amd import _build
+    with pytest.raises(SystemExit):
+        _build.make_parser().parse_args(["--no-hip", "--sanitize", "--ctest"])   # the round-1 CI bug
 
 
 def test_build_stamp_follows_content_not_mtime(tmp_path, monkeypatch):
@@ -147,3 +203,24 @@ def test_build_stamp_follows_content_not_mtime(tmp_path, monkeypatch):
     f.write_text("int a = 1;\n")                   # edited
     assert not _build._up_to_date([out])
     assert not _build._up_to_date([tmp_path / "missing.so"])
+
+
+def test_docs_tooling_matches_the_tree(tmp_path):
+    """docs/conf.py runs without Sphinx installed, every _toc entry is a page,
+    every page is in the _toc, and readthedocs/dependabot point at real paths."""
+    import runpy
+    conf = runpy.run_path(str(REPO / "docs" / "conf.py"))
+    assert conf["project"] and conf["version"] == yaml.safe_load((REPO / "helm/amd-gpu/Chart.yaml").read_text())[
+        "appVersion"]
+    toc = yaml.safe_load((REPO / "docs/sphinx/_toc.yml.in").read_text())
+    files = [toc["root"]] + [e["file"] for s in toc["subtrees"] for e in s["entries"]]
+    for f in files:
+        assert (REPO / "docs" / f"{f}.md").exists(), f
+    pages = {p.stem for p in (REPO / "docs").glob("*.md")}
+    assert pages == set(files), pages ^ set(files)
+    rtd = yaml.safe_load((REPO / ".readthedocs.yaml").read_text())
+    assert (REPO / rtd["sphinx"]["configuration"]).exists()
+    assert all((REPO / r["requirements"]).exists() for r in rtd["python"]["install"])
+    dep = yaml.safe_load((REPO / ".github/dependabot.yml").read_text())
+    for u in dep["updates"]:
+        assert (REPO / u["directory"].lstrip("/")).is_dir()
