@@ -132,6 +132,10 @@ typedef struct {
   double kernel_us;       // dispatch start -> end (HSA profiling)
   double arrival_spread_us;  // first to last workgroup arrival (s_memrealtime)
   double total_us;
+  // > 0: an earlier sweep on this device has not completed for this long; its
+  // queue and buffers stay allocated and no new sweep is submitted (at most one
+  // outstanding sweep per device, so a wedged GPU leaks one queue, not one per cadence)
+  double in_flight_s;
   char error[160];
 } mi355x_sweep_result;
 

@@ -39,6 +39,7 @@
   X(hsa_signal_destroy)                      \
   X(hsa_signal_store_screlease)              \
   X(hsa_signal_wait_scacquire)               \
+  X(hsa_signal_load_scacquire)               \
   X(hsa_amd_profiling_set_profiler_enabled)  \
   X(hsa_amd_profiling_get_dispatch_time)     \
   X(hsa_amd_agent_memory_pool_get_info)      \

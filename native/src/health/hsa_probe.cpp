@@ -251,9 +251,14 @@ namespace {
 void release_residents();
 }  // namespace
 
+namespace {
+void forget_in_flight_sweeps();
+}  // namespace
+
 extern "C" void mi355x_hsa_probe_shutdown(void) {
   mi355x_hsa_probe_release();
   release_residents();
+  forget_in_flight_sweeps();
   std::lock_guard<std::mutex> lk(g_rt.mu);
   if (g_rt.inited && g_rt.init_status == HSA_STATUS_SUCCESS) H().hsa_shut_down();
   if (g_rt.kfd_fd >= 0) close(g_rt.kfd_fd);
@@ -775,6 +780,60 @@ done:
   return out->ok ? 0 : 1;
 }
 
+namespace {
+
+// A chip sweep whose completion signal did not fire within its deadline: the
+// dispatch may still write its records, so none of its resources can be freed
+// until it completes. One per device at most (mi355x_hsa_chip_sweep refuses to
+// submit another while it is outstanding).
+struct SweepInFlight {
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t sig{};
+  void* bufs[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::chrono::steady_clock::time_point since{};
+
+  void release() {
+    for (void* b : bufs)
+      if (b) H().hsa_amd_memory_pool_free(b);
+    if (sig.handle) H().hsa_signal_destroy(sig);
+    if (queue) H().hsa_queue_destroy(queue);
+    if (exe.handle) H().hsa_executable_destroy(exe);
+    if (reader.handle) H().hsa_code_object_reader_destroy(reader);
+  }
+};
+std::mutex g_sweep_mu;
+std::vector<std::pair<int, SweepInFlight>> g_sweep_in_flight;
+
+// true (and out filled) when an earlier sweep on `ordinal` is still running;
+// a completed one is freed here.
+bool sweep_still_in_flight(int ordinal, mi355x_sweep_result* out) {
+  std::lock_guard<std::mutex> lk(g_sweep_mu);
+  for (auto it = g_sweep_in_flight.begin(); it != g_sweep_in_flight.end(); ++it) {
+    if (it->first != ordinal) continue;
+    if (H().hsa_signal_load_scacquire(it->second.sig) < 1) {
+      it->second.release();
+      g_sweep_in_flight.erase(it);
+      return false;
+    }
+    out->in_flight_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - it->second.since).count();
+    out->hsa_error = -1;
+    std::snprintf(out->error, sizeof(out->error), "earlier chip sweep still in flight for %.1fs (not completed)",
+                  out->in_flight_s);
+    return true;
+  }
+  return false;
+}
+
+// runtime shutdown: an outstanding sweep's resources go with the runtime
+void forget_in_flight_sweeps() {
+  std::lock_guard<std::mutex> lk(g_sweep_mu);
+  g_sweep_in_flight.clear();
+}
+
+}  // namespace
+
 extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, double timeout_s,
                                      mi355x_sweep_result* out) {
   using clk = std::chrono::steady_clock;
@@ -791,6 +850,10 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
   }
   if (ordinal < 0 || ordinal >= n) {
     std::snprintf(out->error, sizeof(out->error), "no such GPU agent (count=%d)", n);
+    return 1;
+  }
+  if (sweep_still_in_flight(ordinal, out)) {
+    out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
     return 1;
   }
   const Agent& ag = g_rt.gpus[ordinal];
@@ -898,6 +961,18 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
     in_flight = true;
     std::snprintf(out->error, sizeof(out->error), "chip sweep did not complete within %.1fs", timeout_s);
     out->hsa_error = -1;
+    SweepInFlight f;
+    f.reader = reader;
+    f.exe = exe;
+    f.queue = queue;
+    f.sig = sig;
+    f.bufs[0] = kargs;
+    f.bufs[1] = arrive;
+    f.bufs[2] = tiles;
+    f.bufs[3] = records;
+    f.since = t0;
+    std::lock_guard<std::mutex> lk(g_sweep_mu);
+    g_sweep_in_flight.emplace_back(ordinal, f);
     goto done;
   }
   {

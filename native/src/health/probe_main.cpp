@@ -225,11 +225,11 @@ std::string sweep_json(const mi355x_sweep_result& r) {
                 "\"cu_count\":%d,\"num_xcc\":%d,\"records_ok\":%d,\"mfma_bad\":%u,\"lds_bad\":%u,"
                 "\"tile_bad\":%u,\"cus_covered\":%d,\"xccs_covered\":%d,\"all_resident\":%s,"
                 "\"wgs_per_xcc\":%s,\"kernel_us\":%.2f,\"arrival_spread_us\":%.2f,\"total_us\":%.1f,"
-                "\"error\":\"%s\"}",
+                "\"in_flight_s\":%.2f,\"error\":\"%s\"}",
                 r.ordinal, r.ok ? "true" : "false", r.hsa_error, r.nonce, r.iters, r.grid, r.cu_count, r.num_xcc,
                 r.records_ok, r.mfma_bad, r.lds_bad, r.tile_bad, r.cus_covered, r.xccs_covered,
                 r.all_resident ? "true" : "false", per.c_str(), r.kernel_us, r.arrival_spread_us, r.total_us,
-                json_escape(r.error).c_str());
+                r.in_flight_s, json_escape(r.error).c_str());
   return buf;
 }
 

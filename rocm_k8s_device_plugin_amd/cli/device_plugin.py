@@ -57,7 +57,12 @@ def build_parser() -> flags.GoFlagParser:
     p.add_int("liveness_fail_threshold", 2, "consecutive probe failures before a device turns Unhealthy")
     p.add_float("liveness_busy_grace", 300.0, "seconds a probe may stay queued behind other processes' work on "
                                               "its GPU (a tenant kernel holding every CU) before it counts as a "
-                                              "failure")
+                                              "failure; applies in every liveness mode (kept queues: the queued "
+                                              "dispatch's late verdict is awaited; otherwise a deadline miss on "
+                                              "a busy GPU is inconclusive)")
+    p.add_float("liveness_unknown_busy_grace", 30.0, "the busy grace while busy GPUs cannot be told from idle ones "
+                                                     "(kfd process list unreadable): every GPU counts as busy, "
+                                                     "so the grace is shorter")
     p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
     p.add_bool("smi_events", False, "subscribe to amd-smi GPU events; a device is Unhealthy between a "
                                     "gpu_pre_reset and its gpu_post_reset, other events are counted")
@@ -126,7 +131,8 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
                           smi_ecc=ns.smi_ecc, smi_events=ns.smi_events, smi_xgmi=ns.smi_xgmi, dev_root=ns.dev_root,
                           liveness_mode=ns.liveness_mode, chip_sweep_every=ns.liveness_chip_sweep_every,
                           liveness_keep_queues=ns.liveness_keep_queues,
-                          liveness_busy_grace_s=ns.liveness_busy_grace)
+                          liveness_busy_grace_s=ns.liveness_busy_grace,
+                          liveness_unknown_busy_grace_s=ns.liveness_unknown_busy_grace)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         from .. import cdi

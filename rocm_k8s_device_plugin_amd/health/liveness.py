@@ -146,6 +146,10 @@ class LivenessProber:
         self._server_backoff = 0  # sweeps to run in spawn mode after a server failure
         self._pending_nonce: Dict[int, int] = {}   # ordinal -> nonce of the server's outstanding dispatch
 
+    @property
+    def server_running(self) -> bool:
+        return self._server is not None and self._server.alive
+
     def _kfd_entries(self) -> set:
         try:
             return set(os.listdir(self.kfd_proc_dir))
@@ -237,8 +241,11 @@ class LivenessProber:
             except ProcessLookupError:
                 pass
             await proc.wait()
+            # the dispatch did not complete: on a GPU that runs a tenant's kernels
+            # this is inconclusive (HealthMonitor applies the busy grace), as in
+            # the kept-queue server
             return ProbeOutcome(False, f"deadline exceeded ({self.timeout_s:.1f}s)",
-                                (time.perf_counter() - t0) * 1e3)
+                                (time.perf_counter() - t0) * 1e3, pending=kind != "sweep")
         dt = (time.perf_counter() - t0) * 1e3
         try:
             doc = json.loads(out.decode().strip().splitlines()[-1])
@@ -273,12 +280,19 @@ class LivenessProber:
             if d is None:
                 out[o] = ProbeOutcome(False, "device missing from probe server reply", dt)
                 continue
+            if kind == "sweep":
+                # sweeps run on their own queue: the kept probe slot (and its
+                # pending dispatch, if any) is untouched by them
+                out[o] = self._judge(bool(d.get("ok")), d, nonces[o], dt)
+                continue
             # a late verdict answers the dispatch (and nonce) of the probe that left it pending
             expect = self._pending_nonce.pop(o, nonces[o]) if d.get("late") else nonces[o]
             r = self._judge(bool(d.get("ok")), d, expect, dt)
             if not r.ok and float(d.get("pending_s") or 0) > 0:
                 r.pending = True
                 self._pending_nonce.setdefault(o, nonces[o])
+            elif not r.ok and d.get("hip_error") == -1 and not self.keep_queues:
+                r.pending = True     # timed out without a kept slot: no late verdict will follow
             elif not d.get("late"):
                 self._pending_nonce.pop(o, None)
             out[o] = r
@@ -343,9 +357,12 @@ class LivenessProber:
                 with TRACER.span("liveness.request", "health", ordinals=len(uniq), kind=kind):
                     results = await self._probe_server(uniq, kind)
                 failed = [o for o in uniq if not results[o].ok and not (results[o].pending and o in busy)]
-                if not self.keep_queues and any(r.detail.get("hip_error") == -1 for r in results.values()):
+                if not self.keep_queues and any(r.detail.get("hip_error") == -1 or r.detail.get("hsa_error") == -1
+                                                for r in results.values()):
                     # without kept queues a timed-out dispatch's queue (and its 181 MB
-                    # save area) can never be freed by the server: restart it
+                    # save area) can never be freed by the server: restart it. (A timed-out
+                    # chip sweep is held by the server, one per device, and freed once it
+                    # completes; a restart frees it at once.)
                     await self.close()
                 if failed:
                     results.update(await self._confirm_failures(failed, results, kind))

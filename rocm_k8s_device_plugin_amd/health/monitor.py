@@ -71,6 +71,10 @@ class HealthConfig:
     # GPU (a tenant kernel holding every CU) is inconclusive for this long
     # before it counts as a failure
     liveness_busy_grace_s: float = 300.0
+    # the same grace while which GPUs are busy is unknown (kfd process list
+    # unreadable, or the probe server's own kfd entry unresolved): every GPU
+    # then counts as busy, so the grace is kept short to bound the blind spot
+    liveness_unknown_busy_grace_s: float = 30.0
     recover_threshold: int = 1
     smi_ecc: bool = False
     smi_events: bool = False
@@ -117,6 +121,7 @@ class HealthMonitor:
         self.last_sweep_ms = 0.0
         self.fabric = FabricWatcher(inventory, fabric_source) if self.cfg.smi_xgmi else None
         self._smi_held = False   # amd-smi kept initialised while its sources are on (smi_hold)
+        self.busy_state_known = True   # last sweep could tell busy GPUs from idle ones
 
     # ------------------------------------------------------------------ fabric
     def degraded_links(self):
@@ -256,12 +261,18 @@ class HealthMonitor:
         return self.prober.own_kfd_entries_for({self._gpu_id(d) for d in probed})
 
     def _busy_devices(self, dev_ids) -> set:
-        """Devices whose GPU runs other processes' queues (unknown -> all)."""
+        """Devices whose GPU runs other processes' queues (unknown -> all, and
+        busy_state_known is cleared so the short grace applies)."""
         own = self._own_entries()
+        unresolved = not own and self.prober is not None and self.prober.server_running and \
+            self.prober.keep_queues
         try:
             busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
-        except KfdBusyUnknown:
+        except KfdBusyUnknown as e:
+            self._set_busy_known(False, str(e))
             return set(dev_ids)
+        # the server's own kept queues could not be told apart from a tenant's
+        self._set_busy_known(not unresolved, "probe server's kfd entry unresolved")
         out = set()
         for dev_id in dev_ids:
             d = self.inv.by_id.get(dev_id)
@@ -270,6 +281,19 @@ class HealthMonitor:
             if gid and gid in busy:
                 out.add(dev_id)
         return out
+
+    def _set_busy_known(self, known: bool, why: str) -> None:
+        if known != self.busy_state_known:
+            if known:
+                _log.info("busy-GPU state readable again")
+            else:
+                _log.warning("busy-GPU state unknown (%s): every GPU counts as busy, pending probes get "
+                             "a %.0fs grace instead of %.0fs", why, self.cfg.liveness_unknown_busy_grace_s,
+                             self.cfg.liveness_busy_grace_s)
+        self.busy_state_known = known
+        from ..utils.metrics import REGISTRY
+        REGISTRY.set("mi355x_dp_busy_state_known", 1.0 if known else 0.0,
+                     help="1 if busy GPUs can be told from idle ones (kfd process list readable)")
 
     async def _liveness(self, ords: Dict[str, int], busy_devs=frozenset()):
         every = self.cfg.chip_sweep_every
@@ -323,6 +347,8 @@ class HealthMonitor:
             outcomes = await self._liveness(ords, busy_devs)
             from ..utils.metrics import REGISTRY
             now = time.monotonic()
+            grace = self.cfg.liveness_busy_grace_s if self.busy_state_known else \
+                min(self.cfg.liveness_busy_grace_s, self.cfg.liveness_unknown_busy_grace_s)
             for dev_id, o in outcomes.items():
                 REGISTRY.set("mi355x_dp_liveness_probe_ms", float(o.latency_ms),
                              help="last liveness probe round trip", device=dev_id)
@@ -333,7 +359,7 @@ class HealthMonitor:
                     if not tr.live and tr.oks >= self.cfg.recover_threshold:
                         tr.live = True
                 elif o.pending and dev_id in busy_devs and \
-                        now - (tr.pending_since or now) < self.cfg.liveness_busy_grace_s:
+                        now - (tr.pending_since or now) < grace:
                     # queued behind a tenant's kernel: neither a pass nor a failure yet
                     tr.pending_since = tr.pending_since or now
                     REGISTRY.inc("mi355x_dp_liveness_inconclusive_total", help="probes queued behind a busy GPU",

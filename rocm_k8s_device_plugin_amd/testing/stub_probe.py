@@ -61,6 +61,7 @@ def serve():
     t = time.monotonic_ns()
     print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "t_start_ns": t, "t_runtime_ns": t}),
           flush=True)
+    slots = {}   # ordinal -> nonce of the kept slot's outstanding dispatch (like --keep)
     for line in sys.stdin:
         parts = line.split()
         if not parts or parts[0] == "quit":
@@ -83,12 +84,18 @@ def serve():
                 d.update(hip_error=-1, mismatches=0, error="dispatch did not complete within 1.0s")
                 devs.append(d)
                 continue
-            if mode == "pending":   # kept-queue server: dispatch still queued behind other work
+            if mode == "pending" and kind != "sweep":   # kept-queue server: dispatch still queued behind other work
+                slots.setdefault(o, int(n, 0))
                 d = _device(int(o), "fail", int(n, 0))
                 d.update(hip_error=-1, mismatches=0, pending_s=1.0, error="dispatch pending for 1.0s (not completed)")
                 devs.append(d)
                 continue
-            devs.append(_device(int(o), mode, int(n, 0)))
+            if kind != "sweep" and o in slots:   # the outstanding dispatch completed: its late verdict
+                d = _device(int(o), mode, slots.pop(o))
+                d["late"] = 1
+                devs.append(d)
+                continue
+            devs.append(_device(int(o), "ok" if mode == "pending" else mode, int(n, 0)))
         print(json.dumps({"ok": all(d["ok"] for d in devs), "hip_device_count": 8, "sweep": kind == "sweep",
                           "t_ready_ns": time.monotonic_ns(), "devices": devs}), flush=True)
     return 0

@@ -220,8 +220,11 @@ def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
     root = os.path.join(sysfs_root, "class/kfd/kfd/proc")
     try:
         pids = os.listdir(root)
-    except OSError:
-        return busy
+    except FileNotFoundError:
+        return busy             # no kfd process list at all: no process has queues
+    except OSError as e:
+        # the list itself is unreadable: every GPU may be running work
+        raise KfdBusyUnknown(f"{root}: {e}") from e
     skip = set(exclude)
     for pid in pids:
         if pid in skip:

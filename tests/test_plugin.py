@@ -948,3 +948,111 @@ def test_server_kfd_entry_ambiguity_resolved_by_queue_coverage(tmp_path):
             await prober.close()
 
     run(go())
+
+
+def test_chip_sweep_leaves_a_pending_probe_slot_alone(tmp_path):
+    """A probe left pending behind a tenant, then a chip sweep of that GPU (its
+    own queue), then the next probe: the late verdict still carries the first
+    probe's nonce and is accepted -- no stale-result failure, no fresh-process
+    re-probe, no server restart."""
+    log_path = tmp_path / "starts.log"
+    ctl, prober = _stub_prober(tmp_path, {"3": "pending"})
+    prober.extra_env["MI355X_STUB_PROBE_LOG"] = str(log_path)
+    ords = {f"dev{i}": i for i in range(4)}
+
+    async def go():
+        try:
+            r1 = await prober.probe(ords, busy={3})
+            assert r1["dev3"].pending and not r1["dev3"].ok
+            ctl.write_text("{}")                      # the tenant finished
+            assert all(r.ok for r in (await prober.sweep(ords)).values())
+            r3 = await prober.probe(ords)
+            assert r3["dev3"].ok and r3["dev3"].detail.get("late") == 1, r3["dev3"]
+            assert prober.server_restarts == 0 and prober.server_starts == 1
+        finally:
+            await prober.close()
+
+    run(go())
+    assert [x for x in log_path.read_text().split() if x == "3"] == []
+
+
+def test_kfd_proc_list_unreadable_is_busy_unknown(tmp_path, monkeypatch):
+    """An unreadable kfd process list itself (not just one process' queues)
+    means busy state unknown, never 'every GPU idle'; a missing list is idle."""
+    from rocm_k8s_device_plugin_amd import topology as T
+    fi = make_mi355x_node(tmp_path / "n")
+    root = fi.sysfs / "class/kfd/kfd/proc"
+    root.mkdir(parents=True, exist_ok=True)
+    real_listdir = os.listdir
+
+    def listdir(p):
+        if str(p).endswith("kfd/kfd/proc"):
+            raise PermissionError(13, "Permission denied")
+        return real_listdir(p)
+
+    monkeypatch.setattr(T.os, "listdir", listdir)
+    with pytest.raises(T.KfdBusyUnknown):
+        T.kfd_busy_gpu_ids(str(fi.sysfs))
+    monkeypatch.setattr(T.os, "listdir", real_listdir)
+    assert T.kfd_busy_gpu_ids(str(tmp_path / "nothing")) == set()
+
+
+def test_busy_unknown_uses_the_short_grace(tmp_path, monkeypatch):
+    """When busy GPUs cannot be identified every GPU counts as busy (no chip
+    sweep), but a pending probe only gets -liveness_unknown_busy_grace, not
+    the full busy grace: a GPU wedged while idle is still reported."""
+    from rocm_k8s_device_plugin_amd.health import monitor as M
+    from rocm_k8s_device_plugin_amd.utils.metrics import REGISTRY
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    dev = inv.devices[3].id
+
+    def unknown(*a, **k):
+        raise M.KfdBusyUnknown("proc: Permission denied")
+
+    monkeypatch.setattr(M, "kfd_busy_gpu_ids", unknown)
+    ctl, prober = _stub_prober(tmp_path, {"3": "pending"})
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=2,
+                                          liveness_busy_grace_s=300.0, liveness_unknown_busy_grace_s=0.0),
+                        prober=prober, ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+
+    async def go():
+        try:
+            for _ in range(2):
+                await mon.check_once()
+        finally:
+            await mon.close()
+
+    run(go())
+    assert not mon.busy_state_known
+    assert mon.health(dev) == "Unhealthy"
+    assert all(mon.health(d.id) == "Healthy" for d in inv.devices if d.id != dev)
+    assert "mi355x_dp_busy_state_known 0" in REGISTRY.render()
+
+
+def test_spawn_mode_deadline_on_busy_gpu_is_inconclusive(tmp_path):
+    """Without kept queues (spawn mode) a deadline miss on a GPU that runs a
+    tenant's kernels is inconclusive under the busy grace, like a pending
+    kept-queue probe; on an idle GPU it is a failure."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    busy_dev, idle_dev = inv.devices[3].id, inv.devices[5].id
+    _busy_gpu(fi, inv, busy_dev)
+    ctl = tmp_path / "probe_ctl.json"
+    ctl.write_text(json.dumps({"3": "hang", "5": "hang"}))
+    prober = LivenessProber(exe=STUB, argv_prefix=[sys.executable], timeout_s=1.0, mode="spawn",
+                            extra_env={"MI355X_STUB_PROBE_CONTROL": str(ctl)},
+                            kfd_proc_dir=str(fi.sysfs / "class/kfd/kfd/proc"))
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=1,
+                                          liveness_mode="spawn"),
+                        prober=prober, ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+
+    async def go():
+        try:
+            await mon.check_once()
+        finally:
+            await mon.close()
+
+    run(go(), timeout=60)
+    assert mon.health(busy_dev) == "Healthy"
+    assert mon.health(idle_dev) == "Unhealthy"
