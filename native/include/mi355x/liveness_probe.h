@@ -71,6 +71,10 @@ void mi355x_hsa_probe_release(void);
 // after a failed probe). A kept probe is one AQL packet: no kfd ioctl, so no
 // HWS runlist update that would preempt the queues of the pods on that GPU.
 void mi355x_hsa_probe_keep(int on);
+// Debug fault injection: flip one bit of output word `word` (0..1023; -1 = off)
+// of every later probe on `ordinal` (-1 = all devices) before verification.
+// The verdict path (tile compare, JSON, plugin health) sees a wrong MFMA result.
+void mi355x_hsa_probe_corrupt(int word, int ordinal);
 // Runtime start-up split of the last mi355x_hsa_probe_init (us): dlopen of
 // ROCr (its constructors), pre-open of /dev/kfd (on a second thread,
 // overlapped with the dlopen), hsa_init, agent enumeration, pool discovery.

@@ -22,6 +22,7 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -469,6 +470,13 @@ void submit_dispatch(ProbeResources& r, const KernelInfo& k, uint32_t nonce, int
 // Bounded wait for the dispatch submitted on r (nonce / iters as submitted),
 // then the verdict. Returns false, with out->hip_error = -1, if it has not
 // completed yet: r must then never be freed (the kernel may still write to it).
+// Debug fault injection (mi355x_hsa_probe_corrupt): flip one bit of output
+// word `word` of probes on `ordinal` (-1 = every device) after the dispatch
+// completed and before the tile is verified -- a stand-in for a wrong MFMA
+// result that drives the real verdict path end to end.
+std::atomic<int> g_corrupt_word{-1};
+std::atomic<int> g_corrupt_ordinal{-1};
+
 bool wait_and_verify(const Agent& ag, ProbeResources& r, uint32_t nonce, int iters, double timeout_s,
                      mi355x_probe_result* out) {
   using clk = std::chrono::steady_clock;
@@ -490,6 +498,14 @@ bool wait_and_verify(const Agent& ag, ProbeResources& r, uint32_t nonce, int ite
     out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
   out->nonce = nonce;
   out->iters = iters;
+  const int cw = g_corrupt_word.load(std::memory_order_relaxed);
+  const int co = g_corrupt_ordinal.load(std::memory_order_relaxed);
+  if (cw >= 0 && cw < MI355X_PROBE_OUT && (co < 0 || co == out->ordinal)) {
+    uint32_t bits;
+    std::memcpy(&bits, &r.h_out[cw], sizeof(bits));
+    bits ^= 1u;
+    std::memcpy(&r.h_out[cw], &bits, sizeof(bits));
+  }
   mi355x::verify_tile(r.h_out, r.h_meta, nonce, iters, out);
   return true;
 }
@@ -540,6 +556,11 @@ Resident* resident_slot(int ordinal) {
 }
 
 }  // namespace
+
+extern "C" void mi355x_hsa_probe_corrupt(int word, int ordinal) {
+  g_corrupt_word.store(word, std::memory_order_relaxed);
+  g_corrupt_ordinal.store(ordinal, std::memory_order_relaxed);
+}
 
 extern "C" void mi355x_hsa_probe_keep(int on) {
   std::lock_guard<std::mutex> lk(g_resident_mu);

@@ -6,6 +6,7 @@
 //   mi355x-liveness-probe --sweep [--devices ..]   (every CU of every XCD, see mi355x_chip_sweep)
 //   mi355x-liveness-probe --peer [--devices ..] [--peer-bytes B] [--peer-reps R]
 //                                      (DMA copy over every GPU pair's link, verified)
+//   --corrupt-word K[@O] / $MI355X_PROBE_CORRUPT_FILE: debug fault injection (see refresh_fault_injection)
 //
 // Built twice from this file: `mi355x-liveness-probe` launches through ROCr
 // directly (MI355X_PROBE_HSA; links only libhsa-runtime64, one AQL dispatch),
@@ -113,7 +114,9 @@ void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
 void teardown() { mi355x_hsa_probe_release(); }
 void runtime_shutdown() { mi355x_hsa_probe_shutdown(); }
 void keep_resources(bool on) { mi355x_hsa_probe_keep(on ? 1 : 0); }
+void set_corrupt(int word, int ordinal) { mi355x_hsa_probe_corrupt(word, ordinal); }
 #else
+void set_corrupt(int, int) {}
 void keep_resources(bool) {}  // the HIP build reuses its runtime's queues anyway
 void init_phases(double out[5]) { out[0] = out[1] = out[2] = out[3] = out[4] = 0; }
 void defer_teardown() {}
@@ -142,6 +145,43 @@ int peer(int a, int b, uint32_t, uint64_t bytes, int reps, double, mi355x_peer_r
   return 1;
 }
 #endif
+
+// Debug fault injection for tests of the verdict path on real hardware:
+// "K" or "K@O" (flip one bit of output word K, on ordinal O only) from
+// --corrupt-word, or from the file named by $MI355X_PROBE_CORRUPT_FILE, which
+// is re-read before every request so a test can turn it on and off under a
+// running server. Empty / missing = off.
+int g_flag_corrupt_word = -1;
+int g_flag_corrupt_ordinal = -1;
+
+void parse_corrupt(const char* spec, int* word, int* ordinal) {
+  *word = -1;
+  *ordinal = -1;
+  if (!spec || !*spec) return;
+  char* end = nullptr;
+  const long w = std::strtol(spec, &end, 0);
+  if (end == spec) return;
+  *word = static_cast<int>(w);
+  if (*end == '@') *ordinal = std::atoi(end + 1);
+}
+
+void refresh_fault_injection() {
+  int word = g_flag_corrupt_word, ordinal = g_flag_corrupt_ordinal;
+  if (const char* path = std::getenv("MI355X_PROBE_CORRUPT_FILE")) {
+    char buf[64] = {0};
+    if (FILE* f = std::fopen(path, "r")) {
+      if (!std::fgets(buf, sizeof(buf), f)) buf[0] = 0;
+      std::fclose(f);
+    }
+    int fw, fo;
+    parse_corrupt(buf, &fw, &fo);
+    if (fw >= 0) {
+      word = fw;
+      ordinal = fo;
+    }
+  }
+  set_corrupt(word, ordinal);
+}
 
 // Probe (or identify) a set of ordinals, one host thread per GPU so an 8-GPU
 // request pays one device setup, not eight. Returns true when all are live.
@@ -323,6 +363,7 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
       while (*p == ' ') ++p;
     }
     std::vector<mi355x_probe_result> results;
+    refresh_fault_injection();
     defer_teardown();
     std::string body;
     bool ok;
@@ -396,11 +437,14 @@ int main(int argc, char** argv) {
       sweep_mode = true;
     } else if (a == "--peer-bytes") {
       peer_bytes = std::strtoull(next("--peer-bytes"), nullptr, 0);
+    } else if (a == "--corrupt-word") {
+      parse_corrupt(next("--corrupt-word"), &g_flag_corrupt_word, &g_flag_corrupt_ordinal);
     } else if (a == "--peer-reps") {
       peer_reps = std::atoi(next("--peer-reps"));
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
-                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve [--keep]] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep]\n",
+                  "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve [--keep]] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep] "
+                  "[--corrupt-word K[@ORDINAL]]\n",
                   argv[0]);
       return 0;
     } else {
@@ -460,6 +504,7 @@ int main(int argc, char** argv) {
   std::vector<mi355x_probe_result> results;
   // Queues/executables are torn down after the verdict is printed: the caller
   // (container runtime, health loop) only waits for the JSON line.
+  refresh_fault_injection();
   defer_teardown();
   const bool all_ok = run_batch(ords, nonces, iters, timeout_s, identify, n, results);
   const uint64_t t_ready = mono_ns();

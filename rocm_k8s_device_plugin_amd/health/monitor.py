@@ -42,7 +42,7 @@ from ..utils import log
 from ..utils.trace import TRACER
 from . import exporter
 from .fabric import FabricWatcher
-from .liveness import LivenessProber
+from .liveness import LivenessProber, ProbeOutcome
 
 _log = log.get("health")
 
@@ -122,6 +122,7 @@ class HealthMonitor:
         self.fabric = FabricWatcher(inventory, fabric_source) if self.cfg.smi_xgmi else None
         self._smi_held = False   # amd-smi kept initialised while its sources are on (smi_hold)
         self.busy_state_known = True   # last sweep could tell busy GPUs from idle ones
+        self.identity_remaps = 0       # sweeps whose probe replies did not match the positional ordinals
 
     # ------------------------------------------------------------------ fabric
     def degraded_links(self):
@@ -295,6 +296,88 @@ class HealthMonitor:
         REGISTRY.set("mi355x_dp_busy_state_known", 1.0 if known else 0.0,
                      help="1 if busy GPUs can be told from idle ones (kfd process list readable)")
 
+    @staticmethod
+    def _reply_identity(detail: dict):
+        """(kfd node id, pci domain, kfd-style location_id) of the agent that
+        answered, from the probe reply; None when the reply carries none."""
+        nid = int(detail.get("kfd_node_id", -1) if detail.get("kfd_node_id") is not None else -1)
+        loc = dom = None
+        bus_id = detail.get("pci_bus_id") or ""
+        try:
+            d, b, df = bus_id.split(":")
+            dev, fn = df.split(".")
+            dom, loc = int(d, 16), (int(b, 16) << 8) | (int(dev, 16) << 3) | int(fn, 16)
+        except ValueError:
+            pass
+        if nid < 0 and loc is None:
+            return None
+        return nid, dom, loc
+
+    def _identity_matches(self, dev_id: str, ident) -> bool:
+        d = self.inv.by_id.get(dev_id)
+        if d is None or ident is None:
+            return True
+        nid, dom, loc = ident
+        # the PCI location (partition index in the function bits) is exact; the
+        # agent's node id is the thunk's index, renumbered when the device
+        # cgroup hides GPUs (measured on MI355X), so it is only a fallback
+        if loc is not None and d.location_id:
+            return (dom, loc) == (d.domain, d.location_id)
+        if nid >= 0 and d.node_id >= 0:
+            return nid == d.node_id
+        return True
+
+    def _verify_identity(self, ords: Dict[str, int], outcomes: Dict[str, ProbeOutcome]) -> Dict[str, ProbeOutcome]:
+        """Check that every reply came from the device its verdict is written to.
+
+        Ordinals are positional (ROCr enumerates accessible GPU nodes in kfd node
+        order, hip_ordinals); a different enumeration (a hidden node, CPX
+        partitions ordered differently) would put verdicts on the wrong kubelet
+        IDs. Each reply names its agent's PCI location (kfd location_id, with
+        the partition index in the function bits), so on any mismatch the verdicts of this
+        sweep are re-keyed by identity, the ordinal map is rebuilt from the
+        replies, and a device no reply identifies loses its ordinal (reported
+        "no HIP device for this ID")."""
+        idents = {dev: self._reply_identity(o.detail) for dev, o in outcomes.items()}
+        bad = sorted(dev for dev in outcomes if not self._identity_matches(dev, idents[dev]))
+        if not bad:
+            return outcomes
+        from ..utils.metrics import REGISTRY
+        by_node, by_loc = {}, {}
+        for dev, o in outcomes.items():
+            ident = idents[dev]
+            if ident is None:
+                continue
+            nid, dom, loc = ident
+            if loc is not None:
+                by_loc[(dom, loc)] = (ords[dev], o)
+            elif nid >= 0:
+                by_node[nid] = (ords[dev], o)
+        fixed: Dict[str, ProbeOutcome] = {}
+        new_ords: Dict[str, int] = {}
+        for dev in ords:
+            d = self.inv.by_id.get(dev)
+            hit = None
+            if d is not None:
+                hit = by_loc.get((d.domain, d.location_id)) if d.location_id else None
+                if hit is None and d.node_id >= 0:
+                    hit = by_node.get(d.node_id)
+            if hit is not None and self._identity_matches(dev, self._reply_identity(hit[1].detail)):
+                new_ords[dev] = hit[0]
+                fixed[dev] = hit[1]
+        for dev, ordinal in new_ords.items():
+            if ords.get(dev) != ordinal:
+                _log.error("probe identity: device %s is ordinal %d, not %s (verdict re-keyed)", dev, ordinal,
+                           ords.get(dev))
+        lost = sorted(set(ords) - set(new_ords))
+        if lost:
+            _log.error("probe identity: no probed agent matches %s; they lose their ordinal", lost)
+        self._ordinals = new_ords
+        self.identity_remaps += 1
+        REGISTRY.inc("mi355x_dp_probe_identity_mismatch_total",
+                     help="sweeps whose probe replies came from other devices than the positional ordinal map")
+        return fixed
+
     async def _liveness(self, ords: Dict[str, int], busy_devs=frozenset()):
         every = self.cfg.chip_sweep_every
         busy = {o for d, o in ords.items() if d in busy_devs}
@@ -344,7 +427,8 @@ class HealthMonitor:
         if self.cfg.liveness and self.prober is not None:
             ords = {k: v for k, v in self.ordinals().items() if k in reasons}
             busy_devs = self._busy_devices(ords)
-            outcomes = await self._liveness(ords, busy_devs)
+            outcomes = self._verify_identity(ords, await self._liveness(ords, busy_devs))
+            ords = {k: v for k, v in self.ordinals().items() if k in reasons}
             from ..utils.metrics import REGISTRY
             now = time.monotonic()
             grace = self.cfg.liveness_busy_grace_s if self.busy_state_known else \

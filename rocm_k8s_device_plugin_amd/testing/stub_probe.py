@@ -25,14 +25,23 @@ def _control():
     return {}
 
 
-def _device(ordinal_reported, mode, nonce):
+def _identity(ordinal):
+    """Agent identity per host ordinal from $MI355X_STUB_PROBE_IDENTITY (JSON
+    {ordinal: {"kfd_node_id": N, "pci_bus_id": "dddd:bb:dd.f"}}); unknown otherwise."""
+    raw = os.environ.get("MI355X_STUB_PROBE_IDENTITY")
+    ident = json.loads(raw).get(str(ordinal), {}) if raw else {}
+    return {"kfd_node_id": int(ident.get("kfd_node_id", -1)), "pci_bus_id": ident.get("pci_bus_id", "")}
+
+
+def _device(ordinal_reported, mode, nonce, host_ordinal=None):
     ok = mode == "ok"
-    return {"ordinal": ordinal_reported, "ok": ok or mode == "stale", "hip_error": 0, "mismatches": 0 if ok else 17,
-           "nonce": nonce if mode != "stale" else (nonce + 1) & 0xFFFFFFFF, "xcc_id": 0, "hw_id": 0, "iters": 4,
-           "dispatches": 1, "kfd_node_id": -1, "runtime": "stub", "kernel_us": 3.0, "setup_us": 1.0,
-           "total_us": 5.0, "pci_bus_id": "", "arch": "gfx950", "name": "", "uuid": "", "pci_domain": 0,
-           "pci_bus": 0, "pci_device": 0, "cu_count": 256, "total_mem": 0,
-           "error": "" if ok or mode == "stale" else "17/1024 MFMA results differ from host reference"}
+    return {**_identity(ordinal_reported if host_ordinal is None else host_ordinal),
+            "ordinal": ordinal_reported, "ok": ok or mode == "stale", "hip_error": 0, "mismatches": 0 if ok else 17,
+            "nonce": nonce if mode != "stale" else (nonce + 1) & 0xFFFFFFFF, "xcc_id": 0, "hw_id": 0, "iters": 4,
+            "dispatches": 1, "runtime": "stub", "kernel_us": 3.0, "setup_us": 1.0,
+            "total_us": 5.0, "arch": "gfx950", "name": "", "uuid": "", "pci_domain": 0,
+            "pci_bus": 0, "pci_device": 0, "cu_count": 256, "total_mem": 0,
+            "error": "" if ok or mode == "stale" else "17/1024 MFMA results differ from host reference"}
 
 
 def _kfd_entry():
@@ -134,7 +143,10 @@ def main(argv):
     allow = os.environ.get("MI355X_DEV_ALLOW")
     count = (sum(1 for p in allow.split(";") if "/renderD" in p) if allow is not None
              else max(1, len(wanted)))
-    devs = [_device(int(o), mode, nonce + i) for i, o in enumerate(wanted)]
+    host = os.environ.get("ROCR_VISIBLE_DEVICES")
+    devs = [_device(int(o), mode, nonce + i, host_ordinal=int(host.split(",")[int(o)])
+                    if host and int(o) < len(host.split(",")) else None)
+            for i, o in enumerate(wanted)]
     ok = all(d["ok"] for d in devs)
     doc = {"ok": ok, "hip_device_count": count, "identify": False, "t_start_ns": t, "t_runtime_ns": t,
            "t_ready_ns": time.monotonic_ns(), "devices": devs}

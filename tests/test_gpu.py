@@ -33,6 +33,13 @@ def ordinals(inv):
     return hip_ordinals(inv, "/dev")
 
 
+def _location(reply):
+    """(domain, kfd-style location_id) from a probe reply's dddd:bb:dd.f."""
+    d, b, df = reply["pci_bus_id"].split(":")
+    dev, fn = df.split(".")
+    return int(d, 16), (int(b, 16) << 8) | (int(dev, 16) << 3) | int(fn, 16)
+
+
 def test_inprocess_mfma_probe(hip):
     n = hip.device_count()
     assert n >= 1
@@ -62,11 +69,12 @@ def test_inprocess_hsa_direct_probe(hip, inv):
         assert r["nonce"] == nonce and r["mismatches"] == 0
         assert 0 < r["kernel_us"] < 10000
         # DRIVER_NODE_ID is the thunk's node index, which is renumbered when the
-        # container's device cgroup hides GPUs; match the agent by PCI location
+        # container's device cgroup hides GPUs; match the agent by its full PCI
+        # location (kfd location_id: bus, device and function = partition index)
         assert r["kfd_node_id"] >= 0
-        devs = [d for d in inv.devices if d.identity == "kfd" and (d.location_id >> 8) & 0xFF == r["pci_bus"]]
+        devs = [d for d in inv.devices if _location(r) == (d.domain, d.location_id)]
         assert len(devs) == 1, (r, inv.devices)
-        assert r["pci_domain"] == devs[0].domain
+        assert devs[0].identity == "kfd"
 
 
 @pytest.mark.parametrize("runtime", ["hsa", "hip"])
@@ -181,6 +189,102 @@ def test_liveness_monitor_marks_live_devices_healthy(inv, ordinals):
     asyncio.run(mon.check_once())
     snap = mon.snapshot()
     assert all(v.health == "Healthy" for v in snap.values()), snap
+
+
+def test_probe_replies_carry_the_identity_of_their_device(inv, ordinals):
+    """Every reply of the real server names the device its verdict is written
+    to (full location_id), so the monitor's identity check never re-keys."""
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig, HealthMonitor
+    from rocm_k8s_device_plugin_amd.topology import Inventory
+    acc = Inventory(sysfs_root="/sys", devices=tuple(inv.by_id[i] for i in ordinals), topology=inv.topology,
+                    driver_loaded=True, kfd_present=True)
+    mon = HealthMonitor(acc, HealthConfig(exporter_socket=None, liveness=True, liveness_timeout_s=60))
+
+    async def go():
+        try:
+            res = await mon.prober.probe(dict(ordinals))
+            for dev_id, r in res.items():
+                assert r.ok, r
+                assert _location(r.detail) == (acc.by_id[dev_id].domain, acc.by_id[dev_id].location_id), \
+                    (dev_id, r.detail["pci_bus_id"])
+            for _ in range(3):
+                await mon.check_once()
+        finally:
+            await mon.close()
+
+    asyncio.run(go())
+    assert mon.identity_remaps == 0 and mon.ordinals() == dict(ordinals)
+    assert all(v.health == "Healthy" for v in mon.snapshot().values())
+
+
+def test_corrupted_tile_turns_device_unhealthy_in_listandwatch(inv, ordinals, tmp_path, monkeypatch):
+    """Fault injection on the real probe (one output bit flipped before
+    verification, $MI355X_PROBE_CORRUPT_FILE re-read per request): the persistent
+    server fails the tile, the fresh-process confirmation fails it too, and the
+    kubelet's ListAndWatch stream shows the device Unhealthy; clearing the fault
+    brings it back Healthy."""
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+    from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+    from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+    from rocm_k8s_device_plugin_amd.topology import Inventory
+
+    dev_id, o = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
+    acc = Inventory(sysfs_root="/sys", devices=(inv.by_id[dev_id],), topology=inv.topology,
+                    driver_loaded=True, kfd_present=True)
+    fault = tmp_path / "corrupt"
+    fault.write_text("")
+    monkeypatch.setenv("MI355X_PROBE_CORRUPT_FILE", str(fault))
+
+    async def wait_health(k, want, timeout):
+        deadline = asyncio.get_running_loop().time() + timeout
+        while True:
+            st = k.resources["amd.com/gpu"]
+            if st.devices.get(dev_id) == want:
+                return
+            left = deadline - asyncio.get_running_loop().time()
+            assert left > 0, f"{dev_id} never became {want}: {st.devices}"
+            try:
+                await k.wait_for_update("amd.com/gpu", st.updates, timeout=min(left, 2.0))
+            except TimeoutError:
+                pass
+
+    async def go(tmp):
+        k = FakeKubelet(tmp)
+        await k.start()
+        impl = ContainerImpl("single", "/sys", HealthConfig(exporter_socket=None, liveness=True,
+                                                            liveness_timeout_s=30, fail_threshold=2),
+                             inventory=acc)
+        impl.monitor._ordinals = {dev_id: o}
+        mgr = PluginManager(impl, ManagerConfig(pulse_s=0.3, plugin_dir=tmp, handle_signals=False))
+        t = asyncio.create_task(mgr.run())
+        try:
+            await k.wait_for_resource("amd.com/gpu", 1, timeout=30)
+            await wait_health(k, "Healthy", 30)
+            fault.write_text("17")     # every agent: the confirming process sees this GPU as its ordinal 0
+            await wait_health(k, "Unhealthy", 60)
+            reasons = impl.monitor.snapshot()[dev_id].reasons
+            assert any("differ" in r for r in reasons), reasons
+            fault.write_text("")
+            await wait_health(k, "Healthy", 60)
+            assert impl.monitor.identity_remaps == 0
+            assert impl.monitor.prober.server_starts >= 1
+        finally:
+            mgr.request_stop()
+            await t
+            await k.stop()
+
+    asyncio.run(asyncio.wait_for(go(str(tmp_path)), 180))
+
+
+def test_probe_cli_corrupt_word_fails_the_tile():
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    p = subprocess.run([str(probe_executable("hsa")), "--devices", "0", "--corrupt-word", "3"], capture_output=True,
+                       timeout=120)
+    doc = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    assert p.returncode == 1 and not doc["ok"], doc
+    d = doc["devices"][0]
+    assert d["mismatches"] == 1 and d["hip_error"] == 0, d
 
 
 def test_persistent_probe_server(ordinals):

@@ -1056,3 +1056,65 @@ def test_spawn_mode_deadline_on_busy_gpu_is_inconclusive(tmp_path):
     run(go(), timeout=60)
     assert mon.health(busy_dev) == "Healthy"
     assert mon.health(idle_dev) == "Unhealthy"
+
+
+def _bus_id(d):
+    loc = d.location_id
+    return f"{d.domain:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+
+
+@pytest.mark.parametrize("mode", ["single", "cpx"])
+def test_probe_identity_rekeys_verdicts(tmp_path, mode):
+    """The positional ordinal map is wrong (ROCr enumerated the agents in
+    another order): every reply names its agent (kfd node, location_id with
+    the partition index in the function bits), so the failing agent's verdict
+    lands on its own kubelet ID and the ordinal map is rebuilt from the replies."""
+    fi = make_mi355x_node(tmp_path / "n", **({"compute_partition": "CPX"} if mode == "cpx" else {}))
+    inv = discover(str(fi.sysfs))
+    n = len(inv.devices)
+    truth = {d.id: i for i, d in enumerate(inv.devices)}               # what ROCr really enumerates
+    wrong = {d.id: n - 1 - i for i, d in enumerate(inv.devices)}        # what the plugin assumed
+    ident = {str(i): {"kfd_node_id": d.node_id, "pci_bus_id": _bus_id(d)} for i, d in enumerate(inv.devices)}
+    ctl, prober = _stub_prober(tmp_path, {"3": "fail"})
+    prober.extra_env["MI355X_STUB_PROBE_IDENTITY"] = json.dumps(ident)
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=1),
+                        prober=prober, ordinal_map=wrong)
+
+    async def go():
+        try:
+            await mon.check_once()
+            await mon.check_once()
+        finally:
+            await mon.close()
+
+    run(go(), timeout=60)
+    bad = inv.devices[3].id
+    assert mon.health(bad) == "Unhealthy"
+    assert all(mon.health(d.id) == "Healthy" for d in inv.devices if d.id != bad)
+    assert mon.ordinals() == truth
+    assert mon.identity_remaps == 1                   # second sweep already used the rebuilt map
+
+
+def test_probe_identity_unmatched_device_loses_its_ordinal(tmp_path):
+    """A reply from an agent no advertised device corresponds to: the device
+    the verdict was meant for is reported without a HIP device, not Healthy."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ident = {str(i): {"kfd_node_id": d.node_id, "pci_bus_id": _bus_id(d)} for i, d in enumerate(inv.devices)}
+    ident["5"] = {"kfd_node_id": 999, "pci_bus_id": "0000:ff:00.0"}
+    ctl, prober = _stub_prober(tmp_path, {})
+    prober.extra_env["MI355X_STUB_PROBE_IDENTITY"] = json.dumps(ident)
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True),
+                        prober=prober, ordinal_map={d.id: i for i, d in enumerate(inv.devices)})
+
+    async def go():
+        try:
+            await mon.check_once()
+        finally:
+            await mon.close()
+
+    run(go(), timeout=60)
+    victim = inv.devices[5].id
+    assert mon.health(victim) == "Unhealthy"
+    assert any("no HIP device" in r for r in mon.snapshot()[victim].reasons)
+    assert sum(mon.health(d.id) == "Healthy" for d in inv.devices) == len(inv.devices) - 1
