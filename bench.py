@@ -98,6 +98,17 @@ def make_parser():
                     help="> 0: run the plugin as the health DaemonSet does (MFMA liveness via the kept-queue probe "
                          "server, amd-smi ECC / events / xGMI link state) with this pulse in seconds, while pods "
                          "are admitted (BASELINE config: health-check DaemonSet enabled)")
+    ap.add_argument("--advertise", type=int, default=0,
+                    help="advertise M devices and request --gpus N of them per pod (default M = N: the headline, "
+                         "'GPUs advertised at N'). With M > N the timed admissions start from a fragmented "
+                         "availability (--hold devices held by other pods), so GetPreferredAllocation searches")
+    ap.add_argument("--hold", type=int, default=-1,
+                    help="with M > N: devices held by other pods during the run (default (M-N)//2, alternating "
+                         "positions so every hive is fragmented)")
+    ap.add_argument("--fragmented-compare", type=int, default=5,
+                    help="with M = N and more accessible devices than N: extra untimed admissions of N out of "
+                         "every accessible device from a fragmented availability (a second plugin instance), "
+                         "reported in extra.fragmented_n_of_m (BASELINE config: full-node hive-aware allocation)")
     ap.add_argument("--json-out", default="")
     return ap
 
@@ -111,6 +122,78 @@ def pct(xs, q):
     if not s:
         return float("nan")
     return s[min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))]
+
+
+def alloc_summary(pl, steps):
+    """GetPreferredAllocation over admissions that all start from the same
+    availability: RPC time, whether the search ran (no short-circuit), its
+    candidate count, and the chosen set against the reference's ordered BFS
+    (C++ re-simulation) on that availability."""
+    if not steps:
+        return {}
+    avail = pl.available()
+    n = len(steps[0][3])
+    ref = pl.allocator.reference_allocate(avail, [], n) if len(avail) > n else None
+    chosen = {tuple(x[3]) for x in steps}
+    return {"available": len(avail),
+            "preferred_rpc_p50_ms": round(pct([x[0] for x in steps], .5), 4),
+            "preferred_used": all(x[4] for x in steps),
+            "short_circuit_steps": sum(1 for x in steps if x[1]),
+            "candidates": max(x[2] for x in steps),
+            "chosen": [list(c) for c in sorted(chosen)],
+            "reference_candidates": ref["candidates"] if ref else None,
+            "same_set_as_reference": (chosen == {tuple(sorted(ref["ids"]))}) if ref else None}
+
+
+def fragment(ids, n, hold=-1):
+    """Devices other pods hold: alternating positions (every hive loses some),
+    (M-N)//2 of them by default, never leaving fewer than n free."""
+    m = len(ids)
+    h = (m - n) // 2 if hold < 0 else hold
+    h = max(0, min(h, m - n))
+    return (list(ids[1::2]) + list(ids[0::2]))[:h]
+
+
+class PluginUnderTest:
+    """Rank 0: the real plugin advertising `devs` (real discovery data, real
+    allocator and gRPC servicer) behind a fake kubelet on its own UDS dir."""
+
+    def __init__(self, loop, tmp, name, sysfs, devs, full, ords, hcfg, pulse_s):
+        from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+        from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
+        from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+        from rocm_k8s_device_plugin_amd.topology import Inventory
+        self.loop = loop
+        self.devs = tuple(devs)
+        self.inv = Inventory(sysfs_root=sysfs, devices=self.devs, topology=full.topology,
+                             driver_loaded=full.driver_loaded, kfd_present=full.kfd_present)
+        self.impl = ContainerImpl("single", sysfs, hcfg, inventory=self.inv)
+        pdir = os.path.join(tmp, name)
+        self.kubelet = FakeKubelet(pdir)
+        loop.run_until_complete(self.kubelet.start())
+        self.mgr = PluginManager(self.impl, ManagerConfig(pulse_s=pulse_s, plugin_dir=pdir, handle_signals=False))
+        self.task = loop.create_task(self.mgr.run())
+        loop.run_until_complete(self.kubelet.wait_for_resource("amd.com/gpu", len(self.devs), timeout=30))
+        self.minor_to_ord = {dv.render_minor: ords[dv.id] for dv in self.devs}
+        self.minor_to_paths = {dv.render_minor: dv.dev_paths() for dv in self.devs}
+        self.held = []
+
+    def hold(self, ids):
+        """Mark `ids` allocated to other pods (kubelet's view: not available)."""
+        self.kubelet.resources["amd.com/gpu"].allocated.update(ids)
+        self.held = list(ids)
+
+    @property
+    def allocator(self):
+        return self.mgr.plugins["gpu"].ctx.allocator
+
+    def available(self):
+        return self.kubelet.healthy_free("amd.com/gpu")
+
+    def stop(self):
+        self.loop.run_until_complete(self.kubelet.stop())
+        self.mgr.request_stop()
+        self.loop.run_until_complete(self.task)
 
 
 class Dist:
@@ -186,15 +269,14 @@ def main():
     from rocm_k8s_device_plugin_amd.container_runtime import render_minors_from_specs, start_container
 
     loop = None
-    kubelet = mgr = mgr_task = impl = None
-    minor_to_ord = {}
+    plug = impl = None
     tmp = None
+    m_adv = args.advertise or n
+    if m_adv < n:
+        raise SystemExit(f"--advertise {m_adv} < --gpus {n}")
     if d.rank == 0:
         from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
-        from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
-        from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
-        from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
-        from rocm_k8s_device_plugin_amd.topology import Inventory, discover, hip_ordinals
+        from rocm_k8s_device_plugin_amd.topology import discover, hip_ordinals
         from rocm_k8s_device_plugin_amd.utils import log as ulog
         ulog.setup(0)
         import logging
@@ -209,25 +291,18 @@ def main():
         full = discover(sysfs)
         ords = hip_ordinals(full, devroot, check_access=not args.fixture)
         usable = sorted((dv for dv in full.devices if dv.id in ords), key=lambda dv: ords[dv.id])
-        if len(usable) < n:
-            raise SystemExit(f"only {len(usable)} accessible GPU devices on this node, need {n}")
-        adv = tuple(usable[:n])     # "GPUs advertised at N"
-        inv = Inventory(sysfs_root=sysfs, devices=adv, topology=full.topology, driver_loaded=full.driver_loaded,
-                        kfd_present=full.kfd_present)
-        minor_to_ord = {dv.render_minor: ords[dv.id] for dv in adv}
-        minor_to_paths = {dv.render_minor: dv.dev_paths() for dv in adv}
+        if len(usable) < m_adv:
+            raise SystemExit(f"only {len(usable)} accessible GPU devices on this node, need {m_adv}")
+        adv = tuple(usable[:m_adv])     # "GPUs advertised at N" (or M with --advertise)
         adv_ordinals = [ords[dv.id] for dv in adv]
         hp = args.health_pulse if not args.fixture else 0.0
         hcfg = (HealthConfig(exporter_socket=None, liveness=True, smi_ecc=True, smi_events=True, smi_xgmi=True)
                 if hp > 0 else HealthConfig(exporter_socket=None))
-        impl = ContainerImpl("single", sysfs, hcfg, inventory=inv)
-        pdir = os.path.join(tmp, "device-plugins")
         loop = asyncio.new_event_loop()
-        kubelet = FakeKubelet(pdir)
-        loop.run_until_complete(kubelet.start())
-        mgr = PluginManager(impl, ManagerConfig(pulse_s=hp, plugin_dir=pdir, handle_signals=False))
-        mgr_task = loop.create_task(mgr.run())
-        loop.run_until_complete(kubelet.wait_for_resource("amd.com/gpu", n, timeout=30))
+        plug = PluginUnderTest(loop, tmp, "device-plugins", sysfs, adv, full, ords, hcfg, hp)
+        impl, inv = plug.impl, plug.inv
+        if m_adv > n:
+            plug.hold(fragment([dv.id for dv in adv], n, args.hold))
         gpu_info = {"ids": [dv.id for dv in adv], "gfx_target_version": sorted({dv.gfx_target_version for dv in adv}),
                     "hive_ids": sorted({str(dv.hive_id) for dv in adv}),
                     "partition": sorted({dv.partition_type for dv in adv})}
@@ -246,18 +321,29 @@ def main():
             return loop.run_until_complete(asyncio.to_thread(functools.partial(fn, *a, **kw)))
         return fn(*a, **kw)
 
+    alloc_steps = []   # per timed admission: (preferred RPC ms, short-circuit, candidates, chosen set)
+
     def one_step(record: bool, runtime: str = args.container_runtime, sink=None, settle: str = args.settle,
-                 init_sink=None, mode: str = args.container_mode, dev_view: str = args.dev_view):
+                 init_sink=None, mode: str = args.container_mode, dev_view: str = args.dev_view, pl=None,
+                 alloc_sink=None):
         if d.rank == 0:
+            pl = pl or plug
             t0 = time.monotonic_ns()
-            adm = loop.run_until_complete(kubelet.admit("amd.com/gpu", n))
+            adm = loop.run_until_complete(pl.kubelet.admit("amd.com/gpu", n))
+            st = pl.allocator.stats
+            a_rec = (adm.preferred_ms, bool(st.last_short_circuit), int(st.last_candidates),
+                     sorted(adm.device_ids), adm.preferred_used)
+            if record:
+                alloc_steps.append(a_rec)
+            if alloc_sink is not None:
+                alloc_sink.append(a_rec)
             car = adm.response.container_responses[0]
             minors = render_minors_from_specs(car)
-            ordl = [minor_to_ord[m] for m in minors]
+            ordl = [pl.minor_to_ord[m] for m in minors]
             mounts = [(m.container_path, m.host_path) for m in car.mounts]
             # the container's /dev: the DeviceSpecs, per allocated GPU (card + render node)
             spec_paths = {ds.host_path for ds in car.devices}
-            groups = [[p for p in minor_to_paths[m] if p in spec_paths] for m in minors]
+            groups = [[p for p in pl.minor_to_paths[m] if p in spec_paths] for m in minors]
             payload = (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids), mounts, groups)
         else:
             payload = None
@@ -289,7 +375,7 @@ def main():
         slowest = max(allr, key=lambda m: m[1])
         t_ready = slowest[1]
         if d.rank == 0:
-            kubelet.release("amd.com/gpu", ids)
+            pl.kubelet.release("amd.com/gpu", ids)
         # pod termination: the driver finishes tearing down each container's
         # kfd process ~150 ms after it exits (bench latency excludes this wait)
         # N containers exiting together may be torn down one after another: allow
@@ -351,6 +437,25 @@ def main():
         for _ in range(args.b2b_compare):
             one_step(False, sink=b2b_lat, settle="none")
 
+    # N of every accessible device, from a fragmented availability (second plugin
+    # instance; the headline plugin keeps advertising exactly N)
+    frag = None
+    frag_lat, frag_alloc = [], []
+    do_frag = d.bcast(d.rank == 0 and m_adv == n and args.fragmented_compare > 0 and len(usable) > n)
+    if do_frag:
+        fplug = None
+        if d.rank == 0:
+            fplug = PluginUnderTest(loop, tmp, "device-plugins-all", sysfs, usable, full, ords,
+                                    HealthConfig(exporter_socket=None), 0.0)
+            fplug.hold(fragment([dv.id for dv in usable], n, args.hold))
+        for _ in range(args.fragmented_compare):
+            one_step(False, sink=frag_lat, pl=fplug, alloc_sink=frag_alloc)
+        if d.rank == 0:
+            frag = {"advertised": len(usable), "requested": n, "held": fplug.held,
+                    "latency_p50_ms": round(pct(frag_lat, .5), 3),
+                    **alloc_summary(fplug, frag_alloc)}
+            fplug.stop()
+
     rccl = None
     if args.collectives and d.world > 1:
         # the pod's GPUs as a torchrun workload sees them: one rank per GPU, RCCL over xGMI
@@ -369,7 +474,7 @@ def main():
     extra = {}
     if d.rank == 0:
         # allocator microbenchmark on the same request (ours vs the reference's ordered BFS)
-        pol = mgr.plugins["gpu"].ctx.allocator
+        pol = plug.allocator
         avail = [dv.id for dv in impl.devices("gpu")]
         t = time.perf_counter()
         for _ in range(200):  # both sides called straight into C++ (no trace/stats wrapper)
@@ -425,13 +530,16 @@ def main():
         from rocm_k8s_device_plugin_amd.parallel.fabric import Fabric
         extra["fabric"] = Fabric(inv).report([dv.id for dv in adv]).as_dict()
         extra["rccl"] = rccl
+        # the timed admissions' GetPreferredAllocation (with M > N: a real search
+        # over the fragmented availability) and the N-of-all-devices comparison
+        extra["timed_allocation"] = dict({"advertised": m_adv, "requested": n, "held": plug.held},
+                                         **alloc_summary(plug, alloc_steps))
+        extra["fragmented_n_of_m"] = frag
         if args.peer_check and not args.fixture:
             from rocm_k8s_device_plugin_amd.health.peer import probe_peers
             rep = probe_peers(adv_ordinals, nbytes=64 << 20, reps=3, timeout_s=120)
             extra["peer_probe"] = dict(rep.summary(), wall_ms=round(rep.wall_ms, 1))
-        loop.run_until_complete(kubelet.stop())
-        mgr.request_stop()
-        loop.run_until_complete(mgr_task)
+        plug.stop()
         loop.close()
         out = {
             "metric": METRIC,
@@ -450,7 +558,8 @@ def main():
                      if not args.fixture else "synthetic 8xMI355X sysfs fixture; stub-probe containers (CPU only)"),
             "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
                        "global_batch": n, "seq_len": None,
-                       "parallelism": (f"{n} GPUs advertised, 1 pod requesting {n}, " +
+                       "parallelism": (f"{m_adv} GPUs advertised, 1 pod requesting {n}, " +
+                                       (f"{len(plug.held)} held by other pods, " if plug.held else "") +
                                        ("1 container process with all N GPUs" if args.container_mode == "pod"
                                         else "1 container process per GPU")),
                        "between_admissions": ("previous pod's kfd teardown complete" if args.settle == "kfd"

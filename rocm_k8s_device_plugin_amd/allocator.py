@@ -24,6 +24,7 @@ class AllocStats:
     last_us: float = 0.0
     last_candidates: int = 0
     last_weight: int = -1
+    last_short_circuit: bool = False
 
 
 class Policy:
@@ -93,6 +94,7 @@ class BestEffortPolicy(Policy):
         self.stats.last_us = dt
         self.stats.last_candidates = r["candidates"]
         self.stats.last_weight = r["weight"]
+        self.stats.last_short_circuit = bool(r["short_circuit"])
         if r["error"]:
             raise AllocationError(r["error"])
         return list(r["ids"])

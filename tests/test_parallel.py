@@ -106,3 +106,25 @@ def test_bench_fixture_reports_fabric_and_collectives():
     e = d["extra"]
     assert e["container_dev_view"] == "specs" and e["latency_p50_ms_container_mode_per-gpu"] > 0
     assert len(e["steps_ms"]) == 2
+    # 2 of the fixture's 8 GPUs from a fragmented availability (second plugin
+    # instance, containers split one per rank as in the headline run)
+    fr = e["fragmented_n_of_m"]
+    assert fr["advertised"] == 8 and fr["requested"] == 2 and fr["short_circuit_steps"] == 0
+    assert fr["candidates"] > 0 and fr["same_set_as_reference"] is True
+
+
+def test_bench_n_of_m_searches_inside_the_timed_step():
+    """--gpus 3 --advertise 8: every timed admission's GetPreferredAllocation is
+    a real search (no short-circuit, candidates > 0) over a fragmented
+    availability, and picks the reference BFS's set."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    p = subprocess.run([sys.executable, "bench.py", "--fixture", "--gpus", "3", "--advertise", "8", "--steps", "3",
+                        "--warmup", "1"], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    ta = d["extra"]["timed_allocation"]
+    assert ta["advertised"] == 8 and ta["requested"] == 3 and len(ta["held"]) == 2 and ta["available"] == 6
+    assert ta["preferred_used"] and ta["short_circuit_steps"] == 0 and ta["candidates"] > 0
+    assert ta["same_set_as_reference"] is True and len(ta["chosen"]) == 1
+    assert "8 GPUs advertised, 1 pod requesting 3, 2 held" in d["config"]["parallelism"]
+    assert d["extra"]["fragmented_n_of_m"] is None       # only with M = N
