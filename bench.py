@@ -109,6 +109,11 @@ def make_parser():
                     help="with M = N and more accessible devices than N: extra untimed admissions of N out of "
                          "every accessible device from a fragmented availability (a second plugin instance), "
                          "reported in extra.fragmented_n_of_m (BASELINE config: full-node hive-aware allocation)")
+    ap.add_argument("--grpc-server", default="native", choices=["native", "aio"],
+                    help="the plugin's kubelet-facing gRPC server (-grpc_server)")
+    ap.add_argument("--kubelet-client", default="", choices=["", "native", "aio"],
+                    help="the fake kubelet's admission RPC client: native (a native HTTP/2 client, like kubelet's "
+                         "grpc-go) or aio (grpc.aio in the bench's event loop); default native with the native server")
     ap.add_argument("--json-out", default="")
     return ap
 
@@ -158,7 +163,8 @@ class PluginUnderTest:
     """Rank 0: the real plugin advertising `devs` (real discovery data, real
     allocator and gRPC servicer) behind a fake kubelet on its own UDS dir."""
 
-    def __init__(self, loop, tmp, name, sysfs, devs, full, ords, hcfg, pulse_s):
+    def __init__(self, loop, tmp, name, sysfs, devs, full, ords, hcfg, pulse_s, grpc_server="native",
+                 kubelet_client="native"):
         from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
         from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
         from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
@@ -169,9 +175,10 @@ class PluginUnderTest:
                              driver_loaded=full.driver_loaded, kfd_present=full.kfd_present)
         self.impl = ContainerImpl("single", sysfs, hcfg, inventory=self.inv)
         pdir = os.path.join(tmp, name)
-        self.kubelet = FakeKubelet(pdir)
+        self.kubelet = FakeKubelet(pdir, rpc_client=kubelet_client)
         loop.run_until_complete(self.kubelet.start())
-        self.mgr = PluginManager(self.impl, ManagerConfig(pulse_s=pulse_s, plugin_dir=pdir, handle_signals=False))
+        self.mgr = PluginManager(self.impl, ManagerConfig(pulse_s=pulse_s, plugin_dir=pdir, handle_signals=False,
+                                                          grpc_server=grpc_server))
         self.task = loop.create_task(self.mgr.run())
         loop.run_until_complete(self.kubelet.wait_for_resource("amd.com/gpu", len(self.devs), timeout=30))
         self.minor_to_ord = {dv.render_minor: ords[dv.id] for dv in self.devs}
@@ -185,7 +192,19 @@ class PluginUnderTest:
 
     @property
     def allocator(self):
+        self.mgr.plugins["gpu"].sync()     # native server: apply its pending call events first
         return self.mgr.plugins["gpu"].ctx.allocator
+
+    def server_ms(self, reset=False):
+        """Native server: server-side time per RPC (request read -> response queued)."""
+        p = self.mgr.plugins["gpu"]
+        p.sync()
+        if p.native is None:
+            return {}
+        out = {rpc: list(q) for rpc, q in p.native.recent_ms.items()}
+        if reset:
+            p.native.recent_ms.clear()
+        return out
 
     def available(self):
         return self.kubelet.healthy_free("amd.com/gpu")
@@ -299,7 +318,9 @@ def main():
         hcfg = (HealthConfig(exporter_socket=None, liveness=True, smi_ecc=True, smi_events=True, smi_xgmi=True)
                 if hp > 0 else HealthConfig(exporter_socket=None))
         loop = asyncio.new_event_loop()
-        plug = PluginUnderTest(loop, tmp, "device-plugins", sysfs, adv, full, ords, hcfg, hp)
+        kclient = args.kubelet_client or ("native" if args.grpc_server == "native" else "aio")
+        plug = PluginUnderTest(loop, tmp, "device-plugins", sysfs, adv, full, ords, hcfg, hp,
+                               grpc_server=args.grpc_server, kubelet_client=kclient)
         impl, inv = plug.impl, plug.inv
         if m_adv > n:
             plug.hold(fragment([dv.id for dv in adv], n, args.hold))
@@ -401,12 +422,15 @@ def main():
 
     for _ in range(args.warmup):
         one_step(False)
+    if d.rank == 0:
+        plug.server_ms(reset=True)
     d.sync()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         one_step(True)
     d.sync()
     elapsed = time.perf_counter() - t_start
+    server_ms = plug.server_ms() if d.rank == 0 else {}
     elapsed = d.max(elapsed)
     hip_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
     other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
@@ -446,7 +470,8 @@ def main():
         fplug = None
         if d.rank == 0:
             fplug = PluginUnderTest(loop, tmp, "device-plugins-all", sysfs, usable, full, ords,
-                                    HealthConfig(exporter_socket=None), 0.0)
+                                    HealthConfig(exporter_socket=None), 0.0, grpc_server=args.grpc_server,
+                                    kubelet_client=kclient)
             fplug.hold(fragment([dv.id for dv in usable], n, args.hold))
         for _ in range(args.fragmented_compare):
             one_step(False, sink=frag_lat, pl=fplug, alloc_sink=frag_alloc)
@@ -500,6 +525,11 @@ def main():
                              "reference_candidates": refk["candidates"], "ours_candidates": mine["candidates"],
                              "same_set": sorted(mine["ids"]) == sorted(refk["ids"])}
         extra = {"plugin_rpc_p50_ms": round(pct(rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rpc_ms, .99), 4),
+                 "grpc_server": args.grpc_server, "kubelet_client": kclient,
+                 # breakdown of plugin_rpc (kubelet's GetPreferredAllocation + Allocate round trips): the
+                 # plugin's own time per RPC, measured inside the native server (empty with -grpc_server aio)
+                 "plugin_server_p50_us": {rpc: round(pct(v, .5) * 1e3, 1) for rpc, v in sorted(server_ms.items())
+                                          if rpc in ("GetPreferredAllocation", "Allocate")},
                  "allocate_rpc_p50_ms": round(pct(alloc_rpc_ms, .5), 4),
                  "container_start_to_ready_p50_ms": round(pct(ready_ms, .5), 3),
                  "latency_p99_ms": round(pct(lat_ms, .99), 3), "latency_mean_ms": round(statistics.mean(lat_ms), 3),

@@ -14,6 +14,8 @@
 namespace py = pybind11;
 using namespace mi355x;
 
+void bind_rpc(py::module_& m);  // rpc_module.cpp
+
 namespace {
 
 py::dict link_to_dict(const KfdLink& l) {
@@ -196,7 +198,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("cross_hive_penalty", &AllocatorOptions::cross_hive_penalty)
       .def_readwrite("degraded_links", &AllocatorOptions::degraded_links);
 
-  py::class_<HiveAllocator>(m, "HiveAllocator")
+  // shared: the native gRPC server keeps using an allocator snapshot while
+  // Python initialises its replacement
+  py::class_<HiveAllocator, std::shared_ptr<HiveAllocator>>(m, "HiveAllocator")
       .def(py::init<>())
       .def("init", &HiveAllocator::init, py::arg("devices"), py::arg("topology"),
            py::arg("options") = AllocatorOptions())
@@ -395,4 +399,5 @@ PYBIND11_MODULE(_native, m) {
     out["gpus"] = gpus;
     return out;
   });
+  bind_rpc(m);
 }

@@ -1,0 +1,114 @@
+// v1beta1.DevicePlugin on the native gRPC server.
+//
+// The kubelet's admission RPCs are answered without entering Python:
+//   GetPreferredAllocation  protobuf decode -> HiveAllocator -> encode
+//   Allocate                per-device response fragments prepared by the
+//                           plugin (DeviceSpecs, CDI devices, annotation names)
+//   GetDevicePluginOptions  bytes prepared by the plugin
+//   ListAndWatch            first message = the current list (prepared bytes),
+//                           later lists pushed by the plugin on health changes
+//   PreStartContainer       empty response
+// Whatever has no prepared state (allocator disabled, Allocate mounts that
+// are created per request, tracing) goes to a fallback: the Python servicer.
+// Every call leaves an event (timing, allocator outcome, allocated IDs) in a
+// queue signalled through an eventfd, so logs and metrics stay in Python, off
+// the RPC path.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "mi355x/allocator.h"
+#include "mi355x/grpc_server.h"
+
+namespace mi355x::rpc {
+
+// Allocate fast path: every ContainerAllocateResponse is
+//   container_prefix + per_device[id] for each requested id (request order)
+//   + (annotation_key set) annotations{annotation_key: join(annotation_names[id], ",")}
+// as raw protobuf field bytes; an unknown ID is an INVALID_ARGUMENT error.
+struct AllocateTemplate {
+  std::string resource;  // for error messages
+  std::string container_prefix;
+  std::unordered_map<std::string, std::string> per_device;
+  std::string annotation_key;
+  std::unordered_map<std::string, std::string> annotation_names;
+};
+
+struct RpcEvent {
+  std::string rpc;
+  int status = 0;
+  std::string message;
+  uint64_t t0_ns = 0;   // CLOCK_MONOTONIC
+  uint64_t dur_ns = 0;
+  bool native = true;   // false: served by the fallback
+  // GetPreferredAllocation (last container request) / Allocate
+  int candidates = -1;
+  bool short_circuit = false;
+  int weight = -1;
+  double alloc_us = 0;
+  uint64_t alloc_t0_ns = 0;
+  std::vector<std::string> ids;  // chosen (preferred) / allocated IDs, all containers
+};
+
+class DevicePluginService {
+ public:
+  using Fallback = std::function<Reply(const std::string& method, const std::string& request)>;
+
+  DevicePluginService();
+  ~DevicePluginService();
+
+  // Routes /v1beta1.DevicePlugin/* on `srv` (before srv.start()).
+  void attach(GrpcServer& srv);
+
+  // The fallback is fixed before the server starts.
+  void set_fallback(Fallback f);
+  void set_options(std::optional<std::string> bytes);
+  void set_allocator(std::shared_ptr<const HiveAllocator> a);
+  void set_allocate_template(std::optional<AllocateTemplate> t);
+  void set_device_list(std::optional<std::string> bytes);
+  // route everything to the fallback (e.g. while tracing)
+  void set_native_enabled(bool on);
+
+  std::vector<RpcEvent> drain_events();
+  int event_fd() const { return evfd_; }
+  static const char* path(const char* method);
+
+ private:
+  Reply preferred(const std::string& req, RpcEvent* ev);
+  Reply allocate(const std::string& req, RpcEvent* ev);
+  Reply fallback(const char* method, const std::string& req, RpcEvent* ev);
+  void record(RpcEvent ev);
+
+  mutable std::mutex mu_;
+  std::shared_ptr<const Fallback> fallback_;
+  std::shared_ptr<const std::string> options_;
+  std::shared_ptr<const HiveAllocator> alloc_;
+  std::shared_ptr<const AllocateTemplate> tmpl_;
+  std::shared_ptr<const std::string> list_;
+  bool native_ = true;
+
+  std::mutex ev_mu_;
+  std::vector<RpcEvent> events_;
+  int evfd_ = -1;
+};
+
+// ---- minimal protobuf wire format (device-plugin messages) ----------------
+namespace pb {
+void put_varint(std::string* out, uint64_t v);
+void put_tag(std::string* out, int field, int wire);
+void put_bytes(std::string* out, int field, const std::string& v);
+void put_bool(std::string* out, int field, bool v);
+// Parses a message's length-delimited / varint fields in order: calls
+// on_bytes(field, data, len) and on_varint(field, value). false = malformed.
+bool scan(const char* p, size_t n, const std::function<bool(int, const char*, size_t)>& on_bytes,
+          const std::function<bool(int, uint64_t)>& on_varint);
+}  // namespace pb
+
+}  // namespace mi355x::rpc

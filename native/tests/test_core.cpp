@@ -13,8 +13,15 @@
 #include <thread>
 #include <vector>
 
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include "../src/rpc/hpack.h"
 #include "mi355x/allocator.h"
+#include "mi355x/dp_service.h"
 #include "mi355x/gpu_discovery.h"
+#include "mi355x/grpc_server.h"
 #include "mi355x/kfd_topology.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
@@ -169,6 +176,212 @@ static void test_degraded_links(const std::string& ref) {
   }
 }
 
+static std::string unhex(const char* h) {
+  std::string o;
+  for (size_t i = 0; h[i] && h[i + 1]; i += 2) o.push_back(static_cast<char>(std::stoi(std::string(h + i, 2), nullptr, 16)));
+  return o;
+}
+
+static void test_hpack() {
+  using namespace mi355x::rpc;
+  CHECK(huffman_kraft_sum() == (1ull << 30));  // complete prefix code
+  const char* vec[][2] = {{"www.example.com", "f1e3c2e5f23a6ba0ab90f4ff"},
+                          {"no-cache", "a8eb10649cbf"},
+                          {"custom-key", "25a849e95ba97d7f"},
+                          {"custom-value", "25a849e95bb8e8b4bf"},
+                          {"Mon, 21 Oct 2013 20:13:21 GMT", "d07abe941054d444a8200595040b8166e082a62d1bff"}};
+  for (auto& v : vec) {
+    std::string enc, dec;
+    huffman_encode(v[0], &enc);
+    CHECK(enc == unhex(v[1]));
+    const std::string raw = unhex(v[1]);
+    CHECK(huffman_decode(reinterpret_cast<const uint8_t*>(raw.data()), raw.size(), &dec) && dec == v[0]);
+  }
+  std::string junk;
+  const uint8_t eos_pad[] = {0xff, 0xff, 0xff, 0xff};  // EOS in the string: invalid
+  CHECK(!huffman_decode(eos_pad, sizeof(eos_pad), &junk));
+  // RFC 7541 C.4: three requests sharing one dynamic table
+  HpackDecoder dec;
+  HeaderList hl;
+  const std::string r1 = unhex("828684418cf1e3c2e5f23a6ba0ab90f4ff");
+  CHECK(dec.decode(reinterpret_cast<const uint8_t*>(r1.data()), r1.size(), &hl));
+  CHECK(hl.size() == 4 && hl[3].first == ":authority" && hl[3].second == "www.example.com");
+  CHECK(dec.table_bytes() == 57);
+  hl.clear();
+  const std::string r2 = unhex("828684be5886a8eb10649cbf");
+  CHECK(dec.decode(reinterpret_cast<const uint8_t*>(r2.data()), r2.size(), &hl));
+  CHECK(hl.size() == 5 && hl[3].second == "www.example.com" && hl[4].first == "cache-control" &&
+        hl[4].second == "no-cache");
+  CHECK(dec.table_bytes() == 110);
+  hl.clear();
+  const std::string r3 = unhex("828785bf408825a849e95ba97d7f8925a849e95bb8e8b4bf");
+  CHECK(dec.decode(reinterpret_cast<const uint8_t*>(r3.data()), r3.size(), &hl));
+  CHECK(hl.size() == 5 && hl[2].second == "/index.html" && hl[4].first == "custom-key" &&
+        hl[4].second == "custom-value");
+  CHECK(dec.table_bytes() == 164);
+  hl.clear();
+  const std::string bad = unhex("8286bf");  // index 63 does not exist in a fresh table
+  HpackDecoder fresh;
+  CHECK(!fresh.decode(reinterpret_cast<const uint8_t*>(bad.data()), bad.size(), &hl));
+}
+
+// ---- raw HTTP/2 client for the native gRPC server --------------------------
+namespace h2t {
+std::string frame(uint8_t type, uint8_t flags, uint32_t sid, const std::string& p) {
+  std::string f;
+  f.push_back(static_cast<char>(p.size() >> 16));
+  f.push_back(static_cast<char>(p.size() >> 8));
+  f.push_back(static_cast<char>(p.size()));
+  f.push_back(static_cast<char>(type));
+  f.push_back(static_cast<char>(flags));
+  for (int i = 3; i >= 0; --i) f.push_back(static_cast<char>(sid >> (8 * i)));
+  return f + p;
+}
+std::string request(uint32_t sid, const std::string& path, const std::string& msg) {
+  std::string h;
+  mi355x::rpc::hpack_put_indexed(&h, 3);  // :method POST
+  mi355x::rpc::hpack_put_indexed(&h, 6);  // :scheme http
+  mi355x::rpc::hpack_put_literal(&h, 4, path);
+  mi355x::rpc::hpack_put_literal(&h, 31, "application/grpc");
+  mi355x::rpc::hpack_put_literal(&h, "te", "trailers");
+  std::string body;
+  body.push_back(0);
+  for (int i = 3; i >= 0; --i) body.push_back(static_cast<char>(msg.size() >> (8 * i)));
+  body += msg;
+  return frame(1, 4, sid, h) + frame(0, 1, sid, body);
+}
+struct Result {
+  int grpc_status = -1;
+  std::vector<std::string> messages;
+};
+// reads frames until END_STREAM on `sid`
+bool read_call(int fd, uint32_t sid, Result* r, mi355x::rpc::HpackDecoder* dec, size_t max_messages = 100) {
+  std::string buf, data;
+  char tmp[4096];
+  while (true) {
+    while (buf.size() >= 9) {
+      const auto* h = reinterpret_cast<const uint8_t*>(buf.data());
+      const size_t len = (size_t(h[0]) << 16) | (size_t(h[1]) << 8) | h[2];
+      if (buf.size() < 9 + len) break;
+      const uint8_t type = h[3], flags = h[4];
+      const uint32_t s = ((h[5] & 0x7f) << 24) | (h[6] << 16) | (h[7] << 8) | h[8];
+      std::string p = buf.substr(9, len);
+      buf.erase(0, 9 + len);
+      if (s != sid) continue;
+      if (type == 3) {  // RST_STREAM
+        r->grpc_status = -2;
+        return true;
+      }
+      if (type == 1) {
+        mi355x::rpc::HeaderList hl;
+        if (!dec->decode(reinterpret_cast<const uint8_t*>(p.data()), p.size(), &hl)) return false;
+        for (auto& [k, v] : hl)
+          if (k == "grpc-status") r->grpc_status = std::atoi(v.c_str());
+      } else if (type == 0) {
+        data += p;
+        while (data.size() >= 5) {
+          const size_t n = (size_t(uint8_t(data[1])) << 24) | (size_t(uint8_t(data[2])) << 16) |
+                           (size_t(uint8_t(data[3])) << 8) | uint8_t(data[4]);
+          if (data.size() < 5 + n) break;
+          r->messages.push_back(data.substr(5, n));
+          data.erase(0, 5 + n);
+          if (r->messages.size() >= max_messages) return true;
+        }
+      }
+      if (flags & 1) return true;
+    }
+    const ssize_t n = ::read(fd, tmp, sizeof(tmp));
+    if (n <= 0) return false;
+    buf.append(tmp, static_cast<size_t>(n));
+  }
+}
+int connect_unix(const std::string& path) {
+  const int fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
+  sockaddr_un a{};
+  a.sun_family = AF_UNIX;
+  std::snprintf(a.sun_path, sizeof(a.sun_path), "%s", path.c_str());
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  std::string pre = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n" + frame(4, 0, 0, "");
+  if (::write(fd, pre.data(), pre.size()) != static_cast<ssize_t>(pre.size())) return -1;
+  return fd;
+}
+}  // namespace h2t
+
+static void test_grpc_server() {
+  using namespace mi355x::rpc;
+  char tmpl[] = "/tmp/mi355x-rpc-XXXXXX";
+  const char* dir = ::mkdtemp(tmpl);
+  if (!dir) {
+    ++g_skip;
+    return;
+  }
+  const std::string sock = std::string(dir) + "/dp.sock";
+  GrpcServer srv;
+  DevicePluginService svc;
+  svc.attach(srv);
+  svc.set_options(std::string("\x10\x01", 2));  // get_preferred_allocation_available
+  AllocateTemplate t;
+  t.resource = "gpu";
+  t.per_device["a"] = "A";
+  svc.set_allocate_template(t);
+  svc.set_device_list(std::string("L0"));
+  CHECK(srv.start(sock).empty());
+  const int fd = h2t::connect_unix(sock);
+  CHECK(fd >= 0);
+  if (fd < 0) return;
+  HpackDecoder dec;
+  auto call = [&](uint32_t sid, const char* method, const std::string& msg, h2t::Result* r) {
+    const std::string req = h2t::request(sid, std::string("/v1beta1.DevicePlugin/") + method, msg);
+    return ::write(fd, req.data(), req.size()) == static_cast<ssize_t>(req.size()) && h2t::read_call(fd, sid, r, &dec);
+  };
+  h2t::Result r1;
+  CHECK(call(1, "GetDevicePluginOptions", "", &r1) && r1.grpc_status == 0 && r1.messages.size() == 1 &&
+        r1.messages[0] == std::string("\x10\x01", 2));
+  std::string areq;  // AllocateRequest{container_requests{devices_ids: "a"}}
+  {
+    std::string c;
+    pb::put_bytes(&c, 1, "a");
+    pb::put_bytes(&areq, 1, c);
+  }
+  h2t::Result r2;
+  CHECK(call(3, "Allocate", areq, &r2) && r2.grpc_status == 0 && r2.messages.size() == 1);
+  if (r2.messages.size() == 1) CHECK(r2.messages[0] == std::string("\x0a\x01" "A", 3));
+  std::string bad;
+  {
+    std::string c;
+    pb::put_bytes(&c, 1, "zz");
+    pb::put_bytes(&bad, 1, c);
+  }
+  h2t::Result r3;
+  CHECK(call(5, "Allocate", bad, &r3) && r3.grpc_status == kInvalidArgument);
+  h2t::Result r4;
+  CHECK(call(7, "Nope", "", &r4) && r4.grpc_status == kUnimplemented);
+  // ListAndWatch: the list, then broadcasts from another thread
+  const std::string lw = h2t::request(9, DevicePluginService::path("ListAndWatch"), "");
+  CHECK(::write(fd, lw.data(), lw.size()) == static_cast<ssize_t>(lw.size()));
+  h2t::Result r5;
+  CHECK(h2t::read_call(fd, 9, &r5, &dec, 1) && r5.messages.size() == 1 && r5.messages[0] == "L0");
+  std::thread pusher([&] {
+    for (int i = 1; i <= 20; ++i) {
+      while (srv.broadcast(DevicePluginService::path("ListAndWatch"), "L" + std::to_string(i)) == 0)
+        std::this_thread::yield();
+    }
+  });
+  h2t::Result r6;
+  CHECK(h2t::read_call(fd, 9, &r6, &dec, 20) && r6.messages.size() == 20 && r6.messages.back() == "L20");
+  pusher.join();
+  srv.stop(0.5);  // the open stream ends with OK trailers
+  h2t::Result r7;
+  CHECK(h2t::read_call(fd, 9, &r7, &dec) && r7.grpc_status == 0);
+  CHECK(svc.drain_events().size() == 4);  // options, 2x Allocate, ListAndWatch (unknown methods are not service calls)
+  ::close(fd);
+  ::unlink(sock.c_str());
+  ::rmdir(dir);
+}
+
 int main(int argc, char** argv) {
   std::string repo = argc > 1 ? argv[1] : "testdata";
   std::string ref = argc > 2 ? argv[2] : "/root/reference/testdata";
@@ -177,6 +390,8 @@ int main(int argc, char** argv) {
   test_allocator_reference_contract(ref);
   test_errors();
   test_degraded_links(ref);
+  test_hpack();
+  test_grpc_server();
   std::printf("test_core: %d passed, %d failed, %d skipped\n", g_pass, g_fail, g_skip);
   return g_fail ? 1 : 0;
 }

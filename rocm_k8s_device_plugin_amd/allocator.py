@@ -76,9 +76,13 @@ class BestEffortPolicy(Policy):
         direct xGMI link is down (health/fabric.py); they score as the worst
         link until the next init without them."""
         self._opts.degraded_links = sorted(tuple(sorted(p)) for p in degraded_links)
-        err = self._alloc.init(self.to_alloc_devices(devices), topology, self._opts)
+        # a fresh native allocator per init: the native gRPC server may still be
+        # answering with the previous one (it holds a shared snapshot)
+        alloc = core().HiveAllocator()
+        err = alloc.init(self.to_alloc_devices(devices), topology, self._opts)
         if err:
             raise AllocationError(err)
+        self._alloc = alloc
 
     @property
     def native(self):

@@ -70,6 +70,8 @@ def build_parser() -> flags.GoFlagParser:
                                   "stops counting as xGMI-connected in preferred allocation (devices stay Healthy)")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
+    p.add_str("grpc_server", "native", "kubelet-facing gRPC server: native (C++ HTTP/2; admission RPCs answered "
+                                       "without Python) or aio (Python grpc.aio)")
     p.add_bool("dry_run", False, "print what this node would advertise (implementation, resources, devices, "
                                  "health after one sweep, preferred allocations per size) as JSON and exit")
     p.add_float("topology_watch", 5.0, "seconds between checks for a GPU topology change (kfd generation, "
@@ -112,6 +114,8 @@ def validate(ns) -> Optional[str]:
         return str(e)
     if ns.liveness_mode not in ("persistent", "spawn"):
         return f"invalid liveness_mode provided: {ns.liveness_mode}, supported values are persistent or spawn"
+    if ns.grpc_server not in ("native", "aio"):
+        return f"invalid grpc_server provided: {ns.grpc_server}, supported values are native or aio"
     return None
 
 
@@ -236,7 +240,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         print(json.dumps(asyncio.run(dry_run_report(impl, sweep=ns.pulse > 0)), indent=1))
         return 0
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
-                       metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch)
+                       metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch, grpc_server=ns.grpc_server)
     from ..utils.trace import TRACER
     TRACER.configure(ns.trace_file or None)
     try:

@@ -299,6 +299,35 @@ class ContainerImpl(DeviceImpl):
                     _log.warning("node view unavailable: %s", e)
         return resp
 
+    def allocate_template(self, ctx: PluginContext) -> Optional[dict]:
+        """Allocate response fragments per device for the native server's fast
+        path (plugin/native_server.py); parsed, its responses equal allocate()'s.
+        None when a response needs per-request work (topology / node views)."""
+        if self.topology_views is not None or self.node_view is not None:
+            return None
+        specs = cdi.DEVICE_SPECS in self.list_strategies
+        prefix = pb.ContainerAllocateResponse()
+        if specs:
+            prefix.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
+        per_device, names = {}, {}
+        annotate = self._cdi and cdi.CDI_ANNOTATIONS in self.list_strategies
+        try:
+            for d in self.inv.devices:
+                car = pb.ContainerAllocateResponse()
+                if specs:
+                    for p in d.dev_paths():
+                        car.devices.add(container_path=p, host_path=p, permissions="rw")
+                if self._cdi and cdi.CDI_CRI in self.list_strategies:
+                    car.cdi_devices.add(name=cdi.qualified_name(ctx.resource, d.id))
+                if annotate:
+                    names[d.id] = cdi.qualified_name(ctx.resource, d.id)
+                per_device[d.id] = car.SerializeToString()
+        except ValueError:   # a device ID CDI cannot name: allocate() reports it per request
+            return None
+        return {"resource": ctx.resource, "container_prefix": prefix.SerializeToString(), "per_device": per_device,
+                "annotation_key": cdi.annotation_key(ctx.resource) if annotate else "",
+                "annotation_names": names}
+
     def preferred_allocation(self, ctx: PluginContext,
                              req: pb.PreferredAllocationRequest) -> pb.PreferredAllocationResponse:
         resp = pb.PreferredAllocationResponse()

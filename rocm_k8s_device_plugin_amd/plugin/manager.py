@@ -39,6 +39,7 @@ from ..utils import log
 from ..utils.broadcast import Broadcast
 from ..utils.metrics import REGISTRY, serve_metrics
 from .base import DeviceImpl, PluginContext, new_context
+from .native_server import NativePluginServer
 from .servicer import DevicePluginServicer
 
 _log = log.get("manager")
@@ -58,6 +59,9 @@ class ManagerConfig:
     metrics_port: int = 0
     handle_signals: bool = True
     topology_watch_s: float = 5.0   # re-discovery check period (partition switches); 0 = off
+    # kubelet-facing gRPC server: "native" (C++ HTTP/2, plugin/native_server.py)
+    # or "aio" (Python grpc.aio, plugin/servicer.py)
+    grpc_server: str = "native"
 
 
 class ResourcePlugin:
@@ -71,6 +75,7 @@ class ResourcePlugin:
         self.stop_bc = Broadcast()
         self.servicer: Optional[DevicePluginServicer] = None
         self.server: Optional[grpc.aio.Server] = None
+        self.native: Optional[NativePluginServer] = None
         self.running = False
         self.started = False
         self.registrations = 0
@@ -83,7 +88,14 @@ class ResourcePlugin:
         except Exception as e:  # reference: log and do not start the server
             _log.error('Failed to start plugin "%s": %s', self.name, e)
             self.started = False
+        if self.native is not None and self.started:
+            self.native.refresh()   # new allocator / devices for the native server
         return self.started
+
+    def sync(self) -> None:
+        """Apply the native server's pending call events (stats, logs, metrics) now."""
+        if self.native is not None:
+            self.native.drain()
 
     def _cleanup(self) -> None:
         try:
@@ -95,6 +107,12 @@ class ResourcePlugin:
         self._cleanup()
         os.makedirs(os.path.dirname(self.socket), exist_ok=True)
         self.stop_bc = Broadcast()
+        if self.mgr.cfg.grpc_server == "native":
+            native = NativePluginServer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
+                                        self.mgr.cfg.send_every_pulse)
+            await native.start(self.socket)
+            self.native = native
+            return
         self.servicer = DevicePluginServicer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
                                              self.mgr.cfg.send_every_pulse)
         server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
@@ -141,6 +159,9 @@ class ResourcePlugin:
 
     async def _stop_locked(self) -> None:
         self.stop_bc.close()
+        if self.native is not None:
+            await self.native.stop(grace=0.5)
+            self.native = None
         if self.server is not None:
             await self.server.stop(grace=0.5)
             self.server = None
@@ -153,9 +174,13 @@ class ResourcePlugin:
 
 
 class PluginManager:
+    GRPC_SERVERS = ("native", "aio")
+
     def __init__(self, impl: Optional[DeviceImpl], cfg: Optional[ManagerConfig] = None):
         self.impl = impl
         self.cfg = cfg or ManagerConfig()
+        if self.cfg.grpc_server not in self.GRPC_SERVERS:
+            raise ValueError(f"grpc server must be one of {self.GRPC_SERVERS}, got {self.cfg.grpc_server!r}")
         self.kubelet_socket = self.cfg.kubelet_socket or os.path.join(self.cfg.plugin_dir, "kubelet.sock")
         self.plugins: Dict[str, ResourcePlugin] = {}
         self.pulse = Broadcast()

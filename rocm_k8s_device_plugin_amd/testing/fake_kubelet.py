@@ -38,6 +38,7 @@ class ResourceState:
     task: Optional[asyncio.Task] = None
     event: asyncio.Event = field(default_factory=asyncio.Event)
     stream_error: Optional[str] = None
+    native: object = None   # core().GrpcClient when rpc_client == "native"
 
 
 @dataclass
@@ -51,8 +52,33 @@ class Admission:
     preferred_used: bool
 
 
+class NativeRpcError(grpc.RpcError):
+    """An error status from the native client (same role as AioRpcError)."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"status {status}: {message}")
+        self.status, self.message = status, message
+
+    def code(self):
+        return next((c for c in grpc.StatusCode if c.value[0] == self.status), grpc.StatusCode.UNAVAILABLE)
+
+    def details(self):
+        return self.message
+
+
 class FakeKubelet:
-    def __init__(self, plugin_dir: str):
+    RPC_CLIENTS = ("aio", "native")
+
+    def __init__(self, plugin_dir: str, rpc_client: str = "aio"):
+        """`rpc_client`: how admit() calls GetPreferredAllocation / Allocate.
+        "aio": grpc.aio on this event loop (works with any plugin server);
+        "native": the native blocking HTTP/2 client (core().GrpcClient) -- a
+        kubelet-like native caller, for timing the plugin rather than the
+        interpreter. It blocks the loop for the call, so the plugin must not be
+        served from this same loop (use it with the native server only)."""
+        if rpc_client not in self.RPC_CLIENTS:
+            raise ValueError(f"rpc_client must be one of {self.RPC_CLIENTS}")
+        self.rpc_client = rpc_client
         self.plugin_dir = plugin_dir
         self.socket = os.path.join(plugin_dir, "kubelet.sock")
         self.server: Optional[grpc.aio.Server] = None
@@ -96,6 +122,9 @@ class FakeKubelet:
             st.event.set()
 
     async def _drop(self, st: ResourceState) -> None:
+        if st.native is not None:
+            st.native.close()
+            st.native = None
         if st.task is not None:
             st.task.cancel()
             await asyncio.gather(st.task, return_exceptions=True)
@@ -192,10 +221,10 @@ class FakeKubelet:
             req.container_requests.add(available_deviceIDs=avail, must_include_deviceIDs=list(must_include),
                                        allocation_size=count)
             try:
-                resp = await st.stub.GetPreferredAllocation(req, timeout=10)
+                resp = await self._call(st, "GetPreferredAllocation", req, pb.PreferredAllocationResponse)
                 chosen = list(resp.container_responses[0].deviceIDs)
                 used = True
-            except grpc.aio.AioRpcError:
+            except grpc.RpcError:
                 chosen = list(must_include)
             pref_ms = (time.perf_counter() - t0) * 1e3
         if len(chosen) != count:  # kubelet's own fallback: fill in order
@@ -207,10 +236,28 @@ class FakeKubelet:
         t1 = time.perf_counter()
         areq = pb.AllocateRequest()
         areq.container_requests.add(devices_ids=chosen)
-        aresp = await st.stub.Allocate(areq, timeout=10)
+        aresp = await self._call(st, "Allocate", areq, pb.AllocateResponse)
         t2 = time.perf_counter()
         st.allocated.update(chosen)
         return Admission(resource, chosen, aresp, pref_ms, (t2 - t1) * 1e3, (t2 - t0) * 1e3, used)
+
+    async def _call(self, st: ResourceState, method: str, req, resp_type):
+        if self.rpc_client == "aio":
+            return await getattr(st.stub, method)(req, timeout=10)
+        if st.native is None:
+            from ..ops.native import core
+            st.native = core().GrpcClient()
+            err = st.native.connect(os.path.join(self.plugin_dir, st.endpoint))
+            if err:
+                st.native = None
+                raise NativeRpcError(-1, err)
+        status, msg, body = st.native.unary(f"/{pb.PACKAGE}.DevicePlugin/{method}", req.SerializeToString(), 10.0)
+        if status != 0:
+            if status < 0:
+                st.native.close()
+                st.native = None
+            raise NativeRpcError(status, msg)
+        return resp_type.FromString(body)
 
     def release(self, resource: str, ids: Sequence[str]) -> None:
         self.resources[resource].allocated.difference_update(ids)

@@ -43,6 +43,16 @@ class Tracer:
             with self._lock:
                 self._events.append(ev)
 
+    def complete(self, name: str, cat: str, t0_ns: int, dur_ns: int, **args: Any) -> None:
+        """A span recorded elsewhere (the native gRPC server): CLOCK_MONOTONIC ns,
+        the same clock as perf_counter_ns on Linux."""
+        if not self.enabled:
+            return
+        ev = {"name": name, "cat": cat, "ph": "X", "ts": t0_ns / 1e3, "dur": dur_ns / 1e3, "pid": self._pid,
+              "tid": 0, "args": {k: str(v) for k, v in args.items()}}
+        with self._lock:
+            self._events.append(ev)
+
     def instant(self, name: str, cat: str = "plugin", **args: Any) -> None:
         if not self.enabled:
             return
