@@ -220,8 +220,11 @@ async def dry_run_report(impl: Optional[DeviceImpl], sweep: bool) -> dict:
 def main(argv: Optional[List[str]] = None) -> int:
     p = build_parser()
     ns = p.parse_args(argv)
-    logger = log.setup(ns.v, json_format=ns.log_format == "json", stderr_threshold=ns.stderrthreshold,
-                       logtostderr=ns.logtostderr)
+    try:
+        logger = log.setup_from_flags(ns, program="k8s-device-plugin")
+    except ValueError as e:
+        print(f"invalid logging flags: {e}", file=sys.stderr)
+        return 1
     err = validate(ns)
     if err:
         logger.error("%s", err)

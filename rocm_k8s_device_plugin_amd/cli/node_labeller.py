@@ -33,6 +33,8 @@ def build_parser() -> flags.GoFlagParser:
     flags.add_glog_flags(p)
     p.add_str("node_name", os.environ.get("DS_NODE_NAME", ""), "node to label (default $DS_NODE_NAME)")
     p.add_float("resync", 300.0, "seconds between label re-asserts (0 = apply once and exit)")
+    p.add_bool("watch", True, "watch the node and re-apply labels as soon as they are stripped or the node is "
+                              "re-created (needs the 'watch' verb on nodes, as in the upstream ClusterRole)")
     p.add_bool("dry_run", False, "print the generated labels as JSON and exit")
     p.add_str("sysfs_root", "/sys", "sysfs mount to read")
     p.add_str("dev_root", "/dev", "device node directory")
@@ -62,7 +64,11 @@ def enabled_labels(ns) -> dict:
 
 def main(argv: Optional[List[str]] = None) -> int:
     ns = build_parser().parse_args(argv)
-    logger = log.setup(ns.v, json_format=ns.log_format == "json")
+    try:
+        logger = log.setup_from_flags(ns, program="k8s-node-labeller")
+    except ValueError as e:
+        print(f"invalid logging flags: {e}", file=sys.stderr)
+        return 1
     if ns.driver_type not in ("",) + C.DRIVER_TYPES:
         logger.error("invalid driver_type %s", ns.driver_type)
         return 1
@@ -83,7 +89,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     except Exception as e:
         logger.error("unable to set up kubernetes client: %s", e)
         return 1
-    lab = NodeLabeller(client, node, gen, resync_s=ns.resync)
+    lab = NodeLabeller(client, node, gen, resync_s=ns.resync, watch=ns.watch)
     for s in (signal.SIGTERM, signal.SIGINT):
         signal.signal(s, lambda *_: lab.stop())
     lab.run(once=ns.resync <= 0)

@@ -2,16 +2,21 @@
 
 Reference: reconcileNodeLabels (cmd/k8s-node-labeller/controller.go:23-58)
 driven by a Create-only predicate on the node named ``$DS_NODE_NAME``
-(main.go:551-577) — labels are computed once at startup and applied once.
+(main.go:551-577) — labels are computed once at startup and applied once
+(and again when the Node object is re-created).
 
-Here the desired labels are recomputed on every pass (hardware state such as
-partition mode can change under a running DaemonSet) and re-asserted every
-``resync_s`` seconds, so labels removed or edited by someone else come back
-(SURVEY Appendix B #11). Each pass: GET node -> diff against
-(labels - known AMD keys) + desired -> merge PATCH only if something changed.
+Here the node is watched (``watch=1`` with a fieldSelector on its name,
+reconnected with backoff, re-listed after 410 Gone): any event whose labels
+differ from the desired ones — the node re-created, a label stripped or edited
+by someone else — triggers a reconcile at once. The
+desired labels are also recomputed and re-asserted every ``resync_s`` seconds
+(hardware state such as partition mode can change under a running
+DaemonSet). Each pass: GET node -> diff against (labels - known AMD keys) +
+desired -> merge PATCH only if something changed.
 """
 from __future__ import annotations
 
+import http.client
 import threading
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Optional
@@ -45,24 +50,38 @@ class ReconcileStats:
     errors: int = 0
     last_error: str = ""
     last_patch: Dict[str, Optional[str]] = field(default_factory=dict)
+    watch_events: int = 0
+    watch_kicks: int = 0      # events that triggered a reconcile
+    watch_errors: int = 0
+    watch_restarts: int = 0
 
 
 class NodeLabeller:
     def __init__(self, client: KubeClient, node_name: str, generate: Callable[[], Dict[str, str]],
-                 resync_s: float = 300.0, retry_s: float = 5.0):
+                 resync_s: float = 300.0, retry_s: float = 5.0, watch: bool = True, watch_timeout_s: int = 300,
+                 watch_backoff_max_s: float = 30.0):
         self.client = client
         self.node = node_name
         self.generate = generate
         self.resync_s = resync_s
         self.retry_s = retry_s
+        self.watch = watch
+        self.watch_timeout_s = watch_timeout_s
+        self.watch_backoff_max_s = watch_backoff_max_s
         self.stats = ReconcileStats()
         self._stop = threading.Event()
+        self._kick = threading.Event()
+        self._desired: Optional[Dict[str, str]] = None
+        self._rv = ""
+        self._stream = None
+        self._watch_thread: Optional[threading.Thread] = None
 
     def reconcile_once(self) -> bool:
         """Returns True on success (whether or not a patch was needed)."""
         self.stats.passes += 1
         try:
             desired = self.generate()
+            self._desired = desired
             node = self.client.get_node(self.node)
             current = (node.get("metadata") or {}).get("labels") or {}
             patch = label_patch(current, desired)
@@ -100,17 +119,71 @@ class NodeLabeller:
                 if e.status != 409 or i == attempts - 1:
                     raise
 
+    # ------------------------------------------------------------ watch
+    def _needs_reconcile(self, node: dict) -> bool:
+        if self._desired is None:
+            return True
+        labels = (node.get("metadata") or {}).get("labels") or {}
+        return bool(label_patch(labels, self._desired))
+
+    def _watch_loop(self) -> None:
+        backoff = 0.2
+        while not self._stop.is_set():
+            try:
+                stream = self.client.watch_node(self.node, self._rv, timeout_s=self.watch_timeout_s)
+                self._stream = stream
+                if self._stop.is_set():
+                    stream.close()
+                    return
+                self.stats.watch_restarts += 1
+                backoff = 0.2
+                for ev in stream:
+                    self.stats.watch_events += 1
+                    typ, obj = ev.get("type"), ev.get("object") or {}
+                    if typ == "ERROR":
+                        if obj.get("code") == 410:      # resourceVersion too old: re-list
+                            self._rv = ""
+                            self._kick.set()
+                        break
+                    rv = (obj.get("metadata") or {}).get("resourceVersion")
+                    if rv:
+                        self._rv = rv
+                    if typ in ("ADDED", "MODIFIED") and self._needs_reconcile(obj):
+                        self.stats.watch_kicks += 1
+                        self._kick.set()
+            except (KubeError, OSError, ValueError, http.client.HTTPException) as e:
+                if self._stop.is_set():
+                    return
+                if isinstance(e, KubeError) and e.status == 410:
+                    self._rv = ""
+                self.stats.watch_errors += 1
+                _log.warning("watch of node %s failed (%s); retrying in %.1fs", self.node, e, backoff)
+                self._stop.wait(backoff)
+                backoff = min(backoff * 2, self.watch_backoff_max_s)
+            finally:
+                self._stream = None
+
     def stop(self) -> None:
         self._stop.set()
+        self._kick.set()
+        s = self._stream
+        if s is not None:
+            s.close()
+        if self._watch_thread is not None and self._watch_thread is not threading.current_thread():
+            self._watch_thread.join(5)
 
     def run(self, once: bool = False) -> None:
+        if self.watch and not once and self._watch_thread is None:
+            self._watch_thread = threading.Thread(target=self._watch_loop, name="node-watch", daemon=True)
+            self._watch_thread.start()
         while not self._stop.is_set():
+            self._kick.clear()
             ok = self.reconcile_once()
             if once and ok:
                 return
             wait = self.resync_s if ok else self.retry_s
             if wait <= 0:
-                if ok:
+                if ok and not self.watch:
                     return
-                wait = self.retry_s
-            self._stop.wait(wait)
+                wait = self.retry_s if not ok else 3600.0
+            self._kick.wait(wait)

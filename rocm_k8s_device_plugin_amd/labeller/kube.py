@@ -13,11 +13,14 @@ embedded or file CA), ``$KUBECONFIG``, in-cluster service account
 from __future__ import annotations
 
 import base64
+import http.client
 import json
 import os
+import socket
 import ssl
 import tempfile
 import urllib.error
+import urllib.parse
 import urllib.request
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -115,6 +118,46 @@ def get_config(kubeconfig: str = "") -> KubeConfig:
     return in_cluster_config()
 
 
+class WatchStream:
+    """Newline-delimited JSON watch events of one HTTP response; close() from
+    another thread ends a blocked read (the socket is shut down)."""
+
+    def __init__(self, resp):
+        self._resp = resp
+        self.closed = False
+
+    def __iter__(self):
+        try:
+            while not self.closed:
+                line = self._resp.readline()
+                if not line:
+                    return
+                line = line.strip()
+                if line:
+                    yield json.loads(line)
+        except (OSError, ValueError, http.client.HTTPException):
+            if not self.closed:
+                raise
+        finally:
+            self.closed = True
+            try:
+                self._resp.close()   # by the reading thread only: http.client is not thread-safe
+            except OSError:
+                pass
+
+    def close(self) -> None:
+        """Ends the stream from any thread: the socket is shut down, so a
+        blocked read returns and the reading thread releases the response."""
+        if self.closed:
+            return
+        self.closed = True
+        try:
+            sock = self._resp.fp.raw._sock   # http.client internals
+            sock.shutdown(socket.SHUT_RDWR)
+        except (AttributeError, OSError):
+            pass
+
+
 class KubeClient:
     def __init__(self, cfg: KubeConfig, timeout_s: float = 15.0):
         self.cfg = cfg
@@ -146,6 +189,27 @@ class KubeClient:
     def patch_node_labels(self, name: str, labels: Dict[str, Optional[str]]) -> dict:
         return self._request("PATCH", f"/api/v1/nodes/{name}", {"metadata": {"labels": labels}},
                              "application/merge-patch+json")
+
+    def watch_node(self, name: str, resource_version: str = "", timeout_s: int = 300) -> "WatchStream":
+        """Watch one node (``GET /api/v1/nodes?watch=1&fieldSelector=metadata.name=<name>``):
+        an iterator of ``{"type": ADDED|MODIFIED|DELETED|BOOKMARK|ERROR, "object": {...}}``
+        until the server ends the watch (``timeoutSeconds``) or close() is called."""
+        q = {"watch": "1", "fieldSelector": f"metadata.name={name}", "timeoutSeconds": str(int(timeout_s)),
+             "allowWatchBookmarks": "true"}
+        if resource_version:
+            q["resourceVersion"] = resource_version
+        req = urllib.request.Request(self.cfg.server + "/api/v1/nodes?" + urllib.parse.urlencode(q), method="GET")
+        req.add_header("Accept", "application/json")
+        req.add_header("User-Agent", "mi355x-node-labeller")
+        if self.cfg.token:
+            req.add_header("Authorization", f"Bearer {self.cfg.token}")
+        try:
+            resp = urllib.request.urlopen(req, timeout=timeout_s + 30, context=self._ssl)
+        except urllib.error.HTTPError as e:
+            raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from e
+        except urllib.error.URLError as e:
+            raise KubeError(0, str(e.reason)) from e
+        return WatchStream(resp)
 
     def update_node(self, name: str, node: dict) -> dict:
         """Full-object update (PUT); fails with 409 if resourceVersion is stale."""

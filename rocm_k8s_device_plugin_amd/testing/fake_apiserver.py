@@ -1,11 +1,17 @@
 """A tiny fake kube-apiserver for labeller tests: GET / PATCH (JSON merge
-patch) / PUT of ``/api/v1/nodes/<name>`` over plain HTTP, bearer-token check,
-request log. Runs in a background thread (stdlib only)."""
+patch) / PUT of ``/api/v1/nodes/<name>`` and node watches
+(``GET /api/v1/nodes?watch=1&fieldSelector=metadata.name=<n>``, chunked
+newline-delimited JSON events, ``timeoutSeconds``, 410 ERROR events for a
+resourceVersion older than ``min_rv``) over plain HTTP/1.1, bearer-token
+check, request log. Runs in a background thread (stdlib only)."""
 from __future__ import annotations
 
 import copy
 import json
+import queue
 import threading
+import time
+import urllib.parse
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Dict, List, Optional, Tuple
 
@@ -29,12 +35,60 @@ class FakeApiServer:
         self.requests: List[Tuple[str, str, Optional[dict]]] = []
         self.fail_next: int = 0          # respond 500 to the next N requests
         self.forbid: set = set()         # HTTP methods answered with 403 (RBAC without that verb)
+        self.min_rv = 0                  # watches from an older resourceVersion get a 410 ERROR event
+        self.watchers: List[Tuple[str, "queue.Queue"]] = []
+        self.watch_starts = 0
         self._lock = threading.Lock()
         srv = self
 
         class Handler(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
             def log_message(self, *a):  # quiet
                 pass
+
+            def _chunk(self, obj) -> None:
+                raw = (json.dumps(obj) + "\n").encode()
+                self.wfile.write(f"{len(raw):x}\r\n".encode() + raw + b"\r\n")
+                self.wfile.flush()
+
+            def _watch(self, q):
+                name = (q.get("fieldSelector", [""])[0].partition("metadata.name=")[2])
+                rv = q.get("resourceVersion", [""])[0]
+                timeout = float(q.get("timeoutSeconds", ["300"])[0])
+                events: "queue.Queue" = queue.Queue()
+                with srv._lock:
+                    node = copy.deepcopy(srv.nodes.get(name))
+                    srv.watchers.append((name, events))
+                    srv.watch_starts += 1
+                self.send_response(200)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Transfer-Encoding", "chunked")
+                self.end_headers()
+                try:
+                    if rv and int(rv) < srv.min_rv:
+                        self._chunk({"type": "ERROR", "object": {"kind": "Status", "code": 410,
+                                                                 "message": "too old resource version"}})
+                    else:
+                        if node is not None and (not rv or node["metadata"]["resourceVersion"] != rv):
+                            self._chunk({"type": "ADDED" if not rv else "MODIFIED", "object": node})
+                        end = time.monotonic() + timeout
+                        while time.monotonic() < end:
+                            try:
+                                ev = events.get(timeout=min(0.05, max(0.0, end - time.monotonic())))
+                            except queue.Empty:
+                                continue
+                            if ev is None:        # expire_watches()
+                                break
+                            self._chunk(ev)
+                    self.wfile.write(b"0\r\n\r\n")
+                    self.wfile.flush()
+                except OSError:
+                    pass
+                finally:
+                    with srv._lock:
+                        srv.watchers = [w for w in srv.watchers if w[1] is not events]
+                self.close_connection = True
 
             def _auth(self) -> bool:
                 if srv.token and self.headers.get("Authorization") != f"Bearer {srv.token}":
@@ -57,6 +111,14 @@ class FakeApiServer:
                 return None
 
             def _handle(self, method):
+                url = urllib.parse.urlparse(self.path)
+                q = urllib.parse.parse_qs(url.query)
+                if method == "GET" and url.path.rstrip("/") == "/api/v1/nodes" and q.get("watch") == ["1"]:
+                    with srv._lock:
+                        srv.requests.append(("WATCH", self.path, None))
+                    if not self._auth():
+                        return
+                    return self._watch(q)
                 n = int(self.headers.get("Content-Length") or 0)
                 body = json.loads(self.rfile.read(n)) if n else None
                 with srv._lock:
@@ -83,9 +145,7 @@ class FakeApiServer:
                         if body["metadata"].get("resourceVersion") != node["metadata"].get("resourceVersion"):
                             return self._send(409, {"kind": "Status", "message": "conflict"})
                         node = body
-                    rv = int(node["metadata"].get("resourceVersion", "1")) + 1
-                    node["metadata"]["resourceVersion"] = str(rv)
-                    srv.nodes[name] = node
+                    srv._store(name, node, "MODIFIED")
                     return self._send(200, node)
 
             def do_GET(self):  # noqa: N802
@@ -104,9 +164,40 @@ class FakeApiServer:
     def url(self) -> str:
         return f"http://127.0.0.1:{self.httpd.server_address[1]}"
 
+    def _store(self, name: str, node: dict, event: str) -> None:
+        """(lock held) bump the resourceVersion, store, notify watchers."""
+        self._rv_counter = max(getattr(self, "_rv_counter", 1), int(node["metadata"].get("resourceVersion", "1"))) + 1
+        node["metadata"]["resourceVersion"] = str(self._rv_counter)
+        self.nodes[name] = node
+        for n, q in self.watchers:
+            if n == name:
+                q.put({"type": event, "object": copy.deepcopy(node)})
+
     def add_node(self, name: str, labels: Optional[Dict[str, str]] = None) -> None:
-        self.nodes[name] = {"apiVersion": "v1", "kind": "Node",
-                            "metadata": {"name": name, "labels": dict(labels or {}), "resourceVersion": "1"}}
+        with self._lock:
+            self._store(name, {"apiVersion": "v1", "kind": "Node",
+                               "metadata": {"name": name, "labels": dict(labels or {}), "resourceVersion": "1"}},
+                        "ADDED")
+
+    def set_labels(self, name: str, labels: Dict[str, str]) -> None:
+        """Replace a node's labels (someone else editing the node)."""
+        with self._lock:
+            node = copy.deepcopy(self.nodes[name])
+            node["metadata"]["labels"] = dict(labels)
+            self._store(name, node, "MODIFIED")
+
+    def delete_node(self, name: str) -> None:
+        with self._lock:
+            node = self.nodes.pop(name)
+            for n, q in self.watchers:
+                if n == name:
+                    q.put({"type": "DELETED", "object": node})
+
+    def expire_watches(self) -> None:
+        """End every open watch (as the apiserver does at timeoutSeconds)."""
+        with self._lock:
+            for _, q in self.watchers:
+                q.put(None)
 
     def labels(self, name: str) -> Dict[str, str]:
         return dict(self.nodes[name]["metadata"].get("labels") or {})

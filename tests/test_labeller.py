@@ -317,3 +317,107 @@ def test_node_name_sources(tmp_path, monkeypatch):
     assert cli.node_name_from(ns, str(f)) == "gpu-node-7"
     ns = cli.build_parser().parse_args(["-node_name", "n1"])
     assert cli.node_name_from(ns, str(f)) == "n1"
+
+
+def _wait(pred, timeout=5.0):
+    import time
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if pred():
+            return True
+        time.sleep(0.01)
+    return pred()
+
+
+def _running_labeller(tmp_path, srv, **kw):
+    import threading
+    fi = make_mi355x_node(tmp_path)
+    client = KubeClient(KubeConfig(server=srv.url, token="tok"))
+    enabled = {**ALL, "firmware": False, "family": False}
+    lab = NodeLabeller(client, "node-w", lambda: L.generate_labels(enabled, "container", str(fi.sysfs), str(fi.dev)),
+                       resync_s=300, **kw)
+    t = threading.Thread(target=lab.run, daemon=True)
+    t.start()
+    return lab, t
+
+
+def test_watch_restores_a_stripped_label_within_a_second(tmp_path):
+    """Labels stripped by someone else come back from the watch event, not
+    the 300 s resync (reference: controller-runtime watch, main.go:551-580)."""
+    import time
+    srv = FakeApiServer(token="tok").start()
+    lab = t = None
+    try:
+        srv.add_node("node-w", {"kubernetes.io/hostname": "node-w"})
+        lab, t = _running_labeller(tmp_path, srv)
+        assert _wait(lambda: srv.labels("node-w").get("amd.com/gpu.vram") == "288G")
+        assert _wait(lambda: srv.watch_starts >= 1)
+        passes = lab.stats.passes
+        labels = srv.labels("node-w")
+        labels.pop("amd.com/gpu.vram")
+        t0 = time.monotonic()
+        srv.set_labels("node-w", labels)
+        assert _wait(lambda: srv.labels("node-w").get("amd.com/gpu.vram") == "288G", 1.0)
+        assert time.monotonic() - t0 < 1.0
+        assert lab.stats.watch_kicks >= 1 and lab.stats.passes > passes
+        # our own PATCH comes back as an event that needs nothing: no reconcile loop
+        time.sleep(0.3)
+        settled = lab.stats.passes
+        time.sleep(0.3)
+        assert lab.stats.passes == settled
+    finally:
+        if lab is not None:
+            lab.stop()
+            t.join(5)
+        srv.stop()
+
+
+def test_watch_relabels_a_recreated_node_and_survives_watch_expiry(tmp_path):
+    srv = FakeApiServer(token="tok").start()
+    lab = t = None
+    try:
+        srv.add_node("node-w")
+        lab, t = _running_labeller(tmp_path, srv)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-w"))
+        assert _wait(lambda: srv.watch_starts >= 1)
+        srv.expire_watches()                       # apiserver ends the watch: reconnect
+        assert _wait(lambda: srv.watch_starts >= 2)
+        srv.delete_node("node-w")
+        srv.add_node("node-w", {"kubernetes.io/hostname": "node-w"})   # re-created without labels
+        assert _wait(lambda: srv.labels("node-w").get("amd.com/gpu.vram") == "288G", 2.0)
+        # a watch from a compacted resourceVersion gets 410: re-list, keep going
+        starts = srv.watch_starts
+        srv.min_rv = 10 ** 6
+        srv.expire_watches()
+        assert _wait(lambda: srv.watch_starts >= starts + 2)    # 410, then a fresh watch (no resourceVersion)
+        srv.min_rv = 0
+        assert t.is_alive() and lab.stats.watch_errors == 0
+    finally:
+        if lab is not None:
+            lab.stop()
+            t.join(5)
+            assert not t.is_alive()
+        srv.stop()
+
+
+def test_watch_failure_backs_off_and_resync_still_applies(tmp_path):
+    """Without the watch verb (403) the labeller logs, backs off and keeps its
+    periodic resync."""
+    srv = FakeApiServer(token="tok").start()
+    lab = t = None
+    try:
+        srv.add_node("node-w")
+        srv.forbid = set()
+        orig = srv.requests
+        lab, t = _running_labeller(tmp_path, srv, watch_backoff_max_s=0.2)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-w"))
+        assert _wait(lambda: srv.watch_starts >= 1)
+        srv.token = "other"          # every later request is 401, the watch included
+        srv.expire_watches()
+        assert _wait(lambda: lab.stats.watch_errors >= 2, 5.0)
+        assert orig is srv.requests and t.is_alive()
+    finally:
+        if lab is not None:
+            lab.stop()
+            t.join(5)
+        srv.stop()
