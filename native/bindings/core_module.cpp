@@ -196,7 +196,9 @@ PYBIND11_MODULE(_native, m) {
            py::arg("missing_pair_is_worst") = true, py::arg("cross_hive_penalty") = 100)
       .def_readwrite("missing_pair_is_worst", &AllocatorOptions::missing_pair_is_worst)
       .def_readwrite("cross_hive_penalty", &AllocatorOptions::cross_hive_penalty)
-      .def_readwrite("degraded_links", &AllocatorOptions::degraded_links);
+      .def_readwrite("degraded_links", &AllocatorOptions::degraded_links)
+      .def_readwrite("extended_search", &AllocatorOptions::extended_search)
+      .def_readwrite("extended_node_limit", &AllocatorOptions::extended_node_limit);
 
   // shared: the native gRPC server keeps using an allocator snapshot while
   // Python initialises its replacement

@@ -59,6 +59,15 @@ struct AllocatorOptions {
   // still reads xGMI, but traffic between them now takes another path, so the
   // pair scores as the worst link ("other") and packing avoids it
   std::vector<std::pair<std::string, std::string>> degraded_links;
+  // Off (default): the reference's candidate family (whole GPUs + one partial
+  // prefix), exact reference tie-breaks. On: an exact search over how many
+  // devices to take from every class of interchangeable devices (several
+  // partial GPUs allowed), minimising the same total pair weight; ties go to
+  // fewer physical GPUs, then the better kfd links between them (lower kfd
+  // link weight, then higher max_bandwidth), then the anti-fragmentation order.
+  bool extended_search = false;
+  // extended search: node budget before falling back to the reference family
+  uint64_t extended_node_limit = 2000000;
 };
 
 struct AllocResult {
@@ -115,12 +124,17 @@ class HiveAllocator {
   // groups restricted to available-and-not-required members, in reference order
   std::vector<std::vector<int>> filtered_groups(const std::vector<int>& avail_idx,
                                                 const std::vector<int>& req_idx) const;
+  // extended_search: false when the node budget ran out (caller falls back)
+  bool allocate_extended(const std::vector<int>& avail_idx, const std::vector<int>& req_idx, int size,
+                         AllocResult* out) const;
 
   AllocatorOptions opt_;
   std::vector<AllocDevice> devs_;
   std::unordered_map<std::string, int> index_;
   std::vector<int> w_;         // n*n pair weights
   std::vector<int> link_;      // n*n best link type (0 = none)
+  std::vector<int> link_kw_;   // n*n kfd link weight of that link (0 = unknown)
+  std::vector<int64_t> link_bw_;  // n*n kfd max_bandwidth of that link (MB/s, 0 = unknown)
   std::vector<Group> groups_;
   std::vector<int> dev_group_;  // device index -> group index
   size_t linked_pairs_ = 0;

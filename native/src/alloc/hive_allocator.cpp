@@ -62,6 +62,8 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
   dev_group_.clear();
   w_.clear();
   link_.clear();
+  link_kw_.clear();
+  link_bw_.clear();
   linked_pairs_ = from_keys_ = inferred_pairs_ = 0;
   opt_ = opt;
   if (devs.empty()) return "Devices list is empty. Unable to calculate pair wise weights";
@@ -77,15 +79,23 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
   }
 
   link_.assign(static_cast<size_t>(n) * n, 0);
+  link_kw_.assign(static_cast<size_t>(n) * n, 0);
+  link_bw_.assign(static_cast<size_t>(n) * n, 0);
   for (const KfdLink& l : topo.all_gpu_links()) {
     auto a = node2dev.find(l.node_from), b = node2dev.find(l.node_to);
     if (a == node2dev.end() || b == node2dev.end() || a->second == b->second) continue;
     int i = a->second, j = b->second;
-    int& cur = link_[static_cast<size_t>(i) * n + j];
+    const size_t ij = static_cast<size_t>(i) * n + j, ji = static_cast<size_t>(j) * n + i;
+    int& cur = link_[ij];
     int t = l.type <= 0 ? kLinkOther : l.type;
-    if (cur == 0 || link_rank(t) < link_rank(cur)) {
+    const bool better_type = cur == 0 || link_rank(t) < link_rank(cur);
+    const bool same_type_better = cur == t && ((l.weight > 0 && (link_kw_[ij] == 0 || l.weight < link_kw_[ij])) ||
+                                               (l.weight == link_kw_[ij] && l.max_bandwidth > link_bw_[ij]));
+    if (better_type || same_type_better) {
       cur = t;
-      link_[static_cast<size_t>(j) * n + i] = t;
+      link_[ji] = t;
+      link_kw_[ij] = link_kw_[ji] = l.weight;
+      link_bw_[ij] = link_bw_[ji] = l.max_bandwidth;
     }
   }
   std::unordered_set<int> froms;
@@ -253,6 +263,7 @@ AllocResult HiveAllocator::allocate(const std::vector<std::string>& available,
   std::vector<int> avail_idx, req_idx;
   res.error = validate(available, required, size, &res, &avail_idx, &req_idx);
   if (!res.error.empty() || res.short_circuit) return res;
+  if (opt_.extended_search && allocate_extended(avail_idx, req_idx, size, &res)) return res;
 
   const size_t n = devs_.size();
   auto W = [&](int a, int b) { return static_cast<int64_t>(w_[static_cast<size_t>(a) * n + b]); };
@@ -371,6 +382,218 @@ AllocResult HiveAllocator::allocate(const std::vector<std::string>& available,
   }
   for (int q : req_idx) res.ids.push_back(devs_[q].id);
   return res;
+}
+
+bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const std::vector<int>& req_idx, int size,
+                                      AllocResult* out) const {
+  const size_t n = devs_.size();
+  auto at = [&](int a, int b) { return static_cast<size_t>(a) * n + b; };
+  const auto fg = filtered_groups(avail_idx, req_idx);
+  const int need = size - static_cast<int>(req_idx.size());
+  // the free devices in anti-fragmentation order (fg: fewest free first)
+  std::vector<int> pool, pool_group;
+  for (size_t g = 0; g < fg.size(); ++g)
+    for (int m : fg[g]) {
+      pool.push_back(m);
+      pool_group.push_back(dev_group_[m]);  // physical GPU
+    }
+  std::vector<int> cand = pool;  // every device a chosen set can contain
+  cand.insert(cand.end(), req_idx.begin(), req_idx.end());
+
+  // classes of interchangeable free devices: same GPU and identical weights
+  // and kfd link figures to every other device a set can contain
+  auto same_row = [&](int a, int b) {
+    for (int x : cand) {
+      if (x == a || x == b) continue;
+      if (w_[at(a, x)] != w_[at(b, x)] || link_kw_[at(a, x)] != link_kw_[at(b, x)] ||
+          link_bw_[at(a, x)] != link_bw_[at(b, x)])
+        return false;
+    }
+    return true;
+  };
+  struct Class {
+    int group;
+    std::vector<int> members;  // pool order
+  };
+  std::vector<Class> cls;
+  for (size_t i = 0; i < pool.size(); ++i) {
+    int found = -1;
+    for (size_t c = 0; c < cls.size() && found < 0; ++c)
+      if (cls[c].group == pool_group[i] && same_row(cls[c].members[0], pool[i])) {
+        // transitivity within the class: the new device must match every member
+        bool all = true;
+        for (int m : cls[c].members) all = all && same_row(m, pool[i]);
+        if (all) found = static_cast<int>(c);
+      }
+    if (found < 0) {
+      cls.push_back(Class{pool_group[i], {pool[i]}});
+    } else {
+      cls[found].members.push_back(pool[i]);
+    }
+  }
+  const int K = static_cast<int>(cls.size());
+  // class-level aggregates
+  std::vector<int64_t> wi(K, 0), wr(K, 0), kwr(K, 0), bwr(K, 0);
+  std::vector<int64_t> wc(static_cast<size_t>(K) * K, 0), kwc(static_cast<size_t>(K) * K, 0),
+      bwc(static_cast<size_t>(K) * K, 0);
+  for (int c = 0; c < K; ++c) {
+    const int a = cls[c].members[0];
+    if (cls[c].members.size() > 1) wi[c] = w_[at(a, cls[c].members[1])];
+    for (int q : req_idx) {
+      wr[c] += w_[at(a, q)];
+      kwr[c] += link_kw_[at(a, q)];
+      bwr[c] += link_bw_[at(a, q)];
+    }
+    for (int d = 0; d < K; ++d) {
+      if (d == c) continue;
+      const int b = cls[d].members[0];
+      wc[static_cast<size_t>(c) * K + d] = w_[at(a, b)];
+      kwc[static_cast<size_t>(c) * K + d] = link_kw_[at(a, b)];
+      bwc[static_cast<size_t>(c) * K + d] = link_bw_[at(a, b)];
+    }
+  }
+  int64_t RR = 0;
+  std::vector<char> req_group(groups_.size(), 0);
+  for (size_t i = 0; i < req_idx.size(); ++i) {
+    req_group[dev_group_[req_idx[i]]] = 1;
+    for (size_t j = i + 1; j < req_idx.size(); ++j) RR += w_[at(req_idx[i], req_idx[j])];
+  }
+  std::vector<int> suffix_cap(K + 1, 0);
+  for (int c = K - 1; c >= 0; --c) suffix_cap[c] = suffix_cap[c + 1] + static_cast<int>(cls[c].members.size());
+  // smallest weight of a pair drawn from classes c.. (for the lower bound)
+  std::vector<int64_t> wmin_suffix(K + 1, std::numeric_limits<int64_t>::max());
+  for (int c = K - 1; c >= 0; --c) {
+    int64_t m = wmin_suffix[c + 1];
+    if (cls[c].members.size() > 1) m = std::min(m, wi[c]);
+    for (int d = c + 1; d < K; ++d) m = std::min(m, wc[static_cast<size_t>(c) * K + d]);
+    wmin_suffix[c] = m;
+  }
+  // symmetry: class c is interchangeable with c-1 (same size, same weights and
+  // link figures to everything else). Taking no more from c than from c-1
+  // loses no optimum: the tie-break prefers earlier pool positions anyway.
+  std::vector<char> sym_prev(K, 0);
+  for (int c = 1; c < K; ++c) {
+    const int b = c - 1;
+    bool same = cls[c].members.size() == cls[b].members.size() && wi[c] == wi[b] && wr[c] == wr[b] &&
+                kwr[c] == kwr[b] && bwr[c] == bwr[b];
+    for (int d = 0; d < K && same; ++d) {
+      if (d == b || d == c) continue;
+      same = wc[static_cast<size_t>(c) * K + d] == wc[static_cast<size_t>(b) * K + d] &&
+             kwc[static_cast<size_t>(c) * K + d] == kwc[static_cast<size_t>(b) * K + d] &&
+             bwc[static_cast<size_t>(c) * K + d] == bwc[static_cast<size_t>(b) * K + d];
+    }
+    sym_prev[c] = same;
+  }
+  std::vector<std::pair<int64_t, int>> unit;  // scratch for the bound
+  unit.reserve(K);
+
+  struct Key {
+    int64_t w = std::numeric_limits<int64_t>::max();
+    int gpus = 0;
+    int64_t kw = 0;   // lower better
+    int64_t bw = 0;   // higher better
+    std::vector<int> picks;  // pool positions of the chosen devices (sorted): anti-fragmentation order
+  } best;
+  bool found = false;
+  std::vector<int> k(K, 0);
+  std::vector<int> group_uses(groups_.size(), 0);
+  for (int q : req_idx) group_uses[dev_group_[q]]++;
+  uint64_t nodes = 0, leaves = 0;
+  bool aborted = false;
+  std::vector<int> pos_in_pool(n, -1);
+  for (size_t i = 0; i < pool.size(); ++i) pos_in_pool[pool[i]] = static_cast<int>(i);
+
+  // w: weight of the chosen free devices among themselves and with the required set
+  auto dfs = [&](auto&& self, int c, int cnt, int64_t w, int64_t kw, int64_t bw, int gpus) -> void {
+    if (aborted) return;
+    if (++nodes > opt_.extended_node_limit) {
+      aborted = true;
+      return;
+    }
+    const int m = need - cnt;
+    if (m == 0) {
+      ++leaves;
+      const int64_t total = w + RR;
+      Key key;
+      key.w = total;
+      key.gpus = gpus;
+      key.kw = kw;
+      key.bw = bw;
+      for (int d = 0; d < K; ++d)
+        for (int i = 0; i < k[d]; ++i) key.picks.push_back(pos_in_pool[cls[d].members[i]]);
+      std::sort(key.picks.begin(), key.picks.end());
+      bool better = !found || key.w < best.w ||
+                    (key.w == best.w &&
+                     (key.gpus < best.gpus ||
+                      (key.gpus == best.gpus &&
+                       (key.kw < best.kw || (key.kw == best.kw && (key.bw > best.bw ||
+                                                                  (key.bw == best.bw && key.picks < best.picks)))))));
+      if (better) {
+        best = std::move(key);
+        found = true;
+      }
+      return;
+    }
+    if (c >= K || suffix_cap[c] < m) return;
+    if (found) {
+      // lower bound: the m cheapest attachments to what is chosen (per class,
+      // up to its size) plus every pair among the m new devices at the
+      // smallest pair weight left
+      unit.clear();
+      for (int d = c; d < K; ++d) {
+        int64_t a = wr[d];
+        for (int e = 0; e < c; ++e)
+          if (k[e]) a += static_cast<int64_t>(k[e]) * wc[static_cast<size_t>(d) * K + e];
+        unit.emplace_back(a, static_cast<int>(cls[d].members.size()));
+      }
+      std::sort(unit.begin(), unit.end());
+      int64_t lb = 0;
+      int left = m;
+      for (auto& [a, cap] : unit) {
+        const int t = std::min(left, cap);
+        lb += a * t;
+        left -= t;
+        if (!left) break;
+      }
+      lb += static_cast<int64_t>(m) * (m - 1) / 2 * wmin_suffix[c];
+      if (w + RR + lb > best.w) return;
+    }
+    int cap = std::min<int>(m, static_cast<int>(cls[c].members.size()));
+    if (c > 0 && sym_prev[c]) cap = std::min(cap, k[c - 1]);
+    for (int take = cap; take >= 0; --take) {
+      int64_t dw = static_cast<int64_t>(take) * (take - 1) / 2 * wi[c] + take * wr[c];
+      int64_t dkw = take * kwr[c], dbw = take * bwr[c];
+      for (int d = 0; d < c; ++d) {
+        if (!k[d]) continue;
+        dw += static_cast<int64_t>(take) * k[d] * wc[static_cast<size_t>(c) * K + d];
+        if (cls[d].group != cls[c].group) {
+          dkw += static_cast<int64_t>(take) * k[d] * kwc[static_cast<size_t>(c) * K + d];
+          dbw += static_cast<int64_t>(take) * k[d] * bwc[static_cast<size_t>(c) * K + d];
+        }
+      }
+      const int g = cls[c].group;
+      const bool new_gpu = take > 0 && group_uses[g] == 0;
+      k[c] = take;
+      group_uses[g] += take;
+      self(self, c + 1, cnt + take, w + dw, kw + dkw, bw + dbw, gpus + (new_gpu ? 1 : 0));
+      group_uses[g] -= take;
+      k[c] = 0;
+      if (aborted) return;
+    }
+  };
+  int req_gpus = 0;
+  for (char r : req_group) req_gpus += r;
+  dfs(dfs, 0, 0, 0, 0, 0, req_gpus);
+  if (aborted) return false;
+  out->candidates = leaves;
+  if (!found) {
+    out->error = kNoCandidate;
+    return true;
+  }
+  out->weight = best.w;
+  for (int p : best.picks) out->ids.push_back(devs_[pool[p]].id);
+  for (int q : req_idx) out->ids.push_back(devs_[q].id);
+  return true;
 }
 
 AllocResult HiveAllocator::reference_allocate(const std::vector<std::string>& available,

@@ -121,6 +121,24 @@ static void test_allocator_reference_contract(const std::string& ref) {
     });
   for (auto& x : th) x.join();
   CHECK(bad == 0);
+  // extended search: never heavier than the reference family, valid sets, concurrent-safe
+  AllocatorOptions ext;
+  ext.extended_search = true;
+  HiveAllocator x;
+  CHECK(x.init(devs, topo, ext).empty());
+  for (int k = 1; k <= 62; k += 5) {
+    auto e = x.allocate(all, {}, k);
+    auto b = a.allocate(all, {}, k);
+    CHECK(e.error.empty() && e.ids.size() == static_cast<size_t>(k) && e.weight <= b.weight);
+  }
+  std::vector<std::thread> th2;
+  for (int t = 0; t < 4; ++t)
+    th2.emplace_back([&] {
+      for (int i = 0; i < 20; ++i)
+        if (x.allocate(all, {"test2"}, 12).ids.size() != 12) ++bad;
+    });
+  for (auto& t : th2) t.join();
+  CHECK(bad == 0);
 }
 
 static void test_errors() {

@@ -47,10 +47,15 @@ def group_key(d) -> str:
 class BestEffortPolicy(Policy):
     """Hive-aware optimal subset selection with the reference's tie-breaks."""
 
-    def __init__(self, missing_pair_is_worst: bool = True, cross_hive_penalty: int = 100):
+    def __init__(self, missing_pair_is_worst: bool = True, cross_hive_penalty: int = 100,
+                 extended_search: bool = False):
+        """`extended_search`: search every split of the request over classes of
+        interchangeable devices (several partial GPUs; kfd link weight /
+        bandwidth tie-breaks) instead of the reference's candidate family."""
         n = core()
         self._opts = n.AllocatorOptions(missing_pair_is_worst=missing_pair_is_worst,
                                         cross_hive_penalty=cross_hive_penalty)
+        self._opts.extended_search = bool(extended_search)
         self._alloc = n.HiveAllocator()
         self.stats = AllocStats()
 

@@ -70,6 +70,9 @@ def build_parser() -> flags.GoFlagParser:
                                   "stops counting as xGMI-connected in preferred allocation (devices stay Healthy)")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
+    p.add_bool("allocator_extended_search", False, "GetPreferredAllocation searches every split of a request over "
+                                                   "interchangeable devices (several partial GPUs) and breaks ties "
+                                                   "by kfd link weight/bandwidth; off = the reference's candidates")
     p.add_str("grpc_server", "native", "kubelet-facing gRPC server: native (C++ HTTP/2; admission RPCs answered "
                                        "without Python) or aio (Python grpc.aio)")
     p.add_bool("dry_run", False, "print what this node would advertise (implementation, resources, devices, "
@@ -243,7 +246,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         print(json.dumps(asyncio.run(dry_run_report(impl, sweep=ns.pulse > 0)), indent=1))
         return 0
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
-                       metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch, grpc_server=ns.grpc_server)
+                       metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch, grpc_server=ns.grpc_server,
+                       allocator_extended_search=ns.allocator_extended_search)
     from ..utils.trace import TRACER
     TRACER.configure(ns.trace_file or None)
     try:

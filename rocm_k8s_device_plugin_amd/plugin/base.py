@@ -42,10 +42,10 @@ class PluginContext:
         return self.allocator_error
 
 
-def new_context(resource: str) -> PluginContext:
+def new_context(resource: str, extended_search: bool = False) -> PluginContext:
     """One allocator per resource, like the reference's lister.NewPlugin (manager.go:96-104)."""
     try:
-        alloc = BestEffortPolicy()
+        alloc = BestEffortPolicy(extended_search=extended_search)
     except ImportError:
         alloc = None
     return PluginContext(resource=resource, allocator=alloc)

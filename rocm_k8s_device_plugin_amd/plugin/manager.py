@@ -62,6 +62,8 @@ class ManagerConfig:
     # kubelet-facing gRPC server: "native" (C++ HTTP/2, plugin/native_server.py)
     # or "aio" (Python grpc.aio, plugin/servicer.py)
     grpc_server: str = "native"
+    # GetPreferredAllocation beyond the reference's candidate family (allocator.py)
+    allocator_extended_search: bool = False
 
 
 class ResourcePlugin:
@@ -71,7 +73,7 @@ class ResourcePlugin:
         cfg = mgr.cfg
         self.resource_name = f"{cfg.namespace}/{name}"
         self.socket = os.path.join(cfg.plugin_dir, f"{cfg.namespace}_{name}")
-        self.ctx: PluginContext = new_context(name)
+        self.ctx: PluginContext = new_context(name, extended_search=cfg.allocator_extended_search)
         self.stop_bc = Broadcast()
         self.servicer: Optional[DevicePluginServicer] = None
         self.server: Optional[grpc.aio.Server] = None

@@ -259,3 +259,103 @@ def test_fragmented_nodes_match_reference_bfs(ref_testdata, name):
         assert sorted(ours["ids"]) == sorted(ref["ids"]), (av, req, k)
 
     check()
+
+
+# ---------------------------------------------------------------- extended search (opt-in)
+
+def _gpu_of(i):
+    # synthetic ids: test<k> is GPU k-1's first partition, amdgpu_xcp_<8i+j> its j-th
+    return int(i[4:]) - 1 if i.startswith("test") else int(i.rsplit("_", 1)[1]) // 8
+
+
+def _optimum(pol, av, req, k):
+    nat = pol.native
+    best = None
+    rest = [i for i in av if i not in req]
+    for combo in itertools.combinations(rest, k - len(req)):
+        s = list(combo) + list(req)
+        w = sum(nat.pair_weight(a, b) for a, b in itertools.combinations(s, 2))
+        g = len({_gpu_of(x) for x in s})
+        if best is None or (w, g) < best:
+            best = (w, g)
+    return best
+
+
+@pytest.mark.parametrize("topo", ["mi300cpx", "mi308"])
+def test_extended_search_is_optimal_on_small_partition_subsets(ref_testdata, topo):
+    """With extended_search the chosen set has the minimum total pair weight
+    over ALL subsets (brute force on <= 12 available partitions, random
+    must-include), and among those the fewest physical GPUs."""
+    pol, ids = make_policy(ref_testdata, topo, extended_search=True)
+    ref_pol, _ = make_policy(ref_testdata, topo)
+    rng = random.Random(11)
+    checked = 0
+    for _ in range(120):
+        av = rng.sample(ids, rng.randint(3, 12))
+        k = rng.randint(1, len(av) - 1)
+        req = rng.sample(av, rng.randint(0, min(2, k)))
+        if len(req) == k:
+            continue
+        r = pol.explain(av, req, k)
+        assert not r["error"] and len(r["ids"]) == k and set(req) <= set(r["ids"]) <= set(av), r
+        w_opt, g_opt = _optimum(pol, av, req, k)
+        assert r["weight"] == w_opt, (av, req, k, r)
+        assert len({_gpu_of(x) for x in r["ids"]}) == g_opt, (av, req, k, r)
+        # never worse than the reference's candidate family on the same weights
+        assert r["weight"] <= ref_pol.explain(av, req, k)["weight"]
+        checked += 1
+    assert checked > 80
+
+
+def test_extended_search_off_by_default_keeps_the_reference_answer(ref_testdata):
+    pol_off, ids = make_policy(ref_testdata, "mi300cpx")
+    rng = random.Random(5)
+    for _ in range(30):
+        av = rng.sample(ids, rng.randint(4, 40))
+        k = rng.randint(1, len(av) - 1)
+        assert pol_off.explain(av, [], k)["ids"] == pol_off.reference_allocate(av, [], k)["ids"]
+
+
+def test_extended_search_full_cpx_node_is_fast_and_packs(ref_testdata):
+    """64 partitions: whole-node sizes finish within the node budget (no fallback needed)
+    and a request of one GPU's worth lands on one GPU."""
+    import time
+    pol, ids = make_policy(ref_testdata, "mi300cpx", extended_search=True)
+    for k in (1, 4, 8, 9, 16, 31, 32, 48):
+        t = time.perf_counter()
+        r = pol.explain(ids, [], k)
+        dt = time.perf_counter() - t
+        assert not r["error"] and len(r["ids"]) == k
+        assert dt < 2.0, (k, dt)
+        if k in (8, 16, 32):
+            assert len({_gpu_of(x) for x in r["ids"]}) == k // 8
+
+
+@pytest.mark.parametrize("cp,mp,hive", [("cpx", "nps2", 8), ("qpx", "nps2", 4), ("dpx", "nps1", 4)])
+def test_extended_search_optimal_on_mi355x_fixture(tmp_path, cp, mp, hive):
+    """MI355X partition fixtures (NPS2: a GPU's partitions sit in two NUMA
+    classes; two hives): brute-force optimum on <= 12 available devices."""
+    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+    from rocm_k8s_device_plugin_amd.topology import discover
+    fi = make_mi355x_node(tmp_path / "n", compute_partition=cp.upper(), memory_partition=mp.upper(),
+                          hive_size=hive)
+    inv = discover(str(fi.sysfs))
+    pol = BestEffortPolicy(extended_search=True)
+    pol.init(inv.devices, inv.topology)
+    gpu = {d.id: d.unique_id for d in inv.devices}
+    ids = [d.id for d in inv.devices]
+    rng = random.Random(3)
+    for _ in range(60):
+        av = rng.sample(ids, rng.randint(3, min(12, len(ids))))
+        k = rng.randint(1, len(av) - 1)
+        req = rng.sample(av, rng.randint(0, min(2, k - 1)))
+        r = pol.explain(av, req, k)
+        assert not r["error"], r
+        best = None
+        rest = [i for i in av if i not in req]
+        for combo in itertools.combinations(rest, k - len(req)):
+            s = list(combo) + req
+            w = sum(pol.native.pair_weight(a, b) for a, b in itertools.combinations(s, 2))
+            key = (w, len({gpu[x] for x in s}))
+            best = key if best is None or key < best else best
+        assert (r["weight"], len({gpu[x] for x in r["ids"]})) == best, (av, req, k, r)
