@@ -84,17 +84,20 @@ void bind_rpc(py::module_& m) {
           "set_allocate_template",
           [](PyDevicePluginServer& s, const std::string& resource, const std::string& prefix,
              const std::unordered_map<std::string, std::string>& per_device, const std::string& annotation_key,
-             const std::unordered_map<std::string, std::string>& annotation_names) {
+             const std::unordered_map<std::string, std::string>& annotation_names,
+             const std::string& container_nonempty) {
             AllocateTemplate t;
             t.resource = resource;
             t.container_prefix = prefix;
             t.per_device = per_device;
+            t.container_nonempty = container_nonempty;
             t.annotation_key = annotation_key;
             t.annotation_names = annotation_names;
             s.svc.set_allocate_template(std::move(t));
           },
           py::arg("resource"), py::arg("container_prefix"), py::arg("per_device"), py::arg("annotation_key") = "",
-          py::arg("annotation_names") = std::unordered_map<std::string, std::string>())
+          py::arg("annotation_names") = std::unordered_map<std::string, std::string>(),
+          py::arg("container_nonempty") = "")
       .def("clear_allocate_template", [](PyDevicePluginServer& s) { s.svc.set_allocate_template(std::nullopt); })
       .def("set_device_list", [](PyDevicePluginServer& s, std::optional<std::string> b) { s.svc.set_device_list(b); })
       .def("set_native_enabled", [](PyDevicePluginServer& s, bool on) { s.svc.set_native_enabled(on); })

@@ -31,12 +31,14 @@ namespace mi355x::rpc {
 
 // Allocate fast path: every ContainerAllocateResponse is
 //   container_prefix + per_device[id] for each requested id (request order)
+//   + (at least one id) container_nonempty
 //   + (annotation_key set) annotations{annotation_key: join(annotation_names[id], ",")}
 // as raw protobuf field bytes; an unknown ID is an INVALID_ARGUMENT error.
 struct AllocateTemplate {
   std::string resource;  // for error messages
   std::string container_prefix;
   std::unordered_map<std::string, std::string> per_device;
+  std::string container_nonempty;  // e.g. the node-view mounts of a container that got devices
   std::string annotation_key;
   std::unordered_map<std::string, std::string> annotation_names;
 };

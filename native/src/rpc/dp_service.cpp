@@ -270,6 +270,7 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
             },
             nullptr);
         if (!scanned) return false;
+        if (any) car += t->container_nonempty;
         if (any && !t->annotation_key.empty()) {
           std::string entry;
           pb::put_bytes(&entry, 1, t->annotation_key);

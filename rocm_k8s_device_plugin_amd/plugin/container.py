@@ -54,10 +54,11 @@ class ContainerImpl(DeviceImpl):
         self._cdi = any(s != cdi.DEVICE_SPECS for s in self.list_strategies)
         self.sysfs_root = sysfs_root
         # opt-in: per-allocation filtered kfd topology bind-mounted into the container
-        self.topology_views = (TopologyViews(topology_view_dir, os.path.join(sysfs_root, "class/kfd/kfd/topology"))
-                               if topology_view_dir else None)
+        self._listeners: List = []   # called when what Allocate returns changes (native server templates)
+        self._topology_views = (TopologyViews(topology_view_dir, os.path.join(sysfs_root, "class/kfd/kfd/topology"))
+                                if topology_view_dir else None)
         # opt-in: NUMA-node sysfs without the per-CPU cache walk ROCr does at start-up
-        self.node_view = NodeView(node_view_dir, sysfs_root) if node_view_dir else None
+        self._node_view = NodeView(node_view_dir, sysfs_root) if node_view_dir else None
         if self.node_view is not None:  # build at start-up, not inside the first Allocate
             try:
                 self.node_view.path()
@@ -299,12 +300,52 @@ class ContainerImpl(DeviceImpl):
                     _log.warning("node view unavailable: %s", e)
         return resp
 
+    # what Allocate returns can change at run time (views switched on/off):
+    # the native server's prepared fragments follow through these listeners
+    def add_change_listener(self, fn) -> None:
+        self._listeners.append(fn)
+
+    def remove_change_listener(self, fn) -> None:
+        if fn in self._listeners:
+            self._listeners.remove(fn)
+
+    def _changed(self) -> None:
+        for fn in list(self._listeners):
+            fn()
+
+    @property
+    def topology_views(self):
+        return self._topology_views
+
+    @topology_views.setter
+    def topology_views(self, v) -> None:
+        self._topology_views = v
+        self._changed()
+
+    @property
+    def node_view(self):
+        return self._node_view
+
+    @node_view.setter
+    def node_view(self, v) -> None:
+        self._node_view = v
+        self._changed()
+
     def allocate_template(self, ctx: PluginContext) -> Optional[dict]:
         """Allocate response fragments per device for the native server's fast
         path (plugin/native_server.py); parsed, its responses equal allocate()'s.
-        None when a response needs per-request work (topology / node views)."""
-        if self.topology_views is not None or self.node_view is not None:
+        None when a response needs per-request work (topology views: one per
+        allocated node set)."""
+        if self.topology_views is not None:
             return None
+        nonempty = b""
+        if self.node_view is not None:
+            try:
+                nonempty = pb.ContainerAllocateResponse(mounts=[
+                    pb.Mount(container_path=ctr, host_path=host, read_only=True)
+                    for host, ctr in self.node_view.mounts()]).SerializeToString()
+            except OSError:   # allocate() reports it per request
+                return None
         specs = cdi.DEVICE_SPECS in self.list_strategies
         prefix = pb.ContainerAllocateResponse()
         if specs:
@@ -326,7 +367,7 @@ class ContainerImpl(DeviceImpl):
             return None
         return {"resource": ctx.resource, "container_prefix": prefix.SerializeToString(), "per_device": per_device,
                 "annotation_key": cdi.annotation_key(ctx.resource) if annotate else "",
-                "annotation_names": names}
+                "annotation_names": names, "container_nonempty": nonempty}
 
     def preferred_allocation(self, ctx: PluginContext,
                              req: pb.PreferredAllocationRequest) -> pb.PreferredAllocationResponse:

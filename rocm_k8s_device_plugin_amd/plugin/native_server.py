@@ -140,6 +140,8 @@ class NativePluginServer:
 
     # ------------------------------------------------------------ lifecycle
     async def start(self, socket: str) -> None:
+        if hasattr(self.impl, "add_change_listener"):
+            self.impl.add_change_listener(self.refresh)
         self.refresh()
         err = self.srv.start(socket)
         if err:
@@ -149,6 +151,8 @@ class NativePluginServer:
         self._task = asyncio.create_task(self._watch())
 
     async def stop(self, grace: float = 0.5) -> None:
+        if hasattr(self.impl, "remove_change_listener"):
+            self.impl.remove_change_listener(self.refresh)
         if self._task is not None:
             self._task.cancel()
             await asyncio.gather(self._task, return_exceptions=True)

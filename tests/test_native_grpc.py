@@ -202,13 +202,15 @@ async def _drive(st, reqs):
 
 
 @pytest.mark.parametrize("mode,strategies", [("spx", (cdi.DEVICE_SPECS,)), ("cpx", (cdi.DEVICE_SPECS,)),
-                                             ("spx", (cdi.DEVICE_SPECS, cdi.CDI_CRI, cdi.CDI_ANNOTATIONS))])
+                                             ("spx", (cdi.DEVICE_SPECS, cdi.CDI_CRI, cdi.CDI_ANNOTATIONS)),
+                                             ("spx-nodeview", (cdi.DEVICE_SPECS,))])
 def test_native_answers_equal_the_aio_servicer(tmp_path, mode, strategies):
     fi = make_mi355x_node(tmp_path / "n", **({"compute_partition": "CPX"} if mode == "cpx" else {}))
     out = {}
     for server in ("aio", "native"):
+        extra = {"node_view_dir": str(tmp_path / "nv")} if mode == "spx-nodeview" else {}
         impl = ContainerImpl("single", str(fi.sysfs), HealthConfig(exporter_socket=None),
-                             device_list_strategy=strategies, cdi_spec_dir=str(tmp_path / f"cdi-{server}"))
+                             device_list_strategy=strategies, cdi_spec_dir=str(tmp_path / f"cdi-{server}"), **extra)
 
         async def fn(k, mgr, st):
             ids = sorted(st.devices)
@@ -476,3 +478,34 @@ def test_cli_grpc_server_flag(tmp_path):
     assert cli.validate(cli.build_parser().parse_args(["-grpc_server", "aio"])) is None
     with pytest.raises(ValueError):
         PluginManager(None, ManagerConfig(grpc_server="bogus"))
+
+
+def test_views_switched_at_run_time_reach_the_native_allocate(tmp_path):
+    """Setting -node_view's view on a running plugin (what bench.py does for its
+    comparison) updates the prepared Allocate fragments: the mounts come back
+    without a Python fallback; a topology view switches Allocate to the fallback."""
+    from rocm_k8s_device_plugin_amd.node_view import NodeView
+    from rocm_k8s_device_plugin_amd.topology_view import TopologyViews
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = _impl(fi)
+
+    async def fn(k, mgr, st):
+        a0 = await k.admit("amd.com/gpu", 1)
+        assert not a0.response.container_responses[0].mounts
+        k.release("amd.com/gpu", a0.device_ids)
+        impl.node_view = NodeView(str(tmp_path / "nv"), str(fi.sysfs))
+        a1 = await k.admit("amd.com/gpu", 1)
+        k.release("amd.com/gpu", a1.device_ids)
+        plugin = mgr.plugins["gpu"]
+        plugin.sync()
+        fb = plugin.native.fallbacks
+        impl.topology_views = TopologyViews(str(tmp_path / "tv"), str(fi.sysfs / "class/kfd/kfd/topology"))
+        a2 = await k.admit("amd.com/gpu", 1)
+        plugin.sync()
+        return a1, a2, fb, plugin.native.fallbacks
+
+    a1, a2, fb_before, fb_after = run(_with_plugin(tmp_path, impl, "native", fn))
+    m1 = a1.response.container_responses[0].mounts
+    assert m1 and all(m.read_only for m in m1)
+    assert fb_before == 0
+    assert fb_after == 1 and any(m.container_path.endswith("topology") for m in a2.response.container_responses[0].mounts)
