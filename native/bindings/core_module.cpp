@@ -387,6 +387,7 @@ PYBIND11_MODULE(_native, m) {
       d["memory_partition"] = g.memory_partition;
       d["vram_mb"] = g.vram_mb;
       d["ecc_ok"] = g.ecc_ok;
+      d["gfx_activity"] = g.gfx_activity;
       d["ecc_correctable"] = g.ecc_correctable;
       d["ecc_uncorrectable"] = g.ecc_uncorrectable;
       d["drm_render"] = g.drm_render;

@@ -38,6 +38,7 @@ struct SmiGpu {
   std::string hip_uuid;
   std::string driver_name;      // amdsmi_get_gpu_driver_info
   std::string driver_version;
+  int gfx_activity = -1;        // amdsmi_get_gpu_activity, % (-1 = unavailable)
 };
 
 struct SmiSnapshot {

@@ -42,6 +42,7 @@ struct SmiLib {
   decltype(&amdsmi_get_gpu_xgmi_link_status) link_status = nullptr;
   decltype(&amdsmi_get_link_metrics) link_metrics = nullptr;
   decltype(&amdsmi_get_gpu_driver_info) driver = nullptr;
+  decltype(&amdsmi_get_gpu_activity) activity = nullptr;
 };
 
 template <typename T>
@@ -79,6 +80,7 @@ const SmiLib& smi() {
     bind(l.h, "amdsmi_get_gpu_xgmi_link_status", &l.link_status);
     bind(l.h, "amdsmi_get_link_metrics", &l.link_metrics);
     bind(l.h, "amdsmi_get_gpu_driver_info", &l.driver);
+    bind(l.h, "amdsmi_get_gpu_activity", &l.activity);
   });
   return l;
 }
@@ -217,6 +219,8 @@ SmiSnapshot smi_snapshot() {
           g.hip_uuid = en.hip_uuid;
         }
         amdsmi_driver_info_t di{};
+        amdsmi_engine_usage_t eu{};
+        if (L.activity && L.activity(h, &eu) == AMDSMI_STATUS_SUCCESS) g.gfx_activity = static_cast<int>(eu.gfx_activity);
         if (L.driver && L.driver(h, &di) == AMDSMI_STATUS_SUCCESS) {
           g.driver_name = di.driver_name;
           g.driver_version = di.driver_version;

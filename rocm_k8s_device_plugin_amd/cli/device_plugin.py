@@ -60,6 +60,8 @@ def build_parser() -> flags.GoFlagParser:
                                               "failure; applies in every liveness mode (kept queues: the queued "
                                               "dispatch's late verdict is awaited; otherwise a deadline miss on "
                                               "a busy GPU is inconclusive)")
+    p.add_bool("liveness_corroborate", True, "a probe pending on a busy GPU stays inconclusive only while amd-smi "
+                                             "reports GFX activity; 0% on 2 consecutive sweeps ends the busy grace")
     p.add_float("liveness_unknown_busy_grace", 30.0, "the busy grace while busy GPUs cannot be told from idle ones "
                                                      "(kfd process list unreadable): every GPU counts as busy, "
                                                      "so the grace is shorter")
@@ -139,7 +141,8 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
                           liveness_mode=ns.liveness_mode, chip_sweep_every=ns.liveness_chip_sweep_every,
                           liveness_keep_queues=ns.liveness_keep_queues,
                           liveness_busy_grace_s=ns.liveness_busy_grace,
-                          liveness_unknown_busy_grace_s=ns.liveness_unknown_busy_grace)
+                          liveness_unknown_busy_grace_s=ns.liveness_unknown_busy_grace,
+                          liveness_corroborate=ns.liveness_corroborate)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         from .. import cdi

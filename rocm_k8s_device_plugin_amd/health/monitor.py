@@ -75,6 +75,11 @@ class HealthConfig:
     # unreadable, or the probe server's own kfd entry unresolved): every GPU
     # then counts as busy, so the grace is kept short to bound the blind spot
     liveness_unknown_busy_grace_s: float = 30.0
+    # a pending probe on a "busy" GPU is only inconclusive while the GPU is
+    # actually executing: amd-smi reporting 0% GFX activity on this many
+    # consecutive sweeps ends the grace (a wedged queue, not a long kernel)
+    liveness_corroborate: bool = True
+    liveness_idle_sweeps: int = 2
     recover_threshold: int = 1
     smi_ecc: bool = False
     smi_events: bool = False
@@ -89,6 +94,7 @@ class _Track:
     live: bool = True
     last_reason: str = ""
     pending_since: Optional[float] = None   # first inconclusive (busy GPU) probe
+    idle_pending: int = 0                   # consecutive pending sweeps with 0% GFX activity
 
 
 class HealthMonitor:
@@ -96,7 +102,8 @@ class HealthMonitor:
                  prober: Optional[LivenessProber] = None,
                  ordinal_map: Optional[Mapping[str, int]] = None,
                  exporter_fn: Optional[Callable] = None, event_source=None,
-                 fabric_source: Optional[Callable[[], dict]] = None):
+                 fabric_source: Optional[Callable[[], dict]] = None,
+                 activity_source: Optional[Callable[[], Dict[str, int]]] = None):
         self.inv = inventory
         self.cfg = cfg or HealthConfig()
         self.prober = prober
@@ -123,6 +130,7 @@ class HealthMonitor:
         self._smi_held = False   # amd-smi kept initialised while its sources are on (smi_hold)
         self.busy_state_known = True   # last sweep could tell busy GPUs from idle ones
         self.identity_remaps = 0       # sweeps whose probe replies did not match the positional ordinals
+        self._activity_source = activity_source   # bdf -> GFX activity % (amd-smi by default)
 
     # ------------------------------------------------------------------ fabric
     def degraded_links(self):
@@ -283,6 +291,19 @@ class HealthMonitor:
                 out.add(dev_id)
         return out
 
+    def _gfx_activity(self) -> Dict[str, int]:
+        """bdf -> GFX engine activity % (amd-smi); {} when unavailable."""
+        if self._activity_source is not None:
+            return self._activity_source()
+        n = core()
+        if not n.smi_available():
+            return {}
+        self._smi_hold()
+        snap = n.smi_snapshot()
+        if not snap["ok"]:
+            return {}
+        return {g["bdf"]: int(g.get("gfx_activity", -1)) for g in snap["gpus"] if g.get("gfx_activity", -1) >= 0}
+
     def _set_busy_known(self, known: bool, why: str) -> None:
         if known != self.busy_state_known:
             if known:
@@ -433,16 +454,29 @@ class HealthMonitor:
             now = time.monotonic()
             grace = self.cfg.liveness_busy_grace_s if self.busy_state_known else \
                 min(self.cfg.liveness_busy_grace_s, self.cfg.liveness_unknown_busy_grace_s)
+            idle_wedged = set()
+            waiting = [d for d, o in outcomes.items() if o.pending and d in busy_devs]
+            if waiting and self.cfg.liveness_corroborate:
+                act = await asyncio.to_thread(self._gfx_activity)
+                for dev_id in waiting:
+                    d = self.inv.by_id.get(dev_id)
+                    a = act.get(d.bdf, -1) if d is not None else -1
+                    tr = self._track[dev_id]
+                    tr.idle_pending = tr.idle_pending + 1 if a == 0 else 0
+                    if tr.idle_pending >= self.cfg.liveness_idle_sweeps:
+                        idle_wedged.add(dev_id)
             for dev_id, o in outcomes.items():
                 REGISTRY.set("mi355x_dp_liveness_probe_ms", float(o.latency_ms),
                              help="last liveness probe round trip", device=dev_id)
                 tr = self._track[dev_id]
+                if not o.pending:
+                    tr.idle_pending = 0
                 if o.ok:
                     tr.fails, tr.oks = 0, tr.oks + 1
                     tr.pending_since = None
                     if not tr.live and tr.oks >= self.cfg.recover_threshold:
                         tr.live = True
-                elif o.pending and dev_id in busy_devs and \
+                elif o.pending and dev_id in busy_devs and dev_id not in idle_wedged and \
                         now - (tr.pending_since or now) < grace:
                     # queued behind a tenant's kernel: neither a pass nor a failure yet
                     tr.pending_since = tr.pending_since or now
@@ -451,6 +485,12 @@ class HealthMonitor:
                 else:
                     tr.oks, tr.fails = 0, tr.fails + 1
                     tr.last_reason = o.reason
+                    if dev_id in idle_wedged:
+                        tr.last_reason += (f" while the GPU reports 0% GFX activity ({tr.idle_pending} sweeps): "
+                                           "no tenant kernel is running")
+                        from ..utils.metrics import REGISTRY as _R
+                        _R.inc("mi355x_dp_liveness_idle_pending_total", help="pending probes on an idle GFX engine",
+                               device=dev_id)
                     if not o.pending:
                         tr.pending_since = None
                     if tr.live and tr.fails >= self.cfg.fail_threshold:

@@ -52,6 +52,15 @@ def test_inprocess_mfma_probe(hip):
         assert 0 <= r["xcc_id"] < 8
 
 
+def test_inprocess_probe_kernel_time_excludes_code_object_load(hip):
+    """kernel_us is a warm launch; the cold one (lazy code-object load) is first_launch_us."""
+    r = hip.probe(0, 99, 4)
+    assert r["ok"], r
+    assert 0 < r["kernel_us"] < 200, r          # rocprof: 2.8-5 us; event pair overhead on top
+    if r["first_launch"]:
+        assert r["first_launch_us"] > r["kernel_us"]
+
+
 def test_inprocess_probe_many_iters(hip):
     r = hip.probe(0, 7, 64)
     assert r["ok"] and r["iters"] == 64, r
@@ -533,6 +542,9 @@ def test_smi_cross_check(inv):
         json.dump(snap, f, indent=1, default=str)
     bdfs = {g["bdf"] for g in snap["gpus"]}
     assert bdfs & {d.bdf for d in inv.devices}
+    # GFX activity corroborates pending probes on busy GPUs (health/monitor.py)
+    mine = [g for g in snap["gpus"] if g["bdf"] in {d.bdf for d in inv.devices if d.identity == "kfd"}]
+    assert mine and all(0 <= g["gfx_activity"] <= 100 for g in mine), mine
 
 
 def test_drm_gpu_info(inv, ordinals):

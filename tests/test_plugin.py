@@ -1118,3 +1118,34 @@ def test_probe_identity_unmatched_device_loses_its_ordinal(tmp_path):
     assert mon.health(victim) == "Unhealthy"
     assert any("no HIP device" in r for r in mon.snapshot()[victim].reasons)
     assert sum(mon.health(d.id) == "Healthy" for d in inv.devices) == len(inv.devices) - 1
+
+
+@pytest.mark.parametrize("activity,unhealthy", [(0, True), (87, False), (None, False)])
+def test_busy_grace_needs_gfx_activity(tmp_path, activity, unhealthy):
+    """A pending probe on a GPU that runs another process's queues is
+    inconclusive only while the GPU is executing: amd-smi reporting 0% GFX
+    activity on consecutive sweeps (a wedged queue, not a long tenant kernel)
+    ends the 300 s grace; with activity, or without amd-smi, the grace holds."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    dev = inv.devices[3]
+    _busy_gpu(fi, inv, dev.id)
+    ctl, prober = _stub_prober(tmp_path, {"3": "pending"})
+    src = (lambda: {}) if activity is None else (lambda: {d.bdf: (activity if d.id == dev.id else 50)
+                                                          for d in inv.devices})
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=2,
+                                          liveness_busy_grace_s=300.0), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)}, activity_source=src)
+
+    async def go():
+        try:
+            for _ in range(4):
+                await mon.check_once()
+        finally:
+            await mon.close()
+
+    run(go())
+    assert (mon.health(dev.id) == "Unhealthy") == unhealthy
+    if unhealthy:
+        assert any("0% GFX activity" in r for r in mon.snapshot()[dev.id].reasons)
+    assert all(mon.health(d.id) == "Healthy" for d in inv.devices if d.id != dev.id)

@@ -5,7 +5,7 @@ real plugin (fake kubelet, ListAndWatch), with a Chrome trace.
 Reports per-sweep latency, per-device probe latency and the verdicts; every
 accessible device must stay Healthy for the whole run.
 
-  python tools/health_sweep_gpu.py --sweeps 20 --out gpurun_out/health_sweep.json --trace t.json
+  python tools/experiments/health_sweep_gpu.py --sweeps 20 --out gpurun_out/health_sweep.json --trace t.json
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ import sys
 import tempfile
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig, HealthMonitor  # noqa: E402
 from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl  # noqa: E402

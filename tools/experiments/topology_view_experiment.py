@@ -11,7 +11,7 @@ import sys
 import tempfile
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rocm_k8s_device_plugin_amd.ops.native import probe_executable  # noqa: E402
 from rocm_k8s_device_plugin_amd.topology import discover, hip_ordinals  # noqa: E402
 from rocm_k8s_device_plugin_amd.topology_view import KFD_TOPOLOGY_CONTAINER_PATH, build_view  # noqa: E402

@@ -3,13 +3,13 @@
 the MI355X_INITPROF_REDIRECT specs that make native/tools/rocr_initprof.cpp
 see them where the container would (in-process stand-in for the bind mounts).
 
-  python tools/view_emulation.py OUTDIR   -> JSON {"node": spec, "topology": spec, "both": spec, ...}
+  python tools/experiments/view_emulation.py OUTDIR   -> JSON {"node": spec, "topology": spec, "both": spec, ...}
 """
 import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from rocm_k8s_device_plugin_amd.node_view import build_node_view  # noqa: E402
 from rocm_k8s_device_plugin_amd.topology_view import build_view  # noqa: E402
