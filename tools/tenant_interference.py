@@ -17,6 +17,7 @@ GEMMs slower than 1.5x the median ("stalls"), throughput, and the sweep
 latency.
 
   python tools/tenant_interference.py --seconds 6 --pulse 0.05 --out gpurun_out/tenant_interference.json
+  python tools/tenant_interference.py --procs 8 --streams 4 --modes none,keep,none   # multi-process tenants
 """
 from __future__ import annotations
 
@@ -34,29 +35,62 @@ sys.path.insert(0, REPO)
 
 TENANT = r"""
 import json, sys, time, torch
-n, seconds = int(sys.argv[1]), float(sys.argv[2])
-a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
-b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
-c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
-for _ in range(20):
-    torch.matmul(a, b, out=c)
+n, seconds, nstreams = int(sys.argv[1]), float(sys.argv[2]), int(sys.argv[3])
+# one GEMM chain per stream (HIP maps streams onto up to GPU_MAX_HW_QUEUES kfd queues)
+streams = [torch.cuda.Stream() for _ in range(nstreams)] if nstreams > 1 else [torch.cuda.current_stream()]
+bufs = [(torch.randn(n, n, device="cuda", dtype=torch.bfloat16), torch.randn(n, n, device="cuda", dtype=torch.bfloat16),
+         torch.empty(n, n, device="cuda", dtype=torch.bfloat16)) for _ in streams]
+for s, (a, b, c) in zip(streams, bufs):
+    with torch.cuda.stream(s):
+        for _ in range(10):
+            torch.matmul(a, b, out=c)
 torch.cuda.synchronize()
 print("READY", flush=True)
 sys.stdin.readline()                      # go
 evs, t_end = [], time.perf_counter() + seconds
-while time.perf_counter() < t_end:        # batches of 50 GEMMs, each bracketed by events
-    batch = [torch.cuda.Event(enable_timing=True) for _ in range(51)]
-    batch[0].record()
-    for i in range(50):
-        torch.matmul(a, b, out=c)
-        batch[i + 1].record()
-    evs.append(batch)
+while time.perf_counter() < t_end:        # batches of 50 GEMMs per stream, each bracketed by events
+    round_ = []
+    for s, (a, b, c) in zip(streams, bufs):
+        with torch.cuda.stream(s):
+            batch = [torch.cuda.Event(enable_timing=True) for _ in range(51)]
+            batch[0].record()
+            for i in range(50):
+                torch.matmul(a, b, out=c)
+                batch[i + 1].record()
+        round_.append(batch)
+    evs.append(round_)
     if len(evs) > 2:
-        evs[-3][-1].synchronize()        # keep at most ~2 batches queued ahead
+        for batch in evs[-3]:
+            batch[-1].synchronize()       # keep at most ~2 rounds queued ahead
 torch.cuda.synchronize()
-ms = [batch[i].elapsed_time(batch[i + 1]) for batch in evs for i in range(50)]
+ms = [batch[i].elapsed_time(batch[i + 1]) for round_ in evs for batch in round_ for i in range(50)]
 print(json.dumps({"n": n, "gemms": len(ms), "ms": ms}), flush=True)
 """
+
+
+def kfd_queue_count(gpu_id: int) -> int:
+    """User queues on the GPU, every process (kfd proc entries)."""
+    root, n = "/sys/class/kfd/kfd/proc", 0
+    try:
+        for pid in os.listdir(root):
+            qd = os.path.join(root, pid, "queues")
+            try:
+                for q in os.listdir(qd):
+                    with open(os.path.join(qd, q, "gpuid")) as f:
+                        n += int(f.read().strip() or 0) == gpu_id
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return -1
+    return n
+
+
+def gpu0_kfd_id() -> int:
+    from rocm_k8s_device_plugin_amd.topology import discover, hip_ordinals
+    inv = discover("/sys")
+    ords = hip_ordinals(inv, "/dev")
+    dev = min(ords, key=ords.get)
+    return inv.topology.node(inv.by_id[dev].node_id).gpu_id
 
 
 def stats(ms, n):
@@ -77,10 +111,14 @@ async def run_mode(mode: str, a) -> dict:
         prober = LivenessProber(timeout_s=a.probe_timeout, mode="persistent", keep_queues=(mode == "keep"))
         res = await prober.probe({"gpu0": 0})          # server up before the tenant starts timing
         assert all(r.ok for r in res.values()), res
-    tenant = subprocess.Popen([sys.executable, "-c", TENANT, str(a.n), str(a.seconds)], stdin=subprocess.PIPE,
-                              stdout=subprocess.PIPE, text=True, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
-    line = await asyncio.to_thread(tenant.stdout.readline)
-    assert line.strip() == "READY", line
+    tenants = [subprocess.Popen([sys.executable, "-c", TENANT, str(a.n), str(a.seconds), str(a.streams)],
+                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                                env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+               for _ in range(a.procs)]
+    for tenant in tenants:
+        line = await asyncio.to_thread(tenant.stdout.readline)
+        assert line.strip() == "READY", line
+    queues = kfd_queue_count(a.gpu_id) if a.gpu_id else -1
     stop = asyncio.Event()
     sweep_ms = []
     counts = {"ok": 0, "ok_late": 0, "pending": 0, "failed": 0}
@@ -101,10 +139,11 @@ async def run_mode(mode: str, a) -> dict:
             except asyncio.TimeoutError:
                 pass
 
-    tenant.stdin.write("go\n")
-    tenant.stdin.flush()
+    for tenant in tenants:
+        tenant.stdin.write("go\n")
+        tenant.stdin.flush()
     task = asyncio.create_task(health_loop()) if prober else None
-    out = await asyncio.to_thread(tenant.stdout.readline)
+    outs = [await asyncio.to_thread(tenant.stdout.readline) for tenant in tenants]
     if prober is not None and prober._server is not None:
         try:
             with open(f"/proc/{prober._server.proc.pid}/status") as f:
@@ -115,10 +154,14 @@ async def run_mode(mode: str, a) -> dict:
     if task:
         await task
         await prober.close()
-    rc = await asyncio.to_thread(tenant.wait)
-    assert rc == 0, rc
-    doc = json.loads(out)
-    r = {"mode": mode, "pulse_s": a.pulse if prober else None, "gemm_n": a.n, **stats(doc["ms"], a.n),
+    for tenant in tenants:
+        rc = await asyncio.to_thread(tenant.wait)
+        assert rc == 0, rc
+    docs = [json.loads(out) for out in outs]
+    ms = [x for doc in docs for x in doc["ms"]]
+    r = {"mode": mode, "pulse_s": a.pulse if prober else None, "gemm_n": a.n, "tenant_procs": a.procs,
+         "streams_per_proc": a.streams, "kfd_queues_on_gpu": queues, **stats(ms, a.n),
+         "per_proc_gemms": [doc["gemms"] for doc in docs],
          "health_sweeps": len(sweep_ms),
          "health_sweep_ms_p50": round(statistics.median(sweep_ms), 3) if sweep_ms else None,
          # the probe's wait behind the tenant's kernels (long GEMMs: --n 32768 / 65536)
@@ -139,8 +182,14 @@ def main():
     ap.add_argument("--modes", default="none,per_sweep,keep,none")
     ap.add_argument("--probe-timeout", type=float, default=30.0,
                     help="liveness deadline; below the tenant's kernel time probes come back pending")
+    ap.add_argument("--procs", type=int, default=1, help="tenant processes on GPU 0")
+    ap.add_argument("--streams", type=int, default=1, help="GEMM streams (HIP queues) per tenant process")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
+    try:
+        a.gpu_id = gpu0_kfd_id()
+    except Exception:
+        a.gpu_id = 0
 
     async def go():
         return [await run_mode(m, a) for m in a.modes.split(",")]
