@@ -62,6 +62,9 @@ def build_parser() -> flags.GoFlagParser:
                                               "a busy GPU is inconclusive)")
     p.add_bool("liveness_corroborate", True, "a probe pending on a busy GPU stays inconclusive only while amd-smi "
                                              "reports GFX activity; 0% on 2 consecutive sweeps ends the busy grace")
+    p.add_int("liveness_crowded_procs", 7, "with this many other processes holding queues on a GPU (or too few "
+                                           "free kfd queues) the probe server steps off it, so it adds no process or "
+                                           "queue to an oversubscribed HWS runlist; 0 = off")
     p.add_float("liveness_unknown_busy_grace", 30.0, "the busy grace while busy GPUs cannot be told from idle ones "
                                                      "(kfd process list unreadable): every GPU counts as busy, "
                                                      "so the grace is shorter")
@@ -142,7 +145,8 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
                           liveness_keep_queues=ns.liveness_keep_queues,
                           liveness_busy_grace_s=ns.liveness_busy_grace,
                           liveness_unknown_busy_grace_s=ns.liveness_unknown_busy_grace,
-                          liveness_corroborate=ns.liveness_corroborate)
+                          liveness_corroborate=ns.liveness_corroborate,
+                          liveness_crowded_procs=ns.liveness_crowded_procs)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         from .. import cdi

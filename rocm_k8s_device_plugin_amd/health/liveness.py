@@ -145,10 +145,20 @@ class LivenessProber:
         self._server: Optional[_ProbeServer] = None
         self._server_backoff = 0  # sweeps to run in spawn mode after a server failure
         self._pending_nonce: Dict[int, int] = {}   # ordinal -> nonce of the server's outstanding dispatch
+        # host ordinals the server may touch (None = every GPU). A GPU left out
+        # gets no queue, no ROCr state and no runlist slot from the server.
+        self._visible: Optional[tuple] = None
+        self._server_visible: Optional[tuple] = None
 
     @property
     def server_running(self) -> bool:
         return self._server is not None and self._server.alive
+
+    def set_visible(self, ordinals: Optional[Collection[int]]) -> None:
+        """Restrict the persistent server to these host ordinals (None = all).
+        A change restarts the server on its next request (rare: the health
+        monitor changes it when a GPU gets or stops being crowded)."""
+        self._visible = None if ordinals is None else tuple(sorted(set(int(o) for o in ordinals)))
 
     def _kfd_entries(self) -> set:
         try:
@@ -261,19 +271,35 @@ class LivenessProber:
     # ------------------------------------------------------------ persistent
     async def _probe_server(self, uniq, kind: str = "probe") -> Dict[int, ProbeOutcome]:
         t0 = time.perf_counter()
+        visible = self._visible
+        if visible is not None and not set(uniq) <= set(visible):
+            visible = tuple(sorted(set(visible) | set(uniq)))
+        if self._server is not None and self._server.alive and visible != self._server_visible:
+            await self.close()          # the GPUs the server may touch changed
         if self._server is None or not self._server.alive:
             argv = [*self.argv_prefix, self._exe(), "--serve", *(["--keep"] if self.keep_queues else [])]
+            env = self._env(None)
+            if visible is not None:
+                env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in visible)
             before = self._kfd_entries()
-            self._server = await _ProbeServer.start(argv, self._env(None), self.timeout_s)
+            self._server = await _ProbeServer.start(argv, env, self.timeout_s)
+            self._server_visible = visible
             self._own_kfd = frozenset(self._kfd_entries() - before)
             self.server_starts += 1
+        # the server numbers the GPUs it sees; with a visibility list those are its positions
+        local = {o: (self._server_visible.index(o) if self._server_visible is not None else o) for o in uniq}
+        host = {v: k for k, v in local.items()}
         nonces = {o: self._nonce(o) for o in uniq}
         # the server's own dispatch wait ends before our deadline for the reply
         inner = self.timeout_s - min(0.5, 0.25 * self.timeout_s)
-        line = f"{kind} {self.iters} {inner:.2f} " + " ".join(f"{o}:{nonces[o]}" for o in uniq)
+        line = f"{kind} {self.iters} {inner:.2f} " + " ".join(f"{local[o]}:{nonces[o]}" for o in uniq)
         doc = await self._server.request(line, self.timeout_s)
         dt = (time.perf_counter() - t0) * 1e3
-        by_ord = {d.get("ordinal"): d for d in doc.get("devices") or []}
+        by_ord = {}
+        for d in doc.get("devices") or []:
+            if d.get("ordinal") in host:
+                d = dict(d, ordinal=host[d.get("ordinal")])
+                by_ord[d["ordinal"]] = d
         out = {}
         for o in uniq:
             d = by_ord.get(o)
@@ -303,6 +329,7 @@ class LivenessProber:
         if self._server is not None:
             await self._server.kill()
             self._server = None
+            self._server_visible = None
 
     async def sweep(self, ordinals: Mapping[str, int]) -> Dict[str, ProbeOutcome]:
         """The full-chip sweep (every CU of every XCD) instead of the one-wave probe.

@@ -37,7 +37,7 @@ from typing import Callable, Dict, Mapping, Optional, Tuple
 
 from ..ops.native import core
 from ..proto import deviceplugin as dp
-from ..topology import Inventory, KfdBusyUnknown, hip_ordinals, kfd_busy_gpu_ids
+from ..topology import Inventory, KfdBusyUnknown, hip_ordinals, kfd_busy_gpu_ids, kfd_gpu_load
 from ..utils import log
 from ..utils.trace import TRACER
 from . import exporter
@@ -80,6 +80,16 @@ class HealthConfig:
     # consecutive sweeps ends the grace (a wedged queue, not a long kernel)
     liveness_corroborate: bool = True
     liveness_idle_sweeps: int = 2
+    # crowded GPUs: with this many other processes holding queues on a GPU
+    # (or their queues leaving fewer than 2 of the GPU's kfd num_cp_queues)
+    # the HWS runlist is oversubscribed and every extra process/queue lengthens
+    # the tenants' time slices (measured: 8 tenant processes x 4 queues, p99.9
+    # GEMM 14 -> 34 ms with the kept probe queue, profiles/README.md §3n). The
+    # probe server then steps off that GPU (no queue, no runlist slot); while
+    # the GPU reports GFX activity its tenants are the liveness evidence, at 0%
+    # it is probed from a fresh process. 0 = off.
+    liveness_crowded_procs: int = 7
+    liveness_crowded_release_sweeps: int = 5   # uncrowded sweeps before the server takes the GPU back
     recover_threshold: int = 1
     smi_ecc: bool = False
     smi_events: bool = False
@@ -131,6 +141,9 @@ class HealthMonitor:
         self.busy_state_known = True   # last sweep could tell busy GPUs from idle ones
         self.identity_remaps = 0       # sweeps whose probe replies did not match the positional ordinals
         self._activity_source = activity_source   # bdf -> GFX activity % (amd-smi by default)
+        self._load: Dict[int, Tuple[int, int]] = {}  # kfd gpu_id -> (other processes, their queues)
+        self._crowded: Dict[str, int] = {}          # device -> uncrowded sweeps seen since it got crowded
+        self.crowded_skips = 0
 
     # ------------------------------------------------------------------ fabric
     def degraded_links(self):
@@ -276,8 +289,10 @@ class HealthMonitor:
         unresolved = not own and self.prober is not None and self.prober.server_running and \
             self.prober.keep_queues
         try:
-            busy = kfd_busy_gpu_ids(self.inv.sysfs_root, exclude=own)
+            self._load = kfd_gpu_load(self.inv.sysfs_root, exclude=own)
+            busy = set(self._load)
         except KfdBusyUnknown as e:
+            self._load = {}
             self._set_busy_known(False, str(e))
             return set(dev_ids)
         # the server's own kept queues could not be told apart from a tenant's
@@ -393,11 +408,40 @@ class HealthMonitor:
         lost = sorted(set(ords) - set(new_ords))
         if lost:
             _log.error("probe identity: no probed agent matches %s; they lose their ordinal", lost)
-        self._ordinals = new_ords
+        keep = {k: v for k, v in (self._ordinals or {}).items() if k not in ords}
+        self._ordinals = {**keep, **new_ords}
         self.identity_remaps += 1
         REGISTRY.inc("mi355x_dp_probe_identity_mismatch_total",
                      help="sweeps whose probe replies came from other devices than the positional ordinal map")
         return fixed
+
+    def _update_crowded(self, dev_ids) -> set:
+        """Devices whose GPU is crowded now or was within the release window."""
+        lim = self.cfg.liveness_crowded_procs
+        if lim <= 0:
+            self._crowded.clear()
+            return set()
+        out = set()
+        for dev_id in dev_ids:
+            d = self.inv.by_id.get(dev_id)
+            node = self.inv.topology.node(d.node_id) if d is not None and d.node_id >= 0 else None
+            gid = self._gpu_id(dev_id)
+            procs, queues = self._load.get(gid, (0, 0))
+            cp = int(node.prop("num_cp_queues", 0)) if node is not None else 0
+            crowded = procs >= lim or (cp > 0 and queues + 2 > cp)
+            if crowded:
+                if dev_id not in self._crowded:
+                    _log.info("GPU of %s is crowded (%d other processes, %d queues): the probe server steps off it",
+                              dev_id, procs, queues)
+                self._crowded[dev_id] = 0
+            elif dev_id in self._crowded:
+                self._crowded[dev_id] += 1
+                if self._crowded[dev_id] >= self.cfg.liveness_crowded_release_sweeps:
+                    del self._crowded[dev_id]
+                    _log.info("GPU of %s is no longer crowded: probing it again", dev_id)
+            if dev_id in self._crowded:
+                out.add(dev_id)
+        return out
 
     async def _liveness(self, ords: Dict[str, int], busy_devs=frozenset()):
         every = self.cfg.chip_sweep_every
@@ -448,7 +492,26 @@ class HealthMonitor:
         if self.cfg.liveness and self.prober is not None:
             ords = {k: v for k, v in self.ordinals().items() if k in reasons}
             busy_devs = self._busy_devices(ords)
-            outcomes = self._verify_identity(ords, await self._liveness(ords, busy_devs))
+            crowded = self._update_crowded(ords)
+            probe_ords = {k: v for k, v in ords.items() if k not in crowded}
+            if hasattr(self.prober, "set_visible"):
+                self.prober.set_visible(sorted(set(probe_ords.values())) if crowded else None)
+            if not probe_ords and crowded and getattr(self.prober, "server_running", False):
+                await self.prober.close()       # every GPU crowded: hold nothing on any of them
+            outcomes = self._verify_identity(probe_ords, await self._liveness(probe_ords, busy_devs)) \
+                if probe_ords else {}
+            if crowded:
+                act = await asyncio.to_thread(self._gfx_activity)
+                from ..utils.metrics import REGISTRY
+                for dev_id in sorted(crowded):
+                    d = self.inv.by_id.get(dev_id)
+                    if d is not None and act.get(d.bdf, -1) == 0:
+                        # crowded but idle: nothing to disturb, probe it from a fresh process
+                        outcomes[dev_id] = await self.prober.probe_ordinal(ords[dev_id])
+                    else:
+                        self.crowded_skips += 1
+                        REGISTRY.inc("mi355x_dp_liveness_crowded_skips_total",
+                                     help="probes skipped on GPUs crowded with tenant processes", device=dev_id)
             ords = {k: v for k, v in self.ordinals().items() if k in reasons}
             from ..utils.metrics import REGISTRY
             now = time.monotonic()

@@ -71,6 +71,12 @@ def serve():
     print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "t_start_ns": t, "t_runtime_ns": t}),
           flush=True)
     slots = {}   # ordinal -> nonce of the kept slot's outstanding dispatch (like --keep)
+    # like ROCr: with ROCR_VISIBLE_DEVICES the server numbers only those GPUs
+    vis = [x for x in os.environ.get("ROCR_VISIBLE_DEVICES", "").split(",") if x]
+    starts_log = os.environ.get("MI355X_STUB_PROBE_LOG")
+    if starts_log and vis:
+        with open(starts_log, "a") as f:
+            f.write("visible=" + ",".join(vis) + "\n")
     for line in sys.stdin:
         parts = line.split()
         if not parts or parts[0] == "quit":
@@ -80,7 +86,8 @@ def serve():
         devs = []
         for tok in parts[3:]:
             o, n = tok.split(":")
-            mode = ctl.get(o, "ok")
+            hosto = vis[int(o)] if vis and int(o) < len(vis) else o
+            mode = ctl.get(hosto, "ok")
             if mode == "server_fail":
                 mode = "fail"
             if mode == "hang":
@@ -89,22 +96,22 @@ def serve():
                 print("segfault-ish noise", flush=True)
                 return 139
             if mode == "timeout":   # server without kept queues: the dispatch did not complete
-                d = _device(int(o), "fail", int(n, 0))
+                d = _device(int(o), "fail", int(n, 0), host_ordinal=int(hosto))
                 d.update(hip_error=-1, mismatches=0, error="dispatch did not complete within 1.0s")
                 devs.append(d)
                 continue
             if mode == "pending" and kind != "sweep":   # kept-queue server: dispatch still queued behind other work
                 slots.setdefault(o, int(n, 0))
-                d = _device(int(o), "fail", int(n, 0))
+                d = _device(int(o), "fail", int(n, 0), host_ordinal=int(hosto))
                 d.update(hip_error=-1, mismatches=0, pending_s=1.0, error="dispatch pending for 1.0s (not completed)")
                 devs.append(d)
                 continue
             if kind != "sweep" and o in slots:   # the outstanding dispatch completed: its late verdict
-                d = _device(int(o), mode, slots.pop(o))
+                d = _device(int(o), mode, slots.pop(o), host_ordinal=int(hosto))
                 d["late"] = 1
                 devs.append(d)
                 continue
-            devs.append(_device(int(o), "ok" if mode == "pending" else mode, int(n, 0)))
+            devs.append(_device(int(o), "ok" if mode == "pending" else mode, int(n, 0), host_ordinal=int(hosto)))
         print(json.dumps({"ok": all(d["ok"] for d in devs), "hip_device_count": 8, "sweep": kind == "sweep",
                           "t_ready_ns": time.monotonic_ns(), "devices": devs}), flush=True)
     return 0

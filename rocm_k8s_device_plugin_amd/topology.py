@@ -209,19 +209,18 @@ class KfdBusyUnknown(Exception):
     are busy is unknown, so callers must treat every GPU as busy."""
 
 
-def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
-    """kfd gpu_ids that currently have user queues, from any process on the host
-    (``/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/gpuid``) except the ``exclude``d
-    entries (the plugin's own probe server). A GPU without queues runs no work;
-    the liveness loop runs its full-chip sweep only on those. Raises
+def kfd_gpu_load(sysfs_root: str = "/sys", exclude=()) -> Dict[int, Tuple[int, int]]:
+    """kfd gpu_id -> (processes with user queues on it, user queues on it),
+    from every process on the host (``/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/gpuid``)
+    except the ``exclude``d entries (the plugin's own probe server). Raises
     KfdBusyUnknown when a process' queues are unreadable (not when it merely
     exited meanwhile)."""
-    busy = set()
+    load: Dict[int, List[int]] = {}
     root = os.path.join(sysfs_root, "class/kfd/kfd/proc")
     try:
         pids = os.listdir(root)
     except FileNotFoundError:
-        return busy             # no kfd process list at all: no process has queues
+        return {}               # no kfd process list at all: no process has queues
     except OSError as e:
         # the list itself is unreadable: every GPU may be running work
         raise KfdBusyUnknown(f"{root}: {e}") from e
@@ -236,12 +235,26 @@ def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
             raise KfdBusyUnknown(f"{qdir}: {e}") from e
         except OSError:
             continue            # the process exited meanwhile
+        mine: Dict[int, int] = {}
         for q in qids:
             try:
                 with open(os.path.join(qdir, q, "gpuid")) as f:
-                    busy.add(int(f.read().strip() or 0))
+                    g = int(f.read().strip() or 0)
             except PermissionError as e:
                 raise KfdBusyUnknown(f"{qdir}/{q}: {e}") from e
             except (OSError, ValueError):
                 continue
-    return busy
+            mine[g] = mine.get(g, 0) + 1
+        for g, nq in mine.items():
+            cur = load.setdefault(g, [0, 0])
+            cur[0] += 1
+            cur[1] += nq
+    return {g: (v[0], v[1]) for g, v in load.items()}
+
+
+def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
+    """kfd gpu_ids that currently have user queues, from any process on the host
+    except the ``exclude``d entries (the plugin's own probe server). A GPU
+    without queues runs no work; the liveness loop runs its full-chip sweep
+    only on those. Raises KfdBusyUnknown (see kfd_gpu_load)."""
+    return set(kfd_gpu_load(sysfs_root, exclude))

@@ -1149,3 +1149,52 @@ def test_busy_grace_needs_gfx_activity(tmp_path, activity, unhealthy):
     if unhealthy:
         assert any("0% GFX activity" in r for r in mon.snapshot()[dev.id].reasons)
     assert all(mon.health(d.id) == "Healthy" for d in inv.devices if d.id != dev.id)
+
+
+def test_crowded_gpu_gets_no_probe_server_queue(tmp_path):
+    """7 other processes with queues on one GPU (an oversubscribed HWS
+    runlist): the probe server is restarted without that GPU (ROCr never opens
+    it: no queue, no runlist slot) and its probe is skipped while the GPU is
+    computing; at 0% GFX activity it is probed from a fresh process instead.
+    Uncrowded again, the GPU returns to the server after the release window."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    dev = inv.devices[3]
+    for pid in range(800, 807):
+        _busy_gpu(fi, inv, dev.id, pid=str(pid))
+    log_path = tmp_path / "starts.log"
+    ctl, prober = _stub_prober(tmp_path, {"3": "fail"})
+    prober.extra_env["MI355X_STUB_PROBE_LOG"] = str(log_path)
+    prober.kfd_proc_dir = str(fi.sysfs / "class/kfd/kfd/proc")
+    activity = {"v": 60}
+    mon = HealthMonitor(inv, HealthConfig(exporter_socket=None, liveness=True, fail_threshold=2,
+                                          liveness_crowded_release_sweeps=2), prober=prober,
+                        ordinal_map={d.id: i for i, d in enumerate(inv.devices)},
+                        activity_source=lambda: {d.bdf: (activity["v"] if d.id == dev.id else 40)
+                                                 for d in inv.devices})
+
+    async def go():
+        try:
+            for _ in range(3):
+                await mon.check_once()
+            assert mon.health(dev.id) == "Healthy" and mon.crowded_skips == 3
+            assert prober._server_visible == (0, 1, 2, 4, 5, 6, 7)
+            activity["v"] = 0                     # crowded but idle: a fresh process probes it
+            for _ in range(2):
+                await mon.check_once()
+            assert mon.health(dev.id) == "Unhealthy"
+            ctl.write_text("{}")
+            import shutil
+            for pid in range(800, 807):
+                shutil.rmtree(fi.sysfs / "class/kfd/kfd/proc" / str(pid))
+            for _ in range(4):
+                await mon.check_once()
+            assert prober._server_visible is None and mon.health(dev.id) == "Healthy"
+        finally:
+            await mon.close()
+
+    run(go(), timeout=120)
+    log = log_path.read_text().split()
+    assert "visible=0,1,2,4,5,6,7" in log
+    assert log.count("3") >= 2                   # the fresh-process probes of the idle crowded GPU
+    assert all(mon.health(d.id) == "Healthy" for d in inv.devices if d.id != dev.id)

@@ -107,7 +107,23 @@ def stats(ms, n):
 async def run_mode(mode: str, a) -> dict:
     from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
     prober = None
-    if mode != "none":
+    monitor = None
+    if mode == "monitor":
+        # the health monitor as the plugin runs it: kept queues, busy grace,
+        # GFX-activity corroboration and the crowded-GPU step-off
+        from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig, HealthMonitor
+        from rocm_k8s_device_plugin_amd.topology import Inventory, discover, hip_ordinals
+        inv = discover("/sys")
+        ords = hip_ordinals(inv, "/dev")
+        dev = min(ords, key=ords.get)
+        acc = Inventory(sysfs_root="/sys", devices=(inv.by_id[dev],), topology=inv.topology, driver_loaded=True,
+                        kfd_present=True)
+        monitor = HealthMonitor(acc, HealthConfig(exporter_socket=None, liveness=True,
+                                                  liveness_timeout_s=a.probe_timeout),
+                                ordinal_map={dev: ords[dev]})
+        await monitor.check_once()
+        prober = monitor.prober
+    elif mode != "none":
         prober = LivenessProber(timeout_s=a.probe_timeout, mode="persistent", keep_queues=(mode == "keep"))
         res = await prober.probe({"gpu0": 0})          # server up before the tenant starts timing
         assert all(r.ok for r in res.values()), res
@@ -127,6 +143,17 @@ async def run_mode(mode: str, a) -> dict:
     async def health_loop():
         while not stop.is_set():
             t0 = time.perf_counter()
+            if monitor is not None:
+                skips = monitor.crowded_skips
+                await monitor.check_once()
+                counts["crowded_skip" if monitor.crowded_skips > skips else "swept"] = \
+                    counts.get("crowded_skip" if monitor.crowded_skips > skips else "swept", 0) + 1
+                sweep_ms.append((time.perf_counter() - t0) * 1e3)
+                try:
+                    await asyncio.wait_for(stop.wait(), a.pulse)
+                except asyncio.TimeoutError:
+                    pass
+                continue
             # the tenant's queue makes GPU 0 busy: a probe queued behind a long
             # kernel comes back pending and is answered late by the next sweep
             res = await prober.probe({"gpu0": 0}, busy={0})
@@ -144,6 +171,7 @@ async def run_mode(mode: str, a) -> dict:
         tenant.stdin.flush()
     task = asyncio.create_task(health_loop()) if prober else None
     outs = [await asyncio.to_thread(tenant.stdout.readline) for tenant in tenants]
+    server_alive_end = bool(prober is not None and prober._server is not None and prober._server.alive)
     if prober is not None and prober._server is not None:
         try:
             with open(f"/proc/{prober._server.proc.pid}/status") as f:
@@ -153,7 +181,10 @@ async def run_mode(mode: str, a) -> dict:
     stop.set()
     if task:
         await task
-        await prober.close()
+        if monitor is not None:
+            await monitor.close()
+        else:
+            await prober.close()
     for tenant in tenants:
         rc = await asyncio.to_thread(tenant.wait)
         assert rc == 0, rc
@@ -169,7 +200,9 @@ async def run_mode(mode: str, a) -> dict:
          "health_sweep_ms_max": round(max(sweep_ms), 3) if sweep_ms else None,
          "probe_timeout_s": a.probe_timeout if prober else None, "probe_outcomes": counts if prober else None,
          "probe_server_rss_mb_end": round(rss_kb[0] / 1024, 1) if rss_kb else None,
-         "probe_server_starts": prober.server_starts if prober else None}
+         "probe_server_starts": prober.server_starts if prober else None,
+         "probe_server_alive_at_end": server_alive_end if prober else None,
+         "health": (monitor.snapshot()[next(iter(monitor.snapshot()))].health if monitor is not None else None)}
     print(json.dumps(r), flush=True)
     return r
 
