@@ -509,3 +509,76 @@ def test_views_switched_at_run_time_reach_the_native_allocate(tmp_path):
     assert m1 and all(m.read_only for m in m1)
     assert fb_before == 0
     assert fb_after == 1 and any(m.container_path.endswith("topology") for m in a2.response.container_responses[0].mounts)
+
+
+def _raw_server(tmp_path, fallback=None):
+    srv = N.DevicePluginServer()
+    if fallback is not None:
+        srv.set_fallback(fallback)
+    sock = str(tmp_path / "r.sock")
+    assert srv.start(sock) == ""
+    return srv, sock
+
+
+def test_large_request_needs_server_window_updates(tmp_path):
+    """A request larger than the 64 KiB initial windows (and a header block
+    split into CONTINUATION frames) arrives intact."""
+    seen = {}
+
+    def fb(method, req):
+        r = pb.PreferredAllocationRequest.FromString(req)
+        seen["n"] = len(r.container_requests[0].available_deviceIDs)
+        return 0, "", pb.PreferredAllocationResponse().SerializeToString()
+
+    srv, sock = _raw_server(tmp_path, fb)
+    try:
+        ch = grpc.insecure_channel(f"unix:{sock}")
+        r = pb.PreferredAllocationRequest()
+        ids = [f"amdgpu_xcp_{i:06d}_" + "y" * 40 for i in range(5000)]
+        r.container_requests.add(available_deviceIDs=ids, allocation_size=3)
+        assert r.ByteSize() > 4 * 65535
+        pb.DevicePluginStub(ch).GetPreferredAllocation(r, timeout=10, metadata=[("x-big", "z" * 30000)])
+        assert seen["n"] == 5000
+        ch.close()
+    finally:
+        srv.stop(0.1)
+
+
+def test_client_keepalive_pings_on_a_long_stream(tmp_path):
+    """kubelet-style long-lived ListAndWatch with client keepalive PINGs every
+    100 ms: every PING is acknowledged and the stream stays open."""
+    srv, sock = _raw_server(tmp_path)
+    srv.set_device_list(pb.ListAndWatchResponse(devices=[pb.Device(ID="a", health=pb.HEALTHY)]).SerializeToString())
+    try:
+        ch = grpc.insecure_channel(f"unix:{sock}", options=[("grpc.keepalive_time_ms", 100),
+                                                            ("grpc.keepalive_timeout_ms", 1000),
+                                                            ("grpc.keepalive_permit_without_calls", 1),
+                                                            ("grpc.http2.max_pings_without_data", 0)])
+        it = pb.DevicePluginStub(ch).ListAndWatch(pb.Empty(), timeout=10)
+        assert next(it).devices[0].ID == "a"
+        time.sleep(1.0)                                  # ~10 keepalive PINGs
+        srv.publish_list(pb.ListAndWatchResponse(devices=[pb.Device(ID="b", health=pb.UNHEALTHY)])
+                         .SerializeToString())
+        assert next(it).devices[0].ID == "b"
+        assert srv.stats()["protocol_errors"] == 0
+        it.cancel()
+        ch.close()
+    finally:
+        srv.stop(0.1)
+
+
+def test_server_restart_on_the_same_socket_path(tmp_path):
+    """The plugin restarts its server on kubelet restarts: a new server binds the
+    same path (stale socket file replaced) and clients reconnect."""
+    srv, sock = _raw_server(tmp_path)
+    srv.set_options(pb.DevicePluginOptions(get_preferred_allocation_available=True).SerializeToString())
+    srv.stop(0.1)
+    srv2 = N.DevicePluginServer()
+    srv2.set_options(pb.DevicePluginOptions().SerializeToString())
+    assert srv2.start(sock) == ""
+    try:
+        ch = grpc.insecure_channel(f"unix:{sock}")
+        assert not pb.DevicePluginStub(ch).GetDevicePluginOptions(pb.Empty(), timeout=5).get_preferred_allocation_available
+        ch.close()
+    finally:
+        srv2.stop(0.1)
