@@ -4,6 +4,7 @@
 
 #include "mi355x/allocator.h"
 #include "mi355x/constants.h"
+#include "mi355x/dir_watch.h"
 #include "mi355x/drm_query.h"
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/kfd_topology.h"
@@ -402,5 +403,11 @@ PYBIND11_MODULE(_native, m) {
     out["gpus"] = gpus;
     return out;
   });
+  py::class_<DirWatcher>(m, "DirWatcher")
+      .def(py::init<>())
+      .def("open", &DirWatcher::open, py::arg("dir"))
+      .def("fileno", &DirWatcher::fd)
+      .def("read_events", &DirWatcher::read_events)
+      .def("close", &DirWatcher::close);
   bind_rpc(m);
 }

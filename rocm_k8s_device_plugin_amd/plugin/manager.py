@@ -285,33 +285,82 @@ class PluginManager:
         except FileNotFoundError:
             return None
 
+    def _open_dir_watch(self):
+        """inotify on the plugin directory (the reference's dpm uses fsnotify):
+        a kubelet restart is seen at once instead of at the next poll. None
+        when unavailable (the poll alone then notices changes)."""
+        try:
+            from ..ops.native import core
+            w = core().DirWatcher()
+        except Exception:
+            return None
+        err = w.open(os.path.dirname(self.kubelet_socket) or ".")
+        if err:
+            _log.info("no inotify watch of the kubelet directory (%s); polling every %.1fs", err,
+                      self.cfg.watch_interval_s)
+            return None
+        return w
+
     async def _watch_kubelet(self) -> None:
         last = self._sock_id()
         next_retry = 0.0
-        while not self.stopped.is_set():
-            try:
-                await asyncio.wait_for(self.stopped.wait(), self.cfg.watch_interval_s)
-                return
-            except asyncio.TimeoutError:
-                pass
-            cur = self._sock_id()
-            if cur == last:
-                # kubelet is up but a plugin never got registered (e.g. the socket
-                # appeared before kubelet was serving): keep retrying, rate-limited
-                now = time.monotonic()
-                pending = [p for p in self.plugins.values() if p.started and not p.running]
-                if cur is not None and pending and now >= next_retry:
-                    next_retry = now + max(self.cfg.retry_wait_s, self.cfg.watch_interval_s)
-                    await asyncio.gather(*(p.start_server() for p in pending))
-                continue
-            if cur is None:
-                _log.info("kubelet socket removed; stopping plugin servers")
-                await self._stop_servers()
-            else:
-                _log.info("kubelet socket (re)created; restarting plugin servers and re-registering")
-                await self._stop_servers()
-                await self._start_all()
-            last = cur
+        loop = asyncio.get_running_loop()
+        watch = self._open_dir_watch()
+        kick = asyncio.Event()
+        if watch is not None:
+            sock_name = os.path.basename(self.kubelet_socket)
+
+            def on_events():
+                # only kubelet.sock (or the directory itself) matters: the
+                # plugins' own sockets live in the same directory
+                if any(name in (sock_name, "") for name, _ in watch.read_events()):
+                    kick.set()
+
+            loop.add_reader(watch.fileno(), on_events)
+        try:
+            await self._watch_kubelet_loop(last, next_retry, kick, watch)
+        finally:
+            if watch is not None:
+                loop.remove_reader(watch.fileno())
+                watch.close()
+
+    async def _watch_kubelet_loop(self, last, next_retry, kick, watch) -> None:
+        stop_wait = asyncio.ensure_future(self.stopped.wait())
+        try:
+            while not self.stopped.is_set():
+                kick_wait = asyncio.ensure_future(kick.wait())
+                # with inotify the poll is only a safety net (e.g. the directory was replaced)
+                timeout = self.cfg.watch_interval_s if watch is None else max(self.cfg.watch_interval_s, 5.0)
+                await asyncio.wait({stop_wait, kick_wait}, timeout=timeout, return_when=asyncio.FIRST_COMPLETED)
+                kick_wait.cancel()
+                kick.clear()
+                if self.stopped.is_set():
+                    return
+                last, next_retry = await self._kubelet_check(last, next_retry)
+        finally:
+            stop_wait.cancel()
+
+    async def _kubelet_check(self, last, next_retry):
+        """One look at kubelet.sock: (re)start / stop servers on a change, retry
+        pending registrations (rate-limited). Returns the new (last, next_retry)."""
+        cur = self._sock_id()
+        if cur == last:
+            # kubelet is up but a plugin never got registered (e.g. the socket
+            # appeared before kubelet was serving): keep retrying, rate-limited
+            now = time.monotonic()
+            pending = [p for p in self.plugins.values() if p.started and not p.running]
+            if cur is not None and pending and now >= next_retry:
+                next_retry = now + max(self.cfg.retry_wait_s, self.cfg.watch_interval_s)
+                await asyncio.gather(*(p.start_server() for p in pending))
+            return last, next_retry
+        if cur is None:
+            _log.info("kubelet socket removed; stopping plugin servers")
+            await self._stop_servers()
+        else:
+            _log.info("kubelet socket (re)created; restarting plugin servers and re-registering")
+            await self._stop_servers()
+            await self._start_all()
+        return cur, next_retry
 
     async def run(self) -> None:
         loop = asyncio.get_running_loop()

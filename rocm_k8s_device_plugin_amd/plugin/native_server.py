@@ -103,7 +103,15 @@ class NativePluginServer:
     # ------------------------------------------------------------ events
     def drain(self) -> None:
         """Logs, metrics and trace spans of the calls served since the last drain."""
-        for ev in self.srv.drain_events():
+        evs = self.srv.drain_events()
+        if evs:
+            st = self.srv.stats()
+            for k in ("connections", "calls", "protocol_errors"):
+                REGISTRY.set(f"mi355x_dp_grpc_{k}", float(st[k]), help=f"native gRPC server: {k.replace('_', ' ')}",
+                             resource=self.ctx.resource)
+            REGISTRY.set("mi355x_dp_listandwatch_open_streams", float(self.srv.open_streams()),
+                         help="ListAndWatch streams open on the native server", resource=self.ctx.resource)
+        for ev in evs:
             rpc, ms = ev["rpc"], ev["dur_ns"] / 1e6
             self.calls += 1
             q = self.recent_ms.setdefault(rpc, collections.deque(maxlen=4096))

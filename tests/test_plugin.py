@@ -41,8 +41,8 @@ async def plugin_env(tmp_path, impl, pulse=0.0, start_kubelet=True, **mcfg):
     k = FakeKubelet(pdir)
     if start_kubelet:
         await k.start()
-    cfg = ManagerConfig(pulse_s=pulse, plugin_dir=pdir, handle_signals=False, retry_wait_s=0.05,
-                        watch_interval_s=0.05, **mcfg)
+    cfg = ManagerConfig(**{"pulse_s": pulse, "plugin_dir": pdir, "handle_signals": False, "retry_wait_s": 0.05,
+                           "watch_interval_s": 0.05, **mcfg})
     mgr = PluginManager(impl, cfg)
     task = asyncio.create_task(mgr.run())
     try:
@@ -1198,3 +1198,23 @@ def test_crowded_gpu_gets_no_probe_server_queue(tmp_path):
     assert "visible=0,1,2,4,5,6,7" in log
     assert log.count("3") >= 2                   # the fresh-process probes of the idle crowded GPU
     assert all(mon.health(d.id) == "Healthy" for d in inv.devices if d.id != dev.id)
+
+
+def test_kubelet_restart_seen_by_inotify_not_the_poll(tmp_path):
+    """With a 30 s poll interval, a kubelet restart still re-registers within
+    a second: the manager waits on an inotify watch of the plugin directory
+    (the reference's dpm uses fsnotify)."""
+    import time as _t
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = container(fi)
+
+    async def go():
+        async with plugin_env(tmp_path, impl, watch_interval_s=30.0) as (k, mgr):
+            await k.wait_for_resource("amd.com/gpu", 8)
+            t0 = _t.monotonic()
+            await k.restart()
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=10)
+            return _t.monotonic() - t0, len(k.registrations)
+
+    dt, regs = run(go())
+    assert regs == 2 and dt < 1.5, dt
