@@ -110,11 +110,17 @@ class ResourcePlugin:
         os.makedirs(os.path.dirname(self.socket), exist_ok=True)
         self.stop_bc = Broadcast()
         if self.mgr.cfg.grpc_server == "native":
-            native = NativePluginServer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
-                                        self.mgr.cfg.send_every_pulse)
-            await native.start(self.socket)
-            self.native = native
-            return
+            try:
+                native = NativePluginServer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
+                                            self.mgr.cfg.send_every_pulse)
+                await native.start(self.socket)
+                self.native = native
+                return
+            except (OSError, ImportError, AttributeError) as e:
+                # never leave the node unserved over the fast path: serve it from Python
+                _log.warning("native gRPC server unavailable (%s); serving %s with grpc.aio", e, self.resource_name)
+                REGISTRY.inc("mi355x_dp_grpc_native_fallbacks_total", resource=self.name)
+                self._cleanup()
         self.servicer = DevicePluginServicer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
                                              self.mgr.cfg.send_every_pulse)
         server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])

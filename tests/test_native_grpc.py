@@ -582,3 +582,21 @@ def test_server_restart_on_the_same_socket_path(tmp_path):
         ch.close()
     finally:
         srv2.stop(0.1)
+
+
+def test_native_start_failure_falls_back_to_aio(tmp_path, monkeypatch):
+    """If the native server cannot start, the plugin serves the node from grpc.aio."""
+    from rocm_k8s_device_plugin_amd.plugin import native_server as ns_mod
+    fi = make_mi355x_node(tmp_path / "n")
+
+    async def broken(self, socket):
+        raise OSError("bind: injected")
+
+    monkeypatch.setattr(ns_mod.NativePluginServer, "start", broken)
+
+    async def fn(k, mgr, st):
+        adm = await k.admit("amd.com/gpu", 2)
+        return mgr.plugins["gpu"].native, mgr.plugins["gpu"].server, adm
+
+    native, server, adm = run(_with_plugin(tmp_path, _impl(fi), "native", fn))
+    assert native is None and server is not None and len(adm.device_ids) == 2
