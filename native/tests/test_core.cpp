@@ -400,6 +400,81 @@ static void test_grpc_server() {
   ::rmdir(dir);
 }
 
+// Random and mutated input for the HPACK decoder and the HTTP/2 frame parser:
+// nothing may crash or hang (run under ASan/UBSan by the sanitizer ctest), and
+// the server must keep answering a well-formed client afterwards.
+static void test_fuzz_rpc() {
+  using namespace mi355x::rpc;
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  auto rnd = [&x]() {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    return x;
+  };
+  const std::string valid[] = {unhex("828684418cf1e3c2e5f23a6ba0ab90f4ff"), unhex("828684be5886a8eb10649cbf"),
+                               unhex("828785bf408825a849e95ba97d7f8925a849e95bb8e8b4bf")};
+  int decoded = 0;
+  for (int i = 0; i < 20000; ++i) {
+    std::string b;
+    if (i % 2) {
+      b = valid[i % 3];
+      for (int m = 0; m < 1 + static_cast<int>(rnd() % 4); ++m) b[rnd() % b.size()] = static_cast<char>(rnd());
+    } else {
+      b.resize(rnd() % 64);
+      for (auto& c : b) c = static_cast<char>(rnd());
+    }
+    HpackDecoder dec(static_cast<size_t>(rnd() % 5000));
+    HeaderList hl;
+    decoded += dec.decode(reinterpret_cast<const uint8_t*>(b.data()), b.size(), &hl);
+    std::string h;
+    huffman_decode(reinterpret_cast<const uint8_t*>(b.data()), b.size(), &h);
+  }
+  CHECK(decoded > 0);
+
+  char tmpl[] = "/tmp/mi355x-fuzz-XXXXXX";
+  const char* dir = ::mkdtemp(tmpl);
+  if (!dir) {
+    ++g_skip;
+    return;
+  }
+  const std::string sock = std::string(dir) + "/f.sock";
+  GrpcServer srv;
+  DevicePluginService svc;
+  svc.attach(srv);
+  svc.set_options(std::string("\x10\x01", 2));
+  CHECK(srv.start(sock).empty());
+  for (int i = 0; i < 300; ++i) {
+    const int fd = h2t::connect_unix(sock);
+    if (fd < 0) continue;
+    std::string junk;
+    // random frames after a valid preface: random type / flags / stream / payload
+    for (int f = 0; f < 1 + static_cast<int>(rnd() % 6); ++f) {
+      std::string p(rnd() % 80, '\0');
+      for (auto& c : p) c = static_cast<char>(rnd());
+      junk += h2t::frame(static_cast<uint8_t>(rnd() % 11), static_cast<uint8_t>(rnd()),
+                         static_cast<uint32_t>(rnd() % 16), p);
+    }
+    if (::write(fd, junk.data(), junk.size()) < 0) {
+    }
+    ::shutdown(fd, SHUT_WR);
+    char buf[4096];
+    while (::read(fd, buf, sizeof(buf)) > 0) {
+    }
+    ::close(fd);
+  }
+  const int fd = h2t::connect_unix(sock);
+  HpackDecoder dec;
+  h2t::Result r;
+  const std::string req = h2t::request(1, "/v1beta1.DevicePlugin/GetDevicePluginOptions", "");
+  CHECK(fd >= 0 && ::write(fd, req.data(), req.size()) == static_cast<ssize_t>(req.size()) &&
+        h2t::read_call(fd, 1, &r, &dec) && r.grpc_status == 0 && r.messages.size() == 1);
+  if (fd >= 0) ::close(fd);
+  srv.stop(0.1);
+  ::unlink(sock.c_str());
+  ::rmdir(dir);
+}
+
 int main(int argc, char** argv) {
   std::string repo = argc > 1 ? argv[1] : "testdata";
   std::string ref = argc > 2 ? argv[2] : "/root/reference/testdata";
@@ -410,6 +485,7 @@ int main(int argc, char** argv) {
   test_degraded_links(ref);
   test_hpack();
   test_grpc_server();
+  test_fuzz_rpc();
   std::printf("test_core: %d passed, %d failed, %d skipped\n", g_pass, g_fail, g_skip);
   return g_fail ? 1 : 0;
 }
