@@ -61,7 +61,7 @@ def build_parser() -> flags.GoFlagParser:
                                               "dispatch's late verdict is awaited; otherwise a deadline miss on "
                                               "a busy GPU is inconclusive)")
     p.add_bool("liveness_corroborate", True, "a probe pending on a busy GPU stays inconclusive only while amd-smi "
-                                             "reports GFX activity; 0% on 2 consecutive sweeps ends the busy grace")
+                                             "reports GFX activity; 0%% on 2 consecutive sweeps ends the busy grace")
     p.add_int("liveness_crowded_procs", 7, "with this many other processes holding queues on a GPU (or too few "
                                            "free kfd queues) the probe server steps off it, so it adds no process or "
                                            "queue to an oversubscribed HWS runlist; 0 = off")

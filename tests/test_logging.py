@@ -106,3 +106,18 @@ def test_device_plugin_cli_writes_log_files(tmp_path):
     bad = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.device_plugin", "-dry_run",
                           "-vmodule=broken"], capture_output=True, text=True, timeout=120, env=env)
     assert bad.returncode == 1 and "vmodule" in bad.stderr
+
+
+@pytest.mark.parametrize("cli,flags", [
+    ("device_plugin", ("-pulse", "-driver_type", "-resource_naming_strategy", "-kubelet_dir", "-log_dir",
+                       "-liveness_corroborate", "-grpc_server")),
+    ("node_labeller", ("-watch", "-log_dir", "-vmodule")),
+])
+def test_cli_help_renders(cli, flags):
+    """-h must render every help string (argparse %-formats them) and name the
+    reference's flags (cmd/k8s-device-plugin/main.go:53-55)."""
+    p = subprocess.run([sys.executable, "-m", f"rocm_k8s_device_plugin_amd.cli.{cli}", "-h"], capture_output=True,
+                       text=True, timeout=120, env=dict(os.environ, PYTHONPATH=REPO))
+    assert p.returncode == 0, p.stderr[-1500:]
+    for f in flags:
+        assert f in p.stdout, f
