@@ -491,10 +491,15 @@ def main():
         else:
             sizes = args.collective_sizes or "64K"
             ops, iters, dtype = ("all_reduce", "all_gather"), 3, d.torch.float32
-        rows = coll.run([coll.parse_size(x) for x in sizes.split(",") if x], ops, iters=iters, warmup=3,
-                        dtype=dtype)
-        rccl = coll.summary(rows)
-        rccl["backend"] = d.dist.get_backend()
+        # a secondary measurement: a failure is reported in the JSON line, not
+        # allowed to take the headline down with it
+        try:
+            rows = coll.run([coll.parse_size(x) for x in sizes.split(",") if x], ops, iters=iters, warmup=3,
+                            dtype=dtype)
+            rccl = coll.summary(rows)
+            rccl["backend"] = d.dist.get_backend()
+        except Exception as e:  # noqa: BLE001
+            rccl = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     extra = {}
     if d.rank == 0:
@@ -558,7 +563,10 @@ def main():
                  "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
                  "reference_algorithm_candidates": ref["candidates"], "allocator_sweep": sweep, "gpus": gpu_info}
         from rocm_k8s_device_plugin_amd.parallel.fabric import Fabric
-        extra["fabric"] = Fabric(inv).report([dv.id for dv in adv]).as_dict()
+        try:
+            extra["fabric"] = Fabric(inv).report([dv.id for dv in adv]).as_dict()
+        except Exception as e:  # noqa: BLE001
+            extra["fabric"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         extra["rccl"] = rccl
         # the timed admissions' GetPreferredAllocation (with M > N: a real search
         # over the fragmented availability) and the N-of-all-devices comparison
@@ -567,8 +575,11 @@ def main():
         extra["fragmented_n_of_m"] = frag
         if args.peer_check and not args.fixture:
             from rocm_k8s_device_plugin_amd.health.peer import probe_peers
-            rep = probe_peers(adv_ordinals, nbytes=64 << 20, reps=3, timeout_s=120)
-            extra["peer_probe"] = dict(rep.summary(), wall_ms=round(rep.wall_ms, 1))
+            try:
+                rep = probe_peers(adv_ordinals, nbytes=64 << 20, reps=3, timeout_s=120)
+                extra["peer_probe"] = dict(rep.summary(), wall_ms=round(rep.wall_ms, 1))
+            except Exception as e:  # noqa: BLE001
+                extra["peer_probe"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         plug.stop()
         loop.close()
         out = {
