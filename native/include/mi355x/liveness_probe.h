@@ -145,6 +145,46 @@ typedef struct {
 
 int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, double timeout_s, mi355x_sweep_result* out);
 
+// ---- throughput check (idle GPUs only: it owns the chip for a few ms) --------
+// HBM: fill `bytes` of device memory with an address-derived pattern (write
+// bandwidth), read it back and verify every word (read bandwidth). MFMA: two
+// register-resident bf16 v_mfma_f32_32x32x16 chains per wave, two waves per
+// SIMD on every CU (sustained TFLOP/s), with each workgroup's shader clock
+// from s_memtime / s_memrealtime, folded per XCD; every wave's accumulator
+// checksum must be bit-identical (same operands everywhere).
+typedef struct {
+  int ordinal;
+  int ok;                    // pattern exact, checksums identical, every record present, all XCDs ran
+  int hsa_error;
+  uint32_t nonce;
+  uint64_t bytes;
+  int cu_count;
+  int num_xcc;
+  double fill_us;            // kernel times (HSA dispatch profiling)
+  double check_us;
+  double hbm_write_gbps;
+  double hbm_read_gbps;
+  uint64_t hbm_bad_words;    // 32-bit words read back wrong
+  int64_t hbm_first_bad;     // lowest failing 16-byte unit, -1 if none
+  int mfma_iters;            // MFMA pairs per wave
+  int mfma_grid;             // workgroups (MI355X_BURN_WGS_PER_CU per CU)
+  int mfma_records_ok;
+  int mfma_checksum_mismatch;  // waves whose checksum differs from workgroup 0 wave 0
+  int mfma_xccs;             // distinct XCDs that ran burn workgroups
+  double mfma_us;
+  double mfma_tflops;        // dense bf16, from the dispatch time
+  double clock_mhz_min;      // per-workgroup shader clock during the MFMA loop
+  double clock_mhz_median;
+  double clock_mhz_max;
+  double xcd_clock_mhz[16];  // median per XCD (0 = no workgroup seen)
+  double total_us;
+  double in_flight_s;        // > 0: an earlier sweep / check on this device has not completed
+  char error[160];
+} mi355x_perf_result;
+
+int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes, int mfma_iters, double timeout_s,
+                          mi355x_perf_result* out);
+
 #ifdef __cplusplus
 }
 #endif

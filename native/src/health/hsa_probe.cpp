@@ -812,7 +812,7 @@ struct SweepInFlight {
   hsa_executable_t exe{};
   hsa_queue_t* queue = nullptr;
   hsa_signal_t sig{};
-  void* bufs[4] = {nullptr, nullptr, nullptr, nullptr};
+  void* bufs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::chrono::steady_clock::time_point since{};
 
   void release() {
@@ -827,24 +827,32 @@ struct SweepInFlight {
 std::mutex g_sweep_mu;
 std::vector<std::pair<int, SweepInFlight>> g_sweep_in_flight;
 
-// true (and out filled) when an earlier sweep on `ordinal` is still running;
-// a completed one is freed here.
-bool sweep_still_in_flight(int ordinal, mi355x_sweep_result* out) {
+// > 0 (seconds outstanding) when an earlier sweep or throughput check on
+// `ordinal` is still running; a completed one is freed here.
+double in_flight_for(int ordinal) {
   std::lock_guard<std::mutex> lk(g_sweep_mu);
   for (auto it = g_sweep_in_flight.begin(); it != g_sweep_in_flight.end(); ++it) {
     if (it->first != ordinal) continue;
     if (H().hsa_signal_load_scacquire(it->second.sig) < 1) {
       it->second.release();
       g_sweep_in_flight.erase(it);
-      return false;
+      return 0;
     }
-    out->in_flight_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - it->second.since).count();
-    out->hsa_error = -1;
-    std::snprintf(out->error, sizeof(out->error), "earlier chip sweep still in flight for %.1fs (not completed)",
-                  out->in_flight_s);
-    return true;
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - it->second.since).count();
+    return s > 0 ? s : 1e-9;
   }
-  return false;
+  return 0;
+}
+
+template <typename R>
+bool sweep_still_in_flight(int ordinal, R* out) {
+  const double s = in_flight_for(ordinal);
+  if (s <= 0) return false;
+  out->in_flight_s = s;
+  out->hsa_error = -1;
+  std::snprintf(out->error, sizeof(out->error), "earlier chip sweep / check still in flight for %.1fs (not completed)",
+                s);
+  return true;
 }
 
 // runtime shutdown: an outstanding sweep's resources go with the runtime
@@ -1056,6 +1064,291 @@ done:
     if (arrive) H().hsa_amd_memory_pool_free(arrive);
     if (tiles) H().hsa_amd_memory_pool_free(tiles);
     if (records) H().hsa_amd_memory_pool_free(records);
+    if (sig.handle) H().hsa_signal_destroy(sig);
+    if (queue) H().hsa_queue_destroy(queue);
+    if (exe.handle) H().hsa_executable_destroy(exe);
+    if (reader.handle) H().hsa_code_object_reader_destroy(reader);
+  }
+  out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+  return out->ok ? 0 : 1;
+}
+
+namespace {
+
+// One AQL kernel dispatch (barrier bit, system-scope fences), no wait.
+void submit_kernel(hsa_queue_t* queue, uint64_t kobj, uint32_t gseg, uint32_t pseg, void* kargs, uint32_t wgs,
+                   uint32_t wg_threads, hsa_signal_t sig) {
+  H().hsa_signal_store_screlease(sig, 1);
+  const uint64_t idx = H().hsa_queue_add_write_index_screlease(queue, 1);
+  auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address) + (idx & (queue->size - 1));
+  std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
+  pkt->workgroup_size_x = static_cast<uint16_t>(wg_threads);
+  pkt->workgroup_size_y = 1;
+  pkt->workgroup_size_z = 1;
+  pkt->grid_size_x = wgs * wg_threads;
+  pkt->grid_size_y = 1;
+  pkt->grid_size_z = 1;
+  pkt->private_segment_size = pseg;
+  pkt->group_segment_size = gseg;
+  pkt->kernel_object = kobj;
+  pkt->kernarg_address = kargs;
+  pkt->completion_signal = sig;
+  const uint16_t header = static_cast<uint16_t>(
+      (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16), __ATOMIC_RELEASE);
+  H().hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+}
+
+double dispatch_us(const Agent& ag, hsa_signal_t sig) {
+  hsa_amd_profiling_dispatch_time_t dt{};
+  if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, sig, &dt) != HSA_STATUS_SUCCESS || !g_rt.ts_freq) return 0;
+  return static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
+}
+
+double median_of(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+}  // namespace
+
+extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes, int mfma_iters, double timeout_s,
+                                     mi355x_perf_result* out) {
+  using clk = std::chrono::steady_clock;
+  std::memset(out, 0, sizeof(*out));
+  out->ordinal = ordinal;
+  out->nonce = nonce;
+  out->hbm_first_bad = -1;
+  // 16-byte units, at least one full grid-stride round, at most 64 GiB
+  bytes = bytes < (64ull << 20) ? (64ull << 20) : (bytes > (64ull << 30) ? (64ull << 30) : bytes);
+  bytes &= ~static_cast<uint64_t>(0xFFFFF);
+  out->bytes = bytes;
+  out->mfma_iters = mfma_iters < 1 ? 1 : (mfma_iters > (1 << 22) ? (1 << 22) : mfma_iters);
+  const auto t0 = clk::now();
+  const int n = mi355x_hsa_probe_init();
+  if (n < 0) {
+    out->hsa_error = n;
+    std::snprintf(out->error, sizeof(out->error), "hsa_init: %.140s", H().loaded ? "runtime init failed" : H().error);
+    return 1;
+  }
+  if (ordinal < 0 || ordinal >= n) {
+    std::snprintf(out->error, sizeof(out->error), "no such GPU agent (count=%d)", n);
+    return 1;
+  }
+  if (sweep_still_in_flight(ordinal, out)) {
+    out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+    return 1;
+  }
+  const Agent& ag = g_rt.gpus[ordinal];
+  uint32_t cus = 0, xcc = 0;
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cus);
+  H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_NUM_XCC), &xcc);
+  out->cu_count = static_cast<int>(cus);
+  out->num_xcc = static_cast<int>(xcc);
+  if (cus == 0 || cus > 1024 || !g_rt.has_fine || !g_rt.has_kernarg || !ag.has_coarse) {
+    std::snprintf(out->error, sizeof(out->error), "unexpected agent (cus=%u) or missing memory pool", cus);
+    return 1;
+  }
+  const uint32_t fill_wgs = cus * MI355X_HBM_FILL_WGS_PER_CU;
+  const uint32_t check_wgs = cus * MI355X_HBM_CHECK_WGS_PER_CU;
+  const uint32_t burn_wgs = cus * MI355X_BURN_WGS_PER_CU;
+  out->mfma_grid = static_cast<int>(burn_wgs);
+
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t sig{};
+  uint32_t* buf = nullptr;      // device, `bytes`
+  uint32_t* counters = nullptr; // device, [0] bad words, [2..3] first bad unit
+  uint32_t* h_counters = nullptr;
+  uint32_t* records = nullptr;  // host-visible, burn_wgs records
+  char* kargs = nullptr;        // 3 slots of kKernargBytes
+  bool in_flight = false;
+  hsa_status_t s = HSA_STATUS_SUCCESS;
+  struct K {
+    const char* name;
+    uint64_t kobj = 0;
+    uint32_t kseg = 0, gseg = 0, pseg = 0;
+  } ks[3] = {{"mi355x_hbm_fill.kd"}, {"mi355x_hbm_check.kd"}, {"mi355x_mfma_burn.kd"}};
+  const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
+  const size_t rec_bytes = static_cast<size_t>(burn_wgs) * MI355X_PERF_REC_WORDS * sizeof(uint32_t);
+  auto fail = [&](hsa_status_t st, const char* what) {
+    out->hsa_error = static_cast<int>(st);
+    const char* msg = nullptr;
+    H().hsa_status_string(st, &msg);
+    std::snprintf(out->error, sizeof(out->error), "%s: %s", what, msg ? msg : "hsa error");
+  };
+  // a dispatch that did not complete: nothing it may still write can be freed
+  auto abandon = [&](const char* what) {
+    in_flight = true;
+    std::snprintf(out->error, sizeof(out->error), "%s did not complete within %.1fs", what, timeout_s);
+    out->hsa_error = -1;
+    SweepInFlight f;
+    f.reader = reader;
+    f.exe = exe;
+    f.queue = queue;
+    f.sig = sig;
+    f.bufs[0] = kargs;
+    f.bufs[1] = buf;
+    f.bufs[2] = counters;
+    f.bufs[3] = h_counters;
+    f.bufs[4] = records;
+    f.since = t0;
+    std::lock_guard<std::mutex> lk(g_sweep_mu);
+    g_sweep_in_flight.emplace_back(ordinal, f);
+  };
+#define PERF_CHECK(expr, what) \
+  if ((s = (expr)) != HSA_STATUS_SUCCESS) { fail(s, what); goto done; }
+
+  PERF_CHECK(H().hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader), "code object");
+  PERF_CHECK(H().hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe),
+             "executable create");
+  PERF_CHECK(H().hsa_executable_load_agent_code_object(exe, ag.agent, reader, nullptr, nullptr), "load code object");
+  PERF_CHECK(H().hsa_executable_freeze(exe, nullptr), "freeze");
+  for (K& k : ks) {
+    hsa_executable_symbol_t sym{};
+    PERF_CHECK(H().hsa_executable_get_symbol_by_name(exe, k.name, &ag.agent, &sym), "kernel symbol");
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.kobj);
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kseg);
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.gseg);
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.pseg);
+  }
+  if (ks[0].kseg < sizeof(mi355x_hbm_args) || ks[0].kseg > kKernargBytes || ks[1].kseg < sizeof(mi355x_hbm_args) ||
+      ks[1].kseg > kKernargBytes || ks[2].kseg < sizeof(mi355x_burn_args) || ks[2].kseg > kKernargBytes) {
+    std::snprintf(out->error, sizeof(out->error), "perf kernarg segments %u/%u/%u: code object / host ABI mismatch",
+                  ks[0].kseg, ks[1].kseg, ks[2].kseg);
+    goto done;
+  }
+  PERF_CHECK(H().hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX,
+                                  &queue), "queue create");
+  H().hsa_amd_profiling_set_profiler_enabled(queue, 1);
+  PERF_CHECK(H().hsa_signal_create(1, 0, nullptr, &sig), "signal create");
+  PERF_CHECK(H().hsa_amd_memory_pool_allocate(ag.coarse, bytes, 0, reinterpret_cast<void**>(&buf)), "alloc HBM buffer");
+  PERF_CHECK(H().hsa_amd_memory_pool_allocate(ag.coarse, 4096, 0, reinterpret_cast<void**>(&counters)),
+             "alloc counters");
+  PERF_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.fine, 4096, 0, reinterpret_cast<void**>(&h_counters)),
+             "alloc host counters");
+  PERF_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.fine, rec_bytes, 0, reinterpret_cast<void**>(&records)),
+             "alloc records");
+  PERF_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.kernarg, 3 * kKernargBytes, 0, reinterpret_cast<void**>(&kargs)),
+             "alloc kernarg");
+  PERF_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, h_counters), "allow counters");
+  PERF_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, records), "allow records");
+  PERF_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, kargs), "allow kernarg");
+  // counters: word 0 = 0 (bad words), words 2..3 = all ones (first bad unit)
+  PERF_CHECK(H().hsa_amd_memory_fill(counters, 0u, 2), "zero counters");
+  PERF_CHECK(H().hsa_amd_memory_fill(counters + 2, 0xFFFFFFFFu, 2), "init first-bad");
+  std::memset(records, 0, rec_bytes);
+  std::memset(kargs, 0, 3 * kKernargBytes);
+  {
+    auto* fa = reinterpret_cast<mi355x_hbm_args*>(kargs);
+    auto* ca = reinterpret_cast<mi355x_hbm_args*>(kargs + kKernargBytes);
+    auto* ba = reinterpret_cast<mi355x_burn_args*>(kargs + 2 * kKernargBytes);
+    fa->buf = ca->buf = buf;
+    fa->n16 = ca->n16 = bytes / 16;
+    fa->bad = ca->bad = counters;
+    fa->first_bad = ca->first_bad = reinterpret_cast<uint64_t*>(counters + 2);
+    fa->threads = static_cast<uint64_t>(fill_wgs) * MI355X_PERF_THREADS;
+    ca->threads = static_cast<uint64_t>(check_wgs) * MI355X_PERF_THREADS;
+    fa->seed = ca->seed = nonce * 0x01000193u + 0x7F4A7C15u;
+    ba->records = records;
+    ba->nonce = nonce;
+    ba->iters = out->mfma_iters;
+  }
+  submit_kernel(queue, ks[0].kobj, ks[0].gseg, ks[0].pseg, kargs, fill_wgs, MI355X_PERF_THREADS, sig);
+  if (!wait_signal(sig, timeout_s)) {
+    abandon("HBM fill");
+    goto done;
+  }
+  out->fill_us = dispatch_us(ag, sig);
+  submit_kernel(queue, ks[1].kobj, ks[1].gseg, ks[1].pseg, kargs + kKernargBytes, check_wgs, MI355X_PERF_THREADS,
+                sig);
+  if (!wait_signal(sig, timeout_s)) {
+    abandon("HBM check");
+    goto done;
+  }
+  out->check_us = dispatch_us(ag, sig);
+  submit_kernel(queue, ks[2].kobj, ks[2].gseg, ks[2].pseg, kargs + 2 * kKernargBytes, burn_wgs, MI355X_PERF_THREADS,
+                sig);
+  if (!wait_signal(sig, timeout_s)) {
+    abandon("MFMA burn");
+    goto done;
+  }
+  out->mfma_us = dispatch_us(ag, sig);
+  // device counters -> host (async copy, bounded wait on the same signal)
+  H().hsa_signal_store_screlease(sig, 1);
+  PERF_CHECK(H().hsa_amd_memory_async_copy(h_counters, g_rt.cpu, counters, ag.agent, 16, 0, nullptr, sig),
+             "copy counters");
+  if (!wait_signal(sig, timeout_s)) {
+    abandon("counter copy");
+    goto done;
+  }
+  {
+    out->hbm_bad_words = h_counters[0];
+    const uint64_t first = (static_cast<uint64_t>(h_counters[3]) << 32) | h_counters[2];
+    out->hbm_first_bad = first == ~0ull ? -1 : static_cast<int64_t>(first);
+    if (out->fill_us > 0) out->hbm_write_gbps = static_cast<double>(bytes) / (out->fill_us * 1e3);
+    if (out->check_us > 0) out->hbm_read_gbps = static_cast<double>(bytes) / (out->check_us * 1e3);
+    const double flops = 2.0 * 32 * 32 * 16 * 2.0 * static_cast<double>(out->mfma_iters) *
+                         (MI355X_PERF_THREADS / 64) * static_cast<double>(burn_wgs);
+    if (out->mfma_us > 0) out->mfma_tflops = flops / (out->mfma_us * 1e6);
+    std::vector<double> clocks;
+    std::vector<std::vector<double>> per_xcd(16);
+    uint32_t ref = 0;
+    bool have_ref = false;
+    uint32_t xmask = 0;
+    for (uint32_t w = 0; w < burn_wgs; ++w) {
+      const uint32_t* r = records + static_cast<size_t>(w) * MI355X_PERF_REC_WORDS;
+      if (r[MI355X_PREC_MAGIC] != MI355X_PERF_MAGIC || r[MI355X_PREC_WG] != w || r[MI355X_PREC_NONCE] != (nonce ^ w))
+        continue;
+      ++out->mfma_records_ok;
+      for (int v = 0; v < MI355X_PERF_THREADS / 64; ++v) {
+        if (!have_ref) {
+          ref = r[MI355X_PREC_SUM + v];
+          have_ref = true;
+        } else if (r[MI355X_PREC_SUM + v] != ref) {
+          ++out->mfma_checksum_mismatch;
+        }
+      }
+      const uint64_t rt0 = (static_cast<uint64_t>(r[MI355X_PREC_RT0_HI]) << 32) | r[MI355X_PREC_RT0_LO];
+      const uint64_t rt1 = (static_cast<uint64_t>(r[MI355X_PREC_RT1_HI]) << 32) | r[MI355X_PREC_RT1_LO];
+      const uint64_t cyc = (static_cast<uint64_t>(r[MI355X_PREC_CYC_HI]) << 32) | r[MI355X_PREC_CYC_LO];
+      const uint32_t x = r[MI355X_PREC_XCC] & 0xF;
+      xmask |= 1u << x;
+      if (rt1 > rt0) {
+        const double mhz = static_cast<double>(cyc) / (static_cast<double>(rt1 - rt0) / 100.0);  // ticks per us
+        clocks.push_back(mhz);
+        per_xcd[x].push_back(mhz);
+      }
+    }
+    out->mfma_xccs = __builtin_popcount(xmask);
+    if (!clocks.empty()) {
+      out->clock_mhz_min = *std::min_element(clocks.begin(), clocks.end());
+      out->clock_mhz_max = *std::max_element(clocks.begin(), clocks.end());
+      out->clock_mhz_median = median_of(clocks);
+    }
+    for (int x = 0; x < 16; ++x) out->xcd_clock_mhz[x] = median_of(per_xcd[x]);
+    out->ok = out->hbm_bad_words == 0 && out->mfma_checksum_mismatch == 0 &&
+              out->mfma_records_ok == static_cast<int>(burn_wgs) &&
+              (out->num_xcc <= 0 || out->mfma_xccs == out->num_xcc);
+    if (!out->ok)
+      std::snprintf(out->error, sizeof(out->error),
+                    "hbm_bad_words=%llu first_bad_unit=%lld mfma records %d/%u checksum mismatches %d, %d/%d XCDs ran",
+                    static_cast<unsigned long long>(out->hbm_bad_words), static_cast<long long>(out->hbm_first_bad),
+                    out->mfma_records_ok, burn_wgs, out->mfma_checksum_mismatch, out->mfma_xccs, out->num_xcc);
+  }
+#undef PERF_CHECK
+done:
+  if (!in_flight) {
+    if (kargs) H().hsa_amd_memory_pool_free(kargs);
+    if (records) H().hsa_amd_memory_pool_free(records);
+    if (h_counters) H().hsa_amd_memory_pool_free(h_counters);
+    if (counters) H().hsa_amd_memory_pool_free(counters);
+    if (buf) H().hsa_amd_memory_pool_free(buf);
     if (sig.handle) H().hsa_signal_destroy(sig);
     if (queue) H().hsa_queue_destroy(queue);
     if (exe.handle) H().hsa_executable_destroy(exe);

@@ -81,3 +81,68 @@ MI355X_HD uint32_t sweep_nonce(uint32_t nonce, uint32_t wg, uint32_t wave) { ret
 MI355X_HD uint32_t sweep_lds_pattern(uint32_t i, uint32_t nonce, uint32_t wg) {
   return (i * 2654435761u) ^ (nonce + wg * 0x9E3779B1u);
 }
+
+// ---- throughput check (mi355x_hbm_fill / mi355x_hbm_check / mi355x_mfma_burn) ----
+// A GPU can be alive and exact yet slow: a stuck-low clock, an XCD held back,
+// an HBM stack running degraded. On an idle GPU the plugin can measure what a
+// tenant would get: HBM write and read bandwidth over a patterned buffer (every
+// 16-byte unit verified on the read pass) and sustained bf16 MFMA throughput
+// with the shader clock of every workgroup (s_memtime over s_memrealtime).
+#define MI355X_PERF_THREADS 256
+// grid shapes measured on MI355X: plain 16-byte stores peak at 4 workgroups
+// per CU (5.3-5.5 TB/s; nontemporal ones 5.0-5.2; tools/experiments/
+// hbm_stream_variants.hip, 8 GiB). For loads, 16 per CU wins on repeated
+// passes over 8 GiB (6.5-6.7 TB/s vs 6.3) but loses on the check's single
+// pass right after the fill (1-4 GiB: 3.8-4.8 TB/s vs 5.0-6.1 at 8 per CU,
+// tools/gpurun_perfcheck.sh), so the check uses 8.
+#define MI355X_HBM_FILL_WGS_PER_CU 4
+#define MI355X_HBM_CHECK_WGS_PER_CU 8
+#define MI355X_BURN_WGS_PER_CU 2   // 8 waves per CU = 2 per SIMD
+#define MI355X_PERF_REC_WORDS 16
+#define MI355X_PERF_MAGIC 0x50455246u /* "PERF" */
+// mfma_burn record words (one record per workgroup)
+#define MI355X_PREC_MAGIC 0
+#define MI355X_PREC_WG 1
+#define MI355X_PREC_XCC 2
+#define MI355X_PREC_HWID 3
+#define MI355X_PREC_RT0_LO 4      // s_memrealtime (100 MHz) before the MFMA loop
+#define MI355X_PREC_RT0_HI 5
+#define MI355X_PREC_RT1_LO 6      // after it
+#define MI355X_PREC_RT1_HI 7
+#define MI355X_PREC_CYC_LO 8      // s_memtime (shader clock) ticks over the loop
+#define MI355X_PREC_CYC_HI 9
+#define MI355X_PREC_NONCE 10
+#define MI355X_PREC_SUM 12        // 4 words: each wave's accumulator checksum (identical everywhere)
+
+struct mi355x_hbm_args {
+  uint32_t* buf;        // device memory, n16 * 16 bytes
+  uint64_t n16;         // 16-byte units
+  uint32_t* bad;        // device-visible counter of mismatching 32-bit words (check pass)
+  uint64_t* first_bad;  // lowest mismatching 16-byte unit (check pass), UINT64_MAX if none
+  uint64_t threads;     // lanes in the grid (the grid stride; passed so the kernels need no hidden args)
+  uint32_t seed;
+  uint32_t pad;
+};
+
+struct mi355x_burn_args {
+  uint32_t* records;    // host-visible, grid * MI355X_PERF_REC_WORDS
+  uint32_t nonce;
+  int32_t iters;        // MFMA pairs per wave
+};
+
+// 32-bit word `word` of the patterned buffer: a bijection of the word index
+// (odd multiplier), so a stuck or aliased address bit reads another value
+MI355X_HD uint32_t hbm_pattern(uint64_t word, uint32_t seed) {
+  return (uint32_t)(word ^ (word >> 32)) * 0x9E3779B1u + seed;
+}
+
+// bf16 bit pattern of a pseudo-random operand in +-[2^-7, 2^-1): every MFMA
+// input bit toggles (zero or small-integer operands run at a higher clock than
+// real data, MI355X_MICROARCH.md "DVFS give-back")
+MI355X_HD uint16_t burn_bf16_bits(uint32_t lane, uint32_t j, uint32_t nonce) {
+  uint32_t h = (lane * 0x9E3779B1u) ^ (j * 0x85EBCA77u) ^ nonce;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return (uint16_t)((h & 0x807Fu) | ((120u + (h >> 8) % 7u) << 7));
+}

@@ -146,3 +146,114 @@ extern "C" __global__ __launch_bounds__(MI355X_SWEEP_THREADS) void mi355x_chip_s
     rec[MI355X_REC_MAGIC] = MI355X_SWEEP_MAGIC;
   }
 }
+
+// ---- throughput check: see liveness_kernel.h ---------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Grid-stride over 16-byte units; the check pass keeps 4 nontemporal loads in
+// flight per lane (grid shapes: liveness_kernel.h).
+extern "C" __global__ __launch_bounds__(MI355X_PERF_THREADS) void mi355x_hbm_fill(mi355x_hbm_args args) {
+  u32x4* buf = reinterpret_cast<u32x4*>(args.buf);
+  const uint64_t stride = args.threads;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * MI355X_PERF_THREADS + threadIdx.x; i < args.n16;
+       i += stride) {
+    const uint64_t w = i * 4;
+    u32x4 v;
+    v.x = hbm_pattern(w, args.seed);
+    v.y = hbm_pattern(w + 1, args.seed);
+    v.z = hbm_pattern(w + 2, args.seed);
+    v.w = hbm_pattern(w + 3, args.seed);
+    buf[i] = v;
+  }
+}
+
+__device__ inline uint32_t hbm_mismatches(const u32x4 v, uint64_t unit, uint32_t seed) {
+  const uint64_t w = unit * 4;
+  return (v.x != hbm_pattern(w, seed)) + (v.y != hbm_pattern(w + 1, seed)) + (v.z != hbm_pattern(w + 2, seed)) +
+         (v.w != hbm_pattern(w + 3, seed));
+}
+
+extern "C" __global__ __launch_bounds__(MI355X_PERF_THREADS) void mi355x_hbm_check(mi355x_hbm_args args) {
+  const u32x4* buf = reinterpret_cast<const u32x4*>(args.buf);
+  const uint64_t stride = args.threads;
+  const uint64_t n = args.n16;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * MI355X_PERF_THREADS + threadIdx.x;
+  uint32_t bad = 0;
+  uint64_t first = ~0ull;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(&buf[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t m = hbm_mismatches(v[u], i + u * stride, args.seed);
+      if (m) {
+        bad += m;
+        first = first < i + u * stride ? first : i + u * stride;
+      }
+    }
+  }
+  for (; i < n; i += stride) {
+    const uint32_t m = hbm_mismatches(__builtin_nontemporal_load(&buf[i]), i, args.seed);
+    if (m) {
+      bad += m;
+      first = first < i ? first : i;
+    }
+  }
+  if (bad) {
+    atomicAdd(args.bad, bad);
+    atomicMin(reinterpret_cast<unsigned long long*>(args.first_bad), static_cast<unsigned long long>(first));
+  }
+}
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Register-resident v_mfma_f32_32x32x16_bf16 chains, two per wave, two waves
+// per SIMD: the matrix cores' sustained rate at the clock the chip holds under
+// this load. Every wave gets the same operands, so every accumulator checksum
+// must be bit-identical across waves, CUs and XCDs (the host compares them).
+extern "C" __global__ __launch_bounds__(MI355X_PERF_THREADS) void mi355x_mfma_burn(mi355x_burn_args args) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = threadIdx.x >> 6;
+  bf16x8 a, b, c, d;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = __builtin_bit_cast(__bf16, burn_bf16_bits(lane, j, args.nonce));
+    b[j] = __builtin_bit_cast(__bf16, burn_bf16_bits(lane, j + 8, args.nonce));
+    c[j] = __builtin_bit_cast(__bf16, burn_bf16_bits(lane, j + 16, args.nonce));
+    d[j] = __builtin_bit_cast(__bf16, burn_bf16_bits(lane, j + 24, args.nonce));
+  }
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+  __syncthreads();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < args.iters; ++it) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c, d, acc1, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += acc0[r] - acc1[r];
+  // the wave's checksum: lane sums folded across the wave
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  const uint64_t c1 = __builtin_amdgcn_s_memtime();
+  const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+  uint32_t* rec = args.records + static_cast<size_t>(blockIdx.x) * MI355X_PERF_REC_WORDS;
+  if (lane == 0) rec[MI355X_PREC_SUM + wave] = __builtin_bit_cast(uint32_t, s);
+  if (threadIdx.x == 0) {
+    const uint64_t cyc = c1 - c0;
+    rec[MI355X_PREC_WG] = blockIdx.x;
+    rec[MI355X_PREC_XCC] = __builtin_amdgcn_s_getreg(MI355X_HWREG_XCC_ID) & 0xF;
+    rec[MI355X_PREC_HWID] = __builtin_amdgcn_s_getreg(MI355X_HWREG_HW_ID);
+    rec[MI355X_PREC_RT0_LO] = static_cast<uint32_t>(rt0);
+    rec[MI355X_PREC_RT0_HI] = static_cast<uint32_t>(rt0 >> 32);
+    rec[MI355X_PREC_RT1_LO] = static_cast<uint32_t>(rt1);
+    rec[MI355X_PREC_RT1_HI] = static_cast<uint32_t>(rt1 >> 32);
+    rec[MI355X_PREC_CYC_LO] = static_cast<uint32_t>(cyc);
+    rec[MI355X_PREC_CYC_HI] = static_cast<uint32_t>(cyc >> 32);
+    rec[MI355X_PREC_NONCE] = args.nonce ^ blockIdx.x;
+    rec[MI355X_PREC_MAGIC] = MI355X_PERF_MAGIC;
+  }
+}

@@ -4,6 +4,7 @@
 //   mi355x-liveness-probe [--devices all|0,2,..] [--nonce N] [--iters N] [--identify] [--timeout S]
 //   mi355x-liveness-probe --serve [--keep]  (long-lived; requests on stdin, see serve())
 //   mi355x-liveness-probe --sweep [--devices ..]   (every CU of every XCD, see mi355x_chip_sweep)
+//   mi355x-liveness-probe --perf [--perf-mib M]     (HBM bandwidth + pattern, sustained MFMA rate, clocks)
 //   mi355x-liveness-probe --peer [--devices ..] [--peer-bytes B] [--peer-reps R]
 //                                      (DMA copy over every GPU pair's link, verified)
 //   --corrupt-word K[@O] / $MI355X_PROBE_CORRUPT_FILE: debug fault injection (see refresh_fault_injection)
@@ -109,6 +110,9 @@ int peer(int a, int b, uint32_t nonce, uint64_t bytes, int reps, double timeout_
 int chip_sweep(int o, uint32_t nonce, int iters, double timeout_s, mi355x_sweep_result* r) {
   return mi355x_hsa_chip_sweep(o, nonce, iters, timeout_s, r);
 }
+int perf_check(int o, uint32_t nonce, uint64_t bytes, int iters, double timeout_s, mi355x_perf_result* r) {
+  return mi355x_hsa_perf_check(o, nonce, bytes, iters, timeout_s, r);
+}
 void init_phases(double out[5]) { mi355x_hsa_init_phases(out); }
 void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
 void teardown() { mi355x_hsa_probe_release(); }
@@ -133,6 +137,15 @@ int chip_sweep(int o, uint32_t nonce, int iters, double, mi355x_sweep_result* r)
   r->nonce = nonce;
   r->iters = iters;
   std::snprintf(r->error, sizeof(r->error), "--sweep needs the HSA-direct build (mi355x-liveness-probe)");
+  return 1;
+}
+int perf_check(int o, uint32_t nonce, uint64_t bytes, int iters, double, mi355x_perf_result* r) {
+  std::memset(r, 0, sizeof(*r));
+  r->ordinal = o;
+  r->nonce = nonce;
+  r->bytes = bytes;
+  r->mfma_iters = iters;
+  std::snprintf(r->error, sizeof(r->error), "--perf needs the HSA-direct build (mi355x-liveness-probe)");
   return 1;
 }
 int peer(int a, int b, uint32_t, uint64_t bytes, int reps, double, mi355x_peer_result* r) {
@@ -301,6 +314,60 @@ bool run_sweeps(const std::vector<int>& ords, const std::vector<uint32_t>& nonce
   return ok;
 }
 
+std::string perf_json(const mi355x_perf_result& r) {
+  std::string per = "[";
+  for (int i = 0; i < 16 && i < (r.num_xcc > 0 ? r.num_xcc : 8); ++i) {
+    char v[32];
+    std::snprintf(v, sizeof(v), "%s%.0f", i ? "," : "", r.xcd_clock_mhz[i]);
+    per += v;
+  }
+  per += "]";
+  char buf[1536];
+  std::snprintf(buf, sizeof(buf),
+                "{\"ordinal\":%d,\"ok\":%s,\"hsa_error\":%d,\"nonce\":%u,\"bytes\":%llu,\"cu_count\":%d,"
+                "\"num_xcc\":%d,\"fill_us\":%.1f,\"check_us\":%.1f,\"hbm_write_gbps\":%.1f,\"hbm_read_gbps\":%.1f,"
+                "\"hbm_bad_words\":%llu,\"hbm_first_bad\":%lld,\"mfma_iters\":%d,\"mfma_grid\":%d,"
+                "\"mfma_records_ok\":%d,\"mfma_checksum_mismatch\":%d,\"mfma_xccs\":%d,\"mfma_us\":%.1f,"
+                "\"mfma_tflops\":%.1f,\"clock_mhz_min\":%.0f,\"clock_mhz_median\":%.0f,\"clock_mhz_max\":%.0f,"
+                "\"xcd_clock_mhz\":%s,\"total_us\":%.1f,\"in_flight_s\":%.2f,\"error\":\"%s\"}",
+                r.ordinal, r.ok ? "true" : "false", r.hsa_error, r.nonce, static_cast<unsigned long long>(r.bytes),
+                r.cu_count, r.num_xcc, r.fill_us, r.check_us, r.hbm_write_gbps, r.hbm_read_gbps,
+                static_cast<unsigned long long>(r.hbm_bad_words), static_cast<long long>(r.hbm_first_bad),
+                r.mfma_iters, r.mfma_grid, r.mfma_records_ok, r.mfma_checksum_mismatch, r.mfma_xccs, r.mfma_us,
+                r.mfma_tflops, r.clock_mhz_min, r.clock_mhz_median, r.clock_mhz_max, per.c_str(), r.total_us,
+                r.in_flight_s, json_escape(r.error).c_str());
+  return buf;
+}
+
+// --perf: the throughput check on each selected GPU (parallel host threads;
+// every GPU has its own HBM and matrix cores).
+bool run_perf(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, uint64_t bytes, int iters,
+              double timeout_s, int n, std::string& json) {
+  std::vector<mi355x_perf_result> res(ords.size());
+  std::vector<int> rcs(ords.size(), 1);
+  auto one = [&](size_t i) {
+    if (ords[i] < 0 || ords[i] >= n) {
+      std::memset(&res[i], 0, sizeof(res[i]));
+      res[i].ordinal = ords[i];
+      std::snprintf(res[i].error, sizeof(res[i].error), "no such GPU (count=%d)", n);
+      return;
+    }
+    rcs[i] = perf_check(ords[i], nonces[i], bytes, iters, timeout_s, &res[i]);
+  };
+  std::vector<std::thread> ths;
+  for (size_t i = 0; i < ords.size(); ++i) ths.emplace_back(one, i);
+  for (auto& t : ths) t.join();
+  bool ok = !ords.empty();
+  json = "[";
+  for (size_t i = 0; i < res.size(); ++i) {
+    ok = ok && rcs[i] == 0;
+    if (i) json += ",";
+    json += perf_json(res[i]);
+  }
+  json += "]";
+  return ok;
+}
+
 std::string devices_json(const std::vector<mi355x_probe_result>& results) {
   std::string o = "[";
   for (size_t i = 0; i < results.size(); ++i) {
@@ -340,9 +407,17 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
     int iters = 0;
     double timeout_s = 0;
     int consumed = 0;
+    unsigned long long perf_mib = 0;
     const bool sweep_req = line.compare(0, 6, "sweep ") == 0;
-    const char* fmt = sweep_req ? "sweep %d %lf %n" : "probe %d %lf %n";
-    if (std::sscanf(line.c_str(), fmt, &iters, &timeout_s, &consumed) < 2 || consumed == 0) {
+    const bool perf_req = line.compare(0, 5, "perf ") == 0;
+    bool parsed;
+    if (perf_req) {  // perf <mfma_iters> <timeout_s> <mib> <ordinal>:<nonce> ...
+      parsed = std::sscanf(line.c_str(), "perf %d %lf %llu %n", &iters, &timeout_s, &perf_mib, &consumed) >= 3;
+    } else {
+      parsed = std::sscanf(line.c_str(), sweep_req ? "sweep %d %lf %n" : "probe %d %lf %n", &iters, &timeout_s,
+                           &consumed) >= 2;
+    }
+    if (!parsed || consumed == 0) {
       std::printf("{\"ok\":false,\"error\":\"bad request\",\"devices\":[]}\n");
       std::fflush(stdout);
       continue;
@@ -369,13 +444,15 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
     bool ok;
     if (sweep_req) {
       ok = run_sweeps(ords, nonces, iters, timeout_s, n, body);
+    } else if (perf_req) {
+      ok = run_perf(ords, nonces, static_cast<uint64_t>(perf_mib) << 20, iters, timeout_s, n, body);
     } else {
       ok = run_batch(ords, nonces, iters, timeout_s, false, n, results);
       body = devices_json(results);
     }
-    std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"sweep\":%s,\"t_ready_ns\":%llu,\"devices\":%s}\n",
-                ok ? "true" : "false", n, sweep_req ? "true" : "false", static_cast<unsigned long long>(mono_ns()),
-                body.c_str());
+    std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"sweep\":%s,\"perf\":%s,\"t_ready_ns\":%llu,\"devices\":%s}\n",
+                ok ? "true" : "false", n, sweep_req ? "true" : "false", perf_req ? "true" : "false",
+                static_cast<unsigned long long>(mono_ns()), body.c_str());
     std::fflush(stdout);
     teardown();  // queues/executables go, the runtime (and the kfd process) stays
   }
@@ -398,6 +475,9 @@ int main(int argc, char** argv) {
   bool keep = false;  // --serve --keep: per-device queue/executable/buffers live across requests
   bool peer_mode = false;
   bool sweep_mode = false;
+  bool perf_mode = false;
+  uint64_t perf_mib = 4096;
+  int perf_iters = 1 << 16;
   uint64_t peer_bytes = 64ull << 20;
   int peer_reps = 3;
   for (int i = 1; i < argc; ++i) {
@@ -435,6 +515,12 @@ int main(int argc, char** argv) {
       peer_mode = true;
     } else if (a == "--sweep") {
       sweep_mode = true;
+    } else if (a == "--perf") {
+      perf_mode = true;
+    } else if (a == "--perf-mib") {
+      perf_mib = std::strtoull(next("--perf-mib"), nullptr, 0);
+    } else if (a == "--perf-iters") {
+      perf_iters = std::atoi(next("--perf-iters"));
     } else if (a == "--peer-bytes") {
       peer_bytes = std::strtoull(next("--peer-bytes"), nullptr, 0);
     } else if (a == "--corrupt-word") {
@@ -444,6 +530,7 @@ int main(int argc, char** argv) {
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
                   "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve [--keep]] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep] "
+                  "[--perf [--perf-mib M] [--perf-iters N]] "
                   "[--corrupt-word K[@ORDINAL]]\n",
                   argv[0]);
       return 0;
@@ -491,6 +578,16 @@ int main(int argc, char** argv) {
   if (peer_mode) return run_peer(ords, nonce, peer_bytes, peer_reps, timeout_s, n);
   std::vector<uint32_t> nonces;
   for (size_t i = 0; i < ords.size(); ++i) nonces.push_back(nonce + static_cast<uint32_t>(i));
+  if (perf_mode) {
+    std::string body;
+    const bool ok = run_perf(ords, nonces, perf_mib << 20, perf_iters, timeout_s, n, body);
+    std::printf("{\"ok\":%s,\"perf\":true,\"hip_device_count\":%d,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
+                "\"t_ready_ns\":%llu,\"devices\":%s}\n",
+                ok ? "true" : "false", n, static_cast<unsigned long long>(t_start),
+                static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(mono_ns()), body.c_str());
+    std::fflush(stdout);
+    return ok ? 0 : 1;
+  }
   if (sweep_mode) {
     std::string body;
     const bool ok = run_sweeps(ords, nonces, iters, timeout_s, n, body);

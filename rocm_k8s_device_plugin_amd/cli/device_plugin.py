@@ -68,6 +68,15 @@ def build_parser() -> flags.GoFlagParser:
     p.add_float("liveness_unknown_busy_grace", 30.0, "the busy grace while busy GPUs cannot be told from idle ones "
                                                      "(kfd process list unreadable): every GPU counts as busy, "
                                                      "so the grace is shorter")
+    p.add_int("perf_check_every", 0, "every N-th pulse (and the first) run the throughput check on GPUs with no "
+                                      "running work: HBM write/read bandwidth over a verified pattern, sustained "
+                                      "bf16 MFMA rate, per-XCD clocks (~40 ms of the chip); 0 = off")
+    p.add_int("perf_mib", 4096, "throughput check: HBM buffer (MiB)")
+    p.add_str("perf_action", "report", "a GPU under the throughput floors is logged and exported (report) or also "
+                                       "withdrawn until a check passes (unhealthy); wrong data is always a failure")
+    p.add_float("perf_min_hbm_read_gbps", 3000.0, "throughput floor: HBM read GB/s per whole MI355X")
+    p.add_float("perf_min_mfma_tflops", 700.0, "throughput floor: dense bf16 MFMA TFLOP/s per whole MI355X")
+    p.add_float("perf_min_xcd_clock_ratio", 0.6, "throughput floor: slowest XCD's clock over the median XCD's")
     p.add_bool("smi_ecc", False, "mark a device Unhealthy when its amd-smi uncorrectable ECC count rises")
     p.add_bool("smi_events", False, "subscribe to amd-smi GPU events; a device is Unhealthy between a "
                                     "gpu_pre_reset and its gpu_post_reset, other events are counted")
@@ -122,6 +131,10 @@ def validate(ns) -> Optional[str]:
         return str(e)
     if ns.liveness_mode not in ("persistent", "spawn"):
         return f"invalid liveness_mode provided: {ns.liveness_mode}, supported values are persistent or spawn"
+    if ns.perf_action not in ("report", "unhealthy"):
+        return f"invalid perf_action provided: {ns.perf_action}, supported values are report or unhealthy"
+    if ns.perf_check_every > 0 and not ns.liveness:
+        return "perf_check_every needs -liveness (the throughput check runs in the probe server)"
     if ns.grpc_server not in ("native", "aio"):
         return f"invalid grpc_server provided: {ns.grpc_server}, supported values are native or aio"
     return None
@@ -146,7 +159,11 @@ def create_impl(name: str, ns, device_count: Optional[int]) -> DeviceImpl:
                           liveness_busy_grace_s=ns.liveness_busy_grace,
                           liveness_unknown_busy_grace_s=ns.liveness_unknown_busy_grace,
                           liveness_corroborate=ns.liveness_corroborate,
-                          liveness_crowded_procs=ns.liveness_crowded_procs)
+                          liveness_crowded_procs=ns.liveness_crowded_procs,
+                          perf_check_every=ns.perf_check_every, perf_mib=ns.perf_mib, perf_action=ns.perf_action,
+                          perf_min_hbm_read_gbps=ns.perf_min_hbm_read_gbps,
+                          perf_min_mfma_tflops=ns.perf_min_mfma_tflops,
+                          perf_min_xcd_clock_ratio=ns.perf_min_xcd_clock_ratio)
         view_dir = os.path.join(ns.kubelet_dir, "mi355x-topology") if ns.topology_view else None
         node_dir = os.path.join(ns.kubelet_dir, "mi355x-node") if ns.node_view else None
         from .. import cdi

@@ -149,6 +149,9 @@ class LivenessProber:
         # gets no queue, no ROCr state and no runlist slot from the server.
         self._visible: Optional[tuple] = None
         self._server_visible: Optional[tuple] = None
+        # throughput check (kind "perf"): HBM buffer size and MFMA pairs per wave
+        self.perf_mib = 4096
+        self.perf_iters = 1 << 16
 
     @property
     def server_running(self) -> bool:
@@ -235,7 +238,11 @@ class LivenessProber:
     async def probe_ordinal(self, ordinal: int, nonce: Optional[int] = None, kind: str = "probe") -> ProbeOutcome:
         nonce = self._nonce(ordinal) if nonce is None else nonce
         argv = [*self.argv_prefix, self._exe(), "--devices", "0", "--iters", str(self.iters), "--nonce", str(nonce),
-                "--timeout", f"{max(0.5, self.timeout_s - 0.5):.2f}"] + (["--sweep"] if kind == "sweep" else [])
+                "--timeout", f"{max(0.5, self.timeout_s - 0.5):.2f}"]
+        if kind == "sweep":
+            argv.append("--sweep")
+        elif kind == "perf":
+            argv += ["--perf", "--perf-mib", str(self.perf_mib), "--perf-iters", str(self.perf_iters)]
         t0 = time.perf_counter()
         try:
             proc = await asyncio.create_subprocess_exec(
@@ -255,7 +262,7 @@ class LivenessProber:
             # this is inconclusive (HealthMonitor applies the busy grace), as in
             # the kept-queue server
             return ProbeOutcome(False, f"deadline exceeded ({self.timeout_s:.1f}s)",
-                                (time.perf_counter() - t0) * 1e3, pending=kind != "sweep")
+                                (time.perf_counter() - t0) * 1e3, pending=kind == "probe")
         dt = (time.perf_counter() - t0) * 1e3
         try:
             doc = json.loads(out.decode().strip().splitlines()[-1])
@@ -292,7 +299,9 @@ class LivenessProber:
         nonces = {o: self._nonce(o) for o in uniq}
         # the server's own dispatch wait ends before our deadline for the reply
         inner = self.timeout_s - min(0.5, 0.25 * self.timeout_s)
-        line = f"{kind} {self.iters} {inner:.2f} " + " ".join(f"{local[o]}:{nonces[o]}" for o in uniq)
+        head = f"perf {self.perf_iters} {inner:.2f} {self.perf_mib}" if kind == "perf" else \
+            f"{kind} {self.iters} {inner:.2f}"
+        line = head + " " + " ".join(f"{local[o]}:{nonces[o]}" for o in uniq)
         doc = await self._server.request(line, self.timeout_s)
         dt = (time.perf_counter() - t0) * 1e3
         by_ord = {}
@@ -306,9 +315,9 @@ class LivenessProber:
             if d is None:
                 out[o] = ProbeOutcome(False, "device missing from probe server reply", dt)
                 continue
-            if kind == "sweep":
-                # sweeps run on their own queue: the kept probe slot (and its
-                # pending dispatch, if any) is untouched by them
+            if kind in ("sweep", "perf"):
+                # sweeps and throughput checks run on their own queue: the kept
+                # probe slot (and its pending dispatch, if any) is untouched by them
                 out[o] = self._judge(bool(d.get("ok")), d, nonces[o], dt)
                 continue
             # a late verdict answers the dispatch (and nonce) of the probe that left it pending
@@ -337,6 +346,14 @@ class LivenessProber:
         It holds each CU's whole LDS for ~50 us and waits for the entire grid to
         be resident, so callers run it only on GPUs without foreign work."""
         return await self.probe(ordinals, kind="sweep")
+
+    async def perf(self, ordinals: Mapping[str, int]) -> Dict[str, ProbeOutcome]:
+        """The throughput check (HBM pattern write/read bandwidth, sustained bf16
+        MFMA rate, per-XCD shader clocks; liveness_kernel.h). `ok` covers
+        correctness only (every word read back exact, identical MFMA checksums,
+        every XCD ran); the rates are in `detail` for the caller's thresholds.
+        It owns the chip for tens of ms: idle GPUs only."""
+        return await self.probe(ordinals, kind="perf")
 
     async def _confirm_failures(self, failed, results, kind: str) -> Dict[int, ProbeOutcome]:
         """Re-probe the devices the server failed, each in a fresh process.

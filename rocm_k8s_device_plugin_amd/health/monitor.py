@@ -91,6 +91,23 @@ class HealthConfig:
     liveness_crowded_procs: int = 7
     liveness_crowded_release_sweeps: int = 5   # uncrowded sweeps before the server takes the GPU back
     recover_threshold: int = 1
+    # throughput check (opt-in): every N-th sweep (and the first), GPUs with no
+    # other process's queues get HBM write/read bandwidth over a verified
+    # pattern, the sustained bf16 MFMA rate and per-XCD shader clocks
+    # (LivenessProber.perf, ~40 ms of the chip per GPU at the defaults). Data
+    # read back wrong is always a failure; rates under the floors (scaled by the
+    # device's share of a whole MI355X's 256 CUs) or an XCD clocked far below
+    # its siblings make the GPU "degraded": logged and exported, and with
+    # perf_action "unhealthy" withdrawn until a later check passes. Floors are
+    # about half of what an MI355X measures (profiles/README.md §10).
+    perf_check_every: int = 0
+    perf_mib: int = 4096
+    perf_mfma_iters: int = 65536
+    perf_action: str = "report"             # report | unhealthy
+    perf_min_hbm_read_gbps: float = 3000.0
+    perf_min_hbm_write_gbps: float = 2000.0
+    perf_min_mfma_tflops: float = 700.0
+    perf_min_xcd_clock_ratio: float = 0.6   # slowest XCD's clock over the median XCD's
     smi_ecc: bool = False
     smi_events: bool = False
     smi_xgmi: bool = False             # watch xGMI link state (placement input, health/fabric.py)
@@ -144,6 +161,9 @@ class HealthMonitor:
         self._load: Dict[int, Tuple[int, int]] = {}  # kfd gpu_id -> (other processes, their queues)
         self._crowded: Dict[str, int] = {}          # device -> uncrowded sweeps seen since it got crowded
         self.crowded_skips = 0
+        self._perf: Dict[str, Tuple[str, str]] = {}  # device -> (ok | degraded | failed, reason)
+        self.perf_last: Dict[str, dict] = {}         # device -> last throughput-check reply
+        self.perf_checks = 0
 
     # ------------------------------------------------------------------ fabric
     def degraded_links(self):
@@ -459,6 +479,66 @@ class HealthMonitor:
             out.update(await self.prober.probe(rest, busy=busy))
         return out
 
+    # ------------------------------------------------------------ throughput
+    PERF_STATES = {"ok": 0.0, "degraded": 1.0, "failed": 2.0}
+
+    def perf_problems(self, d: dict) -> list:
+        """Why a (correct) throughput-check reply counts as degraded; [] if not."""
+        c = self.cfg
+        cus = int(d.get("cu_count") or 0)
+        share = min(1.0, cus / 256.0) if cus > 0 else 1.0   # a CPX partition has 1/8 of the CUs
+        out = []
+        for key, floor, what, unit in (("hbm_read_gbps", c.perf_min_hbm_read_gbps, "HBM read", "GB/s"),
+                                       ("hbm_write_gbps", c.perf_min_hbm_write_gbps, "HBM write", "GB/s"),
+                                       ("mfma_tflops", c.perf_min_mfma_tflops, "bf16 MFMA", "TFLOP/s")):
+            v = float(d.get(key) or 0.0)
+            if floor > 0 and v < floor * share:
+                out.append(f"{what} {v:.0f} {unit} < {floor * share:.0f}")
+        clocks = [float(x) for x in (d.get("xcd_clock_mhz") or []) if x and float(x) > 0]
+        if len(clocks) >= 2 and c.perf_min_xcd_clock_ratio > 0:
+            med = sorted(clocks)[len(clocks) // 2]
+            i = min(range(len(clocks)), key=clocks.__getitem__)
+            if clocks[i] < c.perf_min_xcd_clock_ratio * med:
+                out.append(f"XCD {i} at {clocks[i]:.0f} MHz vs median {med:.0f} MHz under MFMA load")
+        return out
+
+    async def _perf_check(self, ords: Dict[str, int]) -> None:
+        from ..utils.metrics import REGISTRY
+        p = self.prober
+        p.perf_mib, p.perf_iters = self.cfg.perf_mib, self.cfg.perf_mfma_iters
+        with TRACER.span("health.perf_check", "health", devices=len(ords)):
+            res = await p.perf(ords)
+        self.perf_checks += 1
+        REGISTRY.inc("mi355x_dp_perf_checks_total", help="throughput checks run (HBM pattern + MFMA + clocks)")
+        for dev, o in res.items():
+            d = o.detail or {}
+            self.perf_last[dev] = d
+            if not o.ok:
+                state, why = "failed", f"throughput check: {o.reason}"
+            else:
+                probs = self.perf_problems(d)
+                state, why = ("degraded", "throughput check: " + "; ".join(probs)) if probs else ("ok", "")
+            prev = self._perf.get(dev, ("ok", ""))[0]
+            if state != prev:
+                (_log.info if state == "ok" else _log.warning)("device %s: throughput check %s -> %s %s", dev, prev,
+                                                               state, why)
+            self._perf[dev] = (state, why)
+            REGISTRY.set("mi355x_dp_perf_state", self.PERF_STATES[state],
+                         help="last throughput check: 0 ok, 1 degraded (rates under the floors), 2 failed", device=dev)
+            if o.ok:
+                for key, name, hlp in (("hbm_read_gbps", "mi355x_dp_perf_hbm_read_gbps", "HBM read bandwidth"),
+                                       ("hbm_write_gbps", "mi355x_dp_perf_hbm_write_gbps", "HBM write bandwidth"),
+                                       ("mfma_tflops", "mi355x_dp_perf_mfma_tflops", "sustained dense bf16 MFMA rate"),
+                                       ("clock_mhz_median", "mi355x_dp_perf_clock_mhz",
+                                        "median workgroup shader clock under MFMA load")):
+                    REGISTRY.set(name, float(d.get(key) or 0.0), help=f"last throughput check: {hlp}", device=dev)
+                for x, mhz in enumerate(d.get("xcd_clock_mhz") or []):
+                    REGISTRY.set("mi355x_dp_perf_xcd_clock_mhz", float(mhz),
+                                 help="last throughput check: median shader clock per XCD", device=dev, xcd=str(x))
+
+    def perf_verdicts(self) -> Dict[str, Tuple[str, str]]:
+        return dict(self._perf)
+
     # ------------------------------------------------------------------ sweep
     async def close(self) -> None:
         if self.prober is not None:
@@ -563,6 +643,16 @@ class HealthMonitor:
             for dev_id in reasons:
                 if dev_id not in ords:
                     reasons[dev_id].append("no HIP device for this ID (render node inaccessible?)")
+            every = self.cfg.perf_check_every
+            if every > 0 and self.sweeps % every == 0:
+                idle = self._idle_devices(probe_ords)
+                cand = {k: v for k, v in probe_ords.items() if k in idle and self._track[k].live and k in ords}
+                if cand:
+                    await self._perf_check(cand)
+            for dev_id, (state, why) in self._perf.items():
+                if dev_id in reasons and (state == "failed" or
+                                          (state == "degraded" and self.cfg.perf_action == "unhealthy")):
+                    reasons[dev_id].append(why)
 
         if self.cfg.smi_ecc:
             for dev_id, r in (await asyncio.to_thread(self._smi_ecc)).items():   # amd-smi off the event loop

@@ -10,6 +10,8 @@ per ROCr ordinal comes from the JSON file named by $MI355X_STUB_PROBE_CONTROL
 Exercises the real LivenessProber code path: process spawn, server protocol,
 deadline kill, fallback to per-device isolation, output parsing, nonce check,
 hysteresis. Each start appends a line to $MI355X_STUB_PROBE_LOG if set.
+Throughput-check replies ("perf" requests / --perf) follow the control file's
+"perf" map, e.g. ``{"perf": {"3": "slow_xcd", "4": "corrupt"}}``.
 """
 import json
 import os
@@ -42,6 +44,24 @@ def _device(ordinal_reported, mode, nonce, host_ordinal=None):
             "total_us": 5.0, "arch": "gfx950", "name": "", "uuid": "", "pci_domain": 0,
             "pci_bus": 0, "pci_device": 0, "cu_count": 256, "total_mem": 0,
             "error": "" if ok or mode == "stale" else "17/1024 MFMA results differ from host reference"}
+
+
+def _perf_device(ordinal_reported, mode, nonce, host_ordinal=None):
+    """Throughput-check reply (kind "perf"); modes from the control file's
+    "perf" map: slow_hbm, slow_mfma, slow_xcd (one XCD at a third of the clock),
+    corrupt (HBM words read back wrong)."""
+    xcd = [1530.0] * 8
+    if mode == "slow_xcd":
+        xcd[3] = 510.0
+    d = {**_identity(ordinal_reported if host_ordinal is None else host_ordinal),
+         "ordinal": ordinal_reported, "ok": mode != "corrupt", "hsa_error": 0, "nonce": nonce, "bytes": 4 << 30,
+         "cu_count": 256, "num_xcc": 8, "hbm_write_gbps": 4600.0, "hbm_read_gbps": 1500.0 if mode == "slow_hbm" else 6000.0,
+         "hbm_bad_words": 3 if mode == "corrupt" else 0, "hbm_first_bad": 4096 if mode == "corrupt" else -1,
+         "mfma_iters": 65536, "mfma_grid": 512, "mfma_records_ok": 512, "mfma_checksum_mismatch": 0, "mfma_xccs": 8,
+         "mfma_tflops": 400.0 if mode == "slow_mfma" else 1550.0, "clock_mhz_min": min(xcd), "clock_mhz_median": 1530.0,
+         "clock_mhz_max": max(xcd), "xcd_clock_mhz": xcd, "total_us": 35000.0, "in_flight_s": 0.0,
+         "error": "hbm_bad_words=3 first_bad_unit=4096" if mode == "corrupt" else ""}
+    return d
 
 
 def _kfd_entry():
@@ -84,9 +104,13 @@ def serve():
         kind = parts[0]
         ctl = _control()
         devs = []
-        for tok in parts[3:]:
+        for tok in parts[4:] if kind == "perf" else parts[3:]:
             o, n = tok.split(":")
             hosto = vis[int(o)] if vis and int(o) < len(vis) else o
+            if kind == "perf":
+                devs.append(_perf_device(int(o), ctl.get("perf", {}).get(hosto, "ok"), int(n, 0),
+                                         host_ordinal=int(hosto)))
+                continue
             mode = ctl.get(hosto, "ok")
             if mode == "server_fail":
                 mode = "fail"
@@ -130,6 +154,10 @@ def main(argv):
         if a == "--nonce":
             nonce = int(argv[i + 1], 0)
     ordinal = os.environ.get("ROCR_VISIBLE_DEVICES", "0").split(",")[0]
+    if "--perf" in argv:
+        d = _perf_device(0, _control().get("perf", {}).get(ordinal, "ok"), nonce, host_ordinal=int(ordinal))
+        print(json.dumps({"ok": d["ok"], "perf": True, "hip_device_count": 1, "devices": [d]}))
+        return 0 if d["ok"] else 1
     mode = _control().get(ordinal, "ok")
     if mode == "server_fail":
         mode = "ok"

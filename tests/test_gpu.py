@@ -503,6 +503,39 @@ def test_chip_sweep_covers_every_cu_and_xcd(ordinals):
     assert r.ok and r.detail["cus_covered"] == r.detail["cu_count"], r
 
 
+def test_perf_check_measures_hbm_and_mfma(ordinals):
+    """Throughput check on the real GPU: the HBM pattern reads back exact, every
+    XCD runs MFMA workgroups with identical checksums, and the rates are those
+    of a healthy MI355X (well above the monitor's default floors)."""
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    o = sorted(ordinals.values())[0]
+    env = dict(os.environ, ROCR_VISIBLE_DEVICES=str(o))
+    p = subprocess.run([str(probe_executable("hsa")), "--perf", "--perf-mib", "2048", "--perf-iters", "32768",
+                        "--devices", "0", "--timeout", "20"], stdout=subprocess.PIPE, env=env, timeout=120)
+    d = json.loads(p.stdout.decode().strip().splitlines()[-1])["devices"][0]
+    assert p.returncode == 0 and d["ok"], d
+    assert d["hbm_bad_words"] == 0 and d["hbm_first_bad"] == -1 and d["mfma_checksum_mismatch"] == 0, d
+    assert d["mfma_records_ok"] == d["mfma_grid"] == 2 * d["cu_count"] and d["mfma_xccs"] == d["num_xcc"] == 8, d
+    floors = HealthConfig()
+    assert d["hbm_read_gbps"] > floors.perf_min_hbm_read_gbps, d
+    assert d["hbm_write_gbps"] > floors.perf_min_hbm_write_gbps, d
+    assert d["mfma_tflops"] > floors.perf_min_mfma_tflops, d
+    assert all(500 < c < 2500 for c in d["xcd_clock_mhz"]), d
+    # the monitor's path: the persistent server's "perf" request
+    prober = LivenessProber(timeout_s=60)
+    prober.perf_mib, prober.perf_iters = 1024, 16384
+
+    async def go():
+        res = await prober.perf({"gpu": o})
+        await prober.close()
+        return res["gpu"]
+
+    r = asyncio.run(go())
+    assert r.ok and r.detail["hbm_bad_words"] == 0 and r.detail["mfma_xccs"] == 8, r
+
+
 def test_node_labeller_on_real_mi355x():
     """All label kinds on the real node: schema keys present and MI355X values."""
     from rocm_k8s_device_plugin_amd import constants as C
