@@ -536,6 +536,32 @@ def test_perf_check_measures_hbm_and_mfma(ordinals):
     assert r.ok and r.detail["hbm_bad_words"] == 0 and r.detail["mfma_xccs"] == 8, r
 
 
+def test_monitor_perf_check_on_idle_gpu(inv, ordinals):
+    """The health monitor's cadence: liveness, then the throughput check on the
+    idle GPU in the same sweep; a healthy MI355X clears every floor."""
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig, HealthMonitor
+    from rocm_k8s_device_plugin_amd.topology import Inventory
+    accessible = tuple(d for d in inv.devices if d.id in ordinals)
+    sub = Inventory(sysfs_root="/sys", devices=accessible, topology=inv.topology, driver_loaded=True,
+                    kfd_present=True)
+    mon = HealthMonitor(sub, HealthConfig(exporter_socket=None, liveness=True, perf_check_every=1, perf_mib=1024,
+                                          perf_mfma_iters=16384, perf_action="unhealthy"),
+                        ordinal_map={d.id: ordinals[d.id] for d in accessible})
+    # this pytest process holds HIP queues on the GPU from earlier tests, so the
+    # kfd process list (rightly) shows it busy; idle detection is CPU-tested
+    mon._idle_devices = lambda dev_ids: set(dev_ids)
+
+    async def go():
+        await mon.check_once()
+        await mon.close()
+
+    asyncio.run(go())
+    assert mon.perf_checks == 1
+    assert all(state == "ok" for state, _ in mon.perf_verdicts().values()), mon.perf_verdicts()
+    assert all(v.health == "Healthy" for v in mon.snapshot().values()), mon.snapshot()
+    assert all(d["mfma_tflops"] > 700 for d in mon.perf_last.values()), mon.perf_last
+
+
 def test_node_labeller_on_real_mi355x():
     """All label kinds on the real node: schema keys present and MI355X values."""
     from rocm_k8s_device_plugin_amd import constants as C
