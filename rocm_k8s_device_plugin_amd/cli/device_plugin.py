@@ -240,6 +240,14 @@ async def dry_run_report(impl: Optional[DeviceImpl], sweep: bool) -> dict:
         fab = mon.fabric
         out["xgmi"] = {"readings": fab.readings, "error": fab.error,
                        "degraded_pairs": [list(p) for p in sorted(fab.degraded)], "links_down": fab.links_down}
+    if mon is not None and getattr(mon, "perf_last", None):
+        # -perf_check_every: the first sweep ran the throughput check on the idle GPUs
+        keys = ("hbm_write_gbps", "hbm_read_gbps", "hbm_bad_words", "mfma_tflops", "clock_mhz_median",
+                "xcd_clock_mhz", "total_us")
+        out["throughput"] = {dev: {"state": mon.perf_verdicts().get(dev, ("ok", ""))[0],
+                                   "reason": mon.perf_verdicts().get(dev, ("ok", ""))[1],
+                                   **{k: d.get(k) for k in keys if k in d}}
+                             for dev, d in sorted(mon.perf_last.items())}
     await impl.close()
     return out
 

@@ -110,3 +110,16 @@ def test_perf_cli_validation(tmp_path):
     bad = subprocess.run(base + ["-liveness", "-perf_check_every", "5", "-perf_action", "drain"], capture_output=True,
                          text=True, timeout=120, env=env)
     assert bad.returncode != 0 and "perf_action" in bad.stderr
+
+
+def test_perf_in_dry_run(tmp_path):
+    """-dry_run with -pulse and -perf_check_every reports each idle GPU's throughput."""
+    from rocm_k8s_device_plugin_amd.cli.device_plugin import dry_run_report
+    from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+    fi, ctl, mon = _monitor(tmp_path, {"perf": {"2": "slow_hbm"}})
+    impl = ContainerImpl("single", str(fi.sysfs), inventory=mon.inv, monitor=mon)
+    doc = asyncio.run(asyncio.wait_for(dry_run_report(impl, sweep=True), 60))
+    thr = doc["throughput"]
+    assert len(thr) == 8 and thr[fi.bdfs[2]]["state"] == "degraded" and "HBM read 1500" in thr[fi.bdfs[2]]["reason"]
+    assert thr[fi.bdfs[0]]["state"] == "ok" and thr[fi.bdfs[0]]["hbm_read_gbps"] == 6000.0
+    json.dumps(doc)
