@@ -97,7 +97,8 @@ def load_kubeconfig(path: str) -> KubeConfig:
     )
 
 
-def in_cluster_config(sa_dir: str = SA_DIR) -> KubeConfig:
+def in_cluster_config(sa_dir: Optional[str] = None) -> KubeConfig:
+    sa_dir = sa_dir or SA_DIR
     host = os.environ.get("KUBERNETES_SERVICE_HOST")
     port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
     if not host:

@@ -29,7 +29,7 @@ def merge_patch(target, patch):
 
 
 class FakeApiServer:
-    def __init__(self, token: Optional[str] = "test-token"):
+    def __init__(self, token: Optional[str] = "test-token", tls: Optional[Tuple[str, str]] = None):
         self.token = token
         self.nodes: Dict[str, dict] = {}
         self.requests: List[Tuple[str, str, Optional[dict]]] = []
@@ -158,11 +158,22 @@ class FakeApiServer:
                 self._handle("PUT")
 
         self.httpd = ThreadingHTTPServer(("127.0.0.1", 0), Handler)
+        self.scheme = "http"
+        if tls is not None:   # (cert chain PEM, key PEM): serve HTTPS like a real apiserver
+            import ssl
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(*tls)
+            self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True)
+            self.scheme = "https"
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
 
     @property
+    def port(self) -> int:
+        return self.httpd.server_address[1]
+
+    @property
     def url(self) -> str:
-        return f"http://127.0.0.1:{self.httpd.server_address[1]}"
+        return f"{self.scheme}://127.0.0.1:{self.port}"
 
     def _store(self, name: str, node: dict, event: str) -> None:
         """(lock held) bump the resourceVersion, store, notify watchers."""

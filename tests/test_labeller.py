@@ -421,3 +421,60 @@ def test_watch_failure_backs_off_and_resync_still_applies(tmp_path):
             lab.stop()
             t.join(5)
         srv.stop()
+
+
+def _tls_material(d):
+    """A CA and a server certificate for 127.0.0.1 signed by it (openssl CLI)."""
+    import shutil
+    import subprocess
+    if not shutil.which("openssl"):
+        pytest.skip("openssl not installed")
+
+    def run(*a):
+        subprocess.run(["openssl", *a], check=True, capture_output=True, timeout=60)
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "ca.key"), "-out", str(d / "ca.crt"),
+        "-days", "2", "-subj", "/CN=test-ca")
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "srv.key"), "-out", str(d / "srv.csr"),
+        "-subj", "/CN=kubernetes")
+    (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1,DNS:kubernetes.default.svc\n")
+    run("x509", "-req", "-in", str(d / "srv.csr"), "-CA", str(d / "ca.crt"), "-CAkey", str(d / "ca.key"),
+        "-CAcreateserial", "-out", str(d / "srv.crt"), "-days", "2", "-extfile", str(d / "ext.cnf"))
+    return str(d / "srv.crt"), str(d / "srv.key"), str(d / "ca.crt")
+
+
+def test_labeller_in_cluster_over_tls(tmp_path, monkeypatch):
+    """The production path: in-cluster service-account token and CA bundle, HTTPS
+    with certificate verification (main.go uses controller-runtime's
+    GetConfigOrDie, which resolves to the same in-cluster config)."""
+    from rocm_k8s_device_plugin_amd.cli import node_labeller
+    from rocm_k8s_device_plugin_amd.labeller import kube
+    crt, key, ca = _tls_material(tmp_path)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="sa-token", tls=(crt, key)).start()
+    try:
+        srv.add_node("worker-9")
+        sa = tmp_path / "sa"
+        sa.mkdir()
+        (sa / "token").write_text("sa-token\n")
+        (sa / "ca.crt").write_text(open(ca).read())
+        monkeypatch.setattr(kube, "SA_DIR", str(sa))
+        monkeypatch.delenv("KUBECONFIG", raising=False)
+        monkeypatch.setenv("KUBERNETES_SERVICE_HOST", "127.0.0.1")
+        monkeypatch.setenv("KUBERNETES_SERVICE_PORT", str(srv.port))
+        cfg = kube.in_cluster_config(str(sa))
+        assert cfg.server == f"https://127.0.0.1:{srv.port}" and cfg.ca_file == str(sa / "ca.crt")
+        rc = node_labeller.main(["-node_name", "worker-9", "-resync", "0", "-mode", "-cu-count",
+                                 "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)])
+        assert rc == 0
+        got = srv.labels("worker-9")
+        assert got["amd.com/gpu.mode"] == "container" and got["amd.com/gpu.cu-count"] == "256"
+        # a CA that did not sign the server certificate is refused, not ignored
+        other = tmp_path / "other"
+        other.mkdir()
+        _, _, bad_ca = _tls_material(other)
+        bad = KubeClient(KubeConfig(server=cfg.server, token="sa-token", ca_file=bad_ca))
+        with pytest.raises(Exception) as ei:
+            bad.get_node("worker-9")
+        assert "CERTIFICATE_VERIFY_FAILED" in str(ei.value) or "certificate verify failed" in str(ei.value)
+    finally:
+        srv.stop()
