@@ -403,7 +403,7 @@ static void test_grpc_server() {
 // Random and mutated input for the HPACK decoder and the HTTP/2 frame parser:
 // nothing may crash or hang (run under ASan/UBSan by the sanitizer ctest), and
 // the server must keep answering a well-formed client afterwards.
-static void test_fuzz_rpc() {
+static void test_fuzz_rpc(const std::string& ref) {
   using namespace mi355x::rpc;
   uint64_t x = 0x9E3779B97F4A7C15ull;
   auto rnd = [&x]() {
@@ -469,6 +469,60 @@ static void test_fuzz_rpc() {
   const std::string req = h2t::request(1, "/v1beta1.DevicePlugin/GetDevicePluginOptions", "");
   CHECK(fd >= 0 && ::write(fd, req.data(), req.size()) == static_cast<ssize_t>(req.size()) &&
         h2t::read_call(fd, 1, &r, &dec) && r.grpc_status == 0 && r.messages.size() == 1);
+  // well-formed calls with random / mutated protobuf bodies: every one gets a
+  // gRPC status (the allocator on the reference's MI300X CPX capture when present)
+  auto topo = KfdTopology::load(ref + "/topo-mi300-cpx/topology/nodes");
+  const auto devs = synthetic_devices(8, 8, 2, 2, 64);
+  if (!topo.nodes().empty()) {
+    auto a = std::make_shared<HiveAllocator>();
+    CHECK(a->init(devs, topo).empty());
+    svc.set_allocator(a);
+  }
+  AllocateTemplate t;
+  t.resource = "gpu";
+  for (const auto& d : devs) t.per_device[d.id] = "spec-" + d.id;
+  svc.set_allocate_template(t);
+  std::string pref_ok, alloc_ok;
+  {
+    std::string c;
+    for (int i = 0; i < 12; ++i) pb::put_bytes(&c, 1, devs[i].id);
+    pb::put_bytes(&c, 2, devs[3].id);
+    pb::put_varint(&c, (3 << 3) | 0);
+    pb::put_varint(&c, 4);
+    pb::put_bytes(&pref_ok, 1, c);
+    std::string ac;
+    pb::put_bytes(&ac, 1, devs[0].id);
+    pb::put_bytes(&ac, 1, devs[9].id);
+    pb::put_bytes(&alloc_ok, 1, ac);
+  }
+  const char* methods[] = {"GetPreferredAllocation", "Allocate", "PreStartContainer", "GetDevicePluginOptions"};
+  int answered = 0, ok_calls = 0;
+  uint32_t sid = 3;
+  for (int i = 0; i < 3000 && fd >= 0; ++i, sid += 2) {
+    const int m = static_cast<int>(rnd() % 4);
+    std::string body = m == 0 ? pref_ok : alloc_ok;
+    switch (rnd() % 4) {
+      case 0:
+        break;  // valid
+      case 1:   // a few random bytes changed
+        for (int k = 0; k < 1 + static_cast<int>(rnd() % 3); ++k) body[rnd() % body.size()] = static_cast<char>(rnd());
+        break;
+      case 2:   // truncated
+        body.resize(rnd() % body.size());
+        break;
+      default:  // random bytes
+        body.assign(rnd() % 48, '\0');
+        for (auto& ch : body) ch = static_cast<char>(rnd());
+    }
+    h2t::Result rr;
+    const std::string q = h2t::request(sid, std::string("/v1beta1.DevicePlugin/") + methods[m], body);
+    if (::write(fd, q.data(), q.size()) != static_cast<ssize_t>(q.size()) || !h2t::read_call(fd, sid, &rr, &dec)) break;
+    answered += rr.grpc_status >= 0;
+    ok_calls += rr.grpc_status == 0;
+  }
+  CHECK(answered == 3000);
+  CHECK(ok_calls > 300);
+  svc.drain_events();
   if (fd >= 0) ::close(fd);
   srv.stop(0.1);
   ::unlink(sock.c_str());
@@ -485,7 +539,7 @@ int main(int argc, char** argv) {
   test_degraded_links(ref);
   test_hpack();
   test_grpc_server();
-  test_fuzz_rpc();
+  test_fuzz_rpc(ref);
   std::printf("test_core: %d passed, %d failed, %d skipped\n", g_pass, g_fail, g_skip);
   return g_fail ? 1 : 0;
 }
