@@ -523,6 +523,10 @@ class HealthMonitor:
                 (_log.info if state == "ok" else _log.warning)("device %s: throughput check %s -> %s %s", dev, prev,
                                                                state, why)
             self._perf[dev] = (state, why)
+            if log.V(2) and o.ok:
+                _log.info("device %s: throughput HBM write %.0f / read %.0f GB/s, bf16 MFMA %.0f TFLOP/s at %.0f MHz "
+                          "(XCD clocks %s)", dev, d.get("hbm_write_gbps", 0), d.get("hbm_read_gbps", 0),
+                          d.get("mfma_tflops", 0), d.get("clock_mhz_median", 0), d.get("xcd_clock_mhz"))
             REGISTRY.set("mi355x_dp_perf_state", self.PERF_STATES[state],
                          help="last throughput check: 0 ok, 1 degraded (rates under the floors), 2 failed", device=dev)
             if o.ok:
