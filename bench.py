@@ -111,7 +111,7 @@ def make_parser():
                          "reported in extra.fragmented_n_of_m (BASELINE config: full-node hive-aware allocation)")
     ap.add_argument("--grpc-server", default="native", choices=["native", "aio"],
                     help="the plugin's kubelet-facing gRPC server (-grpc_server)")
-    ap.add_argument("--kubelet-client", default="", choices=["", "native", "aio"],
+    ap.add_argument("--kubelet-client", default="", choices=["", "native", "native-thread", "aio"],
                     help="the fake kubelet's admission RPC client: native (a native HTTP/2 client, like kubelet's "
                          "grpc-go) or aio (grpc.aio in the bench's event loop); default native with the native server")
     ap.add_argument("--json-out", default="")
@@ -319,6 +319,8 @@ def main():
                 if hp > 0 else HealthConfig(exporter_socket=None))
         loop = asyncio.new_event_loop()
         kclient = args.kubelet_client or ("native" if args.grpc_server == "native" else "aio")
+        if kclient == "native" and args.grpc_server != "native":
+            kclient = "native-thread"   # a blocking call on the loop that serves grpc.aio would deadlock
         plug = PluginUnderTest(loop, tmp, "device-plugins", sysfs, adv, full, ords, hcfg, hp,
                                grpc_server=args.grpc_server, kubelet_client=kclient)
         impl, inv = plug.impl, plug.inv

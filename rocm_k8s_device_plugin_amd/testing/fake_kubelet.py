@@ -67,7 +67,7 @@ class NativeRpcError(grpc.RpcError):
 
 
 class FakeKubelet:
-    RPC_CLIENTS = ("aio", "native")
+    RPC_CLIENTS = ("aio", "native", "native-thread")
 
     def __init__(self, plugin_dir: str, rpc_client: str = "aio"):
         """`rpc_client`: how admit() calls GetPreferredAllocation / Allocate.
@@ -75,7 +75,9 @@ class FakeKubelet:
         "native": the native blocking HTTP/2 client (core().GrpcClient) -- a
         kubelet-like native caller, for timing the plugin rather than the
         interpreter. It blocks the loop for the call, so the plugin must not be
-        served from this same loop (use it with the native server only)."""
+        served from this same loop (use it with the native server only);
+        "native-thread": the same client called from a worker thread (works with
+        any server, at the cost of a thread hop per call)."""
         if rpc_client not in self.RPC_CLIENTS:
             raise ValueError(f"rpc_client must be one of {self.RPC_CLIENTS}")
         self.rpc_client = rpc_client
@@ -251,7 +253,11 @@ class FakeKubelet:
             if err:
                 st.native = None
                 raise NativeRpcError(-1, err)
-        status, msg, body = st.native.unary(f"/{pb.PACKAGE}.DevicePlugin/{method}", req.SerializeToString(), 10.0)
+        path, data = f"/{pb.PACKAGE}.DevicePlugin/{method}", req.SerializeToString()
+        if self.rpc_client == "native-thread":
+            status, msg, body = await asyncio.to_thread(st.native.unary, path, data, 10.0)
+        else:
+            status, msg, body = st.native.unary(path, data, 10.0)
         if status != 0:
             if status < 0:
                 st.native.close()

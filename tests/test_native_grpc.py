@@ -600,3 +600,18 @@ def test_native_start_failure_falls_back_to_aio(tmp_path, monkeypatch):
 
     native, server, adm = run(_with_plugin(tmp_path, _impl(fi), "native", fn))
     assert native is None and server is not None and len(adm.device_ids) == 2
+
+
+@pytest.mark.parametrize("server", ["native", "aio"])
+def test_native_client_on_a_worker_thread_works_with_either_server(tmp_path, server):
+    """The fake kubelet's native client, called from a worker thread, admits
+    against both servers (the inline native client would block the event loop
+    that serves grpc.aio, so bench.py switches to the threaded one there)."""
+    fi = make_mi355x_node(tmp_path / "n")
+
+    async def fn(k, mgr, st):
+        k.rpc_client = "native-thread"
+        adms = [await k.admit("amd.com/gpu", n) for n in (1, 2, 4)]
+        return [len(a.device_ids) for a in adms]
+
+    assert run(_with_plugin(tmp_path, _impl(fi), server, fn)) == [1, 2, 4]

@@ -8,7 +8,7 @@
    the reference's own MI300X-CPX / MI210 captures when mounted.
 2. Admission over UDS gRPC through the fake kubelet on a synthetic 8x MI355X
    node: GetPreferredAllocation + Allocate p50/p99 at 1/2/4/8 GPUs, whole node
-   free and fragmented.
+   free and fragmented, and on the 8x8 CPX node; native server and grpc.aio.
 
   python tools/bench_alloc.py --out profiles/alloc_bench.json
 """
@@ -93,7 +93,7 @@ def synthetic_ref_devices(dev_count, parts, numa_count, start, end):
     return out
 
 
-async def admission(sysfs, n_adv, n_req, steps, fragment):
+async def admission(sysfs, n_adv, n_req, steps, fragment, server="native", client="native"):
     from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
     from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
     from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
@@ -105,9 +105,9 @@ async def admission(sysfs, n_adv, n_req, steps, fragment):
                     kfd_present=True)
     impl = ContainerImpl("single", sysfs, HealthConfig(exporter_socket=None), inventory=inv)
     with tempfile.TemporaryDirectory() as d:
-        k = FakeKubelet(d)
+        k = FakeKubelet(d, rpc_client=client)
         await k.start()
-        mgr = PluginManager(impl, ManagerConfig(pulse_s=0, plugin_dir=d, handle_signals=False))
+        mgr = PluginManager(impl, ManagerConfig(pulse_s=0, plugin_dir=d, handle_signals=False, grpc_server=server))
         task = asyncio.create_task(mgr.run())
         await k.wait_for_resource("amd.com/gpu", n_adv)
         rng = random.Random(5)
@@ -124,7 +124,7 @@ async def admission(sysfs, n_adv, n_req, steps, fragment):
         mgr.request_stop()
         await task
         await k.stop()
-    return {"advertised": n_adv, "requested": n_req, "fragmented": fragment,
+    return {"server": server, "kubelet_client": client, "advertised": n_adv, "requested": n_req, "fragmented": fragment,
             "admission_p50_ms": round(pct(lat, .5), 4), "admission_p99_ms": round(pct(lat, .99), 4),
             "preferred_p50_ms": round(pct(pref, .5), 4)}
 
@@ -153,15 +153,23 @@ def main():
                 pol = BestEffortPolicy()
                 pol.init(devs, load_topology(nodes_dir=os.path.join(REF, path)))
                 res["allocator"] += bench_topology(name, pol, [x[0] for x in devs], sizes, rng)
+        # the plugin-owned part of admission over UDS: kubelet's GetPreferredAllocation +
+        # Allocate round trips, native C++ server (default) and grpc.aio, both called
+        # from the native client (kubelet itself is a compiled grpc-go client)
         fi = make_mi355x_node(os.path.join(d, "adm"))
-        for n in (1, 2, 4, 8):
-            r = asyncio.run(admission(str(fi.sysfs), n, n, a.steps, False))
-            print(json.dumps(r), flush=True)
-            res["admission"].append(r)
-        for n in (1, 2, 4, 7):
-            r = asyncio.run(admission(str(fi.sysfs), 8, n, a.steps, True))
-            print(json.dumps(r), flush=True)
-            res["admission"].append(r)
+        cpx = make_mi355x_node(os.path.join(d, "adm_cpx"), compute_partition="cpx")
+        # ("native-thread": the same client on a worker thread, needed when the server runs on this
+        # process' event loop -- grpc.aio -- and used for both servers for a like-for-like pair)
+        for server, client in (("native", "native"), ("native", "native-thread"), ("aio", "native-thread")):
+            runs = [(fi, n, n, False) for n in (1, 2, 4, 8)] + [(fi, 8, n, True) for n in (1, 2, 4, 7)] + \
+                [(cpx, 64, n, True) for n in (1, 8, 32)]
+            for node, n_adv, n_req, frag in runs:
+                r = asyncio.run(admission(str(node.sysfs), n_adv, n_req, a.steps, frag, server=server,
+                                          client=client))
+                if node is cpx:
+                    r["partition"] = "cpx"
+                print(json.dumps(r), flush=True)
+                res["admission"].append(r)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
