@@ -140,6 +140,7 @@ typedef struct {
   // queue and buffers stay allocated and no new sweep is submitted (at most one
   // outstanding sweep per device, so a wedged GPU leaks one queue, not one per cadence)
   double in_flight_s;
+  int kept_queue;         // ran on the device's kept probe queue (--serve --keep), no queue of its own
   char error[160];
 } mi355x_sweep_result;
 
@@ -179,11 +180,16 @@ typedef struct {
   double xcd_clock_mhz[16];  // median per XCD (0 = no workgroup seen)
   double total_us;
   double in_flight_s;        // > 0: an earlier sweep / check on this device has not completed
+  int kept_queue;            // ran on the device's kept probe queue (--serve --keep)
   char error[160];
 } mi355x_perf_result;
 
 int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes, int mfma_iters, double timeout_s,
                           mi355x_perf_result* out);
+// Debug fault injection: the fill pass writes 16-byte unit `unit` with its
+// first word inverted, so the check pass must report exactly one bad word
+// there (UINT64_MAX = off).
+void mi355x_hsa_perf_poison(uint64_t unit);
 
 #ifdef __cplusplus
 }

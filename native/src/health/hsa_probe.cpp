@@ -288,6 +288,19 @@ extern "C" int mi355x_hsa_probe_identify(int ordinal, mi355x_probe_result* out) 
 
 namespace {
 
+// A completion signal shared by whoever may still need it: a chip sweep or
+// throughput check whose dispatch outlived its deadline is referenced both by
+// the in-flight registry and by the kept queue it was submitted on.
+struct SigRef {
+  hsa_signal_t s{};
+  SigRef() = default;
+  SigRef(const SigRef&) = delete;
+  SigRef& operator=(const SigRef&) = delete;
+  ~SigRef() {
+    if (s.handle) H().hsa_signal_destroy(s);
+  }
+};
+
 // Everything one probe allocates. Released right after the verdict, or — for
 // the container entrypoint, which reports "ready" as soon as the verdict is
 // known — after the JSON line is out (mi355x_hsa_probe_defer_release).
@@ -530,6 +543,10 @@ struct Resident {
   uint32_t pending_nonce = 0;
   int pending_iters = 1;
   std::chrono::steady_clock::time_point pending_since{};
+  // a chip sweep / throughput check submitted on this kept queue that did not
+  // complete within its deadline: probes report pending until it has
+  std::shared_ptr<SigRef> blocker;
+  std::chrono::steady_clock::time_point blocked_since{};
 };
 std::mutex g_resident_mu;
 bool g_keep = false;
@@ -541,7 +558,10 @@ void release_residents() {
   std::lock_guard<std::mutex> lk(g_resident_mu);
   for (auto& e : g_resident) {
     std::lock_guard<std::mutex> lk2(e.second->mu);
-    if (e.second->ready && !e.second->pending) e.second->r.release();
+    if (e.second->ready && !e.second->pending && !e.second->blocker) e.second->r.release();
+    if (e.second->blocker && e.second->blocker->s.handle &&
+        H().hsa_signal_load_scacquire(e.second->blocker->s) >= 1)
+      e.second->blocker->s = hsa_signal_t{};  // still running: leave it to the runtime's teardown
     e.second->ready = false;
   }
   g_resident.clear();
@@ -611,6 +631,17 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
         return finish();
       }
       slot->ready = true;
+    }
+    if (slot->blocker) {
+      if (H().hsa_signal_load_scacquire(slot->blocker->s) >= 1) {
+        const double s_out = std::chrono::duration<double>(clk::now() - slot->blocked_since).count();
+        std::snprintf(out->error, sizeof(out->error),
+                      "chip sweep / throughput check on this device's queue pending for %.1fs (not completed)", s_out);
+        out->pending_s = s_out;
+        out->hip_error = -1;
+        return finish();
+      }
+      slot->blocker.reset();
     }
     if (slot->pending) {
       // the previous probe's dispatch is still outstanding: wait for it (it
@@ -808,20 +839,20 @@ namespace {
 // until it completes. One per device at most (mi355x_hsa_chip_sweep refuses to
 // submit another while it is outstanding).
 struct SweepInFlight {
-  hsa_code_object_reader_t reader{};
+  hsa_code_object_reader_t reader{};  // null when the kept queue / executable were borrowed
   hsa_executable_t exe{};
   hsa_queue_t* queue = nullptr;
-  hsa_signal_t sig{};
+  std::shared_ptr<SigRef> sig;
   void* bufs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::chrono::steady_clock::time_point since{};
 
   void release() {
     for (void* b : bufs)
       if (b) H().hsa_amd_memory_pool_free(b);
-    if (sig.handle) H().hsa_signal_destroy(sig);
     if (queue) H().hsa_queue_destroy(queue);
     if (exe.handle) H().hsa_executable_destroy(exe);
     if (reader.handle) H().hsa_code_object_reader_destroy(reader);
+    sig.reset();
   }
 };
 std::mutex g_sweep_mu;
@@ -833,7 +864,7 @@ double in_flight_for(int ordinal) {
   std::lock_guard<std::mutex> lk(g_sweep_mu);
   for (auto it = g_sweep_in_flight.begin(); it != g_sweep_in_flight.end(); ++it) {
     if (it->first != ordinal) continue;
-    if (H().hsa_signal_load_scacquire(it->second.sig) < 1) {
+    if (H().hsa_signal_load_scacquire(it->second.sig->s) < 1) {
       it->second.release();
       g_sweep_in_flight.erase(it);
       return 0;
@@ -858,7 +889,181 @@ bool sweep_still_in_flight(int ordinal, R* out) {
 // runtime shutdown: an outstanding sweep's resources go with the runtime
 void forget_in_flight_sweeps() {
   std::lock_guard<std::mutex> lk(g_sweep_mu);
+  // a dispatch still running may yet decrement its completion signal: leave
+  // the signal to the runtime's own teardown instead of destroying it here
+  for (auto& e : g_sweep_in_flight)
+    if (e.second.sig && e.second.sig->s.handle && H().hsa_signal_load_scacquire(e.second.sig->s) >= 1)
+      e.second.sig->s = hsa_signal_t{};
   g_sweep_in_flight.clear();
+}
+
+}  // namespace
+
+namespace {
+
+// One AQL kernel dispatch (barrier bit, system-scope fences), no wait.
+void submit_kernel(hsa_queue_t* queue, uint64_t kobj, uint32_t gseg, uint32_t pseg, void* kargs, uint32_t wgs,
+                   uint32_t wg_threads, hsa_signal_t sig) {
+  H().hsa_signal_store_screlease(sig, 1);
+  const uint64_t idx = H().hsa_queue_add_write_index_screlease(queue, 1);
+  auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address) + (idx & (queue->size - 1));
+  std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
+  pkt->workgroup_size_x = static_cast<uint16_t>(wg_threads);
+  pkt->workgroup_size_y = 1;
+  pkt->workgroup_size_z = 1;
+  pkt->grid_size_x = wgs * wg_threads;
+  pkt->grid_size_y = 1;
+  pkt->grid_size_z = 1;
+  pkt->private_segment_size = pseg;
+  pkt->group_segment_size = gseg;
+  pkt->kernel_object = kobj;
+  pkt->kernarg_address = kargs;
+  pkt->completion_signal = sig;
+  const uint16_t header = static_cast<uint16_t>(
+      (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16), __ATOMIC_RELEASE);
+  H().hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+}
+
+double dispatch_us(const Agent& ag, hsa_signal_t sig) {
+  hsa_amd_profiling_dispatch_time_t dt{};
+  if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, sig, &dt) != HSA_STATUS_SUCCESS || !g_rt.ts_freq) return 0;
+  return static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
+}
+
+double median_of(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+struct KernelSym {
+  uint64_t kobj = 0;
+  uint32_t kseg = 0, gseg = 0, pseg = 0;
+};
+
+// The queue and executable a chip sweep or throughput check runs on. With kept
+// resources (--serve --keep) the device's kept queue and executable are
+// borrowed -- set up here if no probe has yet -- so the check adds no kfd
+// queue: no 181 MB context-save area, no HWS runlist update. The slot's mutex
+// is held meanwhile, so no probe packet interleaves. Otherwise a private queue
+// and executable are created for the check and destroyed after it.
+struct DeviceWork {
+  explicit DeviceWork(const Agent& a) : ag(a) {}
+  DeviceWork(const DeviceWork&) = delete;
+  DeviceWork& operator=(const DeviceWork&) = delete;
+  ~DeviceWork() {
+    if (abandoned || borrowed()) return;
+    if (queue) H().hsa_queue_destroy(queue);
+    if (exe.handle) H().hsa_executable_destroy(exe);
+    if (reader.handle) H().hsa_code_object_reader_destroy(reader);
+  }
+  bool borrowed() const { return slot != nullptr; }
+
+  hsa_status_t open(int ordinal, const char** what) {
+    bool keep;
+    {
+      std::lock_guard<std::mutex> lk(g_resident_mu);
+      keep = g_keep;
+    }
+    if (keep) {
+      Resident* s = resident_slot(ordinal);
+      std::unique_lock<std::mutex> lk(s->mu);
+      if (!s->ready && !s->pending && !s->blocker) {
+        mi355x_probe_result scratch;
+        std::memset(&scratch, 0, sizeof(scratch));
+        if (setup_resources(ag, s->r, s->k, &scratch))
+          s->ready = true;
+        else
+          s->r.release();
+      }
+      if (s->ready && !s->pending && !s->blocker) {
+        slot = s;
+        slot_lk = std::move(lk);
+        exe = s->r.exe;
+        queue = s->r.queue;
+      }
+    }
+    hsa_status_t st = HSA_STATUS_SUCCESS;
+    if (!borrowed()) {
+      const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
+      if ((st = H().hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader)) != 0)
+        return *what = "code object", st;
+      if ((st = H().hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr,
+                                              &exe)) != 0)
+        return *what = "executable create", st;
+      if ((st = H().hsa_executable_load_agent_code_object(exe, ag.agent, reader, nullptr, nullptr)) != 0)
+        return *what = "load code object", st;
+      if ((st = H().hsa_executable_freeze(exe, nullptr)) != 0) return *what = "freeze", st;
+      if ((st = H().hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX,
+                                     &queue)) != 0)
+        return *what = "queue create", st;
+      H().hsa_amd_profiling_set_profiler_enabled(queue, 1);
+    }
+    if ((st = H().hsa_signal_create(1, 0, nullptr, &sig->s)) != 0) return *what = "signal create", st;
+    return st;
+  }
+
+  hsa_status_t symbol(const char* name, KernelSym* k) {
+    hsa_executable_symbol_t sym{};
+    const hsa_status_t st = H().hsa_executable_get_symbol_by_name(exe, name, &ag.agent, &sym);
+    if (st != HSA_STATUS_SUCCESS) return st;
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k->kobj);
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k->kseg);
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k->gseg);
+    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k->pseg);
+    return st;
+  }
+
+  void submit(const KernelSym& k, void* kargs, uint32_t wgs, uint32_t wg_threads) {
+    submit_kernel(queue, k.kobj, k.gseg, k.pseg, kargs, wgs, wg_threads, sig->s);
+  }
+
+  // A dispatch did not complete within its deadline: everything it may still
+  // write goes to the in-flight registry (at most one per device: later sweeps
+  // and checks fail fast until it completes), and a borrowed kept queue blocks
+  // probes until then.
+  void abandon(int ordinal, std::initializer_list<void*> bufs, std::chrono::steady_clock::time_point since) {
+    abandoned = true;
+    SweepInFlight f;
+    if (!borrowed()) {
+      f.reader = reader;
+      f.exe = exe;
+      f.queue = queue;
+    }
+    f.sig = sig;
+    int i = 0;
+    for (void* b : bufs)
+      if (i < 6) f.bufs[i++] = b;
+    f.since = since;
+    {
+      std::lock_guard<std::mutex> lk(g_sweep_mu);
+      g_sweep_in_flight.emplace_back(ordinal, f);
+    }
+    if (borrowed()) {
+      slot->blocker = sig;
+      slot->blocked_since = std::chrono::steady_clock::now();
+    }
+  }
+
+  const Agent& ag;
+  Resident* slot = nullptr;
+  std::unique_lock<std::mutex> slot_lk;
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  hsa_queue_t* queue = nullptr;
+  std::shared_ptr<SigRef> sig = std::make_shared<SigRef>();
+  bool abandoned = false;
+};
+
+void set_hsa_error(int* err, char* buf, size_t n, hsa_status_t st, const char* what) {
+  *err = static_cast<int>(st);
+  const char* msg = nullptr;
+  H().hsa_status_string(st, &msg);
+  std::snprintf(buf, n, "%s: %s", what, msg ? msg : "hsa error");
 }
 
 }  // namespace
@@ -871,6 +1076,10 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
   out->nonce = nonce;
   out->iters = iters < 1 ? 1 : (iters > 64 ? 64 : iters);
   const auto t0 = clk::now();
+  auto finish = [&] {
+    out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+    return out->ok ? 0 : 1;
+  };
   const int n = mi355x_hsa_probe_init();
   if (n < 0) {
     out->hsa_error = n;
@@ -881,10 +1090,7 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
     std::snprintf(out->error, sizeof(out->error), "no such GPU agent (count=%d)", n);
     return 1;
   }
-  if (sweep_still_in_flight(ordinal, out)) {
-    out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
-    return 1;
-  }
+  if (sweep_still_in_flight(ordinal, out)) return finish();
   const Agent& ag = g_rt.gpus[ordinal];
   uint32_t cus = 0, xcc = 0;
   H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cus);
@@ -898,49 +1104,41 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
   const uint32_t grid = cus;
   out->grid = static_cast<int>(grid);
 
-  hsa_code_object_reader_t reader{};
-  hsa_executable_t exe{};
-  hsa_queue_t* queue = nullptr;
-  hsa_signal_t sig{};
+  DeviceWork w(ag);
+  const char* what = "";
+  hsa_status_t s = w.open(ordinal, &what);
+  if (s != HSA_STATUS_SUCCESS) {
+    set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, what);
+    return finish();
+  }
+  out->kept_queue = w.borrowed() ? 1 : 0;
+  KernelSym k;
+  if ((s = w.symbol("mi355x_chip_sweep.kd", &k)) != HSA_STATUS_SUCCESS) {
+    set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, "kernel symbol");
+    return finish();
+  }
+  if (k.kseg < sizeof(mi355x_sweep_args) || k.kseg > kKernargBytes) {
+    std::snprintf(out->error, sizeof(out->error), "sweep kernarg segment %u: code object / host ABI mismatch", k.kseg);
+    return finish();
+  }
   uint32_t* records = nullptr;
   float* tiles = nullptr;
   uint32_t* arrive = nullptr;
   mi355x_sweep_args* kargs = nullptr;
-  bool in_flight = false;
-  hsa_status_t s = HSA_STATUS_SUCCESS;
-  uint64_t kobj = 0;
-  uint32_t kseg = 0, gseg = 0, pseg = 0;
-  hsa_executable_symbol_t sym{};
-  const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
   const size_t rec_bytes = static_cast<size_t>(grid) * MI355X_SWEEP_REC_WORDS * sizeof(uint32_t);
   const size_t tile_bytes = static_cast<size_t>(grid) * MI355X_PROBE_OUT * sizeof(float);
-  auto fail = [&](hsa_status_t st, const char* what) {
-    out->hsa_error = static_cast<int>(st);
-    const char* msg = nullptr;
-    H().hsa_status_string(st, &msg);
-    std::snprintf(out->error, sizeof(out->error), "%s: %s", what, msg ? msg : "hsa error");
+  auto free_bufs = [&] {
+    if (kargs) H().hsa_amd_memory_pool_free(kargs);
+    if (arrive) H().hsa_amd_memory_pool_free(arrive);
+    if (tiles) H().hsa_amd_memory_pool_free(tiles);
+    if (records) H().hsa_amd_memory_pool_free(records);
   };
-#define SWEEP_CHECK(expr, what) \
-  if ((s = (expr)) != HSA_STATUS_SUCCESS) { fail(s, what); goto done; }
-
-  SWEEP_CHECK(H().hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader), "code object");
-  SWEEP_CHECK(H().hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe),
-              "executable create");
-  SWEEP_CHECK(H().hsa_executable_load_agent_code_object(exe, ag.agent, reader, nullptr, nullptr), "load code object");
-  SWEEP_CHECK(H().hsa_executable_freeze(exe, nullptr), "freeze");
-  SWEEP_CHECK(H().hsa_executable_get_symbol_by_name(exe, "mi355x_chip_sweep.kd", &ag.agent, &sym), "kernel symbol");
-  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &kobj);
-  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kseg);
-  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &gseg);
-  H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &pseg);
-  if (kseg < sizeof(mi355x_sweep_args) || kseg > kKernargBytes) {
-    std::snprintf(out->error, sizeof(out->error), "sweep kernarg segment %u: code object / host ABI mismatch", kseg);
-    goto done;
+#define SWEEP_CHECK(expr, label)                                                              \
+  if ((s = (expr)) != HSA_STATUS_SUCCESS) {                                                   \
+    set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, label);                 \
+    free_bufs();                                                                              \
+    return finish();                                                                          \
   }
-  SWEEP_CHECK(H().hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX,
-                                   &queue), "queue create");
-  H().hsa_amd_profiling_set_profiler_enabled(queue, 1);
-  SWEEP_CHECK(H().hsa_signal_create(1, 0, nullptr, &sig), "signal create");
   SWEEP_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.fine, rec_bytes, 0, reinterpret_cast<void**>(&records)),
               "alloc records");
   SWEEP_CHECK(H().hsa_amd_memory_pool_allocate(g_rt.fine, tile_bytes, 0, reinterpret_cast<void**>(&tiles)),
@@ -952,6 +1150,7 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
   SWEEP_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, tiles), "allow tiles");
   SWEEP_CHECK(H().hsa_amd_agents_allow_access(1, &ag.agent, nullptr, kargs), "allow kernarg");
   SWEEP_CHECK(H().hsa_amd_memory_fill(arrive, 0u, 4096 / 4), "zero arrive");
+#undef SWEEP_CHECK
   std::memset(records, 0, rec_bytes);
   std::memset(tiles, 0xFF, tile_bytes);
   std::memset(kargs, 0, kKernargBytes);
@@ -962,53 +1161,14 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
   kargs->iters = out->iters;
   kargs->grid = grid;
   kargs->wait_ticks = 2000000;  // 20 ms at the 100 MHz s_memrealtime clock
-  {
-    const uint64_t idx = H().hsa_queue_add_write_index_screlease(queue, 1);
-    auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address) + (idx & (queue->size - 1));
-    std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
-    pkt->workgroup_size_x = MI355X_SWEEP_THREADS;
-    pkt->workgroup_size_y = 1;
-    pkt->workgroup_size_z = 1;
-    pkt->grid_size_x = grid * MI355X_SWEEP_THREADS;
-    pkt->grid_size_y = 1;
-    pkt->grid_size_z = 1;
-    pkt->private_segment_size = pseg;
-    pkt->group_segment_size = gseg;
-    pkt->kernel_object = kobj;
-    pkt->kernarg_address = kargs;
-    pkt->completion_signal = sig;
-    const uint16_t header = static_cast<uint16_t>(
-        (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
-        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-        (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16),
-                     __ATOMIC_RELEASE);
-    H().hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
-  }
-  if (!wait_signal(sig, timeout_s)) {
-    in_flight = true;
+  w.submit(k, kargs, grid, MI355X_SWEEP_THREADS);
+  if (!wait_signal(w.sig->s, timeout_s)) {
     std::snprintf(out->error, sizeof(out->error), "chip sweep did not complete within %.1fs", timeout_s);
     out->hsa_error = -1;
-    SweepInFlight f;
-    f.reader = reader;
-    f.exe = exe;
-    f.queue = queue;
-    f.sig = sig;
-    f.bufs[0] = kargs;
-    f.bufs[1] = arrive;
-    f.bufs[2] = tiles;
-    f.bufs[3] = records;
-    f.since = t0;
-    std::lock_guard<std::mutex> lk(g_sweep_mu);
-    g_sweep_in_flight.emplace_back(ordinal, f);
-    goto done;
+    w.abandon(ordinal, {kargs, arrive, tiles, records}, t0);
+    return finish();
   }
-  {
-    hsa_amd_profiling_dispatch_time_t dt{};
-    if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, sig, &dt) == HSA_STATUS_SUCCESS && g_rt.ts_freq)
-      out->kernel_us = static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
-  }
+  out->kernel_us = dispatch_us(ag, w.sig->s);
   {
     std::vector<uint32_t> keys;
     keys.reserve(grid);
@@ -1057,64 +1217,15 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
                     "%d/%d workgroups correct (mfma_bad=%u lds_bad=%u tile_bad=%u), %d/%d XCDs ran", out->records_ok,
                     grid, out->mfma_bad, out->lds_bad, out->tile_bad, out->xccs_covered, out->num_xcc);
   }
-#undef SWEEP_CHECK
-done:
-  if (!in_flight) {
-    if (kargs) H().hsa_amd_memory_pool_free(kargs);
-    if (arrive) H().hsa_amd_memory_pool_free(arrive);
-    if (tiles) H().hsa_amd_memory_pool_free(tiles);
-    if (records) H().hsa_amd_memory_pool_free(records);
-    if (sig.handle) H().hsa_signal_destroy(sig);
-    if (queue) H().hsa_queue_destroy(queue);
-    if (exe.handle) H().hsa_executable_destroy(exe);
-    if (reader.handle) H().hsa_code_object_reader_destroy(reader);
-  }
-  out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
-  return out->ok ? 0 : 1;
+  free_bufs();
+  return finish();
 }
 
 namespace {
-
-// One AQL kernel dispatch (barrier bit, system-scope fences), no wait.
-void submit_kernel(hsa_queue_t* queue, uint64_t kobj, uint32_t gseg, uint32_t pseg, void* kargs, uint32_t wgs,
-                   uint32_t wg_threads, hsa_signal_t sig) {
-  H().hsa_signal_store_screlease(sig, 1);
-  const uint64_t idx = H().hsa_queue_add_write_index_screlease(queue, 1);
-  auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address) + (idx & (queue->size - 1));
-  std::memset(reinterpret_cast<char*>(pkt) + 4, 0, sizeof(*pkt) - 4);
-  pkt->workgroup_size_x = static_cast<uint16_t>(wg_threads);
-  pkt->workgroup_size_y = 1;
-  pkt->workgroup_size_z = 1;
-  pkt->grid_size_x = wgs * wg_threads;
-  pkt->grid_size_y = 1;
-  pkt->grid_size_z = 1;
-  pkt->private_segment_size = pseg;
-  pkt->group_segment_size = gseg;
-  pkt->kernel_object = kobj;
-  pkt->kernarg_address = kargs;
-  pkt->completion_signal = sig;
-  const uint16_t header = static_cast<uint16_t>(
-      (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
-      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-  __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header | (static_cast<uint32_t>(setup) << 16), __ATOMIC_RELEASE);
-  H().hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
-}
-
-double dispatch_us(const Agent& ag, hsa_signal_t sig) {
-  hsa_amd_profiling_dispatch_time_t dt{};
-  if (H().hsa_amd_profiling_get_dispatch_time(ag.agent, sig, &dt) != HSA_STATUS_SUCCESS || !g_rt.ts_freq) return 0;
-  return static_cast<double>(dt.end - dt.start) * 1e6 / static_cast<double>(g_rt.ts_freq);
-}
-
-double median_of(std::vector<double> v) {
-  if (v.empty()) return 0;
-  std::sort(v.begin(), v.end());
-  return v[v.size() / 2];
-}
-
+std::atomic<uint64_t> g_perf_poison{~0ull};
 }  // namespace
+
+extern "C" void mi355x_hsa_perf_poison(uint64_t unit) { g_perf_poison.store(unit, std::memory_order_relaxed); }
 
 extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes, int mfma_iters, double timeout_s,
                                      mi355x_perf_result* out) {
@@ -1129,6 +1240,10 @@ extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes
   out->bytes = bytes;
   out->mfma_iters = mfma_iters < 1 ? 1 : (mfma_iters > (1 << 22) ? (1 << 22) : mfma_iters);
   const auto t0 = clk::now();
+  auto finish = [&] {
+    out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+    return out->ok ? 0 : 1;
+  };
   const int n = mi355x_hsa_probe_init();
   if (n < 0) {
     out->hsa_error = n;
@@ -1139,10 +1254,7 @@ extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes
     std::snprintf(out->error, sizeof(out->error), "no such GPU agent (count=%d)", n);
     return 1;
   }
-  if (sweep_still_in_flight(ordinal, out)) {
-    out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
-    return 1;
-  }
+  if (sweep_still_in_flight(ordinal, out)) return finish();
   const Agent& ag = g_rt.gpus[ordinal];
   uint32_t cus = 0, xcc = 0;
   H().hsa_agent_get_info(ag.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cus);
@@ -1158,75 +1270,52 @@ extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes
   const uint32_t burn_wgs = cus * MI355X_BURN_WGS_PER_CU;
   out->mfma_grid = static_cast<int>(burn_wgs);
 
-  hsa_code_object_reader_t reader{};
-  hsa_executable_t exe{};
-  hsa_queue_t* queue = nullptr;
-  hsa_signal_t sig{};
-  uint32_t* buf = nullptr;      // device, `bytes`
-  uint32_t* counters = nullptr; // device, [0] bad words, [2..3] first bad unit
-  uint32_t* h_counters = nullptr;
-  uint32_t* records = nullptr;  // host-visible, burn_wgs records
-  char* kargs = nullptr;        // 3 slots of kKernargBytes
-  bool in_flight = false;
-  hsa_status_t s = HSA_STATUS_SUCCESS;
-  struct K {
-    const char* name;
-    uint64_t kobj = 0;
-    uint32_t kseg = 0, gseg = 0, pseg = 0;
-  } ks[3] = {{"mi355x_hbm_fill.kd"}, {"mi355x_hbm_check.kd"}, {"mi355x_mfma_burn.kd"}};
-  const size_t co_size = static_cast<size_t>(mi355x_hsaco_end - mi355x_hsaco_start);
-  const size_t rec_bytes = static_cast<size_t>(burn_wgs) * MI355X_PERF_REC_WORDS * sizeof(uint32_t);
-  auto fail = [&](hsa_status_t st, const char* what) {
-    out->hsa_error = static_cast<int>(st);
-    const char* msg = nullptr;
-    H().hsa_status_string(st, &msg);
-    std::snprintf(out->error, sizeof(out->error), "%s: %s", what, msg ? msg : "hsa error");
-  };
-  // a dispatch that did not complete: nothing it may still write can be freed
-  auto abandon = [&](const char* what) {
-    in_flight = true;
-    std::snprintf(out->error, sizeof(out->error), "%s did not complete within %.1fs", what, timeout_s);
-    out->hsa_error = -1;
-    SweepInFlight f;
-    f.reader = reader;
-    f.exe = exe;
-    f.queue = queue;
-    f.sig = sig;
-    f.bufs[0] = kargs;
-    f.bufs[1] = buf;
-    f.bufs[2] = counters;
-    f.bufs[3] = h_counters;
-    f.bufs[4] = records;
-    f.since = t0;
-    std::lock_guard<std::mutex> lk(g_sweep_mu);
-    g_sweep_in_flight.emplace_back(ordinal, f);
-  };
-#define PERF_CHECK(expr, what) \
-  if ((s = (expr)) != HSA_STATUS_SUCCESS) { fail(s, what); goto done; }
-
-  PERF_CHECK(H().hsa_code_object_reader_create_from_memory(mi355x_hsaco_start, co_size, &reader), "code object");
-  PERF_CHECK(H().hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe),
-             "executable create");
-  PERF_CHECK(H().hsa_executable_load_agent_code_object(exe, ag.agent, reader, nullptr, nullptr), "load code object");
-  PERF_CHECK(H().hsa_executable_freeze(exe, nullptr), "freeze");
-  for (K& k : ks) {
-    hsa_executable_symbol_t sym{};
-    PERF_CHECK(H().hsa_executable_get_symbol_by_name(exe, k.name, &ag.agent, &sym), "kernel symbol");
-    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.kobj);
-    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kseg);
-    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.gseg);
-    H().hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.pseg);
+  DeviceWork w(ag);
+  const char* what = "";
+  hsa_status_t s = w.open(ordinal, &what);
+  if (s != HSA_STATUS_SUCCESS) {
+    set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, what);
+    return finish();
   }
+  out->kept_queue = w.borrowed() ? 1 : 0;
+  KernelSym ks[3];
+  const char* names[3] = {"mi355x_hbm_fill.kd", "mi355x_hbm_check.kd", "mi355x_mfma_burn.kd"};
+  for (int i = 0; i < 3; ++i)
+    if ((s = w.symbol(names[i], &ks[i])) != HSA_STATUS_SUCCESS) {
+      set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, "kernel symbol");
+      return finish();
+    }
   if (ks[0].kseg < sizeof(mi355x_hbm_args) || ks[0].kseg > kKernargBytes || ks[1].kseg < sizeof(mi355x_hbm_args) ||
       ks[1].kseg > kKernargBytes || ks[2].kseg < sizeof(mi355x_burn_args) || ks[2].kseg > kKernargBytes) {
     std::snprintf(out->error, sizeof(out->error), "perf kernarg segments %u/%u/%u: code object / host ABI mismatch",
                   ks[0].kseg, ks[1].kseg, ks[2].kseg);
-    goto done;
+    return finish();
   }
-  PERF_CHECK(H().hsa_queue_create(ag.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX,
-                                  &queue), "queue create");
-  H().hsa_amd_profiling_set_profiler_enabled(queue, 1);
-  PERF_CHECK(H().hsa_signal_create(1, 0, nullptr, &sig), "signal create");
+  uint32_t* buf = nullptr;       // device, `bytes`
+  uint32_t* counters = nullptr;  // device, [0] bad words, [2..3] first bad unit
+  uint32_t* h_counters = nullptr;
+  uint32_t* records = nullptr;   // host-visible, burn_wgs records
+  char* kargs = nullptr;         // 3 slots of kKernargBytes
+  const size_t rec_bytes = static_cast<size_t>(burn_wgs) * MI355X_PERF_REC_WORDS * sizeof(uint32_t);
+  auto free_bufs = [&] {
+    if (kargs) H().hsa_amd_memory_pool_free(kargs);
+    if (records) H().hsa_amd_memory_pool_free(records);
+    if (h_counters) H().hsa_amd_memory_pool_free(h_counters);
+    if (counters) H().hsa_amd_memory_pool_free(counters);
+    if (buf) H().hsa_amd_memory_pool_free(buf);
+  };
+  auto abandon = [&](const char* stage) {
+    std::snprintf(out->error, sizeof(out->error), "%s did not complete within %.1fs", stage, timeout_s);
+    out->hsa_error = -1;
+    w.abandon(ordinal, {kargs, buf, counters, h_counters, records}, t0);
+    return finish();
+  };
+#define PERF_CHECK(expr, label)                                                               \
+  if ((s = (expr)) != HSA_STATUS_SUCCESS) {                                                   \
+    set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, label);                 \
+    free_bufs();                                                                              \
+    return finish();                                                                          \
+  }
   PERF_CHECK(H().hsa_amd_memory_pool_allocate(ag.coarse, bytes, 0, reinterpret_cast<void**>(&buf)), "alloc HBM buffer");
   PERF_CHECK(H().hsa_amd_memory_pool_allocate(ag.coarse, 4096, 0, reinterpret_cast<void**>(&counters)),
              "alloc counters");
@@ -1242,6 +1331,7 @@ extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes
   // counters: word 0 = 0 (bad words), words 2..3 = all ones (first bad unit)
   PERF_CHECK(H().hsa_amd_memory_fill(counters, 0u, 2), "zero counters");
   PERF_CHECK(H().hsa_amd_memory_fill(counters + 2, 0xFFFFFFFFu, 2), "init first-bad");
+  std::memset(h_counters, 0xA5, 16);   // overwritten by the burn kernel's copy
   std::memset(records, 0, rec_bytes);
   std::memset(kargs, 0, 3 * kKernargBytes);
   {
@@ -1254,39 +1344,25 @@ extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes
     fa->first_bad = ca->first_bad = reinterpret_cast<uint64_t*>(counters + 2);
     fa->threads = static_cast<uint64_t>(fill_wgs) * MI355X_PERF_THREADS;
     ca->threads = static_cast<uint64_t>(check_wgs) * MI355X_PERF_THREADS;
+    fa->poison_unit = g_perf_poison.load(std::memory_order_relaxed);
+    ca->poison_unit = ~0ull;
     fa->seed = ca->seed = nonce * 0x01000193u + 0x7F4A7C15u;
     ba->records = records;
+    ba->hbm_counters = counters;
+    ba->hbm_counters_host = h_counters;
     ba->nonce = nonce;
     ba->iters = out->mfma_iters;
   }
-  submit_kernel(queue, ks[0].kobj, ks[0].gseg, ks[0].pseg, kargs, fill_wgs, MI355X_PERF_THREADS, sig);
-  if (!wait_signal(sig, timeout_s)) {
-    abandon("HBM fill");
-    goto done;
-  }
-  out->fill_us = dispatch_us(ag, sig);
-  submit_kernel(queue, ks[1].kobj, ks[1].gseg, ks[1].pseg, kargs + kKernargBytes, check_wgs, MI355X_PERF_THREADS,
-                sig);
-  if (!wait_signal(sig, timeout_s)) {
-    abandon("HBM check");
-    goto done;
-  }
-  out->check_us = dispatch_us(ag, sig);
-  submit_kernel(queue, ks[2].kobj, ks[2].gseg, ks[2].pseg, kargs + 2 * kKernargBytes, burn_wgs, MI355X_PERF_THREADS,
-                sig);
-  if (!wait_signal(sig, timeout_s)) {
-    abandon("MFMA burn");
-    goto done;
-  }
-  out->mfma_us = dispatch_us(ag, sig);
-  // device counters -> host (async copy, bounded wait on the same signal)
-  H().hsa_signal_store_screlease(sig, 1);
-  PERF_CHECK(H().hsa_amd_memory_async_copy(h_counters, g_rt.cpu, counters, ag.agent, 16, 0, nullptr, sig),
-             "copy counters");
-  if (!wait_signal(sig, timeout_s)) {
-    abandon("counter copy");
-    goto done;
-  }
+  w.submit(ks[0], kargs, fill_wgs, MI355X_PERF_THREADS);
+  if (!wait_signal(w.sig->s, timeout_s)) return abandon("HBM fill");
+  out->fill_us = dispatch_us(ag, w.sig->s);
+  w.submit(ks[1], kargs + kKernargBytes, check_wgs, MI355X_PERF_THREADS);
+  if (!wait_signal(w.sig->s, timeout_s)) return abandon("HBM check");
+  out->check_us = dispatch_us(ag, w.sig->s);
+  w.submit(ks[2], kargs + 2 * kKernargBytes, burn_wgs, MI355X_PERF_THREADS);
+  if (!wait_signal(w.sig->s, timeout_s)) return abandon("MFMA burn");
+  out->mfma_us = dispatch_us(ag, w.sig->s);
+#undef PERF_CHECK
   {
     out->hbm_bad_words = h_counters[0];
     const uint64_t first = (static_cast<uint64_t>(h_counters[3]) << 32) | h_counters[2];
@@ -1341,19 +1417,6 @@ extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes
                     static_cast<unsigned long long>(out->hbm_bad_words), static_cast<long long>(out->hbm_first_bad),
                     out->mfma_records_ok, burn_wgs, out->mfma_checksum_mismatch, out->mfma_xccs, out->num_xcc);
   }
-#undef PERF_CHECK
-done:
-  if (!in_flight) {
-    if (kargs) H().hsa_amd_memory_pool_free(kargs);
-    if (records) H().hsa_amd_memory_pool_free(records);
-    if (h_counters) H().hsa_amd_memory_pool_free(h_counters);
-    if (counters) H().hsa_amd_memory_pool_free(counters);
-    if (buf) H().hsa_amd_memory_pool_free(buf);
-    if (sig.handle) H().hsa_signal_destroy(sig);
-    if (queue) H().hsa_queue_destroy(queue);
-    if (exe.handle) H().hsa_executable_destroy(exe);
-    if (reader.handle) H().hsa_code_object_reader_destroy(reader);
-  }
-  out->total_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
-  return out->ok ? 0 : 1;
+  free_bufs();
+  return finish();
 }

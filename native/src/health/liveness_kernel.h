@@ -120,12 +120,18 @@ struct mi355x_hbm_args {
   uint32_t* bad;        // device-visible counter of mismatching 32-bit words (check pass)
   uint64_t* first_bad;  // lowest mismatching 16-byte unit (check pass), UINT64_MAX if none
   uint64_t threads;     // lanes in the grid (the grid stride; passed so the kernels need no hidden args)
+  uint64_t poison_unit; // fill: write this 16-byte unit's first word inverted (fault injection); UINT64_MAX = off
   uint32_t seed;
   uint32_t pad;
 };
 
 struct mi355x_burn_args {
   uint32_t* records;    // host-visible, grid * MI355X_PERF_REC_WORDS
+  // the check pass's device counters (4 words), copied by workgroup 0 to the
+  // host-visible words after the records: no runtime copy (a device-to-host
+  // copy makes ROCr create another queue, +189 MB in the probe server)
+  const uint32_t* hbm_counters;
+  uint32_t* hbm_counters_host;
   uint32_t nonce;
   int32_t iters;        // MFMA pairs per wave
 };

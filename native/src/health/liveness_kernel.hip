@@ -163,6 +163,7 @@ extern "C" __global__ __launch_bounds__(MI355X_PERF_THREADS) void mi355x_hbm_fil
     v.y = hbm_pattern(w + 1, args.seed);
     v.z = hbm_pattern(w + 2, args.seed);
     v.w = hbm_pattern(w + 3, args.seed);
+    if (i == args.poison_unit) v.x = ~v.x;
     buf[i] = v;
   }
 }
@@ -242,6 +243,7 @@ extern "C" __global__ __launch_bounds__(MI355X_PERF_THREADS) void mi355x_mfma_bu
   const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
   uint32_t* rec = args.records + static_cast<size_t>(blockIdx.x) * MI355X_PERF_REC_WORDS;
   if (lane == 0) rec[MI355X_PREC_SUM + wave] = __builtin_bit_cast(uint32_t, s);
+  if (blockIdx.x == 0 && threadIdx.x < 4) args.hbm_counters_host[threadIdx.x] = args.hbm_counters[threadIdx.x];
   if (threadIdx.x == 0) {
     const uint64_t cyc = c1 - c0;
     rec[MI355X_PREC_WG] = blockIdx.x;

@@ -113,6 +113,7 @@ int chip_sweep(int o, uint32_t nonce, int iters, double timeout_s, mi355x_sweep_
 int perf_check(int o, uint32_t nonce, uint64_t bytes, int iters, double timeout_s, mi355x_perf_result* r) {
   return mi355x_hsa_perf_check(o, nonce, bytes, iters, timeout_s, r);
 }
+void perf_poison(uint64_t unit) { mi355x_hsa_perf_poison(unit); }
 void init_phases(double out[5]) { mi355x_hsa_init_phases(out); }
 void defer_teardown() { mi355x_hsa_probe_defer_release(1); }
 void teardown() { mi355x_hsa_probe_release(); }
@@ -139,6 +140,7 @@ int chip_sweep(int o, uint32_t nonce, int iters, double, mi355x_sweep_result* r)
   std::snprintf(r->error, sizeof(r->error), "--sweep needs the HSA-direct build (mi355x-liveness-probe)");
   return 1;
 }
+void perf_poison(uint64_t) {}
 int perf_check(int o, uint32_t nonce, uint64_t bytes, int iters, double, mi355x_perf_result* r) {
   std::memset(r, 0, sizeof(*r));
   r->ordinal = o;
@@ -278,11 +280,11 @@ std::string sweep_json(const mi355x_sweep_result& r) {
                 "\"cu_count\":%d,\"num_xcc\":%d,\"records_ok\":%d,\"mfma_bad\":%u,\"lds_bad\":%u,"
                 "\"tile_bad\":%u,\"cus_covered\":%d,\"xccs_covered\":%d,\"all_resident\":%s,"
                 "\"wgs_per_xcc\":%s,\"kernel_us\":%.2f,\"arrival_spread_us\":%.2f,\"total_us\":%.1f,"
-                "\"in_flight_s\":%.2f,\"error\":\"%s\"}",
+                "\"in_flight_s\":%.2f,\"kept_queue\":%s,\"error\":\"%s\"}",
                 r.ordinal, r.ok ? "true" : "false", r.hsa_error, r.nonce, r.iters, r.grid, r.cu_count, r.num_xcc,
                 r.records_ok, r.mfma_bad, r.lds_bad, r.tile_bad, r.cus_covered, r.xccs_covered,
                 r.all_resident ? "true" : "false", per.c_str(), r.kernel_us, r.arrival_spread_us, r.total_us,
-                r.in_flight_s, json_escape(r.error).c_str());
+                r.in_flight_s, r.kept_queue ? "true" : "false", json_escape(r.error).c_str());
   return buf;
 }
 
@@ -329,13 +331,13 @@ std::string perf_json(const mi355x_perf_result& r) {
                 "\"hbm_bad_words\":%llu,\"hbm_first_bad\":%lld,\"mfma_iters\":%d,\"mfma_grid\":%d,"
                 "\"mfma_records_ok\":%d,\"mfma_checksum_mismatch\":%d,\"mfma_xccs\":%d,\"mfma_us\":%.1f,"
                 "\"mfma_tflops\":%.1f,\"clock_mhz_min\":%.0f,\"clock_mhz_median\":%.0f,\"clock_mhz_max\":%.0f,"
-                "\"xcd_clock_mhz\":%s,\"total_us\":%.1f,\"in_flight_s\":%.2f,\"error\":\"%s\"}",
+                "\"xcd_clock_mhz\":%s,\"total_us\":%.1f,\"in_flight_s\":%.2f,\"kept_queue\":%s,\"error\":\"%s\"}",
                 r.ordinal, r.ok ? "true" : "false", r.hsa_error, r.nonce, static_cast<unsigned long long>(r.bytes),
                 r.cu_count, r.num_xcc, r.fill_us, r.check_us, r.hbm_write_gbps, r.hbm_read_gbps,
                 static_cast<unsigned long long>(r.hbm_bad_words), static_cast<long long>(r.hbm_first_bad),
                 r.mfma_iters, r.mfma_grid, r.mfma_records_ok, r.mfma_checksum_mismatch, r.mfma_xccs, r.mfma_us,
                 r.mfma_tflops, r.clock_mhz_min, r.clock_mhz_median, r.clock_mhz_max, per.c_str(), r.total_us,
-                r.in_flight_s, json_escape(r.error).c_str());
+                r.in_flight_s, r.kept_queue ? "true" : "false", json_escape(r.error).c_str());
   return buf;
 }
 
@@ -521,6 +523,8 @@ int main(int argc, char** argv) {
       perf_mib = std::strtoull(next("--perf-mib"), nullptr, 0);
     } else if (a == "--perf-iters") {
       perf_iters = std::atoi(next("--perf-iters"));
+    } else if (a == "--poison-hbm") {
+      perf_poison(std::strtoull(next("--poison-hbm"), nullptr, 0));
     } else if (a == "--peer-bytes") {
       peer_bytes = std::strtoull(next("--peer-bytes"), nullptr, 0);
     } else if (a == "--corrupt-word") {
@@ -530,7 +534,7 @@ int main(int argc, char** argv) {
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
                   "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve [--keep]] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep] "
-                  "[--perf [--perf-mib M] [--perf-iters N]] "
+                  "[--perf [--perf-mib M] [--perf-iters N] [--poison-hbm UNIT]] "
                   "[--corrupt-word K[@ORDINAL]]\n",
                   argv[0]);
       return 0;

@@ -536,6 +536,49 @@ def test_perf_check_measures_hbm_and_mfma(ordinals):
     assert r.ok and r.detail["hbm_bad_words"] == 0 and r.detail["mfma_xccs"] == 8, r
 
 
+def test_perf_check_finds_an_injected_hbm_fault(ordinals):
+    """--poison-hbm U: the fill writes unit U with one word inverted; the check
+    pass must count exactly that word and name that unit."""
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    o = sorted(ordinals.values())[0]
+    env = dict(os.environ, ROCR_VISIBLE_DEVICES=str(o))
+    unit = 12_345_677
+    p = subprocess.run([str(probe_executable("hsa")), "--perf", "--perf-mib", "512", "--perf-iters", "1024",
+                        "--poison-hbm", str(unit), "--devices", "0", "--timeout", "20"], stdout=subprocess.PIPE,
+                       env=env, timeout=120)
+    d = json.loads(p.stdout.decode().strip().splitlines()[-1])["devices"][0]
+    assert p.returncode == 1 and not d["ok"], d
+    assert d["hbm_bad_words"] == 1 and d["hbm_first_bad"] == unit and d["mfma_checksum_mismatch"] == 0, d
+    assert "hbm_bad_words=1" in d["error"], d
+
+
+def test_sweep_and_perf_check_borrow_the_kept_queue(ordinals):
+    """With kept queues the chip sweep and the throughput check run on the
+    device's kept probe queue (set up by whichever comes first), so the probe
+    server holds two 181 MB save areas per GPU (its queue, ROCr's internal
+    one), not three; probes before and after still verify fresh nonces."""
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    o = sorted(ordinals.values())[0]
+    prober = LivenessProber(timeout_s=60)
+    prober.perf_mib, prober.perf_iters = 1024, 8192
+
+    async def go():
+        sw = (await prober.sweep({"gpu": o}))["gpu"]      # first request: sets the kept slot up
+        pr = (await prober.probe({"gpu": o}))["gpu"]
+        pf = (await prober.perf({"gpu": o}))["gpu"]
+        sw2 = (await prober.sweep({"gpu": o}))["gpu"]
+        pr2 = (await prober.probe({"gpu": o}))["gpu"]
+        with open(f"/proc/{prober._server.proc.pid}/status") as f:
+            rss_mb = [int(line.split()[1]) for line in f if line.startswith("VmRSS")][0] / 1024
+        await prober.close()
+        return sw, pr, pf, sw2, pr2, rss_mb
+
+    sw, pr, pf, sw2, pr2, rss_mb = asyncio.run(go())
+    assert sw.ok and sw2.ok and pf.ok and pr.ok and pr2.ok, (sw, pr, pf, sw2, pr2)
+    assert sw.detail["kept_queue"] and sw2.detail["kept_queue"] and pf.detail["kept_queue"], (sw, pf, sw2)
+    assert rss_mb < 450, rss_mb
+
+
 def test_monitor_perf_check_on_idle_gpu(inv, ordinals):
     """The health monitor's cadence: liveness, then the throughput check on the
     idle GPU in the same sweep; a healthy MI355X clears every floor."""
