@@ -162,10 +162,12 @@ typedef struct {
   int cu_count;
   int num_xcc;
   double fill_us;            // kernel times (HSA dispatch profiling)
-  double check_us;
+  double check_us;           // first read pass (right after the fill)
+  double check2_us;          // second read pass
   double hbm_write_gbps;
-  double hbm_read_gbps;
-  uint64_t hbm_bad_words;    // 32-bit words read back wrong
+  double hbm_read_gbps;      // from the faster read pass
+  uint64_t hbm_bad_words;    // 32-bit words read back wrong (the pass that found more)
+  uint64_t hbm_bad_words_pass2;
   int64_t hbm_first_bad;     // lowest failing 16-byte unit, -1 if none
   int mfma_iters;            // MFMA pairs per wave
   int mfma_grid;             // workgroups (MI355X_BURN_WGS_PER_CU per CU)

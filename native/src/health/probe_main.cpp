@@ -327,14 +327,14 @@ std::string perf_json(const mi355x_perf_result& r) {
   char buf[1536];
   std::snprintf(buf, sizeof(buf),
                 "{\"ordinal\":%d,\"ok\":%s,\"hsa_error\":%d,\"nonce\":%u,\"bytes\":%llu,\"cu_count\":%d,"
-                "\"num_xcc\":%d,\"fill_us\":%.1f,\"check_us\":%.1f,\"hbm_write_gbps\":%.1f,\"hbm_read_gbps\":%.1f,"
-                "\"hbm_bad_words\":%llu,\"hbm_first_bad\":%lld,\"mfma_iters\":%d,\"mfma_grid\":%d,"
+                "\"num_xcc\":%d,\"fill_us\":%.1f,\"check_us\":%.1f,\"check2_us\":%.1f,\"hbm_write_gbps\":%.1f,"
+                "\"hbm_read_gbps\":%.1f,\"hbm_bad_words\":%llu,\"hbm_bad_words_pass2\":%llu,\"hbm_first_bad\":%lld,\"mfma_iters\":%d,\"mfma_grid\":%d,"
                 "\"mfma_records_ok\":%d,\"mfma_checksum_mismatch\":%d,\"mfma_xccs\":%d,\"mfma_us\":%.1f,"
                 "\"mfma_tflops\":%.1f,\"clock_mhz_min\":%.0f,\"clock_mhz_median\":%.0f,\"clock_mhz_max\":%.0f,"
                 "\"xcd_clock_mhz\":%s,\"total_us\":%.1f,\"in_flight_s\":%.2f,\"kept_queue\":%s,\"error\":\"%s\"}",
                 r.ordinal, r.ok ? "true" : "false", r.hsa_error, r.nonce, static_cast<unsigned long long>(r.bytes),
-                r.cu_count, r.num_xcc, r.fill_us, r.check_us, r.hbm_write_gbps, r.hbm_read_gbps,
-                static_cast<unsigned long long>(r.hbm_bad_words), static_cast<long long>(r.hbm_first_bad),
+                r.cu_count, r.num_xcc, r.fill_us, r.check_us, r.check2_us, r.hbm_write_gbps, r.hbm_read_gbps,
+                static_cast<unsigned long long>(r.hbm_bad_words), static_cast<unsigned long long>(r.hbm_bad_words_pass2), static_cast<long long>(r.hbm_first_bad),
                 r.mfma_iters, r.mfma_grid, r.mfma_records_ok, r.mfma_checksum_mismatch, r.mfma_xccs, r.mfma_us,
                 r.mfma_tflops, r.clock_mhz_min, r.clock_mhz_median, r.clock_mhz_max, per.c_str(), r.total_us,
                 r.in_flight_s, r.kept_queue ? "true" : "false", json_escape(r.error).c_str());
