@@ -1104,21 +1104,21 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
   const uint32_t grid = cus;
   out->grid = static_cast<int>(grid);
 
-  DeviceWork w(ag);
+  DeviceWork dw(ag);
   const char* what = "";
-  hsa_status_t s = w.open(ordinal, &what);
+  hsa_status_t s = dw.open(ordinal, &what);
   if (s != HSA_STATUS_SUCCESS) {
     set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, what);
     return finish();
   }
-  out->kept_queue = w.borrowed() ? 1 : 0;
-  KernelSym k;
-  if ((s = w.symbol("mi355x_chip_sweep.kd", &k)) != HSA_STATUS_SUCCESS) {
+  out->kept_queue = dw.borrowed() ? 1 : 0;
+  KernelSym ksym;
+  if ((s = dw.symbol("mi355x_chip_sweep.kd", &ksym)) != HSA_STATUS_SUCCESS) {
     set_hsa_error(&out->hsa_error, out->error, sizeof(out->error), s, "kernel symbol");
     return finish();
   }
-  if (k.kseg < sizeof(mi355x_sweep_args) || k.kseg > kKernargBytes) {
-    std::snprintf(out->error, sizeof(out->error), "sweep kernarg segment %u: code object / host ABI mismatch", k.kseg);
+  if (ksym.kseg < sizeof(mi355x_sweep_args) || ksym.kseg > kKernargBytes) {
+    std::snprintf(out->error, sizeof(out->error), "sweep kernarg segment %u: code object / host ABI mismatch", ksym.kseg);
     return finish();
   }
   uint32_t* records = nullptr;
@@ -1161,14 +1161,14 @@ extern "C" int mi355x_hsa_chip_sweep(int ordinal, uint32_t nonce, int iters, dou
   kargs->iters = out->iters;
   kargs->grid = grid;
   kargs->wait_ticks = 2000000;  // 20 ms at the 100 MHz s_memrealtime clock
-  w.submit(k, kargs, grid, MI355X_SWEEP_THREADS);
-  if (!wait_signal(w.sig->s, timeout_s)) {
+  dw.submit(ksym, kargs, grid, MI355X_SWEEP_THREADS);
+  if (!wait_signal(dw.sig->s, timeout_s)) {
     std::snprintf(out->error, sizeof(out->error), "chip sweep did not complete within %.1fs", timeout_s);
     out->hsa_error = -1;
-    w.abandon(ordinal, {kargs, arrive, tiles, records}, t0);
+    dw.abandon(ordinal, {kargs, arrive, tiles, records}, t0);
     return finish();
   }
-  out->kernel_us = dispatch_us(ag, w.sig->s);
+  out->kernel_us = dispatch_us(ag, dw.sig->s);
   {
     std::vector<uint32_t> keys;
     keys.reserve(grid);

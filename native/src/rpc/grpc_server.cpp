@@ -297,7 +297,7 @@ struct GrpcServer::Impl {
     for (uint32_t sid : done) finish_stream(c, sid);
   }
 
-  void queue_message(Conn& c, Stream& s, const std::string& msg) {
+  void queue_message(Conn&, Stream& s, const std::string& msg) {
     s.out.append(grpc_frame(msg));
   }
 
