@@ -1387,9 +1387,10 @@ extern "C" int mi355x_hsa_perf_check(int ordinal, uint32_t nonce, uint64_t bytes
     uint32_t ref = 0;
     bool have_ref = false;
     uint32_t xmask = 0;
-    for (uint32_t w = 0; w < burn_wgs; ++w) {
-      const uint32_t* r = records + static_cast<size_t>(w) * MI355X_PERF_REC_WORDS;
-      if (r[MI355X_PREC_MAGIC] != MI355X_PERF_MAGIC || r[MI355X_PREC_WG] != w || r[MI355X_PREC_NONCE] != (nonce ^ w))
+    for (uint32_t wg = 0; wg < burn_wgs; ++wg) {
+      const uint32_t* r = records + static_cast<size_t>(wg) * MI355X_PERF_REC_WORDS;
+      if (r[MI355X_PREC_MAGIC] != MI355X_PERF_MAGIC || r[MI355X_PREC_WG] != wg ||
+          r[MI355X_PREC_NONCE] != (nonce ^ wg))
         continue;
       ++out->mfma_records_ok;
       for (int v = 0; v < MI355X_PERF_THREADS / 64; ++v) {
