@@ -35,15 +35,21 @@ from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet  # noqa:
 from rocm_k8s_device_plugin_amd.topology import discover, hip_ordinals  # noqa: E402
 
 
+_TICK = os.sysconf("SC_CLK_TCK")
+
+
 def proc_stats(pid: int) -> dict:
-    out = {"rss_mb": None, "fds": None}
+    out = {"rss_mb": None, "fds": None, "cpu_s": None}
     try:
         with open(f"/proc/{pid}/status") as f:
             for line in f:
                 if line.startswith("VmRSS"):
                     out["rss_mb"] = round(int(line.split()[1]) / 1024, 1)
         out["fds"] = len(os.listdir(f"/proc/{pid}/fd"))
-    except OSError:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        out["cpu_s"] = round((int(fields[11]) + int(fields[12])) / _TICK, 2)   # utime + stime
+    except (OSError, ValueError, IndexError):
         pass
     return out
 
@@ -120,23 +126,26 @@ async def main_async(a) -> dict:
             next_report = time.monotonic() + a.report
             first = None
             while time.monotonic() < t_end:
-                t0 = time.monotonic_ns()
-                try:
-                    adm = await k.admit("amd.com/gpu", 1)
-                    car = adm.response.container_responses[0]
-                    ol = [minor_to_ord[m] for m in render_minors_from_specs(car)]
-                    paths = ["/dev/kfd"] + [ds.host_path for ds in car.devices if "/dri/" in ds.host_path]
-                    r = await asyncio.to_thread(start_container, ol, timeout_s=60, device_paths=paths)
-                    k.release("amd.com/gpu", adm.device_ids)
-                    if r.ok:
-                        lat.append((r.t_ready_ns - t0) / 1e6)
-                    else:
+                if a.idle:   # no pods: what the daemon itself costs between admissions
+                    await asyncio.sleep(max(0.0, min(1.0, next_report - time.monotonic())))
+                else:
+                    t0 = time.monotonic_ns()
+                    try:
+                        adm = await k.admit("amd.com/gpu", 1)
+                        car = adm.response.container_responses[0]
+                        ol = [minor_to_ord[m] for m in render_minors_from_specs(car)]
+                        paths = ["/dev/kfd"] + [ds.host_path for ds in car.devices if "/dri/" in ds.host_path]
+                        r = await asyncio.to_thread(start_container, ol, timeout_s=60, device_paths=paths)
+                        k.release("amd.com/gpu", adm.device_ids)
+                        if r.ok:
+                            lat.append((r.t_ready_ns - t0) / 1e6)
+                        else:
+                            fails += 1
+                        await asyncio.to_thread(wait_kfd_released, r.kfd_lingering, 1.0)
+                    except Exception as e:  # noqa: BLE001
                         fails += 1
-                    await asyncio.to_thread(wait_kfd_released, r.kfd_lingering, 1.0)
-                except Exception as e:  # noqa: BLE001
-                    fails += 1
-                    print(json.dumps({"error": f"{type(e).__name__}: {e}"[:300]}), flush=True)
-                n += 1
+                        print(json.dumps({"error": f"{type(e).__name__}: {e}"[:300]}), flush=True)
+                    n += 1
                 if time.monotonic() >= next_report:
                     next_report += a.report
                     kids = children(plugin.pid)
@@ -163,7 +172,7 @@ async def main_async(a) -> dict:
                 plugin.kill()
                 rc = "killed"
             await k.stop()
-        return {"seconds": a.seconds, "pulse_s": a.pulse, "admissions": n, "failures": fails,
+        return {"seconds": a.seconds, "pulse_s": a.pulse, "idle": a.idle, "admissions": n, "failures": fails,
                 "ready_p50_ms": round(statistics.median(lat), 2) if lat else None,
                 "ready_p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))], 2) if lat else None,
                 "plugin_exit": rc, "first": rows[0] if rows else None, "last": rows[-1] if rows else None,
@@ -176,6 +185,7 @@ def main():
     ap.add_argument("--pulse", type=int, default=1, help="plugin -pulse (whole seconds, as upstream)")
     ap.add_argument("--perf-every", type=int, default=40, help="throughput check every N pulses")
     ap.add_argument("--report", type=float, default=30)
+    ap.add_argument("--idle", action="store_true", help="no admissions: the daemon's own steady-state cost")
     ap.add_argument("--log", default="/tmp/soak_plugin.log")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
