@@ -478,3 +478,36 @@ def test_labeller_in_cluster_over_tls(tmp_path, monkeypatch):
         assert "CERTIFICATE_VERIFY_FAILED" in str(ei.value) or "certificate verify failed" in str(ei.value)
     finally:
         srv.stop()
+
+
+def test_partition_switch_relabels_on_the_next_resync(tmp_path):
+    """Labels are generated again on every reconcile, so a compute/memory
+    partition switch reaches the node on the next pass (the reference computes
+    them once at start-up)."""
+    import shutil
+    root = tmp_path / "n"
+    fi = make_mi355x_node(root)
+    srv = FakeApiServer(token="tok").start()
+    try:
+        srv.add_node("worker-3")
+        client = KubeClient(KubeConfig(server=srv.url, token="tok"))
+        enabled = {"compute-memory-partition": True, "cu-count": True, "mode": True}
+        lab = NodeLabeller(client, "worker-3",
+                           lambda: L.generate_labels(enabled, "container", str(fi.sysfs), str(fi.dev)),
+                           resync_s=0, watch=False)
+        assert lab.reconcile_once()
+        before = srv.labels("worker-3")
+        assert before["amd.com/gpu.compute-memory-partition"] == "spx_nps1"
+        assert before["amd.com/gpu.cu-count"] == "256"
+        # the driver now shows CPX / NPS2 (a fresh tree swapped in, as after a switch)
+        new = tmp_path / "n.new"
+        make_mi355x_node(new, compute_partition="cpx", memory_partition="nps2")
+        shutil.rmtree(root / "sys")
+        os.rename(new / "sys", root / "sys")
+        assert lab.reconcile_once()
+        after = srv.labels("worker-3")
+        assert after["amd.com/gpu.compute-memory-partition"] == "cpx_nps2"
+        assert after["amd.com/gpu.cu-count"] == "32"
+        assert not any(k.startswith("beta.amd.com/gpu.compute-memory-partition.spx") for k in after)
+    finally:
+        srv.stop()
