@@ -35,6 +35,8 @@ def build_parser() -> flags.GoFlagParser:
     p.add_float("resync", 300.0, "seconds between label re-asserts (0 = apply once and exit)")
     p.add_bool("watch", True, "watch the node and re-apply labels as soon as they are stripped or the node is "
                               "re-created (needs the 'watch' verb on nodes, as in the upstream ClusterRole)")
+    p.add_float("topology_watch", 5.0, "seconds between checks of the GPU topology (kfd generation_id, partition "
+                                       "modes); a change relabels the node at once (0 = off: next resync)")
     p.add_bool("dry_run", False, "print the generated labels as JSON and exit")
     p.add_str("sysfs_root", "/sys", "sysfs mount to read")
     p.add_str("dev_root", "/dev", "device node directory")
@@ -89,7 +91,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     except Exception as e:
         logger.error("unable to set up kubernetes client: %s", e)
         return 1
-    lab = NodeLabeller(client, node, gen, resync_s=ns.resync, watch=ns.watch)
+    from ..topology import topology_signature
+    lab = NodeLabeller(client, node, gen, resync_s=ns.resync, watch=ns.watch,
+                       change_source=lambda: topology_signature(ns.sysfs_root), change_interval_s=ns.topology_watch)
     for s in (signal.SIGTERM, signal.SIGINT):
         signal.signal(s, lambda *_: lab.stop())
     lab.run(once=ns.resync <= 0)

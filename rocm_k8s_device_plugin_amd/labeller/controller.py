@@ -54,12 +54,14 @@ class ReconcileStats:
     watch_kicks: int = 0      # events that triggered a reconcile
     watch_errors: int = 0
     watch_restarts: int = 0
+    topology_changes: int = 0  # GPU topology fingerprint changes seen (each relabels at once)
 
 
 class NodeLabeller:
     def __init__(self, client: KubeClient, node_name: str, generate: Callable[[], Dict[str, str]],
                  resync_s: float = 300.0, retry_s: float = 5.0, watch: bool = True, watch_timeout_s: int = 300,
-                 watch_backoff_max_s: float = 30.0):
+                 watch_backoff_max_s: float = 30.0, change_source: Optional[Callable[[], object]] = None,
+                 change_interval_s: float = 5.0):
         self.client = client
         self.node = node_name
         self.generate = generate
@@ -75,6 +77,12 @@ class NodeLabeller:
         self._rv = ""
         self._stream = None
         self._watch_thread: Optional[threading.Thread] = None
+        # GPU topology fingerprint (kfd generation_id + partition modes): a
+        # change -- a partition switch -- relabels at once instead of at the
+        # next resync
+        self.change_source = change_source
+        self.change_interval_s = change_interval_s
+        self._change_thread: Optional[threading.Thread] = None
 
     def reconcile_once(self) -> bool:
         """Returns True on success (whether or not a patch was needed)."""
@@ -172,10 +180,34 @@ class NodeLabeller:
         if self._watch_thread is not None and self._watch_thread is not threading.current_thread():
             self._watch_thread.join(5)
 
+    def _change_loop(self) -> None:
+        try:
+            last = self.change_source()
+        except Exception:  # noqa: BLE001
+            last = None
+        seen = last
+        while not self._stop.wait(self.change_interval_s):
+            try:
+                cur = self.change_source()
+            except Exception:  # noqa: BLE001
+                continue
+            # act once the new fingerprint has held for one interval: a switch
+            # passes through states with devices half gone
+            if cur != last and cur == seen:
+                last = cur
+                self.stats.topology_changes += 1
+                _log.info("GPU topology changed (partition switch?): relabelling node %s", self.node)
+                self._kick.set()
+            seen = cur
+
     def run(self, once: bool = False) -> None:
         if self.watch and not once and self._watch_thread is None:
             self._watch_thread = threading.Thread(target=self._watch_loop, name="node-watch", daemon=True)
             self._watch_thread.start()
+        if self.change_source is not None and self.change_interval_s > 0 and not once and \
+                self._change_thread is None:
+            self._change_thread = threading.Thread(target=self._change_loop, name="topology-watch", daemon=True)
+            self._change_thread.start()
         while not self._stop.is_set():
             self._kick.clear()
             ok = self.reconcile_once()

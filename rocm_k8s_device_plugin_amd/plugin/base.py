@@ -96,6 +96,10 @@ class DeviceImpl(abc.ABC):
         manager then re-initialises every resource's allocator."""
         return 0
 
+    def topology_fingerprint(self):
+        """Cheap value that changes when the GPU topology does (None: not tracked)."""
+        return None
+
     async def reload_topology(self) -> Optional[dict]:
         """Re-discover devices if the node's GPU topology changed; None if the
         advertised devices are unchanged (see ContainerImpl.reload_topology)."""

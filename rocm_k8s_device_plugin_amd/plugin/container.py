@@ -26,7 +26,7 @@ from .. import constants as C
 from ..allocator import AllocationError
 from ..health.monitor import HealthConfig, HealthMonitor
 from ..proto import deviceplugin as pb
-from ..topology import Gpu, Inventory, discover
+from ..topology import Gpu, Inventory, discover, topology_signature
 from ..node_view import NodeView
 from ..topology_view import KFD_TOPOLOGY_CONTAINER_PATH, TopologyViews
 from ..utils import log
@@ -191,25 +191,10 @@ class ContainerImpl(DeviceImpl):
 
     # ---------------------------------------------------------------- topology reload
     def _signature(self) -> tuple:
-        """Cheap fingerprint of the GPU topology: kfd's generation_id (bumped
-        by the driver when kfd nodes come or go) and every amdgpu PCI
-        function's current partition modes (~17 small reads on 8 GPUs)."""
-        def rd(path):
-            try:
-                with open(path) as f:
-                    return f.read().strip()
-            except OSError:
-                return None
-        root = self.sysfs_root
-        gen = rd(os.path.join(root, "class/kfd/kfd/topology/generation_id"))
-        drv = os.path.join(root, "module/amdgpu/drivers/pci:amdgpu")
-        try:
-            bdfs = sorted(e for e in os.listdir(drv) if ":" in e)
-        except OSError:
-            bdfs = []
-        parts = tuple((b, rd(os.path.join(drv, b, "current_compute_partition")),
-                       rd(os.path.join(drv, b, "current_memory_partition"))) for b in bdfs)
-        return gen, parts
+        return topology_signature(self.sysfs_root)
+
+    def topology_fingerprint(self):
+        return None if self._pinned else self._signature()
 
     async def reload_topology(self) -> Optional[dict]:
         """Re-discover when the topology fingerprint changed.

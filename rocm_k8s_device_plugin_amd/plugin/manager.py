@@ -246,6 +246,7 @@ class PluginManager:
     async def _topology_loop(self) -> None:
         """Every topology_watch_s: has the node's GPU topology changed (e.g. an
         amd-smi partition switch)? Then advertise what is there now."""
+        seen = None
         while not self.stopped.is_set():
             try:
                 await asyncio.wait_for(self.stopped.wait(), self.cfg.topology_watch_s)
@@ -253,6 +254,12 @@ class PluginManager:
             except asyncio.TimeoutError:
                 pass
             try:
+                # re-discover once a new fingerprint has held for one interval:
+                # a partition switch passes through states with devices half gone
+                fp = self.impl.topology_fingerprint()
+                if fp is not None and fp != seen:
+                    seen = fp
+                    continue
                 async with self._impl_lock:
                     change = await self.impl.reload_topology()
                 if change:

@@ -258,3 +258,25 @@ def kfd_busy_gpu_ids(sysfs_root: str = "/sys", exclude=()) -> set:
     without queues runs no work; the liveness loop runs its full-chip sweep
     only on those. Raises KfdBusyUnknown (see kfd_gpu_load)."""
     return set(kfd_gpu_load(sysfs_root, exclude))
+
+
+def topology_signature(sysfs_root: str = "/sys") -> tuple:
+    """Cheap fingerprint of the GPU topology: kfd's generation_id (bumped by the
+    driver when kfd nodes come or go) and every amdgpu PCI function's current
+    partition modes (~17 small reads on 8 GPUs). Used by the plugin's and the
+    labeller's ``-topology_watch``."""
+    def rd(path):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return None
+    gen = rd(os.path.join(sysfs_root, "class/kfd/kfd/topology/generation_id"))
+    drv = os.path.join(sysfs_root, "module/amdgpu/drivers/pci:amdgpu")
+    try:
+        bdfs = sorted(e for e in os.listdir(drv) if ":" in e)
+    except OSError:
+        bdfs = []
+    parts = tuple((b, rd(os.path.join(drv, b, "current_compute_partition")),
+                   rd(os.path.join(drv, b, "current_memory_partition"))) for b in bdfs)
+    return gen, parts

@@ -511,3 +511,43 @@ def test_partition_switch_relabels_on_the_next_resync(tmp_path):
         assert not any(k.startswith("beta.amd.com/gpu.compute-memory-partition.spx") for k in after)
     finally:
         srv.stop()
+
+
+def test_topology_watch_relabels_within_a_second(tmp_path):
+    """-topology_watch: the labeller polls the GPU topology fingerprint and
+    relabels on a change without waiting for the (here 1 h) resync."""
+    import shutil
+    import threading
+    import time
+    from rocm_k8s_device_plugin_amd.topology import topology_signature
+    root = tmp_path / "n"
+    fi = make_mi355x_node(root)
+    srv = FakeApiServer(token="tok").start()
+    lab = None
+    try:
+        srv.add_node("worker-4")
+        client = KubeClient(KubeConfig(server=srv.url, token="tok"))
+        enabled = {"compute-memory-partition": True}
+        lab = NodeLabeller(client, "worker-4",
+                           lambda: L.generate_labels(enabled, "container", str(fi.sysfs), str(fi.dev)),
+                           resync_s=3600, watch=False, change_source=lambda: topology_signature(str(fi.sysfs)),
+                           change_interval_s=0.1)
+        t = threading.Thread(target=lab.run, daemon=True)
+        t.start()
+        deadline = time.monotonic() + 10
+        while srv.labels("worker-4").get("amd.com/gpu.compute-memory-partition") != "spx_nps1":
+            assert time.monotonic() < deadline
+            time.sleep(0.02)
+        new = tmp_path / "n.new"
+        make_mi355x_node(new, compute_partition="dpx", generation=2)
+        shutil.rmtree(root / "sys")
+        os.rename(new / "sys", root / "sys")
+        t0 = time.monotonic()
+        while srv.labels("worker-4").get("amd.com/gpu.compute-memory-partition") != "dpx_nps1":
+            assert time.monotonic() - t0 < 1.0, srv.labels("worker-4")
+            time.sleep(0.02)
+        assert lab.stats.topology_changes == 1
+    finally:
+        if lab is not None:
+            lab.stop()
+        srv.stop()
