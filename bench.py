@@ -85,6 +85,9 @@ def make_parser():
                     help="extra untimed admissions with the other --dev-view, reported for comparison")
     ap.add_argument("--b2b-compare", type=int, default=5,
                     help="extra untimed admissions with --settle none, reported for comparison")
+    ap.add_argument("--throughput-check", type=int, default=1,
+                    help="after the timed steps, the throughput check (HBM pattern bandwidth, bf16 MFMA rate, "
+                         "per-XCD clocks) on the advertised GPUs, reported in extra.gpu_throughput (1 = on)")
     ap.add_argument("--peer-check", type=int, default=1,
                     help="after the timed loop, DMA-copy + verify over every pair of the N GPUs' links (H2); "
                          "reported in extra.peer_probe, never part of the metric")
@@ -213,6 +216,26 @@ class PluginUnderTest:
         self.loop.run_until_complete(self.kubelet.stop())
         self.mgr.request_stop()
         self.loop.run_until_complete(self.task)
+
+
+def throughput_check(ordinals) -> dict:
+    """The health monitor's throughput check on the pod's GPUs, once, after the
+    timed steps (context for the latency numbers: what the GPUs deliver)."""
+    import subprocess
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    env = {k: v for k, v in os.environ.items() if k not in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
+    try:
+        p = subprocess.run([str(probe_executable("hsa")), "--perf", "--perf-mib", "4096", "--perf-iters", "65536",
+                            "--devices", "all", "--timeout", "30"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           env=env, timeout=120)
+        devs = json.loads(p.stdout.decode().strip().splitlines()[-1])["devices"]
+    except Exception as e:  # noqa: BLE001 -- context only, never fails the run
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    keys = ("ok", "hbm_write_gbps", "hbm_read_gbps", "hbm_bad_words", "mfma_tflops", "clock_mhz_median",
+            "xcd_clock_mhz", "error")
+    return {"bytes": 4 << 30, "mfma_pairs_per_wave": 65536,
+            "devices": [{"ordinal": o, **{k: d.get(k) for k in keys}} for o, d in zip(ordinals, devs)]}
 
 
 class Dist:
@@ -575,6 +598,8 @@ def main():
         extra["timed_allocation"] = dict({"advertised": m_adv, "requested": n, "held": plug.held},
                                          **alloc_summary(plug, alloc_steps))
         extra["fragmented_n_of_m"] = frag
+        if args.throughput_check and not args.fixture:
+            extra["gpu_throughput"] = throughput_check(adv_ordinals)
         if args.peer_check and not args.fixture:
             from rocm_k8s_device_plugin_amd.health.peer import probe_peers
             try:
