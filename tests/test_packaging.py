@@ -224,3 +224,13 @@ def test_docs_tooling_matches_the_tree(tmp_path):
     dep = yaml.safe_load((REPO / ".github/dependabot.yml").read_text())
     for u in dep["updates"]:
         assert (REPO / u["directory"].lstrip("/")).is_dir()
+
+
+def test_alert_rules_use_exported_metrics():
+    """example/monitoring/prometheusrule.yaml names only metrics the plugin exports."""
+    import re
+    rules = yaml.safe_load((REPO / "example/monitoring/prometheusrule.yaml").read_text())
+    exprs = [r["expr"] for g in rules["spec"]["groups"] for r in g["rules"]]
+    used = {m for e in exprs for m in re.findall(r"mi355x_dp_[a-z_]+", e)}
+    src = "\n".join(p.read_text() for p in (REPO / "rocm_k8s_device_plugin_amd").rglob("*.py"))
+    assert used and all(f'"{m}"' in src for m in used), sorted(m for m in used if f'"{m}"' not in src)
