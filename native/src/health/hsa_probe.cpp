@@ -634,7 +634,9 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     }
     if (slot->blocker) {
       if (H().hsa_signal_load_scacquire(slot->blocker->s) >= 1) {
-        const double s_out = std::chrono::duration<double>(clk::now() - slot->blocked_since).count();
+        // > 0 however recent: pending_s > 0 is what marks the verdict inconclusive
+        const double s_out =
+            std::max(1e-3, std::chrono::duration<double>(clk::now() - slot->blocked_since).count());
         std::snprintf(out->error, sizeof(out->error),
                       "chip sweep / throughput check on this device's queue pending for %.1fs (not completed)", s_out);
         out->pending_s = s_out;
@@ -647,7 +649,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
       // the previous probe's dispatch is still outstanding: wait for it (it
       // carries its own nonce), never stack a second one behind it
       if (!wait_and_verify(ag, slot->r, slot->pending_nonce, slot->pending_iters, timeout_s, out)) {
-        const double s_out = std::chrono::duration<double>(clk::now() - slot->pending_since).count();
+        const double s_out = std::max(1e-3, std::chrono::duration<double>(clk::now() - slot->pending_since).count());
         std::snprintf(out->error, sizeof(out->error), "dispatch pending for %.1fs (not completed)", s_out);
         out->pending_s = s_out;
         return finish();
@@ -661,7 +663,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
         slot->pending_nonce = nonce;
         slot->pending_iters = out->iters;
         slot->pending_since = t0;
-        out->pending_s = std::chrono::duration<double>(clk::now() - t0).count();
+        out->pending_s = std::max(1e-3, std::chrono::duration<double>(clk::now() - t0).count());
         return finish();
       }
     }
@@ -1045,7 +1047,7 @@ struct DeviceWork {
     }
     if (borrowed()) {
       slot->blocker = sig;
-      slot->blocked_since = std::chrono::steady_clock::now();
+      slot->blocked_since = since;  // when the sweep / check was submitted
     }
   }
 

@@ -579,6 +579,48 @@ def test_sweep_and_perf_check_borrow_the_kept_queue(ordinals):
     assert rss_mb < 450, rss_mb
 
 
+def test_check_past_its_deadline_on_the_kept_queue(ordinals):
+    """The abandon path on hardware, without a hang: a throughput check whose
+    MFMA burn (~0.3 s here) outlives a 1 us deadline is reported in flight (its
+    signal and buffers go to the in-flight registry, the kept queue is marked
+    blocked; a probe meanwhile reports pending); once the kernel has finished,
+    probes, sweeps and checks on that GPU run normally again."""
+    import time
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    o = sorted(ordinals.values())[0]
+    env = dict(os.environ, ROCR_VISIBLE_DEVICES=str(o))
+    p = subprocess.Popen([str(probe_executable("hsa")), "--serve", "--keep"], stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, env=env, text=True)
+    try:
+        assert json.loads(p.stdout.readline())["ok"]
+
+        def req(line):
+            p.stdin.write(line + "\n")
+            p.stdin.flush()
+            return json.loads(p.stdout.readline())
+
+        assert req("probe 4 10 0:1")["devices"][0]["ok"]                 # sets the kept slot up
+        late = req("perf 4194304 0.000001 64 0:2")["devices"][0]          # burn >> the 1 us deadline
+        assert not late["ok"] and late["hsa_error"] == -1 and late["kept_queue"], late
+        assert "MFMA burn did not complete" in late["error"], late
+        blocked = req("probe 4 0.05 0:3")["devices"][0]                   # queued behind the burn
+        assert not blocked["ok"] and blocked["pending_s"] > 0, blocked
+        time.sleep(1.0)                                                   # the burn has finished
+        after = req("probe 4 10 0:4")["devices"][0]
+        assert after["ok"] and after["nonce"] == 4, after
+        sweep = req("sweep 4 10 0:5")["devices"][0]
+        assert sweep["ok"] and sweep["kept_queue"], sweep
+        perf = req("perf 1024 10 64 0:6")["devices"][0]
+        assert perf["ok"] and perf["kept_queue"] and perf["hbm_bad_words"] == 0, perf
+        p.stdin.write("quit\n")
+        p.stdin.flush()
+        assert p.wait(timeout=30) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+
+
 def test_monitor_perf_check_on_idle_gpu(inv, ordinals):
     """The health monitor's cadence: liveness, then the throughput check on the
     idle GPU in the same sweep; a healthy MI355X clears every floor."""
