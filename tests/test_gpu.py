@@ -579,6 +579,28 @@ def test_sweep_and_perf_check_borrow_the_kept_queue(ordinals):
     assert rss_mb < 450, rss_mb
 
 
+def test_probe_server_killed_between_sweeps_is_replaced(ordinals):
+    """SIGKILL of the real probe server (OOM killer, operator): the next sweep
+    starts a new one and verifies a fresh nonce; no verdict is lost."""
+    import signal as _signal
+    from rocm_k8s_device_plugin_amd.health.liveness import LivenessProber
+    o = sorted(ordinals.values())[0]
+    prober = LivenessProber(timeout_s=60)
+
+    async def go():
+        first = (await prober.probe({"gpu": o}))["gpu"]
+        os.kill(prober._server.proc.pid, _signal.SIGKILL)
+        await asyncio.sleep(0.5)
+        second = (await prober.probe({"gpu": o}))["gpu"]
+        starts = prober.server_starts
+        await prober.close()
+        return first, second, starts
+
+    first, second, starts = asyncio.run(go())
+    assert first.ok and second.ok, (first, second)
+    assert starts == 2 and second.detail["nonce"] != first.detail["nonce"]
+
+
 def test_check_past_its_deadline_on_the_kept_queue(ordinals):
     """The abandon path on hardware, without a hang: a throughput check whose
     MFMA burn (~0.3 s here) outlives a 1 us deadline is reported in flight (its
