@@ -126,3 +126,38 @@ def test_single_strategy_turning_heterogeneous_advertises_nothing(tmp_path):
             assert st.devices == {}
 
     run(go())
+
+
+def test_topology_watch_waits_for_a_fingerprint_to_hold(tmp_path):
+    """A fingerprint seen once (a switch half done) does not trigger a
+    re-discovery; one that holds for a second poll does."""
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = ContainerImpl("single", str(fi.sysfs), HealthConfig(exporter_socket=None))
+    seq = ["A", "A", "B", "A", "A", "C", "C"]
+    polls, reloads = [], []
+
+    def fingerprint():
+        v = seq[min(len(polls), len(seq) - 1)]
+        polls.append(v)
+        return v
+
+    async def reload_topology():
+        reloads.append(polls[-1])
+        return None
+
+    impl.topology_fingerprint = fingerprint
+    impl.reload_topology = reload_topology
+    mgr = PluginManager(impl, ManagerConfig(pulse_s=0, plugin_dir=str(tmp_path / "dp"), handle_signals=False,
+                                            topology_watch_s=0.01))
+
+    async def go():
+        mgr._impl_lock = asyncio.Lock()   # run() creates it on its loop
+        task = asyncio.create_task(mgr._topology_loop())
+        while len(polls) < len(seq):
+            await asyncio.sleep(0.005)
+        mgr.stopped.set()
+        await asyncio.wait_for(task, 5)
+
+    run(go())
+    # first sighting of each value skips (A, B, A again, C); stable repeats re-discover
+    assert reloads[:3] == ["A", "A", "C"], reloads
