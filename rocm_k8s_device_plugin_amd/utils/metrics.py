@@ -9,19 +9,22 @@ from __future__ import annotations
 
 import asyncio
 import bisect
+from collections import deque
 import threading
-from typing import Dict, List, Optional, Tuple
+from typing import Deque, Dict, List, Optional, Tuple
 
 _BUCKETS_MS = [0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 25, 50, 100, 250, 500, 1000, 2500, 5000, 10000]
 
 
 class Histogram:
-    def __init__(self, name: str, help: str, keep_samples: int = 100000):
+    # quantile() looks at the most recent samples only: a daemon that runs for
+    # months must not keep every observation (the buckets keep the totals)
+    def __init__(self, name: str, help: str, keep_samples: int = 4096):
         self.name, self.help = name, help
         self.counts = [0] * (len(_BUCKETS_MS) + 1)
         self.sum = 0.0
         self.n = 0
-        self.samples: List[float] = []
+        self.samples: Deque[float] = deque(maxlen=keep_samples)
         self.keep = keep_samples
         self._lock = threading.Lock()
 
@@ -30,8 +33,7 @@ class Histogram:
             self.counts[bisect.bisect_left(_BUCKETS_MS, ms)] += 1
             self.sum += ms
             self.n += 1
-            if len(self.samples) < self.keep:
-                self.samples.append(ms)
+            self.samples.append(ms)
 
     def quantile(self, q: float) -> float:
         with self._lock:

@@ -1218,3 +1218,14 @@ def test_kubelet_restart_seen_by_inotify_not_the_poll(tmp_path):
 
     dt, regs = run(go())
     assert regs == 2 and dt < 1.5, dt
+
+
+def test_histograms_keep_a_bounded_window():
+    """A long-running daemon keeps bucket totals for every observation but only a
+    recent window of raw samples (found by the 15-minute MI355X soak)."""
+    from rocm_k8s_device_plugin_amd.utils.metrics import Histogram
+    h = Histogram("x", "")
+    for i in range(20000):
+        h.observe(float(i))
+    assert h.n == 20000 and sum(h.counts) == 20000 and len(h.samples) == 4096
+    assert h.quantile(0.0) == 20000 - 4096
