@@ -254,6 +254,7 @@ void release_residents();
 
 namespace {
 void forget_in_flight_sweeps();
+double in_flight_for(int ordinal);
 }  // namespace
 
 extern "C" void mi355x_hsa_probe_shutdown(void) {
@@ -644,6 +645,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
         return finish();
       }
       slot->blocker.reset();
+      in_flight_for(ordinal);  // frees the completed sweep / check's buffers now, not at the next one
     }
     if (slot->pending) {
       // the previous probe's dispatch is still outstanding: wait for it (it
