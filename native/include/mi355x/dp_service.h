@@ -1,5 +1,12 @@
 // v1beta1.DevicePlugin on the native gRPC server.
 //
+// Reference semantics: AMDGPUPlugin (internal/pkg/plugin/plugin.go:132-186),
+// the container DeviceImpl's Allocate / GetPreferredAllocation
+// (internal/pkg/amdgpu/amdgpu.go:255-319) and the wire contract
+// (vendor/k8s.io/kubelet/pkg/apis/deviceplugin/v1beta1/api.proto). Error
+// strings match the reference's (GetPreferredAllocation:
+// "unable to get preferred allocation list. Error:...", amdgpu.go:310-311).
+//
 // The kubelet's admission RPCs are answered without entering Python:
 //   GetPreferredAllocation  protobuf decode -> HiveAllocator -> encode
 //   Allocate                per-device response fragments prepared by the
