@@ -11,6 +11,7 @@ COPY native native
 COPY rocm_k8s_device_plugin_amd rocm_k8s_device_plugin_amd
 RUN python3 rocm_k8s_device_plugin_amd/_build.py && \
     rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe --help >/dev/null && \
+    rocm_k8s_device_plugin_amd/bin/mi355x-device-plugin -h >/dev/null && \
     python3 -c "import rocm_k8s_device_plugin_amd.proto.deviceplugin, rocm_k8s_device_plugin_amd.proto.metricssvc"
 
 FROM ${ROCM_IMAGE}
@@ -21,5 +22,8 @@ RUN apt-get update && apt-get install -y --no-install-recommends python3 python3
 WORKDIR /root
 COPY --from=build /src/rocm_k8s_device_plugin_amd /opt/mi355x-dp/rocm_k8s_device_plugin_amd
 COPY scripts/k8s-device-plugin /root/k8s-device-plugin
+# the same plugin as one native process (container driver, no Python in it):
+# command: ["./mi355x-device-plugin", "-pulse=30"]
+RUN ln -s /opt/mi355x-dp/rocm_k8s_device_plugin_amd/bin/mi355x-device-plugin /root/mi355x-device-plugin
 ENV MI355X_DP_HOME=/opt/mi355x-dp MI355X_DP_NO_AUTOBUILD=1
 CMD ["./k8s-device-plugin", "-logtostderr=true", "-stderrthreshold=INFO", "-v=5"]

@@ -1,0 +1,243 @@
+"""The native daemon (`mi355x-device-plugin`, native/src/daemon/): the device
+plugin as one C++ process, driven end to end by the fake kubelet on generated
+MI355X sysfs trees. Its ListAndWatch lists, GetPreferredAllocation and
+Allocate answers must equal the Python plugin's (ContainerImpl) on the same
+node; registration, kubelet restarts, exporter health and SIGTERM follow the
+reference (cmd/k8s-device-plugin/main.go, vendored dpm manager/plugin)."""
+import asyncio
+import os
+import random
+import signal
+import subprocess
+import time
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+from rocm_k8s_device_plugin_amd.plugin.base import new_context
+from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+from rocm_k8s_device_plugin_amd.testing.fake_exporter import FakeExporter
+from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+
+EXE = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} was not built")
+
+
+def run(coro, timeout=60):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+async def _daemon(kdir, fi, *extra):
+    return await asyncio.create_subprocess_exec(
+        EXE, "-kubelet_dir", kdir, "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), *extra,
+        stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
+
+
+async def _stop(proc):
+    if proc.returncode is None:
+        proc.send_signal(signal.SIGTERM)
+    _, err = await asyncio.wait_for(proc.communicate(), 20)
+    return proc.returncode, err.decode(errors="replace")
+
+
+def _python_impl(fi, strategy="single"):
+    return ContainerImpl(strategy, str(fi.sysfs), HealthConfig(exporter_socket=None))
+
+
+@pytest.mark.parametrize("partition,strategy,resource", [("spx", "single", "gpu"), ("cpx", "single", "gpu"),
+                                                         ("cpx", "mixed", "cpx_nps1")])
+def test_answers_equal_the_python_plugin(tmp_path, partition, strategy, resource):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition=partition)
+    impl = _python_impl(fi, strategy)
+    ctx = new_context(resource)
+    impl.start(ctx)
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", "", "-resource_naming_strategy", strategy)
+        try:
+            st = await k.wait_for_resource(f"amd.com/{resource}", len(impl.devices(resource)), timeout=20)
+            # the list kubelet received, device for device
+            want = {d.ID: d.health for d in impl.enumerate(ctx)}
+            assert st.devices == want
+            opts = await k._call(st, "GetDevicePluginOptions", pb.Empty(), pb.DevicePluginOptions)
+            assert opts == impl.options(ctx)
+            rng = random.Random(3)
+            ids = sorted(want)
+            for _ in range(25):
+                avail = sorted(rng.sample(ids, rng.randint(1, len(ids))))
+                size = rng.randint(1, len(avail))
+                must = sorted(rng.sample(avail, rng.randint(0, min(2, size))))
+                preq = pb.PreferredAllocationRequest(container_requests=[pb.ContainerPreferredAllocationRequest(
+                    available_deviceIDs=avail, must_include_deviceIDs=must, allocation_size=size)])
+                got = await k._call(st, "GetPreferredAllocation", preq, pb.PreferredAllocationResponse)
+                assert got == impl.preferred_allocation(ctx, preq)
+                chosen = list(got.container_responses[0].deviceIDs)
+                areq = pb.AllocateRequest(container_requests=[pb.ContainerAllocateRequest(devices_ids=chosen),
+                                                              pb.ContainerAllocateRequest(devices_ids=[])])
+                assert await k._call(st, "Allocate", areq, pb.AllocateResponse) == impl.allocate(ctx, areq)
+            pre = await k._call(st, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=ids[:1]),
+                                pb.PreStartContainerResponse)
+            assert pre == pb.PreStartContainerResponse()
+            reg = k.registrations[-1]
+            assert (reg.version, reg.endpoint, reg.resource_name) == ("v1beta1", f"amd.com_{resource}",
+                                                                      f"amd.com/{resource}")
+            assert reg.options.get_preferred_allocation_available
+        finally:
+            rc, err = await _stop(proc)
+            await k.stop()
+        assert rc == 0, err[-2000:]
+        assert not os.path.exists(os.path.join(kdir, f"amd.com_{resource}"))   # socket removed on SIGTERM
+
+    run(go())
+
+
+def test_unknown_device_id_is_invalid_argument(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", "")
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            with pytest.raises(Exception) as ei:
+                await k._call(st, "Allocate", pb.AllocateRequest(container_requests=[
+                    pb.ContainerAllocateRequest(devices_ids=["nope"])]), pb.AllocateResponse)
+            assert "unknown device ID 'nope'" in str(ei.value.details() if hasattr(ei.value, "details") else ei.value)
+        finally:
+            await _stop(proc)
+            await k.stop()
+
+    run(go())
+
+
+def test_kubelet_restart_re_registers(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", "")
+        try:
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            first = k.register_times["amd.com/gpu"]
+            t0 = time.monotonic()
+            await k.restart(downtime_s=0.2)
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            assert k.register_times["amd.com/gpu"] > first
+            assert k.register_times["amd.com/gpu"] - t0 < 2.0      # inotify, not a poll
+            adm = await k.admit("amd.com/gpu", 2)
+            assert len(adm.device_ids) == 2 and st.devices
+        finally:
+            rc, err = await _stop(proc)
+            await k.stop()
+        assert rc == 0, err[-2000:]
+
+    run(go())
+
+
+def test_exporter_verdict_reaches_listandwatch(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    sock = str(tmp_path / "exp" / "exporter.sock")
+
+    async def go():
+        exp = FakeExporter(sock, {b: "healthy" for b in fi.bdfs})
+        await exp.start()
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", sock, "-pulse", "1")
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            assert all(h == "Healthy" for h in st.devices.values())
+            u = st.updates
+            exp.states[fi.bdfs[5]] = "unhealthy"
+            st = await k.wait_for_update("amd.com/gpu", u, timeout=10)
+            assert st.devices[fi.bdfs[5]] == "Unhealthy"
+            assert sum(h == "Unhealthy" for h in st.devices.values()) == 1
+            exp.states[fi.bdfs[5]] = "healthy"
+            st = await k.wait_for_update("amd.com/gpu", st.updates, timeout=10)
+            assert all(h == "Healthy" for h in st.devices.values())
+        finally:
+            rc, err = await _stop(proc)
+            await k.stop()
+            await exp.stop()
+        assert rc == 0, err[-2000:]
+
+    run(go())
+
+
+def test_kfd_node_loss_marks_the_device_unhealthy(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", "", "-pulse", "1")
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            impl = _python_impl(fi)
+            dev = impl.inv.by_id[fi.bdfs[2]]
+            os.unlink(fi.sysfs / f"class/kfd/kfd/topology/nodes/{dev.node_id}/properties")
+            st = await k.wait_for_update("amd.com/gpu", st.updates, timeout=10)
+            assert st.devices[fi.bdfs[2]] == "Unhealthy"
+        finally:
+            await _stop(proc)
+            await k.stop()
+
+    run(go())
+
+
+def test_starts_before_the_kubelet_and_registers_when_it_comes(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+
+    async def go():
+        proc = await _daemon(kdir, fi, "-exporter_socket", "")
+        await asyncio.sleep(0.5)
+        k = FakeKubelet(kdir)
+        await k.start()
+        try:
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+        finally:
+            await _stop(proc)
+            await k.stop()
+
+    run(go())
+
+
+def test_flags(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    base = [EXE, "-kubelet_dir", str(tmp_path / "dp"), "-sysfs_root", str(fi.sysfs)]
+    p = subprocess.run(base + ["-driver_type", "gpu"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 1 and "invalid driver_type provided: gpu" in p.stderr
+    p = subprocess.run(base + ["-resource_naming_strategy", "x"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 1 and "invalid resource_naming_strategy" in p.stderr
+    p = subprocess.run(base + ["-pulse=-1"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 1 and "pulse must be a non-negative integer" in p.stderr
+    p = subprocess.run(base + ["-driver_type=vf-passthrough"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 1 and "full plugin" in p.stderr
+    p = subprocess.run([EXE, "-h"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 0 and "-resource_naming_strategy" in p.stdout
+    # heterogeneous partitions with the single strategy: the reference's init error
+    het = make_mi355x_node(tmp_path / "het", per_gpu_compute=["spx"] * 4 + ["cpx"] * 4)
+    p = subprocess.run([EXE, "-kubelet_dir", str(tmp_path / "dp2"), "-sysfs_root", str(het.sysfs)],
+                       capture_output=True, text=True, timeout=30)
+    assert p.returncode == 1 and "not supported with single strategy" in p.stderr
