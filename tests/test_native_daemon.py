@@ -22,7 +22,8 @@ from rocm_k8s_device_plugin_amd.testing.fake_exporter import FakeExporter
 from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
 from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
 
-EXE = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+# MI355X_NATIVE_DAEMON_EXE: run these tests against another build (e.g. the ASan / TSan ctest builds)
+EXE = os.environ.get("MI355X_NATIVE_DAEMON_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -119,8 +120,9 @@ def test_unknown_device_id_is_invalid_argument(tmp_path):
                     pb.ContainerAllocateRequest(devices_ids=["nope"])]), pb.AllocateResponse)
             assert "unknown device ID 'nope'" in str(ei.value.details() if hasattr(ei.value, "details") else ei.value)
         finally:
-            await _stop(proc)
+            rc, err = await _stop(proc)
             await k.stop()
+        assert rc == 0, err[-2000:]
 
     run(go())
 
@@ -198,8 +200,9 @@ def test_kfd_node_loss_marks_the_device_unhealthy(tmp_path):
             st = await k.wait_for_update("amd.com/gpu", st.updates, timeout=10)
             assert st.devices[fi.bdfs[2]] == "Unhealthy"
         finally:
-            await _stop(proc)
+            rc, err = await _stop(proc)
             await k.stop()
+        assert rc == 0, err[-2000:]
 
     run(go())
 
@@ -217,8 +220,9 @@ def test_starts_before_the_kubelet_and_registers_when_it_comes(tmp_path):
         try:
             await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
         finally:
-            await _stop(proc)
+            rc, err = await _stop(proc)
             await k.stop()
+        assert rc == 0, err[-2000:]
 
     run(go())
 
