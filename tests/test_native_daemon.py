@@ -245,3 +245,46 @@ def test_flags(tmp_path):
     p = subprocess.run([EXE, "-kubelet_dir", str(tmp_path / "dp2"), "-sysfs_root", str(het.sysfs)],
                        capture_output=True, text=True, timeout=30)
     assert p.returncode == 1 and "not supported with single strategy" in p.stderr
+
+
+@pytest.mark.gpu
+def test_real_node_answers_equal_the_python_plugin(tmp_path):
+    """On the MI355X box's own /sys (where kfd denies the GPUs outside this
+    container's cgroup): the same devices, health, options and Allocate answers
+    as the Python plugin."""
+    impl = ContainerImpl("single", "/sys", HealthConfig(exporter_socket=None))
+    ctx = new_context("gpu")
+    impl.start(ctx)
+    want = {d.ID: d.health for d in impl.enumerate(ctx)}
+    assert want, "no GPUs discovered on the box"
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        t0 = time.monotonic()
+        proc = await asyncio.create_subprocess_exec(EXE, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1",
+                                                    stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", len(want), timeout=20)
+            registered_s = k.register_times["amd.com/gpu"] - t0
+            assert st.devices == want
+            assert await k._call(st, "GetDevicePluginOptions", pb.Empty(), pb.DevicePluginOptions) == impl.options(ctx)
+            ids = sorted(want)
+            for size in sorted({1, min(2, len(ids)), len(ids)}):
+                preq = pb.PreferredAllocationRequest(container_requests=[pb.ContainerPreferredAllocationRequest(
+                    available_deviceIDs=ids, allocation_size=size)])
+                got = await k._call(st, "GetPreferredAllocation", preq, pb.PreferredAllocationResponse)
+                assert got == impl.preferred_allocation(ctx, preq)
+                areq = pb.AllocateRequest(container_requests=[pb.ContainerAllocateRequest(
+                    devices_ids=list(got.container_responses[0].deviceIDs))])
+                assert await k._call(st, "Allocate", areq, pb.AllocateResponse) == impl.allocate(ctx, areq)
+            await asyncio.sleep(1.5)     # a health pulse on the live kfd nodes changes nothing
+            assert k.resources["amd.com/gpu"].devices == want
+        finally:
+            rc, err = await _stop(proc)
+            await k.stop()
+        assert rc == 0, err[-2000:]
+        print(f"native daemon on the box: {len(want)} devices, registered {registered_s * 1e3:.1f} ms after exec")
+
+    run(go())
