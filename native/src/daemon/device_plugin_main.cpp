@@ -193,6 +193,7 @@ struct Resource {
   std::string list;                    // serialized ListAndWatchResponse
   bool registered = false;
   std::chrono::steady_clock::time_point next_register{};
+  int retry_ms = 100;  // kubelet.sock appears (bind) just before kubelet listens: retry soon, then back off to 3 s
 };
 
 std::string list_bytes(const Resource& r) {
@@ -447,13 +448,16 @@ int main(int argc, char** argv) {
   DirWatcher watch;
   const std::string werr = watch.open(f.kubelet_dir);
   if (!werr.empty()) logf('W', "no inotify watch on %s (%s): polling every second", f.kubelet_dir.c_str(), werr.c_str());
+  auto try_register = [&](Resource& r) {
+    r.registered = register_with_kubelet(r, kubelet_sock, f.register_timeout_s);
+    r.next_register = std::chrono::steady_clock::now() + std::chrono::milliseconds(r.retry_ms);
+    r.retry_ms = r.registered ? 100 : std::min(2 * r.retry_ms, 3000);
+  };
   auto start_all = [&] {
     for (auto& r : resources) {
       stop_server(r);
-      if (start_server(r)) {
-        r.registered = register_with_kubelet(r, kubelet_sock, f.register_timeout_s);
-        r.next_register = std::chrono::steady_clock::now() + std::chrono::seconds(3);
-      }
+      r.retry_ms = 100;
+      if (start_server(r)) try_register(r);
     }
   };
   if (path_exists(kubelet_sock)) start_all();
@@ -465,10 +469,11 @@ int main(int argc, char** argv) {
     pollfd pfd[2] = {{g_sig_pipe[0], POLLIN, 0}, {watch.fd(), POLLIN, 0}};
     const int nfd = watch.fd() >= 0 ? 2 : 1;
     auto wait_ms = std::chrono::duration_cast<std::chrono::milliseconds>(next_pulse - clk::now()).count();
-    if (watch.fd() < 0 || std::any_of(resources.begin(), resources.end(), [](const Resource& r) {
-          return r.server && !r.registered;
-        }))
-      wait_ms = std::min<long long>(wait_ms, 1000);
+    if (watch.fd() < 0) wait_ms = std::min<long long>(wait_ms, 1000);
+    for (const auto& r : resources)
+      if (r.server && !r.registered)
+        wait_ms = std::min<long long>(
+            wait_ms, std::chrono::duration_cast<std::chrono::milliseconds>(r.next_register - clk::now()).count() + 1);
     ::poll(pfd, nfd, static_cast<int>(std::max<long long>(0, wait_ms)));
     if (g_stop) break;
     bool kubelet_event = false;
@@ -489,10 +494,7 @@ int main(int argc, char** argv) {
     }
     // registrations that failed (kubelet not serving yet): retry, rate-limited
     for (auto& r : resources)
-      if (r.server && !r.registered && present && clk::now() >= r.next_register) {
-        r.registered = register_with_kubelet(r, kubelet_sock, f.register_timeout_s);
-        r.next_register = clk::now() + std::chrono::seconds(3);
-      }
+      if (r.server && !r.registered && present && clk::now() >= r.next_register) try_register(r);
     if (f.pulse > 0 && clk::now() >= next_pulse) {
       next_pulse = clk::now() + std::chrono::seconds(f.pulse);
       const auto exporter = exporter_health(f.exporter_socket);
