@@ -23,7 +23,7 @@ WORKDIR /root
 COPY --from=build /src/rocm_k8s_device_plugin_amd /opt/mi355x-dp/rocm_k8s_device_plugin_amd
 COPY scripts/k8s-device-plugin /root/k8s-device-plugin
 # the same plugin as one native process (container driver, no Python in it):
-# command: ["./mi355x-device-plugin", "-pulse=30"]
+# command: ["./mi355x-device-plugin", "-pulse=30"]   (Helm: dp.native=true)
 RUN ln -s /opt/mi355x-dp/rocm_k8s_device_plugin_amd/bin/mi355x-device-plugin /root/mi355x-device-plugin
 ENV MI355X_DP_HOME=/opt/mi355x-dp MI355X_DP_NO_AUTOBUILD=1
 CMD ["./k8s-device-plugin", "-logtostderr=true", "-stderrthreshold=INFO", "-v=5"]

@@ -234,3 +234,13 @@ def test_alert_rules_use_exported_metrics():
     used = {m for e in exprs for m in re.findall(r"mi355x_dp_[a-z_]+", e)}
     src = "\n".join(p.read_text() for p in (REPO / "rocm_k8s_device_plugin_amd").rglob("*.py"))
     assert used and all(f'"{m}"' in src for m in used), sorted(m for m in used if f'"{m}"' not in src)
+
+
+def test_helm_native_daemon_switch():
+    """dp.native runs the native daemon; it refuses the features only the full plugin has."""
+    t = (REPO / "helm/amd-gpu/templates/deviceplugin-daemonset.yaml").read_text()
+    assert 'command: ["./mi355x-device-plugin"]' in t and "{{- if .Values.dp.native }}" in t
+    assert 'fail "dp.native' in t
+    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["dp"]["native"] is False
+    for df in ("Dockerfile", "ubi-dp.Dockerfile"):
+        assert "bin/mi355x-device-plugin /root/mi355x-device-plugin" in (REPO / df).read_text(), df

@@ -16,6 +16,7 @@ COPY --from=build /opt/rocm/lib/libhsa-runtime64.so* /opt/rocm/lib/librocprofile
 WORKDIR /root
 COPY --from=build /src/rocm_k8s_device_plugin_amd /opt/mi355x-dp/rocm_k8s_device_plugin_amd
 COPY scripts/k8s-device-plugin /root/k8s-device-plugin
+RUN ln -s /opt/mi355x-dp/rocm_k8s_device_plugin_amd/bin/mi355x-device-plugin /root/mi355x-device-plugin
 COPY LICENSE* /licenses/
 ENV MI355X_DP_HOME=/opt/mi355x-dp MI355X_DP_NO_AUTOBUILD=1 LD_LIBRARY_PATH=/opt/rocm/lib
 CMD ["./k8s-device-plugin", "-logtostderr=true", "-stderrthreshold=INFO", "-v=5", "-pulse=30"]
