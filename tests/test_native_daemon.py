@@ -184,6 +184,35 @@ def test_exporter_verdict_reaches_listandwatch(tmp_path):
     run(go())
 
 
+def test_exporter_verdict_covers_every_partition_of_the_gpu(tmp_path):
+    """CPX: the exporter's per-BDF verdict marks all 8 partitions of that GPU."""
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="cpx")
+    kdir = str(tmp_path / "dp")
+    sock = str(tmp_path / "exp" / "exporter.sock")
+    impl = _python_impl(fi)
+    parts = [d.id for d in impl.inv.devices if d.bdf == fi.bdfs[3]]
+    assert len(parts) == 8
+
+    async def go():
+        exp = FakeExporter(sock, {b: "healthy" for b in fi.bdfs})
+        await exp.start()
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", sock, "-pulse", "1")
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 64, timeout=20)
+            exp.states[fi.bdfs[3]] = "unhealthy"
+            st = await k.wait_for_update("amd.com/gpu", st.updates, timeout=10)
+            assert sorted(i for i, h in st.devices.items() if h == "Unhealthy") == sorted(parts)
+        finally:
+            rc, err = await _stop(proc)
+            await k.stop()
+            await exp.stop()
+        assert rc == 0, err[-2000:]
+
+    run(go())
+
+
 def test_kfd_node_loss_marks_the_device_unhealthy(tmp_path):
     fi = make_mi355x_node(tmp_path / "n")
     kdir = str(tmp_path / "dp")
