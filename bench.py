@@ -608,6 +608,12 @@ def main():
             except Exception as e:  # noqa: BLE001
                 extra["peer_probe"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         plug.stop()
+        # tasks still parked (watchers, event waits): cancel them before the loop goes
+        rest = [t for t in asyncio.all_tasks(loop) if not t.done()]
+        for t in rest:
+            t.cancel()
+        if rest:
+            loop.run_until_complete(asyncio.gather(*rest, return_exceptions=True))
         loop.close()
         out = {
             "metric": METRIC,
