@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import http.client
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Optional
 
@@ -144,7 +145,7 @@ class NodeLabeller:
                     stream.close()
                     return
                 self.stats.watch_restarts += 1
-                backoff = 0.2
+                opened = time.monotonic()
                 for ev in stream:
                     self.stats.watch_events += 1
                     typ, obj = ev.get("type"), ev.get("object") or {}
@@ -159,6 +160,14 @@ class NodeLabeller:
                     if typ in ("ADDED", "MODIFIED") and self._needs_reconcile(obj):
                         self.stats.watch_kicks += 1
                         self._kick.set()
+                # a stream that lived its timeout reconnects at once; one the
+                # server ends right away (proxy, overloaded apiserver) backs off
+                # like an error instead of spinning on reconnects
+                if time.monotonic() - opened >= 1.0:
+                    backoff = 0.2
+                elif not self._stop.is_set():
+                    self._stop.wait(backoff)
+                    backoff = min(backoff * 2, self.watch_backoff_max_s)
             except (KubeError, OSError, ValueError, http.client.HTTPException) as e:
                 if self._stop.is_set():
                     return

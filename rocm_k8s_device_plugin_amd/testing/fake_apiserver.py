@@ -38,6 +38,7 @@ class FakeApiServer:
         self.min_rv = 0                  # watches from an older resourceVersion get a 410 ERROR event
         self.watchers: List[Tuple[str, "queue.Queue"]] = []
         self.watch_starts = 0
+        self.watch_max_s: Optional[float] = None   # end every watch after this long (a proxy that cuts streams)
         self._lock = threading.Lock()
         srv = self
 
@@ -56,6 +57,8 @@ class FakeApiServer:
                 name = (q.get("fieldSelector", [""])[0].partition("metadata.name=")[2])
                 rv = q.get("resourceVersion", [""])[0]
                 timeout = float(q.get("timeoutSeconds", ["300"])[0])
+                if srv.watch_max_s is not None:
+                    timeout = min(timeout, srv.watch_max_s)
                 events: "queue.Queue" = queue.Queue()
                 with srv._lock:
                     node = copy.deepcopy(srv.nodes.get(name))

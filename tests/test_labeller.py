@@ -2,6 +2,7 @@
 reconcile loop against a fake apiserver."""
 import json
 import os
+import time
 
 import pytest
 
@@ -416,6 +417,27 @@ def test_watch_failure_backs_off_and_resync_still_applies(tmp_path):
         srv.expire_watches()
         assert _wait(lambda: lab.stats.watch_errors >= 2, 5.0)
         assert orig is srv.requests and t.is_alive()
+    finally:
+        if lab is not None:
+            lab.stop()
+            t.join(5)
+        srv.stop()
+
+
+def test_watch_cut_right_away_backs_off_instead_of_spinning(tmp_path):
+    """A server (or proxy) that ends every watch stream at once is reconnected
+    with backoff, not in a tight loop; a stripped label still comes back."""
+    srv = FakeApiServer(token="tok").start()
+    lab = t = None
+    try:
+        srv.add_node("node-w")
+        srv.watch_max_s = 0.0
+        lab, t = _running_labeller(tmp_path, srv, watch_backoff_max_s=0.4)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-w"))
+        time.sleep(2.0)
+        # backoff 0.2, 0.4, 0.4, ...: a handful of reconnects in 2 s (a spin makes hundreds)
+        assert 2 <= srv.watch_starts <= 12, srv.watch_starts
+        assert lab.stats.watch_errors == 0 and t.is_alive()
     finally:
         if lab is not None:
             lab.stop()
