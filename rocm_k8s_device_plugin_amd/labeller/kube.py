@@ -9,6 +9,12 @@ changes to other fields and needs no resourceVersion retry loop.
 Config sources, in order: ``--kubeconfig`` (token or client-certificate auth,
 embedded or file CA), ``$KUBECONFIG``, in-cluster service account
 (KUBERNETES_SERVICE_HOST/PORT + /var/run/secrets/kubernetes.io/serviceaccount).
+
+Token files (the service account's projected token, a kubeconfig
+``tokenFile``) are re-read when they change: kubelet rotates projected tokens
+well inside their lifetime, and client-go -- which the reference's
+controller-runtime uses -- reloads them the same way. A 401 re-reads the file
+at once and retries the request one time.
 """
 from __future__ import annotations
 
@@ -43,6 +49,23 @@ class KubeConfig:
     cert_file: Optional[str] = None
     key_file: Optional[str] = None
     insecure: bool = False
+    token_file: Optional[str] = None
+    _token_mtime: int = -1
+
+    def bearer(self, force: bool = False) -> Optional[str]:
+        """The current token: re-read from token_file when its mtime changed
+        (or when forced after a 401); the last good value if the read fails."""
+        if self.token_file:
+            try:
+                mt = os.stat(self.token_file).st_mtime_ns
+                if force or mt != self._token_mtime:
+                    with open(self.token_file) as f:
+                        tok = f.read().strip()
+                    if tok:
+                        self.token, self._token_mtime = tok, mt
+            except OSError:
+                pass
+        return self.token
 
     def ssl_context(self) -> Optional[ssl.SSLContext]:
         if not self.server.startswith("https"):
@@ -83,18 +106,20 @@ def load_kubeconfig(path: str) -> KubeConfig:
         return p if not p or os.path.isabs(p) else os.path.join(base, p)
 
     token = user.get("token")
-    if not token and user.get("tokenFile"):
-        with open(rel(user["tokenFile"])) as f:
-            token = f.read().strip()
-    return KubeConfig(
+    token_file = rel(user["tokenFile"]) if not token and user.get("tokenFile") else None
+    cfg = KubeConfig(
         server=cluster.get("server", "").rstrip("/"),
         token=token,
+        token_file=token_file,
         ca_file=rel(cluster.get("certificate-authority")) or _materialise(cluster.get("certificate-authority-data"),
                                                                           ".crt"),
         cert_file=rel(user.get("client-certificate")) or _materialise(user.get("client-certificate-data"), ".crt"),
         key_file=rel(user.get("client-key")) or _materialise(user.get("client-key-data"), ".key"),
         insecure=bool(cluster.get("insecure-skip-tls-verify")),
     )
+    if token_file and not cfg.bearer():
+        raise KubeError(0, f"kubeconfig tokenFile {token_file} is unreadable or empty")
+    return cfg
 
 
 def in_cluster_config(sa_dir: Optional[str] = None) -> KubeConfig:
@@ -105,10 +130,12 @@ def in_cluster_config(sa_dir: Optional[str] = None) -> KubeConfig:
         raise KubeError(0, "not running in a cluster (KUBERNETES_SERVICE_HOST unset) and no kubeconfig given")
     if ":" in host and not host.startswith("["):
         host = f"[{host}]"
-    with open(os.path.join(sa_dir, "token")) as f:
-        token = f.read().strip()
     ca = os.path.join(sa_dir, "ca.crt")
-    return KubeConfig(server=f"https://{host}:{port}", token=token, ca_file=ca if os.path.exists(ca) else None)
+    cfg = KubeConfig(server=f"https://{host}:{port}", token_file=os.path.join(sa_dir, "token"),
+                     ca_file=ca if os.path.exists(ca) else None)
+    if not cfg.bearer():
+        raise KubeError(0, f"service-account token {cfg.token_file} is unreadable or empty")
+    return cfg
 
 
 def get_config(kubeconfig: str = "") -> KubeConfig:
@@ -166,20 +193,24 @@ class KubeClient:
         self._ssl = cfg.ssl_context()
 
     def _request(self, method: str, path: str, body: Optional[dict] = None,
-                 content_type: str = "application/json") -> dict:
+                 content_type: str = "application/json", _retry: bool = True) -> dict:
         data = json.dumps(body).encode() if body is not None else None
         req = urllib.request.Request(self.cfg.server + path, data=data, method=method)
         req.add_header("Accept", "application/json")
         req.add_header("User-Agent", "mi355x-node-labeller")
         if data is not None:
             req.add_header("Content-Type", content_type)
-        if self.cfg.token:
-            req.add_header("Authorization", f"Bearer {self.cfg.token}")
+        tok = self.cfg.bearer()
+        if tok:
+            req.add_header("Authorization", f"Bearer {tok}")
         try:
             with urllib.request.urlopen(req, timeout=self.timeout_s, context=self._ssl) as resp:
                 raw = resp.read()
         except urllib.error.HTTPError as e:
-            raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from e
+            msg = e.read().decode(errors="replace")[:500]
+            if e.code == 401 and _retry and self.cfg.token_file and self.cfg.bearer(force=True) != tok:
+                return self._request(method, path, body, content_type, _retry=False)   # rotated token
+            raise KubeError(e.code, msg) from e
         except urllib.error.URLError as e:
             raise KubeError(0, str(e.reason)) from e
         return json.loads(raw) if raw else {}
@@ -202,8 +233,9 @@ class KubeClient:
         req = urllib.request.Request(self.cfg.server + "/api/v1/nodes?" + urllib.parse.urlencode(q), method="GET")
         req.add_header("Accept", "application/json")
         req.add_header("User-Agent", "mi355x-node-labeller")
-        if self.cfg.token:
-            req.add_header("Authorization", f"Bearer {self.cfg.token}")
+        tok = self.cfg.bearer()
+        if tok:
+            req.add_header("Authorization", f"Bearer {tok}")
         try:
             resp = urllib.request.urlopen(req, timeout=timeout_s + 30, context=self._ssl)
         except urllib.error.HTTPError as e:

@@ -424,6 +424,44 @@ def test_watch_failure_backs_off_and_resync_still_applies(tmp_path):
         srv.stop()
 
 
+def test_rotated_service_account_token_is_picked_up(tmp_path, monkeypatch):
+    """kubelet rewrites the projected token inside its lifetime: requests use
+    the new file content (mtime change), and a 401 re-reads the file once."""
+    from rocm_k8s_device_plugin_amd.labeller import kube
+    srv = FakeApiServer(token="tok-1").start()
+    try:
+        srv.add_node("n1")
+        sa = tmp_path / "sa"
+        sa.mkdir()
+        (sa / "token").write_text("tok-1\n")
+        monkeypatch.setenv("KUBERNETES_SERVICE_HOST", "127.0.0.1")
+        cfg = kube.in_cluster_config(str(sa))
+        cfg.server = srv.url                       # plain HTTP fake
+        c = KubeClient(cfg)
+        assert c.get_node("n1")["metadata"]["name"] == "n1"
+        # rotation: the server and the file move to tok-2 together
+        srv.token = "tok-2"
+        (sa / "token").write_text("tok-2\n")
+        os.utime(sa / "token", ns=(time.time_ns(), time.time_ns() + 10**9))
+        assert c.get_node("n1")["metadata"]["name"] == "n1" and cfg.token == "tok-2"
+        # the server moved on first (mtime unchanged): the 401 forces a re-read
+        st = os.stat(sa / "token")
+        srv.token = "tok-3"
+        (sa / "token").write_text("tok-3\n")
+        os.utime(sa / "token", ns=(st.st_atime_ns, st.st_mtime_ns))
+        assert c.get_node("n1")["metadata"]["name"] == "n1" and cfg.token == "tok-3"
+        # a stale file stays a 401 (one retry, no loop)
+        srv.token = "tok-4"
+        with pytest.raises(KubeError) as ei:
+            c.get_node("n1")
+        assert ei.value.status == 401
+        (sa / "token").unlink()
+        with pytest.raises(KubeError):
+            kube.in_cluster_config(str(sa))
+    finally:
+        srv.stop()
+
+
 def test_watch_cut_right_away_backs_off_instead_of_spinning(tmp_path):
     """A server (or proxy) that ends every watch stream at once is reconnected
     with backoff, not in a tight loop; a stripped label still comes back."""
