@@ -1,0 +1,986 @@
+// mi355x-node-labeller: the node labeller as one native process.
+//
+// The reference ships its labeller as a compiled binary
+// (cmd/k8s-node-labeller/main.go). This is the same job built from the
+// framework's C++ core, with no interpreter in the process:
+//
+//   flags        one boolean per label kind (-vram, -cu-count, ... main.go:507-528),
+//                -driver_type, node name from -node_name / $DS_NODE_NAME /
+//                /labeller/hostname; -resync, -watch, -topology_watch, -dry_run,
+//                -sysfs_root, -dev_root as in the Python CLI; glog flags accepted
+//   labels       the 13 generators of main.go:123-385 plus the opt-in
+//                gfx-target / xgmi-hive-count / xgmi-links-down, over the kfd
+//                topology, sysfs, libdrm and amd-smi; container -> VF -> PF
+//                (main.go:389-505); values sanitised to the Kubernetes rules.
+//                Output is identical to rocm_k8s_device_plugin_amd/labeller/labels.py
+//                (tests/test_native_labeller.py compares them on every fixture mode)
+//   apiserver    in-cluster service account (token re-read when kubelet rotates
+//                it), HTTPS with the cluster CA; GET the Node, JSON merge-PATCH
+//                of metadata.labels; GET + PUT (409 retry) when RBAC has no
+//                "patch" (controller.go:23-58 does the Update)
+//   watch        ?watch=1&fieldSelector=metadata.name=<node>: a node re-created
+//                or a label stripped is relabelled at once (the reference
+//                reconciles on Create events, main.go:551-577); 410 re-lists;
+//                reconnects with backoff; labels re-asserted every -resync
+//   topology     kfd generation_id + partition modes polled every
+//                -topology_watch s: a partition switch relabels at once
+//
+// -kubeconfig (out-of-cluster) is served by the Python CLI
+// (scripts/k8s-node-labeller); this binary is the in-cluster DaemonSet entrypoint.
+#include <fcntl.h>
+#include <poll.h>
+#include <signal.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <functional>
+#include <map>
+#include <optional>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../kube/http.h"
+#include "../kube/json.h"
+#include "mi355x/drm_query.h"
+#include "mi355x/gpu_discovery.h"
+#include "mi355x/kfd_topology.h"
+#include "mi355x/pci_scan.h"
+#include "mi355x/smi_query.h"
+#include "mi355x/sysfs.h"
+
+namespace {
+
+using namespace mi355x;
+using Labels = std::map<std::string, std::string>;
+
+// ---- logging (glog line format) --------------------------------------------
+int g_verbosity = 0;
+
+void logf(char sev, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+void logf(char sev, const char* fmt, ...) {
+  timespec ts{};
+  clock_gettime(CLOCK_REALTIME, &ts);
+  tm t{};
+  localtime_r(&ts.tv_sec, &t);
+  char msg[2048];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_end(ap);
+  std::fprintf(stderr, "%c%02d%02d %02d:%02d:%02d.%06ld %7d node_labeller_main.cpp] %s\n", sev, t.tm_mon + 1,
+               t.tm_mday, t.tm_hour, t.tm_min, t.tm_sec, ts.tv_nsec / 1000, static_cast<int>(getpid()), msg);
+}
+
+// ---- label kinds (constants.go:21 order, then the opt-in additions) ------------
+const std::vector<std::string> kKinds = {
+    "mode", "firmware", "family", "driver-version", "driver-src-version", "device-id", "product-name", "vram",
+    "simd-count", "cu-count", "compute-memory-partition", "compute-partitioning-supported",
+    "memory-partitioning-supported", "gfx-target", "xgmi-hive-count", "xgmi-links-down"};
+const char* kAmd = "amd.com";
+const char* kBeta = "beta.amd.com";
+
+struct Flags {
+  std::map<std::string, bool> enabled;
+  std::string driver_type;
+  std::string node_name;
+  std::string kubeconfig;
+  double resync_s = 300.0;
+  bool watch = true;
+  double topology_watch_s = 5.0;
+  bool dry_run = false;
+  std::string sysfs_root = "/sys";
+  std::string dev_root = "/dev";
+  std::string sa_dir = "/var/run/secrets/kubernetes.io/serviceaccount";
+  std::string apiserver;  // overrides KUBERNETES_SERVICE_HOST/PORT (tests, host-network debugging)
+  std::string token_file;
+  std::string ca_file;
+  double watch_backoff_max_s = 30.0;
+  int watch_timeout_s = 300;
+};
+
+bool parse_bool(const std::string& v, bool* out) {
+  if (v.empty() || v == "1" || v == "t" || v == "T" || v == "true" || v == "TRUE" || v == "True") return *out = true;
+  if (v == "0" || v == "f" || v == "F" || v == "false" || v == "FALSE" || v == "False") return !(*out = false);
+  return false;
+}
+
+bool parse_double(const std::string& v, double* out) {
+  char* end = nullptr;
+  const double d = std::strtod(v.c_str(), &end);
+  if (end == v.c_str() || *end) return false;
+  *out = d;
+  return true;
+}
+
+// Go flag syntax: -name=value, -name value, --name; booleans only take =value.
+bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
+  for (const auto& k : kKinds) f->enabled[k] = false;
+  if (const char* n = std::getenv("DS_NODE_NAME")) f->node_name = n;
+  static const std::set<std::string> kBool = {"watch", "dry_run", "logtostderr", "alsologtostderr"};
+  static const std::set<std::string> kIgnoredValue = {"stderrthreshold", "log_dir", "vmodule", "log_backtrace_at",
+                                                      "log_format"};
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a.size() < 2 || a[0] != '-') return *err = "unexpected argument " + a, false;
+    a = a.substr(a[1] == '-' ? 2 : 1);
+    std::string name = a, value;
+    bool has_value = false;
+    const size_t eq = a.find('=');
+    if (eq != std::string::npos) {
+      name = a.substr(0, eq);
+      value = a.substr(eq + 1);
+      has_value = true;
+    }
+    if (name == "h" || name == "help") {
+      std::printf("usage: %s [-<label kind> ...] [-driver_type container|vf-passthrough|pf-passthrough] "
+                  "[-node_name NAME] [-resync S] [-watch=false] [-topology_watch S] [-dry_run] "
+                  "[-sysfs_root DIR] [-dev_root DIR] (glog flags accepted)\nlabel kinds:",
+                  argv[0]);
+      for (const auto& k : kKinds) std::printf(" -%s", k.c_str());
+      std::printf("\n");
+      std::exit(0);
+    }
+    const bool is_kind = f->enabled.count(name) > 0;
+    if (is_kind || kBool.count(name)) {
+      bool v = true;
+      if (has_value && !parse_bool(value, &v))
+        return *err = "invalid boolean value \"" + value + "\" for -" + name, false;
+      if (is_kind) f->enabled[name] = v;
+      if (name == "watch") f->watch = v;
+      if (name == "dry_run") f->dry_run = v;
+      continue;
+    }
+    if (!has_value) {
+      if (i + 1 >= argc) return *err = "flag needs an argument: -" + name, false;
+      value = argv[++i];
+    }
+    if (name == "driver_type") {
+      f->driver_type = value;
+    } else if (name == "node_name") {
+      f->node_name = value;
+    } else if (name == "kubeconfig") {
+      f->kubeconfig = value;
+    } else if (name == "resync") {
+      if (!parse_double(value, &f->resync_s)) return *err = "invalid value \"" + value + "\" for -resync", false;
+    } else if (name == "topology_watch") {
+      if (!parse_double(value, &f->topology_watch_s))
+        return *err = "invalid value \"" + value + "\" for -topology_watch", false;
+    } else if (name == "watch_backoff_max") {
+      if (!parse_double(value, &f->watch_backoff_max_s))
+        return *err = "invalid value \"" + value + "\" for -watch_backoff_max", false;
+    } else if (name == "watch_timeout") {
+      f->watch_timeout_s = std::max(1, std::atoi(value.c_str()));
+    } else if (name == "sysfs_root") {
+      f->sysfs_root = value;
+    } else if (name == "dev_root") {
+      f->dev_root = value;
+    } else if (name == "sa_dir") {
+      f->sa_dir = value;
+    } else if (name == "apiserver") {
+      f->apiserver = value;
+    } else if (name == "token_file") {
+      f->token_file = value;
+    } else if (name == "ca_file") {
+      f->ca_file = value;
+    } else if (name == "v") {
+      g_verbosity = std::atoi(value.c_str());
+    } else if (!kIgnoredValue.count(name)) {
+      return *err = "flag provided but not defined: -" + name, false;
+    }
+  }
+  if (!f->driver_type.empty() && f->driver_type != "container" && f->driver_type != "vf-passthrough" &&
+      f->driver_type != "pf-passthrough")
+    return *err = "invalid driver_type " + f->driver_type, false;
+  return true;
+}
+
+// ---- label helpers (main.go:85-116) ----------------------------------------------
+std::string prefix_of(const std::string& kind, bool experimental) {
+  return std::string(experimental ? kBeta : kAmd) + "/gpu." + kind;
+}
+
+void create_labels(const std::string& kind, const std::map<std::string, int>& entries, Labels* out) {
+  for (const bool experimental : {true, false}) {
+    const std::string p = prefix_of(kind, experimental);
+    for (const auto& [k, v] : entries) {
+      (*out)[p + "." + k] = std::to_string(v);
+      if (entries.size() == 1) (*out)[p] = k;
+    }
+  }
+}
+
+bool alnum(char c) { return std::isalnum(static_cast<unsigned char>(c)) != 0; }
+
+// apimachinery IsValidLabelValue: <= 63 chars, alphanumeric at both ends, [-_.A-Za-z0-9] between
+bool valid_label_value(const std::string& v) {
+  if (v.size() > 63) return false;
+  if (v.empty()) return true;
+  if (!alnum(v.front()) || !alnum(v.back())) return false;
+  for (const char c : v)
+    if (!alnum(c) && c != '-' && c != '_' && c != '.') return false;
+  return true;
+}
+
+std::string sanitize_label_value(const std::string& v) {
+  if (valid_label_value(v)) return v;
+  std::string out;
+  for (const char c : v) out.push_back(alnum(c) || c == '-' || c == '_' || c == '.' ? c : '_');
+  if (out.size() > 63) out.resize(63);
+  size_t b = 0, e = out.size();
+  while (b < e && !alnum(out[b])) ++b;
+  while (e > b && !alnum(out[e - 1])) --e;
+  return out.substr(b, e - b);
+}
+
+// amd-smi reports an in-tree amdgpu's version as the kernel banner with its spaces
+// removed ("Linuxversion6.18.54-ant.1(nixbld@...)"): the kernel release is the version
+std::string driver_version_value(const std::string& raw) {
+  size_t i = 0;
+  auto skip_ws = [&] {
+    while (i < raw.size() && std::isspace(static_cast<unsigned char>(raw[i]))) ++i;
+  };
+  if (raw.compare(0, 5, "Linux") != 0) return raw;
+  i = 5;
+  skip_ws();
+  if (raw.compare(i, 7, "version") != 0) return raw;
+  i += 7;
+  skip_ws();
+  if (i >= raw.size() || !std::isdigit(static_cast<unsigned char>(raw[i]))) return raw;
+  size_t e = i;
+  while (e < raw.size() && !std::isspace(static_cast<unsigned char>(raw[e])) && raw[e] != '(') ++e;
+  return raw.substr(i, e - i);
+}
+
+std::string gfx_name(int v) {
+  char b[32];
+  std::snprintf(b, sizeof(b), "gfx%d%x%x", v / 10000, (v / 100) % 100, v % 100);
+  return b;
+}
+
+// ---- container-mode generators (main.go:123-385) --------------------------------
+struct Ctx {
+  std::string sysfs, dev;
+  KfdTopology topo;
+  std::vector<GpuDevice> gpus;
+  std::map<std::string, DrmGpuInfo> drm_info;
+  std::map<std::string, DrmFirmware> drm_fw;
+
+  std::optional<std::string> drm_node(const GpuDevice& g) const {
+    if (g.card >= 0 && path_exists(path_join(dev, "dri/card" + std::to_string(g.card))))
+      return "card" + std::to_string(g.card);
+    if (g.render_minor >= 0 && path_exists(path_join(dev, "dri/renderD" + std::to_string(g.render_minor))))
+      return "renderD" + std::to_string(g.render_minor);
+    if (g.card >= 0) return "card" + std::to_string(g.card);
+    return std::nullopt;
+  }
+  std::optional<std::string> card_attr(const GpuDevice& g, const std::string& attr) const {
+    return read_trimmed(path_join(sysfs, "class/drm/card" + std::to_string(g.card) + "/device/" + attr));
+  }
+  const KfdNode* kfd_node(const GpuDevice& g) const { return g.node_id < 0 ? nullptr : topo.node(g.node_id); }
+};
+
+void gen_firmware(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus) {
+    const auto node = c.drm_node(g);
+    if (!node) {
+      logf('E', "Fail to get firmware versions: no drm node");
+      continue;
+    }
+    auto it = c.drm_fw.find(*node);
+    if (it == c.drm_fw.end()) it = c.drm_fw.emplace(*node, drm_query_firmware(c.dev, c.sysfs, *node)).first;
+    if (!it->second.ok) {
+      logf('E', "Fail to get firmware versions: %s", it->second.error.c_str());
+      continue;
+    }
+    for (const auto& [name, ver] : it->second.feature) counts[name + ".feat." + std::to_string(ver)]++;
+    for (const auto& [name, ver] : it->second.firmware) counts[name + ".fw." + std::to_string(ver)]++;
+  }
+  const std::string p = prefix_of("firmware", true);
+  for (const auto& [k, v] : counts) (*out)[p + "." + k] = std::to_string(v);
+}
+
+void gen_family(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus) {
+    const auto node = c.drm_node(g);
+    if (!node) {
+      logf('E', "Fail to get card family name: no drm node");
+      continue;
+    }
+    auto it = c.drm_info.find(*node);
+    if (it == c.drm_info.end()) it = c.drm_info.emplace(*node, drm_query_gpu_info(c.dev, c.sysfs, *node)).first;
+    if (!it->second.ok) {
+      logf('E', "Fail to get card family name: %s", it->second.error.c_str());
+      continue;
+    }
+    counts[it->second.family]++;
+  }
+  create_labels("family", counts, out);
+}
+
+std::string module_attr(const Ctx& c, const std::string& attr) {
+  for (const auto& g : c.gpus)
+    if (auto v = c.card_attr(g, "driver/module/" + attr)) return *v;
+  return "";
+}
+
+void gen_driver_version(Ctx& c, Labels* out) {
+  std::string v = module_attr(c, "version");
+  if (v.empty()) {
+    // built-in amdgpu / no module version string: /sys/module/amdgpu/version, then amd-smi
+    if (auto m = read_trimmed(path_join(c.sysfs, "module/amdgpu/version")); m && !m->empty()) {
+      v = *m;
+    } else if (!c.gpus.empty() && smi_available()) {
+      const SmiSnapshot s = smi_snapshot();
+      std::set<std::string> mine;
+      for (const auto& g : c.gpus) mine.insert(to_lower(g.bdf));
+      if (s.ok)
+        for (const auto& g : s.gpus)
+          if (mine.count(to_lower(g.bdf)) && !g.driver_version.empty()) {
+            v = driver_version_value(g.driver_version);
+            break;
+          }
+    }
+  }
+  (*out)[prefix_of("driver-version", false)] = v;
+}
+
+void gen_driver_src_version(Ctx& c, Labels* out) {
+  (*out)[prefix_of("driver-src-version", false)] = module_attr(c, "srcversion");
+}
+
+void gen_device_id(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus) {
+    auto v = c.card_attr(g, "device");
+    if (!v) continue;
+    std::string s = *v;
+    if (s.compare(0, 2, "0x") == 0) s = s.substr(2);
+    counts[s]++;
+  }
+  create_labels("device-id", counts, out);
+}
+
+void gen_product_name(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus) {
+    auto v = c.card_attr(g, "product_name");
+    if (!v) continue;
+    std::string s;
+    for (const char ch : trim(*v)) {
+      if (ch == ' ') s.push_back('_');
+      else if (ch != '(' && ch != ')') s.push_back(ch);
+    }
+    if (!s.empty()) counts[s]++;
+  }
+  create_labels("product-name", counts, out);
+}
+
+void gen_vram(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus) {
+    const KfdNode* n = c.kfd_node(g);
+    if (!n || n->mem_banks.empty()) continue;
+    const uint64_t mib = n->mem_banks[0].size_in_bytes / (1024 * 1024);
+    // Go math.Round: half away from zero
+    counts[std::to_string(static_cast<long long>(std::floor(static_cast<double>(mib) / 1024.0 + 0.5))) + "G"]++;
+  }
+  create_labels("vram", counts, out);
+}
+
+void gen_simd_count(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus) {
+    const KfdNode* n = c.kfd_node(g);
+    if (!n || !n->props.count("simd_count")) continue;
+    counts[std::to_string(n->simd_count())]++;
+  }
+  create_labels("simd-count", counts, out);
+}
+
+void gen_cu_count(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus) {
+    const KfdNode* n = c.kfd_node(g);
+    if (!n || n->simd_per_cu() == 0) continue;
+    counts[std::to_string(n->simd_count() / n->simd_per_cu())]++;
+  }
+  create_labels("cu-count", counts, out);
+}
+
+void gen_compute_memory_partition(Ctx& c, Labels* out) {
+  if (!is_homogeneous(c.gpus)) return;
+  for (const auto& [t, n] : partition_config_count(c.gpus))
+    if (n > 0) {
+      (*out)[prefix_of("compute-memory-partition", false)] = t;
+      return;
+    }
+}
+
+void gen_compute_partitioning_supported(Ctx& c, Labels* out) {
+  (*out)[prefix_of("compute-partitioning-supported", false)] =
+      compute_partition_supported(c.sysfs) ? "true" : "false";
+}
+
+void gen_memory_partitioning_supported(Ctx& c, Labels* out) {
+  (*out)[prefix_of("memory-partitioning-supported", false)] = memory_partition_supported(c.sysfs) ? "true" : "false";
+}
+
+void gen_mode(Ctx&, Labels* out) {
+  (*out)[prefix_of("mode", true)] = "container";
+  (*out)[prefix_of("mode", false)] = "container";
+}
+
+void gen_gfx_target(Ctx& c, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& g : c.gpus)
+    if (g.gfx_target_version > 0) counts[gfx_name(g.gfx_target_version)]++;
+  create_labels("gfx-target", counts, out);
+}
+
+void gen_xgmi_hive_count(Ctx& c, Labels* out) {
+  if (c.gpus.empty()) return;
+  std::set<uint64_t> hives;
+  for (const auto& g : c.gpus)
+    if (g.hive_id) hives.insert(g.hive_id);
+  (*out)[prefix_of("xgmi-hive-count", false)] = std::to_string(hives.size());
+}
+
+void gen_xgmi_links_down(Ctx& c, Labels* out) {
+  if (c.gpus.empty()) return;
+  const SmiXgmiSnapshot s = smi_xgmi_links();
+  if (!s.ok) return;
+  std::set<std::string> mine;
+  for (const auto& g : c.gpus) mine.insert(to_lower(g.bdf));
+  int seen = 0, down = 0;
+  for (const auto& g : s.gpus) {
+    if (!mine.count(to_lower(g.bdf)) || !g.status_ok) continue;
+    ++seen;
+    for (const int st : g.status) down += st == 0;
+  }
+  if (seen) (*out)[prefix_of("xgmi-links-down", false)] = std::to_string(down);
+}
+
+using Gen = void (*)(Ctx&, Labels*);
+const std::vector<std::pair<std::string, Gen>> kGenerators = {
+    {"firmware", gen_firmware},
+    {"family", gen_family},
+    {"driver-version", gen_driver_version},
+    {"driver-src-version", gen_driver_src_version},
+    {"device-id", gen_device_id},
+    {"product-name", gen_product_name},
+    {"vram", gen_vram},
+    {"simd-count", gen_simd_count},
+    {"cu-count", gen_cu_count},
+    {"compute-memory-partition", gen_compute_memory_partition},
+    {"compute-partitioning-supported", gen_compute_partitioning_supported},
+    {"memory-partitioning-supported", gen_memory_partitioning_supported},
+    {"mode", gen_mode},
+    {"gfx-target", gen_gfx_target},
+    {"xgmi-hive-count", gen_xgmi_hive_count},
+    {"xgmi-links-down", gen_xgmi_links_down},
+};
+
+Labels container_labels(const Flags& f) {
+  Labels out;
+  Ctx c;
+  c.sysfs = f.sysfs_root;
+  c.dev = f.dev_root;
+  if (is_dir(path_join(f.sysfs_root, "module/amdgpu/drivers"))) {
+    c.topo = KfdTopology::load_sysfs(f.sysfs_root);
+    c.gpus = discover_gpus(f.sysfs_root, c.topo).devices;
+  }
+  if (c.gpus.empty()) {
+    logf('I', "No AMD GPUs found, skipping label generation");
+    return out;
+  }
+  for (const auto& [name, gen] : kGenerators)
+    if (f.enabled.at(name)) gen(c, &out);
+  return out;
+}
+
+void count_functions(const PciScanResult& r, Labels* out) {
+  std::map<std::string, int> counts;
+  for (const auto& [group, fns] : r.groups)
+    for (const auto& fn : fns) counts[fn.device_id]++;
+  create_labels("device-id", counts, out);
+}
+
+// VF passthrough (main.go:438-475)
+Labels vf_labels(const Flags& f) {
+  Labels out;
+  const PciScanResult r = scan_vf_mapping(f.sysfs_root);
+  if (!r.ok || r.groups.empty()) return out;
+  const GimVersions gim = read_gim_versions(f.sysfs_root);
+  if (!gim.ok) return out;
+  if (f.enabled.at("driver-version")) out[prefix_of("driver-version", false)] = gim.version;
+  if (f.enabled.at("driver-src-version")) out[prefix_of("driver-src-version", false)] = gim.srcversion;
+  if (f.enabled.at("mode")) {
+    out[prefix_of("mode", false)] = "vf-passthrough";
+    out[prefix_of("mode", true)] = "vf-passthrough";
+  }
+  if (f.enabled.at("device-id")) count_functions(r, &out);
+  return out;
+}
+
+// PF passthrough (main.go:477-505)
+Labels pf_labels(const Flags& f) {
+  Labels out;
+  const PciScanResult r = scan_pf_mapping(f.sysfs_root);
+  if (!r.ok || r.groups.empty()) return out;
+  if (f.enabled.at("mode")) out[prefix_of("mode", false)] = "pf-passthrough";
+  if (f.enabled.at("device-id")) count_functions(r, &out);
+  return out;
+}
+
+// generateLabels (main.go:389-408): explicit mode, else container -> VF -> PF
+Labels generate_labels(const Flags& f) {
+  Labels out;
+  if (f.driver_type == "container" || f.driver_type.empty()) out = container_labels(f);
+  if (f.driver_type == "vf-passthrough" || (f.driver_type.empty() && out.empty())) out = vf_labels(f);
+  if (f.driver_type == "pf-passthrough" || (f.driver_type.empty() && out.empty())) out = pf_labels(f);
+  for (auto& [k, v] : out) v = sanitize_label_value(v);
+  return out;
+}
+
+// ---- removal sets (main.go:50-83) and the merge patch -------------------------
+std::vector<std::string> all_label_keys() {
+  std::vector<std::string> keys;
+  for (const auto& k : kKinds) keys.push_back(prefix_of(k, false));
+  keys.push_back("amd.com/compute-partitioning-supported");
+  keys.push_back("amd.com/memory-partitioning-supported");
+  keys.push_back("amd.com/compute-memory-partition");
+  return keys;
+}
+
+Labels remove_old_node_labels(Labels l) {
+  for (const auto& k : all_label_keys()) l.erase(k);
+  for (const auto& kind : kKinds) {
+    const std::string k = prefix_of(kind, true);
+    auto it = l.find(k);
+    if (it != l.end()) {
+      l.erase(k + "." + it->second);
+      l.erase(it);
+    }
+    // orphaned beta counters <key>.<value> go too
+    for (auto j = l.lower_bound(k + "."); j != l.end() && j->first.compare(0, k.size() + 1, k + ".") == 0;)
+      j = l.erase(j);
+  }
+  return l;
+}
+
+// key -> value, or nullopt = delete
+std::map<std::string, std::optional<std::string>> label_patch(const Labels& current, const Labels& desired) {
+  Labels target = remove_old_node_labels(current);
+  for (const auto& [k, v] : desired) target[k] = v;
+  std::map<std::string, std::optional<std::string>> patch;
+  for (const auto& [k, v] : current)
+    if (!target.count(k)) patch[k] = std::nullopt;
+  for (const auto& [k, v] : target) {
+    auto it = current.find(k);
+    if (it == current.end() || it->second != v) patch[k] = v;
+  }
+  return patch;
+}
+
+// ---- apiserver client -------------------------------------------------------
+class Kube {
+ public:
+  http::Config cfg;
+  std::string token_file;
+  std::string token;
+  int wake_fd = -1;
+
+  // current bearer token: re-read when the file changes (kubelet rotates projected tokens)
+  const std::string& bearer(bool force = false) {
+    if (!token_file.empty()) {
+      struct stat st {};
+      if (::stat(token_file.c_str(), &st) == 0) {
+        const long long mt = static_cast<long long>(st.st_mtim.tv_sec) * 1000000000LL + st.st_mtim.tv_nsec;
+        if (force || mt != mtime_) {
+          if (auto t = read_trimmed(token_file); t && !t->empty()) {
+            token = *t;
+            mtime_ = mt;
+          }
+        }
+      }
+    }
+    return token;
+  }
+
+  http::Headers headers(const std::string& content_type = "") {
+    http::Headers h = {{"Accept", "application/json"}, {"User-Agent", "mi355x-node-labeller-native"}};
+    if (!content_type.empty()) h.emplace_back("Content-Type", content_type);
+    const std::string& t = bearer();
+    if (!t.empty()) h.emplace_back("Authorization", "Bearer " + t);
+    return h;
+  }
+
+  http::Response call(const std::string& method, const std::string& path, const std::string& body = "",
+                      const std::string& content_type = "") {
+    const std::string before = bearer();
+    http::Response r = http::request(cfg, method, path, headers(content_type), body, wake_fd);
+    if (r.status == 401 && !token_file.empty() && bearer(true) != before)
+      r = http::request(cfg, method, path, headers(content_type), body, wake_fd);  // rotated token: once
+    return r;
+  }
+
+ private:
+  long long mtime_ = -1;
+};
+
+std::string describe(const http::Response& r) {
+  if (r.status == 0) return r.error;
+  return "HTTP " + std::to_string(r.status) + ": " + r.body.substr(0, 300);
+}
+
+std::string path_escape(const std::string& s) {
+  std::string out;
+  for (const char ch : s) {
+    const auto c = static_cast<unsigned char>(ch);
+    if (alnum(ch) || c == '-' || c == '.' || c == '_' || c == '~') {
+      out.push_back(ch);
+    } else {
+      char b[4];
+      std::snprintf(b, sizeof(b), "%%%02X", c);
+      out += b;
+    }
+  }
+  return out;
+}
+
+struct Stats {
+  int passes = 0, patches = 0, updates = 0, errors = 0;
+  int watch_events = 0, watch_kicks = 0, watch_errors = 0, watch_restarts = 0, topology_changes = 0;
+};
+
+class Labeller {
+ public:
+  Labeller(const Flags& f, Kube* k) : f_(f), k_(k) {}
+
+  bool reconcile() {
+    ++st.passes;
+    desired_ = generate_labels(f_);
+    have_desired_ = true;
+    const std::string path = "/api/v1/nodes/" + path_escape(f_.node_name);
+    http::Response r = k_->call("GET", path);
+    if (r.status != 200) return fail("reconcile of node " + f_.node_name + " failed: " + describe(r));
+    auto node = json::parse(r.body);
+    if (!node) return fail("reconcile of node " + f_.node_name + " failed: unparseable Node");
+    const auto patch = label_patch(json::node_labels(*node), desired_);
+    if (patch.empty()) return true;
+    json::Value labels = json::Value::object();
+    for (const auto& [k, v] : patch) labels.set(k, v ? json::Value::string(*v) : json::Value{});
+    json::Value md = json::Value::object();
+    md.set("labels", labels);
+    json::Value body = json::Value::object();
+    body.set("metadata", md);
+    r = k_->call("PATCH", path, json::serialize(body), "application/merge-patch+json");
+    if (r.status == 403) {
+      // the upstream ClusterRole grants "update" but not "patch": GET + Update (controller.go:23-58)
+      if (!update_with_retry(path)) return false;
+    } else if (r.status != 200) {
+      return fail("reconcile of node " + f_.node_name + " failed: " + describe(r));
+    }
+    ++st.patches;
+    logf('I', "node labels updated node=%s changed=%zu", f_.node_name.c_str(), patch.size());
+    return true;
+  }
+
+  bool needs_reconcile(const json::Value& node) const {
+    return !have_desired_ || !label_patch(json::node_labels(node), desired_).empty();
+  }
+
+  Stats st;
+
+ private:
+  bool fail(const std::string& msg) {
+    ++st.errors;
+    logf('E', "%s", msg.c_str());
+    return false;
+  }
+
+  bool update_with_retry(const std::string& path) {
+    for (int attempt = 0; attempt < 5; ++attempt) {
+      http::Response r = k_->call("GET", path);
+      if (r.status != 200) return fail("update of node " + f_.node_name + " failed: " + describe(r));
+      auto node = json::parse(r.body);
+      if (!node || node->kind != json::Value::Object) return fail("update: unparseable Node");
+      Labels l = remove_old_node_labels(json::node_labels(*node));
+      for (const auto& [k, v] : desired_) l[k] = v;
+      json::Value* md = node->get("metadata");
+      if (!md) md = &node->set("metadata", json::Value::object());
+      json::Value labels = json::Value::object();
+      for (const auto& [k, v] : l) labels.set(k, json::Value::string(v));
+      md->set("labels", labels);
+      r = k_->call("PUT", path, json::serialize(*node), "application/json");
+      if (r.status == 200) {
+        ++st.updates;
+        return true;
+      }
+      if (r.status != 409 || attempt == 4) return fail("update of node " + f_.node_name + " failed: " + describe(r));
+    }
+    return false;
+  }
+
+  const Flags& f_;
+  Kube* k_;
+  Labels desired_;
+  bool have_desired_ = false;
+};
+
+// kfd generation_id + every amdgpu function's partition modes (topology.py topology_signature)
+std::string topology_signature(const std::string& sysfs_root) {
+  std::string sig = read_trimmed(path_join(sysfs_root, "class/kfd/kfd/topology/generation_id")).value_or("-");
+  const std::string drv = path_join(sysfs_root, "module/amdgpu/drivers/pci:amdgpu");
+  auto bdfs = list_dir(drv);
+  std::sort(bdfs.begin(), bdfs.end());
+  for (const auto& b : bdfs) {
+    if (b.find(':') == std::string::npos) continue;
+    sig += "|" + b + "=" + read_trimmed(path_join(drv, b + "/current_compute_partition")).value_or("-") + "," +
+           read_trimmed(path_join(drv, b + "/current_memory_partition")).value_or("-");
+  }
+  return sig;
+}
+
+std::string node_name_from(const Flags& f) {
+  if (!f.node_name.empty()) return f.node_name;
+  return read_trimmed("/labeller/hostname").value_or("");
+}
+
+void print_json(const Labels& l) {
+  if (l.empty()) {
+    std::printf("{}\n");
+    return;
+  }
+  std::printf("{\n");
+  size_t i = 0;
+  for (const auto& [k, v] : l)
+    std::printf(" %s: %s%s\n", json::quote(k).c_str(), json::quote(v).c_str(), ++i < l.size() ? "," : "");
+  std::printf("}\n");
+}
+
+volatile sig_atomic_t g_stop = 0;
+int g_sig_pipe[2] = {-1, -1};
+
+void on_signal(int) {
+  g_stop = 1;
+  const char b = 1;
+  if (g_sig_pipe[1] >= 0 && ::write(g_sig_pipe[1], &b, 1) < 0) {
+  }
+}
+
+using clk = std::chrono::steady_clock;
+
+int ms_until(clk::time_point t) {
+  const auto d = std::chrono::duration_cast<std::chrono::milliseconds>(t - clk::now()).count();
+  return static_cast<int>(std::max<long long>(0, std::min<long long>(d, 3600 * 1000)));
+}
+
+clk::time_point after_s(double s) {
+  return clk::now() + std::chrono::microseconds(static_cast<long long>(s * 1e6));
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Flags f;
+  std::string err;
+  if (!parse_flags(argc, argv, &f, &err)) {
+    logf('E', "%s", err.c_str());
+    return 1;
+  }
+  if (f.dry_run) {
+    print_json(generate_labels(f));
+    return 0;
+  }
+  logf('I', "AMD GPU Node Labeller for Kubernetes (MI355X-native, native daemon)");
+  if (!f.kubeconfig.empty()) {
+    logf('E', "-kubeconfig (out-of-cluster) is served by the Python labeller (scripts/k8s-node-labeller); this "
+              "binary runs in-cluster");
+    return 1;
+  }
+  f.node_name = node_name_from(f);
+  if (f.node_name.empty()) {
+    logf('E', "node name unknown: set DS_NODE_NAME or -node_name (or mount /labeller/hostname)");
+    return 1;
+  }
+  Kube kube;
+  if (!f.apiserver.empty()) {
+    kube.cfg.server = f.apiserver;
+  } else {
+    const char* host = std::getenv("KUBERNETES_SERVICE_HOST");
+    const char* port = std::getenv("KUBERNETES_SERVICE_PORT");
+    if (!host || !*host) {
+      logf('E', "unable to set up kubernetes client: not running in a cluster (KUBERNETES_SERVICE_HOST unset)");
+      return 1;
+    }
+    std::string h = host;
+    if (h.find(':') != std::string::npos && h[0] != '[') h = "[" + h + "]";
+    kube.cfg.server = "https://" + h + ":" + (port && *port ? port : "443");
+  }
+  kube.token_file = !f.token_file.empty() ? f.token_file : path_join(f.sa_dir, "token");
+  kube.cfg.ca_file = !f.ca_file.empty() ? f.ca_file
+                     : path_exists(path_join(f.sa_dir, "ca.crt")) ? path_join(f.sa_dir, "ca.crt")
+                                                                   : "";
+  if (kube.bearer().empty() && f.apiserver.empty()) {
+    logf('E', "unable to set up kubernetes client: service-account token %s is unreadable or empty",
+         kube.token_file.c_str());
+    return 1;
+  }
+
+  if (::pipe(g_sig_pipe) != 0) return 1;
+  ::fcntl(g_sig_pipe[0], F_SETFL, O_NONBLOCK);
+  ::fcntl(g_sig_pipe[1], F_SETFL, O_NONBLOCK);
+  struct sigaction sa {};
+  sa.sa_handler = on_signal;
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
+  signal(SIGPIPE, SIG_IGN);
+  kube.wake_fd = g_sig_pipe[0];
+
+  Labeller lab(f, &kube);
+  const bool once = f.resync_s <= 0;
+  if (once) {  // the reference: compute and apply once
+    while (!g_stop) {
+      if (lab.reconcile()) return 0;
+      pollfd p{g_sig_pipe[0], POLLIN, 0};
+      ::poll(&p, 1, 5000);
+    }
+    return 0;
+  }
+
+  bool kick = true;
+  auto next_resync = clk::now();
+  const bool topo_watch = f.topology_watch_s > 0;
+  auto next_topo = after_s(f.topology_watch_s);
+  std::string topo_last = topo_watch ? topology_signature(f.sysfs_root) : "", topo_seen = topo_last;
+  http::Stream stream;
+  bool stream_open = false;
+  auto stream_opened = clk::now();
+  auto watch_retry = clk::now();
+  double backoff = 0.2;
+  std::string rv;
+  const http::Config wcfg = [&] {
+    http::Config c = kube.cfg;
+    c.timeout_s = f.watch_timeout_s + 30.0;
+    return c;
+  }();
+
+  while (!g_stop) {
+    if (kick || clk::now() >= next_resync) {
+      kick = false;
+      const bool ok = lab.reconcile();
+      next_resync = after_s(ok ? f.resync_s : 5.0);
+    }
+    if (topo_watch && clk::now() >= next_topo) {
+      next_topo = after_s(f.topology_watch_s);
+      const std::string cur = topology_signature(f.sysfs_root);
+      // act once the new fingerprint has held one interval (a switch passes through half states)
+      if (cur != topo_last && cur == topo_seen) {
+        topo_last = cur;
+        ++lab.st.topology_changes;
+        logf('I', "GPU topology changed (partition switch?): relabelling node %s", f.node_name.c_str());
+        kick = true;
+      }
+      topo_seen = cur;
+      if (kick) continue;
+    }
+    int wait_ms = ms_until(next_resync);
+    if (topo_watch) wait_ms = std::min(wait_ms, ms_until(next_topo));
+    if (f.watch && !stream_open && clk::now() >= watch_retry) {
+      std::string q = "/api/v1/nodes?watch=1&fieldSelector=" + path_escape("metadata.name=" + f.node_name) +
+                      "&timeoutSeconds=" + std::to_string(f.watch_timeout_s) + "&allowWatchBookmarks=true";
+      if (!rv.empty()) q += "&resourceVersion=" + path_escape(rv);
+      int status = 0;
+      std::string ebody;
+      const std::string e =
+          stream.open(wcfg, q, kube.headers(), &status, &ebody, static_cast<int>(kube.cfg.timeout_s * 1000),
+                      g_sig_pipe[0]);
+      if (g_stop) break;
+      if (!e.empty() || status != 200) {
+        if (status == 410) rv.clear();
+        if (status == 401) kube.bearer(true);
+        ++lab.st.watch_errors;
+        logf('W', "watch of node %s failed (%s); retrying in %.1fs", f.node_name.c_str(),
+             e.empty() ? ("HTTP " + std::to_string(status) + ": " + ebody.substr(0, 200)).c_str() : e.c_str(),
+             backoff);
+        stream.close();
+        watch_retry = after_s(backoff);
+        backoff = std::min(backoff * 2, f.watch_backoff_max_s);
+      } else {
+        stream_open = true;
+        stream_opened = clk::now();
+        ++lab.st.watch_restarts;
+      }
+    }
+    if (!stream_open) {
+      if (f.watch) wait_ms = std::min(wait_ms, ms_until(watch_retry));
+      pollfd p{g_sig_pipe[0], POLLIN, 0};
+      ::poll(&p, 1, wait_ms);
+      continue;
+    }
+    std::string line;
+    const int rc = stream.next_line(&line, wait_ms, g_sig_pipe[0]);
+    if (rc == -2) continue;  // timer due
+    if (rc == -3 || g_stop) break;
+    if (rc == 1) {
+      if (line.find_first_not_of(" \t\r") == std::string::npos) continue;
+      ++lab.st.watch_events;
+      auto ev = json::parse(line);
+      if (!ev) continue;
+      const std::string type = ev->str("type");
+      const json::Value* obj = ev->get("object");
+      if (type == "ERROR") {
+        if (obj && obj->str("code") == "410") {  // resourceVersion too old: re-list
+          rv.clear();
+          kick = true;
+        }
+        stream.close();
+        stream_open = false;
+        watch_retry = after_s(backoff);
+        backoff = std::min(backoff * 2, f.watch_backoff_max_s);
+        continue;
+      }
+      if (obj) {
+        const json::Value* md = obj->get("metadata");
+        if (md && !md->str("resourceVersion").empty()) rv = md->str("resourceVersion");
+        if ((type == "ADDED" || type == "MODIFIED") && lab.needs_reconcile(*obj)) {
+          ++lab.st.watch_kicks;
+          kick = true;
+        }
+      }
+      continue;
+    }
+    // the stream ended (server timeout) or broke
+    stream.close();
+    stream_open = false;
+    const bool lived = clk::now() - stream_opened >= std::chrono::seconds(1);
+    if (rc == 0 && lived) {
+      backoff = 0.2;
+      watch_retry = clk::now();
+    } else {
+      if (rc != 0) {
+        ++lab.st.watch_errors;
+        logf('W', "watch of node %s broke; retrying in %.1fs", f.node_name.c_str(), backoff);
+      }
+      watch_retry = after_s(backoff);  // a server that ends every stream at once is not hammered
+      backoff = std::min(backoff * 2, f.watch_backoff_max_s);
+    }
+  }
+  logf('I', "Received signal, shutting down. passes=%d patches=%d updates=%d errors=%d watch_events=%d "
+            "watch_kicks=%d watch_errors=%d watch_restarts=%d topology_changes=%d",
+       lab.st.passes, lab.st.patches, lab.st.updates, lab.st.errors, lab.st.watch_events, lab.st.watch_kicks,
+       lab.st.watch_errors, lab.st.watch_restarts, lab.st.topology_changes);
+  return 0;
+}

@@ -1,0 +1,271 @@
+"""The native labeller (`mi355x-node-labeller`, native/src/daemon/node_labeller_main.cpp):
+the node labeller as one C++ process. Its labels must equal the Python
+labeller's (labeller/labels.py, the reference schema of
+cmd/k8s-node-labeller/main.go:123-505) on every generated node layout, and
+its apiserver loop follows the Python controller: merge PATCH, GET + PUT when
+RBAC denies patch, a watch that restores stripped labels, rotated tokens,
+TLS with the cluster CA, SIGTERM."""
+import json
+import os
+import signal
+import subprocess
+import time
+
+import pytest
+
+from rocm_k8s_device_plugin_amd import constants as C
+from rocm_k8s_device_plugin_amd.labeller import labels as L
+from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+from rocm_k8s_device_plugin_amd.testing.fake_apiserver import FakeApiServer
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+
+# MI355X_NATIVE_LABELLER_EXE: run against another build (e.g. the sanitizer builds)
+EXE = os.environ.get("MI355X_NATIVE_LABELLER_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-node-labeller")
+KINDS = C.SUPPORTED_LABELS + L.EXTRA_LABELS
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} was not built")
+
+
+def _dry_run(fi, kinds, driver_type=""):
+    argv = [EXE, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)] + [f"-{k}" for k in kinds]
+    if driver_type:
+        argv += ["-driver_type", driver_type]
+    p = subprocess.run(argv, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    return p.stdout
+
+
+def _python(fi, kinds, driver_type=""):
+    return L.generate_labels({k: k in kinds for k in KINDS}, driver_type, str(fi.sysfs), str(fi.dev))
+
+
+LAYOUTS = {
+    "spx": dict(),
+    "cpx": dict(compute_partition="cpx"),
+    "qpx_nps2": dict(compute_partition="qpx", memory_partition="nps2"),
+    "dpx": dict(compute_partition="dpx"),
+    "two_hives": dict(hive_size=4),
+    "mixed_partitions": dict(per_gpu_compute=["spx"] * 4 + ["cpx"] * 4),
+    "no_partition_support": dict(partition_support=False),
+    "vf": dict(mode="vf", vfs_per_gpu=2),
+    "pf": dict(mode="pf"),
+}
+
+
+@pytest.mark.parametrize("layout", sorted(LAYOUTS))
+def test_labels_equal_the_python_labeller(tmp_path, layout):
+    fi = make_mi355x_node(tmp_path, **LAYOUTS[layout])
+    for kinds in (KINDS, ["vram", "cu-count", "simd-count", "device-id", "family"], ["mode"], []):
+        for dt in ("", "container", "vf-passthrough", "pf-passthrough"):
+            out = _dry_run(fi, kinds, dt)
+            want = _python(fi, kinds, dt)
+            assert json.loads(out) == want, (layout, kinds, dt)
+            # byte-identical to the Python CLI's json.dumps(indent=1, sort_keys=True)
+            assert out == json.dumps(want, indent=1, sort_keys=True) + "\n"
+
+
+def test_label_values_are_sanitised_like_the_python_labeller(tmp_path):
+    fi = make_mi355x_node(tmp_path)
+    card = fi.sysfs / "class/drm/card1/device"
+    (card / "product_name").write_text("  AMD Instinct MI355X (OAM) / rev:A?" + "x" * 80 + "\n")
+    mod = card / "driver/module"
+    (mod / "version").write_text("6.12.12+build/meta\n")
+    out = json.loads(_dry_run(fi, KINDS))
+    assert out == _python(fi, KINDS)
+    assert all(len(v) <= 63 for v in out.values())
+
+
+def test_flags_follow_go_syntax(tmp_path):
+    fi = make_mi355x_node(tmp_path)
+    base = [EXE, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)]
+    p = subprocess.run(base + ["--vram=true", "-cu-count=false", "-v=5", "-logtostderr"], capture_output=True,
+                       text=True, timeout=30)
+    assert p.returncode == 0 and set(json.loads(p.stdout)) == {"amd.com/gpu.vram", "amd.com/gpu.vram.288G",
+                                                               "beta.amd.com/gpu.vram", "beta.amd.com/gpu.vram.288G"}
+    for bad in (["-nope"], ["-driver_type", "gim"], ["-vram=maybe"], ["-resync", "x"]):
+        p = subprocess.run(base + bad, capture_output=True, text=True, timeout=30)
+        assert p.returncode == 1, bad
+    p = subprocess.run([EXE, "-h"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 0 and "-compute-memory-partition" in p.stdout
+    # out-of-cluster kubeconfig is the Python CLI's job; no cluster env -> clear error
+    env = {k: v for k, v in os.environ.items() if k not in ("KUBERNETES_SERVICE_HOST", "DS_NODE_NAME")}
+    p = subprocess.run([EXE, "-node_name", "n", "-kubeconfig", "/x"], capture_output=True, text=True, timeout=30,
+                       env=env)
+    assert p.returncode == 1 and "kubeconfig" in p.stderr
+    p = subprocess.run([EXE, "-node_name", "n", "-sa_dir", str(tmp_path)], capture_output=True, text=True, timeout=30,
+                       env=env)
+    assert p.returncode == 1 and "KUBERNETES_SERVICE_HOST" in p.stderr
+    p = subprocess.run([EXE], capture_output=True, text=True, timeout=30, env=env)
+    assert p.returncode == 1 and "node name" in p.stderr
+
+
+def _wait(pred, timeout=5.0):
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return pred()
+
+
+def _start(fi, srv, tmp_path, *extra, token="tok", node="node-n"):
+    tok = tmp_path / "token"
+    tok.write_text(token + "\n")
+    argv = [EXE, "-node_name", node, "-apiserver", srv.url, "-token_file", str(tok), "-sysfs_root", str(fi.sysfs),
+            "-dev_root", str(fi.dev), "-vram", "-cu-count", "-mode", "-device-id", "-compute-memory-partition",
+            *extra]
+    return subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True), tok
+
+
+def _stop(p):
+    if p.poll() is None:
+        p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=20)
+    return p.returncode, err
+
+
+def test_applies_once_with_resync_zero(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="cpx")
+    srv = FakeApiServer(token="tok").start()
+    try:
+        srv.add_node("node-n", {"amd.com/gpu.vram": "1G", "beta.amd.com/gpu.vram": "1G",
+                                "beta.amd.com/gpu.vram.1G": "8", "keep": "me"})
+        p, _ = _start(fi, srv, tmp_path, "-resync", "0")
+        assert p.wait(30) == 0, p.stderr.read()
+        want = L.generate_labels({k: k in ("vram", "cu-count", "mode", "device-id", "compute-memory-partition")
+                                  for k in KINDS}, "", str(fi.sysfs), str(fi.dev))
+        got = srv.labels("node-n")
+        assert got == {**want, "keep": "me"}
+        assert [m for m, *_ in srv.requests] == ["GET", "PATCH"]
+        assert srv.requests[1][2]["metadata"]["labels"]["beta.amd.com/gpu.vram.1G"] is None
+    finally:
+        srv.stop()
+
+
+def test_watch_restores_stripped_labels_and_survives_expiry(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        srv.add_node("node-n")
+        p, _ = _start(fi, srv, tmp_path, "-resync", "300", "-topology_watch", "0")
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"))
+        assert _wait(lambda: srv.watch_starts >= 1)
+        t0 = time.monotonic()
+        srv.set_labels("node-n", {"other": "x"})               # someone strips ours
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 2.0)
+        assert time.monotonic() - t0 < 1.5 and srv.labels("node-n")["other"] == "x"
+        srv.expire_watches()                                     # server ends the stream: reconnect
+        assert _wait(lambda: srv.watch_starts >= 2, 3.0)
+        srv.delete_node("node-n")
+        srv.add_node("node-n")                                   # re-created node
+        assert _wait(lambda: "amd.com/gpu.cu-count" in srv.labels("node-n"), 2.0)
+        # no reconnect spin when the server cuts every watch at once
+        srv.watch_max_s = 0.0
+        srv.expire_watches()
+        n0 = srv.watch_starts
+        time.sleep(1.5)
+        assert srv.watch_starts - n0 <= 10, srv.watch_starts - n0
+        rc, err = _stop(p)
+        assert rc == 0 and "shutting down" in err
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
+def test_update_fallback_when_patch_is_forbidden(tmp_path):
+    """The upstream ClusterRole grants update, not patch: GET + PUT (controller.go:23-58)."""
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    try:
+        srv.add_node("node-n", {"amd.com/gpu.family": "AI", "keep": "me"})
+        srv.forbid = {"PATCH"}
+        p, _ = _start(fi, srv, tmp_path, "-resync", "0")
+        assert p.wait(30) == 0, p.stderr.read()
+        got = srv.labels("node-n")
+        assert got["amd.com/gpu.vram"] == "288G" and got["keep"] == "me" and "amd.com/gpu.family" not in got
+        assert [m for m, *_ in srv.requests] == ["GET", "PATCH", "GET", "PUT"]
+    finally:
+        srv.stop()
+
+
+def test_rotated_token_is_picked_up(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        srv.add_node("node-n")
+        p, tok = _start(fi, srv, tmp_path, "-resync", "0.5", "-watch=false", "-topology_watch", "0")
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"))
+        srv.token = "tok-2"                       # the server moves on; the file follows
+        tok.write_text("tok-2\n")
+        os.utime(tok, ns=(time.time_ns(), time.time_ns() + 10**9))
+        srv.set_labels("node-n", {})
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 3.0)
+        rc, err = _stop(p)
+        assert rc == 0 and "HTTP 401" not in err
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
+def test_topology_change_relabels(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        srv.add_node("node-n")
+        p, _ = _start(fi, srv, tmp_path, "-resync", "300", "-watch=false", "-topology_watch", "0.2")
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.compute-memory-partition") == "spx_nps1")
+        # a partition switch: every GPU's mode file changes (the generated tree keeps the kfd side)
+        drv = fi.sysfs / "module/amdgpu/drivers/pci:amdgpu"
+        for b in sorted(x for x in os.listdir(drv) if ":" in x):
+            (drv / b / "current_memory_partition").write_text("NPS2\n")
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.compute-memory-partition") == "spx_nps2", 3.0)
+        rc, err = _stop(p)
+        assert rc == 0 and "topology_changes=1" in err
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
+def test_in_cluster_https_with_the_cluster_ca(tmp_path, monkeypatch):
+    from test_labeller import _tls_material
+    crt, key, ca = _tls_material(tmp_path)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="sa-token", tls=(crt, key)).start()
+    try:
+        srv.add_node("worker-9")
+        sa = tmp_path / "sa"
+        sa.mkdir()
+        (sa / "token").write_text("sa-token\n")
+        (sa / "ca.crt").write_text(open(ca).read())
+        env = dict(os.environ, KUBERNETES_SERVICE_HOST="127.0.0.1", KUBERNETES_SERVICE_PORT=str(srv.port),
+                   DS_NODE_NAME="worker-9")
+        argv = [EXE, "-sa_dir", str(sa), "-resync", "0", "-mode", "-cu-count", "-sysfs_root", str(fi.sysfs),
+                "-dev_root", str(fi.dev)]
+        p = subprocess.run(argv, capture_output=True, text=True, timeout=60, env=env)
+        assert p.returncode == 0, p.stderr
+        got = srv.labels("worker-9")
+        assert got["amd.com/gpu.mode"] == "container" and got["amd.com/gpu.cu-count"] == "256"
+        # a CA that did not sign the server certificate is refused (retried, never applied)
+        other = tmp_path / "other"
+        other.mkdir()
+        _, _, bad_ca = _tls_material(other)
+        (sa / "ca.crt").write_text(open(bad_ca).read())
+        srv.set_labels("worker-9", {})
+        p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+        time.sleep(1.0)
+        rc, err = _stop(p)
+        assert rc == 0 and "certificate verify failed" in err and srv.labels("worker-9") == {}
+    finally:
+        srv.stop()

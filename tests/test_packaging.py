@@ -244,3 +244,13 @@ def test_helm_native_daemon_switch():
     assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["dp"]["native"] is False
     for df in ("Dockerfile", "ubi-dp.Dockerfile"):
         assert "bin/mi355x-device-plugin /root/mi355x-device-plugin" in (REPO / df).read_text(), df
+
+
+def test_helm_native_labeller_switch():
+    """lbl.native runs the native labeller from the labeller images (off by default)."""
+    t = (REPO / "helm/amd-gpu/templates/labeller.yaml").read_text()
+    assert 'command: ["./mi355x-node-labeller"]' in t and "{{- if .Values.lbl.native }}" in t
+    assert 'command: ["./k8s-node-labeller"]' in t
+    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["lbl"]["native"] is False
+    for df in ("labeller.Dockerfile", "ubi-labeller.Dockerfile"):
+        assert "bin/mi355x-node-labeller /root/mi355x-node-labeller" in (REPO / df).read_text(), df
