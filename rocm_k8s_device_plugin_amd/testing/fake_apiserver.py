@@ -49,7 +49,8 @@ class FakeApiServer:
                 pass
 
             def _chunk(self, obj) -> None:
-                raw = (json.dumps(obj) + "\n").encode()
+                # bytes: sent as they are (malformed-event tests)
+                raw = obj if isinstance(obj, bytes) else (json.dumps(obj) + "\n").encode()
                 self.wfile.write(f"{len(raw):x}\r\n".encode() + raw + b"\r\n")
                 self.wfile.flush()
 
@@ -192,6 +193,13 @@ class FakeApiServer:
             self._store(name, {"apiVersion": "v1", "kind": "Node",
                                "metadata": {"name": name, "labels": dict(labels or {}), "resourceVersion": "1"}},
                         "ADDED")
+
+    def send_raw_event(self, name: str, raw: bytes) -> None:
+        """Write raw bytes into the watch streams of a node (garbage, truncated JSON)."""
+        with self._lock:
+            for n, q in self.watchers:
+                if n == name:
+                    q.put(raw)
 
     def set_labels(self, name: str, labels: Dict[str, str]) -> None:
         """Replace a node's labels (someone else editing the node)."""

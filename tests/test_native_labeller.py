@@ -9,6 +9,7 @@ import json
 import os
 import signal
 import subprocess
+import sys
 import time
 
 import pytest
@@ -268,4 +269,67 @@ def test_in_cluster_https_with_the_cluster_ca(tmp_path, monkeypatch):
         rc, err = _stop(p)
         assert rc == 0 and "certificate verify failed" in err and srv.labels("worker-9") == {}
     finally:
+        srv.stop()
+
+
+@pytest.mark.gpu
+def test_real_node_labels_equal_the_python_labeller():
+    """On the MI355X box's own /sys and /dev (libdrm family/firmware, amd-smi
+    driver version and xGMI links, kfd-denied GPUs): the same labels as the
+    Python labeller, and the process cost of one labelling pass."""
+    t0 = time.monotonic()
+    p = subprocess.Popen([EXE, "-dry_run", *[f"-{k}" for k in KINDS]], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    out, err = p.communicate(timeout=120)
+    wall_ms = (time.monotonic() - t0) * 1e3
+    assert p.returncode == 0, err
+    got = json.loads(out)
+    want = L.generate_labels({k: True for k in KINDS}, "")
+    assert got == want
+    assert got["amd.com/gpu.family"] == "AI" and got["amd.com/gpu.gfx-target"] == "gfx950"
+    # the Python CLI's cost for the same pass, for the footprint comparison
+    t1 = time.monotonic()
+    py = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.node_labeller", "-dry_run",
+                         *[f"-{k}" for k in KINDS]], capture_output=True, text=True, timeout=120)
+    py_ms = (time.monotonic() - t1) * 1e3
+    assert py.returncode == 0 and json.loads(py.stdout) == got
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/native_labeller_box.json", "w") as f:
+        json.dump({"labels": got, "native_dry_run_wall_ms": round(wall_ms, 1),
+                   "python_cli_dry_run_wall_ms": round(py_ms, 1)}, f, indent=1)
+
+
+def test_malformed_watch_events_are_survived(tmp_path):
+    """Garbage, truncated and hostile JSON on the watch stream (random bytes,
+    deep nesting, huge numbers, bad escapes) neither crashes nor wedges the
+    labeller: a later real event still relabels the node."""
+    import random
+    rng = random.Random(7)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        srv.add_node("node-n")
+        p, _ = _start(fi, srv, tmp_path, "-resync", "300", "-topology_watch", "0")
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"))
+        assert _wait(lambda: srv.watch_starts >= 1)
+        good = json.dumps({"type": "MODIFIED", "object": {"metadata": {"name": "node-n", "labels": {}}}})
+        samples = [b"{", b"}", b"[]", b"null", b"\"x\"", b"{\"type\":", b"{\"type\": \"MODIFIED\", \"object\": 7}",
+                   b"{\"type\": \"ERROR\", \"object\": {\"code\": \"x\"}}", b"[" * 5000, b"{\"a\": 1e999999}",
+                   b"{\"a\": \"\\ud800\\u\"}", b"{\"a\": \"\\q\"}", b"\xff\xfe\x00garbage"]
+        for _ in range(60):
+            cut = rng.randrange(1, len(good))
+            samples.append(good[:cut].encode())
+            samples.append(bytes(rng.randrange(256) for _ in range(rng.randrange(1, 200))))
+        for s in samples:
+            srv.send_raw_event("node-n", s.replace(b"\n", b" ") + b"\n")
+        time.sleep(0.5)
+        assert p.poll() is None
+        srv.set_labels("node-n", {})
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 5.0)
+        rc, err = _stop(p)
+        assert rc == 0, err
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
         srv.stop()
