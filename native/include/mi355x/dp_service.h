@@ -40,6 +40,8 @@ namespace mi355x::rpc {
 //   container_prefix + per_device[id] for each requested id (request order)
 //   + (at least one id) container_nonempty
 //   + (annotation_key set) annotations{annotation_key: join(annotation_names[id], ",")}
+//   + (env_key set, at least one id) envs{env_key: join(env_values[id], ",")}
+//     (passthrough: PCI_RESOURCE_AMD_COM_<RES> = the BDFs of every requested group)
 // as raw protobuf field bytes; an unknown ID is an INVALID_ARGUMENT error.
 struct AllocateTemplate {
   std::string resource;  // for error messages
@@ -48,6 +50,8 @@ struct AllocateTemplate {
   std::string container_nonempty;  // e.g. the node-view mounts of a container that got devices
   std::string annotation_key;
   std::unordered_map<std::string, std::string> annotation_names;
+  std::string env_key;
+  std::unordered_map<std::string, std::string> env_values;
 };
 
 struct RpcEvent {

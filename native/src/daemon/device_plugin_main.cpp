@@ -23,11 +23,17 @@
 //                  pushed when a verdict changes (or every pulse with
 //                  -send_every_pulse, the reference's behaviour)
 //   signals        SIGTERM / SIGINT stop the servers and remove the sockets
+//   passthrough    -driver_type vf-passthrough / pf-passthrough (amdgpu_sriov.go,
+//                  amdgpu_pf.go): one device per IOMMU group, Allocate =
+//                  /dev/vfio/<group> + /dev/vfio/vfio (mrw) and
+//                  PCI_RESOURCE_AMD_COM_<RES> = the BDFs of every requested group;
+//                  health = driver present (+ exporter PF verdicts for VFs);
+//                  without -driver_type: container -> VF -> PF (main.go:106-115)
 //
 // The Python CLI (scripts/k8s-device-plugin) is the full-featured entrypoint:
-// VF/PF passthrough, the MFMA liveness probes and throughput checks, amd-smi,
-// CDI, container views, topology reloads, metrics and tracing. This binary is
-// for nodes that want the reference's feature set without Python.
+// the MFMA liveness probes and throughput checks, amd-smi, CDI, container
+// views, topology reloads, metrics and tracing. This binary is for nodes that
+// want the reference's feature set without Python.
 #include <fcntl.h>
 #include <poll.h>
 #include <signal.h>
@@ -54,6 +60,7 @@
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/grpc_server.h"
 #include "mi355x/kfd_topology.h"
+#include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
 
 namespace {
@@ -158,11 +165,12 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
 }
 
 // ---- protobuf messages (v1beta1 field numbers, api.proto) -------------------
-std::string device_spec(const std::string& path) {  // DeviceSpec{container_path=1, host_path=2, permissions=3}
+// DeviceSpec{container_path=1, host_path=2, permissions=3}
+std::string device_spec(const std::string& path, const char* perms = "rw") {
   std::string s;
   pb::put_bytes(&s, 1, path);
   pb::put_bytes(&s, 2, path);
-  pb::put_bytes(&s, 3, "rw");
+  pb::put_bytes(&s, 3, perms);
   return s;
 }
 
@@ -181,9 +189,14 @@ std::string device_msg(const GpuDevice& d, bool healthy) {  // Device{ID=1, heal
 }
 
 // ---- one advertised resource ------------------------------------------------
+enum class Driver { Container, Vf, Pf };
+
 struct Resource {
-  std::string name;  // "gpu", "cpx_nps1", ...
-  std::vector<GpuDevice> devices;
+  std::string name;  // "gpu", "cpx_nps1", "gpu_vf", ...
+  Driver driver = Driver::Container;
+  std::vector<GpuDevice> devices;          // container driver
+  std::vector<std::string> group_ids;      // passthrough: IOMMU groups, numeric order
+  IommuMap groups;                         // group -> PCI functions
   std::string socket;  // <kubelet_dir>/amd.com_<name>
   std::string options;
   std::unique_ptr<rpc::GrpcServer> server;
@@ -198,6 +211,13 @@ struct Resource {
 
 std::string list_bytes(const Resource& r) {
   std::string out;
+  for (const auto& g : r.group_ids) {  // passthrough: Device{ID=group, health}, no topology
+    auto it = r.health.find(g);
+    std::string m;
+    pb::put_bytes(&m, 1, g);
+    pb::put_bytes(&m, 2, it == r.health.end() || it->second ? "Healthy" : "Unhealthy");
+    pb::put_bytes(&out, 1, m);
+  }
   for (const auto& d : r.devices) {
     auto it = r.health.find(d.id);
     pb::put_bytes(&out, 1, device_msg(d, it == r.health.end() || it->second));
@@ -255,6 +275,38 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
   });
   r.service->set_options(r.options);
   if (r.allocator) r.service->set_allocator(r.allocator);
+  r.service->set_allocate_template(t);
+  r.list = list_bytes(r);
+  r.service->set_device_list(r.list);
+}
+
+// passthrough resources: no preferred allocation, vfio Allocate template
+void prepare_passthrough(Resource& r) {
+  r.options.clear();
+  rpc::AllocateTemplate t;
+  t.resource = r.name;
+  std::string up = r.name;
+  for (auto& c : up) c = static_cast<char>(std::toupper(static_cast<unsigned char>(c)));
+  t.env_key = "PCI_RESOURCE_AMD_COM_" + up;
+  pb::put_bytes(&t.container_nonempty, 3, device_spec("/dev/vfio/vfio", "mrw"));
+  for (const auto& g : r.group_ids) {
+    std::string car;
+    pb::put_bytes(&car, 3, device_spec("/dev/vfio/" + g, "mrw"));
+    t.per_device[g] = car;
+    std::string bdfs;
+    for (const auto& fn : r.groups.at(g)) {
+      if (!bdfs.empty()) bdfs += ",";
+      bdfs += r.driver == Driver::Vf ? fn.vf : fn.pf;
+    }
+    t.env_values[g] = bdfs;
+  }
+  r.service = std::make_unique<rpc::DevicePluginService>();
+  r.service->set_fallback([name = r.name](const std::string& method, const std::string&) {
+    // kubelet only asks when get_preferred_allocation_available is set; answer empty as the reference does
+    if (method == "GetPreferredAllocation") return rpc::Reply{rpc::kOk, "", ""};
+    return rpc::Reply{rpc::kUnimplemented, "not served by the native daemon: " + method + " (" + name + ")", ""};
+  });
+  r.service->set_options(r.options);
   r.service->set_allocate_template(t);
   r.list = list_bytes(r);
   r.service->set_device_list(r.list);
@@ -349,9 +401,36 @@ std::map<std::string, bool> exporter_health(const std::string& socket) {
   return out;
 }
 
+bool set_health(Resource& r, const std::string& id, bool ok) {
+  auto it = r.health.find(id);
+  const bool prev = it == r.health.end() || it->second;
+  r.health[id] = ok;
+  if (prev == ok) return false;
+  logf('W', "device %s: %s -> %s", id.c_str(), prev ? "Healthy" : "Unhealthy", ok ? "Healthy" : "Unhealthy");
+  return true;
+}
+
 // one health pass; true when a verdict changed
 bool refresh_health(Resource& r, const Flags& f, const std::map<std::string, bool>& exporter) {
   bool changed = false;
+  if (r.driver == Driver::Vf) {
+    // gim gone -> every group Unhealthy; else a group is Unhealthy if any parent PF is (amdgpu_sriov.go:217-308)
+    const bool gim = is_dir(path_join(f.sysfs_root, "bus/pci/drivers/gim"));
+    for (const auto& g : r.group_ids) {
+      bool ok = gim;
+      for (const auto& fn : r.groups.at(g)) {
+        auto e = exporter.find(fn.pf);
+        if (e != exporter.end() && !e->second) ok = false;
+      }
+      changed |= set_health(r, g, ok);
+    }
+    return changed;
+  }
+  if (r.driver == Driver::Pf) {  // vfio-pci present -> Healthy (amdgpu_pf.go:210-229)
+    const bool vfio = is_dir(path_join(f.sysfs_root, "bus/pci/drivers/vfio-pci"));
+    for (const auto& g : r.group_ids) changed |= set_health(r, g, vfio);
+    return changed;
+  }
   for (const auto& d : r.devices) {
     bool ok = kfd_node_live(f.sysfs_root, d);
     auto e = exporter.find(d.bdf);
@@ -387,11 +466,6 @@ int main(int argc, char** argv) {
     return 1;
   }
   logf('I', "AMD GPU device plugin for Kubernetes (MI355X-native, native daemon)");
-  if (!f.driver_type.empty() && f.driver_type != "container") {
-    logf('E', "driver type %s is served by the full plugin (scripts/k8s-device-plugin); this binary implements "
-              "the container driver", f.driver_type.c_str());
-    return 1;
-  }
   if (::pipe(g_sig_pipe) != 0) return 1;
   ::fcntl(g_sig_pipe[0], F_SETFL, O_NONBLOCK);
   ::fcntl(g_sig_pipe[1], F_SETFL, O_NONBLOCK);
@@ -402,23 +476,19 @@ int main(int argc, char** argv) {
   sigaction(SIGQUIT, &sa, nullptr);
   signal(SIGPIPE, SIG_IGN);
 
-  const bool kfd = is_dir(path_join(f.sysfs_root, "class/kfd"));
   std::vector<Resource> resources;
   KfdTopology topo;
-  if (!kfd) {
-    // the reference starts its manager even when no implementation initialised, and idles
-    logf('E', "Error instantiating driver type container: No kfd found (%s/class/kfd)", f.sysfs_root.c_str());
-  } else {
+  // one driver's resources; "" on success (an empty list = no devices), else the init error
+  auto init_container = [&](std::vector<Resource>* out) -> std::string {
+    if (!is_dir(path_join(f.sysfs_root, "class/kfd"))) return "No kfd found (" + f.sysfs_root + "/class/kfd)";
     topo = KfdTopology::load_sysfs(f.sysfs_root);
     const DiscoveryResult res = discover_gpus(f.sysfs_root, topo);
     for (const auto& w : res.warnings) logf('W', "%s", w.c_str());
     logf('I', "Found %zu AMDGPUs", res.devices.size());
     const bool homogeneous = is_homogeneous(res.devices);
-    if (!homogeneous && f.naming == "single") {
-      logf('E', "Partitions of different styles across GPUs in a node is not supported with single strategy. "
-                "Please start device plugin with mixed strategy");
-      return 1;
-    }
+    if (!homogeneous && f.naming == "single")
+      return "Partitions of different styles across GPUs in a node is not supported with single strategy. "
+             "Please start device plugin with mixed strategy";
     const auto counts = partition_config_count(res.devices);
     std::vector<std::string> names;
     if (!res.devices.empty()) {
@@ -429,18 +499,69 @@ int main(int argc, char** argv) {
           if (c > 0) names.push_back(t);
     }
     const std::set<std::string> unresolved(res.unresolved.begin(), res.unresolved.end());
+    const auto exporter = exporter_health(f.exporter_socket);
     for (const auto& name : names) {
       Resource r;
       r.name = name;
       for (const auto& d : res.devices)
         if (homogeneous || d.partition_type() == name) r.devices.push_back(d);
       r.socket = path_join(f.kubelet_dir, std::string(kResourceNamespace) + "_" + name);
-      resources.push_back(std::move(r));
-    }
-    const auto exporter = exporter_health(f.exporter_socket);
-    for (auto& r : resources) {
       refresh_health(r, f, exporter);
       prepare(r, topo, unresolved);
+      out->push_back(std::move(r));
+    }
+    return "";
+  };
+  auto init_passthrough = [&](Driver drv, std::vector<Resource>* out) -> std::string {
+    const bool vf = drv == Driver::Vf;
+    if (!is_dir(path_join(f.sysfs_root, vf ? "bus/pci/drivers/gim" : "bus/pci/drivers/vfio-pci")))
+      return vf ? "No amd gim driver loaded" : "No vfio-pci driver loaded";
+    const PciScanResult scan = vf ? scan_vf_mapping(f.sysfs_root) : scan_pf_mapping(f.sysfs_root);
+    if (!scan.ok) return std::string("Failed to generate ") + (vf ? "vf" : "pf") + " map: " + scan.error;
+    logf('I', "Found %zu %s IOMMU groups", scan.groups.size(), vf ? "vf-passthrough" : "pf-passthrough");
+    if (scan.groups.empty()) return "";
+    Resource r;
+    r.driver = drv;
+    r.name = f.naming == "mixed" ? (vf ? "gpu_vf" : "gpu_pf") : kDeviceTypeGpu;
+    r.groups = scan.groups;
+    for (const auto& [g, fns] : scan.groups) r.group_ids.push_back(g);
+    std::sort(r.group_ids.begin(), r.group_ids.end(), [](const std::string& x, const std::string& y) {
+      const bool dx = is_all_digits(x), dy = is_all_digits(y);
+      if (dx != dy) return dx;
+      if (dx && x.size() != y.size()) return x.size() < y.size();  // numeric order
+      return x < y;
+    });
+    r.socket = path_join(f.kubelet_dir, std::string(kResourceNamespace) + "_" + r.name);
+    refresh_health(r, f, exporter_health(vf ? f.exporter_socket : ""));
+    prepare_passthrough(r);
+    out->push_back(std::move(r));
+    return "";
+  };
+  auto init_driver = [&](const std::string& type, std::vector<Resource>* out) {
+    if (type == "container") return init_container(out);
+    return init_passthrough(type == "vf-passthrough" ? Driver::Vf : Driver::Pf, out);
+  };
+  if (!f.driver_type.empty()) {
+    const std::string e = init_driver(f.driver_type, &resources);
+    if (!e.empty()) {
+      logf('E', "Error instantiating driver type %s: %s", f.driver_type.c_str(), e.c_str());
+      return 1;
+    }
+  } else {
+    // container -> VF -> PF; the reference starts its manager even when none initialised, and idles
+    for (const char* type : {"container", "vf-passthrough", "pf-passthrough"}) {
+      std::vector<Resource> got;
+      const std::string e = init_driver(type, &got);
+      if (!e.empty()) {
+        logf('W', "%s implementation failed: %s. Trying next...", type, e.c_str());
+        continue;
+      }
+      if (got.empty()) {
+        logf('W', "%s implementation found no devices. Trying next...", type);
+        continue;
+      }
+      resources = std::move(got);
+      break;
     }
   }
 

@@ -246,7 +246,7 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
       [&](int field, const char* p, size_t n) {
         if (field != 1) return true;
         std::string car = t->container_prefix;
-        std::string ann;
+        std::string ann, env;
         bool any = false;
         const bool scanned = pb::scan(
             p, n,
@@ -264,6 +264,13 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
                 if (any) ann += ",";
                 ann += a == t->annotation_names.end() ? id : a->second;
               }
+              if (!t->env_key.empty()) {
+                auto e = t->env_values.find(id);
+                if (e != t->env_values.end() && !e->second.empty()) {
+                  if (!env.empty()) env += ",";
+                  env += e->second;
+                }
+              }
               any = true;
               ev->ids.push_back(std::move(id));
               return true;
@@ -276,6 +283,12 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
           pb::put_bytes(&entry, 1, t->annotation_key);
           pb::put_bytes(&entry, 2, ann);
           pb::put_bytes(&car, 4, entry);
+        }
+        if (any && !t->env_key.empty()) {
+          std::string entry;
+          pb::put_bytes(&entry, 1, t->env_key);
+          pb::put_bytes(&entry, 2, env);
+          pb::put_bytes(&car, 1, entry);
         }
         pb::put_bytes(&body, 1, car);
         return true;

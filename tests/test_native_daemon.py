@@ -265,15 +265,25 @@ def test_flags(tmp_path):
     assert p.returncode == 1 and "invalid resource_naming_strategy" in p.stderr
     p = subprocess.run(base + ["-pulse=-1"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 1 and "pulse must be a non-negative integer" in p.stderr
+    # an explicitly requested driver that cannot start exits 1 (main.go:94-105)
     p = subprocess.run(base + ["-driver_type=vf-passthrough"], capture_output=True, text=True, timeout=30)
-    assert p.returncode == 1 and "full plugin" in p.stderr
+    assert p.returncode == 1 and "No amd gim driver loaded" in p.stderr
+    p = subprocess.run(base + ["-driver_type=pf-passthrough"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 1 and "No vfio-pci driver loaded" in p.stderr
     p = subprocess.run([EXE, "-h"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 0 and "-resource_naming_strategy" in p.stdout
     # heterogeneous partitions with the single strategy: the reference's init error
     het = make_mi355x_node(tmp_path / "het", per_gpu_compute=["spx"] * 4 + ["cpx"] * 4)
-    p = subprocess.run([EXE, "-kubelet_dir", str(tmp_path / "dp2"), "-sysfs_root", str(het.sysfs)],
-                       capture_output=True, text=True, timeout=30)
+    p = subprocess.run([EXE, "-kubelet_dir", str(tmp_path / "dp2"), "-sysfs_root", str(het.sysfs), "-driver_type",
+                        "container"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 1 and "not supported with single strategy" in p.stderr
+    # without -driver_type the next implementations are tried, and with none the daemon idles (main.go:106-119)
+    q = subprocess.Popen([EXE, "-kubelet_dir", str(tmp_path / "dp3"), "-sysfs_root", str(het.sysfs)],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    time.sleep(0.5)
+    q.send_signal(signal.SIGTERM)
+    _, err = q.communicate(timeout=20)
+    assert q.returncode == 0 and "not supported with single strategy" in err and "No vfio-pci driver loaded" in err
 
 
 @pytest.mark.gpu
@@ -315,5 +325,92 @@ def test_real_node_answers_equal_the_python_plugin(tmp_path):
             await k.stop()
         assert rc == 0, err[-2000:]
         print(f"native daemon on the box: {len(want)} devices, registered {registered_s * 1e3:.1f} ms after exec")
+
+    run(go())
+
+
+def _passthrough_impl(fi, mode, strategy):
+    from rocm_k8s_device_plugin_amd.plugin.passthrough import PfImpl, VfImpl
+    cls = VfImpl if mode == "vf" else PfImpl
+    return cls(strategy, str(fi.sysfs), exporter_socket=None)
+
+
+@pytest.mark.parametrize("mode,strategy,resource", [("vf", "single", "gpu"), ("vf", "mixed", "gpu_vf"),
+                                                    ("pf", "single", "gpu"), ("pf", "mixed", "gpu_pf")])
+def test_passthrough_answers_equal_the_python_plugin(tmp_path, mode, strategy, resource):
+    """VF / PF passthrough (amdgpu_sriov.go, amdgpu_pf.go), picked by the
+    container -> VF -> PF auto-selection: one device per IOMMU group, Allocate
+    with the vfio nodes and PCI_RESOURCE_AMD_COM_<RES> listing every requested
+    group's BDFs, no preferred allocation; answers equal the Python impls'."""
+    fi = make_mi355x_node(tmp_path / "n", mode=mode, vfs_per_gpu=2)
+    impl = _passthrough_impl(fi, mode, strategy)
+    ctx = new_context(resource)
+    impl.start(ctx)
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", "", "-resource_naming_strategy", strategy)
+        try:
+            want = {d.ID: d.health for d in impl.enumerate(ctx)}
+            st = await k.wait_for_resource(f"amd.com/{resource}", len(want), timeout=20)
+            assert st.devices == want and len(want) == (16 if mode == "vf" else 8)
+            opts = await k._call(st, "GetDevicePluginOptions", pb.Empty(), pb.DevicePluginOptions)
+            assert opts == impl.options(ctx) and not opts.get_preferred_allocation_available
+            ids = sorted(want)
+            rng = random.Random(5)
+            for _ in range(10):
+                pick = rng.sample(ids, rng.randint(1, 4))
+                areq = pb.AllocateRequest(container_requests=[pb.ContainerAllocateRequest(devices_ids=pick),
+                                                              pb.ContainerAllocateRequest(devices_ids=[])])
+                got = await k._call(st, "Allocate", areq, pb.AllocateResponse)
+                assert got == impl.allocate(ctx, areq)
+                env = got.container_responses[0].envs[f"PCI_RESOURCE_AMD_COM_{resource.upper()}"]
+                assert len(env.split(",")) == len(pick)   # one function per group in these trees
+            preq = pb.PreferredAllocationRequest(container_requests=[pb.ContainerPreferredAllocationRequest(
+                available_deviceIDs=ids, allocation_size=1)])
+            assert await k._call(st, "GetPreferredAllocation", preq, pb.PreferredAllocationResponse) == \
+                pb.PreferredAllocationResponse()
+        finally:
+            rc, err = await _stop(proc)
+            await k.stop()
+        assert rc == 0, err[-2000:]
+
+    run(go())
+
+
+def test_vf_health_follows_gim_and_the_exporter(tmp_path):
+    """A VF group is Unhealthy when its parent PF is (exporter), and every group
+    when the gim driver goes away (amdgpu_sriov.go:217-308)."""
+    import shutil
+    fi = make_mi355x_node(tmp_path / "n", mode="vf", vfs_per_gpu=2)
+    impl = _passthrough_impl(fi, "vf", "single")
+    kdir = str(tmp_path / "dp")
+    sock = str(tmp_path / "exp" / "exporter.sock")
+    bad_pf = fi.bdfs[2]
+    bad_groups = sorted(g for g, fns in impl.groups.items() if any(f.pf == bad_pf for f in fns))
+    assert len(bad_groups) == 2
+
+    async def go():
+        exp = FakeExporter(sock, {b: "healthy" for b in fi.bdfs})
+        await exp.start()
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await _daemon(kdir, fi, "-exporter_socket", sock, "-pulse", "1", "-driver_type", "vf-passthrough")
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 16, timeout=20)
+            assert set(st.devices.values()) == {"Healthy"}
+            exp.states[bad_pf] = "unhealthy"
+            st = await k.wait_for_update("amd.com/gpu", st.updates, timeout=10)
+            assert sorted(i for i, h in st.devices.items() if h == "Unhealthy") == bad_groups
+            shutil.rmtree(fi.sysfs / "bus/pci/drivers/gim")
+            st = await k.wait_for_update("amd.com/gpu", st.updates, timeout=10)
+            assert set(st.devices.values()) == {"Unhealthy"}
+        finally:
+            rc, err = await _stop(proc)
+            await k.stop()
+            await exp.stop()
+        assert rc == 0, err[-2000:]
 
     run(go())
