@@ -281,7 +281,8 @@ std::string start(Conn* c, const Config& cfg, const std::string& method, const s
                   int timeout_ms, int wake_fd) {
   std::string err = c->open(cfg);
   if (!err.empty()) return err;
-  std::string req = method + " " + path + " HTTP/1.1\r\nHost: " + c->host() + "\r\nConnection: close\r\n";
+  const std::string host = c->host().find(':') != std::string::npos ? "[" + c->host() + "]" : c->host();  // IPv6
+  std::string req = method + " " + path + " HTTP/1.1\r\nHost: " + host + "\r\nConnection: close\r\n";
   for (const auto& [k, v] : headers) req += k + ": " + v + "\r\n";
   if (!body.empty() || method == "PATCH" || method == "PUT" || method == "POST")
     req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
