@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Soak of the native daemon (`mi355x-device-plugin`) on a real node.
+
+The daemon registers at a fake kubelet over UDS on the node's own /sys, with a
+1 s health pulse; admissions (GetPreferredAllocation + Allocate of every size
+1..N over the native gRPC server) run back to back with no pause. Every
+--report seconds one JSON line: admissions, errors, RPC latency percentiles,
+and what would leak if anything did: the daemon's RSS, open fds and threads.
+
+  python tools/soak_native.py --seconds 120 --out gpurun_out/soak_native.json
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR  # noqa: E402
+from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet  # noqa: E402
+
+EXE = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+
+
+def proc_stats(pid: int) -> dict:
+    out = {}
+    with open(f"/proc/{pid}/status") as f:
+        for line in f:
+            k, _, v = line.partition(":")
+            if k in ("VmRSS", "Threads"):
+                out[k] = int(v.split()[0])
+    out["fds"] = len(os.listdir(f"/proc/{pid}/fd"))
+    return {"rss_kb": out.get("VmRSS"), "threads": out.get("Threads"), "fds": out["fds"]}
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    return round(xs[min(len(xs) - 1, int(q * len(xs)))], 4) if xs else None
+
+
+async def main(a) -> int:
+    kdir = tempfile.mkdtemp(prefix="soak-native-")
+    k = FakeKubelet(kdir)
+    await k.start()
+    proc = await asyncio.create_subprocess_exec(EXE, "-kubelet_dir", kdir, "-sysfs_root", a.sysfs_root,
+                                                "-pulse", str(a.pulse), "-exporter_socket", "",
+                                                stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
+    rows = []
+    try:
+        st = await k.wait_for_resource("amd.com/gpu", 1, timeout=30)
+        n = len(st.devices)
+        t_end = time.monotonic() + a.seconds
+        next_report = time.monotonic() + a.report
+        adm = errors = 0
+        lat = []
+        first = proc_stats(proc.pid)
+        while time.monotonic() < t_end:
+            size = adm % n + 1
+            try:
+                r = await k.admit("amd.com/gpu", size)
+                lat.append(r.total_ms)
+                k.release("amd.com/gpu", r.device_ids)
+                adm += 1
+            except Exception as e:  # noqa: BLE001
+                errors += 1
+                print(f"admission error: {e}", file=sys.stderr)
+            if time.monotonic() >= next_report:
+                next_report += a.report
+                row = {"t_s": round(a.seconds - (t_end - time.monotonic()), 1), "admissions": adm, "errors": errors,
+                       "rpc_ms_p50": pct(lat, 0.5), "rpc_ms_p99": pct(lat, 0.99), **proc_stats(proc.pid)}
+                rows.append(row)
+                print(json.dumps(row), flush=True)
+                lat = []
+        doc = {"exe": "mi355x-device-plugin", "devices": n, "pulse_s": a.pulse, "seconds": a.seconds,
+               "start": first, "reports": rows, "admissions": adm, "errors": errors,
+               "listandwatch_updates": k.state("amd.com/gpu").updates if hasattr(k, "state") else None}
+    finally:
+        if proc.returncode is None:
+            proc.terminate()
+        _, err = await asyncio.wait_for(proc.communicate(), 20)
+        await k.stop()
+    doc["exit_code"] = proc.returncode
+    doc["stderr_tail"] = err.decode(errors="replace")[-500:]
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(doc, f, indent=1)
+    print(json.dumps({k_: doc[k_] for k_ in ("admissions", "errors", "exit_code")}))
+    return 0 if doc["errors"] == 0 and doc["exit_code"] == 0 else 1
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--seconds", type=float, default=120)
+    ap.add_argument("--report", type=float, default=15)
+    ap.add_argument("--pulse", type=int, default=1)
+    ap.add_argument("--sysfs-root", default="/sys")
+    ap.add_argument("--out", default="")
+    sys.exit(asyncio.run(main(ap.parse_args())))
