@@ -117,7 +117,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       has_value = true;
     }
     if (name == "h" || name == "help") {
-      std::printf("usage: %s [-pulse N] [-driver_type container] [-resource_naming_strategy single|mixed] "
+      std::printf("usage: %s [-pulse N] [-driver_type container|vf-passthrough|pf-passthrough] [-resource_naming_strategy single|mixed] "
                   "[-kubelet_dir DIR] [-sysfs_root DIR] [-dev_root DIR] [-exporter_socket PATH] "
                   "[-send_every_pulse] (glog flags accepted)\n", argv[0]);
       std::exit(0);
