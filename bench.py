@@ -239,52 +239,63 @@ def throughput_check(ordinals) -> dict:
 
 
 class Dist:
-    """torch.distributed when launched by torchrun, else a 1-rank stub."""
+    """Rank coordination for the bench. The measured thing is a kubelet node
+    admitting pods, and a kubelet node has no resident GPU process: the bench
+    and plugin processes must not hold a GPU context, kfd queues or an RCCL
+    communicator while containers initialise their GPUs. So:
+
+    * step barriers and object exchange run over gloo (CPU, TCP) under torchrun;
+      at world = 1 nothing is initialised and torch is not even imported;
+    * ``sync()`` synchronises the GPU only if this process already has a HIP
+      context (it never creates one); the containers' GPU work is complete by
+      construction when a step ends (ready = every MFMA tile verified);
+    * RCCL is created only after the timed loop, for the collectives extra
+      (``rccl_group()``).
+    """
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.launcher = "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or self.world > 1 else "single-process"
         self.torch = None
-        self.cuda = False
-        self.gloo = None
-        try:
-            import torch
-            self.torch = torch
-            self.cuda = torch.cuda.is_available()
-        except Exception:
-            self.torch = None
+        self.dist = None
+        self.cuda = False   # this process drives a GPU (only ever for the RCCL extra)
         if self.world > 1:
+            import torch
             import torch.distributed as dist
-            self.dist = dist
-            if self.cuda:
-                # one rank per GPU over RCCL for the step barriers; object exchange
-                # (allocation -> ranks, ready timestamps -> rank 0) over a gloo group
-                self.torch.cuda.set_device(self.local_rank)
-                dist.init_process_group("nccl", device_id=self.torch.device("cuda", self.local_rank))
-                self.gloo = dist.new_group(backend="gloo")
-            else:
-                dist.init_process_group("gloo")
-                self.gloo = None
+            self.torch, self.dist = torch, dist
+            dist.init_process_group("gloo")
 
     def sync(self):
         if self.world > 1:
             self.dist.barrier()
-        if self.cuda:
-            self.torch.cuda.synchronize()
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+    def rccl_group(self):
+        """After the timed loop: (group, on_gpu) for the collectives extra, one
+        rank per GPU over RCCL when GPUs are visible, else the gloo group."""
+        torch, dist = self.torch, self.dist
+        if not torch.cuda.is_available():
+            return None, False
+        torch.cuda.set_device(self.local_rank)
+        self.cuda = True
+        return dist.new_group(backend="nccl", device_id=torch.device("cuda", self.local_rank)), True
 
     def bcast(self, obj):
         if self.world == 1:
             return obj
         box = [obj]
-        self.dist.broadcast_object_list(box, src=0, group=self.gloo)
+        self.dist.broadcast_object_list(box, src=0)
         return box[0]
 
     def gather(self, obj):
         if self.world == 1:
             return [obj]
         out = [None] * self.world
-        self.dist.all_gather_object(out, obj, group=self.gloo)
+        self.dist.all_gather_object(out, obj)
         return out
 
     def max(self, x: float) -> float:
@@ -293,6 +304,49 @@ class Dist:
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
+
+
+def process_gpu_state() -> dict:
+    """This process's hold on the GPU right now: a torch HIP context, open
+    /dev/kfd and render-node descriptors (a kubelet node has none of these)."""
+    torch = sys.modules.get("torch")
+    kfd = render = 0
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                t = os.readlink(f"/proc/self/fd/{fd}")
+            except OSError:
+                continue
+            kfd += t == "/dev/kfd"
+            render += t.startswith("/dev/dri/renderD")
+    except OSError:
+        pass
+    return {"torch_cuda_initialized": bool(torch is not None and torch.cuda.is_initialized()),
+            "kfd_fds": kfd, "render_fds": render}
+
+
+def tail_attribution(lat, phases, factor=1.5) -> dict:
+    """Every step slower than factor x p50: which phase carries the excess.
+    ``phases`` maps a phase name to its per-step ms (aligned with ``lat``); a
+    slow step is attributed to the phase with the largest excess over its own
+    p50."""
+    if not lat:
+        return {}
+    p50 = pct(lat, .5)
+    med = {k: pct(v, .5) for k, v in phases.items()}
+    slow, by_phase = [], {}
+    for i, x in enumerate(lat):
+        if x <= factor * p50:
+            continue
+        excess = {k: round(v[i] - med[k], 2) for k, v in phases.items()}
+        top = max(excess, key=excess.get)
+        by_phase.setdefault(top, []).append(excess[top])
+        slow.append({"step": i, "latency_ms": round(x, 2), "phase": top, "excess_ms": excess})
+    return {"threshold_ms": round(factor * p50, 2), "p99_over_p50": round(pct(lat, .99) / p50, 3) if p50 else None,
+            "phase_p50_ms": {k: round(v, 3) for k, v in med.items()},
+            "slow_steps": slow,
+            "by_phase": {k: {"steps": len(v), "excess_ms_mean": round(statistics.mean(v), 2)}
+                         for k, v in sorted(by_phase.items())}}
 
 
 def main():
@@ -356,7 +410,8 @@ def main():
         gpu_info = None
 
     rpc_ms, alloc_rpc_ms, lat_ms, ready_ms, kern_us = [], [], [], [], []
-    exec_ms, rt_ms, dev_ms, settle_ms = [], [], [], []
+    exec_ms, rt_ms, dev_ms, settle_ms, prespawn_ms = [], [], [], [], []
+    gpu_state = {"torch_cuda_initialized": False, "kfd_fds": 0, "render_fds": 0}   # worst seen in the timed loop
     from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
 
     def blocking(fn, *a, **kw):
@@ -414,6 +469,11 @@ def main():
             phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
             lingering = r.kfd_lingering
+        if record:   # the containers are up: does the bench / plugin process hold the GPU?
+            st_now = process_gpu_state()
+            gpu_state["torch_cuda_initialized"] |= st_now["torch_cuda_initialized"]
+            gpu_state["kfd_fds"] = max(gpu_state["kfd_fds"], st_now["kfd_fds"])
+            gpu_state["render_fds"] = max(gpu_state["render_fds"], st_now["render_fds"])
         allr = d.gather(mine)
         bad = [m[3] for m in allr if not m[0]]
         if bad:
@@ -444,6 +504,7 @@ def main():
             exec_ms.append((tm - sp) / 1e6)
             rt_ms.append((trt - tm) / 1e6)
             dev_ms.append((t_ready - trt) / 1e6)
+            prespawn_ms.append(max(0.0, (sp - t0) / 1e6 - tot))
 
     for _ in range(args.warmup):
         one_step(False)
@@ -457,6 +518,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     server_ms = plug.server_ms() if d.rank == 0 else {}
     elapsed = d.max(elapsed)
+    rank_gpu_state = d.gather(gpu_state)
     hip_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
     other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
     if n > 1:
@@ -510,19 +572,20 @@ def main():
     if args.collectives and d.world > 1:
         # the pod's GPUs as a torchrun workload sees them: one rank per GPU, RCCL over xGMI
         from rocm_k8s_device_plugin_amd.parallel import collectives as coll
-        if d.cuda:
-            sizes = args.collective_sizes or "1M,64M,256M"
-            ops, iters, dtype = coll.DEFAULT_OPS, 20, d.torch.bfloat16
-        else:
-            sizes = args.collective_sizes or "64K"
-            ops, iters, dtype = ("all_reduce", "all_gather"), 3, d.torch.float32
         # a secondary measurement: a failure is reported in the JSON line, not
         # allowed to take the headline down with it
         try:
+            group, on_gpu = d.rccl_group()   # RCCL is created here, after the timed loop
+            if on_gpu:
+                sizes = args.collective_sizes or "1M,64M,256M"
+                ops, iters, dtype = coll.DEFAULT_OPS, 20, d.torch.bfloat16
+            else:
+                sizes = args.collective_sizes or "64K"
+                ops, iters, dtype = ("all_reduce", "all_gather"), 3, d.torch.float32
             rows = coll.run([coll.parse_size(x) for x in sizes.split(",") if x], ops, iters=iters, warmup=3,
-                            dtype=dtype)
+                            dtype=dtype, group=group)
             rccl = coll.summary(rows)
-            rccl["backend"] = d.dist.get_backend()
+            rccl["backend"] = d.dist.get_backend(group)
         except Exception as e:  # noqa: BLE001
             rccl = {"error": f"{type(e).__name__}: {e}"[:300]}
 
@@ -585,6 +648,16 @@ def main():
                  "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
                                              "gpu_runtime_init": round(pct(rt_ms, .5), 3),
                                              "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
+                 # every timed step above 1.5 x p50, attributed to the admission phase with the largest excess
+                 "tail_attribution": tail_attribution(lat_ms, {
+                     "plugin_rpc": rpc_ms, "runtime_prep": prespawn_ms, "spawn_to_main": exec_ms,
+                     "gpu_runtime_init": rt_ms, "device_setup_and_mfma": dev_ms}),
+                 # the node under test must look like a kubelet node: no GPU context in the bench /
+                 # plugin process(es) while the timed containers initialise (worst over the timed steps)
+                 "launcher": d.launcher,
+                 "bench_process_gpu": {"ranks": rank_gpu_state,
+                                       "clean": not any(s["torch_cuda_initialized"] or s["kfd_fds"]
+                                                        for s in rank_gpu_state)},
                  "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
                  "reference_algorithm_candidates": ref["candidates"], "allocator_sweep": sweep, "gpus": gpu_info}
         from rocm_k8s_device_plugin_amd.parallel.fabric import Fabric
@@ -637,7 +710,8 @@ def main():
                                        ("1 container process with all N GPUs" if args.container_mode == "pod"
                                         else "1 container process per GPU")),
                        "between_admissions": ("previous pod's kfd teardown complete" if args.settle == "kfd"
-                                              else "back-to-back")},
+                                              else "back-to-back"),
+                       "launcher": d.launcher},
             "extra": extra,
         }
         line = json.dumps(out)

@@ -5,8 +5,6 @@
 #include <unordered_set>
 
 #include "mi355x/allocator.h"
-
-#include <set>
 #include "mi355x/constants.h"
 
 namespace mi355x {

@@ -106,6 +106,9 @@ def test_bench_fixture_reports_fabric_and_collectives():
     e = d["extra"]
     assert e["container_dev_view"] == "specs" and e["latency_p50_ms_container_mode_per-gpu"] > 0
     assert len(e["steps_ms"]) == 2
+    # gloo carries the step barriers: no rank holds a GPU context or kfd fd in the timed loop
+    assert e["launcher"] == "torchrun" and d["config"]["launcher"] == "torchrun"
+    assert e["bench_process_gpu"]["clean"] and len(e["bench_process_gpu"]["ranks"]) == 2
     # 2 of the fixture's 8 GPUs from a fragmented availability (second plugin
     # instance, containers split one per rank as in the headline run)
     fr = e["fragmented_n_of_m"]
@@ -128,3 +131,11 @@ def test_bench_n_of_m_searches_inside_the_timed_step():
     assert ta["same_set_as_reference"] is True and len(ta["chosen"]) == 1
     assert "8 GPUs advertised, 1 pod requesting 3, 2 held" in d["config"]["parallelism"]
     assert d["extra"]["fragmented_n_of_m"] is None       # only with M = N
+    e = d["extra"]
+    assert e["launcher"] == "single-process"
+    assert e["bench_process_gpu"] == {"ranks": [{"torch_cuda_initialized": False, "kfd_fds": 0, "render_fds": 0}],
+                                      "clean": True}
+    ta = e["tail_attribution"]
+    assert set(ta["phase_p50_ms"]) == {"plugin_rpc", "runtime_prep", "spawn_to_main", "gpu_runtime_init",
+                                       "device_setup_and_mfma"}
+    assert all(s["latency_ms"] > ta["threshold_ms"] for s in ta["slow_steps"])
