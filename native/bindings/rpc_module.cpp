@@ -141,6 +141,7 @@ void bind_rpc(py::module_& m) {
         d["connections"] = st.connections;
         d["calls"] = st.calls;
         d["streams_open"] = st.streams_open;
+        d["streams_opened"] = st.streams_opened;
         d["protocol_errors"] = st.protocol_errors;
         d["bytes_in"] = st.bytes_in;
         d["bytes_out"] = st.bytes_out;
@@ -151,11 +152,11 @@ void bind_rpc(py::module_& m) {
       .def(py::init<>())
       .def(
           "connect",
-          [](GrpcClient& c, const std::string& path) {
+          [](GrpcClient& c, const std::string& path, double timeout_s) {
             py::gil_scoped_release nogil;
-            return c.connect(path);
+            return c.connect(path, timeout_s);
           },
-          py::arg("unix_path"))
+          py::arg("unix_path"), py::arg("timeout_s") = 10.0)
       .def(
           "unary",
           [](GrpcClient& c, const std::string& path, const std::string& req, double timeout_s) {
@@ -169,6 +170,9 @@ void bind_rpc(py::module_& m) {
           py::arg("path"), py::arg("request"), py::arg("timeout_s") = 10.0,
           "-> (grpc status, message, response bytes); status -1 = transport error")
       .def("close", &GrpcClient::close)
+      .def("set_abort_fd", &GrpcClient::set_abort_fd, py::arg("fd"),
+           "a readable fd ends any wait at once (status -1, 'interrupted'); -1 = none")
+      .def_property_readonly("going_away", &GrpcClient::going_away)
       .def_property_readonly("connected", &GrpcClient::connected);
 
   // HPACK primitives, exposed for the interop / conformance tests

@@ -24,10 +24,13 @@ enum GrpcStatus : int {
   kCancelled = 1,
   kUnknown = 2,
   kInvalidArgument = 3,
-  kInternal = 13,
-  kUnimplemented = 12,
+  kDeadlineExceeded = 4,
+  kPermissionDenied = 7,
   kResourceExhausted = 8,
+  kUnimplemented = 12,
+  kInternal = 13,
   kUnavailable = 14,
+  kUnauthenticated = 16,
 };
 
 struct Reply {
@@ -47,6 +50,7 @@ struct ServerStats {
   uint64_t connections = 0;
   uint64_t calls = 0;
   uint64_t streams_open = 0;
+  uint64_t streams_opened = 0;  // server-streaming calls ever opened (ListAndWatch)
   uint64_t protocol_errors = 0;
   uint64_t bytes_in = 0;
   uint64_t bytes_out = 0;
@@ -85,9 +89,20 @@ class GrpcServer {
   std::atomic<bool> running_{false};
 };
 
-// Minimal blocking unary client over a Unix socket (the benchmark's kubelet
-// stand-in: kubelet's own client is native grpc-go, not an interpreter).
-// One call at a time per client; the connection is reused across calls.
+// Blocking unary client over a Unix socket: the daemons' Registration and
+// metrics-exporter client, and the benchmark's kubelet stand-in (kubelet's own
+// client is grpc-go, not an interpreter). One call at a time per client; the
+// connection is reused across calls until the server sends GOAWAY.
+//
+// HTTP/2 as a grpc-go server expects it (vendor/google.golang.org/grpc/
+// internal/transport/http2_server.go): header blocks of any stream are decoded
+// in arrival order (HEADERS + CONTINUATION, dynamic-table inserts), request
+// DATA waits for the peer's connection and stream windows and never exceeds
+// its SETTINGS_MAX_FRAME_SIZE, SETTINGS and PING are acknowledged, a GOAWAY
+// that leaves the call unprocessed fails it, RST_STREAM and a non-200 :status
+// map to gRPC codes as grpc-go does. Every wait is bounded by the call's
+// deadline and ends early when `abort_fd` (a daemon's signal pipe) becomes
+// readable; EINTR never turns into a blocking read.
 class GrpcClient {
  public:
   GrpcClient();
@@ -95,15 +110,18 @@ class GrpcClient {
   GrpcClient(const GrpcClient&) = delete;
   GrpcClient& operator=(const GrpcClient&) = delete;
 
-  std::string connect(const std::string& unix_path);  // "" or an error
-  // status -1: transport error / timeout (message says which)
+  std::string connect(const std::string& unix_path, double timeout_s = 10.0);  // "" or an error
+  // status -1: transport error / timeout / interrupted (message says which)
   Reply unary(const std::string& path, const std::string& request, double timeout_s);
   void close();
   bool connected() const { return fd_ >= 0; }
+  void set_abort_fd(int fd) { abort_fd_ = fd; }
+  // the server announced GOAWAY: the next call needs a new connection
+  bool going_away() const;
 
  private:
-  bool read_some(int timeout_ms, std::string* err);
   int fd_ = -1;
+  int abort_fd_ = -1;
   uint32_t next_sid_ = 1;
   std::string in_;
   std::unique_ptr<struct ClientState> st_;
