@@ -89,6 +89,9 @@ def build_parser() -> flags.GoFlagParser:
                                                    "by kfd link weight/bandwidth; off = the reference's candidates")
     p.add_str("grpc_server", "native", "kubelet-facing gRPC server: native (C++ HTTP/2; admission RPCs answered "
                                        "without Python) or aio (Python grpc.aio)")
+    p.add_float("grpc_watchdog", 10.0, "native server watchdog: no ListAndWatch stream this many seconds after "
+                                       "Register, or an HTTP/2 protocol error on the plugin socket, re-serves the "
+                                       "resource with grpc.aio and registers again (0 = off)")
     p.add_bool("dry_run", False, "print what this node would advertise (implementation, resources, devices, "
                                  "health after one sweep, preferred allocations per size) as JSON and exit")
     p.add_float("topology_watch", 5.0, "seconds between checks for a GPU topology change (kfd generation, "
@@ -137,6 +140,8 @@ def validate(ns) -> Optional[str]:
         return "perf_check_every needs -liveness (the throughput check runs in the probe server)"
     if ns.grpc_server not in ("native", "aio"):
         return f"invalid grpc_server provided: {ns.grpc_server}, supported values are native or aio"
+    if ns.grpc_watchdog < 0:
+        return "grpc_watchdog must be >= 0"
     return None
 
 
@@ -279,7 +284,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         return 0
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
                        metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch, grpc_server=ns.grpc_server,
-                       allocator_extended_search=ns.allocator_extended_search)
+                       allocator_extended_search=ns.allocator_extended_search, grpc_watchdog_s=ns.grpc_watchdog)
     from ..utils.trace import TRACER
     TRACER.configure(ns.trace_file or None)
     try:

@@ -64,6 +64,10 @@ class ManagerConfig:
     grpc_server: str = "native"
     # GetPreferredAllocation beyond the reference's candidate family (allocator.py)
     allocator_extended_search: bool = False
+    # native transport watchdog: after Register is acknowledged, no ListAndWatch
+    # stream within this many seconds, or any HTTP/2 protocol error on the
+    # plugin socket, moves the resource to grpc.aio and registers again. 0 = off
+    grpc_watchdog_s: float = 10.0
 
 
 class ResourcePlugin:
@@ -82,6 +86,10 @@ class ResourcePlugin:
         self.started = False
         self.registrations = 0
         self._lock = asyncio.Lock()
+        # set by the watchdog: the native transport failed with this kubelet;
+        # the resource is served by grpc.aio for the rest of the process
+        self.native_failed: Optional[str] = None
+        self._watchdog: Optional[asyncio.Task] = None
 
     def start(self) -> bool:
         try:
@@ -109,7 +117,7 @@ class ResourcePlugin:
         self._cleanup()
         os.makedirs(os.path.dirname(self.socket), exist_ok=True)
         self.stop_bc = Broadcast()
-        if self.mgr.cfg.grpc_server == "native":
+        if self.mgr.cfg.grpc_server == "native" and self.native_failed is None:
             try:
                 native = NativePluginServer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
                                             self.mgr.cfg.send_every_pulse)
@@ -151,6 +159,8 @@ class ResourcePlugin:
                     await self._serve()
                     await self._register()
                     self.running = True
+                    if self.native is not None and cfg.grpc_watchdog_s > 0:
+                        self._watchdog = asyncio.create_task(self._watch_native(self.native))
                     log.info_fields(_log, "plugin server started", resource=self.resource_name,
                                     socket=self.socket, startup_ms=f"{(time.perf_counter() - t0) * 1e3:.2f}")
                     return True
@@ -165,7 +175,45 @@ class ResourcePlugin:
                         await asyncio.sleep(cfg.retry_wait_s)
             return False
 
+    async def _watch_native(self, native: NativePluginServer) -> None:
+        """The native HTTP/2 stack has only been proven against grpc-go by
+        emulation (testing/gopeer.py). If the real kubelet cannot complete a
+        call on it, the plugin would stay registered and invisible; the
+        reference's grpc-go server has no such risk (vendored dpm/plugin.go:
+        93-162). So: kubelet opens ListAndWatch right after Register; no stream
+        within grpc_watchdog_s, or protocol errors on the socket, and this
+        resource is re-served with grpc.aio and registered again."""
+        cfg = self.mgr.cfg
+        st0 = native.srv.stats()
+        t0 = time.monotonic()
+        seen_stream = False
+        reason = ""
+        while self.native is native:
+            await asyncio.sleep(min(0.25, cfg.grpc_watchdog_s / 4) if not seen_stream else 1.0)
+            if self.native is not native:
+                return
+            st = native.srv.stats()
+            seen_stream = seen_stream or st["streams_opened"] > st0["streams_opened"]
+            if st["protocol_errors"] > st0["protocol_errors"]:
+                reason = f"{st['protocol_errors'] - st0['protocol_errors']} HTTP/2 protocol error(s) on the plugin socket"
+            elif not seen_stream and time.monotonic() - t0 > cfg.grpc_watchdog_s:
+                reason = f"no ListAndWatch stream within {cfg.grpc_watchdog_s:g}s of Register"
+            if reason:
+                break
+        else:
+            return
+        self.native_failed = reason
+        _log.error("%s: native gRPC transport watchdog: %s; serving with grpc.aio and registering again",
+                   self.resource_name, reason)
+        REGISTRY.inc("mi355x_dp_grpc_native_fallbacks_total", resource=self.name, reason="watchdog")
+        await self.stop_server()
+        await self.start_server()
+
     async def _stop_locked(self) -> None:
+        if self._watchdog is not None and self._watchdog is not asyncio.current_task():
+            self._watchdog.cancel()
+            await asyncio.gather(self._watchdog, return_exceptions=True)
+        self._watchdog = None
         self.stop_bc.close()
         if self.native is not None:
             await self.native.stop(grace=0.5)

@@ -88,6 +88,10 @@ class FakeKubelet:
         self.registrations: List[object] = []
         self.register_times: Dict[str, float] = {}   # resource -> time.monotonic() of its last Register
         self._registered = asyncio.Event()
+        # False: after Register, only GetDevicePluginOptions is called and no
+        # ListAndWatch stream is opened (a kubelet whose client cannot complete
+        # calls on the plugin's transport; drives the plugin's watchdog)
+        self.open_list_and_watch = True
 
     # -------------------------------------------------------------- server side
     async def Register(self, request, context):  # noqa: N802
@@ -111,6 +115,8 @@ class FakeKubelet:
         st.stub = pb.DevicePluginStub(st.channel)
         try:
             st.options = await st.stub.GetDevicePluginOptions(pb.Empty(), timeout=10)
+            while not self.open_list_and_watch:
+                await asyncio.sleep(0.05)
             async for resp in st.stub.ListAndWatch(pb.Empty()):
                 st.devices = {d.ID: d.health for d in resp.devices}
                 st.numa = {d.ID: [n.ID for n in d.topology.nodes] for d in resp.devices}

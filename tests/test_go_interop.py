@@ -1,0 +1,600 @@
+"""Interop of the native HTTP/2 transport with grpc-go, the kubelet's stack.
+
+No Go toolchain exists here, so grpc-go's transport is replayed frame by frame
+from the vendored sources (rocm_k8s_device_plugin_amd/testing/gopeer.py):
+
+* GoClientConn (a kubelet's client connection) against the plugin socket of
+  the native daemon: preface, empty SETTINGS, x/net HPACK with dynamic-table
+  inserts and evictions, ``user-agent`` / ``te`` / ``grpc-timeout``, BDP pings
+  interleaved with DATA, a mid-connection SETTINGS{INITIAL_WINDOW_SIZE} after
+  a BDP update, concurrent streams, RST_STREAM(CANCEL) of ListAndWatch and a
+  re-open, header blocks split by CONTINUATION;
+* GoServer (the kubelet's Registration server, the metrics exporter) against
+  the native client: its SETTINGS, response header blocks split into
+  CONTINUATION frames, server PINGs, SETTINGS changes mid-call, small windows
+  for large requests, GOAWAY ENHANCE_YOUR_CALM ``too_many_pings``, graceful
+  GOAWAY, RST_STREAM(REFUSED_STREAM), non-gRPC HTTP status, a server that
+  never answers (deadline, abort fd).
+
+Reference: vendor/google.golang.org/grpc/internal/transport/{http2_client,
+http2_server,controlbuf,flowcontrol,bdp_estimator}.go, vendor/golang.org/x/net/
+http2/hpack/{encode,tables,static_table}.go.
+"""
+import os
+import re
+import signal
+import socket
+import struct
+import subprocess
+import threading
+import time
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR, core
+from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+from rocm_k8s_device_plugin_amd.testing import gopeer as gp
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+
+EXE = os.environ.get("MI355X_NATIVE_DAEMON_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+XNET = "/root/reference/vendor/golang.org/x/net/http2/hpack"
+DP = "/v1beta1.DevicePlugin/"
+REGISTER = "/v1beta1.Registration/Register"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} was not built")
+
+
+def _wait(cond, timeout=10.0, step=0.02):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if cond():
+            return True
+        time.sleep(step)
+    return cond()
+
+
+# ------------------------------------------------------------------ the peers' own HPACK
+
+def _xnet(name):
+    path = os.path.join(XNET, name)
+    if not os.path.exists(path):
+        pytest.skip("vendored x/net sources not available")
+    with open(path) as f:
+        return f.read()
+
+
+def test_huffman_code_equals_xnet_tables():
+    """The peers' canonical code (from RFC 7541 code lengths) is x/net's table."""
+    src = _xnet("tables.go")
+    codes = src[src.index("var huffmanCodes"):src.index("var huffmanCodeLen")]
+    lens = src[src.index("var huffmanCodeLen"):]
+    codes = [int(x, 16) for x in re.findall(r"0x[0-9a-f]+", codes)]
+    lens = [int(x) for x in re.findall(r"\b\d+\b", lens[lens.index("{"):lens.index("}")])]
+    assert len(codes) == 256 and len(lens) == 256
+    assert gp.HUFF_CODE[:256] == codes and list(gp.HUFF_LEN[:256]) == lens
+
+
+def test_static_table_and_name_index_equal_xnet():
+    src = _xnet("static_table.go")
+    ents = re.findall(r'\{Name: "([^"]*)", Value: "([^"]*)", Sensitive: false\}', src)
+    assert tuple(ents) == gp.STATIC_TABLE
+    by_name = dict(re.findall(r'^\s*"([^"]+)":\s+(\d+),$', src[:src.index("byNameValue")], re.M))
+    assert {k: int(v) for k, v in by_name.items()} == gp._STATIC_NAME
+
+
+def test_go_encoder_rfc7541_c4_request():
+    """RFC 7541 C.4.1-C.4.3: x/net's encoder indexes :authority and custom
+    headers, Huffman-codes them, and refers to the dynamic table on repeats."""
+    enc = gp.GoHpackEncoder()
+    first = enc.encode([(":method", "GET"), (":scheme", "http"), (":path", "/"), (":authority", "www.example.com")])
+    assert first.hex() == "828684418cf1e3c2e5f23a6ba0ab90f4ff"
+    second = enc.encode([(":method", "GET"), (":scheme", "http"), (":path", "/"), (":authority", "www.example.com"),
+                         ("cache-control", "no-cache")])
+    assert second.hex() == "828684be5886a8eb10649cbf"
+    third = enc.encode([(":method", "GET"), (":scheme", "https"), (":path", "/index.html"),
+                        (":authority", "www.example.com"), ("custom-key", "custom-value")])
+    assert third.hex() == "828785bf408825a849e95ba97d7f8925a849e95bb8e8b4bf"
+
+
+def test_go_encoder_streams_decode_with_evictions_natively_and_in_python():
+    """A long grpc-go header sequence (a new grpc-timeout value on every call
+    fills and evicts the dynamic table): the independent Python decoder and
+    the native decoder (one block at a time, fresh table) read the same fields
+    where the block is self-contained."""
+    enc, dec = gp.GoHpackEncoder(), gp.HpackDecoder()
+    conn = gp.GoClientConn.__new__(gp.GoClientConn)
+    conn.user_agent, conn.authority = gp.GRPC_GO_USER_AGENT, "localhost"
+    for i in range(400):
+        fields = conn.request_fields(DP + ("Allocate" if i % 2 else "GetPreferredAllocation"), 9.9 - i * 1e-4)
+        block = enc.encode(fields)
+        assert dec.decode(block) == fields
+    assert enc.evictions > 0 and enc.inserts > 400
+    # a first block decodes natively too (only static / new-name literals)
+    fresh = gp.GoHpackEncoder()
+    f0 = conn.request_fields(DP + "Allocate", 10.0)
+    assert [(k.decode(), v.decode()) for k, v in core().hpack_decode_block(fresh.encode(f0))] == f0
+
+
+def test_encode_duration_matches_grpcutil():
+    assert gp.encode_duration(10.0) == "10000000u"
+    assert gp.encode_duration(0.0999999) == "99999900n"
+    assert gp.encode_duration(3600 * 100) == "360000S" and gp.encode_duration(200e6) == "3333334M" and gp.encode_duration(0) == "0n"
+
+
+# ------------------------------------------------------------------ grpc-go client -> native server
+
+class GoKubelet:
+    """kubelet's Registration server as grpc-go runs it, on <dir>/kubelet.sock."""
+
+    def __init__(self, kdir, config=None):
+        os.makedirs(kdir, exist_ok=True)
+        self.registrations = []
+
+        def register(msg):
+            self.registrations.append(pb.RegisterRequest.FromString(msg))
+            return 0, "", b""
+
+        self.srv = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {REGISTER: register}, config)
+
+    def close(self):
+        self.srv.close()
+
+
+def _daemon(kdir, fi, *extra):
+    return subprocess.Popen([EXE, "-kubelet_dir", kdir, "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                             "-exporter_socket", "", *extra], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                            text=True)
+
+
+def _stop(p):
+    if p.poll() is None:
+        p.send_signal(signal.SIGTERM)
+    try:
+        _, err = p.communicate(timeout=20)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        _, err = p.communicate()
+    return p.returncode, err
+
+
+@pytest.fixture
+def daemon_node(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    kub = GoKubelet(kdir)
+    p = _daemon(kdir, fi)
+    try:
+        assert _wait(lambda: kub.registrations, 20), "the daemon never registered"
+        yield kdir, kub, p
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+        assert rc == 0, err[-2000:]
+
+
+@pytest.mark.parametrize("cfg", [
+    gp.GoServerConfig(continuation_chunk=2),
+    gp.GoServerConfig(ping_before_response=True, settings_after_headers=[(gp.S_INITIAL_WINDOW_SIZE, 1 << 20)]),
+    gp.GoServerConfig(graceful_goaway=True),
+    gp.GoServerConfig(refuse_calls=2),          # REFUSED_STREAM: the daemon retries (100 ms, doubling)
+    gp.GoServerConfig(max_concurrent_streams=1, initial_window=16384),
+], ids=["continuation", "ping+settings", "graceful-goaway", "refused-twice", "tight-limits"])
+def test_daemon_registers_through_grpc_go_server_variants(tmp_path, cfg):
+    """The daemon's native client (Register) against what a grpc-go
+    Registration server may send; runs under ASan/TSan in CI with
+    MI355X_NATIVE_DAEMON_EXE pointing at the sanitizer builds."""
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    kub = GoKubelet(kdir, cfg)
+    p = _daemon(kdir, fi)
+    try:
+        assert _wait(lambda: kub.registrations, 20), "never registered"
+        assert kub.srv.violations == []
+        # and the plugin socket then serves a grpc-go client
+        c = gp.GoClientConn(os.path.join(kdir, "amd.com_gpu"))
+        try:
+            assert c.unary(DP + "GetDevicePluginOptions", b"", 3.0)[0] == 0
+        finally:
+            c.close()
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+    assert rc == 0, err[-2000:]
+    if cfg.refuse_calls:
+        assert kub.srv.refused == 2 and "REFUSED_STREAM" in err
+
+
+def _pref_req(ids, size):
+    r = pb.PreferredAllocationRequest()
+    r.container_requests.add(available_deviceIDs=ids, allocation_size=size)
+    return r.SerializeToString()
+
+
+def test_native_client_registers_like_grpc_go_expects(daemon_node):
+    """Register through the native client against a grpc-go server: request
+    headers, one message, SETTINGS exchange, no protocol violations."""
+    kdir, kub, _ = daemon_node
+    reg = kub.registrations[0]
+    assert reg.version == "v1beta1" and reg.resource_name == "amd.com/gpu" and reg.endpoint == "amd.com_gpu"
+    hdr = dict(kub.srv.calls[0].headers)
+    assert hdr[":method"] == "POST" and hdr[":path"] == REGISTER and hdr["te"] == "trailers"
+    assert hdr["content-type"] == "application/grpc"
+    assert kub.srv.violations == []
+    # the client acknowledged the server preface SETTINGS and sent its own first
+    assert ("SETTINGS", 1, 0) in kub.srv.frames and kub.srv.frames[0][0] == "SETTINGS"
+
+
+def test_grpc_go_client_session_against_the_daemon(daemon_node):
+    kdir, kub, _ = daemon_node
+    c = gp.GoClientConn(os.path.join(kdir, "amd.com_gpu"))
+    try:
+        # server preface acknowledged; options with a deadline (grpc-timeout)
+        code, _, body = c.unary(DP + "GetDevicePluginOptions", b"", timeout_s=10.0)
+        assert code == 0 and pb.DevicePluginOptions.FromString(body).get_preferred_allocation_available
+        # ListAndWatch: no deadline (kubelet's stream context)
+        lw = c.start_call(DP + "ListAndWatch", b"")
+        first = pb.ListAndWatchResponse.FromString(c.next_message(lw))
+        ids = sorted(d.ID for d in first.devices)
+        assert len(ids) == 8
+        # the first DATA of a sample triggers grpc-go's BDP ping, after a connection WINDOW_UPDATE
+        assert c.wait(lambda: gp.BDP_PING in c.ping_acks, 5)
+        sent = [n for n, _, _ in c.sent]
+        assert sent.index("PING") > 0 and "WINDOW_UPDATE" in sent[:sent.index("PING")]
+        # hundreds of admission RPCs on one connection: the dynamic table fills and evicts
+        for i in range(300):
+            size = 1 + i % 8
+            code, msg, body = c.unary(DP + "GetPreferredAllocation", _pref_req(ids, size), timeout_s=10.0 - i * 1e-3)
+            assert code == 0, msg
+            got = list(pb.PreferredAllocationResponse.FromString(body).container_responses[0].deviceIDs)
+            assert len(got) == size
+            a = pb.AllocateRequest()
+            a.container_requests.add(devices_ids=got)
+            code, msg, body = c.unary(DP + "Allocate", a.SerializeToString(), timeout_s=10.0)
+            assert code == 0, msg
+            assert pb.AllocateResponse.FromString(body).container_responses[0].devices
+        assert c.enc.evictions > 0
+        # BDP growth: connection WINDOW_UPDATE + SETTINGS{INITIAL_WINDOW_SIZE} mid-connection
+        acks = c.settings_acks
+        c.update_flow_control(1 << 20)
+        assert c.wait(lambda: c.settings_acks > acks, 5), "SETTINGS change not acknowledged"
+        code, _, _ = c.unary(DP + "GetDevicePluginOptions", b"")
+        assert code == 0
+        # concurrent streams, answered in any order
+        sids = [c.start_call(DP + "GetPreferredAllocation", _pref_req(ids, k % 4 + 1), 5.0) for k in range(16)]
+        assert c.wait(lambda: all(c.streams[s].ended for s in sids), 10)
+        assert all(c.streams[s].status()[0] == 0 for s in sids)
+        # a client PING mid-session
+        c.ping(b"12345678")
+        assert c.wait(lambda: b"12345678" in c.ping_acks, 5)
+        # metadata large enough for HEADERS + CONTINUATION
+        big = [(f"x-md-{k}", "v" * 900) for k in range(30)]
+        sid = c.start_call(DP + "GetDevicePluginOptions", b"", 5.0, metadata=big)
+        assert "CONTINUATION" in [n for n, _, s in c.sent if s == sid]
+        assert c.wait(lambda: c.streams[sid].ended, 5) and c.streams[sid].status()[0] == 0
+        # kubelet drops ListAndWatch (context cancel) and opens it again on the same connection
+        c.cancel(lw)
+        lw2 = c.start_call(DP + "ListAndWatch", b"")
+        again = pb.ListAndWatchResponse.FromString(c.next_message(lw2))
+        assert sorted(d.ID for d in again.devices) == ids
+        # nothing the server objected to
+        assert c.goaway is None and all(c.streams[s].rst_code is None for s in c.streams if s != lw)
+    finally:
+        c.close()
+
+
+def test_two_grpc_go_connections_and_a_restart_of_the_list_stream(daemon_node):
+    """kubelet re-dials after its own restart: a fresh connection (fresh HPACK
+    state) next to a stale one; both answered."""
+    kdir, _, _ = daemon_node
+    a = gp.GoClientConn(os.path.join(kdir, "amd.com_gpu"))
+    b = gp.GoClientConn(os.path.join(kdir, "amd.com_gpu"))
+    try:
+        for c in (a, b, a, b):
+            code, _, body = c.unary(DP + "GetDevicePluginOptions", b"", 3.0)
+            assert code == 0
+        la = a.start_call(DP + "ListAndWatch", b"")
+        lb = b.start_call(DP + "ListAndWatch", b"")
+        assert a.next_message(la) and b.next_message(lb)
+    finally:
+        a.close()
+        b.close()
+
+
+# ------------------------------------------------------------------ native client -> grpc-go server
+
+ECHO = "/test.Echo/Call"
+
+
+def _echo(msg):
+    return 0, "", msg
+
+
+def _client(path, timeout=5.0):
+    c = core().GrpcClient()
+    assert c.connect(path, timeout) == ""
+    return c
+
+
+@pytest.mark.parametrize("cfg,nbytes", [
+    (gp.GoServerConfig(), 10),
+    (gp.GoServerConfig(continuation_chunk=3), 10),                  # every header block in 3-byte fragments
+    (gp.GoServerConfig(ping_before_response=True), 10),
+    (gp.GoServerConfig(settings_after_headers=[(gp.S_INITIAL_WINDOW_SIZE, 1 << 20),
+                                               (gp.S_MAX_FRAME_SIZE, 1 << 20)]), 10),
+    (gp.GoServerConfig(graceful_goaway=True), 10),
+    (gp.GoServerConfig(max_concurrent_streams=1), 10),
+    (gp.GoServerConfig(), 300_000),                                 # larger than the default windows
+    (gp.GoServerConfig(initial_window=16384), 100_000),             # RFC-legal window below grpc-go's minimum
+    (gp.GoServerConfig(continuation_chunk=1, initial_window=16384), 70_000),
+], ids=["plain", "continuation", "server-ping", "settings-mid-call", "graceful-goaway", "one-stream",
+        "large-request", "small-window", "continuation+small-window"])
+def test_native_client_against_grpc_go_server(tmp_path, cfg, nbytes):
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, cfg) as srv:
+        c = _client(path)
+        payload = bytes(range(256)) * (nbytes // 256) + b"x" * (nbytes % 256)
+        status, msg, body = c.unary(ECHO, payload, 10.0)
+        assert (status, msg) == (0, ""), msg
+        assert body == payload
+        if cfg.graceful_goaway:
+            # answered, then the connection is draining: a new call needs a new connection
+            assert c.going_away
+            assert c.unary(ECHO, b"again", 2.0)[0] == -1
+            c = _client(path)
+        for k in range(5):   # the connection (and both HPACK tables) stay in step
+            if c.going_away:  # this server drains after every call
+                c = _client(path)
+            assert c.unary(ECHO, b"m%d" % k, 5.0) == (0, "", b"m%d" % k)
+        assert srv.violations == []
+        c.close()
+
+
+def test_native_client_too_many_pings_goaway(tmp_path):
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(too_many_pings=True)):
+        c = _client(path)
+        t0 = time.monotonic()
+        status, msg, _ = c.unary(ECHO, b"x", 10.0)
+        assert status == -1 and "ENHANCE_YOUR_CALM" in msg and "too_many_pings" in msg
+        assert time.monotonic() - t0 < 2.0 and not c.connected
+
+
+def test_native_client_refused_stream_keeps_the_connection(tmp_path):
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(refuse_calls=1)) as srv:
+        c = _client(path)
+        status, msg, _ = c.unary(ECHO, b"x", 5.0)
+        assert status == 14 and "REFUSED_STREAM" in msg        # UNAVAILABLE, retryable
+        assert c.connected and c.unary(ECHO, b"y", 5.0) == (0, "", b"y")
+        assert srv.connections == 1
+
+
+def test_native_client_http_error_status(tmp_path):
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(http_status=503)):
+        status, msg, _ = _client(path).unary(ECHO, b"x", 5.0)
+        assert status == 14 and "503" in msg
+
+
+def test_native_client_unknown_method_and_grpc_error(tmp_path):
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: lambda m: (9, "precondition: ünïcode", b"")}):
+        c = _client(path)
+        assert c.unary("/nope/Nope", b"", 5.0)[0] == 12
+        status, msg, _ = c.unary(ECHO, b"", 5.0)
+        assert status == 9 and msg.startswith("precondition")
+
+
+def test_native_client_deadline_and_abort_against_a_silent_server(tmp_path):
+    """An exporter that accepts and never answers: the call ends at its
+    deadline, or at once when the abort fd (a daemon's signal pipe) fires."""
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(never_answer=True)):
+        c = _client(path)
+        t0 = time.monotonic()
+        status, msg, _ = c.unary(ECHO, b"x", 0.3)
+        dt = time.monotonic() - t0
+        assert status == -1 and "deadline" in msg and 0.25 < dt < 1.5
+        r, w = os.pipe()
+        try:
+            c = _client(path)
+            c.set_abort_fd(r)
+            threading.Timer(0.2, lambda: os.write(w, b"x")).start()
+            t0 = time.monotonic()
+            status, msg, _ = c.unary(ECHO, b"x", 30.0)
+            assert status == -1 and msg == "interrupted" and time.monotonic() - t0 < 2.0
+        finally:
+            os.close(r)
+            os.close(w)
+
+
+def test_native_client_survives_signals_during_a_call(tmp_path):
+    """EINTR in the wait (a signal handler without SA_RESTART) re-polls with
+    the time left instead of falling into a blocking read."""
+    path = str(tmp_path / "go.sock")
+    old = signal.signal(signal.SIGUSR1, lambda *a: None)
+    try:
+        with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(never_answer=True)):
+            c = _client(path)
+            tid = threading.get_ident()
+            stop = threading.Event()
+
+            def pester():
+                while not stop.wait(0.02):
+                    signal.pthread_kill(tid, signal.SIGUSR1)
+
+            t = threading.Thread(target=pester)
+            t.start()
+            t0 = time.monotonic()
+            try:
+                status, msg, _ = c.unary(ECHO, b"x", 0.5)
+            finally:
+                stop.set()
+                t.join()
+            assert status == -1 and "deadline" in msg and time.monotonic() - t0 < 2.0
+    finally:
+        signal.signal(signal.SIGUSR1, old)
+
+
+# ------------------------------------------------------------------ native server conformance (RFC 7540)
+
+def _raw(path, first_settings=True):
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    s.connect(path)
+    s.sendall(gp.PREFACE + (gp.frame(gp.SETTINGS, 0, 0) if first_settings else b""))
+    return s, gp.FrameReader(s)
+
+
+def _goaway_code(rd, timeout=5.0):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        try:
+            f = rd.read(0.2)
+        except EOFError:
+            return None
+        if f and f[0] == gp.GOAWAY:
+            return struct.unpack(">I", f[3][4:8])[0]
+    return None
+
+
+def _open_lw(s, sid=1):
+    enc = gp.GoHpackEncoder()
+    block = enc.encode([(":method", "POST"), (":scheme", "http"), (":path", DP + "ListAndWatch"),
+                        (":authority", "localhost"), ("content-type", "application/grpc"), ("te", "trailers")])
+    s.sendall(gp.frame(gp.HEADERS, gp.END_HEADERS, sid, block) +
+              gp.frame(gp.DATA, gp.END_STREAM, sid, gp.grpc_message(b"")))
+
+
+@pytest.mark.parametrize("case,want", [
+    ("no-settings-first", gp.PROTOCOL_ERROR),
+    ("rst-idle", gp.PROTOCOL_ERROR),
+    ("window-update-idle", gp.PROTOCOL_ERROR),
+    ("continuation-after-complete-headers", gp.PROTOCOL_ERROR),
+    ("settings-window-overflow", gp.FLOW_CONTROL_ERROR),
+    ("enable-push-2", gp.PROTOCOL_ERROR),
+])
+def test_native_server_connection_errors(daemon_node, case, want):
+    kdir, _, _ = daemon_node
+    path = os.path.join(kdir, "amd.com_gpu")
+    s, rd = _raw(path, first_settings=case != "no-settings-first")
+    try:
+        if case == "no-settings-first":
+            s.sendall(gp.frame(gp.PING, 0, 0, b"\0" * 8))
+        elif case == "rst-idle":
+            s.sendall(gp.frame(gp.RST_STREAM, 0, 7, struct.pack(">I", gp.CANCEL)))
+        elif case == "window-update-idle":
+            s.sendall(gp.frame(gp.WINDOW_UPDATE, 0, 9, struct.pack(">I", 100)))
+        elif case == "continuation-after-complete-headers":
+            _open_lw(s)
+            s.sendall(gp.frame(gp.CONTINUATION, gp.END_HEADERS, 1, b"\x82"))
+        elif case == "settings-window-overflow":
+            _open_lw(s)
+            s.sendall(gp.frame(gp.WINDOW_UPDATE, 0, 1, struct.pack(">I", gp.MAX_WINDOW - 65535)) +
+                      gp.frame(gp.SETTINGS, 0, 0, gp.settings_payload([(gp.S_INITIAL_WINDOW_SIZE, 70000)])))
+        elif case == "enable-push-2":
+            s.sendall(gp.frame(gp.SETTINGS, 0, 0, gp.settings_payload([(gp.S_ENABLE_PUSH, 2)])))
+        assert _goaway_code(rd) == want
+    finally:
+        s.close()
+    # the server keeps serving other connections
+    c = gp.GoClientConn(path)
+    try:
+        assert c.unary(DP + "GetDevicePluginOptions", b"", 3.0)[0] == 0
+    finally:
+        c.close()
+
+
+# ------------------------------------------------------------------ transport watchdog
+
+def _py_plugin(tmp_path, watchdog_s):
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+    from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+    from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
+    fi = make_mi355x_node(tmp_path / "n")
+    impl = ContainerImpl("single", str(fi.sysfs), HealthConfig(exporter_socket=None))
+    pdir = str(tmp_path / "dp")
+    return pdir, PluginManager(impl, ManagerConfig(plugin_dir=pdir, handle_signals=False,
+                                                   grpc_watchdog_s=watchdog_s))
+
+
+async def _until(cond, timeout=10.0):
+    import asyncio
+    deadline = time.monotonic() + timeout
+    while not cond():
+        if time.monotonic() > deadline:
+            raise TimeoutError("condition not reached")
+        await asyncio.sleep(0.02)
+
+
+def test_python_watchdog_reserves_on_aio_when_kubelet_never_lists(tmp_path):
+    """Register acknowledged but kubelet never opens ListAndWatch (it cannot
+    complete calls on the native transport): after -grpc_watchdog the
+    resource is served by grpc.aio and registered again."""
+    import asyncio
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+    pdir, mgr = _py_plugin(tmp_path, 0.5)
+
+    async def go():
+        k = FakeKubelet(pdir)
+        k.open_list_and_watch = False
+        await k.start()
+        task = asyncio.create_task(mgr.run())
+        try:
+            await _until(lambda: len(k.registrations) >= 1)
+            p = mgr.plugins["gpu"]
+            assert p.native is not None
+            t0 = time.monotonic()
+            await _until(lambda: len(k.registrations) >= 2)
+            assert 0.3 < time.monotonic() - t0 < 5.0
+            assert p.native is None and p.server is not None and "no ListAndWatch" in p.native_failed
+            k.open_list_and_watch = True
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=10)
+            assert len(st.devices) == 8
+            # sticky: a kubelet restart re-serves on grpc.aio too
+            await k.restart()
+            await _until(lambda: len(k.registrations) >= 3)
+            assert p.native is None and p.server is not None
+        finally:
+            mgr.request_stop()
+            await asyncio.wait_for(task, 20)
+            await k.stop()
+
+    asyncio.run(asyncio.wait_for(go(), 60))
+
+
+def test_python_watchdog_protocol_errors_move_to_aio(tmp_path):
+    import asyncio
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+    pdir, mgr = _py_plugin(tmp_path, 30.0)
+
+    async def go():
+        k = FakeKubelet(pdir)
+        await k.start()
+        task = asyncio.create_task(mgr.run())
+        try:
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=10)
+            p = mgr.plugins["gpu"]
+            assert p.native is not None and p.native_failed is None
+            await asyncio.sleep(0.5)    # a healthy session raises nothing
+            assert p.native is not None
+            s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            s.connect(p.socket)
+            s.sendall(b"GET / HTTP/1.1\r\nHost: x\r\n\r\n")   # not HTTP/2: a protocol error
+            s.settimeout(5)
+            await asyncio.to_thread(lambda: [None for _ in iter(lambda: s.recv(4096), b"")])   # until it hangs up
+            s.close()
+            await _until(lambda: len(k.registrations) >= 2)
+            assert p.native is None and "protocol error" in p.native_failed
+            await _until(lambda: k.resources["amd.com/gpu"].updates >= 1 and k.resources["amd.com/gpu"].devices)
+        finally:
+            mgr.request_stop()
+            await asyncio.wait_for(task, 20)
+            await k.stop()
+
+    asyncio.run(asyncio.wait_for(go(), 60))
