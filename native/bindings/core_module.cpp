@@ -15,7 +15,8 @@
 namespace py = pybind11;
 using namespace mi355x;
 
-void bind_rpc(py::module_& m);  // rpc_module.cpp
+void bind_rpc(py::module_& m);     // rpc_module.cpp
+void bind_health(py::module_& m);  // health_module.cpp
 
 namespace {
 
@@ -410,4 +411,5 @@ PYBIND11_MODULE(_native, m) {
       .def("read_events", &DirWatcher::read_events)
       .def("close", &DirWatcher::close);
   bind_rpc(m);
+  bind_health(m);
 }

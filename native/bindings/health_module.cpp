@@ -1,0 +1,134 @@
+// pybind11 bindings of the native health engine (mi355x/health_engine.h): the
+// policy the native daemon runs, driven from the tests with the same stub
+// probes and fixtures as the Python monitor's tests.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "mi355x/gpu_discovery.h"
+#include "mi355x/health_engine.h"
+#include "mi355x/kfd_topology.h"
+
+namespace py = pybind11;
+using namespace mi355x;
+
+namespace {
+
+class PyHealthEngine {
+ public:
+  PyHealthEngine(const std::string& sysfs_root, const py::dict& opts) {
+    health::Config c;
+    c.sysfs_root = sysfs_root;
+    auto get = [&](const char* k) -> py::object {
+      if (opts.contains(k)) return py::object(opts[k]);
+      return py::none();
+    };
+    auto s = [&](const char* k, std::string* out) {
+      if (auto v = get(k); !v.is_none()) *out = v.cast<std::string>();
+    };
+    auto d = [&](const char* k, double* out) {
+      if (auto v = get(k); !v.is_none()) *out = v.cast<double>();
+    };
+    auto i = [&](const char* k, int* out) {
+      if (auto v = get(k); !v.is_none()) *out = v.cast<int>();
+    };
+    auto b = [&](const char* k, bool* out) {
+      if (auto v = get(k); !v.is_none()) *out = v.cast<bool>();
+    };
+    s("dev_root", &c.dev_root);
+    s("exporter_socket", &c.exporter_socket);
+    d("exporter_timeout_s", &c.exporter_timeout_s);
+    b("liveness", &c.liveness);
+    i("fail_threshold", &c.fail_threshold);
+    i("recover_threshold", &c.recover_threshold);
+    d("busy_grace_s", &c.busy_grace_s);
+    d("unknown_busy_grace_s", &c.unknown_busy_grace_s);
+    b("corroborate", &c.corroborate);
+    i("idle_sweeps", &c.idle_sweeps);
+    i("crowded_procs", &c.crowded_procs);
+    i("crowded_release_sweeps", &c.crowded_release_sweeps);
+    b("smi_ecc", &c.smi_ecc);
+    b("smi_events", &c.smi_events);
+    s("probe_exe", &c.prober.exe);
+    d("probe_timeout_s", &c.prober.timeout_s);
+    i("probe_iters", &c.prober.iters);
+    i("probe_max_parallel", &c.prober.max_parallel);
+    b("persistent", &c.prober.persistent);
+    b("keep_queues", &c.prober.keep_queues);
+    s("kfd_proc_dir", &c.prober.kfd_proc_dir);
+    if (auto v = get("argv_prefix"); !v.is_none()) c.prober.argv_prefix = v.cast<std::vector<std::string>>();
+    if (auto v = get("extra_env"); !v.is_none())
+      for (auto& [k, val] : v.cast<std::map<std::string, std::string>>()) c.prober.extra_env.emplace_back(k, val);
+    const KfdTopology topo = KfdTopology::load_sysfs(sysfs_root);
+    DiscoveryResult res = discover_gpus(sysfs_root, topo);
+    eng_ = std::make_unique<health::Engine>(std::move(res.devices), topo, c);
+  }
+
+  bool sweep() {
+    py::gil_scoped_release nogil;
+    return eng_->sweep();
+  }
+  py::dict snapshot() const {
+    py::dict out;
+    for (const auto& [id, v] : eng_->snapshot()) out[py::str(id)] = py::make_tuple(v.healthy, v.reasons);
+    return out;
+  }
+  py::dict stats() {
+    py::dict d;
+    d["sweeps"] = eng_->sweeps();
+    d["identity_remaps"] = eng_->identity_remaps();
+    d["crowded_skips"] = eng_->crowded_skips();
+    d["busy_state_known"] = eng_->busy_state_known();
+    d["last_sweep_ms"] = eng_->last_sweep_ms();
+    d["version"] = eng_->version();
+    if (auto* p = eng_->prober()) {
+      d["server_starts"] = p->server_starts;
+      d["server_restarts"] = p->server_restarts;
+      d["fallbacks"] = p->fallbacks;
+      d["server_running"] = p->server_running();
+    }
+    return d;
+  }
+  void set_activity(std::optional<std::map<std::string, int>> a) {
+    if (!a) eng_->activity_source = nullptr;
+    else eng_->activity_source = [a] { return *a; };
+  }
+  void set_exporter(std::optional<std::map<std::string, bool>> h) {
+    if (!h) eng_->exporter_source = nullptr;
+    else eng_->exporter_source = [h] { return *h; };
+  }
+  std::map<std::string, int> ordinals() { return eng_->ordinals(); }
+  void close() {
+    py::gil_scoped_release nogil;
+    eng_->close();
+  }
+
+ private:
+  std::unique_ptr<health::Engine> eng_;
+};
+
+}  // namespace
+
+void bind_health(py::module_& m) {
+  py::class_<PyHealthEngine>(m, "HealthEngine",
+                             "native per-device health engine (the native daemon's); options as health::Config")
+      .def(py::init<const std::string&, const py::dict&>(), py::arg("sysfs_root"), py::arg("options") = py::dict())
+      .def("sweep", &PyHealthEngine::sweep, "one sweep; True when a verdict changed")
+      .def("snapshot", &PyHealthEngine::snapshot, "device id -> (healthy, reasons)")
+      .def("stats", &PyHealthEngine::stats)
+      .def("ordinals", &PyHealthEngine::ordinals)
+      .def("set_activity", &PyHealthEngine::set_activity, py::arg("activity"),
+           "bdf -> GFX activity % used instead of amd-smi (None = amd-smi)")
+      .def("set_exporter", &PyHealthEngine::set_exporter, py::arg("health"),
+           "bdf -> healthy used instead of the exporter socket (None = socket)")
+      .def("close", &PyHealthEngine::close);
+  m.def("exporter_list", [](const std::string& socket, double timeout_s) {
+    std::string err;
+    std::map<std::string, bool> h;
+    {
+      py::gil_scoped_release nogil;
+      h = health::exporter_list(socket, timeout_s, -1, &err);
+    }
+    return py::make_tuple(h, err);
+  });
+}

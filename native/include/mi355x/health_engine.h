@@ -1,0 +1,216 @@
+// Per-device health for the container (KFD) mode, natively: the same sources
+// and policy as the Python health monitor (rocm_k8s_device_plugin_amd/health/
+// monitor.py, liveness.py), so the interpreter-free daemon runs the north-star
+// health path.
+//
+// Reference: a node-global verdict ("Healthy" if any kfd node is a live GPU)
+// copied onto every device and overridden per PCI BDF by the metrics exporter
+// (internal/pkg/amdgpu/amdgpu.go:322-345,865-974; internal/pkg/exporter/
+// health.go:41-79). Here every device gets its own verdict; it is Healthy only
+// if every available source agrees:
+//
+//   kfd       the device's own kfd node still exists and is a live GPU node
+//   exporter  metricssvc.MetricsService/List, per BDF, applied to every
+//             partition of that BDF (10 s deadline, never on the control loop)
+//   liveness  the gfx950 MFMA probe on that exact ROCr agent, from a persistent
+//             `mi355x-liveness-probe --serve [--keep]` child: nonce-checked,
+//             identity-checked (the replying agent's PCI location must be the
+//             device's), hysteresis (fail / recover thresholds), a busy grace
+//             for probes queued behind a tenant's kernel (kfd process list;
+//             shorter when it is unreadable) that ends early when amd-smi
+//             reports 0% GFX activity, crowded GPUs skipped (the server steps
+//             off them), server failures isolated per device in fresh
+//             processes, and server-only failures confirmed in a fresh
+//             process before they count
+//   amd-smi   a rise of the uncorrectable ECC count; a gpu_pre_reset event
+//             keeps the device Unhealthy until its gpu_post_reset
+//
+// sweep() blocks (probes, exporter, amd-smi) and is meant for a worker
+// thread; snapshot() may be called from any thread.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <set>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "mi355x/gpu_discovery.h"
+#include "mi355x/kfd_topology.h"
+
+namespace mi355x {
+class SmiEventWatcher;
+}
+
+namespace mi355x::health {
+
+struct ProbeOutcome {
+  bool ok = false;
+  bool pending = false;    // the dispatch is still queued (kept slot) or missed its deadline on a busy GPU
+  std::string reason;
+  double latency_ms = 0;
+  int kfd_node_id = -1;    // identity of the agent that answered (-1 / "" = not reported)
+  std::string pci_bus_id;  // dddd:bb:dd.f
+};
+
+struct ProberConfig {
+  std::vector<std::string> argv_prefix;  // e.g. {"python3"} for a scripted stand-in
+  std::string exe;                       // mi355x-liveness-probe
+  double timeout_s = 10.0;
+  int iters = 4;
+  int max_parallel = 8;
+  bool persistent = true;                // one --serve child, else a process per device per sweep
+  bool keep_queues = true;               // --serve --keep
+  std::vector<std::pair<std::string, std::string>> extra_env;
+  std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";
+};
+
+// The probe processes (LivenessProber in health/liveness.py).
+class LivenessProber {
+ public:
+  explicit LivenessProber(ProberConfig cfg);
+  ~LivenessProber();
+  LivenessProber(const LivenessProber&) = delete;
+  LivenessProber& operator=(const LivenessProber&) = delete;
+
+  // host ROCr ordinal -> outcome. `busy`: ordinals whose GPU runs other
+  // processes' queues (a pending dispatch there is not re-probed).
+  std::map<int, ProbeOutcome> probe(const std::vector<int>& ordinals, const std::set<int>& busy = {},
+                                    const std::string& kind = "probe");
+  // one device in a fresh process (ROCR_VISIBLE_DEVICES=<ordinal>)
+  ProbeOutcome probe_ordinal(int ordinal, const std::string& kind = "probe");
+  // restrict the server to these host ordinals (nullopt = all); a change restarts it
+  void set_visible(std::optional<std::vector<int>> ordinals);
+  void close();
+  bool server_running() const;
+  // the running server's kfd proc entry names (empty while ambiguous / unknown)
+  std::set<std::string> own_kfd_entries(const std::set<int64_t>& gpu_ids);
+  // a readable fd ends every wait at once (shutdown)
+  void set_abort_fd(int fd) { abort_fd_ = fd; }
+
+  int server_starts = 0, server_restarts = 0, fallbacks = 0, sweeps = 0;
+  const ProberConfig& config() const { return cfg_; }
+
+ private:
+  struct Server;
+  std::map<int, ProbeOutcome> probe_server(const std::vector<int>& uniq, const std::string& kind, std::string* err);
+  std::map<int, ProbeOutcome> spawn_all(const std::vector<int>& ords, const std::string& kind);
+  ProberConfig cfg_;
+  std::unique_ptr<Server> server_;
+  int backoff_ = 0;
+  std::map<int, uint32_t> pending_nonce_;
+  std::optional<std::vector<int>> visible_, server_visible_;
+  std::set<std::string> own_kfd_;
+  int abort_fd_ = -1;
+};
+
+struct Config {
+  std::string sysfs_root = "/sys";
+  std::string dev_root = "/dev";
+  std::string exporter_socket;           // "" = off
+  double exporter_timeout_s = 10.0;
+  bool liveness = false;
+  ProberConfig prober;
+  int fail_threshold = 2;
+  int recover_threshold = 1;
+  double busy_grace_s = 300.0;
+  double unknown_busy_grace_s = 30.0;
+  bool corroborate = true;
+  int idle_sweeps = 2;
+  int crowded_procs = 7;                 // 0 = off
+  int crowded_release_sweeps = 5;
+  bool smi_ecc = false;
+  bool smi_events = false;
+};
+
+struct Verdict {
+  bool healthy = true;
+  std::vector<std::string> reasons;
+};
+
+class Engine {
+ public:
+  Engine(std::vector<GpuDevice> devices, const KfdTopology& topo, Config cfg);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  // One sweep; true when any device's health changed. Blocking.
+  bool sweep();
+  std::map<std::string, Verdict> snapshot() const;
+  uint64_t version() const;
+  void set_abort_fd(int fd);
+  void close();
+
+  // device id -> host ROCr ordinal (positional over accessible kfd GPU nodes)
+  const std::map<std::string, int>& ordinals();
+  // sources a test (or another collector) can replace
+  std::function<std::map<std::string, int>()> activity_source;       // bdf -> GFX activity %, -1 unknown
+  std::function<std::map<std::string, bool>()> exporter_source;      // bdf -> healthy
+
+  LivenessProber* prober() { return prober_.get(); }
+  uint64_t sweeps() const { return sweeps_; }
+  uint64_t identity_remaps() const { return identity_remaps_; }
+  uint64_t crowded_skips() const { return crowded_skips_; }
+  bool busy_state_known() const { return busy_known_; }
+  double last_sweep_ms() const { return last_sweep_ms_; }
+
+ private:
+  struct Track {
+    int fails = 0, oks = 0;
+    bool live = true;
+    std::string last_reason;
+    double pending_since = -1;  // monotonic seconds of the first inconclusive probe
+    int idle_pending = 0;
+  };
+  std::map<std::string, std::string> kfd_verdicts() const;
+  std::map<std::string, bool> exporter_health() const;
+  std::map<std::string, int> gfx_activity();
+  // kfd gpu_id -> (other processes with queues, their queues); false when unreadable
+  bool kfd_load(const std::set<std::string>& exclude, std::map<int64_t, std::pair<int, int>>* out) const;
+  int64_t gpu_id(const std::string& dev) const;
+  std::map<std::string, ProbeOutcome> verify_identity(const std::map<std::string, int>& ords,
+                                                      const std::map<std::string, ProbeOutcome>& outcomes);
+  bool identity_matches(const GpuDevice& d, const ProbeOutcome& o) const;
+  const GpuDevice* dev(const std::string& id) const;
+
+  std::vector<GpuDevice> devices_;
+  std::map<std::string, size_t> by_id_;
+  KfdTopology topo_;
+  Config cfg_;
+  std::unique_ptr<LivenessProber> prober_;
+  std::optional<std::map<std::string, int>> ordinals_;
+  std::map<std::string, Track> track_;
+  std::map<std::string, uint64_t> ecc_;
+  std::map<std::string, std::string> resetting_;  // bdf -> pre-reset message
+  std::map<std::string, int> crowded_;            // device -> uncrowded sweeps since it got crowded
+  std::map<int64_t, std::pair<int, int>> load_;
+  std::unique_ptr<mi355x::SmiEventWatcher> events_;
+  bool events_started_ = false;
+  bool smi_held_ = false;
+  bool busy_known_ = true;
+  uint64_t sweeps_ = 0, identity_remaps_ = 0, crowded_skips_ = 0;
+  double last_sweep_ms_ = 0;
+  int abort_fd_ = -1;
+
+  mutable std::mutex mu_;  // snapshot_ / version_
+  std::map<std::string, Verdict> snapshot_;
+  uint64_t version_ = 0;
+};
+
+// bdf -> healthy from metricssvc.MetricsService/List on `socket` ({} when
+// unavailable); `abort_fd` ends the wait early.
+std::map<std::string, bool> exporter_list(const std::string& socket, double timeout_s, int abort_fd = -1,
+                                          std::string* error = nullptr);
+
+// device id -> host ROCr ordinal: position among kfd GPU nodes with a render
+// node the process can open (ROCr skips the others), in node-id order.
+std::map<std::string, int> hip_ordinals(const std::vector<GpuDevice>& devices, const KfdTopology& topo,
+                                        const std::string& dev_root);
+
+}  // namespace mi355x::health

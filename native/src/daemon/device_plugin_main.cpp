@@ -1,12 +1,17 @@
-// mi355x-device-plugin: the kubelet device plugin as one native process.
+// mi355x-device-plugin: the kubelet device plugin as one native process — the
+// primary entrypoint of this framework (docs/architecture.md).
 //
 // The reference ships its plugin as a single compiled binary
 // (cmd/k8s-device-plugin/main.go). This is the same thing built from the
 // framework's C++ core, with no interpreter in the process:
 //
 //   flags          -pulse, -driver_type, -resource_naming_strategy (main.go:50-75),
-//                  glog flags accepted; -kubelet_dir / -sysfs_root / -dev_root /
-//                  -exporter_socket / -send_every_pulse as in the Python CLI
+//                  glog's -v / -logtostderr / -alsologtostderr / -stderrthreshold /
+//                  -log_dir / -vmodule / -log_backtrace_at (mi355x/glog.h),
+//                  -kubelet_dir / -sysfs_root / -dev_root / -exporter_socket /
+//                  -send_every_pulse, the health flags of the Python CLI
+//                  (-liveness*, -smi_ecc, -smi_events), -allocator_extended_search,
+//                  -grpc_watchdog
 //   discovery      discover_gpus over the kfd topology (gpu_discovery.cpp)
 //   resources      single -> "gpu"; mixed -> "<compute>_<memory>"; heterogeneous
 //                  partitions with single is an error (amdgpu.go:68-88,122-162)
@@ -14,15 +19,21 @@
 //                  with the DevicePlugin service: hive-aware
 //                  GetPreferredAllocation (HiveAllocator), Allocate = /dev/kfd +
 //                  card + renderD per device (amdgpu.go:255-319), ListAndWatch
-//   registration   Register on kubelet.sock through the native client; again
-//                  whenever kubelet.sock is re-created (inotify on the plugin
-//                  directory, as the vendored dpm does with fsnotify)
-//   health         every -pulse: the device's kfd node is a live GPU, and the
-//                  metrics exporter's per-BDF verdict when its socket exists
-//                  (amdgpu.go:322-345, exporter/health.go:41-79); the list is
-//                  pushed when a verdict changes (or every pulse with
-//                  -send_every_pulse, the reference's behaviour)
-//   signals        SIGTERM / SIGINT stop the servers and remove the sockets
+//   registration   Register on kubelet.sock through the native client, on a
+//                  worker thread; again whenever kubelet.sock is replaced
+//                  (inotify on the plugin directory, as the vendored dpm does with
+//                  fsnotify; a 5 s stat poll as a safety net)
+//   health         every -pulse on a worker thread (health_engine.h): kfd node,
+//                  metrics exporter per BDF, the gfx950 MFMA liveness probe server
+//                  with hysteresis, busy grace, identity check and crowded
+//                  step-off, amd-smi ECC and reset events; the list is pushed when
+//                  a verdict changes (or every pulse with -send_every_pulse)
+//   watchdog       Register acknowledged but no ListAndWatch within
+//                  -grpc_watchdog s, or HTTP/2 protocol errors on the plugin
+//                  socket: exit 3 so the DaemonSet restarts the plugin instead of
+//                  leaving it registered and invisible
+//   signals        SIGTERM / SIGINT / SIGQUIT stop the servers, the probe server
+//                  and the workers, and remove the sockets
 //   passthrough    -driver_type vf-passthrough / pf-passthrough (amdgpu_sriov.go,
 //                  amdgpu_pf.go): one device per IOMMU group, Allocate =
 //                  /dev/vfio/<group> + /dev/vfio/vfio (mrw) and
@@ -30,35 +41,39 @@
 //                  health = driver present (+ exporter PF verdicts for VFs);
 //                  without -driver_type: container -> VF -> PF (main.go:106-115)
 //
-// The Python CLI (scripts/k8s-device-plugin) is the full-featured entrypoint:
-// the MFMA liveness probes and throughput checks, amd-smi, CDI, container
-// views, topology reloads, metrics and tracing. This binary is for nodes that
-// want the reference's feature set without Python.
+// The control loop never blocks on a peer: Register and every health source
+// run on worker threads with their own deadlines, and results come back
+// through a pipe the loop polls.
 #include <fcntl.h>
 #include <poll.h>
 #include <signal.h>
 #include <sys/inotify.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
-#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <ctime>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mi355x/allocator.h"
 #include "mi355x/constants.h"
 #include "mi355x/dir_watch.h"
 #include "mi355x/dp_service.h"
+#include "mi355x/glog.h"
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/grpc_server.h"
+#include "mi355x/health_engine.h"
 #include "mi355x/kfd_topology.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
@@ -67,22 +82,7 @@ namespace {
 
 using namespace mi355x;
 namespace pb = mi355x::rpc::pb;
-
-// ---- logging (glog line format) --------------------------------------------
-void logf(char sev, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-void logf(char sev, const char* fmt, ...) {
-  timespec ts{};
-  clock_gettime(CLOCK_REALTIME, &ts);
-  tm t{};
-  localtime_r(&ts.tv_sec, &t);
-  char msg[1024];
-  va_list ap;
-  va_start(ap, fmt);
-  std::vsnprintf(msg, sizeof(msg), fmt, ap);
-  va_end(ap);
-  std::fprintf(stderr, "%c%02d%02d %02d:%02d:%02d.%06ld %7d device_plugin_main.cpp] %s\n", sev, t.tm_mon + 1,
-               t.tm_mday, t.tm_hour, t.tm_min, t.tm_sec, ts.tv_nsec / 1000, static_cast<int>(getpid()), msg);
-}
+using Clock = std::chrono::steady_clock;
 
 // ---- flags ------------------------------------------------------------------
 struct Flags {
@@ -95,15 +95,64 @@ struct Flags {
   std::string exporter_socket = "/var/lib/amd-metrics-exporter/amdgpu_device_metrics_exporter_grpc.socket";
   bool send_every_pulse = false;
   double register_timeout_s = 10.0;
+  double grpc_watchdog_s = 10.0;
+  bool allocator_extended_search = false;
+  // health (same names and defaults as the Python CLI)
+  bool liveness = false;
+  std::string liveness_mode = "persistent";
+  bool liveness_keep_queues = true;
+  double liveness_timeout = 10.0;
+  int liveness_iters = 4;
+  int liveness_fail_threshold = 2;
+  int liveness_recover_threshold = 1;
+  double liveness_busy_grace = 300.0;
+  double liveness_unknown_busy_grace = 30.0;
+  bool liveness_corroborate = true;
+  int liveness_idle_sweeps = 2;
+  int liveness_crowded_procs = 7;
+  int liveness_crowded_release_sweeps = 5;
+  std::string liveness_probe;  // default: mi355x-liveness-probe next to this binary
+  bool smi_ecc = false;
+  bool smi_events = false;
+  glog::Options log;
 };
 
-bool parse_bool(const std::string& v) { return v.empty() || v == "1" || v == "true" || v == "True" || v == "t"; }
+// Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
+const std::set<std::string> kPythonOnly = {
+    "liveness_chip_sweep_every", "perf_check_every", "perf_mib", "perf_action", "perf_min_hbm_read_gbps",
+    "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "smi_xgmi", "metrics_port", "grpc_server",
+    "topology_view", "node_view", "device_list_strategy", "cdi_spec_dir", "trace_file", "dry_run",
+    "topology_watch", "log_format", "config"};
+
+bool parse_bool(const std::string& v, bool* out) {
+  if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
+  if (v == "0" || v == "false" || v == "False" || v == "FALSE" || v == "f" || v == "F") return *out = false, true;
+  return false;
+}
 
 // Go flag syntax: -name=value, -name value, --name, bare booleans.
 bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
-  static const std::set<std::string> kBool = {"send_every_pulse", "logtostderr", "alsologtostderr", "h", "help"};
-  static const std::set<std::string> kIgnoredValue = {"v", "stderrthreshold", "log_dir", "vmodule",
-                                                      "log_backtrace_at", "kubelet-url"};
+  std::map<std::string, bool*> bools = {
+      {"send_every_pulse", &f->send_every_pulse}, {"allocator_extended_search", &f->allocator_extended_search},
+      {"liveness", &f->liveness}, {"liveness_keep_queues", &f->liveness_keep_queues},
+      {"liveness_corroborate", &f->liveness_corroborate}, {"smi_ecc", &f->smi_ecc}, {"smi_events", &f->smi_events}};
+  std::map<std::string, int*> ints = {
+      {"pulse", &f->pulse}, {"liveness_iters", &f->liveness_iters},
+      {"liveness_fail_threshold", &f->liveness_fail_threshold},
+      {"liveness_recover_threshold", &f->liveness_recover_threshold},
+      {"liveness_idle_sweeps", &f->liveness_idle_sweeps}, {"liveness_crowded_procs", &f->liveness_crowded_procs},
+      {"liveness_crowded_release_sweeps", &f->liveness_crowded_release_sweeps}};
+  std::map<std::string, double*> floats = {
+      {"liveness_timeout", &f->liveness_timeout}, {"liveness_busy_grace", &f->liveness_busy_grace},
+      {"liveness_unknown_busy_grace", &f->liveness_unknown_busy_grace}, {"grpc_watchdog", &f->grpc_watchdog_s},
+      {"register_timeout", &f->register_timeout_s}};
+  std::map<std::string, std::string*> strs = {
+      {"driver_type", &f->driver_type}, {"resource_naming_strategy", &f->naming},
+      {"kubelet_dir", &f->kubelet_dir}, {"sysfs_root", &f->sysfs_root}, {"dev_root", &f->dev_root},
+      {"exporter_socket", &f->exporter_socket}, {"liveness_mode", &f->liveness_mode},
+      {"liveness_probe", &f->liveness_probe}};
+  static std::string ignored;
+  strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a.size() < 2 || a[0] != '-') return *err = "unexpected argument " + a, false;
@@ -117,37 +166,50 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       has_value = true;
     }
     if (name == "h" || name == "help") {
-      std::printf("usage: %s [-pulse N] [-driver_type container|vf-passthrough|pf-passthrough] [-resource_naming_strategy single|mixed] "
-                  "[-kubelet_dir DIR] [-sysfs_root DIR] [-dev_root DIR] [-exporter_socket PATH] "
-                  "[-send_every_pulse] (glog flags accepted)\n", argv[0]);
+      std::printf(
+          "usage: %s [-pulse N] [-driver_type container|vf-passthrough|pf-passthrough] "
+          "[-resource_naming_strategy single|mixed] [-kubelet_dir DIR] [-sysfs_root DIR] [-dev_root DIR] "
+          "[-exporter_socket PATH] [-send_every_pulse] [-allocator_extended_search] [-grpc_watchdog S] "
+          "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
+          "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
+          "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] "
+          "[-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
+          "[-log_backtrace_at FILE:N]\n",
+          argv[0]);
       std::exit(0);
     }
-    if (kBool.count(name)) {
-      if (name == "send_every_pulse") f->send_every_pulse = parse_bool(value);
+    if (bools.count(name) || glog::is_bool_flag(name)) {
+      if (glog::is_bool_flag(name)) {
+        glog::parse_flag(name, value, has_value, &f->log, err);
+        if (!err->empty()) return false;
+      } else if (!parse_bool(has_value ? value : "", bools[name])) {
+        return *err = "invalid boolean value \"" + value + "\" for -" + name, false;
+      }
       continue;
     }
+    if (kPythonOnly.count(name))
+      return *err = "-" + name + " is implemented by the Python entrypoint (k8s-device-plugin), not by the native "
+                    "daemon",
+             false;
     if (!has_value) {
       if (i + 1 >= argc) return *err = "flag needs an argument: -" + name, false;
       value = argv[++i];
     }
-    if (name == "pulse") {
+    if (glog::parse_flag(name, value, true, &f->log, err)) {
+      if (!err->empty()) return false;
+    } else if (ints.count(name)) {
       char* end = nullptr;
       const long v = std::strtol(value.c_str(), &end, 10);
-      if (end == value.c_str() || *end) return *err = "invalid value \"" + value + "\" for flag -pulse", false;
-      f->pulse = static_cast<int>(v);
-    } else if (name == "driver_type") {
-      f->driver_type = value;
-    } else if (name == "resource_naming_strategy") {
-      f->naming = value;
-    } else if (name == "kubelet_dir") {
-      f->kubelet_dir = value;
-    } else if (name == "sysfs_root") {
-      f->sysfs_root = value;
-    } else if (name == "dev_root") {
-      f->dev_root = value;
-    } else if (name == "exporter_socket") {
-      f->exporter_socket = value;
-    } else if (!kIgnoredValue.count(name)) {
+      if (value.empty() || *end) return *err = "invalid value \"" + value + "\" for flag -" + name, false;
+      *ints[name] = static_cast<int>(v);
+    } else if (floats.count(name)) {
+      char* end = nullptr;
+      const double v = std::strtod(value.c_str(), &end);
+      if (value.empty() || *end) return *err = "invalid value \"" + value + "\" for flag -" + name, false;
+      *floats[name] = v;
+    } else if (strs.count(name)) {
+      *strs[name] = value;
+    } else {
       return *err = "flag provided but not defined: -" + name, false;
     }
   }
@@ -161,6 +223,11 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
   if (f->naming != "single" && f->naming != "mixed")
     return *err = "invalid resource_naming_strategy provided: " + f->naming + ", supported values are single or mixed",
            false;
+  if (f->liveness_mode != "persistent" && f->liveness_mode != "spawn")
+    return *err = "invalid liveness_mode provided: " + f->liveness_mode + ", supported values are persistent or spawn",
+           false;
+  if (f->grpc_watchdog_s < 0) return *err = "grpc_watchdog must be >= 0", false;
+  if (f->liveness && f->pulse == 0) return *err = "-liveness needs -pulse > 0 (the probe runs once per pulse)", false;
   return true;
 }
 
@@ -204,9 +271,15 @@ struct Resource {
   std::shared_ptr<const HiveAllocator> allocator;
   std::map<std::string, bool> health;  // device id -> healthy
   std::string list;                    // serialized ListAndWatchResponse
+  // registration (worker thread) and the transport watchdog
   bool registered = false;
-  std::chrono::steady_clock::time_point next_register{};
+  bool register_inflight = false;
+  uint64_t server_gen = 0;             // bumped on every (re)start of the server
+  Clock::time_point next_register{};
   int retry_ms = 100;  // kubelet.sock appears (bind) just before kubelet listens: retry soon, then back off to 3 s
+  Clock::time_point registered_at{};
+  uint64_t streams_at_register = 0, perr_at_register = 0;
+  bool list_seen = false;
 };
 
 std::string list_bytes(const Resource& r) {
@@ -227,14 +300,14 @@ std::string list_bytes(const Resource& r) {
 
 std::string group_key(const GpuDevice& d) { return !d.unique_id.empty() ? d.unique_id : "bdf:" + d.bdf; }
 
-void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved) {
+void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved, bool extended) {
   // allocator (BestEffortPolicy.init); on failure kubelet allocates by itself
   bool alloc_ok = true;
   for (const auto& d : r.devices)
     if (unresolved.count(d.id)) alloc_ok = false;
   if (!alloc_ok) {
-    logf('E', "allocator disabled for plugin %s: no physical-GPU identity for some devices. Falling back to "
-              "kubelet default allocation.", r.name.c_str());
+    MI_LOG(kError, "allocator disabled for plugin %s: no physical-GPU identity for some devices. Falling back to "
+                   "kubelet default allocation.", r.name.c_str());
   } else {
     std::vector<AllocDevice> ad;
     for (const auto& d : r.devices) {
@@ -247,11 +320,13 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
       a.inferred_links = d.node_id < 0 && d.identity == "sysfs";
       ad.push_back(a);
     }
+    AllocatorOptions opt;
+    opt.extended_search = extended;
     auto alloc = std::make_shared<HiveAllocator>();
-    const std::string err = alloc->init(ad, topo);
+    const std::string err = alloc->init(ad, topo, opt);
     if (!err.empty()) {
-      logf('E', "allocator init failed for plugin %s. Falling back to kubelet default allocation. Error %s",
-           r.name.c_str(), err.c_str());
+      MI_LOG(kError, "allocator init failed for plugin %s. Falling back to kubelet default allocation. Error %s",
+             r.name.c_str(), err.c_str());
       alloc_ok = false;
     } else {
       r.allocator = alloc;
@@ -317,11 +392,12 @@ bool start_server(Resource& r) {
   r.service->attach(*r.server);
   const std::string err = r.server->start(r.socket);
   if (!err.empty()) {
-    logf('E', "%s: could not serve on %s: %s", r.name.c_str(), r.socket.c_str(), err.c_str());
+    MI_LOG(kError, "%s: could not serve on %s: %s", r.name.c_str(), r.socket.c_str(), err.c_str());
     r.server.reset();
     return false;
   }
-  logf('I', "%s: serving on %s", r.name.c_str(), r.socket.c_str());
+  r.server_gen++;
+  MI_LOG(kInfo, "%s: serving on %s", r.name.c_str(), r.socket.c_str());
   return true;
 }
 
@@ -332,118 +408,107 @@ void stop_server(Resource& r) {
     ::unlink(r.socket.c_str());
   }
   r.registered = false;
+  r.list_seen = false;
 }
 
-// Register{version=1, endpoint=2, resource_name=3, options=4} on kubelet.sock
-bool register_with_kubelet(Resource& r, const std::string& kubelet_sock, double timeout_s) {
-  rpc::GrpcClient c;
-  const std::string err = c.connect(kubelet_sock);
-  if (!err.empty()) {
-    logf('W', "%s: kubelet not reachable at %s: %s", r.name.c_str(), kubelet_sock.c_str(), err.c_str());
-    return false;
+// ---- worker threads -----------------------------------------------------------
+// Jobs run on their own threads; completions are queued here and the control
+// loop is woken through a pipe.
+struct Completion {
+  enum Kind { kRegister, kSweep } kind;
+  size_t resource = 0;
+  uint64_t gen = 0;
+  bool ok = false;
+  std::string message;
+  std::map<std::string, bool> health;  // kSweep: device id -> healthy (every resource's devices)
+};
+
+class Workers {
+ public:
+  Workers() {
+    if (::pipe2(wake_, O_CLOEXEC | O_NONBLOCK) != 0) wake_[0] = wake_[1] = -1;
   }
-  std::string req;
-  pb::put_bytes(&req, 1, "v1beta1");
-  pb::put_bytes(&req, 2, basename(r.socket));
-  pb::put_bytes(&req, 3, std::string(kResourceNamespace) + "/" + r.name);
-  pb::put_bytes(&req, 4, r.options);
-  const rpc::Reply rep = c.unary("/v1beta1.Registration/Register", req, timeout_s);
-  if (rep.status != 0) {
-    logf('E', "%s: Register failed (%d): %s", r.name.c_str(), rep.status, rep.message.c_str());
-    return false;
+  ~Workers() { close(); }
+  int wake_fd() const { return wake_[0]; }
+  void run(std::function<Completion()> job) {
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    std::lock_guard<std::mutex> lk(mu_);
+    threads_.emplace_back(std::thread([this, done, job = std::move(job)] {
+                            Completion c = job();
+                            {
+                              std::lock_guard<std::mutex> lk2(mu_);
+                              done_.push_back(std::move(c));
+                            }
+                            done->store(true);
+                            const char b = 1;
+                            if (::write(wake_[1], &b, 1) < 0) {
+                            }
+                          }),
+                          done);
   }
-  logf('I', "%s: Registration for endpoint %s", r.name.c_str(), basename(r.socket).c_str());
-  return true;
-}
-
-// ---- health -------------------------------------------------------------------
-// The device's kfd node still describes a live GPU (ContainerImpl's kfd verdict).
-bool kfd_node_live(const std::string& sysfs_root, const GpuDevice& d) {
-  if (d.node_id < 0) return true;  // no kfd data for this device (cgroup-denied): not evidence of a fault
-  const auto kv = parse_kv_file(path_join(sysfs_root, "class/kfd/kfd/topology/nodes/" + std::to_string(d.node_id) +
-                                                          "/properties"));
-  if (!kv) return false;
-  const auto cores = kv->find("cpu_cores_count");
-  const auto gfx = kv->find("gfx_target_version");
-  return cores != kv->end() && gfx != kv->end() && parse_i64(cores->second, 1) == 0 &&
-         parse_i64(gfx->second, 0) > 0;
-}
-
-// metricssvc.MetricsService/List -> BDF -> healthy; empty when unavailable
-std::map<std::string, bool> exporter_health(const std::string& socket) {
-  std::map<std::string, bool> out;
-  if (socket.empty() || !path_exists(socket)) return out;
-  rpc::GrpcClient c;
-  if (!c.connect(socket).empty()) return out;
-  const rpc::Reply rep = c.unary("/metricssvc.MetricsService/List", "", 10.0);
-  if (rep.status != 0) {
-    logf('E', "Error getting health info svc : %s", rep.message.c_str());
+  std::vector<Completion> take() {
+    char buf[256];
+    while (::read(wake_[0], buf, sizeof(buf)) > 0) {
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    std::vector<Completion> out;
+    out.swap(done_);
     return out;
   }
-  // GPUStateResponse{GPUState=1: GPUState{ID=1, UUID=2, Health=3, AssociatedWorkload=4, Device=5}}
-  pb::scan(
-      rep.body.data(), rep.body.size(),
-      [&](int field, const char* p, size_t n) {
-        if (field != 1) return true;
-        std::string health, device;
-        pb::scan(
-            p, n,
-            [&](int f, const char* q, size_t m) {
-              if (f == 3) health.assign(q, m);
-              if (f == 5) device.assign(q, m);
-              return true;
-            },
-            [](int, uint64_t) { return true; });
-        if (!device.empty()) out[device] = to_lower(trim(health)) == "healthy";
-        return true;
-      },
-      [](int, uint64_t) { return true; });
-  return out;
-}
-
-bool set_health(Resource& r, const std::string& id, bool ok) {
-  auto it = r.health.find(id);
-  const bool prev = it == r.health.end() || it->second;
-  r.health[id] = ok;
-  if (prev == ok) return false;
-  logf('W', "device %s: %s -> %s", id.c_str(), prev ? "Healthy" : "Unhealthy", ok ? "Healthy" : "Unhealthy");
-  return true;
-}
-
-// one health pass; true when a verdict changed
-bool refresh_health(Resource& r, const Flags& f, const std::map<std::string, bool>& exporter) {
-  bool changed = false;
-  if (r.driver == Driver::Vf) {
-    // gim gone -> every group Unhealthy; else a group is Unhealthy if any parent PF is (amdgpu_sriov.go:217-308)
-    const bool gim = is_dir(path_join(f.sysfs_root, "bus/pci/drivers/gim"));
-    for (const auto& g : r.group_ids) {
-      bool ok = gim;
-      for (const auto& fn : r.groups.at(g)) {
-        auto e = exporter.find(fn.pf);
-        if (e != exporter.end() && !e->second) ok = false;
+  // joins the threads that have finished
+  void reap() {
+    std::vector<std::thread> finished;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto it = threads_.begin(); it != threads_.end();) {
+        if (it->second->load()) {
+          finished.push_back(std::move(it->first));
+          it = threads_.erase(it);
+        } else {
+          ++it;
+        }
       }
-      changed |= set_health(r, g, ok);
     }
-    return changed;
+    for (auto& t : finished) t.join();
   }
-  if (r.driver == Driver::Pf) {  // vfio-pci present -> Healthy (amdgpu_pf.go:210-229)
-    const bool vfio = is_dir(path_join(f.sysfs_root, "bus/pci/drivers/vfio-pci"));
-    for (const auto& g : r.group_ids) changed |= set_health(r, g, vfio);
-    return changed;
-  }
-  for (const auto& d : r.devices) {
-    bool ok = kfd_node_live(f.sysfs_root, d);
-    auto e = exporter.find(d.bdf);
-    if (e != exporter.end() && !e->second) ok = false;
-    auto it = r.health.find(d.id);
-    const bool prev = it == r.health.end() || it->second;
-    if (prev != ok) {
-      logf('W', "device %s: %s -> %s", d.id.c_str(), prev ? "Healthy" : "Unhealthy", ok ? "Healthy" : "Unhealthy");
-      changed = true;
+  void join_all() {
+    std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> ts;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ts.swap(threads_);
     }
-    r.health[d.id] = ok;
+    for (auto& t : ts)
+      if (t.first.joinable()) t.first.join();
   }
-  return changed;
+  void close() {
+    join_all();
+    if (wake_[0] >= 0) ::close(wake_[0]);
+    if (wake_[1] >= 0) ::close(wake_[1]);
+    wake_[0] = wake_[1] = -1;
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> threads_;
+  std::vector<Completion> done_;
+  int wake_[2] = {-1, -1};
+};
+
+// Register{version=1, endpoint=2, resource_name=3, options=4} on kubelet.sock (blocking; worker thread)
+std::string register_with_kubelet(const std::string& name, const std::string& socket, const std::string& options,
+                                  const std::string& kubelet_sock, double timeout_s, int abort_fd) {
+  rpc::GrpcClient c;
+  c.set_abort_fd(abort_fd);
+  const std::string err = c.connect(kubelet_sock, timeout_s);
+  if (!err.empty()) return "kubelet not reachable at " + kubelet_sock + ": " + err;
+  std::string req;
+  pb::put_bytes(&req, 1, "v1beta1");
+  pb::put_bytes(&req, 2, basename(socket));
+  pb::put_bytes(&req, 3, std::string(kResourceNamespace) + "/" + name);
+  pb::put_bytes(&req, 4, options);
+  const rpc::Reply rep = c.unary("/v1beta1.Registration/Register", req, timeout_s);
+  if (rep.status != 0) return "Register failed (" + std::to_string(rep.status) + "): " + rep.message;
+  return "";
 }
 
 volatile sig_atomic_t g_stop = 0;
@@ -456,19 +521,58 @@ void on_signal(int) {
   }
 }
 
+// identity of kubelet.sock: a restart replaces the file (new inode / ctime)
+struct SockId {
+  bool present = false;
+  dev_t dev = 0;
+  ino_t ino = 0;
+  int64_t ctime_ns = 0;
+  bool operator==(const SockId& o) const {
+    return present == o.present && dev == o.dev && ino == o.ino && ctime_ns == o.ctime_ns;
+  }
+  bool operator!=(const SockId& o) const { return !(*this == o); }
+};
+
+SockId sock_id(const std::string& path) {
+  SockId s;
+  struct stat st {};
+  if (::stat(path.c_str(), &st) != 0) return s;
+  s.present = true;
+  s.dev = st.st_dev;
+  s.ino = st.st_ino;
+  s.ctime_ns = static_cast<int64_t>(st.st_ctim.tv_sec) * 1000000000 + st.st_ctim.tv_nsec;
+  return s;
+}
+
+std::string self_dir() {
+  char buf[4096];
+  const ssize_t n = ::readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+  if (n <= 0) return ".";
+  buf[n] = 0;
+  std::string p = buf;
+  return p.substr(0, p.rfind('/'));
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Flags f;
   std::string err;
   if (!parse_flags(argc, argv, &f, &err)) {
-    logf('E', "%s", err.c_str());
+    glog::init(f.log);
+    MI_LOG(kError, "%s", err.c_str());
     return 1;
   }
-  logf('I', "AMD GPU device plugin for Kubernetes (MI355X-native, native daemon)");
-  if (::pipe(g_sig_pipe) != 0) return 1;
-  ::fcntl(g_sig_pipe[0], F_SETFL, O_NONBLOCK);
-  ::fcntl(g_sig_pipe[1], F_SETFL, O_NONBLOCK);
+  if (f.log.program.empty()) f.log.program = "k8s-device-plugin";
+  err = glog::init(f.log);
+  if (!err.empty()) {
+    glog::Options o;
+    glog::init(o);
+    MI_LOG(kError, "%s", err.c_str());
+    return 1;
+  }
+  MI_LOG(kInfo, "AMD GPU device plugin for Kubernetes (MI355X-native, native daemon)");
+  if (::pipe2(g_sig_pipe, O_CLOEXEC | O_NONBLOCK) != 0) return 1;
   struct sigaction sa {};
   sa.sa_handler = on_signal;
   sigaction(SIGTERM, &sa, nullptr);
@@ -478,13 +582,15 @@ int main(int argc, char** argv) {
 
   std::vector<Resource> resources;
   KfdTopology topo;
+  std::vector<GpuDevice> container_devices;  // every advertised container-mode device (health engine)
+  Driver driver = Driver::Container;
   // one driver's resources; "" on success (an empty list = no devices), else the init error
   auto init_container = [&](std::vector<Resource>* out) -> std::string {
     if (!is_dir(path_join(f.sysfs_root, "class/kfd"))) return "No kfd found (" + f.sysfs_root + "/class/kfd)";
     topo = KfdTopology::load_sysfs(f.sysfs_root);
     const DiscoveryResult res = discover_gpus(f.sysfs_root, topo);
-    for (const auto& w : res.warnings) logf('W', "%s", w.c_str());
-    logf('I', "Found %zu AMDGPUs", res.devices.size());
+    for (const auto& w : res.warnings) MI_LOG(kWarning, "%s", w.c_str());
+    MI_LOG(kInfo, "Found %zu AMDGPUs", res.devices.size());
     const bool homogeneous = is_homogeneous(res.devices);
     if (!homogeneous && f.naming == "single")
       return "Partitions of different styles across GPUs in a node is not supported with single strategy. "
@@ -499,15 +605,17 @@ int main(int argc, char** argv) {
           if (c > 0) names.push_back(t);
     }
     const std::set<std::string> unresolved(res.unresolved.begin(), res.unresolved.end());
-    const auto exporter = exporter_health(f.exporter_socket);
+    container_devices.clear();
     for (const auto& name : names) {
       Resource r;
       r.name = name;
       for (const auto& d : res.devices)
-        if (homogeneous || d.partition_type() == name) r.devices.push_back(d);
+        if (homogeneous || d.partition_type() == name) {
+          r.devices.push_back(d);
+          container_devices.push_back(d);
+        }
       r.socket = path_join(f.kubelet_dir, std::string(kResourceNamespace) + "_" + name);
-      refresh_health(r, f, exporter);
-      prepare(r, topo, unresolved);
+      prepare(r, topo, unresolved, f.allocator_extended_search);
       out->push_back(std::move(r));
     }
     return "";
@@ -518,7 +626,7 @@ int main(int argc, char** argv) {
       return vf ? "No amd gim driver loaded" : "No vfio-pci driver loaded";
     const PciScanResult scan = vf ? scan_vf_mapping(f.sysfs_root) : scan_pf_mapping(f.sysfs_root);
     if (!scan.ok) return std::string("Failed to generate ") + (vf ? "vf" : "pf") + " map: " + scan.error;
-    logf('I', "Found %zu %s IOMMU groups", scan.groups.size(), vf ? "vf-passthrough" : "pf-passthrough");
+    MI_LOG(kInfo, "Found %zu %s IOMMU groups", scan.groups.size(), vf ? "vf-passthrough" : "pf-passthrough");
     if (scan.groups.empty()) return "";
     Resource r;
     r.driver = drv;
@@ -532,7 +640,6 @@ int main(int argc, char** argv) {
       return x < y;
     });
     r.socket = path_join(f.kubelet_dir, std::string(kResourceNamespace) + "_" + r.name);
-    refresh_health(r, f, exporter_health(vf ? f.exporter_socket : ""));
     prepare_passthrough(r);
     out->push_back(std::move(r));
     return "";
@@ -544,92 +651,305 @@ int main(int argc, char** argv) {
   if (!f.driver_type.empty()) {
     const std::string e = init_driver(f.driver_type, &resources);
     if (!e.empty()) {
-      logf('E', "Error instantiating driver type %s: %s", f.driver_type.c_str(), e.c_str());
+      MI_LOG(kError, "Error instantiating driver type %s: %s", f.driver_type.c_str(), e.c_str());
       return 1;
     }
+    driver = f.driver_type == "container" ? Driver::Container
+             : f.driver_type == "vf-passthrough" ? Driver::Vf : Driver::Pf;
   } else {
     // container -> VF -> PF; the reference starts its manager even when none initialised, and idles
     for (const char* type : {"container", "vf-passthrough", "pf-passthrough"}) {
       std::vector<Resource> got;
       const std::string e = init_driver(type, &got);
       if (!e.empty()) {
-        logf('W', "%s implementation failed: %s. Trying next...", type, e.c_str());
+        MI_LOG(kWarning, "%s implementation failed: %s. Trying next...", type, e.c_str());
         continue;
       }
       if (got.empty()) {
-        logf('W', "%s implementation found no devices. Trying next...", type);
+        MI_LOG(kWarning, "%s implementation found no devices. Trying next...", type);
         continue;
       }
       resources = std::move(got);
+      driver = std::string(type) == "container" ? Driver::Container
+               : std::string(type) == "vf-passthrough" ? Driver::Vf : Driver::Pf;
       break;
     }
   }
 
+  // ---- health ---------------------------------------------------------------
+  // The shutdown pipe ends every wait of the workers (peer calls, probes).
+  int stop_pipe[2] = {-1, -1};
+  if (::pipe2(stop_pipe, O_CLOEXEC | O_NONBLOCK) != 0) return 1;
+  std::unique_ptr<health::Engine> engine;
+  if (driver == Driver::Container && !container_devices.empty()) {
+    health::Config hc;
+    hc.sysfs_root = f.sysfs_root;
+    hc.dev_root = f.dev_root;
+    hc.exporter_socket = f.exporter_socket;
+    hc.liveness = f.liveness;
+    hc.prober.exe = !f.liveness_probe.empty() ? f.liveness_probe : path_join(self_dir(), "mi355x-liveness-probe");
+    hc.prober.timeout_s = f.liveness_timeout;
+    hc.prober.iters = f.liveness_iters;
+    hc.prober.persistent = f.liveness_mode == "persistent";
+    hc.prober.keep_queues = f.liveness_keep_queues;
+    hc.fail_threshold = f.liveness_fail_threshold;
+    hc.recover_threshold = f.liveness_recover_threshold;
+    hc.busy_grace_s = f.liveness_busy_grace;
+    hc.unknown_busy_grace_s = f.liveness_unknown_busy_grace;
+    hc.corroborate = f.liveness_corroborate;
+    hc.idle_sweeps = f.liveness_idle_sweeps;
+    hc.crowded_procs = f.liveness_crowded_procs;
+    hc.crowded_release_sweeps = f.liveness_crowded_release_sweeps;
+    hc.smi_ecc = f.smi_ecc;
+    hc.smi_events = f.smi_events;
+    engine = std::make_unique<health::Engine>(container_devices, topo, hc);
+    engine->set_abort_fd(stop_pipe[0]);
+    if (f.liveness) MI_LOG(kInfo, "liveness probe: %s (%s)", hc.prober.exe.c_str(), f.liveness_mode.c_str());
+  }
+  // one health pass (blocking; worker thread): device id -> healthy for every resource
+  auto health_pass = [&]() -> std::map<std::string, bool> {
+    std::map<std::string, bool> out;
+    if (driver == Driver::Container) {
+      if (engine) {
+        engine->sweep();
+        for (const auto& [id, v] : engine->snapshot()) out[id] = v.healthy;
+      }
+      return out;
+    }
+    const bool vf = driver == Driver::Vf;
+    // gim gone -> every group Unhealthy; else a group is Unhealthy if any parent PF is (amdgpu_sriov.go:217-308)
+    // vfio-pci present -> Healthy (amdgpu_pf.go:210-229)
+    const bool present = is_dir(path_join(f.sysfs_root, vf ? "bus/pci/drivers/gim" : "bus/pci/drivers/vfio-pci"));
+    std::map<std::string, bool> exporter;
+    if (vf) {
+      std::string e;
+      exporter = health::exporter_list(f.exporter_socket, 10.0, stop_pipe[0], &e);
+      if (!e.empty()) MI_LOG(kError, "Error getting health info svc : %s", e.c_str());
+    }
+    for (const auto& r : resources)
+      for (const auto& g : r.group_ids) {
+        bool ok = present;
+        if (vf)
+          for (const auto& fn : r.groups.at(g))
+            if (auto it = exporter.find(fn.pf); it != exporter.end() && !it->second) ok = false;
+        out[g] = ok;
+      }
+    return out;
+  };
+  // applies verdicts; true when a resource's list changed
+  auto apply_health = [&](Resource& r, const std::map<std::string, bool>& h) {
+    bool changed = false;
+    auto set = [&](const std::string& id) {
+      auto it = h.find(id);
+      if (it == h.end()) return;
+      auto cur = r.health.find(id);
+      const bool prev = cur == r.health.end() || cur->second;
+      if (prev != it->second) changed = true;
+      r.health[id] = it->second;
+    };
+    for (const auto& d : r.devices) set(d.id);
+    for (const auto& g : r.group_ids) set(g);
+    if (changed) {
+      r.list = list_bytes(r);
+      r.service->set_device_list(r.list);
+    }
+    return changed;
+  };
+  if (f.pulse > 0 && !resources.empty()) {
+    // one sweep before registering, so the first ListAndWatch already carries
+    // real verdicts (the reference advertises everything Healthy until its first pulse)
+    const auto h = health_pass();
+    for (auto& r : resources) apply_health(r, h);
+  }
+
   const std::string kubelet_sock = path_join(f.kubelet_dir, "kubelet.sock");
   DirWatcher watch;
-  const std::string werr = watch.open(f.kubelet_dir);
-  if (!werr.empty()) logf('W', "no inotify watch on %s (%s): polling every second", f.kubelet_dir.c_str(), werr.c_str());
-  auto try_register = [&](Resource& r) {
-    r.registered = register_with_kubelet(r, kubelet_sock, f.register_timeout_s);
-    r.next_register = std::chrono::steady_clock::now() + std::chrono::milliseconds(r.retry_ms);
-    r.retry_ms = r.registered ? 100 : std::min(2 * r.retry_ms, 3000);
+  std::string werr = watch.open(f.kubelet_dir);
+  if (!werr.empty()) MI_LOG(kWarning, "no inotify watch on %s (%s): polling every second", f.kubelet_dir.c_str(),
+                            werr.c_str());
+  Workers workers;
+  uint64_t kubelet_gen = 0;  // bumped on every kubelet (re)start: older Register results are stale
+  auto try_register = [&](size_t i) {
+    Resource& r = resources[i];
+    if (r.register_inflight || !r.server) return;
+    r.register_inflight = true;
+    const uint64_t gen = kubelet_gen;
+    workers.run([&f, &kubelet_sock, name = r.name, socket = r.socket, options = r.options, i, gen,
+                 abort_fd = stop_pipe[0]] {
+      Completion c{Completion::kRegister, i, gen, false, "", {}};
+      c.message = register_with_kubelet(name, socket, options, kubelet_sock, f.register_timeout_s, abort_fd);
+      c.ok = c.message.empty();
+      return c;
+    });
   };
   auto start_all = [&] {
-    for (auto& r : resources) {
+    kubelet_gen++;
+    for (size_t i = 0; i < resources.size(); ++i) {
+      Resource& r = resources[i];
       stop_server(r);
       r.retry_ms = 100;
-      if (start_server(r)) try_register(r);
+      r.next_register = Clock::now();
+      if (start_server(r)) {
+        r.register_inflight = false;  // a Register of the previous kubelet completes as stale
+        try_register(i);
+      }
     }
   };
-  if (path_exists(kubelet_sock)) start_all();
+  SockId sock = sock_id(kubelet_sock);
+  if (sock.present) start_all();
 
-  using clk = std::chrono::steady_clock;
-  auto next_pulse = clk::now() + std::chrono::seconds(f.pulse > 0 ? f.pulse : 3600);
-  bool sock_present = path_exists(kubelet_sock);
+  bool sweep_inflight = false;
+  auto next_pulse = Clock::now() + std::chrono::seconds(f.pulse > 0 ? f.pulse : 3600);
+  auto next_stat = Clock::now() + std::chrono::seconds(5);
+  int exit_code = 0;
   while (!g_stop) {
-    pollfd pfd[2] = {{g_sig_pipe[0], POLLIN, 0}, {watch.fd(), POLLIN, 0}};
-    const int nfd = watch.fd() >= 0 ? 2 : 1;
-    auto wait_ms = std::chrono::duration_cast<std::chrono::milliseconds>(next_pulse - clk::now()).count();
-    if (watch.fd() < 0) wait_ms = std::min<long long>(wait_ms, 1000);
-    for (const auto& r : resources)
-      if (r.server && !r.registered)
-        wait_ms = std::min<long long>(
-            wait_ms, std::chrono::duration_cast<std::chrono::milliseconds>(r.next_register - clk::now()).count() + 1);
-    ::poll(pfd, nfd, static_cast<int>(std::max<long long>(0, wait_ms)));
+    std::vector<pollfd> pfd = {{g_sig_pipe[0], POLLIN, 0}, {workers.wake_fd(), POLLIN, 0}};
+    const bool inotify = watch.fd() >= 0;
+    if (inotify) pfd.push_back({watch.fd(), POLLIN, 0});
+    const size_t ev_base = pfd.size();
+    for (const auto& r : resources) pfd.push_back({r.service->event_fd(), POLLIN, 0});
+    const auto now = Clock::now();
+    auto until = [&](Clock::time_point t) -> long long {
+      return std::chrono::duration_cast<std::chrono::milliseconds>(t - now).count() + 1;
+    };
+    long long wait_ms = f.pulse > 0 ? until(next_pulse) : 3600 * 1000;
+    // inotify is the fast path; the stat poll is the safety net (a dead watch, a replaced directory)
+    wait_ms = std::min(wait_ms, inotify ? until(next_stat) : 1000LL);
+    for (const auto& r : resources) {
+      if (r.server && !r.registered && !r.register_inflight) wait_ms = std::min(wait_ms, until(r.next_register));
+      if (r.registered && !r.list_seen && f.grpc_watchdog_s > 0) wait_ms = std::min(wait_ms, 250LL);
+    }
+    if (f.grpc_watchdog_s > 0) wait_ms = std::min(wait_ms, 1000LL);
+    ::poll(pfd.data(), pfd.size(), static_cast<int>(std::max(0LL, wait_ms)));
     if (g_stop) break;
-    bool kubelet_event = false;
-    if (nfd == 2 && (pfd[1].revents & POLLIN)) {
-      for (const auto& [name, mask] : watch.read_events())
-        if (name == "kubelet.sock" || name.empty()) kubelet_event = true;
-    }
-    const bool present = path_exists(kubelet_sock);
-    if (kubelet_event || present != sock_present) {
-      if (present) {
-        logf('I', "kubelet socket (re)created; restarting plugin servers and re-registering");
-        start_all();
-      } else if (sock_present) {
-        logf('I', "kubelet socket removed; stopping plugin servers");
-        for (auto& r : resources) stop_server(r);
+    // ---- RPC events: the reference logs every Allocate
+    for (size_t i = 0; i < resources.size(); ++i)
+      if (pfd[ev_base + i].revents & POLLIN) {
+        uint64_t v;
+        if (::read(resources[i].service->event_fd(), &v, sizeof(v)) < 0) {
+        }
+        for (const auto& ev : resources[i].service->drain_events()) {
+          if (ev.status != 0) {
+            MI_LOG(kError, "%s: %s: %s", resources[i].name.c_str(), ev.rpc.c_str(), ev.message.c_str());
+          } else if (ev.rpc == "Allocate") {
+            std::string ids;
+            for (const auto& id : ev.ids) ids += (ids.empty() ? "" : ",") + id;
+            MI_LOG(kInfo, "Allocating device IDs: %s", ids.c_str());
+          }
+          MI_VLOG(2, "rpc %s resource=%s latency_ms=%.3f", ev.rpc.c_str(), resources[i].name.c_str(),
+                  ev.dur_ns / 1e6);
+        }
       }
-      sock_present = present;
-    }
-    // registrations that failed (kubelet not serving yet): retry, rate-limited
-    for (auto& r : resources)
-      if (r.server && !r.registered && present && clk::now() >= r.next_register) try_register(r);
-    if (f.pulse > 0 && clk::now() >= next_pulse) {
-      next_pulse = clk::now() + std::chrono::seconds(f.pulse);
-      const auto exporter = exporter_health(f.exporter_socket);
-      for (auto& r : resources) {
-        const bool changed = refresh_health(r, f, exporter);
-        if (changed || f.send_every_pulse) {
-          r.list = list_bytes(r);
-          r.service->set_device_list(r.list);
-          if (r.server) r.server->broadcast(rpc::DevicePluginService::path("ListAndWatch"), r.list);
+    // ---- kubelet restarts: act only when kubelet.sock itself was replaced
+    bool look = !inotify || Clock::now() >= next_stat;
+    if (inotify && (pfd[2].revents & POLLIN)) {
+      for (const auto& [name, mask] : watch.read_events()) {
+        if (name == "kubelet.sock") look = true;
+        if (name.empty() && (mask & (IN_IGNORED | IN_DELETE_SELF | IN_MOVE_SELF))) {
+          // the watched directory went away: watch it again once it is back, stat-poll meanwhile
+          watch.close();
+          look = true;
         }
       }
     }
+    if (watch.fd() < 0 && is_dir(f.kubelet_dir) && watch.open(f.kubelet_dir).empty())
+      MI_LOG(kInfo, "inotify watch on %s re-established", f.kubelet_dir.c_str());
+    if (look) {
+      next_stat = Clock::now() + std::chrono::seconds(5);
+      const SockId cur = sock_id(kubelet_sock);
+      if (cur != sock) {
+        if (cur.present) {
+          MI_LOG(kInfo, "kubelet socket (re)created; restarting plugin servers and re-registering");
+          start_all();
+        } else if (sock.present) {
+          MI_LOG(kInfo, "kubelet socket removed; stopping plugin servers");
+          kubelet_gen++;
+          for (auto& r : resources) stop_server(r);
+        }
+        sock = cur;
+      }
+    }
+    // ---- worker completions
+    for (auto& c : workers.take()) {
+      if (c.kind == Completion::kRegister) {
+        Resource& r = resources[c.resource];
+        r.register_inflight = false;
+        if (c.gen != kubelet_gen || !r.server) continue;  // a previous kubelet's answer
+        if (c.ok) {
+          r.registered = true;
+          r.retry_ms = 100;
+          r.registered_at = Clock::now();
+          const auto st = r.server->stats();
+          r.streams_at_register = st.streams_opened;
+          r.perr_at_register = st.protocol_errors;
+          r.list_seen = false;
+          MI_LOG(kInfo, "%s: Registration for endpoint %s", r.name.c_str(), basename(r.socket).c_str());
+        } else {
+          MI_LOG(kError, "%s: %s", r.name.c_str(), c.message.c_str());
+          r.next_register = Clock::now() + std::chrono::milliseconds(r.retry_ms);
+          r.retry_ms = std::min(2 * r.retry_ms, 3000);
+        }
+      } else {
+        sweep_inflight = false;
+        for (auto& r : resources) {
+          const bool changed = apply_health(r, c.health);
+          if ((changed || f.send_every_pulse) && r.server)
+            r.server->broadcast(rpc::DevicePluginService::path("ListAndWatch"), r.list);
+        }
+      }
+    }
+    workers.reap();
+    // ---- registrations that failed (kubelet not serving yet): retry, rate-limited
+    for (size_t i = 0; i < resources.size(); ++i) {
+      Resource& r = resources[i];
+      if (r.server && !r.registered && !r.register_inflight && sock.present && Clock::now() >= r.next_register)
+        try_register(i);
+    }
+    // ---- transport watchdog
+    if (f.grpc_watchdog_s > 0) {
+      std::string why;
+      for (auto& r : resources) {
+        if (!r.registered || !r.server) continue;
+        const auto st = r.server->stats();
+        if (st.streams_opened > r.streams_at_register) r.list_seen = true;
+        if (st.protocol_errors > r.perr_at_register) {
+          why = r.name + ": " + std::to_string(st.protocol_errors - r.perr_at_register) +
+                " HTTP/2 protocol error(s) on the plugin socket";
+        } else if (!r.list_seen && std::chrono::duration<double>(Clock::now() - r.registered_at).count() >
+                                       f.grpc_watchdog_s) {
+          char b[96];
+          std::snprintf(b, sizeof(b), "no ListAndWatch stream within %gs of Register", f.grpc_watchdog_s);
+          why = r.name + ": " + b;
+        }
+        if (!why.empty()) break;
+      }
+      if (!why.empty()) {
+        MI_LOG(kError, "native gRPC transport watchdog: %s; exiting so the plugin is restarted", why.c_str());
+        exit_code = 3;
+        break;
+      }
+    }
+    // ---- health pulse (worker thread; a sweep still running skips this pulse)
+    if (f.pulse > 0 && Clock::now() >= next_pulse) {
+      next_pulse = Clock::now() + std::chrono::seconds(f.pulse);
+      if (sweep_inflight) {
+        MI_LOG(kWarning, "health sweep still running at the next pulse; skipping this pulse");
+      } else if (!resources.empty()) {
+        sweep_inflight = true;
+        workers.run([&health_pass] {
+          Completion c{Completion::kSweep, 0, 0, true, "", {}};
+          c.health = health_pass();
+          return c;
+        });
+      }
+    }
   }
-  logf('I', "Received signal, shutting down.");
+  if (g_stop) MI_LOG(kInfo, "Received signal, shutting down.");
+  const char b = 1;
+  if (::write(stop_pipe[1], &b, 1) < 0) {
+  }
+  workers.join_all();  // every wait ends at the stop pipe
+  if (engine) engine->close();
   for (auto& r : resources) stop_server(r);
-  return 0;
+  return exit_code;
 }

@@ -164,11 +164,11 @@ def _stop(p):
 
 
 @pytest.fixture
-def daemon_node(tmp_path):
+def daemon_node(tmp_path, request):
     fi = make_mi355x_node(tmp_path / "n")
     kdir = str(tmp_path / "dp")
     kub = GoKubelet(kdir)
-    p = _daemon(kdir, fi)
+    p = _daemon(kdir, fi, *getattr(request, "param", ()))
     try:
         assert _wait(lambda: kub.registrations, 20), "the daemon never registered"
         yield kdir, kub, p
@@ -471,6 +471,7 @@ def _open_lw(s, sid=1):
               gp.frame(gp.DATA, gp.END_STREAM, sid, gp.grpc_message(b"")))
 
 
+@pytest.mark.parametrize("daemon_node", [("-grpc_watchdog", "0")], indirect=True)   # errors on purpose
 @pytest.mark.parametrize("case,want", [
     ("no-settings-first", gp.PROTOCOL_ERROR),
     ("rst-idle", gp.PROTOCOL_ERROR),

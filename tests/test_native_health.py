@@ -1,0 +1,457 @@
+"""The native health engine (native/src/health/health_engine.cpp) — what the
+interpreter-free daemon `mi355x-device-plugin` runs each pulse — under the
+same stub-probe fault injection as the Python monitor's tests
+(tests/test_plugin.py): hysteresis, deadlines, stale nonces, garbage output,
+persistent server reuse and restart, server start failure, spawn mode, busy
+grace with amd-smi corroboration, crowded step-off, probe identity re-keying.
+Then end to end through the daemon: verdicts reach kubelet's ListAndWatch,
+a hung metrics exporter blocks neither re-registration nor shutdown, and the
+transport watchdog exits when kubelet never lists.
+
+Reference behaviour replaced: internal/pkg/amdgpu/amdgpu.go:322-345,865-974
+(node-global kfd verdict + exporter per BDF)."""
+import asyncio
+import json
+import os
+import shutil
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR, core
+from rocm_k8s_device_plugin_amd.testing import gopeer as gp
+from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+from rocm_k8s_device_plugin_amd.topology import discover
+
+STUB = os.path.join(os.path.dirname(__file__), "..", "rocm_k8s_device_plugin_amd", "testing", "stub_probe.py")
+EXE = os.environ.get("MI355X_NATIVE_DAEMON_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+
+
+def _busy_gpu(fi, inv, dev_id, pid="777"):
+    """A foreign process with a queue on dev_id's GPU (kfd proc entry)."""
+    node = inv.topology.node(inv.by_id[dev_id].node_id)
+    q = fi.sysfs / "class/kfd/kfd/proc" / pid / "queues" / "0"
+    q.mkdir(parents=True, exist_ok=True)
+    (q / "gpuid").write_text(f"{node.gpu_id}\n")
+
+
+def _engine(fi, tmp_path, control, timeout=2.0, env=None, **opts):
+    ctl = tmp_path / "probe_ctl.json"
+    ctl.write_text(json.dumps(control))
+    extra = {"MI355X_STUB_PROBE_CONTROL": str(ctl), **(env or {})}
+    o = dict(dev_root=str(fi.dev), liveness=True, probe_exe=STUB, argv_prefix=[sys.executable],
+             probe_timeout_s=timeout, extra_env=extra, fail_threshold=2)
+    o.update(opts)
+    return ctl, core().HealthEngine(str(fi.sysfs), o)
+
+
+def _by_ordinal(eng):
+    return {o: d for d, o in eng.ordinals().items()}
+
+
+def _unhealthy(eng):
+    return {d for d, (ok, _) in eng.snapshot().items() if not ok}
+
+
+def test_fault_injection_hysteresis(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl, eng = _engine(fi, tmp_path, {"2": "fail", "5": "hang", "6": "stale", "7": "garbage"}, timeout=1.5)
+    dev = _by_ordinal(eng)
+    assert sorted(dev) == list(range(8))
+    try:
+        assert not eng.sweep() and not _unhealthy(eng)         # 1st failure: below the threshold
+        assert eng.sweep()                                      # 2nd consecutive failure
+        snap = eng.snapshot()
+        assert _unhealthy(eng) == {dev[2], dev[5], dev[6], dev[7]}
+        assert "differ" in snap[dev[2]][1][0]
+        assert "deadline" in snap[dev[5]][1][0]
+        assert "stale" in snap[dev[6]][1][0]
+        assert "unparseable" in snap[dev[7]][1][0]
+        assert eng.stats()["fallbacks"] >= 1                   # the hung server was isolated per device
+        ctl.write_text("{}")                                    # everything recovers
+        assert eng.sweep() and not _unhealthy(eng)
+    finally:
+        eng.close()
+
+
+def test_persistent_server_reused_and_failures_confirmed_fresh(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    log = tmp_path / "starts.log"
+    ctl, eng = _engine(fi, tmp_path, {"3": "fail"}, env={"MI355X_STUB_PROBE_LOG": str(log)})
+    try:
+        for _ in range(3):
+            eng.sweep()
+        assert _unhealthy(eng) == {_by_ordinal(eng)[3]}
+        st = eng.stats()
+        assert st["server_starts"] == 1 and st["server_running"]
+        lines = log.read_text().split()
+        assert lines.count("serve+keep") == 1 and lines.count("3") == 3   # one fresh confirmation per sweep
+    finally:
+        eng.close()
+    assert not eng.stats()["server_running"]
+
+
+def test_stale_server_failure_is_not_reported(tmp_path):
+    """The server fails a device a fresh process finds healthy (stale runtime):
+    the device stays Healthy and the server is restarted."""
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl, eng = _engine(fi, tmp_path, {"4": "server_fail"})
+    try:
+        for _ in range(3):
+            eng.sweep()
+        assert not _unhealthy(eng)
+        st = eng.stats()
+        assert st["server_restarts"] >= 2 and st["server_starts"] >= 3
+    finally:
+        eng.close()
+
+
+def test_server_without_kept_queues_and_spawn_mode(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    log = tmp_path / "starts.log"
+    ctl, eng = _engine(fi, tmp_path, {}, env={"MI355X_STUB_PROBE_LOG": str(log)}, keep_queues=False)
+    try:
+        eng.sweep()
+        assert "serve" in log.read_text().split() and "serve+keep" not in log.read_text().split()
+    finally:
+        eng.close()
+    log.write_text("")
+    ctl, eng = _engine(fi, tmp_path, {"1": "fail"}, env={"MI355X_STUB_PROBE_LOG": str(log)}, persistent=False,
+                       fail_threshold=1)
+    try:
+        eng.sweep()
+        assert _unhealthy(eng) == {_by_ordinal(eng)[1]}
+        assert not any(x.startswith("serve") for x in log.read_text().split())
+        assert sorted(log.read_text().split()) == [str(i) for i in range(8)]
+    finally:
+        eng.close()
+
+
+def test_server_start_failure_falls_back_per_device(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl, eng = _engine(fi, tmp_path, {"serve": "broken", "1": "stale"})
+    try:
+        eng.sweep()
+        eng.sweep()
+        assert _unhealthy(eng) == {_by_ordinal(eng)[1]}
+        assert eng.stats()["fallbacks"] >= 1
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("busy,grace,unhealthy_after", [(True, 300.0, None), (True, 0.0, 2), (False, 300.0, 2)])
+def test_pending_behind_tenant(tmp_path, busy, grace, unhealthy_after):
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    log = tmp_path / "starts.log"
+    ctl, eng = _engine(fi, tmp_path, {"3": "pending"}, env={"MI355X_STUB_PROBE_LOG": str(log)}, busy_grace_s=grace)
+    dev = _by_ordinal(eng)[3]
+    if busy:
+        _busy_gpu(fi, inv, dev)
+    eng.set_activity({})   # amd-smi unavailable: no corroboration, the grace decides
+    healthy = []
+    try:
+        for _ in range(3):
+            eng.sweep()
+            healthy.append(dev not in _unhealthy(eng))
+    finally:
+        eng.close()
+    spawned = [x for x in log.read_text().split() if x == "3"]
+    if unhealthy_after is None:
+        assert healthy == [True, True, True] and spawned == []   # no fresh-process re-probe of a busy GPU
+    else:
+        assert healthy[:unhealthy_after - 1] == [True] * (unhealthy_after - 1) and not healthy[-1]
+        if not busy:
+            assert spawned
+    assert _unhealthy(eng) <= {dev}
+
+
+@pytest.mark.parametrize("activity,unhealthy", [(0, True), (87, False), (None, False)])
+def test_busy_grace_needs_gfx_activity(tmp_path, activity, unhealthy):
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ctl, eng = _engine(fi, tmp_path, {"3": "pending"}, busy_grace_s=300.0)
+    dev = _by_ordinal(eng)[3]
+    _busy_gpu(fi, inv, dev)
+    eng.set_activity({} if activity is None else {d.bdf: (activity if d.id == dev else 50) for d in inv.devices})
+    try:
+        for _ in range(4):
+            eng.sweep()
+    finally:
+        eng.close()
+    assert (dev in _unhealthy(eng)) == unhealthy
+    if unhealthy:
+        assert any("0% GFX activity" in r for r in eng.snapshot()[dev][1])
+    assert _unhealthy(eng) <= {dev}
+
+
+def test_kfd_proc_list_unreadable_means_busy_unknown(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    proc = fi.sysfs / "class/kfd/kfd/proc"
+    (proc / "999" / "queues").mkdir(parents=True)
+    ctl, eng = _engine(fi, tmp_path, {"3": "pending"}, busy_grace_s=300.0, unknown_busy_grace_s=0.0)
+    eng.set_activity({})
+    os.chmod(proc / "999" / "queues", 0)
+    try:
+        if os.access(proc / "999" / "queues", os.R_OK):
+            pytest.skip("running as root: permissions are not enforced")
+        for _ in range(2):
+            eng.sweep()
+        assert not eng.stats()["busy_state_known"]
+        assert _unhealthy(eng) == {_by_ordinal(eng)[3]}      # the short grace (0 s) applied
+    finally:
+        os.chmod(proc / "999" / "queues", 0o755)
+        eng.close()
+
+
+def test_crowded_gpu_gets_no_probe_server_queue(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    log = tmp_path / "starts.log"
+    ctl, eng = _engine(fi, tmp_path, {"3": "fail"}, env={"MI355X_STUB_PROBE_LOG": str(log)},
+                       crowded_release_sweeps=2)
+    dev = _by_ordinal(eng)[3]
+    for pid in range(800, 807):
+        _busy_gpu(fi, inv, dev, pid=str(pid))
+    act = {d.bdf: (60 if d.id == dev else 40) for d in inv.devices}
+    eng.set_activity(act)
+    try:
+        for _ in range(3):
+            eng.sweep()
+        assert dev not in _unhealthy(eng) and eng.stats()["crowded_skips"] == 3
+        act[inv.by_id[dev].bdf] = 0          # crowded but idle: a fresh process probes it
+        eng.set_activity(act)
+        for _ in range(2):
+            eng.sweep()
+        assert dev in _unhealthy(eng)
+        ctl.write_text("{}")
+        for pid in range(800, 807):
+            shutil.rmtree(fi.sysfs / "class/kfd/kfd/proc" / str(pid))
+        for _ in range(4):
+            eng.sweep()
+        assert not _unhealthy(eng)
+    finally:
+        eng.close()
+    words = log.read_text().split()
+    assert "visible=0,1,2,4,5,6,7" in words and words.count("3") >= 2
+
+
+def _bus_id(d):
+    loc = d.location_id
+    return f"{d.domain:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+
+
+@pytest.mark.parametrize("mode", ["single", "cpx"])
+def test_probe_identity_rekeys_verdicts(tmp_path, mode):
+    """ROCr enumerated the agents in another order than the positional map
+    assumes: every reply names its agent, so the failing agent's verdict lands
+    on its own kubelet ID and the ordinal map is rebuilt from the replies."""
+    fi = make_mi355x_node(tmp_path / "n", **({"compute_partition": "CPX"} if mode == "cpx" else {}))
+    inv = discover(str(fi.sysfs))
+    probe_env = {}
+    ctl, eng = _engine(fi, tmp_path, {"3": "fail"}, fail_threshold=1)
+    pos = eng.ordinals()
+    n = len(pos)
+    order = sorted(pos, key=pos.get)
+    # the agent at ordinal i is really device order[n-1-i]
+    ident = {str(i): {"kfd_node_id": inv.by_id[order[n - 1 - i]].node_id,
+                      "pci_bus_id": _bus_id(inv.by_id[order[n - 1 - i]])} for i in range(n)}
+    eng.close()
+    probe_env["MI355X_STUB_PROBE_IDENTITY"] = json.dumps(ident)
+    ctl, eng = _engine(fi, tmp_path, {"3": "fail"}, env=probe_env, fail_threshold=1)
+    try:
+        eng.sweep()
+        eng.sweep()
+        assert _unhealthy(eng) == {order[n - 1 - 3]}
+        assert eng.ordinals() == {order[n - 1 - i]: i for i in range(n)}
+        assert eng.stats()["identity_remaps"] == 1        # the second sweep already used the rebuilt map
+    finally:
+        eng.close()
+
+
+def test_probe_identity_unmatched_device_loses_its_ordinal(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ctl, eng = _engine(fi, tmp_path, {})
+    pos = eng.ordinals()
+    eng.close()
+    ident = {str(o): {"kfd_node_id": inv.by_id[d].node_id, "pci_bus_id": _bus_id(inv.by_id[d])} for d, o in pos.items()}
+    ident["5"] = {"kfd_node_id": 999, "pci_bus_id": "0000:ff:00.0"}
+    ctl, eng = _engine(fi, tmp_path, {}, env={"MI355X_STUB_PROBE_IDENTITY": json.dumps(ident)})
+    try:
+        eng.sweep()
+    finally:
+        eng.close()
+    victim = {o: d for d, o in pos.items()}[5]
+    assert _unhealthy(eng) == {victim}
+    assert any("no HIP device" in r for r in eng.snapshot()[victim][1])
+
+
+def test_kfd_node_loss_and_exporter_reach_partitions(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="CPX")
+    inv = discover(str(fi.sysfs))
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    victim = inv.devices[1]
+    bdf = inv.devices[9].bdf
+    eng.set_exporter({bdf: False})
+    try:
+        (fi.sysfs / "class/kfd/kfd/topology/nodes" / str(victim.node_id) / "properties").unlink()
+        assert eng.sweep()
+        bad = _unhealthy(eng)
+        assert victim.id in bad and "missing" in eng.snapshot()[victim.id][1][0]
+        # the exporter's BDF verdict lands on every partition of that GPU (reference: BDF only)
+        assert {d.id for d in inv.devices if d.bdf == bdf} <= bad
+    finally:
+        eng.close()
+
+
+def test_exporter_list_through_a_grpc_go_exporter(tmp_path):
+    """metricssvc.MetricsService/List against a grpc-go-shaped exporter."""
+    from rocm_k8s_device_plugin_amd.proto import metricssvc as ms
+    resp = ms.GPUStateResponse()
+    resp.GPUState.add(ID="0", Health="healthy", Device="0000:05:00.0")
+    resp.GPUState.add(ID="1", Health="UNHEALTHY", Device="0000:15:00.0")
+    path = str(tmp_path / "exp.sock")
+    with gp.GoServer(path, {"/metricssvc.MetricsService/List": lambda m: (0, "", resp.SerializeToString())},
+                     gp.GoServerConfig(continuation_chunk=4)):
+        h, err = core().exporter_list(path, 5.0)
+    assert err == "" and h == {"0000:05:00.0": True, "0000:15:00.0": False}
+
+
+# ------------------------------------------------------------------ the daemon end to end
+
+def _daemon(kdir, fi, *extra, env=None):
+    return subprocess.Popen([EXE, "-kubelet_dir", kdir, "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                             *extra], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                            env=dict(os.environ, **(env or {})))
+
+
+def _stop(p, timeout=20):
+    if p.poll() is None:
+        p.send_signal(signal.SIGTERM)
+    try:
+        _, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        _, err = p.communicate()
+        return None, err
+    return p.returncode, err
+
+
+def test_daemon_liveness_verdicts_reach_listandwatch(tmp_path):
+    """-liveness with the stub probe: the first list already carries the
+    failing device, a later fault arrives as an update, recovery too."""
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text(json.dumps({"3": "fail"}))
+    log = tmp_path / "starts.log"
+    kdir = str(tmp_path / "dp")
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = {o: d for d, o in eng.ordinals().items()}
+    eng.close()
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        p = _daemon(kdir, fi, "-pulse", "1", "-liveness", "-liveness_probe", STUB, "-liveness_fail_threshold", "1",
+                    "-liveness_timeout", "3", "-exporter_socket", "",
+                    env={"MI355X_STUB_PROBE_CONTROL": str(ctl), "MI355X_STUB_PROBE_LOG": str(log)})
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            assert {d for d, h in st.devices.items() if h == "Unhealthy"} == {dev[3]}   # before any pulse
+            u = st.updates
+            ctl.write_text(json.dumps({"5": "fail"}))
+            st = await k.wait_for_update("amd.com/gpu", u, timeout=20)
+            assert {d for d, h in st.devices.items() if h == "Unhealthy"} == {dev[5]}
+            ctl.write_text("{}")
+            st = await k.wait_for_update("amd.com/gpu", st.updates, timeout=20)
+            assert all(h == "Healthy" for h in st.devices.values())
+        finally:
+            rc, err = await asyncio.to_thread(_stop, p)
+            await k.stop()
+        assert rc == 0, err[-3000:]
+        assert "liveness probe: " in err and "device " + dev[3] in err
+        # one persistent kept-queue server for the daemon's lifetime, killed at shutdown
+        assert log.read_text().split().count("serve+keep") == 1
+
+    asyncio.run(asyncio.wait_for(go(), 90))
+
+
+def test_daemon_hung_exporter_blocks_neither_registration_nor_shutdown(tmp_path):
+    """An exporter that accepts and never answers (10 s deadline per call): a
+    kubelet restart is re-registered within a second, RPCs are answered at
+    once, and SIGTERM during the stuck call ends the daemon promptly."""
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+    exp = gp.GoServer(str(tmp_path / "exp.sock"), {}, gp.GoServerConfig(never_answer=True))
+    regs = []
+
+    def kubelet():
+        return gp.GoServer(os.path.join(kdir, "kubelet.sock"),
+                           {"/v1beta1.Registration/Register": lambda m: (regs.append(time.monotonic()), (0, "", b""))[1]})
+
+    kub = kubelet()
+    p = _daemon(kdir, fi, "-pulse", "1", "-exporter_socket", str(tmp_path / "exp.sock"), "-grpc_watchdog", "0")
+    try:
+        deadline = time.monotonic() + 30
+        while not regs and time.monotonic() < deadline:
+            time.sleep(0.02)
+        assert regs, "never registered"
+        time.sleep(1.5)   # a pulse is now stuck in the exporter call
+        assert exp.calls, "the exporter was not asked"
+        kub.close()
+        kub = kubelet()
+        t0 = time.monotonic()
+        while len(regs) < 2 and time.monotonic() - t0 < 5:
+            time.sleep(0.01)
+        assert len(regs) >= 2 and regs[-1] - t0 < 1.0, "re-registration waited for the exporter"
+        c = gp.GoClientConn(os.path.join(kdir, "amd.com_gpu"))
+        try:
+            t1 = time.monotonic()
+            assert c.unary("/v1beta1.DevicePlugin/GetDevicePluginOptions", b"", 5.0)[0] == 0
+            assert time.monotonic() - t1 < 0.5
+        finally:
+            c.close()
+        t2 = time.monotonic()
+        rc, err = _stop(p)
+        assert rc == 0 and time.monotonic() - t2 < 2.0, err[-2000:]
+    finally:
+        if p.poll() is None:
+            p.kill()
+        kub.close()
+        exp.close()
+
+
+def test_daemon_watchdog_exits_when_kubelet_never_lists(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+    kub = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    t0 = time.monotonic()
+    p = _daemon(kdir, fi, "-grpc_watchdog", "1", "-exporter_socket", "")
+    try:
+        rc, err = _stop(p, timeout=20) if p.wait(timeout=15) is not None else (None, "")
+    finally:
+        kub.close()
+    assert rc == 3 and "no ListAndWatch stream within 1s" in err and time.monotonic() - t0 < 10
+    assert not os.path.exists(os.path.join(kdir, "amd.com_gpu"))      # sockets removed on the way out
+
+
+def test_daemon_refuses_python_only_flags_and_bad_liveness(tmp_path):
+    for args, want in ((["-perf_check_every", "3"], "Python entrypoint"),
+                       (["-liveness"], "-pulse > 0"),
+                       (["-liveness_mode", "bogus"], "liveness_mode"),
+                       (["-vmodule", "nolevel"], "vmodule")):
+        p = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=20)
+        assert p.returncode == 1 and want in p.stderr, (args, p.stderr)
