@@ -21,12 +21,16 @@
 //   watch        ?watch=1&fieldSelector=metadata.name=<node>: a node re-created
 //                or a label stripped is relabelled at once (the reference
 //                reconciles on Create events, main.go:551-577); 410 re-lists;
-//                reconnects with backoff; labels re-asserted every -resync
+//                reconnects with backoff; labels re-asserted every -resync.
+//                -resync 0 is the reference's controller: label at start and
+//                again only when the Node object is re-created (an ADDED event),
+//                never exiting; -once applies once and exits (a Job)
 //   topology     kfd generation_id + partition modes polled every
 //                -topology_watch s: a partition switch relabels at once
-//
-// -kubeconfig (out-of-cluster) is served by the Python CLI
-// (scripts/k8s-node-labeller); this binary is the in-cluster DaemonSet entrypoint.
+//   config       -kubeconfig, else in-cluster unless $KUBECONFIG is set, else
+//                $KUBECONFIG / $HOME/.kube/config (controller-runtime's order,
+//                config.go:116-156): token, tokenFile or client-certificate auth
+//   logging      glog's flags and output rules (mi355x/glog.h)
 #include <fcntl.h>
 #include <poll.h>
 #include <signal.h>
@@ -50,6 +54,8 @@
 
 #include "../kube/http.h"
 #include "../kube/json.h"
+#include "../kube/kubeconfig.h"
+#include "mi355x/glog.h"
 #include "mi355x/drm_query.h"
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/kfd_topology.h"
@@ -61,24 +67,6 @@ namespace {
 
 using namespace mi355x;
 using Labels = std::map<std::string, std::string>;
-
-// ---- logging (glog line format) --------------------------------------------
-int g_verbosity = 0;
-
-void logf(char sev, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-void logf(char sev, const char* fmt, ...) {
-  timespec ts{};
-  clock_gettime(CLOCK_REALTIME, &ts);
-  tm t{};
-  localtime_r(&ts.tv_sec, &t);
-  char msg[2048];
-  va_list ap;
-  va_start(ap, fmt);
-  std::vsnprintf(msg, sizeof(msg), fmt, ap);
-  va_end(ap);
-  std::fprintf(stderr, "%c%02d%02d %02d:%02d:%02d.%06ld %7d node_labeller_main.cpp] %s\n", sev, t.tm_mon + 1,
-               t.tm_mday, t.tm_hour, t.tm_min, t.tm_sec, ts.tv_nsec / 1000, static_cast<int>(getpid()), msg);
-}
 
 // ---- label kinds (constants.go:21 order, then the opt-in additions) ------------
 const std::vector<std::string> kKinds = {
@@ -97,6 +85,7 @@ struct Flags {
   bool watch = true;
   double topology_watch_s = 5.0;
   bool dry_run = false;
+  bool once = false;
   std::string sysfs_root = "/sys";
   std::string dev_root = "/dev";
   std::string sa_dir = "/var/run/secrets/kubernetes.io/serviceaccount";
@@ -105,6 +94,7 @@ struct Flags {
   std::string ca_file;
   double watch_backoff_max_s = 30.0;
   int watch_timeout_s = 300;
+  glog::Options log;
 };
 
 bool parse_bool(const std::string& v, bool* out) {
@@ -125,9 +115,8 @@ bool parse_double(const std::string& v, double* out) {
 bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
   for (const auto& k : kKinds) f->enabled[k] = false;
   if (const char* n = std::getenv("DS_NODE_NAME")) f->node_name = n;
-  static const std::set<std::string> kBool = {"watch", "dry_run", "logtostderr", "alsologtostderr"};
-  static const std::set<std::string> kIgnoredValue = {"stderrthreshold", "log_dir", "vmodule", "log_backtrace_at",
-                                                      "log_format"};
+  static const std::set<std::string> kBool = {"watch", "dry_run", "once"};
+  static const std::set<std::string> kIgnoredValue = {"log_format"};
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a.size() < 2 || a[0] != '-') return *err = "unexpected argument " + a, false;
@@ -142,14 +131,20 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
     }
     if (name == "h" || name == "help") {
       std::printf("usage: %s [-<label kind> ...] [-driver_type container|vf-passthrough|pf-passthrough] "
-                  "[-node_name NAME] [-resync S] [-watch=false] [-topology_watch S] [-dry_run] "
-                  "[-sysfs_root DIR] [-dev_root DIR] (glog flags accepted)\nlabel kinds:",
+                  "[-node_name NAME] [-kubeconfig PATH] [-resync S] [-once] [-watch=false] [-topology_watch S] "
+                  "[-dry_run] [-sysfs_root DIR] [-dev_root DIR] [-v N] [-logtostderr] [-alsologtostderr] "
+                  "[-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] [-log_backtrace_at FILE:N]\nlabel kinds:",
                   argv[0]);
       for (const auto& k : kKinds) std::printf(" -%s", k.c_str());
       std::printf("\n");
       std::exit(0);
     }
     const bool is_kind = f->enabled.count(name) > 0;
+    if (glog::is_bool_flag(name)) {
+      glog::parse_flag(name, value, has_value, &f->log, err);
+      if (!err->empty()) return false;
+      continue;
+    }
     if (is_kind || kBool.count(name)) {
       bool v = true;
       if (has_value && !parse_bool(value, &v))
@@ -157,13 +152,16 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       if (is_kind) f->enabled[name] = v;
       if (name == "watch") f->watch = v;
       if (name == "dry_run") f->dry_run = v;
+      if (name == "once") f->once = v;
       continue;
     }
     if (!has_value) {
       if (i + 1 >= argc) return *err = "flag needs an argument: -" + name, false;
       value = argv[++i];
     }
-    if (name == "driver_type") {
+    if (glog::parse_flag(name, value, true, &f->log, err)) {
+      if (!err->empty()) return false;
+    } else if (name == "driver_type") {
       f->driver_type = value;
     } else if (name == "node_name") {
       f->node_name = value;
@@ -191,8 +189,6 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       f->token_file = value;
     } else if (name == "ca_file") {
       f->ca_file = value;
-    } else if (name == "v") {
-      g_verbosity = std::atoi(value.c_str());
     } else if (!kIgnoredValue.count(name)) {
       return *err = "flag provided but not defined: -" + name, false;
     }
@@ -293,13 +289,13 @@ void gen_firmware(Ctx& c, Labels* out) {
   for (const auto& g : c.gpus) {
     const auto node = c.drm_node(g);
     if (!node) {
-      logf('E', "Fail to get firmware versions: no drm node");
+      MI_LOG(kError, "Fail to get firmware versions: no drm node");
       continue;
     }
     auto it = c.drm_fw.find(*node);
     if (it == c.drm_fw.end()) it = c.drm_fw.emplace(*node, drm_query_firmware(c.dev, c.sysfs, *node)).first;
     if (!it->second.ok) {
-      logf('E', "Fail to get firmware versions: %s", it->second.error.c_str());
+      MI_LOG(kError, "Fail to get firmware versions: %s", it->second.error.c_str());
       continue;
     }
     for (const auto& [name, ver] : it->second.feature) counts[name + ".feat." + std::to_string(ver)]++;
@@ -314,13 +310,13 @@ void gen_family(Ctx& c, Labels* out) {
   for (const auto& g : c.gpus) {
     const auto node = c.drm_node(g);
     if (!node) {
-      logf('E', "Fail to get card family name: no drm node");
+      MI_LOG(kError, "Fail to get card family name: no drm node");
       continue;
     }
     auto it = c.drm_info.find(*node);
     if (it == c.drm_info.end()) it = c.drm_info.emplace(*node, drm_query_gpu_info(c.dev, c.sysfs, *node)).first;
     if (!it->second.ok) {
-      logf('E', "Fail to get card family name: %s", it->second.error.c_str());
+      MI_LOG(kError, "Fail to get card family name: %s", it->second.error.c_str());
       continue;
     }
     counts[it->second.family]++;
@@ -501,7 +497,7 @@ Labels container_labels(const Flags& f) {
     c.gpus = discover_gpus(f.sysfs_root, c.topo).devices;
   }
   if (c.gpus.empty()) {
-    logf('I', "No AMD GPUs found, skipping label generation");
+    MI_LOG(kInfo, "No AMD GPUs found, skipping label generation");
     return out;
   }
   for (const auto& [name, gen] : kGenerators)
@@ -693,7 +689,7 @@ class Labeller {
       return fail("reconcile of node " + f_.node_name + " failed: " + describe(r));
     }
     ++st.patches;
-    logf('I', "node labels updated node=%s changed=%zu", f_.node_name.c_str(), patch.size());
+    MI_LOG(kInfo, "node labels updated node=%s changed=%zu", f_.node_name.c_str(), patch.size());
     return true;
   }
 
@@ -706,7 +702,7 @@ class Labeller {
  private:
   bool fail(const std::string& msg) {
     ++st.errors;
-    logf('E', "%s", msg.c_str());
+    MI_LOG(kError, "%s", msg.c_str());
     return false;
   }
 
@@ -797,44 +793,64 @@ int main(int argc, char** argv) {
   Flags f;
   std::string err;
   if (!parse_flags(argc, argv, &f, &err)) {
-    logf('E', "%s", err.c_str());
+    glog::init(f.log);
+    MI_LOG(kError, "%s", err.c_str());
+    return 1;
+  }
+  if (f.log.program.empty()) f.log.program = "k8s-node-labeller";
+  err = glog::init(f.log);
+  if (!err.empty()) {
+    glog::init(glog::Options());
+    MI_LOG(kError, "%s", err.c_str());
     return 1;
   }
   if (f.dry_run) {
     print_json(generate_labels(f));
     return 0;
   }
-  logf('I', "AMD GPU Node Labeller for Kubernetes (MI355X-native, native daemon)");
-  if (!f.kubeconfig.empty()) {
-    logf('E', "-kubeconfig (out-of-cluster) is served by the Python labeller (scripts/k8s-node-labeller); this "
-              "binary runs in-cluster");
-    return 1;
-  }
+  MI_LOG(kInfo, "AMD GPU Node Labeller for Kubernetes (MI355X-native, native daemon)");
   f.node_name = node_name_from(f);
   if (f.node_name.empty()) {
-    logf('E', "node name unknown: set DS_NODE_NAME or -node_name (or mount /labeller/hostname)");
+    MI_LOG(kError, "node name unknown: set DS_NODE_NAME or -node_name (or mount /labeller/hostname)");
     return 1;
   }
   Kube kube;
-  if (!f.apiserver.empty()) {
+  // controller-runtime GetConfigOrDie: -kubeconfig, else in-cluster unless
+  // $KUBECONFIG is set, else $KUBECONFIG / $HOME/.kube/config
+  const char* svc_host = std::getenv("KUBERNETES_SERVICE_HOST");
+  const bool in_cluster = (svc_host && *svc_host) || !f.apiserver.empty();
+  const std::string kc_path = !f.kubeconfig.empty() ? f.kubeconfig : kube::default_kubeconfig_path(in_cluster);
+  if (!kc_path.empty()) {
+    auto kc = kube::load_kubeconfig(kc_path, &err);
+    if (!kc) {
+      MI_LOG(kError, "unable to set up kubernetes client: %s", err.c_str());
+      return 1;
+    }
+    kube.cfg = kc->http;
+    kube.token = kc->token;
+    kube.token_file = kc->token_file;
+    MI_LOG(kInfo, "kubeconfig %s: server %s", kc_path.c_str(), kube.cfg.server.c_str());
+  } else if (!f.apiserver.empty()) {
     kube.cfg.server = f.apiserver;
   } else {
     const char* host = std::getenv("KUBERNETES_SERVICE_HOST");
     const char* port = std::getenv("KUBERNETES_SERVICE_PORT");
     if (!host || !*host) {
-      logf('E', "unable to set up kubernetes client: not running in a cluster (KUBERNETES_SERVICE_HOST unset)");
+      MI_LOG(kError, "unable to set up kubernetes client: not running in a cluster (KUBERNETES_SERVICE_HOST unset)");
       return 1;
     }
     std::string h = host;
     if (h.find(':') != std::string::npos && h[0] != '[') h = "[" + h + "]";
     kube.cfg.server = "https://" + h + ":" + (port && *port ? port : "443");
   }
-  kube.token_file = !f.token_file.empty() ? f.token_file : path_join(f.sa_dir, "token");
-  kube.cfg.ca_file = !f.ca_file.empty() ? f.ca_file
-                     : path_exists(path_join(f.sa_dir, "ca.crt")) ? path_join(f.sa_dir, "ca.crt")
-                                                                   : "";
-  if (kube.bearer().empty() && f.apiserver.empty()) {
-    logf('E', "unable to set up kubernetes client: service-account token %s is unreadable or empty",
+  if (kc_path.empty()) {
+    kube.token_file = !f.token_file.empty() ? f.token_file : path_join(f.sa_dir, "token");
+    kube.cfg.ca_file = !f.ca_file.empty() ? f.ca_file
+                       : path_exists(path_join(f.sa_dir, "ca.crt")) ? path_join(f.sa_dir, "ca.crt")
+                                                                     : "";
+  }
+  if (kc_path.empty() && kube.bearer().empty() && f.apiserver.empty()) {
+    MI_LOG(kError, "unable to set up kubernetes client: service-account token %s is unreadable or empty",
          kube.token_file.c_str());
     return 1;
   }
@@ -850,8 +866,7 @@ int main(int argc, char** argv) {
   kube.wake_fd = g_sig_pipe[0];
 
   Labeller lab(f, &kube);
-  const bool once = f.resync_s <= 0;
-  if (once) {  // the reference: compute and apply once
+  if (f.once) {  // apply once and exit (a Job)
     while (!g_stop) {
       if (lab.reconcile()) return 0;
       pollfd p{g_sig_pipe[0], POLLIN, 0};
@@ -859,6 +874,10 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  // -resync 0: the reference's controller (main.go:553-586): label at start,
+  // then only when the Node object is (re-)created; no periodic re-assert
+  const bool created_only = f.resync_s <= 0;
+  const double resync_s = created_only ? 3600.0 * 24 * 365 : f.resync_s;
 
   bool kick = true;
   auto next_resync = clk::now();
@@ -881,7 +900,7 @@ int main(int argc, char** argv) {
     if (kick || clk::now() >= next_resync) {
       kick = false;
       const bool ok = lab.reconcile();
-      next_resync = after_s(ok ? f.resync_s : 5.0);
+      next_resync = after_s(ok ? resync_s : 5.0);
     }
     if (topo_watch && clk::now() >= next_topo) {
       next_topo = after_s(f.topology_watch_s);
@@ -890,7 +909,7 @@ int main(int argc, char** argv) {
       if (cur != topo_last && cur == topo_seen) {
         topo_last = cur;
         ++lab.st.topology_changes;
-        logf('I', "GPU topology changed (partition switch?): relabelling node %s", f.node_name.c_str());
+        MI_LOG(kInfo, "GPU topology changed (partition switch?): relabelling node %s", f.node_name.c_str());
         kick = true;
       }
       topo_seen = cur;
@@ -912,7 +931,7 @@ int main(int argc, char** argv) {
         if (status == 410) rv.clear();
         if (status == 401) kube.bearer(true);
         ++lab.st.watch_errors;
-        logf('W', "watch of node %s failed (%s); retrying in %.1fs", f.node_name.c_str(),
+        MI_LOG(kWarning, "watch of node %s failed (%s); retrying in %.1fs", f.node_name.c_str(),
              e.empty() ? ("HTTP " + std::to_string(status) + ": " + ebody.substr(0, 200)).c_str() : e.c_str(),
              backoff);
         stream.close();
@@ -955,7 +974,7 @@ int main(int argc, char** argv) {
       if (obj) {
         const json::Value* md = obj->get("metadata");
         if (md && !md->str("resourceVersion").empty()) rv = md->str("resourceVersion");
-        if ((type == "ADDED" || type == "MODIFIED") && lab.needs_reconcile(*obj)) {
+        if ((type == "ADDED" || (type == "MODIFIED" && !created_only)) && lab.needs_reconcile(*obj)) {
           ++lab.st.watch_kicks;
           kick = true;
         }
@@ -972,13 +991,13 @@ int main(int argc, char** argv) {
     } else {
       if (rc != 0) {
         ++lab.st.watch_errors;
-        logf('W', "watch of node %s broke; retrying in %.1fs", f.node_name.c_str(), backoff);
+        MI_LOG(kWarning, "watch of node %s broke; retrying in %.1fs", f.node_name.c_str(), backoff);
       }
       watch_retry = after_s(backoff);  // a server that ends every stream at once is not hammered
       backoff = std::min(backoff * 2, f.watch_backoff_max_s);
     }
   }
-  logf('I', "Received signal, shutting down. passes=%d patches=%d updates=%d errors=%d watch_events=%d "
+  MI_LOG(kInfo, "Received signal, shutting down. passes=%d patches=%d updates=%d errors=%d watch_events=%d "
             "watch_kicks=%d watch_errors=%d watch_restarts=%d topology_changes=%d",
        lab.st.passes, lab.st.patches, lab.st.updates, lab.st.errors, lab.st.watch_events, lab.st.watch_kicks,
        lab.st.watch_errors, lab.st.watch_restarts, lab.st.topology_changes);

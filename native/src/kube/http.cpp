@@ -1,5 +1,8 @@
 #include "http.h"
 
+#include <openssl/err.h>
+#include <openssl/pem.h>
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -136,9 +139,53 @@ std::string Conn::open(const Config& cfg) {
   SSL_CTX_set_min_proto_version(ctx_, TLS1_2_VERSION);
   if (!cfg.insecure) {
     SSL_CTX_set_verify(ctx_, SSL_VERIFY_PEER, nullptr);
-    const int ok = cfg.ca_file.empty() ? SSL_CTX_set_default_verify_paths(ctx_)
-                                       : SSL_CTX_load_verify_locations(ctx_, cfg.ca_file.c_str(), nullptr);
-    if (ok != 1) return "CA " + cfg.ca_file + ": " + ssl_error();
+    if (!cfg.ca_pem.empty()) {
+      X509_STORE* store = SSL_CTX_get_cert_store(ctx_);
+      BIO* bio = BIO_new_mem_buf(cfg.ca_pem.data(), static_cast<int>(cfg.ca_pem.size()));
+      int n = 0;
+      while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
+        X509_STORE_add_cert(store, x);
+        X509_free(x);
+        ++n;
+      }
+      BIO_free(bio);
+      ERR_clear_error();
+      if (n == 0) return "CA data: no PEM certificate";
+    } else {
+      const int ok = cfg.ca_file.empty() ? SSL_CTX_set_default_verify_paths(ctx_)
+                                         : SSL_CTX_load_verify_locations(ctx_, cfg.ca_file.c_str(), nullptr);
+      if (ok != 1) return "CA " + cfg.ca_file + ": " + ssl_error();
+    }
+  }
+  // client certificate (kubeconfig client-certificate / -data, client-key / -data)
+  if (!cfg.cert_file.empty() || !cfg.cert_pem.empty()) {
+    bool ok;
+    if (!cfg.cert_pem.empty()) {
+      BIO* bio = BIO_new_mem_buf(cfg.cert_pem.data(), static_cast<int>(cfg.cert_pem.size()));
+      X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+      ok = x && SSL_CTX_use_certificate(ctx_, x) == 1;
+      while (ok) {  // the rest of the chain
+        X509* extra = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+        if (!extra) break;
+        if (SSL_CTX_add_extra_chain_cert(ctx_, extra) != 1) X509_free(extra);
+      }
+      ERR_clear_error();
+      if (x) X509_free(x);
+      BIO_free(bio);
+    } else {
+      ok = SSL_CTX_use_certificate_chain_file(ctx_, cfg.cert_file.c_str()) == 1;
+    }
+    if (!ok) return "client certificate: " + ssl_error();
+    if (!cfg.key_pem.empty()) {
+      BIO* bio = BIO_new_mem_buf(cfg.key_pem.data(), static_cast<int>(cfg.key_pem.size()));
+      EVP_PKEY* k = PEM_read_bio_PrivateKey(bio, nullptr, nullptr, nullptr);
+      ok = k && SSL_CTX_use_PrivateKey(ctx_, k) == 1;
+      if (k) EVP_PKEY_free(k);
+      BIO_free(bio);
+    } else {
+      ok = !cfg.key_file.empty() && SSL_CTX_use_PrivateKey_file(ctx_, cfg.key_file.c_str(), SSL_FILETYPE_PEM) == 1;
+    }
+    if (!ok || SSL_CTX_check_private_key(ctx_) != 1) return "client key: " + ssl_error();
   }
   ssl_ = SSL_new(ctx_);
   if (!ssl_) return ssl_error();

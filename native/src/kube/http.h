@@ -15,7 +15,10 @@ namespace mi355x::http {
 
 struct Config {
   std::string server;   // https://host:port or http://host:port
-  std::string ca_file;  // empty: system trust store
+  std::string ca_file;  // empty: system trust store (unless ca_pem)
+  std::string ca_pem;   // CA bundle in memory (kubeconfig certificate-authority-data)
+  // client certificate auth (kubeconfig users[].user): files or PEM in memory
+  std::string cert_file, key_file, cert_pem, key_pem;
   bool insecure = false;
   double timeout_s = 15.0;
 };

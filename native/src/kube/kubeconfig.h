@@ -1,0 +1,38 @@
+// kubeconfig for the native node labeller: the reference labeller takes
+// -kubeconfig through controller-runtime (vendor/sigs.k8s.io/controller-runtime/
+// pkg/client/config/config.go:32-58,116-156): the flag, else in-cluster when
+// $KUBECONFIG is unset, else $KUBECONFIG / $HOME/.kube/config.
+//
+// The file is YAML (or JSON). Only what a client needs is read: the current
+// context's cluster (server, certificate-authority[-data],
+// insecure-skip-tls-verify) and user (token, tokenFile,
+// client-certificate[-data], client-key[-data]); relative paths resolve
+// against the file's directory, as clientcmd does.
+#pragma once
+
+#include <optional>
+#include <string>
+
+#include "http.h"
+#include "json.h"
+
+namespace mi355x::kube {
+
+struct KubeConfig {
+  http::Config http;       // server, CA, client certificate, insecure
+  std::string token;       // static bearer token
+  std::string token_file;  // re-read when it changes
+};
+
+// The YAML subset kubeconfig files use (block and flow mappings / sequences,
+// plain and quoted scalars, literal block scalars, comments) as a JSON value.
+std::optional<json::Value> parse_yaml(const std::string& text, std::string* error);
+
+std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* error);
+
+// controller-runtime's order after the flag: in-cluster unless $KUBECONFIG is
+// set, then $KUBECONFIG (first existing entry) or $HOME/.kube/config.
+// Returns "" when none applies (callers then use the in-cluster config).
+std::string default_kubeconfig_path(bool in_cluster_available);
+
+}  // namespace mi355x::kube

@@ -3,7 +3,7 @@
 Reference: cmd/k8s-node-labeller/main.go:507-590 — one boolean flag per
 label kind (``-vram``, ``-cu-count``, ...), ``-driver_type``, ``-kubeconfig``,
 node name from ``$DS_NODE_NAME``. Same flags here; additions: ``-resync``
-(periodic re-assert; 0 = apply once like the reference), ``-dry_run`` (print
+(periodic re-assert; 0 = as the reference: at start and on Node re-creation), ``-once``, ``-dry_run`` (print
 the labels as JSON and exit), ``-sysfs_root`` / ``-dev_root``, and the opt-in
 extra kinds ``-gfx-target`` / ``-xgmi-hive-count`` / ``-xgmi-links-down``.
 """
@@ -32,12 +32,14 @@ def build_parser() -> flags.GoFlagParser:
     p.add_str("kubeconfig", "", "Paths to a kubeconfig. Only required if out-of-cluster.")
     flags.add_glog_flags(p)
     p.add_str("node_name", os.environ.get("DS_NODE_NAME", ""), "node to label (default $DS_NODE_NAME)")
-    p.add_float("resync", 300.0, "seconds between label re-asserts (0 = apply once and exit)")
+    p.add_float("resync", 300.0, "seconds between label re-asserts (0 = as upstream: label at start and whenever "
+                                 "the Node object is re-created, no periodic re-assert)")
     p.add_bool("watch", True, "watch the node and re-apply labels as soon as they are stripped or the node is "
                               "re-created (needs the 'watch' verb on nodes, as in the upstream ClusterRole)")
     p.add_float("topology_watch", 5.0, "seconds between checks of the GPU topology (kfd generation_id, partition "
                                        "modes); a change relabels the node at once (0 = off: next resync)")
     p.add_bool("dry_run", False, "print the generated labels as JSON and exit")
+    p.add_bool("once", False, "apply the labels once and exit (e.g. from a Job instead of the DaemonSet)")
     p.add_str("sysfs_root", "/sys", "sysfs mount to read")
     p.add_str("dev_root", "/dev", "device node directory")
     p.add_str("log_format", "glog", "glog | json")
@@ -96,7 +98,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                        change_source=lambda: topology_signature(ns.sysfs_root), change_interval_s=ns.topology_watch)
     for s in (signal.SIGTERM, signal.SIGINT):
         signal.signal(s, lambda *_: lab.stop())
-    lab.run(once=ns.resync <= 0)
+    lab.run(once=ns.once, created_only=not ns.once and ns.resync <= 0)
     return 0
 
 

@@ -84,6 +84,7 @@ class NodeLabeller:
         self.change_source = change_source
         self.change_interval_s = change_interval_s
         self._change_thread: Optional[threading.Thread] = None
+        self._created_only = False
 
     def reconcile_once(self) -> bool:
         """Returns True on success (whether or not a patch was needed)."""
@@ -157,7 +158,8 @@ class NodeLabeller:
                     rv = (obj.get("metadata") or {}).get("resourceVersion")
                     if rv:
                         self._rv = rv
-                    if typ in ("ADDED", "MODIFIED") and self._needs_reconcile(obj):
+                    kinds = ("ADDED",) if self._created_only else ("ADDED", "MODIFIED")
+                    if typ in kinds and self._needs_reconcile(obj):
                         self.stats.watch_kicks += 1
                         self._kick.set()
                 # a stream that lived its timeout reconnects at once; one the
@@ -209,7 +211,12 @@ class NodeLabeller:
                 self._kick.set()
             seen = cur
 
-    def run(self, once: bool = False) -> None:
+    def run(self, once: bool = False, created_only: bool = False) -> None:
+        """once: apply the labels and return. created_only: the reference's
+        controller (cmd/k8s-node-labeller/main.go:553-586) -- label at start,
+        then again only when the Node object is (re-)created (a watch ADDED
+        event whose labels differ); no periodic re-assert, never exits."""
+        self._created_only = created_only
         if self.watch and not once and self._watch_thread is None:
             self._watch_thread = threading.Thread(target=self._watch_loop, name="node-watch", daemon=True)
             self._watch_thread.start()
@@ -223,6 +230,8 @@ class NodeLabeller:
             if once and ok:
                 return
             wait = self.resync_s if ok else self.retry_s
+            if created_only and ok:
+                wait = 3600.0   # until a watch event kicks
             if wait <= 0:
                 if ok and not self.watch:
                     return

@@ -29,7 +29,10 @@ def merge_patch(target, patch):
 
 
 class FakeApiServer:
-    def __init__(self, token: Optional[str] = "test-token", tls: Optional[Tuple[str, str]] = None):
+    def __init__(self, token: Optional[str] = "test-token", tls: Optional[Tuple[str, str]] = None,
+                 client_ca: Optional[str] = None):
+        """tls: (cert chain PEM, key PEM) to serve HTTPS; client_ca: also require
+        a client certificate signed by this CA (kubeconfig client-certificate auth)."""
         self.token = token
         self.nodes: Dict[str, dict] = {}
         self.requests: List[Tuple[str, str, Optional[dict]]] = []
@@ -167,6 +170,9 @@ class FakeApiServer:
             import ssl
             ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
             ctx.load_cert_chain(*tls)
+            if client_ca:
+                ctx.verify_mode = ssl.CERT_REQUIRED
+                ctx.load_verify_locations(client_ca)
             self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True)
             self.scheme = "https"
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)

@@ -286,6 +286,66 @@ def test_corrupted_tile_turns_device_unhealthy_in_listandwatch(inv, ordinals, tm
     asyncio.run(asyncio.wait_for(go(str(tmp_path)), 180))
 
 
+def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_path):
+    """The same fault through the interpreter-free daemon: mi355x-device-plugin
+    -liveness runs the kept-queue probe server on the real GPU; a flipped
+    output bit fails the tile (server and fresh-process confirmation), the
+    kubelet's ListAndWatch shows the device Unhealthy, clearing the fault
+    brings it back, and SIGTERM takes the probe server down with the daemon."""
+    import signal
+    from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+
+    exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    dev_id, o = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
+    fault = tmp_path / "corrupt"
+    fault.write_text("")
+    kdir = str(tmp_path / "dp")
+
+    async def wait_health(k, want, timeout):
+        deadline = asyncio.get_running_loop().time() + timeout
+        while True:
+            st = k.resources["amd.com/gpu"]
+            if st.devices.get(dev_id) == want:
+                return
+            left = deadline - asyncio.get_running_loop().time()
+            assert left > 0, f"{dev_id} never became {want}: {st.devices}"
+            try:
+                await k.wait_for_update("amd.com/gpu", st.updates, timeout=min(left, 2.0))
+            except TimeoutError:
+                pass
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        env = dict(os.environ, MI355X_PROBE_CORRUPT_FILE=str(fault))
+        proc = await asyncio.create_subprocess_exec(
+            exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_timeout", "30",
+            "-liveness_fail_threshold", "2", stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE,
+            env=env)
+        try:
+            await k.wait_for_resource("amd.com/gpu", 1, timeout=60)
+            await wait_health(k, "Healthy", 60)
+            fault.write_text("17")
+            await wait_health(k, "Unhealthy", 60)
+            fault.write_text("")
+            await wait_health(k, "Healthy", 60)
+        finally:
+            if proc.returncode is None:
+                proc.send_signal(signal.SIGTERM)
+            _, err = await asyncio.wait_for(proc.communicate(), 30)
+            await k.stop()
+        err = err.decode(errors="replace")
+        assert proc.returncode == 0, err[-3000:]
+        assert f"device {dev_id}: Healthy -> Unhealthy liveness probe:" in err and "differ" in err, err[-3000:]
+        return err
+
+    asyncio.run(asyncio.wait_for(go(), 240))
+    # no probe server left behind
+    left = subprocess.run(["pgrep", "-f", "mi355x-liveness-probe --serve"], capture_output=True, text=True)
+    assert left.stdout.strip() == "", left.stdout
+
+
 def test_probe_cli_corrupt_word_fails_the_tile():
     from rocm_k8s_device_plugin_amd.ops.native import probe_executable
     p = subprocess.run([str(probe_executable("hsa")), "--devices", "0", "--corrupt-word", "3"], capture_output=True,

@@ -252,7 +252,7 @@ def test_labeller_cli_against_fake_apiserver(tmp_path):
         kc.write_text(f"clusters: [{{name: a, cluster: {{server: '{srv.url}'}}}}]\n"
                       "contexts: [{name: a, context: {cluster: a, user: a}}]\ncurrent-context: a\n"
                       "users: [{name: a, user: {}}]\n")
-        rc = node_labeller.main(["-kubeconfig", str(kc), "-node_name", "worker-7", "-resync", "0",
+        rc = node_labeller.main(["-kubeconfig", str(kc), "-node_name", "worker-7", "-once",
                                  "-mode", "-vram", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)])
         assert rc == 0
         got = srv.labels("worker-7")
@@ -523,7 +523,7 @@ def test_labeller_in_cluster_over_tls(tmp_path, monkeypatch):
         monkeypatch.setenv("KUBERNETES_SERVICE_PORT", str(srv.port))
         cfg = kube.in_cluster_config(str(sa))
         assert cfg.server == f"https://127.0.0.1:{srv.port}" and cfg.ca_file == str(sa / "ca.crt")
-        rc = node_labeller.main(["-node_name", "worker-9", "-resync", "0", "-mode", "-cu-count",
+        rc = node_labeller.main(["-node_name", "worker-9", "-once", "-mode", "-cu-count",
                                  "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)])
         assert rc == 0
         got = srv.labels("worker-9")

@@ -1,0 +1,280 @@
+"""glog behaviour and kubeconfig handling of the native binaries.
+
+glog (vendor/github.com/golang/glog/glog_flags.go:388-397, glog_file.go): the
+reference binaries honour -v, -vmodule, -logtostderr=false + -log_dir (one
+file per severity, <program>.<SEV> symlinks), -stderrthreshold and
+-alsologtostderr; a DaemonSet that sets them must not lose its logs when it
+switches to mi355x-device-plugin / mi355x-node-labeller.
+
+kubeconfig (vendor/sigs.k8s.io/controller-runtime/pkg/client/config/
+config.go:32-58,116-156): -kubeconfig, else in-cluster unless $KUBECONFIG is
+set, else $KUBECONFIG; token, tokenFile (relative to the file) and
+client-certificate auth, CA from a file or inline data, block or flow YAML.
+"""
+import base64
+import os
+import signal
+import subprocess
+import time
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+from rocm_k8s_device_plugin_amd.testing import gopeer as gp
+from rocm_k8s_device_plugin_amd.testing.fake_apiserver import FakeApiServer
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+
+DP = os.environ.get("MI355X_NATIVE_DAEMON_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+LBL = os.environ.get("MI355X_NATIVE_LABELLER_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-node-labeller")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("KUBERNETES_SERVICE_HOST", "KUBERNETES_SERVICE_PORT", "KUBECONFIG", "DS_NODE_NAME")}
+    env.update(kw)
+    return env
+
+
+def _wait(pred, timeout=10.0):
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return pred()
+
+
+def _term(p, timeout=20):
+    if p.poll() is None:
+        p.send_signal(signal.SIGTERM)
+    _, err = p.communicate(timeout=timeout)
+    return p.returncode, err
+
+
+# ------------------------------------------------------------------ glog
+
+def test_device_plugin_log_files_per_severity(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    logs = tmp_path / "logs"
+    kdir = tmp_path / "dp"
+    kdir.mkdir()
+    kub = gp.GoServer(str(kdir / "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    p = subprocess.Popen([DP, "-kubelet_dir", str(kdir), "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                          "-exporter_socket", "", "-logtostderr=false", f"-log_dir={logs}", "-vmodule",
+                          "device_plugin_main=2", "-grpc_watchdog", "0"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        assert _wait(lambda: (logs / "k8s-device-plugin.INFO").exists() and
+                     "Registration for endpoint" in (logs / "k8s-device-plugin.INFO").read_text())
+        c = gp.GoClientConn(str(kdir / "amd.com_gpu"))
+        try:
+            assert c.unary("/v1beta1.DevicePlugin/GetDevicePluginOptions", b"", 3.0)[0] == 0
+            a = c.unary("/v1beta1.DevicePlugin/Allocate", b"\x0a\x00", 3.0)    # one empty container request
+            assert a[0] == 0
+        finally:
+            c.close()
+        # -vmodule=device_plugin_main=2: per-RPC lines without -v
+        assert _wait(lambda: "rpc GetDevicePluginOptions resource=gpu" in (logs / "k8s-device-plugin.INFO").read_text())
+    finally:
+        rc, err = _term(p)
+        kub.close()
+    assert rc == 0
+    info = (logs / "k8s-device-plugin.INFO").read_text()
+    target = os.readlink(logs / "k8s-device-plugin.INFO")
+    assert target.startswith("k8s-device-plugin.") and ".log.INFO." in target and target.endswith(f".{p.pid}")
+    assert info.startswith("Log file created at:") and "Log line format: [IWEF]mmdd" in info
+    assert "Found 8 AMDGPUs" in info and "Received signal, shutting down." in info
+    assert "Found 8 AMDGPUs" not in err                     # INFO stays out of stderr (-stderrthreshold=ERROR)
+    assert not (logs / "k8s-device-plugin.ERROR").exists()  # created on first use only
+
+
+def test_labeller_log_files_threshold_and_alsologtostderr(tmp_path):
+    logs = tmp_path / "logs"
+    base = [LBL, "-node_name", "n", "-apiserver", "http://127.0.0.1:9", "-token_file", os.devnull, "-mode",
+            "-logtostderr=false", f"-log_dir={logs}", "-sysfs_root", str(tmp_path)]
+    p = subprocess.Popen(base + ["-once"], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=_env())
+    assert _wait(lambda: (logs / "k8s-node-labeller.ERROR").exists())
+    rc, err = _term(p)
+    assert rc == 0
+    errs = (logs / "k8s-node-labeller.ERROR").read_text()
+    info = (logs / "k8s-node-labeller.INFO").read_text()
+    assert "reconcile of node n failed" in errs and "reconcile of node n failed" in info
+    assert "AMD GPU Node Labeller" in info and "AMD GPU Node Labeller" not in errs
+    assert "reconcile of node n failed" in err and "AMD GPU Node Labeller" not in err
+    # -alsologtostderr: INFO on stderr too; -stderrthreshold=INFO without files: same
+    p = subprocess.Popen(base + ["-once", "-alsologtostderr", f"-log_dir={tmp_path / 'l2'}"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=_env())
+    time.sleep(0.5)
+    rc, err = _term(p)
+    assert "AMD GPU Node Labeller" in err and (tmp_path / "l2" / "k8s-node-labeller.INFO").exists()
+    # a malformed -vmodule is refused, like glog
+    p = subprocess.run([LBL, "-dry_run", "-vmodule", "nolevel"], capture_output=True, text=True, timeout=20)
+    assert p.returncode == 1 and "vmodule" in p.stderr
+
+
+# ------------------------------------------------------------------ kubeconfig
+
+def _tls_material(d, client=False):
+    import shutil
+    if not shutil.which("openssl"):
+        pytest.skip("openssl not installed")
+
+    def run(*a):
+        subprocess.run(["openssl", *a], check=True, capture_output=True, timeout=60)
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "ca.key"), "-out", str(d / "ca.crt"),
+        "-days", "2", "-subj", "/CN=test-ca")
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "srv.key"), "-out", str(d / "srv.csr"),
+        "-subj", "/CN=kubernetes")
+    (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1,DNS:kubernetes.default.svc\n")
+    run("x509", "-req", "-in", str(d / "srv.csr"), "-CA", str(d / "ca.crt"), "-CAkey", str(d / "ca.key"),
+        "-CAcreateserial", "-out", str(d / "srv.crt"), "-days", "2", "-extfile", str(d / "ext.cnf"))
+    if client:
+        run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "cli.key"), "-out", str(d / "cli.csr"),
+            "-subj", "/CN=system:node:worker/O=system:nodes")
+        run("x509", "-req", "-in", str(d / "cli.csr"), "-CA", str(d / "ca.crt"), "-CAkey", str(d / "ca.key"),
+            "-CAcreateserial", "-out", str(d / "cli.crt"), "-days", "2")
+
+
+def _label_once(kc, fi, env=None, extra=()):
+    argv = [LBL, "-node_name", "worker", "-once", "-mode", "-vram", "-sysfs_root", str(fi.sysfs), "-dev_root",
+            str(fi.dev), *extra]
+    if kc is not None:
+        argv += ["-kubeconfig", str(kc)]
+    return subprocess.run(argv, capture_output=True, text=True, timeout=60, env=env or _env())
+
+
+def test_kubeconfig_token_file_relative_block_yaml(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="kc-token").start()
+    try:
+        srv.add_node("worker")
+        d = tmp_path / "cfg"
+        d.mkdir()
+        (d / "tok").write_text("kc-token\n")
+        kc = d / "config"
+        kc.write_text(f"""# a kubeconfig as kubectl writes it
+apiVersion: v1
+kind: Config
+clusters:
+- cluster:
+    server: "{srv.url}/"
+  name: other
+- name: lab
+  cluster:
+    server: {srv.url}
+contexts:
+- context:
+    cluster: lab
+    user: robot   # the labeller's identity
+  name: lab-ctx
+current-context: lab-ctx
+preferences: {{}}
+users:
+- name: robot
+  user:
+    tokenFile: tok
+""")
+        p = _label_once(kc, fi)
+        assert p.returncode == 0, p.stderr
+        got = srv.labels("worker")
+        assert got["amd.com/gpu.mode"] == "container" and got["amd.com/gpu.vram"] == "288G"
+    finally:
+        srv.stop()
+
+
+def test_kubeconfig_flow_yaml_static_token_and_env_order(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="t0").start()
+    try:
+        srv.add_node("worker")
+        kc = tmp_path / "kc"
+        kc.write_text(f"clusters: [{{name: a, cluster: {{server: '{srv.url}'}}}}]\n"
+                      "contexts: [{name: a, context: {cluster: a, user: a}}]\ncurrent-context: a\n"
+                      "users: [{name: a, user: {token: t0}}]\n")
+        assert _label_once(kc, fi).returncode == 0
+        assert srv.labels("worker")["amd.com/gpu.mode"] == "container"
+        # no flag, no in-cluster env: $KUBECONFIG (first existing entry of the list)
+        srv.set_labels("worker", {})
+        p = _label_once(None, fi, env=_env(KUBECONFIG=f"{tmp_path}/missing:{kc}"))
+        assert p.returncode == 0, p.stderr and srv.labels("worker")["amd.com/gpu.mode"] == "container"
+        # a JSON kubeconfig is YAML too
+        kj = tmp_path / "kc.json"
+        kj.write_text('{"clusters": [{"name": "a", "cluster": {"server": "%s"}}], "users": [{"name": "a", "user": '
+                      '{"token": "t0"}}], "contexts": [{"name": "a", "context": {"cluster": "a", "user": "a"}}], '
+                      '"current-context": "a"}' % srv.url)
+        assert _label_once(kj, fi).returncode == 0
+        # a wrong token: a clear error, retried (as the reference's controller retries)
+        kc.write_text(kc.read_text().replace("token: t0", "token: nope"))
+        p = subprocess.Popen([LBL, "-node_name", "worker", "-once", "-mode", "-sysfs_root", str(fi.sysfs),
+                              "-kubeconfig", str(kc)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                             env=_env())
+        time.sleep(0.8)
+        rc, err = _term(p)
+        assert rc == 0 and "HTTP 401" in err
+    finally:
+        srv.stop()
+
+
+@pytest.mark.parametrize("inline", [True, False])
+def test_kubeconfig_client_certificate_over_tls(tmp_path, inline):
+    """Client-certificate auth against an apiserver that requires it, the CA
+    from certificate-authority-data (or a relative certificate-authority path)."""
+    d = tmp_path / "pki"
+    d.mkdir()
+    _tls_material(d, client=True)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token=None, tls=(str(d / "srv.crt"), str(d / "srv.key")), client_ca=str(d / "ca.crt")).start()
+    try:
+        srv.add_node("worker")
+        b64 = lambda f: base64.b64encode((d / f).read_bytes()).decode()   # noqa: E731
+        if inline:
+            cluster = f"certificate-authority-data: {b64('ca.crt')}"
+            user = f"client-certificate-data: {b64('cli.crt')}\n    client-key-data: {b64('cli.key')}"
+        else:
+            cluster = "certificate-authority: pki/ca.crt"
+            user = "client-certificate: pki/cli.crt\n    client-key: pki/cli.key"
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(f"""clusters:
+- name: c
+  cluster:
+    server: {srv.url}
+    {cluster}
+contexts:
+- name: x
+  context: {{cluster: c, user: u}}
+current-context: x
+users:
+- name: u
+  user:
+    {user}
+""")
+        p = _label_once(kc, fi)
+        assert p.returncode == 0, p.stderr
+        assert srv.labels("worker")["amd.com/gpu.vram"] == "288G"
+        # without the client certificate the handshake is refused
+        kc.write_text("\n".join(line for line in kc.read_text().splitlines() if "client-" not in line) + "\n")
+        p = subprocess.Popen([LBL, "-node_name", "worker", "-once", "-mode", "-sysfs_root", str(fi.sysfs),
+                              "-kubeconfig", str(kc)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                             env=_env())
+        time.sleep(1.0)
+        rc, err = _term(p)
+        assert "reconcile of node worker failed" in err
+    finally:
+        srv.stop()
+
+
+def test_kubeconfig_errors_are_reported(tmp_path):
+    for text, want in (("clusters: [", "kubeconfig"), ("users: []\n", "no cluster server"),
+                       ("clusters:\n- name: a\n  cluster:\n    server: http://x\n    certificate-authority-data: '%%%'\n",
+                        "base64")):
+        kc = tmp_path / "kc"
+        kc.write_text(text)
+        p = subprocess.run([LBL, "-node_name", "n", "-kubeconfig", str(kc)], capture_output=True, text=True,
+                           timeout=20, env=_env())
+        assert p.returncode == 1 and want in p.stderr, (text, p.stderr)

@@ -94,8 +94,8 @@ def test_flags_follow_go_syntax(tmp_path):
         assert p.returncode == 1, bad
     p = subprocess.run([EXE, "-h"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 0 and "-compute-memory-partition" in p.stdout
-    # out-of-cluster kubeconfig is the Python CLI's job; no cluster env -> clear error
-    env = {k: v for k, v in os.environ.items() if k not in ("KUBERNETES_SERVICE_HOST", "DS_NODE_NAME")}
+    # an unreadable kubeconfig, no cluster env -> clear errors
+    env = {k: v for k, v in os.environ.items() if k not in ("KUBERNETES_SERVICE_HOST", "DS_NODE_NAME", "KUBECONFIG")}
     p = subprocess.run([EXE, "-node_name", "n", "-kubeconfig", "/x"], capture_output=True, text=True, timeout=30,
                        env=env)
     assert p.returncode == 1 and "kubeconfig" in p.stderr
@@ -131,13 +131,13 @@ def _stop(p):
     return p.returncode, err
 
 
-def test_applies_once_with_resync_zero(tmp_path):
+def test_once_applies_and_exits(tmp_path):
     fi = make_mi355x_node(tmp_path / "n", compute_partition="cpx")
     srv = FakeApiServer(token="tok").start()
     try:
         srv.add_node("node-n", {"amd.com/gpu.vram": "1G", "beta.amd.com/gpu.vram": "1G",
                                 "beta.amd.com/gpu.vram.1G": "8", "keep": "me"})
-        p, _ = _start(fi, srv, tmp_path, "-resync", "0")
+        p, _ = _start(fi, srv, tmp_path, "-once")
         assert p.wait(30) == 0, p.stderr.read()
         want = L.generate_labels({k: k in ("vram", "cu-count", "mode", "device-id", "compute-memory-partition")
                                   for k in KINDS}, "", str(fi.sysfs), str(fi.dev))
@@ -145,6 +145,29 @@ def test_applies_once_with_resync_zero(tmp_path):
         assert got == {**want, "keep": "me"}
         assert [m for m, *_ in srv.requests] == ["GET", "PATCH"]
         assert srv.requests[1][2]["metadata"]["labels"]["beta.amd.com/gpu.vram.1G"] is None
+    finally:
+        srv.stop()
+
+
+def test_resync_zero_is_the_reference_controller(tmp_path):
+    """-resync 0 behaves like the reference's controller (main.go:553-586):
+    labels at start, keeps running, relabels a re-created Node (ADDED), and does
+    not re-assert on other edits (its predicate drops Update events)."""
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    try:
+        srv.add_node("node-n")
+        p, _ = _start(fi, srv, tmp_path, "-resync", "0")
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.mode") == "container", 10), p.stderr
+        assert _wait(lambda: srv.watch_starts >= 1, 5)
+        srv.set_labels("node-n", {"other": "x"})            # an edit strips them: not re-asserted
+        time.sleep(1.5)
+        assert "amd.com/gpu.mode" not in srv.labels("node-n") and p.poll() is None
+        srv.delete_node("node-n")
+        srv.add_node("node-n")                              # the node object is re-created: relabelled
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.mode") == "container", 10)
+        rc, err = _stop(p)
+        assert rc == 0, err
     finally:
         srv.stop()
 
@@ -188,7 +211,7 @@ def test_update_fallback_when_patch_is_forbidden(tmp_path):
     try:
         srv.add_node("node-n", {"amd.com/gpu.family": "AI", "keep": "me"})
         srv.forbid = {"PATCH"}
-        p, _ = _start(fi, srv, tmp_path, "-resync", "0")
+        p, _ = _start(fi, srv, tmp_path, "-once")
         assert p.wait(30) == 0, p.stderr.read()
         got = srv.labels("node-n")
         assert got["amd.com/gpu.vram"] == "288G" and got["keep"] == "me" and "amd.com/gpu.family" not in got
@@ -252,7 +275,7 @@ def test_in_cluster_https_with_the_cluster_ca(tmp_path, monkeypatch):
         (sa / "ca.crt").write_text(open(ca).read())
         env = dict(os.environ, KUBERNETES_SERVICE_HOST="127.0.0.1", KUBERNETES_SERVICE_PORT=str(srv.port),
                    DS_NODE_NAME="worker-9")
-        argv = [EXE, "-sa_dir", str(sa), "-resync", "0", "-mode", "-cu-count", "-sysfs_root", str(fi.sysfs),
+        argv = [EXE, "-sa_dir", str(sa), "-once", "-mode", "-cu-count", "-sysfs_root", str(fi.sysfs),
                 "-dev_root", str(fi.dev)]
         p = subprocess.run(argv, capture_output=True, text=True, timeout=60, env=env)
         assert p.returncode == 0, p.stderr
