@@ -77,6 +77,7 @@
 #include "mi355x/kfd_topology.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
+#include "../kube/yaml.h"
 
 namespace {
 
@@ -114,6 +115,7 @@ struct Flags {
   std::string liveness_probe;  // default: mi355x-liveness-probe next to this binary
   bool smi_ecc = false;
   bool smi_events = false;
+  std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
   glog::Options log;
 };
 
@@ -122,7 +124,7 @@ const std::set<std::string> kPythonOnly = {
     "liveness_chip_sweep_every", "perf_check_every", "perf_mib", "perf_action", "perf_min_hbm_read_gbps",
     "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "smi_xgmi", "metrics_port", "grpc_server",
     "topology_view", "node_view", "device_list_strategy", "cdi_spec_dir", "trace_file", "dry_run",
-    "topology_watch", "log_format", "config"};
+    "topology_watch", "log_format"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -150,7 +152,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"driver_type", &f->driver_type}, {"resource_naming_strategy", &f->naming},
       {"kubelet_dir", &f->kubelet_dir}, {"sysfs_root", &f->sysfs_root}, {"dev_root", &f->dev_root},
       {"exporter_socket", &f->exporter_socket}, {"liveness_mode", &f->liveness_mode},
-      {"liveness_probe", &f->liveness_probe}};
+      {"liveness_probe", &f->liveness_probe}, {"config", &f->config}};
+  if (const char* c = std::getenv("CONFIG_FILE_PATH")) f->config = c;
   static std::string ignored;
   strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
   for (int i = 1; i < argc; ++i) {
@@ -544,6 +547,45 @@ SockId sock_id(const std::string& path) {
   return s;
 }
 
+// AMD_GPU_DEVICE_COUNT, else gpu.device_count of the -config file: advertise
+// the devices of the first N physical GPUs (documented by the reference,
+// docs/user-guide/configuration.md:11,45-91, never implemented there; the
+// Python CLI's topology.device_count_limit_from_env)
+int device_count_limit(const std::string& config, std::string* err) {
+  if (const char* e = std::getenv("AMD_GPU_DEVICE_COUNT"); e && *e) {
+    char* end = nullptr;
+    const long n = std::strtol(e, &end, 10);
+    if (!*end && n >= 0) return static_cast<int>(n);
+  }
+  if (config.empty()) return -1;
+  auto text = read_file(config);
+  if (!text) return *err = "config file " + config + " is unreadable", -1;
+  std::string perr;
+  auto doc = yaml::parse(*text, &perr);
+  if (!doc) return *err = "config file " + config + ": " + perr, -1;
+  const json::Value* gpu = doc->get("gpu");
+  const json::Value* dc = gpu ? gpu->get("device_count") : nullptr;
+  if (!dc || dc->kind == json::Value::Null) return -1;
+  char* end = nullptr;
+  const long n = std::strtol(dc->s.c_str(), &end, 10);
+  if (dc->s.empty() || *end || n < 0) return *err = "config file " + config + ": bad gpu.device_count", -1;
+  return static_cast<int>(n);
+}
+
+std::vector<GpuDevice> limit_physical(const std::vector<GpuDevice>& devs, int limit) {
+  if (limit < 0) return devs;
+  std::vector<std::string> seen;
+  for (const auto& d : devs) {
+    const std::string k = !d.unique_id.empty() ? d.unique_id : d.bdf;
+    if (std::find(seen.begin(), seen.end(), k) == seen.end()) seen.push_back(k);
+  }
+  if (seen.size() > static_cast<size_t>(limit)) seen.resize(static_cast<size_t>(limit));
+  std::vector<GpuDevice> out;
+  for (const auto& d : devs)
+    if (std::find(seen.begin(), seen.end(), !d.unique_id.empty() ? d.unique_id : d.bdf) != seen.end()) out.push_back(d);
+  return out;
+}
+
 std::string self_dir() {
   char buf[4096];
   const ssize_t n = ::readlink("/proc/self/exe", buf, sizeof(buf) - 1);
@@ -580,6 +622,11 @@ int main(int argc, char** argv) {
   sigaction(SIGQUIT, &sa, nullptr);
   signal(SIGPIPE, SIG_IGN);
 
+  const int dev_limit = device_count_limit(f.config, &err);
+  if (!err.empty()) {
+    MI_LOG(kError, "%s", err.c_str());
+    return 1;
+  }
   std::vector<Resource> resources;
   KfdTopology topo;
   std::vector<GpuDevice> container_devices;  // every advertised container-mode device (health engine)
@@ -588,7 +635,8 @@ int main(int argc, char** argv) {
   auto init_container = [&](std::vector<Resource>* out) -> std::string {
     if (!is_dir(path_join(f.sysfs_root, "class/kfd"))) return "No kfd found (" + f.sysfs_root + "/class/kfd)";
     topo = KfdTopology::load_sysfs(f.sysfs_root);
-    const DiscoveryResult res = discover_gpus(f.sysfs_root, topo);
+    DiscoveryResult res = discover_gpus(f.sysfs_root, topo);
+    res.devices = limit_physical(res.devices, dev_limit);
     for (const auto& w : res.warnings) MI_LOG(kWarning, "%s", w.c_str());
     MI_LOG(kInfo, "Found %zu AMDGPUs", res.devices.size());
     const bool homogeneous = is_homogeneous(res.devices);

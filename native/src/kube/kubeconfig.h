@@ -24,10 +24,6 @@ struct KubeConfig {
   std::string token_file;  // re-read when it changes
 };
 
-// The YAML subset kubeconfig files use (block and flow mappings / sequences,
-// plain and quoted scalars, literal block scalars, comments) as a JSON value.
-std::optional<json::Value> parse_yaml(const std::string& text, std::string* error);
-
 std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* error);
 
 // controller-runtime's order after the flag: in-cluster unless $KUBECONFIG is

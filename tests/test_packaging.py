@@ -1,4 +1,5 @@
 """Drop-in packaging checks: DaemonSet manifests, Helm values, images, examples."""
+import json
 import os
 import re
 from pathlib import Path
@@ -237,13 +238,35 @@ def test_alert_rules_use_exported_metrics():
 
 
 def test_helm_native_daemon_switch():
-    """dp.native runs the native daemon; it refuses the features only the full plugin has."""
+    """dp.native (the default) runs the native daemon, health flags included; a
+    feature only the Python CLI has switches the chart to it instead of failing."""
     t = (REPO / "helm/amd-gpu/templates/deviceplugin-daemonset.yaml").read_text()
-    assert 'command: ["./mi355x-device-plugin"]' in t and "{{- if .Values.dp.native }}" in t
-    assert 'fail "dp.native' in t
-    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["dp"]["native"] is False
-    for df in ("Dockerfile", "ubi-dp.Dockerfile"):
-        assert "bin/mi355x-device-plugin /root/mi355x-device-plugin" in (REPO / df).read_text(), df
+    assert 'command: ["./mi355x-device-plugin"]' in t and "{{- if $native }}" in t
+    assert "fail " not in t
+    native_branch = t[t.index("{{- if $native }}"):t.index("{{- else if")]
+    for flag in ("-liveness=true", "-smi_ecc=true", "-smi_events=true", "-liveness_keep_queues"):
+        assert flag in native_branch
+    assert "$pyOnly := or $cdi .Values.dp.smi.xgmi .Values.dp.metricsPort" in t
+    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["dp"]["native"] is True
+
+
+def test_launcher_dispatches_native_first(tmp_path):
+    """./k8s-device-plugin (the image command) runs the native daemon; a
+    Python-only flag (here -dry_run) runs the Python CLI."""
+    import subprocess
+    import sys
+    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+    launcher = str(REPO / "scripts/k8s-device-plugin")
+    p = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and "mi355x-device-plugin" in p.stdout and "-liveness_probe" in p.stdout, p.stderr
+    fi = make_mi355x_node(tmp_path / "n")
+    p = subprocess.run([launcher, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                        "-exporter_socket", "", "-kubelet_dir", str(tmp_path / "dp")], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0 and json.loads(p.stdout)["resources"], p.stderr[-2000:]
+    env = dict(os.environ, MI355X_DP_IMPL="python")
+    p = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0 and "-grpc_server" in p.stdout
 
 
 def test_helm_native_labeller_switch():
