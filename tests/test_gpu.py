@@ -286,6 +286,24 @@ def test_corrupted_tile_turns_device_unhealthy_in_listandwatch(inv, ordinals, tm
     asyncio.run(asyncio.wait_for(go(str(tmp_path)), 180))
 
 
+def _probe_children(ppid):
+    """PIDs of mi355x-liveness-probe processes whose parent is `ppid`."""
+    out = set()
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                stat = f.read()
+            with open(f"/proc/{d}/cmdline", "rb") as f:
+                cmd = f.read()
+        except OSError:
+            continue
+        if int(stat.rsplit(")", 1)[1].split()[1]) == ppid and b"mi355x-liveness-probe" in cmd:
+            out.add(int(d))
+    return out
+
+
 def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_path):
     """The same fault through the interpreter-free daemon: mi355x-device-plugin
     -liveness runs the kept-queue probe server on the real GPU; a flipped
@@ -326,6 +344,8 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
         try:
             await k.wait_for_resource("amd.com/gpu", 1, timeout=60)
             await wait_health(k, "Healthy", 60)
+            children.update(_probe_children(proc.pid))
+            assert children, "no probe server under the daemon"
             fault.write_text("17")
             await wait_health(k, "Unhealthy", 60)
             fault.write_text("")
@@ -340,10 +360,10 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
         assert f"device {dev_id}: Healthy -> Unhealthy liveness probe:" in err and "differ" in err, err[-3000:]
         return err
 
+    children = set()
     asyncio.run(asyncio.wait_for(go(), 240))
-    # no probe server left behind
-    left = subprocess.run(["pgrep", "-f", "mi355x-liveness-probe --serve"], capture_output=True, text=True)
-    assert left.stdout.strip() == "", left.stdout
+    # the daemon's probe server went down with it
+    assert not [pid for pid in children if os.path.exists(f"/proc/{pid}")], children
 
 
 def test_probe_cli_corrupt_word_fails_the_tile():
