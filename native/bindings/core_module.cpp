@@ -200,6 +200,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("cross_hive_penalty", &AllocatorOptions::cross_hive_penalty)
       .def_readwrite("degraded_links", &AllocatorOptions::degraded_links)
       .def_readwrite("extended_search", &AllocatorOptions::extended_search)
+      .def_readwrite("extended_search_auto", &AllocatorOptions::extended_search_auto)
       .def_readwrite("extended_node_limit", &AllocatorOptions::extended_node_limit);
 
   // shared: the native gRPC server keeps using an allocator snapshot while
@@ -239,6 +240,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("num_from_keys", &HiveAllocator::num_from_keys)
       .def_property_readonly("num_inferred_pairs", &HiveAllocator::num_inferred_pairs)
       .def("pair_weight", &HiveAllocator::pair_weight)
+      .def_property_readonly("extended", &HiveAllocator::extended)
       .def("link_type", &HiveAllocator::link_type);
 
   py::class_<PciFunctionInfo>(m, "PciFunctionInfo")

@@ -66,6 +66,13 @@ struct AllocatorOptions {
   // fewer physical GPUs, then the better kfd links between them (lower kfd
   // link weight, then higher max_bandwidth), then the anti-fragmentation order.
   bool extended_search = false;
+  // Auto (the plugins' default): extended search on nodes where some physical
+  // GPU is split into several devices (partition modes), the reference family
+  // on whole-GPU nodes, where it already enumerates every GPU subset. Measured:
+  // on fragmented partitioned nodes the reference family was never heavier than
+  // the optimum, but broke ties onto more physical GPUs (profiles/
+  // allocator_default_vs_optimum.json); every Appendix A.1 row is unchanged.
+  bool extended_search_auto = false;
   // extended search: node budget before falling back to the reference family
   uint64_t extended_node_limit = 2000000;
 };
@@ -111,6 +118,8 @@ class HiveAllocator {
   int pair_weight(const std::string& a, const std::string& b) const;
   int link_type(const std::string& a, const std::string& b) const;
   const AllocatorOptions& options() const { return opt_; }
+  // effective search mode after init (extended_search, or auto resolved)
+  bool extended() const { return opt_.extended_search; }
 
  private:
   struct Group {

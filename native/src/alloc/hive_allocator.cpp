@@ -174,6 +174,10 @@ std::string HiveAllocator::init(const std::vector<AllocDevice>& devs, const KfdT
       int nb = devs_[b].node_id < 0 ? std::numeric_limits<int>::max() : devs_[b].node_id;
       return na < nb;
     });
+  if (opt_.extended_search_auto) {
+    opt_.extended_search = false;
+    for (const auto& g : groups_) opt_.extended_search |= g.members.size() > 1;
+  }
   return "";
 }
 

@@ -97,7 +97,8 @@ struct Flags {
   bool send_every_pulse = false;
   double register_timeout_s = 10.0;
   double grpc_watchdog_s = 10.0;
-  bool allocator_extended_search = false;
+  bool allocator_extended_search = false;  // forces "extended"
+  std::string allocator_search = "auto";   // auto | reference | extended
   // health (same names and defaults as the Python CLI)
   bool liveness = false;
   std::string liveness_mode = "persistent";
@@ -152,7 +153,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"driver_type", &f->driver_type}, {"resource_naming_strategy", &f->naming},
       {"kubelet_dir", &f->kubelet_dir}, {"sysfs_root", &f->sysfs_root}, {"dev_root", &f->dev_root},
       {"exporter_socket", &f->exporter_socket}, {"liveness_mode", &f->liveness_mode},
-      {"liveness_probe", &f->liveness_probe}, {"config", &f->config}};
+      {"liveness_probe", &f->liveness_probe}, {"config", &f->config}, {"allocator_search", &f->allocator_search}};
   if (const char* c = std::getenv("CONFIG_FILE_PATH")) f->config = c;
   static std::string ignored;
   strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
@@ -172,7 +173,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       std::printf(
           "usage: %s [-pulse N] [-driver_type container|vf-passthrough|pf-passthrough] "
           "[-resource_naming_strategy single|mixed] [-kubelet_dir DIR] [-sysfs_root DIR] [-dev_root DIR] "
-          "[-exporter_socket PATH] [-send_every_pulse] [-allocator_extended_search] [-grpc_watchdog S] "
+          "[-exporter_socket PATH] [-send_every_pulse] [-allocator_search auto|reference|extended] "
+          "[-allocator_extended_search] [-grpc_watchdog S] [-config FILE] "
           "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
           "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] "
@@ -230,6 +232,11 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
     return *err = "invalid liveness_mode provided: " + f->liveness_mode + ", supported values are persistent or spawn",
            false;
   if (f->grpc_watchdog_s < 0) return *err = "grpc_watchdog must be >= 0", false;
+  if (f->allocator_search != "auto" && f->allocator_search != "reference" && f->allocator_search != "extended")
+    return *err = "invalid allocator_search provided: " + f->allocator_search +
+                  ", supported values are auto, reference, extended",
+           false;
+  if (f->allocator_extended_search) f->allocator_search = "extended";
   if (f->liveness && f->pulse == 0) return *err = "-liveness needs -pulse > 0 (the probe runs once per pulse)", false;
   return true;
 }
@@ -303,7 +310,8 @@ std::string list_bytes(const Resource& r) {
 
 std::string group_key(const GpuDevice& d) { return !d.unique_id.empty() ? d.unique_id : "bdf:" + d.bdf; }
 
-void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved, bool extended) {
+void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved,
+             const std::string& search) {
   // allocator (BestEffortPolicy.init); on failure kubelet allocates by itself
   bool alloc_ok = true;
   for (const auto& d : r.devices)
@@ -324,7 +332,8 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
       ad.push_back(a);
     }
     AllocatorOptions opt;
-    opt.extended_search = extended;
+    opt.extended_search = search == "extended";
+    opt.extended_search_auto = search == "auto";  // extended on partitioned nodes
     auto alloc = std::make_shared<HiveAllocator>();
     const std::string err = alloc->init(ad, topo, opt);
     if (!err.empty()) {
@@ -663,7 +672,7 @@ int main(int argc, char** argv) {
           container_devices.push_back(d);
         }
       r.socket = path_join(f.kubelet_dir, std::string(kResourceNamespace) + "_" + name);
-      prepare(r, topo, unresolved, f.allocator_extended_search);
+      prepare(r, topo, unresolved, f.allocator_search);
       out->push_back(std::move(r));
     }
     return "";

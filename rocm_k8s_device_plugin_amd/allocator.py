@@ -47,15 +47,20 @@ def group_key(d) -> str:
 class BestEffortPolicy(Policy):
     """Hive-aware optimal subset selection with the reference's tie-breaks."""
 
+    SEARCH_MODES = ("auto", "reference", "extended")
+
     def __init__(self, missing_pair_is_worst: bool = True, cross_hive_penalty: int = 100,
-                 extended_search: bool = False):
-        """`extended_search`: search every split of the request over classes of
-        interchangeable devices (several partial GPUs; kfd link weight /
-        bandwidth tie-breaks) instead of the reference's candidate family."""
+                 extended_search=False):
+        """`extended_search`: True searches every split of the request over
+        classes of interchangeable devices (several partial GPUs; kfd link
+        weight / bandwidth tie-breaks) instead of the reference's candidate
+        family; "auto" does so only on nodes with partitioned GPUs (the
+        plugins' default, see AllocatorOptions::extended_search_auto)."""
         n = core()
         self._opts = n.AllocatorOptions(missing_pair_is_worst=missing_pair_is_worst,
                                         cross_hive_penalty=cross_hive_penalty)
-        self._opts.extended_search = bool(extended_search)
+        self._opts.extended_search_auto = extended_search == "auto"
+        self._opts.extended_search = extended_search is True or extended_search == "extended"
         self._alloc = n.HiveAllocator()
         self.stats = AllocStats()
 

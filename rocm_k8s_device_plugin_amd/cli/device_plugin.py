@@ -84,9 +84,11 @@ def build_parser() -> flags.GoFlagParser:
                                   "stops counting as xGMI-connected in preferred allocation (devices stay Healthy)")
     p.add_bool("send_every_pulse", False, "re-send the full device list on every pulse (reference behaviour)")
     p.add_int("metrics_port", 0, "serve Prometheus /metrics on this port (0 = off)")
-    p.add_bool("allocator_extended_search", False, "GetPreferredAllocation searches every split of a request over "
-                                                   "interchangeable devices (several partial GPUs) and breaks ties "
-                                                   "by kfd link weight/bandwidth; off = the reference's candidates")
+    p.add_str("allocator_search", "auto", "GetPreferredAllocation search: auto (extended on nodes with partitioned "
+                                          "GPUs, the reference's candidates on whole-GPU nodes), reference, extended")
+    p.add_bool("allocator_extended_search", False, "force the extended search: every split of a request over "
+                                                   "interchangeable devices (several partial GPUs), ties broken by "
+                                                   "fewer GPUs, then kfd link weight/bandwidth")
     p.add_str("grpc_server", "native", "kubelet-facing gRPC server: native (C++ HTTP/2; admission RPCs answered "
                                        "without Python) or aio (Python grpc.aio)")
     p.add_float("grpc_watchdog", 10.0, "native server watchdog: no ListAndWatch stream this many seconds after "
@@ -140,6 +142,8 @@ def validate(ns) -> Optional[str]:
         return "perf_check_every needs -liveness (the throughput check runs in the probe server)"
     if ns.grpc_server not in ("native", "aio"):
         return f"invalid grpc_server provided: {ns.grpc_server}, supported values are native or aio"
+    if ns.allocator_search not in ("auto", "reference", "extended"):
+        return f"invalid allocator_search provided: {ns.allocator_search}, supported values are auto, reference, extended"
     if ns.grpc_watchdog < 0:
         return "grpc_watchdog must be >= 0"
     return None
@@ -284,7 +288,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         return 0
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
                        metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch, grpc_server=ns.grpc_server,
-                       allocator_extended_search=ns.allocator_extended_search, grpc_watchdog_s=ns.grpc_watchdog)
+                       allocator_extended_search="extended" if ns.allocator_extended_search else ns.allocator_search,
+                       grpc_watchdog_s=ns.grpc_watchdog)
     from ..utils.trace import TRACER
     TRACER.configure(ns.trace_file or None)
     try:

@@ -42,7 +42,7 @@ class PluginContext:
         return self.allocator_error
 
 
-def new_context(resource: str, extended_search: bool = False) -> PluginContext:
+def new_context(resource: str, extended_search="auto") -> PluginContext:
     """One allocator per resource, like the reference's lister.NewPlugin (manager.go:96-104)."""
     try:
         alloc = BestEffortPolicy(extended_search=extended_search)

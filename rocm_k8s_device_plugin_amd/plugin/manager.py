@@ -62,8 +62,9 @@ class ManagerConfig:
     # kubelet-facing gRPC server: "native" (C++ HTTP/2, plugin/native_server.py)
     # or "aio" (Python grpc.aio, plugin/servicer.py)
     grpc_server: str = "native"
-    # GetPreferredAllocation beyond the reference's candidate family (allocator.py)
-    allocator_extended_search: bool = False
+    # GetPreferredAllocation search: "auto" (extended on partitioned nodes),
+    # "reference" (the reference's candidate family), "extended" / True (allocator.py)
+    allocator_extended_search: object = "auto"
     # native transport watchdog: after Register is acknowledged, no ListAndWatch
     # stream within this many seconds, or any HTTP/2 protocol error on the
     # plugin socket, moves the resource to grpc.aio and registers again. 0 = off

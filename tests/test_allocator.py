@@ -359,3 +359,24 @@ def test_extended_search_optimal_on_mi355x_fixture(tmp_path, cp, mp, hive):
             key = (w, len({gpu[x] for x in s}))
             best = key if best is None or key < best else best
         assert (r["weight"], len({gpu[x] for x in r["ids"]})) == best, (av, req, k, r)
+
+
+def test_auto_search_is_extended_only_on_partitioned_nodes(ref_testdata, tmp_path):
+    """The plugins' default ("auto"): whole-GPU nodes keep the reference's
+    candidate family (it already enumerates every GPU subset there),
+    partitioned nodes get the extended search. Every Appendix A.1 expectation
+    holds under it (test_reference_contract covers the reference mode; here
+    the same rows through auto)."""
+    from rocm_k8s_device_plugin_amd.plugin.base import new_context
+    pol, ids = make_policy(ref_testdata, "mi210", extended_search="auto")
+    assert not pol.native.extended
+    pol, ids = make_policy(ref_testdata, "mi300cpx", extended_search="auto")
+    assert pol.native.extended
+    for name, size, avail, req, filt, expected in CASES:
+        if expected is None:
+            continue
+        p, all_ids = make_policy(ref_testdata, name, extended_search="auto")
+        av = [i for i in (avail or all_ids) if i not in filt]
+        assert sorted(p.allocate(av, req, size)) == sorted(expected), (name, size)
+    ctx = new_context("gpu")
+    assert ctx.allocator._opts.extended_search_auto
