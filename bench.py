@@ -628,6 +628,8 @@ def main():
                  "latency_p99_ms": round(pct(lat_ms, .99), 3), "latency_mean_ms": round(statistics.mean(lat_ms), 3),
                  "container_runtime": args.container_runtime,
                  "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
+                 "latency_p99_ms_with_hip_runtime_container": round(pct(hip_lat, .99), 3) if hip_lat else None,
+                 "hip_runtime_container_steps": len(hip_lat),
                  "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
                  "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
                  "container_mode": args.container_mode,
