@@ -7,6 +7,7 @@
 
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/health_engine.h"
+#include "mi355x/metrics.h"
 #include "mi355x/kfd_topology.h"
 
 namespace py = pybind11;
@@ -122,6 +123,23 @@ void bind_health(py::module_& m) {
       .def("set_exporter", &PyHealthEngine::set_exporter, py::arg("health"),
            "bdf -> healthy used instead of the exporter socket (None = socket)")
       .def("close", &PyHealthEngine::close);
+  // a private registry (the process-wide one is metrics::global(), see `metrics_render`)
+  py::class_<metrics::Registry>(m, "MetricsRegistry", "Prometheus registry of the native daemon (mi355x/metrics.h)")
+      .def(py::init<>())
+      .def("inc", [](metrics::Registry& r, const std::string& name, double v, const std::string& help,
+                     const std::map<std::string, std::string>& labels) {
+             r.inc(name, metrics::Labels(labels.begin(), labels.end()), v, help);
+           }, py::arg("name"), py::arg("v") = 1.0, py::arg("help") = "", py::arg("labels") = std::map<std::string, std::string>())
+      .def("set", [](metrics::Registry& r, const std::string& name, double v, const std::string& help,
+                     const std::map<std::string, std::string>& labels) {
+             r.set(name, v, metrics::Labels(labels.begin(), labels.end()), help);
+           }, py::arg("name"), py::arg("v"), py::arg("help") = "", py::arg("labels") = std::map<std::string, std::string>())
+      .def("observe_ms", [](metrics::Registry& r, const std::string& name, double ms, const std::string& help,
+                            const std::map<std::string, std::string>& labels) {
+             r.observe_ms(name, ms, metrics::Labels(labels.begin(), labels.end()), help);
+           }, py::arg("name"), py::arg("ms"), py::arg("help") = "", py::arg("labels") = std::map<std::string, std::string>())
+      .def("render", &metrics::Registry::render);
+  m.def("metrics_render", [] { return metrics::global().render(); }, "the process-wide native registry");
   m.def("exporter_list", [](const std::string& socket, double timeout_s) {
     std::string err;
     std::map<std::string, bool> h;

@@ -11,7 +11,7 @@
 //                  -kubelet_dir / -sysfs_root / -dev_root / -exporter_socket /
 //                  -send_every_pulse, the health flags of the Python CLI
 //                  (-liveness*, -smi_ecc, -smi_events), -allocator_extended_search,
-//                  -grpc_watchdog
+//                  -grpc_watchdog, -metrics_port
 //   discovery      discover_gpus over the kfd topology (gpu_discovery.cpp)
 //   resources      single -> "gpu"; mixed -> "<compute>_<memory>"; heterogeneous
 //                  partitions with single is an error (amdgpu.go:68-88,122-162)
@@ -32,6 +32,8 @@
 //                  -grpc_watchdog s, or HTTP/2 protocol errors on the plugin
 //                  socket: exit 3 so the DaemonSet restarts the plugin instead of
 //                  leaving it registered and invisible
+//   metrics        -metrics_port: Prometheus /metrics on a thread of its own,
+//                  the Python CLI's series (mi355x/metrics.h)
 //   signals        SIGTERM / SIGINT / SIGQUIT stop the servers, the probe server
 //                  and the workers, and remove the sockets
 //   passthrough    -driver_type vf-passthrough / pf-passthrough (amdgpu_sriov.go,
@@ -75,6 +77,7 @@
 #include "mi355x/grpc_server.h"
 #include "mi355x/health_engine.h"
 #include "mi355x/kfd_topology.h"
+#include "mi355x/metrics.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
 #include "../kube/yaml.h"
@@ -117,13 +120,14 @@ struct Flags {
   bool smi_ecc = false;
   bool smi_events = false;
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
+  int metrics_port = 0;  // Prometheus /metrics (0 = off)
   glog::Options log;
 };
 
 // Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
 const std::set<std::string> kPythonOnly = {
     "liveness_chip_sweep_every", "perf_check_every", "perf_mib", "perf_action", "perf_min_hbm_read_gbps",
-    "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "smi_xgmi", "metrics_port", "grpc_server",
+    "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "smi_xgmi", "grpc_server",
     "topology_view", "node_view", "device_list_strategy", "cdi_spec_dir", "trace_file", "dry_run",
     "topology_watch", "log_format"};
 
@@ -144,7 +148,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"liveness_fail_threshold", &f->liveness_fail_threshold},
       {"liveness_recover_threshold", &f->liveness_recover_threshold},
       {"liveness_idle_sweeps", &f->liveness_idle_sweeps}, {"liveness_crowded_procs", &f->liveness_crowded_procs},
-      {"liveness_crowded_release_sweeps", &f->liveness_crowded_release_sweeps}};
+      {"liveness_crowded_release_sweeps", &f->liveness_crowded_release_sweeps}, {"metrics_port", &f->metrics_port}};
   std::map<std::string, double*> floats = {
       {"liveness_timeout", &f->liveness_timeout}, {"liveness_busy_grace", &f->liveness_busy_grace},
       {"liveness_unknown_busy_grace", &f->liveness_unknown_busy_grace}, {"grpc_watchdog", &f->grpc_watchdog_s},
@@ -174,7 +178,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "usage: %s [-pulse N] [-driver_type container|vf-passthrough|pf-passthrough] "
           "[-resource_naming_strategy single|mixed] [-kubelet_dir DIR] [-sysfs_root DIR] [-dev_root DIR] "
           "[-exporter_socket PATH] [-send_every_pulse] [-allocator_search auto|reference|extended] "
-          "[-allocator_extended_search] [-grpc_watchdog S] [-config FILE] "
+          "[-allocator_extended_search] [-grpc_watchdog S] [-config FILE] [-metrics_port N] "
           "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
           "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] "
@@ -220,6 +224,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
   }
   // validateFlags (main.go:59-75)
   if (f->pulse < 0) return *err = "pulse must be a non-negative integer", false;
+  if (f->metrics_port < 0 || f->metrics_port > 65535) return *err = "metrics_port must be in 0..65535", false;
   if (!f->driver_type.empty() && f->driver_type != "container" && f->driver_type != "vf-passthrough" &&
       f->driver_type != "pf-passthrough")
     return *err = "invalid driver_type provided: " + f->driver_type +
@@ -433,6 +438,7 @@ struct Completion {
   bool ok = false;
   std::string message;
   std::map<std::string, bool> health;  // kSweep: device id -> healthy (every resource's devices)
+  double sweep_ms = 0;
 };
 
 class Workers {
@@ -648,6 +654,13 @@ int main(int argc, char** argv) {
     res.devices = limit_physical(res.devices, dev_limit);
     for (const auto& w : res.warnings) MI_LOG(kWarning, "%s", w.c_str());
     MI_LOG(kInfo, "Found %zu AMDGPUs", res.devices.size());
+    auto& m = metrics::global();
+    m.set("mi355x_dp_kfd_unreadable_nodes", static_cast<double>(res.kfd_unreadable_nodes.size()), {},
+          "kfd topology nodes whose properties the plugin cannot read (EPERM)");
+    m.set("mi355x_dp_devices_identity_from_sysfs", res.recovered_devices, {},
+          "devices identified from PCI sysfs because their kfd node is unreadable");
+    m.set("mi355x_dp_devices_identity_unknown", static_cast<double>(res.unresolved.size()), {},
+          "devices without a known physical GPU / xGMI hive (placement not topology-aware)");
     const bool homogeneous = is_homogeneous(res.devices);
     if (!homogeneous && f.naming == "single")
       return "Partitions of different styles across GPUs in a node is not supported with single strategy. "
@@ -819,6 +832,16 @@ int main(int argc, char** argv) {
     for (auto& r : resources) apply_health(r, h);
   }
 
+  metrics::HttpEndpoint metrics_http;
+  if (f.metrics_port > 0) {
+    const std::string merr = metrics_http.start("0.0.0.0", f.metrics_port);
+    if (!merr.empty()) {
+      MI_LOG(kError, "cannot serve /metrics: %s", merr.c_str());
+      return 1;
+    }
+    MI_LOG(kInfo, "serving Prometheus /metrics on :%d", metrics_http.port());
+  }
+
   const std::string kubelet_sock = path_join(f.kubelet_dir, "kubelet.sock");
   DirWatcher watch;
   std::string werr = watch.open(f.kubelet_dir);
@@ -833,7 +856,7 @@ int main(int argc, char** argv) {
     const uint64_t gen = kubelet_gen;
     workers.run([&f, &kubelet_sock, name = r.name, socket = r.socket, options = r.options, i, gen,
                  abort_fd = stop_pipe[0]] {
-      Completion c{Completion::kRegister, i, gen, false, "", {}};
+      Completion c{Completion::kRegister, i, gen, false, "", {}, 0};
       c.message = register_with_kubelet(name, socket, options, kubelet_sock, f.register_timeout_s, abort_fd);
       c.ok = c.message.empty();
       return c;
@@ -885,8 +908,25 @@ int main(int argc, char** argv) {
         uint64_t v;
         if (::read(resources[i].service->event_fd(), &v, sizeof(v)) < 0) {
         }
-        for (const auto& ev : resources[i].service->drain_events()) {
+        const auto evs = resources[i].service->drain_events();
+        auto& m = metrics::global();
+        const metrics::Labels res_l = {{"resource", resources[i].name}};
+        if (!evs.empty() && resources[i].server) {
+          const auto st = resources[i].server->stats();
+          m.set("mi355x_dp_grpc_connections", static_cast<double>(st.connections), res_l,
+                "native gRPC server: connections");
+          m.set("mi355x_dp_grpc_calls", static_cast<double>(st.calls), res_l, "native gRPC server: calls");
+          m.set("mi355x_dp_grpc_protocol_errors", static_cast<double>(st.protocol_errors), res_l,
+                "native gRPC server: protocol errors");
+          m.set("mi355x_dp_listandwatch_open_streams", static_cast<double>(st.streams_open), res_l,
+                "ListAndWatch streams open on the native server");
+        }
+        for (const auto& ev : evs) {
+          m.observe_ms("mi355x_dp_rpc_seconds", ev.dur_ns / 1e6, {{"resource", resources[i].name}, {"rpc", ev.rpc}},
+                       "device plugin RPC latency");
+          if (ev.rpc == "ListAndWatch") m.inc("mi355x_dp_listandwatch_streams_total", res_l);
           if (ev.status != 0) {
+            m.inc("mi355x_dp_rpc_errors_total", {{"resource", resources[i].name}, {"rpc", ev.rpc}});
             MI_LOG(kError, "%s: %s: %s", resources[i].name.c_str(), ev.rpc.c_str(), ev.message.c_str());
           } else if (ev.rpc == "Allocate") {
             std::string ids;
@@ -940,6 +980,7 @@ int main(int argc, char** argv) {
           r.streams_at_register = st.streams_opened;
           r.perr_at_register = st.protocol_errors;
           r.list_seen = false;
+          metrics::global().inc("mi355x_dp_registrations_total", {{"resource", r.name}});
           MI_LOG(kInfo, "%s: Registration for endpoint %s", r.name.c_str(), basename(r.socket).c_str());
         } else {
           MI_LOG(kError, "%s: %s", r.name.c_str(), c.message.c_str());
@@ -948,11 +989,15 @@ int main(int argc, char** argv) {
         }
       } else {
         sweep_inflight = false;
+        metrics::global().observe_ms("mi355x_dp_health_sweep_seconds", c.sweep_ms, {}, "health sweep latency");
+        bool any_changed = false;
         for (auto& r : resources) {
           const bool changed = apply_health(r, c.health);
+          any_changed = any_changed || changed;
           if ((changed || f.send_every_pulse) && r.server)
             r.server->broadcast(rpc::DevicePluginService::path("ListAndWatch"), r.list);
         }
+        if (any_changed) metrics::global().inc("mi355x_dp_health_changes_total");
       }
     }
     workers.reap();
@@ -994,8 +1039,10 @@ int main(int argc, char** argv) {
       } else if (!resources.empty()) {
         sweep_inflight = true;
         workers.run([&health_pass] {
-          Completion c{Completion::kSweep, 0, 0, true, "", {}};
+          Completion c{Completion::kSweep, 0, 0, true, "", {}, 0};
+          const auto t0 = Clock::now();
           c.health = health_pass();
+          c.sweep_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
           return c;
         });
       }

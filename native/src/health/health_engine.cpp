@@ -20,6 +20,7 @@
 
 #include "../kube/json.h"
 #include "mi355x/glog.h"
+#include "mi355x/metrics.h"
 #include "mi355x/grpc_server.h"
 #include "mi355x/smi_query.h"
 #include "mi355x/sysfs.h"
@@ -846,6 +847,8 @@ std::map<std::string, ProbeOutcome> Engine::verify_identity(const std::map<std::
   for (const auto& [id, o] : new_ords) merged[id] = o;
   ordinals_ = merged;
   identity_remaps_++;
+  metrics::global().inc("mi355x_dp_probe_identity_mismatch_total", {}, 1.0,
+                        "sweeps whose probe replies came from other devices than the positional ordinal map");
   return fixed;
 }
 
@@ -887,6 +890,8 @@ bool Engine::sweep() {
                 now_known ? "busy-GPU state readable again"
                           : "busy-GPU state unknown: every GPU counts as busy, pending probes get the short grace");
     busy_known_ = now_known;
+    metrics::global().set("mi355x_dp_busy_state_known", now_known ? 1.0 : 0.0, {},
+                          "1 if busy GPUs can be told from idle ones (kfd process list readable)");
     // crowded GPUs: the probe server steps off them
     std::set<std::string> crowded;
     if (cfg_.crowded_procs > 0) {
@@ -944,6 +949,8 @@ bool Engine::sweep() {
           outcomes[id] = prober_->probe_ordinal(ords[id]);  // crowded but idle: probe from a fresh process
         } else {
           crowded_skips_++;
+          metrics::global().inc("mi355x_dp_liveness_crowded_skips_total", {{"device", id}}, 1.0,
+                                "probes skipped on GPUs crowded with tenant processes");
         }
       }
     }
@@ -968,6 +975,8 @@ bool Engine::sweep() {
     }
     for (const auto& [id, o] : outcomes) {
       Track& tr = track_[id];
+      metrics::global().set("mi355x_dp_liveness_probe_ms", o.latency_ms, {{"device", id}},
+                            "last liveness probe round trip");
       if (!o.pending) tr.idle_pending = 0;
       if (o.ok) {
         tr.fails = 0;
@@ -977,13 +986,18 @@ bool Engine::sweep() {
       } else if (o.pending && busy_devs.count(id) && !idle_wedged.count(id) &&
                  now - (tr.pending_since >= 0 ? tr.pending_since : now) < grace) {
         if (tr.pending_since < 0) tr.pending_since = now;  // queued behind a tenant: inconclusive
+        metrics::global().inc("mi355x_dp_liveness_inconclusive_total", {{"device", id}}, 1.0,
+                              "probes queued behind a busy GPU");
       } else {
         tr.oks = 0;
         tr.fails++;
         tr.last_reason = o.reason;
-        if (idle_wedged.count(id))
+        if (idle_wedged.count(id)) {
           tr.last_reason += " while the GPU reports 0% GFX activity (" + std::to_string(tr.idle_pending) +
                             " sweeps): no tenant kernel is running";
+          metrics::global().inc("mi355x_dp_liveness_idle_pending_total", {{"device", id}}, 1.0,
+                                "pending probes on an idle GFX engine");
+        }
         if (!o.pending) tr.pending_since = -1;
         if (tr.live && tr.fails >= cfg_.fail_threshold) tr.live = false;
       }
@@ -1024,6 +1038,8 @@ bool Engine::sweep() {
     }
     if (events_ && events_->running()) {
       for (const auto& ev : events_->poll(0)) {
+        metrics::global().inc("mi355x_dp_gpu_events_total", {{"bdf", ev.bdf}, {"event", ev.name}}, 1.0,
+                              "amd-smi GPU events");
         if (ev.name == "gpu_pre_reset") {
           resetting_[ev.bdf] = ev.message;
           MI_LOG(kWarning, "GPU %s: reset starting (%s)", ev.bdf.c_str(), ev.message.c_str());
@@ -1058,6 +1074,9 @@ bool Engine::sweep() {
     }
     if (changed) version_++;
     snapshot_ = std::move(next);
+    for (const auto& [id, v] : snapshot_)
+      metrics::global().set("mi355x_dp_device_healthy", v.healthy ? 1.0 : 0.0, {{"device", id}},
+                            "1 if the device is advertised Healthy");
   }
   sweeps_++;
   last_sweep_ms_ = (mono_s() - t0) * 1e3;

@@ -1,0 +1,136 @@
+"""Prometheus metrics of the native daemon (native/src/util/metrics.cpp).
+
+The native registry renders exactly what the Python registry renders for the
+same observations (names, label order, buckets, number formatting), and
+`mi355x-device-plugin -metrics_port` serves the series the Python CLI does:
+per-RPC latency histograms, registrations, ListAndWatch streams, the native
+server's counters, health sweeps and per-device verdicts, liveness round
+trips. The reference exposes no metrics."""
+import asyncio
+import json
+import os
+import re
+import socket
+import sys
+import urllib.error
+import urllib.request
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.ops.native import core
+from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+from rocm_k8s_device_plugin_amd.utils.metrics import Registry
+
+from test_native_health import STUB, _daemon, _stop
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+
+
+def test_registry_renders_like_python():
+    py, nat = Registry(), core().MetricsRegistry()
+    ops = [("inc", "mi355x_dp_registrations_total", 1.0, "", {"resource": "gpu"}),
+           ("inc", "mi355x_dp_registrations_total", 1.0, "", {"resource": "gpu"}),
+           ("inc", "mi355x_dp_rpc_errors_total", 1.0, "", {"rpc": "Allocate", "resource": "cpx_nps1"}),
+           ("inc", "mi355x_dp_health_changes_total", 1.0, "", {}),
+           ("set", "mi355x_dp_device_healthy", 0.0, "1 if the device is advertised Healthy", {"device": "0000:11:00.0"}),
+           ("set", "mi355x_dp_device_healthy", 1.0, "1 if the device is advertised Healthy", {"device": "0000:01:00.0"}),
+           ("set", "mi355x_dp_liveness_probe_ms", 0.3612, "last liveness probe round trip", {"device": "x"}),
+           ("set", "mi355x_dp_busy_state_known", 1.0, "busy", {})]
+    for kind, name, v, hlp, lab in ops:
+        getattr(py, kind)(name, v, help=hlp, **lab)
+        getattr(nat, kind)(name, v, hlp, lab)
+    for ms in (0.04, 0.05, 0.051, 0.19, 3.0, 12.5, 99999.0):
+        py.histogram("mi355x_dp_rpc_seconds", "device plugin RPC latency", rpc="Allocate", resource="gpu").observe(ms)
+        nat.observe_ms("mi355x_dp_rpc_seconds", ms, "device plugin RPC latency", {"rpc": "Allocate", "resource": "gpu"})
+    py.histogram("mi355x_dp_health_sweep_seconds", "health sweep latency").observe(6.25)
+    nat.observe_ms("mi355x_dp_health_sweep_seconds", 6.25, "health sweep latency", {})
+    assert nat.render() == py.render()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _get(port, path):
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+            return r.status, r.read().decode()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode()
+
+
+def _series(text):
+    out = {}
+    for line in text.splitlines():
+        if line and not line.startswith("#"):
+            k, v = line.rsplit(" ", 1)
+            out[k] = float(v)
+    return out
+
+
+def test_daemon_serves_metrics(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text(json.dumps({"3": "fail"}))
+    kdir = str(tmp_path / "dp")
+    port = _free_port()
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = {o: d for d, o in eng.ordinals().items()}
+    eng.close()
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        p = _daemon(kdir, fi, "-pulse", "1", "-liveness", "-liveness_probe", STUB, "-liveness_fail_threshold", "1",
+                    "-liveness_timeout", "3", "-exporter_socket", "", "-metrics_port", str(port),
+                    env={"MI355X_STUB_PROBE_CONTROL": str(ctl)})
+        try:
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            adm = await k.admit("amd.com/gpu", 2)
+            assert len(adm.device_ids) == 2
+            await asyncio.sleep(2.5)   # a pulse or two
+            status, text = await asyncio.to_thread(_get, port, "/metrics")
+            assert status == 200
+            hz = await asyncio.to_thread(_get, port, "/healthz")
+            nf = await asyncio.to_thread(_get, port, "/nope")
+        finally:
+            rc, err = await asyncio.to_thread(_stop, p)
+            await k.stop()
+        assert rc == 0, err[-3000:]
+        return text, hz, nf
+
+    text, hz, nf = asyncio.run(asyncio.wait_for(go(), 90))
+    assert hz == (200, "ok\n") and nf[0] == 404
+    s = _series(text)
+    assert s['mi355x_dp_registrations_total{resource="gpu"}'] >= 1
+    assert s['mi355x_dp_rpc_seconds_count{resource="gpu",rpc="Allocate"}'] == 1
+    assert s['mi355x_dp_rpc_seconds_count{resource="gpu",rpc="GetPreferredAllocation"}'] == 1
+    assert s['mi355x_dp_rpc_seconds_bucket{resource="gpu",rpc="Allocate",le="+Inf"}'] == 1
+    assert s['mi355x_dp_grpc_calls{resource="gpu"}'] >= 2
+    assert s['mi355x_dp_listandwatch_open_streams{resource="gpu"}'] >= 1
+    assert s["mi355x_dp_health_sweep_seconds_count"] >= 1
+    assert s[f'mi355x_dp_device_healthy{{device="{dev[3]}"}}'] == 0.0
+    assert sum(v for k, v in s.items() if k.startswith("mi355x_dp_device_healthy")) == 7.0
+    assert s[f'mi355x_dp_liveness_probe_ms{{device="{dev[0]}"}}'] > 0
+    assert "mi355x_dp_busy_state_known" in s   # 0 here: the stub server has no kfd entry of its own
+    assert s["mi355x_dp_devices_identity_unknown"] == 0.0
+    assert "# TYPE mi355x_dp_rpc_seconds histogram" in text
+    assert re.search(r'^mi355x_dp_rpc_seconds_bucket\{resource="gpu",rpc="Allocate",le="5e-05"\} \d+$', text, re.M)
+
+
+def test_daemon_metrics_port_in_use_is_an_error(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    with socket.socket() as s:
+        s.bind(("0.0.0.0", 0))
+        s.listen(1)
+        port = s.getsockname()[1]
+        p = _daemon(str(tmp_path / "dp"), fi, "-metrics_port", str(port), "-exporter_socket", "")
+        rc, err = _stop(p) if p.wait(timeout=20) is not None else (None, "")
+    assert rc == 1 and "cannot serve /metrics" in err
