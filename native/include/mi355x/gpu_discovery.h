@@ -71,6 +71,12 @@ struct DiscoveryResult {
   std::vector<std::string> unresolved;    // device IDs with no identity (placement must not trust them)
 };
 
+// Cheap fingerprint of the node's GPU topology: kfd's generation_id (bumped
+// when kfd nodes come or go) and every amdgpu function's current compute /
+// memory partition (topology.py topology_signature). Polled by both daemons'
+// -topology_watch; a change is followed by a full re-discovery.
+std::string topology_signature(const std::string& sysfs_root);
+
 // Logical devices one physical GPU splits into in compute mode `mode`
 // (lower-case); CPX = one per XCC. 0 = unknown mode or XCC count.
 int partitions_for_mode(const std::string& mode, int total_xcc);

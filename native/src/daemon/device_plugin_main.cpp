@@ -11,7 +11,7 @@
 //                  -kubelet_dir / -sysfs_root / -dev_root / -exporter_socket /
 //                  -send_every_pulse, the health flags of the Python CLI
 //                  (-liveness*, -smi_ecc, -smi_events), -allocator_extended_search,
-//                  -grpc_watchdog, -metrics_port
+//                  -grpc_watchdog, -metrics_port, -topology_watch
 //   discovery      discover_gpus over the kfd topology (gpu_discovery.cpp)
 //   resources      single -> "gpu"; mixed -> "<compute>_<memory>"; heterogeneous
 //                  partitions with single is an error (amdgpu.go:68-88,122-162)
@@ -32,6 +32,8 @@
 //                  -grpc_watchdog s, or HTTP/2 protocol errors on the plugin
 //                  socket: exit 3 so the DaemonSet restarts the plugin instead of
 //                  leaving it registered and invisible
+//   topology       -topology_watch: a partition switch is re-discovered and
+//                  re-advertised (resources stop, change or appear)
 //   metrics        -metrics_port: Prometheus /metrics on a thread of its own,
 //                  the Python CLI's series (mi355x/metrics.h)
 //   signals        SIGTERM / SIGINT / SIGQUIT stop the servers, the probe server
@@ -121,6 +123,7 @@ struct Flags {
   bool smi_events = false;
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
+  double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
   glog::Options log;
 };
 
@@ -128,8 +131,7 @@ struct Flags {
 const std::set<std::string> kPythonOnly = {
     "liveness_chip_sweep_every", "perf_check_every", "perf_mib", "perf_action", "perf_min_hbm_read_gbps",
     "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "smi_xgmi", "grpc_server",
-    "topology_view", "node_view", "device_list_strategy", "cdi_spec_dir", "trace_file", "dry_run",
-    "topology_watch", "log_format"};
+    "topology_view", "node_view", "device_list_strategy", "cdi_spec_dir", "trace_file", "dry_run", "log_format"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -152,7 +154,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
   std::map<std::string, double*> floats = {
       {"liveness_timeout", &f->liveness_timeout}, {"liveness_busy_grace", &f->liveness_busy_grace},
       {"liveness_unknown_busy_grace", &f->liveness_unknown_busy_grace}, {"grpc_watchdog", &f->grpc_watchdog_s},
-      {"register_timeout", &f->register_timeout_s}};
+      {"register_timeout", &f->register_timeout_s}, {"topology_watch", &f->topology_watch_s}};
   std::map<std::string, std::string*> strs = {
       {"driver_type", &f->driver_type}, {"resource_naming_strategy", &f->naming},
       {"kubelet_dir", &f->kubelet_dir}, {"sysfs_root", &f->sysfs_root}, {"dev_root", &f->dev_root},
@@ -178,7 +180,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "usage: %s [-pulse N] [-driver_type container|vf-passthrough|pf-passthrough] "
           "[-resource_naming_strategy single|mixed] [-kubelet_dir DIR] [-sysfs_root DIR] [-dev_root DIR] "
           "[-exporter_socket PATH] [-send_every_pulse] [-allocator_search auto|reference|extended] "
-          "[-allocator_extended_search] [-grpc_watchdog S] [-config FILE] [-metrics_port N] "
+          "[-allocator_extended_search] [-grpc_watchdog S] [-config FILE] [-metrics_port N] [-topology_watch S] "
           "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
           "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] "
@@ -237,6 +239,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
     return *err = "invalid liveness_mode provided: " + f->liveness_mode + ", supported values are persistent or spawn",
            false;
   if (f->grpc_watchdog_s < 0) return *err = "grpc_watchdog must be >= 0", false;
+  if (f->topology_watch_s < 0) return *err = "topology_watch must be >= 0", false;
   if (f->allocator_search != "auto" && f->allocator_search != "reference" && f->allocator_search != "extended")
     return *err = "invalid allocator_search provided: " + f->allocator_search +
                   ", supported values are auto, reference, extended",
@@ -281,6 +284,8 @@ struct Resource {
   IommuMap groups;                         // group -> PCI functions
   std::string socket;  // <kubelet_dir>/amd.com_<name>
   std::string options;
+  rpc::AllocateTemplate tmpl;
+  bool gone = false;  // removed by a topology change: no server, no devices (the slot keeps indices stable)
   std::unique_ptr<rpc::GrpcServer> server;
   std::unique_ptr<rpc::DevicePluginService> service;
   std::shared_ptr<const HiveAllocator> allocator;
@@ -368,6 +373,7 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
   r.service->set_options(r.options);
   if (r.allocator) r.service->set_allocator(r.allocator);
   r.service->set_allocate_template(t);
+  r.tmpl = t;
   r.list = list_bytes(r);
   r.service->set_device_list(r.list);
 }
@@ -413,7 +419,8 @@ bool start_server(Resource& r) {
     r.server.reset();
     return false;
   }
-  r.server_gen++;
+  static uint64_t seq = 0;
+  r.server_gen = ++seq;  // unique across slots: a Register answer names the server it was for
   MI_LOG(kInfo, "%s: serving on %s", r.name.c_str(), r.socket.c_str());
   return true;
 }
@@ -439,6 +446,7 @@ struct Completion {
   std::string message;
   std::map<std::string, bool> health;  // kSweep: device id -> healthy (every resource's devices)
   double sweep_ms = 0;
+  uint64_t server_gen = 0;              // kRegister: the server the Register was for
 };
 
 class Workers {
@@ -751,7 +759,9 @@ int main(int argc, char** argv) {
   int stop_pipe[2] = {-1, -1};
   if (::pipe2(stop_pipe, O_CLOEXEC | O_NONBLOCK) != 0) return 1;
   std::unique_ptr<health::Engine> engine;
-  if (driver == Driver::Container && !container_devices.empty()) {
+  auto make_engine = [&] {
+    engine.reset();
+    if (driver != Driver::Container || container_devices.empty()) return;
     health::Config hc;
     hc.sysfs_root = f.sysfs_root;
     hc.dev_root = f.dev_root;
@@ -775,7 +785,8 @@ int main(int argc, char** argv) {
     engine = std::make_unique<health::Engine>(container_devices, topo, hc);
     engine->set_abort_fd(stop_pipe[0]);
     if (f.liveness) MI_LOG(kInfo, "liveness probe: %s (%s)", hc.prober.exe.c_str(), f.liveness_mode.c_str());
-  }
+  };
+  make_engine();
   // one health pass (blocking; worker thread): device id -> healthy for every resource
   auto health_pass = [&]() -> std::map<std::string, bool> {
     std::map<std::string, bool> out;
@@ -855,8 +866,8 @@ int main(int argc, char** argv) {
     r.register_inflight = true;
     const uint64_t gen = kubelet_gen;
     workers.run([&f, &kubelet_sock, name = r.name, socket = r.socket, options = r.options, i, gen,
-                 abort_fd = stop_pipe[0]] {
-      Completion c{Completion::kRegister, i, gen, false, "", {}, 0};
+                 sgen = r.server_gen, abort_fd = stop_pipe[0]] {
+      Completion c{Completion::kRegister, i, gen, false, "", {}, 0, sgen};
       c.message = register_with_kubelet(name, socket, options, kubelet_sock, f.register_timeout_s, abort_fd);
       c.ok = c.message.empty();
       return c;
@@ -880,6 +891,102 @@ int main(int argc, char** argv) {
 
   bool sweep_inflight = false;
   auto next_pulse = Clock::now() + std::chrono::seconds(f.pulse > 0 ? f.pulse : 3600);
+
+  // ---- topology watch (container driver): an amd-smi partition switch changes
+  // the devices; vanished resources stop serving (kubelet drops them when the
+  // stream ends), kept ones get the new devices, allocator and list, new ones
+  // register; the health engine is rebuilt (a probe server's agents were
+  // enumerated at its start). The Python CLI's reload_topology (plugin/container.py).
+  const bool topo_watch = f.topology_watch_s > 0 && driver == Driver::Container;
+  const auto topo_period = std::chrono::milliseconds(static_cast<long long>(f.topology_watch_s * 1000));
+  std::string topo_sig = topo_watch ? topology_signature(f.sysfs_root) : "", topo_seen = topo_sig;
+  auto next_topo = Clock::now() + topo_period;
+  auto reload_topology = [&](const std::string& sig) {
+    std::vector<Resource> fresh;
+    const std::string e = init_container(&fresh);  // re-reads topo and container_devices
+    topo_sig = sig;
+    std::map<std::string, std::string> before, after;  // device id -> partition type
+    std::string old_names, new_names;
+    for (const auto& r : resources)
+      if (!r.gone) {
+        old_names += (old_names.empty() ? "" : ",") + r.name;
+        for (const auto& d : r.devices) before[d.id] = d.partition_type();
+      }
+    if (e.empty())
+      for (const auto& r : fresh) {
+        new_names += (new_names.empty() ? "" : ",") + r.name;
+        for (const auto& d : r.devices) after[d.id] = d.partition_type();
+      }
+    if (before == after) return;
+    metrics::global().inc("mi355x_dp_topology_reloads_total");
+    MI_LOG(kWarning, "GPU topology changed: %zu -> %zu devices; resources [%s] -> [%s]", before.size(), after.size(),
+           old_names.c_str(), new_names.c_str());
+    const std::string lw = rpc::DevicePluginService::path("ListAndWatch");
+    if (!e.empty()) {
+      MI_LOG(kError, "GPU topology changed: %s. Advertising no devices until then.", e.c_str());
+      for (auto& r : resources) {
+        if (r.gone) continue;
+        r.devices.clear();
+        r.health.clear();
+        r.allocator.reset();
+        r.service->set_allocator(nullptr);
+        r.list = list_bytes(r);
+        r.service->set_device_list(r.list);
+        if (r.server) r.server->broadcast(lw, r.list);
+      }
+      container_devices.clear();
+      make_engine();
+      return;
+    }
+    std::set<std::string> names;
+    for (const auto& fr : fresh) names.insert(fr.name);
+    for (auto& r : resources)
+      if (!r.gone && !names.count(r.name)) {
+        MI_LOG(kWarning, "resource %s no longer exists: stopping its plugin server", r.name.c_str());
+        stop_server(r);
+        r.gone = true;
+        r.devices.clear();
+        r.health.clear();
+      }
+    for (auto& fr : fresh) {
+      auto it = std::find_if(resources.begin(), resources.end(), [&](const Resource& r) { return r.name == fr.name; });
+      if (it != resources.end() && !it->gone) {
+        Resource& r = *it;
+        const bool opts_changed = r.options != fr.options;
+        std::map<std::string, bool> kept;
+        for (const auto& d : fr.devices)
+          if (auto h = r.health.find(d.id); h != r.health.end()) kept[d.id] = h->second;
+        r.devices = std::move(fr.devices);
+        r.health = std::move(kept);
+        r.allocator = fr.allocator;
+        r.options = fr.options;
+        r.tmpl = fr.tmpl;
+        r.service->set_options(r.options);
+        r.service->set_allocator(r.allocator);
+        r.service->set_allocate_template(r.tmpl);
+        r.list = list_bytes(r);
+        r.service->set_device_list(r.list);
+        if (r.server) r.server->broadcast(lw, r.list);
+        if (opts_changed && r.server) {  // kubelet reads the options at registration
+          r.registered = false;
+          r.next_register = Clock::now();
+        }
+        continue;
+      }
+      size_t i;
+      if (it != resources.end()) {
+        *it = std::move(fr);
+        i = static_cast<size_t>(it - resources.begin());
+      } else {
+        resources.push_back(std::move(fr));
+        i = resources.size() - 1;
+      }
+      MI_LOG(kInfo, "new resource %s (%zu devices)", resources[i].name.c_str(), resources[i].devices.size());
+      if (sock.present && start_server(resources[i])) try_register(i);
+    }
+    make_engine();
+    if (f.pulse > 0) next_pulse = Clock::now();  // verdicts for the new devices now
+  };
   auto next_stat = Clock::now() + std::chrono::seconds(5);
   int exit_code = 0;
   while (!g_stop) {
@@ -900,6 +1007,7 @@ int main(int argc, char** argv) {
       if (r.registered && !r.list_seen && f.grpc_watchdog_s > 0) wait_ms = std::min(wait_ms, 250LL);
     }
     if (f.grpc_watchdog_s > 0) wait_ms = std::min(wait_ms, 1000LL);
+    if (topo_watch) wait_ms = std::min(wait_ms, until(next_topo));
     ::poll(pfd.data(), pfd.size(), static_cast<int>(std::max(0LL, wait_ms)));
     if (g_stop) break;
     // ---- RPC events: the reference logs every Allocate
@@ -970,6 +1078,7 @@ int main(int argc, char** argv) {
     for (auto& c : workers.take()) {
       if (c.kind == Completion::kRegister) {
         Resource& r = resources[c.resource];
+        if (c.server_gen != r.server_gen) continue;  // an earlier server's answer (restart, topology change)
         r.register_inflight = false;
         if (c.gen != kubelet_gen || !r.server) continue;  // a previous kubelet's answer
         if (c.ok) {
@@ -1031,6 +1140,17 @@ int main(int argc, char** argv) {
         break;
       }
     }
+    // ---- topology watch: a new signature must hold for one interval (a partition
+    // switch passes through states with devices half gone); never under a sweep
+    if (topo_watch && Clock::now() >= next_topo) {
+      next_topo = Clock::now() + topo_period;
+      const std::string cur = topology_signature(f.sysfs_root);
+      if (cur != topo_seen) {
+        topo_seen = cur;
+      } else if (cur != topo_sig && !sweep_inflight) {
+        reload_topology(cur);
+      }
+    }
     // ---- health pulse (worker thread; a sweep still running skips this pulse)
     if (f.pulse > 0 && Clock::now() >= next_pulse) {
       next_pulse = Clock::now() + std::chrono::seconds(f.pulse);
@@ -1039,7 +1159,7 @@ int main(int argc, char** argv) {
       } else if (!resources.empty()) {
         sweep_inflight = true;
         workers.run([&health_pass] {
-          Completion c{Completion::kSweep, 0, 0, true, "", {}, 0};
+          Completion c{Completion::kSweep, 0, 0, true, "", {}, 0, 0};
           const auto t0 = Clock::now();
           c.health = health_pass();
           c.sweep_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();

@@ -735,20 +735,6 @@ class Labeller {
   bool have_desired_ = false;
 };
 
-// kfd generation_id + every amdgpu function's partition modes (topology.py topology_signature)
-std::string topology_signature(const std::string& sysfs_root) {
-  std::string sig = read_trimmed(path_join(sysfs_root, "class/kfd/kfd/topology/generation_id")).value_or("-");
-  const std::string drv = path_join(sysfs_root, "module/amdgpu/drivers/pci:amdgpu");
-  auto bdfs = list_dir(drv);
-  std::sort(bdfs.begin(), bdfs.end());
-  for (const auto& b : bdfs) {
-    if (b.find(':') == std::string::npos) continue;
-    sig += "|" + b + "=" + read_trimmed(path_join(drv, b + "/current_compute_partition")).value_or("-") + "," +
-           read_trimmed(path_join(drv, b + "/current_memory_partition")).value_or("-");
-  }
-  return sig;
-}
-
 std::string node_name_from(const Flags& f) {
   if (!f.node_name.empty()) return f.node_name;
   return read_trimmed("/labeller/hostname").value_or("");

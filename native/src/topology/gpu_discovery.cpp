@@ -375,4 +375,17 @@ FirmwareInfo parse_debugfs_firmware_info(const std::string& path) {
   return fi;
 }
 
+std::string topology_signature(const std::string& sysfs_root) {
+  std::string sig = read_trimmed(path_join(sysfs_root, "class/kfd/kfd/topology/generation_id")).value_or("-");
+  const std::string drv = path_join(sysfs_root, "module/amdgpu/drivers/pci:amdgpu");
+  auto bdfs = list_dir(drv);
+  std::sort(bdfs.begin(), bdfs.end());
+  for (const auto& b : bdfs) {
+    if (b.find(':') == std::string::npos) continue;
+    sig += "|" + b + "=" + read_trimmed(path_join(drv, b + "/current_compute_partition")).value_or("-") + "," +
+           read_trimmed(path_join(drv, b + "/current_memory_partition")).value_or("-");
+  }
+  return sig;
+}
+
 }  // namespace mi355x
