@@ -71,6 +71,7 @@
 #include <vector>
 
 #include "mi355x/allocator.h"
+#include "mi355x/cdi.h"
 #include "mi355x/constants.h"
 #include "mi355x/dir_watch.h"
 #include "mi355x/dp_service.h"
@@ -124,6 +125,9 @@ struct Flags {
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
   double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
+  std::string device_list_strategy = "device-specs";
+  std::string cdi_spec_dir = "/var/run/cdi";
+  cdi::Strategies lists;  // parsed -device_list_strategy
   glog::Options log;
 };
 
@@ -131,7 +135,7 @@ struct Flags {
 const std::set<std::string> kPythonOnly = {
     "liveness_chip_sweep_every", "perf_check_every", "perf_mib", "perf_action", "perf_min_hbm_read_gbps",
     "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "smi_xgmi", "grpc_server",
-    "topology_view", "node_view", "device_list_strategy", "cdi_spec_dir", "trace_file", "dry_run", "log_format"};
+    "topology_view", "node_view", "trace_file", "dry_run", "log_format"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -159,7 +163,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"driver_type", &f->driver_type}, {"resource_naming_strategy", &f->naming},
       {"kubelet_dir", &f->kubelet_dir}, {"sysfs_root", &f->sysfs_root}, {"dev_root", &f->dev_root},
       {"exporter_socket", &f->exporter_socket}, {"liveness_mode", &f->liveness_mode},
-      {"liveness_probe", &f->liveness_probe}, {"config", &f->config}, {"allocator_search", &f->allocator_search}};
+      {"liveness_probe", &f->liveness_probe}, {"config", &f->config}, {"allocator_search", &f->allocator_search},
+      {"device_list_strategy", &f->device_list_strategy}, {"cdi_spec_dir", &f->cdi_spec_dir}};
   if (const char* c = std::getenv("CONFIG_FILE_PATH")) f->config = c;
   static std::string ignored;
   strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
@@ -181,6 +186,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-resource_naming_strategy single|mixed] [-kubelet_dir DIR] [-sysfs_root DIR] [-dev_root DIR] "
           "[-exporter_socket PATH] [-send_every_pulse] [-allocator_search auto|reference|extended] "
           "[-allocator_extended_search] [-grpc_watchdog S] [-config FILE] [-metrics_port N] [-topology_watch S] "
+          "[-device_list_strategy device-specs|cdi-cri|cdi-annotations[,...]] [-cdi_spec_dir DIR] "
           "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
           "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] "
@@ -240,6 +246,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
            false;
   if (f->grpc_watchdog_s < 0) return *err = "grpc_watchdog must be >= 0", false;
   if (f->topology_watch_s < 0) return *err = "topology_watch must be >= 0", false;
+  if (!cdi::parse_strategies(f->device_list_strategy, &f->lists, err)) return false;
   if (f->allocator_search != "auto" && f->allocator_search != "reference" && f->allocator_search != "extended")
     return *err = "invalid allocator_search provided: " + f->allocator_search +
                   ", supported values are auto, reference, extended",
@@ -321,7 +328,7 @@ std::string list_bytes(const Resource& r) {
 std::string group_key(const GpuDevice& d) { return !d.unique_id.empty() ? d.unique_id : "bdf:" + d.bdf; }
 
 void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved,
-             const std::string& search) {
+             const std::string& search, const cdi::Strategies& lists) {
   // allocator (BestEffortPolicy.init); on failure kubelet allocates by itself
   bool alloc_ok = true;
   for (const auto& d : r.devices)
@@ -356,13 +363,24 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
   }
   r.options.clear();
   if (alloc_ok) pb::put_bool(&r.options, 2, true);  // get_preferred_allocation_available
+  // ContainerAllocateResponse{devices=3 (DeviceSpec), annotations=4, cdi_devices=5 (CDIDevice{name=1})}
   rpc::AllocateTemplate t;
   t.resource = r.name;
-  pb::put_bytes(&t.container_prefix, 3, device_spec("/dev/kfd"));
+  if (lists.specs) pb::put_bytes(&t.container_prefix, 3, device_spec("/dev/kfd"));
+  if (lists.annotations) t.annotation_key = cdi::annotation_key(r.name);
   for (const auto& d : r.devices) {
     std::string car;
-    if (d.card >= 0) pb::put_bytes(&car, 3, device_spec("/dev/dri/card" + std::to_string(d.card)));
-    if (d.render_minor >= 0) pb::put_bytes(&car, 3, device_spec("/dev/dri/renderD" + std::to_string(d.render_minor)));
+    if (lists.specs) {
+      if (d.card >= 0) pb::put_bytes(&car, 3, device_spec("/dev/dri/card" + std::to_string(d.card)));
+      if (d.render_minor >= 0)
+        pb::put_bytes(&car, 3, device_spec("/dev/dri/renderD" + std::to_string(d.render_minor)));
+    }
+    if (lists.cri) {
+      std::string dev;
+      pb::put_bytes(&dev, 1, cdi::qualified_name(r.name, d.id));
+      pb::put_bytes(&car, 5, dev);
+    }
+    if (lists.annotations) t.annotation_names[d.id] = cdi::qualified_name(r.name, d.id);
     t.per_device[d.id] = car;
   }
   r.service = std::make_unique<rpc::DevicePluginService>();
@@ -693,7 +711,7 @@ int main(int argc, char** argv) {
           container_devices.push_back(d);
         }
       r.socket = path_join(f.kubelet_dir, std::string(kResourceNamespace) + "_" + name);
-      prepare(r, topo, unresolved, f.allocator_search);
+      prepare(r, topo, unresolved, f.allocator_search, f.lists);
       out->push_back(std::move(r));
     }
     return "";
@@ -752,6 +770,27 @@ int main(int argc, char** argv) {
                : std::string(type) == "vf-passthrough" ? Driver::Vf : Driver::Pf;
       break;
     }
+  }
+
+  // ---- CDI specs (-device_list_strategy cdi-*): written before registration,
+  // since kubelet may hand a CDI name to the runtime as soon as it allocates
+  auto write_cdi = [&](const std::set<std::string>& stale) -> std::string {
+    if (driver != Driver::Container || !f.lists.cdi()) return "";
+    std::map<std::string, std::vector<GpuDevice>> members;
+    for (const auto& r : resources)
+      if (!r.gone) members[r.name] = r.devices;
+    std::vector<std::string> paths;
+    const std::string e = cdi::write_specs(f.cdi_spec_dir, members, stale, &paths);
+    if (e.empty()) {
+      std::string all;
+      for (const auto& p : paths) all += (all.empty() ? "" : ", ") + p;
+      MI_LOG(kInfo, "CDI specs written: %s", all.c_str());
+    }
+    return e;
+  };
+  if (const std::string e = write_cdi({}); !e.empty()) {
+    MI_LOG(kError, "cannot write CDI specs to %s: %s", f.cdi_spec_dir.c_str(), e.c_str());
+    return 1;
   }
 
   // ---- health ---------------------------------------------------------------
@@ -918,6 +957,9 @@ int main(int argc, char** argv) {
         for (const auto& d : r.devices) after[d.id] = d.partition_type();
       }
     if (before == after) return;
+    std::set<std::string> old_set;
+    for (const auto& r : resources)
+      if (!r.gone) old_set.insert(r.name);
     metrics::global().inc("mi355x_dp_topology_reloads_total");
     MI_LOG(kWarning, "GPU topology changed: %zu -> %zu devices; resources [%s] -> [%s]", before.size(), after.size(),
            old_names.c_str(), new_names.c_str());
@@ -934,6 +976,8 @@ int main(int argc, char** argv) {
         r.service->set_device_list(r.list);
         if (r.server) r.server->broadcast(lw, r.list);
       }
+      if (const std::string ce = write_cdi(old_set); !ce.empty())
+        MI_LOG(kError, "CDI specs not updated after the topology change: %s", ce.c_str());
       container_devices.clear();
       make_engine();
       return;
@@ -984,6 +1028,8 @@ int main(int argc, char** argv) {
       MI_LOG(kInfo, "new resource %s (%zu devices)", resources[i].name.c_str(), resources[i].devices.size());
       if (sock.present && start_server(resources[i])) try_register(i);
     }
+    if (const std::string ce = write_cdi(old_set); !ce.empty())
+      MI_LOG(kError, "CDI specs not updated after the topology change: %s", ce.c_str());
     make_engine();
     if (f.pulse > 0) next_pulse = Clock::now();  // verdicts for the new devices now
   };
