@@ -333,21 +333,46 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
             except TimeoutError:
                 pass
 
+    import socket
+    import urllib.request
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+
+    def metrics():
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+            return {k: float(v) for k, v in (ln.rsplit(" ", 1) for ln in r.read().decode().splitlines()
+                                             if ln and not ln.startswith("#"))}
+
     async def go():
         k = FakeKubelet(kdir)
         await k.start()
         env = dict(os.environ, MI355X_PROBE_CORRUPT_FILE=str(fault))
         proc = await asyncio.create_subprocess_exec(
             exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_timeout", "30",
-            "-liveness_fail_threshold", "2", stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE,
-            env=env)
+            "-liveness_fail_threshold", "2", "-metrics_port", str(port), "-device_list_strategy",
+            "device-specs,cdi-cri", "-cdi_spec_dir", str(tmp_path / "cdi"), stdout=asyncio.subprocess.DEVNULL,
+            stderr=asyncio.subprocess.PIPE, env=env)
         try:
             await k.wait_for_resource("amd.com/gpu", 1, timeout=60)
             await wait_health(k, "Healthy", 60)
             children.update(_probe_children(proc.pid))
             assert children, "no probe server under the daemon"
+            # CDI names next to the DeviceSpecs, the spec file on disk
+            adm = await k.admit("amd.com/gpu", 1, must_include=[dev_id])
+            car = adm.response.container_responses[0]
+            assert [c.name for c in car.cdi_devices] == [f"amd.com/gpu={dev_id}"] and car.devices
+            assert (tmp_path / "cdi" / "amd.com-gpu.json").exists()
+            k.release("amd.com/gpu", adm.device_ids)
+            m = await asyncio.to_thread(metrics)
+            assert m[f'mi355x_dp_device_healthy{{device="{dev_id}"}}'] == 1.0
+            assert m[f'mi355x_dp_liveness_probe_ms{{device="{dev_id}"}}'] > 0
+            # the real kept-queue server's own kfd entry is found: busy state is known
+            assert m["mi355x_dp_busy_state_known"] == 1.0
             fault.write_text("17")
             await wait_health(k, "Unhealthy", 60)
+            m = await asyncio.to_thread(metrics)
+            assert m[f'mi355x_dp_device_healthy{{device="{dev_id}"}}'] == 0.0
             fault.write_text("")
             await wait_health(k, "Healthy", 60)
         finally:
