@@ -50,6 +50,8 @@ class PyHealthEngine {
     i("crowded_release_sweeps", &c.crowded_release_sweeps);
     b("smi_ecc", &c.smi_ecc);
     b("smi_events", &c.smi_events);
+    b("smi_xgmi", &c.smi_xgmi);
+    s("xgmi_file", &c.xgmi_file);
     s("probe_exe", &c.prober.exe);
     d("probe_timeout_s", &c.prober.timeout_s);
     i("probe_iters", &c.prober.iters);
@@ -90,6 +92,9 @@ class PyHealthEngine {
     }
     return d;
   }
+  std::vector<std::pair<std::string, std::string>> degraded_links() const { return eng_->degraded_links(); }
+  uint64_t fabric_version() const { return eng_->fabric_version(); }
+  std::map<std::string, int> links_down() const { return eng_->links_down(); }
   void set_activity(std::optional<std::map<std::string, int>> a) {
     if (!a) eng_->activity_source = nullptr;
     else eng_->activity_source = [a] { return *a; };
@@ -122,6 +127,9 @@ void bind_health(py::module_& m) {
            "bdf -> GFX activity % used instead of amd-smi (None = amd-smi)")
       .def("set_exporter", &PyHealthEngine::set_exporter, py::arg("health"),
            "bdf -> healthy used instead of the exporter socket (None = socket)")
+      .def("degraded_links", &PyHealthEngine::degraded_links, "xGMI pairs (allocator group keys) degraded")
+      .def("fabric_version", &PyHealthEngine::fabric_version)
+      .def("links_down", &PyHealthEngine::links_down)
       .def("close", &PyHealthEngine::close);
   // a private registry (the process-wide one is metrics::global(), see `metrics_render`)
   py::class_<metrics::Registry>(m, "MetricsRegistry", "Prometheus registry of the native daemon (mi355x/metrics.h)")

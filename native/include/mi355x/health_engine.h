@@ -25,6 +25,12 @@
 //   amd-smi   a rise of the uncorrectable ECC count; a gpu_pre_reset event
 //             keeps the device Unhealthy until its gpu_post_reset
 //
+// and, as a placement input rather than a verdict, xGMI link state
+// (-smi_xgmi, health/fabric.py): a link up in the first reading and down
+// later degrades that GPU pair (or every xGMI pair of the GPU when amd-smi
+// cannot name the peer); the daemon re-initialises its allocators with the
+// degraded pairs scoring as the worst link. The devices stay Healthy.
+//
 // sweep() blocks (probes, exporter, amd-smi) and is meant for a worker
 // thread; snapshot() may be called from any thread.
 #pragma once
@@ -42,6 +48,7 @@
 
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/kfd_topology.h"
+#include "mi355x/smi_query.h"
 
 namespace mi355x {
 class SmiEventWatcher;
@@ -126,6 +133,8 @@ struct Config {
   int crowded_release_sweeps = 5;
   bool smi_ecc = false;
   bool smi_events = false;
+  bool smi_xgmi = false;
+  std::string xgmi_file;  // JSON snapshot (smi_xgmi_links' shape) read instead of amd-smi: fault injection
 };
 
 struct Verdict {
@@ -152,6 +161,12 @@ class Engine {
   // sources a test (or another collector) can replace
   std::function<std::map<std::string, int>()> activity_source;       // bdf -> GFX activity %, -1 unknown
   std::function<std::map<std::string, bool>()> exporter_source;      // bdf -> healthy
+  std::function<SmiXgmiSnapshot()> xgmi_source;                      // instead of amd-smi / xgmi_file
+
+  // xGMI pairs (allocator group keys, ordered) degraded since the first reading
+  std::vector<std::pair<std::string, std::string>> degraded_links() const;
+  uint64_t fabric_version() const;  // bumped whenever the degraded set changes
+  std::map<std::string, int> links_down() const;  // bdf -> links down vs the first reading
 
   LivenessProber* prober() { return prober_.get(); }
   uint64_t sweeps() const { return sweeps_; }
@@ -178,6 +193,8 @@ class Engine {
                                                       const std::map<std::string, ProbeOutcome>& outcomes);
   bool identity_matches(const GpuDevice& d, const ProbeOutcome& o) const;
   const GpuDevice* dev(const std::string& id) const;
+  void fabric_check();
+  SmiXgmiSnapshot read_xgmi();
 
   std::vector<GpuDevice> devices_;
   std::map<std::string, size_t> by_id_;
@@ -197,8 +214,15 @@ class Engine {
   uint64_t sweeps_ = 0, identity_remaps_ = 0, crowded_skips_ = 0;
   double last_sweep_ms_ = 0;
   int abort_fd_ = -1;
+  // xGMI baseline: bdf -> (links up, -1 unknown; peers seen live)
+  std::map<std::string, std::pair<int, std::set<std::string>>> xgmi_base_;
+  std::map<std::string, std::string> gpu_by_bdf_;  // lower-case bdf -> allocator group key
+  std::string xgmi_error_;
 
-  mutable std::mutex mu_;  // snapshot_ / version_
+  mutable std::mutex mu_;  // snapshot_ / version_ / degraded_ / fabric_version_ / links_down_
+  std::set<std::pair<std::string, std::string>> degraded_;
+  std::map<std::string, int> links_down_;
+  uint64_t fabric_version_ = 0;
   std::map<std::string, Verdict> snapshot_;
   uint64_t version_ = 0;
 };

@@ -122,6 +122,7 @@ struct Flags {
   std::string liveness_probe;  // default: mi355x-liveness-probe next to this binary
   bool smi_ecc = false;
   bool smi_events = false;
+  bool smi_xgmi = false;  // xGMI link state re-weights preferred allocation
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
   double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
@@ -134,7 +135,7 @@ struct Flags {
 // Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
 const std::set<std::string> kPythonOnly = {
     "liveness_chip_sweep_every", "perf_check_every", "perf_mib", "perf_action", "perf_min_hbm_read_gbps",
-    "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "smi_xgmi", "grpc_server",
+    "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "grpc_server",
     "topology_view", "node_view", "trace_file", "dry_run", "log_format"};
 
 bool parse_bool(const std::string& v, bool* out) {
@@ -148,7 +149,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
   std::map<std::string, bool*> bools = {
       {"send_every_pulse", &f->send_every_pulse}, {"allocator_extended_search", &f->allocator_extended_search},
       {"liveness", &f->liveness}, {"liveness_keep_queues", &f->liveness_keep_queues},
-      {"liveness_corroborate", &f->liveness_corroborate}, {"smi_ecc", &f->smi_ecc}, {"smi_events", &f->smi_events}};
+      {"liveness_corroborate", &f->liveness_corroborate}, {"smi_ecc", &f->smi_ecc}, {"smi_events", &f->smi_events},
+      {"smi_xgmi", &f->smi_xgmi}};
   std::map<std::string, int*> ints = {
       {"pulse", &f->pulse}, {"liveness_iters", &f->liveness_iters},
       {"liveness_fail_threshold", &f->liveness_fail_threshold},
@@ -189,7 +191,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-device_list_strategy device-specs|cdi-cri|cdi-annotations[,...]] [-cdi_spec_dir DIR] "
           "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
           "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
-          "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] "
+          "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
           "[-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
           "[-log_backtrace_at FILE:N]\n",
           argv[0]);
@@ -327,6 +329,31 @@ std::string list_bytes(const Resource& r) {
 
 std::string group_key(const GpuDevice& d) { return !d.unique_id.empty() ? d.unique_id : "bdf:" + d.bdf; }
 
+// BestEffortPolicy.init over `devs`; `degraded`: xGMI pairs (group keys) scored as the worst link
+std::shared_ptr<const HiveAllocator> build_allocator(const std::vector<GpuDevice>& devs, const KfdTopology& topo,
+                                                     const std::string& search,
+                                                     const std::vector<std::pair<std::string, std::string>>& degraded,
+                                                     std::string* err) {
+  std::vector<AllocDevice> ad;
+  for (const auto& d : devs) {
+    AllocDevice a;
+    a.id = d.id;
+    a.node_id = d.node_id;
+    a.numa_node = d.numa_node;
+    a.unique_id = group_key(d);
+    a.hive_id = d.hive_id;
+    a.inferred_links = d.node_id < 0 && d.identity == "sysfs";
+    ad.push_back(a);
+  }
+  AllocatorOptions opt;
+  opt.extended_search = search == "extended";
+  opt.extended_search_auto = search == "auto";  // extended on partitioned nodes
+  opt.degraded_links = degraded;
+  auto alloc = std::make_shared<HiveAllocator>();
+  *err = alloc->init(ad, topo, opt);
+  return alloc;
+}
+
 void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved,
              const std::string& search, const cdi::Strategies& lists) {
   // allocator (BestEffortPolicy.init); on failure kubelet allocates by itself
@@ -337,22 +364,8 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
     MI_LOG(kError, "allocator disabled for plugin %s: no physical-GPU identity for some devices. Falling back to "
                    "kubelet default allocation.", r.name.c_str());
   } else {
-    std::vector<AllocDevice> ad;
-    for (const auto& d : r.devices) {
-      AllocDevice a;
-      a.id = d.id;
-      a.node_id = d.node_id;
-      a.numa_node = d.numa_node;
-      a.unique_id = group_key(d);
-      a.hive_id = d.hive_id;
-      a.inferred_links = d.node_id < 0 && d.identity == "sysfs";
-      ad.push_back(a);
-    }
-    AllocatorOptions opt;
-    opt.extended_search = search == "extended";
-    opt.extended_search_auto = search == "auto";  // extended on partitioned nodes
-    auto alloc = std::make_shared<HiveAllocator>();
-    const std::string err = alloc->init(ad, topo, opt);
+    std::string err;
+    auto alloc = build_allocator(r.devices, topo, search, {}, &err);
     if (!err.empty()) {
       MI_LOG(kError, "allocator init failed for plugin %s. Falling back to kubelet default allocation. Error %s",
              r.name.c_str(), err.c_str());
@@ -798,6 +811,7 @@ int main(int argc, char** argv) {
   int stop_pipe[2] = {-1, -1};
   if (::pipe2(stop_pipe, O_CLOEXEC | O_NONBLOCK) != 0) return 1;
   std::unique_ptr<health::Engine> engine;
+  uint64_t fabric_seen = 0;  // engine->fabric_version() the allocators were built for
   auto make_engine = [&] {
     engine.reset();
     if (driver != Driver::Container || container_devices.empty()) return;
@@ -821,7 +835,10 @@ int main(int argc, char** argv) {
     hc.crowded_release_sweeps = f.liveness_crowded_release_sweeps;
     hc.smi_ecc = f.smi_ecc;
     hc.smi_events = f.smi_events;
+    hc.smi_xgmi = f.smi_xgmi;
+    if (const char* x = std::getenv("MI355X_SMI_XGMI_FILE"); x && *x) hc.xgmi_file = x;  // fault injection
     engine = std::make_unique<health::Engine>(container_devices, topo, hc);
+    fabric_seen = 0;
     engine->set_abort_fd(stop_pipe[0]);
     if (f.liveness) MI_LOG(kInfo, "liveness probe: %s (%s)", hc.prober.exe.c_str(), f.liveness_mode.c_str());
   };
@@ -1153,6 +1170,25 @@ int main(int argc, char** argv) {
             r.server->broadcast(rpc::DevicePluginService::path("ListAndWatch"), r.list);
         }
         if (any_changed) metrics::global().inc("mi355x_dp_health_changes_total");
+        // xGMI link state changed: every allocator re-weighted on the degraded pairs
+        if (engine && engine->fabric_version() != fabric_seen) {
+          fabric_seen = engine->fabric_version();
+          const auto degraded = engine->degraded_links();
+          for (auto& r : resources) {
+            if (r.gone || !r.allocator) continue;
+            std::string aerr;
+            auto a = build_allocator(r.devices, topo, f.allocator_search, degraded, &aerr);
+            if (!aerr.empty()) {
+              MI_LOG(kError, "%s: allocator re-weighting failed: %s", r.name.c_str(), aerr.c_str());
+              continue;
+            }
+            r.allocator = a;
+            r.service->set_allocator(a);
+          }
+          metrics::global().inc("mi355x_dp_fabric_reweights_total");
+          MI_LOG(kWarning, "xGMI link state changed: preferred allocation re-weighted (%zu degraded GPU pairs)",
+                 degraded.size());
+        }
       }
     }
     workers.reap();

@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -670,6 +671,9 @@ Engine::Engine(std::vector<GpuDevice> devices, const KfdTopology& topo, Config c
     by_id_[devices_[i].id] = i;
     track_[devices_[i].id] = Track{};
     snapshot_[devices_[i].id] = Verdict{};
+    std::string b = devices_[i].bdf;
+    for (auto& c : b) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+    gpu_by_bdf_.emplace(b, !devices_[i].unique_id.empty() ? devices_[i].unique_id : "bdf:" + devices_[i].bdf);
   }
   if (cfg_.liveness) {
     if (cfg_.prober.kfd_proc_dir.empty() || cfg_.prober.kfd_proc_dir == "/sys/class/kfd/kfd/proc")
@@ -1056,6 +1060,8 @@ bool Engine::sweep() {
         reasons[d.id].push_back("GPU reset in progress (amd-smi gpu_pre_reset, no post_reset yet)");
   }
 
+  if (cfg_.smi_xgmi) fabric_check();
+
   std::map<std::string, Verdict> next;
   for (auto& [id, rs] : reasons) next[id] = Verdict{rs.empty(), rs};
   bool changed = false;
@@ -1081,6 +1087,148 @@ bool Engine::sweep() {
   sweeps_++;
   last_sweep_ms_ = (mono_s() - t0) * 1e3;
   return changed;
+}
+
+// ---- xGMI link state (health/fabric.py FabricWatcher) ----------------------------
+namespace {
+constexpr int kLinkUp = 1;
+constexpr int kLinkTypeXgmi = 2;
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+
+// the JSON shape of core().smi_xgmi_links()
+SmiXgmiSnapshot xgmi_from_json(const std::string& text) {
+  SmiXgmiSnapshot snap;
+  std::string err;
+  auto doc = json::parse(text, &err);
+  if (!doc || doc->kind != json::Value::Object) {
+    snap.error = "xgmi snapshot: " + (err.empty() ? std::string("not an object") : err);
+    return snap;
+  }
+  auto flag = [](const json::Value* v) { return v && v->kind == json::Value::Bool && v->b; };
+  auto num = [](const json::Value* v, long long dflt) {
+    return v && v->kind == json::Value::Number ? std::strtoll(v->s.c_str(), nullptr, 10) : dflt;
+  };
+  snap.ok = flag(doc->get("ok"));
+  snap.error = doc->str("error");
+  if (const json::Value* gpus = doc->get("gpus"); gpus && gpus->kind == json::Value::Array)
+    for (const auto& g : gpus->arr) {
+      SmiXgmiLinks l;
+      l.bdf = g.str("bdf");
+      l.status_ok = flag(g.get("status_ok"));
+      if (const json::Value* st = g.get("status"); st && st->kind == json::Value::Array)
+        for (const auto& x : st->arr) l.status.push_back(static_cast<int>(num(&x, -1)));
+      l.metrics_ok = flag(g.get("metrics_ok"));
+      if (const json::Value* ps = g.get("peers"); ps && ps->kind == json::Value::Array)
+        for (const auto& p : ps->arr) {
+          SmiLinkPeer q;
+          q.peer_bdf = p.str("peer_bdf");
+          q.link_type = static_cast<int>(num(p.get("link_type"), -1));
+          q.bit_rate_gbps = static_cast<uint32_t>(num(p.get("bit_rate_gbps"), 1));
+          l.peers.push_back(q);
+        }
+      snap.gpus.push_back(std::move(l));
+    }
+  return snap;
+}
+}  // namespace
+
+SmiXgmiSnapshot Engine::read_xgmi() {
+  if (xgmi_source) return xgmi_source();
+  if (!cfg_.xgmi_file.empty()) {
+    auto text = read_file(cfg_.xgmi_file);
+    if (!text) {
+      SmiXgmiSnapshot s;
+      s.error = "xgmi snapshot " + cfg_.xgmi_file + " unreadable";
+      return s;
+    }
+    return xgmi_from_json(*text);
+  }
+  return smi_xgmi_links();
+}
+
+void Engine::fabric_check() {
+  const SmiXgmiSnapshot snap = read_xgmi();
+  if (!snap.ok) {
+    if (snap.error != xgmi_error_) MI_LOG(kWarning, "xGMI link state unavailable: %s", snap.error.c_str());
+    xgmi_error_ = snap.error;
+    return;
+  }
+  xgmi_error_.clear();
+  std::set<std::pair<std::string, std::string>> degraded;
+  std::map<std::string, int> down;
+  auto pair = [](const std::string& a, const std::string& b) { return a <= b ? std::make_pair(a, b) : std::make_pair(b, a); };
+  for (const auto& g : snap.gpus) {
+    const std::string bdf = lower(g.bdf);
+    auto me_it = gpu_by_bdf_.find(bdf);
+    if (me_it == gpu_by_bdf_.end()) continue;  // a GPU this plugin does not advertise
+    const std::string& me = me_it->second;
+    int up = -1;
+    if (g.status_ok) up = static_cast<int>(std::count(g.status.begin(), g.status.end(), kLinkUp));
+    std::set<std::string> live;
+    if (g.metrics_ok)
+      for (const auto& p : g.peers) {
+        const std::string pb = lower(p.peer_bdf);
+        if (p.link_type == kLinkTypeXgmi && gpu_by_bdf_.count(pb) && p.bit_rate_gbps > 0) live.insert(pb);
+      }
+    auto base = xgmi_base_.find(bdf);
+    if (base == xgmi_base_.end()) {
+      xgmi_base_[bdf] = {up, live};
+      continue;
+    }
+    std::vector<std::string> lost_peers;
+    for (const auto& pb : base->second.second)
+      if (!live.count(pb)) lost_peers.push_back(pb);
+    const int lost_links = base->second.first >= 0 && up >= 0 ? base->second.first - up : 0;
+    if (!lost_peers.empty()) {
+      for (const auto& pb : lost_peers) degraded.insert(pair(me, gpu_by_bdf_.at(pb)));
+    } else if (lost_links > 0) {
+      // no peer can be named: every xGMI pair of this GPU
+      std::set<std::string> peers = base->second.second;
+      if (peers.empty())
+        for (const auto& [b, k] : gpu_by_bdf_)
+          if (b != bdf) peers.insert(b);
+      for (const auto& pb : peers) {
+        auto o = gpu_by_bdf_.find(pb);
+        if (o != gpu_by_bdf_.end() && o->second != me) degraded.insert(pair(me, o->second));
+      }
+    }
+    if (lost_links > 0 || !lost_peers.empty())
+      down[bdf] = std::max(lost_links, static_cast<int>(lost_peers.size()));
+  }
+  int total = 0;
+  for (const auto& [b, n] : down) total += n;
+  std::lock_guard<std::mutex> lk(mu_);
+  links_down_ = down;
+  if (degraded == degraded_) return;
+  for (const auto& p : degraded)
+    if (!degraded_.count(p))
+      MI_LOG(kWarning, "xGMI link between GPUs %s and %s is down: multi-GPU placement avoids the pair",
+             p.first.c_str(), p.second.c_str());
+  for (const auto& p : degraded_)
+    if (!degraded.count(p))
+      MI_LOG(kWarning, "xGMI link between GPUs %s and %s is back up", p.first.c_str(), p.second.c_str());
+  degraded_ = std::move(degraded);
+  fabric_version_++;
+  metrics::global().set("mi355x_dp_xgmi_links_down", total, {}, "xGMI links down vs the first reading");
+}
+
+std::vector<std::pair<std::string, std::string>> Engine::degraded_links() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return {degraded_.begin(), degraded_.end()};
+}
+
+uint64_t Engine::fabric_version() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return fabric_version_;
+}
+
+std::map<std::string, int> Engine::links_down() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return links_down_;
 }
 
 }  // namespace mi355x::health

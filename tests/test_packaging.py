@@ -245,9 +245,9 @@ def test_helm_native_daemon_switch():
     assert "fail " not in t
     native_branch = t[t.index("{{- if $native }}"):t.index("{{- else if")]
     for flag in ("-liveness=true", "-smi_ecc=true", "-smi_events=true", "-liveness_keep_queues", "-metrics_port",
-                 "-device_list_strategy", "-cdi_spec_dir"):
+                 "-device_list_strategy", "-cdi_spec_dir", "-smi_xgmi"):
         assert flag in native_branch
-    assert "$pyOnly := or .Values.dp.smi.xgmi .Values.dp.liveness.chipSweepEvery" in t
+    assert "$pyOnly := or .Values.dp.liveness.chipSweepEvery .Values.dp.liveness.perfCheckEvery" in t
     assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["dp"]["native"] is True
 
 
