@@ -51,6 +51,15 @@ class PyHealthEngine {
     b("smi_ecc", &c.smi_ecc);
     b("smi_events", &c.smi_events);
     b("smi_xgmi", &c.smi_xgmi);
+    i("chip_sweep_every", &c.chip_sweep_every);
+    i("perf_check_every", &c.perf_check_every);
+    s("perf_action", &c.perf_action);
+    d("perf_min_hbm_read_gbps", &c.perf_min_hbm_read_gbps);
+    d("perf_min_hbm_write_gbps", &c.perf_min_hbm_write_gbps);
+    d("perf_min_mfma_tflops", &c.perf_min_mfma_tflops);
+    d("perf_min_xcd_clock_ratio", &c.perf_min_xcd_clock_ratio);
+    i("perf_mib", &c.prober.perf_mib);
+    i("perf_iters", &c.prober.perf_iters);
     s("xgmi_file", &c.xgmi_file);
     s("probe_exe", &c.prober.exe);
     d("probe_timeout_s", &c.prober.timeout_s);
@@ -84,6 +93,8 @@ class PyHealthEngine {
     d["busy_state_known"] = eng_->busy_state_known();
     d["last_sweep_ms"] = eng_->last_sweep_ms();
     d["version"] = eng_->version();
+    d["chip_sweeps"] = eng_->chip_sweeps();
+    d["perf_checks"] = eng_->perf_checks();
     if (auto* p = eng_->prober()) {
       d["server_starts"] = p->server_starts;
       d["server_restarts"] = p->server_restarts;
@@ -94,6 +105,16 @@ class PyHealthEngine {
   }
   std::vector<std::pair<std::string, std::string>> degraded_links() const { return eng_->degraded_links(); }
   uint64_t fabric_version() const { return eng_->fabric_version(); }
+  std::map<std::string, std::pair<std::string, std::string>> perf_verdicts() const { return eng_->perf_verdicts(); }
+  std::vector<std::string> perf_problems(const py::dict& d) const {
+    health::ProbeOutcome o;
+    for (auto [k, v] : d) {
+      const std::string key = k.cast<std::string>();
+      if (key == "xcd_clock_mhz") o.xcd_clock_mhz = v.cast<std::vector<double>>();
+      else o.detail[key] = v.cast<double>();
+    }
+    return eng_->perf_problems(o);
+  }
   std::map<std::string, int> links_down() const { return eng_->links_down(); }
   void set_activity(std::optional<std::map<std::string, int>> a) {
     if (!a) eng_->activity_source = nullptr;
@@ -129,6 +150,8 @@ void bind_health(py::module_& m) {
            "bdf -> healthy used instead of the exporter socket (None = socket)")
       .def("degraded_links", &PyHealthEngine::degraded_links, "xGMI pairs (allocator group keys) degraded")
       .def("fabric_version", &PyHealthEngine::fabric_version)
+      .def("perf_verdicts", &PyHealthEngine::perf_verdicts, "device -> (ok | degraded | failed, reason)")
+      .def("perf_problems", &PyHealthEngine::perf_problems, py::arg("detail"))
       .def("links_down", &PyHealthEngine::links_down)
       .def("close", &PyHealthEngine::close);
   // a private registry (the process-wide one is metrics::global(), see `metrics_render`)

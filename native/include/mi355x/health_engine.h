@@ -63,6 +63,9 @@ struct ProbeOutcome {
   double latency_ms = 0;
   int kfd_node_id = -1;    // identity of the agent that answered (-1 / "" = not reported)
   std::string pci_bus_id;  // dddd:bb:dd.f
+  // throughput check replies: cu_count, hbm_read_gbps, hbm_write_gbps, mfma_tflops, clock_mhz_median
+  std::map<std::string, double> detail;
+  std::vector<double> xcd_clock_mhz;
 };
 
 struct ProberConfig {
@@ -75,6 +78,8 @@ struct ProberConfig {
   bool keep_queues = true;               // --serve --keep
   std::vector<std::pair<std::string, std::string>> extra_env;
   std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";
+  int perf_mib = 4096;        // throughput check: HBM buffer
+  int perf_iters = 1 << 16;   // throughput check: MFMA pairs per wave
 };
 
 // The probe processes (LivenessProber in health/liveness.py).
@@ -133,6 +138,18 @@ struct Config {
   int crowded_release_sweeps = 5;
   bool smi_ecc = false;
   bool smi_events = false;
+  // every N-th sweep (and the first): the full-chip sweep instead of the
+  // one-wave probe on GPUs no other process has queues on (0 = off)
+  int chip_sweep_every = 0;
+  // every N-th sweep (and the first): the throughput check on idle, live GPUs
+  // (HBM pattern bandwidth, bf16 MFMA rate, per-XCD clocks); floors per whole
+  // MI355X, scaled by the device's CU share; "unhealthy" withdraws degraded GPUs
+  int perf_check_every = 0;
+  std::string perf_action = "report";
+  double perf_min_hbm_read_gbps = 3000.0;
+  double perf_min_hbm_write_gbps = 2000.0;
+  double perf_min_mfma_tflops = 700.0;
+  double perf_min_xcd_clock_ratio = 0.6;
   bool smi_xgmi = false;
   std::string xgmi_file;  // JSON snapshot (smi_xgmi_links' shape) read instead of amd-smi: fault injection
 };
@@ -172,6 +189,12 @@ class Engine {
   uint64_t sweeps() const { return sweeps_; }
   uint64_t identity_remaps() const { return identity_remaps_; }
   uint64_t crowded_skips() const { return crowded_skips_; }
+  uint64_t chip_sweeps() const { return chip_sweeps_; }
+  uint64_t perf_checks() const { return perf_checks_; }
+  // device -> (ok | degraded | failed, reason) of its last throughput check
+  std::map<std::string, std::pair<std::string, std::string>> perf_verdicts() const;
+  // why a correct throughput reply counts as degraded ([] if it does not)
+  std::vector<std::string> perf_problems(const ProbeOutcome& o) const;
   bool busy_state_known() const { return busy_known_; }
   double last_sweep_ms() const { return last_sweep_ms_; }
 
@@ -194,6 +217,7 @@ class Engine {
   bool identity_matches(const GpuDevice& d, const ProbeOutcome& o) const;
   const GpuDevice* dev(const std::string& id) const;
   void fabric_check();
+  void perf_check(const std::map<std::string, int>& ords);
   SmiXgmiSnapshot read_xgmi();
 
   std::vector<GpuDevice> devices_;
@@ -211,7 +235,8 @@ class Engine {
   bool events_started_ = false;
   bool smi_held_ = false;
   bool busy_known_ = true;
-  uint64_t sweeps_ = 0, identity_remaps_ = 0, crowded_skips_ = 0;
+  uint64_t sweeps_ = 0, identity_remaps_ = 0, crowded_skips_ = 0, chip_sweeps_ = 0, perf_checks_ = 0;
+  std::map<std::string, std::pair<std::string, std::string>> perf_;  // guarded by mu_
   double last_sweep_ms_ = 0;
   int abort_fd_ = -1;
   // xGMI baseline: bdf -> (links up, -1 unknown; peers seen live)

@@ -123,6 +123,13 @@ struct Flags {
   bool smi_ecc = false;
   bool smi_events = false;
   bool smi_xgmi = false;  // xGMI link state re-weights preferred allocation
+  int liveness_chip_sweep_every = 0;
+  int perf_check_every = 0;
+  int perf_mib = 4096;
+  std::string perf_action = "report";
+  double perf_min_hbm_read_gbps = 3000.0;
+  double perf_min_mfma_tflops = 700.0;
+  double perf_min_xcd_clock_ratio = 0.6;
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
   double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
@@ -133,10 +140,8 @@ struct Flags {
 };
 
 // Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
-const std::set<std::string> kPythonOnly = {
-    "liveness_chip_sweep_every", "perf_check_every", "perf_mib", "perf_action", "perf_min_hbm_read_gbps",
-    "perf_min_mfma_tflops", "perf_min_xcd_clock_ratio", "grpc_server",
-    "topology_view", "node_view", "trace_file", "dry_run", "log_format"};
+const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view", "trace_file", "dry_run",
+                                           "log_format"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -156,17 +161,22 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"liveness_fail_threshold", &f->liveness_fail_threshold},
       {"liveness_recover_threshold", &f->liveness_recover_threshold},
       {"liveness_idle_sweeps", &f->liveness_idle_sweeps}, {"liveness_crowded_procs", &f->liveness_crowded_procs},
-      {"liveness_crowded_release_sweeps", &f->liveness_crowded_release_sweeps}, {"metrics_port", &f->metrics_port}};
+      {"liveness_crowded_release_sweeps", &f->liveness_crowded_release_sweeps}, {"metrics_port", &f->metrics_port},
+      {"liveness_chip_sweep_every", &f->liveness_chip_sweep_every}, {"perf_check_every", &f->perf_check_every},
+      {"perf_mib", &f->perf_mib}};
   std::map<std::string, double*> floats = {
       {"liveness_timeout", &f->liveness_timeout}, {"liveness_busy_grace", &f->liveness_busy_grace},
       {"liveness_unknown_busy_grace", &f->liveness_unknown_busy_grace}, {"grpc_watchdog", &f->grpc_watchdog_s},
-      {"register_timeout", &f->register_timeout_s}, {"topology_watch", &f->topology_watch_s}};
+      {"register_timeout", &f->register_timeout_s}, {"topology_watch", &f->topology_watch_s},
+      {"perf_min_hbm_read_gbps", &f->perf_min_hbm_read_gbps}, {"perf_min_mfma_tflops", &f->perf_min_mfma_tflops},
+      {"perf_min_xcd_clock_ratio", &f->perf_min_xcd_clock_ratio}};
   std::map<std::string, std::string*> strs = {
       {"driver_type", &f->driver_type}, {"resource_naming_strategy", &f->naming},
       {"kubelet_dir", &f->kubelet_dir}, {"sysfs_root", &f->sysfs_root}, {"dev_root", &f->dev_root},
       {"exporter_socket", &f->exporter_socket}, {"liveness_mode", &f->liveness_mode},
       {"liveness_probe", &f->liveness_probe}, {"config", &f->config}, {"allocator_search", &f->allocator_search},
-      {"device_list_strategy", &f->device_list_strategy}, {"cdi_spec_dir", &f->cdi_spec_dir}};
+      {"device_list_strategy", &f->device_list_strategy}, {"cdi_spec_dir", &f->cdi_spec_dir},
+      {"perf_action", &f->perf_action}};
   if (const char* c = std::getenv("CONFIG_FILE_PATH")) f->config = c;
   static std::string ignored;
   strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
@@ -191,7 +201,9 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-device_list_strategy device-specs|cdi-cri|cdi-annotations[,...]] [-cdi_spec_dir DIR] "
           "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
           "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
-          "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
+          "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
+          "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
+          "[-perf_min_mfma_tflops X] [-perf_min_xcd_clock_ratio X]]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
           "[-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
           "[-log_backtrace_at FILE:N]\n",
           argv[0]);
@@ -255,6 +267,11 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
            false;
   if (f->allocator_extended_search) f->allocator_search = "extended";
   if (f->liveness && f->pulse == 0) return *err = "-liveness needs -pulse > 0 (the probe runs once per pulse)", false;
+  if (f->perf_action != "report" && f->perf_action != "unhealthy")
+    return *err = "invalid perf_action provided: " + f->perf_action + ", supported values are report or unhealthy",
+           false;
+  if (f->perf_check_every > 0 && !f->liveness)
+    return *err = "perf_check_every needs -liveness (the throughput check runs in the probe server)", false;
   return true;
 }
 
@@ -836,6 +853,13 @@ int main(int argc, char** argv) {
     hc.smi_ecc = f.smi_ecc;
     hc.smi_events = f.smi_events;
     hc.smi_xgmi = f.smi_xgmi;
+    hc.chip_sweep_every = f.liveness_chip_sweep_every;
+    hc.perf_check_every = f.perf_check_every;
+    hc.perf_action = f.perf_action;
+    hc.perf_min_hbm_read_gbps = f.perf_min_hbm_read_gbps;
+    hc.perf_min_mfma_tflops = f.perf_min_mfma_tflops;
+    hc.perf_min_xcd_clock_ratio = f.perf_min_xcd_clock_ratio;
+    hc.prober.perf_mib = f.perf_mib;
     if (const char* x = std::getenv("MI355X_SMI_XGMI_FILE"); x && *x) hc.xgmi_file = x;  // fault injection
     engine = std::make_unique<health::Engine>(container_devices, topo, hc);
     fabric_seen = 0;

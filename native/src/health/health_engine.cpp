@@ -206,6 +206,11 @@ ProbeOutcome judge(bool doc_ok, const json::Value* d, uint32_t nonce, double ms,
   if (d) {
     o.kfd_node_id = static_cast<int>(jnum(d, "kfd_node_id", -1));
     o.pci_bus_id = jstr(d, "pci_bus_id");
+    for (const char* k : {"cu_count", "hbm_read_gbps", "hbm_write_gbps", "mfma_tflops", "clock_mhz_median"})
+      if (const json::Value* v = d->get(k); v && v->kind == json::Value::Number) o.detail[k] = std::strtod(v->s.c_str(), nullptr);
+    if (const json::Value* x = d->get("xcd_clock_mhz"); x && x->kind == json::Value::Array)
+      for (const auto& c : x->arr)
+        if (c.kind == json::Value::Number) o.xcd_clock_mhz.push_back(std::strtod(c.s.c_str(), nullptr));
   }
   if (rc != 0 || !doc_ok || !jbool(d, "ok")) {
     o.reason = jstr(d, "error");
@@ -325,6 +330,10 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
                                    std::string("--timeout"), std::string(tmo)})
         argv.push_back(a);
       if (kind == "sweep") argv.push_back("--sweep");
+      if (kind == "perf")
+        for (const std::string& a : {std::string("--perf"), std::string("--perf-mib"), std::to_string(cfg_.perf_mib),
+                                     std::string("--perf-iters"), std::to_string(cfg_.perf_iters)})
+          argv.push_back(a);
       std::string err;
       j.t0 = mono_s();
       if (!spawn_child(argv, child_env(cfg_, std::to_string(j.ordinal)), false, &j.c, &err)) {
@@ -455,7 +464,10 @@ std::map<int, ProbeOutcome> LivenessProber::probe_server(const std::vector<int>&
   for (int o : uniq) nonces[o] = make_nonce(o);
   const double inner = cfg_.timeout_s - std::min(0.5, 0.25 * cfg_.timeout_s);
   char head[96];
-  std::snprintf(head, sizeof(head), "%s %d %.2f", kind.c_str(), cfg_.iters, inner);
+  if (kind == "perf")
+    std::snprintf(head, sizeof(head), "perf %d %.2f %d", cfg_.perf_iters, inner, cfg_.perf_mib);
+  else
+    std::snprintf(head, sizeof(head), "%s %d %.2f", kind.c_str(), cfg_.iters, inner);
   std::string line = head;
   for (int o : uniq) line += " " + std::to_string(local[o]) + ":" + std::to_string(nonces[o]);
   if (!write_all(server_->c.in, line + "\n")) {
@@ -930,18 +942,35 @@ bool Engine::sweep() {
     } else {
       prober_->set_visible(std::nullopt);
     }
+    // idle GPUs (no other process's queues) for the full-chip sweep and the
+    // throughput check; none while busy state is unknown (both hold every CU)
+    std::set<std::string> idle;
+    if (known)
+      for (const auto& [id, o] : probe_ords)
+        if (int64_t g = gpu_id(id); g && !load_.count(g)) idle.insert(id);
     std::map<std::string, ProbeOutcome> outcomes;
     if (!probe_ords.empty()) {
-      std::vector<int> uniq;
-      std::set<int> busy_ords;
-      for (const auto& [id, o] : probe_ords) {
-        uniq.push_back(o);
-        if (busy_devs.count(id)) busy_ords.insert(o);
-      }
-      const auto by_ord = prober_->probe(uniq, busy_ords);
+      const bool chip = cfg_.chip_sweep_every > 0 && sweeps_ % static_cast<uint64_t>(cfg_.chip_sweep_every) == 0;
+      if (chip && !known) MI_LOG(kWarning, "full-chip sweep skipped: busy-GPU state unknown");
       std::map<std::string, ProbeOutcome> raw;
-      for (const auto& [id, o] : probe_ords)
-        if (auto it = by_ord.find(o); it != by_ord.end()) raw[id] = it->second;
+      auto run = [&](const std::map<std::string, int>& sel, const char* kind) {
+        std::vector<int> uniq;
+        std::set<int> busy_ords;
+        for (const auto& [id, o] : sel) {
+          uniq.push_back(o);
+          if (busy_devs.count(id)) busy_ords.insert(o);
+        }
+        const auto by_ord = prober_->probe(uniq, busy_ords, kind);
+        for (const auto& [id, o] : sel)
+          if (auto it = by_ord.find(o); it != by_ord.end()) raw[id] = it->second;
+      };
+      std::map<std::string, int> swept, rest;
+      for (const auto& [id, o] : probe_ords) (chip && idle.count(id) ? swept : rest)[id] = o;
+      if (!swept.empty()) {
+        run(swept, "sweep");
+        chip_sweeps_++;
+      }
+      if (!rest.empty()) run(rest, "probe");
       outcomes = verify_identity(probe_ords, raw);
     }
     if (!crowded.empty()) {
@@ -1009,6 +1038,16 @@ bool Engine::sweep() {
     }
     for (auto& [id, rs] : reasons)
       if (!ords.count(id)) rs.push_back("no HIP device for this ID (render node inaccessible?)");
+    if (cfg_.perf_check_every > 0 && sweeps_ % static_cast<uint64_t>(cfg_.perf_check_every) == 0) {
+      std::map<std::string, int> cand;
+      for (const auto& [id, o] : probe_ords)
+        if (idle.count(id) && track_[id].live && ords.count(id)) cand[id] = o;
+      if (!cand.empty()) perf_check(cand);
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& [id, pv] : perf_)
+      if (reasons.count(id) && (pv.first == "failed" || (pv.first == "degraded" && cfg_.perf_action == "unhealthy")))
+        reasons[id].push_back(pv.second);
   }
 
   if (cfg_.smi_ecc && smi_available()) {
@@ -1229,6 +1268,107 @@ uint64_t Engine::fabric_version() const {
 std::map<std::string, int> Engine::links_down() const {
   std::lock_guard<std::mutex> lk(mu_);
   return links_down_;
+}
+
+// ---- throughput check (health/monitor.py _perf_check) ----------------------------
+std::vector<std::string> Engine::perf_problems(const ProbeOutcome& o) const {
+  auto get = [&](const char* k) {
+    auto it = o.detail.find(k);
+    return it == o.detail.end() ? 0.0 : it->second;
+  };
+  const double cus = get("cu_count");
+  const double share = cus > 0 ? std::min(1.0, cus / 256.0) : 1.0;  // a CPX partition has 1/8 of the CUs
+  std::vector<std::string> out;
+  struct Floor {
+    const char* key;
+    double floor;
+    const char* what;
+    const char* unit;
+  };
+  for (const Floor& f : {Floor{"hbm_read_gbps", cfg_.perf_min_hbm_read_gbps, "HBM read", "GB/s"},
+                         Floor{"hbm_write_gbps", cfg_.perf_min_hbm_write_gbps, "HBM write", "GB/s"},
+                         Floor{"mfma_tflops", cfg_.perf_min_mfma_tflops, "bf16 MFMA", "TFLOP/s"}}) {
+    const double v = get(f.key);
+    if (f.floor > 0 && v < f.floor * share) {
+      char b[128];
+      std::snprintf(b, sizeof(b), "%s %.0f %s < %.0f", f.what, v, f.unit, f.floor * share);
+      out.push_back(b);
+    }
+  }
+  std::vector<double> clocks;
+  for (double c : o.xcd_clock_mhz)
+    if (c > 0) clocks.push_back(c);
+  if (clocks.size() >= 2 && cfg_.perf_min_xcd_clock_ratio > 0) {
+    std::vector<double> sorted = clocks;
+    std::sort(sorted.begin(), sorted.end());
+    const double med = sorted[sorted.size() / 2];
+    const size_t i = static_cast<size_t>(std::min_element(clocks.begin(), clocks.end()) - clocks.begin());
+    if (clocks[i] < cfg_.perf_min_xcd_clock_ratio * med) {
+      char b[128];
+      std::snprintf(b, sizeof(b), "XCD %zu at %.0f MHz vs median %.0f MHz under MFMA load", i, clocks[i], med);
+      out.push_back(b);
+    }
+  }
+  return out;
+}
+
+void Engine::perf_check(const std::map<std::string, int>& ords) {
+  std::vector<int> uniq;
+  for (const auto& [id, o] : ords) uniq.push_back(o);
+  const auto by_ord = prober_->probe(uniq, {}, "perf");
+  perf_checks_++;
+  auto& m = metrics::global();
+  m.inc("mi355x_dp_perf_checks_total", {}, 1.0, "throughput checks run (HBM pattern + MFMA + clocks)");
+  static const std::map<std::string, double> kState = {{"ok", 0.0}, {"degraded", 1.0}, {"failed", 2.0}};
+  for (const auto& [id, ord] : ords) {
+    auto it = by_ord.find(ord);
+    if (it == by_ord.end()) continue;
+    const ProbeOutcome& o = it->second;
+    std::string state = "ok", why;
+    if (!o.ok) {
+      state = "failed";
+      why = "throughput check: " + o.reason;
+    } else if (const auto probs = perf_problems(o); !probs.empty()) {
+      state = "degraded";
+      why = "throughput check: ";
+      for (size_t i = 0; i < probs.size(); ++i) why += (i ? "; " : "") + probs[i];
+    }
+    std::string prev = "ok";
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (auto p = perf_.find(id); p != perf_.end()) prev = p->second.first;
+      perf_[id] = {state, why};
+    }
+    if (state != prev)
+      glog::log(state == "ok" ? glog::kInfo : glog::kWarning, __FILE__, __LINE__, "device %s: throughput check %s -> %s %s",
+                id.c_str(), prev.c_str(), state.c_str(), why.c_str());
+    auto get = [&](const char* k) {
+      auto d = o.detail.find(k);
+      return d == o.detail.end() ? 0.0 : d->second;
+    };
+    if (o.ok)
+      MI_VLOG(2, "device %s: throughput HBM write %.0f / read %.0f GB/s, bf16 MFMA %.0f TFLOP/s at %.0f MHz", id.c_str(),
+              get("hbm_write_gbps"), get("hbm_read_gbps"), get("mfma_tflops"), get("clock_mhz_median"));
+    const metrics::Labels dev = {{"device", id}};
+    m.set("mi355x_dp_perf_state", kState.at(state), dev,
+          "last throughput check: 0 ok, 1 degraded (rates under the floors), 2 failed");
+    if (o.ok) {
+      m.set("mi355x_dp_perf_hbm_read_gbps", get("hbm_read_gbps"), dev, "last throughput check: HBM read bandwidth");
+      m.set("mi355x_dp_perf_hbm_write_gbps", get("hbm_write_gbps"), dev, "last throughput check: HBM write bandwidth");
+      m.set("mi355x_dp_perf_mfma_tflops", get("mfma_tflops"), dev,
+            "last throughput check: sustained dense bf16 MFMA rate");
+      m.set("mi355x_dp_perf_clock_mhz", get("clock_mhz_median"), dev,
+            "last throughput check: median workgroup shader clock under MFMA load");
+      for (size_t x = 0; x < o.xcd_clock_mhz.size(); ++x)
+        m.set("mi355x_dp_perf_xcd_clock_mhz", o.xcd_clock_mhz[x], {{"device", id}, {"xcd", std::to_string(x)}},
+              "last throughput check: median shader clock per XCD");
+    }
+  }
+}
+
+std::map<std::string, std::pair<std::string, std::string>> Engine::perf_verdicts() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return perf_;
 }
 
 }  // namespace mi355x::health

@@ -238,16 +238,17 @@ def test_alert_rules_use_exported_metrics():
 
 
 def test_helm_native_daemon_switch():
-    """dp.native (the default) runs the native daemon, health flags included; a
-    feature only the Python CLI has switches the chart to it instead of failing."""
+    """dp.native (the default) runs the native daemon with every chart value
+    (health, amd-smi, CDI, metrics, chip sweep, throughput check)."""
     t = (REPO / "helm/amd-gpu/templates/deviceplugin-daemonset.yaml").read_text()
     assert 'command: ["./mi355x-device-plugin"]' in t and "{{- if $native }}" in t
     assert "fail " not in t
     native_branch = t[t.index("{{- if $native }}"):t.index("{{- else if")]
     for flag in ("-liveness=true", "-smi_ecc=true", "-smi_events=true", "-liveness_keep_queues", "-metrics_port",
-                 "-device_list_strategy", "-cdi_spec_dir", "-smi_xgmi"):
+                 "-device_list_strategy", "-cdi_spec_dir", "-smi_xgmi",
+                 "-liveness_chip_sweep_every", "-perf_check_every", "-perf_action"):
         assert flag in native_branch
-    assert "$pyOnly := or .Values.dp.liveness.chipSweepEvery .Values.dp.liveness.perfCheckEvery" in t
+    assert "{{- $native := .Values.dp.native -}}" in t
     assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["dp"]["native"] is True
 
 
