@@ -969,6 +969,8 @@ bool Engine::sweep() {
       if (!swept.empty()) {
         run(swept, "sweep");
         chip_sweeps_++;
+        metrics::global().inc("mi355x_dp_chip_sweeps_total", {}, 1.0,
+                              "full-chip sweeps run (every CU of every XCD on the idle GPUs)");
       }
       if (!rest.empty()) run(rest, "probe");
       outcomes = verify_identity(probe_ords, raw);

@@ -474,6 +474,8 @@ class HealthMonitor:
             swept = await self.prober.sweep({k: v for k, v in ords.items() if k in idle})
             out.update(swept)
             self.chip_sweeps += 1
+            from ..utils.metrics import REGISTRY
+            REGISTRY.inc("mi355x_dp_chip_sweeps_total", help="full-chip sweeps run (every CU of every XCD on the idle GPUs)")
         rest = {k: v for k, v in ords.items() if k not in idle}
         if rest:
             out.update(await self.prober.probe(rest, busy=busy))

@@ -391,6 +391,60 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
     assert not [pid for pid in children if os.path.exists(f"/proc/{pid}")], children
 
 
+def test_native_daemon_chip_sweep_and_throughput_check(ordinals, tmp_path):
+    """mi355x-device-plugin runs the full-chip sweep and the throughput check
+    through its kept-queue probe server on the real GPU; the rates reach
+    /metrics and the device stays Healthy."""
+    import signal
+    import socket
+    import urllib.request
+    from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+
+    exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    dev_id = sorted(ordinals.items(), key=lambda kv: kv[1])[0][0]
+    kdir = str(tmp_path / "dp")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+
+    def metrics():
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+            return {k: float(v) for k, v in (ln.rsplit(" ", 1) for ln in r.read().decode().splitlines()
+                                             if ln and not ln.startswith("#"))}
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        proc = await asyncio.create_subprocess_exec(
+            exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_timeout", "30",
+            "-liveness_chip_sweep_every", "2", "-perf_check_every", "3", "-perf_mib", "1024",
+            "-metrics_port", str(port), stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 1, timeout=60)
+            m = {}
+            for _ in range(120):
+                m = await asyncio.to_thread(metrics)
+                if m.get("mi355x_dp_chip_sweeps_total", 0) >= 2 and m.get("mi355x_dp_perf_checks_total", 0) >= 1:
+                    break
+                await asyncio.sleep(0.5)
+            assert m.get("mi355x_dp_chip_sweeps_total", 0) >= 2, m
+            assert m[f'mi355x_dp_perf_state{{device="{dev_id}"}}'] == 0.0, m
+            assert m[f'mi355x_dp_perf_hbm_read_gbps{{device="{dev_id}"}}'] > 1000
+            assert m[f'mi355x_dp_perf_mfma_tflops{{device="{dev_id}"}}'] > 500
+            assert k.resources["amd.com/gpu"].devices[dev_id] == "Healthy"
+        finally:
+            if proc.returncode is None:
+                proc.send_signal(signal.SIGTERM)
+            _, err = await asyncio.wait_for(proc.communicate(), 30)
+            await k.stop()
+        assert proc.returncode == 0, err.decode(errors="replace")[-3000:]
+        return m
+
+    m = asyncio.run(asyncio.wait_for(go(), 240))
+    print(json.dumps({k: v for k, v in m.items() if "perf" in k or "chip" in k}))
+
+
 def test_probe_cli_corrupt_word_fails_the_tile():
     from rocm_k8s_device_plugin_amd.ops.native import probe_executable
     p = subprocess.run([str(probe_executable("hsa")), "--devices", "0", "--corrupt-word", "3"], capture_output=True,
