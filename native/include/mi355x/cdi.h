@@ -29,6 +29,7 @@ constexpr const char* kCdiAnnotations = "cdi-annotations";
 
 struct Strategies {
   bool specs = true, cri = false, annotations = false;
+  std::vector<std::string> order = {"device-specs"};  // as given (unique)
   bool cdi() const { return cri || annotations; }
 };
 

@@ -63,7 +63,8 @@ struct ProbeOutcome {
   double latency_ms = 0;
   int kfd_node_id = -1;    // identity of the agent that answered (-1 / "" = not reported)
   std::string pci_bus_id;  // dddd:bb:dd.f
-  // throughput check replies: cu_count, hbm_read_gbps, hbm_write_gbps, mfma_tflops, clock_mhz_median
+  // throughput check replies: cu_count, hbm_read_gbps, hbm_write_gbps, hbm_bad_words, mfma_tflops,
+  // clock_mhz_median, total_us
   std::map<std::string, double> detail;
   std::vector<double> xcd_clock_mhz;
 };
@@ -184,6 +185,8 @@ class Engine {
   std::vector<std::pair<std::string, std::string>> degraded_links() const;
   uint64_t fabric_version() const;  // bumped whenever the degraded set changes
   std::map<std::string, int> links_down() const;  // bdf -> links down vs the first reading
+  uint64_t xgmi_readings() const;
+  std::string xgmi_error() const;
 
   LivenessProber* prober() { return prober_.get(); }
   uint64_t sweeps() const { return sweeps_; }
@@ -193,6 +196,7 @@ class Engine {
   uint64_t perf_checks() const { return perf_checks_; }
   // device -> (ok | degraded | failed, reason) of its last throughput check
   std::map<std::string, std::pair<std::string, std::string>> perf_verdicts() const;
+  std::map<std::string, ProbeOutcome> perf_last() const;  // device -> its last throughput-check reply
   // why a correct throughput reply counts as degraded ([] if it does not)
   std::vector<std::string> perf_problems(const ProbeOutcome& o) const;
   bool busy_state_known() const { return busy_known_; }
@@ -237,6 +241,8 @@ class Engine {
   bool busy_known_ = true;
   uint64_t sweeps_ = 0, identity_remaps_ = 0, crowded_skips_ = 0, chip_sweeps_ = 0, perf_checks_ = 0;
   std::map<std::string, std::pair<std::string, std::string>> perf_;  // guarded by mu_
+  std::map<std::string, ProbeOutcome> perf_last_;                     // guarded by mu_
+  uint64_t xgmi_readings_ = 0;
   double last_sweep_ms_ = 0;
   int abort_fd_ = -1;
   // xGMI baseline: bdf -> (links up, -1 unknown; peers seen live)

@@ -58,6 +58,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -83,6 +84,7 @@
 #include "mi355x/metrics.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
+#include "../kube/json.h"
 #include "../kube/yaml.h"
 
 namespace {
@@ -131,6 +133,7 @@ struct Flags {
   double perf_min_mfma_tflops = 700.0;
   double perf_min_xcd_clock_ratio = 0.6;
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
+  bool dry_run = false;  // print the node report (what kubelet would be told) and exit
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
   double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
   std::string device_list_strategy = "device-specs";
@@ -140,8 +143,7 @@ struct Flags {
 };
 
 // Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
-const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view", "trace_file", "dry_run",
-                                           "log_format"};
+const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view", "trace_file", "log_format"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -155,7 +157,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"send_every_pulse", &f->send_every_pulse}, {"allocator_extended_search", &f->allocator_extended_search},
       {"liveness", &f->liveness}, {"liveness_keep_queues", &f->liveness_keep_queues},
       {"liveness_corroborate", &f->liveness_corroborate}, {"smi_ecc", &f->smi_ecc}, {"smi_events", &f->smi_events},
-      {"smi_xgmi", &f->smi_xgmi}};
+      {"smi_xgmi", &f->smi_xgmi}, {"dry_run", &f->dry_run}};
   std::map<std::string, int*> ints = {
       {"pulse", &f->pulse}, {"liveness_iters", &f->liveness_iters},
       {"liveness_fail_threshold", &f->liveness_fail_threshold},
@@ -204,7 +206,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
           "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
           "[-perf_min_mfma_tflops X] [-perf_min_xcd_clock_ratio X]]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
-          "[-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
+          "[-dry_run] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
           "[-log_backtrace_at FILE:N]\n",
           argv[0]);
       std::exit(0);
@@ -666,6 +668,111 @@ std::string self_dir() {
   return p.substr(0, p.rfind('/'));
 }
 
+// ---- -dry_run: the node report (cli/device_plugin.py dry_run_report) ----------
+json::Value jnum(double v) {
+  json::Value x;
+  x.kind = json::Value::Number;
+  char b[64];
+  if (v == static_cast<double>(static_cast<long long>(v)) && std::fabs(v) < 1e15)
+    std::snprintf(b, sizeof(b), "%lld", static_cast<long long>(v));
+  else
+    std::snprintf(b, sizeof(b), "%.17g", v);
+  x.s = b;
+  return x;
+}
+json::Value jbool(bool v) {
+  json::Value x;
+  x.kind = json::Value::Bool;
+  x.b = v;
+  return x;
+}
+json::Value jarr() {
+  json::Value x;
+  x.kind = json::Value::Array;
+  return x;
+}
+json::Value jnull() { return json::Value{}; }
+
+// xGMI fabric of an allocated set (parallel/fabric.py Fabric.report): whether it
+// is one hive, and the ring all-reduce bound its links imply (GB/s)
+struct FabricReport {
+  bool one_hive = false;
+  bool has_bound = false;
+  double bound_gbs = 0;
+};
+
+int model_xgmi_link_mbps(int device_id, int gfx) {  // models/gpu.py xgmi_link_mbps
+  switch (device_id) {
+    case 0x75a3: case 0x75b3: return 76000;  // MI355X (measured)
+    case 0x74a1: case 0x74a2: return 64000;  // MI300X / MI308X
+    case 0x740f: return 50000;               // MI210
+  }
+  switch (gfx) {
+    case 90500: return 76000;
+    case 90402: return 64000;
+    case 90010: return 50000;
+  }
+  return 0;
+}
+
+FabricReport fabric_report(const std::vector<const GpuDevice*>& devs, const KfdTopology& topo) {
+  std::map<std::pair<int, int>, std::pair<int, int64_t>> links;  // io_links win over p2p_links
+  for (const KfdNode* n : topo.gpu_nodes()) {
+    for (const auto& l : n->p2p_links) links[{l.node_from, l.node_to}] = {l.type, l.max_bandwidth};
+    for (const auto& l : n->io_links) links[{l.node_from, l.node_to}] = {l.type, l.max_bandwidth};
+  }
+  auto link = [&](const GpuDevice* a, const GpuDevice* b) -> std::pair<std::string, int64_t> {
+    if (!a->unique_id.empty() && a->unique_id == b->unique_id) return {"same_gpu", 0};
+    auto it = links.find({a->node_id, b->node_id});
+    if (it == links.end()) it = links.find({b->node_id, a->node_id});
+    if (it == links.end()) return {"unknown", 0};
+    int64_t bw = it->second.second;
+    if (it->second.first == kLinkXgmi) {
+      if (bw <= 0) bw = model_xgmi_link_mbps(a->pci_device_id, a->gfx_target_version);
+      return {"xgmi", bw};
+    }
+    if (it->second.first == kLinkPcie) return {"pcie", bw};
+    return {"unknown", bw};
+  };
+  FabricReport rep;
+  std::vector<const GpuDevice*> reps;
+  std::set<std::string> seen;
+  std::set<uint64_t> hives;
+  for (const GpuDevice* d : devs) {
+    hives.insert(d->hive_id);
+    if (seen.insert(!d->unique_id.empty() ? d->unique_id : d->bdf).second) reps.push_back(d);
+  }
+  rep.one_hive = hives.size() == 1 && !hives.count(0);
+  if (reps.size() <= 1) return rep;
+  int64_t egress_min = -1;
+  std::vector<std::pair<std::string, int64_t>> slow;
+  for (const GpuDevice* a : reps) {
+    int64_t eg = 0;
+    for (const GpuDevice* b : reps) {
+      if (a == b) continue;
+      const auto [cls, bw] = link(a, b);
+      if (cls == "xgmi") eg += bw;
+      else slow.emplace_back(cls, bw);
+    }
+    egress_min = egress_min < 0 ? eg : std::min(egress_min, eg);
+  }
+  if (slow.empty() && egress_min > 0) {
+    rep.has_bound = true;
+    rep.bound_gbs = static_cast<double>(egress_min) / 1000.0;
+  } else if (std::any_of(slow.begin(), slow.end(), [](const auto& x) { return x.first == "unknown"; })) {
+    // no bound without kfd links
+  } else if (!slow.empty()) {
+    int64_t mn = -1;
+    for (const auto& [c, bw] : slow)
+      if (bw > 0) mn = mn < 0 ? bw : std::min(mn, bw);
+    if (mn > 0) {
+      rep.has_bound = true;
+      rep.bound_gbs = static_cast<double>(mn) / 1000.0;
+    }
+  }
+  return rep;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -701,6 +808,8 @@ int main(int argc, char** argv) {
   std::vector<Resource> resources;
   KfdTopology topo;
   std::vector<GpuDevice> container_devices;  // every advertised container-mode device (health engine)
+  std::vector<std::string> discovery_warnings;
+  bool impl_ok = true;  // a driver initialised (auto mode: container -> VF -> PF)
   Driver driver = Driver::Container;
   // one driver's resources; "" on success (an empty list = no devices), else the init error
   auto init_container = [&](std::vector<Resource>* out) -> std::string {
@@ -709,6 +818,7 @@ int main(int argc, char** argv) {
     DiscoveryResult res = discover_gpus(f.sysfs_root, topo);
     res.devices = limit_physical(res.devices, dev_limit);
     for (const auto& w : res.warnings) MI_LOG(kWarning, "%s", w.c_str());
+    discovery_warnings = res.warnings;
     MI_LOG(kInfo, "Found %zu AMDGPUs", res.devices.size());
     auto& m = metrics::global();
     m.set("mi355x_dp_kfd_unreadable_nodes", static_cast<double>(res.kfd_unreadable_nodes.size()), {},
@@ -784,6 +894,7 @@ int main(int argc, char** argv) {
              : f.driver_type == "vf-passthrough" ? Driver::Vf : Driver::Pf;
   } else {
     // container -> VF -> PF; the reference starts its manager even when none initialised, and idles
+    bool impl_found = false;
     for (const char* type : {"container", "vf-passthrough", "pf-passthrough"}) {
       std::vector<Resource> got;
       const std::string e = init_driver(type, &got);
@@ -796,10 +907,12 @@ int main(int argc, char** argv) {
         continue;
       }
       resources = std::move(got);
+      impl_found = true;
       driver = std::string(type) == "container" ? Driver::Container
                : std::string(type) == "vf-passthrough" ? Driver::Vf : Driver::Pf;
       break;
     }
+    impl_ok = impl_found;
   }
 
   // ---- CDI specs (-device_list_strategy cdi-*): written before registration,
@@ -921,6 +1034,120 @@ int main(int argc, char** argv) {
     // real verdicts (the reference advertises everything Healthy until its first pulse)
     const auto h = health_pass();
     for (auto& r : resources) apply_health(r, h);
+  }
+
+  if (f.dry_run) {
+    json::Value out = json::Value::object();
+    const char* impl_name = driver == Driver::Container ? "container" : driver == Driver::Vf ? "vf-passthrough"
+                                                                                            : "pf-passthrough";
+    out.set("implementation", impl_ok ? json::Value::string(impl_name) : jnull());
+    json::Value res = json::Value::object();
+    for (const auto& r : resources) {
+      json::Value rv = json::Value::object();
+      json::Value devs = jarr();
+      std::vector<std::string> ids;
+      auto health_of = [&](const std::string& id) {
+        auto it = r.health.find(id);
+        return json::Value::string(it == r.health.end() || it->second ? "Healthy" : "Unhealthy");
+      };
+      for (const auto& g : r.group_ids) {
+        json::Value d = json::Value::object();
+        d.set("id", json::Value::string(g));
+        d.set("health", health_of(g));
+        d.set("numa", jarr());
+        devs.arr.push_back(d);
+        ids.push_back(g);
+      }
+      std::map<std::string, const GpuDevice*> by_id;
+      for (const auto& gd : r.devices) {
+        json::Value d = json::Value::object();
+        d.set("id", json::Value::string(gd.id));
+        d.set("health", health_of(gd.id));
+        json::Value numa = jarr();
+        if (gd.numa_node >= 0) numa.arr.push_back(jnum(gd.numa_node));
+        d.set("numa", numa);
+        devs.arr.push_back(d);
+        ids.push_back(gd.id);
+        by_id[gd.id] = &gd;
+      }
+      rv.set("devices", devs);
+      rv.set("preferred_allocation", jbool(r.allocator != nullptr));
+      if (r.allocator && !ids.empty()) {
+        json::Value prefs = json::Value::object();
+        std::set<int> ks = {1, 2, 4, 8, static_cast<int>(ids.size())};
+        for (int k : ks) {
+          if (k < 1 || k > static_cast<int>(ids.size())) continue;
+          const AllocResult a = r.allocator->allocate(ids, {}, k);
+          json::Value pv = json::Value::object();
+          json::Value chosen = jarr();
+          std::vector<const GpuDevice*> set;
+          for (const auto& id : a.ids) {
+            chosen.arr.push_back(json::Value::string(id));
+            if (by_id.count(id)) set.push_back(by_id[id]);
+          }
+          pv.set("ids", chosen);
+          if (driver == Driver::Container) {
+            const FabricReport fr = fabric_report(set, topo);
+            pv.set("one_hive", jbool(fr.one_hive));
+            pv.set("allreduce_bound_gbs", fr.has_bound ? jnum(fr.bound_gbs) : jnull());
+          }
+          prefs.set(std::to_string(k), pv);
+        }
+        rv.set("allocations", prefs);
+      }
+      res.set(std::string(kResourceNamespace) + "/" + r.name, rv);
+    }
+    out.set("resources", res);
+    if (driver == Driver::Container && impl_ok) {
+      json::Value w = jarr();
+      for (const auto& x : discovery_warnings) w.arr.push_back(json::Value::string(x));
+      out.set("warnings", w);
+      json::Value ls = jarr();
+      for (const auto& x : f.lists.order) ls.arr.push_back(json::Value::string(x));
+      out.set("device_list_strategy", ls);
+      if (f.lists.cdi()) out.set("cdi_spec_dir", json::Value::string(f.cdi_spec_dir));
+    }
+    if (engine && f.smi_xgmi) {
+      json::Value x = json::Value::object();
+      x.set("readings", jnum(static_cast<double>(engine->xgmi_readings())));
+      x.set("error", json::Value::string(engine->xgmi_error()));
+      json::Value pairs = jarr();
+      for (const auto& [a, b] : engine->degraded_links()) {
+        json::Value pr = jarr();
+        pr.arr.push_back(json::Value::string(a));
+        pr.arr.push_back(json::Value::string(b));
+        pairs.arr.push_back(pr);
+      }
+      x.set("degraded_pairs", pairs);
+      json::Value down = json::Value::object();
+      for (const auto& [bdf, n] : engine->links_down()) down.set(bdf, jnum(n));
+      x.set("links_down", down);
+      out.set("xgmi", x);
+    }
+    if (engine && !engine->perf_last().empty()) {
+      const auto verdicts = engine->perf_verdicts();
+      json::Value thr = json::Value::object();
+      for (const auto& [dev, o] : engine->perf_last()) {
+        json::Value t = json::Value::object();
+        auto v = verdicts.find(dev);
+        t.set("state", json::Value::string(v == verdicts.end() ? "ok" : v->second.first));
+        t.set("reason", json::Value::string(v == verdicts.end() ? "" : v->second.second));
+        for (const char* k : {"hbm_write_gbps", "hbm_read_gbps", "hbm_bad_words", "mfma_tflops", "clock_mhz_median"})
+          if (auto d = o.detail.find(k); d != o.detail.end()) t.set(k, jnum(d->second));
+        if (!o.xcd_clock_mhz.empty()) {
+          json::Value xs = jarr();
+          for (double c : o.xcd_clock_mhz) xs.arr.push_back(jnum(c));
+          t.set("xcd_clock_mhz", xs);
+        }
+        if (auto d = o.detail.find("total_us"); d != o.detail.end()) t.set("total_us", jnum(d->second));
+        thr.set(dev, t);
+      }
+      out.set("throughput", thr);
+    }
+    std::printf("%s\n", json::serialize(out).c_str());
+    std::fflush(stdout);
+    if (engine) engine->close();
+    return 0;
   }
 
   metrics::HttpEndpoint metrics_http;

@@ -206,7 +206,8 @@ ProbeOutcome judge(bool doc_ok, const json::Value* d, uint32_t nonce, double ms,
   if (d) {
     o.kfd_node_id = static_cast<int>(jnum(d, "kfd_node_id", -1));
     o.pci_bus_id = jstr(d, "pci_bus_id");
-    for (const char* k : {"cu_count", "hbm_read_gbps", "hbm_write_gbps", "mfma_tflops", "clock_mhz_median"})
+    for (const char* k : {"cu_count", "hbm_read_gbps", "hbm_write_gbps", "hbm_bad_words", "mfma_tflops",
+                          "clock_mhz_median", "total_us"})
       if (const json::Value* v = d->get(k); v && v->kind == json::Value::Number) o.detail[k] = std::strtod(v->s.c_str(), nullptr);
     if (const json::Value* x = d->get("xcd_clock_mhz"); x && x->kind == json::Value::Array)
       for (const auto& c : x->arr)
@@ -1199,6 +1200,7 @@ void Engine::fabric_check() {
     return;
   }
   xgmi_error_.clear();
+  xgmi_readings_++;
   std::set<std::pair<std::string, std::string>> degraded;
   std::map<std::string, int> down;
   auto pair = [](const std::string& a, const std::string& b) { return a <= b ? std::make_pair(a, b) : std::make_pair(b, a); };
@@ -1340,6 +1342,7 @@ void Engine::perf_check(const std::map<std::string, int>& ords) {
       std::lock_guard<std::mutex> lk(mu_);
       if (auto p = perf_.find(id); p != perf_.end()) prev = p->second.first;
       perf_[id] = {state, why};
+      perf_last_[id] = o;
     }
     if (state != prev)
       glog::log(state == "ok" ? glog::kInfo : glog::kWarning, __FILE__, __LINE__, "device %s: throughput check %s -> %s %s",
@@ -1367,6 +1370,14 @@ void Engine::perf_check(const std::map<std::string, int>& ords) {
     }
   }
 }
+
+std::map<std::string, ProbeOutcome> Engine::perf_last() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return perf_last_;
+}
+
+uint64_t Engine::xgmi_readings() const { return xgmi_readings_; }
+std::string Engine::xgmi_error() const { return xgmi_error_; }
 
 std::map<std::string, std::pair<std::string, std::string>> Engine::perf_verdicts() const {
   std::lock_guard<std::mutex> lk(mu_);

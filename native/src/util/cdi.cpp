@@ -69,6 +69,7 @@ std::string edits_json(const std::vector<std::string>& paths, int lvl) {
 bool parse_strategies(const std::string& value, Strategies* out, std::string* err) {
   Strategies s;
   s.specs = false;
+  s.order.clear();
   bool any = false;
   size_t start = 0;
   const std::string v = value.empty() ? kDeviceSpecs : value;
@@ -80,6 +81,9 @@ bool parse_strategies(const std::string& value, Strategies* out, std::string* er
     item.erase(item.find_last_not_of(" \t") + 1);
     start = end + 1;
     if (item.empty()) continue;
+    if (std::find(s.order.begin(), s.order.end(), item) == s.order.end() &&
+        (item == kDeviceSpecs || item == kCdiCri || item == kCdiAnnotations))
+      s.order.push_back(item);
     if (item == kDeviceSpecs) s.specs = true;
     else if (item == kCdiCri) s.cri = true;
     else if (item == kCdiAnnotations) s.annotations = true;
@@ -89,7 +93,10 @@ bool parse_strategies(const std::string& value, Strategies* out, std::string* er
              false;
     any = true;
   }
-  if (!any) s.specs = true;
+  if (!any) {
+    s.specs = true;
+    s.order = {kDeviceSpecs};
+  }
   *out = s;
   return true;
 }

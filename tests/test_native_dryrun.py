@@ -1,0 +1,86 @@
+"""`mi355x-device-plugin -dry_run`: the node report (what kubelet would be
+told, the preferred sets for 1/2/4/8/all devices with their xGMI fabric, CDI
+settings, health) equals the Python CLI's `-dry_run` on the same node; with
+the health engine on, it carries the throughput check and xGMI sections."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+
+from test_native_health import EXE, STUB
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+
+
+def _norm(doc):
+    for r in doc["resources"].values():
+        r["devices"] = sorted(r["devices"], key=lambda d: d["id"])
+    return doc
+
+
+def _both(fi, tmp_path, *args):
+    common = ["-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket", "",
+              "-kubelet_dir", str(tmp_path / "dp"), *args]
+    nat = subprocess.run([EXE, *common], capture_output=True, text=True, timeout=60)
+    assert nat.returncode == 0, nat.stderr[-2000:]
+    py = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.device_plugin", *common],
+                        capture_output=True, text=True, timeout=120, env=dict(os.environ, PYTHONPATH=REPO))
+    assert py.returncode == 0, py.stderr[-2000:]
+    return _norm(json.loads(nat.stdout)), _norm(json.loads(py.stdout))
+
+
+@pytest.mark.parametrize("partition,args", [
+    ("spx", []),
+    ("cpx", []),
+    ("cpx", ["-resource_naming_strategy", "mixed", "-device_list_strategy", "cdi-cri,device-specs"]),
+    ("dpx", ["-pulse", "1"]),
+])
+def test_report_equals_the_python_cli(tmp_path, partition, args):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition=partition)
+    extra = list(args)
+    if "-device_list_strategy" in extra:
+        extra += ["-cdi_spec_dir", str(tmp_path / "cdi")]
+    nat, py = _both(fi, tmp_path, *extra)
+    assert nat == py
+    assert nat["implementation"] == "container" and nat["resources"]
+    for r in nat["resources"].values():
+        assert r["preferred_allocation"] and "1" in r["allocations"]
+
+
+def test_whole_node_allocation_reports_the_ring_bound(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    nat, _ = _both(fi, tmp_path)
+    a8 = nat["resources"]["amd.com/gpu"]["allocations"]["8"]
+    assert len(a8["ids"]) == 8 and a8["one_hive"] and a8["allreduce_bound_gbs"] == 7 * 76.0
+
+
+def test_report_with_health_engine_sections(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text(json.dumps({"perf": {"2": "slow_hbm"}}))
+    xg = tmp_path / "xgmi.json"
+    xg.write_text(json.dumps({"ok": True, "error": "", "gpus": []}))
+    p = subprocess.run([EXE, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                        "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_probe", STUB,
+                        "-perf_check_every", "1", "-smi_xgmi"], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, MI355X_STUB_PROBE_CONTROL=str(ctl), MI355X_SMI_XGMI_FILE=str(xg)))
+    assert p.returncode == 0, p.stderr[-2000:]
+    doc = json.loads(p.stdout)
+    thr = doc["throughput"]
+    assert len(thr) == 8 and sorted(s["state"] for s in thr.values()).count("degraded") == 1
+    slow = [d for d, s in thr.items() if s["state"] == "degraded"][0]
+    assert "HBM read 1500" in thr[slow]["reason"] and thr[slow]["hbm_read_gbps"] == 1500
+    ok = [s for s in thr.values() if s["state"] == "ok"][0]
+    assert ok["hbm_read_gbps"] == 6000 and len(ok["xcd_clock_mhz"]) == 8
+    assert doc["xgmi"] == {"readings": 1, "error": "", "degraded_pairs": [], "links_down": {}}
+    assert all(d["health"] == "Healthy" for d in doc["resources"]["amd.com/gpu"]["devices"])

@@ -253,8 +253,8 @@ def test_helm_native_daemon_switch():
 
 
 def test_launcher_dispatches_native_first(tmp_path):
-    """./k8s-device-plugin (the image command) runs the native daemon; a
-    Python-only flag (here -dry_run) runs the Python CLI."""
+    """./k8s-device-plugin (the image command) runs the native daemon (here its
+    -dry_run report); a Python-only flag (-grpc_server) runs the Python CLI."""
     import subprocess
     import sys
     from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
@@ -262,10 +262,14 @@ def test_launcher_dispatches_native_first(tmp_path):
     p = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=60)
     assert p.returncode == 0 and "mi355x-device-plugin" in p.stdout and "-liveness_probe" in p.stdout, p.stderr
     fi = make_mi355x_node(tmp_path / "n")
-    p = subprocess.run([launcher, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
-                        "-exporter_socket", "", "-kubelet_dir", str(tmp_path / "dp")], capture_output=True, text=True,
-                       timeout=120)
+    base = [launcher, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket", "",
+            "-kubelet_dir", str(tmp_path / "dp")]
+    p = subprocess.run(base, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and json.loads(p.stdout)["resources"], p.stderr[-2000:]
+    assert "native daemon" in p.stderr                      # mi355x-device-plugin's banner
+    p = subprocess.run(base + ["-grpc_server", "aio"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and json.loads(p.stdout)["resources"], p.stderr[-2000:]
+    assert "native daemon" not in p.stderr
     env = dict(os.environ, MI355X_DP_IMPL="python")
     p = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode == 0 and "-grpc_server" in p.stdout
