@@ -17,11 +17,16 @@
 //                         file's base name without extension, or on the path
 //                         when the pattern contains '/')
 //   -log_backtrace_at=f:N a record logged from file f, line N carries a stack trace
+//   -log_format=json      one JSON object per record instead of the glog line:
+//                         {"ts", "level", "src", "msg"} plus the record's fields,
+//                         as the Python CLIs' JsonFormatter (utils/log.py) writes
 //
 // Thread-safe; line format "Lmmdd hh:mm:ss.uuuuuu tid file:line] msg".
 #pragma once
 
 #include <string>
+#include <utility>
+#include <vector>
 
 namespace mi355x::glog {
 
@@ -36,7 +41,10 @@ struct Options {
   std::string vmodule;
   std::string log_backtrace_at;
   std::string program;  // file name prefix (default: basename of argv[0])
+  bool json = false;    // -log_format=json
 };
+
+using Fields = std::vector<std::pair<std::string, std::string>>;
 
 // One command-line flag: true if `name` is a glog flag (then *err may be set
 // for a bad value). `has_value` = "-name=value" form; boolean flags accept
@@ -48,6 +56,9 @@ bool is_bool_flag(const std::string& name);
 std::string init(const Options& o);
 
 void log(Severity sev, const char* file, int line, const char* fmt, ...) __attribute__((format(printf, 4, 5)));
+// A record with structured fields: "msg k=v ..." in glog format, extra keys in JSON
+// (utils/log.py info_fields).
+void log_fields(Severity sev, const char* file, int line, const std::string& msg, const Fields& fields);
 bool vlog_is_on(int level, const char* file);
 // path of the current file of `sev` ("" before the first record / with -logtostderr)
 std::string file_path(Severity sev);
@@ -55,6 +66,8 @@ std::string file_path(Severity sev);
 }  // namespace mi355x::glog
 
 #define MI_LOG(sev, ...) ::mi355x::glog::log(::mi355x::glog::sev, __FILE__, __LINE__, __VA_ARGS__)
+#define MI_LOG_FIELDS(sev, msg, ...) \
+  ::mi355x::glog::log_fields(::mi355x::glog::sev, __FILE__, __LINE__, msg, ::mi355x::glog::Fields __VA_ARGS__)
 #define MI_VLOG(level, ...)                                      \
   do {                                                           \
     if (::mi355x::glog::vlog_is_on(level, __FILE__)) MI_LOG(kInfo, __VA_ARGS__); \

@@ -143,7 +143,7 @@ struct Flags {
 };
 
 // Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
-const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view", "trace_file", "log_format"};
+const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view", "trace_file"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -206,7 +206,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
           "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
           "[-perf_min_mfma_tflops X] [-perf_min_xcd_clock_ratio X]]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
-          "[-dry_run] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
+          "[-dry_run] [-log_format glog|json] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
           "[-log_backtrace_at FILE:N]\n",
           argv[0]);
       std::exit(0);
@@ -1355,8 +1355,12 @@ int main(int argc, char** argv) {
             for (const auto& id : ev.ids) ids += (ids.empty() ? "" : ",") + id;
             MI_LOG(kInfo, "Allocating device IDs: %s", ids.c_str());
           }
-          MI_VLOG(2, "rpc %s resource=%s latency_ms=%.3f", ev.rpc.c_str(), resources[i].name.c_str(),
-                  ev.dur_ns / 1e6);
+          if (glog::vlog_is_on(2, __FILE__)) {
+            char ms[32];
+            std::snprintf(ms, sizeof(ms), "%.3f", ev.dur_ns / 1e6);
+            MI_LOG_FIELDS(kInfo, "rpc", ({{"rpc", ev.rpc}, {"resource", resources[i].name}, {"latency_ms", ms},
+                                          {"native", "True"}}));
+          }
         }
       }
     // ---- kubelet restarts: act only when kubelet.sock itself was replaced

@@ -116,7 +116,6 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
   for (const auto& k : kKinds) f->enabled[k] = false;
   if (const char* n = std::getenv("DS_NODE_NAME")) f->node_name = n;
   static const std::set<std::string> kBool = {"watch", "dry_run", "once"};
-  static const std::set<std::string> kIgnoredValue = {"log_format"};
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a.size() < 2 || a[0] != '-') return *err = "unexpected argument " + a, false;
@@ -189,7 +188,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       f->token_file = value;
     } else if (name == "ca_file") {
       f->ca_file = value;
-    } else if (!kIgnoredValue.count(name)) {
+    } else {
       return *err = "flag provided but not defined: -" + name, false;
     }
   }
@@ -689,7 +688,7 @@ class Labeller {
       return fail("reconcile of node " + f_.node_name + " failed: " + describe(r));
     }
     ++st.patches;
-    MI_LOG(kInfo, "node labels updated node=%s changed=%zu", f_.node_name.c_str(), patch.size());
+    MI_LOG_FIELDS(kInfo, "node labels updated", ({{"node", f_.node_name}, {"changed", std::to_string(patch.size())}}));
     return true;
   }
 

@@ -1,6 +1,8 @@
 // glog output rules for the native daemons (see mi355x/glog.h).
 #include "mi355x/glog.h"
 
+#include "../kube/json.h"
+
 #include <execinfo.h>
 #include <fnmatch.h>
 #include <pwd.h>
@@ -136,6 +138,12 @@ bool parse_flag(const std::string& name, const std::string& value, bool has_valu
   if (name == "log_dir") return o->log_dir = value, true;
   if (name == "vmodule") return o->vmodule = value, true;
   if (name == "log_backtrace_at") return o->log_backtrace_at = value, true;
+  if (name == "log_format") {
+    if (value == "json") o->json = true;
+    else if (value == "glog" || value.empty()) o->json = false;
+    else *err = "invalid value \"" + value + "\" for flag -log_format (glog | json)";
+    return true;
+  }
   return false;
 }
 
@@ -201,34 +209,50 @@ std::string file_path(Severity sev) {
   return s.paths[sev];
 }
 
-void log(Severity sev, const char* file, int line, const char* fmt, ...) {
+namespace {
+
+const char* kJsonLevel[4] = {"INFO", "WARNING", "ERROR", "CRITICAL"};  // Python logging level names
+
+void emit(Severity sev, const char* file, int line, const std::string& msg, const Fields& fields) {
   timespec ts{};
   clock_gettime(CLOCK_REALTIME, &ts);
   tm lt{};
   localtime_r(&ts.tv_sec, &lt);
-  char msg[2048];
-  va_list ap;
-  va_start(ap, fmt);
-  std::vsnprintf(msg, sizeof(msg), fmt, ap);
-  va_end(ap);
   const char* base = std::strrchr(file, '/');
   base = base ? base + 1 : file;
-  char head[128];
-  std::snprintf(head, sizeof(head), "%c%02d%02d %02d:%02d:%02d.%06ld %7ld %s:%d] ", kSevChar[sev], lt.tm_mon + 1,
-                lt.tm_mday, lt.tm_hour, lt.tm_min, lt.tm_sec, ts.tv_nsec / 1000, static_cast<long>(::syscall(SYS_gettid)),
-                base, line);
-  std::string rec = std::string(head) + msg + "\n";
   State& s = state();
   std::lock_guard<std::mutex> lk(s.mu);
+  const Options& o = s.opt;
+  std::string rec;
+  if (o.json) {
+    char t[48];
+    std::snprintf(t, sizeof(t), "%lld.%06ld", static_cast<long long>(ts.tv_sec), ts.tv_nsec / 1000);
+    rec = std::string("{\"ts\": ") + t + ", \"level\": \"" + kJsonLevel[sev] + "\", \"src\": " +
+          json::quote(std::string(base) + ":" + std::to_string(line)) + ", \"msg\": " + json::quote(msg);
+    for (const auto& [k, v] : fields) rec += ", " + json::quote(k) + ": " + json::quote(v);
+  } else {
+    char head[128];
+    std::snprintf(head, sizeof(head), "%c%02d%02d %02d:%02d:%02d.%06ld %7ld %s:%d] ", kSevChar[sev], lt.tm_mon + 1,
+                  lt.tm_mday, lt.tm_hour, lt.tm_min, lt.tm_sec, ts.tv_nsec / 1000,
+                  static_cast<long>(::syscall(SYS_gettid)), base, line);
+    rec = head + msg;
+    for (const auto& [k, v] : fields) rec += " " + k + "=" + v;
+  }
+  std::string trace;
   if (s.bt_line == line && s.bt_file == base) {
     void* frames[64];
     const int n = ::backtrace(frames, 64);
     if (char** syms = ::backtrace_symbols(frames, n)) {
-      for (int i = 1; i < n; ++i) rec += std::string("    ") + syms[i] + "\n";
+      for (int i = 2; i < n; ++i) trace += std::string("    ") + syms[i] + "\n";
       std::free(syms);
     }
   }
-  const Options& o = s.opt;
+  if (o.json) {
+    if (!trace.empty()) rec += ", \"exc\": " + json::quote(trace);
+    rec += "}\n";
+  } else {
+    rec += "\n" + trace;
+  }
   if (o.logtostderr || o.alsologtostderr || sev >= o.stderrthreshold) {
     std::fputs(rec.c_str(), stderr);
     std::fflush(stderr);
@@ -242,6 +266,21 @@ void log(Severity sev, const char* file, int line, const char* fmt, ...) {
       }
     }
   }
+}
+
+}  // namespace
+
+void log(Severity sev, const char* file, int line, const char* fmt, ...) {
+  char msg[2048];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_end(ap);
+  emit(sev, file, line, msg, {});
+}
+
+void log_fields(Severity sev, const char* file, int line, const std::string& msg, const Fields& fields) {
+  emit(sev, file, line, msg, fields);
 }
 
 }  // namespace mi355x::glog

@@ -80,7 +80,8 @@ def test_device_plugin_log_files_per_severity(tmp_path):
         finally:
             c.close()
         # -vmodule=device_plugin_main=2: per-RPC lines without -v
-        assert _wait(lambda: "rpc GetDevicePluginOptions resource=gpu" in (logs / "k8s-device-plugin.INFO").read_text())
+        assert _wait(lambda: "rpc rpc=GetDevicePluginOptions resource=gpu latency_ms="
+                     in (logs / "k8s-device-plugin.INFO").read_text())
     finally:
         rc, err = _term(p)
         kub.close()
@@ -116,6 +117,49 @@ def test_labeller_log_files_threshold_and_alsologtostderr(tmp_path):
     # a malformed -vmodule is refused, like glog
     p = subprocess.run([LBL, "-dry_run", "-vmodule", "nolevel"], capture_output=True, text=True, timeout=20)
     assert p.returncode == 1 and "vmodule" in p.stderr
+
+
+def test_json_log_format_in_both_binaries(tmp_path):
+    """-log_format=json: one JSON object per record with the Python CLIs' keys
+    (utils/log.py JsonFormatter) and structured fields as keys."""
+    import json
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = tmp_path / "dp"
+    kdir.mkdir()
+    kub = gp.GoServer(str(kdir / "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    p = subprocess.Popen([DP, "-kubelet_dir", str(kdir), "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                          "-exporter_socket", "", "-log_format=json", "-v", "2", "-grpc_watchdog", "0"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        assert _wait(lambda: os.path.exists(kdir / "amd.com_gpu"))
+        time.sleep(0.3)
+        c = gp.GoClientConn(str(kdir / "amd.com_gpu"))
+        try:
+            assert c.unary("/v1beta1.DevicePlugin/GetDevicePluginOptions", b"", 3.0)[0] == 0
+        finally:
+            c.close()
+        time.sleep(0.3)
+    finally:
+        rc, err = _term(p)
+        kub.close()
+    assert rc == 0
+    recs = [json.loads(line) for line in err.splitlines() if line.strip()]
+    assert recs and all(set(r) >= {"ts", "level", "src", "msg"} for r in recs)
+    assert any(r["msg"] == "Found 8 AMDGPUs" and r["level"] == "INFO" and r["src"].startswith("device_plugin_main.cpp:")
+               for r in recs)
+    rpc = [r for r in recs if r["msg"] == "rpc" and r.get("rpc") == "GetDevicePluginOptions"]
+    assert rpc and rpc[0]["resource"] == "gpu" and float(rpc[0]["latency_ms"]) >= 0
+    # the labeller: same format; a bad value is refused by both
+    q = subprocess.Popen([LBL, "-node_name", "n", "-apiserver", "http://127.0.0.1:9", "-token_file", os.devnull,
+                          "-mode", "-once", "-log_format", "json", "-sysfs_root", str(tmp_path)],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=_env())
+    time.sleep(1.0)   # the apiserver is unreachable: -once keeps retrying
+    _, lerr = _term(q)
+    lrecs = [json.loads(line) for line in lerr.splitlines() if line.strip()]
+    assert any("reconcile of node n failed" in r["msg"] and r["level"] == "ERROR" for r in lrecs)
+    for exe in (DP, LBL):
+        bad = subprocess.run([exe, "-log_format", "xml"], capture_output=True, text=True, timeout=20)
+        assert bad.returncode == 1 and "log_format" in bad.stderr
 
 
 # ------------------------------------------------------------------ kubeconfig
