@@ -82,6 +82,7 @@
 #include "mi355x/health_engine.h"
 #include "mi355x/kfd_topology.h"
 #include "mi355x/metrics.h"
+#include "mi355x/trace.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
 #include "../kube/json.h"
@@ -134,6 +135,7 @@ struct Flags {
   double perf_min_xcd_clock_ratio = 0.6;
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
   bool dry_run = false;  // print the node report (what kubelet would be told) and exit
+  std::string trace_file;  // Chrome-trace spans, written at shutdown
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
   double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
   std::string device_list_strategy = "device-specs";
@@ -143,7 +145,7 @@ struct Flags {
 };
 
 // Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
-const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view", "trace_file"};
+const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -178,7 +180,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"exporter_socket", &f->exporter_socket}, {"liveness_mode", &f->liveness_mode},
       {"liveness_probe", &f->liveness_probe}, {"config", &f->config}, {"allocator_search", &f->allocator_search},
       {"device_list_strategy", &f->device_list_strategy}, {"cdi_spec_dir", &f->cdi_spec_dir},
-      {"perf_action", &f->perf_action}};
+      {"perf_action", &f->perf_action}, {"trace_file", &f->trace_file}};
   if (const char* c = std::getenv("CONFIG_FILE_PATH")) f->config = c;
   static std::string ignored;
   strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
@@ -206,7 +208,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
           "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
           "[-perf_min_mfma_tflops X] [-perf_min_xcd_clock_ratio X]]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
-          "[-dry_run] [-log_format glog|json] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
+          "[-dry_run] [-trace_file PATH] [-log_format glog|json] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
           "[-log_backtrace_at FILE:N]\n",
           argv[0]);
       std::exit(0);
@@ -792,6 +794,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   MI_LOG(kInfo, "AMD GPU device plugin for Kubernetes (MI355X-native, native daemon)");
+  trace::global().configure(f.trace_file);
   if (::pipe2(g_sig_pipe, O_CLOEXEC | O_NONBLOCK) != 0) return 1;
   struct sigaction sa {};
   sa.sa_handler = on_signal;
@@ -1344,6 +1347,17 @@ int main(int argc, char** argv) {
                 "ListAndWatch streams open on the native server");
         }
         for (const auto& ev : evs) {
+          if (trace::global().enabled()) {
+            std::string ids;
+            for (const auto& id : ev.ids) ids += (ids.empty() ? "" : ",") + id;
+            trace::global().complete(ev.rpc, "rpc", ev.t0_ns, ev.dur_ns,
+                                     {{"resource", resources[i].name}, {"native", ev.native ? "True" : "False"},
+                                      {"ids", ids}});
+            if (ev.alloc_t0_ns)
+              trace::global().complete("allocator.allocate", "alloc", ev.alloc_t0_ns,
+                                       static_cast<uint64_t>(ev.alloc_us * 1e3),
+                                       {{"candidates", std::to_string(ev.candidates)}, {"native", "True"}});
+          }
           m.observe_ms("mi355x_dp_rpc_seconds", ev.dur_ns / 1e6, {{"resource", resources[i].name}, {"rpc", ev.rpc}},
                        "device plugin RPC latency");
           if (ev.rpc == "ListAndWatch") m.inc("mi355x_dp_listandwatch_streams_total", res_l);
@@ -1421,8 +1435,12 @@ int main(int argc, char** argv) {
         for (auto& r : resources) {
           const bool changed = apply_health(r, c.health);
           any_changed = any_changed || changed;
-          if ((changed || f.send_every_pulse) && r.server)
+          if ((changed || f.send_every_pulse) && r.server) {
             r.server->broadcast(rpc::DevicePluginService::path("ListAndWatch"), r.list);
+            trace::global().instant("ListAndWatch.send", "rpc",
+                                    {{"resource", r.name}, {"health_version", std::to_string(engine ? engine->version() : 0)},
+                                     {"streams", std::to_string(r.server->stats().streams_open)}});
+          }
         }
         if (any_changed) metrics::global().inc("mi355x_dp_health_changes_total");
         // xGMI link state changed: every allocator re-weighted on the degraded pairs
@@ -1512,5 +1530,7 @@ int main(int argc, char** argv) {
   workers.join_all();  // every wait ends at the stop pipe
   if (engine) engine->close();
   for (auto& r : resources) stop_server(r);
+  if (const std::string te = trace::global().flush(); !te.empty())
+    MI_LOG(kError, "cannot write the trace file: %s", te.c_str());
   return exit_code;
 }

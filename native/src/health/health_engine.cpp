@@ -22,6 +22,7 @@
 #include "../kube/json.h"
 #include "mi355x/glog.h"
 #include "mi355x/metrics.h"
+#include "mi355x/trace.h"
 #include "mi355x/grpc_server.h"
 #include "mi355x/smi_query.h"
 #include "mi355x/sysfs.h"
@@ -370,6 +371,11 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
     }
     for (auto& j : jobs) {
       const double ms = (mono_s() - j.t0) * 1e3;
+      if (trace::global().enabled()) {
+        const uint64_t dur = static_cast<uint64_t>(ms * 1e6);
+        trace::global().complete("liveness.probe", "health", trace::now_ns() - dur, dur,
+                                 {{"ordinal", std::to_string(j.ordinal)}, {"kind", kind}});
+      }
       if (!j.c.eof) {  // deadline (or shutdown): the dispatch did not complete
         kill_child(&j.c);
         ProbeOutcome o;
@@ -417,6 +423,7 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
 
 std::map<int, ProbeOutcome> LivenessProber::probe_server(const std::vector<int>& uniq, const std::string& kind,
                                                          std::string* err) {
+  trace::Span span("liveness.request", "health", {{"ordinals", std::to_string(uniq.size())}, {"kind", kind}});
   const double t0 = mono_s();
   std::optional<std::vector<int>> visible = visible_;
   if (visible) {
@@ -870,6 +877,7 @@ std::map<std::string, ProbeOutcome> Engine::verify_identity(const std::map<std::
 }
 
 bool Engine::sweep() {
+  trace::Span span("health.sweep", "health", {{"devices", std::to_string(devices_.size())}});
   const double t0 = mono_s();
   std::map<std::string, std::vector<std::string>> reasons;
   for (const auto& d : devices_) reasons[d.id];
@@ -1317,6 +1325,7 @@ std::vector<std::string> Engine::perf_problems(const ProbeOutcome& o) const {
 }
 
 void Engine::perf_check(const std::map<std::string, int>& ords) {
+  trace::Span span("health.perf_check", "health", {{"devices", std::to_string(ords.size())}});
   std::vector<int> uniq;
   for (const auto& [id, o] : ords) uniq.push_back(o);
   const auto by_ord = prober_->probe(uniq, {}, "perf");

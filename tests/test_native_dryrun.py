@@ -84,3 +84,43 @@ def test_report_with_health_engine_sections(tmp_path):
     assert ok["hbm_read_gbps"] == 6000 and len(ok["xcd_clock_mhz"]) == 8
     assert doc["xgmi"] == {"readings": 1, "error": "", "degraded_pairs": [], "links_down": {}}
     assert all(d["health"] == "Healthy" for d in doc["resources"]["amd.com/gpu"]["devices"])
+
+
+def test_trace_file_spans(tmp_path):
+    """-trace_file: Chrome-trace spans of the admission path (RPC -> allocator)
+    and the health path (sweep -> probe request), written at shutdown."""
+    import asyncio
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+    from test_native_health import _stop
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text("{}")
+    kdir, trace = str(tmp_path / "dp"), tmp_path / "trace.json"
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        p = subprocess.Popen([EXE, "-kubelet_dir", kdir, "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                              "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_probe", STUB,
+                              "-trace_file", str(trace)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                             text=True, env=dict(os.environ, MI355X_STUB_PROBE_CONTROL=str(ctl)))
+        try:
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            await k.admit("amd.com/gpu", 3)
+            await asyncio.sleep(1.2)
+        finally:
+            rc, err = await asyncio.to_thread(_stop, p)
+            await k.stop()
+        assert rc == 0, err[-2000:]
+
+    asyncio.run(asyncio.wait_for(go(), 60))
+    doc = json.loads(trace.read_text())
+    ev = doc["traceEvents"]
+    names = {e["name"] for e in ev}
+    assert {"GetPreferredAllocation", "Allocate", "allocator.allocate", "health.sweep", "liveness.request"} <= names
+    alloc = [e for e in ev if e["name"] == "Allocate"][0]
+    assert alloc["ph"] == "X" and alloc["cat"] == "rpc" and alloc["args"]["resource"] == "gpu"
+    assert len(alloc["args"]["ids"].split(",")) == 3 and alloc["dur"] >= 0
+    sweep = [e for e in ev if e["name"] == "health.sweep"][0]
+    req = [e for e in ev if e["name"] == "liveness.request"][0]
+    assert sweep["ts"] <= req["ts"] and req["ts"] + req["dur"] <= sweep["ts"] + sweep["dur"] + 1   # nested
