@@ -392,7 +392,7 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
 
 
 def _foreign_queue_pids(gpu_id, exclude=()):
-    """PIDs (kfd proc entries) other than `exclude` with a user queue on kfd gpu_id."""
+    """kfd proc entries (host PIDs) other than `exclude` with a user queue on kfd gpu_id."""
     root = "/sys/class/kfd/kfd/proc"
     out = set()
     for pid in os.listdir(root) if os.path.isdir(root) else []:
@@ -432,6 +432,10 @@ def test_native_daemon_chip_sweep_and_throughput_check(inv, ordinals, tmp_path):
             return {k: float(v) for k, v in (ln.rsplit(" ", 1) for ln in r.read().decode().splitlines()
                                              if ln and not ln.startswith("#"))}
 
+    # processes that already hold queues on this GPU (kfd names them by host PID; e.g. this pytest
+    # process after the in-process HIP tests): then the daemon must leave the GPU alone
+    busy = bool(_foreign_queue_pids(gpu_id))
+
     async def go():
         k = FakeKubelet(kdir)
         await k.start()
@@ -442,14 +446,10 @@ def test_native_daemon_chip_sweep_and_throughput_check(inv, ordinals, tmp_path):
         try:
             st = await k.wait_for_resource("amd.com/gpu", 1, timeout=60)
             m = {}
-            busy = False
             for _ in range(120):
                 m = await asyncio.to_thread(metrics)
                 if m.get("mi355x_dp_chip_sweeps_total", 0) >= 2 and m.get("mi355x_dp_perf_checks_total", 0) >= 1:
                     break
-                # another process with queues on this GPU (e.g. this pytest process after the in-process
-                # HIP tests): the daemon must leave the GPU alone
-                busy = bool(_foreign_queue_pids(gpu_id, exclude={proc.pid} | _probe_children(proc.pid)))
                 if busy and m.get("mi355x_dp_liveness_probe_ms{device=\"%s\"}" % dev_id, 0) > 0:
                     break
                 await asyncio.sleep(0.5)
