@@ -38,6 +38,7 @@ namespace mi355x::rpc {
 
 // Allocate fast path: every ContainerAllocateResponse is
 //   container_prefix + per_device[id] for each requested id (request order)
+//   + (at least one id) container_extra(ids)   (per-request fields, e.g. a topology-view mount)
 //   + (at least one id) container_nonempty
 //   + (annotation_key set) annotations{annotation_key: join(annotation_names[id], ",")}
 //   + (env_key set, at least one id) envs{env_key: join(env_values[id], ",")}
@@ -47,6 +48,7 @@ struct AllocateTemplate {
   std::string resource;  // for error messages
   std::string container_prefix;
   std::unordered_map<std::string, std::string> per_device;
+  std::function<std::string(const std::vector<std::string>& ids)> container_extra;  // optional; runs on the server thread
   std::string container_nonempty;  // e.g. the node-view mounts of a container that got devices
   std::string annotation_key;
   std::unordered_map<std::string, std::string> annotation_names;

@@ -83,6 +83,7 @@
 #include "mi355x/kfd_topology.h"
 #include "mi355x/metrics.h"
 #include "mi355x/trace.h"
+#include "mi355x/views.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
 #include "../kube/json.h"
@@ -136,6 +137,8 @@ struct Flags {
   std::string config;  // YAML config file (gpu.device_count), default $CONFIG_FILE_PATH
   bool dry_run = false;  // print the node report (what kubelet would be told) and exit
   std::string trace_file;  // Chrome-trace spans, written at shutdown
+  bool node_view = false;      // experimental: NUMA-node sysfs view without per-CPU cache descriptors
+  bool topology_view = false;  // experimental: per-allocation filtered kfd topology
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
   double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
   std::string device_list_strategy = "device-specs";
@@ -145,7 +148,7 @@ struct Flags {
 };
 
 // Flags only the Python CLI implements (k8s-device-plugin): refused with a pointer to it.
-const std::set<std::string> kPythonOnly = {"grpc_server", "topology_view", "node_view"};
+const std::set<std::string> kPythonOnly = {"grpc_server"};
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
@@ -159,7 +162,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"send_every_pulse", &f->send_every_pulse}, {"allocator_extended_search", &f->allocator_extended_search},
       {"liveness", &f->liveness}, {"liveness_keep_queues", &f->liveness_keep_queues},
       {"liveness_corroborate", &f->liveness_corroborate}, {"smi_ecc", &f->smi_ecc}, {"smi_events", &f->smi_events},
-      {"smi_xgmi", &f->smi_xgmi}, {"dry_run", &f->dry_run}};
+      {"smi_xgmi", &f->smi_xgmi}, {"dry_run", &f->dry_run}, {"node_view", &f->node_view},
+      {"topology_view", &f->topology_view}};
   std::map<std::string, int*> ints = {
       {"pulse", &f->pulse}, {"liveness_iters", &f->liveness_iters},
       {"liveness_fail_threshold", &f->liveness_fail_threshold},
@@ -208,7 +212,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
           "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
           "[-perf_min_mfma_tflops X] [-perf_min_xcd_clock_ratio X]]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
-          "[-dry_run] [-trace_file PATH] [-log_format glog|json] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
+          "[-dry_run] [-trace_file PATH] [-node_view] [-topology_view] [-log_format glog|json] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
           "[-log_backtrace_at FILE:N]\n",
           argv[0]);
       std::exit(0);
@@ -375,8 +379,24 @@ std::shared_ptr<const HiveAllocator> build_allocator(const std::vector<GpuDevice
   return alloc;
 }
 
+// the opt-in container start-up views (mi355x/views.h)
+struct ViewCtx {
+  std::shared_ptr<views::NodeView> node;
+  std::shared_ptr<views::TopologyViews> topo;
+};
+
+// Mount{container_path=1, host_path=2, read_only=3}, as ContainerAllocateResponse.mounts (2)
+std::string mount_field(const std::string& host, const std::string& ctr) {
+  std::string m, out;
+  pb::put_bytes(&m, 1, ctr);
+  pb::put_bytes(&m, 2, host);
+  pb::put_bool(&m, 3, true);
+  pb::put_bytes(&out, 2, m);
+  return out;
+}
+
 void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved,
-             const std::string& search, const cdi::Strategies& lists) {
+             const std::string& search, const cdi::Strategies& lists, const ViewCtx& vc) {
   // allocator (BestEffortPolicy.init); on failure kubelet allocates by itself
   bool alloc_ok = true;
   for (const auto& d : r.devices)
@@ -417,6 +437,27 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
     if (lists.annotations) t.annotation_names[d.id] = cdi::qualified_name(r.name, d.id);
     t.per_device[d.id] = car;
   }
+  if (vc.topo) {  // one filtered topology per distinct allocated node set, built on first use
+    std::map<std::string, int> node_of;
+    for (const auto& d : r.devices) node_of[d.id] = d.node_id;
+    t.container_extra = [views = vc.topo, node_of](const std::vector<std::string>& ids) -> std::string {
+      std::vector<int> nodes;
+      for (const auto& id : ids) {
+        auto it = node_of.find(id);
+        if (it == node_of.end() || it->second < 0) return "";
+        nodes.push_back(it->second);
+      }
+      std::string err;
+      const std::string path = views->get(nodes, &err);
+      if (path.empty()) {  // never fail an admission over an optimisation
+        MI_LOG(kWarning, "topology view unavailable: %s", err.c_str());
+        return "";
+      }
+      return mount_field(path, views::kKfdTopologyContainerPath);
+    };
+  }
+  if (vc.node)
+    for (const auto& [host, ctr] : vc.node->mounts()) t.container_nonempty += mount_field(host, ctr);
   r.service = std::make_unique<rpc::DevicePluginService>();
   r.service->set_fallback([name = r.name](const std::string& method, const std::string&) {
     // everything the native daemon serves has prepared state; a method without it is not implemented
@@ -812,6 +853,19 @@ int main(int argc, char** argv) {
   KfdTopology topo;
   std::vector<GpuDevice> container_devices;  // every advertised container-mode device (health engine)
   std::vector<std::string> discovery_warnings;
+  ViewCtx view_ctx;
+  if (f.topology_view)
+    view_ctx.topo = std::make_shared<views::TopologyViews>(path_join(f.kubelet_dir, "mi355x-topology"),
+                                                           path_join(f.sysfs_root, "class/kfd/kfd/topology"));
+  if (f.node_view) {  // built at start-up, not inside the first Allocate
+    auto nv = std::make_shared<views::NodeView>(path_join(f.kubelet_dir, "mi355x-node"), f.sysfs_root);
+    if (const std::string e = nv->build(); !e.empty()) {
+      MI_LOG(kWarning, "node view unavailable: %s", e.c_str());
+    } else {
+      MI_LOG(kInfo, "node view: %d links, %d per-CPU cache directories left out", nv->links, nv->hidden);
+      view_ctx.node = nv;
+    }
+  }
   bool impl_ok = true;  // a driver initialised (auto mode: container -> VF -> PF)
   Driver driver = Driver::Container;
   // one driver's resources; "" on success (an empty list = no devices), else the init error
@@ -854,7 +908,7 @@ int main(int argc, char** argv) {
           container_devices.push_back(d);
         }
       r.socket = path_join(f.kubelet_dir, std::string(kResourceNamespace) + "_" + name);
-      prepare(r, topo, unresolved, f.allocator_search, f.lists);
+      prepare(r, topo, unresolved, f.allocator_search, f.lists, view_ctx);
       out->push_back(std::move(r));
     }
     return "";

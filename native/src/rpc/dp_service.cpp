@@ -248,6 +248,7 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
         std::string car = t->container_prefix;
         std::string ann, env;
         bool any = false;
+        std::vector<std::string> ids;
         const bool scanned = pb::scan(
             p, n,
             [&](int f, const char* q, size_t m) {
@@ -272,11 +273,13 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
                 }
               }
               any = true;
+              if (t->container_extra) ids.push_back(id);
               ev->ids.push_back(std::move(id));
               return true;
             },
             nullptr);
         if (!scanned) return false;
+        if (any && t->container_extra) car += t->container_extra(ids);
         if (any) car += t->container_nonempty;
         if (any && !t->annotation_key.empty()) {
           std::string entry;
