@@ -449,7 +449,7 @@ def test_daemon_watchdog_exits_when_kubelet_never_lists(tmp_path):
 
 
 def test_daemon_refuses_python_only_flags_and_bad_liveness(tmp_path):
-    for args, want in ((["-node_view"], "Python entrypoint"),
+    for args, want in ((["-grpc_server", "aio"], "Python entrypoint"),
                        (["-liveness"], "-pulse > 0"),
                        (["-liveness_mode", "bogus"], "liveness_mode"),
                        (["-vmodule", "nolevel"], "vmodule")):
