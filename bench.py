@@ -27,9 +27,11 @@ GPUs advertised at 1/2/4/8 MI355X"). One timed step is one pod admission:
      block ~100-150 ms in open("/dev/kfd") (profiles/README.md §3c) — reported
      as latency_p50_ms_back_to_back.
 
-The plugin is the real one (real /sys discovery, real C++ allocator, real
-gRPC servicer); only kubelet and the CRI runtime are stand-ins (see
-rocm_k8s_device_plugin_amd/testing/fake_kubelet.py, container_runtime.py).
+The plugin is the real one: by default the native daemon mi355x-device-plugin
+(the primary entrypoint: real /sys discovery, C++ allocator and gRPC server;
+--plugin python runs the Python CLI's plugin instead); only kubelet and the
+CRI runtime are stand-ins (see rocm_k8s_device_plugin_amd/testing/
+fake_kubelet.py, container_runtime.py).
 
   python bench.py --gpus N --steps K --warmup W
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
@@ -112,8 +114,12 @@ def make_parser():
                     help="with M = N and more accessible devices than N: extra untimed admissions of N out of "
                          "every accessible device from a fragmented availability (a second plugin instance), "
                          "reported in extra.fragmented_n_of_m (BASELINE config: full-node hive-aware allocation)")
+    ap.add_argument("--plugin", default="native", choices=["native", "python"],
+                    help="the device plugin under test: native = the mi355x-device-plugin daemon (the primary "
+                         "entrypoint, what ./k8s-device-plugin runs); python = the Python CLI's plugin in this "
+                         "process (--grpc-server picks its transport; used automatically with --health-pulse)")
     ap.add_argument("--grpc-server", default="native", choices=["native", "aio"],
-                    help="the plugin's kubelet-facing gRPC server (-grpc_server)")
+                    help="with --plugin python: the plugin's kubelet-facing gRPC server (-grpc_server)")
     ap.add_argument("--kubelet-client", default="", choices=["", "native", "native-thread", "aio"],
                     help="the fake kubelet's admission RPC client: native (a native HTTP/2 client, like kubelet's "
                          "grpc-go) or aio (grpc.aio in the bench's event loop); default native with the native server")
@@ -162,9 +168,130 @@ def fragment(ids, n, hold=-1):
     return (list(ids[1::2]) + list(ids[0::2]))[:h]
 
 
+class _AllocStats:
+    last_short_circuit = False
+    last_candidates = -1
+
+
+class _DaemonAllocator:
+    """The daemon's allocator as the bench's microbenchmarks see it: the same
+    C++ HiveAllocator on the same devices (BestEffortPolicy, -allocator_search
+    auto), plus the last GetPreferredAllocation outcome the daemon logged."""
+
+    def __init__(self, devs, topology, stats):
+        from rocm_k8s_device_plugin_amd.allocator import BestEffortPolicy
+        self._pol = BestEffortPolicy(extended_search="auto")
+        self._pol.init(list(devs), topology)
+        self.stats = stats
+
+    @property
+    def native(self):
+        return self._pol.native
+
+    def reference_allocate(self, *a):
+        return self._pol.reference_allocate(*a)
+
+
+class NativePluginUnderTest:
+    """Rank 0: the native daemon mi355x-device-plugin (the primary entrypoint)
+    advertising `devs` (-device_ids) behind a fake kubelet on its own UDS dir.
+    Its per-RPC records (-log_format json -v 2: server-side latency, the
+    allocator's candidates / short-circuit) are read from its stderr."""
+
+    def __init__(self, loop, tmp, name, sysfs, devroot, devs, full, ords, kubelet_client="native", extra=()):
+        import subprocess
+        import threading
+        from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+        from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+        self.loop = loop
+        self.devs = tuple(devs)
+        pdir = os.path.join(tmp, name)
+        self.kubelet = FakeKubelet(pdir, rpc_client=kubelet_client)
+        loop.run_until_complete(self.kubelet.start())
+        self.stats = _AllocStats()
+        self.recent = {}
+        self._cv = threading.Condition()
+        self._allocates_seen = 0
+        self._allocates_made = 0
+        exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+        self.proc = subprocess.Popen(
+            [exe, "-kubelet_dir", pdir, "-sysfs_root", sysfs, "-dev_root", devroot, "-exporter_socket", "",
+             "-device_ids", ",".join(dv.id for dv in self.devs), "-log_format", "json", "-v", "2", *extra],
+            stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        self._reader = threading.Thread(target=self._read, daemon=True)
+        self._reader.start()
+        admit = self.kubelet.admit
+
+        async def counted_admit(*a, **kw):
+            r = await admit(*a, **kw)
+            with self._cv:
+                self._allocates_made += 1
+            return r
+        self.kubelet.admit = counted_admit
+        loop.run_until_complete(self.kubelet.wait_for_resource("amd.com/gpu", len(self.devs), timeout=30))
+        self._alloc = _DaemonAllocator(self.devs, full.topology, self.stats)
+        self.minor_to_ord = {dv.render_minor: ords[dv.id] for dv in self.devs}
+        self.minor_to_paths = {dv.render_minor: dv.dev_paths() for dv in self.devs}
+        self.held = []
+
+    def _read(self):
+        for line in self.proc.stderr:
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            if r.get("msg") != "rpc":
+                continue
+            with self._cv:
+                self.recent.setdefault(r["rpc"], []).append(float(r["latency_ms"]))
+                if r["rpc"] == "GetPreferredAllocation" and "candidates" in r:
+                    self.stats.last_candidates = int(r["candidates"])
+                    self.stats.last_short_circuit = r.get("short_circuit") == "True"
+                if r["rpc"] == "Allocate":
+                    self._allocates_seen += 1
+                    self._cv.notify_all()
+
+    def sync(self, timeout=2.0):
+        """Wait until the daemon has logged every Allocate the kubelet made."""
+        with self._cv:
+            self._cv.wait_for(lambda: self._allocates_seen >= self._allocates_made, timeout)
+
+    def hold(self, ids):
+        self.kubelet.resources["amd.com/gpu"].allocated.update(ids)
+        self.held = list(ids)
+
+    @property
+    def allocator(self):
+        self.sync()
+        return self._alloc
+
+    def server_ms(self, reset=False):
+        self.sync()
+        with self._cv:
+            out = {rpc: list(v) for rpc, v in self.recent.items()}
+            if reset:
+                self.recent.clear()
+        return out
+
+    def available(self):
+        return self.kubelet.healthy_free("amd.com/gpu")
+
+    def stop(self):
+        import signal
+        self.loop.run_until_complete(self.kubelet.stop())
+        if self.proc.poll() is None:
+            self.proc.send_signal(signal.SIGTERM)
+        try:
+            self.proc.wait(timeout=20)
+        except Exception:  # noqa: BLE001
+            self.proc.kill()
+            self.proc.wait()
+        self._reader.join(timeout=5)
+
+
 class PluginUnderTest:
-    """Rank 0: the real plugin advertising `devs` (real discovery data, real
-    allocator and gRPC servicer) behind a fake kubelet on its own UDS dir."""
+    """Rank 0: the Python CLI's plugin advertising `devs` (real discovery data,
+    real allocator and gRPC servicer) behind a fake kubelet on its own UDS dir."""
 
     def __init__(self, loop, tmp, name, sysfs, devs, full, ords, hcfg, pulse_s, grpc_server="native",
                  kubelet_client="native"):
@@ -395,12 +522,24 @@ def main():
         hcfg = (HealthConfig(exporter_socket=None, liveness=True, smi_ecc=True, smi_events=True, smi_xgmi=True)
                 if hp > 0 else HealthConfig(exporter_socket=None))
         loop = asyncio.new_event_loop()
-        kclient = args.kubelet_client or ("native" if args.grpc_server == "native" else "aio")
-        if kclient == "native" and args.grpc_server != "native":
+        # the health DaemonSet variant (--health-pulse, sub-second pulses) runs on the Python plugin
+        plugin_kind = "native-daemon" if args.plugin == "native" and hp == 0 else "python"
+
+        def make_plugin(name, devs, extra=()):
+            if plugin_kind == "native-daemon":
+                return NativePluginUnderTest(loop, tmp, name, sysfs, devroot, devs, full, ords,
+                                             kubelet_client=kclient, extra=extra)
+            return PluginUnderTest(loop, tmp, name, sysfs, devs, full, ords,
+                                   hcfg if name == "device-plugins" else HealthConfig(exporter_socket=None),
+                                   hp if name == "device-plugins" else 0.0, grpc_server=args.grpc_server,
+                                   kubelet_client=kclient)
+        grpc_native = plugin_kind == "native-daemon" or args.grpc_server == "native"
+        kclient = args.kubelet_client or ("native" if grpc_native else "aio")
+        if kclient == "native" and not grpc_native:
             kclient = "native-thread"   # a blocking call on the loop that serves grpc.aio would deadlock
-        plug = PluginUnderTest(loop, tmp, "device-plugins", sysfs, adv, full, ords, hcfg, hp,
-                               grpc_server=args.grpc_server, kubelet_client=kclient)
-        impl, inv = plug.impl, plug.inv
+        plug = make_plugin("device-plugins", adv)
+        impl = getattr(plug, "impl", None)
+        inv = getattr(plug, "inv", None) or full
         if m_adv > n:
             plug.hold(fragment([dv.id for dv in adv], n, args.hold))
         gpu_info = {"ids": [dv.id for dv in adv], "gfx_target_version": sorted({dv.gfx_target_version for dv in adv}),
@@ -525,17 +664,24 @@ def main():
         for _ in range(args.mode_compare):
             one_step(False, sink=other_mode_lat, mode=other_mode)
     if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
-        # the plugin returns -node_view mounts from now on (alias = host path: the
-        # fake runtime applies mounts by redirection and cannot add the alias mount)
+        # the plugin returns -node_view mounts (alias = host path: the fake runtime
+        # applies mounts by redirection and cannot add the alias mount)
+        nvplug = None
         if d.rank == 0:
-            from rocm_k8s_device_plugin_amd.node_view import NodeView
-            impl.node_view = NodeView(os.path.join(tmp, "node-view"), sysfs,
-                                      alias=os.path.join(sysfs, "devices/system/node"))
-            impl.node_view.path()  # built at plugin start-up in a real deployment
+            node_dir = os.path.join(sysfs, "devices/system/node")
+            if plugin_kind == "native-daemon":
+                nvplug = make_plugin("device-plugins-node-view", adv, ["-node_view", "-node_view_alias", node_dir])
+            else:
+                from rocm_k8s_device_plugin_amd.node_view import NodeView
+                impl.node_view = NodeView(os.path.join(tmp, "node-view"), sysfs, alias=node_dir)
+                impl.node_view.path()  # built at plugin start-up in a real deployment
         for _ in range(args.node_view_compare):
-            one_step(False, sink=nv_lat, init_sink=nv_init)
+            one_step(False, sink=nv_lat, init_sink=nv_init, pl=nvplug)
         if d.rank == 0:
-            impl.node_view = None
+            if nvplug is not None:
+                nvplug.stop()
+            else:
+                impl.node_view = None
     vis_lat = []
     other_view = "visible-devices" if args.dev_view == "specs" else "specs"
     if not args.fixture and args.container_runtime == "hsa":
@@ -556,9 +702,7 @@ def main():
     if do_frag:
         fplug = None
         if d.rank == 0:
-            fplug = PluginUnderTest(loop, tmp, "device-plugins-all", sysfs, usable, full, ords,
-                                    HealthConfig(exporter_socket=None), 0.0, grpc_server=args.grpc_server,
-                                    kubelet_client=kclient)
+            fplug = make_plugin("device-plugins-all", usable)
             fplug.hold(fragment([dv.id for dv in usable], n, args.hold))
         for _ in range(args.fragmented_compare):
             one_step(False, sink=frag_lat, pl=fplug, alloc_sink=frag_alloc)
@@ -593,7 +737,7 @@ def main():
     if d.rank == 0:
         # allocator microbenchmark on the same request (ours vs the reference's ordered BFS)
         pol = plug.allocator
-        avail = [dv.id for dv in impl.devices("gpu")]
+        avail = [dv.id for dv in adv]
         t = time.perf_counter()
         for _ in range(200):  # both sides called straight into C++ (no trace/stats wrapper)
             pol.native.allocate(avail, [], n)
@@ -618,9 +762,12 @@ def main():
                              "reference_candidates": refk["candidates"], "ours_candidates": mine["candidates"],
                              "same_set": sorted(mine["ids"]) == sorted(refk["ids"])}
         extra = {"plugin_rpc_p50_ms": round(pct(rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rpc_ms, .99), 4),
-                 "grpc_server": args.grpc_server, "kubelet_client": kclient,
+                 "plugin": plugin_kind,
+                 "grpc_server": "native" if plugin_kind == "native-daemon" else args.grpc_server,
+                 "kubelet_client": kclient,
                  # breakdown of plugin_rpc (kubelet's GetPreferredAllocation + Allocate round trips): the
-                 # plugin's own time per RPC, measured inside the native server (empty with -grpc_server aio)
+                 # plugin's own time per RPC, measured inside the native server (empty with -grpc_server aio;
+                 # the daemon's from its per-RPC log records)
                  "plugin_server_p50_us": {rpc: round(pct(v, .5) * 1e3, 1) for rpc, v in sorted(server_ms.items())
                                           if rpc in ("GetPreferredAllocation", "Allocate")},
                  "allocate_rpc_p50_ms": round(pct(alloc_rpc_ms, .5), 4),
@@ -713,7 +860,7 @@ def main():
                                         else "1 container process per GPU")),
                        "between_admissions": ("previous pod's kfd teardown complete" if args.settle == "kfd"
                                               else "back-to-back"),
-                       "launcher": d.launcher},
+                       "launcher": d.launcher, "plugin": plugin_kind},
             "extra": extra,
         }
         line = json.dumps(out)

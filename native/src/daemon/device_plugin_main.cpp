@@ -139,6 +139,8 @@ struct Flags {
   std::string trace_file;  // Chrome-trace spans, written at shutdown
   bool node_view = false;      // experimental: NUMA-node sysfs view without per-CPU cache descriptors
   bool topology_view = false;  // experimental: per-allocation filtered kfd topology
+  std::string node_view_alias = views::kNodeAlias;  // where the real node directory is mounted in the container
+  std::string device_ids;  // advertise only these device IDs (comma-separated; default: every discovered one)
   int metrics_port = 0;  // Prometheus /metrics (0 = off)
   double topology_watch_s = 5.0;  // re-discovery check period (partition switches); 0 = off
   std::string device_list_strategy = "device-specs";
@@ -184,7 +186,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       {"exporter_socket", &f->exporter_socket}, {"liveness_mode", &f->liveness_mode},
       {"liveness_probe", &f->liveness_probe}, {"config", &f->config}, {"allocator_search", &f->allocator_search},
       {"device_list_strategy", &f->device_list_strategy}, {"cdi_spec_dir", &f->cdi_spec_dir},
-      {"perf_action", &f->perf_action}, {"trace_file", &f->trace_file}};
+      {"perf_action", &f->perf_action}, {"trace_file", &f->trace_file}, {"node_view_alias", &f->node_view_alias},
+      {"device_ids", &f->device_ids}};
   if (const char* c = std::getenv("CONFIG_FILE_PATH")) f->config = c;
   static std::string ignored;
   strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
@@ -212,7 +215,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
           "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
           "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
           "[-perf_min_mfma_tflops X] [-perf_min_xcd_clock_ratio X]]] [-smi_ecc] [-smi_events] [-smi_xgmi] "
-          "[-dry_run] [-trace_file PATH] [-node_view] [-topology_view] [-log_format glog|json] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
+          "[-dry_run] [-trace_file PATH] [-node_view [-node_view_alias PATH]] [-topology_view] [-device_ids ID,...] [-log_format glog|json] [-v N] [-logtostderr] [-alsologtostderr] [-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] "
           "[-log_backtrace_at FILE:N]\n",
           argv[0]);
       std::exit(0);
@@ -858,7 +861,8 @@ int main(int argc, char** argv) {
     view_ctx.topo = std::make_shared<views::TopologyViews>(path_join(f.kubelet_dir, "mi355x-topology"),
                                                            path_join(f.sysfs_root, "class/kfd/kfd/topology"));
   if (f.node_view) {  // built at start-up, not inside the first Allocate
-    auto nv = std::make_shared<views::NodeView>(path_join(f.kubelet_dir, "mi355x-node"), f.sysfs_root);
+    auto nv = std::make_shared<views::NodeView>(path_join(f.kubelet_dir, "mi355x-node"), f.sysfs_root,
+                                                f.node_view_alias);
     if (const std::string e = nv->build(); !e.empty()) {
       MI_LOG(kWarning, "node view unavailable: %s", e.c_str());
     } else {
@@ -874,6 +878,20 @@ int main(int argc, char** argv) {
     topo = KfdTopology::load_sysfs(f.sysfs_root);
     DiscoveryResult res = discover_gpus(f.sysfs_root, topo);
     res.devices = limit_physical(res.devices, dev_limit);
+    if (!f.device_ids.empty()) {  // -device_ids: a node shared between plugin instances, or GPUs held back
+      std::set<std::string> want;
+      for (size_t a = 0; a <= f.device_ids.size();) {
+        size_t b = f.device_ids.find(',', a);
+        if (b == std::string::npos) b = f.device_ids.size();
+        if (b > a) want.insert(f.device_ids.substr(a, b - a));
+        a = b + 1;
+      }
+      std::vector<GpuDevice> kept;
+      for (const auto& d : res.devices)
+        if (want.erase(d.id)) kept.push_back(d);
+      for (const auto& id : want) MI_LOG(kWarning, "-device_ids: %s is not a discovered device", id.c_str());
+      res.devices = std::move(kept);
+    }
     for (const auto& w : res.warnings) MI_LOG(kWarning, "%s", w.c_str());
     discovery_warnings = res.warnings;
     MI_LOG(kInfo, "Found %zu AMDGPUs", res.devices.size());
@@ -1426,8 +1444,12 @@ int main(int argc, char** argv) {
           if (glog::vlog_is_on(2, __FILE__)) {
             char ms[32];
             std::snprintf(ms, sizeof(ms), "%.3f", ev.dur_ns / 1e6);
-            MI_LOG_FIELDS(kInfo, "rpc", ({{"rpc", ev.rpc}, {"resource", resources[i].name}, {"latency_ms", ms},
-                                          {"native", "True"}}));
+            glog::Fields fl = {{"rpc", ev.rpc}, {"resource", resources[i].name}, {"latency_ms", ms}, {"native", "True"}};
+            if (ev.rpc == "GetPreferredAllocation" && ev.candidates >= 0) {
+              fl.emplace_back("candidates", std::to_string(ev.candidates));
+              fl.emplace_back("short_circuit", ev.short_circuit ? "True" : "False");
+            }
+            MI_LOG_FIELDS(kInfo, "rpc", (fl));
           }
         }
       }

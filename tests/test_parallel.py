@@ -105,6 +105,9 @@ def test_bench_fixture_reports_fabric_and_collectives():
     # render nodes, and the per-GPU comparison split them one per rank
     e = d["extra"]
     assert e["container_dev_view"] == "specs" and e["latency_p50_ms_container_mode_per-gpu"] > 0
+    # the plugin under test is the primary entrypoint, the native daemon
+    assert e["plugin"] == "native-daemon" == d["config"]["plugin"]
+    assert set(e["plugin_server_p50_us"]) == {"GetPreferredAllocation", "Allocate"}
     assert len(e["steps_ms"]) == 2
     # gloo carries the step barriers: no rank holds a GPU context or kfd fd in the timed loop
     assert e["launcher"] == "torchrun" and d["config"]["launcher"] == "torchrun"
@@ -139,3 +142,13 @@ def test_bench_n_of_m_searches_inside_the_timed_step():
     assert set(ta["phase_p50_ms"]) == {"plugin_rpc", "runtime_prep", "spawn_to_main", "gpu_runtime_init",
                                        "device_setup_and_mfma"}
     assert all(s["latency_ms"] > ta["threshold_ms"] for s in ta["slow_steps"])
+
+
+def test_bench_python_plugin_option():
+    """--plugin python: the Python CLI's plugin in the bench process serves the admissions."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    p = subprocess.run([sys.executable, "bench.py", "--fixture", "--steps", "2", "--warmup", "1", "--plugin",
+                        "python"], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["extra"]["plugin"] == "python" and d["extra"]["plugin_server_p50_us"]
