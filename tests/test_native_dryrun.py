@@ -124,3 +124,13 @@ def test_trace_file_spans(tmp_path):
     sweep = [e for e in ev if e["name"] == "health.sweep"][0]
     req = [e for e in ev if e["name"] == "liveness.request"][0]
     assert sweep["ts"] <= req["ts"] and req["ts"] + req["dur"] <= sweep["ts"] + sweep["dur"] + 1   # nested
+
+
+def test_device_ids_restricts_the_advertised_set(tmp_path):
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="cpx")
+    keep = ["amdgpu_xcp_1", "amdgpu_xcp_9", fi.bdfs[0]]
+    p = subprocess.run([EXE, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket",
+                        "", "-device_ids", ",".join(keep + ["bogus"])], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr[-2000:]
+    devs = {d["id"] for d in json.loads(p.stdout)["resources"]["amd.com/gpu"]["devices"]}
+    assert devs == set(keep) and "-device_ids: bogus is not a discovered device" in p.stderr
