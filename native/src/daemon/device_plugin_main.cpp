@@ -1335,6 +1335,7 @@ int main(int argc, char** argv) {
         r.devices.clear();
         r.health.clear();
       }
+    std::vector<size_t> to_start;  // new resources: served and registered once their CDI specs exist
     for (auto& fr : fresh) {
       auto it = std::find_if(resources.begin(), resources.end(), [&](const Resource& r) { return r.name == fr.name; });
       if (it != resources.end() && !it->gone) {
@@ -1369,10 +1370,13 @@ int main(int argc, char** argv) {
         i = resources.size() - 1;
       }
       MI_LOG(kInfo, "new resource %s (%zu devices)", resources[i].name.c_str(), resources[i].devices.size());
-      if (sock.present && start_server(resources[i])) try_register(i);
+      to_start.push_back(i);
     }
+    // before any new resource registers: kubelet may hand its CDI names to the runtime at once
     if (const std::string ce = write_cdi(old_set); !ce.empty())
       MI_LOG(kError, "CDI specs not updated after the topology change: %s", ce.c_str());
+    for (size_t i : to_start)
+      if (sock.present && start_server(resources[i])) try_register(i);
     make_engine();
     if (f.pulse > 0) next_pulse = Clock::now();  // verdicts for the new devices now
   };
