@@ -992,6 +992,7 @@ struct Call {
   int grpc_status = -1;
   std::string grpc_message;
   std::string data;
+  uint32_t recv_unacked = 0;  // stream bytes received since our last WINDOW_UPDATE for it
   bool done = false;
   bool failed = false;
   Reply fail;
@@ -1283,14 +1284,22 @@ Reply GrpcClient::unary(const std::string& path, const std::string& request, dou
           pad = p[0];
         }
         if (sid != call.sid) return true;  // a stream we gave up on
-        if (len) {
-          call.data.append(reinterpret_cast<const char*>(p + (pad ? 1 : 0)), len - (pad ? pad + 1 : 0));
-          std::string wu;
-          put_be32(&wu, static_cast<uint32_t>(len));
-          put_frame(&pending_out, kWindowUpdate, 0, call.sid, wu.data(), wu.size());
-        }
+        if (len) call.data.append(reinterpret_cast<const char*>(p + (pad ? 1 : 0)), len - (pad ? pad + 1 : 0));
         if (call.data.size() > kMaxMessage + 5) return conn_fail("response message too large");
-        if (flags & kEndStream) call.done = true;
+        if (flags & kEndStream) {
+          call.done = true;  // a closed stream needs no credit
+        } else {
+          // stream credit in batches of half the initial window (grpc-go's inFlow
+          // acks at a quarter): a unary reply of a few hundred bytes costs the
+          // server no extra wakeup
+          call.recv_unacked += static_cast<uint32_t>(len);
+          if (call.recv_unacked >= 32768) {
+            std::string wu;
+            put_be32(&wu, call.recv_unacked);
+            put_frame(&pending_out, kWindowUpdate, 0, call.sid, wu.data(), wu.size());
+            call.recv_unacked = 0;
+          }
+        }
         return true;
       }
       default:
@@ -1355,9 +1364,11 @@ Reply GrpcClient::unary(const std::string& path, const std::string& request, dou
     if (call.done) break;  // answered (or reset) before the request was complete
   }
   while (!call.done) {
-    if (!flush(&err)) return fail(-1, err, true);
     if (!process()) return fail(call.fail.status, call.fail.message, true);
     if (call.done) break;
+    // everything process() queued (WINDOW_UPDATE, SETTINGS / PING acks) goes out
+    // before we wait: the peer may be blocked on exactly that credit
+    if (!flush(&err)) return fail(-1, err, true);
     if (!read_more(&err)) return fail(-1, err, true);
   }
   if (!flush(&err)) return fail(-1, err, true);
