@@ -570,13 +570,6 @@ def main():
             pl = pl or plug
             t0 = time.monotonic_ns()
             adm = loop.run_until_complete(pl.kubelet.admit("amd.com/gpu", n))
-            st = pl.allocator.stats
-            a_rec = (adm.preferred_ms, bool(st.last_short_circuit), int(st.last_candidates),
-                     sorted(adm.device_ids), adm.preferred_used)
-            if record:
-                alloc_steps.append(a_rec)
-            if alloc_sink is not None:
-                alloc_sink.append(a_rec)
             car = adm.response.container_responses[0]
             minors = render_minors_from_specs(car)
             ordl = [pl.minor_to_ord[m] for m in minors]
@@ -614,6 +607,16 @@ def main():
             gpu_state["kfd_fds"] = max(gpu_state["kfd_fds"], st_now["kfd_fds"])
             gpu_state["render_fds"] = max(gpu_state["render_fds"], st_now["render_fds"])
         allr = d.gather(mine)
+        if d.rank == 0:
+            # the allocator's outcome for this admission, read once the pod is up (the
+            # native daemon reports it in its log: waiting for that must not delay the pod)
+            st = pl.allocator.stats
+            a_rec = (adm.preferred_ms, bool(st.last_short_circuit), int(st.last_candidates),
+                     sorted(adm.device_ids), adm.preferred_used)
+            if record:
+                alloc_steps.append(a_rec)
+            if alloc_sink is not None:
+                alloc_sink.append(a_rec)
         bad = [m[3] for m in allr if not m[0]]
         if bad:
             raise SystemExit(f"container failed to become ready: {bad[0]}")

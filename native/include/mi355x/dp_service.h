@@ -22,6 +22,7 @@
 // the RPC path.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -100,6 +101,7 @@ class DevicePluginService {
   Reply allocate(const std::string& req, RpcEvent* ev);
   Reply fallback(const char* method, const std::string& req, RpcEvent* ev);
   void record(RpcEvent ev);
+  void notify();  // eventfd, if events were recorded since the last call (I/O thread, after the writes)
 
   mutable std::mutex mu_;
   std::shared_ptr<const Fallback> fallback_;
@@ -111,6 +113,7 @@ class DevicePluginService {
 
   std::mutex ev_mu_;
   std::vector<RpcEvent> events_;
+  std::atomic<bool> notify_pending_{false};
   int evfd_ = -1;
 };
 

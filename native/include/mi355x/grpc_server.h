@@ -66,6 +66,8 @@ class GrpcServer {
   // Registration happens before start().
   void add_unary(const std::string& path, UnaryFn fn);
   void add_server_stream(const std::string& path, StreamOpenFn open, StreamCloseFn close = nullptr);
+  // called on the I/O thread after each round's responses are written (before start())
+  void set_after_io(std::function<void()> fn);
 
   // Binds the Unix socket (an existing file at `path` is replaced) and starts
   // the I/O thread. Returns "" or an error message.

@@ -164,6 +164,13 @@ void DevicePluginService::record(RpcEvent ev) {
     if (events_.size() >= kMaxEvents) events_.erase(events_.begin(), events_.begin() + kMaxEvents / 2);
     events_.push_back(std::move(ev));
   }
+  // the consumer is woken once the response is on the wire (after_io below), so
+  // its wakeup never competes with the reply the caller is waiting for
+  notify_pending_.store(true, std::memory_order_release);
+}
+
+void DevicePluginService::notify() {
+  if (!notify_pending_.exchange(false, std::memory_order_acq_rel)) return;
   const uint64_t one = 1;
   ssize_t r = ::write(evfd_, &one, sizeof(one));
   (void)r;
@@ -303,6 +310,7 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
 }
 
 void DevicePluginService::attach(GrpcServer& srv) {
+  srv.set_after_io([this] { notify(); });
   auto wrap = [this](const char* method, std::function<Reply(const std::string&, RpcEvent*)> fn) {
     return [this, method, fn](const std::string& req) {
       RpcEvent ev;

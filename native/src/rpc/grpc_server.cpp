@@ -786,6 +786,7 @@ struct GrpcServer::Impl {
         if (c->dead || (c->closing && drained && (c->goaway_sent || c->streams.empty()))) dead.push_back(fd);
       }
       for (int fd : dead) close_conn(fd);
+      if (after_io) after_io();
       if (stopping) {
         bool all_drained = true;
         for (auto& [fd, c] : conns) all_drained = all_drained && c->out.empty();
@@ -797,6 +798,8 @@ struct GrpcServer::Impl {
     for (int fd : fds) close_conn(fd);
   }
 
+  std::function<void()> after_io;
+
   void wake() {
     const uint64_t one = 1;
     ssize_t r = ::write(evfd, &one, sizeof(one));
@@ -807,6 +810,8 @@ struct GrpcServer::Impl {
 GrpcServer::GrpcServer() : impl_(new Impl) {}
 
 GrpcServer::~GrpcServer() { stop(0.0); }
+
+void GrpcServer::set_after_io(std::function<void()> fn) { impl_->after_io = std::move(fn); }
 
 void GrpcServer::add_unary(const std::string& path, UnaryFn fn) {
   Impl::Route r;
