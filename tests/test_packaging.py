@@ -276,10 +276,26 @@ def test_launcher_dispatches_native_first(tmp_path):
 
 
 def test_helm_native_labeller_switch():
-    """lbl.native runs the native labeller from the labeller images (off by default)."""
+    """lbl.native (the default) runs the native labeller from the labeller images."""
     t = (REPO / "helm/amd-gpu/templates/labeller.yaml").read_text()
     assert 'command: ["./mi355x-node-labeller"]' in t and "{{- if .Values.lbl.native }}" in t
     assert 'command: ["./k8s-node-labeller"]' in t
-    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["lbl"]["native"] is False
+    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["lbl"]["native"] is True
     for df in ("labeller.Dockerfile", "ubi-labeller.Dockerfile"):
         assert "bin/mi355x-node-labeller /root/mi355x-node-labeller" in (REPO / df).read_text(), df
+
+
+def test_labeller_launcher_dispatches_native_first(tmp_path):
+    """./k8s-node-labeller runs the native labeller; MI355X_LBL_IMPL=python the Python one."""
+    import subprocess
+    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+    launcher = str(REPO / "scripts/k8s-node-labeller")
+    fi = make_mi355x_node(tmp_path / "n")
+    args = [launcher, "-dry_run", "-node_name", "n", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+            "-vram", "-device-id"]
+    nat = subprocess.run(args, capture_output=True, text=True, timeout=60)
+    py = subprocess.run(args, capture_output=True, text=True, timeout=120, env=dict(os.environ, MI355X_LBL_IMPL="python"))
+    assert nat.returncode == 0 and py.returncode == 0, (nat.stderr[-1000:], py.stderr[-1000:])
+    assert json.loads(nat.stdout) == json.loads(py.stdout)
+    h = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=60)
+    assert h.stdout.startswith("usage: ") and "mi355x-node-labeller" in h.stdout   # the native binary answered
