@@ -40,6 +40,19 @@ def proc_stats(pid: int) -> dict:
     return {"rss_kb": out.get("VmRSS"), "threads": out.get("Threads"), "fds": out["fds"]}
 
 
+def children(ppid: int) -> list:
+    out = []
+    for d in os.listdir("/proc"):
+        if d.isdigit():
+            try:
+                with open(f"/proc/{d}/stat") as f:
+                    if int(f.read().rsplit(")", 1)[1].split()[1]) == ppid:
+                        out.append(int(d))
+            except (OSError, ValueError, IndexError):
+                pass
+    return out
+
+
 def pct(xs, q):
     xs = sorted(xs)
     return round(xs[min(len(xs) - 1, int(q * len(xs)))], 4) if xs else None
@@ -49,8 +62,11 @@ async def main(a) -> int:
     kdir = tempfile.mkdtemp(prefix="soak-native-")
     k = FakeKubelet(kdir)
     await k.start()
+    extra = a.extra.split() if a.extra else []
+    if a.metrics_port:
+        extra += ["-metrics_port", str(a.metrics_port)]
     proc = await asyncio.create_subprocess_exec(EXE, "-kubelet_dir", kdir, "-sysfs_root", a.sysfs_root,
-                                                "-pulse", str(a.pulse), "-exporter_socket", "",
+                                                "-pulse", str(a.pulse), "-exporter_socket", "", *extra,
                                                 stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
     rows = []
     try:
@@ -62,7 +78,8 @@ async def main(a) -> int:
         lat = []
         first = proc_stats(proc.pid)
         while time.monotonic() < t_end:
-            size = adm % n + 1
+            healthy = len(k.healthy_free("amd.com/gpu")) + 0
+            size = adm % max(1, min(n, healthy)) + 1
             try:
                 r = await k.admit("amd.com/gpu", size)
                 lat.append(r.total_ms)
@@ -74,11 +91,19 @@ async def main(a) -> int:
             if time.monotonic() >= next_report:
                 next_report += a.report
                 row = {"t_s": round(a.seconds - (t_end - time.monotonic()), 1), "admissions": adm, "errors": errors,
-                       "rpc_ms_p50": pct(lat, 0.5), "rpc_ms_p99": pct(lat, 0.99), **proc_stats(proc.pid)}
+                       "rpc_ms_p50": pct(lat, 0.5), "rpc_ms_p99": pct(lat, 0.99), **proc_stats(proc.pid),
+                       "children": [proc_stats(c) for c in children(proc.pid)]}
                 rows.append(row)
                 print(json.dumps(row), flush=True)
                 lat = []
+        metrics = None
+        if a.metrics_port:
+            import urllib.request
+            with urllib.request.urlopen(f"http://127.0.0.1:{a.metrics_port}/metrics", timeout=5) as r:
+                metrics = {ln.rsplit(" ", 1)[0]: float(ln.rsplit(" ", 1)[1]) for ln in r.read().decode().splitlines()
+                           if ln and not ln.startswith("#") and "_bucket" not in ln}
         doc = {"exe": "mi355x-device-plugin", "devices": n, "pulse_s": a.pulse, "seconds": a.seconds,
+               "flags": extra, "metrics_end": metrics,
                "start": first, "reports": rows, "admissions": adm, "errors": errors,
                "listandwatch_updates": k.state("amd.com/gpu").updates if hasattr(k, "state") else None}
     finally:
@@ -102,4 +127,6 @@ if __name__ == "__main__":
     ap.add_argument("--pulse", type=int, default=1)
     ap.add_argument("--sysfs-root", default="/sys")
     ap.add_argument("--out", default="")
+    ap.add_argument("--extra", default="", help="more daemon flags, space-separated")
+    ap.add_argument("--metrics-port", type=int, default=0)
     sys.exit(asyncio.run(main(ap.parse_args())))
