@@ -461,8 +461,10 @@ def test_native_daemon_chip_sweep_and_throughput_check(inv, ordinals, tmp_path):
             else:
                 assert m.get("mi355x_dp_chip_sweeps_total", 0) >= 2, m
                 assert m[f'mi355x_dp_perf_state{{device="{dev_id}"}}'] == 0.0, m
-                assert m[f'mi355x_dp_perf_hbm_read_gbps{{device="{dev_id}"}}'] > 1000
-                assert m[f'mi355x_dp_perf_mfma_tflops{{device="{dev_id}"}}'] > 500
+                # plausible MI355X rates (HBM3E peak 8 TB/s, dense bf16 2.5 PFLOP/s): broken dispatch
+                # timing (e.g. under a kernel-tracing profiler) shows as absurd values
+                assert 1000 < m[f'mi355x_dp_perf_hbm_read_gbps{{device="{dev_id}"}}'] < 9000, m
+                assert 500 < m[f'mi355x_dp_perf_mfma_tflops{{device="{dev_id}"}}'] < 2600, m
             assert k.resources["amd.com/gpu"].devices[dev_id] == "Healthy"
         finally:
             if proc.returncode is None:
