@@ -7,6 +7,7 @@
 // flush (shutdown); timestamps are CLOCK_MONOTONIC microseconds.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <deque>
 #include <mutex>
@@ -21,7 +22,7 @@ using Args = std::vector<std::pair<std::string, std::string>>;
 class Tracer {
  public:
   void configure(const std::string& path, size_t max_events = 200000);
-  bool enabled() const { return enabled_; }
+  bool enabled() const { return enabled_.load(std::memory_order_relaxed); }
   // a span recorded elsewhere (the gRPC server's RPC events): monotonic ns
   void complete(const std::string& name, const std::string& cat, uint64_t t0_ns, uint64_t dur_ns, const Args& args);
   void instant(const std::string& name, const std::string& cat, const Args& args);
@@ -30,7 +31,7 @@ class Tracer {
 
  private:
   void push(std::string ev);
-  bool enabled_ = false;
+  std::atomic<bool> enabled_{false};
   std::string path_;
   size_t max_ = 200000;
   mutable std::mutex mu_;
