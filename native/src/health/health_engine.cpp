@@ -589,6 +589,11 @@ std::map<int, ProbeOutcome> LivenessProber::probe(const std::vector<int>& ordina
       sweeps++;
       return res;
     }
+    if (err == "interrupted") {  // shutdown: no fresh processes now
+      std::map<int, ProbeOutcome> out;
+      for (int o : uniq) out[o].reason = "probe interrupted (shutdown)";
+      return out;
+    }
     // a wedged device stalls the whole server: drop it and isolate per device
     MI_LOG(kWarning, "probe server failed (%s); re-probing each device in its own process", err.c_str());
     fallbacks++;

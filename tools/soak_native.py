@@ -65,9 +65,12 @@ async def main(a) -> int:
     extra = a.extra.split() if a.extra else []
     if a.metrics_port:
         extra += ["-metrics_port", str(a.metrics_port)]
+    # the daemon logs every Allocate (as the reference does): its stderr goes to a file, a
+    # pipe nobody reads would fill and block its control loop (and with it the health pulses)
+    errf = open(os.path.join(kdir, "daemon.stderr"), "w+b")
     proc = await asyncio.create_subprocess_exec(EXE, "-kubelet_dir", kdir, "-sysfs_root", a.sysfs_root,
                                                 "-pulse", str(a.pulse), "-exporter_socket", "", *extra,
-                                                stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
+                                                stdout=asyncio.subprocess.DEVNULL, stderr=errf)
     rows = []
     try:
         st = await k.wait_for_resource("amd.com/gpu", 1, timeout=30)
@@ -109,8 +112,12 @@ async def main(a) -> int:
     finally:
         if proc.returncode is None:
             proc.terminate()
-        _, err = await asyncio.wait_for(proc.communicate(), 20)
+        await asyncio.wait_for(proc.wait(), 20)
         await k.stop()
+        errf.seek(0, os.SEEK_END)
+        errf.seek(max(0, errf.tell() - 4000))
+        err = errf.read()
+        errf.close()
     doc["exit_code"] = proc.returncode
     doc["stderr_tail"] = err.decode(errors="replace")[-500:]
     if a.out:
