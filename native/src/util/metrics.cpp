@@ -217,7 +217,15 @@ void HttpEndpoint::loop() {
     if (p[1].revents) return;
     if (!(p[0].revents & POLLIN)) continue;
     const int c = ::accept4(fd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
-    if (c < 0) continue;
+    if (c < 0) {
+      // out of fds (EMFILE/ENFILE) leaves the connection queued and the listener
+      // readable: back off instead of spinning on it
+      if (errno != EAGAIN && errno != EINTR && errno != ECONNABORTED) {
+        pollfd q{stop_[0], POLLIN, 0};
+        ::poll(&q, 1, 100);
+      }
+      continue;
+    }
     // the request head, within 5 s
     std::string req;
     const auto deadline = Clock::now() + std::chrono::seconds(5);
