@@ -1,6 +1,7 @@
 // The YAML subset configuration files use (see yaml.h).
 #include "yaml.h"
 
+#include <cstdint>
 #include <vector>
 
 namespace mi355x::yaml {
@@ -59,6 +60,14 @@ class Parser {
 
   std::optional<json::Value> document() {
     if (lines_.empty()) return json::Value::object();
+    const char c0 = lines_[0].text[0];
+    if (c0 == '[' || c0 == '{') {  // a flow collection as the document, possibly over several lines
+      std::string all;
+      for (const auto& l : lines_) all += (all.empty() ? "" : " ") + l.text;
+      auto v = scalar_or_flow(all, lines_[0].no);
+      if (!err_->empty()) return std::nullopt;
+      return v;
+    }
     size_t i = 0;
     auto v = block(&i, lines_[0].indent);
     if (v && i < lines_.size()) fail(lines_[i].no, "unexpected content");
@@ -221,6 +230,63 @@ class Parser {
     return json::Value::string(t);
   }
 
+  static void utf8(std::string* out, uint32_t cp) {
+    if (cp < 0x80) {
+      out->push_back(static_cast<char>(cp));
+    } else if (cp < 0x800) {
+      out->push_back(static_cast<char>(0xC0 | (cp >> 6)));
+      out->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+      out->push_back(static_cast<char>(0xE0 | (cp >> 12)));
+      out->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+      out->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    } else {
+      out->push_back(static_cast<char>(0xF0 | (cp >> 18)));
+      out->push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+      out->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+      out->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    }
+  }
+
+  // a double-quoted scalar's escape at s[*p] == '\\' (YAML 1.2 5.7); *p ends on its last character
+  static bool escape(const std::string& s, size_t* p, std::string* out) {
+    const char e = s[++*p];
+    switch (e) {
+      case '0': out->push_back('\0'); return true;
+      case 'a': out->push_back('\a'); return true;
+      case 'b': out->push_back('\b'); return true;
+      case 't': case '\t': out->push_back('\t'); return true;
+      case 'n': out->push_back('\n'); return true;
+      case 'v': out->push_back('\v'); return true;
+      case 'f': out->push_back('\f'); return true;
+      case 'r': out->push_back('\r'); return true;
+      case 'e': out->push_back('\x1b'); return true;
+      case ' ': case '"': case '/': case '\\': out->push_back(e); return true;
+      case 'N': utf8(out, 0x85); return true;
+      case '_': utf8(out, 0xA0); return true;
+      case 'L': utf8(out, 0x2028); return true;
+      case 'P': utf8(out, 0x2029); return true;
+      case 'x': case 'u': case 'U': {
+        const size_t n = e == 'x' ? 2 : e == 'u' ? 4 : 8;
+        if (*p + n >= s.size()) return false;
+        uint32_t cp = 0;
+        for (size_t k = 1; k <= n; ++k) {
+          const char h = s[*p + k];
+          const int d = h >= '0' && h <= '9' ? h - '0' : h >= 'a' && h <= 'f' ? h - 'a' + 10
+                        : h >= 'A' && h <= 'F' ? h - 'A' + 10 : -1;
+          if (d < 0) return false;
+          cp = cp * 16 + static_cast<uint32_t>(d);
+        }
+        if (cp > 0x10FFFF) return false;
+        *p += n;
+        utf8(out, cp);
+        return true;
+      }
+      default:
+        return false;
+    }
+  }
+
   // a value starting at s[*p]; in_flow: plain scalars end at , ] }
   std::optional<json::Value> flow(const std::string& s, size_t* p, int no, bool in_flow) {
     while (*p < s.size() && s[*p] == ' ') ++*p;
@@ -230,8 +296,7 @@ class Parser {
       std::string out;
       for (++*p; *p < s.size() && s[*p] != '"'; ++*p) {
         if (s[*p] == '\\' && *p + 1 < s.size()) {
-          const char e = s[++*p];
-          out.push_back(e == 'n' ? '\n' : e == 't' ? '\t' : e);
+          if (!escape(s, p, &out)) return fail(no, "bad escape in a double-quoted scalar"), std::nullopt;
         } else {
           out.push_back(s[*p]);
         }
@@ -333,10 +398,15 @@ class Parser {
 std::optional<json::Value> parse(const std::string& text, std::string* error) {
   std::string err;
   const size_t first = text.find_first_not_of(" \t\r\n");
-  if (first != std::string::npos && text[first] == '{') {  // JSON kubeconfig
-    auto v = json::parse(text, &err);
-    if (!v && error) *error = err;
-    return v;
+  if (first != std::string::npos && (text[first] == '{' || text[first] == '[')) {
+    // JSON (a JSON kubeconfig); else a YAML flow collection, whose error is
+    // reported only when the text is not JSON either
+    if (auto v = json::parse(text, &err)) return v;
+    std::string yerr;
+    Parser p(text, &yerr);
+    if (auto v = p.document()) return v;
+    if (error) *error = err;
+    return std::nullopt;
   }
   Parser p(text, &err);
   auto v = p.document();

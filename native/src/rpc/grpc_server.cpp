@@ -111,6 +111,23 @@ std::string percent_encode(const std::string& s) {
   return o;
 }
 
+// grpc-message as grpc-go sends it: percent-encoded (a malformed escape is kept as is)
+std::string percent_decode(const std::string& s) {
+  auto hexv = [](char h) {
+    return h >= '0' && h <= '9' ? h - '0' : h >= 'a' && h <= 'f' ? h - 'a' + 10 : h >= 'A' && h <= 'F' ? h - 'A' + 10 : -1;
+  };
+  std::string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && hexv(s[i + 1]) >= 0 && hexv(s[i + 2]) >= 0) {
+      o.push_back(static_cast<char>(hexv(s[i + 1]) * 16 + hexv(s[i + 2])));
+      i += 2;
+    } else {
+      o.push_back(s[i]);
+    }
+  }
+  return o;
+}
+
 struct Stream {
   uint32_t id = 0;
   std::string header_block;
@@ -1163,7 +1180,7 @@ Reply GrpcClient::unary(const std::string& path, const std::string& request, dou
       if (k == ":status") call.http_status = std::atoi(v.c_str());
       else if (k == "content-type") call.content_type = v;
       else if (k == "grpc-status") call.grpc_status = std::atoi(v.c_str());
-      else if (k == "grpc-message") call.grpc_message = v;
+      else if (k == "grpc-message") call.grpc_message = percent_decode(v);
     }
     call.headers_seen = true;
     if (end_stream) call.done = true;

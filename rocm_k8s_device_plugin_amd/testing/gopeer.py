@@ -377,6 +377,15 @@ def grpc_message(msg: bytes) -> bytes:
     return b"\x00" + struct.pack(">I", len(msg)) + msg
 
 
+def encode_grpc_message(msg: str) -> str:
+    """grpc-go's encodeGrpcMessage (internal/transport/http_util.go:224-262):
+    printable ASCII but '%' passes through, every other byte is %XX."""
+    out = []
+    for b in msg.encode("utf-8", "surrogateescape"):
+        out.append(chr(b) if 0x20 <= b <= 0x7E and b != 0x25 else "%%%02X" % b)
+    return "".join(out)
+
+
 def encode_duration(seconds: float) -> str:
     """grpcutil.EncodeDuration: the finest unit that fits in 8 digits, rounded up."""
     ns = int(round(seconds * 1e9))
@@ -1056,7 +1065,8 @@ class _ServerConn:
         code, message, resp = h(msg) if h is not None else (12, f"unknown method {hdr.get(':path')}", b"")
         if code != 0:   # trailers-only
             self._headers(sid, [(":status", "200"), ("content-type", "application/grpc"),
-                                ("grpc-status", str(code)), ("grpc-message", message)], True)
+                                ("grpc-status", str(code)), ("grpc-message", encode_grpc_message(message))],
+                          True)
         else:
             self._headers(sid, [(":status", "200"), ("content-type", "application/grpc")], False)
             if cfg.settings_after_headers:

@@ -388,7 +388,8 @@ def test_native_client_unknown_method_and_grpc_error(tmp_path):
         c = _client(path)
         assert c.unary("/nope/Nope", b"", 5.0)[0] == 12
         status, msg, _ = c.unary(ECHO, b"", 5.0)
-        assert status == 9 and msg.startswith("precondition")
+        # sent percent-encoded as grpc-go does (encodeGrpcMessage), decoded by the client
+        assert status == 9 and msg == "precondition: ünïcode"
 
 
 def test_native_client_deadline_and_abort_against_a_silent_server(tmp_path):

@@ -162,6 +162,11 @@ def test_ci_command_lines_pass_the_real_argument_parsers():
                 _build.make_parser().parse_args(argv[3:])
             elif argv[1] == "bench.py":
                 bench.make_parser().parse_args(argv[2:])
+            elif argv[1] == "tools/fuzz_native.py":
+                fspec = importlib.util.spec_from_file_location("fuzz_native", REPO / "tools" / "fuzz_native.py")
+                fzm = importlib.util.module_from_spec(fspec)
+                fspec.loader.exec_module(fzm)
+                fzm.make_parser().parse_args(argv[2:])
             elif argv[1:3] == ["-m", "pytest"]:
                 r = subprocess.run([sys.executable, "-m", "pytest", *argv[3:], "--collect-only", "-q",
                                     "-p", "no:cacheprovider"], cwd=REPO, capture_output=True, text=True, timeout=300)
