@@ -100,8 +100,19 @@ class Parser {
     return std::string::npos;
   }
 
+  // nesting bound (block and flow collections): a hostile or broken file
+  // must not exhaust the stack (the JSON reader has the same bound)
+  static constexpr int kMaxDepth = 128;
+  struct Nest {
+    explicit Nest(int* d) : d_(d) { ++*d_; }
+    ~Nest() { --*d_; }
+    int* d_;
+  };
+
   std::optional<json::Value> block(size_t* i, int indent) {
+    Nest nest(&depth_);
     if (*i >= lines_.size()) return json::Value{};
+    if (depth_ > kMaxDepth) return fail(lines_[*i].no, "nested too deeply"), std::nullopt;
     if (is_seq_item(lines_[*i].text)) return sequence(i, indent);
     return mapping(i, indent);
   }
@@ -289,6 +300,8 @@ class Parser {
 
   // a value starting at s[*p]; in_flow: plain scalars end at , ] }
   std::optional<json::Value> flow(const std::string& s, size_t* p, int no, bool in_flow) {
+    Nest nest(&depth_);
+    if (depth_ > kMaxDepth) return fail(no, "nested too deeply"), std::nullopt;
     while (*p < s.size() && s[*p] == ' ') ++*p;
     if (*p >= s.size()) return json::Value{};
     const char c = s[*p];
@@ -389,6 +402,7 @@ class Parser {
   }
 
   std::string* err_;
+  int depth_ = 0;
   std::vector<std::string> raw_;
   std::vector<Line> lines_;
 };
