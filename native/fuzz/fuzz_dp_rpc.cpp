@@ -2,9 +2,10 @@
 // well-formed gRPC calls: the protobuf a kubelet sends, mutated. Byte 0 picks
 // the method, the rest is the request message. Invariants:
 //   * every call gets a gRPC status (never a transport failure);
-//   * GetPreferredAllocation OK -> one answer per container request, each of
-//     exactly allocation_size distinct IDs, all available, every
-//     must_include ID among them;
+//   * GetPreferredAllocation OK -> one answer per container request; for a
+//     request kubelet can send (no repeated IDs, must_include within available)
+//     exactly allocation_size distinct IDs, all available, every must_include
+//     ID among them;
 //   * Allocate OK -> one ContainerAllocateResponse per container request with
 //     /dev/kfd plus the card and render node of every requested ID, in order;
 //     an unknown ID is INVALID_ARGUMENT.
@@ -124,6 +125,12 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
       const std::set<std::string> chosen(got[i].begin(), got[i].end());
       const bool dup_free = avail.size() == req[i].a.size() && must.size() == req[i].b.size();
       if (!dup_free) continue;  // kubelet never repeats an ID; the reference returns such lists as given
+      // kubelet's must-include IDs are a subset of the available ones; the reference's
+      // short-circuits (|available| == size -> available, |must| == size -> must) return
+      // other requests' lists unchanged (besteffort_policy.go:110-116), and so does this one
+      bool must_in_avail = true;
+      for (const auto& id : must) must_in_avail = must_in_avail && avail.count(id);
+      if (!must_in_avail) continue;
       if (static_cast<int64_t>(got[i].size()) != req[i].size || chosen.size() != got[i].size())
         fail("GetPreferredAllocation: wrong number of distinct IDs");
       for (const auto& id : chosen)
