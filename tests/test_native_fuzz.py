@@ -1,7 +1,8 @@
 """Coverage-guided fuzzing of the native parsers, short runs (tools/fuzz_native.py).
 
 Every libFuzzer target in native/fuzz/ runs for a few seconds from its seed
-corpus under ASan, then everything it kept is replayed under ASan + UBSan; the
+corpus under ASan, then everything it kept is replayed under ASan + UBSan (and
+under TSan for the targets that drive the threaded server or a peer thread); the
 inputs that once broke a target (native/fuzz/regressions/) are replayed too.
 Long campaigns: ``python tools/fuzz_native.py --seconds 600`` (profiles/r3/
 fuzz_native.json). CPU only.
@@ -39,6 +40,8 @@ def test_every_target_runs_clean_from_its_seeds(built, tmp_path):
         rows = list(ex.map(lambda t: fz.run_target(t, SECONDS, tmp_path, seeds[t], env), fz.TARGETS))
     for r in rows:
         assert r["rc"] == 0 and r["replay_rc"] == 0 and not r["findings"], (r["target"], r["error_tail"])
+        if r["target"] in fz.TSAN_TARGETS:    # the server's / peer's threads, under TSan
+            assert r["tsan_replay_rc"] == 0, (r["target"], r["error_tail"])
         assert r["execs"] >= (20 if r["target"] == "sysfs" else 500), r
         # the targets reach code beyond the harness (coverage feedback works)
         assert r["coverage_edges"] and r["coverage_edges"] > 100, r

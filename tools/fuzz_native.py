@@ -35,7 +35,10 @@ sys.path.insert(0, str(REPO))
 NATIVE = REPO / "native"
 BUILD = REPO / "build" / "native-fuzz"            # coverage + ASan
 BUILD_REPLAY = REPO / "build" / "native-fuzz-replay"  # ASan + full UBSan, runs the corpus once
+BUILD_TSAN = REPO / "build" / "native-fuzz-tsan"      # TSan, runs the corpus of the threaded targets once
 TARGETS = ("hpack", "json", "yaml", "sysfs", "h2_server", "h2_client", "dp_rpc", "http_client")
+# targets whose code under test runs on more than one thread (the server's I/O thread, the HTTP peer thread)
+TSAN_TARGETS = ("h2_server", "dp_rpc", "h2_client", "http_client")
 CLANG = Path("/opt/rocm/lib/llvm/bin/clang++")
 
 
@@ -61,14 +64,15 @@ def available() -> bool:
 
 def build(jobs: int = 8) -> None:
     gen = ["-G", "Ninja"] if shutil.which("ninja") else []
-    for mode, bdir in (("fuzz", BUILD), ("replay", BUILD_REPLAY)):
+    for mode, bdir in (("fuzz", BUILD), ("replay", BUILD_REPLAY), ("tsan", BUILD_TSAN)):
         bdir.mkdir(parents=True, exist_ok=True)
         cache = bdir / "CMakeCache.txt"
         if not cache.exists() or f"MI355X_FUZZ:STRING={mode}" not in cache.read_text():
             subprocess.run(["cmake", "-S", str(NATIVE), "-B", str(bdir), *gen, f"-DCMAKE_CXX_COMPILER={clang()}",
                             f"-DMI355X_FUZZ={mode}", "-DMI355X_BUILD_HIP=OFF",
                             f"-DPython3_EXECUTABLE={sys.executable}"], check=True, stdout=subprocess.DEVNULL)
-        r = subprocess.run(["cmake", "--build", str(bdir), "-j", str(jobs)], capture_output=True, text=True)
+        only = [x for t in TSAN_TARGETS for x in ("--target", f"fuzz_{t}")] if mode == "tsan" else []
+        r = subprocess.run(["cmake", "--build", str(bdir), "-j", str(jobs), *only], capture_output=True, text=True)
         if r.returncode != 0:
             sys.stderr.write(r.stdout[-6000:] + r.stderr[-3000:])
             raise RuntimeError(f"fuzz build ({mode}) failed")
@@ -184,51 +188,67 @@ _STAT = re.compile(r"^stat::(\w+):\s+(\d+)", re.M)
 _COV = re.compile(r"#(\d+)\s+(?:INITED|NEW|REDUCE|pulse|DONE)\s+cov: (\d+) ft: (\d+) corp: (\d+)")
 
 
+def _replay(build: Path, t: str, name: str, work: Path, dirs, env: Dict[str, str], timeout_s: float):
+    """Every input in `dirs` once through `build`'s fuzz_<t>: (rc, inputs run, reproducers, stderr)."""
+    art = work / "artifacts" / f"{t}-{name}"
+    art.mkdir(parents=True, exist_ok=True)
+    p = subprocess.run([str(build / f"fuzz_{t}"), "-runs=0", "-timeout=60", "-rss_limit_mb=4096",
+                        f"-artifact_prefix={art}/", *map(str, dirs)],
+                       env=env, capture_output=True, text=True, errors="replace", timeout=timeout_s)
+    (work / f"{t}-{name}.log").write_text(p.stderr)
+    m = re.search(r"#(\d+)\s+(?:INITED|DONE)", p.stderr)
+    return p.returncode, int(m.group(1)) if m else 0, sorted(f"{name}/{x.name}" for x in art.iterdir()), p.stderr
+
+
 def run_target(t: str, seconds: float, work: Path, seeds: Path, env: Dict[str, str]) -> dict:
-    exe = BUILD / f"fuzz_{t}"
+    """Fuzz `t` for `seconds` (coverage + ASan), then replay everything it kept
+    under ASan + UBSan, and for the threaded targets under TSan."""
     corpus = work / "corpus" / t
     art = work / "artifacts" / t
     corpus.mkdir(parents=True, exist_ok=True)
     art.mkdir(parents=True, exist_ok=True)
     # sockets live here: keep the path well under the 108-byte sun_path limit
     scratch = Path(tempfile.mkdtemp(prefix=f"mf-{t}-", dir="/tmp"))
-    e = dict(os.environ, **env, MI355X_FUZZ_TMP=str(scratch))
-    if t == "sysfs":  # a private copy per run: the target rewrites files in place
-        mut = work / "sysfs-mut"
-        shutil.rmtree(mut, ignore_errors=True)
-        shutil.copytree(env["MI355X_FUZZ_SYSFS_MUT"], mut, symlinks=True)
-        e["MI355X_FUZZ_SYSFS_MUT"] = str(mut)
-    argv = [str(exe), f"-max_total_time={int(max(1, seconds))}", "-timeout=25", "-rss_limit_mb=4096",
-            "-print_final_stats=1", "-max_len=65536", f"-artifact_prefix={art}/", str(corpus), str(seeds)]
-    t0 = time.monotonic()
-    p = subprocess.run(argv, env=e, capture_output=True, text=True, errors="replace", timeout=seconds + 300)
-    wall = time.monotonic() - t0
-    log = p.stderr
-    (work / f"{t}.log").write_text(log)
-    stats = {k: int(v) for k, v in _STAT.findall(log)}
-    cov = _COV.findall(log)
-    # every input the run kept (and the seeds), once more under the full UBSan build
-    rart = work / "artifacts" / f"{t}-replay"
-    rart.mkdir(parents=True, exist_ok=True)
-    rp = subprocess.run([str(BUILD_REPLAY / f"fuzz_{t}"), "-runs=0", "-timeout=25", "-rss_limit_mb=4096",
-                         f"-artifact_prefix={rart}/", str(corpus), str(seeds)],
-                        env=e, capture_output=True, text=True, errors="replace", timeout=seconds + 600)
-    (work / f"{t}-replay.log").write_text(rp.stderr)
-    shutil.rmtree(scratch, ignore_errors=True)
-    m = re.search(r"#(\d+)\s+(?:INITED|DONE)", rp.stderr)
-    replayed = int(m.group(1)) if m else 0
-    findings = sorted(x.name for x in art.iterdir()) + sorted(f"replay/{x.name}" for x in rart.iterdir())
-    if rp.returncode != 0 and p.returncode == 0:
-        log += "\n--- replay ---\n" + rp.stderr
+    try:
+        e = dict(os.environ, **env, MI355X_FUZZ_TMP=str(scratch))
+        if t == "sysfs":  # a private copy per run: the target rewrites files in place
+            mut = work / "sysfs-mut"
+            shutil.rmtree(mut, ignore_errors=True)
+            shutil.copytree(env["MI355X_FUZZ_SYSFS_MUT"], mut, symlinks=True)
+            e["MI355X_FUZZ_SYSFS_MUT"] = str(mut)
+        argv = [str(BUILD / f"fuzz_{t}"), f"-max_total_time={int(max(1, seconds))}", "-timeout=25",
+                "-rss_limit_mb=4096", "-print_final_stats=1", "-max_len=65536", f"-artifact_prefix={art}/",
+                str(corpus), str(seeds)]
+        t0 = time.monotonic()
+        p = subprocess.run(argv, env=e, capture_output=True, text=True, errors="replace", timeout=seconds + 300)
+        wall = time.monotonic() - t0
+        log = p.stderr
+        (work / f"{t}.log").write_text(log)
+        stats = {k: int(v) for k, v in _STAT.findall(log)}
+        cov = _COV.findall(log)
+        findings = sorted(x.name for x in art.iterdir())
+        rrc, replayed, rfind, rerr = _replay(BUILD_REPLAY, t, "replay", work, (corpus, seeds), e, seconds + 600)
+        findings += rfind
+        if rrc != 0:
+            log += "\n--- replay (ASan + UBSan) ---\n" + rerr
+        trc = None
+        if t in TSAN_TARGETS:
+            trc, _, tfind, terr = _replay(BUILD_TSAN, t, "tsan", work, (corpus, seeds),
+                                          dict(e, TSAN_OPTIONS="halt_on_error=1"), seconds + 1200)
+            findings += tfind
+            if trc != 0:
+                log += "\n--- replay (TSan) ---\n" + terr
+    finally:
+        shutil.rmtree(scratch, ignore_errors=True)
+    ok = p.returncode == 0 and rrc == 0 and not trc
     return {"target": t, "rc": p.returncode, "seconds": round(wall, 1),
             "execs": stats.get("number_of_executed_units", 0),
             "execs_per_s": stats.get("average_exec_per_sec", 0),
             "peak_rss_mb": stats.get("peak_rss_mb", 0),
             "coverage_edges": int(cov[-1][1]) if cov else None, "features": int(cov[-1][2]) if cov else None,
             "corpus": len(list(corpus.iterdir())), "seeds": len(list(seeds.iterdir())),
-            "replayed_full_ubsan": replayed, "replay_rc": rp.returncode,
-            "findings": findings,
-            "error_tail": "" if p.returncode == 0 and rp.returncode == 0 else "\n".join(log.splitlines()[-40:])}
+            "replayed_full_ubsan": replayed, "replay_rc": rrc, "tsan_replay_rc": trc,
+            "findings": findings, "error_tail": "" if ok else "\n".join(log.splitlines()[-40:])}
 
 
 def make_parser() -> argparse.ArgumentParser:
@@ -260,7 +280,8 @@ def main(argv=None) -> int:
             raise SystemExit(f"unknown target {t}")
     with ThreadPoolExecutor(max_workers=max(1, a.parallel)) as ex:
         rows = list(ex.map(lambda t: run_target(t, a.seconds, work, seeds[t], env), targets))
-    summary = {"tool": "tools/fuzz_native.py", "engine": "libFuzzer", "sanitizers": "fuzzing: ASan (+ leak check); replay of every corpus input: ASan + UBSan (all but null)",
+    summary = {"tool": "tools/fuzz_native.py", "engine": "libFuzzer", "sanitizers": "fuzzing: ASan (+ leak check); replay of every corpus input: ASan + UBSan (all but null); "
+               "threaded targets' corpora once more under TSan",
                "seconds_per_target": a.seconds, "work": str(work), "targets": rows,
                "total_execs": sum(r["execs"] for r in rows),
                "findings": sum(len(r["findings"]) for r in rows)}
@@ -268,7 +289,8 @@ def main(argv=None) -> int:
     print(text)
     if a.json:
         Path(a.json).write_text(text + "\n")
-    return 0 if all(r["rc"] == 0 and r["replay_rc"] == 0 and not r["findings"] for r in rows) else 1
+    return 0 if all(r["rc"] == 0 and r["replay_rc"] == 0 and not r["tsan_replay_rc"] and not r["findings"]
+                    for r in rows) else 1
 
 
 if __name__ == "__main__":
