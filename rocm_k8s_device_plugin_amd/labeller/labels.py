@@ -162,6 +162,36 @@ def sanitize_label_value(v: str) -> str:
     return re.sub(r"^[^A-Za-z0-9]+|[^A-Za-z0-9]+$", "", out)
 
 
+_DNS_LABEL_RE = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?$")
+
+
+def valid_label_key(k: str) -> bool:
+    """apimachinery IsQualifiedName: an optional DNS-subdomain prefix and '/',
+    then a name of <= 63 characters shaped like a label value (non-empty)."""
+    prefix, _, name = k.rpartition("/") if "/" in k else ("", "", k)
+    if not name or len(name) > 63 or not _LABEL_VALUE_RE.match(name):
+        return False
+    if "/" in k:
+        if not prefix or len(prefix) > 253:
+            return False
+        if not all(len(part) <= 63 and _DNS_LABEL_RE.match(part) for part in prefix.split(".")):
+            return False
+    return True
+
+
+def clean_labels(labels: Dict[str, str]) -> Dict[str, str]:
+    """Values sanitised; a label whose key is invalid (a value that went into
+    the key: product name, firmware name) is dropped with a warning, since the
+    apiserver would reject the whole patch."""
+    out = {}
+    for k, v in labels.items():
+        if not valid_label_key(k):
+            _log.warning("dropping label %s: not a valid Kubernetes label key", k)
+            continue
+        out[k] = sanitize_label_value(v)
+    return out
+
+
 def _driver_version_value(raw: str) -> str:
     # amd-smi reports an in-tree amdgpu's version as the kernel banner with the
     # spaces removed ("Linuxversion6.18.54-ant.1(nixbld@...)..." on the MI355X
@@ -388,7 +418,7 @@ def generate_container_labels(enabled: Dict[str, bool], ctx: LabelContext) -> Di
         if not enabled.get(name):
             continue
         results.update(gen(ctx))
-    return {k: sanitize_label_value(v) for k, v in results.items()}
+    return clean_labels(results)
 
 
 def generate_vf_labels(enabled: Dict[str, bool], sysfs_root: str) -> Dict[str, str]:
@@ -448,8 +478,7 @@ def generate_labels(enabled: Dict[str, bool], driver_type: str = "", sysfs_root:
 
     if driver_type == C.CONTAINER:
         return container()
-    def clean(labels):
-        return {k: sanitize_label_value(v) for k, v in labels.items()}
+    clean = clean_labels
 
     if driver_type == C.VF_PASSTHROUGH:
         return clean(generate_vf_labels(enabled, sysfs_root))

@@ -42,7 +42,7 @@ def test_every_target_runs_clean_from_its_seeds(built, tmp_path):
         assert r["rc"] == 0 and r["replay_rc"] == 0 and not r["findings"], (r["target"], r["error_tail"])
         if r["target"] in fz.TSAN_TARGETS:    # the server's / peer's threads, under TSan
             assert r["tsan_replay_rc"] == 0, (r["target"], r["error_tail"])
-        assert r["execs"] >= (20 if r["target"] == "sysfs" else 500), r
+        assert r["execs"] >= (20 if r["target"] in ("sysfs", "labels") else 500), r
         # the targets reach code beyond the harness (coverage feedback works)
         assert r["coverage_edges"] and r["coverage_edges"] > 100, r
         assert r["replayed_full_ubsan"] >= r["seeds"], r
@@ -57,7 +57,7 @@ def test_regression_inputs_replay_clean(built, tmp_path):
         assert d.name in fz.TARGETS, d
         short = tempfile.mkdtemp(prefix="mf-reg-", dir="/tmp")  # socket paths under the sun_path limit
         e = dict(os.environ, **env, MI355X_FUZZ_TMP=short)
-        if d.name == "sysfs":
+        if d.name in ("sysfs", "labels"):
             mut = tmp_path / "mut"
             shutil.copytree(env["MI355X_FUZZ_SYSFS_MUT"], mut, symlinks=True)
             e["MI355X_FUZZ_SYSFS_MUT"] = str(mut)

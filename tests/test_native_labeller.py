@@ -80,6 +80,21 @@ def test_label_values_are_sanitised_like_the_python_labeller(tmp_path):
     out = json.loads(_dry_run(fi, KINDS))
     assert out == _python(fi, KINDS)
     assert all(len(v) <= 63 for v in out.values())
+    # a value that goes into a key ("<prefix>.<product name>" counters) must not make the
+    # key invalid: the apiserver would reject the whole patch; such labels are dropped
+    assert all(L.valid_label_key(k) and L.sanitize_label_value(v) == v for k, v in out.items())
+    assert not [k for k in out if "OAM" in k]                # card1's counter key is dropped
+    assert out["amd.com/gpu.product-name.AMD_Instinct_MI355X"] == "7"   # the other GPUs' is kept
+    assert out["amd.com/gpu.vram.288G"] == "8"     # and the rest of the node's labels
+
+
+@pytest.mark.parametrize("key,ok", [
+    ("amd.com/gpu.vram", True), ("beta.amd.com/gpu.firmware.SMC.fw.12", True), ("gpu", True),
+    ("amd.com/" + "x" * 63, True), ("amd.com/" + "x" * 64, False), ("amd.com/gpu.product-name.a/b", False),
+    ("Amd.com/gpu", False), ("amd.com/", False), ("/gpu", False), ("amd..com/gpu", False),
+    ("amd.com/gpu.name.A?", False), ("amd.com/-gpu", False), ("a" * 254 + "/x", False)])
+def test_label_key_validation(key, ok):
+    assert L.valid_label_key(key) is ok
 
 
 def test_flags_follow_go_syntax(tmp_path):

@@ -36,7 +36,7 @@ NATIVE = REPO / "native"
 BUILD = REPO / "build" / "native-fuzz"            # coverage + ASan
 BUILD_REPLAY = REPO / "build" / "native-fuzz-replay"  # ASan + full UBSan, runs the corpus once
 BUILD_TSAN = REPO / "build" / "native-fuzz-tsan"      # TSan, runs the corpus of the threaded targets once
-TARGETS = ("hpack", "json", "yaml", "sysfs", "h2_server", "h2_client", "dp_rpc", "http_client")
+TARGETS = ("hpack", "json", "yaml", "sysfs", "labels", "h2_server", "h2_client", "dp_rpc", "http_client")
 # targets whose code under test runs on more than one thread (the server's I/O thread, the HTTP peer thread)
 TSAN_TARGETS = ("h2_server", "dp_rpc", "h2_client", "http_client")
 CLANG = Path("/opt/rocm/lib/llvm/bin/clang++")
@@ -148,6 +148,7 @@ def make_seeds(work: Path, env: Dict[str, str]) -> Dict[str, Path]:
 
     seeds["sysfs"] += [b"", bytes([0, 0, 5, 0]) + b"bad\n\n", bytes([7, 0, 0xFF, 0xFF]),
                        bytes([40, 0, 12, 0]) + b"node_to 999\n"]
+    seeds["labels"] += seeds["sysfs"] + [bytes([0x60, 0, 20, 0]) + b"AMD Instinct (x) /?\n"]
 
     gpa = pb.PreferredAllocationRequest(container_requests=[pb.ContainerPreferredAllocationRequest(
         available_deviceIDs=ids[:16], must_include_deviceIDs=ids[:1], allocation_size=4)]).SerializeToString()
@@ -211,8 +212,8 @@ def run_target(t: str, seconds: float, work: Path, seeds: Path, env: Dict[str, s
     scratch = Path(tempfile.mkdtemp(prefix=f"mf-{t}-", dir="/tmp"))
     try:
         e = dict(os.environ, **env, MI355X_FUZZ_TMP=str(scratch))
-        if t == "sysfs":  # a private copy per run: the target rewrites files in place
-            mut = work / "sysfs-mut"
+        if t in ("sysfs", "labels"):  # a private copy per run: the target rewrites files in place
+            mut = work / f"sysfs-mut-{t}"
             shutil.rmtree(mut, ignore_errors=True)
             shutil.copytree(env["MI355X_FUZZ_SYSFS_MUT"], mut, symlinks=True)
             e["MI355X_FUZZ_SYSFS_MUT"] = str(mut)
