@@ -1,0 +1,157 @@
+"""Concurrent admissions against the native daemon under exporter health
+flips, a CPX -> SPX partition switch and a kubelet restart, all at once (CPU,
+fixtures + fake kubelet + fake exporter). tests/test_stress.py runs the same
+scenario against the Python plugin.
+
+Eight kubelet-side channels hammer GetPreferredAllocation + Allocate on the
+plugin socket. Every answer must be exact: the chosen set has the requested
+size, includes every must-include ID and stays within the available IDs. The
+Allocate specs must match one device snapshot, old or new, never a mix. The
+only errors allowed are the ones the moment explains: an ID the daemon no
+longer advertises, or a socket being re-created by the kubelet restart. Run
+with MI355X_NATIVE_DAEMON_EXE pointing at the ASan/UBSan or TSan build (CI
+does), the same test checks the daemon's threads: the I/O thread, the worker
+threads and the control loop.
+"""
+import asyncio
+import random
+import subprocess
+
+import grpc
+
+from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+from rocm_k8s_device_plugin_amd.testing.fake_exporter import FakeExporter
+from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+from rocm_k8s_device_plugin_amd.topology import discover
+
+from test_native_health import EXE, _stop
+from test_reload import repartition
+
+
+def _specs_by_id(inv):
+    return {d.id: set(["/dev/kfd"] + d.dev_paths()) for d in inv.devices}
+
+
+def test_native_daemon_under_admissions_flips_switch_and_kubelet_restart(tmp_path):
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=False)
+    root = tmp_path / "n"
+    fi = make_mi355x_node(root, compute_partition="cpx")          # 64 devices
+    old_specs = _specs_by_id(discover(str(fi.sysfs)))
+    new_specs = {}
+    sock = str(tmp_path / "exp" / "exporter.sock")
+    kdir = str(tmp_path / "dp")
+    rng = random.Random(4321)
+    stats = {"ok": 0, "stale": 0, "pref_err": 0, "unavailable": 0}
+    ids_now = list(old_specs)
+
+    async def client(seconds):
+        ch = grpc.aio.insecure_channel(f"unix://{kdir}/amd.com_gpu")
+        stub = pb.DevicePluginStub(ch)
+        loop = asyncio.get_running_loop()
+        end = loop.time() + seconds
+        try:
+            while loop.time() < end:
+                ids = list(ids_now)
+                avail = rng.sample(ids, rng.randint(1, len(ids)))
+                size = rng.randint(1, len(avail))
+                must = rng.sample(avail, rng.randint(0, min(2, size)))
+                req = pb.PreferredAllocationRequest()
+                req.container_requests.add(available_deviceIDs=avail, must_include_deviceIDs=must,
+                                           allocation_size=size)
+                try:
+                    pref = await stub.GetPreferredAllocation(req, timeout=10)
+                except grpc.aio.AioRpcError as e:
+                    if e.code() == grpc.StatusCode.UNAVAILABLE:        # the socket is being re-created
+                        stats["unavailable"] += 1
+                        await asyncio.sleep(0.02)
+                        continue
+                    # only an ID the daemon no longer advertises (after the switch) may fail
+                    assert e.code() == grpc.StatusCode.UNKNOWN, e
+                    stats["pref_err"] += 1
+                    continue
+                got = list(pref.container_responses[0].deviceIDs)
+                assert len(got) == size and len(set(got)) == size, (got, size)
+                assert set(must) <= set(got) <= set(avail)
+                areq = pb.AllocateRequest()
+                areq.container_requests.add(devices_ids=got)
+                try:
+                    resp = await stub.Allocate(areq, timeout=10)
+                except grpc.aio.AioRpcError as e:
+                    if e.code() == grpc.StatusCode.UNAVAILABLE:
+                        stats["unavailable"] += 1
+                        continue
+                    assert e.code() == grpc.StatusCode.INVALID_ARGUMENT, e
+                    stats["stale"] += 1
+                    continue
+                paths = {d.host_path for d in resp.container_responses[0].devices}
+                for snap in (old_specs, new_specs):
+                    if snap and all(i in snap for i in got) and paths == set().union(*(snap[i] for i in got)):
+                        break
+                else:
+                    raise AssertionError(f"Allocate specs {sorted(paths)} match no snapshot for {got}")
+                assert sum(d.host_path == "/dev/kfd" for d in resp.container_responses[0].devices) == 1
+                stats["ok"] += 1
+        finally:
+            await ch.close()
+
+    async def go():
+        exp = FakeExporter(sock, {b: "healthy" for b in fi.bdfs})
+        await exp.start()
+        k = FakeKubelet(kdir)
+        await k.start()
+        # the log goes to a file: an unread pipe would block the daemon's writes (as a
+        # container runtime never does) and stall its control loop
+        log = open(tmp_path / "daemon.log", "w")
+        p = subprocess.Popen([EXE, "-kubelet_dir", kdir, "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                              "-exporter_socket", sock, "-pulse", "1", "-topology_watch", "0.05"],
+                             stdout=subprocess.DEVNULL, stderr=log, text=True)
+        try:
+            await k.wait_for_resource("amd.com/gpu", 64, timeout=20)
+
+            async def flipper():
+                for _ in range(250):
+                    for b in fi.bdfs:
+                        exp.states[b] = "unhealthy" if rng.random() < 0.3 else "healthy"
+                    await asyncio.sleep(0.01)
+                for b in fi.bdfs:
+                    exp.states[b] = "healthy"
+
+            async def switcher():
+                await asyncio.sleep(0.6)
+                repartition(root, compute_partition="spx", generation=2)
+                new_specs.update(_specs_by_id(discover(str(fi.sysfs))))
+                ids_now[:] = list(new_specs)
+
+            async def kubelet_restart():
+                await asyncio.sleep(1.4)
+                await k.restart(downtime_s=0.1)
+
+            await asyncio.gather(flipper(), switcher(), kubelet_restart(), *(client(3.0) for _ in range(8)))
+            # after the storm: 8 whole GPUs advertised on the restarted kubelet, all healthy
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            for _ in range(300):
+                if sorted(st.devices) == sorted(fi.bdfs) and all(h == "Healthy" for h in st.devices.values()):
+                    break
+                await asyncio.sleep(0.05)
+            assert sorted(st.devices) == sorted(fi.bdfs), sorted(st.devices)
+            assert all(h == "Healthy" for h in st.devices.values()), st.devices
+            adm = await k.admit("amd.com/gpu", 2)
+            assert len(adm.device_ids) == 2 and p.poll() is None
+        finally:
+            rc, _ = await asyncio.to_thread(_stop, p)
+            log.close()
+            err = (tmp_path / "daemon.log").read_text()
+            await k.stop()
+            await exp.stop()
+        assert rc == 0, err[-4000:]
+        assert "ERROR: AddressSanitizer" not in err and "WARNING: ThreadSanitizer" not in err, err[-4000:]
+        return err
+
+    err = asyncio.run(asyncio.wait_for(go(), 150))
+    print("native stress", stats)
+    assert stats["ok"] >= 300, stats
+    # the storm overlapped the traffic: answers after the switch, errors for IDs it removed
+    assert stats["pref_err"] + stats["stale"] > 0, stats
+    assert "GPU topology changed" in err
