@@ -10,6 +10,7 @@
 #include <string>
 
 #include "../src/kube/labels.h"
+#include "mi355x/glog.h"
 #include "sysfs_mutator.h"
 
 using namespace mi355x;
@@ -21,6 +22,9 @@ labeller::LabelOptions g_opt;
 }  // namespace
 
 extern "C" int LLVMFuzzerInitialize(int*, char***) {
+  glog::Options quiet;  // the generators log every libdrm / sysfs miss: gigabytes over a campaign
+  quiet.discard = true;
+  glog::init(quiet);
   g_tree = std::make_unique<fuzz::SysfsMutator>(fuzz::env_or_die("MI355X_FUZZ_SYSFS_MUT"));
   g_opt.sysfs_root = g_tree->root();
   g_opt.dev_root = fuzz::scratch_dir() + "/dev";  // no /dev/dri nodes: libdrm queries fail fast

@@ -16,6 +16,10 @@
 //   -v=N / -vmodule=p=N   VLOG(n) enabled globally / per source file (glob on the
 //                         file's base name without extension, or on the path
 //                         when the pattern contains '/')
+//   -log_link=DIR         also a <program>.<SEV> symlink in DIR to each log file
+//                         (glog_file.go:45,133-137)
+//   -logbuflevel=N        accepted (glog_file.go:46); records are never buffered:
+//                         each is written and flushed as it is logged
 //   -log_backtrace_at=f:N a record logged from file f, line N carries a stack trace
 //   -log_format=json      one JSON object per record instead of the glog line:
 //                         {"ts", "level", "src", "msg"} plus the record's fields,
@@ -42,6 +46,9 @@ struct Options {
   std::string log_backtrace_at;
   std::string program;  // file name prefix (default: basename of argv[0])
   bool json = false;    // -log_format=json
+  std::string log_link; // -log_link
+  int logbuflevel = 0;  // -logbuflevel (accepted, see above)
+  bool discard = false; // not a flag: drop every record (fuzz targets, embedders)
 };
 
 using Fields = std::vector<std::pair<std::string, std::string>>;

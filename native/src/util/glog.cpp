@@ -96,6 +96,12 @@ FILE* open_file(State& s, int sev, const tm& lt) {
   ::unlink(link.c_str());
   if (::symlink(name.c_str(), link.c_str()) != 0) {
   }
+  if (!o.log_link.empty()) {  // glog_file.go:133-137: a link to the full path
+    const std::string l2 = o.log_link + "/" + prog + "." + kSevName[sev];
+    ::unlink(l2.c_str());
+    if (::symlink(path.c_str(), l2.c_str()) != 0) {
+    }
+  }
   s.paths[sev] = path;
   return f;
 }
@@ -136,6 +142,14 @@ bool parse_flag(const std::string& name, const std::string& value, bool has_valu
     return true;
   }
   if (name == "log_dir") return o->log_dir = value, true;
+  if (name == "log_link") return o->log_link = value, true;
+  if (name == "logbuflevel") {
+    char* end = nullptr;
+    const long v = std::strtol(value.c_str(), &end, 10);
+    if (value.empty() || *end) *err = "invalid value \"" + value + "\" for flag -logbuflevel";
+    o->logbuflevel = static_cast<int>(v);
+    return true;
+  }
   if (name == "vmodule") return o->vmodule = value, true;
   if (name == "log_backtrace_at") return o->log_backtrace_at = value, true;
   if (name == "log_format") {
@@ -223,6 +237,7 @@ void emit(Severity sev, const char* file, int line, const std::string& msg, cons
   State& s = state();
   std::lock_guard<std::mutex> lk(s.mu);
   const Options& o = s.opt;
+  if (o.discard) return;
   std::string rec;
   if (o.json) {
     char t[48];

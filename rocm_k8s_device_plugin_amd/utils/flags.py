@@ -53,12 +53,15 @@ class GoFlagParser(argparse.ArgumentParser):
 
 
 def add_glog_flags(p: GoFlagParser) -> None:
-    """glog's standard flags (glog_flags.go:388-397)."""
+    """glog's standard flags (glog_flags.go:388-397, glog_file.go:44-46)."""
     p.add_int("v", 0, "log level for V logs")
     p.add_bool("logtostderr", True, "log to standard error instead of files")
     p.add_bool("alsologtostderr", False, "log to standard error as well as files")
     p.add_str("stderrthreshold", "ERROR", "logs at or above this threshold go to stderr")
     p.add_str("log_dir", "", "If non-empty, write log files in this directory")
+    p.add_str("log_link", "", "If non-empty, add symbolic links in this directory to the log files")
+    p.add_int("logbuflevel", 0, "Buffer log messages logged at this level or lower (accepted; records are "
+              "written and flushed as they are logged)")
     p.add_str("vmodule", "", "comma-separated list of pattern=N settings for file-filtered logging")
     p.add_str("log_backtrace_at", "", "when logging hits line file:N, emit a stack trace")
 

@@ -73,9 +73,10 @@ class _GlogFileHandler(logging.Handler):
     with glog's header, plus the ``<prog>.<SEV>`` symlink to it
     (vendor/github.com/golang/glog/glog_file.go semantics)."""
 
-    def __init__(self, log_dir: str, program: str, severity: str, level: int, formatter: logging.Formatter):
+    def __init__(self, log_dir: str, program: str, severity: str, level: int, formatter: logging.Formatter,
+                 log_link: str = ""):
         super().__init__(level)
-        self.log_dir, self.program, self.severity = log_dir, program, severity
+        self.log_dir, self.program, self.severity, self.log_link = log_dir, program, severity, log_link
         self.setFormatter(formatter)
         self._f = None
         self.path = ""
@@ -105,6 +106,14 @@ class _GlogFileHandler(logging.Handler):
             os.symlink(name, link)
         except OSError:
             pass
+        if self.log_link:   # -log_link: a link to the full path (glog_file.go:133-137)
+            link2 = os.path.join(self.log_link, f"{self.program}.{self.severity}")
+            try:
+                if os.path.islink(link2) or os.path.exists(link2):
+                    os.unlink(link2)
+                os.symlink(self.path, link2)
+            except OSError:
+                pass
 
     def emit(self, record: logging.LogRecord) -> None:
         try:
@@ -160,7 +169,7 @@ def parse_vmodule(spec: str) -> List[Tuple[str, int]]:
 
 def setup(verbosity: int = 0, json_format: bool = False, stderr_threshold: str = "ERROR",
           logtostderr: bool = True, alsologtostderr: bool = False, log_dir: str = "", vmodule: str = "",
-          log_backtrace_at: str = "", program: Optional[str] = None) -> logging.Logger:
+          log_backtrace_at: str = "", program: Optional[str] = None, log_link: str = "") -> logging.Logger:
     """glog's output rules: -logtostderr sends everything to stderr and writes no
     files; otherwise every severity has its own file under -log_dir (default:
     the temp dir) and records at or above -stderrthreshold (everything with
@@ -184,7 +193,7 @@ def setup(verbosity: int = 0, json_format: bool = False, stderr_threshold: str =
         prog = program or os.path.basename(sys.argv[0] or "mi355x-device-plugin").removesuffix(".py") or "python"
         d = log_dir or os.environ.get("TMPDIR") or "/tmp"
         for sev, level in _SEVERITIES:
-            lg.addHandler(_GlogFileHandler(d, prog, sev, level, fmt))
+            lg.addHandler(_GlogFileHandler(d, prog, sev, level, fmt, log_link))
     if log_backtrace_at:
         # on the handlers: logger filters do not see records of child loggers
         bt = _BacktraceAt(log_backtrace_at)
@@ -199,7 +208,8 @@ def setup_from_flags(ns, program: str) -> logging.Logger:
     """setup() from the glog flags of utils.flags.add_glog_flags (+ -log_format)."""
     return setup(ns.v, json_format=getattr(ns, "log_format", "glog") == "json", stderr_threshold=ns.stderrthreshold,
                  logtostderr=ns.logtostderr, alsologtostderr=ns.alsologtostderr, log_dir=ns.log_dir,
-                 vmodule=ns.vmodule, log_backtrace_at=ns.log_backtrace_at, program=program)
+                 vmodule=ns.vmodule, log_backtrace_at=ns.log_backtrace_at, program=program,
+                 log_link=getattr(ns, "log_link", ""))
 
 
 def get(name: str = "") -> logging.Logger:

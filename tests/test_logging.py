@@ -51,6 +51,23 @@ def test_log_dir_files_per_severity(tmp_path, capsys):
     assert "error-line" in stderr and "warning-line" not in stderr   # -stderrthreshold=ERROR
 
 
+def test_log_link_and_logbuflevel(tmp_path, capsys):
+    """glog_file.go:44-46,133-137: -log_link adds a <prog>.<SEV> link to the full
+    path in another directory; -logbuflevel is accepted (records are never buffered)."""
+    from rocm_k8s_device_plugin_amd.utils import flags as F
+    p = F.GoFlagParser(prog="k8s-device-plugin")
+    F.add_glog_flags(p)
+    ns = p.parse_args(["-logtostderr=false", f"-log_dir={tmp_path / 'logs'}", f"-log_link={tmp_path}",
+                       "-logbuflevel=-1"])
+    assert ns.logbuflevel == -1
+    log.setup_from_flags(ns, "k8s-device-plugin")
+    _emit()
+    target = os.readlink(tmp_path / "logs" / "k8s-device-plugin.INFO")
+    assert os.readlink(tmp_path / "k8s-device-plugin.INFO") == str(tmp_path / "logs" / target)
+    assert "info-line" in (tmp_path / "k8s-device-plugin.INFO").read_text()
+    log.setup(0)
+
+
 def test_alsologtostderr_and_threshold(tmp_path, capsys):
     log.setup(0, logtostderr=False, alsologtostderr=True, log_dir=str(tmp_path), program="p")
     _emit()

@@ -67,7 +67,8 @@ def test_device_plugin_log_files_per_severity(tmp_path):
     kub = gp.GoServer(str(kdir / "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
     p = subprocess.Popen([DP, "-kubelet_dir", str(kdir), "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
                           "-exporter_socket", "", "-logtostderr=false", f"-log_dir={logs}", "-vmodule",
-                          "device_plugin_main=2", "-grpc_watchdog", "0"],
+                          "device_plugin_main=2", "-grpc_watchdog", "0", f"-log_link={tmp_path}",
+                          "-logbuflevel=-1"],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     try:
         assert _wait(lambda: (logs / "k8s-device-plugin.INFO").exists() and
@@ -90,6 +91,8 @@ def test_device_plugin_log_files_per_severity(tmp_path):
     target = os.readlink(logs / "k8s-device-plugin.INFO")
     assert target.startswith("k8s-device-plugin.") and ".log.INFO." in target and target.endswith(f".{p.pid}")
     assert info.startswith("Log file created at:") and "Log line format: [IWEF]mmdd" in info
+    # -log_link: a second link, to the full path (glog_file.go:133-137); -logbuflevel accepted
+    assert os.readlink(tmp_path / "k8s-device-plugin.INFO") == str(logs / target)
     assert "Found 8 AMDGPUs" in info and "Received signal, shutting down." in info
     assert "Found 8 AMDGPUs" not in err                     # INFO stays out of stderr (-stderrthreshold=ERROR)
     assert not (logs / "k8s-device-plugin.ERROR").exists()  # created on first use only
