@@ -258,6 +258,9 @@ class Engine {
   uint64_t version_ = 0;
 };
 
+// bdf -> healthy from a metricssvc GPUStateResponse body ({} and *error when malformed)
+std::map<std::string, bool> parse_exporter_states(const std::string& body, std::string* error = nullptr);
+
 // bdf -> healthy from metricssvc.MetricsService/List on `socket` ({} when
 // unavailable); `abort_fd` ends the wait early.
 std::map<std::string, bool> exporter_list(const std::string& socket, double timeout_s, int abort_fd = -1,

@@ -20,6 +20,7 @@
 #include <cstring>
 
 #include "../kube/json.h"
+#include "mi355x/dp_service.h"
 #include "mi355x/glog.h"
 #include "mi355x/metrics.h"
 #include "mi355x/trace.h"
@@ -606,6 +607,35 @@ std::map<int, ProbeOutcome> LivenessProber::probe(const std::vector<int>& ordina
 }
 
 // =============================================================== helpers
+// GPUStateResponse{GPUState=1: GPUState{ID=1, UUID=2, Health=3, AssociatedWorkload=4, Device=5}}
+// (internal/pkg/exporter/metricssvc/metricssvc.pb.go:95-110,284-291), decoded
+// strictly as protobuf does: a malformed message is an error, not a partial map
+std::map<std::string, bool> parse_exporter_states(const std::string& body, std::string* error) {
+  std::map<std::string, bool> out;
+  const bool ok = rpc::pb::scan(
+      body.data(), body.size(),
+      [&](int f, const char* p, size_t n) {
+        if (f != 1) return true;
+        std::string health, device;
+        const bool inner = rpc::pb::scan(
+            p, n,
+            [&](int g, const char* q, size_t m) {
+              if (g == 3) health.assign(q, m);
+              else if (g == 5) device.assign(q, m);
+              return true;
+            },
+            nullptr);
+        if (inner && !device.empty()) out[device] = to_lower(trim(health)) == "healthy";
+        return inner;
+      },
+      nullptr);
+  if (!ok) {
+    if (error) *error = "malformed GPUStateResponse from the metrics exporter";
+    return {};
+  }
+  return out;
+}
+
 std::map<std::string, bool> exporter_list(const std::string& socket, double timeout_s, int abort_fd,
                                           std::string* error) {
   std::map<std::string, bool> out;
@@ -622,53 +652,7 @@ std::map<std::string, bool> exporter_list(const std::string& socket, double time
     if (error) *error = rep.message;
     return out;
   }
-  // GPUStateResponse{GPUState=1: GPUState{ID=1, UUID=2, Health=3, AssociatedWorkload=4, Device=5}}
-  auto fields = [](const std::string& msg, auto&& fn) {
-    size_t i = 0;
-    while (i < msg.size()) {
-      uint64_t key = 0;
-      int shift = 0;
-      while (i < msg.size()) {
-        const uint8_t b = static_cast<uint8_t>(msg[i++]);
-        key |= static_cast<uint64_t>(b & 0x7F) << shift;
-        shift += 7;
-        if (!(b & 0x80)) break;
-      }
-      const int field = static_cast<int>(key >> 3), wt = static_cast<int>(key & 7);
-      if (wt == 2) {
-        uint64_t len = 0;
-        shift = 0;
-        while (i < msg.size()) {
-          const uint8_t b = static_cast<uint8_t>(msg[i++]);
-          len |= static_cast<uint64_t>(b & 0x7F) << shift;
-          shift += 7;
-          if (!(b & 0x80)) break;
-        }
-        if (len > msg.size() - i) return;
-        fn(field, msg.substr(i, len));
-        i += len;
-      } else if (wt == 0) {
-        while (i < msg.size() && (static_cast<uint8_t>(msg[i++]) & 0x80)) {
-        }
-      } else if (wt == 1) {
-        i += 8;
-      } else if (wt == 5) {
-        i += 4;
-      } else {
-        return;
-      }
-    }
-  };
-  fields(rep.body, [&](int f, const std::string& gpu) {
-    if (f != 1) return;
-    std::string health, device;
-    fields(gpu, [&](int g, const std::string& v) {
-      if (g == 3) health = v;
-      if (g == 5) device = v;
-    });
-    if (!device.empty()) out[device] = to_lower(trim(health)) == "healthy";
-  });
-  return out;
+  return parse_exporter_states(rep.body, error);
 }
 
 std::map<std::string, int> hip_ordinals(const std::vector<GpuDevice>& devices, const KfdTopology& topo,

@@ -36,7 +36,8 @@ NATIVE = REPO / "native"
 BUILD = REPO / "build" / "native-fuzz"            # coverage + ASan
 BUILD_REPLAY = REPO / "build" / "native-fuzz-replay"  # ASan + full UBSan, runs the corpus once
 BUILD_TSAN = REPO / "build" / "native-fuzz-tsan"      # TSan, runs the corpus of the threaded targets once
-TARGETS = ("hpack", "json", "yaml", "sysfs", "labels", "h2_server", "h2_client", "dp_rpc", "http_client")
+TARGETS = ("hpack", "json", "yaml", "sysfs", "labels", "exporter", "h2_server", "h2_client", "dp_rpc",
+           "http_client")
 # targets whose code under test runs on more than one thread (the server's I/O thread, the HTTP peer thread)
 TSAN_TARGETS = ("h2_server", "dp_rpc", "h2_client", "http_client")
 CLANG = Path("/opt/rocm/lib/llvm/bin/clang++")
@@ -148,6 +149,12 @@ def make_seeds(work: Path, env: Dict[str, str]) -> Dict[str, Path]:
 
     seeds["sysfs"] += [b"", bytes([0, 0, 5, 0]) + b"bad\n\n", bytes([7, 0, 0xFF, 0xFF]),
                        bytes([40, 0, 12, 0]) + b"node_to 999\n"]
+    from rocm_k8s_device_plugin_amd.proto import metricssvc as ms
+    states = ms.GPUStateResponse()
+    for i, bdf in enumerate(sorted({d.id[:12] for d in discover(env["MI355X_FUZZ_SYSFS"]).devices})):
+        states.GPUState.add(ID=str(i), UUID=f"u{i}", Health="healthy" if i % 3 else "Unhealthy", Device=bdf,
+                            AssociatedWorkload=["pod-a"])
+    seeds["exporter"] += [states.SerializeToString(), b"", b"\x0a\x02\x2a\x00"]
     seeds["labels"] += seeds["sysfs"] + [bytes([0x60, 0, 20, 0]) + b"AMD Instinct (x) /?\n"]
 
     gpa = pb.PreferredAllocationRequest(container_requests=[pb.ContainerPreferredAllocationRequest(
