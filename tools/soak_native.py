@@ -6,6 +6,11 @@ The daemon registers at a fake kubelet over UDS on the node's own /sys, with a
 1..N over the native gRPC server) run back to back with no pause. Every
 --report seconds one JSON line: admissions, errors, RPC latency percentiles,
 and what would leak if anything did: the daemon's RSS, open fds and threads.
+With --container-interval S, every S seconds one admission's container is
+started for real (container_runtime.start_container: a fresh process whose
+/dev is the Allocate DeviceSpecs runs the MFMA kernel), on the GPU the
+daemon's liveness loop is probing: containers must all come up, and the
+device must stay Healthy in ListAndWatch.
 
   python tools/soak_native.py --seconds 120 --out gpurun_out/soak_native.json
 """
@@ -58,6 +63,24 @@ def pct(xs, q):
     return round(xs[min(len(xs) - 1, int(q * len(xs)))], 4) if xs else None
 
 
+async def run_container(adm, minor_to_ord: dict, cont: dict) -> None:
+    """The admitted pod's container, for real (blocking; the kfd teardown of the
+    previous one is waited out first, as kubelet does before reusing devices)."""
+    from rocm_k8s_device_plugin_amd.container_runtime import (render_minors_from_specs, start_container,
+                                                              wait_kfd_released)
+    car = adm.response.container_responses[0]
+    ordl = [minor_to_ord[m] for m in render_minors_from_specs(car)]
+    paths = ["/dev/kfd"] + [d.host_path for d in car.devices if d.host_path.startswith("/dev/dri/")]
+    res = await asyncio.to_thread(start_container, ordl, 60.0, device_paths=paths)
+    cont["started"] += 1
+    if res.ok:
+        cont["ready_ms"].append((res.t_ready_ns - res.t_start_ns) / 1e6)
+    else:
+        cont["failed"] += 1
+        cont["errors"].append(res.error[:200])
+    await asyncio.to_thread(wait_kfd_released, res.kfd_lingering, 1.0)
+
+
 async def main(a) -> int:
     kdir = tempfile.mkdtemp(prefix="soak-native-")
     k = FakeKubelet(kdir)
@@ -80,14 +103,27 @@ async def main(a) -> int:
         adm = errors = 0
         lat = []
         first = proc_stats(proc.pid)
+        cont = {"started": 0, "failed": 0, "ready_ms": [], "errors": [], "unhealthy_seen": 0}
+        minor_to_ord = {}
+        if a.container_interval > 0:
+            from rocm_k8s_device_plugin_amd.topology import discover, hip_ordinals
+            inv = discover(a.sysfs_root)
+            ords = hip_ordinals(inv, "/dev", check_access=True)
+            minor_to_ord = {dv.render_minor: ords[dv.id] for dv in inv.devices if dv.id in ords}
+        next_container = time.monotonic() + (a.container_interval if a.container_interval > 0 else 1e18)
         while time.monotonic() < t_end:
             healthy = len(k.healthy_free("amd.com/gpu")) + 0
             size = adm % max(1, min(n, healthy)) + 1
             try:
-                r = await k.admit("amd.com/gpu", size)
+                r = await k.admit("amd.com/gpu", 1 if time.monotonic() >= next_container else size)
                 lat.append(r.total_ms)
-                k.release("amd.com/gpu", r.device_ids)
                 adm += 1
+                if time.monotonic() >= next_container:
+                    next_container = time.monotonic() + a.container_interval
+                    await run_container(r, minor_to_ord, cont)
+                    unhealthy = [d for d, h in k.resources["amd.com/gpu"].devices.items() if h != "Healthy"]
+                    cont["unhealthy_seen"] += any(d in r.device_ids for d in unhealthy)
+                k.release("amd.com/gpu", r.device_ids)
             except Exception as e:  # noqa: BLE001
                 errors += 1
                 print(f"admission error: {e}", file=sys.stderr)
@@ -96,6 +132,11 @@ async def main(a) -> int:
                 row = {"t_s": round(a.seconds - (t_end - time.monotonic()), 1), "admissions": adm, "errors": errors,
                        "rpc_ms_p50": pct(lat, 0.5), "rpc_ms_p99": pct(lat, 0.99), **proc_stats(proc.pid),
                        "children": [proc_stats(c) for c in children(proc.pid)]}
+                if a.container_interval > 0:
+                    row["containers"] = {"started": cont["started"], "failed": cont["failed"],
+                                         "ready_ms_p50": pct(cont["ready_ms"], 0.5),
+                                         "ready_ms_p99": pct(cont["ready_ms"], 0.99),
+                                         "device_unhealthy_after": cont["unhealthy_seen"]}
                 rows.append(row)
                 print(json.dumps(row), flush=True)
                 lat = []
@@ -107,6 +148,11 @@ async def main(a) -> int:
                            if ln and not ln.startswith("#") and "_bucket" not in ln}
         doc = {"exe": "mi355x-device-plugin", "devices": n, "pulse_s": a.pulse, "seconds": a.seconds,
                "flags": extra, "metrics_end": metrics,
+               "containers": ({"interval_s": a.container_interval, "started": cont["started"],
+                               "failed": cont["failed"], "errors": cont["errors"][:5],
+                               "ready_ms_p50": pct(cont["ready_ms"], 0.5), "ready_ms_p99": pct(cont["ready_ms"], 0.99),
+                               "device_unhealthy_after": cont["unhealthy_seen"]}
+                              if a.container_interval > 0 else None),
                "start": first, "reports": rows, "admissions": adm, "errors": errors,
                "listandwatch_updates": k.state("amd.com/gpu").updates if hasattr(k, "state") else None}
     finally:
@@ -124,7 +170,8 @@ async def main(a) -> int:
         with open(a.out, "w") as f:
             json.dump(doc, f, indent=1)
     print(json.dumps({k_: doc[k_] for k_ in ("admissions", "errors", "exit_code")}))
-    return 0 if doc["errors"] == 0 and doc["exit_code"] == 0 else 1
+    bad_containers = doc["containers"] and (doc["containers"]["failed"] or doc["containers"]["device_unhealthy_after"])
+    return 0 if doc["errors"] == 0 and doc["exit_code"] == 0 and not bad_containers else 1
 
 
 if __name__ == "__main__":
@@ -136,4 +183,6 @@ if __name__ == "__main__":
     ap.add_argument("--out", default="")
     ap.add_argument("--extra", default="", help="more daemon flags, space-separated")
     ap.add_argument("--metrics-port", type=int, default=0)
+    ap.add_argument("--container-interval", type=float, default=0.0,
+                    help="every S seconds start one admission's container on the GPU (0 = never)")
     sys.exit(asyncio.run(main(ap.parse_args())))
