@@ -314,7 +314,10 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
     from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
     from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
 
-    exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    # MI355X_NATIVE_DAEMON_EXE: the same test against another build (e.g. ASan/UBSan, host code only);
+    # the probe server is always this tree's gfx950 build
+    exe = os.environ.get("MI355X_NATIVE_DAEMON_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    probe = os.path.join(str(PKG_DIR), "bin", "mi355x-liveness-probe")
     dev_id, o = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
     fault = tmp_path / "corrupt"
     fault.write_text("")
@@ -349,7 +352,8 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
         await k.start()
         env = dict(os.environ, MI355X_PROBE_CORRUPT_FILE=str(fault))
         proc = await asyncio.create_subprocess_exec(
-            exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_timeout", "30",
+            exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_probe", probe,
+            "-liveness_timeout", "30",
             "-liveness_fail_threshold", "2", "-metrics_port", str(port), "-device_list_strategy",
             "device-specs,cdi-cri", "-cdi_spec_dir", str(tmp_path / "cdi"), stdout=asyncio.subprocess.DEVNULL,
             stderr=asyncio.subprocess.PIPE, env=env)
@@ -382,6 +386,7 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
             await k.stop()
         err = err.decode(errors="replace")
         assert proc.returncode == 0, err[-3000:]
+        assert "ERROR: AddressSanitizer" not in err and "runtime error:" not in err, err[-3000:]
         assert f"device {dev_id}: Healthy -> Unhealthy liveness probe:" in err and "differ" in err, err[-3000:]
         return err
 
@@ -419,7 +424,10 @@ def test_native_daemon_chip_sweep_and_throughput_check(inv, ordinals, tmp_path):
     from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
     from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
 
-    exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    # MI355X_NATIVE_DAEMON_EXE: the same test against another build (e.g. ASan/UBSan, host code only);
+    # the probe server is always this tree's gfx950 build
+    exe = os.environ.get("MI355X_NATIVE_DAEMON_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    probe = os.path.join(str(PKG_DIR), "bin", "mi355x-liveness-probe")
     dev_id = sorted(ordinals.items(), key=lambda kv: kv[1])[0][0]
     gpu_id = inv.topology.node(inv.by_id[dev_id].node_id).gpu_id
     kdir = str(tmp_path / "dp")
@@ -440,7 +448,8 @@ def test_native_daemon_chip_sweep_and_throughput_check(inv, ordinals, tmp_path):
         k = FakeKubelet(kdir)
         await k.start()
         proc = await asyncio.create_subprocess_exec(
-            exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_timeout", "30",
+            exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_probe", probe,
+            "-liveness_timeout", "30",
             "-liveness_chip_sweep_every", "2", "-perf_check_every", "3", "-perf_mib", "1024",
             "-metrics_port", str(port), stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
         try:
@@ -471,7 +480,9 @@ def test_native_daemon_chip_sweep_and_throughput_check(inv, ordinals, tmp_path):
                 proc.send_signal(signal.SIGTERM)
             _, err = await asyncio.wait_for(proc.communicate(), 30)
             await k.stop()
-        assert proc.returncode == 0, err.decode(errors="replace")[-3000:]
+        err = err.decode(errors="replace")
+        assert proc.returncode == 0, err[-3000:]
+        assert "ERROR: AddressSanitizer" not in err and "runtime error:" not in err, err[-3000:]
         return m
 
     m = asyncio.run(asyncio.wait_for(go(), 240))

@@ -321,6 +321,7 @@ def test_real_node_labels_equal_the_python_labeller():
     out, err = p.communicate(timeout=120)
     wall_ms = (time.monotonic() - t0) * 1e3
     assert p.returncode == 0, err
+    assert "ERROR: AddressSanitizer" not in err and "runtime error:" not in err, err[-3000:]
     got = json.loads(out)
     want = L.generate_labels({k: True for k in KINDS}, "")
     assert got == want
