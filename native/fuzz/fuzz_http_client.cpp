@@ -36,6 +36,7 @@ Server& server() {
   static Server* s = [] {
     auto* sv = new Server;
     sv->fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (sv->fd < 0) fail("socket");
     const int one = 1;
     ::setsockopt(sv->fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
     sockaddr_in a{};

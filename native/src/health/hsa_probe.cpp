@@ -698,9 +698,8 @@ namespace {
 bool wait_signal(hsa_signal_t sig, double timeout_s) {
   using clk = std::chrono::steady_clock;
   const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
-  hsa_signal_value_t v;
-  while ((v = H().hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
-                                            HSA_WAIT_STATE_BLOCKED)) >= 1) {
+  while (H().hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
+                                       HSA_WAIT_STATE_BLOCKED) >= 1) {
     if (clk::now() > deadline) return false;
   }
   return true;

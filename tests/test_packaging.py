@@ -162,6 +162,11 @@ def test_ci_command_lines_pass_the_real_argument_parsers():
                 _build.make_parser().parse_args(argv[3:])
             elif argv[1] == "bench.py":
                 bench.make_parser().parse_args(argv[2:])
+            elif argv[1] == "tools/analyze_native.py":
+                aspec = importlib.util.spec_from_file_location("analyze_native", REPO / "tools" / "analyze_native.py")
+                anm = importlib.util.module_from_spec(aspec)
+                aspec.loader.exec_module(anm)
+                anm.make_parser().parse_args(argv[2:])
             elif argv[1] == "tools/fuzz_native.py":
                 fspec = importlib.util.spec_from_file_location("fuzz_native", REPO / "tools" / "fuzz_native.py")
                 fzm = importlib.util.module_from_spec(fspec)
