@@ -1074,4 +1074,10 @@ class _ServerConn:
             self._data(sid, grpc_message(resp))
             self._headers(sid, [("grpc-status", "0"), ("grpc-message", "")], True)
         if cfg.graceful_goaway:
-            self.send(frame(GOAWAY, 0, 0, struct.pack(">II", self.last_sid, NO_ERROR)))
+            # A client that saw the first GOAWAY may close as soon as its last
+            # stream ends (RFC 7540 6.8); grpc-go's loopy writer drops the
+            # write error of the final GOAWAY in that case.
+            try:
+                self.send(frame(GOAWAY, 0, 0, struct.pack(">II", self.last_sid, NO_ERROR)))
+            except (BrokenPipeError, ConnectionResetError):
+                raise EOFError("client closed after the drain")
