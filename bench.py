@@ -123,6 +123,10 @@ def make_parser():
     ap.add_argument("--kubelet-client", default="", choices=["", "native", "native-thread", "aio"],
                     help="the fake kubelet's admission RPC client: native (a native HTTP/2 client, like kubelet's "
                          "grpc-go) or aio (grpc.aio in the bench's event loop); default native with the native server")
+    ap.add_argument("--extras-deadline", type=float, default=300.0,
+                    help="seconds after the timed loop for every secondary measurement (comparisons, RCCL, peer "
+                         "probe, throughput check); past it rank 0 prints the headline line with what it has and "
+                         "every rank exits 0, so a hung extra cannot take the measured headline with it (0 = none)")
     ap.add_argument("--json-out", default="")
     return ap
 
@@ -433,6 +437,82 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+class ExtrasGuard:
+    """Bounds the secondary measurements that follow the timed loop.
+
+    Everything after the timed loop (comparison admissions, RCCL collectives,
+    the xGMI peer probe, the throughput check) is context, not the metric, and
+    some of it runs code that can hang on a sick node (an RCCL communicator, a
+    DMA that never completes). The headline is complete when the timed loop
+    ends, so a timer armed there bounds the rest: when it fires, or when a
+    stage raises (its own failure, or a peer rank that already left), rank 0 prints
+    the headline line with ``extra.extras_incomplete`` naming the stage that
+    was running, and every rank leaves with status 0 (``os._exit``: a thread
+    stuck in a collective cannot be joined). Exactly one line is printed
+    whichever path gets there first."""
+
+    def __init__(self, rank: int, deadline_s: float):
+        import threading
+        self.rank, self.deadline_s = rank, deadline_s
+        self.stage = "start"
+        self.fallback = None          # rank 0: (error) -> the headline line without the unfinished extras
+        self._lock = threading.Lock()
+        self._printed = False
+        self._timer = None
+        self._plugins = []            # plugin daemons to SIGKILL when the timer fires (no orphans)
+        if deadline_s > 0:
+            # ranks > 0 leave a little later, so rank 0's line is out first
+            self._timer = threading.Timer(deadline_s + (0 if rank == 0 else 5.0), self._fire)
+            self._timer.daemon = True
+            self._timer.start()
+
+    def enter(self, stage: str) -> None:
+        self.stage = stage
+
+    def kill_on_fire(self, plugin) -> None:
+        self._plugins.append(plugin)
+
+    def emit(self, line: str) -> bool:
+        """Print the JSON line unless the other path already has; True if printed here."""
+        with self._lock:
+            if self._printed:
+                return False
+            self._printed = True
+        os.write(1, (line + "\n").encode())
+        return True
+
+    def _fire(self) -> None:
+        self.abandon(None)
+
+    def abandon(self, error) -> None:
+        """Leave now: rank 0 prints the headline line (unless it already has)
+        with the unfinished stage, plugin daemons are killed, exit status 0.
+        ``error`` is None when the deadline passed, else why the stage failed."""
+        why = (f"exceeded --extras-deadline {self.deadline_s:g}s" if error is None else f"failed: {error}")
+        msg = f"bench: secondary measurements {why} in stage '{self.stage}'"
+        if self.rank == 0 and self.fallback is not None:
+            try:
+                self.emit(self.fallback(error))
+            except Exception as e:  # noqa: BLE001
+                msg += f"; headline line failed: {type(e).__name__}: {e}"
+        for pl in self._plugins:
+            proc = getattr(pl, "proc", None)
+            if proc is not None and proc.poll() is None:
+                try:
+                    proc.kill()
+                except OSError:
+                    pass
+        try:
+            sys.stdout.flush()
+            os.write(2, (msg + "\n").encode())
+        finally:
+            os._exit(0)
+
+    def cancel(self) -> None:
+        if self._timer is not None:
+            self._timer.cancel()
+
+
 def process_gpu_state() -> dict:
     """This process's hold on the GPU right now: a torch HIP context, open
     /dev/kfd and render-node descriptors (a kubelet node has none of these)."""
@@ -661,217 +741,264 @@ def main():
     server_ms = plug.server_ms() if d.rank == 0 else {}
     elapsed = d.max(elapsed)
     rank_gpu_state = d.gather(gpu_state)
-    hip_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
-    other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
-    if n > 1:
-        for _ in range(args.mode_compare):
-            one_step(False, sink=other_mode_lat, mode=other_mode)
-    if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
-        # the plugin returns -node_view mounts (alias = host path: the fake runtime
-        # applies mounts by redirection and cannot add the alias mount)
-        nvplug = None
-        if d.rank == 0:
-            node_dir = os.path.join(sysfs, "devices/system/node")
-            if plugin_kind == "native-daemon":
-                nvplug = make_plugin("device-plugins-node-view", adv, ["-node_view", "-node_view_alias", node_dir])
-            else:
-                from rocm_k8s_device_plugin_amd.node_view import NodeView
-                impl.node_view = NodeView(os.path.join(tmp, "node-view"), sysfs, alias=node_dir)
-                impl.node_view.path()  # built at plugin start-up in a real deployment
-        for _ in range(args.node_view_compare):
-            one_step(False, sink=nv_lat, init_sink=nv_init, pl=nvplug)
-        if d.rank == 0:
-            if nvplug is not None:
-                nvplug.stop()
-            else:
-                impl.node_view = None
-    vis_lat = []
-    other_view = "visible-devices" if args.dev_view == "specs" else "specs"
-    if not args.fixture and args.container_runtime == "hsa":
-        for _ in range(args.visibility_compare):
-            one_step(False, sink=vis_lat, dev_view=other_view)
-    if not args.fixture and args.container_runtime == "hsa":
-        for _ in range(args.hip_compare):
-            one_step(False, runtime="hip", sink=hip_lat)
-    if not args.fixture and args.settle == "kfd":
-        for _ in range(args.b2b_compare):
-            one_step(False, sink=b2b_lat, settle="none")
 
-    # N of every accessible device, from a fragmented availability (second plugin
-    # instance; the headline plugin keeps advertising exactly N)
-    frag = None
-    frag_lat, frag_alloc = [], []
-    do_frag = d.bcast(d.rank == 0 and m_adv == n and args.fragmented_compare > 0 and len(usable) > n)
-    if do_frag:
-        fplug = None
-        if d.rank == 0:
-            fplug = make_plugin("device-plugins-all", usable)
-            fplug.hold(fragment([dv.id for dv in usable], n, args.hold))
-        for _ in range(args.fragmented_compare):
-            one_step(False, sink=frag_lat, pl=fplug, alloc_sink=frag_alloc)
-        if d.rank == 0:
-            frag = {"advertised": len(usable), "requested": n, "held": fplug.held,
-                    "latency_p50_ms": round(pct(frag_lat, .5), 3),
-                    **alloc_summary(fplug, frag_alloc)}
-            fplug.stop()
-
-    rccl = None
-    if args.collectives and d.world > 1:
-        # the pod's GPUs as a torchrun workload sees them: one rank per GPU, RCCL over xGMI
-        from rocm_k8s_device_plugin_amd.parallel import collectives as coll
-        # a secondary measurement: a failure is reported in the JSON line, not
-        # allowed to take the headline down with it
-        try:
-            group, on_gpu = d.rccl_group()   # RCCL is created here, after the timed loop
-            if on_gpu:
-                sizes = args.collective_sizes or "1M,64M,256M"
-                ops, iters, dtype = coll.DEFAULT_OPS, 20, d.torch.bfloat16
-            else:
-                sizes = args.collective_sizes or "64K"
-                ops, iters, dtype = ("all_reduce", "all_gather"), 3, d.torch.float32
-            rows = coll.run([coll.parse_size(x) for x in sizes.split(",") if x], ops, iters=iters, warmup=3,
-                            dtype=dtype, group=group)
-            rccl = coll.summary(rows)
-            rccl["backend"] = d.dist.get_backend(group)
-        except Exception as e:  # noqa: BLE001
-            rccl = {"error": f"{type(e).__name__}: {e}"[:300]}
-
-    extra = {}
+    # the headline is measured: from here on everything is bounded by the guard
+    guard = ExtrasGuard(d.rank, args.extras_deadline)
+    core = {}
     if d.rank == 0:
-        # allocator microbenchmark on the same request (ours vs the reference's ordered BFS)
-        pol = plug.allocator
-        avail = [dv.id for dv in adv]
-        t = time.perf_counter()
-        for _ in range(200):  # both sides called straight into C++ (no trace/stats wrapper)
-            pol.native.allocate(avail, [], n)
-        ours = (time.perf_counter() - t) / 200 * 1e6
-        t = time.perf_counter()
-        for _ in range(20):
-            ref = pol.reference_allocate(avail, [], n)
-        refu = (time.perf_counter() - t) / 20 * 1e6
-        # every smaller request on the same N advertised GPUs (the allocations a
-        # shared node serves): our set search vs the reference's ordered BFS,
-        # both in C++ on the same weights, same chosen set required
-        sweep = {}
-        for k in range(1, n):
-            t = time.perf_counter()
-            for _ in range(50):
-                mine = pol.native.allocate(avail, [], k)
-            mine_us = (time.perf_counter() - t) / 50 * 1e6
-            t = time.perf_counter()
-            for _ in range(3):
-                refk = pol.reference_allocate(avail, [], k)
-            sweep[str(k)] = {"ours_us": round(mine_us, 2), "reference_us": round((time.perf_counter() - t) / 3 * 1e6, 2),
-                             "reference_candidates": refk["candidates"], "ours_candidates": mine["candidates"],
-                             "same_set": sorted(mine["ids"]) == sorted(refk["ids"])}
-        extra = {"plugin_rpc_p50_ms": round(pct(rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rpc_ms, .99), 4),
-                 "plugin": plugin_kind,
-                 "grpc_server": "native" if plugin_kind == "native-daemon" else args.grpc_server,
-                 "kubelet_client": kclient,
-                 # breakdown of plugin_rpc (kubelet's GetPreferredAllocation + Allocate round trips): the
-                 # plugin's own time per RPC, measured inside the native server (empty with -grpc_server aio;
-                 # the daemon's from its per-RPC log records)
-                 "plugin_server_p50_us": {rpc: round(pct(v, .5) * 1e3, 1) for rpc, v in sorted(server_ms.items())
-                                          if rpc in ("GetPreferredAllocation", "Allocate")},
-                 "allocate_rpc_p50_ms": round(pct(alloc_rpc_ms, .5), 4),
-                 "container_start_to_ready_p50_ms": round(pct(ready_ms, .5), 3),
-                 "latency_p99_ms": round(pct(lat_ms, .99), 3), "latency_mean_ms": round(statistics.mean(lat_ms), 3),
-                 "container_runtime": args.container_runtime,
-                 "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
-                 "latency_p99_ms_with_hip_runtime_container": round(pct(hip_lat, .99), 3) if hip_lat else None,
-                 "hip_runtime_container_steps": len(hip_lat),
-                 "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
-                 "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
-                 "container_mode": args.container_mode,
-                 "container_dev_view": args.dev_view,
-                 "health_loop": ({"pulse_s": args.health_pulse, "sweeps": impl.monitor.sweeps,
-                                  "sweep_ms_last": round(impl.monitor.last_sweep_ms, 3),
-                                  "unhealthy": sorted(k for k, v in impl.monitor.snapshot().items()
-                                                      if v.health != "Healthy")}
-                                 if args.health_pulse > 0 and not args.fixture else None),
-                 f"latency_p50_ms_dev_view_{other_view}": round(pct(vis_lat, .5), 3) if vis_lat else None,
-                 f"latency_p50_ms_container_mode_{other_mode}": round(pct(other_mode_lat, .5), 3) if other_mode_lat
-                 else None,
-                 "latency_p50_ms_node_view_emulated": round(pct(nv_lat, .5), 3) if nv_lat else None,
-                 "node_view_emulated_runtime_init_p50_ms": round(pct(nv_init, .5), 3) if nv_init else None,
-                 "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
-                 # per timed step, for tail analysis: latency, ROCr init, settle wait before the next step
-                 "steps_ms": [[round(a, 2), round(b, 2), round(c, 1)] for a, b, c in zip(lat_ms, rt_ms, settle_ms)],
-                 "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
-                                             "gpu_runtime_init": round(pct(rt_ms, .5), 3),
-                                             "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
-                 # every timed step above 1.5 x p50, attributed to the admission phase with the largest excess
-                 "tail_attribution": tail_attribution(lat_ms, {
-                     "plugin_rpc": rpc_ms, "runtime_prep": prespawn_ms, "spawn_to_main": exec_ms,
-                     "gpu_runtime_init": rt_ms, "device_setup_and_mfma": dev_ms}),
-                 # the node under test must look like a kubelet node: no GPU context in the bench /
-                 # plugin process(es) while the timed containers initialise (worst over the timed steps)
-                 "launcher": d.launcher,
-                 "bench_process_gpu": {"ranks": rank_gpu_state,
-                                       "clean": not any(s["torch_cuda_initialized"] or s["kfd_fds"]
-                                                        for s in rank_gpu_state)},
-                 "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
-                 "reference_algorithm_candidates": ref["candidates"], "allocator_sweep": sweep, "gpus": gpu_info}
-        from rocm_k8s_device_plugin_amd.parallel.fabric import Fabric
-        try:
-            extra["fabric"] = Fabric(inv).report([dv.id for dv in adv]).as_dict()
-        except Exception as e:  # noqa: BLE001
-            extra["fabric"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        extra["rccl"] = rccl
-        # the timed admissions' GetPreferredAllocation (with M > N: a real search
-        # over the fragmented availability) and the N-of-all-devices comparison
-        extra["timed_allocation"] = dict({"advertised": m_adv, "requested": n, "held": plug.held},
-                                         **alloc_summary(plug, alloc_steps))
-        extra["fragmented_n_of_m"] = frag
-        if args.throughput_check and not args.fixture:
-            extra["gpu_throughput"] = throughput_check(adv_ordinals)
-        if args.peer_check and not args.fixture:
-            from rocm_k8s_device_plugin_amd.health.peer import probe_peers
+        guard.kill_on_fire(plug)
+        core = {"plugin_rpc_p50_ms": round(pct(rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rpc_ms, .99), 4),
+                "plugin": plugin_kind,
+                "grpc_server": "native" if plugin_kind == "native-daemon" else args.grpc_server,
+                "kubelet_client": kclient,
+                # breakdown of plugin_rpc (kubelet's GetPreferredAllocation + Allocate round trips): the
+                # plugin's own time per RPC, measured inside the native server (empty with -grpc_server aio;
+                # the daemon's from its per-RPC log records)
+                "plugin_server_p50_us": {rpc: round(pct(v, .5) * 1e3, 1) for rpc, v in sorted(server_ms.items())
+                                         if rpc in ("GetPreferredAllocation", "Allocate")},
+                "allocate_rpc_p50_ms": round(pct(alloc_rpc_ms, .5), 4),
+                "container_start_to_ready_p50_ms": round(pct(ready_ms, .5), 3),
+                "latency_p99_ms": round(pct(lat_ms, .99), 3), "latency_mean_ms": round(statistics.mean(lat_ms), 3),
+                "container_runtime": args.container_runtime,
+                "settle": args.settle, "settle_wait_p50_ms": round(pct(settle_ms, .5), 2) if settle_ms else None,
+                "container_mode": args.container_mode,
+                "container_dev_view": args.dev_view,
+                "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
+                # per timed step, for tail analysis: latency, ROCr init, settle wait before the next step
+                "steps_ms": [[round(a, 2), round(b, 2), round(c, 1)] for a, b, c in zip(lat_ms, rt_ms, settle_ms)],
+                "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
+                                            "gpu_runtime_init": round(pct(rt_ms, .5), 3),
+                                            "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
+                # every timed step above 1.5 x p50, attributed to the admission phase with the largest excess
+                "tail_attribution": tail_attribution(lat_ms, {
+                    "plugin_rpc": rpc_ms, "runtime_prep": prespawn_ms, "spawn_to_main": exec_ms,
+                    "gpu_runtime_init": rt_ms, "device_setup_and_mfma": dev_ms}),
+                # the node under test must look like a kubelet node: no GPU context in the bench /
+                # plugin process(es) while the timed containers initialise (worst over the timed steps)
+                "launcher": d.launcher,
+                "bench_process_gpu": {"ranks": rank_gpu_state,
+                                      "clean": not any(s["torch_cuda_initialized"] or s["kfd_fds"]
+                                                       for s in rank_gpu_state)},
+                "gpus": gpu_info}
+        held = list(plug.held)
+
+        def result_line(extra: dict) -> str:
+            return json.dumps({
+                "metric": METRIC,
+                "value": round(pct(lat_ms, .5), 3),
+                "unit": "ms",
+                "n_gpus": n,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 3),
+                "higher_is_better": False,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "fp32",
+                "data": ("synthetic pod specs requesting amd.com/gpu=N; real /sys discovery, fake kubelet over UDS, "
+                         "container = fresh process whose /dev is the Allocate DeviceSpecs running the MFMA liveness "
+                         "kernel" if not args.fixture else
+                         "synthetic 8xMI355X sysfs fixture; stub-probe containers (CPU only)"),
+                "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
+                           "global_batch": n, "seq_len": None,
+                           "parallelism": (f"{m_adv} GPUs advertised, 1 pod requesting {n}, " +
+                                           (f"{len(held)} held by other pods, " if held else "") +
+                                           ("1 container process with all N GPUs" if args.container_mode == "pod"
+                                            else "1 container process per GPU")),
+                           "between_admissions": ("previous pod's kfd teardown complete" if args.settle == "kfd"
+                                                  else "back-to-back"),
+                           "launcher": d.launcher, "plugin": plugin_kind},
+                "extra": extra,
+            })
+
+        def emit(line: str) -> None:
+            if guard.emit(line) and args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+
+        def partial_line(error) -> str:
+            line = result_line(dict(core, extras_incomplete={"deadline_s": args.extras_deadline,
+                                                             "stage": guard.stage, "error": error}))
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+            return line
+
+        guard.fallback = partial_line
+
+    def extras():
+        """The secondary measurements and, on rank 0, the JSON line."""
+        hip_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
+        other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
+        if n > 1:
+            guard.enter("container_mode_compare")
+            for _ in range(args.mode_compare):
+                one_step(False, sink=other_mode_lat, mode=other_mode)
+        if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
+            # the plugin returns -node_view mounts (alias = host path: the fake runtime
+            # applies mounts by redirection and cannot add the alias mount)
+            nvplug = None
+            if d.rank == 0:
+                node_dir = os.path.join(sysfs, "devices/system/node")
+                if plugin_kind == "native-daemon":
+                    nvplug = make_plugin("device-plugins-node-view", adv, ["-node_view", "-node_view_alias", node_dir])
+                else:
+                    from rocm_k8s_device_plugin_amd.node_view import NodeView
+                    impl.node_view = NodeView(os.path.join(tmp, "node-view"), sysfs, alias=node_dir)
+                    impl.node_view.path()  # built at plugin start-up in a real deployment
+            if nvplug is not None:
+                guard.kill_on_fire(nvplug)
+            guard.enter("node_view_compare")
+            for _ in range(args.node_view_compare):
+                one_step(False, sink=nv_lat, init_sink=nv_init, pl=nvplug)
+            if d.rank == 0:
+                if nvplug is not None:
+                    nvplug.stop()
+                else:
+                    impl.node_view = None
+        vis_lat = []
+        other_view = "visible-devices" if args.dev_view == "specs" else "specs"
+        if not args.fixture and args.container_runtime == "hsa":
+            guard.enter("dev_view_compare")
+            for _ in range(args.visibility_compare):
+                one_step(False, sink=vis_lat, dev_view=other_view)
+        if not args.fixture and args.container_runtime == "hsa":
+            guard.enter("hip_runtime_compare")
+            for _ in range(args.hip_compare):
+                one_step(False, runtime="hip", sink=hip_lat)
+        if not args.fixture and args.settle == "kfd":
+            guard.enter("back_to_back_compare")
+            for _ in range(args.b2b_compare):
+                one_step(False, sink=b2b_lat, settle="none")
+
+        # N of every accessible device, from a fragmented availability (second plugin
+        # instance; the headline plugin keeps advertising exactly N)
+        frag = None
+        frag_lat, frag_alloc = [], []
+        do_frag = d.bcast(d.rank == 0 and m_adv == n and args.fragmented_compare > 0 and len(usable) > n)
+        if do_frag:
+            fplug = None
+            if d.rank == 0:
+                fplug = make_plugin("device-plugins-all", usable)
+                fplug.hold(fragment([dv.id for dv in usable], n, args.hold))
+                guard.kill_on_fire(fplug)
+            guard.enter("fragmented_compare")
+            for _ in range(args.fragmented_compare):
+                one_step(False, sink=frag_lat, pl=fplug, alloc_sink=frag_alloc)
+            if d.rank == 0:
+                frag = {"advertised": len(usable), "requested": n, "held": fplug.held,
+                        "latency_p50_ms": round(pct(frag_lat, .5), 3),
+                        **alloc_summary(fplug, frag_alloc)}
+                fplug.stop()
+
+        rccl = None
+        if args.collectives and d.world > 1:
+            # the pod's GPUs as a torchrun workload sees them: one rank per GPU, RCCL over xGMI
+            from rocm_k8s_device_plugin_amd.parallel import collectives as coll
+            # a secondary measurement: a failure is reported in the JSON line, not
+            # allowed to take the headline down with it
+            guard.enter("collectives")
             try:
-                rep = probe_peers(adv_ordinals, nbytes=64 << 20, reps=3, timeout_s=120)
-                extra["peer_probe"] = dict(rep.summary(), wall_ms=round(rep.wall_ms, 1))
+                group, on_gpu = d.rccl_group()   # RCCL is created here, after the timed loop
+                if on_gpu:
+                    sizes = args.collective_sizes or "1M,64M,256M"
+                    ops, iters, dtype = coll.DEFAULT_OPS, 20, d.torch.bfloat16
+                else:
+                    sizes = args.collective_sizes or "64K"
+                    ops, iters, dtype = ("all_reduce", "all_gather"), 3, d.torch.float32
+                rows = coll.run([coll.parse_size(x) for x in sizes.split(",") if x], ops, iters=iters, warmup=3,
+                                dtype=dtype, group=group)
+                rccl = coll.summary(rows)
+                rccl["backend"] = d.dist.get_backend(group)
             except Exception as e:  # noqa: BLE001
-                extra["peer_probe"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        plug.stop()
-        # tasks still parked (watchers, event waits): cancel them before the loop goes
-        rest = [t for t in asyncio.all_tasks(loop) if not t.done()]
-        for t in rest:
-            t.cancel()
-        if rest:
-            loop.run_until_complete(asyncio.gather(*rest, return_exceptions=True))
-        loop.close()
-        out = {
-            "metric": METRIC,
-            "value": round(pct(lat_ms, .5), 3),
-            "unit": "ms",
-            "n_gpus": n,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 3),
-            "higher_is_better": False,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": ("synthetic pod specs requesting amd.com/gpu=N; real /sys discovery, fake kubelet over UDS, "
-                     "container = fresh process whose /dev is the Allocate DeviceSpecs running the MFMA liveness kernel"
-                     if not args.fixture else "synthetic 8xMI355X sysfs fixture; stub-probe containers (CPU only)"),
-            "config": {"model": "example/pod/alexnet-gpu.yaml-style pod, amd.com/gpu=N",
-                       "global_batch": n, "seq_len": None,
-                       "parallelism": (f"{m_adv} GPUs advertised, 1 pod requesting {n}, " +
-                                       (f"{len(plug.held)} held by other pods, " if plug.held else "") +
-                                       ("1 container process with all N GPUs" if args.container_mode == "pod"
-                                        else "1 container process per GPU")),
-                       "between_admissions": ("previous pod's kfd teardown complete" if args.settle == "kfd"
-                                              else "back-to-back"),
-                       "launcher": d.launcher, "plugin": plugin_kind},
-            "extra": extra,
-        }
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+                rccl = {"error": f"{type(e).__name__}: {e}"[:300]}
+
+        extra = {}
+        if d.rank == 0:
+            guard.enter("allocator_microbench")
+            # allocator microbenchmark on the same request (ours vs the reference's ordered BFS)
+            pol = plug.allocator
+            avail = [dv.id for dv in adv]
+            t = time.perf_counter()
+            for _ in range(200):  # both sides called straight into C++ (no trace/stats wrapper)
+                pol.native.allocate(avail, [], n)
+            ours = (time.perf_counter() - t) / 200 * 1e6
+            t = time.perf_counter()
+            for _ in range(20):
+                ref = pol.reference_allocate(avail, [], n)
+            refu = (time.perf_counter() - t) / 20 * 1e6
+            # every smaller request on the same N advertised GPUs (the allocations a
+            # shared node serves): our set search vs the reference's ordered BFS,
+            # both in C++ on the same weights, same chosen set required
+            sweep = {}
+            for k in range(1, n):
+                t = time.perf_counter()
+                for _ in range(50):
+                    mine = pol.native.allocate(avail, [], k)
+                mine_us = (time.perf_counter() - t) / 50 * 1e6
+                t = time.perf_counter()
+                for _ in range(3):
+                    refk = pol.reference_allocate(avail, [], k)
+                sweep[str(k)] = {"ours_us": round(mine_us, 2), "reference_us": round((time.perf_counter() - t) / 3 * 1e6, 2),
+                                 "reference_candidates": refk["candidates"], "ours_candidates": mine["candidates"],
+                                 "same_set": sorted(mine["ids"]) == sorted(refk["ids"])}
+            extra = dict(core, **{
+                "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
+                "latency_p99_ms_with_hip_runtime_container": round(pct(hip_lat, .99), 3) if hip_lat else None,
+                "hip_runtime_container_steps": len(hip_lat),
+                "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
+                "health_loop": ({"pulse_s": args.health_pulse, "sweeps": impl.monitor.sweeps,
+                                 "sweep_ms_last": round(impl.monitor.last_sweep_ms, 3),
+                                 "unhealthy": sorted(k for k, v in impl.monitor.snapshot().items()
+                                                     if v.health != "Healthy")}
+                                if args.health_pulse > 0 and not args.fixture else None),
+                f"latency_p50_ms_dev_view_{other_view}": round(pct(vis_lat, .5), 3) if vis_lat else None,
+                f"latency_p50_ms_container_mode_{other_mode}": round(pct(other_mode_lat, .5), 3) if other_mode_lat
+                else None,
+                "latency_p50_ms_node_view_emulated": round(pct(nv_lat, .5), 3) if nv_lat else None,
+                "node_view_emulated_runtime_init_p50_ms": round(pct(nv_init, .5), 3) if nv_init else None,
+                "allocator_us": round(ours, 2), "reference_algorithm_us": round(refu, 2),
+                "reference_algorithm_candidates": ref["candidates"], "allocator_sweep": sweep})
+            from rocm_k8s_device_plugin_amd.parallel.fabric import Fabric
+            try:
+                extra["fabric"] = Fabric(inv).report([dv.id for dv in adv]).as_dict()
+            except Exception as e:  # noqa: BLE001
+                extra["fabric"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            extra["rccl"] = rccl
+            # the timed admissions' GetPreferredAllocation (with M > N: a real search
+            # over the fragmented availability) and the N-of-all-devices comparison
+            extra["timed_allocation"] = dict({"advertised": m_adv, "requested": n, "held": plug.held},
+                                             **alloc_summary(plug, alloc_steps))
+            extra["fragmented_n_of_m"] = frag
+            if args.throughput_check and not args.fixture:
+                guard.enter("throughput_check")
+                extra["gpu_throughput"] = throughput_check(adv_ordinals)
+            if args.peer_check and not args.fixture:
+                from rocm_k8s_device_plugin_amd.health.peer import probe_peers
+                guard.enter("peer_probe")
+                try:
+                    rep = probe_peers(adv_ordinals, nbytes=64 << 20, reps=3, timeout_s=120)
+                    extra["peer_probe"] = dict(rep.summary(), wall_ms=round(rep.wall_ms, 1))
+                except Exception as e:  # noqa: BLE001
+                    extra["peer_probe"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            guard.enter("plugin_stop")
+            plug.stop()
+            # tasks still parked (watchers, event waits): cancel them before the loop goes
+            rest = [t for t in asyncio.all_tasks(loop) if not t.done()]
+            for t in rest:
+                t.cancel()
+            if rest:
+                loop.run_until_complete(asyncio.gather(*rest, return_exceptions=True))
+            loop.close()
+            emit(result_line(extra))
+
+    try:
+        extras()
+    except (Exception, SystemExit) as e:  # noqa: BLE001
+        # a failed extra (or a peer rank that left) is reported, never fatal to the measured headline
+        guard.abandon(f"{type(e).__name__}: {e}"[:300])
     d.close()
+    guard.cancel()
 
 
 if __name__ == "__main__":

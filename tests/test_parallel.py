@@ -152,3 +152,35 @@ def test_bench_python_plugin_option():
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert d["extra"]["plugin"] == "python" and d["extra"]["plugin_server_p50_us"]
+
+
+def test_bench_extras_deadline_keeps_the_headline():
+    """A secondary measurement that overruns --extras-deadline (standing in for
+    a hung RCCL communicator or DMA on a sick node): rank 0 still prints exactly
+    one headline line, naming the unfinished stage, every rank exits 0 (rank 1
+    sees rank 0 leave mid-collective), and no plugin daemon is left behind."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--fixture", "--steps", "2",
+           "--warmup", "1", "--extras-deadline", "0.5"]
+    proc = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                            start_new_session=True)   # its own process group: whatever it leaves is ours
+    try:
+        out, err = proc.communicate(timeout=300)
+    finally:
+        if proc.poll() is None:
+            os.killpg(proc.pid, 9)
+    assert proc.returncode == 0, err[-2000:]
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0 and d["ms_per_step"] > 0
+    inc = d["extra"]["extras_incomplete"]
+    assert inc["deadline_s"] == 0.5 and inc["stage"] != "start"
+    # the timed loop's own numbers are all there
+    e = d["extra"]
+    assert len(e["steps_ms"]) == 2 and e["bench_process_gpu"]["clean"] and e["plugin"] == "native-daemon"
+    assert "exceeded --extras-deadline" in err
+    ps = subprocess.run(["ps", "-eo", "pgid=,cmd="], capture_output=True, text=True).stdout
+    left = [l for l in ps.splitlines() if l.split(None, 1)[0] == str(proc.pid)]
+    assert not left, left
