@@ -460,6 +460,7 @@ class ExtrasGuard:
         self._printed = False
         self._timer = None
         self._plugins = []            # plugin daemons to SIGKILL when the timer fires (no orphans)
+        self.tmp = None               # rank 0's scratch directory (sockets, logs, fixture tree)
         if deadline_s > 0:
             # ranks > 0 leave a little later, so rank 0's line is out first
             self._timer = threading.Timer(deadline_s + (0 if rank == 0 else 5.0), self._fire)
@@ -502,6 +503,9 @@ class ExtrasGuard:
                     proc.kill()
                 except OSError:
                     pass
+        if self.tmp:
+            import shutil
+            shutil.rmtree(self.tmp, ignore_errors=True)
         try:
             sys.stdout.flush()
             os.write(2, (msg + "\n").encode())
@@ -747,6 +751,7 @@ def main():
     core = {}
     if d.rank == 0:
         guard.kill_on_fire(plug)
+        guard.tmp = tmp
         core = {"plugin_rpc_p50_ms": round(pct(rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rpc_ms, .99), 4),
                 "plugin": plugin_kind,
                 "grpc_server": "native" if plugin_kind == "native-daemon" else args.grpc_server,
@@ -990,6 +995,8 @@ def main():
             if rest:
                 loop.run_until_complete(asyncio.gather(*rest, return_exceptions=True))
             loop.close()
+            import shutil
+            shutil.rmtree(tmp, ignore_errors=True)
             emit(result_line(extra))
 
     try:

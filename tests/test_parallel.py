@@ -3,6 +3,7 @@ import json
 import os
 import socket
 import subprocess
+import time
 import sys
 
 import pytest
@@ -176,11 +177,16 @@ def test_bench_extras_deadline_keeps_the_headline():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0 and d["ms_per_step"] > 0
     inc = d["extra"]["extras_incomplete"]
-    assert inc["deadline_s"] == 0.5 and inc["stage"] != "start"
+    assert inc["deadline_s"] == 0.5 and inc["stage"] and inc["error"] is None
     # the timed loop's own numbers are all there
     e = d["extra"]
     assert len(e["steps_ms"]) == 2 and e["bench_process_gpu"]["clean"] and e["plugin"] == "native-daemon"
     assert "exceeded --extras-deadline" in err
-    ps = subprocess.run(["ps", "-eo", "pgid=,cmd="], capture_output=True, text=True).stdout
-    left = [l for l in ps.splitlines() if l.split(None, 1)[0] == str(proc.pid)]
+    # a SIGKILLed daemon may linger for a moment (or as a zombie if PID 1 does not reap)
+    for _ in range(40):
+        ps = subprocess.run(["ps", "-eo", "pgid=,stat=,cmd="], capture_output=True, text=True).stdout
+        left = [l for l in ps.splitlines() if l.split(None, 2)[0] == str(proc.pid) and not l.split()[1].startswith("Z")]
+        if not left:
+            break
+        time.sleep(0.1)
     assert not left, left
