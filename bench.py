@@ -479,7 +479,9 @@ class ExtrasGuard:
             if self._printed:
                 return False
             self._printed = True
-        os.write(1, (line + "\n").encode())
+        data = memoryview((line + "\n").encode())
+        while data:   # a blocking pipe can still take a large line in parts
+            data = data[os.write(1, data):]
         return True
 
     def _fire(self) -> None:
