@@ -64,10 +64,13 @@ def make_parser():
     ap.add_argument("--fixture", action="store_true",
                     help="CPU-only: synthetic 8x MI355X sysfs, containers are no-op processes")
     ap.add_argument("--container-timeout", type=float, default=120.0)
-    ap.add_argument("--container-runtime", default="hsa", choices=["hsa", "hip"],
-                    help="how the container entrypoint reaches the GPU: ROCr-direct or the HIP runtime")
-    ap.add_argument("--hip-compare", type=int, default=5,
-                    help="extra untimed admissions with HIP-runtime containers, reported for comparison")
+    ap.add_argument("--container-runtime", default="hip", choices=["hip", "hsa"],
+                    help="how the container entrypoint reaches the GPU: hip = a HIP program (BASELINE.md: the "
+                         "container finishes HIP init and one MFMA liveness kernel; the headline), hsa = the "
+                         "same kernel launched through ROCr directly (no libamdhip64, no HIP device set-up)")
+    ap.add_argument("--runtime-compare", type=int, default=-1,
+                    help="admissions with the other --container-runtime after the timed loop, reported for "
+                         "comparison (-1 = as many as --steps; 0 = off)")
     ap.add_argument("--settle", default="kfd", choices=["kfd", "none"],
                     help="between admissions wait until the previous containers' kfd processes are torn down "
                          "(the previous pod has terminated) or start the next one immediately")
@@ -202,7 +205,8 @@ class NativePluginUnderTest:
     Its per-RPC records (-log_format json -v 2: server-side latency, the
     allocator's candidates / short-circuit) are read from its stderr."""
 
-    def __init__(self, loop, tmp, name, sysfs, devroot, devs, full, ords, kubelet_client="native", extra=()):
+    def __init__(self, loop, tmp, name, sysfs, devroot, devs, full, ords, kubelet_client="native", extra=(),
+                 metrics_port=0):
         import subprocess
         import threading
         from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
@@ -218,6 +222,9 @@ class NativePluginUnderTest:
         self._allocates_seen = 0
         self._allocates_made = 0
         exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+        self.metrics_port = metrics_port
+        if metrics_port:
+            extra = (*extra, "-metrics_port", str(metrics_port))
         self.proc = subprocess.Popen(
             [exe, "-kubelet_dir", pdir, "-sysfs_root", sysfs, "-dev_root", devroot, "-exporter_socket", "",
              "-device_ids", ",".join(dv.id for dv in self.devs), "-log_format", "json", "-v", "2", *extra],
@@ -279,6 +286,34 @@ class NativePluginUnderTest:
 
     def available(self):
         return self.kubelet.healthy_free("amd.com/gpu")
+
+    def metrics(self) -> dict:
+        """The daemon's /metrics as {series name (with labels): value}."""
+        import urllib.request
+        if not self.metrics_port:
+            return {}
+        with urllib.request.urlopen(f"http://127.0.0.1:{self.metrics_port}/metrics", timeout=5) as r:
+            text = r.read().decode()
+        out = {}
+        for line in text.splitlines():
+            if line and not line.startswith("#"):
+                k, _, v = line.rpartition(" ")
+                try:
+                    out[k] = float(v)
+                except ValueError:
+                    pass
+        return out
+
+    def health_report(self, pulse_s) -> dict:
+        """The health DaemonSet loop as the daemon reports it (/metrics) and as
+        kubelet sees it (the ListAndWatch device table)."""
+        m = self.metrics()
+        n = int(m.get("mi355x_dp_health_sweep_seconds_count", 0))
+        st = self.kubelet.resources.get("amd.com/gpu")
+        return {"plugin": "native-daemon", "pulse_s": pulse_s, "sweeps": n,
+                "sweep_ms_mean": round(m.get("mi355x_dp_health_sweep_seconds_sum", 0.0) * 1e3 / n, 3) if n else None,
+                "health_changes": int(m.get("mi355x_dp_health_changes_total", 0)),
+                "unhealthy": sorted(d for d, h in (st.devices.items() if st else ()) if h != "Healthy")}
 
     def stop(self):
         import signal
@@ -347,6 +382,13 @@ class PluginUnderTest:
         self.loop.run_until_complete(self.kubelet.stop())
         self.mgr.request_stop()
         self.loop.run_until_complete(self.task)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def throughput_check(ordinals) -> dict:
@@ -458,6 +500,7 @@ class ExtrasGuard:
         self.fallback = None          # rank 0: (error) -> the headline line without the unfinished extras
         self._lock = threading.Lock()
         self._printed = False
+        self._written = threading.Event()   # the printed line (and --json-out) is complete
         self._timer = None
         self._plugins = []            # plugin daemons to SIGKILL when the timer fires (no orphans)
         self.tmp = None               # rank 0's scratch directory (sockets, logs, fixture tree)
@@ -473,15 +516,23 @@ class ExtrasGuard:
     def kill_on_fire(self, plugin) -> None:
         self._plugins.append(plugin)
 
-    def emit(self, line: str) -> bool:
-        """Print the JSON line unless the other path already has; True if printed here."""
+    def emit(self, line: str, json_out: str = "") -> bool:
+        """Print the JSON line (and write it to ``json_out``) unless the other
+        path already has; True if written here. Whoever wins writes both, so
+        stdout and --json-out always carry the same line."""
         with self._lock:
             if self._printed:
                 return False
             self._printed = True
-        data = memoryview((line + "\n").encode())
-        while data:   # a blocking pipe can still take a large line in parts
-            data = data[os.write(1, data):]
+        try:
+            data = memoryview((line + "\n").encode())
+            while data:   # a blocking pipe can still take a large line in parts
+                data = data[os.write(1, data):]
+            if json_out:
+                with open(json_out, "w") as f:
+                    f.write(line + "\n")
+        finally:
+            self._written.set()
         return True
 
     def _fire(self) -> None:
@@ -494,10 +545,17 @@ class ExtrasGuard:
         why = (f"exceeded --extras-deadline {self.deadline_s:g}s" if error is None else f"failed: {error}")
         msg = f"bench: secondary measurements {why} in stage '{self.stage}'"
         if self.rank == 0 and self.fallback is not None:
-            try:
-                self.emit(self.fallback(error))
-            except Exception as e:  # noqa: BLE001
-                msg += f"; headline line failed: {type(e).__name__}: {e}"
+            with self._lock:
+                printed = self._printed
+            if printed:
+                # the full line is out or being written by the main thread: let it finish
+                self._written.wait(10.0)
+                msg = f"bench: {why} in stage '{self.stage}' after the headline line was written"
+            else:
+                try:
+                    self.emit(*self.fallback(error))
+                except Exception as e:  # noqa: BLE001
+                    msg += f"; headline line failed: {type(e).__name__}: {e}"
         for pl in self._plugins:
             proc = getattr(pl, "proc", None)
             if proc is not None and proc.poll() is None:
@@ -579,6 +637,7 @@ def main():
 
     loop = None
     plug = impl = None
+    plugin_kind = None
     tmp = None
     m_adv = args.advertise or n
     if m_adv < n:
@@ -608,13 +667,21 @@ def main():
         hcfg = (HealthConfig(exporter_socket=None, liveness=True, smi_ecc=True, smi_events=True, smi_xgmi=True)
                 if hp > 0 else HealthConfig(exporter_socket=None))
         loop = asyncio.new_event_loop()
-        # the health DaemonSet variant (--health-pulse, sub-second pulses) runs on the Python plugin
-        plugin_kind = "native-daemon" if args.plugin == "native" and hp == 0 else "python"
+        plugin_kind = "native-daemon" if args.plugin == "native" else "python"
+        # the health DaemonSet variant (k8s-ds-amdgpu-dp-health.yaml: -pulse=2 plus the MFMA liveness
+        # probe server and amd-smi ECC / events / xGMI) on the daemon; -pulse is whole seconds
+        health_flags = ()
+        if hp > 0 and plugin_kind == "native-daemon":
+            health_flags = ("-pulse", str(max(1, int(round(hp)))), "-liveness", "-smi_ecc", "-smi_events",
+                            "-smi_xgmi")
 
         def make_plugin(name, devs, extra=()):
             if plugin_kind == "native-daemon":
+                main_plugin = name == "device-plugins"
                 return NativePluginUnderTest(loop, tmp, name, sysfs, devroot, devs, full, ords,
-                                             kubelet_client=kclient, extra=extra)
+                                             kubelet_client=kclient,
+                                             extra=(*extra, *(health_flags if main_plugin else ())),
+                                             metrics_port=free_port() if main_plugin and health_flags else 0)
             return PluginUnderTest(loop, tmp, name, sysfs, devs, full, ords,
                                    hcfg if name == "device-plugins" else HealthConfig(exporter_socket=None),
                                    hp if name == "device-plugins" else 0.0, grpc_server=args.grpc_server,
@@ -635,14 +702,14 @@ def main():
         gpu_info = None
 
     rpc_ms, alloc_rpc_ms, lat_ms, ready_ms, kern_us = [], [], [], [], []
-    exec_ms, rt_ms, dev_ms, settle_ms, prespawn_ms = [], [], [], [], []
+    exec_ms, rt_ms, dev_ms, settle_ms, prespawn_ms, setup_ms, launch_ms = [], [], [], [], [], [], []
     gpu_state = {"torch_cuda_initialized": False, "kfd_fds": 0, "render_fds": 0}   # worst seen in the timed loop
     from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
 
     def blocking(fn, *a, **kw):
         """Run fn; with the health loop on, on a worker thread while rank 0's
         event loop keeps sweeping (so sweeps overlap the container start)."""
-        if loop is not None and args.health_pulse > 0 and not args.fixture:
+        if loop is not None and args.health_pulse > 0 and not args.fixture and plugin_kind == "python":
             import functools
             return loop.run_until_complete(asyncio.to_thread(functools.partial(fn, *a, **kw)))
         return fn(*a, **kw)
@@ -670,7 +737,7 @@ def main():
         t0, ordl, tot, amsl, ids, mounts, groups = payload
         if mode == "pod" and d.rank != 0:
             # the pod's single container runs on rank 0; other ranks only keep step
-            mine = (True, 0, 0.0, "", (0, 0, 0))
+            mine = (True, 0, 0.0, "", (0, 0, 0, 0.0))
             lingering = frozenset()
         else:
             pod = mode == "pod" or d.world == 1
@@ -684,7 +751,9 @@ def main():
             r = blocking(start_container, mine_ord, timeout_s=args.container_timeout, runtime=runtime,
                          mounts=mounts if not args.fixture else (), device_paths=paths, **stub)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
-            phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)))
+            # device set-up (HIP: hipSetDevice .. stream/buffers/events; HSA: queue, code object, buffers)
+            sus = max((dv.get("setup_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
+            phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)), sus / 1e3)
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
             lingering = r.kfd_lingering
         if record:   # the containers are up: does the bench / plugin process hold the GPU?
@@ -718,7 +787,7 @@ def main():
         waited = blocking(wait_kfd_released, lingering, timeout_s=cap) if settle == "kfd" else 0.0
         if record:
             settle_ms.append(waited)
-        sp, tm, trt = slowest[4]   # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC)
+        sp, tm, trt, su = slowest[4]   # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC), device set-up ms
         if sink is not None:
             sink.append((t_ready - t0) / 1e6)
         if init_sink is not None:
@@ -732,6 +801,8 @@ def main():
             exec_ms.append((tm - sp) / 1e6)
             rt_ms.append((trt - tm) / 1e6)
             dev_ms.append((t_ready - trt) / 1e6)
+            setup_ms.append(min(su, (t_ready - trt) / 1e6))
+            launch_ms.append(max(0.0, (t_ready - trt) / 1e6 - su))
             prespawn_ms.append(max(0.0, (sp - t0) / 1e6 - tot))
 
     for _ in range(args.warmup):
@@ -773,13 +844,18 @@ def main():
                 "mfma_kernel_us_p50": round(pct(kern_us, .5), 2),
                 # per timed step, for tail analysis: latency, ROCr init, settle wait before the next step
                 "steps_ms": [[round(a, 2), round(b, 2), round(c, 1)] for a, b, c in zip(lat_ms, rt_ms, settle_ms)],
-                "container_phases_p50_ms": {"spawn_to_main": round(pct(exec_ms, .5), 3),
+                # exec_and_library_load: fork/exec + the dynamic loader (HIP: libamdhip64 and its
+                # constructors, before main); gpu_runtime_init: hipGetDeviceCount (hipInit, ROCr start-up;
+                # HSA: hsa_init); device_setup: hipSetDevice .. stream, buffers, events (HSA: queue, code
+                # object, buffers); launch_and_verify: first launch to the verified MFMA tile
+                "container_phases_p50_ms": {"exec_and_library_load": round(pct(exec_ms, .5), 3),
                                             "gpu_runtime_init": round(pct(rt_ms, .5), 3),
-                                            "device_setup_and_mfma": round(pct(dev_ms, .5), 3)},
+                                            "device_setup": round(pct(setup_ms, .5), 3),
+                                            "launch_and_verify": round(pct(launch_ms, .5), 3)},
                 # every timed step above 1.5 x p50, attributed to the admission phase with the largest excess
                 "tail_attribution": tail_attribution(lat_ms, {
-                    "plugin_rpc": rpc_ms, "runtime_prep": prespawn_ms, "spawn_to_main": exec_ms,
-                    "gpu_runtime_init": rt_ms, "device_setup_and_mfma": dev_ms}),
+                    "plugin_rpc": rpc_ms, "runtime_prep": prespawn_ms, "exec_and_library_load": exec_ms,
+                    "gpu_runtime_init": rt_ms, "device_setup": setup_ms, "launch_and_verify": launch_ms}),
                 # the node under test must look like a kubelet node: no GPU context in the bench /
                 # plugin process(es) while the timed containers initialise (worst over the timed steps)
                 "launcher": d.launcher,
@@ -819,29 +895,29 @@ def main():
             })
 
         def emit(line: str) -> None:
-            if guard.emit(line) and args.json_out:
-                with open(args.json_out, "w") as f:
-                    f.write(line + "\n")
+            guard.emit(line, args.json_out)
 
-        def partial_line(error) -> str:
-            line = result_line(dict(core, extras_incomplete={"deadline_s": args.extras_deadline,
-                                                             "stage": guard.stage, "error": error}))
-            if args.json_out:
-                with open(args.json_out, "w") as f:
-                    f.write(line + "\n")
-            return line
+        def partial_line(error):
+            """(line, json_out) for the guard: the headline without the unfinished extras."""
+            return (result_line(dict(core, extras_incomplete={"deadline_s": args.extras_deadline,
+                                                              "stage": guard.stage, "error": error})),
+                    args.json_out)
 
         guard.fallback = partial_line
 
+    other_runtime = "hsa" if args.container_runtime == "hip" else "hip"
+    rt_key = "rocr_direct_container" if other_runtime == "hsa" else "hip_runtime_container"
+    rt_compare_steps = args.steps if args.runtime_compare < 0 else args.runtime_compare
+
     def extras():
         """The secondary measurements and, on rank 0, the JSON line."""
-        hip_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
+        rt_lat, b2b_lat, nv_lat, nv_init, other_mode_lat = [], [], [], [], []
         other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
         if n > 1:
             guard.enter("container_mode_compare")
             for _ in range(args.mode_compare):
                 one_step(False, sink=other_mode_lat, mode=other_mode)
-        if not args.fixture and args.container_runtime == "hsa" and args.node_view_compare > 0:
+        if not args.fixture and args.node_view_compare > 0:
             # the plugin returns -node_view mounts (alias = host path: the fake runtime
             # applies mounts by redirection and cannot add the alias mount)
             nvplug = None
@@ -865,14 +941,15 @@ def main():
                     impl.node_view = None
         vis_lat = []
         other_view = "visible-devices" if args.dev_view == "specs" else "specs"
-        if not args.fixture and args.container_runtime == "hsa":
+        if not args.fixture:
             guard.enter("dev_view_compare")
             for _ in range(args.visibility_compare):
                 one_step(False, sink=vis_lat, dev_view=other_view)
-        if not args.fixture and args.container_runtime == "hsa":
-            guard.enter("hip_runtime_compare")
-            for _ in range(args.hip_compare):
-                one_step(False, runtime="hip", sink=hip_lat)
+        if not args.fixture and rt_compare_steps > 0:
+            # the other entrypoint, as many admissions as the headline (same settle, same view)
+            guard.enter(f"{other_runtime}_runtime_compare")
+            for _ in range(rt_compare_steps):
+                one_step(False, runtime=other_runtime, sink=rt_lat)
         if not args.fixture and args.settle == "kfd":
             guard.enter("back_to_back_compare")
             for _ in range(args.b2b_compare):
@@ -920,6 +997,15 @@ def main():
             except Exception as e:  # noqa: BLE001
                 rccl = {"error": f"{type(e).__name__}: {e}"[:300]}
 
+        def health_loop_report():
+            if args.health_pulse <= 0 or args.fixture:
+                return None
+            if plugin_kind == "native-daemon":
+                return plug.health_report(float(health_flags[1]))
+            return {"plugin": "python", "pulse_s": args.health_pulse, "sweeps": impl.monitor.sweeps,
+                    "sweep_ms_last": round(impl.monitor.last_sweep_ms, 3),
+                    "unhealthy": sorted(k for k, v in impl.monitor.snapshot().items() if v.health != "Healthy")}
+
         extra = {}
         if d.rank == 0:
             guard.enter("allocator_microbench")
@@ -950,15 +1036,11 @@ def main():
                                  "reference_candidates": refk["candidates"], "ours_candidates": mine["candidates"],
                                  "same_set": sorted(mine["ids"]) == sorted(refk["ids"])}
             extra = dict(core, **{
-                "latency_p50_ms_with_hip_runtime_container": round(pct(hip_lat, .5), 3) if hip_lat else None,
-                "latency_p99_ms_with_hip_runtime_container": round(pct(hip_lat, .99), 3) if hip_lat else None,
-                "hip_runtime_container_steps": len(hip_lat),
+                f"latency_p50_ms_{rt_key}": round(pct(rt_lat, .5), 3) if rt_lat else None,
+                f"latency_p99_ms_{rt_key}": round(pct(rt_lat, .99), 3) if rt_lat else None,
+                f"{rt_key}_steps": len(rt_lat),
                 "latency_p50_ms_back_to_back": round(pct(b2b_lat, .5), 3) if b2b_lat else None,
-                "health_loop": ({"pulse_s": args.health_pulse, "sweeps": impl.monitor.sweeps,
-                                 "sweep_ms_last": round(impl.monitor.last_sweep_ms, 3),
-                                 "unhealthy": sorted(k for k, v in impl.monitor.snapshot().items()
-                                                     if v.health != "Healthy")}
-                                if args.health_pulse > 0 and not args.fixture else None),
+                "health_loop": health_loop_report(),
                 f"latency_p50_ms_dev_view_{other_view}": round(pct(vis_lat, .5), 3) if vis_lat else None,
                 f"latency_p50_ms_container_mode_{other_mode}": round(pct(other_mode_lat, .5), 3) if other_mode_lat
                 else None,

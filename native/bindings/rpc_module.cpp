@@ -143,6 +143,7 @@ void bind_rpc(py::module_& m) {
         d["streams_open"] = st.streams_open;
         d["streams_opened"] = st.streams_opened;
         d["protocol_errors"] = st.protocol_errors;
+        d["caller_protocol_errors"] = st.caller_protocol_errors;
         d["bytes_in"] = st.bytes_in;
         d["bytes_out"] = st.bytes_out;
         return d;

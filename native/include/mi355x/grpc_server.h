@@ -52,6 +52,9 @@ struct ServerStats {
   uint64_t streams_open = 0;
   uint64_t streams_opened = 0;  // server-streaming calls ever opened (ListAndWatch)
   uint64_t protocol_errors = 0;
+  // protocol errors on connections that had made a call on a served route:
+  // kubelet's connection, as opposed to a stray client (a health checker, curl)
+  uint64_t caller_protocol_errors = 0;
   uint64_t bytes_in = 0;
   uint64_t bytes_out = 0;
 };

@@ -1,0 +1,122 @@
+// The native device-plugin daemon: discovery -> resources -> per-resource
+// gRPC servers -> registration with kubelet -> the control loop.
+//
+// Ownership: the Daemon owns the ResourceRegistry (resources, their servers
+// and DevicePlugin services, each resource's Registration state), the
+// HealthController (health engine + sweep bookkeeping), the worker pool and
+// the kubelet-socket watch. Only the control loop (run()) touches them; worker
+// threads get self-contained jobs (a Register request by value, a sweep job
+// from HealthController::job()) and hand back a Completion.
+//
+// Control loop (one poll per turn, never blocking on a peer):
+//   RPC events        the reference logs every Allocate; metrics, traces
+//   kubelet.sock      inotify + 5 s stat poll: a replaced socket restarts the
+//                     servers and re-registers (vendored dpm/manager.go:73-84)
+//   completions       Register answers (Registration::complete), sweep results
+//                     (health -> ListAndWatch lists, xGMI re-weighting)
+//   registrations     due Registers go out (backoff, re-register on lost streams)
+//   watchdog          Registration::observe: exit 3 when kubelet never lists
+//   topology          -topology_watch: a partition switch is re-discovered and
+//                     re-advertised, never under a sweep
+//   pulse             one sweep per -pulse on a worker thread
+#pragma once
+
+#include <signal.h>
+
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "flags.h"
+#include "health_controller.h"
+#include "resources.h"
+#include "topology_watch.h"
+#include "workers.h"
+#include "mi355x/dir_watch.h"
+
+namespace mi355x::daemon {
+
+struct Completion {
+  enum Kind { kRegister, kSweep } kind = kRegister;
+  // kRegister
+  size_t resource = 0;
+  uint64_t server_gen = 0;   // the server the Register was for
+  uint64_t kubelet_gen = 0;  // the kubelet it was sent to
+  bool ok = false;
+  std::string message;
+  // kSweep
+  SweepResult sweep;
+};
+
+// Register{version=1, endpoint=2, resource_name=3, options=4} on kubelet.sock (blocking; worker thread)
+std::string register_with_kubelet(const std::string& name, const std::string& socket, const std::string& options,
+                                  const std::string& kubelet_sock, double timeout_s, int abort_fd);
+
+class Daemon {
+ public:
+  explicit Daemon(Flags f);
+  ~Daemon();
+  Daemon(const Daemon&) = delete;
+  Daemon& operator=(const Daemon&) = delete;
+
+  // Discovery, CDI specs, the first health sweep; -dry_run prints its report.
+  // Returns -1 to go on with run(), else the exit code.
+  int init();
+  // The control loop until `*stop` (set by a signal handler that also writes
+  // to `sig_fd`) or the watchdog trips; returns the exit code.
+  int run(int sig_fd, const volatile sig_atomic_t* stop);
+
+ private:
+  std::string write_cdi(const std::set<std::string>& stale);
+  void rebuild_health();
+  void start_all();
+  void try_register(size_t i);
+  void on_rpc_events(size_t i);
+  void on_kubelet_socket(bool look);
+  void on_completions();
+  void on_sweep(const SweepResult& r);
+  std::string watchdog();
+  void topology_tick();
+  void reload_topology(const std::string& sig);
+  void pulse_tick();
+  int poll_timeout_ms(Clock::time_point now) const;
+  void shutdown();
+
+  Flags f_;
+  int dev_limit_ = -1;
+  ViewCtx views_;
+  bool impl_ok_ = true;
+  Driver driver_ = Driver::Container;
+  KfdTopology topo_;
+  std::vector<GpuDevice> container_devices_;
+  std::vector<std::string> warnings_;
+  ResourceRegistry reg_;
+  int stop_pipe_[2] = {-1, -1};  // ends every wait of the workers (peer calls, probes)
+  std::unique_ptr<HealthController> health_;
+  Workers<Completion> workers_;
+  // kubelet
+  std::string kubelet_sock_;
+  DirWatcher watch_;
+  uint64_t kubelet_gen_ = 0;  // bumped on every kubelet (re)start: older Register results are stale
+  struct SockId {
+    bool present = false;
+    uint64_t dev = 0, ino = 0;
+    int64_t ctime_ns = 0;
+    bool operator==(const SockId& o) const {
+      return present == o.present && dev == o.dev && ino == o.ino && ctime_ns == o.ctime_ns;
+    }
+    bool operator!=(const SockId& o) const { return !(*this == o); }
+  };
+  static SockId sock_id(const std::string& path);
+  SockId sock_;
+  Clock::time_point next_stat_{};
+  // pulse + topology watch
+  Clock::time_point next_pulse_{};
+  bool topo_watch_ = false;
+  std::chrono::milliseconds topo_period_{0};
+  TopologyWatch topo_state_;
+  Clock::time_point next_topo_{};
+};
+
+}  // namespace mi355x::daemon

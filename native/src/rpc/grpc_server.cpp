@@ -167,6 +167,7 @@ struct Conn {
   bool closing = false;
   bool epollout = false;
   bool dead = false;
+  bool made_call = false;  // a call on a served route (a device-plugin client, i.e. kubelet)
 };
 
 }  // namespace
@@ -203,6 +204,7 @@ struct GrpcServer::Impl {
   uint64_t next_call = 1;
 
   std::atomic<uint64_t> n_conns{0}, n_calls{0}, n_proto_err{0}, bytes_in{0}, bytes_out{0}, n_stream_opens{0};
+  std::atomic<uint64_t> n_caller_err{0};  // protocol errors on connections that had made a served call
 
   // ------------------------------------------------------------------ output
   void send_settings(Conn& c) {
@@ -229,6 +231,7 @@ struct GrpcServer::Impl {
 
   void conn_error(Conn& c, uint32_t code, const char* why) {
     n_proto_err++;
+    if (c.made_call) n_caller_err++;
     goaway(c, code, why);
     c.closing = true;
     c.errored = true;
@@ -331,6 +334,7 @@ struct GrpcServer::Impl {
     n_calls++;
     auto r = routes.find(s.path);
     if (r == routes.end()) return trailers_only(c, s, kUnimplemented, "unknown method " + s.path);
+    c.made_call = true;
     if (s.data.size() < 5) return trailers_only(c, s, kInternal, "missing request message");
     const auto* d = reinterpret_cast<const uint8_t*>(s.data.data());
     if (d[0] != 0) return trailers_only(c, s, kUnimplemented, "grpc compression is not supported");
@@ -944,6 +948,7 @@ ServerStats GrpcServer::stats() const {
   s.streams_open = open_streams("");
   s.streams_opened = impl_->n_stream_opens.load();
   s.protocol_errors = impl_->n_proto_err.load();
+  s.caller_protocol_errors = impl_->n_caller_err.load();
   s.bytes_in = impl_->bytes_in.load();
   s.bytes_out = impl_->bytes_out.load();
   return s;
@@ -1070,19 +1075,30 @@ std::string GrpcClient::connect(const std::string& unix_path, double timeout_s) 
   const int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
   if (fd < 0) return std::string("socket: ") + std::strerror(errno);
   const auto deadline = Clock::now() + std::chrono::microseconds(static_cast<int64_t>(timeout_s * 1e6));
-  if (::connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
-    if (errno != EAGAIN && errno != EINPROGRESS && errno != EINTR) {
+  // A non-blocking AF_UNIX connect() never completes later: EAGAIN means the
+  // listen backlog is full and the socket stays unconnected (poll() would
+  // report it at once with SO_ERROR 0). So try again until it succeeds, in
+  // short steps bounded by the deadline and the abort fd.
+  while (::connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+    if (errno == EINTR) continue;
+    if (errno != EAGAIN) {
       const std::string err = std::string("connect ") + unix_path + ": " + std::strerror(errno);
       ::close(fd);
       return err;
     }
-    // listen backlog full: wait for room (bounded by the deadline / abort fd)
-    const Ready r = wait_fd(fd, POLLOUT, abort_fd_, deadline);
-    int soerr = 0;
-    socklen_t sl = sizeof(soerr);
-    if (r != Ready::kOk || ::getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl) != 0 || soerr != 0) {
+    const auto step = std::min<Clock::duration>(std::chrono::milliseconds(5), deadline - Clock::now());
+    if (step <= Clock::duration::zero()) {
       ::close(fd);
-      return std::string("connect ") + unix_path + ": " + (r != Ready::kOk ? ready_error(r) : std::strerror(soerr));
+      return std::string("connect ") + unix_path + ": listen backlog full until the deadline";
+    }
+    if (abort_fd_ >= 0) {
+      pollfd p{abort_fd_, POLLIN, 0};
+      if (::poll(&p, 1, static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(step).count()) + 1) > 0) {
+        ::close(fd);
+        return std::string("connect ") + unix_path + ": interrupted";
+      }
+    } else {
+      std::this_thread::sleep_for(step);
     }
   }
   fd_ = fd;
@@ -1142,6 +1158,24 @@ Reply GrpcClient::unary(const std::string& path, const std::string& request, dou
         return false;
       }
       *err = "write failed";
+      // the server may have closed right after a GOAWAY that says why (e.g.
+      // ENHANCE_YOUR_CALM for too many pings): read what it sent and name it
+      char buf[65536];
+      ssize_t r;
+      while ((r = ::read(fd_, buf, sizeof(buf))) > 0) in_.append(buf, static_cast<size_t>(r));
+      for (size_t o = 0; in_.size() - o >= 9;) {
+        const auto* f = reinterpret_cast<const uint8_t*>(in_.data() + o);
+        const size_t len = (static_cast<size_t>(f[0]) << 16) | (static_cast<size_t>(f[1]) << 8) | f[2];
+        if (in_.size() - o < 9 + len) break;
+        if (f[3] == kGoaway && len >= 8) {
+          st.going_away = true;
+          st.goaway_code = be32(f + 13);
+          st.goaway_debug.assign(reinterpret_cast<const char*>(f + 17), std::min<size_t>(len - 8, 256));
+          *err = "connection closed after GOAWAY " + std::string(h2_error_name(st.goaway_code)) +
+                 (st.goaway_debug.empty() ? "" : " (" + st.goaway_debug + ")");
+        }
+        o += 9 + len;
+      }
       return false;
     }
     pending_out.clear();

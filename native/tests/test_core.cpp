@@ -18,6 +18,10 @@
 #include <unistd.h>
 
 #include "../src/rpc/hpack.h"
+#include "health_controller.h"
+#include "registration.h"
+#include "topology_watch.h"
+#include "workers.h"
 #include "mi355x/allocator.h"
 #include "mi355x/dp_service.h"
 #include "mi355x/gpu_discovery.h"
@@ -529,6 +533,179 @@ static void test_fuzz_rpc(const std::string& ref) {
   ::rmdir(dir);
 }
 
+
+// ---- daemon parts (native/src/daemon): registration rules, watchdog, topology watch, sweeps
+static rpc::ServerStats stats(uint64_t opened, uint64_t open, uint64_t perr, uint64_t caller_perr) {
+  rpc::ServerStats st;
+  st.streams_opened = opened;
+  st.streams_open = open;
+  st.protocol_errors = perr;
+  st.caller_protocol_errors = caller_perr;
+  return st;
+}
+
+static void test_registration_generations() {
+  using daemon::Registration;
+  using Outcome = daemon::Registration::Outcome;
+  const auto t0 = daemon::Clock::now();
+  auto ms = [&](int n) { return t0 + std::chrono::milliseconds(n); };
+  daemon::RegistrationPolicy pol;
+  pol.watchdog_s = 1.0;
+  pol.reregister_s = 0.5;
+  Registration r(pol);
+  CHECK(!r.due(t0));                       // no server yet
+  r.server_started(7, t0);
+  CHECK(r.due(t0) && r.server_gen() == 7);
+  r.begin(/*kubelet_gen=*/1, stats(0, 0, 0, 0));
+  CHECK(r.inflight() && !r.due(t0));
+  // an answer for an earlier server: ignored outright (stays in flight)
+  CHECK(r.complete(6, 1, 1, true, ms(5)) == Outcome::kStale && r.inflight() && !r.registered());
+  // an answer from the previous kubelet: in-flight ends, nothing registered, due again
+  CHECK(r.complete(7, 1, 2, true, ms(5)) == Outcome::kStale && !r.inflight() && !r.registered() && r.due(ms(5)));
+  // failures back off: 100 ms, doubling, capped at 3 s
+  r.begin(2, stats(0, 0, 0, 0));
+  CHECK(r.complete(7, 2, 2, false, ms(10)) == Outcome::kFailed);
+  CHECK(!r.due(ms(100)) && r.due(ms(110)));
+  int expect = 200;
+  for (int i = 0; i < 8; ++i) {
+    r.begin(2, stats(0, 0, 0, 0));
+    r.complete(7, 2, 2, false, ms(10));
+    CHECK(r.retry_ms() == std::min(expect * 2, 3000) || r.retry_ms() == 3000);
+    expect = std::min(expect * 2, 3000);
+  }
+  // success resets the backoff
+  r.begin(2, stats(0, 0, 0, 0));
+  CHECK(r.complete(7, 2, 2, true, ms(20)) == Outcome::kRegistered && r.registered() && r.retry_ms() == 100);
+  CHECK(r.registrations() == 1);
+  // a server restart (new generation) makes the old answer stale and registers again
+  r.server_started(8, ms(30));
+  CHECK(!r.registered() && r.due(ms(30)));
+  CHECK(r.complete(7, 2, 2, true, ms(31)) == Outcome::kStale);
+  r.server_stopped();
+  CHECK(!r.due(ms(40)));
+}
+
+static void test_registration_watchdog() {
+  using daemon::Registration;
+  const auto t0 = daemon::Clock::now();
+  auto ms = [&](int n) { return t0 + std::chrono::milliseconds(n); };
+  daemon::RegistrationPolicy pol;
+  pol.watchdog_s = 1.0;
+  pol.reregister_s = 0.5;
+  {  // kubelet never lists: trips after watchdog_s, not before
+    Registration r(pol);
+    r.server_started(1, t0);
+    r.begin(1, stats(3, 0, 0, 0));
+    r.complete(1, 1, 1, true, ms(10));
+    CHECK(r.armed() && r.observe(stats(3, 0, 0, 0), ms(900)).empty());
+    CHECK(r.observe(stats(3, 0, 0, 0), ms(1100)).find("no ListAndWatch stream within 1s") != std::string::npos);
+  }
+  {  // kubelet opens ListAndWatch before its Register answer reaches us: counted (baseline at begin())
+    Registration r(pol);
+    r.server_started(1, t0);
+    r.begin(1, stats(0, 0, 0, 0));
+    CHECK(r.observe(stats(1, 1, 0, 0), ms(5)).empty() && r.list_seen());  // stream opened while in flight
+    r.complete(1, 1, 1, true, ms(10));
+    CHECK(r.observe(stats(1, 1, 0, 0), ms(5000)).empty() && !r.armed());
+  }
+  {  // stray clients (errors on connections without a call) never trip it; kubelet's connection does
+    Registration r(pol);
+    r.server_started(1, t0);
+    r.begin(1, stats(0, 0, 5, 1));
+    r.complete(1, 1, 1, true, ms(10));
+    CHECK(r.observe(stats(0, 0, 9, 1), ms(100)).empty());
+    CHECK(r.observe(stats(0, 0, 9, 2), ms(200)).find("kubelet's connection") != std::string::npos);
+  }
+  {  // after ListAndWatch: disarmed for good, even for errors on kubelet's connection
+    Registration r(pol);
+    r.server_started(1, t0);
+    r.begin(1, stats(0, 0, 0, 0));
+    r.complete(1, 1, 1, true, ms(10));
+    CHECK(r.observe(stats(1, 1, 0, 0), ms(20)).empty() && r.list_seen());
+    CHECK(r.observe(stats(1, 1, 4, 4), ms(30)).empty() && r.observe(stats(1, 1, 4, 4), ms(60000)).empty());
+    // every stream closed for reregister_s: register again (once)
+    CHECK(r.observe(stats(1, 0, 4, 4), ms(100)).empty() && r.registered());
+    CHECK(r.observe(stats(1, 0, 4, 4), ms(400)).empty() && r.registered());
+    CHECK(r.observe(stats(1, 0, 4, 4), ms(700)).empty() && !r.registered() && r.due(ms(700)));
+    CHECK(r.reregistrations() == 1);
+    // the new registration is watched again from its own baseline
+    r.begin(1, stats(1, 0, 4, 4));
+    r.complete(1, 1, 1, true, ms(710));
+    CHECK(r.armed() && r.observe(stats(2, 1, 4, 4), ms(720)).empty() && r.list_seen());
+  }
+  {  // a stream that comes back in time cancels the re-registration
+    Registration r(pol);
+    r.server_started(1, t0);
+    r.begin(1, stats(0, 0, 0, 0));
+    r.complete(1, 1, 1, true, ms(10));
+    r.observe(stats(1, 1, 0, 0), ms(20));
+    r.observe(stats(1, 0, 0, 0), ms(100));
+    r.observe(stats(2, 1, 0, 0), ms(300));
+    CHECK(r.observe(stats(2, 1, 0, 0), ms(900)).empty() && r.registered() && r.reregistrations() == 0);
+  }
+  {  // -grpc_watchdog 0: never trips; poll deadlines stay sane
+    daemon::RegistrationPolicy off = pol;
+    off.watchdog_s = 0;
+    Registration r(off);
+    r.server_started(1, t0);
+    r.begin(1, stats(0, 0, 0, 0));
+    r.complete(1, 1, 1, true, ms(10));
+    CHECK(r.observe(stats(0, 0, 3, 3), ms(100000)).empty() && !r.armed());
+    CHECK(r.next_event(ms(10)) >= ms(10));
+  }
+}
+
+static void test_topology_watch() {
+  daemon::TopologyWatch w("a");
+  CHECK(!w.observe("a", true));
+  CHECK(!w.observe("b", true));   // first sight of a new signature: wait one period
+  CHECK(!w.observe("b", false));  // held, but a sweep is running: not now
+  CHECK(w.observe("b", true));
+  w.applied("b");
+  CHECK(!w.observe("b", true) && w.current() == "b");
+  CHECK(!w.observe("c", true) && !w.observe("d", true));  // still changing: nothing
+  CHECK(w.observe("d", true));
+}
+
+static void test_health_controller_generations(const std::string& tmp) {
+  // passthrough sweeps on worker threads against a reload on the control thread
+  // (run under TSan in CI: the job shares nothing with the controller)
+  daemon::Flags f;
+  f.sysfs_root = tmp + "/no-such-sysfs";
+  f.exporter_socket = "";
+  daemon::HealthController hc(f, -1);
+  std::vector<daemon::Resource> rs(1);
+  rs[0].group_ids = {"3", "4"};
+  rs[0].groups["3"] = {PciFunctionInfo{}};
+  rs[0].groups["4"] = {PciFunctionInfo{}};
+  hc.rebuild(daemon::Driver::Pf, {}, KfdTopology{}, rs);
+  daemon::Workers<daemon::SweepResult> w;
+  hc.started();
+  w.run(hc.job());
+  CHECK(hc.inflight() && !hc.may_reload());
+  std::vector<daemon::SweepResult> got;
+  for (int i = 0; i < 500 && got.empty(); ++i) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    got = w.take();
+  }
+  CHECK(got.size() == 1 && hc.finished(got[0]) && hc.may_reload());
+  CHECK(got.size() == 1 && got[0].health.size() == 2 && !got[0].health.at("3"));  // vfio-pci absent: Unhealthy
+  // a reload while a sweep runs: the old sweep's result is dropped
+  hc.started();
+  w.run(hc.job());
+  rs[0].group_ids = {"5"};
+  rs[0].groups["5"] = {PciFunctionInfo{}};
+  hc.rebuild(daemon::Driver::Pf, {}, KfdTopology{}, rs);
+  w.join_all();
+  got = w.take();
+  CHECK(got.size() == 1 && !hc.finished(got[0]));
+  hc.started();
+  w.run(hc.job());
+  w.join_all();
+  got = w.take();
+  CHECK(got.size() == 1 && hc.finished(got[0]) && got[0].health.count("5") == 1);
+}
+
 int main(int argc, char** argv) {
   std::string repo = argc > 1 ? argv[1] : "testdata";
   std::string ref = argc > 2 ? argv[2] : "/root/reference/testdata";
@@ -540,6 +717,16 @@ int main(int argc, char** argv) {
   test_hpack();
   test_grpc_server();
   test_fuzz_rpc(ref);
+  test_registration_generations();
+  test_registration_watchdog();
+  test_topology_watch();
+  {
+    char dir[] = "/tmp/mi355x-test-core-XXXXXX";
+    if (::mkdtemp(dir)) {
+      test_health_controller_generations(dir);
+      ::rmdir(dir);
+    }
+  }
   std::printf("test_core: %d passed, %d failed, %d skipped\n", g_pass, g_fail, g_skip);
   return g_fail ? 1 : 0;
 }

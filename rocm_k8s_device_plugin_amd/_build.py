@@ -71,6 +71,22 @@ def _up_to_date(targets) -> bool:
     return f"digest={_source_digest()}" in STAMP.read_text().split()
 
 
+def git_describe() -> str:
+    """The version the native binaries report: $GIT_DESCRIBE (image builds),
+    else ``git describe --always --long --dirty`` of this tree (the reference's
+    Dockerfile:21), else "" (no git metadata, e.g. a copied tree: keep what the
+    last build stamped)."""
+    env = os.environ.get("GIT_DESCRIBE", "").strip()
+    if env:
+        return env
+    try:
+        r = subprocess.run(["git", "-C", str(REPO_DIR), "describe", "--always", "--long", "--dirty"],
+                           stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, timeout=10)
+    except (OSError, subprocess.TimeoutExpired):
+        return ""
+    return r.stdout.strip() if r.returncode == 0 else ""
+
+
 def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = None,
           jobs: int | None = None, quiet: bool = True) -> None:
     """Configure + build. ``hip=None`` builds the HIP probe when hipcc exists."""
@@ -86,6 +102,9 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
         f"-DMI355X_SANITIZE={sanitize}",
         "-DCMAKE_BUILD_TYPE=Release",
     ]
+    describe = git_describe()
+    if describe:
+        cfg.append(f"-DMI355X_GIT_DESCRIBE={describe}")
     if sanitize:
         # sanitizer builds are for ctest only; keep the package outputs untouched
         cfg.append(f"-DMI355X_PKG_DIR={bdir / 'pkg'}")
@@ -93,10 +112,10 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
     if not (bdir / "CMakeCache.txt").exists() or sanitize:
         subprocess.run(cfg, check=True, stdout=out)
     else:
-        # re-run configure only if the HIP option flipped
+        # re-run configure only if the HIP option or the version stamp changed
         cache = (bdir / "CMakeCache.txt").read_text()
         want = f"MI355X_BUILD_HIP:BOOL={'ON' if hip else 'OFF'}"
-        if want not in cache:
+        if want not in cache or (describe and f"MI355X_GIT_DESCRIBE:STRING={describe}\n" not in cache):
             subprocess.run(cfg, check=True, stdout=out)
     j = jobs or min(8, os.cpu_count() or 4)
     res = subprocess.run(["cmake", "--build", str(bdir), "-j", str(j)], stdout=subprocess.PIPE,

@@ -134,9 +134,10 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
         env["ROCR_VISIBLE_DEVICES"] = ",".join(str(o) for o in ordinals)
     redirect = mount_redirects(mounts)
     if redirect:
-        if runtime not in ("hsa", "mountemu"):
-            raise ValueError("mounts can only be applied to the HSA entrypoint (mount emulation build)")
-        runtime = "mountemu"
+        # both interposing builds (HSA mountemu, HIP devemu) apply mounts by redirection
+        runtime = {"hsa": "mountemu", "hip": "hip-devemu"}.get(runtime, runtime)
+        if runtime not in ("mountemu", "hip-devemu"):
+            raise ValueError(f"mounts cannot be applied to the {runtime!r} entrypoint (no path interposition)")
         env["MI355X_INITPROF_REDIRECT"] = redirect
     argv = [*argv_prefix, exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
             "--iters", str(iters), "--timeout", str(min(timeout_s, 30.0))]

@@ -158,10 +158,13 @@ class ResourcePlugin:
                 try:
                     t0 = time.perf_counter()
                     await self._serve()
+                    # the watchdog's baseline is taken before Register goes out: kubelet may
+                    # open ListAndWatch before its Register answer reaches us
+                    st0 = self.native.srv.stats() if self.native is not None else None
                     await self._register()
                     self.running = True
                     if self.native is not None and cfg.grpc_watchdog_s > 0:
-                        self._watchdog = asyncio.create_task(self._watch_native(self.native))
+                        self._watchdog = asyncio.create_task(self._watch_native(self.native, st0))
                     log.info_fields(_log, "plugin server started", resource=self.resource_name,
                                     socket=self.socket, startup_ms=f"{(time.perf_counter() - t0) * 1e3:.2f}")
                     return True
@@ -176,28 +179,32 @@ class ResourcePlugin:
                         await asyncio.sleep(cfg.retry_wait_s)
             return False
 
-    async def _watch_native(self, native: NativePluginServer) -> None:
+    async def _watch_native(self, native: NativePluginServer, st0: dict) -> None:
         """The native HTTP/2 stack has only been proven against grpc-go by
         emulation (testing/gopeer.py). If the real kubelet cannot complete a
         call on it, the plugin would stay registered and invisible; the
         reference's grpc-go server has no such risk (vendored dpm/plugin.go:
-        93-162). So: kubelet opens ListAndWatch right after Register; no stream
-        within grpc_watchdog_s, or protocol errors on the socket, and this
-        resource is re-served with grpc.aio and registered again."""
+        93-162). So, until kubelet's first ListAndWatch (counted from `st0`,
+        the server's counters when Register was sent): no stream within
+        grpc_watchdog_s, or a protocol error on a connection that has made a
+        DevicePlugin call (kubelet's, not a stray client's), and this resource
+        is re-served with grpc.aio and registered again. Once ListAndWatch has
+        been seen the watchdog is done: a misbehaving client later loses only
+        its own connection (GOAWAY), as with grpc-go (server.go:984-998)."""
         cfg = self.mgr.cfg
-        st0 = native.srv.stats()
         t0 = time.monotonic()
-        seen_stream = False
         reason = ""
         while self.native is native:
-            await asyncio.sleep(min(0.25, cfg.grpc_watchdog_s / 4) if not seen_stream else 1.0)
+            await asyncio.sleep(min(0.25, cfg.grpc_watchdog_s / 4))
             if self.native is not native:
                 return
             st = native.srv.stats()
-            seen_stream = seen_stream or st["streams_opened"] > st0["streams_opened"]
-            if st["protocol_errors"] > st0["protocol_errors"]:
-                reason = f"{st['protocol_errors'] - st0['protocol_errors']} HTTP/2 protocol error(s) on the plugin socket"
-            elif not seen_stream and time.monotonic() - t0 > cfg.grpc_watchdog_s:
+            if st["streams_opened"] > st0["streams_opened"]:
+                return                      # kubelet lists: disarmed
+            if st["caller_protocol_errors"] > st0["caller_protocol_errors"]:
+                reason = (f"{st['caller_protocol_errors'] - st0['caller_protocol_errors']} HTTP/2 protocol error(s) "
+                          f"on kubelet's connection before its ListAndWatch")
+            elif time.monotonic() - t0 > cfg.grpc_watchdog_s:
                 reason = f"no ListAndWatch stream within {cfg.grpc_watchdog_s:g}s of Register"
             if reason:
                 break

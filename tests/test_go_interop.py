@@ -33,6 +33,7 @@ import pytest
 
 from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR, core
 from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+from rocm_k8s_device_plugin_amd.testing import go_kubelet
 from rocm_k8s_device_plugin_amd.testing import gopeer as gp
 from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
 
@@ -129,21 +130,11 @@ def test_encode_duration_matches_grpcutil():
 
 # ------------------------------------------------------------------ grpc-go client -> native server
 
-class GoKubelet:
-    """kubelet's Registration server as grpc-go runs it, on <dir>/kubelet.sock."""
-
-    def __init__(self, kdir, config=None):
-        os.makedirs(kdir, exist_ok=True)
-        self.registrations = []
-
-        def register(msg):
-            self.registrations.append(pb.RegisterRequest.FromString(msg))
-            return 0, "", b""
-
-        self.srv = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {REGISTER: register}, config)
-
-    def close(self):
-        self.srv.close()
+def GoKubelet(kdir, config=None, **kw):
+    """kubelet's Registration server as grpc-go runs it, on <dir>/kubelet.sock;
+    by default it connects back and opens ListAndWatch inside its Register
+    handler, as kubelet does (testing/go_kubelet.py)."""
+    return go_kubelet.GoKubelet(kdir, config=config, **kw)
 
 
 def _daemon(kdir, fi, *extra):
@@ -170,7 +161,7 @@ def daemon_node(tmp_path, request):
     kub = GoKubelet(kdir)
     p = _daemon(kdir, fi, *getattr(request, "param", ()))
     try:
-        assert _wait(lambda: kub.registrations, 20), "the daemon never registered"
+        assert _wait(lambda: kub.registrations and kub.updates(), 20), "the daemon never registered / listed"
         yield kdir, kub, p
     finally:
         rc, err = _stop(p)
@@ -472,7 +463,6 @@ def _open_lw(s, sid=1):
               gp.frame(gp.DATA, gp.END_STREAM, sid, gp.grpc_message(b"")))
 
 
-@pytest.mark.parametrize("daemon_node", [("-grpc_watchdog", "0")], indirect=True)   # errors on purpose
 @pytest.mark.parametrize("case,want", [
     ("no-settings-first", gp.PROTOCOL_ERROR),
     ("rst-idle", gp.PROTOCOL_ERROR),
@@ -512,7 +502,126 @@ def test_native_server_connection_errors(daemon_node, case, want):
         c.close()
 
 
-# ------------------------------------------------------------------ transport watchdog
+# ------------------------------------------------------------------ transport watchdog (native daemon)
+
+def _stray_clients(path):
+    """What may poke a plugin socket besides kubelet: curl, a socket health
+    check, a client with a bad preface, and each connection error above on a
+    connection that made no DevicePlugin call."""
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)     # connect and leave
+    s.connect(path)
+    s.close()
+    for payload in (b"GET / HTTP/1.1\r\nHost: x\r\n\r\n", b"PRI * HTTP/2.0\r\n\r\nXX\r\n\r\n" + b"\0" * 9):
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect(path)
+        s.sendall(payload)
+        s.settimeout(5)
+        try:
+            while s.recv(4096):    # until the server hangs up
+                pass
+        except OSError:
+            pass
+        s.close()
+    for case in ("no-settings-first", "rst-idle", "window-update-idle", "enable-push-2"):
+        s, rd = _raw(path, first_settings=case != "no-settings-first")
+        try:
+            s.sendall({"no-settings-first": gp.frame(gp.PING, 0, 0, b"\0" * 8),
+                       "rst-idle": gp.frame(gp.RST_STREAM, 0, 7, struct.pack(">I", gp.CANCEL)),
+                       "window-update-idle": gp.frame(gp.WINDOW_UPDATE, 0, 9, struct.pack(">I", 100)),
+                       "enable-push-2": gp.frame(gp.SETTINGS, 0, 0, gp.settings_payload([(gp.S_ENABLE_PUSH, 2)]))}[case])
+            assert _goaway_code(rd) is not None, case
+        finally:
+            s.close()
+
+
+@pytest.mark.parametrize("daemon_node", [("-pulse", "1", "-send_every_pulse")], indirect=True)
+def test_stray_clients_never_trip_the_watchdog(daemon_node):
+    """Default -grpc_watchdog (10 s), kubelet listing: stray or malformed
+    clients get GOAWAY and lose only their own connection (grpc-go
+    server.go:984-998); the daemon stays up, kubelet's stream keeps receiving
+    lists and nothing registers again."""
+    kdir, kub, p = daemon_node
+    path = os.path.join(kdir, "amd.com_gpu")
+    _stray_clients(path)
+    n = kub.updates()
+    assert _wait(lambda: kub.updates() >= n + 2, 10), "kubelet's stream stopped receiving lists"
+    assert p.poll() is None and len(kub.registrations) == 1 and not kub.stream_ended.is_set()
+    assert list(kub.lists[-1].values()).count("Healthy") == 8
+    c = gp.GoClientConn(path)
+    try:
+        assert c.unary(DP + "GetDevicePluginOptions", b"", 3.0)[0] == 0
+    finally:
+        c.close()
+
+
+def test_watchdog_counts_a_list_opened_before_the_register_answer(tmp_path):
+    """kubelet opens ListAndWatch inside its Register handler (eager GoKubelet):
+    the stream exists before the daemon reads the Register answer. The
+    watchdog's baseline is taken when Register is sent, so it is counted."""
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    kub = GoKubelet(kdir, eager=True)
+    p = _daemon(kdir, fi, "-grpc_watchdog", "1")
+    try:
+        assert _wait(lambda: kub.updates(), 20)
+        time.sleep(2.5)     # well past -grpc_watchdog
+        assert p.poll() is None and len(kub.registrations) == 1
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+    assert rc == 0 and "transport watchdog" not in err, err[-2000:]
+
+
+def test_watchdog_trips_on_a_protocol_error_of_kubelets_connection(tmp_path):
+    """Before the first ListAndWatch, a protocol error on a connection that has
+    made a DevicePlugin call (kubelet's) means kubelet cannot use this
+    transport: exit 3 so the DaemonSet restarts the plugin."""
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    kub = GoKubelet(kdir, list_and_watch=False)
+    p = _daemon(kdir, fi, "-grpc_watchdog", "30")
+    try:
+        assert _wait(lambda: kub.registrations, 20)
+        path = os.path.join(kdir, "amd.com_gpu")
+        _stray_clients(path)                 # stray clients: still nothing
+        time.sleep(0.5)
+        assert p.poll() is None
+        c = gp.GoClientConn(path)            # kubelet's connection: a call, then a protocol error
+        try:
+            assert c.unary(DP + "GetDevicePluginOptions", b"", 3.0)[0] == 0
+            c._send(gp.frame(gp.RST_STREAM, 0, 99, struct.pack(">I", gp.CANCEL)), raw=True)
+            assert p.wait(timeout=10) == 3
+        finally:
+            c.close()
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+    assert rc == 3 and "protocol error(s) on kubelet's connection before its ListAndWatch" in err, err[-2000:]
+
+
+def test_daemon_registers_again_when_kubelet_drops_the_stream(tmp_path):
+    """kubelet ends ListAndWatch when it drops a plugin (runClient ->
+    disconnectClient): with kubelet.sock unchanged the daemon registers again
+    after -reregister s and the new stream gets the devices."""
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    kub = GoKubelet(kdir)
+    p = _daemon(kdir, fi, "-reregister", "0.5")
+    try:
+        assert _wait(lambda: kub.updates(), 20)
+        n = kub.updates()
+        kub.end_stream()
+        assert _wait(lambda: len(kub.registrations) == 2 and kub.updates() > n, 10), (kub.registrations, kub.errors)
+        assert len(kub.lists[-1]) == 8
+        time.sleep(1.0)      # one re-registration, not a loop
+        assert len(kub.registrations) == 2 and p.poll() is None
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+    assert rc == 0 and "registering again" in err, err[-2000:]
+
+
+# ------------------------------------------------------------------ transport watchdog (Python plugin)
 
 def _py_plugin(tmp_path, watchdog_s):
     from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
@@ -570,10 +679,13 @@ def test_python_watchdog_reserves_on_aio_when_kubelet_never_lists(tmp_path):
     asyncio.run(asyncio.wait_for(go(), 60))
 
 
-def test_python_watchdog_protocol_errors_move_to_aio(tmp_path):
+def test_python_watchdog_ignores_stray_clients_and_disarms_after_list(tmp_path):
+    """A stray client's protocol error (plain HTTP/1.1 on the socket, a bad
+    preface, ...) closes only its own connection: once kubelet lists, the
+    Python plugin stays on the native server and registers nothing again."""
     import asyncio
     from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
-    pdir, mgr = _py_plugin(tmp_path, 30.0)
+    pdir, mgr = _py_plugin(tmp_path, 1.0)
 
     async def go():
         k = FakeKubelet(pdir)
@@ -583,16 +695,49 @@ def test_python_watchdog_protocol_errors_move_to_aio(tmp_path):
             await k.wait_for_resource("amd.com/gpu", 8, timeout=10)
             p = mgr.plugins["gpu"]
             assert p.native is not None and p.native_failed is None
-            await asyncio.sleep(0.5)    # a healthy session raises nothing
+            await asyncio.to_thread(_stray_clients, p.socket)
+            await asyncio.sleep(2.0)    # past grpc_watchdog_s
+            assert p.native is not None and p.native_failed is None and len(k.registrations) == 1
+        finally:
+            mgr.request_stop()
+            await asyncio.wait_for(task, 20)
+            await k.stop()
+
+    asyncio.run(asyncio.wait_for(go(), 60))
+
+
+def test_python_watchdog_protocol_error_on_kubelets_connection_moves_to_aio(tmp_path):
+    """Before ListAndWatch, a protocol error on a connection that made a
+    DevicePlugin call (kubelet's) re-serves the resource on grpc.aio."""
+    import asyncio
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+    pdir, mgr = _py_plugin(tmp_path, 30.0)
+
+    def kubelet_conn_error(path):
+        c = gp.GoClientConn(path)
+        try:
+            assert c.unary(DP + "GetDevicePluginOptions", b"", 3.0)[0] == 0
+            c._send(gp.frame(gp.RST_STREAM, 0, 99, struct.pack(">I", gp.CANCEL)), raw=True)
+            assert _goaway_code(c.rd) == gp.PROTOCOL_ERROR
+        finally:
+            c.close()
+
+    async def go():
+        k = FakeKubelet(pdir)
+        k.open_list_and_watch = False
+        await k.start()
+        task = asyncio.create_task(mgr.run())
+        try:
+            await _until(lambda: len(k.registrations) >= 1)
+            p = mgr.plugins["gpu"]
             assert p.native is not None
-            s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
-            s.connect(p.socket)
-            s.sendall(b"GET / HTTP/1.1\r\nHost: x\r\n\r\n")   # not HTTP/2: a protocol error
-            s.settimeout(5)
-            await asyncio.to_thread(lambda: [None for _ in iter(lambda: s.recv(4096), b"")])   # until it hangs up
-            s.close()
+            await asyncio.to_thread(_stray_clients, p.socket)
+            await asyncio.sleep(0.6)
+            assert p.native is not None and p.native_failed is None
+            await asyncio.to_thread(kubelet_conn_error, p.socket)
             await _until(lambda: len(k.registrations) >= 2)
-            assert p.native is None and "protocol error" in p.native_failed
+            assert p.native is None and "kubelet's connection" in p.native_failed
+            k.open_list_and_watch = True
             await _until(lambda: k.resources["amd.com/gpu"].updates >= 1 and k.resources["amd.com/gpu"].devices)
         finally:
             mgr.request_stop()

@@ -67,7 +67,7 @@ def test_device_plugin_log_files_per_severity(tmp_path):
     kub = gp.GoServer(str(kdir / "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
     p = subprocess.Popen([DP, "-kubelet_dir", str(kdir), "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
                           "-exporter_socket", "", "-logtostderr=false", f"-log_dir={logs}", "-vmodule",
-                          "device_plugin_main=2", "-grpc_watchdog", "0", f"-log_link={tmp_path}",
+                          "daemon=2", "-grpc_watchdog", "0", f"-log_link={tmp_path}",
                           "-logbuflevel=-1"],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     try:
@@ -80,7 +80,7 @@ def test_device_plugin_log_files_per_severity(tmp_path):
             assert a[0] == 0
         finally:
             c.close()
-        # -vmodule=device_plugin_main=2: per-RPC lines without -v
+        # -vmodule=daemon=2: per-RPC lines without -v
         assert _wait(lambda: "rpc rpc=GetDevicePluginOptions resource=gpu latency_ms="
                      in (logs / "k8s-device-plugin.INFO").read_text())
     finally:
@@ -148,7 +148,7 @@ def test_json_log_format_in_both_binaries(tmp_path):
     assert rc == 0
     recs = [json.loads(line) for line in err.splitlines() if line.strip()]
     assert recs and all(set(r) >= {"ts", "level", "src", "msg"} for r in recs)
-    assert any(r["msg"] == "Found 8 AMDGPUs" and r["level"] == "INFO" and r["src"].startswith("device_plugin_main.cpp:")
+    assert any(r["msg"] == "Found 8 AMDGPUs" and r["level"] == "INFO" and r["src"].startswith("resources.cpp:")
                for r in recs)
     rpc = [r for r in recs if r["msg"] == "rpc" and r.get("rpc") == "GetDevicePluginOptions"]
     assert rpc and rpc[0]["resource"] == "gpu" and float(rpc[0]["latency_ms"]) >= 0

@@ -448,8 +448,10 @@ def test_daemon_watchdog_exits_when_kubelet_never_lists(tmp_path):
     assert not os.path.exists(os.path.join(kdir, "amd.com_gpu"))      # sockets removed on the way out
 
 
-def test_daemon_refuses_python_only_flags_and_bad_liveness(tmp_path):
-    for args, want in ((["-grpc_server", "aio"], "Python entrypoint"),
+def test_daemon_refuses_unknown_flags_and_bad_liveness(tmp_path):
+    # -grpc_server was the Python CLI's transport switch; the daemon is the only
+    # plugin entrypoint, so it is an undefined flag like any other (Go's flag wording)
+    for args, want in ((["-grpc_server", "aio"], "flag provided but not defined: -grpc_server"),
                        (["-liveness"], "-pulse > 0"),
                        (["-liveness_mode", "bogus"], "liveness_mode"),
                        (["-vmodule", "nolevel"], "vmodule")):

@@ -140,8 +140,8 @@ def test_bench_n_of_m_searches_inside_the_timed_step():
     assert e["bench_process_gpu"] == {"ranks": [{"torch_cuda_initialized": False, "kfd_fds": 0, "render_fds": 0}],
                                       "clean": True}
     ta = e["tail_attribution"]
-    assert set(ta["phase_p50_ms"]) == {"plugin_rpc", "runtime_prep", "spawn_to_main", "gpu_runtime_init",
-                                       "device_setup_and_mfma"}
+    assert set(ta["phase_p50_ms"]) == {"plugin_rpc", "runtime_prep", "exec_and_library_load", "gpu_runtime_init",
+                                       "device_setup", "launch_and_verify"}
     assert all(s["latency_ms"] > ta["threshold_ms"] for s in ta["slow_steps"])
 
 

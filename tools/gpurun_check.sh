@@ -1,0 +1,56 @@
+#!/bin/bash
+# The one maintained GPU-box script (gpurun): each argument is a step, run in
+# order; a failed step ends the call (no further GPU work after a failure).
+#
+#   smoke   __graft_entry__.smoke()                       -> gpurun_out/smoke.log
+#   tests   pytest -m gpu                                 -> gpurun_out/gputests.log
+#   bench   default bench (N=1, 20 steps)                 -> gpurun_out/bench.json
+#   bench100  100 timed admissions                        -> gpurun_out/bench100.json
+#   health  bench with the health DaemonSet loop (-pulse 2, liveness, amd-smi) -> gpurun_out/bench_health.json
+#   prof    rocprofv3 kernel stats of a short bench       -> gpurun_out/prof_bench/
+#
+#   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() { echo "== $1 $(date +%T)"; }
+for s in "$@"; do
+  case "$s" in
+    smoke)
+      step smoke
+      timeout -k 10 240 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+        || { tail -30 gpurun_out/smoke.log; exit 1; }
+      tail -3 gpurun_out/smoke.log ;;
+    tests)
+      step tests
+      timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > gpurun_out/gputests.log 2>&1 || { tail -40 gpurun_out/gputests.log; exit 1; }
+      tail -3 gpurun_out/gputests.log ;;
+    bench)
+      step bench
+      timeout -k 10 400 python3 bench.py --json-out gpurun_out/bench.json > gpurun_out/bench.log 2>&1 \
+        || { tail -20 gpurun_out/bench.log; exit 1; }
+      cut -c1-600 gpurun_out/bench.json ;;
+    bench100)
+      step bench100
+      timeout -k 10 600 python3 bench.py --steps 100 --warmup 5 --json-out gpurun_out/bench100.json \
+        > gpurun_out/bench100.log 2>&1 || { tail -20 gpurun_out/bench100.log; exit 1; }
+      cut -c1-600 gpurun_out/bench100.json ;;
+    health)
+      step health
+      timeout -k 10 400 python3 bench.py --steps 30 --health-pulse 2 --runtime-compare 0 \
+        --json-out gpurun_out/bench_health.json > gpurun_out/bench_health.log 2>&1 \
+        || { tail -20 gpurun_out/bench_health.log; exit 1; }
+      python3 -c "import json; d=json.load(open('gpurun_out/bench_health.json')); print(d['value'], d['extra']['health_loop'])" ;;
+    prof)
+      step prof
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o bench \
+        -- python3 bench.py --steps 5 --warmup 1 > gpurun_out/prof_bench.log 2>&1 \
+        || { tail -20 gpurun_out/prof_bench.log; exit 1; }
+      find gpurun_out/prof_bench -name "*kernel_stats.csv" ;;
+    *)
+      echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
