@@ -64,6 +64,7 @@
 #include "mi355x/pci_scan.h"
 #include "mi355x/smi_query.h"
 #include "mi355x/sysfs.h"
+#include "mi355x/versions.h"
 
 namespace {
 
@@ -92,6 +93,8 @@ struct Flags {
   int watch_timeout_s = 300;
   glog::Options log;
 };
+
+constexpr const char* kTitle = "AMD GPU Node Labeller for Kubernetes (MI355X-native, native daemon)";
 
 bool parse_bool(const std::string& v, bool* out) {
   if (v.empty() || v == "1" || v == "t" || v == "T" || v == "true" || v == "TRUE" || v == "True") return *out = true;
@@ -124,7 +127,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       value = a.substr(eq + 1);
       has_value = true;
     }
-    if (name == "h" || name == "help") {
+    if (name == "h" || name == "help") {  // the version banner, then the flags (main.go flag.Usage)
+      for (const auto& line : versions::banner(kTitle, argv[0], f->sysfs_root)) std::printf("%s\n", line.c_str());
       std::printf("usage: %s [-<label kind> ...] [-driver_type container|vf-passthrough|pf-passthrough] "
                   "[-node_name NAME] [-kubeconfig PATH] [-resync S] [-once] [-watch=false] [-topology_watch S] "
                   "[-dry_run] [-sysfs_root DIR] [-dev_root DIR] [-v N] [-logtostderr] [-alsologtostderr] "
@@ -450,7 +454,7 @@ int main(int argc, char** argv) {
     print_json(labeller::generate_labels(label_options(f)));
     return 0;
   }
-  MI_LOG(kInfo, "AMD GPU Node Labeller for Kubernetes (MI355X-native, native daemon)");
+  for (const auto& line : versions::banner(kTitle, argv[0], f.sysfs_root)) MI_LOG(kInfo, "%s", line.c_str());
   f.node_name = node_name_from(f);
   if (f.node_name.empty()) {
     MI_LOG(kError, "node name unknown: set DS_NODE_NAME or -node_name (or mount /labeller/hostname)");

@@ -308,4 +308,6 @@ def test_labeller_launcher_dispatches_native_first(tmp_path):
     assert nat.returncode == 0 and py.returncode == 0, (nat.stderr[-1000:], py.stderr[-1000:])
     assert json.loads(nat.stdout) == json.loads(py.stdout)
     h = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=60)
-    assert h.stdout.startswith("usage: ") and "mi355x-node-labeller" in h.stdout   # the native binary answered
+    lines = h.stdout.splitlines()   # the native binary answered: its version banner, then the usage
+    assert lines[0].startswith("AMD GPU Node Labeller") and "mi355x-node-labeller version " in lines[1]
+    assert lines[3].startswith("usage: ")
