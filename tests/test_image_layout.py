@@ -1,0 +1,232 @@
+"""Every deploy path runs from the image it names.
+
+The reference builds the image its manifests and chart use (/root/reference/
+Dockerfile:14-33 -> k8s-ds-amdgpu-dp.yaml, helm/amd-gpu/values.yaml:7-11).
+Here, without a container runtime:
+
+1. the image each manifest / rendered chart names must be one the Makefile
+   builds (IMAGE_REPO:VERSION -> Dockerfile, :labeller-VERSION ->
+   labeller.Dockerfile; VERSION = the chart's appVersion);
+2. that Dockerfile's runtime stage (COPY / ln -s / WORKDIR / ENV / CMD) is
+   replayed into a temporary root, with the build stage's outputs taken from
+   this tree's in-tree build;
+3. the container's command (or the image CMD) and args run from that root,
+   in the working directory the pod spec or the image sets, with -dry_run
+   against the synthetic MI355X node: the process must exit 0 and report the
+   node's resources (device plugin) or labels (labeller). A flag the binary
+   does not know, or a command the image does not have, fails here.
+
+The chart is rendered by testing/helm_lite.py (no helm binary in this image)
+for its default values and for every value that changes the command line.
+"""
+import glob
+import json
+import os
+import re
+import shlex
+import shutil
+import subprocess
+
+import pytest
+import yaml
+
+from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+from rocm_k8s_device_plugin_amd.testing.helm_lite import rendered_objects
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHART = os.path.join(REPO, "helm", "amd-gpu")
+MANIFESTS = ["k8s-ds-amdgpu-dp.yaml", "k8s-ds-amdgpu-dp-health.yaml", "k8s-ds-amdgpu-labeller.yaml"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from rocm_k8s_device_plugin_amd import _build
+    _build.ensure_built(hip=None)
+
+
+# ------------------------------------------------------------------ Makefile: image -> Dockerfile
+def image_map():
+    mk = open(os.path.join(REPO, "Makefile")).read()
+    repo = re.search(r"^IMAGE_REPO \?= (\S+)$", mk, re.M).group(1)
+    version = yaml.safe_load(open(os.path.join(CHART, "Chart.yaml")))["appVersion"]
+    out = {}
+    for df, tag in re.findall(r"-f (\S+) -t \$\(IMAGE_REPO\):(\S+)", mk):
+        out[f"{repo}:{tag.replace('$(VERSION)', version)}"] = df
+    return out
+
+
+# ------------------------------------------------------------------ Dockerfile runtime stage
+def runtime_stage(dockerfile):
+    text = open(os.path.join(REPO, dockerfile)).read().replace("\\\n", " ")
+    lines = [l.strip() for l in text.splitlines() if l.strip() and not l.strip().startswith("#")]
+    stages, cur = [], None
+    for l in lines:
+        op, _, rest = l.partition(" ")
+        if op.upper() == "FROM":
+            cur = []
+            stages.append(cur)
+        elif cur is not None:
+            cur.append((op.upper(), rest.strip()))
+    return stages[-1]
+
+
+def replay(dockerfile, root):
+    """The runtime stage's file system under `root`: {"workdir", "env", "cmd", "runs"}."""
+    st = {"workdir": "/", "env": {}, "cmd": None, "runs": []}
+    for op, rest in runtime_stage(dockerfile):
+        if op == "WORKDIR":
+            st["workdir"] = rest
+            os.makedirs(root + rest, exist_ok=True)
+        elif op == "COPY":
+            args = shlex.split(rest)
+            frm = None
+            if args[0].startswith("--from="):
+                frm, args = args[0][len("--from="):], args[1:]
+            srcs, dst = args[:-1], args[-1]
+            for src in srcs:
+                if frm is not None:
+                    if not src.startswith("/src/"):
+                        continue         # system libraries of the build stage (the host has its own)
+                    paths = glob.glob(os.path.join(REPO, src[len("/src/"):]))
+                else:
+                    paths = glob.glob(os.path.join(REPO, src))
+                assert paths or frm is None or "*" in src, f"{dockerfile}: COPY {src}: nothing built there"
+                for p in paths:
+                    target = root + dst + (os.path.basename(p) if dst.endswith("/") else "")
+                    os.makedirs(os.path.dirname(target), exist_ok=True)
+                    if os.path.isdir(p):
+                        shutil.copytree(p, target, symlinks=True, dirs_exist_ok=True)
+                    else:
+                        shutil.copy2(p, target)
+        elif op == "RUN":
+            st["runs"].append(rest)
+            for part in rest.split("&&"):
+                words = shlex.split(part)
+                if words[:2] == ["ln", "-s"]:
+                    target, link = words[2], words[3]
+                    os.makedirs(os.path.dirname(root + link), exist_ok=True)
+                    os.symlink(root + target, root + link)
+        elif op == "ENV":
+            for kv in shlex.split(rest):
+                k, _, v = kv.partition("=")
+                st["env"][k] = v
+        elif op == "CMD":
+            st["cmd"] = json.loads(rest)
+    return st
+
+
+# ------------------------------------------------------------------ running a container spec
+def containers(objs):
+    for o in objs:
+        if o.get("kind") == "DaemonSet":
+            for c in o["spec"]["template"]["spec"]["containers"]:
+                yield o["metadata"]["name"], c
+
+
+def run_container(c, tmp_path, fi):
+    """Run container spec `c` from its image's replayed root; (returncode, stdout, stderr, kind)."""
+    images = image_map()
+    assert c["image"] in images, f"{c['image']} is not an image this build makes ({sorted(images)})"
+    df = images[c["image"]]
+    root = str(tmp_path / "root")
+    shutil.rmtree(root, ignore_errors=True)
+    os.makedirs(root)
+    st = replay(df, root)
+    argv = list(c.get("command") or st["cmd"][:1]) + list(c.get("args") if "args" in c or "command" in c
+                                                         else st["cmd"][1:])
+    cwd = root + (c.get("workingDir") or st["workdir"])
+    exe = argv[0] if argv[0].startswith("/") else os.path.normpath(os.path.join(cwd, argv[0]))
+    if argv[0].startswith("/"):
+        exe = root + argv[0]
+    assert os.access(exe, os.X_OK), f"{df}: {argv[0]} does not exist in the image (from {cwd})"
+    labeller = "labeller" in df
+    extra = (["-dry_run", "-node_name", "node-0", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)]
+             if labeller else
+             ["-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-kubelet_dir", str(tmp_path / "dp"),
+              "-exporter_socket", "", "-cdi_spec_dir", str(tmp_path / "cdi"), "-liveness_timeout", "5"])
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MI355X_")}
+    env.update({k: (root + v if v.startswith("/opt/mi355x") else v) for k, v in st["env"].items()})
+    p = subprocess.run([exe] + argv[1:] + extra, cwd=cwd, env=env, capture_output=True, text=True, timeout=120)
+    return p.returncode, p.stdout, p.stderr, "labeller" if labeller else "device-plugin"
+
+
+def check_ok(c, tmp_path, fi):
+    rc, out, err, kind = run_container(c, tmp_path, fi)
+    assert rc == 0, (c.get("command"), c.get("args"), err[-2000:])
+    doc = json.loads(out)
+    if kind == "labeller":
+        assert doc and all(k.startswith(("amd.com/", "beta.amd.com/")) for k in doc), doc
+    else:
+        devs = [d for r in doc["resources"].values() for d in r["devices"]]
+        assert doc["implementation"] == "container" and len(devs) == 8, doc
+    return doc
+
+
+@pytest.fixture(scope="module")
+def node(tmp_path_factory):
+    return make_mi355x_node(tmp_path_factory.mktemp("node"))
+
+
+# ------------------------------------------------------------------ the tests
+def test_every_image_named_is_built_here():
+    images = image_map()
+    assert set(images.values()) == {"Dockerfile", "labeller.Dockerfile", "ubi-dp.Dockerfile", "ubi-labeller.Dockerfile"}
+    named = set()
+    for m in MANIFESTS:
+        named |= {c["image"] for _, c in containers(yaml.safe_load_all(open(os.path.join(REPO, m))))}
+    named |= {c["image"] for _, c in containers(rendered_objects(CHART, {"labeller": {"enabled": True}}))}
+    assert named and named <= set(images), named - set(images)
+    assert not any("rocm/k8s-device-plugin" in i for i in named)      # never the upstream image
+
+
+@pytest.mark.parametrize("df", ["Dockerfile", "labeller.Dockerfile", "ubi-dp.Dockerfile", "ubi-labeller.Dockerfile"])
+def test_runtime_stage_has_no_interpreter(df, tmp_path):
+    """The images run the native binaries only: no Python, grpcio or protobuf."""
+    st = replay(df, str(tmp_path))
+    runs = " ".join(st["runs"])
+    assert not re.search(r"python|pip|grpcio|protobuf", runs), runs
+    bins = os.listdir(tmp_path / "opt" / "mi355x" / "bin")
+    want = {"mi355x-node-labeller"} if "labeller" in df else {"mi355x-device-plugin", "mi355x-liveness-probe"}
+    assert set(bins) == want
+    assert st["cmd"][0] == ("./k8s-node-labeller" if "labeller" in df else "./k8s-device-plugin")
+
+
+@pytest.mark.parametrize("manifest", MANIFESTS)
+def test_manifest_containers_run_from_their_image(manifest, tmp_path, node):
+    cs = list(containers(yaml.safe_load_all(open(os.path.join(REPO, manifest)))))
+    assert cs
+    for _, c in cs:
+        check_ok(c, tmp_path, node)
+
+
+CHART_VALUES = {
+    "defaults": {"labeller": {"enabled": True}},
+    "health": {"dp": {"pulse": 2, "liveness": {"enabled": True, "chipSweepEvery": 3, "perfCheckEvery": 5,
+                                                 "perfAction": "unhealthy"},
+                      "smi": {"ecc": True, "events": True, "xgmi": True}}},
+    "cdi-metrics": {"dp": {"cdi": {"enabled": True, "strategy": "device-specs,cdi-cri"}, "metricsPort": 9400}},
+    "mixed-args": {"dp": {"args": ["-resource_naming_strategy=mixed", "-allocator_search=extended"]},
+                   "labeller": {"enabled": True}, "lbl": {"args": ["-vram", "-compute-memory-partition"], "resync": 0}},
+}
+
+
+@pytest.mark.parametrize("name", sorted(CHART_VALUES))
+def test_chart_containers_run_from_their_image(name, tmp_path, node):
+    cs = list(containers(rendered_objects(CHART, CHART_VALUES[name])))
+    assert len(cs) == (2 if CHART_VALUES[name].get("labeller", {}).get("enabled") else 1)
+    for _, c in cs:
+        doc = check_ok(c, tmp_path, node)
+        if name == "cdi-metrics" and "resources" in doc:
+            assert doc["device_list_strategy"] == ["device-specs", "cdi-cri"]
+            assert (tmp_path / "cdi").is_dir() and os.listdir(tmp_path / "cdi")
+
+
+def test_a_wrong_flag_or_command_fails(tmp_path, node):
+    c = dict(next(containers(yaml.safe_load_all(open(os.path.join(REPO, "k8s-ds-amdgpu-dp-health.yaml")))))[1])
+    bad = dict(c, args=list(c["args"]) + ["-liveness_sweep_evry=3"])
+    rc, _, err, _ = run_container(bad, tmp_path, node)
+    assert rc == 1 and "flag provided but not defined: -liveness_sweep_evry" in err
+    with pytest.raises(AssertionError, match="does not exist in the image"):
+        run_container(dict(c, command=["./k8s-device-plugin-py"]), tmp_path, node)
+    with pytest.raises(AssertionError, match="is not an image this build makes"):
+        run_container(dict(c, image="docker.io/rocm/k8s-device-plugin:1.31.0.2"), tmp_path, node)

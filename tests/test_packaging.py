@@ -247,67 +247,52 @@ def test_alert_rules_use_exported_metrics():
     assert used and all(f'"{m}"' in src for m in used), sorted(m for m in used if f'"{m}"' not in src)
 
 
-def test_helm_native_daemon_switch():
-    """dp.native (the default) runs the native daemon with every chart value
-    (health, amd-smi, CDI, metrics, chip sweep, throughput check)."""
+def test_helm_runs_the_native_binaries():
+    """Every chart value runs on the native daemon / labeller: ./k8s-device-plugin
+    and ./k8s-node-labeller, which the images link to the native binaries
+    (tests/test_image_layout.py runs each rendered command from the image)."""
     t = (REPO / "helm/amd-gpu/templates/deviceplugin-daemonset.yaml").read_text()
-    assert 'command: ["./mi355x-device-plugin"]' in t and "{{- if $native }}" in t
-    assert "fail " not in t
-    native_branch = t[t.index("{{- if $native }}"):t.index("{{- else if")]
+    assert 'command: ["./k8s-device-plugin"]' in t and "$native" not in t and "else if" not in t
     for flag in ("-liveness=true", "-smi_ecc=true", "-smi_events=true", "-liveness_keep_queues", "-metrics_port",
                  "-device_list_strategy", "-cdi_spec_dir", "-smi_xgmi",
                  "-liveness_chip_sweep_every", "-perf_check_every", "-perf_action"):
-        assert flag in native_branch
-    assert "{{- $native := .Values.dp.native -}}" in t
-    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["dp"]["native"] is True
+        assert flag in t
+    values = yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())
+    assert "native" not in values["dp"] and "native" not in values["lbl"]
+    lt = (REPO / "helm/amd-gpu/templates/labeller.yaml").read_text()
+    assert 'command: ["./k8s-node-labeller"]' in lt and "lbl.native" not in lt
+    for df in ("Dockerfile", "ubi-dp.Dockerfile"):
+        assert "ln -s /opt/mi355x/bin/mi355x-device-plugin /root/k8s-device-plugin" in (REPO / df).read_text(), df
+    for df in ("labeller.Dockerfile", "ubi-labeller.Dockerfile"):
+        assert "ln -s /opt/mi355x/bin/mi355x-node-labeller /root/k8s-node-labeller" in (REPO / df).read_text(), df
 
 
-def test_launcher_dispatches_native_first(tmp_path):
-    """./k8s-device-plugin (the image command) runs the native daemon (here its
-    -dry_run report); a Python-only flag (-grpc_server) runs the Python CLI."""
+def test_launchers_run_the_native_binaries(tmp_path):
+    """scripts/k8s-device-plugin and scripts/k8s-node-labeller (a source
+    checkout's ./k8s-*) exec the native binaries; the labeller's labels equal
+    the Python labeller's (the test oracle)."""
     import subprocess
     import sys
     from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
     launcher = str(REPO / "scripts/k8s-device-plugin")
     p = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=60)
-    assert p.returncode == 0 and "mi355x-device-plugin" in p.stdout and "-liveness_probe" in p.stdout, p.stderr
+    assert p.returncode == 0 and "mi355x-device-plugin version" in p.stdout and "-liveness_probe" in p.stdout
     fi = make_mi355x_node(tmp_path / "n")
     base = [launcher, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket", "",
             "-kubelet_dir", str(tmp_path / "dp")]
     p = subprocess.run(base, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and json.loads(p.stdout)["resources"], p.stderr[-2000:]
-    assert "native daemon" in p.stderr                      # mi355x-device-plugin's banner
+    assert "native daemon" in p.stderr
     p = subprocess.run(base + ["-grpc_server", "aio"], capture_output=True, text=True, timeout=120)
-    assert p.returncode == 0 and json.loads(p.stdout)["resources"], p.stderr[-2000:]
-    assert "native daemon" not in p.stderr
-    env = dict(os.environ, MI355X_DP_IMPL="python")
-    p = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=120, env=env)
-    assert p.returncode == 0 and "-grpc_server" in p.stdout
-
-
-def test_helm_native_labeller_switch():
-    """lbl.native (the default) runs the native labeller from the labeller images."""
-    t = (REPO / "helm/amd-gpu/templates/labeller.yaml").read_text()
-    assert 'command: ["./mi355x-node-labeller"]' in t and "{{- if .Values.lbl.native }}" in t
-    assert 'command: ["./k8s-node-labeller"]' in t
-    assert yaml.safe_load((REPO / "helm/amd-gpu/values.yaml").read_text())["lbl"]["native"] is True
-    for df in ("labeller.Dockerfile", "ubi-labeller.Dockerfile"):
-        assert "bin/mi355x-node-labeller /root/mi355x-node-labeller" in (REPO / df).read_text(), df
-
-
-def test_labeller_launcher_dispatches_native_first(tmp_path):
-    """./k8s-node-labeller runs the native labeller; MI355X_LBL_IMPL=python the Python one."""
-    import subprocess
-    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
-    launcher = str(REPO / "scripts/k8s-node-labeller")
-    fi = make_mi355x_node(tmp_path / "n")
-    args = [launcher, "-dry_run", "-node_name", "n", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
-            "-vram", "-device-id"]
-    nat = subprocess.run(args, capture_output=True, text=True, timeout=60)
-    py = subprocess.run(args, capture_output=True, text=True, timeout=120, env=dict(os.environ, MI355X_LBL_IMPL="python"))
+    assert p.returncode == 1 and "flag provided but not defined: -grpc_server" in p.stderr
+    lbl = str(REPO / "scripts/k8s-node-labeller")
+    args = ["-dry_run", "-node_name", "n", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-vram", "-device-id"]
+    nat = subprocess.run([lbl, *args], capture_output=True, text=True, timeout=60)
+    py = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.node_labeller", *args],
+                        capture_output=True, text=True, timeout=120, cwd=str(REPO))
     assert nat.returncode == 0 and py.returncode == 0, (nat.stderr[-1000:], py.stderr[-1000:])
     assert json.loads(nat.stdout) == json.loads(py.stdout)
-    h = subprocess.run([launcher, "-h"], capture_output=True, text=True, timeout=60)
+    h = subprocess.run([lbl, "-h"], capture_output=True, text=True, timeout=60)
     lines = h.stdout.splitlines()   # the native binary answered: its version banner, then the usage
     assert lines[0].startswith("AMD GPU Node Labeller") and "mi355x-node-labeller version " in lines[1]
     assert lines[3].startswith("usage: ")
