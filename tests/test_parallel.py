@@ -177,7 +177,7 @@ def test_bench_extras_deadline_keeps_the_headline():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0 and d["ms_per_step"] > 0
     inc = d["extra"]["extras_incomplete"]
-    assert inc["deadline_s"] == 0.5 and inc["stage"] and inc["error"] is None
+    assert inc["deadline_s"] == 0.5 and inc["stage"] and inc["error"] is None, (inc, err[-3000:])
     # the timed loop's own numbers are all there
     e = d["extra"]
     assert len(e["steps_ms"]) == 2 and e["bench_process_gpu"]["clean"] and e["plugin"] == "native-daemon"
@@ -190,3 +190,83 @@ def test_bench_extras_deadline_keeps_the_headline():
             break
         time.sleep(0.1)
     assert not left, left
+
+
+# ------------------------------------------------------------------ the driver's multi-GPU run, rehearsed on CPU
+def _ps_group(pgid):
+    ps = subprocess.run(["ps", "-eo", "pgid=,stat=,cmd="], capture_output=True, text=True).stdout
+    return [l for l in ps.splitlines() if l.split(None, 2)[0] == str(pgid) and not l.split()[1].startswith("Z")]
+
+
+def _bench_ranks(n, *args, torchrun=True, timeout=300):
+    """bench.py as the driver launches it at N (torchrun, one rank per GPU) on the
+    synthetic 8x MI355X node; returns (the one JSON line, stderr). Fails if
+    anything of the run's process group (a plugin daemon, a rank) outlives it."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    if torchrun:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(n), "--master-addr",
+               "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(n), "--fixture", *args]
+    else:
+        cmd = [sys.executable, "bench.py", "--gpus", str(n), "--fixture", *args]
+    proc = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                            start_new_session=True)
+    t0 = time.monotonic()
+    try:
+        out, err = proc.communicate(timeout=timeout)
+    finally:
+        if proc.poll() is None:
+            os.killpg(proc.pid, 9)
+    assert proc.returncode == 0, err[-3000:]
+    assert time.monotonic() - t0 < timeout
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    for _ in range(40):            # a SIGKILLed daemon may linger for a moment
+        left = _ps_group(proc.pid)
+        if not left:
+            break
+        time.sleep(0.1)
+    assert not left, left
+    return json.loads(lines[0]), err
+
+
+@pytest.mark.parametrize("n,mode", [(4, "pod"), (4, "per-gpu"), (8, "pod"), (8, "per-gpu")])
+def test_bench_torchrun_n_ranks_on_the_fixture(n, mode):
+    """BASELINE configs #3 / #5 at N = 4 and 8 under torchrun, in both container
+    modes: one headline line from rank 0 with N ranks' state, gloo
+    collectives over N ranks, and the allocated set's fabric (one xGMI hive,
+    N(N-1)/2 links)."""
+    d, _ = _bench_ranks(n, "--steps", "3", "--warmup", "1", "--container-mode", mode, "--mode-compare", "2",
+                        "--fragmented-compare", "2")
+    e = d["extra"]
+    assert d["n_gpus"] == n and d["steps"] == 3 and d["value"] > 0 and "extras_incomplete" not in e
+    assert e["launcher"] == "torchrun" == d["config"]["launcher"] and e["container_mode"] == mode
+    assert e["bench_process_gpu"]["clean"] and len(e["bench_process_gpu"]["ranks"]) == n
+    assert e["rccl"]["backend"] == "gloo" and e["rccl"]["ok"]
+    assert all(r["ranks"] == n for r in e["rccl"]["rows"])
+    assert e["fabric"]["one_hive"] and e["fabric"]["pairs"]["xgmi"] == n * (n - 1) // 2
+    other = "per-gpu" if mode == "pod" else "pod"
+    assert e[f"latency_p50_ms_container_mode_{other}"] > 0
+    assert e["timed_allocation"]["advertised"] == n and len(e["steps_ms"]) == 3
+
+
+def test_bench_torchrun_8_ranks_extras_deadline_fires():
+    """At 8 ranks a deadline that fires inside the extras (rank 0 leaves while
+    the others wait in a collective): still exactly one headline line, every
+    rank exits 0, no daemon left."""
+    d, err = _bench_ranks(8, "--steps", "2", "--warmup", "1", "--extras-deadline", "0.5")
+    e = d["extra"]
+    inc = e["extras_incomplete"]
+    assert inc["deadline_s"] == 0.5 and inc["stage"], inc
+    assert d["n_gpus"] == 8 and len(e["steps_ms"]) == 2 and e["bench_process_gpu"]["clean"]
+    assert len(e["bench_process_gpu"]["ranks"]) == 8
+    assert "exceeded --extras-deadline" in err or "failed:" in err
+
+
+def test_bench_single_process_8_gpus_on_the_fixture():
+    """python bench.py --gpus 8 --fixture (no torchrun): the launcher is the
+    single process, one pod with 8 GPUs, no collectives."""
+    d, _ = _bench_ranks(8, "--steps", "3", "--warmup", "1", torchrun=False)
+    e = d["extra"]
+    assert d["n_gpus"] == 8 and e["launcher"] == "single-process" and e["rccl"] is None
+    assert e["bench_process_gpu"]["clean"] and len(e["bench_process_gpu"]["ranks"]) == 1
+    assert e["fabric"]["pairs"]["xgmi"] == 28 and e["timed_allocation"]["advertised"] == 8
