@@ -24,7 +24,7 @@ GPUs advertised at 1/2/4/8 MI355X"). One timed step is one pod admission:
      processes exit and the driver tears down their kfd processes. The next
      admission starts once /sys/class/kfd/kfd/proc no longer lists them
      (--settle kfd); with --settle none it would start inside that teardown and
-     block ~100-150 ms in open("/dev/kfd") (profiles/README.md §3c) — reported
+     block ~100-150 ms in open("/dev/kfd") (profiles/archive/measurements_r1_r3.md §3c) — reported
      as latency_p50_ms_back_to_back.
 
 The plugin is the real one: by default the native daemon mi355x-device-plugin

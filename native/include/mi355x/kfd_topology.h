@@ -112,7 +112,7 @@ class KfdTopology {
   const std::string& nodes_dir() const { return nodes_dir_; }
   // Node directories whose properties file exists but cannot be read. kfd
   // answers EPERM for GPUs the reader's device cgroup denies (measured on the
-  // gpurun box: 7 of 8 GPU nodes, profiles/sysfs_access_box.json), so these
+  // gpurun box: 7 of 8 GPU nodes, profiles/archive/sysfs_access_box.json), so these
   // are GPUs the process cannot see through kfd, not missing GPUs.
   const std::vector<int>& unreadable_node_ids() const { return unreadable_; }
 

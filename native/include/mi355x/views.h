@@ -5,7 +5,7 @@
 //   node view      /sys/devices/system/node without the per-CPU cache
 //                  descriptors ROCr walks at start-up (7,650 of hsa_init's 9,486
 //                  sysfs opens on a 256-CPU MI355X host; hsa_init 48 -> 14-16 ms
-//                  in emulation, profiles/README.md §3e). Everything else stays
+//                  in emulation, profiles/archive/measurements_r1_r3.md §3e). Everything else stays
 //                  live: symlinks into the real node directory, bind-mounted
 //                  read-only at an alias path, and into /sys/devices/system/cpu.
 //   topology view  per distinct allocated GPU set, a copy of the kfd topology

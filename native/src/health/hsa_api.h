@@ -1,7 +1,7 @@
 // ROCr entry points used by the HSA-direct probe, resolved at run time.
 //
 // libhsa-runtime64's static constructors cost ~8.7 ms per process (measured:
-// dlopen 10.3 ms vs 0.1 ms of relocation, profiles/README.md §3d). Linked
+// dlopen 10.3 ms vs 0.1 ms of relocation, profiles/archive/measurements_r1_r3.md §3d). Linked
 // normally, that cost is paid before main() and nothing can overlap it.
 // Loaded with dlopen() from main(), it runs while another thread opens
 // /dev/kfd — the kernel-side kfd process creation, the other fixed cost of a

@@ -91,10 +91,10 @@ MI355X_HD uint32_t sweep_lds_pattern(uint32_t i, uint32_t nonce, uint32_t wg) {
 #define MI355X_PERF_THREADS 256
 // grid shapes measured on MI355X: plain 16-byte stores peak at 1 workgroup
 // per CU (5.8 TB/s vs 5.3-5.4 at 4 per CU; nontemporal stores are slower;
-// tools/experiments/hbm_{stream,fill}_variants.hip, 8 GiB). For loads, 16 per CU wins on repeated
+// tools/archive/experiments/hbm_{stream,fill}_variants.hip, 8 GiB). For loads, 16 per CU wins on repeated
 // passes over 8 GiB (6.5-6.7 TB/s vs 6.3) but loses on the check's single
 // pass right after the fill (1-4 GiB: 3.8-4.8 TB/s vs 5.0-6.1 at 8 per CU,
-// tools/gpurun_perfcheck.sh), so the check uses 8.
+// tools/archive/gpurun_perfcheck.sh), so the check uses 8.
 #define MI355X_HBM_FILL_WGS_PER_CU 1
 #define MI355X_HBM_CHECK_WGS_PER_CU 8
 #define MI355X_BURN_WGS_PER_CU 2   // 8 waves per CU = 2 per SIMD

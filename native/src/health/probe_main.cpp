@@ -387,10 +387,10 @@ std::string devices_json(const std::vector<mi355x_probe_result>& results) {
 // (PR_SET_PDEATHSIG). Spawning a fresh probe process per pulse would create
 // and tear down a kfd process each time, and a GPU process that starts while
 // such a teardown is in flight blocks in open("/dev/kfd") for up to ~150 ms
-// (profiles/README.md §3c): a pod admitted during a health sweep would pay it.
+// (profiles/archive/measurements_r1_r3.md §3c): a pod admitted during a health sweep would pay it.
 // With --keep the per-device queue, executable and buffers also stay: a probe
 // is then one AQL packet, with no queue creation (an HWS runlist update that
-// preempts every queue on that GPU, ~5 ms, profiles/README.md §3f) per pulse.
+// preempts every queue on that GPU, ~5 ms, profiles/archive/measurements_r1_r3.md §3f) per pulse.
 int serve(int n, uint64_t t_start, uint64_t t_runtime) {
   prctl(PR_SET_PDEATHSIG, SIGKILL);
   if (getppid() == 1) return 0;  // parent already gone
@@ -620,7 +620,7 @@ int main(int argc, char** argv) {
   std::fflush(stdout);
   // After the verdict. The exit mode was an experiment: the kernel's kfd
   // process teardown after we are gone costs the same either way
-  // (profiles/README.md §3c).
+  // (profiles/archive/measurements_r1_r3.md §3c).
   const int code = all_ok ? 0 : 1;
   if (exit_mode == "fast") std::_Exit(code);
   teardown();

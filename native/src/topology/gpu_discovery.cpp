@@ -63,7 +63,7 @@ bool bdf_location(const std::string& bdf, int* domain, int* location) {
 // unique_id as hex on the PCI device ("%016llx") and kfd prints the same
 // value in decimal; the xGMI hive id is the same decimal number kfd shows as
 // hive_id. Both are plain device attributes (no device-cgroup check), unlike
-// every file under a kfd GPU node (profiles/sysfs_access_box.json).
+// every file under a kfd GPU node (profiles/archive/sysfs_access_box.json).
 void recover_from_sysfs(GpuDevice* g, const std::string& dev_dir) {
   if (auto v = read_trimmed(path_join(dev_dir, "unique_id"))) {
     std::string hex = *v;
@@ -191,7 +191,7 @@ DiscoveryResult discover_gpus(const std::string& sysfs_root, const KfdTopology& 
   // that follows a GPU's primary card/render minor belongs to that GPU, and
   // partition i (i >= 1) of it uses the block's i-th xcp device. On the
   // MI355X box: GPU card0 -> amdgpu_xcp_0..6 = card1..7, card8 -> xcp_7..13 =
-  // card9..15 (profiles/sysfs_access_box.json). Used only for GPUs whose kfd
+  // card9..15 (profiles/archive/sysfs_access_box.json). Used only for GPUs whose kfd
   // nodes are unreadable; kfd's own render-minor map decides otherwise.
   std::vector<const GpuDevice*> primaries;
   for (auto& p : pci_devs)

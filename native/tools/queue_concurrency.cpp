@@ -2,7 +2,7 @@
 // (measurement tool, not shipped)
 //
 // A pod-mode container with N GPUs creates 2N queues (its own + ROCr's
-// internal one per GPU, profiles/README.md §3f); each is ~3.7 ms of
+// internal one per GPU, profiles/archive/measurements_r1_r3.md §3f); each is ~3.7 ms of
 // AMDKFD_IOC_SVM (the 181 MB CWSR area) + 1 ms of CREATE_QUEUE. The SVM call
 // takes the process' mmap lock and CREATE_QUEUE the process-wide kfd mutex,
 // so N threads creating queues on N GPUs would run one after another. On a

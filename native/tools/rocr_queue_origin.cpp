@@ -2,7 +2,7 @@
 // each one costs in host memory (measurement tool, not shipped).
 //
 // The persistent probe server holds two 181 MB context-save (CWSR) areas per
-// GPU (profiles/README.md §3f, §3i): its own queue and one ROCr creates
+// GPU (profiles/archive/measurements_r1_r3.md §3f, §3i): its own queue and one ROCr creates
 // behind the API. This tool interposes ioctl() (the executable exports it,
 // -rdynamic; ROCr's thunk resolves ioctl against the executable first) and,
 // for every AMDKFD_IOC_CREATE_QUEUE, records the arguments the thunk passes

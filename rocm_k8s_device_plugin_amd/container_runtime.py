@@ -77,7 +77,7 @@ def wait_kfd_released(entries: Iterable[str], timeout_s: float = 0.5, proc_dir: 
     A GPU process's kfd teardown continues for ~150 ms after the process has
     exited, and any GPU process that starts meanwhile blocks in
     open("/dev/kfd") until it is done (measured on MI355X,
-    profiles/README.md §3c). The procfs entry disappears exactly when the
+    profiles/archive/measurements_r1_r3.md §3c). The procfs entry disappears exactly when the
     teardown completes, so this is the point at which the previous pod has
     really terminated — what kubelet waits for before reusing its devices.
     The entries are host PIDs that appeared while our container ran, so another

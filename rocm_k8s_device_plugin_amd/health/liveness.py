@@ -4,7 +4,7 @@ Two modes, both under a hard deadline enforced from here:
 
 ``persistent`` (default): one long-lived ``mi355x-liveness-probe --serve``
 child keeps the GPU runtime initialised and answers one request per sweep,
-probing every device in parallel. Measured on MI355X (profiles/README.md §3c):
+probing every device in parallel. Measured on MI355X (profiles/archive/measurements_r1_r3.md §3c):
 each GPU process that exits leaves ~150 ms of kfd teardown in the kernel, and a
 GPU process that starts meanwhile (a pod's runtime init) blocks in
 ``open("/dev/kfd")`` for it. A prober that spawned a process per device per

@@ -84,7 +84,7 @@ class HealthConfig:
     # (or their queues leaving fewer than 2 of the GPU's kfd num_cp_queues)
     # the HWS runlist is oversubscribed and every extra process/queue lengthens
     # the tenants' time slices (measured: 8 tenant processes x 4 queues, p99.9
-    # GEMM 14 -> 34 ms with the kept probe queue, profiles/README.md §3n). The
+    # GEMM 14 -> 34 ms with the kept probe queue, profiles/archive/measurements_r1_r3.md §3n). The
     # probe server then steps off that GPU (no queue, no runlist slot); while
     # the GPU reports GFX activity its tenants are the liveness evidence, at 0%
     # it is probed from a fresh process. 0 = off.
@@ -99,7 +99,7 @@ class HealthConfig:
     # device's share of a whole MI355X's 256 CUs) or an XCD clocked far below
     # its siblings make the GPU "degraded": logged and exported, and with
     # perf_action "unhealthy" withdrawn until a later check passes. Floors are
-    # about half of what an MI355X measures (profiles/README.md §10).
+    # about half of what an MI355X measures (profiles/archive/measurements_r1_r3.md §10).
     perf_check_every: int = 0
     perf_mib: int = 4096
     perf_mfma_iters: int = 65536

@@ -7,7 +7,7 @@ looks like — XCDs, CUs, HBM, xGMI links, partition modes — so that
 
 * discovery can flag a node whose partitions do not add up (a half-applied
   partition switch, stale ``amdgpu_xcp_*`` platform devices: both seen on real
-  MI355X hosts, profiles/README.md §5) instead of advertising it silently
+  MI355X hosts, profiles/archive/measurements_r1_r3.md §5) instead of advertising it silently
   (``check_inventory``);
 * the fabric model (``parallel/fabric.py``) has a per-link bandwidth when the
   kfd io_links do not report one;
@@ -15,7 +15,7 @@ looks like — XCDs, CUs, HBM, xGMI links, partition modes — so that
   same numbers the checks use.
 
 Every entry says where its numbers come from: ``measured`` = read on a real
-MI355X gpurun box (profiles/real_sysfs_inventory_box.json,
+MI355X gpurun box (profiles/archive/real_sysfs_inventory_box.json,
 amdsmi_snapshot_box.json, drm_info_box.json); ``reference-fixture`` = the
 captured sysfs trees under /root/reference/testdata (SURVEY §2.1 C28);
 ``spec`` = vendor specification, not verified here.

@@ -1,6 +1,6 @@
 """NUMA-node sysfs view without per-CPU cache descriptors (opt-in: ``-node_view``).
 
-Measured on an 8x MI355X host with 256 CPUs (profiles/README.md §3e): ROCr's
+Measured on an 8x MI355X host with 256 CPUs (profiles/archive/measurements_r1_r3.md §3e): ROCr's
 ``hsa_init`` opens 9,486 sysfs files, and 7,650 of them are the CPU cache
 descriptors it reaches through ``/sys/devices/system/node/node<N>/cpu<M>/cache/
 index<K>/*`` — for every CPU of the host, whatever the container's cpuset.

@@ -62,7 +62,7 @@ class FixtureSpec:
     # "compact": one amdgpu_xcp_<8g+p> per extra partition, drm minors numbered
     # over active partitions only (the reference test-ID scheme).
     # "kernel": what amdgpu does (amdgpu_xcp_dev_alloc; measured on the MI355X
-    # box, profiles/sysfs_access_box.json): every GPU owns a block of 8 drm
+    # box, profiles/archive/sysfs_access_box.json): every GPU owns a block of 8 drm
     # minors in probe order (its own + 7 amdgpu_xcp_* devices, present even in
     # SPX), xcp index 7*rank + slot - 1; inactive slots have no kfd node.
     xcp_layout: str = "compact"
@@ -339,7 +339,7 @@ def make_mi355x_node(root: os.PathLike, spec: Optional[FixtureSpec] = None, **kw
 def deny_kfd_nodes(fi: FixtureInfo, node_ids) -> None:
     """Make kfd GPU nodes unreadable the way a device cgroup does: kfd then
     answers EPERM for every file under the node (properties, gpu_id, name,
-    io_links, p2p_links, mem_banks; profiles/sysfs_access_box.json). Tests run
+    io_links, p2p_links, mem_banks; profiles/archive/sysfs_access_box.json). Tests run
     as root, which ignores permission bits, so each file becomes a directory:
     it still exists but cannot be read as a file."""
     nodes = fi.sysfs / "class/kfd/kfd/topology/nodes"

@@ -2,7 +2,7 @@
 
 kfd answers EPERM for every file under the topology node of a GPU the
 reader's device cgroup denies: the gpurun box shows 7 of 8 GPU nodes that way
-(profiles/sysfs_access_box.json), and a non-privileged plugin pod without
+(profiles/archive/sysfs_access_box.json), and a non-privileged plugin pod without
 /dev (the drop-in Helm chart's default) sees all of them that way. The
 reference then drops every amdgpu_xcp_* partition (its render node is not in
 the kfd map, internal/pkg/amdgpu/amdgpu.go:521-565) and places by weight 0

@@ -31,7 +31,7 @@ def test_view_hides_only_node_relative_cpu_caches(tmp_path):
     root = _sysfs(tmp_path)
     src = root / "devices/system/node"
     dst = tmp_path / "view"
-    # alias = the real directory itself, as in tools/experiments/view_emulation.py
+    # alias = the real directory itself, as in tools/archive/experiments/view_emulation.py
     links, hidden = build_node_view(str(src), str(dst), alias=str(src), cpu_root=str(root / "devices/system/cpu"))
     assert hidden == 6
     # live files through symlinks, CPU entries except the cache directory

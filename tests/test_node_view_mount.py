@@ -3,7 +3,7 @@ namespace — skipped otherwise).
 
 The GPU box cannot bind-mount (no root, no user namespaces), so the view's
 effect on ROCr is measured there with the mounts emulated by path
-redirection (profiles/README.md §3e). What a container runtime does with the
+redirection (profiles/archive/measurements_r1_r3.md §3e). What a container runtime does with the
 Allocate mounts — bind the real node directory at the alias, then the view
 over /sys/devices/system/node, both read-only and in that order — is done here
 for real on this host's sysfs, and generic consumers are checked inside the

@@ -856,7 +856,7 @@ def _busy_gpu(fi, inv, dev_id, pid="777"):
 @pytest.mark.parametrize("busy,grace,unhealthy_after", [(True, 300.0, None), (True, 0.0, 2), (False, 300.0, 2)])
 def test_liveness_pending_behind_tenant(tmp_path, busy, grace, unhealthy_after):
     """A probe whose dispatch stays queued behind a tenant's kernel (measured on
-    MI355X: 390 ms waits behind 441 ms GEMMs, profiles/README.md) is
+    MI355X: 390 ms waits behind 441 ms GEMMs, profiles/archive/measurements_r1_r3.md) is
     inconclusive on a GPU that runs other processes' queues, for up to
     -liveness_busy_grace; on an idle GPU, or after the grace, it is a failure
     (confirmed in a fresh process first)."""

@@ -97,7 +97,7 @@ def test_discover_mi355x_modes(tmp_path, mode, parts, nps):
 
 
 def test_real_box_layout_quirks(tmp_path):
-    """What the MI355X box showed (profiles/README.md §5): SPX, yet 7 amdgpu_xcp_*
+    """What the MI355X box showed (profiles/archive/measurements_r1_r3.md §5): SPX, yet 7 amdgpu_xcp_*
     platform devices per GPU with drm nodes that kfd does not know; those must not
     become kubelet devices."""
     fi = make_mi355x_node(tmp_path)

@@ -18,7 +18,7 @@ and reports, per layout, the share of requests where the default's total pair
 weight exceeds the optimum, the mean / max excess, how many more physical GPUs
 the default's set spans, and both searches' time.
 
-  python tools/alloc_gap.py [--samples 2000] [--json-out profiles/allocator_default_vs_optimum.json]
+  python tools/alloc_gap.py [--samples 2000] [--json-out profiles/archive/allocator_default_vs_optimum.json]
 """
 from __future__ import annotations
 

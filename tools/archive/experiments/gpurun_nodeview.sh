@@ -7,7 +7,7 @@ HSACO="$PWD/rocm_k8s_device_plugin_amd/kernels/liveness_gfx950.hsaco"
 g++ -O2 -std=c++17 -rdynamic -DMI355X_PROBE_HSA=1 -DMI355X_HSACO_PATH="\"$HSACO\"" -Inative/include -Inative/src/health \
   -I/opt/rocm/include native/src/health/probe_main.cpp native/src/health/hsa_probe.cpp native/tools/probe_emu.cpp \
   -o gpurun_out/probe_emu -ldl -pthread || exit 1
-python tools/experiments/view_emulation.py /tmp/mi355x_views > gpurun_out/view_emulation.json || exit 1
+python tools/archive/experiments/view_emulation.py /tmp/mi355x_views > gpurun_out/view_emulation.json || exit 1
 spec() { python -c "import json;print(json.load(open('gpurun_out/view_emulation.json'))['$1'])"; }
 NODE=$(spec node); BOTH=$(spec both)
 sweep() {  # tag, extra args...

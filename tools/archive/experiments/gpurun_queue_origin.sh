@@ -18,7 +18,7 @@ run() {
     | sed "s/^{/{\"variant\":\"$label\",/" >> $OUT || return 1
   env "$@" ROCR_VISIBLE_DEVICES=0 timeout -k 5 60 gpurun_out/rqo "$CO" --code-first \
     | sed "s/^{/{\"variant\":\"$label\",/" >> $OUT || return 1
-  env "$@" timeout -k 5 90 python3 tools/experiments/queue_origin_rss.py "$label" >> $RSS || return 1
+  env "$@" timeout -k 5 90 python3 tools/archive/experiments/queue_origin_rss.py "$label" >> $RSS || return 1
   echo "variant $label done"
 }
 run default X=1 \

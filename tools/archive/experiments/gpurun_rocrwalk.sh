@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 g++ -O2 -std=c++17 -rdynamic -I/opt/rocm/include native/tools/rocr_initprof.cpp -o gpurun_out/rocr_initprof -ldl -pthread || exit 1
-python tools/experiments/view_emulation.py /tmp/mi355x_views > gpurun_out/view_emulation.json || exit 1
+python tools/archive/experiments/view_emulation.py /tmp/mi355x_views > gpurun_out/view_emulation.json || exit 1
 cat gpurun_out/view_emulation.json | cut -c1-400; echo
 spec() { python -c "import json;print(json.load(open('gpurun_out/view_emulation.json'))['$1'])"; }
 run() {  # label, env assignment...; 12 fresh processes, 300 ms apart (past the previous kfd teardown)

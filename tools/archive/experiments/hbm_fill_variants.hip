@@ -1,4 +1,4 @@
-// Write shapes for the throughput check's fill pass (tools/experiments/gpurun_hbm_variants.sh):
+// Write shapes for the throughput check's fill pass (tools/archive/experiments/gpurun_hbm_variants.sh):
 // 16 B per lane grid-stride (current) vs 64 B contiguous per lane, dword stores, and grid sizes.
 #include <hip/hip_runtime.h>
 #include <algorithm>

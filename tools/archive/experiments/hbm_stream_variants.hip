@@ -1,4 +1,4 @@
-// Store / load shapes for the throughput check's HBM kernels (tools/gpurun_perfcheck.sh):
+// Store / load shapes for the throughput check's HBM kernels (tools/archive/gpurun_perfcheck.sh):
 // which one reaches the achievable HBM rate on MI355X. hipcc --offload-arch=gfx950 -O3.
 #include <hip/hip_runtime.h>
 #include <cstdio>

@@ -5,7 +5,7 @@ real plugin (fake kubelet, ListAndWatch), with a Chrome trace.
 Reports per-sweep latency, per-device probe latency and the verdicts; every
 accessible device must stay Healthy for the whole run.
 
-  python tools/experiments/health_sweep_gpu.py --sweeps 20 --out gpurun_out/health_sweep.json --trace t.json
+  python tools/archive/experiments/health_sweep_gpu.py --sweeps 20 --out gpurun_out/health_sweep.json --trace t.json
 """
 from __future__ import annotations
 

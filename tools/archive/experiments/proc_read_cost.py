@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Cost of the /proc and sysfs files a GPU runtime parses at start-up.
 
-  python tools/experiments/proc_read_cost.py --out gpurun_out/proc_read_cost.json
+  python tools/archive/experiments/proc_read_cost.py --out gpurun_out/proc_read_cost.json
 """
 import argparse
 import glob

@@ -1,6 +1,6 @@
 """RSS and kfd queues of the kept-queue probe server under the current env.
 
-Runs by tools/experiments/gpurun_queue_origin.sh once per ROCr env variant
+Runs by tools/archive/experiments/gpurun_queue_origin.sh once per ROCr env variant
 (the prober passes its environment to the server): two probes, then the
 server's VmRSS and the types of its kfd queues. One JSON line.
 """

@@ -3,7 +3,7 @@
 the MI355X_INITPROF_REDIRECT specs that make native/tools/rocr_initprof.cpp
 see them where the container would (in-process stand-in for the bind mounts).
 
-  python tools/experiments/view_emulation.py OUTDIR   -> JSON {"node": spec, "topology": spec, "both": spec, ...}
+  python tools/archive/experiments/view_emulation.py OUTDIR   -> JSON {"node": spec, "topology": spec, "both": spec, ...}
 """
 import json
 import os

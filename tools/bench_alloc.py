@@ -10,7 +10,7 @@
    node: GetPreferredAllocation + Allocate p50/p99 at 1/2/4/8 GPUs, whole node
    free and fragmented, and on the 8x8 CPX node; native server and grpc.aio.
 
-  python tools/bench_alloc.py --out profiles/alloc_bench.json
+  python tools/bench_alloc.py --out profiles/archive/alloc_bench.json
 """
 from __future__ import annotations
 

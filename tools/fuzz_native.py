@@ -9,7 +9,7 @@ emulation in testing/gopeer.py, the kubelet protobuf messages, fixture Nodes
 and kubeconfigs), runs every target for a time budget and writes a JSON
 summary (executions, coverage, corpus, findings).
 
-    python tools/fuzz_native.py --seconds 600 --json profiles/r3/fuzz_native.json
+    python tools/fuzz_native.py --seconds 600 --json profiles/archive/r3/fuzz_native.json
     python tools/fuzz_native.py --targets h2_server,dp_rpc --seconds 60
 
 A finding leaves its reproducer in <work>/artifacts/<target>/; re-run it with

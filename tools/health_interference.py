@@ -10,7 +10,7 @@ p50 Allocate->ready latency of those containers for:
   persistent  one long-lived probe server (--serve)
 
 Every GPU process that exits leaves kfd teardown work behind that blocks the
-next process' open("/dev/kfd") (profiles/README.md §3c), so the spawn mode is
+next process' open("/dev/kfd") (profiles/archive/measurements_r1_r3.md §3c), so the spawn mode is
 expected to inject that wait into container start-up; the server does not.
 
   python tools/health_interference.py --containers 15 --pulse 0.3 --out gpurun_out/health_interference.json

@@ -3,7 +3,7 @@
 
 Each kfd queue on MI355X carries a context-save (CWSR) area of
 num_xcc x cwsr_size = 8 x 22.7 MB = 181 MB that ROCr's thunk maps for the GPU
-(profiles/README.md §3f). The kept-queue server (`-liveness_keep_queues`,
+(profiles/archive/measurements_r1_r3.md §3f). The kept-queue server (`-liveness_keep_queues`,
 default) holds its queues between pulses, so this measures what that costs
 the node: the server's RSS / anonymous / pinned memory and the host's
 MemAvailable, before and after the first sweep, with and without kept queues.
