@@ -703,6 +703,7 @@ def main():
 
     rpc_ms, alloc_rpc_ms, lat_ms, ready_ms, kern_us = [], [], [], [], []
     exec_ms, rt_ms, dev_ms, settle_ms, prespawn_ms, setup_ms, launch_ms = [], [], [], [], [], [], []
+    dev_phases = []   # per timed step: the slowest device's set-up phases (probe phase_us)
     gpu_state = {"torch_cuda_initialized": False, "kfd_fds": 0, "render_fds": 0}   # worst seen in the timed loop
     from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
 
@@ -737,7 +738,7 @@ def main():
         t0, ordl, tot, amsl, ids, mounts, groups = payload
         if mode == "pod" and d.rank != 0:
             # the pod's single container runs on rank 0; other ranks only keep step
-            mine = (True, 0, 0.0, "", (0, 0, 0, 0.0))
+            mine = (True, 0, 0.0, "", (0, 0, 0, 0.0, {}))
             lingering = frozenset()
         else:
             pod = mode == "pod" or d.world == 1
@@ -752,8 +753,11 @@ def main():
                          mounts=mounts if not args.fixture else (), device_paths=paths, **stub)
             kus = max((dv.get("kernel_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
             # device set-up (HIP: hipSetDevice .. stream/buffers/events; HSA: queue, code object, buffers)
-            sus = max((dv.get("setup_us", 0.0) for dv in r.doc.get("devices", [])), default=0.0)
-            phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)), sus / 1e3)
+            devs = r.doc.get("devices", [])
+            sus = max((dv.get("setup_us", 0.0) for dv in devs), default=0.0)
+            slow_dev = max(devs, key=lambda dv: dv.get("total_us", 0.0), default={})
+            phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)), sus / 1e3,
+                      slow_dev.get("phase_us") or {})
             mine = (r.ok, r.t_ready_ns, kus, r.error, phases)
             lingering = r.kfd_lingering
         if record:   # the containers are up: does the bench / plugin process hold the GPU?
@@ -787,7 +791,7 @@ def main():
         waited = blocking(wait_kfd_released, lingering, timeout_s=cap) if settle == "kfd" else 0.0
         if record:
             settle_ms.append(waited)
-        sp, tm, trt, su = slowest[4]   # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC), device set-up ms
+        sp, tm, trt, su, dph = slowest[4]   # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC), set-up ms, phases
         if sink is not None:
             sink.append((t_ready - t0) / 1e6)
         if init_sink is not None:
@@ -802,6 +806,7 @@ def main():
             rt_ms.append((trt - tm) / 1e6)
             dev_ms.append((t_ready - trt) / 1e6)
             setup_ms.append(min(su, (t_ready - trt) / 1e6))
+            dev_phases.append(dph)
             launch_ms.append(max(0.0, (t_ready - trt) / 1e6 - su))
             prespawn_ms.append(max(0.0, (sp - t0) / 1e6 - tot))
 
@@ -852,6 +857,11 @@ def main():
                                             "gpu_runtime_init": round(pct(rt_ms, .5), 3),
                                             "device_setup": round(pct(setup_ms, .5), 3),
                                             "launch_and_verify": round(pct(launch_ms, .5), 3)},
+                # device_setup + launch_and_verify of the slowest GPU, as the container entrypoint timed them
+                # (HIP: hipSetDevice + identity, stream = its hardware queue, pinned / device buffers + events,
+                # launch -> verified tile; HSA: code object, queue, buffers, dispatch)
+                "device_phases_p50_us": {k: round(pct([p[k] for p in dev_phases if k in p], .5), 1)
+                                         for k in sorted({k for p in dev_phases for k in p})},
                 # every timed step above 1.5 x p50, attributed to the admission phase with the largest excess
                 "tail_attribution": tail_attribution(lat_ms, {
                     "plugin_rpc": rpc_ms, "runtime_prep": prespawn_ms, "exec_and_library_load": exec_ms,

@@ -86,9 +86,19 @@ extern "C" int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355
   hipStream_t stream = nullptr;
   float ms = 0.f;
 
+  // phase_us: [device (hipSetDevice + identity), stream (its hardware queue), buffers (pinned +
+  // device memory, events), dispatch_wait (launch -> tile back)], as the HSA path reports them
+  auto lap = [&, t = t0]() mutable {
+    const auto now = std::chrono::steady_clock::now();
+    const double us = std::chrono::duration<double, std::micro>(now - t).count();
+    t = now;
+    return us;
+  };
   PROBE_CHECK(hipSetDevice(ordinal), "hipSetDevice");
   fill_identity(ordinal, out);
+  out->phase_us[0] = lap();
   PROBE_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+  out->phase_us[1] = lap();
   PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_out), MI355X_PROBE_OUT * sizeof(float),
                             hipHostMallocCoherent),
               "hipHostMalloc(out)");
@@ -103,6 +113,7 @@ extern "C" int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355
   PROBE_CHECK(hipEventCreate(&ev0), "hipEventCreate");
   PROBE_CHECK(hipEventCreate(&ev1), "hipEventCreate");
   t_setup = std::chrono::steady_clock::now();
+  out->phase_us[2] = lap();
   PROBE_CHECK(hipEventRecord(ev0, stream), "hipEventRecord");
   hipLaunchKernelGGL(mi355x_mfma_liveness, dim3(1), dim3(64), 0, stream, h_out, h_meta, d_scratch, nonce,
                      out->iters);
@@ -110,6 +121,7 @@ extern "C" int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355
   PROBE_CHECK(hipGetLastError(), "launch");
   PROBE_CHECK(hipEventRecord(ev1, stream), "hipEventRecord");
   PROBE_CHECK(hipStreamSynchronize(stream), "hipStreamSynchronize");
+  out->phase_us[3] = lap();
   PROBE_CHECK(hipEventElapsedTime(&ms, ev0, ev1), "hipEventElapsedTime");
   out->kernel_us = ms * 1000.0;
   mi355x::verify_tile(h_out, h_meta, nonce, out->iters, out);

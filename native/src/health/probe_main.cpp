@@ -78,6 +78,14 @@ std::string json_escape(const char* s) {
   return o;
 }
 
+// phase_us of one device: HSA build = code object, queue, buffers, dispatch;
+// HIP build = hipSetDevice + identity, the stream's queue, buffers + events, dispatch
+#ifdef MI355X_PROBE_HSA
+#define PHASE_NAMES "\"code_object\":%.1f,\"queue\":%.1f,\"buffers\":%.1f,\"dispatch_wait\":%.1f"
+#else
+#define PHASE_NAMES "\"device\":%.1f,\"stream\":%.1f,\"buffers\":%.1f,\"dispatch_wait\":%.1f"
+#endif
+
 std::string device_json(const mi355x_probe_result& r) {
   char buf[2048];
   std::snprintf(
@@ -85,7 +93,7 @@ std::string device_json(const mi355x_probe_result& r) {
       "{\"ordinal\":%d,\"ok\":%s,\"hip_error\":%d,\"mismatches\":%d,\"nonce\":%u,\"xcc_id\":%u,"
       "\"hw_id\":%u,\"iters\":%d,\"dispatches\":%d,\"kfd_node_id\":%d,\"runtime\":\"%s\","
       "\"kernel_us\":%.3f,\"setup_us\":%.3f,\"total_us\":%.3f,"
-      "\"phase_us\":{\"code_object\":%.1f,\"queue\":%.1f,\"buffers\":%.1f,\"dispatch_wait\":%.1f},"
+      "\"phase_us\":{" PHASE_NAMES "},"
       "\"pci_bus_id\":\"%s\","
       "\"arch\":\"%s\",\"name\":\"%s\",\"uuid\":\"%s\",\"pci_domain\":%d,\"pci_bus\":%d,"
       "\"pci_device\":%d,\"cu_count\":%d,\"total_mem\":%llu,\"late\":%s,\"pending_s\":%.3f,\"error\":\"%s\"}",
