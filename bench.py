@@ -663,7 +663,8 @@ def main():
             raise SystemExit(f"only {len(usable)} accessible GPU devices on this node, need {m_adv}")
         adv = tuple(usable[:m_adv])     # "GPUs advertised at N" (or M with --advertise)
         adv_ordinals = [ords[dv.id] for dv in adv]
-        hp = args.health_pulse if not args.fixture else 0.0
+        # the Python plugin's health loop needs a GPU; the daemon's runs on the fixture with its sysfs sources
+        hp = args.health_pulse if not args.fixture or args.plugin == "native" else 0.0
         hcfg = (HealthConfig(exporter_socket=None, liveness=True, smi_ecc=True, smi_events=True, smi_xgmi=True)
                 if hp > 0 else HealthConfig(exporter_socket=None))
         loop = asyncio.new_event_loop()
@@ -672,8 +673,8 @@ def main():
         # probe server and amd-smi ECC / events / xGMI) on the daemon; -pulse is whole seconds
         health_flags = ()
         if hp > 0 and plugin_kind == "native-daemon":
-            health_flags = ("-pulse", str(max(1, int(round(hp)))), "-liveness", "-smi_ecc", "-smi_events",
-                            "-smi_xgmi")
+            health_flags = ("-pulse", str(max(1, int(round(hp)))),
+                            *(() if args.fixture else ("-liveness", "-smi_ecc", "-smi_events", "-smi_xgmi")))
 
         def make_plugin(name, devs, extra=()):
             if plugin_kind == "native-daemon":
@@ -1008,7 +1009,7 @@ def main():
                 rccl = {"error": f"{type(e).__name__}: {e}"[:300]}
 
         def health_loop_report():
-            if args.health_pulse <= 0 or args.fixture:
+            if args.health_pulse <= 0 or (args.fixture and plugin_kind != "native-daemon"):
                 return None
             if plugin_kind == "native-daemon":
                 return plug.health_report(float(health_flags[1]))

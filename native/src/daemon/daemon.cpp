@@ -159,7 +159,9 @@ int Daemon::init() {
   if (f_.pulse > 0 && !reg_.empty()) {
     // one sweep before registering, so the first ListAndWatch already carries
     // real verdicts (the reference advertises everything Healthy until its first pulse)
-    reg_.apply_health(health_->sweep_now().health);
+    const SweepResult first = health_->sweep_now();
+    metrics::global().observe_ms("mi355x_dp_health_sweep_seconds", first.sweep_ms, {}, "health sweep latency");
+    reg_.apply_health(first.health);
   }
   if (f_.dry_run) {
     const auto eng = health_->engine();

@@ -270,3 +270,15 @@ def test_bench_single_process_8_gpus_on_the_fixture():
     assert d["n_gpus"] == 8 and e["launcher"] == "single-process" and e["rccl"] is None
     assert e["bench_process_gpu"]["clean"] and len(e["bench_process_gpu"]["ranks"]) == 1
     assert e["fabric"]["pairs"]["xgmi"] == 28 and e["timed_allocation"]["advertised"] == 8
+
+
+def test_bench_health_pulse_runs_on_the_native_daemon():
+    """--health-pulse (BASELINE config: health-check DaemonSet enabled) drives
+    the native daemon with -pulse; its sweeps are counted from the daemon's
+    /metrics (on the fixture: the sysfs sources; on a GPU also liveness and
+    amd-smi)."""
+    d, _ = _bench_ranks(1, "--steps", "30", "--warmup", "1", "--health-pulse", "1", torchrun=False)
+    hl = d["extra"]["health_loop"]
+    assert d["config"]["plugin"] == "native-daemon" and hl["plugin"] == "native-daemon"
+    assert hl["pulse_s"] == 1.0 and hl["sweeps"] >= 1 and hl["sweep_ms_mean"] is not None
+    assert hl["unhealthy"] == [] and hl["health_changes"] == 0
