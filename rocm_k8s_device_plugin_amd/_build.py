@@ -112,10 +112,16 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
     if not (bdir / "CMakeCache.txt").exists() or sanitize:
         subprocess.run(cfg, check=True, stdout=out)
     else:
-        # re-run configure only if the HIP option or the version stamp changed
+        # re-run configure only if the HIP option flipped, or for a new version
+        # stamp when something is rebuilt anyway (sources changed since the last
+        # build) or one is given explicitly ($GIT_DESCRIBE): a commit alone must
+        # not relink the binaries under a running test suite
         cache = (bdir / "CMakeCache.txt").read_text()
         want = f"MI355X_BUILD_HIP:BOOL={'ON' if hip else 'OFF'}"
-        if want not in cache or (describe and f"MI355X_GIT_DESCRIBE:STRING={describe}\n" not in cache):
+        restamp = bool(describe) and f"MI355X_GIT_DESCRIBE:STRING={describe}\n" not in cache and (
+            bool(os.environ.get("GIT_DESCRIBE")) or not STAMP.exists()
+            or f"digest={_source_digest()}" not in STAMP.read_text().split())
+        if want not in cache or restamp:
             subprocess.run(cfg, check=True, stdout=out)
     j = jobs or min(8, os.cpu_count() or 4)
     res = subprocess.run(["cmake", "--build", str(bdir), "-j", str(j)], stdout=subprocess.PIPE,
