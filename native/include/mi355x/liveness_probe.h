@@ -53,6 +53,9 @@ typedef struct {
 int mi355x_probe_device_count(void);
 int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355x_probe_result* out);
 int mi355x_probe_identify(int ordinal, mi355x_probe_result* out);
+// 1 (default): the probe creates its own non-blocking stream; 0: it uses the
+// null stream (measurement of what the stream's queue costs a HIP program)
+void mi355x_probe_set_stream_mode(int own);
 
 // ---- HSA-direct path ------------------------------------------------------
 // hsa_init + GPU agent enumeration; returns the number of GPU agents or

@@ -51,7 +51,11 @@ void fill_identity(int ordinal, mi355x_probe_result* out) {
   std::snprintf(out->runtime, sizeof(out->runtime), "hip");
 }
 
+int g_own_stream = 1;
+
 }  // namespace
+
+extern "C" void mi355x_probe_set_stream_mode(int own) { g_own_stream = own ? 1 : 0; }
 
 extern "C" int mi355x_probe_device_count(void) {
   int n = 0;
@@ -97,7 +101,7 @@ extern "C" int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355
   PROBE_CHECK(hipSetDevice(ordinal), "hipSetDevice");
   fill_identity(ordinal, out);
   out->phase_us[0] = lap();
-  PROBE_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+  if (g_own_stream) PROBE_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
   out->phase_us[1] = lap();
   PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_out), MI355X_PROBE_OUT * sizeof(float),
                             hipHostMallocCoherent),

@@ -128,7 +128,9 @@ void teardown() { mi355x_hsa_probe_release(); }
 void runtime_shutdown() { mi355x_hsa_probe_shutdown(); }
 void keep_resources(bool on) { mi355x_hsa_probe_keep(on ? 1 : 0); }
 void set_corrupt(int word, int ordinal) { mi355x_hsa_probe_corrupt(word, ordinal); }
+void set_stream_mode(bool) {}  // the HSA path has one queue per device
 #else
+void set_stream_mode(bool own) { mi355x_probe_set_stream_mode(own ? 1 : 0); }
 void set_corrupt(int, int) {}
 void keep_resources(bool) {}  // the HIP build reuses its runtime's queues anyway
 void init_phases(double out[5]) { out[0] = out[1] = out[2] = out[3] = out[4] = 0; }
@@ -537,13 +539,20 @@ int main(int argc, char** argv) {
       peer_bytes = std::strtoull(next("--peer-bytes"), nullptr, 0);
     } else if (a == "--corrupt-word") {
       parse_corrupt(next("--corrupt-word"), &g_flag_corrupt_word, &g_flag_corrupt_ordinal);
+    } else if (a == "--hip-stream") {
+      const std::string m = next("--hip-stream");
+      if (m != "own" && m != "null") {
+        std::fprintf(stderr, "--hip-stream must be own|null\n");
+        return 2;
+      }
+      set_stream_mode(m == "own");
     } else if (a == "--peer-reps") {
       peer_reps = std::atoi(next("--peer-reps"));
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: %s [--devices all|0,1,..] [--nonce N] [--iters N] [--identify] [--timeout S] "
                   "[--sample-init PERIOD_US] [--exit shutdown|release|fast] [--serve [--keep]] [--peer [--peer-bytes B] [--peer-reps R]] [--sweep] "
                   "[--perf [--perf-mib M] [--perf-iters N] [--poison-hbm UNIT]] "
-                  "[--corrupt-word K[@ORDINAL]]\n",
+                  "[--corrupt-word K[@ORDINAL]] [--hip-stream own|null]\n",
                   argv[0]);
       return 0;
     } else {

@@ -8,6 +8,8 @@
 #   bench100  100 timed admissions                        -> gpurun_out/bench100.json
 #   health  bench with the health DaemonSet loop (-pulse 2, liveness, amd-smi) -> gpurun_out/bench_health.json
 #   prof    rocprofv3 kernel stats of a short bench       -> gpurun_out/prof_bench/
+#   profprobe  rocprofv3 kernel stats of one HIP container entrypoint -> gpurun_out/prof_probe/
+#   hipvariants  tools/hip_setup_variants.py (own vs null stream)     -> gpurun_out/hip_setup_variants.json
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
 set -o pipefail
@@ -49,6 +51,17 @@ for s in "$@"; do
         -- python3 bench.py --steps 5 --warmup 1 > gpurun_out/prof_bench.log 2>&1 \
         || { tail -20 gpurun_out/prof_bench.log; exit 1; }
       find gpurun_out/prof_bench -name "*kernel_stats.csv" ;;
+    profprobe)
+      step profprobe
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_probe -o probe \
+        -- ./rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe-hip --devices 0 > gpurun_out/prof_probe.log 2>&1 \
+        || { tail -20 gpurun_out/prof_probe.log; exit 1; }
+      find gpurun_out/prof_probe -name "*kernel_stats.csv" ;;
+    hipvariants)
+      step hipvariants
+      timeout -k 10 300 python3 tools/hip_setup_variants.py --runs 20 --json-out gpurun_out/hip_setup_variants.json \
+        > gpurun_out/hip_setup_variants.log 2>&1 || { tail -20 gpurun_out/hip_setup_variants.log; exit 1; }
+      cat gpurun_out/hip_setup_variants.json ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
