@@ -10,6 +10,7 @@
 #   prof    rocprofv3 kernel stats of a short bench       -> gpurun_out/prof_bench/
 #   profprobe  rocprofv3 kernel stats of one HIP container entrypoint -> gpurun_out/prof_probe/
 #   hipvariants  tools/hip_setup_variants.py (own vs null stream)     -> gpurun_out/hip_setup_variants.json
+#   soak    4 min native daemon soak, every health source on, a HIP container every second -> gpurun_out/soak_native.json
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
 set -o pipefail
@@ -62,6 +63,13 @@ for s in "$@"; do
       timeout -k 10 300 python3 tools/hip_setup_variants.py --runs 20 --json-out gpurun_out/hip_setup_variants.json \
         > gpurun_out/hip_setup_variants.log 2>&1 || { tail -20 gpurun_out/hip_setup_variants.log; exit 1; }
       cat gpurun_out/hip_setup_variants.json ;;
+    soak)
+      step soak
+      timeout -k 10 420 python3 tools/soak_native.py --seconds 240 --report 30 --container-interval 1 \
+        --extra "-liveness -liveness_chip_sweep_every 10 -perf_check_every 60 -smi_ecc -smi_events -smi_xgmi" \
+        --out gpurun_out/soak_native.json > gpurun_out/soak_native.log 2>&1 \
+        || { tail -20 gpurun_out/soak_native.log; exit 1; }
+      tail -c 1500 gpurun_out/soak_native.json ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac

@@ -32,6 +32,7 @@ from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR  # noqa: E402
 from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet  # noqa: E402
 
 EXE = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+CONTAINER_RUNTIME = "hip"   # the container is a HIP program, --container-runtime
 
 
 def proc_stats(pid: int) -> dict:
@@ -71,7 +72,7 @@ async def run_container(adm, minor_to_ord: dict, cont: dict) -> None:
     car = adm.response.container_responses[0]
     ordl = [minor_to_ord[m] for m in render_minors_from_specs(car)]
     paths = ["/dev/kfd"] + [d.host_path for d in car.devices if d.host_path.startswith("/dev/dri/")]
-    res = await asyncio.to_thread(start_container, ordl, 60.0, device_paths=paths)
+    res = await asyncio.to_thread(start_container, ordl, 60.0, device_paths=paths, runtime=CONTAINER_RUNTIME)
     cont["started"] += 1
     if res.ok:
         cont["ready_ms"].append((res.t_ready_ns - res.t_start_ns) / 1e6)
@@ -82,6 +83,8 @@ async def run_container(adm, minor_to_ord: dict, cont: dict) -> None:
 
 
 async def main(a) -> int:
+    global CONTAINER_RUNTIME
+    CONTAINER_RUNTIME = a.container_runtime
     kdir = tempfile.mkdtemp(prefix="soak-native-")
     k = FakeKubelet(kdir)
     await k.start()
@@ -183,6 +186,7 @@ if __name__ == "__main__":
     ap.add_argument("--out", default="")
     ap.add_argument("--extra", default="", help="more daemon flags, space-separated")
     ap.add_argument("--metrics-port", type=int, default=0)
+    ap.add_argument("--container-runtime", default="hip", choices=["hip", "hsa"])
     ap.add_argument("--container-interval", type=float, default=0.0,
                     help="every S seconds start one admission's container on the GPU (0 = never)")
     sys.exit(asyncio.run(main(ap.parse_args())))
