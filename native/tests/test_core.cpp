@@ -655,6 +655,66 @@ static void test_registration_watchdog() {
   }
 }
 
+
+// random event sequences against Registration: its invariants hold in every state
+static void test_registration_random_sequences() {
+  using daemon::Registration;
+  daemon::RegistrationPolicy pol;
+  pol.watchdog_s = 0.5;
+  pol.reregister_s = 0.2;
+  uint64_t seed = 0x9e3779b97f4a7c15ull;
+  auto rnd = [&](uint64_t n) {
+    seed ^= seed << 13;
+    seed ^= seed >> 7;
+    seed ^= seed << 17;
+    return seed % n;
+  };
+  int bad = 0;
+  for (int run = 0; run < 200; ++run) {
+    Registration r(pol);
+    auto now = daemon::Clock::now();
+    uint64_t sgen = 0, kgen = 1, opened = 0, open = 0, caller = 0;
+    bool tripped = false;
+    std::vector<std::pair<uint64_t, uint64_t>> pending;  // (server gen, kubelet gen) of Registers in flight
+    for (int step = 0; step < 300 && !tripped; ++step) {
+      now += std::chrono::milliseconds(rnd(120));
+      switch (rnd(9)) {
+        case 0: r.server_started(++sgen, now); open = 0; break;
+        case 1: r.server_stopped(); open = 0; break;
+        case 2: ++kgen; break;
+        case 3:
+          if (r.due(now)) {
+            r.begin(kgen, stats(opened, open, 0, caller));
+            pending.emplace_back(sgen, kgen);
+          }
+          break;
+        case 4:
+          if (!pending.empty()) {
+            const size_t k = rnd(pending.size());
+            r.complete(pending[k].first, pending[k].second, kgen, rnd(4) != 0, now);
+            pending.erase(pending.begin() + static_cast<long>(k));
+          }
+          break;
+        case 5: ++opened; ++open; break;                 // kubelet opens a stream
+        case 6: if (open) --open; break;                 // a stream ends
+        case 7: if (rnd(8) == 0) ++caller; break;        // a protocol error on a calling connection
+        case 8: r.force(now); break;
+      }
+      const bool was_seen = r.list_seen();
+      const std::string why = r.observe(stats(opened, open, 0, caller), now);
+      if (!why.empty()) {
+        tripped = true;
+        if (was_seen) ++bad;                              // never after ListAndWatch was seen
+      }
+      if (r.registered() && !r.serving()) ++bad;
+      if (r.due(now) && (r.registered() || r.inflight() || !r.serving())) ++bad;
+      if (r.armed() && r.list_seen()) ++bad;
+      if (r.next_event(now) < now) ++bad;
+    }
+  }
+  CHECK(bad == 0);
+}
+
 static void test_topology_watch() {
   daemon::TopologyWatch w("a");
   CHECK(!w.observe("a", true));
@@ -719,6 +779,7 @@ int main(int argc, char** argv) {
   test_fuzz_rpc(ref);
   test_registration_generations();
   test_registration_watchdog();
+  test_registration_random_sequences();
   test_topology_watch();
   {
     char dir[] = "/tmp/mi355x-test-core-XXXXXX";
