@@ -95,6 +95,7 @@ class ExtrasGuard:
         self.fallback = None          # rank 0: (error) -> the headline line without the unfinished extras
         self._lock = threading.Lock()
         self._printed = False
+        self._abandoning = False
         self._written = threading.Event()   # the printed line (and --json-out) is complete
         self._timer = None
         self._plugins = []            # plugin daemons to SIGKILL when the timer fires (no orphans)
@@ -136,7 +137,16 @@ class ExtrasGuard:
     def abandon(self, error) -> None:
         """Leave now: rank 0 prints the headline line (unless it already has)
         with the unfinished stage, plugin daemons are killed, exit status 0.
-        ``error`` is None when the deadline passed, else why the stage failed."""
+        ``error`` is None when the deadline passed, else why the stage failed.
+        The first caller leaves; a second one (the main thread failing because
+        the timer already killed a plugin daemon) waits for that exit."""
+        import time
+        with self._lock:
+            first = not self._abandoning
+            self._abandoning = True
+        if not first:
+            while True:
+                time.sleep(3600)
         why = (f"exceeded --extras-deadline {self.deadline_s:g}s" if error is None else f"failed: {error}")
         msg = f"bench: secondary measurements {why} in stage '{self.stage}'"
         if self.rank == 0 and self.fallback is not None:
@@ -151,19 +161,22 @@ class ExtrasGuard:
                     self.emit(*self.fallback(error))
                 except Exception as e:  # noqa: BLE001
                     msg += f"; headline line failed: {type(e).__name__}: {e}"
-        for pl in self._plugins:
-            proc = getattr(pl, "proc", None)
-            if proc is not None and proc.poll() is None:
-                try:
-                    proc.kill()
-                except OSError:
-                    pass
-        if self.tmp:
-            import shutil
-            shutil.rmtree(self.tmp, ignore_errors=True)
         try:
-            sys.stdout.flush()
-            os.write(2, (msg + "\n").encode())
+            try:
+                sys.stdout.flush()
+                os.write(2, (msg + "\n").encode())
+            except OSError:
+                pass
+            for pl in self._plugins:
+                proc = getattr(pl, "proc", None)
+                if proc is not None and proc.poll() is None:
+                    try:
+                        proc.kill()
+                    except OSError:
+                        pass
+            if self.tmp:
+                import shutil
+                shutil.rmtree(self.tmp, ignore_errors=True)
         finally:
             os._exit(0)
 
