@@ -604,7 +604,9 @@ def test_topology_watch_relabels_within_a_second(tmp_path):
         os.rename(new / "sys", root / "sys")
         t0 = time.monotonic()
         while srv.labels("worker-4").get("amd.com/gpu.compute-memory-partition") != "dpx_nps1":
-            assert time.monotonic() - t0 < 1.0, srv.labels("worker-4")
+            # ~0.2 s when idle (two 0.1 s polls + one relabel); 3 s leaves room for a loaded CI host,
+            # still far from the 1 h resync
+            assert time.monotonic() - t0 < 3.0, srv.labels("worker-4")
             time.sleep(0.02)
         assert lab.stats.topology_changes == 1
     finally:
