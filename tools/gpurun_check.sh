@@ -5,11 +5,13 @@
 #   smoke   __graft_entry__.smoke()                       -> gpurun_out/smoke.log
 #   tests   pytest -m gpu                                 -> gpurun_out/gputests.log
 #   bench   default bench (N=1, 20 steps)                 -> gpurun_out/bench.json
+#   torchrun1 the driver's torchrun launch at N = 1       -> gpurun_out/bench_torchrun1.json
 #   bench100  100 timed admissions                        -> gpurun_out/bench100.json
 #   health  bench with the health DaemonSet loop (-pulse 2, liveness, amd-smi) -> gpurun_out/bench_health.json
 #   prof    rocprofv3 kernel stats of a short bench       -> gpurun_out/prof_bench/
 #   profprobe  rocprofv3 kernel stats of one HIP container entrypoint -> gpurun_out/prof_probe/
 #   hipvariants  tools/hip_setup_variants.py (own vs null stream)     -> gpurun_out/hip_setup_variants.json
+#   asan    the native-daemon GPU tests against the ASan/UBSan builds in asan_bin/
 #   soak    4 min native daemon soak, every health source on, a HIP container every second -> gpurun_out/soak_native.json
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
@@ -35,6 +37,13 @@ for s in "$@"; do
       timeout -k 10 400 python3 bench.py --json-out gpurun_out/bench.json > gpurun_out/bench.log 2>&1 \
         || { tail -20 gpurun_out/bench.log; exit 1; }
       cut -c1-600 gpurun_out/bench.json ;;
+    torchrun1)
+      # the driver's launch line at N = 1
+      step torchrun1
+      timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29511 bench.py --gpus 1 --steps 20 --warmup 3 --json-out gpurun_out/bench_torchrun1.json \
+        > gpurun_out/bench_torchrun1.log 2>&1 || { tail -20 gpurun_out/bench_torchrun1.log; exit 1; }
+      cut -c1-400 gpurun_out/bench_torchrun1.json ;;
     bench100)
       step bench100
       timeout -k 10 600 python3 bench.py --steps 100 --warmup 5 --json-out gpurun_out/bench100.json \
@@ -70,6 +79,14 @@ for s in "$@"; do
         --out gpurun_out/soak_native.json > gpurun_out/soak_native.log 2>&1 \
         || { tail -20 gpurun_out/soak_native.log; exit 1; }
       tail -c 1500 gpurun_out/soak_native.json ;;
+    asan)
+      # the GPU tests that drive the native daemons, against their ASan/UBSan builds (host code only;
+      # asan_bin/ holds build/native-address-undefined/pkg/bin/*, copied before the call)
+      step asan
+      MI355X_NATIVE_DAEMON_EXE=$PWD/asan_bin/mi355x-device-plugin MI355X_NATIVE_LABELLER_EXE=$PWD/asan_bin/mi355x-node-labeller \
+        timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "native or daemon or labeller" \
+        > gpurun_out/gputests_asan.log 2>&1 || { tail -40 gpurun_out/gputests_asan.log; exit 1; }
+      tail -3 gpurun_out/gputests_asan.log ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
