@@ -154,6 +154,15 @@ def test_ci_command_lines_pass_the_real_argument_parsers():
         where = f"{wf}: {name}: {' '.join(argv)}"
         if argv[0] in ("git", "helm"):
             continue
+        if argv[0] == "make":            # a Makefile target, with VAR=value overrides only
+            targets = re.findall(r"^([A-Za-z0-9_-]+):", (REPO / "Makefile").read_text(), re.M)
+            assert all(a in targets or re.fullmatch(r"[A-Z_]+=\S*", a) for a in argv[1:]), where
+            checked += 1
+            continue
+        if argv[0] == "docker":          # docker run of an image the Makefile builds
+            from test_image_layout import image_map
+            assert argv[1] == "run" and any(a in image_map() for a in argv), where
+            continue
         assert argv[0] in ("python3", "python"), where
         if argv[1:4] == ["-m", "pip", "install"]:
             continue
