@@ -1,0 +1,57 @@
+"""testing/helm_lite.py: the Go text/template + sprig subset the chart uses,
+with Go's semantics (checked on hand-computed expectations)."""
+import pytest
+
+from rocm_k8s_device_plugin_amd.testing.helm_lite import Renderer, TemplateError, _parse, _tokenize
+
+
+def render(src, values=None, defines_src=""):
+    defines = {}
+    if defines_src:
+        _parse(_tokenize(defines_src), defines)
+    tree = _parse(_tokenize(src), defines)
+    ctx = {"Values": values or {}, "Chart": {"Name": "c", "AppVersion": "1.2"}, "Release": {"Namespace": "ns"}}
+    return Renderer(defines).run(tree, ctx, {"$": ctx})
+
+
+def test_trim_markers_and_fields():
+    assert render("a  {{- .Values.x -}}  b", {"x": "X"}) == "aXb"
+    assert render("a {{ .Values.x }} b", {"x": 3.0}) == "a 3 b"          # float64 10 prints as 10
+    assert render("{{ .Values.missing }}|") == "|"                      # <no value> -> ""
+    assert render("{{/* a comment */}}ok") == "ok"
+
+
+def test_if_else_truthiness():
+    src = "{{ if .Values.a }}A{{ else if .Values.b }}B{{ else }}C{{ end }}"
+    assert render(src, {"a": 1.0}) == "A"
+    assert render(src, {"a": 0.0, "b": "x"}) == "B"
+    assert render(src, {"a": "", "b": []}) == "C"
+    assert render("{{ if and .Values.a (not .Values.b) }}y{{ end }}", {"a": True, "b": False}) == "y"
+
+
+def test_pipelines_default_ternary_or():
+    assert render('{{ .Values.tag | default .Chart.AppVersion }}', {"tag": ""}) == "1.2"
+    assert render('{{ .Values.tag | default .Chart.AppVersion }}', {"tag": "t"}) == "t"
+    assert render('{{ .Values.p | default (ternary 10 0 (or .Values.a .Values.b)) }}', {"p": 0.0, "b": True}) == "10"
+    assert render('{{ printf "labeller-%s" .Chart.AppVersion }}') == "labeller-1.2"
+    assert render('{{ ne .Values.k false }}', {"k": False}) == "false"
+
+
+def test_range_with_variables_and_quote():
+    assert render('{{- range .Values.args }}[{{ . | quote }}]{{- end }}', {"args": ["-a", "b c"]}) == '["-a"]["b c"]'
+    assert render('{{- $x := .Values.v -}}{{ if $x }}{{ $x }}{{ end }}', {"v": "q"}) == "q"
+    assert render('{{ with .Values.m }}{{ .k }}{{ end }}', {"m": {"k": "v"}}) == "v"
+
+
+def test_include_nindent_toyaml():
+    defs = '{{- define "lbl" -}}a: {{ .Chart.Name }}\nb: 1{{- end -}}'
+    assert render('x:{{- include "lbl" . | nindent 2 }}', defines_src=defs) == "x:\n  a: c\n  b: 1"
+    assert render('r: {{- toYaml .Values.r | nindent 2 }}', {"r": {}}) == "r:\n  {}"
+    assert render('r: {{- toYaml .Values.r | nindent 2 }}', {"r": {"b": 1, "a": "x"}}) == "r:\n  a: x\n  b: 1"
+
+
+def test_errors():
+    with pytest.raises(TemplateError):
+        render("{{ nosuchfunc 1 }}")
+    with pytest.raises(TemplateError):
+        render("{{ if .Values.a }}unterminated")
