@@ -44,12 +44,8 @@ def _tokenize(src: str) -> List[Tuple[str, str]]:
     for m in _ACTION.finditer(src):
         text = src[pos:m.start()]
         ltrim, body, rtrim = m.group(1) == "-", m.group(2), m.group(3) == "-"
-        if ltrim:
-            text = text.rstrip()
-            if out and out[-1][0] == "text":
-                pass
-        out.append(("text", text))
-        out.append(("action", body.strip() if True else body))
+        out.append(("text", text.rstrip() if ltrim else text))
+        out.append(("action", body.strip()))
         out.append(("rtrim", "1" if rtrim else ""))
         pos = m.end()
     out.append(("text", src[pos:]))
