@@ -1,4 +1,4 @@
-// Native gRPC client (GrpcClient in src/rpc/grpc_server.cpp): the daemons'
+// Native gRPC client (GrpcClient in src/rpc/grpc_client.cpp): the daemons'
 // Register call to kubelet and List call to the metrics exporter. The input
 // is everything the server side sends on the connection (SETTINGS, HEADERS /
 // CONTINUATION with HPACK, DATA, PING, GOAWAY, RST_STREAM, WINDOW_UPDATE, ...),

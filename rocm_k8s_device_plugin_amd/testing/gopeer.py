@@ -2,7 +2,7 @@
 
 The kubelet is a grpc-go program: it is the *client* of every DevicePlugin
 RPC and the *server* of Registration (the metrics exporter is a grpc-go
-server too). The native HTTP/2 stack (native/src/rpc/grpc_server.cpp) must
+server too). The native HTTP/2 stack (native/src/rpc/grpc_server.cpp, grpc_client.cpp) must
 therefore interoperate with grpc-go's transport, which no Go toolchain here
 can run. These peers replay, frame by frame, what that transport does, taken
 from the vendored sources (reference paths below are under
