@@ -210,6 +210,23 @@ class Engine {
     double pending_since = -1;  // monotonic seconds of the first inconclusive probe
     int idle_pending = 0;
   };
+  using Reasons = std::map<std::string, std::vector<std::string>>;  // device -> why it is Unhealthy
+  // the phases of sweep()
+  void liveness_pass(Reasons* reasons);
+  void ecc_pass(Reasons* reasons);
+  void events_pass(Reasons* reasons);
+  bool publish(Reasons reasons);
+  // liveness_pass's steps
+  std::map<std::string, int> judged_ordinals(const Reasons& reasons);
+  bool update_busy_state(const std::map<std::string, int>& ords, std::set<std::string>* busy);
+  std::set<std::string> update_crowded(const std::map<std::string, int>& ords);
+  std::map<std::string, ProbeOutcome> run_probes(const std::map<std::string, int>& probe_ords,
+                                                 const std::set<std::string>& busy, const std::set<std::string>& idle,
+                                                 bool known);
+  void probe_crowded(const std::set<std::string>& crowded, const std::map<std::string, int>& ords,
+                     std::map<std::string, ProbeOutcome>* outcomes);
+  void judge_liveness(const std::map<std::string, ProbeOutcome>& outcomes, const std::set<std::string>& busy,
+                      Reasons* reasons);
   std::map<std::string, std::string> kfd_verdicts() const;
   std::map<std::string, bool> exporter_health() const;
   std::map<std::string, int> gfx_activity();
