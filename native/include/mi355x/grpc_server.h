@@ -3,7 +3,7 @@
 //
 // The kubelet is a Go gRPC client; the reference answers it from grpc-go. A
 // Python grpc.aio server puts ~0.6-0.9 ms of interpreter and event-loop work
-// on every GetPreferredAllocation / Allocate (profiles/rpc_native_box.json).
+// on every GetPreferredAllocation / Allocate (profiles/archive/measurements_r1_r3.md §6).
 // This server speaks the subset of HTTP/2 + gRPC a kubelet uses (unary and
 // server-streaming calls, HPACK with Huffman, flow control, PING, GOAWAY) on
 // one I/O thread with epoll; handlers run on that thread.

@@ -1,9 +1,10 @@
 // HSA-direct launcher for the gfx950 MFMA liveness kernel.
 //
-// The HIP runtime costs ~170 ms of start-up before the first kernel can run
-// (measured on MI355X, profiles/round1_container_ready.md), which is pure
-// overhead for a 2.4 us liveness dispatch that the plugin runs on every
-// device every pulse. This path talks to ROCr directly:
+// A HIP program pays ~60 ms of runtime start-up and ~21 ms of per-device
+// queue set-up before its first kernel (MI355X, profiles/r4/bench100_hip.json
+// extra.container_phases_p50_ms), pure overhead for a few-us liveness dispatch
+// that the plugin runs on every device every pulse. This path talks to ROCr
+// directly:
 //
 //   hsa_init -> GPU agents (ROCR_VISIBLE_DEVICES honoured)
 //   code object: the embedded liveness_gfx950.hsaco -> executable -> kernel object

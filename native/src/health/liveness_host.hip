@@ -2,7 +2,7 @@
 //
 // Output and meta live in coherent pinned host memory and are poisoned by the
 // CPU, so the probe issues exactly ONE GPU dispatch (no memset/blit kernels —
-// the first version issued five, see profiles/round1_probe_rocprof.md).
+// the first version issued five, see profiles/archive/measurements_r1_r3.md §1).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
