@@ -433,6 +433,219 @@ clk::time_point after_s(double s) {
   return clk::now() + std::chrono::microseconds(static_cast<long long>(s * 1e6));
 }
 
+// The apiserver client as controller-runtime's GetConfigOrDie sets it up:
+// -kubeconfig, else in-cluster unless $KUBECONFIG is set, else $KUBECONFIG /
+// $HOME/.kube/config; in-cluster: the service account's token and CA.
+bool configure_kube(const Flags& f, Kube* kube) {
+  std::string err;
+  const char* svc_host = std::getenv("KUBERNETES_SERVICE_HOST");
+  const bool in_cluster = (svc_host && *svc_host) || !f.apiserver.empty();
+  const std::string kc_path = !f.kubeconfig.empty() ? f.kubeconfig : kube::default_kubeconfig_path(in_cluster);
+  if (!kc_path.empty()) {
+    auto kc = kube::load_kubeconfig(kc_path, &err);
+    if (!kc) {
+      MI_LOG(kError, "unable to set up kubernetes client: %s", err.c_str());
+      return false;
+    }
+    kube->cfg = kc->http;
+    kube->token = kc->token;
+    kube->token_file = kc->token_file;
+    MI_LOG(kInfo, "kubeconfig %s: server %s", kc_path.c_str(), kube->cfg.server.c_str());
+    return true;
+  }
+  if (!f.apiserver.empty()) {
+    kube->cfg.server = f.apiserver;
+  } else {
+    const char* host = std::getenv("KUBERNETES_SERVICE_HOST");
+    const char* port = std::getenv("KUBERNETES_SERVICE_PORT");
+    if (!host || !*host) {
+      MI_LOG(kError, "unable to set up kubernetes client: not running in a cluster (KUBERNETES_SERVICE_HOST unset)");
+      return false;
+    }
+    std::string h = host;
+    if (h.find(':') != std::string::npos && h[0] != '[') h = "[" + h + "]";
+    kube->cfg.server = "https://" + h + ":" + (port && *port ? port : "443");
+  }
+  kube->token_file = !f.token_file.empty() ? f.token_file : path_join(f.sa_dir, "token");
+  kube->cfg.ca_file = !f.ca_file.empty() ? f.ca_file
+                      : path_exists(path_join(f.sa_dir, "ca.crt")) ? path_join(f.sa_dir, "ca.crt")
+                                                                    : "";
+  if (kube->bearer().empty() && f.apiserver.empty()) {
+    MI_LOG(kError, "unable to set up kubernetes client: service-account token %s is unreadable or empty",
+           kube->token_file.c_str());
+    return false;
+  }
+  return true;
+}
+
+// The watch of this node's object (?watch=1&fieldSelector=metadata.name=<node>):
+// an ADDED event (and, unless -resync 0, a MODIFIED one whose labels differ
+// from the desired set) asks for a reconcile; 410 re-lists; a failed or
+// short-lived stream is reopened with exponential backoff, a stream the server
+// ended after its timeout at once.
+class NodeWatch {
+ public:
+  enum Event { kIdle, kKick, kStop };
+
+  NodeWatch(const Flags& f, Kube* kube, Labeller* lab, bool created_only, int wake_fd)
+      : f_(f), kube_(kube), lab_(lab), created_only_(created_only), wake_fd_(wake_fd), cfg_(kube->cfg) {
+    cfg_.timeout_s = f.watch_timeout_s + 30.0;
+  }
+
+  // Waits up to wait_ms for the next watch event (or only for a signal while
+  // no stream is open), opening the stream first when it is due.
+  Event wait(int wait_ms) {
+    if (f_.watch && !open_ && clk::now() >= retry_) {
+      open();
+      if (g_stop) return kStop;
+    }
+    if (!open_) {
+      if (f_.watch) wait_ms = std::min(wait_ms, ms_until(retry_));
+      pollfd p{wake_fd_, POLLIN, 0};
+      ::poll(&p, 1, wait_ms);
+      return kIdle;
+    }
+    std::string line;
+    const int rc = stream_.next_line(&line, wait_ms, wake_fd_);
+    if (rc == -2) return kIdle;  // timer due
+    if (rc == -3 || g_stop) return kStop;
+    if (rc == 1) return on_line(line);
+    ended(rc);
+    return kIdle;
+  }
+
+ private:
+  void open() {
+    std::string q = "/api/v1/nodes?watch=1&fieldSelector=" + path_escape("metadata.name=" + f_.node_name) +
+                    "&timeoutSeconds=" + std::to_string(f_.watch_timeout_s) + "&allowWatchBookmarks=true";
+    if (!rv_.empty()) q += "&resourceVersion=" + path_escape(rv_);
+    int status = 0;
+    std::string ebody;
+    const std::string e = stream_.open(cfg_, q, kube_->headers(), &status, &ebody,
+                                       static_cast<int>(kube_->cfg.timeout_s * 1000), wake_fd_);
+    if (g_stop) return;
+    if (!e.empty() || status != 200) {
+      if (status == 410) rv_.clear();
+      if (status == 401) kube_->bearer(true);
+      ++lab_->st.watch_errors;
+      MI_LOG(kWarning, "watch of node %s failed (%s); retrying in %.1fs", f_.node_name.c_str(),
+             e.empty() ? ("HTTP " + std::to_string(status) + ": " + ebody.substr(0, 200)).c_str() : e.c_str(),
+             backoff_);
+      stream_.close();
+      back_off();
+      return;
+    }
+    open_ = true;
+    opened_ = clk::now();
+    ++lab_->st.watch_restarts;
+  }
+
+  Event on_line(const std::string& line) {
+    if (line.find_first_not_of(" \t\r") == std::string::npos) return kIdle;
+    ++lab_->st.watch_events;
+    auto ev = json::parse(line);
+    if (!ev) return kIdle;
+    const std::string type = ev->str("type");
+    const json::Value* obj = ev->get("object");
+    if (type == "ERROR") {
+      const bool gone = obj && obj->str("code") == "410";  // resourceVersion too old: re-list
+      if (gone) rv_.clear();
+      stream_.close();
+      open_ = false;
+      back_off();
+      return gone ? kKick : kIdle;
+    }
+    if (!obj) return kIdle;
+    const json::Value* md = obj->get("metadata");
+    if (md && !md->str("resourceVersion").empty()) rv_ = md->str("resourceVersion");
+    if ((type == "ADDED" || (type == "MODIFIED" && !created_only_)) && lab_->needs_reconcile(*obj)) {
+      ++lab_->st.watch_kicks;
+      return kKick;
+    }
+    return kIdle;
+  }
+
+  // the stream ended (server timeout, rc 0) or broke
+  void ended(int rc) {
+    stream_.close();
+    open_ = false;
+    const bool lived = clk::now() - opened_ >= std::chrono::seconds(1);
+    if (rc == 0 && lived) {
+      backoff_ = 0.2;
+      retry_ = clk::now();
+      return;
+    }
+    if (rc != 0) {
+      ++lab_->st.watch_errors;
+      MI_LOG(kWarning, "watch of node %s broke; retrying in %.1fs", f_.node_name.c_str(), backoff_);
+    }
+    back_off();  // a server that ends every stream at once is not hammered
+  }
+
+  void back_off() {
+    retry_ = after_s(backoff_);
+    backoff_ = std::min(backoff_ * 2, f_.watch_backoff_max_s);
+  }
+
+  const Flags& f_;
+  Kube* kube_;
+  Labeller* lab_;
+  const bool created_only_;
+  const int wake_fd_;
+  http::Config cfg_;  // the apiserver's, with a timeout past the watch's own
+  http::Stream stream_;
+  bool open_ = false;
+  clk::time_point opened_ = clk::now();
+  clk::time_point retry_ = clk::now();
+  double backoff_ = 0.2;
+  std::string rv_;
+};
+
+// The controller loop: reconcile at start, every -resync s, on watch events
+// and on a partition switch (a kfd fingerprint that held one -topology_watch
+// interval: a switch passes through half states).
+int run(const Flags& f, Labeller& lab, Kube& kube) {
+  // -resync 0: the reference's controller (main.go:553-586): label at start,
+  // then only when the Node object is (re-)created; no periodic re-assert
+  const bool created_only = f.resync_s <= 0;
+  const double resync_s = created_only ? 3600.0 * 24 * 365 : f.resync_s;
+  NodeWatch watch(f, &kube, &lab, created_only, g_sig_pipe[0]);
+  bool kick = true;
+  auto next_resync = clk::now();
+  const bool topo_watch = f.topology_watch_s > 0;
+  auto next_topo = after_s(f.topology_watch_s);
+  std::string topo_last = topo_watch ? topology_signature(f.sysfs_root) : "", topo_seen = topo_last;
+  while (!g_stop) {
+    if (kick || clk::now() >= next_resync) {
+      kick = false;
+      const bool ok = lab.reconcile();
+      next_resync = after_s(ok ? resync_s : 5.0);
+    }
+    if (topo_watch && clk::now() >= next_topo) {
+      next_topo = after_s(f.topology_watch_s);
+      const std::string cur = topology_signature(f.sysfs_root);
+      if (cur != topo_last && cur == topo_seen) {
+        topo_last = cur;
+        ++lab.st.topology_changes;
+        MI_LOG(kInfo, "GPU topology changed (partition switch?): relabelling node %s", f.node_name.c_str());
+        kick = true;
+      }
+      topo_seen = cur;
+      if (kick) continue;
+    }
+    int wait_ms = ms_until(next_resync);
+    if (topo_watch) wait_ms = std::min(wait_ms, ms_until(next_topo));
+    const NodeWatch::Event ev = watch.wait(wait_ms);
+    if (ev == NodeWatch::kStop) break;
+    if (ev == NodeWatch::kKick) kick = true;
+  }
+  MI_LOG(kInfo, "Received signal, shutting down. passes=%d patches=%d updates=%d errors=%d watch_events=%d "
+                "watch_kicks=%d watch_errors=%d watch_restarts=%d topology_changes=%d",
+         lab.st.passes, lab.st.patches, lab.st.updates, lab.st.errors, lab.st.watch_events, lab.st.watch_kicks,
+         lab.st.watch_errors, lab.st.watch_restarts, lab.st.topology_changes);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -461,45 +674,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   Kube kube;
-  // controller-runtime GetConfigOrDie: -kubeconfig, else in-cluster unless
-  // $KUBECONFIG is set, else $KUBECONFIG / $HOME/.kube/config
-  const char* svc_host = std::getenv("KUBERNETES_SERVICE_HOST");
-  const bool in_cluster = (svc_host && *svc_host) || !f.apiserver.empty();
-  const std::string kc_path = !f.kubeconfig.empty() ? f.kubeconfig : kube::default_kubeconfig_path(in_cluster);
-  if (!kc_path.empty()) {
-    auto kc = kube::load_kubeconfig(kc_path, &err);
-    if (!kc) {
-      MI_LOG(kError, "unable to set up kubernetes client: %s", err.c_str());
-      return 1;
-    }
-    kube.cfg = kc->http;
-    kube.token = kc->token;
-    kube.token_file = kc->token_file;
-    MI_LOG(kInfo, "kubeconfig %s: server %s", kc_path.c_str(), kube.cfg.server.c_str());
-  } else if (!f.apiserver.empty()) {
-    kube.cfg.server = f.apiserver;
-  } else {
-    const char* host = std::getenv("KUBERNETES_SERVICE_HOST");
-    const char* port = std::getenv("KUBERNETES_SERVICE_PORT");
-    if (!host || !*host) {
-      MI_LOG(kError, "unable to set up kubernetes client: not running in a cluster (KUBERNETES_SERVICE_HOST unset)");
-      return 1;
-    }
-    std::string h = host;
-    if (h.find(':') != std::string::npos && h[0] != '[') h = "[" + h + "]";
-    kube.cfg.server = "https://" + h + ":" + (port && *port ? port : "443");
-  }
-  if (kc_path.empty()) {
-    kube.token_file = !f.token_file.empty() ? f.token_file : path_join(f.sa_dir, "token");
-    kube.cfg.ca_file = !f.ca_file.empty() ? f.ca_file
-                       : path_exists(path_join(f.sa_dir, "ca.crt")) ? path_join(f.sa_dir, "ca.crt")
-                                                                     : "";
-  }
-  if (kc_path.empty() && kube.bearer().empty() && f.apiserver.empty()) {
-    MI_LOG(kError, "unable to set up kubernetes client: service-account token %s is unreadable or empty",
-         kube.token_file.c_str());
-    return 1;
-  }
+  if (!configure_kube(f, &kube)) return 1;
 
   if (::pipe(g_sig_pipe) != 0) return 1;
   ::fcntl(g_sig_pipe[0], F_SETFL, O_NONBLOCK);
@@ -520,132 +695,5 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  // -resync 0: the reference's controller (main.go:553-586): label at start,
-  // then only when the Node object is (re-)created; no periodic re-assert
-  const bool created_only = f.resync_s <= 0;
-  const double resync_s = created_only ? 3600.0 * 24 * 365 : f.resync_s;
-
-  bool kick = true;
-  auto next_resync = clk::now();
-  const bool topo_watch = f.topology_watch_s > 0;
-  auto next_topo = after_s(f.topology_watch_s);
-  std::string topo_last = topo_watch ? topology_signature(f.sysfs_root) : "", topo_seen = topo_last;
-  http::Stream stream;
-  bool stream_open = false;
-  auto stream_opened = clk::now();
-  auto watch_retry = clk::now();
-  double backoff = 0.2;
-  std::string rv;
-  const http::Config wcfg = [&] {
-    http::Config c = kube.cfg;
-    c.timeout_s = f.watch_timeout_s + 30.0;
-    return c;
-  }();
-
-  while (!g_stop) {
-    if (kick || clk::now() >= next_resync) {
-      kick = false;
-      const bool ok = lab.reconcile();
-      next_resync = after_s(ok ? resync_s : 5.0);
-    }
-    if (topo_watch && clk::now() >= next_topo) {
-      next_topo = after_s(f.topology_watch_s);
-      const std::string cur = topology_signature(f.sysfs_root);
-      // act once the new fingerprint has held one interval (a switch passes through half states)
-      if (cur != topo_last && cur == topo_seen) {
-        topo_last = cur;
-        ++lab.st.topology_changes;
-        MI_LOG(kInfo, "GPU topology changed (partition switch?): relabelling node %s", f.node_name.c_str());
-        kick = true;
-      }
-      topo_seen = cur;
-      if (kick) continue;
-    }
-    int wait_ms = ms_until(next_resync);
-    if (topo_watch) wait_ms = std::min(wait_ms, ms_until(next_topo));
-    if (f.watch && !stream_open && clk::now() >= watch_retry) {
-      std::string q = "/api/v1/nodes?watch=1&fieldSelector=" + path_escape("metadata.name=" + f.node_name) +
-                      "&timeoutSeconds=" + std::to_string(f.watch_timeout_s) + "&allowWatchBookmarks=true";
-      if (!rv.empty()) q += "&resourceVersion=" + path_escape(rv);
-      int status = 0;
-      std::string ebody;
-      const std::string e =
-          stream.open(wcfg, q, kube.headers(), &status, &ebody, static_cast<int>(kube.cfg.timeout_s * 1000),
-                      g_sig_pipe[0]);
-      if (g_stop) break;
-      if (!e.empty() || status != 200) {
-        if (status == 410) rv.clear();
-        if (status == 401) kube.bearer(true);
-        ++lab.st.watch_errors;
-        MI_LOG(kWarning, "watch of node %s failed (%s); retrying in %.1fs", f.node_name.c_str(),
-             e.empty() ? ("HTTP " + std::to_string(status) + ": " + ebody.substr(0, 200)).c_str() : e.c_str(),
-             backoff);
-        stream.close();
-        watch_retry = after_s(backoff);
-        backoff = std::min(backoff * 2, f.watch_backoff_max_s);
-      } else {
-        stream_open = true;
-        stream_opened = clk::now();
-        ++lab.st.watch_restarts;
-      }
-    }
-    if (!stream_open) {
-      if (f.watch) wait_ms = std::min(wait_ms, ms_until(watch_retry));
-      pollfd p{g_sig_pipe[0], POLLIN, 0};
-      ::poll(&p, 1, wait_ms);
-      continue;
-    }
-    std::string line;
-    const int rc = stream.next_line(&line, wait_ms, g_sig_pipe[0]);
-    if (rc == -2) continue;  // timer due
-    if (rc == -3 || g_stop) break;
-    if (rc == 1) {
-      if (line.find_first_not_of(" \t\r") == std::string::npos) continue;
-      ++lab.st.watch_events;
-      auto ev = json::parse(line);
-      if (!ev) continue;
-      const std::string type = ev->str("type");
-      const json::Value* obj = ev->get("object");
-      if (type == "ERROR") {
-        if (obj && obj->str("code") == "410") {  // resourceVersion too old: re-list
-          rv.clear();
-          kick = true;
-        }
-        stream.close();
-        stream_open = false;
-        watch_retry = after_s(backoff);
-        backoff = std::min(backoff * 2, f.watch_backoff_max_s);
-        continue;
-      }
-      if (obj) {
-        const json::Value* md = obj->get("metadata");
-        if (md && !md->str("resourceVersion").empty()) rv = md->str("resourceVersion");
-        if ((type == "ADDED" || (type == "MODIFIED" && !created_only)) && lab.needs_reconcile(*obj)) {
-          ++lab.st.watch_kicks;
-          kick = true;
-        }
-      }
-      continue;
-    }
-    // the stream ended (server timeout) or broke
-    stream.close();
-    stream_open = false;
-    const bool lived = clk::now() - stream_opened >= std::chrono::seconds(1);
-    if (rc == 0 && lived) {
-      backoff = 0.2;
-      watch_retry = clk::now();
-    } else {
-      if (rc != 0) {
-        ++lab.st.watch_errors;
-        MI_LOG(kWarning, "watch of node %s broke; retrying in %.1fs", f.node_name.c_str(), backoff);
-      }
-      watch_retry = after_s(backoff);  // a server that ends every stream at once is not hammered
-      backoff = std::min(backoff * 2, f.watch_backoff_max_s);
-    }
-  }
-  MI_LOG(kInfo, "Received signal, shutting down. passes=%d patches=%d updates=%d errors=%d watch_events=%d "
-            "watch_kicks=%d watch_errors=%d watch_restarts=%d topology_changes=%d",
-       lab.st.passes, lab.st.patches, lab.st.updates, lab.st.errors, lab.st.watch_events, lab.st.watch_kicks,
-       lab.st.watch_errors, lab.st.watch_restarts, lab.st.topology_changes);
-  return 0;
+  return run(f, lab, kube);
 }
