@@ -219,6 +219,41 @@ def test_watch_restores_stripped_labels_and_survives_expiry(tmp_path):
         srv.stop()
 
 
+def test_watch_from_a_compacted_resource_version_relists(tmp_path):
+    """A watch resumed from a compacted resourceVersion gets a 410 ERROR event:
+    the labeller re-lists (a reconcile: GET of the node) and watches again
+    without a resourceVersion, so later edits are still seen."""
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        srv.add_node("node-n")
+        p, _ = _start(fi, srv, tmp_path, "-resync", "300", "-topology_watch", "0", "-watch_backoff_max", "0.2")
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"))
+        assert _wait(lambda: srv.watch_starts >= 1)
+
+        def gets():
+            return sum(1 for m, path, _ in list(srv.requests) if m == "GET")
+
+        gets0, starts = gets(), srv.watch_starts
+        srv.min_rv = 10 ** 6
+        srv.expire_watches()                       # reconnects from its last resourceVersion: 410
+        assert _wait(lambda: srv.watch_starts >= starts + 2, 5.0)
+        srv.min_rv = 0
+        watches = [path for m, path, _ in list(srv.requests) if m == "WATCH"][starts:]
+        assert "resourceVersion=" in watches[0]    # the resumed watch
+        assert _wait(lambda: gets() > gets0, 3.0)  # the re-list
+        assert any("resourceVersion=" not in w for w in watches[1:]), watches
+        srv.set_labels("node-n", {"other": "x"})   # the fresh watch still restores stripped labels
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 3.0)
+        rc, err = _stop(p)
+        assert rc == 0, err
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
 def test_update_fallback_when_patch_is_forbidden(tmp_path):
     """The upstream ClusterRole grants update, not patch: GET + PUT (controller.go:23-58)."""
     fi = make_mi355x_node(tmp_path / "n")
