@@ -58,6 +58,8 @@ using Fields = std::vector<std::pair<std::string, std::string>>;
 // a bare "-name".
 bool parse_flag(const std::string& name, const std::string& value, bool has_value, Options* o, std::string* err);
 bool is_bool_flag(const std::string& name);
+// true for every flag parse_flag handles (defined-flag check before a value is consumed)
+bool is_flag(const std::string& name);
 
 // Applies the options ("" or an error, e.g. a malformed -vmodule).
 std::string init(const Options& o);

@@ -54,8 +54,14 @@ int main(int argc, char** argv) {
   using namespace mi355x;
   daemon::Flags f;
   std::string err;
-  bool help = false;
-  if (!daemon::parse_flags(argc, argv, &f, &err, &help)) {
+  bool help = false, syntax = false;
+  if (!daemon::parse_flags(argc, argv, &f, &err, &help, &syntax)) {
+    if (syntax) {  // the flag package's failure: the error, then flag.Usage (main.go:43-49), exit 2
+      std::fprintf(stderr, "%s\n", err.c_str());
+      for (const auto& line : versions::banner(kTitle, argv[0], f.sysfs_root)) std::fprintf(stderr, "%s\n", line.c_str());
+      std::fprintf(stderr, "%s", daemon::usage(argv[0]).c_str());
+      return 2;
+    }
     glog::init(f.log);
     MI_LOG(kError, "%s", err.c_str());
     return 1;

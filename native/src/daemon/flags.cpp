@@ -33,8 +33,11 @@ std::string usage(const std::string& argv0) {
          "[-vmodule P=N] [-log_backtrace_at FILE:N]\n";
 }
 
-bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help) {
+bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, bool* syntax) {
   *help = false;
+  bool syntax_scratch = false;
+  if (!syntax) syntax = &syntax_scratch;
+  *syntax = false;
   std::map<std::string, bool*> bools = {
       {"send_every_pulse", &f->send_every_pulse}, {"allocator_extended_search", &f->allocator_extended_search},
       {"liveness", &f->liveness}, {"liveness_keep_queues", &f->liveness_keep_queues},
@@ -67,10 +70,18 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help) 
   if (const char* c = std::getenv("CONFIG_FILE_PATH")) f->config = c;
   static std::string ignored;
   strs["kubelet-url"] = &ignored;  // accepted for compatibility (docs promise it; registration uses the UDS)
+  // the flag package's own errors (exit 2 in main)
+  auto bad = [&](std::string msg) {
+    *err = std::move(msg);
+    *syntax = true;
+    return false;
+  };
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
-    if (a.size() < 2 || a[0] != '-') return *err = "unexpected argument " + a, false;
+    if (a == "--") break;                            // terminator, consumed
+    if (a.size() < 2 || a[0] != '-') break;          // first non-flag argument: parsing stops
     a = a.substr(a[1] == '-' ? 2 : 1);
+    if (a.empty() || a[0] == '-' || a[0] == '=') return bad("bad flag syntax: " + std::string(argv[i]));
     std::string name = a, value;
     bool has_value = false;
     const size_t eq = a.find('=');
@@ -80,35 +91,35 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help) 
       has_value = true;
     }
     if (name == "h" || name == "help") return *help = true, true;
+    if (!bools.count(name) && !ints.count(name) && !floats.count(name) && !strs.count(name) && !glog::is_flag(name))
+      return bad("flag provided but not defined: -" + name);
     if (bools.count(name) || glog::is_bool_flag(name)) {
       if (glog::is_bool_flag(name)) {
         glog::parse_flag(name, value, has_value, &f->log, err);
-        if (!err->empty()) return false;
+        if (!err->empty()) return bad(*err);
       } else if (!parse_bool(has_value ? value : "", bools[name])) {
-        return *err = "invalid boolean value \"" + value + "\" for -" + name, false;
+        return bad("invalid boolean value \"" + value + "\" for -" + name);
       }
       continue;
     }
     if (!has_value) {
-      if (i + 1 >= argc) return *err = "flag needs an argument: -" + name, false;
+      if (i + 1 >= argc) return bad("flag needs an argument: -" + name);
       value = argv[++i];
     }
     if (glog::parse_flag(name, value, true, &f->log, err)) {
-      if (!err->empty()) return false;
+      if (!err->empty()) return bad(*err);
     } else if (ints.count(name)) {
       char* end = nullptr;
       const long v = std::strtol(value.c_str(), &end, 10);
-      if (value.empty() || *end) return *err = "invalid value \"" + value + "\" for flag -" + name, false;
+      if (value.empty() || *end) return bad("invalid value \"" + value + "\" for flag -" + name);
       *ints[name] = static_cast<int>(v);
     } else if (floats.count(name)) {
       char* end = nullptr;
       const double v = std::strtod(value.c_str(), &end);
-      if (value.empty() || *end) return *err = "invalid value \"" + value + "\" for flag -" + name, false;
+      if (value.empty() || *end) return bad("invalid value \"" + value + "\" for flag -" + name);
       *floats[name] = v;
-    } else if (strs.count(name)) {
-      *strs[name] = value;
     } else {
-      return *err = "flag provided but not defined: -" + name, false;
+      *strs[name] = value;
     }
   }
   // validateFlags (main.go:59-75)

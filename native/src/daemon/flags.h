@@ -67,10 +67,13 @@ struct Flags {
   glog::Options log;
 };
 
-// Go flag syntax (-name=value, -name value, --name, bare booleans) plus
-// validateFlags (main.go:59-75). false and *err on a bad command line;
-// -h / -help set *help and return true.
-bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help);
+// Go flag syntax (-name=value, -name value, --name, bare booleans; parsing
+// stops at the first non-flag argument or after "--") plus validateFlags
+// (main.go:59-75). false and *err on a bad command line, with *syntax set when
+// the flag package itself would have refused it (an undefined flag, a missing
+// or unparsable value: Go prints the error and the usage and exits 2) rather
+// than validateFlags (logged, exit 1). -h / -help set *help and return true.
+bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, bool* syntax = nullptr);
 
 // the flag synopsis printed by -h (after the version banner)
 std::string usage(const std::string& argv0);

@@ -110,15 +110,41 @@ bool parse_double(const std::string& v, double* out) {
   return true;
 }
 
-// Go flag syntax: -name=value, -name value, --name; booleans only take =value.
-bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
+// the version banner, then the flags (main.go flag.Usage)
+void print_usage(FILE* out, const char* argv0, const std::string& sysfs_root) {
+  for (const auto& line : versions::banner(kTitle, argv0, sysfs_root)) std::fprintf(out, "%s\n", line.c_str());
+  std::fprintf(out, "usage: %s [-<label kind> ...] [-driver_type container|vf-passthrough|pf-passthrough] "
+               "[-node_name NAME] [-kubeconfig PATH] [-resync S] [-once] [-watch=false] [-topology_watch S] "
+               "[-dry_run] [-sysfs_root DIR] [-dev_root DIR] [-v N] [-logtostderr] [-alsologtostderr] "
+               "[-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] [-log_backtrace_at FILE:N]\nlabel kinds:",
+               argv0);
+  for (const auto& k : kKinds) std::fprintf(out, " -%s", k.c_str());
+  std::fprintf(out, "\n");
+}
+
+// Go flag syntax: -name=value, -name value, --name; booleans only take =value;
+// parsing stops at the first non-flag argument or after "--". *syntax: the
+// flag package itself would have refused the line (exit 2 with the usage);
+// otherwise the error is the labeller's own validation (exit 1).
+bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* syntax) {
   for (const auto& k : kKinds) f->enabled[k] = false;
   if (const char* n = std::getenv("DS_NODE_NAME")) f->node_name = n;
   static const std::set<std::string> kBool = {"watch", "dry_run", "once"};
+  static const std::set<std::string> kValued = {"driver_type", "node_name", "kubeconfig", "resync", "topology_watch",
+                                                "watch_backoff_max", "watch_timeout", "sysfs_root", "dev_root",
+                                                "sa_dir", "apiserver", "token_file", "ca_file"};
+  *syntax = false;
+  auto bad = [&](std::string msg) {
+    *err = std::move(msg);
+    *syntax = true;
+    return false;
+  };
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
-    if (a.size() < 2 || a[0] != '-') return *err = "unexpected argument " + a, false;
+    if (a == "--") break;                            // terminator, consumed
+    if (a.size() < 2 || a[0] != '-') break;          // first non-flag argument: parsing stops
     a = a.substr(a[1] == '-' ? 2 : 1);
+    if (a.empty() || a[0] == '-' || a[0] == '=') return bad("bad flag syntax: " + std::string(argv[i]));
     std::string name = a, value;
     bool has_value = false;
     const size_t eq = a.find('=');
@@ -127,27 +153,21 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       value = a.substr(eq + 1);
       has_value = true;
     }
-    if (name == "h" || name == "help") {  // the version banner, then the flags (main.go flag.Usage)
-      for (const auto& line : versions::banner(kTitle, argv[0], f->sysfs_root)) std::printf("%s\n", line.c_str());
-      std::printf("usage: %s [-<label kind> ...] [-driver_type container|vf-passthrough|pf-passthrough] "
-                  "[-node_name NAME] [-kubeconfig PATH] [-resync S] [-once] [-watch=false] [-topology_watch S] "
-                  "[-dry_run] [-sysfs_root DIR] [-dev_root DIR] [-v N] [-logtostderr] [-alsologtostderr] "
-                  "[-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] [-log_backtrace_at FILE:N]\nlabel kinds:",
-                  argv[0]);
-      for (const auto& k : kKinds) std::printf(" -%s", k.c_str());
-      std::printf("\n");
+    if (name == "h" || name == "help") {
+      print_usage(stdout, argv[0], f->sysfs_root);
       std::exit(0);
     }
     const bool is_kind = f->enabled.count(name) > 0;
+    if (!is_kind && !kBool.count(name) && !kValued.count(name) && !glog::is_flag(name))
+      return bad("flag provided but not defined: -" + name);
     if (glog::is_bool_flag(name)) {
       glog::parse_flag(name, value, has_value, &f->log, err);
-      if (!err->empty()) return false;
+      if (!err->empty()) return bad(*err);
       continue;
     }
     if (is_kind || kBool.count(name)) {
       bool v = true;
-      if (has_value && !parse_bool(value, &v))
-        return *err = "invalid boolean value \"" + value + "\" for -" + name, false;
+      if (has_value && !parse_bool(value, &v)) return bad("invalid boolean value \"" + value + "\" for -" + name);
       if (is_kind) f->enabled[name] = v;
       if (name == "watch") f->watch = v;
       if (name == "dry_run") f->dry_run = v;
@@ -155,11 +175,11 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       continue;
     }
     if (!has_value) {
-      if (i + 1 >= argc) return *err = "flag needs an argument: -" + name, false;
+      if (i + 1 >= argc) return bad("flag needs an argument: -" + name);
       value = argv[++i];
     }
     if (glog::parse_flag(name, value, true, &f->log, err)) {
-      if (!err->empty()) return false;
+      if (!err->empty()) return bad(*err);
     } else if (name == "driver_type") {
       f->driver_type = value;
     } else if (name == "node_name") {
@@ -167,15 +187,18 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
     } else if (name == "kubeconfig") {
       f->kubeconfig = value;
     } else if (name == "resync") {
-      if (!parse_double(value, &f->resync_s)) return *err = "invalid value \"" + value + "\" for -resync", false;
+      if (!parse_double(value, &f->resync_s)) return bad("invalid value \"" + value + "\" for flag -resync");
     } else if (name == "topology_watch") {
       if (!parse_double(value, &f->topology_watch_s))
-        return *err = "invalid value \"" + value + "\" for -topology_watch", false;
+        return bad("invalid value \"" + value + "\" for flag -topology_watch");
     } else if (name == "watch_backoff_max") {
       if (!parse_double(value, &f->watch_backoff_max_s))
-        return *err = "invalid value \"" + value + "\" for -watch_backoff_max", false;
+        return bad("invalid value \"" + value + "\" for flag -watch_backoff_max");
     } else if (name == "watch_timeout") {
-      f->watch_timeout_s = std::max(1, std::atoi(value.c_str()));
+      char* end = nullptr;
+      const long v = std::strtol(value.c_str(), &end, 10);
+      if (value.empty() || *end) return bad("invalid value \"" + value + "\" for flag -watch_timeout");
+      f->watch_timeout_s = static_cast<int>(std::max(1L, v));
     } else if (name == "sysfs_root") {
       f->sysfs_root = value;
     } else if (name == "dev_root") {
@@ -188,8 +211,6 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err) {
       f->token_file = value;
     } else if (name == "ca_file") {
       f->ca_file = value;
-    } else {
-      return *err = "flag provided but not defined: -" + name, false;
     }
   }
   if (!f->driver_type.empty() && f->driver_type != "container" && f->driver_type != "vf-passthrough" &&
@@ -651,7 +672,13 @@ int run(const Flags& f, Labeller& lab, Kube& kube) {
 int main(int argc, char** argv) {
   Flags f;
   std::string err;
-  if (!parse_flags(argc, argv, &f, &err)) {
+  bool syntax = false;
+  if (!parse_flags(argc, argv, &f, &err, &syntax)) {
+    if (syntax) {  // the flag package's failure: the error, then the usage, exit 2
+      std::fprintf(stderr, "%s\n", err.c_str());
+      print_usage(stderr, argv[0], f.sysfs_root);
+      return 2;
+    }
     glog::init(f.log);
     MI_LOG(kError, "%s", err.c_str());
     return 1;

@@ -110,6 +110,14 @@ FILE* open_file(State& s, int sev, const tm& lt) {
 
 bool is_bool_flag(const std::string& name) { return name == "logtostderr" || name == "alsologtostderr"; }
 
+bool is_flag(const std::string& name) {
+  static const char* kNames[] = {"logtostderr", "alsologtostderr", "v", "stderrthreshold", "log_dir", "log_link",
+                                 "logbuflevel", "vmodule", "log_backtrace_at", "log_format"};
+  for (const char* n : kNames)
+    if (name == n) return true;
+  return false;
+}
+
 bool parse_flag(const std::string& name, const std::string& value, bool has_value, Options* o, std::string* err) {
   auto as_bool = [&](bool* out) {
     if (!has_value || value == "1" || value == "true" || value == "True" || value == "TRUE" || value == "t" ||

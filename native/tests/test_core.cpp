@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include "../src/rpc/hpack.h"
+#include "flags.h"
 #include "health_controller.h"
 #include "registration.h"
 #include "topology_watch.h"
@@ -727,6 +728,37 @@ static void test_topology_watch() {
   CHECK(w.observe("d", true));
 }
 
+// Go's flag package: syntax errors (exit 2) vs validateFlags (exit 1), the
+// first non-flag argument or "--" ends parsing, an undefined flag is refused
+// before it can take the next argument as its value
+static void test_flags_go_semantics() {
+  auto parse = [](std::vector<std::string> args, bool* syntax, std::string* err, daemon::Flags* out = nullptr) {
+    args.insert(args.begin(), "k8s-device-plugin");
+    std::vector<char*> argv;
+    for (auto& a : args) argv.push_back(a.data());
+    daemon::Flags f;
+    bool help = false;
+    const bool ok = daemon::parse_flags(static_cast<int>(argv.size()), argv.data(), &f, err, &help, syntax);
+    if (out) *out = f;
+    return ok;
+  };
+  bool syn = false;
+  std::string err;
+  daemon::Flags f;
+  CHECK(parse({"-pulse=30", "--driver_type", "container", "-v=5", "-logtostderr"}, &syn, &err, &f) && f.pulse == 30 &&
+        f.driver_type == "container" && f.log.v == 5);
+  CHECK(!parse({"-nope", "-pulse=3"}, &syn, &err) && syn && err == "flag provided but not defined: -nope");
+  CHECK(!parse({"-pulse", "x"}, &syn, &err) && syn && err.find("invalid value") == 0);
+  CHECK(!parse({"-pulse"}, &syn, &err) && syn && err == "flag needs an argument: -pulse");
+  CHECK(!parse({"-liveness=maybe"}, &syn, &err) && syn);
+  CHECK(!parse({"---pulse=1"}, &syn, &err) && syn && err.find("bad flag syntax") == 0);
+  CHECK(!parse({"-pulse=-1"}, &syn, &err) && !syn && err == "pulse must be a non-negative integer");
+  CHECK(!parse({"-driver_type", "gim"}, &syn, &err) && !syn);
+  CHECK(parse({"-pulse=2", "extra", "-nope"}, &syn, &err, &f) && f.pulse == 2);  // stops at "extra"
+  CHECK(parse({"-pulse=2", "--", "-nope"}, &syn, &err, &f) && f.pulse == 2);
+  CHECK(parse({"-pulse=2", "-", "-nope"}, &syn, &err, &f) && f.pulse == 2);      // "-" is an argument
+}
+
 static void test_health_controller_generations(const std::string& tmp) {
   // passthrough sweeps on worker threads against a reload on the control thread
   // (run under TSan in CI: the job shares nothing with the controller)
@@ -781,6 +813,7 @@ int main(int argc, char** argv) {
   test_registration_watchdog();
   test_registration_random_sequences();
   test_topology_watch();
+  test_flags_go_semantics();
   {
     char dir[] = "/tmp/mi355x-test-core-XXXXXX";
     if (::mkdtemp(dir)) {

@@ -225,7 +225,7 @@ def test_a_wrong_flag_or_command_fails(tmp_path, node):
     c = dict(next(containers(yaml.safe_load_all(open(os.path.join(REPO, "k8s-ds-amdgpu-dp-health.yaml")))))[1])
     bad = dict(c, args=list(c["args"]) + ["-liveness_sweep_evry=3"])
     rc, _, err, _ = run_container(bad, tmp_path, node)
-    assert rc == 1 and "flag provided but not defined: -liveness_sweep_evry" in err
+    assert rc == 2 and "flag provided but not defined: -liveness_sweep_evry" in err   # Go's flag package: exit 2
     with pytest.raises(AssertionError, match="does not exist in the image"):
         run_container(dict(c, command=["./k8s-device-plugin-py"]), tmp_path, node)
     with pytest.raises(AssertionError, match="is not an image this build makes"):

@@ -162,7 +162,8 @@ def test_json_log_format_in_both_binaries(tmp_path):
     assert any("reconcile of node n failed" in r["msg"] and r["level"] == "ERROR" for r in lrecs)
     for exe in (DP, LBL):
         bad = subprocess.run([exe, "-log_format", "xml"], capture_output=True, text=True, timeout=20)
-        assert bad.returncode == 1 and "log_format" in bad.stderr
+        # an unparsable flag value is the flag package's error: usage, exit 2
+        assert bad.returncode == 2 and "log_format" in bad.stderr
 
 
 # ------------------------------------------------------------------ kubeconfig

@@ -450,10 +450,14 @@ def test_daemon_watchdog_exits_when_kubelet_never_lists(tmp_path):
 
 def test_daemon_refuses_unknown_flags_and_bad_liveness(tmp_path):
     # -grpc_server was the Python CLI's transport switch; the daemon is the only
-    # plugin entrypoint, so it is an undefined flag like any other (Go's flag wording)
-    for args, want in ((["-grpc_server", "aio"], "flag provided but not defined: -grpc_server"),
-                       (["-liveness"], "-pulse > 0"),
-                       (["-liveness_mode", "bogus"], "liveness_mode"),
-                       (["-vmodule", "nolevel"], "vmodule")):
+    # plugin entrypoint, so it is an undefined flag like any other: Go's flag
+    # package prints the error and the usage and exits 2; validation errors
+    # (validateFlags, main.go:59-75) are logged and exit 1
+    for args, want, rc in ((["-grpc_server", "aio"], "flag provided but not defined: -grpc_server", 2),
+                           (["-liveness"], "-pulse > 0", 1),
+                           (["-liveness_mode", "bogus"], "liveness_mode", 1),
+                           (["-vmodule", "nolevel"], "vmodule", 1)):
         p = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=20)
-        assert p.returncode == 1 and want in p.stderr, (args, p.stderr)
+        assert p.returncode == rc and want in p.stderr, (args, p.stderr)
+    p = subprocess.run([EXE, "-grpc_server", "aio"], capture_output=True, text=True, timeout=20)
+    assert "usage:" in p.stderr.lower() and not p.stdout

@@ -104,9 +104,15 @@ def test_flags_follow_go_syntax(tmp_path):
                        text=True, timeout=30)
     assert p.returncode == 0 and set(json.loads(p.stdout)) == {"amd.com/gpu.vram", "amd.com/gpu.vram.288G",
                                                                "beta.amd.com/gpu.vram", "beta.amd.com/gpu.vram.288G"}
-    for bad in (["-nope"], ["-driver_type", "gim"], ["-vram=maybe"], ["-resync", "x"]):
+    # the flag package's own errors exit 2 (with the usage); the labeller's validation exits 1
+    for bad, rc in ((["-nope"], 2), (["-driver_type", "gim"], 1), (["-vram=maybe"], 2), (["-resync", "x"], 2),
+                    (["-watch_timeout", "x"], 2), (["---vram"], 2), (["-resync"], 2)):
         p = subprocess.run(base + bad, capture_output=True, text=True, timeout=30)
-        assert p.returncode == 1, bad
+        assert p.returncode == rc, (bad, p.returncode, p.stderr)
+    # parsing stops at the first non-flag argument and after "--", as Go's does
+    for tail in (["extra", "-nope"], ["--", "-nope"]):
+        p = subprocess.run(base + ["-vram"] + tail, capture_output=True, text=True, timeout=30)
+        assert p.returncode == 0 and "amd.com/gpu.vram" in json.loads(p.stdout), (tail, p.stderr)
     p = subprocess.run([EXE, "-h"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 0 and "-compute-memory-partition" in p.stdout
     # an unreadable kubeconfig, no cluster env -> clear errors

@@ -293,7 +293,7 @@ def test_launchers_run_the_native_binaries(tmp_path):
     assert p.returncode == 0 and json.loads(p.stdout)["resources"], p.stderr[-2000:]
     assert "native daemon" in p.stderr
     p = subprocess.run(base + ["-grpc_server", "aio"], capture_output=True, text=True, timeout=120)
-    assert p.returncode == 1 and "flag provided but not defined: -grpc_server" in p.stderr
+    assert p.returncode == 2 and "flag provided but not defined: -grpc_server" in p.stderr   # Go's flag package
     lbl = str(REPO / "scripts/k8s-node-labeller")
     args = ["-dry_run", "-node_name", "n", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-vram", "-device-id"]
     nat = subprocess.run([lbl, *args], capture_output=True, text=True, timeout=60)
