@@ -144,8 +144,11 @@ class NativePluginUnderTest:
         m = self.metrics()
         n = int(m.get("mi355x_dp_health_sweep_seconds_count", 0))
         st = self.kubelet.resources.get("amd.com/gpu")
+        # the mean includes the start-up sweep (probe server and amd-smi start); the p50 is the
+        # upper bound of the histogram bucket that holds the median sweep
         return {"plugin": "native-daemon", "pulse_s": pulse_s, "sweeps": n,
                 "sweep_ms_mean": round(m.get("mi355x_dp_health_sweep_seconds_sum", 0.0) * 1e3 / n, 3) if n else None,
+                "sweep_ms_p50_at_most": _bucket_quantile_ms(m, "mi355x_dp_health_sweep_seconds", .5),
                 "health_changes": int(m.get("mi355x_dp_health_changes_total", 0)),
                 "unhealthy": sorted(d for d, h in (st.devices.items() if st else ()) if h != "Healthy")}
 
@@ -160,6 +163,25 @@ class NativePluginUnderTest:
             self.proc.kill()
             self.proc.wait()
         self._reader.join(timeout=5)
+
+
+def _bucket_quantile_ms(m: dict, name: str, q: float):
+    """Upper bound (ms) of the Prometheus histogram bucket holding quantile q, from
+    a parsed /metrics dict ({'name_bucket{le="0.005"}': count, ...}); None if empty."""
+    import math
+    buckets = []
+    for k, v in m.items():
+        if k.startswith(name + "_bucket{") and 'le="' in k:
+            le = k.split('le="', 1)[1].split('"', 1)[0]
+            buckets.append((math.inf if le == "+Inf" else float(le), v))
+    buckets.sort()
+    total = buckets[-1][1] if buckets else 0
+    if not total:
+        return None
+    for le, cum in buckets:
+        if cum >= q * total:
+            return None if math.isinf(le) else round(le * 1e3, 3)
+    return None
 
 
 class PluginUnderTest:

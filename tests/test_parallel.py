@@ -281,4 +281,5 @@ def test_bench_health_pulse_runs_on_the_native_daemon():
     hl = d["extra"]["health_loop"]
     assert d["config"]["plugin"] == "native-daemon" and hl["plugin"] == "native-daemon"
     assert hl["pulse_s"] == 1.0 and hl["sweeps"] >= 1 and hl["sweep_ms_mean"] is not None
+    assert hl["sweep_ms_p50_at_most"] is not None and hl["sweep_ms_p50_at_most"] > 0
     assert hl["unhealthy"] == [] and hl["health_changes"] == 0
