@@ -1081,6 +1081,45 @@ def test_collectives_cli_on_rccl():
         assert r["ok"] is True and r["ranks"] == 1 and r["dtype"] == "bfloat16"
 
 
+_BENCH_RCCL = r"""
+import json, torch, torch.distributed as dist
+from rocm_k8s_device_plugin_amd.benchmark.coord import Dist
+from rocm_k8s_device_plugin_amd.parallel import collectives as coll
+d = Dist()
+if d.world == 1:            # bench.py creates the gloo world only at N > 1; do it here for one rank
+    dist.init_process_group("gloo")
+    d.torch, d.dist = torch, dist
+group, on_gpu = d.rccl_group()  # what bench.py's collectives stage calls after the timed loop
+rows = coll.run([1 << 20, 16 << 20], coll.DEFAULT_OPS, iters=3, warmup=1, dtype=torch.bfloat16, group=group)
+print(json.dumps({"backend": dist.get_backend(group), "on_gpu": on_gpu, "cuda": d.cuda, "summary": coll.summary(rows)}))
+dist.destroy_process_group()
+"""
+
+
+def test_bench_rccl_group_on_top_of_the_gloo_world(tmp_path):
+    """bench.py's collectives stage: an RCCL group created on the GPU after the
+    timed loop, on top of the gloo world the ranks coordinate over (one rank
+    here; the driver's 8-GPU run uses 8)."""
+    import socket
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = tmp_path / "bench_rccl.py"
+    script.write_text(_BENCH_RCCL)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=repo + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), str(script)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["backend"] == "nccl" and out["on_gpu"] is True and out["cuda"] is True, out
+    summ = out["summary"]
+    assert summ["ok"] is True and set(summ["busbw_gbs"]) == {"all_reduce", "all_gather", "reduce_scatter",
+                                                             "all_to_all"}, summ
+
+
 def test_topology_watch_signature_on_real_sysfs():
     """The reload fingerprint reads on the real box (kfd generation_id + partition modes) and is stable."""
     from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
