@@ -87,12 +87,22 @@ def git_describe() -> str:
     return r.stdout.strip() if r.returncode == 0 else ""
 
 
+def variant_dir(sanitize: str = "", coverage: bool = False) -> Path:
+    """The build tree of a variant: the package build, a sanitizer build or the gcov build."""
+    if coverage:
+        return REPO_DIR / "build" / "native-coverage"
+    return BUILD_DIR if not sanitize else REPO_DIR / "build" / f"native-{sanitize.replace(',', '-')}"
+
+
 def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = None,
-          jobs: int | None = None, quiet: bool = True) -> None:
-    """Configure + build. ``hip=None`` builds the HIP probe when hipcc exists."""
+          jobs: int | None = None, quiet: bool = True, coverage: bool = False) -> None:
+    """Configure + build. ``hip=None`` builds the HIP probe when hipcc exists.
+    ``sanitize`` / ``coverage``: a host-only variant in its own tree, with its
+    binaries under ``<tree>/pkg`` (the package outputs stay untouched)."""
     if hip is None:
         hip = hipcc_available()
-    bdir = build_dir or (BUILD_DIR if not sanitize else REPO_DIR / "build" / f"native-{sanitize.replace(',', '-')}")
+    bdir = build_dir or variant_dir(sanitize, coverage)
+    variant = bool(sanitize) or coverage
     bdir.mkdir(parents=True, exist_ok=True)
     gen = ["-G", "Ninja"] if shutil.which("ninja") else []
     cfg = [
@@ -100,16 +110,17 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
         f"-DPython3_EXECUTABLE={sys.executable}",
         f"-DMI355X_BUILD_HIP={'ON' if hip else 'OFF'}",
         f"-DMI355X_SANITIZE={sanitize}",
+        f"-DMI355X_COVERAGE={'ON' if coverage else 'OFF'}",
         "-DCMAKE_BUILD_TYPE=Release",
     ]
     describe = git_describe()
     if describe:
         cfg.append(f"-DMI355X_GIT_DESCRIBE={describe}")
-    if sanitize:
-        # sanitizer builds are for ctest only; keep the package outputs untouched
+    if variant:
+        # sanitizer / coverage builds keep the package outputs untouched
         cfg.append(f"-DMI355X_PKG_DIR={bdir / 'pkg'}")
     out = subprocess.DEVNULL if quiet else None
-    if not (bdir / "CMakeCache.txt").exists() or sanitize:
+    if not (bdir / "CMakeCache.txt").exists() or variant:
         subprocess.run(cfg, check=True, stdout=out)
     else:
         # re-run configure only if the HIP option flipped, or for a new version
@@ -129,7 +140,7 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
     if res.returncode != 0:
         sys.stderr.write(res.stdout)
         raise RuntimeError("native build failed")
-    if not sanitize and build_dir is None:
+    if not variant and build_dir is None:
         STAMP.parent.mkdir(parents=True, exist_ok=True)
         STAMP.write_text(f"hip={hip}\ndigest={_source_digest()}\n")
     if not quiet:
@@ -171,9 +182,9 @@ def ensure_built(hip: bool | None = None) -> None:
     _checked.add(hip)
 
 
-def run_ctest(sanitize: str = "") -> subprocess.CompletedProcess:
-    bdir = BUILD_DIR if not sanitize else REPO_DIR / "build" / f"native-{sanitize.replace(',', '-')}"
-    build(hip=False if sanitize else None, sanitize=sanitize)
+def run_ctest(sanitize: str = "", coverage: bool = False) -> subprocess.CompletedProcess:
+    bdir = variant_dir(sanitize, coverage)
+    build(hip=False if (sanitize or coverage) else None, sanitize=sanitize, coverage=coverage)
     env = dict(os.environ)
     if "thread" in sanitize:
         env.setdefault("TSAN_OPTIONS", "halt_on_error=1")

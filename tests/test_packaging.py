@@ -176,6 +176,12 @@ def test_ci_command_lines_pass_the_real_argument_parsers():
                 anm = importlib.util.module_from_spec(aspec)
                 aspec.loader.exec_module(anm)
                 anm.make_parser().parse_args(argv[2:])
+            elif argv[1] == "tools/native_coverage.py":
+                cspec = importlib.util.spec_from_file_location("native_coverage", REPO / "tools" / "native_coverage.py")
+                cvm = importlib.util.module_from_spec(cspec)
+                cspec.loader.exec_module(cvm)
+                cvm.make_parser().parse_args(argv[2:])
+                assert all((REPO / t).exists() for t in cvm.TESTS), where
             elif argv[1] == "tools/fuzz_native.py":
                 fspec = importlib.util.spec_from_file_location("fuzz_native", REPO / "tools" / "fuzz_native.py")
                 fzm = importlib.util.module_from_spec(fspec)

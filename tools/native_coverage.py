@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Line coverage of the native host code by the CPU test suite (gcov).
+
+Builds the gcov variant of the native tree (``build/native-coverage``, host
+code only, ``-O0 --coverage``), runs the C++ unit tests (ctest) and the test
+files that drive the two native binaries with ``MI355X_NATIVE_DAEMON_EXE`` /
+``MI355X_NATIVE_LABELLER_EXE`` pointing at the instrumented builds, then asks
+gcov for every source's executed lines. Prints a per-file / per-directory
+table and writes the JSON summary (``--json-out``).
+
+Only code the tests reach through those binaries and test_core counts: the
+Python extension the rest of the suite imports is the package build, not this
+one, and GPU-only paths (the HSA / HIP probes) are not run on the CPU.
+
+    python tools/native_coverage.py --json-out profiles/r4/native_coverage_cpu.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+# the test files whose native processes honour MI355X_NATIVE_{DAEMON,LABELLER}_EXE
+# (and the files that import their EXE)
+TESTS = ["tests/test_native_daemon.py", "tests/test_native_health.py", "tests/test_native_labeller.py",
+         "tests/test_native_config_logging.py", "tests/test_native_stress.py", "tests/test_go_interop.py",
+         "tests/test_native_cdi.py", "tests/test_native_reload.py", "tests/test_native_views.py",
+         "tests/test_native_metrics.py", "tests/test_native_dryrun.py", "tests/test_native_perf.py",
+         "tests/test_native_fabric.py"]
+
+_LINES = re.compile(r"Lines executed:\s*([\d.]+)% of (\d+)")
+
+
+def make_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--json-out", default="", help="write the summary here")
+    ap.add_argument("--workers", type=int, default=4, help="pytest-xdist workers (0 = serial)")
+    ap.add_argument("--tests", nargs="*", default=TESTS, help="test files to run against the instrumented binaries")
+    ap.add_argument("--no-build", action="store_true", help="reuse the existing coverage build")
+    return ap
+
+
+def gcov_file(gcda: Path) -> tuple[str, int, int] | None:
+    """(source path relative to the repo, lines executed, executable lines) of one object's .gcda."""
+    r = subprocess.run(["gcov", "-n", "-o", str(gcda.parent), str(gcda)], capture_output=True, text=True,
+                       cwd=str(gcda.parent))
+    cur = None
+    for line in r.stdout.splitlines():
+        if line.startswith("File '"):
+            cur = line[6:-1]
+        m = _LINES.search(line)
+        if m and cur:
+            path = Path(cur)
+            if not path.is_absolute():
+                path = (gcda.parent / path).resolve()
+            try:
+                rel = path.resolve().relative_to(REPO)
+            except ValueError:
+                cur = None
+                continue
+            if str(rel).startswith("native/src/") and rel.name == gcda.name.replace(".gcda", ""):
+                total = int(m.group(2))
+                return str(rel), round(float(m.group(1)) * total / 100.0), total
+            cur = None
+    return None
+
+
+def main(argv=None) -> int:
+    a = make_parser().parse_args(argv)
+    from rocm_k8s_device_plugin_amd import _build
+    bdir = _build.variant_dir(coverage=True)
+    if not a.no_build:
+        _build.build(hip=False, coverage=True)
+    for g in bdir.rglob("*.gcda"):
+        g.unlink()
+    ct = _build.run_ctest(coverage=True)
+    if ct.returncode != 0:
+        sys.stderr.write(ct.stdout[-3000:])
+        return 1
+    env = dict(os.environ, MI355X_NATIVE_DAEMON_EXE=str(bdir / "pkg" / "bin" / "mi355x-device-plugin"),
+               MI355X_NATIVE_LABELLER_EXE=str(bdir / "pkg" / "bin" / "mi355x-node-labeller"))
+    cmd = [sys.executable, "-m", "pytest", *a.tests, "-q", "-m", "not gpu", "-p", "no:cacheprovider"]
+    if a.workers > 0:
+        cmd += ["-n", str(a.workers)]
+    t = subprocess.run(cmd, cwd=str(REPO), env=env, capture_output=True, text=True)
+    tail = (t.stdout.strip().splitlines() or [""])[-1]
+    print(f"pytest: {tail}")
+    files = {}
+    for gcda in sorted(bdir.rglob("*.gcda")):
+        got = gcov_file(gcda)
+        if not got:
+            continue
+        rel, hit, total = got
+        h0, t0 = files.get(rel, (0, 0))
+        # a source built into two targets reports its lines twice: keep the better-covered object
+        files[rel] = max((h0, t0), (hit, total), key=lambda x: (x[0], -x[1]))
+    by_dir: dict[str, list[int]] = {}
+    for rel, (hit, total) in files.items():
+        d = str(Path(rel).parent)
+        s = by_dir.setdefault(d, [0, 0])
+        s[0] += hit
+        s[1] += total
+    hit_all = sum(h for h, _ in files.values())
+    tot_all = sum(t for _, t in files.values())
+    for rel, (hit, total) in sorted(files.items()):
+        print(f"{100.0 * hit / total if total else 0:6.1f}%  {hit:5d}/{total:<5d}  {rel}")
+    print(f"{100.0 * hit_all / tot_all if tot_all else 0:6.1f}%  {hit_all:5d}/{tot_all:<5d}  total")
+    if a.json_out:
+        doc = {"what": "gcov line coverage of the native host code: ctest (test_core) plus the CPU tests that drive "
+                       "mi355x-device-plugin and mi355x-node-labeller (tools/native_coverage.py)",
+               "tests": a.tests, "pytest": tail, "ctest_ok": ct.returncode == 0,
+               "total": {"lines": tot_all, "executed": hit_all,
+                         "pct": round(100.0 * hit_all / tot_all, 1) if tot_all else None},
+               "by_dir": {d: {"lines": s[1], "executed": s[0], "pct": round(100.0 * s[0] / s[1], 1) if s[1] else None}
+                          for d, s in sorted(by_dir.items())},
+               "files": {rel: {"lines": t_, "executed": h, "pct": round(100.0 * h / t_, 1) if t_ else None}
+                         for rel, (h, t_) in sorted(files.items())}}
+        Path(a.json_out).parent.mkdir(parents=True, exist_ok=True)
+        Path(a.json_out).write_text(json.dumps(doc, indent=1) + "\n")
+    return 0 if t.returncode == 0 else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
