@@ -11,6 +11,8 @@
 #include "mi355x/pci_scan.h"
 #include "mi355x/smi_query.h"
 #include "mi355x/sysfs.h"
+#include "../src/kube/json.h"
+#include "../src/kube/yaml.h"
 
 namespace py = pybind11;
 using namespace mi355x;
@@ -259,6 +261,15 @@ PYBIND11_MODULE(_native, m) {
     return py::make_tuple(g.version, g.srcversion);
   }, py::arg("sysfs_root") = "/sys");
 
+  m.def(
+      "yaml_to_json",
+      [](const std::string& text) -> py::tuple {
+        std::string err;
+        auto v = yaml::parse(text, &err);
+        if (!v) return py::make_tuple(py::none(), err);
+        return py::make_tuple(json::serialize(*v), std::string());
+      },
+      py::arg("text"), "the config-file YAML reader (kubeconfig, -config): (JSON text, '') or (None, error)");
   m.def("family_id_to_string", &family_id_to_string);
   m.def("drm_available", &drm_available);
   m.def("drm_is_amd_card", &drm_is_amd_card);

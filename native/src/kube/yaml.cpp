@@ -14,21 +14,40 @@ struct Line {
   int no;
 };
 
-// strips a trailing " # comment" outside quotes
-std::string strip_comment(const std::string& s) {
+// "# comment" to the end of each line, outside quoted scalars (which may span lines)
+std::string strip_comments(const std::string& s) {
+  std::string out;
   char q = 0;
-  for (size_t i = 0; i < s.size(); ++i) {
-    const char c = s[i];
+  for (size_t k = 0; k < s.size(); ++k) {
+    const char ch = s[k];
+    const char prev = k ? s[k - 1] : '\n';
     if (q) {
-      if (c == q && !(q == '"' && i && s[i - 1] == '\\')) q = 0;
-    } else if (c == '"' || c == '\'') {
-      if (i == 0 || s[i - 1] == ' ' || s[i - 1] == ':' || s[i - 1] == '[' || s[i - 1] == '{' || s[i - 1] == ',')
-        q = c;
-    } else if (c == '#' && (i == 0 || s[i - 1] == ' ' || s[i - 1] == '\t')) {
-      return s.substr(0, i);
+      if (q == '"' && ch == '\\' && k + 1 < s.size()) {
+        out += ch;
+        out += s[++k];
+        continue;
+      }
+      if (ch == q) {
+        if (q == '\'' && k + 1 < s.size() && s[k + 1] == '\'') {
+          out += "''";
+          ++k;
+          continue;
+        }
+        q = 0;
+      }
+      out += ch;
+    } else if ((ch == '"' || ch == '\'') && (prev == ' ' || prev == '\n' || prev == ':' || prev == '[' ||
+                                             prev == '{' || prev == ',' || prev == '\t')) {
+      q = ch;
+      out += ch;
+    } else if (ch == '#' && (prev == ' ' || prev == '\t' || prev == '\n')) {
+      while (k < s.size() && s[k] != '\n') ++k;
+      if (k < s.size()) out += '\n';
+    } else {
+      out += ch;
     }
   }
-  return s;
+  return out;
 }
 
 std::string rtrim(std::string s) {
@@ -52,7 +71,7 @@ class Parser {
       std::string t = rtrim(r);
       size_t ind = 0;
       while (ind < t.size() && t[ind] == ' ') ++ind;
-      std::string body = rtrim(strip_comment(t.substr(ind)));
+      std::string body = rtrim(strip_comments(t.substr(ind)));
       if (body.empty() || body == "---" || body == "...") continue;
       lines_.push_back({static_cast<int>(ind), body, no});
     }
@@ -63,8 +82,11 @@ class Parser {
     const char c0 = lines_[0].text[0];
     if (c0 == '[' || c0 == '{') {  // a flow collection as the document, possibly over several lines
       std::string all;
-      for (const auto& l : lines_) all += (all.empty() ? "" : " ") + l.text;
-      auto v = scalar_or_flow(all, lines_[0].no);
+      for (const auto& r : raw_) {
+        const std::string t = rtrim(r);
+        if (t != "---" && t != "...") all += t + "\n";
+      }
+      auto v = scalar_or_flow(strip_comments(all), lines_[0].no);
       if (!err_->empty()) return std::nullopt;
       return v;
     }
@@ -89,7 +111,12 @@ class Parser {
     for (size_t i = 0; i < t.size(); ++i) {
       const char c = t[i];
       if (q) {
-        if (c == q) q = 0;
+        if (q == '"' && c == '\\') {
+          ++i;  // an escaped character, e.g. \"
+        } else if (c == q) {
+          if (q == '\'' && i + 1 < t.size() && t[i + 1] == '\'') ++i;  // '' inside a single-quoted key
+          else q = 0;
+        }
         continue;
       }
       if ((c == '"' || c == '\'') && i == 0) q = c;
@@ -136,6 +163,15 @@ class Parser {
         continue;
       }
       const int item_indent = indent + static_cast<int>(l.text.size() - rest.size());
+      if (is_seq_item(rest)) {
+        // "- - item": a sequence whose first item sits on this line
+        l.indent = item_indent;
+        l.text = rest;
+        auto v = sequence(i, item_indent);
+        if (!v) return std::nullopt;
+        arr.arr.push_back(std::move(*v));
+        continue;
+      }
       if (key_colon(rest) != std::string::npos && rest[0] != '{' && rest[0] != '[') {
         // "- key: value": a mapping whose first entry sits on this line
         l.indent = item_indent;
@@ -143,11 +179,16 @@ class Parser {
         auto v = mapping(i, item_indent);
         if (!v) return std::nullopt;
         arr.arr.push_back(std::move(*v));
-      } else {
-        auto v = scalar_or_flow(rest, l.no);
+      } else if (rest[0] == '|' || rest[0] == '>') {
+        ++*i;
+        auto v = block_scalar(rest, l.no, indent, i);
         if (!v) return std::nullopt;
         arr.arr.push_back(std::move(*v));
+      } else {
         ++*i;
+        auto v = scalar_or_flow(continued(rest, l.no, indent, i), l.no);
+        if (!v) return std::nullopt;
+        arr.arr.push_back(std::move(*v));
       }
     }
     return arr;
@@ -163,33 +204,19 @@ class Parser {
         return std::nullopt;
       }
       std::string key = l.text.substr(0, c);
-      if (key.size() >= 2 && (key[0] == '"' || key[0] == '\'') && key.back() == key[0])
-        key = key.substr(1, key.size() - 2);
+      while (!key.empty() && (key.back() == ' ' || key.back() == '\t')) key.pop_back();
+      if (!key.empty() && (key[0] == '"' || key[0] == '\'')) {  // a quoted key: escapes and '' resolved
+        auto k = scalar_or_flow(key, l.no);
+        if (!k || k->kind != json::Value::String) return fail(l.no, "bad quoted key"), std::nullopt;
+        key = k->s;
+      }
       std::string val = c + 1 < l.text.size() ? l.text.substr(c + 1) : "";
       while (!val.empty() && val[0] == ' ') val.erase(0, 1);
       ++*i;
-      if (val == "|" || val == "|-" || val == ">" || val == ">-") {  // block scalar
-        std::string out;
-        int bi = -1;
-        size_t r = static_cast<size_t>(l.no);  // raw_ index of the next line
-        while (r < raw_.size()) {
-          const std::string& rl = raw_[r];
-          size_t ind = 0;
-          while (ind < rl.size() && rl[ind] == ' ') ++ind;
-          if (rtrim(rl).empty()) {
-            out += "\n";
-            ++r;
-            continue;
-          }
-          if (static_cast<int>(ind) <= indent) break;
-          if (bi < 0) bi = static_cast<int>(ind);
-          out += rtrim(rl.substr(std::min<size_t>(static_cast<size_t>(bi), ind))) + (val[0] == '>' ? " " : "\n");
-          ++r;
-        }
-        while (*i < lines_.size() && lines_[*i].no <= static_cast<int>(r)) ++*i;
-        if (val.size() == 2)
-          while (!out.empty() && (out.back() == '\n' || out.back() == ' ')) out.pop_back();
-        obj.set(key, json::Value::string(out));
+      if (!val.empty() && (val[0] == '|' || val[0] == '>')) {  // block scalar
+        auto v = block_scalar(val, l.no, indent, i);
+        if (!v) return std::nullopt;
+        obj.set(key, std::move(*v));
         continue;
       }
       if (val.empty()) {
@@ -206,18 +233,120 @@ class Parser {
         }
         continue;
       }
-      auto v = scalar_or_flow(val, l.no);
+      auto v = scalar_or_flow(continued(val, l.no, indent, i), l.no);
       if (!v) return std::nullopt;
       obj.set(key, std::move(*v));
     }
     return obj;
   }
 
+  // A value that goes on over the following lines indented deeper than its
+  // parent (`indent`): a folded plain or quoted scalar, or a flow collection.
+  // Returns the value's text with the line breaks kept (flow() folds them) and
+  // comments removed; consumes those lines. A value alone on its line is returned as is.
+  std::string continued(const std::string& first, int no, int indent, size_t* i) {
+    // the next non-blank raw line decides (a comment-like continuation of a quoted
+    // scalar, e.g. `  #"`, is not in lines_)
+    for (size_t r = static_cast<size_t>(no); r < raw_.size(); ++r) {
+      const std::string rl = rtrim(raw_[r]);
+      size_t ind = 0;
+      while (ind < rl.size() && rl[ind] == ' ') ++ind;
+      if (ind == rl.size()) continue;
+      if (static_cast<int>(ind) <= indent) return first;
+      break;
+    }
+    std::string text = first;
+    size_t r = static_cast<size_t>(no);  // raw_ index of the next line
+    size_t last = r;
+    std::string pending;
+    while (r < raw_.size()) {
+      const std::string rl = rtrim(raw_[r]);
+      size_t ind = 0;
+      while (ind < rl.size() && rl[ind] == ' ') ++ind;
+      if (ind == rl.size()) {  // blank: a line break inside the value, unless the value ends here
+        pending += "\n";
+        ++r;
+        continue;
+      }
+      if (static_cast<int>(ind) <= indent) break;
+      text += pending + "\n" + rl;
+      pending.clear();
+      last = ++r;
+    }
+    while (*i < lines_.size() && lines_[*i].no <= static_cast<int>(last)) ++*i;
+    return strip_comments(text);
+  }
+
+  // `|` / `>` with an optional chomping (`-` strip, `+` keep, default clip) and
+  // indentation indicator, its content on the following lines (YAML 1.2 8.1)
+  std::optional<json::Value> block_scalar(const std::string& head, int no, int indent, size_t* i) {
+    const bool folded = head[0] == '>';
+    char chomp = 0;
+    int explicit_indent = 0;
+    for (size_t k = 1; k < head.size(); ++k) {
+      const char ch = head[k];
+      if ((ch == '-' || ch == '+') && !chomp) chomp = ch;
+      else if (ch >= '1' && ch <= '9' && !explicit_indent) explicit_indent = ch - '0';
+      else if (ch == ' ' || ch == '\t') break;  // a comment may follow (already stripped)
+      else return fail(no, "bad block scalar header"), std::nullopt;
+    }
+    std::vector<std::string> content;  // lines without the block's indentation; "" = blank
+    int bi = explicit_indent ? indent + explicit_indent : -1;
+    size_t r = static_cast<size_t>(no);
+    while (r < raw_.size()) {
+      const std::string rl = rtrim(raw_[r]);
+      size_t ind = 0;
+      while (ind < rl.size() && rl[ind] == ' ') ++ind;
+      if (ind == rl.size()) {
+        content.emplace_back();
+        ++r;
+        continue;
+      }
+      if (static_cast<int>(ind) <= indent) break;
+      if (bi < 0) bi = static_cast<int>(ind);
+      if (static_cast<int>(ind) < bi) return fail(r + 1, "block scalar line indented less than its first line"), std::nullopt;
+      content.push_back(rl.substr(static_cast<size_t>(bi)));
+      ++r;
+    }
+    size_t used = r;
+    int trail = 0;
+    while (!content.empty() && content.back().empty()) {
+      content.pop_back();
+      ++trail;
+    }
+    std::string body;
+    if (!folded) {
+      for (size_t k = 0; k < content.size(); ++k) body += (k ? "\n" : "") + content[k];
+    } else {
+      int blanks = 0;
+      bool first = true, prev_more = false;
+      for (const auto& ln : content) {
+        if (ln.empty()) {
+          ++blanks;
+          continue;
+        }
+        const bool more = ln[0] == ' ' || ln[0] == '\t';  // more-indented lines keep their breaks
+        if (first) body.append(static_cast<size_t>(blanks), '\n');
+        else if (!blanks && !more && !prev_more) body += ' ';
+        else if (!more && !prev_more) body.append(static_cast<size_t>(blanks), '\n');
+        else body.append(static_cast<size_t>(blanks) + 1, '\n');
+        body += ln;
+        first = false;
+        blanks = 0;
+        prev_more = more;
+      }
+    }
+    if (!content.empty() && chomp != '-') body += '\n';
+    if (chomp == '+') body.append(static_cast<size_t>(trail), '\n');
+    while (*i < lines_.size() && lines_[*i].no <= static_cast<int>(used)) ++*i;
+    return json::Value::string(body);
+  }
+
   std::optional<json::Value> scalar_or_flow(const std::string& s, int no) {
     size_t p = 0;
     auto v = flow(s, &p, no, false);
     if (!v) return std::nullopt;
-    while (p < s.size() && s[p] == ' ') ++p;
+    while (p < s.size() && (s[p] == ' ' || s[p] == '\t' || s[p] == '\n')) ++p;
     if (p != s.size()) {
       fail(no, "trailing characters after a value");
       return std::nullopt;
@@ -298,20 +427,89 @@ class Parser {
     }
   }
 
-  // a value starting at s[*p]; in_flow: plain scalars end at , ] }
+  static bool space(char ch) { return ch == ' ' || ch == '\t' || ch == '\n'; }
+
+  // Line folding inside a flow scalar (YAML 1.2 6.5) at s[*p] == '\n': the
+  // trailing white space before the break is dropped from *out (down to
+  // `keep`), a single break becomes a space, n empty lines n line feeds; *p
+  // ends on the last skipped character.
+  static void fold(const std::string& s, size_t* p, std::string* out, size_t keep) {
+    out->resize(keep);
+    size_t breaks = 1, q = *p + 1;
+    while (q < s.size() && (s[q] == ' ' || s[q] == '\t' || s[q] == '\n')) breaks += s[q++] == '\n';
+    if (breaks == 1) out->push_back(' ');
+    else out->append(breaks - 1, '\n');
+    *p = q - 1;
+  }
+
+  // a plain scalar's text from s[*p]: to the end (block context) or to , ] } / ": " (flow context), folded
+  static std::string plain_text(const std::string& s, size_t* p, bool in_flow) {
+    std::string out;
+    size_t keep = 0;
+    for (; *p < s.size(); ++*p) {
+      const char ch = s[*p];
+      if (in_flow && (ch == ',' || ch == ']' || ch == '}')) break;
+      if (ch == ':' && (in_flow || (*p + 1 < s.size() && s[*p + 1] == '\n')) &&
+          (*p + 1 == s.size() || space(s[*p + 1])))
+        break;
+      if (ch == '\n') {
+        fold(s, p, &out, keep);
+        keep = out.size();
+        continue;
+      }
+      out.push_back(ch);
+      if (ch != ' ' && ch != '\t') keep = out.size();
+    }
+    out.resize(keep);
+    return out;
+  }
+
+  // a value starting at s[*p]; in_flow: plain scalars end at , ] } and ": "; line breaks fold
   std::optional<json::Value> flow(const std::string& s, size_t* p, int no, bool in_flow) {
     Nest nest(&depth_);
     if (depth_ > kMaxDepth) return fail(no, "nested too deeply"), std::nullopt;
-    while (*p < s.size() && s[*p] == ' ') ++*p;
+    while (*p < s.size() && space(s[*p])) ++*p;
     if (*p >= s.size()) return json::Value{};
     const char c = s[*p];
+    if (c == '!') {  // a standard tag: !!str !!null !!bool !!int !!float !!map !!seq
+      size_t e = *p;
+      while (e < s.size() && !space(s[e])) ++e;
+      const std::string tag = s.substr(*p, e - *p);
+      *p = e;
+      while (*p < s.size() && (s[*p] == ' ' || s[*p] == '\t')) ++*p;
+      const bool quoted = *p < s.size() && (s[*p] == '"' || s[*p] == '\'');
+      if (tag == "!!str" && !quoted) return json::Value::string(plain_text(s, p, in_flow));
+      auto v = flow(s, p, no, in_flow);
+      if (!v) return std::nullopt;
+      if (tag == "!!null") return json::Value{};
+      if (tag == "!!bool" && v->kind == json::Value::String) {
+        json::Value b = plain(v->s);
+        if (b.kind != json::Value::Bool) return fail(no, "!!bool on a non-boolean"), std::nullopt;
+        return b;
+      }
+      if (tag == "!!str" || tag == "!!bool" || tag == "!!int" || tag == "!!float" || tag == "!!map" ||
+          tag == "!!seq")
+        return v;  // numbers stay text, as plain ones do
+      return fail(no, "unsupported tag " + tag), std::nullopt;
+    }
     if (c == '"') {
       std::string out;
+      size_t keep = 0;  // out.size() up to the last character a line break must not trim
       for (++*p; *p < s.size() && s[*p] != '"'; ++*p) {
         if (s[*p] == '\\' && *p + 1 < s.size()) {
-          if (!escape(s, p, &out)) return fail(no, "bad escape in a double-quoted scalar"), std::nullopt;
+          if (s[*p + 1] == '\n') {  // an escaped line break: joined without a space
+            ++*p;
+            while (*p + 1 < s.size() && (s[*p + 1] == ' ' || s[*p + 1] == '\t')) ++*p;
+          } else if (!escape(s, p, &out)) {
+            return fail(no, "bad escape in a double-quoted scalar"), std::nullopt;
+          }
+          keep = out.size();
+        } else if (s[*p] == '\n') {
+          fold(s, p, &out, keep);
+          keep = out.size();
         } else {
           out.push_back(s[*p]);
+          if (s[*p] != ' ' && s[*p] != '\t') keep = out.size();
         }
       }
       if (*p >= s.size()) return fail(no, "unterminated string"), std::nullopt;
@@ -320,16 +518,24 @@ class Parser {
     }
     if (c == '\'') {
       std::string out;
+      size_t keep = 0;
       for (++*p; *p < s.size(); ++*p) {
         if (s[*p] == '\'') {
           if (*p + 1 < s.size() && s[*p + 1] == '\'') {
             out.push_back('\'');
+            keep = out.size();
             ++*p;
             continue;
           }
           break;
         }
+        if (s[*p] == '\n') {
+          fold(s, p, &out, keep);
+          keep = out.size();
+          continue;
+        }
         out.push_back(s[*p]);
+        if (s[*p] != ' ' && s[*p] != '\t') keep = out.size();
       }
       if (*p >= s.size()) return fail(no, "unterminated string"), std::nullopt;
       ++*p;
@@ -340,7 +546,7 @@ class Parser {
       arr.kind = json::Value::Array;
       ++*p;
       while (true) {
-        while (*p < s.size() && s[*p] == ' ') ++*p;
+        while (*p < s.size() && space(s[*p])) ++*p;
         if (*p < s.size() && s[*p] == ']') {
           ++*p;
           return arr;
@@ -348,7 +554,7 @@ class Parser {
         auto v = flow(s, p, no, true);
         if (!v) return std::nullopt;
         arr.arr.push_back(std::move(*v));
-        while (*p < s.size() && s[*p] == ' ') ++*p;
+        while (*p < s.size() && space(s[*p])) ++*p;
         if (*p < s.size() && s[*p] == ',') {
           ++*p;
           continue;
@@ -364,20 +570,25 @@ class Parser {
       json::Value obj = json::Value::object();
       ++*p;
       while (true) {
-        while (*p < s.size() && s[*p] == ' ') ++*p;
+        while (*p < s.size() && space(s[*p])) ++*p;
         if (*p < s.size() && s[*p] == '}') {
           ++*p;
           return obj;
         }
+        const bool quoted_key = s[*p] == '"' || s[*p] == '\'';
         auto k = flow(s, p, no, true);
         if (!k) return std::nullopt;
-        while (*p < s.size() && s[*p] == ' ') ++*p;
+        while (*p < s.size() && space(s[*p])) ++*p;
         if (*p >= s.size() || s[*p] != ':') return fail(no, "expected : in a flow mapping"), std::nullopt;
         ++*p;
         auto v = flow(s, p, no, true);
         if (!v) return std::nullopt;
-        obj.set(k->kind == json::Value::String ? k->s : json::serialize(*k), std::move(*v));
-        while (*p < s.size() && s[*p] == ' ') ++*p;
+        // a plain key is text (as in block mappings), a quoted one its unescaped value
+        std::string key = k->kind == json::Value::String ? k->s
+                          : k->kind == json::Value::Bool ? (k->b ? "true" : "false")
+                          : k->kind == json::Value::Null && !quoted_key ? "null" : json::serialize(*k);
+        obj.set(key, std::move(*v));
+        while (*p < s.size() && space(s[*p])) ++*p;
         if (*p < s.size() && s[*p] == ',') {
           ++*p;
           continue;
@@ -389,16 +600,7 @@ class Parser {
         return fail(no, "expected , or } in a flow mapping"), std::nullopt;
       }
     }
-    // plain scalar: to the end (block context) or to , ] } / ": " (flow context)
-    size_t e = *p;
-    while (e < s.size()) {
-      if (in_flow && (s[e] == ',' || s[e] == ']' || s[e] == '}')) break;
-      if (in_flow && s[e] == ':' && (e + 1 == s.size() || s[e + 1] == ' ')) break;
-      ++e;
-    }
-    std::string t = rtrim(s.substr(*p, e - *p));
-    *p = e;
-    return plain(t);
+    return plain(plain_text(s, p, in_flow));
   }
 
   std::string* err_;

@@ -30,6 +30,20 @@ def _auto_build_allowed() -> bool:
     return os.environ.get("MI355X_DP_NO_AUTOBUILD", "") not in ("1", "true", "yes")
 
 
+def _load_from(path: str):
+    """The same extension from another build (MI355X_NATIVE_CORE_SO: e.g. the gcov
+    build tools/native_coverage.py measures the test suite with)."""
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location("rocm_k8s_device_plugin_amd._native", path)
+    if spec is None or spec.loader is None:
+        raise ImportError(f"cannot load {path}")
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[spec.name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def core():
     """The `_native` host extension."""
     global _core
@@ -38,6 +52,9 @@ def core():
     with _lock:
         if _core is None:
             try:
+                if os.environ.get("MI355X_NATIVE_CORE_SO"):
+                    _core = _load_from(os.environ["MI355X_NATIVE_CORE_SO"])
+                    return _core
                 if _auto_build_allowed():
                     from .. import _build
                     _build.ensure_built(hip=None)

@@ -1,0 +1,81 @@
+"""The native YAML reader (native/src/kube/yaml.cpp: kubeconfig and the device
+plugin's -config file) against PyYAML on the same documents.
+
+Hypothesis builds mappings of strings, booleans, nulls, lists and nested
+mappings; PyYAML writes each one in block, flow and mixed style, with every
+scalar quoting style and line widths that fold long scalars; the native reader
+must return what ``yaml.safe_load`` returns. Plain scalars that are not
+booleans or null stay strings in the native reader (configs read them as
+text), so the generated documents hold no numbers: PyYAML quotes any string
+that would resolve to one.
+"""
+import json
+
+import pytest
+import yaml
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from rocm_k8s_device_plugin_amd.ops.native import core
+
+# keys and values over characters that exercise quoting, escapes, comments and indicators
+_CHARS = st.characters(codec="utf-8", exclude_categories=("Cs", "Cc"), exclude_characters="\ufeff\x85\u2028\u2029")
+_TEXT = st.text(alphabet=st.one_of(st.sampled_from(list("ab -:#,[]{}'\"&*!|>%@`?\\\t/.0123456789")), _CHARS),
+                max_size=24)
+_KEY = st.text(alphabet=st.sampled_from(list("abcdefxyz_-./0123456789 :#'\"")), min_size=1, max_size=12)
+_SCALAR = st.one_of(_TEXT, st.booleans(), st.none())
+_VALUE = st.recursive(_SCALAR, lambda c: st.one_of(st.lists(c, max_size=4),
+                                                   st.dictionaries(_KEY, c, max_size=4)), max_leaves=16)
+_DOC = st.dictionaries(_KEY, _VALUE, min_size=1, max_size=6)
+
+
+def native(text):
+    out, err = core().yaml_to_json(text)
+    assert out is not None, f"native reader refused:\n{text}\n-> {err}"
+    return json.loads(out)
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(doc=_DOC, flow=st.sampled_from([False, True, None]), style=st.sampled_from([None, '"', "'"]),
+       width=st.integers(min_value=20, max_value=120), unicode=st.booleans())
+def test_native_reader_equals_pyyaml(doc, flow, style, width, unicode):
+    text = yaml.safe_dump(doc, default_flow_style=flow, default_style=style, width=width, allow_unicode=unicode,
+                          sort_keys=False)
+    assert native(text) == yaml.safe_load(text), text
+
+
+@pytest.mark.parametrize("text", [
+    # kubeconfig as kubectl writes it
+    "apiVersion: v1\nkind: Config\nclusters:\n- cluster:\n    certificate-authority-data: QUJD\n"
+    "    server: https://10.0.0.1:6443\n  name: c\ncontexts:\n- context:\n    cluster: c\n    user: u\n  name: x\n"
+    "current-context: x\nusers:\n- name: u\n  user:\n    token: abc # trailing comment\n",
+    # the device plugin's -config file
+    "gpu:\n  device_count: 4\n",
+    # block scalars with chomping indicators, comments, blank lines, nested sequences
+    "a: |+\n  keep\n\n\nb: >\n  folded\n  line\n\n  para\nc: |-\n  strip\n# comment\nd:\n- - x\n  - y\n- z\n",
+    # quoted scalars with escapes, and a multi-line plain scalar
+    "e: \"tab\\tnl\\n\\u00e9 \\\"q\\\"\"\nf: 'it''s'\ng: plain scalar\n  continued here\n",
+])
+def test_hand_written_documents(text):
+    assert native(text) == _stringify(yaml.safe_load(text))
+
+
+def _stringify(v):
+    """PyYAML's ints become the native reader's strings (its plain scalars are text)."""
+    if isinstance(v, dict):
+        return {k: _stringify(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_stringify(x) for x in v]
+    if isinstance(v, (int, float)) and not isinstance(v, bool):
+        return str(v)
+    return v
+
+
+@pytest.mark.parametrize("text", ["a: [b, c\n", "a: 'open\n", "a:\n  - b\n c: d\n", "- a\nb: c\n", "{\"a\": 1",
+                                  "a: \"x\\q\"\n", "a: !custom x\n", "a: |\n    x\n  y\n"])
+def test_malformed_documents_are_refused(text):
+    """Documents PyYAML refuses are refused here too, with an error."""
+    with pytest.raises(yaml.YAMLError):
+        yaml.safe_load(text)
+    out, err = core().yaml_to_json(text)
+    assert out is None and err, (text, out)

@@ -8,9 +8,10 @@ files that drive the two native binaries with ``MI355X_NATIVE_DAEMON_EXE`` /
 gcov for every source's executed lines. Prints a per-file / per-directory
 table and writes the JSON summary (``--json-out``).
 
-Only code the tests reach through those binaries and test_core counts: the
-Python extension the rest of the suite imports is the package build, not this
-one, and GPU-only paths (the HSA / HIP probes) are not run on the CPU.
+The suite's in-process extension is the instrumented one too
+(``MI355X_NATIVE_CORE_SO``), so the Python tests that drive the native engine,
+allocator and parsers through the bindings count. GPU-only paths (the HSA /
+HIP probes, amd-smi and libdrm queries) do not run on the CPU.
 
     python tools/native_coverage.py --json-out profiles/r4/native_coverage_cpu.json
 """
@@ -28,7 +29,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 # the test files whose native processes honour MI355X_NATIVE_{DAEMON,LABELLER}_EXE
-# (and the files that import their EXE)
+# (and the files that import their EXE); the default run is the whole CPU suite
 TESTS = ["tests/test_native_daemon.py", "tests/test_native_health.py", "tests/test_native_labeller.py",
          "tests/test_native_config_logging.py", "tests/test_native_stress.py", "tests/test_go_interop.py",
          "tests/test_native_cdi.py", "tests/test_native_reload.py", "tests/test_native_views.py",
@@ -42,7 +43,9 @@ def make_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--json-out", default="", help="write the summary here")
     ap.add_argument("--workers", type=int, default=4, help="pytest-xdist workers (0 = serial)")
-    ap.add_argument("--tests", nargs="*", default=TESTS, help="test files to run against the instrumented binaries")
+    ap.add_argument("--tests", nargs="*", default=["tests/"],
+                    help="what pytest runs against the instrumented builds (default: the whole CPU suite)")
+    ap.add_argument("--native-only", action="store_true", help="only the test files that drive the two binaries")
     ap.add_argument("--no-build", action="store_true", help="reuse the existing coverage build")
     return ap
 
@@ -84,9 +87,13 @@ def main(argv=None) -> int:
     if ct.returncode != 0:
         sys.stderr.write(ct.stdout[-3000:])
         return 1
+    so = next((bdir / "pkg").glob("_native*.so"), None)
     env = dict(os.environ, MI355X_NATIVE_DAEMON_EXE=str(bdir / "pkg" / "bin" / "mi355x-device-plugin"),
                MI355X_NATIVE_LABELLER_EXE=str(bdir / "pkg" / "bin" / "mi355x-node-labeller"))
-    cmd = [sys.executable, "-m", "pytest", *a.tests, "-q", "-m", "not gpu", "-p", "no:cacheprovider"]
+    if so is not None:
+        env["MI355X_NATIVE_CORE_SO"] = str(so)   # the suite's in-process native core, instrumented too
+    tests = TESTS if a.native_only else a.tests
+    cmd = [sys.executable, "-m", "pytest", *tests, "-q", "-m", "not gpu", "-p", "no:cacheprovider"]
     if a.workers > 0:
         cmd += ["-n", str(a.workers)]
     t = subprocess.run(cmd, cwd=str(REPO), env=env, capture_output=True, text=True)
@@ -113,9 +120,10 @@ def main(argv=None) -> int:
         print(f"{100.0 * hit / total if total else 0:6.1f}%  {hit:5d}/{total:<5d}  {rel}")
     print(f"{100.0 * hit_all / tot_all if tot_all else 0:6.1f}%  {hit_all:5d}/{tot_all:<5d}  total")
     if a.json_out:
-        doc = {"what": "gcov line coverage of the native host code: ctest (test_core) plus the CPU tests that drive "
-                       "mi355x-device-plugin and mi355x-node-labeller (tools/native_coverage.py)",
-               "tests": a.tests, "pytest": tail, "ctest_ok": ct.returncode == 0,
+        doc = {"what": "gcov line coverage of the native host code: ctest (test_core) plus the CPU tests, with the "
+                       "instrumented mi355x-device-plugin, mi355x-node-labeller and _native extension "
+                       "(tools/native_coverage.py)",
+               "tests": tests, "pytest": tail, "ctest_ok": ct.returncode == 0,
                "total": {"lines": tot_all, "executed": hit_all,
                          "pct": round(100.0 * hit_all / tot_all, 1) if tot_all else None},
                "by_dir": {d: {"lines": s[1], "executed": s[0], "pct": round(100.0 * s[0] / s[1], 1) if s[1] else None}
