@@ -270,6 +270,15 @@ PYBIND11_MODULE(_native, m) {
         return py::make_tuple(json::serialize(*v), std::string());
       },
       py::arg("text"), "the config-file YAML reader (kubeconfig, -config): (JSON text, '') or (None, error)");
+  m.def(
+      "json_roundtrip",
+      [](const std::string& text) -> py::tuple {
+        std::string err;
+        auto v = json::parse(text, &err);
+        if (!v) return py::make_tuple(py::none(), err);
+        return py::make_tuple(json::serialize(*v), std::string());
+      },
+      py::arg("text"), "the labeller's JSON reader + writer (Node objects, watch events): (JSON text, '') or (None, error)");
   m.def("family_id_to_string", &family_id_to_string);
   m.def("drm_available", &drm_available);
   m.def("drm_is_amd_card", &drm_is_amd_card);

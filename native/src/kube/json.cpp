@@ -125,16 +125,31 @@ struct Parser {
     }
     return fail("unterminated string");
   }
+  // RFC 8259: -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?, kept as its source text
   bool number(Value* v) {
     const size_t s = i;
+    auto digit = [&] { return i < t.size() && t[i] >= '0' && t[i] <= '9'; };
+    auto digits = [&] {
+      if (!digit()) return false;
+      while (digit()) ++i;
+      return true;
+    };
     if (i < t.size() && t[i] == '-') ++i;
-    bool digits = false;
-    while (i < t.size() && ((t[i] >= '0' && t[i] <= '9') || t[i] == '.' || t[i] == 'e' || t[i] == 'E' ||
-                            t[i] == '+' || t[i] == '-')) {
-      digits = true;
+    if (i < t.size() && t[i] == '0') {
       ++i;
+      if (digit()) return fail("bad number (leading zero)");
+    } else if (!digits()) {
+      return fail("bad number");
     }
-    if (!digits) return fail("bad number");
+    if (i < t.size() && t[i] == '.') {
+      ++i;
+      if (!digits()) return fail("bad number (no digits after the point)");
+    }
+    if (i < t.size() && (t[i] == 'e' || t[i] == 'E')) {
+      ++i;
+      if (i < t.size() && (t[i] == '+' || t[i] == '-')) ++i;
+      if (!digits()) return fail("bad number (no exponent digits)");
+    }
     v->kind = Value::Number;
     v->s = t.substr(s, i - s);
     return true;
