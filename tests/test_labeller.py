@@ -342,7 +342,7 @@ def _running_labeller(tmp_path, srv, **kw):
     return lab, t
 
 
-def test_watch_restores_a_stripped_label_within_a_second(tmp_path):
+def test_watch_restores_a_stripped_label_within_seconds(tmp_path):
     """Labels stripped by someone else come back from the watch event, not
     the 300 s resync (reference: controller-runtime watch, main.go:551-580)."""
     import time
@@ -358,8 +358,9 @@ def test_watch_restores_a_stripped_label_within_a_second(tmp_path):
         labels.pop("amd.com/gpu.vram")
         t0 = time.monotonic()
         srv.set_labels("node-w", labels)
-        assert _wait(lambda: srv.labels("node-w").get("amd.com/gpu.vram") == "288G", 1.0)
-        assert time.monotonic() - t0 < 1.0
+        # seconds, not the 300 s resync (bounded loosely: the suite may run on a loaded host)
+        assert _wait(lambda: srv.labels("node-w").get("amd.com/gpu.vram") == "288G", 3.0)
+        assert time.monotonic() - t0 < 3.0
         assert lab.stats.watch_kicks >= 1 and lab.stats.passes > passes
         # our own PATCH comes back as an event that needs nothing: no reconcile loop
         time.sleep(0.3)

@@ -99,6 +99,9 @@ def main(argv=None) -> int:
     t = subprocess.run(cmd, cwd=str(REPO), env=env, capture_output=True, text=True)
     tail = (t.stdout.strip().splitlines() or [""])[-1]
     print(f"pytest: {tail}")
+    for line in t.stdout.splitlines():
+        if line.startswith(("FAILED", "ERROR")):
+            print(line)
     files = {}
     for gcda in sorted(bdir.rglob("*.gcda")):
         got = gcov_file(gcda)
