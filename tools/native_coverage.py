@@ -47,6 +47,11 @@ def make_parser() -> argparse.ArgumentParser:
                     help="what pytest runs against the instrumented builds (default: the whole CPU suite)")
     ap.add_argument("--native-only", action="store_true", help="only the test files that drive the two binaries")
     ap.add_argument("--no-build", action="store_true", help="reuse the existing coverage build")
+    ap.add_argument("--merge", default="",
+                    help="a GCOV_PREFIX tree from a GPU-box run of the same build (GCOV_PREFIX_STRIP=3: "
+                         "<dir>/native-coverage/...), merged into this run's counts before the report")
+    ap.add_argument("--stage", default="",
+                    help="copy the instrumented _native, daemon and labeller here for a GPU-box run, then exit")
     return ap
 
 
@@ -81,9 +86,23 @@ def main(argv=None) -> int:
     bdir = _build.variant_dir(coverage=True)
     if not a.no_build:
         _build.build(hip=False, coverage=True)
+    if a.stage:
+        import shutil
+        dst = Path(a.stage)
+        dst.mkdir(parents=True, exist_ok=True)
+        for f in [*(bdir / "pkg").glob("_native*.so"), bdir / "pkg" / "bin" / "mi355x-device-plugin",
+                  bdir / "pkg" / "bin" / "mi355x-node-labeller"]:
+            shutil.copy2(f, dst / f.name)
+        print(f"staged in {dst}; on the box: MI355X_NATIVE_CORE_SO / MI355X_NATIVE_DAEMON_EXE / "
+              f"MI355X_NATIVE_LABELLER_EXE pointing there, GCOV_PREFIX=<dir> GCOV_PREFIX_STRIP=3")
+        return 0
     for g in bdir.rglob("*.gcda"):
         g.unlink()
-    ct = _build.run_ctest(coverage=True)
+    if a.no_build:  # the build as it is: a rebuild would restamp versions.cpp and orphan a box run's counts
+        ct = subprocess.run(["ctest", "--test-dir", str(bdir), "--output-on-failure"], stdout=subprocess.PIPE,
+                            stderr=subprocess.STDOUT, text=True)
+    else:
+        ct = _build.run_ctest(coverage=True)
     if ct.returncode != 0:
         sys.stderr.write(ct.stdout[-3000:])
         return 1
@@ -102,6 +121,19 @@ def main(argv=None) -> int:
     for line in t.stdout.splitlines():
         if line.startswith(("FAILED", "ERROR")):
             print(line)
+    if a.merge:
+        # counts from the GPU box (same build, relocated by GCOV_PREFIX) added to this run's
+        import shutil
+        import tempfile
+        box = Path(a.merge) / bdir.name
+        with tempfile.TemporaryDirectory() as out:
+            r = subprocess.run(["gcov-tool", "merge", "-o", out, str(box), str(bdir)], capture_output=True, text=True)
+            if r.returncode != 0:
+                sys.stderr.write(r.stderr[-2000:])
+                return 1
+            for g in Path(out).rglob("*.gcda"):
+                shutil.copy2(g, bdir / g.relative_to(out))
+        print(f"merged {sum(1 for _ in box.rglob('*.gcda'))} profiles from {box}")
     files = {}
     for gcda in sorted(bdir.rglob("*.gcda")):
         got = gcov_file(gcda)
@@ -127,6 +159,7 @@ def main(argv=None) -> int:
                        "instrumented mi355x-device-plugin, mi355x-node-labeller and _native extension "
                        "(tools/native_coverage.py)",
                "tests": tests, "pytest": tail, "ctest_ok": ct.returncode == 0,
+               "merged_gpu_run": a.merge or None,
                "total": {"lines": tot_all, "executed": hit_all,
                          "pct": round(100.0 * hit_all / tot_all, 1) if tot_all else None},
                "by_dir": {d: {"lines": s[1], "executed": s[0], "pct": round(100.0 * s[0] / s[1], 1) if s[1] else None}
