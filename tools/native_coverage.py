@@ -42,7 +42,8 @@ _LINES = re.compile(r"Lines executed:\s*([\d.]+)% of (\d+)")
 def make_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--json-out", default="", help="write the summary here")
-    ap.add_argument("--workers", type=int, default=4, help="pytest-xdist workers (0 = serial)")
+    ap.add_argument("--workers", type=int, default=0,
+                    help="pytest-xdist workers (default serial: the -O0 build is slow and the stress tests are throughput-bound)")
     ap.add_argument("--tests", nargs="*", default=["tests/"],
                     help="what pytest runs against the instrumented builds (default: the whole CPU suite)")
     ap.add_argument("--native-only", action="store_true", help="only the test files that drive the two binaries")
