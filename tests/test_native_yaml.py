@@ -26,7 +26,7 @@ _KEY = st.text(alphabet=st.sampled_from(list("abcdefxyz_-./0123456789 :#'\"")), 
 _SCALAR = st.one_of(_TEXT, st.booleans(), st.none())
 _VALUE = st.recursive(_SCALAR, lambda c: st.one_of(st.lists(c, max_size=4),
                                                    st.dictionaries(_KEY, c, max_size=4)), max_leaves=16)
-_DOC = st.dictionaries(_KEY, _VALUE, min_size=1, max_size=6)
+_DOC = st.one_of(st.dictionaries(_KEY, _VALUE, min_size=1, max_size=6), st.lists(_VALUE, min_size=1, max_size=5))
 
 
 def native(text):
