@@ -113,6 +113,24 @@ def test_examples_parse_and_request_gpus():
     assert pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == 1
 
 
+def test_cpx_example_requests_a_resource_the_plugin_advertises(tmp_path):
+    """example/pod/cpx-partitions.yaml: its resource and node selector are what
+    the plugin (mixed naming) and the labeller produce on an MI355X CPX / NPS1 node."""
+    from rocm_k8s_device_plugin_amd import constants as C
+    from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+    from rocm_k8s_device_plugin_amd.labeller import labels as L
+    from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
+    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+    pod = _docs("example/pod/cpx-partitions.yaml")[0]
+    (res, n), = pod["spec"]["containers"][0]["resources"]["limits"].items()
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="cpx")
+    names = ContainerImpl("mixed", str(fi.sysfs), HealthConfig(exporter_socket=None)).resource_names()
+    assert res == f"amd.com/{names[0]}" and names == ["cpx_nps1"] and n == 2
+    labels = L.generate_labels({k: k == "compute-memory-partition" for k in C.SUPPORTED_LABELS + L.EXTRA_LABELS}, "",
+                               str(fi.sysfs), str(fi.dev))
+    assert pod["spec"]["nodeSelector"].items() <= labels.items()
+
+
 def _workflow_commands():
     """(workflow, step name, argv) for every command line of every run: step."""
     import shlex
