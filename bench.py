@@ -134,6 +134,29 @@ def parse_args(argv=None):
     return make_parser().parse_args(argv)
 
 
+def host_info(node) -> dict:
+    """The tree's git describe, ROCm and amdgpu driver versions, the host's CPU count
+    (ROCr's start-up walks every CPU's cache descriptors) and the kernel release."""
+    import platform
+    from rocm_k8s_device_plugin_amd import _build
+    from rocm_k8s_device_plugin_amd.utils import versions
+    v = versions.versions(node.sysfs)
+    describe = _build.git_describe()
+    if not describe:  # a tree without .git (a GPU box's copy): the version the daemon was built with
+        import re
+        import subprocess
+        from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+        try:
+            out = subprocess.run([os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin"), "-h"],
+                                 capture_output=True, text=True, timeout=10).stdout
+            m = re.search(r" version (\S+)", out)
+            describe = m.group(1) if m else ""
+        except (OSError, subprocess.TimeoutExpired):
+            describe = ""
+    return {"git_describe": describe or None, "rocm": v["rocm"], "amdgpu": v["amdgpu"],
+            "host_cpus": os.cpu_count(), "kernel": platform.release()}
+
+
 def result_line(args, d, n, m_adv, held, plugin_kind, elapsed, latency_ms, extra: dict) -> str:
     """The one JSON line the driver reads (value = p50 of the timed admissions)."""
     from rocm_k8s_device_plugin_amd.benchmark.stats import pct
@@ -230,7 +253,9 @@ def main():
             "bench_process_gpu": {"ranks": rank_gpu_state,
                                   "clean": not any(s["torch_cuda_initialized"] or s["kfd_fds"]
                                                    for s in rank_gpu_state)},
-            "gpus": node.gpu_info()})
+            "gpus": node.gpu_info(),
+            # what produced the number: the build, the host's ROCm / amdgpu, the daemon's own banner
+            "host": host_info(node)})
         held = list(plug.held)
 
         def line(extra):

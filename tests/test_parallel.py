@@ -270,6 +270,7 @@ def test_bench_single_process_8_gpus_on_the_fixture():
     assert d["n_gpus"] == 8 and e["launcher"] == "single-process" and e["rccl"] is None
     assert e["bench_process_gpu"]["clean"] and len(e["bench_process_gpu"]["ranks"]) == 1
     assert e["fabric"]["pairs"]["xgmi"] == 28 and e["timed_allocation"]["advertised"] == 8
+    assert e["host"]["git_describe"] and e["host"]["host_cpus"] >= 1 and e["host"]["kernel"]
 
 
 def test_bench_health_pulse_runs_on_the_native_daemon():
