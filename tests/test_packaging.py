@@ -131,6 +131,16 @@ def test_cpx_example_requests_a_resource_the_plugin_advertises(tmp_path):
     assert pod["spec"]["nodeSelector"].items() <= labels.items()
 
 
+@pytest.mark.parametrize("tool", sorted(p.name for p in (REPO / "tools").glob("*.py")))
+def test_every_tool_parses_its_arguments(tool):
+    """Each maintained measurement tool starts (its --help runs without a GPU)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, str(REPO / "tools" / tool), "--help"], capture_output=True, text=True,
+                       timeout=120, cwd=REPO)
+    assert r.returncode == 0 and "usage" in r.stdout.lower(), r.stderr[-1500:]
+
+
 def _workflow_commands():
     """(workflow, step name, argv) for every command line of every run: step."""
     import shlex
