@@ -46,6 +46,7 @@ class Registry {
   mutable std::mutex mu_;
   std::map<Key, double> counters_, gauges_;
   std::map<Key, Hist> hist_;
+  void note_help(const std::string& name, const std::string& help);  // caller holds mu_
   std::map<std::string, std::string> help_;
 };
 

@@ -232,9 +232,10 @@ void Daemon::on_rpc_events(size_t i) {
     }
     m.observe_ms("mi355x_dp_rpc_seconds", ev.dur_ns / 1e6, {{"resource", r.name}, {"rpc", ev.rpc}},
                  "device plugin RPC latency");
-    if (ev.rpc == "ListAndWatch") m.inc("mi355x_dp_listandwatch_streams_total", res_l);
+    if (ev.rpc == "ListAndWatch")
+      m.inc("mi355x_dp_listandwatch_streams_total", res_l, 1.0, "ListAndWatch streams kubelet opened");
     if (ev.status != 0) {
-      m.inc("mi355x_dp_rpc_errors_total", {{"resource", r.name}, {"rpc", ev.rpc}});
+      m.inc("mi355x_dp_rpc_errors_total", {{"resource", r.name}, {"rpc", ev.rpc}}, 1.0, "device plugin RPCs answered with an error");
       MI_LOG(kError, "%s: %s: %s", r.name.c_str(), ev.rpc.c_str(), ev.message.c_str());
     } else if (ev.rpc == "Allocate") {
       std::string ids;
@@ -303,11 +304,12 @@ void Daemon::on_sweep(const SweepResult& s) {
                                {"streams", std::to_string(r.server->stats().streams_open)}});
     }
   }
-  if (any_changed) metrics::global().inc("mi355x_dp_health_changes_total");
+  if (any_changed) metrics::global().inc("mi355x_dp_health_changes_total", {}, 1.0, "sweeps that changed some device's health");
   // xGMI link state changed: every allocator re-weighted on the degraded pairs
   if (health_->fabric_changed(s)) {
     reg_.reweight(topo_, f_.allocator_search, s.degraded);
-    metrics::global().inc("mi355x_dp_fabric_reweights_total");
+    metrics::global().inc("mi355x_dp_fabric_reweights_total", {}, 1.0,
+                          "preferred-allocation re-weightings after an xGMI link state change");
     MI_LOG(kWarning, "xGMI link state changed: preferred allocation re-weighted (%zu degraded GPU pairs)",
            s.degraded.size());
   }
@@ -323,7 +325,7 @@ void Daemon::on_completions() {
     Resource& r = reg_.at(c.resource);
     switch (r.reg.complete(c.server_gen, c.kubelet_gen, kubelet_gen_, c.ok && r.server != nullptr, Clock::now())) {
       case Registration::Outcome::kRegistered:
-        metrics::global().inc("mi355x_dp_registrations_total", {{"resource", r.name}});
+        metrics::global().inc("mi355x_dp_registrations_total", {{"resource", r.name}}, 1.0, "Register calls kubelet accepted");
         MI_LOG(kInfo, "%s: Registration for endpoint %s", r.name.c_str(), basename(r.socket).c_str());
         break;
       case Registration::Outcome::kFailed:
@@ -344,7 +346,8 @@ std::string Daemon::watchdog() {
     const std::string why = r.reg.observe(r.server->stats(), now);
     if (!why.empty()) return r.name + ": " + why;
     if (r.reg.reregistrations() != before) {
-      metrics::global().inc("mi355x_dp_reregistrations_total", {{"resource", r.name}});
+      metrics::global().inc("mi355x_dp_reregistrations_total", {{"resource", r.name}}, 1.0,
+                            "registrations again after kubelet closed every ListAndWatch stream");
       MI_LOG(kWarning, "%s: kubelet closed every ListAndWatch stream for %gs; registering again", r.name.c_str(),
              f_.reregister_s);
     }
@@ -371,7 +374,7 @@ void Daemon::reload_topology(const std::string& sig) {
       for (const auto& d : r.devices) after[d.id] = d.partition_type();
     }
   if (before == after) return;
-  metrics::global().inc("mi355x_dp_topology_reloads_total");
+  metrics::global().inc("mi355x_dp_topology_reloads_total", {}, 1.0, "GPU topology changes (partition switches) applied");
   MI_LOG(kWarning, "GPU topology changed: %zu -> %zu devices; resources [%s] -> [%s]", before.size(), after.size(),
          old_names.c_str(), new_names.c_str());
   const auto now = Clock::now();

@@ -79,16 +79,22 @@ Registry::Key Registry::key(const std::string& name, Labels labels) {
   return {name, std::move(labels)};
 }
 
+// the first non-empty HELP text a family gets is kept (a call site without one adds none)
+void Registry::note_help(const std::string& name, const std::string& help) {
+  auto [it, fresh] = help_.emplace(name, help);
+  if (!fresh && it->second.empty() && !help.empty()) it->second = help;
+}
+
 void Registry::inc(const std::string& name, const Labels& labels, double v, const std::string& help) {
   std::lock_guard<std::mutex> lk(mu_);
   counters_[key(name, labels)] += v;
-  help_.emplace(name, help);
+  note_help(name, help);
 }
 
 void Registry::set(const std::string& name, double v, const Labels& labels, const std::string& help) {
   std::lock_guard<std::mutex> lk(mu_);
   gauges_[key(name, labels)] = v;
-  help_.emplace(name, help);
+  note_help(name, help);
 }
 
 void Registry::observe_ms(const std::string& name, double ms, const Labels& labels, const std::string& help) {
@@ -100,7 +106,7 @@ void Registry::observe_ms(const std::string& name, double ms, const Labels& labe
   h.counts[i]++;
   h.sum_ms += ms;
   h.n++;
-  help_.emplace(name, help);
+  note_help(name, help);
 }
 
 double Registry::value(const std::string& name, const Labels& labels) const {

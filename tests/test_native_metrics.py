@@ -67,6 +67,8 @@ def _get(port, path):
 
 
 def _series(text):
+    """{series (with labels): value}; the page must also parse as Prometheus reads it."""
+    _check_exposition(text)
     out = {}
     for line in text.splitlines():
         if line and not line.startswith("#"):
@@ -123,6 +125,38 @@ def test_daemon_serves_metrics(tmp_path):
     assert s["mi355x_dp_devices_identity_unknown"] == 0.0
     assert "# TYPE mi355x_dp_rpc_seconds histogram" in text
     assert re.search(r'^mi355x_dp_rpc_seconds_bucket\{resource="gpu",rpc="Allocate",le="5e-05"\} \d+$', text, re.M)
+
+
+def _check_exposition(text):
+    """The page as Prometheus reads it (prometheus_client's text parser): every
+    sample belongs to a family with HELP and TYPE, counters are *_total,
+    histogram buckets are cumulative up to +Inf == _count, values are finite."""
+    import math
+    from prometheus_client.parser import text_string_to_metric_families
+    fams = list(text_string_to_metric_families(text))
+    assert fams and len({f.name for f in fams}) == len(fams)
+    n_samples = sum(len(f.samples) for f in fams)
+    assert n_samples == sum(1 for ln in text.splitlines() if ln and not ln.startswith("#"))
+    for f in fams:
+        assert f.documentation, f.name
+        assert f.type in ("counter", "gauge", "histogram"), (f.name, f.type)
+        for smp in f.samples:
+            assert math.isfinite(smp.value) or smp.labels.get("le") == "+Inf", smp
+        if f.type == "counter":
+            assert all(s.name.endswith(("_total", "_created")) for s in f.samples), f.name
+        if f.type == "histogram":
+            series = {}
+            for s in f.samples:
+                key = tuple(sorted((k, v) for k, v in s.labels.items() if k != "le"))
+                series.setdefault(key, {"b": [], "count": None})
+                if s.name.endswith("_bucket"):
+                    series[key]["b"].append((float(s.labels["le"]), s.value))
+                elif s.name.endswith("_count"):
+                    series[key]["count"] = s.value
+            for key, d in series.items():
+                b = sorted(d["b"])
+                assert b and b[-1][0] == math.inf and b[-1][1] == d["count"], (f.name, key)
+                assert all(x[1] <= y[1] for x, y in zip(b, b[1:])), (f.name, key, b)
 
 
 def test_daemon_metrics_port_in_use_is_an_error(tmp_path):
