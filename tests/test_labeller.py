@@ -599,10 +599,10 @@ def test_topology_watch_relabels_within_a_second(tmp_path):
         while srv.labels("worker-4").get("amd.com/gpu.compute-memory-partition") != "spx_nps1":
             assert time.monotonic() < deadline
             time.sleep(0.02)
-        new = tmp_path / "n.new"
-        make_mi355x_node(new, compute_partition="dpx", generation=2)
-        shutil.rmtree(root / "sys")
-        os.rename(new / "sys", root / "sys")
+        # swapped in two renames, as the driver's view changes at once (an rmtree of the old tree
+        # first would leave half a tree to poll for as long as the deletion takes on a loaded host)
+        from test_reload import repartition
+        repartition(root, compute_partition="dpx", generation=2)
         t0 = time.monotonic()
         while srv.labels("worker-4").get("amd.com/gpu.compute-memory-partition") != "dpx_nps1":
             # ~0.2 s when idle (two 0.1 s polls + one relabel); 3 s leaves room for a loaded CI host,
