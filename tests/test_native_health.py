@@ -415,17 +415,19 @@ def test_daemon_hung_exporter_blocks_neither_registration_nor_shutdown(tmp_path)
         t0 = time.monotonic()
         while len(regs) < 2 and time.monotonic() - t0 < 5:
             time.sleep(0.01)
-        assert len(regs) >= 2 and regs[-1] - t0 < 1.0, "re-registration waited for the exporter"
+        # the exporter call hangs for its 10 s deadline: anything well under that did not wait for it
+        # (bounds loose enough for a loaded CI host)
+        assert len(regs) >= 2 and regs[-1] - t0 < 3.0, "re-registration waited for the exporter"
         c = gp.GoClientConn(os.path.join(kdir, "amd.com_gpu"))
         try:
             t1 = time.monotonic()
             assert c.unary("/v1beta1.DevicePlugin/GetDevicePluginOptions", b"", 5.0)[0] == 0
-            assert time.monotonic() - t1 < 0.5
+            assert time.monotonic() - t1 < 2.0
         finally:
             c.close()
         t2 = time.monotonic()
         rc, err = _stop(p)
-        assert rc == 0 and time.monotonic() - t2 < 2.0, err[-2000:]
+        assert rc == 0 and time.monotonic() - t2 < 5.0, err[-2000:]
     finally:
         if p.poll() is None:
             p.kill()
