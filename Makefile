@@ -14,7 +14,7 @@ GIT_DESCRIBE ?= $(shell git describe --always --long --dirty 2>/dev/null || echo
 DOCKER ?= docker
 BUILD_ARGS = --build-arg GIT_DESCRIBE=$(GIT_DESCRIBE)
 
-.PHONY: images push native test test-gpu
+.PHONY: images push native test test-gpu sanitizers coverage fuzz bench
 
 images:
 	$(DOCKER) build $(BUILD_ARGS) -f Dockerfile -t $(IMAGE_REPO):$(VERSION) .
@@ -36,3 +36,20 @@ test:
 
 test-gpu:
 	python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+
+# ctest under ASan+UBSan and under TSan (host-only builds in build/native-<sanitizer>)
+sanitizers:
+	python3 -m rocm_k8s_device_plugin_amd._build --no-hip --sanitize address,undefined --ctest
+	python3 -m rocm_k8s_device_plugin_amd._build --no-hip --sanitize thread --ctest
+
+# gcov line coverage of the native host code by the CPU suite (docs/development.md)
+coverage:
+	python3 tools/native_coverage.py --json-out build/native_coverage.json
+
+# libFuzzer over every native parser (clang), 60 s per target
+fuzz:
+	python3 tools/fuzz_native.py --seconds 60 --json build/fuzz_native.json
+
+# the headline benchmark on this node (needs an MI355X)
+bench:
+	python3 bench.py --gpus 1 --steps 20 --warmup 3
