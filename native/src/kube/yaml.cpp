@@ -442,16 +442,20 @@ class Parser {
     *p = q - 1;
   }
 
-  // a plain scalar's text from s[*p]: to the end (block context) or to , ] } / ": " (flow context), folded
-  static std::string plain_text(const std::string& s, size_t* p, bool in_flow) {
+  // a plain scalar's text from s[*p]: to the end (block context) or to , ] } / ": " (flow context), folded.
+  // In block context a ": " (or a ':' ending a line) inside it is a mapping where none may start
+  // (YAML 1.2 7.3.3): *colon is set and the text so far returned.
+  static std::string plain_text(const std::string& s, size_t* p, bool in_flow, bool* colon = nullptr) {
     std::string out;
     size_t keep = 0;
     for (; *p < s.size(); ++*p) {
       const char ch = s[*p];
       if (in_flow && (ch == ',' || ch == ']' || ch == '}')) break;
-      if (ch == ':' && (in_flow || (*p + 1 < s.size() && s[*p + 1] == '\n')) &&
-          (*p + 1 == s.size() || space(s[*p + 1])))
+      if (ch == ':' && (*p + 1 == s.size() || space(s[*p + 1]))) {
+        if (in_flow) break;
+        if (colon) *colon = true;
         break;
+      }
       if (ch == '\n') {
         fold(s, p, &out, keep);
         keep = out.size();
@@ -478,7 +482,12 @@ class Parser {
       *p = e;
       while (*p < s.size() && (s[*p] == ' ' || s[*p] == '\t')) ++*p;
       const bool quoted = *p < s.size() && (s[*p] == '"' || s[*p] == '\'');
-      if (tag == "!!str" && !quoted) return json::Value::string(plain_text(s, p, in_flow));
+      if (tag == "!!str" && !quoted) {
+        bool colon = false;
+        std::string text = plain_text(s, p, in_flow, &colon);
+        if (colon) return fail(no, "mapping values are not allowed here"), std::nullopt;
+        return json::Value::string(text);
+      }
       auto v = flow(s, p, no, in_flow);
       if (!v) return std::nullopt;
       if (tag == "!!null") return json::Value{};
@@ -600,7 +609,10 @@ class Parser {
         return fail(no, "expected , or } in a flow mapping"), std::nullopt;
       }
     }
-    return plain(plain_text(s, p, in_flow));
+    bool colon = false;
+    std::string text = plain_text(s, p, in_flow, &colon);
+    if (colon) return fail(no, "mapping values are not allowed here"), std::nullopt;
+    return plain(text);
   }
 
   std::string* err_;

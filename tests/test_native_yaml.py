@@ -72,7 +72,9 @@ def _stringify(v):
 
 
 @pytest.mark.parametrize("text", ["a: [b, c\n", "a: 'open\n", "a:\n  - b\n c: d\n", "- a\nb: c\n", "{\"a\": 1",
-                                  "a: \"x\\q\"\n", "a: !custom x\n", "a: |\n    x\n  y\n"])
+                                  "a: \"x\\q\"\n", "a: !custom x\n", "a: |\n    x\n  y\n",
+                                  # a mapping indicator inside a plain scalar (an indentation mistake)
+                                  "a: b\n  c: d\n", "a: b c: d\n", "a: v:\n", "- b\n  c: d\n"])
 def test_malformed_documents_are_refused(text):
     """Documents PyYAML refuses are refused here too, with an error."""
     with pytest.raises(yaml.YAMLError):
