@@ -56,6 +56,12 @@ int mi355x_probe_identify(int ordinal, mi355x_probe_result* out);
 // 1 (default): the probe creates its own non-blocking stream; 0: it uses the
 // null stream (measurement of what the stream's queue costs a HIP program)
 void mi355x_probe_set_stream_mode(int own);
+// 1: a probe's stream, events and buffers are kept until mi355x_probe_release()
+// instead of freed before it returns -- the container entrypoint reports
+// "ready" at the verified tile and tears down after its JSON line is out, as
+// the HSA path does (mi355x_hsa_probe_defer_release)
+void mi355x_probe_defer_release(int on);
+void mi355x_probe_release(void);
 
 // ---- HSA-direct path ------------------------------------------------------
 // hsa_init + GPU agent enumeration; returns the number of GPU agents or

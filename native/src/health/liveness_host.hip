@@ -8,6 +8,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "liveness_kernel.h"
 #include "mi355x/liveness_probe.h"
@@ -53,7 +55,43 @@ void fill_identity(int ordinal, mi355x_probe_result* out) {
 
 int g_own_stream = 1;
 
+// What one probe allocated, freed after the verdict (now, or after the JSON
+// line with mi355x_probe_defer_release)
+struct HipResources {
+  float* h_out = nullptr;
+  uint32_t* h_meta = nullptr;
+  float* d_scratch = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipStream_t stream = nullptr;
+
+  void release() const {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (h_out) (void)hipHostFree(h_out);
+    if (h_meta) (void)hipHostFree(h_meta);
+    if (d_scratch) (void)hipFree(d_scratch);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+std::mutex g_deferred_mu;  // probes of several devices run on parallel threads
+bool g_defer_release = false;
+std::vector<HipResources> g_deferred;
+
 }  // namespace
+
+extern "C" void mi355x_probe_defer_release(int on) {
+  std::lock_guard<std::mutex> lk(g_deferred_mu);
+  g_defer_release = on != 0;
+}
+
+extern "C" void mi355x_probe_release(void) {
+  std::vector<HipResources> todo;
+  {
+    std::lock_guard<std::mutex> lk(g_deferred_mu);
+    todo.swap(g_deferred);
+  }
+  for (const auto& r : todo) r.release();
+}
 
 extern "C" void mi355x_probe_set_stream_mode(int own) { g_own_stream = own ? 1 : 0; }
 
@@ -132,12 +170,16 @@ extern "C" int mi355x_probe_device(int ordinal, uint32_t nonce, int iters, mi355
 
 done:
   out->setup_us = std::chrono::duration<double, std::micro>(t_setup - t0).count();
-  if (ev0) (void)hipEventDestroy(ev0);
-  if (ev1) (void)hipEventDestroy(ev1);
-  if (h_out) (void)hipHostFree(h_out);
-  if (h_meta) (void)hipHostFree(h_meta);
-  if (d_scratch) (void)hipFree(d_scratch);
-  if (stream) (void)hipStreamDestroy(stream);
   out->total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  {
+    const HipResources r{h_out, h_meta, d_scratch, ev0, ev1, stream};
+    std::unique_lock<std::mutex> lk(g_deferred_mu);
+    if (g_defer_release) {
+      g_deferred.push_back(r);
+    } else {
+      lk.unlock();
+      r.release();
+    }
+  }
   return out->ok ? 0 : 1;
 }

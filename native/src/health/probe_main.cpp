@@ -134,8 +134,8 @@ void set_stream_mode(bool own) { mi355x_probe_set_stream_mode(own ? 1 : 0); }
 void set_corrupt(int, int) {}
 void keep_resources(bool) {}  // the HIP build reuses its runtime's queues anyway
 void init_phases(double out[5]) { out[0] = out[1] = out[2] = out[3] = out[4] = 0; }
-void defer_teardown() {}
-void teardown() {}
+void defer_teardown() { mi355x_probe_defer_release(1); }
+void teardown() { mi355x_probe_release(); }
 void runtime_shutdown() {}
 int device_count() { return mi355x_probe_device_count(); }
 int probe(int o, uint32_t nonce, int iters, double, mi355x_probe_result* r) {
