@@ -157,6 +157,13 @@ def host_info(node) -> dict:
             "host_cpus": os.cpu_count(), "kernel": platform.release()}
 
 
+def _safe_host_info(node) -> dict:
+    try:
+        return host_info(node)
+    except Exception as e:  # noqa: BLE001 - context only: never at the headline's expense
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
+
+
 def result_line(args, d, n, m_adv, held, plugin_kind, elapsed, latency_ms, extra: dict) -> str:
     """The one JSON line the driver reads (value = p50 of the timed admissions)."""
     from rocm_k8s_device_plugin_amd.benchmark.stats import pct
@@ -255,7 +262,7 @@ def main():
                                                    for s in rank_gpu_state)},
             "gpus": node.gpu_info(),
             # what produced the number: the build, the host's ROCm / amdgpu, the daemon's own banner
-            "host": host_info(node)})
+            "host": _safe_host_info(node)})
         held = list(plug.held)
 
         def line(extra):
