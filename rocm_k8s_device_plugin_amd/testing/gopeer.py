@@ -819,6 +819,17 @@ class GoServerConfig:
     never_answer: bool = False                      # read the call, never respond (hung exporter)
     settings_after_headers: Optional[List[Tuple[int, int]]] = None   # a SETTINGS change mid-call
     refuse_calls: int = 0                           # the first N calls get RST_STREAM(REFUSED_STREAM)
+    # What other HTTP/2 servers (C++ gRPC, a proxy in front of an exporter) may
+    # send and grpc-go never does. RFC 7540 allows all of it; the client must cope.
+    pad: int = 0                                    # > 0: every HEADERS / DATA frame PADDED with this many bytes
+    priority_in_headers: bool = False               # HEADERS frames carry the PRIORITY flag (5 bytes)
+    noise_frames: bool = False                      # a PRIORITY and an unknown-type frame ahead of the response
+    rst_code: Optional[int] = None                  # answer every call with RST_STREAM(rst_code)
+    goaway_first: Optional[int] = None              # GOAWAY(last stream 0, this code) instead of an answer
+    # protocol violations the client must turn into a clean error
+    oversized_data: bool = False                    # a 20000-byte DATA frame (above our 16384 maximum)
+    interrupted_headers: bool = False               # HEADERS without END_HEADERS, then DATA
+    orphan_continuation: bool = False               # CONTINUATION with no HEADERS before it
 
 
 class GoServer:
@@ -915,21 +926,37 @@ class _ServerConn:
     def send(self, data: bytes) -> None:
         self.sock.sendall(data)
 
+    def _padded(self, flags: int, payload: bytes, prio: bool = False) -> Tuple[int, bytes]:
+        """(flags, payload) with the configured padding / priority fields added."""
+        if prio:
+            flags |= PRIORITY_FLAG
+            payload = struct.pack(">IB", 0, 15) + payload      # no dependency, weight 16
+        if self.cfg.pad:
+            flags |= PADDED
+            payload = bytes([self.cfg.pad]) + payload + b"\0" * self.cfg.pad
+        return flags, payload
+
     def _headers(self, sid: int, fields, end_stream: bool) -> None:
         block = self.enc.encode(fields)
-        chunk = self.cfg.continuation_chunk or self.peer_max_frame
+        # padding and priority fields count against the frame size
+        room = self.peer_max_frame - (1 + self.cfg.pad if self.cfg.pad else 0) - (5 if self.cfg.priority_in_headers else 0)
+        chunk = self.cfg.continuation_chunk or room
         parts = [block[i:i + chunk] for i in range(0, len(block), chunk)] or [b""]
         out = []
         for i, part in enumerate(parts):
             last = i == len(parts) - 1
             flags = (END_HEADERS if last else 0) | (END_STREAM if i == 0 and end_stream else 0)
+            if i == 0:
+                flags, part = self._padded(flags, part, self.cfg.priority_in_headers)
             out.append(frame(HEADERS if i == 0 else CONTINUATION, flags, sid, part))
         self.send(b"".join(out))
 
     def _data(self, sid: int, payload: bytes) -> None:
         """DATA within the client's windows (waits for its WINDOW_UPDATEs)."""
         while payload:
-            q = min(self.conn_send_window, self.stream_send.get(sid, self.peer_initial_window), self.peer_max_frame)
+            extra = 1 + self.cfg.pad if self.cfg.pad else 0     # padding is flow-controlled too
+            q = min(self.conn_send_window, self.stream_send.get(sid, self.peer_initial_window),
+                    self.peer_max_frame) - extra
             if q <= 0:
                 f = self.rd.read(5.0)
                 if f is None:
@@ -937,9 +964,10 @@ class _ServerConn:
                 self._on_frame(*f)
                 continue
             chunk, payload = payload[:q], payload[q:]
-            self.conn_send_window -= len(chunk)
-            self.stream_send[sid] = self.stream_send.get(sid, self.peer_initial_window) - len(chunk)
-            self.send(frame(DATA, 0, sid, chunk))
+            self.conn_send_window -= len(chunk) + extra
+            self.stream_send[sid] = self.stream_send.get(sid, self.peer_initial_window) - len(chunk) - extra
+            fl, pl = self._padded(0, chunk)
+            self.send(frame(DATA, fl, sid, pl))
 
     def run(self) -> None:
         settings = [(S_MAX_FRAME_SIZE, 16384)]
@@ -1060,6 +1088,26 @@ class _ServerConn:
             self.send(frame(PING, 0, 0, BDP_PING))
         if cfg.http_status != 200:
             self._headers(sid, [(":status", str(cfg.http_status)), ("content-type", "text/plain")], True)
+            return
+        if cfg.rst_code is not None:
+            self.send(frame(RST_STREAM, 0, sid, struct.pack(">I", cfg.rst_code)))
+            return
+        if cfg.goaway_first is not None:
+            self.send(frame(GOAWAY, 0, 0, struct.pack(">II", 0, cfg.goaway_first) + b"shutting down"))
+            return
+        if cfg.noise_frames:
+            self.send(frame(PRIORITY, 0, sid, struct.pack(">IB", 0, 15)) + frame(0xFA, 0x3, sid, b"ext") +
+                      frame(0xFB, 0, 0, b""))
+        if cfg.oversized_data:
+            self._headers(sid, [(":status", "200"), ("content-type", "application/grpc")], False)
+            self.send(frame(DATA, 0, sid, b"\0" * 20000))
+            return
+        if cfg.interrupted_headers:
+            block = self.enc.encode([(":status", "200"), ("content-type", "application/grpc")])
+            self.send(frame(HEADERS, 0, sid, block) + frame(DATA, 0, sid, grpc_message(b"x")))
+            return
+        if cfg.orphan_continuation:
+            self.send(frame(CONTINUATION, END_HEADERS, sid, self.enc.encode([(":status", "200")])))
             return
         h = self.srv.handlers.get(hdr.get(":path", ""))
         code, message, resp = h(msg) if h is not None else (12, f"unknown method {hdr.get(':path')}", b"")

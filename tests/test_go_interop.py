@@ -14,7 +14,10 @@ from the vendored sources (rocm_k8s_device_plugin_amd/testing/gopeer.py):
   CONTINUATION frames, server PINGs, SETTINGS changes mid-call, small windows
   for large requests, GOAWAY ENHANCE_YOUR_CALM ``too_many_pings``, graceful
   GOAWAY, RST_STREAM(REFUSED_STREAM), non-gRPC HTTP status, a server that
-  never answers (deadline, abort fd).
+  never answers (deadline, abort fd); and what other HTTP/2 servers may send
+  (padding, HEADERS priority, PRIORITY / unknown frames, other RST_STREAM
+  codes, GOAWAY before the call) or break (oversized frames, interrupted or
+  orphan header blocks).
 
 Reference: vendor/google.golang.org/grpc/internal/transport/{http2_client,
 http2_server,controlbuf,flowcontrol,bdp_estimator}.go, vendor/golang.org/x/net/
@@ -371,6 +374,73 @@ def test_native_client_http_error_status(tmp_path):
     with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(http_status=503)):
         status, msg, _ = _client(path).unary(ECHO, b"x", 5.0)
         assert status == 14 and "503" in msg
+
+
+@pytest.mark.parametrize("http,status", [(400, 13), (401, 16), (403, 7), (404, 12), (418, 2)])
+def test_native_client_http_status_mapping(tmp_path, http, status):
+    """A non-gRPC HTTP answer (a proxy in front of the exporter) maps as grpc-go's HTTPStatusConvTab."""
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(http_status=http)):
+        got, msg, _ = _client(path).unary(ECHO, b"x", 5.0)
+        assert got == status and str(http) in msg
+
+
+@pytest.mark.parametrize("cfg", [
+    gp.GoServerConfig(pad=7),
+    gp.GoServerConfig(pad=255),
+    gp.GoServerConfig(priority_in_headers=True),
+    gp.GoServerConfig(pad=3, priority_in_headers=True, continuation_chunk=4),
+    gp.GoServerConfig(noise_frames=True),
+], ids=["pad7", "pad255", "priority", "pad+priority+continuation", "priority-and-unknown-frames"])
+def test_native_client_accepts_what_other_http2_servers_send(tmp_path, cfg):
+    """Padding, HEADERS priority fields, PRIORITY and unknown extension frames
+    are legal HTTP/2 (RFC 7540 6.1, 6.2, 6.3, 4.1) that grpc-go never sends: the
+    answer is read past them, padding included, and the connection stays usable."""
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, cfg) as srv:
+        c = _client(path)
+        for payload in (b"", b"hello", bytes(range(256)) * 300):   # 76.8 kB: several DATA frames and credits
+            assert c.unary(ECHO, payload, 10.0) == (0, "", payload)
+        assert c.connected and srv.violations == []
+
+
+@pytest.mark.parametrize("code,status", [(gp.CANCEL, 1), (gp.ENHANCE_YOUR_CALM, 8), (12, 7), (2, 13)])
+def test_native_client_rst_stream_codes(tmp_path, code, status):
+    """RST_STREAM codes map as grpc-go's http2ErrConvTab; the connection survives a reset stream."""
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(rst_code=code)):
+        c = _client(path)
+        got, msg, _ = c.unary(ECHO, b"x", 5.0)
+        assert got == status and "RST_STREAM" in msg
+        assert c.connected
+
+
+def test_native_client_goaway_before_the_call(tmp_path):
+    """GOAWAY with a last-stream-id below ours: the call was never processed; the
+    error names the code and the debug text, and the connection is closed."""
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(goaway_first=gp.NO_ERROR)):
+        c = _client(path)
+        status, msg, _ = c.unary(ECHO, b"x", 5.0)
+        assert status == -1 and "before the call" in msg and "shutting down" in msg
+        assert not c.connected and c.unary(ECHO, b"y", 1.0)[0] == -1
+
+
+@pytest.mark.parametrize("cfg,text", [
+    (gp.GoServerConfig(oversized_data=True), "frame larger than 16384"),
+    (gp.GoServerConfig(interrupted_headers=True), "CONTINUATION expected"),
+    (gp.GoServerConfig(orphan_continuation=True), "CONTINUATION without HEADERS"),
+], ids=["oversized-frame", "interrupted-header-block", "orphan-continuation"])
+def test_native_client_protocol_violations_end_the_call_cleanly(tmp_path, cfg, text):
+    """A peer that breaks the framing rules: the call fails at once with the
+    reason, the connection is dropped, and a fresh one works."""
+    path = str(tmp_path / "go.sock")
+    with gp.GoServer(path, {ECHO: _echo}, cfg):
+        c = _client(path)
+        t0 = time.monotonic()
+        status, msg, _ = c.unary(ECHO, b"x", 5.0)
+        assert status == -1 and text in msg, msg
+        assert time.monotonic() - t0 < 2.0 and not c.connected
 
 
 def test_native_client_unknown_method_and_grpc_error(tmp_path):
