@@ -12,6 +12,7 @@
 #   profprobe  rocprofv3 kernel stats of one HIP container entrypoint -> gpurun_out/prof_probe/
 #   hipvariants  tools/hip_setup_variants.py (own vs null stream)     -> gpurun_out/hip_setup_variants.json
 #   asan    the native-daemon GPU tests against the ASan/UBSan builds in asan_bin/
+#   tsan    the same against the ThreadSanitizer builds in tsan_bin/
 #   soak    4 min native daemon soak, every health source on, a HIP container every second -> gpurun_out/soak_native.json
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
@@ -87,6 +88,16 @@ for s in "$@"; do
         timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "native or daemon or labeller" \
         > gpurun_out/gputests_asan.log 2>&1 || { tail -40 gpurun_out/gputests_asan.log; exit 1; }
       tail -3 gpurun_out/gputests_asan.log ;;
+    tsan)
+      # the same GPU tests against the ThreadSanitizer builds (host code only; tsan_bin/ holds
+      # build/native-thread/pkg/bin/*): the health engine, probe-server supervision and RPC threads
+      # racing for real, with the GPU liveness path on; the first report fails the daemon
+      step tsan
+      TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
+      MI355X_NATIVE_DAEMON_EXE=$PWD/tsan_bin/mi355x-device-plugin MI355X_NATIVE_LABELLER_EXE=$PWD/tsan_bin/mi355x-node-labeller \
+        timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "native or daemon or labeller" \
+        > gpurun_out/gputests_tsan.log 2>&1 || { tail -40 gpurun_out/gputests_tsan.log; exit 1; }
+      tail -3 gpurun_out/gputests_tsan.log ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
