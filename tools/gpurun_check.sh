@@ -93,8 +93,17 @@ for s in "$@"; do
       # build/native-thread/pkg/bin/*): the health engine, probe-server supervision and RPC threads
       # racing for real, with the GPU liveness path on; the first report fails the daemon
       step tsan
-      TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
-      MI355X_NATIVE_DAEMON_EXE=$PWD/tsan_bin/mi355x-device-plugin MI355X_NATIVE_LABELLER_EXE=$PWD/tsan_bin/mi355x-node-labeller \
+      # TSan's fixed shadow layout needs ASLR off for its processes (the box's kernel randomises
+      # with more bits than the runtime accepts): launchers that start each binary under setarch -R
+      w=$(mktemp -d)
+      for b in mi355x-device-plugin mi355x-node-labeller; do
+        printf '#!/bin/bash\nexec setarch "$(uname -m)" -R %s "$@"\n' "$PWD/tsan_bin/$b" > "$w/$b" && chmod +x "$w/$b"
+      done
+      # first the binary alone on the real node (a runtime that cannot map its shadow fails here)
+      TSAN_OPTIONS="halt_on_error=1 suppressions=$PWD/native/tsan.supp" timeout -k 10 60 "$w/mi355x-device-plugin" -dry_run \
+        > gpurun_out/tsan_dry_run.json 2> gpurun_out/tsan_dry_run.err || { tail -30 gpurun_out/tsan_dry_run.err; exit 1; }
+      TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$PWD/native/tsan.supp" \
+      MI355X_NATIVE_DAEMON_EXE=$w/mi355x-device-plugin MI355X_NATIVE_LABELLER_EXE=$w/mi355x-node-labeller \
         timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "native or daemon or labeller" \
         > gpurun_out/gputests_tsan.log 2>&1 || { tail -40 gpurun_out/gputests_tsan.log; exit 1; }
       tail -3 gpurun_out/gputests_tsan.log ;;
