@@ -13,6 +13,7 @@
 #   hipvariants  tools/hip_setup_variants.py (own vs null stream)     -> gpurun_out/hip_setup_variants.json
 #   asan    the native-daemon GPU tests against the ASan/UBSan builds in asan_bin/
 #   tsan    the same against the ThreadSanitizer builds in tsan_bin/
+#   tsansoak  2 min soak of the ThreadSanitizer daemon, every health source on, HIP containers -> gpurun_out/soak_tsan.json
 #   soak    4 min native daemon soak, every health source on, a HIP container every second -> gpurun_out/soak_native.json
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
@@ -21,6 +22,18 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
+# TSan's fixed shadow layout needs ASLR off for its processes (the box's kernel randomises
+# with more bits than the runtime accepts): launchers that start each tsan_bin/ binary
+# under setarch -R, in a fresh directory printed on stdout
+tsan_launchers() {
+  local w b
+  w=$(mktemp -d)
+  for b in mi355x-device-plugin mi355x-node-labeller; do
+    printf '#!/bin/bash\nexec setarch "$(uname -m)" -R %s "$@"\n' "$PWD/tsan_bin/$b" > "$w/$b" && chmod +x "$w/$b"
+  done
+  echo "$w"
+}
+TSAN_ENV="halt_on_error=1 second_deadlock_stack=1 suppressions=$PWD/native/tsan.supp"
 for s in "$@"; do
   case "$s" in
     smoke)
@@ -93,20 +106,25 @@ for s in "$@"; do
       # build/native-thread/pkg/bin/*): the health engine, probe-server supervision and RPC threads
       # racing for real, with the GPU liveness path on; the first report fails the daemon
       step tsan
-      # TSan's fixed shadow layout needs ASLR off for its processes (the box's kernel randomises
-      # with more bits than the runtime accepts): launchers that start each binary under setarch -R
-      w=$(mktemp -d)
-      for b in mi355x-device-plugin mi355x-node-labeller; do
-        printf '#!/bin/bash\nexec setarch "$(uname -m)" -R %s "$@"\n' "$PWD/tsan_bin/$b" > "$w/$b" && chmod +x "$w/$b"
-      done
+      w=$(tsan_launchers)
       # first the binary alone on the real node (a runtime that cannot map its shadow fails here)
-      TSAN_OPTIONS="halt_on_error=1 suppressions=$PWD/native/tsan.supp" timeout -k 10 60 "$w/mi355x-device-plugin" -dry_run \
+      TSAN_OPTIONS="$TSAN_ENV" timeout -k 10 60 "$w/mi355x-device-plugin" -dry_run \
         > gpurun_out/tsan_dry_run.json 2> gpurun_out/tsan_dry_run.err || { tail -30 gpurun_out/tsan_dry_run.err; exit 1; }
-      TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$PWD/native/tsan.supp" \
+      TSAN_OPTIONS="$TSAN_ENV" \
       MI355X_NATIVE_DAEMON_EXE=$w/mi355x-device-plugin MI355X_NATIVE_LABELLER_EXE=$w/mi355x-node-labeller \
         timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "native or daemon or labeller" \
         > gpurun_out/gputests_tsan.log 2>&1 || { tail -40 gpurun_out/gputests_tsan.log; exit 1; }
       tail -3 gpurun_out/gputests_tsan.log ;;
+    tsansoak)
+      # 2 minutes of the soak against the ThreadSanitizer daemon: admissions back to back, a HIP
+      # container every 2 s, liveness + chip sweep + throughput check + the three amd-smi sources
+      step tsansoak
+      w=$(tsan_launchers)
+      TSAN_OPTIONS="$TSAN_ENV" timeout -k 10 300 python3 tools/soak_native.py --seconds 120 --report 20 \
+        --container-interval 2 --exe "$w/mi355x-device-plugin" \
+        --extra "-liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
+        --out gpurun_out/soak_tsan.json > gpurun_out/soak_tsan.log 2>&1 || { tail -c 3000 gpurun_out/soak_tsan.json; exit 1; }
+      tail -c 800 gpurun_out/soak_tsan.json ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac

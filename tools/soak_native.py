@@ -64,6 +64,30 @@ def pct(xs, q):
     return round(xs[min(len(xs) - 1, int(q * len(xs)))], 4) if xs else None
 
 
+
+SANITIZER_MARKERS = (b"WARNING: ThreadSanitizer", b"ERROR: AddressSanitizer", b"ERROR: LeakSanitizer", b"runtime error:")
+
+
+def sanitizer_reports(f):
+    """(count, first report text) of sanitizer findings in the daemon's whole stderr
+    file, read in chunks (a long soak logs every Allocate: hundreds of MB)."""
+    f.seek(0)
+    count, first, tail = 0, "", b""
+    while True:
+        chunk = f.read(1 << 22)
+        if not chunk:
+            break
+        buf = tail + chunk
+        for m in SANITIZER_MARKERS:
+            # markers wholly inside the carried-over tail were counted with the previous chunk
+            count += buf.count(m) - tail.count(m)
+            if not first and m in buf:
+                i = buf.index(m)
+                first = buf[i:i + 3000].decode(errors="replace")
+        tail = buf[-64:]
+    return count, first
+
+
 async def run_container(adm, minor_to_ord: dict, cont: dict) -> None:
     """The admitted pod's container, for real (blocking; the kfd teardown of the
     previous one is waited out first, as kubelet does before reusing devices)."""
@@ -94,7 +118,7 @@ async def main(a) -> int:
     # the daemon logs every Allocate (as the reference does): its stderr goes to a file, a
     # pipe nobody reads would fill and block its control loop (and with it the health pulses)
     errf = open(os.path.join(kdir, "daemon.stderr"), "w+b")
-    proc = await asyncio.create_subprocess_exec(EXE, "-kubelet_dir", kdir, "-sysfs_root", a.sysfs_root,
+    proc = await asyncio.create_subprocess_exec(a.exe, "-kubelet_dir", kdir, "-sysfs_root", a.sysfs_root,
                                                 "-pulse", str(a.pulse), "-exporter_socket", "", *extra,
                                                 stdout=asyncio.subprocess.DEVNULL, stderr=errf)
     rows = []
@@ -149,7 +173,7 @@ async def main(a) -> int:
             with urllib.request.urlopen(f"http://127.0.0.1:{a.metrics_port}/metrics", timeout=5) as r:
                 metrics = {ln.rsplit(" ", 1)[0]: float(ln.rsplit(" ", 1)[1]) for ln in r.read().decode().splitlines()
                            if ln and not ln.startswith("#") and "_bucket" not in ln}
-        doc = {"exe": "mi355x-device-plugin", "devices": n, "pulse_s": a.pulse, "seconds": a.seconds,
+        doc = {"exe": os.path.basename(a.exe), "exe_path": a.exe, "devices": n, "pulse_s": a.pulse, "seconds": a.seconds,
                "flags": extra, "metrics_end": metrics,
                "containers": ({"interval_s": a.container_interval, "started": cont["started"],
                                "failed": cont["failed"], "errors": cont["errors"][:5],
@@ -166,15 +190,19 @@ async def main(a) -> int:
         errf.seek(0, os.SEEK_END)
         errf.seek(max(0, errf.tell() - 4000))
         err = errf.read()
+        reports, first_report = sanitizer_reports(errf)
         errf.close()
     doc["exit_code"] = proc.returncode
+    doc["sanitizer_reports"] = reports
+    if first_report:
+        doc["first_sanitizer_report"] = first_report
     doc["stderr_tail"] = err.decode(errors="replace")[-500:]
     if a.out:
         with open(a.out, "w") as f:
             json.dump(doc, f, indent=1)
     print(json.dumps({k_: doc[k_] for k_ in ("admissions", "errors", "exit_code")}))
     bad_containers = doc["containers"] and (doc["containers"]["failed"] or doc["containers"]["device_unhealthy_after"])
-    return 0 if doc["errors"] == 0 and doc["exit_code"] == 0 and not bad_containers else 1
+    return 0 if doc["errors"] == 0 and doc["exit_code"] == 0 and not bad_containers and not reports else 1
 
 
 if __name__ == "__main__":
@@ -185,6 +213,8 @@ if __name__ == "__main__":
     ap.add_argument("--sysfs-root", default="/sys")
     ap.add_argument("--out", default="")
     ap.add_argument("--extra", default="", help="more daemon flags, space-separated")
+    ap.add_argument("--exe", default=os.environ.get("MI355X_NATIVE_DAEMON_EXE") or EXE,
+                    help="the daemon binary (e.g. a ThreadSanitizer build; default: this tree's)")
     ap.add_argument("--metrics-port", type=int, default=0)
     ap.add_argument("--container-runtime", default="hip", choices=["hip", "hsa"])
     ap.add_argument("--container-interval", type=float, default=0.0,
