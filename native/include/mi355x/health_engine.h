@@ -59,6 +59,7 @@ namespace mi355x::health {
 struct ProbeOutcome {
   bool ok = false;
   bool pending = false;    // the dispatch is still queued (kept slot) or missed its deadline on a busy GPU
+  bool interrupted = false;  // shutdown cut the probe short: no verdict either way
   std::string reason;
   double latency_ms = 0;
   int kfd_node_id = -1;    // identity of the agent that answered (-1 / "" = not reported)

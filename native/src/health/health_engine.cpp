@@ -427,6 +427,10 @@ void Engine::judge_liveness(const std::map<std::string, ProbeOutcome>& outcomes,
   }
   for (const auto& [id, o] : outcomes) {
     Track& tr = track_[id];
+    if (o.interrupted) {  // the daemon is stopping: the track keeps its last verdict
+      if (!tr.live) (*reasons)[id].push_back("liveness probe: " + tr.last_reason);
+      continue;
+    }
     metrics::global().set("mi355x_dp_liveness_probe_ms", o.latency_ms, {{"device", id}},
                           "last liveness probe round trip");
     if (!o.pending) tr.idle_pending = 0;
@@ -794,6 +798,7 @@ void Engine::perf_check(const std::map<std::string, int>& ords) {
     auto it = by_ord.find(ord);
     if (it == by_ord.end()) continue;
     const ProbeOutcome& o = it->second;
+    if (o.interrupted) continue;  // stopped by the shutdown, not failed: the last result stands
     std::string state = "ok", why;
     if (!o.ok) {
       state = "failed";

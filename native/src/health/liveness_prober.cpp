@@ -385,6 +385,7 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
         o.reason = aborted ? "probe interrupted (shutdown)" : why;
         o.latency_ms = ms;
         o.pending = kind == "probe" && !aborted;  // inconclusive on a busy GPU
+        o.interrupted = aborted;
         out[j.ordinal] = o;
         continue;
       }
@@ -592,7 +593,10 @@ std::map<int, ProbeOutcome> LivenessProber::probe(const std::vector<int>& ordina
     }
     if (err == "interrupted") {  // shutdown: no fresh processes now
       std::map<int, ProbeOutcome> out;
-      for (int o : uniq) out[o].reason = "probe interrupted (shutdown)";
+      for (int o : uniq) {
+        out[o].reason = "probe interrupted (shutdown)";
+        out[o].interrupted = true;
+      }
       return out;
     }
     // a wedged device stalls the whole server: drop it and isolate per device

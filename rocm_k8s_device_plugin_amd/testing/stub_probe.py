@@ -49,7 +49,7 @@ def _device(ordinal_reported, mode, nonce, host_ordinal=None):
 def _perf_device(ordinal_reported, mode, nonce, host_ordinal=None):
     """Throughput-check reply (kind "perf"); modes from the control file's
     "perf" map: slow_hbm, slow_mfma, slow_xcd (one XCD at a third of the clock),
-    corrupt (HBM words read back wrong)."""
+    corrupt (HBM words read back wrong); hang (the server never answers; serve mode only)."""
     xcd = [1530.0] * 8
     if mode == "slow_xcd":
         xcd[3] = 510.0
@@ -108,8 +108,10 @@ def serve():
             o, n = tok.split(":")
             hosto = vis[int(o)] if vis and int(o) < len(vis) else o
             if kind == "perf":
-                devs.append(_perf_device(int(o), ctl.get("perf", {}).get(hosto, "ok"), int(n, 0),
-                                         host_ordinal=int(hosto)))
+                pmode = ctl.get("perf", {}).get(hosto, "ok")
+                if pmode == "hang":   # a check that never finishes (the daemon stops meanwhile)
+                    time.sleep(3600)
+                devs.append(_perf_device(int(o), pmode, int(n, 0), host_ordinal=int(hosto)))
                 continue
             mode = ctl.get(hosto, "ok")
             if mode == "server_fail":

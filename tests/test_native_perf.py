@@ -180,3 +180,41 @@ def test_daemon_perf_check_and_validation(tmp_path):
                         "perf_action")):
         p = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=20)
         assert p.returncode == 1 and want in p.stderr, (args, p.stderr)
+
+
+def test_daemon_shutdown_during_a_throughput_check_changes_no_verdict(tmp_path):
+    """SIGTERM while a throughput check is in flight: the check is cut short,
+    which is no verdict. No device flips to Unhealthy on the way out (found in
+    an MI355X soak, where the last check of the run logged `ok -> failed ...
+    probe interrupted (shutdown)` and `Healthy -> Unhealthy`)."""
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text("{}")
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = _by_ordinal(eng)
+    eng.close()
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        p = subprocess.Popen([EXE, "-kubelet_dir", kdir, "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                              "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_probe", STUB,
+                              "-liveness_fail_threshold", "1", "-liveness_timeout", "30", "-perf_check_every", "1",
+                              "-perf_action", "unhealthy"],
+                             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                             env=dict(os.environ, MI355X_STUB_PROBE_CONTROL=str(ctl)))
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            assert all(h == "Healthy" for h in st.devices.values())
+            ctl.write_text(json.dumps({"perf": {"2": "hang"}}))   # the next check never returns
+            await asyncio.sleep(3.0)
+        finally:
+            rc, err = await asyncio.to_thread(_stop, p)
+            await k.stop()
+        assert rc == 0, err[-3000:]
+        assert "-> Unhealthy" not in err and "-> failed" not in err, err[-3000:]
+        assert all(h == "Healthy" for h in k.resources["amd.com/gpu"].devices.values())
+        return dev
+
+    asyncio.run(asyncio.wait_for(go(), 60))
