@@ -194,6 +194,10 @@ async def main(a) -> int:
         errf.close()
     doc["exit_code"] = proc.returncode
     doc["sanitizer_reports"] = reports
+    # stopping the daemon must not flip a device (a check cut short by the shutdown is no verdict)
+    tail_text = err.decode(errors="replace")
+    after = tail_text[tail_text.find("Received signal"):] if "Received signal" in tail_text else ""
+    doc["transitions_after_shutdown"] = after.count("-> Unhealthy") + after.count("-> failed")
     if first_report:
         doc["first_sanitizer_report"] = first_report
     doc["stderr_tail"] = err.decode(errors="replace")[-500:]
@@ -202,7 +206,8 @@ async def main(a) -> int:
             json.dump(doc, f, indent=1)
     print(json.dumps({k_: doc[k_] for k_ in ("admissions", "errors", "exit_code")}))
     bad_containers = doc["containers"] and (doc["containers"]["failed"] or doc["containers"]["device_unhealthy_after"])
-    return 0 if doc["errors"] == 0 and doc["exit_code"] == 0 and not bad_containers and not reports else 1
+    ok = doc["errors"] == 0 and doc["exit_code"] == 0 and not bad_containers and not reports
+    return 0 if ok and not doc["transitions_after_shutdown"] else 1
 
 
 if __name__ == "__main__":
