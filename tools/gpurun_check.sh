@@ -14,7 +14,7 @@
 #   asan    the native-daemon GPU tests against the ASan/UBSan builds in asan_bin/
 #   tsan    the same against the ThreadSanitizer builds in tsan_bin/
 #   asansoak  the same soak against the ASan/UBSan daemon in asan_bin/ -> gpurun_out/soak_asan.json
-#   tsansoak  2 min soak of the ThreadSanitizer daemon, every health source on, HIP containers -> gpurun_out/soak_tsan.json
+#   tsansoak  2 min (SOAK_SECONDS) soak of the ThreadSanitizer daemon, every health source on, HIP containers -> gpurun_out/soak_tsan.json
 #   soak    4 min native daemon soak, every health source on, a HIP container every second -> gpurun_out/soak_native.json
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
@@ -121,16 +121,16 @@ for s in "$@"; do
       # container every 2 s, liveness + chip sweep + throughput check + the three amd-smi sources
       step tsansoak
       w=$(tsan_launchers)
-      TSAN_OPTIONS="$TSAN_ENV" timeout -k 10 300 python3 tools/soak_native.py --seconds 120 --report 20 \
-        --container-interval 2 --exe "$w/mi355x-device-plugin" \
+      TSAN_OPTIONS="$TSAN_ENV" timeout -k 10 $(( ${SOAK_SECONDS:-120} + 180 )) python3 tools/soak_native.py --seconds "${SOAK_SECONDS:-120}" \
+        --report 20 --container-interval 2 --exe "$w/mi355x-device-plugin" \
         --extra "-liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_tsan.json > gpurun_out/soak_tsan.log 2>&1 || { tail -c 3000 gpurun_out/soak_tsan.json; exit 1; }
       tail -c 800 gpurun_out/soak_tsan.json ;;
     asansoak)
       # the same 2-minute soak against the ASan/UBSan daemon (asan_bin/)
       step asansoak
-      UBSAN_OPTIONS="print_stacktrace=1" timeout -k 10 300 python3 tools/soak_native.py --seconds 120 --report 20 \
-        --container-interval 2 --exe "$PWD/asan_bin/mi355x-device-plugin" \
+      UBSAN_OPTIONS="print_stacktrace=1" timeout -k 10 $(( ${SOAK_SECONDS:-120} + 180 )) python3 tools/soak_native.py --seconds "${SOAK_SECONDS:-120}" \
+        --report 20 --container-interval 2 --exe "$PWD/asan_bin/mi355x-device-plugin" \
         --extra "-liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_asan.json > gpurun_out/soak_asan.log 2>&1 || { tail -c 3000 gpurun_out/soak_asan.json; exit 1; }
       tail -c 800 gpurun_out/soak_asan.json ;;
