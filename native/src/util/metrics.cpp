@@ -283,6 +283,18 @@ void HttpEndpoint::loop() {
         break;
       }
     }
+    // Lingering close: a client whose request was not read to the end (a head
+    // cut at 16 KiB, a body) would otherwise get a RST, which can destroy the
+    // response in flight. Half-close, then drain until it closes (200 ms at most).
+    ::shutdown(c, SHUT_WR);
+    const auto ldeadline = Clock::now() + std::chrono::milliseconds(200);
+    char sink[4096];
+    while (Clock::now() < ldeadline) {
+      pollfd q{c, POLLIN, 0};
+      if (::poll(&q, 1, 50) < 0 && errno != EINTR) break;
+      const ssize_t n = ::read(c, sink, sizeof(sink));
+      if (n == 0 || (n < 0 && errno != EAGAIN && errno != EINTR)) break;
+    }
     ::close(c);
   }
 }

@@ -168,3 +168,67 @@ def test_daemon_metrics_port_in_use_is_an_error(tmp_path):
         p = _daemon(str(tmp_path / "dp"), fi, "-metrics_port", str(port), "-exporter_socket", "")
         rc, err = _stop(p) if p.wait(timeout=20) is not None else (None, "")
     assert rc == 1 and "cannot serve /metrics" in err
+
+
+def _raw_http(port, chunks, gap=0.0, read=True, timeout=10.0):
+    """Send a request head in pieces; returns (status line, seconds to the answer)."""
+    import time
+    with socket.create_connection(("127.0.0.1", port), timeout=timeout) as c:
+        t0 = time.monotonic()
+        for ch in chunks:
+            c.sendall(ch)
+            time.sleep(gap)
+        if not read:
+            return None, 0.0
+        data = b""
+        while True:
+            b = c.recv(65536)
+            if not b:
+                break
+            data += b
+        return data.split(b"\r\n", 1)[0].decode(), time.monotonic() - t0
+
+
+def test_metrics_endpoint_survives_awkward_clients(tmp_path):
+    """The /metrics endpoint is one thread serving one connection at a time, so
+    every wait is bounded: a head sent in pieces is answered; a client that sends
+    nothing delays the next scrape by at most the 5 s head deadline; a head
+    without an end (16 KiB of header) and a client that leaves early cost nothing."""
+    import threading
+    import time
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = str(tmp_path / "dp")
+    port = _free_port()
+    p = _daemon(kdir, fi, "-exporter_socket", "", "-metrics_port", str(port))
+    try:
+        deadline = time.monotonic() + 20
+        while time.monotonic() < deadline:
+            try:
+                if _get(port, "/healthz")[0] == 200:
+                    break
+            except OSError:
+                time.sleep(0.05)
+        # a slow client: the head arrives in three pieces 0.2 s apart
+        line, _ = _raw_http(port, [b"GET /met", b"rics HTTP/1.1\r\nHost: x\r\n", b"\r\n"], gap=0.2)
+        assert line == "HTTP/1.0 200 OK"
+        # LF-only line ends are accepted too
+        assert _raw_http(port, [b"GET /healthz HTTP/1.0\n\n"])[0] == "HTTP/1.0 200 OK"
+        # a client that leaves before finishing its head
+        _raw_http(port, [b"GET /metrics HTT"], read=False)
+        # a head that never ends: cut at 16 KiB and answered (the path is still read)
+        line, dt = _raw_http(port, [b"GET /metrics HTTP/1.1\r\nX-Pad: " + b"a" * 20000])
+        assert line == "HTTP/1.0 200 OK" and dt < 5.0
+        # a silent client holds the endpoint until its 5 s head deadline; a scrape behind it waits, then succeeds
+        silent = socket.create_connection(("127.0.0.1", port))
+        time.sleep(0.1)
+        got = {}
+        th = threading.Thread(target=lambda: got.update(r=_raw_http(port, [b"GET /metrics HTTP/1.1\r\n\r\n"])))
+        th.start()
+        th.join(15)
+        silent.close()
+        line, dt = got["r"]
+        assert line == "HTTP/1.0 200 OK" and dt < 6.5
+        assert _get(port, "/metrics")[0] == 200
+    finally:
+        rc, err = _stop(p)
+    assert rc == 0, err[-3000:]
