@@ -342,6 +342,17 @@ def _running_labeller(tmp_path, srv, **kw):
     return lab, t
 
 
+def _quiet(lab, for_s=0.5, limit_s=10.0):
+    """Wait until the labeller has started no pass for `for_s`; its pass count then."""
+    import time
+    last, since, t0 = lab.stats.passes, time.monotonic(), time.monotonic()
+    while time.monotonic() - since < for_s and time.monotonic() - t0 < limit_s:
+        time.sleep(0.05)
+        if lab.stats.passes != last:
+            last, since = lab.stats.passes, time.monotonic()
+    return last
+
+
 def test_watch_restores_a_stripped_label_within_seconds(tmp_path):
     """Labels stripped by someone else come back from the watch event, not
     the 300 s resync (reference: controller-runtime watch, main.go:551-580)."""
@@ -353,7 +364,9 @@ def test_watch_restores_a_stripped_label_within_seconds(tmp_path):
         lab, t = _running_labeller(tmp_path, srv)
         assert _wait(lambda: srv.labels("node-w").get("amd.com/gpu.vram") == "288G")
         assert _wait(lambda: srv.watch_starts >= 1)
-        passes = lab.stats.passes
+        # let the passes of the start-up (and of our own first PATCH's event) finish first: a pass
+        # counts when it starts, so one still running would restore the label uncounted
+        passes = _quiet(lab)
         labels = srv.labels("node-w")
         labels.pop("amd.com/gpu.vram")
         t0 = time.monotonic()
@@ -364,13 +377,8 @@ def test_watch_restores_a_stripped_label_within_seconds(tmp_path):
         assert time.monotonic() - t0 < 5.0
         assert lab.stats.watch_kicks >= 1 and lab.stats.passes > passes
         # our own PATCH comes back as an event that needs nothing: no reconcile loop. Let a pass
-        # that is still running finish (quiet for 0.5 s), then nothing more may start.
-        last, quiet_since = lab.stats.passes, time.monotonic()
-        while time.monotonic() - quiet_since < 0.5 and time.monotonic() - t0 < 10:
-            time.sleep(0.05)
-            if lab.stats.passes != last:
-                last, quiet_since = lab.stats.passes, time.monotonic()
-        settled = lab.stats.passes
+        # that is still running finish, then nothing more may start.
+        settled = _quiet(lab)
         time.sleep(0.6)
         assert lab.stats.passes == settled
     finally:
