@@ -32,6 +32,9 @@
 #include "init_sampler.h"
 #include "mi355x/liveness_probe.h"
 
+// defined by the container-emulation builds (native/tools/probe_emu.cpp) only
+extern "C" __attribute__((weak)) const char* mi355x_probe_view_json();
+
 namespace {
 
 double cpu_ms(double* user_ms = nullptr) {
@@ -570,6 +573,8 @@ int main(int argc, char** argv) {
   double cpu_user_runtime = 0;
   const double cpu_runtime = cpu_ms(&cpu_user_runtime);
   const long long syscr_runtime = read_syscalls();
+  // the view's effect on the runtime's start-up walk, read at the same point as syscr
+  const std::string view_runtime = mi355x_probe_view_json ? mi355x_probe_view_json() : "";
   double iph[5];
   init_phases(iph);
   if (serve_mode) {
@@ -629,11 +634,12 @@ int main(int argc, char** argv) {
   const double cpu_ready = cpu_ms();
   std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
               "\"t_ready_ns\":%llu,\"cpu_ms_runtime\":%.2f,\"cpu_user_ms_runtime\":%.2f,\"cpu_ms_ready\":%.2f,\"read_syscalls_runtime\":%lld,"
-              "\"init_us\":{\"dlopen\":%.1f,\"kfd_open\":%.1f,\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"init_profile\":%s,\"devices\":%s}\n",
+              "\"init_us\":{\"dlopen\":%.1f,\"kfd_open\":%.1f,\"hsa_init\":%.1f,\"agents\":%.1f,\"pools\":%.1f},\"init_profile\":%s,"
+              "\"view\":%s,\"devices\":%s}\n",
               all_ok ? "true" : "false", n, identify ? "true" : "false", static_cast<unsigned long long>(t_start),
               static_cast<unsigned long long>(t_runtime), static_cast<unsigned long long>(t_ready), cpu_runtime,
               cpu_user_runtime, cpu_ready, syscr_runtime, iph[0], iph[1], iph[2], iph[3], iph[4], init_profile.c_str(),
-              devices_json(results).c_str());
+              mi355x_probe_view_json ? view_runtime.c_str() : "null", devices_json(results).c_str());
   std::fflush(stdout);
   // After the verdict. The exit mode was an experiment: the kernel's kfd
   // process teardown after we are gone costs the same either way

@@ -47,6 +47,24 @@ bool g_count = true;                               // $MI355X_INITPROF_COUNT != 
 thread_local std::string t_path;
 std::atomic<long> g_hidden{0};
 thread_local bool t_in_hook = false;
+// lock-free, always on: what the container view changed (the probe's "view" field)
+std::atomic<long> g_seen{0};             // paths through the hooks
+std::atomic<long> g_node_cache_ok{0};    // successful opens under /sys/devices/system/node/node*/cpu*/cache
+
+// a path under the NUMA-node tree's per-CPU cache descriptors (the -node_view hides them)
+bool node_cpu_cache(const char* p) {
+  static const char kNode[] = "/sys/devices/system/node/node";
+  if (!p || std::strncmp(p, kNode, sizeof(kNode) - 1) != 0) return false;
+  const char* cpu = std::strstr(p + sizeof(kNode) - 1, "/cpu");
+  return cpu && std::strstr(cpu, "/cache") != nullptr;
+}
+
+template <typename R>
+R tally(const char* path, R r, bool ok) {
+  g_seen.fetch_add(1, std::memory_order_relaxed);
+  if (ok && node_cpu_cache(path)) g_node_cache_ok.fetch_add(1, std::memory_order_relaxed);
+  return r;
+}
 
 
 std::string fold(const char* p) {
@@ -127,7 +145,8 @@ int open(const char* path, int flags, ...) {
     errno = ENOENT;
     return -1;
   }
-  return fn(map_path(path), flags, mode);
+  const int fd = fn(map_path(path), flags, mode);
+  return tally(path, fd, fd >= 0);
 }
 
 int open64(const char* path, int flags, ...) {
@@ -143,7 +162,8 @@ int open64(const char* path, int flags, ...) {
     errno = ENOENT;
     return -1;
   }
-  return fn(map_path(path), flags, mode);
+  const int fd = fn(map_path(path), flags, mode);
+  return tally(path, fd, fd >= 0);
 }
 
 int openat(int dirfd, const char* path, int flags, ...) {
@@ -159,7 +179,8 @@ int openat(int dirfd, const char* path, int flags, ...) {
     errno = ENOENT;
     return -1;
   }
-  return fn(dirfd, map_path(path), flags, mode);
+  const int fd = fn(dirfd, map_path(path), flags, mode);
+  return tally(path, fd, fd >= 0);
 }
 
 FILE* fopen(const char* path, const char* mode) {
@@ -168,7 +189,8 @@ FILE* fopen(const char* path, const char* mode) {
     errno = ENOENT;
     return nullptr;
   }
-  return fn(map_path(path), mode);
+  FILE* f = fn(map_path(path), mode);
+  return tally(path, f, f != nullptr);
 }
 
 FILE* fopen64(const char* path, const char* mode) {
@@ -177,7 +199,8 @@ FILE* fopen64(const char* path, const char* mode) {
     errno = ENOENT;
     return nullptr;
   }
-  return fn(map_path(path), mode);
+  FILE* f = fn(map_path(path), mode);
+  return tally(path, f, f != nullptr);
 }
 
 DIR* opendir(const char* path) {
@@ -186,7 +209,8 @@ DIR* opendir(const char* path) {
     errno = ENOENT;
     return nullptr;
   }
-  return fn(map_path(path));
+  DIR* d = fn(map_path(path));
+  return tally(path, d, d != nullptr);
 }
 
 }  // extern "C"
@@ -234,6 +258,13 @@ inline void path_interpose_configure() {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_counts) g_counts->clear();  // ignore the dynamic loader's own opens
   }
+}
+
+// {"paths":N,"node_cpu_cache_opens":N,"redirected":N,"dev_hidden":N}: cheap enough for every container
+inline std::string path_interpose_view_json() {
+  return "{\"paths\":" + std::to_string(g_seen.load()) + ",\"node_cpu_cache_opens\":" +
+         std::to_string(g_node_cache_ok.load()) + ",\"redirected\":" + std::to_string(g_redirected.load()) +
+         ",\"hidden\":" + std::to_string(g_hidden.load()) + "}";
 }
 
 // {"opens":N,"hidden":N,"redirected":N,"by_template":{...top 40...}}

@@ -11,4 +11,13 @@ namespace {
 struct Configure {
   Configure() { path_interpose_configure(); }
 } configure_at_start;
+std::string g_view_json;
 }  // namespace
+
+// probe_main.cpp prints this as the reply's "view" field when it is linked in:
+// what the emulated view did to the runtime's file walk (paths seen, per-CPU
+// cache descriptors opened under the NUMA-node tree, redirected, refused)
+extern "C" const char* mi355x_probe_view_json() {
+  g_view_json = path_interpose_view_json();
+  return g_view_json.c_str();
+}

@@ -139,7 +139,11 @@ def start_container(ordinals: Sequence[int], timeout_s: float = 60.0, iters: int
         if runtime not in ("mountemu", "hip-devemu"):
             raise ValueError(f"mounts cannot be applied to the {runtime!r} entrypoint (no path interposition)")
         env["MI355X_INITPROF_REDIRECT"] = redirect
-    argv = [*argv_prefix, exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
+    if runtime in ("mountemu", "hip-devemu"):
+        # an emulated container pays only the path checks of its view, never the
+        # measurement build's per-path counting (a lock and a map insert per open)
+        env.setdefault("MI355X_INITPROF_COUNT", "0")
+    argv =[*argv_prefix, exe or str(probe_executable(runtime)), "--devices", ",".join(str(i) for i in range(len(ordinals))),
             "--iters", str(iters), "--timeout", str(min(timeout_s, 30.0))]
     before = kfd_processes()
     t0 = time.monotonic_ns()
