@@ -458,7 +458,7 @@ int Daemon::run(int sig_fd, const volatile sig_atomic_t* stop) {
   topo_state_ = TopologyWatch(topo_watch_ ? topology_signature(f_.sysfs_root) : "");
   next_topo_ = t0 + topo_period_;
   sock_ = sock_id(kubelet_sock_);
-  if (sock_.present) start_all();
+  if (sock_.present && !*stop) start_all();  // a signal during init(): straight to shutdown
 
   int exit_code = 0;
   while (!*stop) {

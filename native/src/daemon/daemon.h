@@ -66,6 +66,10 @@ class Daemon {
   // The control loop until `*stop` (set by a signal handler that also writes
   // to `sig_fd`) or the watchdog trips; returns the exit code.
   int run(int sig_fd, const volatile sig_atomic_t* stop);
+  // Write end of the pipe that ends every wait of the workers (peer calls,
+  // probes, the first sweep in init()): a signal handler writes one byte to it,
+  // so a stop during a slow probe is not held until the probe's deadline.
+  int stop_fd() const { return stop_pipe_[1]; }
 
  private:
   std::string write_cdi(const std::set<std::string>& stale);

@@ -20,7 +20,8 @@
 //   health         every -pulse on a worker thread (daemon/health_controller.h)
 //   control loop   daemon/daemon.h
 //   signals        SIGTERM / SIGINT / SIGQUIT stop the servers, the probe server
-//                  and the workers, and remove the sockets
+//                  and the workers, and remove the sockets; a probe in flight
+//                  (also the first sweep, before registration) ends at once
 #include <fcntl.h>
 #include <signal.h>
 #include <unistd.h>
@@ -40,11 +41,14 @@ constexpr const char* kTitle = "AMD GPU device plugin for Kubernetes (MI355X-nat
 
 volatile sig_atomic_t g_stop = 0;
 int g_sig_pipe[2] = {-1, -1};
+volatile int g_daemon_stop_fd = -1;  // the daemon's stop pipe: aborts in-flight probes and peer calls
 
 void on_signal(int) {
   g_stop = 1;
   const char b = 1;
   if (g_sig_pipe[1] >= 0 && ::write(g_sig_pipe[1], &b, 1) < 0) {
+  }
+  if (g_daemon_stop_fd >= 0 && ::write(g_daemon_stop_fd, &b, 1) < 0) {
   }
 }
 
@@ -90,6 +94,8 @@ int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
 
   daemon::Daemon d(f);
+  g_daemon_stop_fd = d.stop_fd();
+  if (g_stop) return 0;     // a signal before the daemon existed
   const int rc = d.init();
   if (rc >= 0) return rc;
   return d.run(g_sig_pipe[0], &g_stop);

@@ -4,16 +4,9 @@
 #include <map>
 #include <set>
 
+#include "mi355x/goflag.h"
+
 namespace mi355x::daemon {
-namespace {
-
-bool parse_bool(const std::string& v, bool* out) {
-  if (v.empty() || v == "1" || v == "true" || v == "True" || v == "TRUE" || v == "t" || v == "T") return *out = true, true;
-  if (v == "0" || v == "false" || v == "False" || v == "FALSE" || v == "f" || v == "F") return *out = false, true;
-  return false;
-}
-
-}  // namespace
 
 std::string usage(const std::string& argv0) {
   return "usage: " + argv0 +
@@ -35,6 +28,7 @@ std::string usage(const std::string& argv0) {
 
 bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, bool* syntax) {
   *help = false;
+  err->clear();
   bool syntax_scratch = false;
   if (!syntax) syntax = &syntax_scratch;
   *syntax = false;
@@ -97,7 +91,9 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, 
       if (glog::is_bool_flag(name)) {
         glog::parse_flag(name, value, has_value, &f->log, err);
         if (!err->empty()) return bad(*err);
-      } else if (!parse_bool(has_value ? value : "", bools[name])) {
+      } else if (!has_value) {
+        *bools[name] = true;                          // -flag alone sets a boolean
+      } else if (!goflag::parse_bool(value, bools[name])) {
         return bad("invalid boolean value \"" + value + "\" for -" + name);
       }
       continue;
@@ -109,15 +105,9 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, 
     if (glog::parse_flag(name, value, true, &f->log, err)) {
       if (!err->empty()) return bad(*err);
     } else if (ints.count(name)) {
-      char* end = nullptr;
-      const long v = std::strtol(value.c_str(), &end, 10);
-      if (value.empty() || *end) return bad("invalid value \"" + value + "\" for flag -" + name);
-      *ints[name] = static_cast<int>(v);
+      if (!goflag::parse_int_flag(value, ints[name])) return bad("invalid value \"" + value + "\" for flag -" + name);
     } else if (floats.count(name)) {
-      char* end = nullptr;
-      const double v = std::strtod(value.c_str(), &end);
-      if (value.empty() || *end) return bad("invalid value \"" + value + "\" for flag -" + name);
-      *floats[name] = v;
+      if (!goflag::parse_float(value, floats[name])) return bad("invalid value \"" + value + "\" for flag -" + name);
     } else {
       *strs[name] = value;
     }

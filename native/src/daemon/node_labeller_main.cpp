@@ -58,6 +58,7 @@
 #include "../kube/kubeconfig.h"
 #include "../kube/labels.h"
 #include "mi355x/glog.h"
+#include "mi355x/goflag.h"
 #include "mi355x/drm_query.h"
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/kfd_topology.h"
@@ -96,19 +97,6 @@ struct Flags {
 
 constexpr const char* kTitle = "AMD GPU Node Labeller for Kubernetes (MI355X-native, native daemon)";
 
-bool parse_bool(const std::string& v, bool* out) {
-  if (v.empty() || v == "1" || v == "t" || v == "T" || v == "true" || v == "TRUE" || v == "True") return *out = true;
-  if (v == "0" || v == "f" || v == "F" || v == "false" || v == "FALSE" || v == "False") return !(*out = false);
-  return false;
-}
-
-bool parse_double(const std::string& v, double* out) {
-  char* end = nullptr;
-  const double d = std::strtod(v.c_str(), &end);
-  if (end == v.c_str() || *end) return false;
-  *out = d;
-  return true;
-}
 
 // the version banner, then the flags (main.go flag.Usage)
 void print_usage(FILE* out, const char* argv0, const std::string& sysfs_root) {
@@ -167,7 +155,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* syntax
     }
     if (is_kind || kBool.count(name)) {
       bool v = true;
-      if (has_value && !parse_bool(value, &v)) return bad("invalid boolean value \"" + value + "\" for -" + name);
+      if (has_value && !goflag::parse_bool(value, &v)) return bad("invalid boolean value \"" + value + "\" for -" + name);
       if (is_kind) f->enabled[name] = v;
       if (name == "watch") f->watch = v;
       if (name == "dry_run") f->dry_run = v;
@@ -187,18 +175,17 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* syntax
     } else if (name == "kubeconfig") {
       f->kubeconfig = value;
     } else if (name == "resync") {
-      if (!parse_double(value, &f->resync_s)) return bad("invalid value \"" + value + "\" for flag -resync");
+      if (!goflag::parse_float(value, &f->resync_s)) return bad("invalid value \"" + value + "\" for flag -resync");
     } else if (name == "topology_watch") {
-      if (!parse_double(value, &f->topology_watch_s))
+      if (!goflag::parse_float(value, &f->topology_watch_s))
         return bad("invalid value \"" + value + "\" for flag -topology_watch");
     } else if (name == "watch_backoff_max") {
-      if (!parse_double(value, &f->watch_backoff_max_s))
+      if (!goflag::parse_float(value, &f->watch_backoff_max_s))
         return bad("invalid value \"" + value + "\" for flag -watch_backoff_max");
     } else if (name == "watch_timeout") {
-      char* end = nullptr;
-      const long v = std::strtol(value.c_str(), &end, 10);
-      if (value.empty() || *end) return bad("invalid value \"" + value + "\" for flag -watch_timeout");
-      f->watch_timeout_s = static_cast<int>(std::max(1L, v));
+      int v = 0;
+      if (!goflag::parse_int_flag(value, &v)) return bad("invalid value \"" + value + "\" for flag -watch_timeout");
+      f->watch_timeout_s = std::max(1, v);
     } else if (name == "sysfs_root") {
       f->sysfs_root = value;
     } else if (name == "dev_root") {

@@ -450,8 +450,11 @@ std::map<int, ProbeOutcome> LivenessProber::probe_server(const std::vector<int>&
     auto doc = g == Got::kLine ? json::parse(hello) : std::nullopt;
     if (!doc || !jbool(&*doc, "serve") || !jbool(&*doc, "ok")) {
       kill_child(&srv->c);
-      *err = g == Got::kTimeout ? "probe server did not start within the deadline"
-                                : "probe server failed to start: " + hello.substr(0, 200);
+      // shutdown interrupted the start: "interrupted", so probe() reports interrupted
+      // outcomes instead of falling back to fresh GPU processes while the daemon stops
+      *err = g == Got::kAbort     ? "interrupted"
+             : g == Got::kTimeout ? "probe server did not start within the deadline"
+                                  : "probe server failed to start: " + hello.substr(0, 200);
       return {};
     }
     server_ = std::move(srv);

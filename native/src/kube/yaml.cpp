@@ -245,14 +245,19 @@ class Parser {
   // Returns the value's text with the line breaks kept (flow() folds them) and
   // comments removed; consumes those lines. A value alone on its line is returned as is.
   std::string continued(const std::string& first, int no, int indent, size_t* i) {
-    // the next non-blank raw line decides (a comment-like continuation of a quoted
-    // scalar, e.g. `  #"`, is not in lines_)
+    // A comment-only line ends a plain scalar, however deep it is indented
+    // (`device_count: 2` then `    # two GPUs` is 2, as PyYAML reads it). Inside a
+    // quoted scalar or a flow collection the same line is content or a comment
+    // the flow reader strips (a comment-like continuation of a quoted scalar,
+    // e.g. `  #"`, is not in lines_).
+    const bool plain = first.empty() || (first[0] != '"' && first[0] != '\'' && first[0] != '[' && first[0] != '{');
+    // the next non-blank raw line decides
     for (size_t r = static_cast<size_t>(no); r < raw_.size(); ++r) {
       const std::string rl = rtrim(raw_[r]);
       size_t ind = 0;
       while (ind < rl.size() && rl[ind] == ' ') ++ind;
       if (ind == rl.size()) continue;
-      if (static_cast<int>(ind) <= indent) return first;
+      if (static_cast<int>(ind) <= indent || (plain && rl[ind] == '#')) return first;
       break;
     }
     std::string text = first;
@@ -268,7 +273,7 @@ class Parser {
         ++r;
         continue;
       }
-      if (static_cast<int>(ind) <= indent) break;
+      if (static_cast<int>(ind) <= indent || (plain && rl[ind] == '#')) break;
       text += pending + "\n" + rl;
       pending.clear();
       last = ++r;

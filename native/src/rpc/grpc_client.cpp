@@ -391,13 +391,17 @@ Reply GrpcClient::unary(const std::string& path, const std::string& request, dou
           put_frame(&pending_out, kWindowUpdate, 0, 0, wu.data(), wu.size());
           st.recv_unacked = 0;
         }
-        size_t pad = 0;
+        // the payload without the pad-length byte and the padding (RFC 7540 6.1;
+        // PADDED with a pad length of 0 still carries the length byte)
+        const uint8_t* body = p;
+        size_t body_len = len;
         if (flags & kPadded) {
           if (len < 1 || p[0] >= len) return conn_fail("protocol error: bad padding");
-          pad = p[0];
+          body_len = len - 1 - p[0];
+          ++body;
         }
         if (sid != call.sid) return true;  // a stream we gave up on
-        if (len) call.data.append(reinterpret_cast<const char*>(p + (pad ? 1 : 0)), len - (pad ? pad + 1 : 0));
+        if (body_len) call.data.append(reinterpret_cast<const char*>(body), body_len);
         if (call.data.size() > kMaxMessage + 5) return conn_fail("response message too large");
         if (flags & kEndStream) {
           call.done = true;  // a closed stream needs no credit

@@ -2,6 +2,7 @@
 #include "mi355x/glog.h"
 
 #include "../kube/json.h"
+#include "mi355x/goflag.h"
 
 #include <execinfo.h>
 #include <fnmatch.h>
@@ -120,23 +121,17 @@ bool is_flag(const std::string& name) {
 
 bool parse_flag(const std::string& name, const std::string& value, bool has_value, Options* o, std::string* err) {
   auto as_bool = [&](bool* out) {
-    if (!has_value || value == "1" || value == "true" || value == "True" || value == "TRUE" || value == "t" ||
-        value == "T") {
-      *out = true;
-    } else if (value == "0" || value == "false" || value == "False" || value == "FALSE" || value == "f" ||
-               value == "F") {
-      *out = false;
-    } else {
-      *err = "invalid boolean value \"" + value + "\" for -" + name;
-    }
+    if (!has_value) *out = true;
+    else if (!goflag::parse_bool(value, out)) *err = "invalid boolean value \"" + value + "\" for -" + name;
   };
   if (name == "logtostderr") return as_bool(&o->logtostderr), true;
   if (name == "alsologtostderr") return as_bool(&o->alsologtostderr), true;
-  if (name == "v") {
-    char* end = nullptr;
-    const long v = std::strtol(value.c_str(), &end, 10);
-    if (value.empty() || *end) *err = "invalid value \"" + value + "\" for flag -v";
-    o->v = static_cast<int>(v);
+  if (name == "v") {  // glog's Level: strconv.ParseInt(value, 10, 32)
+    int64_t v = 0;
+    if (goflag::parse_int(value, 10, 32, &v))
+      o->v = static_cast<int>(v);
+    else
+      *err = "invalid value \"" + value + "\" for flag -v";
     return true;
   }
   if (name == "stderrthreshold") {
@@ -151,11 +146,8 @@ bool parse_flag(const std::string& name, const std::string& value, bool has_valu
   }
   if (name == "log_dir") return o->log_dir = value, true;
   if (name == "log_link") return o->log_link = value, true;
-  if (name == "logbuflevel") {
-    char* end = nullptr;
-    const long v = std::strtol(value.c_str(), &end, 10);
-    if (value.empty() || *end) *err = "invalid value \"" + value + "\" for flag -logbuflevel";
-    o->logbuflevel = static_cast<int>(v);
+  if (name == "logbuflevel") {  // an int flag
+    if (!goflag::parse_int_flag(value, &o->logbuflevel)) *err = "invalid value \"" + value + "\" for flag -logbuflevel";
     return true;
   }
   if (name == "vmodule") return o->vmodule = value, true;

@@ -757,6 +757,30 @@ static void test_flags_go_semantics() {
   CHECK(parse({"-pulse=2", "extra", "-nope"}, &syn, &err, &f) && f.pulse == 2);  // stops at "extra"
   CHECK(parse({"-pulse=2", "--", "-nope"}, &syn, &err, &f) && f.pulse == 2);
   CHECK(parse({"-pulse=2", "-", "-nope"}, &syn, &err, &f) && f.pulse == 2);      // "-" is an argument
+  // strconv.ParseBool: an empty value is an error, not true
+  CHECK(!parse({"-liveness="}, &syn, &err) && syn && err == "invalid boolean value \"\" for -liveness");
+  CHECK(!parse({"-logtostderr="}, &syn, &err) && syn);
+  CHECK(parse({"-liveness", "-pulse=1"}, &syn, &err, &f) && f.liveness);
+  CHECK(parse({"-liveness=F", "-pulse=1"}, &syn, &err, &f) && !f.liveness);
+  // strconv.ParseInt(s, 0, 64): base prefixes, leading-0 octal, '_' between digits, range
+  CHECK(parse({"-pulse=0x1e"}, &syn, &err, &f) && f.pulse == 30);
+  CHECK(parse({"-pulse=0o17"}, &syn, &err, &f) && f.pulse == 15);
+  CHECK(parse({"-pulse=017"}, &syn, &err, &f) && f.pulse == 15);
+  CHECK(parse({"-pulse=0b101"}, &syn, &err, &f) && f.pulse == 5);
+  CHECK(parse({"-pulse=1_000"}, &syn, &err, &f) && f.pulse == 1000);
+  CHECK(parse({"-pulse=+7"}, &syn, &err, &f) && f.pulse == 7);
+  CHECK(parse({"-pulse=0"}, &syn, &err, &f) && f.pulse == 0);
+  for (const char* badv : {"-pulse=08", "-pulse=1__0", "-pulse=_1", "-pulse=1_", "-pulse=0x", "-pulse=1.5",
+                           "-pulse= 3", "-pulse=99999999999", "-pulse=9223372036854775808"})
+    CHECK(!parse({badv}, &syn, &err) && syn && err.find("invalid value") == 0);
+  // glog's -v: strconv.ParseInt(s, 10, 32), so leading zeros are decimal and prefixes are refused
+  CHECK(parse({"-v=05"}, &syn, &err, &f) && f.log.v == 5);
+  CHECK(!parse({"-v=0x5"}, &syn, &err) && syn);
+  CHECK(!parse({"-v=4294967296"}, &syn, &err) && syn);
+  // strconv.ParseFloat
+  CHECK(parse({"-liveness_timeout=2.5e1"}, &syn, &err, &f) && f.liveness_timeout == 25.0);
+  CHECK(!parse({"-liveness_timeout= 2"}, &syn, &err) && syn);
+  CHECK(!parse({"-liveness_timeout=1e999"}, &syn, &err) && syn);
 }
 
 static void test_health_controller_generations(const std::string& tmp) {

@@ -51,6 +51,37 @@ class StepRecords:
     settle_ms: List[float] = field(default_factory=list)
     device_phases: List[Dict[str, float]] = field(default_factory=list)
     alloc: List[tuple] = field(default_factory=list)           # (preferred ms, short circuit, candidates, ids, used)
+    # the slowest container's own counters up to "GPU runtime initialised": read
+    # syscalls (/proc/self/io syscr), CPU ms, hsa_init us (HSA entrypoint only) and
+    # the emulated view's counters (cache descriptors opened, paths redirected)
+    read_syscalls: List[int] = field(default_factory=list)
+    cpu_ms_runtime: List[float] = field(default_factory=list)
+    hsa_init_ms: List[float] = field(default_factory=list)
+    node_cache_opens: List[int] = field(default_factory=list)
+
+    def phases(self) -> Dict[str, List[float]]:
+        """Per-step ms of each admission phase (aligned with latency_ms)."""
+        return {"plugin_rpc": self.rpc_ms, "runtime_prep": self.prespawn_ms, "exec_and_library_load": self.exec_ms,
+                "gpu_runtime_init": self.runtime_ms, "device_setup": self.setup_ms,
+                "launch_and_verify": self.launch_ms}
+
+    def row(self) -> Optional[dict]:
+        """A comparison row: latency p50 / p99, phase p50s, tail attribution and
+        the containers' start-up counters (None without steps)."""
+        if not self.latency_ms:
+            return None
+        med = lambda xs: round(pct(xs, .5), 3) if xs else None
+        return {"steps": len(self.latency_ms), "latency_p50_ms": med(self.latency_ms),
+                "latency_p99_ms": round(pct(self.latency_ms, .99), 3),
+                "phases_p50_ms": {k: med(v) for k, v in self.phases().items()},
+                "tail_attribution": tail_attribution(self.latency_ms, self.phases()),
+                "counters_p50": self.counters()}
+
+    def counters(self) -> dict:
+        med = lambda xs: round(pct(xs, .5), 3) if xs else None
+        return {"read_syscalls": med(self.read_syscalls), "cpu_ms_runtime": med(self.cpu_ms_runtime),
+                "hsa_init_ms": med([x for x in self.hsa_init_ms if x > 0]),
+                "node_cpu_cache_opens": med(self.node_cache_opens)}
 
 
 class Admissions:
@@ -93,7 +124,7 @@ class Admissions:
         d, a_ = self.d, self.args
         if mode == "pod" and d.rank != 0:
             # the pod's single container runs on rank 0; other ranks only keep step
-            return (True, 0, 0.0, "", (0, 0, 0, 0.0, {})), frozenset()
+            return (True, 0, 0.0, "", (0, 0, 0, 0.0, {}, (None, None, 0.0, None))), frozenset()
         pod = mode == "pod" or d.world == 1
         mine_ord = ordl if pod else [ordl[d.rank]]
         paths = None
@@ -109,19 +140,21 @@ class Admissions:
         # device set-up (HIP: hipSetDevice .. stream/buffers/events; HSA: queue, code object, buffers)
         sus = max((dv.get("setup_us", 0.0) for dv in devs), default=0.0)
         slow_dev = max(devs, key=lambda dv: dv.get("total_us", 0.0), default={})
+        view = r.doc.get("view") or {}
+        counters = (r.doc.get("read_syscalls_runtime"), r.doc.get("cpu_ms_runtime"),
+                    (r.doc.get("init_us") or {}).get("hsa_init", 0.0) / 1e3, view.get("node_cpu_cache_opens"))
         phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)), sus / 1e3,
-                  slow_dev.get("phase_us") or {})
+                  slow_dev.get("phase_us") or {}, counters)
         return (r.ok, r.t_ready_ns, kus, r.error, phases), r.kfd_lingering
 
     # ------------------------------------------------------------------ one step
-    def step(self, record: bool, runtime: Optional[str] = None, sink=None, settle: Optional[str] = None,
-             init_sink=None, mode: Optional[str] = None, dev_view: Optional[str] = None, pl=None,
-             alloc_sink=None) -> None:
-        """One admission. ``record``: a timed step (goes into ``rec``); ``sink`` /
-        ``init_sink`` / ``alloc_sink``: lists a comparison collects its latency,
-        runtime-init and allocation outcome in; the other keywords override the
-        run's --container-runtime / --settle / --container-mode / --dev-view and
-        the plugin admitted against."""
+    def step(self, record, runtime: Optional[str] = None, settle: Optional[str] = None,
+             mode: Optional[str] = None, dev_view: Optional[str] = None, pl=None, alloc_sink=None) -> None:
+        """One admission. ``record``: True for a timed step (goes into ``rec``),
+        a StepRecords a comparison row collects its steps in, or False (warm-up);
+        ``alloc_sink``: a list a comparison collects the allocation outcome in; the
+        other keywords override the run's --container-runtime / --settle /
+        --container-mode / --dev-view and the plugin admitted against."""
         from rocm_k8s_device_plugin_amd.container_runtime import wait_kfd_released
         a_, d, n, rec = self.args, self.d, self.n, self.rec
         runtime = runtime or a_.container_runtime
@@ -136,7 +169,8 @@ class Admissions:
             payload = None
         t0, ordl, tot, amsl, ids, mounts, groups = d.bcast(payload)
         mine, lingering = self._container(runtime, mode, dev_view, ordl, mounts, groups)
-        if record:   # the containers are up: does the bench / plugin process hold the GPU?
+        into = rec if record is True else (record or None)
+        if record is True:   # the containers are up: does the bench / plugin process hold the GPU?
             st_now = process_gpu_state()
             self.gpu_state["torch_cuda_initialized"] |= st_now["torch_cuda_initialized"]
             self.gpu_state["kfd_fds"] = max(self.gpu_state["kfd_fds"], st_now["kfd_fds"])
@@ -148,8 +182,8 @@ class Admissions:
             st = pl.allocator.stats
             a_rec = (adm.preferred_ms, bool(st.last_short_circuit), int(st.last_candidates),
                      sorted(adm.device_ids), adm.preferred_used)
-            if record:
-                rec.alloc.append(a_rec)
+            if into is not None:
+                into.alloc.append(a_rec)
             if alloc_sink is not None:
                 alloc_sink.append(a_rec)
         bad = [m[3] for m in allr if not m[0]]
@@ -165,15 +199,20 @@ class Admissions:
         # ~0.25 s each (measured ~0.15 s), capped so a stuck entry cannot stall the run
         cap = min(3.0, 0.25 + 0.25 * max(len(lingering), n))  # one process with N GPUs tears down N VMs
         waited = self._blocking(wait_kfd_released, lingering, timeout_s=cap) if settle == "kfd" else 0.0
-        sp, tm, trt, su, dph = slowest[4]   # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC), set-up ms, phases
+        # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC), set-up ms, phases, counters
+        sp, tm, trt, su, dph, (syscr, cpu_rt, hsa_ms, cache_opens) = slowest[4]
         lat = (t_ready - t0) / 1e6
-        if sink is not None:
-            sink.append(lat)
-        if init_sink is not None:
-            init_sink.append((trt - tm) / 1e6)
-        if not record:
+        if into is None:
             return
+        rec = into
         dev = (t_ready - trt) / 1e6
+        if syscr is not None:
+            rec.read_syscalls.append(syscr)
+        if cpu_rt is not None:
+            rec.cpu_ms_runtime.append(cpu_rt)
+        rec.hsa_init_ms.append(hsa_ms or 0.0)
+        if cache_opens is not None:
+            rec.node_cache_opens.append(cache_opens)
         rec.settle_ms.append(waited)
         rec.latency_ms.append(lat)
         rec.rpc_ms.append(tot)
@@ -221,7 +260,8 @@ class Admissions:
             "device_phases_p50_us": {k: round(pct([p[k] for p in rec.device_phases if k in p], .5), 1)
                                      for k in sorted({k for p in rec.device_phases for k in p})},
             # every timed step above 1.5 x p50, attributed to the admission phase with the largest excess
-            "tail_attribution": tail_attribution(rec.latency_ms, {
-                "plugin_rpc": rec.rpc_ms, "runtime_prep": rec.prespawn_ms, "exec_and_library_load": rec.exec_ms,
-                "gpu_runtime_init": rec.runtime_ms, "device_setup": rec.setup_ms, "launch_and_verify": rec.launch_ms}),
+            "tail_attribution": tail_attribution(rec.latency_ms, rec.phases()),
+            # the containers' own start-up counters (read syscalls, CPU ms): what a comparison row's
+            # view or runtime changes deterministically, next to its wall-clock time
+            "container_counters_p50": rec.counters(),
         }

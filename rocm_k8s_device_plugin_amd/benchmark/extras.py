@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 import time
 
+from .admission import StepRecords
 from .stats import alloc_summary, fragment, pct
 
 
@@ -22,23 +23,28 @@ class Extras:
         self.rt_key = "rocr_direct_container" if self.other_runtime == "hsa" else "hip_runtime_container"
         self.other_mode = "per-gpu" if args.container_mode == "pod" else "pod"
         self.other_view = "visible-devices" if args.dev_view == "specs" else "specs"
-        self.out = {}
+        self.out = {"comparisons": {}}
 
     def _p50(self, xs, key, q=.5):
         self.out[key] = round(pct(xs, q), 3) if xs else None
 
+    def _row(self, name: str, rec: StepRecords) -> None:
+        """A comparison row in full (p50, p99, phases, tail attribution, container counters)."""
+        self.out["comparisons"][name] = rec.row()
+
     # ------------------------------------------------------------------ comparison admissions
     def container_mode_compare(self):
-        lat = []
+        rec = StepRecords()
         if self.n > 1:
             self.guard.enter("container_mode_compare")
             for _ in range(self.args.mode_compare):
-                self.adm.step(False, sink=lat, mode=self.other_mode)
-        self._p50(lat, f"latency_p50_ms_container_mode_{self.other_mode}")
+                self.adm.step(rec, mode=self.other_mode)
+        self._p50(rec.latency_ms, f"latency_p50_ms_container_mode_{self.other_mode}")
+        self._row(f"container_mode_{self.other_mode}", rec)
 
     def node_view_compare(self):
         a_, d, node = self.args, self.d, self.node
-        lat, init = [], []
+        rec = StepRecords()
         if not a_.fixture and a_.node_view_compare > 0:
             # the plugin returns -node_view mounts (alias = host path: the fake runtime
             # applies mounts by redirection and cannot add the alias mount)
@@ -56,51 +62,55 @@ class Extras:
                     impl.node_view.path()  # built at plugin start-up in a real deployment
             self.guard.enter("node_view_compare")
             for _ in range(a_.node_view_compare):
-                self.adm.step(False, sink=lat, init_sink=init, pl=nvplug)
+                self.adm.step(rec, pl=nvplug)
             if d.rank == 0:
                 if nvplug is not None:
                     nvplug.stop()
                 else:
                     impl.node_view = None
-        self._p50(lat, "latency_p50_ms_node_view_emulated")
-        self._p50(init, "node_view_emulated_runtime_init_p50_ms")
+        self._p50(rec.latency_ms, "latency_p50_ms_node_view_emulated")
+        self._p50(rec.runtime_ms, "node_view_emulated_runtime_init_p50_ms")
+        self._row("node_view_emulated", rec)
 
     def dev_view_compare(self):
-        lat = []
+        rec = StepRecords()
         if not self.args.fixture:
             self.guard.enter("dev_view_compare")
             for _ in range(self.args.visibility_compare):
-                self.adm.step(False, sink=lat, dev_view=self.other_view)
-        self._p50(lat, f"latency_p50_ms_dev_view_{self.other_view}")
+                self.adm.step(rec, dev_view=self.other_view)
+        self._p50(rec.latency_ms, f"latency_p50_ms_dev_view_{self.other_view}")
+        self._row(f"dev_view_{self.other_view}", rec)
 
     def runtime_compare(self):
         """The other container entrypoint, as many admissions as the headline
         (same settle, same view): with the default HIP container, ROCr-direct."""
         a_ = self.args
         steps = a_.steps if a_.runtime_compare < 0 else a_.runtime_compare
-        lat = []
+        rec = StepRecords()
         if not a_.fixture and steps > 0:
             self.guard.enter(f"{self.other_runtime}_runtime_compare")
             for _ in range(steps):
-                self.adm.step(False, runtime=self.other_runtime, sink=lat)
-        self._p50(lat, f"latency_p50_ms_{self.rt_key}")
-        self._p50(lat, f"latency_p99_ms_{self.rt_key}", .99)
-        self.out[f"{self.rt_key}_steps"] = len(lat)
+                self.adm.step(rec, runtime=self.other_runtime)
+        self._p50(rec.latency_ms, f"latency_p50_ms_{self.rt_key}")
+        self._p50(rec.latency_ms, f"latency_p99_ms_{self.rt_key}", .99)
+        self.out[f"{self.rt_key}_steps"] = len(rec.latency_ms)
+        self._row(self.rt_key, rec)
 
     def back_to_back_compare(self):
-        lat = []
+        rec = StepRecords()
         if not self.args.fixture and self.args.settle == "kfd":
             self.guard.enter("back_to_back_compare")
             for _ in range(self.args.b2b_compare):
-                self.adm.step(False, sink=lat, settle="none")
-        self._p50(lat, "latency_p50_ms_back_to_back")
+                self.adm.step(rec, settle="none")
+        self._p50(rec.latency_ms, "latency_p50_ms_back_to_back")
+        self._row("back_to_back", rec)
 
     def fragmented_compare(self):
         """N of every accessible device, from a fragmented availability (a second
         plugin instance; the headline plugin keeps advertising exactly N)."""
         a_, d, n, node = self.args, self.d, self.n, self.node
         frag = None
-        lat, alloc = [], []
+        rec, alloc = StepRecords(), []
         do = d.bcast(d.rank == 0 and node.m_adv == n and a_.fragmented_compare > 0 and len(node.usable) > n)
         if do:
             fplug = None
@@ -110,12 +120,13 @@ class Extras:
                 self.guard.kill_on_fire(fplug)
             self.guard.enter("fragmented_compare")
             for _ in range(a_.fragmented_compare):
-                self.adm.step(False, sink=lat, pl=fplug, alloc_sink=alloc)
+                self.adm.step(rec, pl=fplug, alloc_sink=alloc)
             if d.rank == 0:
                 frag = {"advertised": len(node.usable), "requested": n, "held": fplug.held,
-                        "latency_p50_ms": round(pct(lat, .5), 3), **alloc_summary(fplug, alloc)}
+                        "latency_p50_ms": round(pct(rec.latency_ms, .5), 3), **alloc_summary(fplug, alloc)}
                 fplug.stop()
         self.out["fragmented_n_of_m"] = frag
+        self._row("fragmented_n_of_m", rec)
 
     # ------------------------------------------------------------------ data plane
     def collectives(self):

@@ -821,7 +821,8 @@ class GoServerConfig:
     refuse_calls: int = 0                           # the first N calls get RST_STREAM(REFUSED_STREAM)
     # What other HTTP/2 servers (C++ gRPC, a proxy in front of an exporter) may
     # send and grpc-go never does. RFC 7540 allows all of it; the client must cope.
-    pad: int = 0                                    # > 0: every HEADERS / DATA frame PADDED with this many bytes
+    pad: Optional[int] = None                       # not None: every HEADERS / DATA frame PADDED with this many
+                                                    # bytes (0: the flag and the pad-length byte, no padding)
     priority_in_headers: bool = False               # HEADERS frames carry the PRIORITY flag (5 bytes)
     noise_frames: bool = False                      # a PRIORITY and an unknown-type frame ahead of the response
     rst_code: Optional[int] = None                  # answer every call with RST_STREAM(rst_code)
@@ -931,7 +932,7 @@ class _ServerConn:
         if prio:
             flags |= PRIORITY_FLAG
             payload = struct.pack(">IB", 0, 15) + payload      # no dependency, weight 16
-        if self.cfg.pad:
+        if self.cfg.pad is not None:
             flags |= PADDED
             payload = bytes([self.cfg.pad]) + payload + b"\0" * self.cfg.pad
         return flags, payload
@@ -939,7 +940,8 @@ class _ServerConn:
     def _headers(self, sid: int, fields, end_stream: bool) -> None:
         block = self.enc.encode(fields)
         # padding and priority fields count against the frame size
-        room = self.peer_max_frame - (1 + self.cfg.pad if self.cfg.pad else 0) - (5 if self.cfg.priority_in_headers else 0)
+        room = self.peer_max_frame - (1 + self.cfg.pad if self.cfg.pad is not None else 0) - \
+            (5 if self.cfg.priority_in_headers else 0)
         chunk = self.cfg.continuation_chunk or room
         parts = [block[i:i + chunk] for i in range(0, len(block), chunk)] or [b""]
         out = []
@@ -954,7 +956,7 @@ class _ServerConn:
     def _data(self, sid: int, payload: bytes) -> None:
         """DATA within the client's windows (waits for its WINDOW_UPDATEs)."""
         while payload:
-            extra = 1 + self.cfg.pad if self.cfg.pad else 0     # padding is flow-controlled too
+            extra = 1 + self.cfg.pad if self.cfg.pad is not None else 0     # padding is flow-controlled too
             q = min(self.conn_send_window, self.stream_send.get(sid, self.peer_initial_window),
                     self.peer_max_frame) - extra
             if q <= 0:

@@ -5,7 +5,8 @@ Speaks the same CLI and JSON contract, one-shot and ``--serve``. Behaviour
 per ROCr ordinal comes from the JSON file named by $MI355X_STUB_PROBE_CONTROL
 (re-read on every request), e.g.
 ``{"0": "ok", "3": "fail", "5": "hang", "6": "stale", "7": "garbage"}``
-(missing ordinals are "ok"; "serve": "broken" makes --serve fail to start;
+(missing ordinals are "ok"; "serve": "broken" makes --serve fail to start,
+"serve": "slow_start" delays its hello by "serve_start_s" seconds;
 "server_fail" fails only inside --serve: a stale server runtime).
 Exercises the real LivenessProber code path: process spawn, server protocol,
 deadline kill, fallback to per-device isolation, output parsing, nonce check,
@@ -86,6 +87,8 @@ def serve():
     if ctl.get("serve") == "broken":
         print(json.dumps({"serve": True, "ok": False, "hip_device_count": 0}), flush=True)
         return 2
+    if ctl.get("serve") == "slow_start":   # a runtime start-up that outlasts the caller's patience
+        time.sleep(float(ctl.get("serve_start_s", 30)))
     _kfd_entry()
     t = time.monotonic_ns()
     print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "t_start_ns": t, "t_runtime_ns": t}),

@@ -354,9 +354,10 @@ def test_native_client_too_many_pings_goaway(tmp_path):
     with gp.GoServer(path, {ECHO: _echo}, gp.GoServerConfig(too_many_pings=True)):
         c = _client(path)
         t0 = time.monotonic()
-        status, msg, _ = c.unary(ECHO, b"x", 10.0)
-        assert status == -1 and "ENHANCE_YOUR_CALM" in msg and "too_many_pings" in msg
-        assert time.monotonic() - t0 < 2.0 and not c.connected
+        status, msg, _ = c.unary(ECHO, b"x", 60.0)
+        assert status == -1 and "ENHANCE_YOUR_CALM" in msg and "too_many_pings" in msg, msg
+        # the GOAWAY ends the call: far sooner than its deadline, however loaded the machine
+        assert time.monotonic() - t0 < 30.0 and not c.connected
 
 
 def test_native_client_refused_stream_keeps_the_connection(tmp_path):
@@ -386,12 +387,13 @@ def test_native_client_http_status_mapping(tmp_path, http, status):
 
 
 @pytest.mark.parametrize("cfg", [
+    gp.GoServerConfig(pad=0),
     gp.GoServerConfig(pad=7),
     gp.GoServerConfig(pad=255),
     gp.GoServerConfig(priority_in_headers=True),
     gp.GoServerConfig(pad=3, priority_in_headers=True, continuation_chunk=4),
     gp.GoServerConfig(noise_frames=True),
-], ids=["pad7", "pad255", "priority", "pad+priority+continuation", "priority-and-unknown-frames"])
+], ids=["pad0", "pad7", "pad255", "priority", "pad+priority+continuation", "priority-and-unknown-frames"])
 def test_native_client_accepts_what_other_http2_servers_send(tmp_path, cfg):
     """Padding, HEADERS priority fields, PRIORITY and unknown extension frames
     are legal HTTP/2 (RFC 7540 6.1, 6.2, 6.3, 4.1) that grpc-go never sends: the
@@ -438,9 +440,10 @@ def test_native_client_protocol_violations_end_the_call_cleanly(tmp_path, cfg, t
     with gp.GoServer(path, {ECHO: _echo}, cfg):
         c = _client(path)
         t0 = time.monotonic()
-        status, msg, _ = c.unary(ECHO, b"x", 5.0)
+        status, msg, _ = c.unary(ECHO, b"x", 60.0)
         assert status == -1 and text in msg, msg
-        assert time.monotonic() - t0 < 2.0 and not c.connected
+        # at once, not at the deadline (bounded loosely: a loaded CI host)
+        assert time.monotonic() - t0 < 30.0 and not c.connected
 
 
 def test_native_client_unknown_method_and_grpc_error(tmp_path):
@@ -462,15 +465,15 @@ def test_native_client_deadline_and_abort_against_a_silent_server(tmp_path):
         t0 = time.monotonic()
         status, msg, _ = c.unary(ECHO, b"x", 0.3)
         dt = time.monotonic() - t0
-        assert status == -1 and "deadline" in msg and 0.25 < dt < 1.5
+        assert status == -1 and "deadline" in msg and 0.25 < dt < 10.0
         r, w = os.pipe()
         try:
             c = _client(path)
             c.set_abort_fd(r)
             threading.Timer(0.2, lambda: os.write(w, b"x")).start()
             t0 = time.monotonic()
-            status, msg, _ = c.unary(ECHO, b"x", 30.0)
-            assert status == -1 and msg == "interrupted" and time.monotonic() - t0 < 2.0
+            status, msg, _ = c.unary(ECHO, b"x", 120.0)
+            assert status == -1 and msg == "interrupted" and time.monotonic() - t0 < 60.0
         finally:
             os.close(r)
             os.close(w)
@@ -499,7 +502,8 @@ def test_native_client_survives_signals_during_a_call(tmp_path):
             finally:
                 stop.set()
                 t.join()
-            assert status == -1 and "deadline" in msg and time.monotonic() - t0 < 2.0
+            # EINTR every 20 ms must not restart the 0.5 s deadline (which would never end)
+            assert status == -1 and "deadline" in msg and time.monotonic() - t0 < 15.0
     finally:
         signal.signal(signal.SIGUSR1, old)
 

@@ -127,7 +127,7 @@ def test_flags_follow_go_syntax(tmp_path):
     assert p.returncode == 1 and "node name" in p.stderr
 
 
-def _wait(pred, timeout=5.0):
+def _wait(pred, timeout=30.0):
     end = time.monotonic() + timeout
     while time.monotonic() < end:
         if pred():
@@ -180,13 +180,13 @@ def test_resync_zero_is_the_reference_controller(tmp_path):
         srv.add_node("node-n")
         p, _ = _start(fi, srv, tmp_path, "-resync", "0")
         assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.mode") == "container", 10), p.stderr
-        assert _wait(lambda: srv.watch_starts >= 1, 5)
+        assert _wait(lambda: srv.watch_starts >= 1, 30.0)
         srv.set_labels("node-n", {"other": "x"})            # an edit strips them: not re-asserted
         time.sleep(1.5)
         assert "amd.com/gpu.mode" not in srv.labels("node-n") and p.poll() is None
         srv.delete_node("node-n")
         srv.add_node("node-n")                              # the node object is re-created: relabelled
-        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.mode") == "container", 10)
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.mode") == "container", 30.0)
         rc, err = _stop(p)
         assert rc == 0, err
     finally:
@@ -204,13 +204,14 @@ def test_watch_restores_stripped_labels_and_survives_expiry(tmp_path):
         assert _wait(lambda: srv.watch_starts >= 1)
         t0 = time.monotonic()
         srv.set_labels("node-n", {"other": "x"})               # someone strips ours
-        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 2.0)
-        assert time.monotonic() - t0 < 1.5 and srv.labels("node-n")["other"] == "x"
+        # from the watch event, not the 300 s resync (bounded loosely: a loaded CI host)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 60.0)
+        assert time.monotonic() - t0 < 60.0 and srv.labels("node-n")["other"] == "x"
         srv.expire_watches()                                     # server ends the stream: reconnect
-        assert _wait(lambda: srv.watch_starts >= 2, 3.0)
+        assert _wait(lambda: srv.watch_starts >= 2, 30.0)
         srv.delete_node("node-n")
         srv.add_node("node-n")                                   # re-created node
-        assert _wait(lambda: "amd.com/gpu.cu-count" in srv.labels("node-n"), 2.0)
+        assert _wait(lambda: "amd.com/gpu.cu-count" in srv.labels("node-n"), 30.0)
         # no reconnect spin when the server cuts every watch at once
         srv.watch_max_s = 0.0
         srv.expire_watches()
@@ -244,14 +245,14 @@ def test_watch_from_a_compacted_resource_version_relists(tmp_path):
         gets0, starts = gets(), srv.watch_starts
         srv.min_rv = 10 ** 6
         srv.expire_watches()                       # reconnects from its last resourceVersion: 410
-        assert _wait(lambda: srv.watch_starts >= starts + 2, 5.0)
+        assert _wait(lambda: srv.watch_starts >= starts + 2, 30.0)
         srv.min_rv = 0
         watches = [path for m, path, _ in list(srv.requests) if m == "WATCH"][starts:]
         assert "resourceVersion=" in watches[0]    # the resumed watch
         assert _wait(lambda: gets() > gets0, 3.0)  # the re-list
         assert any("resourceVersion=" not in w for w in watches[1:]), watches
         srv.set_labels("node-n", {"other": "x"})   # the fresh watch still restores stripped labels
-        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 3.0)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 30.0)
         rc, err = _stop(p)
         assert rc == 0, err
     finally:
@@ -288,7 +289,7 @@ def test_rotated_token_is_picked_up(tmp_path):
         tok.write_text("tok-2\n")
         os.utime(tok, ns=(time.time_ns(), time.time_ns() + 10**9))
         srv.set_labels("node-n", {})
-        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 3.0)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 30.0)
         rc, err = _stop(p)
         assert rc == 0 and "HTTP 401" not in err
     finally:
@@ -309,7 +310,7 @@ def test_topology_change_relabels(tmp_path):
         drv = fi.sysfs / "module/amdgpu/drivers/pci:amdgpu"
         for b in sorted(x for x in os.listdir(drv) if ":" in x):
             (drv / b / "current_memory_partition").write_text("NPS2\n")
-        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.compute-memory-partition") == "spx_nps2", 3.0)
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.compute-memory-partition") == "spx_nps2", 30.0)
         rc, err = _stop(p)
         assert rc == 0 and "topology_changes=1" in err
     finally:
@@ -406,7 +407,7 @@ def test_malformed_watch_events_are_survived(tmp_path):
         time.sleep(0.5)
         assert p.poll() is None
         srv.set_labels("node-n", {})
-        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 5.0)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 30.0)
         rc, err = _stop(p)
         assert rc == 0, err
     finally:
@@ -428,31 +429,39 @@ def test_no_leaks_under_connection_churn(tmp_path):
         srv.add_node("node-n")
         p, _ = _start(fi, srv, tmp_path, "-resync", "0.1", "-topology_watch", "0.1", "-ca_file", ca,
                       "-watch_backoff_max", "0.1")
-        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 10.0)
+        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 30.0)
 
         def sample():
-            with open(f"/proc/{p.pid}/status") as f:
-                rss = next(int(x.split()[1]) for x in f if x.startswith("VmRSS"))
-            return len(os.listdir(f"/proc/{p.pid}/fd")), rss
+            """(fds, RSS KiB), each the least of a few readings once the labels are back:
+            a connection in flight at one reading is not a leak, a leaked one stays"""
+            _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 30.0)
+            rows = []
+            for _ in range(5):
+                with open(f"/proc/{p.pid}/status") as f:
+                    rss = next(int(x.split()[1]) for x in f if x.startswith("VmRSS"))
+                rows.append((len(os.listdir(f"/proc/{p.pid}/fd")), rss))
+                time.sleep(0.05)
+            return min(r[0] for r in rows), min(r[1] for r in rows)
 
-        def churn(seconds):
-            end = time.monotonic() + seconds
-            while time.monotonic() < end:
+        def churn(requests, cap_s=120.0):
+            """Strip the labels and cut the watch until the labeller has made `requests`
+            more API requests: a fixed amount of reconnecting, however loaded the machine"""
+            target = len(srv.requests) + requests
+            end = time.monotonic() + cap_s
+            while len(srv.requests) < target:
+                assert time.monotonic() < end, f"{len(srv.requests)} of {target} requests after {cap_s} s"
                 srv.set_labels("node-n", {})
                 time.sleep(0.1)
                 srv.expire_watches()
                 time.sleep(0.1)
 
-        churn(2.0)
+        churn(40)
         fds0, rss0 = sample()
-        n0 = len(srv.requests)
-        churn(4.0)
+        churn(150)
         fds1, rss1 = sample()
-        assert len(srv.requests) - n0 > 40            # the churn really reconnected
         assert fds1 <= fds0 + 1, (fds0, fds1)
         if "MI355X_NATIVE_LABELLER_EXE" not in os.environ:   # ASan's quarantine holds freed memory by design
             assert rss1 - rss0 < 2048, (rss0, rss1)           # KiB
-        assert _wait(lambda: "amd.com/gpu.vram" in srv.labels("node-n"), 3.0)
         rc, err = _stop(p)
         assert rc == 0, err[-2000:]
     finally:

@@ -218,3 +218,40 @@ def test_daemon_shutdown_during_a_throughput_check_changes_no_verdict(tmp_path):
         return dev
 
     asyncio.run(asyncio.wait_for(go(), 60))
+
+
+def test_daemon_shutdown_while_the_probe_server_starts_spawns_no_fallback(tmp_path):
+    """SIGTERM while the probe server is still starting (its hello not yet read):
+    that sweep is interrupted, not a failed server start, so the daemon does not
+    fall back to one fresh GPU process per device on its way out."""
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text(json.dumps({"serve": "slow_start", "serve_start_s": 60}))
+    log = tmp_path / "starts.log"
+    kdir = str(tmp_path / "dp")
+
+    async def go():
+        k = FakeKubelet(kdir)
+        await k.start()
+        p = subprocess.Popen([EXE, "-kubelet_dir", kdir, "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                              "-exporter_socket", "", "-pulse", "1", "-liveness", "-liveness_probe", STUB,
+                              "-liveness_timeout", "30"],
+                             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                             env=dict(os.environ, MI355X_STUB_PROBE_CONTROL=str(ctl), MI355X_STUB_PROBE_LOG=str(log)))
+        try:
+            # the first sweep (before registration) starts the server and waits for its hello
+            for _ in range(400):
+                if log.exists() and log.read_text().startswith("serve"):
+                    break
+                await asyncio.sleep(0.05)
+            await asyncio.sleep(0.3)
+        finally:
+            rc, err = await asyncio.to_thread(_stop, p)
+            await k.stop()
+        assert rc == 0, err[-3000:]
+        starts = log.read_text().split()
+        assert starts and all(s.startswith("serve") for s in starts), (starts, err[-3000:])
+        assert "re-probing each device in its own process" not in err, err[-3000:]
+        assert "-> Unhealthy" not in err, err[-3000:]
+
+    asyncio.run(asyncio.wait_for(go(), 60))

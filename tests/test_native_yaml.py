@@ -55,6 +55,9 @@ def test_native_reader_equals_pyyaml(doc, flow, style, width, unicode):
     "a: |+\n  keep\n\n\nb: >\n  folded\n  line\n\n  para\nc: |-\n  strip\n# comment\nd:\n- - x\n  - y\n- z\n",
     # quoted scalars with escapes, and a multi-line plain scalar
     "e: \"tab\\tnl\\n\\u00e9 \\\"q\\\"\"\nf: 'it''s'\ng: plain scalar\n  continued here\n",
+    # comment lines indented deeper than the scalar above them end it
+    "gpu:\n  device_count: 2\n    # two GPUs\n", "- x\n    # note\n", "a: b\n  c\n    # z\n",
+    "a: [1,\n  # c\n  2]\n", "a: \"b\n  # c\n  d\"\n", "gpu:\n  device_count: 2  # two\n      # GPUs\nx: y\n",
 ])
 def test_hand_written_documents(text):
     assert native(text) == _stringify(yaml.safe_load(text))
@@ -74,7 +77,9 @@ def _stringify(v):
 @pytest.mark.parametrize("text", ["a: [b, c\n", "a: 'open\n", "a:\n  - b\n c: d\n", "- a\nb: c\n", "{\"a\": 1",
                                   "a: \"x\\q\"\n", "a: !custom x\n", "a: |\n    x\n  y\n",
                                   # a mapping indicator inside a plain scalar (an indentation mistake)
-                                  "a: b\n  c: d\n", "a: b c: d\n", "a: v:\n", "- b\n  c: d\n"])
+                                  "a: b\n  c: d\n", "a: b c: d\n", "a: v:\n", "- b\n  c: d\n",
+                                  # a plain scalar cannot go on past a comment line
+                                  "a: b\n  # c\n  d\n"])
 def test_malformed_documents_are_refused(text):
     """Documents PyYAML refuses are refused here too, with an error."""
     with pytest.raises(yaml.YAMLError):

@@ -208,9 +208,11 @@ def _replay(build: Path, t: str, name: str, work: Path, dirs, env: Dict[str, str
     return p.returncode, int(m.group(1)) if m else 0, sorted(f"{name}/{x.name}" for x in art.iterdir()), p.stderr
 
 
-def run_target(t: str, seconds: float, work: Path, seeds: Path, env: Dict[str, str]) -> dict:
+def run_target(t: str, seconds: float, work: Path, seeds: Path, env: Dict[str, str], runs: int = 0) -> dict:
     """Fuzz `t` for `seconds` (coverage + ASan), then replay everything it kept
-    under ASan + UBSan, and for the threaded targets under TSan."""
+    under ASan + UBSan, and for the threaded targets under TSan. ``runs`` > 0:
+    stop after that many executions instead, with `seconds` only as a cap (a
+    fixed amount of work however loaded the machine is)."""
     corpus = work / "corpus" / t
     art = work / "artifacts" / t
     corpus.mkdir(parents=True, exist_ok=True)
@@ -226,7 +228,7 @@ def run_target(t: str, seconds: float, work: Path, seeds: Path, env: Dict[str, s
             e["MI355X_FUZZ_SYSFS_MUT"] = str(mut)
         argv = [str(BUILD / f"fuzz_{t}"), f"-max_total_time={int(max(1, seconds))}", "-timeout=25",
                 "-rss_limit_mb=4096", "-print_final_stats=1", "-max_len=65536", f"-artifact_prefix={art}/",
-                str(corpus), str(seeds)]
+                str(corpus), str(seeds)] + ([f"-runs={runs}"] if runs > 0 else [])
         t0 = time.monotonic()
         p = subprocess.run(argv, env=e, capture_output=True, text=True, errors="replace", timeout=seconds + 300)
         wall = time.monotonic() - t0
