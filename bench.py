@@ -102,6 +102,10 @@ def make_parser():
                     help="> 0: run the plugin as the health DaemonSet does (MFMA liveness via the kept-queue probe "
                          "server, amd-smi ECC / events / xGMI link state) with this pulse in seconds, while pods "
                          "are admitted (BASELINE config: health-check DaemonSet enabled)")
+    ap.add_argument("--health-liveness-mode", default="persistent", choices=["persistent", "spawn"],
+                    help="with --health-pulse on the native daemon: -liveness_mode (one kept-queue probe server, or "
+                         "a fresh probe process per device per sweep); extra.health_loop reports the host memory "
+                         "of the daemon and its probe processes over the run")
     ap.add_argument("--advertise", type=int, default=0,
                     help="advertise M devices and request --gpus N of them per pod (default M = N: the headline, "
                          "'GPUs advertised at N'). With M > N the timed admissions start from a fragmented "

@@ -46,7 +46,8 @@ class BenchNode:
         self.health_flags = ()
         if hp > 0 and self.plugin_kind == "native-daemon":
             self.health_flags = ("-pulse", str(max(1, int(round(hp)))),
-                                 *(() if args.fixture else ("-liveness", "-smi_ecc", "-smi_events", "-smi_xgmi")))
+                                 *(() if args.fixture else ("-liveness", "-liveness_mode", args.health_liveness_mode,
+                                                            "-smi_ecc", "-smi_events", "-smi_xgmi")))
         grpc_native = self.plugin_kind == "native-daemon" or args.grpc_server == "native"
         self.kclient = args.kubelet_client or ("native" if grpc_native else "aio")
         if self.kclient == "native" and not grpc_native:

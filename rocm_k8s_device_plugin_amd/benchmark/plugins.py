@@ -33,6 +33,69 @@ class _DaemonAllocator:
         return self._pol.reference_allocate(*a)
 
 
+def _rss_kb(pid: int) -> int:
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for line in f:
+                if line.startswith("VmRSS:"):
+                    return int(line.split()[1])
+    except OSError:
+        pass
+    return 0
+
+
+def _descendants(root: int) -> list:
+    """PIDs below `root` (its probe server, spawned probes and their children)."""
+    kids = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                ppid = int(f.read().rsplit(")", 1)[1].split()[1])
+        except (OSError, ValueError, IndexError):
+            continue
+        kids.setdefault(ppid, []).append(int(d))
+    out, todo = [], [root]
+    while todo:
+        for c in kids.get(todo.pop(), []):
+            out.append(c)
+            todo.append(c)
+    return out
+
+
+class RssSampler:
+    """Host memory of a daemon and every process below it, sampled every
+    `period_s` on a thread: what a DaemonSet's memory request has to cover
+    (the persistent probe server; in spawn mode, the probe processes of a sweep)."""
+
+    def __init__(self, pid: int, period_s: float = 0.1):
+        self.pid, self.period_s = pid, period_s
+        self.rows = []      # (daemon KiB, descendants KiB, descendant count)
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _run(self):
+        while not self._stop.wait(self.period_s):
+            kids = _descendants(self.pid)
+            self.rows.append((_rss_kb(self.pid), sum(_rss_kb(k) for k in kids), len(kids)))
+
+    def stop(self) -> dict:
+        self._stop.set()
+        self._t.join(timeout=5)
+        if not self.rows:
+            return {}
+        from .stats import pct
+        tot = [a + b for a, b, _ in self.rows]
+        return {"samples": len(self.rows), "period_s": self.period_s,
+                "daemon_rss_mb_p50": round(pct([a for a, _, _ in self.rows], .5) / 1024, 1),
+                "children_rss_mb_p50": round(pct([b for _, b, _ in self.rows], .5) / 1024, 1),
+                "children_rss_mb_max": round(max(b for _, b, _ in self.rows) / 1024, 1),
+                "total_rss_mb_p50": round(pct(tot, .5) / 1024, 1), "total_rss_mb_max": round(max(tot) / 1024, 1),
+                "children_max": max(c for _, _, c in self.rows)}
+
+
 class NativePluginUnderTest:
     """Rank 0: the native daemon mi355x-device-plugin (the primary entrypoint)
     advertising `devs` (-device_ids) behind a fake kubelet on its own UDS dir.
@@ -65,6 +128,8 @@ class NativePluginUnderTest:
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
         self._reader = threading.Thread(target=self._read, daemon=True)
         self._reader.start()
+        # the health DaemonSet configuration: its host memory over the whole run
+        self.rss = RssSampler(self.proc.pid) if metrics_port else None
         admit = self.kubelet.admit
 
         async def counted_admit(*a, **kw):
@@ -146,7 +211,8 @@ class NativePluginUnderTest:
         st = self.kubelet.resources.get("amd.com/gpu")
         # the mean includes the start-up sweep (probe server and amd-smi start); the p50 is the
         # upper bound of the histogram bucket that holds the median sweep
-        return {"plugin": "native-daemon", "pulse_s": pulse_s, "sweeps": n,
+        rss = self.rss.stop() if self.rss else {}
+        return {"plugin": "native-daemon", "pulse_s": pulse_s, "sweeps": n, "host_memory": rss,
                 "sweep_ms_mean": round(m.get("mi355x_dp_health_sweep_seconds_sum", 0.0) * 1e3 / n, 3) if n else None,
                 "sweep_ms_p50_at_most": _bucket_quantile_ms(m, "mi355x_dp_health_sweep_seconds", .5),
                 "health_changes": int(m.get("mi355x_dp_health_changes_total", 0)),

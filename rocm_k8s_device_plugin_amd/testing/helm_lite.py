@@ -236,6 +236,7 @@ class Renderer:
             "not": lambda a: not _truthy(a),
             "eq": lambda a, *b: any(a == x for x in b),
             "ne": lambda a, b: a != b,
+            "mul": lambda *a: __import__("math").prod(int(x) for x in a),
             "quote": lambda *a: " ".join('"' + _fmt(x).replace('"', '\\"') + '"' for x in a),
             "toYaml": _to_yaml,
             "nindent": lambda n, s: "\n" + _indent(n, s),

@@ -55,3 +55,35 @@ def test_errors():
         render("{{ nosuchfunc 1 }}")
     with pytest.raises(TemplateError):
         render("{{ if .Values.a }}unterminated")
+
+
+def test_chart_health_defaults_follow_the_measured_choice():
+    """dp.liveness on: the probe server mode and the memory request come from
+    profiles/r5/health_mode_choice.json (persistent; ~370Mi per GPU x 8); an
+    explicit dp.resources wins; the raw health manifest says the same."""
+    import json
+    import os
+
+    import yaml
+
+    from rocm_k8s_device_plugin_amd.testing.helm_lite import rendered_objects
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    chart = os.path.join(repo, "helm", "amd-gpu")
+
+    def dp(values):
+        ds = [o for o in rendered_objects(chart, values)
+              if o.get("kind") == "DaemonSet" and "labeller" not in o["metadata"]["name"]]
+        return ds[0]["spec"]["template"]["spec"]["containers"][0]
+
+    c = dp({"dp": {"liveness": {"enabled": True}}})
+    assert "-liveness_mode=persistent" in c["args"] and c["resources"] == {"requests": {"memory": "2960Mi"}}
+    assert dp({"dp": {"liveness": {"enabled": True, "mode": "spawn"}}})["args"].count("-liveness_mode=spawn") == 1
+    assert dp({"dp": {"liveness": {"enabled": True}, "resources": {"limits": {"memory": "4Gi"}}}})["resources"] == \
+        {"limits": {"memory": "4Gi"}}
+    assert dp({})["resources"] == {}                                  # no liveness: no request (as upstream)
+    choice = json.load(open(os.path.join(repo, "profiles", "r5", "health_mode_choice.json")))
+    per_gpu = max(r["host_memory"]["total_rss_mb_max"] for r in choice["admissions_under_the_loop"].values())
+    assert per_gpu <= 370 and 8 * per_gpu * 1e6 <= 3 * 2 ** 30           # what the requests cover
+    with open(os.path.join(repo, "k8s-ds-amdgpu-dp-health.yaml")) as f:
+        man = yaml.safe_load(f)["spec"]["template"]["spec"]["containers"][0]
+    assert "-liveness_mode=persistent" in man["args"] and man["resources"]["requests"]["memory"] == "3Gi"

@@ -11,6 +11,7 @@ the same GPU every --pulse seconds in one of these modes:
               per pulse, each of which preempts every queue on the GPU)
   keep        persistent probe server with --keep: the queue lives across
               sweeps, a sweep is one AQL packet
+  spawn       a fresh probe process per sweep (-liveness_mode=spawn)
 
 Reports, per mode, the tenant's GEMM time distribution (p50/p99/p99.9/max),
 GEMMs slower than 1.5x the median ("stalls"), throughput, and the sweep
@@ -123,6 +124,10 @@ async def run_mode(mode: str, a) -> dict:
                                 ordinal_map={dev: ords[dev]})
         await monitor.check_once()
         prober = monitor.prober
+    elif mode == "spawn":
+        # -liveness_mode=spawn: a fresh probe process per device per sweep (ROCr start-up,
+        # two queues and the kfd process teardown every pulse; nothing held between pulses)
+        prober = LivenessProber(timeout_s=a.probe_timeout, mode="spawn")
     elif mode != "none":
         prober = LivenessProber(timeout_s=a.probe_timeout, mode="persistent", keep_queues=(mode == "keep"))
         res = await prober.probe({"gpu0": 0})          # server up before the tenant starts timing
