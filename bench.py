@@ -119,10 +119,8 @@ def make_parser():
                          "reported in extra.fragmented_n_of_m (BASELINE config: full-node hive-aware allocation)")
     ap.add_argument("--plugin", default="native", choices=["native", "python"],
                     help="the device plugin under test: native = the mi355x-device-plugin daemon (the primary "
-                         "entrypoint, what ./k8s-device-plugin runs); python = the Python CLI's plugin in this "
-                         "process (--grpc-server picks its transport; used automatically with --health-pulse)")
-    ap.add_argument("--grpc-server", default="native", choices=["native", "aio"],
-                    help="with --plugin python: the plugin's kubelet-facing gRPC server (-grpc_server)")
+                         "entrypoint, what ./k8s-device-plugin runs); python = the Python oracle plugin in this "
+                         "process, on the same C++ gRPC server")
     ap.add_argument("--kubelet-client", default="", choices=["", "native", "native-thread", "aio"],
                     help="the fake kubelet's admission RPC client: native (a native HTTP/2 client, like kubelet's "
                          "grpc-go) or aio (grpc.aio in the bench's event loop); default native with the native server")
@@ -251,11 +249,11 @@ def main():
         guard.tmp = node.tmp
         core = dict(adm.timed_report(), **{
             "plugin": node.plugin_kind,
-            "grpc_server": "native" if node.plugin_kind == "native-daemon" else args.grpc_server,
+            "grpc_server": "native",
             "kubelet_client": node.kclient,
             # breakdown of plugin_rpc (kubelet's GetPreferredAllocation + Allocate round trips): the
-            # plugin's own time per RPC, measured inside the native server (empty with -grpc_server aio;
-            # the daemon's from its per-RPC log records)
+            # plugin's own time per RPC, measured inside the native server (the daemon's from its
+            # per-RPC log records)
             "plugin_server_p50_us": {rpc: round(pct(v, .5) * 1e3, 1) for rpc, v in sorted(server_ms.items())
                                      if rpc in ("GetPreferredAllocation", "Allocate")},
             # the node under test must look like a kubelet node: no GPU context in the bench /

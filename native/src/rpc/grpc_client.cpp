@@ -216,7 +216,9 @@ Reply GrpcClient::unary(const std::string& path, const std::string& request, dou
       }
       *err = "write failed";
       // the server may have closed right after a GOAWAY that says why (e.g.
-      // ENHANCE_YOUR_CALM for too many pings): read what it sent and name it
+      // ENHANCE_YOUR_CALM for too many pings): read what it sent and name it.
+      // The GOAWAY may also have been processed already, in the same read as
+      // the frames whose answer (a SETTINGS ack) this write carried.
       char buf[65536];
       ssize_t r;
       while ((r = ::read(fd_, buf, sizeof(buf))) > 0) in_.append(buf, static_cast<size_t>(r));
@@ -228,11 +230,12 @@ Reply GrpcClient::unary(const std::string& path, const std::string& request, dou
           st.going_away = true;
           st.goaway_code = be32(f + 13);
           st.goaway_debug.assign(reinterpret_cast<const char*>(f + 17), std::min<size_t>(len - 8, 256));
-          *err = "connection closed after GOAWAY " + std::string(h2_error_name(st.goaway_code)) +
-                 (st.goaway_debug.empty() ? "" : " (" + st.goaway_debug + ")");
         }
         o += 9 + len;
       }
+      if (st.going_away)
+        *err = "connection closed after GOAWAY " + std::string(h2_error_name(st.goaway_code)) +
+               (st.goaway_debug.empty() ? "" : " (" + st.goaway_debug + ")");
       return false;
     }
     pending_out.clear();

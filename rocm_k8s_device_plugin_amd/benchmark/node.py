@@ -48,10 +48,8 @@ class BenchNode:
             self.health_flags = ("-pulse", str(max(1, int(round(hp)))),
                                  *(() if args.fixture else ("-liveness", "-liveness_mode", args.health_liveness_mode,
                                                             "-smi_ecc", "-smi_events", "-smi_xgmi")))
-        grpc_native = self.plugin_kind == "native-daemon" or args.grpc_server == "native"
-        self.kclient = args.kubelet_client or ("native" if grpc_native else "aio")
-        if self.kclient == "native" and not grpc_native:
-            self.kclient = "native-thread"   # a blocking call on the loop that serves grpc.aio would deadlock
+        # the daemon and the oracle plugin serve on the same C++ server, off the bench's event loop
+        self.kclient = args.kubelet_client or "native"
 
     def make_plugin(self, name, devs, extra=()):
         """A plugin instance advertising `devs` behind its own fake kubelet;
@@ -64,7 +62,7 @@ class BenchNode:
                                          metrics_port=free_port() if main and self.health_flags else 0)
         return PluginUnderTest(self.loop, self.tmp, name, self.sysfs, devs, self.full, self.ords,
                                self.hcfg if main else self.idle_hcfg, self.health_pulse if main else 0.0,
-                               grpc_server=self.args.grpc_server, kubelet_client=self.kclient)
+                               kubelet_client=self.kclient)
 
     def gpu_info(self) -> dict:
         adv = self.adv

@@ -254,8 +254,7 @@ class PluginUnderTest:
     """Rank 0: the Python CLI's plugin advertising `devs` (real discovery data,
     real allocator and gRPC servicer) behind a fake kubelet on its own UDS dir."""
 
-    def __init__(self, loop, tmp, name, sysfs, devs, full, ords, hcfg, pulse_s, grpc_server="native",
-                 kubelet_client="native"):
+    def __init__(self, loop, tmp, name, sysfs, devs, full, ords, hcfg, pulse_s, kubelet_client="native"):
         from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
         from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
         from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
@@ -268,8 +267,7 @@ class PluginUnderTest:
         pdir = os.path.join(tmp, name)
         self.kubelet = FakeKubelet(pdir, rpc_client=kubelet_client)
         loop.run_until_complete(self.kubelet.start())
-        self.mgr = PluginManager(self.impl, ManagerConfig(pulse_s=pulse_s, plugin_dir=pdir, handle_signals=False,
-                                                          grpc_server=grpc_server))
+        self.mgr = PluginManager(self.impl, ManagerConfig(pulse_s=pulse_s, plugin_dir=pdir, handle_signals=False))
         self.task = loop.create_task(self.mgr.run())
         loop.run_until_complete(self.kubelet.wait_for_resource("amd.com/gpu", len(self.devs), timeout=30))
         self.minor_to_ord = {dv.render_minor: ords[dv.id] for dv in self.devs}

@@ -1,4 +1,9 @@
-"""``k8s-device-plugin`` entry point.
+"""The Python oracle plugin's command line (``python -m
+rocm_k8s_device_plugin_amd.cli.device_plugin``).
+
+Not a product: ``k8s-device-plugin`` is the native daemon everywhere (the
+images, ``scripts/``, the installed console script). This CLI drives the
+Python model the daemon is checked against, with the daemon's flag names.
 
 Reference: cmd/k8s-device-plugin/main.go:34-120. Same flag names and
 semantics (``-pulse``, ``-driver_type``, ``-resource_naming_strategy`` plus
@@ -89,11 +94,6 @@ def build_parser() -> flags.GoFlagParser:
     p.add_bool("allocator_extended_search", False, "force the extended search: every split of a request over "
                                                    "interchangeable devices (several partial GPUs), ties broken by "
                                                    "fewer GPUs, then kfd link weight/bandwidth")
-    p.add_str("grpc_server", "native", "kubelet-facing gRPC server: native (C++ HTTP/2; admission RPCs answered "
-                                       "without Python) or aio (Python grpc.aio)")
-    p.add_float("grpc_watchdog", 10.0, "native server watchdog: no ListAndWatch stream this many seconds after "
-                                       "Register, or an HTTP/2 protocol error on the plugin socket, re-serves the "
-                                       "resource with grpc.aio and registers again (0 = off)")
     p.add_bool("dry_run", False, "print what this node would advertise (implementation, resources, devices, "
                                  "health after one sweep, preferred allocations per size) as JSON and exit")
     p.add_float("topology_watch", 5.0, "seconds between checks for a GPU topology change (kfd generation, "
@@ -140,12 +140,8 @@ def validate(ns) -> Optional[str]:
         return f"invalid perf_action provided: {ns.perf_action}, supported values are report or unhealthy"
     if ns.perf_check_every > 0 and not ns.liveness:
         return "perf_check_every needs -liveness (the throughput check runs in the probe server)"
-    if ns.grpc_server not in ("native", "aio"):
-        return f"invalid grpc_server provided: {ns.grpc_server}, supported values are native or aio"
     if ns.allocator_search not in ("auto", "reference", "extended"):
         return f"invalid allocator_search provided: {ns.allocator_search}, supported values are auto, reference, extended"
-    if ns.grpc_watchdog < 0:
-        return "grpc_watchdog must be >= 0"
     return None
 
 
@@ -287,9 +283,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         print(json.dumps(asyncio.run(dry_run_report(impl, sweep=ns.pulse > 0)), indent=1))
         return 0
     mc = ManagerConfig(pulse_s=float(ns.pulse), plugin_dir=ns.kubelet_dir, send_every_pulse=ns.send_every_pulse,
-                       metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch, grpc_server=ns.grpc_server,
-                       allocator_extended_search="extended" if ns.allocator_extended_search else ns.allocator_search,
-                       grpc_watchdog_s=ns.grpc_watchdog)
+                       metrics_port=ns.metrics_port, topology_watch_s=ns.topology_watch,
+                       allocator_extended_search="extended" if ns.allocator_extended_search else ns.allocator_search)
     from ..utils.trace import TRACER
     TRACER.configure(ns.trace_file or None)
     try:

@@ -1,6 +1,10 @@
-"""Device-plugin lifecycle manager.
+"""Device-plugin lifecycle manager of the Python oracle plugin.
 
-Reference: internal/pkg/manager/manager.go:31-104 (lister, heartbeat) and the
+The product is the native daemon (native/src/daemon: ``./k8s-device-plugin``
+in the images); this manager is the independent Python model its behaviour
+is checked against (equality tests) and the bench's ``--plugin python``. It
+serves through the same C++ HTTP/2 server (plugin/native_server.py) and has no
+second transport. Reference: internal/pkg/manager/manager.go:31-104 (lister, heartbeat) and the
 vendored kubevirt device-plugin-manager (vendor/github.com/kubevirt/
 device-plugin-manager/pkg/dpm/{manager,plugin}.go). Same externally visible
 behaviour:
@@ -40,7 +44,6 @@ from ..utils.broadcast import Broadcast
 from ..utils.metrics import REGISTRY, serve_metrics
 from .base import DeviceImpl, PluginContext, new_context
 from .native_server import NativePluginServer
-from .servicer import DevicePluginServicer
 
 _log = log.get("manager")
 
@@ -59,16 +62,9 @@ class ManagerConfig:
     metrics_port: int = 0
     handle_signals: bool = True
     topology_watch_s: float = 5.0   # re-discovery check period (partition switches); 0 = off
-    # kubelet-facing gRPC server: "native" (C++ HTTP/2, plugin/native_server.py)
-    # or "aio" (Python grpc.aio, plugin/servicer.py)
-    grpc_server: str = "native"
     # GetPreferredAllocation search: "auto" (extended on partitioned nodes),
     # "reference" (the reference's candidate family), "extended" / True (allocator.py)
     allocator_extended_search: object = "auto"
-    # native transport watchdog: after Register is acknowledged, no ListAndWatch
-    # stream within this many seconds, or any HTTP/2 protocol error on the
-    # plugin socket, moves the resource to grpc.aio and registers again. 0 = off
-    grpc_watchdog_s: float = 10.0
 
 
 class ResourcePlugin:
@@ -80,17 +76,11 @@ class ResourcePlugin:
         self.socket = os.path.join(cfg.plugin_dir, f"{cfg.namespace}_{name}")
         self.ctx: PluginContext = new_context(name, extended_search=cfg.allocator_extended_search)
         self.stop_bc = Broadcast()
-        self.servicer: Optional[DevicePluginServicer] = None
-        self.server: Optional[grpc.aio.Server] = None
         self.native: Optional[NativePluginServer] = None
         self.running = False
         self.started = False
         self.registrations = 0
         self._lock = asyncio.Lock()
-        # set by the watchdog: the native transport failed with this kubelet;
-        # the resource is served by grpc.aio for the rest of the process
-        self.native_failed: Optional[str] = None
-        self._watchdog: Optional[asyncio.Task] = None
 
     def start(self) -> bool:
         try:
@@ -118,25 +108,12 @@ class ResourcePlugin:
         self._cleanup()
         os.makedirs(os.path.dirname(self.socket), exist_ok=True)
         self.stop_bc = Broadcast()
-        if self.mgr.cfg.grpc_server == "native" and self.native_failed is None:
-            try:
-                native = NativePluginServer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
-                                            self.mgr.cfg.send_every_pulse)
-                await native.start(self.socket)
-                self.native = native
-                return
-            except (OSError, ImportError, AttributeError) as e:
-                # never leave the node unserved over the fast path: serve it from Python
-                _log.warning("native gRPC server unavailable (%s); serving %s with grpc.aio", e, self.resource_name)
-                REGISTRY.inc("mi355x_dp_grpc_native_fallbacks_total", resource=self.name)
-                self._cleanup()
-        self.servicer = DevicePluginServicer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
-                                             self.mgr.cfg.send_every_pulse)
-        server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
-        server.add_generic_rpc_handlers((pb.device_plugin_handler(self.servicer),))
-        server.add_insecure_port(f"unix:{self.socket}")
-        await server.start()
-        self.server = server
+        # the framework's one kubelet-facing server (C++ HTTP/2, the daemon's); a start
+        # failure is retried like any other (start_server) -- there is no second transport
+        native = NativePluginServer(self.mgr.impl, self.ctx, self.mgr.pulse, self.stop_bc,
+                                    self.mgr.cfg.send_every_pulse)
+        await native.start(self.socket)
+        self.native = native
 
     async def _register(self) -> None:
         sock = self.mgr.kubelet_socket
@@ -158,13 +135,8 @@ class ResourcePlugin:
                 try:
                     t0 = time.perf_counter()
                     await self._serve()
-                    # the watchdog's baseline is taken before Register goes out: kubelet may
-                    # open ListAndWatch before its Register answer reaches us
-                    st0 = self.native.srv.stats() if self.native is not None else None
                     await self._register()
                     self.running = True
-                    if self.native is not None and cfg.grpc_watchdog_s > 0:
-                        self._watchdog = asyncio.create_task(self._watch_native(self.native, st0))
                     log.info_fields(_log, "plugin server started", resource=self.resource_name,
                                     socket=self.socket, startup_ms=f"{(time.perf_counter() - t0) * 1e3:.2f}")
                     return True
@@ -179,56 +151,11 @@ class ResourcePlugin:
                         await asyncio.sleep(cfg.retry_wait_s)
             return False
 
-    async def _watch_native(self, native: NativePluginServer, st0: dict) -> None:
-        """The native HTTP/2 stack has only been proven against grpc-go by
-        emulation (testing/gopeer.py). If the real kubelet cannot complete a
-        call on it, the plugin would stay registered and invisible; the
-        reference's grpc-go server has no such risk (vendored dpm/plugin.go:
-        93-162). So, until kubelet's first ListAndWatch (counted from `st0`,
-        the server's counters when Register was sent): no stream within
-        grpc_watchdog_s, or a protocol error on a connection that has made a
-        DevicePlugin call (kubelet's, not a stray client's), and this resource
-        is re-served with grpc.aio and registered again. Once ListAndWatch has
-        been seen the watchdog is done: a misbehaving client later loses only
-        its own connection (GOAWAY), as with grpc-go (server.go:984-998)."""
-        cfg = self.mgr.cfg
-        t0 = time.monotonic()
-        reason = ""
-        while self.native is native:
-            await asyncio.sleep(min(0.25, cfg.grpc_watchdog_s / 4))
-            if self.native is not native:
-                return
-            st = native.srv.stats()
-            if st["streams_opened"] > st0["streams_opened"]:
-                return                      # kubelet lists: disarmed
-            if st["caller_protocol_errors"] > st0["caller_protocol_errors"]:
-                reason = (f"{st['caller_protocol_errors'] - st0['caller_protocol_errors']} HTTP/2 protocol error(s) "
-                          f"on kubelet's connection before its ListAndWatch")
-            elif time.monotonic() - t0 > cfg.grpc_watchdog_s:
-                reason = f"no ListAndWatch stream within {cfg.grpc_watchdog_s:g}s of Register"
-            if reason:
-                break
-        else:
-            return
-        self.native_failed = reason
-        _log.error("%s: native gRPC transport watchdog: %s; serving with grpc.aio and registering again",
-                   self.resource_name, reason)
-        REGISTRY.inc("mi355x_dp_grpc_native_fallbacks_total", resource=self.name, reason="watchdog")
-        await self.stop_server()
-        await self.start_server()
-
     async def _stop_locked(self) -> None:
-        if self._watchdog is not None and self._watchdog is not asyncio.current_task():
-            self._watchdog.cancel()
-            await asyncio.gather(self._watchdog, return_exceptions=True)
-        self._watchdog = None
         self.stop_bc.close()
         if self.native is not None:
             await self.native.stop(grace=0.5)
             self.native = None
-        if self.server is not None:
-            await self.server.stop(grace=0.5)
-            self.server = None
         self.running = False
         self._cleanup()
 
@@ -238,13 +165,9 @@ class ResourcePlugin:
 
 
 class PluginManager:
-    GRPC_SERVERS = ("native", "aio")
-
     def __init__(self, impl: Optional[DeviceImpl], cfg: Optional[ManagerConfig] = None):
         self.impl = impl
         self.cfg = cfg or ManagerConfig()
-        if self.cfg.grpc_server not in self.GRPC_SERVERS:
-            raise ValueError(f"grpc server must be one of {self.GRPC_SERVERS}, got {self.cfg.grpc_server!r}")
         self.kubelet_socket = self.cfg.kubelet_socket or os.path.join(self.cfg.plugin_dir, "kubelet.sock")
         self.plugins: Dict[str, ResourcePlugin] = {}
         self.pulse = Broadcast()

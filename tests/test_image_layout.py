@@ -230,3 +230,107 @@ def test_a_wrong_flag_or_command_fails(tmp_path, node):
         run_container(dict(c, command=["./k8s-device-plugin-py"]), tmp_path, node)
     with pytest.raises(AssertionError, match="is not an image this build makes"):
         run_container(dict(c, image="docker.io/rocm/k8s-device-plugin:1.31.0.2"), tmp_path, node)
+
+
+# ------------------------------------------------------------------ shared libraries of the runtime stage
+# sonames each runtime base image ships itself (its C/C++ runtime; zlib for the package manager)
+BASE_LIBS = {
+    "ubuntu:22.04": {"libc.so.6", "libm.so.6", "libdl.so.2", "libpthread.so.0", "librt.so.1",
+                     "ld-linux-x86-64.so.2", "libgcc_s.so.1", "libstdc++.so.6", "libz.so.1"},
+    "registry.access.redhat.com/ubi9/ubi-minimal:latest": {"libc.so.6", "libm.so.6", "libdl.so.2", "libpthread.so.0",
+                                                           "librt.so.1", "ld-linux-x86-64.so.2", "libgcc_s.so.1",
+                                                           "libz.so.1"},
+}
+# distro package -> sonames it installs (Ubuntu 22.04 / UBI 9 names)
+PACKAGE_LIBS = {
+    "libdrm2": {"libdrm.so.2"}, "libdrm-amdgpu1": {"libdrm_amdgpu.so.1"}, "libelf1": {"libelf.so.1"},
+    "libnuma1": {"libnuma.so.1"}, "libssl3": {"libssl.so.3", "libcrypto.so.3"}, "libstdc++6": {"libstdc++.so.6"},
+    "libdrm": {"libdrm.so.2", "libdrm_amdgpu.so.1"}, "elfutils-libelf": {"libelf.so.1"},
+    "numactl-libs": {"libnuma.so.1"}, "zlib": {"libz.so.1"}, "libstdc++": {"libstdc++.so.6"},
+    "openssl-libs": {"libssl.so.3", "libcrypto.so.3"},
+}
+# what copied third-party libraries dlopen() at run time, beyond their DT_NEEDED (from
+# their strings; librocprofiler-register's names of other ROCm libraries are ones it looks
+# for among those already loaded, not load targets)
+THIRD_PARTY_DLOPEN = {"libamd_smi": {"libdrm_amdgpu.so.1"}}
+_SONAME = re.compile(rb"(lib[A-Za-z0-9_+-]+\.so(?:\.[0-9]+)*)")
+
+
+def _stem(soname):
+    return soname.split(".so", 1)[0]
+
+
+def _elf_needed(path):
+    out = subprocess.run(["readelf", "-d", path], capture_output=True, text=True, check=True).stdout
+    return set(re.findall(r"\(NEEDED\)\s+Shared library: \[([^\]]+)\]", out))
+
+
+def stage_libraries(dockerfile, drop=None):
+    """(provided sonames, required {(binary or library, soname or dlopen stem)}) of the runtime
+    stage; `drop`: one COPY source to leave out (what removing that line would do)."""
+    text = open(os.path.join(REPO, dockerfile)).read().replace("\\\n", " ")
+    base = [l.split()[1] for l in text.splitlines() if l.strip().upper().startswith("FROM ")][-1]
+    provided = set(BASE_LIBS[base])
+    binaries, libs = [], []
+    for op, rest in runtime_stage(dockerfile):
+        if op == "RUN":
+            for part in rest.split("&&"):
+                w = shlex.split(part)
+                if "install" in w and w[0] in ("apt-get", "microdnf", "dnf"):
+                    for pkg in (x for x in w[w.index("install") + 1:] if not x.startswith("-")):
+                        assert pkg in PACKAGE_LIBS, f"{dockerfile}: package {pkg} is not in PACKAGE_LIBS"
+                        provided |= PACKAGE_LIBS[pkg]
+        elif op == "COPY" and rest.startswith("--from="):
+            for src in shlex.split(rest)[1:-1]:
+                if src == drop:
+                    continue
+                if src.startswith("/src/"):
+                    binaries += glob.glob(os.path.join(REPO, src[len("/src/"):]))
+                else:                       # the build stage's ROCm libraries: this host's copy
+                    found = glob.glob(src)
+                    assert found, f"{dockerfile}: COPY {src}: no such library here"
+                    provided |= {os.path.basename(p) for p in found}
+                    libs += [p for p in found if not os.path.islink(p)]
+    required = set()
+    for b in binaries:
+        required |= {(os.path.basename(b), s) for s in _elf_needed(b)}
+        # our own dlopen() targets: any of a library's names will do (so.1, .so, /opt/rocm/lib/...)
+        required |= {(os.path.basename(b), "dlopen:" + _stem(m.decode()))
+                     for m in _SONAME.findall(open(b, "rb").read())}
+    for lib in libs:
+        name = os.path.basename(lib)
+        required |= {(name, s) for s in _elf_needed(lib)}
+        required |= {(name, "dlopen:" + _stem(s)) for s in THIRD_PARTY_DLOPEN.get(_stem(name), ())}
+    return provided, required
+
+
+def missing_libraries(dockerfile, drop=None):
+    provided, required = stage_libraries(dockerfile, drop)
+    stems = {_stem(s) for s in provided}
+    return sorted((who, need) for who, need in required
+                  if not (need[len("dlopen:"):] in stems if need.startswith("dlopen:") else need in provided))
+
+
+@pytest.mark.parametrize("df", ["Dockerfile", "labeller.Dockerfile", "ubi-dp.Dockerfile", "ubi-labeller.Dockerfile"])
+def test_runtime_stage_provides_every_library_its_binaries_load(df):
+    """Every DT_NEEDED and dlopen() target of the copied binaries, and of the ROCm
+    libraries copied for them, is in the stage: the base image, a package it
+    installs or a library it copies (on the library path: LD_LIBRARY_PATH)."""
+    assert missing_libraries(df) == []
+    st = runtime_stage(df)
+    copied_dirs = {shlex.split(rest)[-1].rstrip("/") for op, rest in st
+                   if op == "COPY" and rest.startswith("--from=") and ".so" in rest}
+    env = dict(kv.partition("=")[::2] for op, rest in st if op == "ENV" for kv in shlex.split(rest))
+    assert copied_dirs <= set(env.get("LD_LIBRARY_PATH", "").split(":")), (copied_dirs, env)
+    assert not re.search(r"^FROM\s+rocm/", open(os.path.join(REPO, df)).read().split(" AS build")[-1], re.M), \
+        "the runtime stage is not a ROCm development image"
+
+
+@pytest.mark.parametrize("df", ["Dockerfile", "labeller.Dockerfile", "ubi-dp.Dockerfile", "ubi-labeller.Dockerfile"])
+def test_the_library_check_fails_without_any_one_copied_library(df):
+    """Dropping any one library COPY source leaves something unresolved."""
+    srcs = [s for op, rest in runtime_stage(df) if op == "COPY" and rest.startswith("--from=")
+            for s in shlex.split(rest)[1:-1] if not s.startswith("/src/")]
+    assert srcs
+    for s in srcs:
+        assert missing_libraries(df, drop=s), f"{df}: removing {s} went unnoticed"

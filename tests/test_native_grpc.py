@@ -160,11 +160,24 @@ def _impl(fi, **kw):
 
 
 async def _with_plugin(tmp_path, impl, grpc_server, fn, pulse=0.0):
+    """`fn(kubelet, mgr, resource state)` against the plugin served by the C++
+    server ("native": the Python oracle's manager) or by grpc.aio ("aio": the
+    oracle servicer on grpcio's own HTTP/2 stack, testing/aio_plugin.py; `mgr`
+    is then the AioPlugin)."""
     pdir = str(tmp_path / f"dp-{grpc_server}")
     k = FakeKubelet(pdir)
     await k.start()
-    mgr = PluginManager(impl, ManagerConfig(pulse_s=pulse, plugin_dir=pdir, handle_signals=False,
-                                            grpc_server=grpc_server))
+    if grpc_server == "aio":
+        from rocm_k8s_device_plugin_amd.testing.aio_plugin import AioPlugin
+        ap = AioPlugin(impl, pdir, impl.resource_names()[0])
+        try:
+            await ap.start()
+            st = await k.wait_for_resource(f"amd.com/{impl.resource_names()[0]}", 1)
+            return await fn(k, ap, st)
+        finally:
+            await ap.stop()
+            await k.stop()
+    mgr = PluginManager(impl, ManagerConfig(pulse_s=pulse, plugin_dir=pdir, handle_signals=False))
     task = asyncio.create_task(mgr.run())
     try:
         st = await k.wait_for_resource(f"amd.com/{impl.resource_names()[0]}", 1)
@@ -215,8 +228,8 @@ def test_native_answers_equal_the_aio_servicer(tmp_path, mode, strategies):
         async def fn(k, mgr, st):
             ids = sorted(st.devices)
             res = await _drive(st, _requests(ids, random.Random(11)))
-            plugin = mgr.plugins[impl.resource_names()[0]]
             if server == "native":
+                plugin = mgr.plugins[impl.resource_names()[0]]
                 plugin.sync()
                 assert plugin.native.calls >= len(res) and plugin.native.fallbacks == 0
             return res, dict(st.devices)
@@ -471,15 +484,6 @@ def test_stop_while_a_fallback_waits_for_the_gil(tmp_path):
     ch.close()
 
 
-def test_cli_grpc_server_flag(tmp_path):
-    from rocm_k8s_device_plugin_amd.cli import device_plugin as cli
-    ns = cli.build_parser().parse_args(["-grpc_server", "bogus"])
-    assert "grpc_server" in (cli.validate(ns) or "")
-    assert cli.validate(cli.build_parser().parse_args(["-grpc_server", "aio"])) is None
-    with pytest.raises(ValueError):
-        PluginManager(None, ManagerConfig(grpc_server="bogus"))
-
-
 def test_views_switched_at_run_time_reach_the_native_allocate(tmp_path):
     """Setting -node_view's view on a running plugin (what bench.py does for its
     comparison) updates the prepared Allocate fragments: the mounts come back
@@ -584,22 +588,39 @@ def test_server_restart_on_the_same_socket_path(tmp_path):
         srv2.stop(0.1)
 
 
-def test_native_start_failure_falls_back_to_aio(tmp_path, monkeypatch):
-    """If the native server cannot start, the plugin serves the node from grpc.aio."""
+def test_native_start_failure_is_retried_not_replaced(tmp_path, monkeypatch):
+    """The server failing to start is retried (the reference's 3 tries, dpm
+    manager.go:205-219) and, once it starts, serves the node; there is no
+    second transport to fall back to."""
     from rocm_k8s_device_plugin_amd.plugin import native_server as ns_mod
     fi = make_mi355x_node(tmp_path / "n")
+    real, tries = ns_mod.NativePluginServer.start, []
 
-    async def broken(self, socket):
-        raise OSError("bind: injected")
+    async def flaky(self, socket):
+        tries.append(socket)
+        if len(tries) == 1:
+            raise OSError("bind: injected")
+        return await real(self, socket)
 
-    monkeypatch.setattr(ns_mod.NativePluginServer, "start", broken)
+    monkeypatch.setattr(ns_mod.NativePluginServer, "start", flaky)
 
-    async def fn(k, mgr, st):
-        adm = await k.admit("amd.com/gpu", 2)
-        return mgr.plugins["gpu"].native, mgr.plugins["gpu"].server, adm
+    async def go():
+        pdir = str(tmp_path / "dp")
+        k = FakeKubelet(pdir)
+        await k.start()
+        mgr = PluginManager(_impl(fi), ManagerConfig(plugin_dir=pdir, handle_signals=False, retry_wait_s=0.05))
+        task = asyncio.create_task(mgr.run())
+        try:
+            await k.wait_for_resource("amd.com/gpu", 1)
+            adm = await k.admit("amd.com/gpu", 2)
+            return mgr.plugins["gpu"].native, adm
+        finally:
+            mgr.request_stop()
+            await asyncio.wait_for(task, 20)
+            await k.stop()
 
-    native, server, adm = run(_with_plugin(tmp_path, _impl(fi), "native", fn))
-    assert native is None and server is not None and len(adm.device_ids) == 2
+    native, adm = run(go())
+    assert len(tries) == 2 and native is not None and len(adm.device_ids) == 2
 
 
 @pytest.mark.parametrize("server", ["native", "aio"])

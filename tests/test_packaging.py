@@ -339,3 +339,26 @@ def test_launchers_run_the_native_binaries(tmp_path):
     lines = h.stdout.splitlines()   # the native binary answered: its version banner, then the usage
     assert lines[0].startswith("AMD GPU Node Labeller") and "mi355x-node-labeller version " in lines[1]
     assert lines[3].startswith("usage: ")
+
+
+
+def test_installed_console_scripts_run_the_native_daemons():
+    """pyproject's console scripts point at cli/launch.py, which execs the native
+    binaries: no installable command runs the Python oracle plugin or labeller."""
+    import re
+    import subprocess
+    import sys
+    text = (REPO / "pyproject.toml").read_text()
+    scripts = dict(re.findall(r'^(k8s-[a-z-]+) = "([^"]+)"', text, re.M))
+    assert scripts == {"k8s-device-plugin": "rocm_k8s_device_plugin_amd.cli.launch:device_plugin",
+                       "k8s-node-labeller": "rocm_k8s_device_plugin_amd.cli.launch:node_labeller"}, scripts
+    for name, target in scripts.items():
+        mod, fn = target.split(":")
+        # what the generated console script does: import the module, call the function
+        code = f"import sys; sys.argv[0] = {name!r}; from {mod} import {fn}; sys.exit({fn}())"
+        p = subprocess.run([sys.executable, "-c", code, "-h"], capture_output=True, text=True, timeout=60,
+                           cwd=str(REPO))
+        assert p.returncode == 0, p.stderr[-1000:]
+        banner = "mi355x-device-plugin version" if name == "k8s-device-plugin" else "version"
+        assert f"{name} version" in p.stdout or banner in p.stdout, p.stdout[:500]
+        assert "native daemon" in p.stdout.splitlines()[0], p.stdout[:300]

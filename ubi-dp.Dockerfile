@@ -14,7 +14,7 @@ RUN GIT_DESCRIBE=${GIT_DESCRIBE} python3 rocm_k8s_device_plugin_amd/_build.py &&
     rocm_k8s_device_plugin_amd/bin/mi355x-device-plugin -h >/dev/null
 
 FROM registry.access.redhat.com/ubi9/ubi-minimal:latest
-RUN microdnf install -y libdrm elfutils-libelf numactl-libs zlib && microdnf clean all
+RUN microdnf install -y libdrm elfutils-libelf numactl-libs zlib libstdc++ && microdnf clean all
 COPY --from=build /opt/rocm/lib/libhsa-runtime64.so* /opt/rocm/lib/librocprofiler-register.so* /opt/rocm/lib/libamd_smi.so* /opt/rocm/lib/
 COPY --from=build /src/rocm_k8s_device_plugin_amd/bin/mi355x-device-plugin /opt/mi355x/bin/mi355x-device-plugin
 COPY --from=build /src/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe /opt/mi355x/bin/mi355x-liveness-probe

@@ -12,7 +12,7 @@ RUN GIT_DESCRIBE=${GIT_DESCRIBE} python3 rocm_k8s_device_plugin_amd/_build.py --
     rocm_k8s_device_plugin_amd/bin/mi355x-node-labeller -h >/dev/null
 
 FROM registry.access.redhat.com/ubi9/ubi-minimal:latest
-RUN microdnf install -y libdrm openssl-libs && microdnf clean all
+RUN microdnf install -y libdrm openssl-libs libstdc++ && microdnf clean all
 COPY --from=build /opt/rocm/lib/libamd_smi.so* /opt/rocm/lib/
 COPY --from=build /src/rocm_k8s_device_plugin_amd/bin/mi355x-node-labeller /opt/mi355x/bin/mi355x-node-labeller
 WORKDIR /root
