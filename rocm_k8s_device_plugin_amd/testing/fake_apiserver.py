@@ -237,3 +237,25 @@ class FakeApiServer:
     def stop(self) -> None:
         self.httpd.shutdown()
         self.httpd.server_close()
+
+
+def tls_material(d):
+    """A CA and a server certificate for 127.0.0.1 signed by it (openssl CLI):
+    (server cert, server key, CA cert) paths under directory `d`."""
+    import shutil
+    import subprocess
+    if not shutil.which("openssl"):
+        import pytest
+        pytest.skip("openssl not installed")
+
+    def run(*a):
+        subprocess.run(["openssl", *a], check=True, capture_output=True, timeout=60)
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "ca.key"), "-out", str(d / "ca.crt"),
+        "-days", "2", "-subj", "/CN=test-ca")
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "srv.key"), "-out", str(d / "srv.csr"),
+        "-subj", "/CN=kubernetes")
+    (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1,DNS:kubernetes.default.svc\n")
+    run("x509", "-req", "-in", str(d / "srv.csr"), "-CA", str(d / "ca.crt"), "-CAkey", str(d / "ca.key"),
+        "-CAcreateserial", "-out", str(d / "srv.crt"), "-days", "2", "-extfile", str(d / "ext.cnf"))
+    return str(d / "srv.crt"), str(d / "srv.key"), str(d / "ca.crt")
+

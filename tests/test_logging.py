@@ -128,7 +128,7 @@ def test_device_plugin_cli_writes_log_files(tmp_path):
 @pytest.mark.parametrize("cli,flags", [
     ("device_plugin", ("-pulse", "-driver_type", "-resource_naming_strategy", "-kubelet_dir", "-log_dir",
                        "-liveness_corroborate", "-allocator_search")),
-    ("node_labeller", ("-watch", "-log_dir", "-vmodule")),
+    ("node_labeller", ("-vram", "-log_dir", "-vmodule", "-dry_run")),
 ])
 def test_cli_help_renders(cli, flags):
     """-h must render every help string (argparse %-formats them) and name the

@@ -136,13 +136,13 @@ def _wait(pred, timeout=30.0):
     return pred()
 
 
-def _start(fi, srv, tmp_path, *extra, token="tok", node="node-n"):
+def _start(fi, srv, tmp_path, *extra, token="tok", node="node-n", stderr=subprocess.PIPE):
     tok = tmp_path / "token"
     tok.write_text(token + "\n")
     argv = [EXE, "-node_name", node, "-apiserver", srv.url, "-token_file", str(tok), "-sysfs_root", str(fi.sysfs),
             "-dev_root", str(fi.dev), "-vram", "-cu-count", "-mode", "-device-id", "-compute-memory-partition",
             *extra]
-    return subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True), tok
+    return subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=stderr, text=True), tok
 
 
 def _stop(p):
@@ -320,7 +320,7 @@ def test_topology_change_relabels(tmp_path):
 
 
 def test_in_cluster_https_with_the_cluster_ca(tmp_path, monkeypatch):
-    from test_labeller import _tls_material
+    from rocm_k8s_device_plugin_amd.testing.fake_apiserver import tls_material as _tls_material
     crt, key, ca = _tls_material(tmp_path)
     fi = make_mi355x_node(tmp_path / "n")
     srv = FakeApiServer(token="sa-token", tls=(crt, key)).start()
@@ -420,7 +420,7 @@ def test_no_leaks_under_connection_churn(tmp_path):
     """Hundreds of TLS connections (resync every 0.1 s, watches cut every
     0.1 s, labels stripped every 0.2 s): open fds and RSS stay flat (and the
     ASan build's leak check at exit stays clean)."""
-    from test_labeller import _tls_material
+    from rocm_k8s_device_plugin_amd.testing.fake_apiserver import tls_material as _tls_material
     crt, key, ca = _tls_material(tmp_path)
     fi = make_mi355x_node(tmp_path / "n")
     srv = FakeApiServer(token="tok", tls=(crt, key)).start()
@@ -464,6 +464,117 @@ def test_no_leaks_under_connection_churn(tmp_path):
             assert rss1 - rss0 < 2048, (rss0, rss1)           # KiB
         rc, err = _stop(p)
         assert rc == 0, err[-2000:]
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
+def test_resync_patches_only_changes_and_survives_apiserver_errors(tmp_path):
+    """The reconcile contract (reference controller.go:23-58, as the resync runs
+    it): stale kinds removed and ours set in one PATCH, nothing written while the
+    node already carries the labels, a deleted label re-asserted at the next
+    resync, a 500 from the apiserver retried rather than fatal."""
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        srv.add_node("node-n", {"amd.com/gpu.family": "stale", "beta.amd.com/gpu.family": "stale",
+                                "beta.amd.com/gpu.family.stale": "8", "kubernetes.io/hostname": "node-n"})
+        p, _ = _start(fi, srv, tmp_path, "-resync", "0.2", "-watch=false", "-topology_watch", "0")
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.vram") == "288G")
+        got = srv.labels("node-n")
+        assert got["kubernetes.io/hostname"] == "node-n"
+        assert "amd.com/gpu.family" not in got and "beta.amd.com/gpu.family.stale" not in got
+        patches = lambda: sum(1 for r in srv.requests if r[0] == "PATCH")   # noqa: E731
+        gets = lambda: sum(1 for r in srv.requests if r[0] == "GET")         # noqa: E731
+        assert patches() == 1
+        g0 = gets()
+        assert _wait(lambda: gets() >= g0 + 3)            # three more resyncs: reads, no writes
+        assert patches() == 1
+        srv.nodes["node-n"]["metadata"]["labels"].pop("amd.com/gpu.vram")
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.vram") == "288G")
+        assert patches() == 2
+        srv.fail_next = 2                                  # the next resyncs get 500s
+        g1 = gets()
+        assert _wait(lambda: gets() >= g1 + 3)
+        srv.nodes["node-n"]["metadata"]["labels"].pop("amd.com/gpu.mode")
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.mode") == "container")
+        assert p.poll() is None
+        rc, err = _stop(p)
+        assert rc == 0, err[-2000:]
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
+def test_unauthorized_token_and_missing_node_are_retried(tmp_path):
+    """401 (a wrong or expired token) and 404 (the node object not created yet)
+    are not fatal: the labeller keeps trying and labels the node once the
+    token is right and the node exists."""
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        log = tmp_path / "labeller.log"
+        p, tok = _start(fi, srv, tmp_path, "-resync", "0.2", "-watch=false", "-topology_watch", "0", token="bad",
+                        stderr=open(log, "w"))
+        assert _wait(lambda: len(srv.requests) >= 2)       # refused, and tried again
+        assert p.poll() is None and not srv.nodes
+        n401 = len(srv.requests)
+        tok.write_text("tok\n")                            # a rotated, now valid token
+        assert _wait(lambda: len(srv.requests) > n401)     # the next try is let in: 404, no node yet
+        assert _wait(lambda: "not found" in open(log).read() or "404" in open(log).read())
+        assert p.poll() is None                            # still running
+        srv.add_node("node-n")
+        assert _wait(lambda: srv.labels("node-n").get("amd.com/gpu.vram") == "288G")
+        rc, _ = _stop(p)
+        err = open(log).read()
+        assert rc == 0, err[-2000:]
+        assert "401" in err or "Unauthorized" in err, err[-2000:]
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
+def test_kubeconfig_with_embedded_ca_and_token_over_https(tmp_path):
+    """-kubeconfig as kubectl writes it: https server, certificate-authority-data,
+    a token user, current-context; the labeller verifies the server with that CA."""
+    import base64
+    from rocm_k8s_device_plugin_amd.testing.fake_apiserver import tls_material as _tls_material
+    crt, key, ca = _tls_material(tmp_path)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="abc", tls=(crt, key)).start()
+    p = None
+    try:
+        srv.add_node("node-k")
+        ca_data = base64.b64encode(open(ca, "rb").read()).decode()
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(f"""apiVersion: v1
+kind: Config
+current-context: c1
+clusters:
+- name: k1
+  cluster: {{server: "{srv.url}/", certificate-authority-data: "{ca_data}"}}
+- name: other
+  cluster: {{server: "https://10.9.9.9:6443"}}
+contexts:
+- name: c0
+  context: {{cluster: other, user: u1}}
+- name: c1
+  context: {{cluster: k1, user: u1}}
+users:
+- name: u1
+  user: {{token: abc}}
+""")
+        p = subprocess.Popen([EXE, "-node_name", "node-k", "-kubeconfig", str(kc), "-once", "-vram", "-mode",
+                              "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)],
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        assert p.wait(60) == 0, p.stderr.read()[-2000:]
+        got = srv.labels("node-k")
+        assert got["amd.com/gpu.vram"] == "288G" and got["amd.com/gpu.mode"] == "container"
     finally:
         if p is not None and p.poll() is None:
             p.kill()

@@ -52,7 +52,11 @@ def test_labeller_manifest():
     assert c["command"] == ["./k8s-node-labeller"]
     assert c["args"] == ["-vram", "-cu-count", "-simd-count", "-device-id", "-family"]
     assert c["env"][0]["name"] == "DS_NODE_NAME"
-    # every labeller arg is a real flag
+    # every labeller arg is a flag of the native labeller the image runs (and of the label oracle)
+    import subprocess
+    exe = REPO / "rocm_k8s_device_plugin_amd" / "bin" / "mi355x-node-labeller"
+    p = subprocess.run([str(exe), "-dry_run", *c["args"]], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr[-1000:]
     from rocm_k8s_device_plugin_amd.cli.node_labeller import build_parser
     build_parser().parse_args(c["args"])
 
@@ -329,8 +333,8 @@ def test_launchers_run_the_native_binaries(tmp_path):
     p = subprocess.run(base + ["-grpc_server", "aio"], capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "flag provided but not defined: -grpc_server" in p.stderr   # Go's flag package
     lbl = str(REPO / "scripts/k8s-node-labeller")
-    args = ["-dry_run", "-node_name", "n", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-vram", "-device-id"]
-    nat = subprocess.run([lbl, *args], capture_output=True, text=True, timeout=60)
+    args = ["-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-vram", "-device-id"]
+    nat = subprocess.run([lbl, "-node_name", "n", *args], capture_output=True, text=True, timeout=60)
     py = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.node_labeller", *args],
                         capture_output=True, text=True, timeout=120, cwd=str(REPO))
     assert nat.returncode == 0 and py.returncode == 0, (nat.stderr[-1000:], py.stderr[-1000:])
