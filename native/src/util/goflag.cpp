@@ -1,6 +1,7 @@
 // Go flag-package value parsing (see mi355x/goflag.h).
 #include "mi355x/goflag.h"
 
+#include <cctype>
 #include <cerrno>
 #include <climits>
 #include <cmath>
@@ -105,7 +106,7 @@ bool parse_int_flag(const std::string& s, int* out) {
 }
 
 bool parse_float(const std::string& s, double* out) {
-  if (s.empty() || s[0] == ' ' || s[0] == '\t' || s[0] == '\n') return false;  // strtod would skip these
+  if (s.empty() || std::isspace(static_cast<unsigned char>(s[0]))) return false;  // strtod would skip these
   if (s.find('_') != std::string::npos) return false;  // only legal in hex floats, which flags never need
   char* end = nullptr;
   errno = 0;
