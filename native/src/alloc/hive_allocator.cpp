@@ -417,14 +417,22 @@ bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const s
     int group;
     std::vector<int> members;  // pool order
   };
+  // equal figures of a and b towards x (one of the columns same_row compares)
+  auto same_col = [&](int a, int b, int x) {
+    return w_[at(a, x)] == w_[at(b, x)] && link_kw_[at(a, x)] == link_kw_[at(b, x)] &&
+           link_bw_[at(a, x)] == link_bw_[at(b, x)];
+  };
   std::vector<Class> cls;
   for (size_t i = 0; i < pool.size(); ++i) {
     int found = -1;
     for (size_t c = 0; c < cls.size() && found < 0; ++c)
       if (cls[c].group == pool_group[i] && same_row(cls[c].members[0], pool[i])) {
-        // transitivity within the class: the new device must match every member
+        // the new device matches every member m: rows of m and of the first member
+        // agree off {first, m}, the new row agrees with the first off {first, new},
+        // so only the first member's own column is left to compare
+        const int f = cls[c].members[0];
         bool all = true;
-        for (int m : cls[c].members) all = all && same_row(m, pool[i]);
+        for (size_t k2 = 1; k2 < cls[c].members.size() && all; ++k2) all = same_col(cls[c].members[k2], pool[i], f);
         if (all) found = static_cast<int>(c);
       }
     if (found < 0) {
@@ -433,6 +441,13 @@ bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const s
       cls[found].members.push_back(pool[i]);
     }
   }
+  // Explore the largest classes first: sets that keep to few, full GPUs have the
+  // most cheap intra-GPU pairs, so the first leaves are near the optimum and the
+  // bound prunes early; classes of one size also become neighbours for the
+  // symmetry rule below. (The order of exploration decides nothing: ties are
+  // broken on the chosen devices' pool positions, fewest-free GPUs first.)
+  std::stable_sort(cls.begin(), cls.end(),
+                   [](const Class& a, const Class& b) { return a.members.size() > b.members.size(); });
   const int K = static_cast<int>(cls.size());
   // class-level aggregates
   std::vector<int64_t> wi(K, 0), wr(K, 0), kwr(K, 0), bwr(K, 0);
@@ -462,14 +477,34 @@ bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const s
   }
   std::vector<int> suffix_cap(K + 1, 0);
   for (int c = K - 1; c >= 0; --c) suffix_cap[c] = suffix_cap[c + 1] + static_cast<int>(cls[c].members.size());
-  // smallest weight of a pair drawn from classes c.. (for the lower bound)
-  std::vector<int64_t> wmin_suffix(K + 1, std::numeric_limits<int64_t>::max());
+  // For the lower bound on the pairs among the devices still to choose from
+  // classes c..: the smallest weight of a pair inside one class and of a pair
+  // across two classes, and the class sizes largest first. With intra-class
+  // pairs the cheaper kind (partitions of one GPU), m devices have at most
+  // P(m) = sum t_i (t_i - 1) / 2 intra pairs, t_i filling the largest classes
+  // first; the rest of the m (m - 1) / 2 pairs cross classes.
+  constexpr int64_t kInf = std::numeric_limits<int64_t>::max() / 4;
+  std::vector<int64_t> wmin_intra(K + 1, kInf), wmin_cross(K + 1, kInf);
   for (int c = K - 1; c >= 0; --c) {
-    int64_t m = wmin_suffix[c + 1];
-    if (cls[c].members.size() > 1) m = std::min(m, wi[c]);
-    for (int d = c + 1; d < K; ++d) m = std::min(m, wc[static_cast<size_t>(c) * K + d]);
-    wmin_suffix[c] = m;
+    wmin_intra[c] = wmin_intra[c + 1];
+    if (cls[c].members.size() > 1) wmin_intra[c] = std::min(wmin_intra[c], wi[c]);
+    wmin_cross[c] = wmin_cross[c + 1];
+    for (int d = c + 1; d < K; ++d) wmin_cross[c] = std::min(wmin_cross[c], wc[static_cast<size_t>(c) * K + d]);
   }
+  auto pair_bound = [&](int c, int m) -> int64_t {
+    const int64_t pairs = static_cast<int64_t>(m) * (m - 1) / 2;
+    if (pairs == 0) return 0;
+    const int64_t wa = wmin_intra[c], wx = wmin_cross[c];
+    if (wa >= wx) return pairs * wx;  // crossing is never dearer: every pair at the cross minimum
+    int64_t intra = 0;
+    int left = m;
+    for (int d = c; d < K && left; ++d) {  // classes are in size order, largest first
+      const int t = std::min<int>(left, static_cast<int>(cls[d].members.size()));
+      intra += static_cast<int64_t>(t) * (t - 1) / 2;
+      left -= t;
+    }
+    return intra * wa + (pairs - intra) * (wx >= kInf ? wa : wx);
+  };
   // symmetry: class c is interchangeable with c-1 (same size, same weights and
   // link figures to everything else). Taking no more from c than from c-1
   // loses no optimum: the tie-break prefers earlier pool positions anyway.
@@ -488,6 +523,31 @@ bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const s
   }
   std::vector<std::pair<int64_t, int>> unit;  // scratch for the bound
   unit.reserve(K);
+  // fewest GPUs not yet in the set that classes c.. must add to supply m more
+  // devices (the GPUs already used supply what they can first)
+  std::vector<int> group_uses(groups_.size(), 0);
+  std::vector<int> new_cap(groups_.size(), 0), caps;
+  caps.reserve(groups_.size());
+  auto new_gpus_needed = [&](int c, int m) -> int {
+    int left = m;
+    std::fill(new_cap.begin(), new_cap.end(), 0);
+    for (int d = c; d < K; ++d) {
+      const int g = cls[d].group, sz = static_cast<int>(cls[d].members.size());
+      if (group_uses[g]) left -= sz;
+      else new_cap[g] += sz;
+    }
+    if (left <= 0) return 0;
+    caps.clear();
+    for (int v : new_cap)
+      if (v) caps.push_back(v);
+    std::sort(caps.rbegin(), caps.rend());
+    int t = 0;
+    for (int v : caps) {
+      ++t;
+      if ((left -= v) <= 0) break;
+    }
+    return t;
+  };
 
   struct Key {
     int64_t w = std::numeric_limits<int64_t>::max();
@@ -498,7 +558,6 @@ bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const s
   } best;
   bool found = false;
   std::vector<int> k(K, 0);
-  std::vector<int> group_uses(groups_.size(), 0);
   for (int q : req_idx) group_uses[dev_group_[q]]++;
   uint64_t nodes = 0, leaves = 0;
   bool aborted = false;
@@ -539,8 +598,7 @@ bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const s
     if (c >= K || suffix_cap[c] < m) return;
     if (found) {
       // lower bound: the m cheapest attachments to what is chosen (per class,
-      // up to its size) plus every pair among the m new devices at the
-      // smallest pair weight left
+      // up to its size) plus the pairs among the m new devices (pair_bound)
       unit.clear();
       for (int d = c; d < K; ++d) {
         int64_t a = wr[d];
@@ -557,8 +615,9 @@ bool HiveAllocator::allocate_extended(const std::vector<int>& avail_idx, const s
         left -= t;
         if (!left) break;
       }
-      lb += static_cast<int64_t>(m) * (m - 1) / 2 * wmin_suffix[c];
+      lb += pair_bound(c, m);
       if (w + RR + lb > best.w) return;
+      if (w + RR + lb == best.w && gpus + new_gpus_needed(c, m) > best.gpus) return;  // can only tie, on more GPUs
     }
     int cap = std::min<int>(m, static_cast<int>(cls[c].members.size()));
     if (c > 0 && sym_prev[c]) cap = std::min(cap, k[c - 1]);

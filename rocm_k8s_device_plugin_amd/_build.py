@@ -99,11 +99,22 @@ def build(hip: bool | None = None, sanitize: str = "", build_dir: Path | None = 
     """Configure + build. ``hip=None`` builds the HIP probe when hipcc exists.
     ``sanitize`` / ``coverage``: a host-only variant in its own tree, with its
     binaries under ``<tree>/pkg`` (the package outputs stay untouched)."""
+    import fcntl
     if hip is None:
         hip = hipcc_available()
     bdir = build_dir or variant_dir(sanitize, coverage)
-    variant = bool(sanitize) or coverage
     bdir.mkdir(parents=True, exist_ok=True)
+    # one build per tree at a time, across processes (pytest workers, ranks)
+    with open(bdir.parent / f".{bdir.name}.build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            _build_tree(bdir, hip, sanitize, coverage, build_dir, jobs, quiet)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_tree(bdir: Path, hip: bool, sanitize: str, coverage: bool, build_dir, jobs, quiet: bool) -> None:
+    variant = bool(sanitize) or coverage
     gen = ["-G", "Ninja"] if shutil.which("ninja") else []
     cfg = [
         "cmake", "-S", str(NATIVE_DIR), "-B", str(bdir), *gen,

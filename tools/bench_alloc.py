@@ -8,9 +8,10 @@
    the reference's own MI300X-CPX / MI210 captures when mounted.
 2. Admission over UDS gRPC through the fake kubelet on a synthetic 8x MI355X
    node: GetPreferredAllocation + Allocate p50/p99 at 1/2/4/8 GPUs, whole node
-   free and fragmented, and on the 8x8 CPX node; native server and grpc.aio.
+   free and fragmented, and on the 8x8 CPX node; the native daemon, and the
+   oracle servicer on grpc.aio for comparison.
 
-  python tools/bench_alloc.py --out profiles/archive/alloc_bench.json
+  python tools/bench_alloc.py --out profiles/r5/alloc_bench.json
 """
 from __future__ import annotations
 
@@ -93,37 +94,57 @@ def synthetic_ref_devices(dev_count, parts, numa_count, start, end):
     return out
 
 
-async def admission(sysfs, n_adv, n_req, steps, fragment, server="native", client="native"):
+async def admission(sysfs, n_adv, n_req, steps, fragment, server="native-daemon", client="native"):
+    """kubelet's GetPreferredAllocation + Allocate round trips against the plugin on
+    `n_adv` advertised devices: the native daemon (the product, as the images run it)
+    or the oracle servicer on grpc.aio (testing/aio_plugin.py, the comparison)."""
+    import signal
+    import subprocess
+
     from rocm_k8s_device_plugin_amd.health.monitor import HealthConfig
+    from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
     from rocm_k8s_device_plugin_amd.plugin.container import ContainerImpl
-    from rocm_k8s_device_plugin_amd.plugin.manager import ManagerConfig, PluginManager
+    from rocm_k8s_device_plugin_amd.testing.aio_plugin import AioPlugin
     from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
     from rocm_k8s_device_plugin_amd.topology import Inventory
 
     full = discover(sysfs)
-    inv = Inventory(sysfs_root=sysfs, devices=full.devices[:n_adv], topology=full.topology, driver_loaded=True,
-                    kfd_present=True)
-    impl = ContainerImpl("single", sysfs, HealthConfig(exporter_socket=None), inventory=inv)
+    devs = full.devices[:n_adv]
     with tempfile.TemporaryDirectory() as d:
         k = FakeKubelet(d, rpc_client=client)
         await k.start()
-        mgr = PluginManager(impl, ManagerConfig(pulse_s=0, plugin_dir=d, handle_signals=False, grpc_server=server))
-        task = asyncio.create_task(mgr.run())
-        await k.wait_for_resource("amd.com/gpu", n_adv)
-        rng = random.Random(5)
-        lat, pref = [], []
-        for i in range(steps):
-            av = None
-            if fragment:
-                ids = k.healthy_free("amd.com/gpu")
-                av = sorted(rng.sample(ids, rng.randint(n_req, len(ids))))
-            a = await k.admit("amd.com/gpu", n_req, available=av)
-            lat.append(a.total_ms)
-            pref.append(a.preferred_ms)
-            k.release("amd.com/gpu", a.device_ids)
-        mgr.request_stop()
-        await task
-        await k.stop()
+        proc = aio = None
+        if server == "native-daemon":
+            exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+            proc = subprocess.Popen([exe, "-kubelet_dir", d, "-sysfs_root", sysfs, "-dev_root",
+                                     os.path.join(os.path.dirname(sysfs), "dev"), "-exporter_socket", "",
+                                     "-device_ids", ",".join(x.id for x in devs)],
+                                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        else:
+            inv = Inventory(sysfs_root=sysfs, devices=devs, topology=full.topology, driver_loaded=True,
+                            kfd_present=True)
+            aio = AioPlugin(ContainerImpl("single", sysfs, HealthConfig(exporter_socket=None), inventory=inv), d)
+            await aio.start()
+        try:
+            await k.wait_for_resource("amd.com/gpu", n_adv)
+            rng = random.Random(5)
+            lat, pref = [], []
+            for i in range(steps):
+                av = None
+                if fragment:
+                    ids = k.healthy_free("amd.com/gpu")
+                    av = sorted(rng.sample(ids, rng.randint(n_req, len(ids))))
+                a = await k.admit("amd.com/gpu", n_req, available=av)
+                lat.append(a.total_ms)
+                pref.append(a.preferred_ms)
+                k.release("amd.com/gpu", a.device_ids)
+        finally:
+            if proc is not None:
+                proc.send_signal(signal.SIGTERM)
+                proc.wait(timeout=20)
+            if aio is not None:
+                await aio.stop()
+            await k.stop()
     return {"server": server, "kubelet_client": client, "advertised": n_adv, "requested": n_req, "fragmented": fragment,
             "admission_p50_ms": round(pct(lat, .5), 4), "admission_p99_ms": round(pct(lat, .99), 4),
             "preferred_p50_ms": round(pct(pref, .5), 4)}
@@ -154,13 +175,15 @@ def main():
                 pol.init(devs, load_topology(nodes_dir=os.path.join(REF, path)))
                 res["allocator"] += bench_topology(name, pol, [x[0] for x in devs], sizes, rng)
         # the plugin-owned part of admission over UDS: kubelet's GetPreferredAllocation +
-        # Allocate round trips, native C++ server (default) and grpc.aio, both called
-        # from the native client (kubelet itself is a compiled grpc-go client)
+        # Allocate round trips against the native daemon, and against the oracle servicer on
+        # grpc.aio for comparison, both called from the native client (kubelet itself is a
+        # compiled grpc-go client)
         fi = make_mi355x_node(os.path.join(d, "adm"))
         cpx = make_mi355x_node(os.path.join(d, "adm_cpx"), compute_partition="cpx")
         # ("native-thread": the same client on a worker thread, needed when the server runs on this
         # process' event loop -- grpc.aio -- and used for both servers for a like-for-like pair)
-        for server, client in (("native", "native"), ("native", "native-thread"), ("aio", "native-thread")):
+        for server, client in (("native-daemon", "native"), ("native-daemon", "native-thread"),
+                               ("aio", "native-thread")):
             runs = [(fi, n, n, False) for n in (1, 2, 4, 8)] + [(fi, 8, n, True) for n in (1, 2, 4, 7)] + \
                 [(cpx, 64, n, True) for n in (1, 8, 32)]
             for node, n_adv, n_req, frag in runs:

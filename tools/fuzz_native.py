@@ -64,6 +64,19 @@ def available() -> bool:
 
 
 def build(jobs: int = 8) -> None:
+    """Configure and build the three fuzz trees; serialised across processes (pytest
+    workers that start together must not run two builds into one tree)."""
+    import fcntl
+    BUILD.parent.mkdir(parents=True, exist_ok=True)
+    with open(BUILD.parent / ".fuzz-build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            _build_locked(jobs)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(jobs: int) -> None:
     gen = ["-G", "Ninja"] if shutil.which("ninja") else []
     for mode, bdir in (("fuzz", BUILD), ("replay", BUILD_REPLAY), ("tsan", BUILD_TSAN)):
         bdir.mkdir(parents=True, exist_ok=True)
