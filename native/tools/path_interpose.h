@@ -50,6 +50,15 @@ thread_local bool t_in_hook = false;
 // lock-free, always on: what the container view changed (the probe's "view" field)
 std::atomic<long> g_seen{0};             // paths through the hooks
 std::atomic<long> g_node_cache_ok{0};    // successful opens under /sys/devices/system/node/node*/cpu*/cache
+std::atomic<long> g_kfd_open_ns{0};      // time in open("/dev/kfd"): it waits for other processes' kfd teardown
+
+bool is_kfd(const char* p) { return p && std::strcmp(p, "/dev/kfd") == 0; }
+
+long mono_ns_now() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1000000000L + ts.tv_nsec;
+}
 
 // a path under the NUMA-node tree's per-CPU cache descriptors (the -node_view hides them)
 bool node_cpu_cache(const char* p) {
@@ -145,7 +154,9 @@ int open(const char* path, int flags, ...) {
     errno = ENOENT;
     return -1;
   }
+  const long t0 = is_kfd(path) ? mono_ns_now() : 0;
   const int fd = fn(map_path(path), flags, mode);
+  if (t0) g_kfd_open_ns.fetch_add(mono_ns_now() - t0, std::memory_order_relaxed);
   return tally(path, fd, fd >= 0);
 }
 
@@ -162,7 +173,9 @@ int open64(const char* path, int flags, ...) {
     errno = ENOENT;
     return -1;
   }
+  const long t0 = is_kfd(path) ? mono_ns_now() : 0;
   const int fd = fn(map_path(path), flags, mode);
+  if (t0) g_kfd_open_ns.fetch_add(mono_ns_now() - t0, std::memory_order_relaxed);
   return tally(path, fd, fd >= 0);
 }
 
@@ -179,7 +192,9 @@ int openat(int dirfd, const char* path, int flags, ...) {
     errno = ENOENT;
     return -1;
   }
+  const long t0 = is_kfd(path) ? mono_ns_now() : 0;
   const int fd = fn(dirfd, map_path(path), flags, mode);
+  if (t0) g_kfd_open_ns.fetch_add(mono_ns_now() - t0, std::memory_order_relaxed);
   return tally(path, fd, fd >= 0);
 }
 
@@ -260,11 +275,13 @@ inline void path_interpose_configure() {
   }
 }
 
-// {"paths":N,"node_cpu_cache_opens":N,"redirected":N,"dev_hidden":N}: cheap enough for every container
+// {"paths":N,"node_cpu_cache_opens":N,"redirected":N,"hidden":N,"kfd_open_us":X}: cheap enough for every container
 inline std::string path_interpose_view_json() {
+  char kfd[32];
+  std::snprintf(kfd, sizeof(kfd), "%.1f", g_kfd_open_ns.load() / 1e3);
   return "{\"paths\":" + std::to_string(g_seen.load()) + ",\"node_cpu_cache_opens\":" +
          std::to_string(g_node_cache_ok.load()) + ",\"redirected\":" + std::to_string(g_redirected.load()) +
-         ",\"hidden\":" + std::to_string(g_hidden.load()) + "}";
+         ",\"hidden\":" + std::to_string(g_hidden.load()) + ",\"kfd_open_us\":" + kfd + "}";
 }
 
 // {"opens":N,"hidden":N,"redirected":N,"by_template":{...top 40...}}

@@ -57,6 +57,7 @@ class StepRecords:
     read_syscalls: List[int] = field(default_factory=list)
     cpu_ms_runtime: List[float] = field(default_factory=list)
     hsa_init_ms: List[float] = field(default_factory=list)
+    kfd_open_ms: List[float] = field(default_factory=list)   # HSA entrypoint: open("/dev/kfd") inside the init
     node_cache_opens: List[int] = field(default_factory=list)
 
     def phases(self) -> Dict[str, List[float]]:
@@ -74,13 +75,19 @@ class StepRecords:
         return {"steps": len(self.latency_ms), "latency_p50_ms": med(self.latency_ms),
                 "latency_p99_ms": round(pct(self.latency_ms, .99), 3),
                 "phases_p50_ms": {k: med(v) for k, v in self.phases().items()},
-                "tail_attribution": tail_attribution(self.latency_ms, self.phases()),
+                "tail_attribution": tail_attribution(self.latency_ms, self.phases(), details=self.details()),
                 "counters_p50": self.counters()}
+
+    def details(self) -> dict:
+        """Per-step detail reported with slow steps: inside the runtime init (HSA
+        entrypoint), the kfd open, which waits for other processes' kfd teardown."""
+        return {"kfd_open_ms": self.kfd_open_ms, "hsa_init_ms": self.hsa_init_ms} if any(self.kfd_open_ms) else {}
 
     def counters(self) -> dict:
         med = lambda xs: round(pct(xs, .5), 3) if xs else None
         return {"read_syscalls": med(self.read_syscalls), "cpu_ms_runtime": med(self.cpu_ms_runtime),
                 "hsa_init_ms": med([x for x in self.hsa_init_ms if x > 0]),
+                "kfd_open_ms": med([x for x in self.kfd_open_ms if x > 0]),
                 "node_cpu_cache_opens": med(self.node_cache_opens)}
 
 
@@ -124,7 +131,7 @@ class Admissions:
         d, a_ = self.d, self.args
         if mode == "pod" and d.rank != 0:
             # the pod's single container runs on rank 0; other ranks only keep step
-            return (True, 0, 0.0, "", (0, 0, 0, 0.0, {}, (None, None, 0.0, None))), frozenset()
+            return (True, 0, 0.0, "", (0, 0, 0, 0.0, {}, (None, None, 0.0, None, 0.0))), frozenset()
         pod = mode == "pod" or d.world == 1
         mine_ord = ordl if pod else [ordl[d.rank]]
         paths = None
@@ -141,8 +148,11 @@ class Admissions:
         sus = max((dv.get("setup_us", 0.0) for dv in devs), default=0.0)
         slow_dev = max(devs, key=lambda dv: dv.get("total_us", 0.0), default={})
         view = r.doc.get("view") or {}
-        counters = (r.doc.get("read_syscalls_runtime"), r.doc.get("cpu_ms_runtime"),
-                    (r.doc.get("init_us") or {}).get("hsa_init", 0.0) / 1e3, view.get("node_cpu_cache_opens"))
+        init_us = r.doc.get("init_us") or {}
+        # open("/dev/kfd"): timed by the container's view (either entrypoint), else by the HSA entrypoint
+        kfd_us = view.get("kfd_open_us", init_us.get("kfd_open", 0.0))
+        counters = (r.doc.get("read_syscalls_runtime"), r.doc.get("cpu_ms_runtime"), init_us.get("hsa_init", 0.0) / 1e3,
+                    view.get("node_cpu_cache_opens"), kfd_us / 1e3)
         phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)), sus / 1e3,
                   slow_dev.get("phase_us") or {}, counters)
         return (r.ok, r.t_ready_ns, kus, r.error, phases), r.kfd_lingering
@@ -200,7 +210,7 @@ class Admissions:
         cap = min(3.0, 0.25 + 0.25 * max(len(lingering), n))  # one process with N GPUs tears down N VMs
         waited = self._blocking(wait_kfd_released, lingering, timeout_s=cap) if settle == "kfd" else 0.0
         # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC), set-up ms, phases, counters
-        sp, tm, trt, su, dph, (syscr, cpu_rt, hsa_ms, cache_opens) = slowest[4]
+        sp, tm, trt, su, dph, (syscr, cpu_rt, hsa_ms, cache_opens, kfd_ms) = slowest[4]
         lat = (t_ready - t0) / 1e6
         if into is None:
             return
@@ -211,6 +221,7 @@ class Admissions:
         if cpu_rt is not None:
             rec.cpu_ms_runtime.append(cpu_rt)
         rec.hsa_init_ms.append(hsa_ms or 0.0)
+        rec.kfd_open_ms.append(kfd_ms or 0.0)
         if cache_opens is not None:
             rec.node_cache_opens.append(cache_opens)
         rec.settle_ms.append(waited)
@@ -260,7 +271,7 @@ class Admissions:
             "device_phases_p50_us": {k: round(pct([p[k] for p in rec.device_phases if k in p], .5), 1)
                                      for k in sorted({k for p in rec.device_phases for k in p})},
             # every timed step above 1.5 x p50, attributed to the admission phase with the largest excess
-            "tail_attribution": tail_attribution(rec.latency_ms, rec.phases()),
+            "tail_attribution": tail_attribution(rec.latency_ms, rec.phases(), details=rec.details()),
             # the containers' own start-up counters (read syscalls, CPU ms): what a comparison row's
             # view or runtime changes deterministically, next to its wall-clock time
             "container_counters_p50": rec.counters(),

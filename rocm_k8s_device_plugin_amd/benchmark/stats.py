@@ -62,11 +62,12 @@ def process_gpu_state() -> dict:
             "kfd_fds": kfd, "render_fds": render}
 
 
-def tail_attribution(lat, phases, factor=1.5) -> dict:
+def tail_attribution(lat, phases, factor=1.5, details=None) -> dict:
     """Every step slower than factor x p50: which phase carries the excess.
     ``phases`` maps a phase name to its per-step ms (aligned with ``lat``); a
     slow step is attributed to the phase with the largest excess over its own
-    p50."""
+    p50. ``details``: more per-step series (e.g. the kfd open inside the
+    runtime init) reported with each slow step, not used for attribution."""
     if not lat:
         return {}
     p50 = pct(lat, .5)
@@ -78,7 +79,11 @@ def tail_attribution(lat, phases, factor=1.5) -> dict:
         excess = {k: round(v[i] - med[k], 2) for k, v in phases.items()}
         top = max(excess, key=excess.get)
         by_phase.setdefault(top, []).append(excess[top])
-        slow.append({"step": i, "latency_ms": round(x, 2), "phase": top, "excess_ms": excess})
+        row = {"step": i, "latency_ms": round(x, 2), "phase": top, "excess_ms": excess}
+        for k, v in (details or {}).items():
+            if i < len(v) and v[i] is not None:
+                row[k] = round(v[i], 2)
+        slow.append(row)
     return {"threshold_ms": round(factor * p50, 2), "p99_over_p50": round(pct(lat, .99) / p50, 3) if p50 else None,
             "phase_p50_ms": {k: round(v, 3) for k, v in med.items()},
             "slow_steps": slow,
