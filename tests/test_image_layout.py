@@ -334,3 +334,30 @@ def test_the_library_check_fails_without_any_one_copied_library(df):
     assert srcs
     for s in srcs:
         assert missing_libraries(df, drop=s), f"{df}: removing {s} went unnoticed"
+
+
+# newest symbol versions the base image's C / C++ runtime provides (jammy: glibc 2.35,
+# libstdc++6 from GCC 12); UBI images copy libraries built on EL9, not this host's
+BASE_SYMBOL_VERSIONS = {"ubuntu:22.04": {"GLIBC": (2, 35), "GLIBCXX": (3, 4, 30)}}
+
+
+@pytest.mark.parametrize("df", ["Dockerfile", "labeller.Dockerfile"])
+def test_runtime_stage_c_runtime_is_new_enough(df):
+    """Every copied binary and library links symbol versions the base image's
+    glibc and libstdc++ have (a binary built against a newer runtime would fail
+    to start on the slim base with 'version GLIBCXX_... not found')."""
+    text = open(os.path.join(REPO, df)).read().replace("\\\n", " ")
+    base = [l.split()[1] for l in text.splitlines() if l.strip().upper().startswith("FROM ")][-1]
+    have = BASE_SYMBOL_VERSIONS[base]
+    files = []
+    for op, rest in runtime_stage(df):
+        if op == "COPY" and rest.startswith("--from="):
+            for src in shlex.split(rest)[1:-1]:
+                files += glob.glob(os.path.join(REPO, src[len("/src/"):]) if src.startswith("/src/") else src)
+    files = [f for f in files if not os.path.islink(f)]
+    assert files
+    for f in files:
+        out = subprocess.run(["readelf", "-V", f], capture_output=True, text=True, check=True).stdout
+        for lib, ver in re.findall(r"Name: (GLIBCXX|GLIBC)_([0-9.]+)", out):
+            need = tuple(int(x) for x in ver.split("."))
+            assert need <= have[lib], f"{df}: {os.path.basename(f)} needs {lib}_{ver}, {base} has {have[lib]}"
