@@ -57,7 +57,8 @@ class StepRecords:
     read_syscalls: List[int] = field(default_factory=list)
     cpu_ms_runtime: List[float] = field(default_factory=list)
     hsa_init_ms: List[float] = field(default_factory=list)
-    kfd_open_ms: List[float] = field(default_factory=list)   # HSA entrypoint: open("/dev/kfd") inside the init
+    kfd_open_ms: List[float] = field(default_factory=list)   # open("/dev/kfd") inside the runtime init
+    kfd_foreign_exits: List[int] = field(default_factory=list)  # other programs' kfd processes gone meanwhile
     node_cache_opens: List[int] = field(default_factory=list)
 
     def phases(self) -> Dict[str, List[float]]:
@@ -81,7 +82,10 @@ class StepRecords:
     def details(self) -> dict:
         """Per-step detail reported with slow steps: inside the runtime init (HSA
         entrypoint), the kfd open, which waits for other processes' kfd teardown."""
-        return {"kfd_open_ms": self.kfd_open_ms, "hsa_init_ms": self.hsa_init_ms} if any(self.kfd_open_ms) else {}
+        if not any(self.kfd_open_ms):
+            return {}
+        return {"kfd_open_ms": self.kfd_open_ms, "hsa_init_ms": self.hsa_init_ms,
+                "host_kfd_exits_meanwhile": self.kfd_foreign_exits}
 
     def counters(self) -> dict:
         med = lambda xs: round(pct(xs, .5), 3) if xs else None
@@ -131,7 +135,7 @@ class Admissions:
         d, a_ = self.d, self.args
         if mode == "pod" and d.rank != 0:
             # the pod's single container runs on rank 0; other ranks only keep step
-            return (True, 0, 0.0, "", (0, 0, 0, 0.0, {}, (None, None, 0.0, None, 0.0))), frozenset()
+            return (True, 0, 0.0, "", (0, 0, 0, 0.0, {}, (None, None, 0.0, None, 0.0, 0))), frozenset()
         pod = mode == "pod" or d.world == 1
         mine_ord = ordl if pod else [ordl[d.rank]]
         paths = None
@@ -152,7 +156,7 @@ class Admissions:
         # open("/dev/kfd"): timed by the container's view (either entrypoint), else by the HSA entrypoint
         kfd_us = view.get("kfd_open_us", init_us.get("kfd_open", 0.0))
         counters = (r.doc.get("read_syscalls_runtime"), r.doc.get("cpu_ms_runtime"), init_us.get("hsa_init", 0.0) / 1e3,
-                    view.get("node_cpu_cache_opens"), kfd_us / 1e3)
+                    view.get("node_cpu_cache_opens"), kfd_us / 1e3, r.kfd_foreign_exits)
         phases = (r.t_start_ns, int(r.doc.get("t_start_ns", 0)), int(r.doc.get("t_runtime_ns", 0)), sus / 1e3,
                   slow_dev.get("phase_us") or {}, counters)
         return (r.ok, r.t_ready_ns, kus, r.error, phases), r.kfd_lingering
@@ -210,7 +214,7 @@ class Admissions:
         cap = min(3.0, 0.25 + 0.25 * max(len(lingering), n))  # one process with N GPUs tears down N VMs
         waited = self._blocking(wait_kfd_released, lingering, timeout_s=cap) if settle == "kfd" else 0.0
         # spawn, main(), GPU runtime ready (CLOCK_MONOTONIC), set-up ms, phases, counters
-        sp, tm, trt, su, dph, (syscr, cpu_rt, hsa_ms, cache_opens, kfd_ms) = slowest[4]
+        sp, tm, trt, su, dph, (syscr, cpu_rt, hsa_ms, cache_opens, kfd_ms, foreign) = slowest[4]
         lat = (t_ready - t0) / 1e6
         if into is None:
             return
@@ -222,6 +226,7 @@ class Admissions:
             rec.cpu_ms_runtime.append(cpu_rt)
         rec.hsa_init_ms.append(hsa_ms or 0.0)
         rec.kfd_open_ms.append(kfd_ms or 0.0)
+        rec.kfd_foreign_exits.append(foreign or 0)
         if cache_opens is not None:
             rec.node_cache_opens.append(cache_opens)
         rec.settle_ms.append(waited)
