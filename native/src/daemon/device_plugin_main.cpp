@@ -41,7 +41,7 @@ constexpr const char* kTitle = "AMD GPU device plugin for Kubernetes (MI355X-nat
 
 volatile sig_atomic_t g_stop = 0;
 int g_sig_pipe[2] = {-1, -1};
-volatile int g_daemon_stop_fd = -1;  // the daemon's stop pipe: aborts in-flight probes and peer calls
+volatile sig_atomic_t g_daemon_stop_fd = -1;  // the daemon's stop pipe: aborts in-flight probes and peer calls
 
 void on_signal(int) {
   g_stop = 1;
@@ -95,6 +95,10 @@ int main(int argc, char** argv) {
 
   daemon::Daemon d(f);
   g_daemon_stop_fd = d.stop_fd();
+  // declared after `d`, so destroyed first: the handler never writes to the pipe `d` closes
+  struct ForgetStopFd {
+    ~ForgetStopFd() { g_daemon_stop_fd = -1; }
+  } forget_stop_fd;
   if (g_stop) return 0;     // a signal before the daemon existed
   const int rc = d.init();
   if (rc >= 0) return rc;
