@@ -250,7 +250,12 @@ class Parser {
     // quoted scalar or a flow collection the same line is content or a comment
     // the flow reader strips (a comment-like continuation of a quoted scalar,
     // e.g. `  #"`, is not in lines_).
-    const bool plain = first.empty() || (first[0] != '"' && first[0] != '\'' && first[0] != '[' && first[0] != '{');
+    size_t v = 0;  // past the node's properties (a tag `!x` / `!!str`, an anchor `&a`)
+    while (v < first.size() && (first[v] == '!' || first[v] == '&')) {
+      while (v < first.size() && first[v] != ' ') ++v;
+      while (v < first.size() && first[v] == ' ') ++v;
+    }
+    const bool plain = v >= first.size() || (first[v] != '"' && first[v] != '\'' && first[v] != '[' && first[v] != '{');
     // the next non-blank raw line decides
     for (size_t r = static_cast<size_t>(no); r < raw_.size(); ++r) {
       const std::string rl = rtrim(raw_[r]);

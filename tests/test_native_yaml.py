@@ -57,7 +57,7 @@ def test_native_reader_equals_pyyaml(doc, flow, style, width, unicode):
     "e: \"tab\\tnl\\n\\u00e9 \\\"q\\\"\"\nf: 'it''s'\ng: plain scalar\n  continued here\n",
     # comment lines indented deeper than the scalar above them end it
     "gpu:\n  device_count: 2\n    # two GPUs\n", "- x\n    # note\n", "a: b\n  c\n    # z\n",
-    "a: [1,\n  # c\n  2]\n", "a: \"b\n  # c\n  d\"\n", "gpu:\n  device_count: 2  # two\n      # GPUs\nx: y\n",
+    "a: [1,\n  # c\n  2]\n", "a: \"b\n  # c\n  d\"\n", "a: !!str \"b\n  # c\n  d\"\n", "gpu:\n  device_count: 2  # two\n      # GPUs\nx: y\n",
 ])
 def test_hand_written_documents(text):
     assert native(text) == _stringify(yaml.safe_load(text))
