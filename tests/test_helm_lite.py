@@ -76,14 +76,16 @@ def test_chart_health_defaults_follow_the_measured_choice():
         return ds[0]["spec"]["template"]["spec"]["containers"][0]
 
     c = dp({"dp": {"liveness": {"enabled": True}}})
-    assert "-liveness_mode=persistent" in c["args"] and c["resources"] == {"requests": {"memory": "2960Mi"}}
+    assert "-liveness_mode=persistent" in c["args"] and c["resources"] == {"requests": {"memory": "3072Mi"}}
     assert dp({"dp": {"liveness": {"enabled": True, "mode": "spawn"}}})["args"].count("-liveness_mode=spawn") == 1
     assert dp({"dp": {"liveness": {"enabled": True}, "resources": {"limits": {"memory": "4Gi"}}}})["resources"] == \
         {"limits": {"memory": "4Gi"}}
     assert dp({})["resources"] == {}                                  # no liveness: no request (as upstream)
     choice = json.load(open(os.path.join(repo, "profiles", "r5", "health_mode_choice.json")))
-    per_gpu = max(r["host_memory"]["total_rss_mb_max"] for r in choice["admissions_under_the_loop"].values())
-    assert per_gpu <= 370 and 8 * per_gpu * 1e6 <= 3 * 2 ** 30           # what the requests cover
+    mem = [r["host_memory"] for r in choice["admissions_under_the_loop"].values()]
+    probe_mib = max(m["children_rss_mb_max"] for m in mem)          # MiB per GPU (1-GPU box)
+    daemon_mib = max(m["daemon_rss_mb_p50"] for m in mem)
+    assert probe_mib <= 384 and 8 * probe_mib + daemon_mib <= 3 * 1024   # what the requests cover on 8 GPUs
     with open(os.path.join(repo, "k8s-ds-amdgpu-dp-health.yaml")) as f:
         man = yaml.safe_load(f)["spec"]["template"]["spec"]["containers"][0]
     assert "-liveness_mode=persistent" in man["args"] and man["resources"]["requests"]["memory"] == "3Gi"
