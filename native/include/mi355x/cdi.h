@@ -42,6 +42,9 @@ std::string kind(const std::string& resource);  // amd.com/<resource>
 std::string qualified_name(const std::string& resource, const std::string& dev_id);  // amd.com/gpu=<id>
 std::string annotation_key(const std::string& resource);  // cdi.k8s.io/amd.com_<resource>
 std::string spec_filename(const std::string& resource);    // amd.com-<resource>.json
+// a JSON string literal as Python's json.dumps writes the str (ensure_ascii); bytes that are
+// not UTF-8 as os.fsdecode's surrogate escapes
+std::string json_str(const std::string& s);
 
 // The spec document of one resource; "" + err when a name is not CDI-valid.
 std::string spec_json(const std::string& resource, const std::vector<GpuDevice>& devices, std::string* err);

@@ -19,29 +19,62 @@ namespace {
 
 bool alnum(char c) { return std::isalnum(static_cast<unsigned char>(c)) != 0; }
 
+}  // namespace
+
 std::string json_str(const std::string& s) {  // json.dumps (ensure_ascii)
   std::string o = "\"";
-  for (unsigned char c : s) {
+  auto u16 = [&o](unsigned v) {
+    char b[8];
+    std::snprintf(b, sizeof(b), "\\u%04x", v);
+    o += b;
+  };
+  for (size_t i = 0; i < s.size(); ++i) {
+    const unsigned char c = static_cast<unsigned char>(s[i]);
     switch (c) {
-      case '"': o += "\\\""; break;
-      case '\\': o += "\\\\"; break;
-      case '\n': o += "\\n"; break;
-      case '\r': o += "\\r"; break;
-      case '\t': o += "\\t"; break;
-      case '\b': o += "\\b"; break;
-      case '\f': o += "\\f"; break;
-      default:
-        if (c < 0x20 || c >= 0x80) {
-          char b[8];
-          std::snprintf(b, sizeof(b), "\\u%04x", c);
-          o += b;
+      case '"': o += "\\\""; continue;
+      case '\\': o += "\\\\"; continue;
+      case '\n': o += "\\n"; continue;
+      case '\r': o += "\\r"; continue;
+      case '\t': o += "\\t"; continue;
+      case '\b': o += "\\b"; continue;
+      case '\f': o += "\\f"; continue;
+      default: break;
+    }
+    if (c < 0x20 || c == 0x7F) {  // json.dumps escapes everything outside ' '..'~'
+      u16(c);
+    } else if (c < 0x80) {
+      o += static_cast<char>(c);
+    } else {
+      // one code point of well-formed UTF-8 -> \uXXXX (a surrogate pair above U+FFFF), as
+      // json.dumps writes a str; any other byte -> \udcXX, the str os.fsdecode makes of it
+      const int n = c >= 0xF0 && c <= 0xF4 ? 4 : c >= 0xE0 && c <= 0xEF ? 3 : c >= 0xC2 && c <= 0xDF ? 2 : 0;
+      unsigned cp = n == 4 ? c & 0x07u : n == 3 ? c & 0x0Fu : c & 0x1Fu;
+      bool ok = n > 0 && i + n <= s.size();
+      for (int k = 1; ok && k < n; ++k) {
+        const unsigned char d = static_cast<unsigned char>(s[i + k]);
+        ok = (d & 0xC0) == 0x80;
+        cp = (cp << 6) | (d & 0x3Fu);
+      }
+      // overlong 3/4-byte forms, UTF-16 surrogates and values past U+10FFFF are not UTF-8
+      ok = ok && !(n == 3 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) &&
+           !(n == 4 && (cp < 0x10000 || cp > 0x10FFFF));
+      if (!ok) {
+        u16(0xDC00u | c);
+      } else {
+        if (cp >= 0x10000) {
+          u16(0xD800u + ((cp - 0x10000) >> 10));
+          u16(0xDC00u + ((cp - 0x10000) & 0x3FF));
         } else {
-          o += static_cast<char>(c);
+          u16(cp);
         }
+        i += n - 1;
+      }
     }
   }
   return o + "\"";
 }
+
+namespace {
 
 // {"hostPath": p, "path": p, "permissions": "rw"} at indent level `lvl` (indent=1)
 std::string node_json(const std::string& path, int lvl) {

@@ -24,10 +24,12 @@
 #include "topology_watch.h"
 #include "workers.h"
 #include "mi355x/allocator.h"
+#include "mi355x/cdi.h"
 #include "mi355x/dp_service.h"
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/grpc_server.h"
 #include "mi355x/kfd_topology.h"
+#include "mi355x/metrics.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/sysfs.h"
 
@@ -781,6 +783,55 @@ static void test_flags_go_semantics() {
   CHECK(parse({"-liveness_timeout=2.5e1"}, &syn, &err, &f) && f.liveness_timeout == 25.0);
   CHECK(!parse({"-liveness_timeout= 2"}, &syn, &err) && syn);
   CHECK(!parse({"-liveness_timeout=1e999"}, &syn, &err) && syn);
+  // '_' right after a base prefix is Go literal syntax too (0x_1e); not before the prefix's digits end
+  CHECK(parse({"-pulse=0x_1e"}, &syn, &err, &f) && f.pulse == 30);
+  CHECK(parse({"-pulse=0b1_01"}, &syn, &err, &f) && f.pulse == 5);
+  CHECK(parse({"-pulse=0o_1_7"}, &syn, &err, &f) && f.pulse == 15);
+  CHECK(parse({"-pulse=-0x_1"}, &syn, &err) == false && !syn);  // parses (-1), then validateFlags refuses it
+  CHECK(!parse({"-pulse=0x1e_"}, &syn, &err) && syn);
+  // validateFlags: enumerated string flags
+  CHECK(!parse({"-allocator_search=fastest"}, &syn, &err) && !syn &&
+        err.find("invalid allocator_search provided: fastest") == 0);
+}
+
+// the CDI spec's strings, byte-for-byte as the Python oracle's json.dumps(os.fsdecode(...)) (expected
+// values generated by Python): UTF-8 as \\uXXXX (surrogate pairs above U+FFFF), other bytes as \\udcXX
+static void test_cdi_json_strings() {
+  CHECK(cdi::json_str(std::string("\xc3\xa9", 2)) == "\"\\u00e9\"");
+  CHECK(cdi::json_str(std::string("\xf0\x9f\x98\x80", 4)) == "\"\\ud83d\\ude00\"");
+  CHECK(cdi::json_str(std::string("\xff", 1)) == "\"\\udcff\"");
+  CHECK(cdi::json_str(std::string("\xe0\x80\x80", 3)) == "\"\\udce0\\udc80\\udc80\"");
+  CHECK(cdi::json_str(std::string("\x61\x22\x62\x5c", 4)) == "\"a\\\"b\\\\\"");
+  CHECK(cdi::json_str(std::string("\x01\x7f", 2)) == "\"\\u0001\\u007f\"");
+  CHECK(cdi::json_str(std::string("\xc3", 1)) == "\"\\udcc3\"");
+  CHECK(cdi::json_str(std::string("\xed\xa0\x80", 3)) == "\"\\udced\\udca0\\udc80\"");
+  CHECK(cdi::json_str(std::string("\xf4\x90\x80\x80", 4)) == "\"\\udcf4\\udc90\\udc80\\udc80\"");
+  CHECK(cdi::json_str(std::string("\x2f\x64\x65\x76\x2f\x64\x72\x69\x2f\x72\x65\x6e\x64\x65\x72\x44\x31\x32\x38", 19)) == "\"/dev/dri/renderD128\"");
+}
+
+static void test_metrics_registry() {
+  metrics::Registry r;
+  r.inc("mi355x_x_total", {{"b", "2"}, {"a", "1"}}, 1.0, "things");
+  r.inc("mi355x_x_total", {{"a", "1"}, {"b", "2"}}, 2.0);  // label order does not make a new series
+  r.set("mi355x_g", 3.5);
+  r.set("mi355x_g", 1.25);
+  r.observe_ms("mi355x_h_seconds", 0.2, {{"rpc", "Allocate"}});
+  r.observe_ms("mi355x_h_seconds", 7000, {{"rpc", "Allocate"}});
+  CHECK(r.value("mi355x_x_total", {{"a", "1"}, {"b", "2"}}) == 3.0);
+  CHECK(r.value("mi355x_g") == 1.25 && r.value("mi355x_absent") == 0.0);
+  CHECK(r.count("mi355x_h_seconds", {{"rpc", "Allocate"}}) == 2 && r.count("mi355x_h_seconds") == 0);
+  const std::string t = r.render();
+  CHECK(t.find("# HELP mi355x_x_total things\n# TYPE mi355x_x_total counter\n") != std::string::npos);
+  CHECK(t.find("mi355x_x_total{a=\"1\",b=\"2\"} 3.0\n") != std::string::npos);
+  CHECK(t.find("# TYPE mi355x_g gauge\nmi355x_g 1.25\n") != std::string::npos);
+  CHECK(t.find("mi355x_h_seconds_bucket{rpc=\"Allocate\",le=\"+Inf\"} 2\n") != std::string::npos);
+  CHECK(t.find("mi355x_h_seconds_count{rpc=\"Allocate\"} 2\n") != std::string::npos);
+  CHECK(t.find("mi355x_h_seconds_sum{rpc=\"Allocate\"} 7.0002\n") != std::string::npos);
+  // buckets (rendered in seconds) are cumulative: 0.2 ms lands in le=0.00025 and every bucket above it
+  CHECK(t.find("mi355x_h_seconds_bucket{rpc=\"Allocate\",le=\"0.0001\"} 0\n") != std::string::npos);
+  CHECK(t.find("mi355x_h_seconds_bucket{rpc=\"Allocate\",le=\"0.00025\"} 1\n") != std::string::npos);
+  r.clear();
+  CHECK(r.render().empty() && r.value("mi355x_g") == 0.0 && r.count("mi355x_h_seconds", {{"rpc", "Allocate"}}) == 0);
 }
 
 static void test_health_controller_generations(const std::string& tmp) {
@@ -838,6 +889,8 @@ int main(int argc, char** argv) {
   test_registration_random_sequences();
   test_topology_watch();
   test_flags_go_semantics();
+  test_metrics_registry();
+  test_cdi_json_strings();
   {
     char dir[] = "/tmp/mi355x-test-core-XXXXXX";
     if (::mkdtemp(dir)) {

@@ -122,6 +122,38 @@ def test_labeller_log_files_threshold_and_alsologtostderr(tmp_path):
     assert p.returncode == 1 and "vmodule" in p.stderr
 
 
+def test_stderrthreshold_names_numbers_and_backtrace_at(tmp_path):
+    """glog's severity flag takes a name in any case or a number
+    (vendor/github.com/golang/glog/glog.go severity.Set); -log_backtrace_at=FILE:N
+    appends a stack trace to the record logged at that line."""
+    fi = make_mi355x_node(tmp_path / "n")
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "native", "src", "daemon",
+                       "resources.cpp")
+    with open(src) as f:
+        line = next(i + 1 for i, s in enumerate(f) if '"Found %zu AMDGPUs"' in s)
+    base = [DP, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket="]
+    for thr, info_on_stderr in (("warning", False), ("0", True), ("INFO", True), ("Error", False), ("2", False)):
+        logs = tmp_path / f"logs-{thr}"
+        p = subprocess.run(base + ["-logtostderr=false", f"-log_dir={logs}", f"-stderrthreshold={thr}"],
+                           capture_output=True, text=True, timeout=30)
+        assert p.returncode == 0, p.stderr
+        assert ("Found 8 AMDGPUs" in p.stderr) == info_on_stderr, thr
+        assert "Found 8 AMDGPUs" in (logs / "k8s-device-plugin.INFO").read_text()
+    bad = subprocess.run(base + ["-stderrthreshold=loud"], capture_output=True, text=True, timeout=30)
+    assert bad.returncode == 2 and 'invalid value "loud" for flag -stderrthreshold' in bad.stderr
+    # the stack follows exactly the record logged at resources.cpp:<line>, nowhere else
+    p = subprocess.run(base + [f"-log_backtrace_at=resources.cpp:{line}"], capture_output=True, text=True,
+                       timeout=30)
+    assert p.returncode == 0, p.stderr
+    out = p.stderr.splitlines()
+    at = next(i for i, s in enumerate(out) if s.endswith(f"resources.cpp:{line}] Found 8 AMDGPUs"))
+    assert out[at + 1].startswith("    ") and out[at + 2].startswith("    ")
+    assert sum(1 for s in out if s.startswith("    ")) == sum(1 for s in out[at + 1:] if s.startswith("    "))
+    for spec in ("nocolon", "resources.cpp:0", "resources.cpp:x"):
+        q = subprocess.run(base + [f"-log_backtrace_at={spec}"], capture_output=True, text=True, timeout=30)
+        assert q.returncode != 0 and "log_backtrace_at" in q.stderr, (spec, q.returncode, q.stderr[-300:])
+
+
 def test_json_log_format_in_both_binaries(tmp_path):
     """-log_format=json: one JSON object per record with the Python CLIs' keys
     (utils/log.py JsonFormatter) and structured fields as keys."""
