@@ -134,3 +134,23 @@ def test_device_ids_restricts_the_advertised_set(tmp_path):
     assert p.returncode == 0, p.stderr[-2000:]
     devs = {d["id"] for d in json.loads(p.stdout)["resources"]["amd.com/gpu"]["devices"]}
     assert devs == set(keep) and "-device_ids: bogus is not a discovered device" in p.stderr
+
+
+@pytest.mark.parametrize("sub", ["topology-parsing/topology", "topology-parsing-mi308/topology",
+                                 "topo-mi300-cpx/topology", "topo-mi210-xgmi-pcie"])
+def test_report_on_reference_captures_equals_the_python_cli(tmp_path, ref_testdata, sub):
+    """The reference's own kfd captures (wrapped with the PCI / drm entries
+    discovery joins them with): same report from both implementations, and on
+    the MI210 capture (two xGMI hives of 4, PCIe between them) a pod of 4
+    stays in one hive (3 xGMI links of 50 GB/s per GPU: a 150 GB/s ring bound)
+    while all 8 span the hives, whose link the capture gives no bandwidth:
+    no bound is claimed for it."""
+    from rocm_k8s_device_plugin_amd.testing.fixtures import wrap_kfd_topology
+    fi = wrap_kfd_topology(ref_testdata / sub, tmp_path / "n")
+    nat, py = _both(fi, tmp_path)
+    assert nat == py
+    if sub == "topo-mi210-xgmi-pcie":
+        allocs = nat["resources"]["amd.com/gpu"]["allocations"]
+        assert allocs["4"]["one_hive"] and allocs["4"]["allreduce_bound_gbs"] == 150
+        assert allocs["2"]["allreduce_bound_gbs"] == 50
+        assert not allocs["8"]["one_hive"] and allocs["8"]["allreduce_bound_gbs"] is None
