@@ -17,6 +17,7 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include "../src/kube/labels.h"
 #include "../src/rpc/hpack.h"
 #include "flags.h"
 #include "health_controller.h"
@@ -809,6 +810,17 @@ static void test_cdi_json_strings() {
   CHECK(cdi::json_str(std::string("\x2f\x64\x65\x76\x2f\x64\x72\x69\x2f\x72\x65\x6e\x64\x65\x72\x44\x31\x32\x38", 19)) == "\"/dev/dri/renderD128\"");
 }
 
+// amd-smi's driver version of an in-tree amdgpu is the kernel banner (spaces removed on the
+// MI355X host): the label takes the release, as labels.py's re.match(r"^Linux\s*version\s*([0-9][^\s(]*)")
+static void test_driver_version_value() {
+  using labeller::driver_version_value;
+  CHECK(driver_version_value("Linuxversion6.18.54-ant.1(nixbld@localhost)(gcc(GCC)15.3.0)#1") == "6.18.54-ant.1");
+  CHECK(driver_version_value("Linux version 6.8.0-45-generic (buildd@lcy02) #45") == "6.8.0-45-generic");
+  CHECK(driver_version_value("Linux  version\t6.1(x)") == "6.1");
+  for (const char* same : {"6.12.12", "Linux version abc", "Linuxversion", "linux version 6.1", "", "Linux"})
+    CHECK(driver_version_value(same) == same);
+}
+
 static void test_metrics_registry() {
   metrics::Registry r;
   r.inc("mi355x_x_total", {{"b", "2"}, {"a", "1"}}, 1.0, "things");
@@ -890,6 +902,7 @@ int main(int argc, char** argv) {
   test_topology_watch();
   test_flags_go_semantics();
   test_metrics_registry();
+  test_driver_version_value();
   test_cdi_json_strings();
   {
     char dir[] = "/tmp/mi355x-test-core-XXXXXX";

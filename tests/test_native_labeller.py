@@ -88,6 +88,20 @@ def test_label_values_are_sanitised_like_the_python_labeller(tmp_path):
     assert out["amd.com/gpu.vram.288G"] == "8"     # and the rest of the node's labels
 
 
+def test_driver_version_fallbacks_equal_the_python_labeller(tmp_path):
+    """No driver/module/version on the cards (amdgpu built in, the MI355X test
+    host): /sys/module/amdgpu/version, then amd-smi (absent here), then the
+    reference's empty value."""
+    fi = make_mi355x_node(tmp_path)
+    kinds = ["driver-version", "driver-src-version"]
+    os.unlink(fi.sysfs / "bus/pci/drivers/amdgpu/module")
+    out = json.loads(_dry_run(fi, kinds))
+    assert out == _python(fi, kinds) and out["amd.com/gpu.driver-version"] == "6.12.12"
+    (fi.sysfs / "module/amdgpu/version").unlink()
+    out = json.loads(_dry_run(fi, kinds))
+    assert out == _python(fi, kinds) and out["amd.com/gpu.driver-version"] == ""
+
+
 @pytest.mark.parametrize("key,ok", [
     ("amd.com/gpu.vram", True), ("beta.amd.com/gpu.firmware.SMC.fw.12", True), ("gpu", True),
     ("amd.com/" + "x" * 63, True), ("amd.com/" + "x" * 64, False), ("amd.com/gpu.product-name.a/b", False),
