@@ -228,10 +228,11 @@ std::shared_ptr<const HiveAllocator> build_allocator(const std::vector<GpuDevice
 // docs/user-guide/configuration.md:11,45-91, never implemented there; the
 // Python CLI's topology.device_count_limit_from_env)
 int device_count_limit(const std::string& config, std::string* err) {
-  if (const char* e = std::getenv("AMD_GPU_DEVICE_COUNT"); e && *e) {
+  if (const char* e = std::getenv("AMD_GPU_DEVICE_COUNT"); e && *e) {  // surrounding blanks ignored
     char* end = nullptr;
     const long n = std::strtol(e, &end, 10);
-    if (!*end && n >= 0) return static_cast<int>(n);
+    while (end && std::isspace(static_cast<unsigned char>(*end))) ++end;
+    if (end != e && !*end && n >= 0) return static_cast<int>(n);
   }
   if (config.empty()) return -1;
   auto text = read_file(config);

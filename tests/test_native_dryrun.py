@@ -154,3 +154,35 @@ def test_report_on_reference_captures_equals_the_python_cli(tmp_path, ref_testda
         assert allocs["4"]["one_hive"] and allocs["4"]["allreduce_bound_gbs"] == 150
         assert allocs["2"]["allreduce_bound_gbs"] == 50
         assert not allocs["8"]["one_hive"] and allocs["8"]["allreduce_bound_gbs"] is None
+
+
+@pytest.mark.parametrize("partition", ["spx", "cpx"])
+def test_device_count_limit_equals_the_python_cli(tmp_path, monkeypatch, partition):
+    """AMD_GPU_DEVICE_COUNT, else gpu.device_count of -config (documented by the
+    reference, docs/user-guide/configuration.md:11,45-91): the first N physical
+    GPUs are advertised, every partition of each."""
+    fi = make_mi355x_node(tmp_path / "n", compute_partition=partition)
+    per_gpu = 8 if partition == "cpx" else 1
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text("gpu:\n  device_count: 5\n    # five GPUs\n")   # an indented comment ends the scalar
+
+    def advertised(doc):
+        return len(doc["resources"]["amd.com/gpu"]["devices"])
+
+    for env, config, gpus in (("2", "", 2), (" 3 ", "", 3), ("x", str(cfg), 5), ("", str(cfg), 5),
+                              ("-1", str(cfg), 5), ("1", str(cfg), 1)):
+        monkeypatch.setenv("AMD_GPU_DEVICE_COUNT", env)
+        nat, py = _both(fi, tmp_path, *(["-config", config] if config else []))
+        assert nat == py, (env, config)
+        assert advertised(nat) == gpus * per_gpu, (env, config)
+    monkeypatch.delenv("AMD_GPU_DEVICE_COUNT")
+    common = ["-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket", ""]
+    bad = tmp_path / "bad.yaml"
+    bad.write_text("gpu:\n  device_count: lots\n")
+    for path, why in ((bad, "bad gpu.device_count"), (tmp_path / "missing.yaml", "is unreadable")):
+        p = subprocess.run([EXE, *common, "-config", str(path)], capture_output=True, text=True, timeout=60)
+        assert p.returncode == 1 and why in p.stderr, p.stderr[-500:]
+        q = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.device_plugin", *common,
+                            "-config", str(path)], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, PYTHONPATH=REPO))
+        assert q.returncode != 0
