@@ -186,3 +186,22 @@ def test_device_count_limit_equals_the_python_cli(tmp_path, monkeypatch, partiti
                             "-config", str(path)], capture_output=True, text=True, timeout=120,
                            env=dict(os.environ, PYTHONPATH=REPO))
         assert q.returncode != 0
+
+
+@pytest.mark.parametrize("unknown", [0, 2])
+def test_kfd_denied_node_report_equals_the_python_cli(tmp_path, unknown):
+    """Every kfd GPU node denied (a container's device cgroup): devices are
+    identified from PCI sysfs; when some lack even a sysfs unique_id the
+    physical-GPU identity is unknown and preferred allocation is switched off
+    (kubelet picks), the devices still advertised."""
+    from rocm_k8s_device_plugin_amd.testing.fixtures import deny_kfd_nodes
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="dpx", xcp_layout="kernel")
+    deny_kfd_nodes(fi, sorted(set(fi.node_ids.values())))
+    for b in fi.bdfs[:unknown]:
+        os.remove(fi.sysfs / "devices/pci0000:00" / b / "unique_id")
+    nat, py = _both(fi, tmp_path)
+    assert nat == py
+    r = nat["resources"]["amd.com/gpu"]
+    assert len(r["devices"]) == 16 and r["preferred_allocation"] is (unknown == 0)
+    assert any("unreadable" in w for w in nat["warnings"])
+    assert bool([w for w in nat["warnings"] if "identity unknown" in w]) is (unknown > 0)
