@@ -698,3 +698,49 @@ def test_daemon_registers_again_when_kubelet_drops_the_stream(tmp_path):
         kub.close()
     assert rc == 0 and "registering again" in err, err[-2000:]
 
+
+
+def test_native_client_connect_waits_out_a_full_listen_backlog(tmp_path):
+    """A non-blocking AF_UNIX connect() answers EAGAIN while kubelet's listen
+    backlog is full: the client retries until the deadline (or the abort fd),
+    and gets in as soon as kubelet accepts one."""
+    path = str(tmp_path / "busy.sock")
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    srv.bind(path)
+    srv.listen(0)
+    pending, accepted = [], []
+    try:
+        while True:
+            s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            s.setblocking(False)
+            try:
+                s.connect(path)
+            except BlockingIOError:
+                s.close()
+                break
+            pending.append(s)
+            if len(pending) > 64:
+                pytest.skip("the listen backlog never filled")
+        c = core().GrpcClient()
+        t0 = time.monotonic()
+        err = c.connect(path, 0.3)
+        assert err.endswith("listen backlog full until the deadline"), err
+        assert 0.25 < time.monotonic() - t0 < 10
+        r, w = os.pipe()
+        try:
+            c.set_abort_fd(r)
+            threading.Timer(0.2, os.write, (w, b"x")).start()
+            assert c.connect(path, 30).endswith(": interrupted")
+        finally:
+            c.set_abort_fd(-1)
+            os.close(r)
+            os.close(w)
+        threading.Timer(0.3, lambda: accepted.append(srv.accept()[0])).start()
+        t0 = time.monotonic()
+        assert c.connect(path, 30) == ""
+        assert 0.2 < time.monotonic() - t0 < 15 and c.connected
+        c.close()
+    finally:
+        for s in pending + accepted:
+            s.close()
+        srv.close()
