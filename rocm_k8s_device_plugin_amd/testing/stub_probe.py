@@ -67,16 +67,25 @@ def _perf_device(ordinal_reported, mode, nonce, host_ordinal=None):
 
 def _kfd_entry():
     """Like a kept-queue server: a kfd proc entry with one queue per GPU id
-    (MI355X_STUB_KFD_PROC / MI355X_STUB_KFD_GPUIDS), removed on exit."""
+    (MI355X_STUB_KFD_PROC / MI355X_STUB_KFD_GPUIDS), removed on exit.
+    MI355X_STUB_KFD_ALSO="<pid>:<gid>,<gid>" adds another process' entry in the
+    same instant (a pod started with the server; left in place)."""
     root, gids = os.environ.get("MI355X_STUB_KFD_PROC"), os.environ.get("MI355X_STUB_KFD_GPUIDS", "")
     if not root:
         return None
     import shutil
+
+    def make(entry, ids):
+        for i, g in enumerate(x for x in ids.split(",") if x):
+            os.makedirs(os.path.join(entry, "queues", str(i)), exist_ok=True)
+            with open(os.path.join(entry, "queues", str(i), "gpuid"), "w") as f:
+                f.write(g + "\n")
     entry = os.path.join(root, str(os.getpid()))
-    for i, g in enumerate(x for x in gids.split(",") if x):
-        os.makedirs(os.path.join(entry, "queues", str(i)), exist_ok=True)
-        with open(os.path.join(entry, "queues", str(i), "gpuid"), "w") as f:
-            f.write(g + "\n")
+    make(entry, gids)
+    also = os.environ.get("MI355X_STUB_KFD_ALSO", "")
+    if also:
+        pid, ids = also.split(":")
+        make(os.path.join(root, pid), ids)
     import atexit
     atexit.register(shutil.rmtree, entry, True)
     return entry

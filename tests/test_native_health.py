@@ -246,6 +246,36 @@ def test_crowded_gpu_gets_no_probe_server_queue(tmp_path):
     assert "visible=0,1,2,4,5,6,7" in words and words.count("3") >= 2
 
 
+def test_own_kfd_entry_told_apart_from_a_pod_started_with_the_server(tmp_path):
+    """A pod's GPU process that appears in the same instant as the probe server
+    leaves two new kfd entries; the server's own is the one with a queue on
+    every probed GPU. Only the pod's GPUs then count as busy: a pending probe
+    there waits out the busy grace, one on an idle GPU is a fault."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    proc = fi.sysfs / "class/kfd/kfd/proc"
+    proc.mkdir(parents=True, exist_ok=True)
+    gid = lambda d: inv.topology.node(inv.by_id[d].node_id).gpu_id   # noqa: E731
+    everyone = ",".join(str(gid(d.id)) for d in inv.devices)
+    ctl, eng = _engine(fi, tmp_path, {}, busy_grace_s=300.0, unknown_busy_grace_s=300.0, keep_queues=True,
+                       env={"MI355X_STUB_KFD_PROC": str(proc), "MI355X_STUB_KFD_GPUIDS": everyone})
+    by_ord = _by_ordinal(eng)
+    pod = [by_ord[2], by_ord[3]]
+    eng.close()
+    ctl, eng = _engine(fi, tmp_path, {"2": "pending", "5": "pending"}, busy_grace_s=300.0,
+                       unknown_busy_grace_s=300.0, keep_queues=True,
+                       env={"MI355X_STUB_KFD_PROC": str(proc), "MI355X_STUB_KFD_GPUIDS": everyone,
+                            "MI355X_STUB_KFD_ALSO": "424242:" + ",".join(str(gid(d)) for d in pod)})
+    eng.set_activity({})
+    try:
+        for _ in range(3):
+            eng.sweep()
+        assert eng.stats()["busy_state_known"]              # the server's entry was resolved
+        assert _unhealthy(eng) == {by_ord[5]}                # idle GPU: pending is a fault
+    finally:
+        eng.close()
+
+
 def _bus_id(d):
     loc = d.location_id
     return f"{d.domain:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
