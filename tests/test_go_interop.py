@@ -580,6 +580,81 @@ def test_native_server_connection_errors(daemon_node, case, want):
         c.close()
 
 
+STREAM_CLOSED = 5
+
+
+def _headers(enc, path, method="POST", ctype="application/grpc"):
+    return enc.encode([(":method", method), (":scheme", "http"), (":path", path), (":authority", "localhost"),
+                       ("content-type", ctype), ("te", "trailers")])
+
+
+def _until(rd, dec, pred, timeout=5.0):
+    """Frames until pred(frame) holds (that frame last). Every HEADERS block is
+    decoded in arrival order (the HPACK dynamic table) and carried decoded."""
+    seen, deadline = [], time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        f = rd.read(0.2)
+        if f is None:
+            continue
+        if f[0] == gp.HEADERS:
+            f = (f[0], f[1], f[2], dec.decode(f[3]))
+        seen.append(f)
+        if pred(f):
+            return seen
+    raise AssertionError(f"no such frame in {[(x[0], x[1], x[2]) for x in seen]}")
+
+
+def _rst_code(frames, sid):
+    return [struct.unpack(">I", f[3])[0] for f in frames if f[0] == gp.RST_STREAM and f[2] == sid]
+
+
+@pytest.mark.parametrize("case", ["content-type", "get-method", "data-after-end", "zero-window-update",
+                                  "stream-window-overflow", "message-too-large"])
+def test_native_server_stream_errors_keep_the_connection(daemon_node, case):
+    """Stream-level errors (RFC 7540 5.4.2) end only their stream: the next call
+    on the same connection is answered."""
+    kdir, _, _ = daemon_node
+    s, rd = _raw(os.path.join(kdir, "amd.com_gpu"))
+    enc, dec = gp.GoHpackEncoder(), gp.HpackDecoder()
+    opts = DP + "GetDevicePluginOptions"
+    try:
+        if case == "content-type":
+            s.sendall(gp.frame(gp.HEADERS, gp.END_HEADERS | gp.END_STREAM, 1, _headers(enc, opts, ctype="text/plain")))
+            fr = _until(rd, dec, lambda f: f[0] == gp.HEADERS and f[2] == 1)
+            assert fr[-1][1] & gp.END_STREAM and (":status", "415") in fr[-1][3]
+        elif case == "get-method":
+            s.sendall(gp.frame(gp.HEADERS, gp.END_HEADERS | gp.END_STREAM, 1, _headers(enc, opts, method="GET")))
+            assert _rst_code(_until(rd, dec, lambda f: f[0] == gp.RST_STREAM), 1) == [gp.PROTOCOL_ERROR]
+        elif case == "data-after-end":
+            s.sendall(gp.frame(gp.HEADERS, gp.END_HEADERS, 1, _headers(enc, opts)) +
+                      gp.frame(gp.DATA, gp.END_STREAM, 1, gp.grpc_message(b"")) +
+                      gp.frame(gp.DATA, 0, 1, gp.grpc_message(b"late")))
+            assert STREAM_CLOSED in _rst_code(_until(rd, dec, lambda f: f[0] == gp.RST_STREAM), 1)
+        elif case in ("zero-window-update", "stream-window-overflow"):
+            _open_lw(s, 1)
+            _until(rd, dec, lambda f: f[0] == gp.DATA and f[2] == 1)        # the list is streaming
+            inc = 0 if case == "zero-window-update" else gp.MAX_WINDOW
+            s.sendall(gp.frame(gp.WINDOW_UPDATE, 0, 1, struct.pack(">I", inc)))
+            want = gp.PROTOCOL_ERROR if inc == 0 else gp.FLOW_CONTROL_ERROR
+            assert _rst_code(_until(rd, dec, lambda f: f[0] == gp.RST_STREAM), 1) == [want]
+        elif case == "message-too-large":
+            # 4 MiB is the gRPC default receive limit; the server returns credit as DATA arrives
+            chunk = b"\0" * 16384
+            out = gp.frame(gp.HEADERS, gp.END_HEADERS, 1, _headers(enc, opts))
+            s.sendall(out + b"".join(gp.frame(gp.DATA, 0, 1, chunk) for _ in range(257)))
+            fr = _until(rd, dec, lambda f: f[0] == gp.RST_STREAM and f[2] == 1)
+            trailers = [f[3] for f in fr if f[0] == gp.HEADERS and f[2] == 1]
+            assert trailers and ("grpc-status", "8") in trailers[-1] and _rst_code(fr, 1) == [gp.CANCEL]
+        # the connection is still good: a call on the next stream is answered
+        s.sendall(gp.frame(gp.HEADERS, gp.END_HEADERS, 3, _headers(enc, opts)) +
+                  gp.frame(gp.DATA, gp.END_STREAM, 3, gp.grpc_message(b"")))
+        fr = _until(rd, dec, lambda f: f[0] == gp.HEADERS and f[2] == 3 and f[1] & gp.END_STREAM)
+        assert not [f for f in fr if f[0] == gp.GOAWAY]
+        assert ("grpc-status", "0") in fr[-1][3]
+    finally:
+        s.close()
+
+
 # ------------------------------------------------------------------ transport watchdog (native daemon)
 
 def _stray_clients(path):
