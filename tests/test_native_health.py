@@ -356,6 +356,13 @@ def test_exporter_list_through_a_grpc_go_exporter(tmp_path):
                      gp.GoServerConfig(continuation_chunk=4)):
         h, err = core().exporter_list(path, 5.0)
     assert err == "" and h == {"0000:05:00.0": True, "0000:15:00.0": False}
+    # no verdict from an exporter that answers nonsense or an error, or is not there
+    for answer, want in (((0, "", b"\x0a\x05ab"), "malformed GPUStateResponse from the metrics exporter"),
+                         ((14, "exporter restarting", b""), "exporter restarting")):
+        with gp.GoServer(path, {"/metricssvc.MetricsService/List": lambda m, a=answer: a}):
+            h, err = core().exporter_list(path, 5.0)
+        assert h == {} and err == want
+    assert core().exporter_list(str(tmp_path / "absent.sock"), 5.0) == ({}, "")
 
 
 # ------------------------------------------------------------------ the daemon end to end
