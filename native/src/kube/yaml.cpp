@@ -461,7 +461,8 @@ class Parser {
     for (; *p < s.size(); ++*p) {
       const char ch = s[*p];
       if (in_flow && (ch == ',' || ch == ']' || ch == '}')) break;
-      if (ch == ':' && (*p + 1 == s.size() || space(s[*p + 1]))) {
+      if (ch == ':' && (*p + 1 == s.size() || space(s[*p + 1]) ||
+                        (in_flow && (s[*p + 1] == ',' || s[*p + 1] == ']' || s[*p + 1] == '}')))) {
         if (in_flow) break;
         if (colon) *colon = true;
         break;
@@ -476,6 +477,13 @@ class Parser {
     }
     out.resize(keep);
     return out;
+  }
+
+  // a flow mapping key: a plain key is text (as in block mappings), a quoted one its unescaped value
+  static std::string flow_key(const json::Value& k, bool quoted) {
+    return k.kind == json::Value::String ? k.s
+           : k.kind == json::Value::Bool ? (k.b ? "true" : "false")
+           : k.kind == json::Value::Null && !quoted ? "null" : json::serialize(k);
   }
 
   // a value starting at s[*p]; in_flow: plain scalars end at , ] } and ": "; line breaks fold
@@ -570,10 +578,20 @@ class Parser {
           ++*p;
           return arr;
         }
+        const bool quoted_key = s[*p] == '"' || s[*p] == '\'';
         auto v = flow(s, p, no, true);
         if (!v) return std::nullopt;
-        arr.arr.push_back(std::move(*v));
         while (*p < s.size() && space(s[*p])) ++*p;
+        if (*p < s.size() && s[*p] == ':') {  // [k: v]: a single-pair mapping as the entry
+          ++*p;
+          auto val = flow(s, p, no, true);
+          if (!val) return std::nullopt;
+          json::Value pair = json::Value::object();
+          pair.set(flow_key(*v, quoted_key), std::move(*val));
+          v = std::move(pair);
+          while (*p < s.size() && space(s[*p])) ++*p;
+        }
+        arr.arr.push_back(std::move(*v));
         if (*p < s.size() && s[*p] == ',') {
           ++*p;
           continue;
@@ -602,11 +620,7 @@ class Parser {
         ++*p;
         auto v = flow(s, p, no, true);
         if (!v) return std::nullopt;
-        // a plain key is text (as in block mappings), a quoted one its unescaped value
-        std::string key = k->kind == json::Value::String ? k->s
-                          : k->kind == json::Value::Bool ? (k->b ? "true" : "false")
-                          : k->kind == json::Value::Null && !quoted_key ? "null" : json::serialize(*k);
-        obj.set(key, std::move(*v));
+        obj.set(flow_key(*k, quoted_key), std::move(*v));
         while (*p < s.size() && space(s[*p])) ++*p;
         if (*p < s.size() && s[*p] == ',') {
           ++*p;

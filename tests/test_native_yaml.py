@@ -58,6 +58,13 @@ def test_native_reader_equals_pyyaml(doc, flow, style, width, unicode):
     # comment lines indented deeper than the scalar above them end it
     "gpu:\n  device_count: 2\n    # two GPUs\n", "- x\n    # note\n", "a: b\n  c\n    # z\n",
     "a: [1,\n  # c\n  2]\n", "a: \"b\n  # c\n  d\"\n", "a: !!str \"b\n  # c\n  d\"\n", "gpu:\n  device_count: 2  # two\n      # GPUs\nx: y\n",
+    # sequence entries that are blocks, empty, or block scalars
+    "-\n  a: 1\n-\n- b\n", "- |\n  text\n  more\n- >-\n  folded\n  text\n",
+    # every double-quoted escape, an explicit indentation indicator, kept and folded blank lines
+    "a: \"\\0\\a\\b\\v\\f\\r\\e\\N\\L\\P\\x41\\u00e9\\U0001F600\\_\\ \\/\"\n", "a: |2\n   x\n  y\n",
+    "a: |+\n  x\n\n\nb: c\n", "a: >\n  one\n\n\n  two\n", "a: \"one\n\n\n  two\"\n",
+    # single-pair mappings inside flow sequences
+    "a: [b: c]\n", "a: [b: c, d, \"e\": [f: g], h:]\n", "[x: 1, y]\n", "a: {b:, c: [d:]}\n", "a: [http://x:80/y, z]\n",
 ])
 def test_hand_written_documents(text):
     assert native(text) == _stringify(yaml.safe_load(text))
