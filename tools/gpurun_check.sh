@@ -16,6 +16,7 @@
 #   asansoak  the same soak against the ASan/UBSan daemon in asan_bin/ -> gpurun_out/soak_asan.json
 #   tsansoak  2 min (SOAK_SECONDS) soak of the ThreadSanitizer daemon, every health source on, HIP containers -> gpurun_out/soak_tsan.json
 #   soak    4 min native daemon soak, every health source on, a HIP container every second -> gpurun_out/soak_native.json
+#   cov     pytest -m gpu against the gcov build in cov_bin/ -> gpurun_out/gcov (merged by tools/native_coverage.py)
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
 set -o pipefail
@@ -134,6 +135,16 @@ for s in "$@"; do
         --extra "-liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_asan.json > gpurun_out/soak_asan.log 2>&1 || { tail -c 3000 gpurun_out/soak_asan.json; exit 1; }
       tail -c 800 gpurun_out/soak_asan.json ;;
+    cov)
+      # the GPU tests against the gcov build staged in cov_bin/ (tools/native_coverage.py --no-build
+      # --stage cov_bin); the counts land under gpurun_out/gcov for --no-build --merge gpurun_out/gcov
+      step cov
+      so=(cov_bin/_native*.so)
+      GCOV_PREFIX=$PWD/gpurun_out/gcov GCOV_PREFIX_STRIP=3 MI355X_NATIVE_CORE_SO=$PWD/${so[0]} \
+      MI355X_NATIVE_DAEMON_EXE=$PWD/cov_bin/mi355x-device-plugin MI355X_NATIVE_LABELLER_EXE=$PWD/cov_bin/mi355x-node-labeller \
+        timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+        > gpurun_out/gputests_cov.log 2>&1 || { tail -40 gpurun_out/gputests_cov.log; exit 1; }
+      tail -3 gpurun_out/gputests_cov.log ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
