@@ -30,9 +30,11 @@ def merge_patch(target, patch):
 
 class FakeApiServer:
     def __init__(self, token: Optional[str] = "test-token", tls: Optional[Tuple[str, str]] = None,
-                 client_ca: Optional[str] = None):
+                 client_ca: Optional[str] = None, host: str = "127.0.0.1"):
         """tls: (cert chain PEM, key PEM) to serve HTTPS; client_ca: also require
-        a client certificate signed by this CA (kubeconfig client-certificate auth)."""
+        a client certificate signed by this CA (kubeconfig client-certificate auth);
+        host: the listen address ("::1" for an IPv6 cluster)."""
+        self.host = host
         self.token = token
         self.nodes: Dict[str, dict] = {}
         self.requests: List[Tuple[str, str, Optional[dict]]] = []
@@ -164,7 +166,14 @@ class FakeApiServer:
             def do_PUT(self):  # noqa: N802
                 self._handle("PUT")
 
-        self.httpd = ThreadingHTTPServer(("127.0.0.1", 0), Handler)
+        server_cls = ThreadingHTTPServer
+        if ":" in host:
+            import socket
+
+            class _V6(ThreadingHTTPServer):
+                address_family = socket.AF_INET6
+            server_cls = _V6
+        self.httpd = server_cls((host, 0), Handler)
         self.scheme = "http"
         if tls is not None:   # (cert chain PEM, key PEM): serve HTTPS like a real apiserver
             import ssl
@@ -183,7 +192,8 @@ class FakeApiServer:
 
     @property
     def url(self) -> str:
-        return f"{self.scheme}://127.0.0.1:{self.port}"
+        host = f"[{self.host}]" if ":" in self.host else self.host
+        return f"{self.scheme}://{host}:{self.port}"
 
     def _store(self, name: str, node: dict, event: str) -> None:
         """(lock held) bump the resourceVersion, store, notify watchers."""
@@ -240,7 +250,7 @@ class FakeApiServer:
 
 
 def tls_material(d):
-    """A CA and a server certificate for 127.0.0.1 signed by it (openssl CLI):
+    """A CA and a server certificate for 127.0.0.1 and ::1 signed by it (openssl CLI):
     (server cert, server key, CA cert) paths under directory `d`."""
     import shutil
     import subprocess
@@ -254,7 +264,7 @@ def tls_material(d):
         "-days", "2", "-subj", "/CN=test-ca")
     run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", str(d / "srv.key"), "-out", str(d / "srv.csr"),
         "-subj", "/CN=kubernetes")
-    (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1,DNS:kubernetes.default.svc\n")
+    (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1,IP:::1,DNS:kubernetes.default.svc\n")
     run("x509", "-req", "-in", str(d / "srv.csr"), "-CA", str(d / "ca.crt"), "-CAkey", str(d / "ca.key"),
         "-CAcreateserial", "-out", str(d / "srv.crt"), "-days", "2", "-extfile", str(d / "ext.cnf"))
     return str(d / "srv.crt"), str(d / "srv.key"), str(d / "ca.crt")

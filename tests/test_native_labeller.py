@@ -333,6 +333,44 @@ def test_topology_change_relabels(tmp_path):
         srv.stop()
 
 
+def test_in_cluster_over_ipv6(tmp_path):
+    """An IPv6 cluster: KUBERNETES_SERVICE_HOST=::1 becomes https://[::1]:port
+    (net.JoinHostPort, as client-go builds it) and the certificate is checked
+    against the IP; -apiserver takes a bracketed URL too."""
+    import socket
+    try:
+        socket.socket(socket.AF_INET6).bind(("::1", 0))
+    except OSError:
+        pytest.skip("no IPv6 loopback")
+    from rocm_k8s_device_plugin_amd.testing.fake_apiserver import tls_material as _tls_material
+    crt, key, ca = _tls_material(tmp_path)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="sa-token", tls=(crt, key), host="::1").start()
+    plain = FakeApiServer(token=None, host="::1").start()
+    try:
+        srv.add_node("worker-6")
+        plain.add_node("worker-6")
+        sa = tmp_path / "sa"
+        sa.mkdir()
+        (sa / "token").write_text("sa-token\n")
+        (sa / "ca.crt").write_text(open(ca).read())
+        env = dict(os.environ, KUBERNETES_SERVICE_HOST="::1", KUBERNETES_SERVICE_PORT=str(srv.port),
+                   DS_NODE_NAME="worker-6")
+        base = [EXE, "-once", "-mode", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)]
+        p = subprocess.run(base + ["-sa_dir", str(sa)], capture_output=True, text=True, timeout=60, env=env)
+        assert p.returncode == 0, p.stderr
+        assert srv.labels("worker-6")["amd.com/gpu.mode"] == "container"
+        assert plain.url.startswith("http://[::1]:")
+        p = subprocess.run(base + ["-node_name", "worker-6", "-apiserver", plain.url, "-token_file", os.devnull],
+                           capture_output=True, text=True, timeout=60,
+                           env={k: v for k, v in os.environ.items() if not k.startswith("KUBERNETES_")})
+        assert p.returncode == 0, p.stderr
+        assert plain.labels("worker-6")["amd.com/gpu.mode"] == "container"
+    finally:
+        srv.stop()
+        plain.stop()
+
+
 def test_in_cluster_https_with_the_cluster_ca(tmp_path, monkeypatch):
     from rocm_k8s_device_plugin_amd.testing.fake_apiserver import tls_material as _tls_material
     crt, key, ca = _tls_material(tmp_path)
