@@ -231,7 +231,7 @@ int device_count_limit(const std::string& config, std::string* err) {
   if (const char* e = std::getenv("AMD_GPU_DEVICE_COUNT"); e && *e) {  // surrounding blanks ignored
     char* end = nullptr;
     const long n = std::strtol(e, &end, 10);
-    while (end && std::isspace(static_cast<unsigned char>(*end))) ++end;
+    while (std::isspace(static_cast<unsigned char>(*end))) ++end;
     if (end != e && !*end && n >= 0) return static_cast<int>(n);
   }
   if (config.empty()) return -1;
