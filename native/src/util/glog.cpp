@@ -134,14 +134,16 @@ bool parse_flag(const std::string& name, const std::string& value, bool has_valu
       *err = "invalid value \"" + value + "\" for flag -v";
     return true;
   }
-  if (name == "stderrthreshold") {
+  if (name == "stderrthreshold") {  // glog's severity.Set: a name in any case, else ParseInt(value, 10, 32)
     std::string u;
     for (char c : value) u.push_back(static_cast<char>(std::toupper(static_cast<unsigned char>(c))));
-    int sev = -1;
-    for (int i = 0; i < 4; ++i)
-      if (u == kSevName[i] || u == std::to_string(i)) sev = i;
-    if (sev < 0) *err = "invalid value \"" + value + "\" for flag -stderrthreshold";
-    else o->stderrthreshold = sev;
+    int64_t sev = -1;
+    bool ok = false;
+    for (int i = 0; i < 4 && !ok; ++i)
+      if (u == kSevName[i]) sev = i, ok = true;
+    if (!ok) ok = goflag::parse_int(value, 10, 32, &sev);
+    if (!ok) *err = "invalid value \"" + value + "\" for flag -stderrthreshold";
+    else o->stderrthreshold = static_cast<int>(sev);
     return true;
   }
   if (name == "log_dir") return o->log_dir = value, true;

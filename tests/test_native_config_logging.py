@@ -132,7 +132,8 @@ def test_stderrthreshold_names_numbers_and_backtrace_at(tmp_path):
     with open(src) as f:
         line = next(i + 1 for i, s in enumerate(f) if '"Found %zu AMDGPUs"' in s)
     base = [DP, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket="]
-    for thr, info_on_stderr in (("warning", False), ("0", True), ("INFO", True), ("Error", False), ("2", False)):
+    for thr, info_on_stderr in (("warning", False), ("0", True), ("INFO", True), ("Error", False), ("2", False),
+                                ("-1", True), ("7", False)):
         logs = tmp_path / f"logs-{thr}"
         p = subprocess.run(base + ["-logtostderr=false", f"-log_dir={logs}", f"-stderrthreshold={thr}"],
                            capture_output=True, text=True, timeout=30)
