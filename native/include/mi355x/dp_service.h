@@ -14,7 +14,8 @@
 //   GetDevicePluginOptions  bytes prepared by the plugin
 //   ListAndWatch            first message = the current list (prepared bytes),
 //                           later lists pushed by the plugin on health changes
-//   PreStartContainer       empty response
+//   PreStartContainer       empty response, or (with a gate) the answer of a
+//                           check of the devices that runs off the I/O thread
 // Whatever has no prepared state (allocator disabled, Allocate mounts that
 // are created per request, tracing) goes to a fallback: the Python servicer.
 // Every call leaves an event (timing, allocator outcome, allocated IDs) in a
@@ -76,12 +77,20 @@ struct RpcEvent {
 class DevicePluginService {
  public:
   using Fallback = std::function<Reply(const std::string& method, const std::string& request)>;
+  // PreStartContainer(devices_ids): called on the I/O thread; must hand the
+  // check to another thread and call done(reply) from there exactly once
+  using PreStartGate = std::function<void(std::vector<std::string> ids, std::function<void(Reply)> done)>;
 
   DevicePluginService();
   ~DevicePluginService();
 
   // Routes /v1beta1.DevicePlugin/* on `srv` (before srv.start()).
   void attach(GrpcServer& srv);
+  // Before `srv` stops: a gate answer that arrives later is dropped (the
+  // server has answered the call UNAVAILABLE) instead of reaching another server.
+  void detach();
+  // nullptr (default): PreStartContainer answers at once, as the reference's no-op
+  void set_prestart_gate(PreStartGate g);
 
   // The fallback is fixed before the server starts.
   void set_fallback(Fallback f);
@@ -103,7 +112,17 @@ class DevicePluginService {
   void record(RpcEvent ev);
   void notify();  // eventfd, if events were recorded since the last call (I/O thread, after the writes)
 
+  // where a deferred PreStartContainer answer goes: the server attached when
+  // the call arrived (a new sink per attach; detach() / the destructor clear it)
+  struct Sink {
+    std::mutex mu;
+    GrpcServer* srv = nullptr;
+  };
+  std::optional<Reply> prestart(uint64_t call_id, const std::string& req);
+
   mutable std::mutex mu_;
+  std::shared_ptr<Sink> sink_;
+  std::shared_ptr<const PreStartGate> gate_;
   std::shared_ptr<const Fallback> fallback_;
   std::shared_ptr<const std::string> options_;
   std::shared_ptr<const HiveAllocator> alloc_;

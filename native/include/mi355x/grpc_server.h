@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <functional>
 #include <memory>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -27,6 +28,7 @@ enum GrpcStatus : int {
   kDeadlineExceeded = 4,
   kPermissionDenied = 7,
   kResourceExhausted = 8,
+  kFailedPrecondition = 9,
   kUnimplemented = 12,
   kInternal = 13,
   kUnavailable = 14,
@@ -45,6 +47,11 @@ using UnaryFn = std::function<Reply(const std::string& request)>;
 // first message and keeps the stream open for broadcast()/send()
 using StreamOpenFn = std::function<Reply(uint64_t call_id, const std::string& request)>;
 using StreamCloseFn = std::function<void(uint64_t call_id)>;
+// unary that may answer later: a reply now, or nullopt and complete(call_id, reply)
+// from any thread once the answer is known (e.g. after a GPU probe). A call the
+// client resets or whose connection ends meanwhile is forgotten; complete() then
+// returns false. Stopping the server answers a pending call UNAVAILABLE.
+using DeferrableUnaryFn = std::function<std::optional<Reply>(uint64_t call_id, const std::string& request)>;
 
 struct ServerStats {
   uint64_t connections = 0;
@@ -69,6 +76,7 @@ class GrpcServer {
   // Registration happens before start().
   void add_unary(const std::string& path, UnaryFn fn);
   void add_server_stream(const std::string& path, StreamOpenFn open, StreamCloseFn close = nullptr);
+  void add_unary_deferrable(const std::string& path, DeferrableUnaryFn fn);
   // called on the I/O thread after each round's responses are written (before start())
   void set_after_io(std::function<void()> fn);
 
@@ -84,6 +92,8 @@ class GrpcServer {
   // Returns the number of streams it was queued on.
   size_t broadcast(const std::string& path, const std::string& msg);
   bool send(uint64_t call_id, const std::string& msg);
+  // the answer of a deferred unary call (thread-safe); false when the call is gone
+  bool complete(uint64_t call_id, Reply reply);
   size_t open_streams(const std::string& path) const;
   ServerStats stats() const;
 

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 
 #include "dry_run.h"
@@ -76,8 +77,57 @@ void Daemon::shutdown() {
     }
   }
   workers_.join_all();  // every wait ends at the stop pipe
+  gate_threads_.join_all();
+  {
+    std::lock_guard<std::mutex> lk(gate_mu_);
+    gate_engine_.reset();
+  }
   if (health_) health_->close();
   reg_.stop_all();
+}
+
+void GateThreads::run(std::function<void()> fn) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto it = ts_.begin(); it != ts_.end();) {
+    if (it->second->load()) {
+      it->first.join();
+      it = ts_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  auto done = std::make_shared<std::atomic<bool>>(false);
+  ts_.emplace_back(std::thread([fn = std::move(fn), done] {
+                     fn();
+                     done->store(true);
+                   }),
+                   done);
+}
+
+void GateThreads::join_all() {
+  std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> ts;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    ts.swap(ts_);
+  }
+  for (auto& t : ts)
+    if (t.first.joinable()) t.first.join();
+}
+
+rpc::Reply prestart_verdict(health::Engine* engine, const std::vector<std::string>& ids) {
+  if (!engine) return rpc::Reply{};
+  const auto t0 = std::chrono::steady_clock::now();
+  std::string bad;
+  for (const auto& [id, o] : engine->probe_now(ids))
+    if (!o.ok && !o.pending && !o.interrupted) bad += (bad.empty() ? "" : "; ") + id + ": " + o.reason;
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  auto& m = metrics::global();
+  m.inc("mi355x_dp_prestart_checks_total", {{"result", bad.empty() ? "ok" : "failed"}}, 1.0,
+        "PreStartContainer liveness checks (-prestart_liveness)");
+  m.observe_ms("mi355x_dp_prestart_check_seconds", ms, {}, "PreStartContainer liveness check latency");
+  if (bad.empty()) return rpc::Reply{};
+  MI_LOG(kError, "PreStartContainer: MFMA liveness check failed (%s)", bad.c_str());
+  return rpc::Reply{rpc::kFailedPrecondition, "MFMA liveness check failed before the container start: " + bad, ""};
 }
 
 // ---- CDI specs (-device_list_strategy cdi-*): written before registration,
@@ -94,7 +144,11 @@ std::string Daemon::write_cdi(const std::set<std::string>& stale) {
   return e;
 }
 
-void Daemon::rebuild_health() { health_->rebuild(driver_, container_devices_, topo_, reg_.all()); }
+void Daemon::rebuild_health() {
+  health_->rebuild(driver_, container_devices_, topo_, reg_.all());
+  std::lock_guard<std::mutex> lk(gate_mu_);
+  gate_engine_ = health_->engine();
+}
 
 int Daemon::init() {
   std::string err;
@@ -104,7 +158,7 @@ int Daemon::init() {
     return 1;
   }
   if (f_.topology_view)
-    views_.topo = std::make_shared<views::TopologyViews>(path_join(f_.kubelet_dir, "mi355x-topology"),
+    serve_.topo = std::make_shared<views::TopologyViews>(path_join(f_.kubelet_dir, "mi355x-topology"),
                                                          path_join(f_.sysfs_root, "class/kfd/kfd/topology"));
   if (f_.node_view) {  // built at start-up, not inside the first Allocate
     auto nv = std::make_shared<views::NodeView>(path_join(f_.kubelet_dir, "mi355x-node"), f_.sysfs_root,
@@ -113,15 +167,26 @@ int Daemon::init() {
       MI_LOG(kWarning, "node view unavailable: %s", e.c_str());
     } else {
       MI_LOG(kInfo, "node view: %d links, %d per-CPU cache directories left out", nv->links, nv->hidden);
-      views_.node = nv;
+      serve_.node = nv;
     }
   }
+  if (f_.prestart_liveness)  // runs on the RPC thread: the probe goes to a gate thread
+    serve_.prestart = [this](std::vector<std::string> ids, std::function<void(rpc::Reply)> done) {
+      std::shared_ptr<health::Engine> engine;
+      {
+        std::lock_guard<std::mutex> lk(gate_mu_);
+        engine = gate_engine_;
+      }
+      gate_threads_.run([engine, ids = std::move(ids), done = std::move(done)] {
+        done(prestart_verdict(engine.get(), ids));
+      });
+    };
   // explicit -driver_type: exit 1 when it cannot start (main.go:94-105); else
   // container -> VF -> PF, and with none the manager still starts and idles (main.go:106-119)
   NodeInventory inv;
   if (!f_.driver_type.empty()) {
     const Driver drv = driver_from_name(f_.driver_type);
-    const std::string e = init_driver(f_, drv, dev_limit_, views_, &inv);
+    const std::string e = init_driver(f_, drv, dev_limit_, serve_, &inv);
     if (!e.empty()) {
       MI_LOG(kError, "Error instantiating driver type %s: %s", f_.driver_type.c_str(), e.c_str());
       return 1;
@@ -130,7 +195,7 @@ int Daemon::init() {
     bool found = false;
     for (Driver drv : {Driver::Container, Driver::Vf, Driver::Pf}) {
       NodeInventory got;
-      const std::string e = init_driver(f_, drv, dev_limit_, views_, &got);
+      const std::string e = init_driver(f_, drv, dev_limit_, serve_, &got);
       if (!e.empty()) {
         MI_LOG(kWarning, "%s implementation failed: %s. Trying next...", driver_name(drv), e.c_str());
         continue;
@@ -357,7 +422,7 @@ std::string Daemon::watchdog() {
 
 void Daemon::reload_topology(const std::string& sig) {
   NodeInventory inv;
-  const std::string e = init_container(f_, dev_limit_, views_, &inv);
+  const std::string e = init_container(f_, dev_limit_, serve_, &inv);
   topo_state_.applied(sig);
   std::map<std::string, std::string> before, after;  // device id -> partition type
   std::string old_names, new_names;

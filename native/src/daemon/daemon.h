@@ -23,9 +23,14 @@
 
 #include <signal.h>
 
+#include <atomic>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "flags.h"
@@ -47,6 +52,25 @@ struct Completion {
   std::string message;
   // kSweep
   SweepResult sweep;
+};
+
+// -prestart_liveness: PreStartContainer's answer from a probe of the
+// container's devices now (blocking; a gate thread). FAILED_PRECONDITION names
+// each device with a definite fault; a pending or interrupted probe, or a
+// device the probe server cannot reach, does not hold the container back.
+rpc::Reply prestart_verdict(health::Engine* engine, const std::vector<std::string>& ids);
+
+// The threads PreStartContainer checks run on (one per check, off the RPC
+// thread): finished ones are joined when the next starts, the rest at shutdown.
+class GateThreads {
+ public:
+  ~GateThreads() { join_all(); }
+  void run(std::function<void()> fn);
+  void join_all();
+
+ private:
+  std::mutex mu_;
+  std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> ts_;
 };
 
 // Register{version=1, endpoint=2, resource_name=3, options=4} on kubelet.sock (blocking; worker thread)
@@ -89,7 +113,7 @@ class Daemon {
 
   Flags f_;
   int dev_limit_ = -1;
-  ViewCtx views_;
+  ServeCtx serve_;
   bool impl_ok_ = true;
   Driver driver_ = Driver::Container;
   KfdTopology topo_;
@@ -99,6 +123,10 @@ class Daemon {
   int stop_pipe_[2] = {-1, -1};  // ends every wait of the workers (peer calls, probes)
   std::unique_ptr<HealthController> health_;
   Workers<Completion> workers_;
+  // -prestart_liveness: the engine the gate probes with (read on RPC threads)
+  std::mutex gate_mu_;
+  std::shared_ptr<health::Engine> gate_engine_;
+  GateThreads gate_threads_;
   // kubelet
   std::string kubelet_sock_;
   DirWatcher watch_;

@@ -16,7 +16,7 @@ std::string usage(const std::string& argv0) {
          "[-allocator_extended_search] [-grpc_watchdog S] [-reregister S] [-register_timeout S] [-config FILE] "
          "[-metrics_port N] [-topology_watch S] "
          "[-device_list_strategy device-specs|cdi-cri|cdi-annotations[,...]] [-cdi_spec_dir DIR] "
-         "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-liveness_timeout S] "
+         "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-prestart_liveness] [-liveness_timeout S] "
          "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
          "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
          "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
@@ -35,6 +35,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, 
   std::map<std::string, bool*> bools = {
       {"send_every_pulse", &f->send_every_pulse}, {"allocator_extended_search", &f->allocator_extended_search},
       {"liveness", &f->liveness}, {"liveness_keep_queues", &f->liveness_keep_queues},
+      {"prestart_liveness", &f->prestart_liveness},
       {"liveness_corroborate", &f->liveness_corroborate}, {"smi_ecc", &f->smi_ecc}, {"smi_events", &f->smi_events},
       {"smi_xgmi", &f->smi_xgmi}, {"dry_run", &f->dry_run}, {"node_view", &f->node_view},
       {"topology_view", &f->topology_view}};
@@ -136,6 +137,8 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, 
            false;
   if (f->allocator_extended_search) f->allocator_search = "extended";
   if (f->liveness && f->pulse == 0) return *err = "-liveness needs -pulse > 0 (the probe runs once per pulse)", false;
+  if (f->prestart_liveness && !f->liveness)
+    return *err = "prestart_liveness needs -liveness (the check runs in the probe server)", false;
   if (f->perf_action != "report" && f->perf_action != "unhealthy")
     return *err = "invalid perf_action provided: " + f->perf_action + ", supported values are report or unhealthy",
            false;

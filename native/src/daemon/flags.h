@@ -31,6 +31,9 @@ struct Flags {
   bool liveness = false;
   std::string liveness_mode = "persistent";
   bool liveness_keep_queues = true;
+  // PreStartContainer probes the container's GPUs (through the probe server) and
+  // fails the start on a definite fault; needs -liveness
+  bool prestart_liveness = false;
   double liveness_timeout = 10.0;
   int liveness_iters = 4;
   int liveness_fail_threshold = 2;

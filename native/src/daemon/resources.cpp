@@ -61,7 +61,7 @@ std::string mount_field(const std::string& host, const std::string& ctr) {
 
 // the container DeviceImpl's Start/GetOptions/Allocate state (amdgpu.go:90-119,165-177,255-297)
 void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& unresolved, const std::string& search,
-             const cdi::Strategies& lists, const ViewCtx& vc) {
+             const cdi::Strategies& lists, const ServeCtx& vc) {
   // allocator (BestEffortPolicy.init); on failure kubelet allocates by itself
   bool alloc_ok = true;
   for (const auto& d : r.devices)
@@ -81,6 +81,7 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
     }
   }
   r.options.clear();
+  if (vc.prestart) pb::put_bool(&r.options, 1, true);  // pre_start_required
   if (alloc_ok) pb::put_bool(&r.options, 2, true);  // get_preferred_allocation_available
   // ContainerAllocateResponse{devices=3 (DeviceSpec), annotations=4, cdi_devices=5 (CDIDevice{name=1})}
   rpc::AllocateTemplate t;
@@ -129,6 +130,7 @@ void prepare(Resource& r, const KfdTopology& topo, const std::set<std::string>& 
     return rpc::Reply{rpc::kUnimplemented, "not served by the native daemon: " + method + " (" + name + ")", ""};
   });
   r.service->set_options(r.options);
+  r.service->set_prestart_gate(vc.prestart);
   if (r.allocator) r.service->set_allocator(r.allocator);
   r.service->set_allocate_template(t);
   r.tmpl = t;
@@ -264,7 +266,7 @@ std::vector<GpuDevice> limit_physical(const std::vector<GpuDevice>& devs, int li
 }
 
 // NewGPUKFDImpl + Init + GetResourceNames (amdgpu.go:56-162)
-std::string init_container(const Flags& f, int dev_limit, const ViewCtx& vc, NodeInventory* out) {
+std::string init_container(const Flags& f, int dev_limit, const ServeCtx& vc, NodeInventory* out) {
   out->driver = Driver::Container;
   if (!is_dir(path_join(f.sysfs_root, "class/kfd"))) return "No kfd found (" + f.sysfs_root + "/class/kfd)";
   out->topo = KfdTopology::load_sysfs(f.sysfs_root);
@@ -345,7 +347,7 @@ std::string init_passthrough(const Flags& f, Driver drv, NodeInventory* out) {
   return "";
 }
 
-std::string init_driver(const Flags& f, Driver drv, int dev_limit, const ViewCtx& vc, NodeInventory* out) {
+std::string init_driver(const Flags& f, Driver drv, int dev_limit, const ServeCtx& vc, NodeInventory* out) {
   if (drv == Driver::Container) return init_container(f, dev_limit, vc, out);
   return init_passthrough(f, drv, out);
 }
@@ -375,6 +377,7 @@ bool ResourceRegistry::start_server(size_t i, Clock::time_point now) {
 void ResourceRegistry::stop_server(size_t i) {
   Resource& r = rs_.at(i);
   if (r.server) {
+    if (r.service) r.service->detach();  // a PreStartContainer answer still on its way is dropped
     r.server->stop(0.5);
     r.server.reset();
     ::unlink(r.socket.c_str());

@@ -32,9 +32,13 @@ const char* driver_name(Driver d);
 Driver driver_from_name(const std::string& name);  // container | vf-passthrough | pf-passthrough
 
 // the opt-in container start-up views (mi355x/views.h)
-struct ViewCtx {
+// What a container resource's service gets from the daemon besides its devices:
+// the start-up views its Allocate returns as mounts, and the PreStartContainer
+// check (-prestart_liveness; set: the options ask kubelet for PreStartContainer)
+struct ServeCtx {
   std::shared_ptr<views::NodeView> node;
   std::shared_ptr<views::TopologyViews> topo;
+  rpc::DevicePluginService::PreStartGate prestart;
 };
 
 struct Resource {
@@ -81,9 +85,9 @@ int device_count_limit(const std::string& config, std::string* err);
 std::vector<GpuDevice> limit_physical(const std::vector<GpuDevice>& devs, int limit);
 
 // One driver's resources: "" on success (no resources = no devices), else the init error.
-std::string init_container(const Flags& f, int dev_limit, const ViewCtx& vc, NodeInventory* out);
+std::string init_container(const Flags& f, int dev_limit, const ServeCtx& vc, NodeInventory* out);
 std::string init_passthrough(const Flags& f, Driver drv, NodeInventory* out);
-std::string init_driver(const Flags& f, Driver drv, int dev_limit, const ViewCtx& vc, NodeInventory* out);
+std::string init_driver(const Flags& f, Driver drv, int dev_limit, const ServeCtx& vc, NodeInventory* out);
 
 // What a topology reload changed (ResourceRegistry::apply_reload).
 struct ReloadPlan {

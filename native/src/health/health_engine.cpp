@@ -578,7 +578,28 @@ bool Engine::publish(Reasons reasons) {
 }
 
 // One sweep: every source adds its reasons; a device with none is Healthy.
+std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::string>& ids) {
+  std::lock_guard<std::mutex> op(op_mu_);
+  if (!cfg_.liveness || !prober_) return {};
+  trace::Span span("liveness.prestart", "health", {{"devices", std::to_string(ids.size())}});
+  std::map<std::string, int> sel;
+  const auto& ords = ordinals();
+  for (const auto& id : ids)
+    if (auto it = ords.find(id); it != ords.end()) sel[id] = it->second;
+  if (sel.empty()) return {};
+  std::vector<int> uniq;
+  for (const auto& [id, o] : sel) uniq.push_back(o);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  const auto by_ord = prober_->probe(uniq, {}, "probe");
+  std::map<std::string, ProbeOutcome> raw;
+  for (const auto& [id, o] : sel)
+    if (auto it = by_ord.find(o); it != by_ord.end()) raw[id] = it->second;
+  return verify_identity(sel, raw);
+}
+
 bool Engine::sweep() {
+  std::lock_guard<std::mutex> op(op_mu_);
   trace::Span span("health.sweep", "health", {{"devices", std::to_string(devices_.size())}});
   const double t0 = mono_s();
   Reasons reasons;

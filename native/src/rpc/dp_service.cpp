@@ -115,7 +115,65 @@ const char* DevicePluginService::path(const char* method) {
 DevicePluginService::DevicePluginService() { evfd_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC); }
 
 DevicePluginService::~DevicePluginService() {
+  detach();
   if (evfd_ >= 0) ::close(evfd_);
+}
+
+void DevicePluginService::detach() {
+  std::shared_ptr<Sink> s;  // outlives the lock on its mutex below
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    s.swap(sink_);
+  }
+  if (!s) return;
+  std::lock_guard<std::mutex> sk(s->mu);  // waits out an answer being delivered
+  s->srv = nullptr;
+}
+
+void DevicePluginService::set_prestart_gate(PreStartGate g) {
+  std::lock_guard<std::mutex> lk(mu_);
+  gate_ = g ? std::make_shared<const PreStartGate>(std::move(g)) : nullptr;
+}
+
+std::optional<Reply> DevicePluginService::prestart(uint64_t call_id, const std::string& req) {
+  RpcEvent ev;
+  ev.rpc = "PreStartContainer";
+  ev.t0_ns = mono_ns();
+  std::vector<std::string> ids;
+  const bool ok = pb::scan(
+      req.data(), req.size(),
+      [&](int f, const char* p, size_t n) {
+        if (f == 1) ids.emplace_back(p, n);
+        return true;
+      },
+      nullptr);
+  std::shared_ptr<const PreStartGate> gate;
+  std::shared_ptr<Sink> sink;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (native_) gate = gate_;
+    sink = sink_;
+  }
+  ev.ids = ids;
+  auto now = [&](Reply r) {
+    ev.dur_ns = mono_ns() - ev.t0_ns;
+    ev.status = r.status;
+    ev.message = r.message;
+    record(std::move(ev));
+    return r;
+  };
+  if (!ok) return now(Reply{kInternal, "malformed PreStartContainerRequest", ""});
+  if (!gate || !sink || ids.empty()) return now(Reply{kOk, "", ""});
+  (*gate)(std::move(ids), [this, sink, call_id, ev](Reply r) mutable {
+    std::lock_guard<std::mutex> lk(sink->mu);
+    if (!sink->srv) return;  // detached: the call was answered UNAVAILABLE at stop (this service may be gone)
+    ev.dur_ns = mono_ns() - ev.t0_ns;
+    ev.status = r.status;
+    ev.message = r.message;
+    record(std::move(ev));
+    sink->srv->complete(call_id, std::move(r));
+  });
+  return std::nullopt;
 }
 
 void DevicePluginService::set_fallback(Fallback f) {
@@ -310,6 +368,12 @@ Reply DevicePluginService::allocate(const std::string& req, RpcEvent* ev) {
 }
 
 void DevicePluginService::attach(GrpcServer& srv) {
+  detach();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    sink_ = std::make_shared<Sink>();
+    sink_->srv = &srv;
+  }
   srv.set_after_io([this] { notify(); });
   auto wrap = [this](const char* method, std::function<Reply(const std::string&, RpcEvent*)> fn) {
     return [this, method, fn](const std::string& req) {
@@ -338,8 +402,8 @@ void DevicePluginService::attach(GrpcServer& srv) {
                      [this](const std::string& req, RpcEvent* ev) { return preferred(req, ev); }));
   srv.add_unary(path("Allocate"),
                 wrap("Allocate", [this](const std::string& req, RpcEvent* ev) { return allocate(req, ev); }));
-  srv.add_unary(path("PreStartContainer"),
-                wrap("PreStartContainer", [](const std::string&, RpcEvent*) { return Reply{kOk, "", ""}; }));
+  srv.add_unary_deferrable(path("PreStartContainer"),
+                           [this](uint64_t call_id, const std::string& req) { return prestart(call_id, req); });
   srv.add_server_stream(path("ListAndWatch"), [this](uint64_t, const std::string& req) {
     RpcEvent ev;
     ev.rpc = "ListAndWatch";

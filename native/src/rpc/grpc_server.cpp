@@ -52,6 +52,7 @@ struct Stream {
   bool trailers_queued = false;
   std::string trailers;  // header block sent (END_STREAM) once `out` has drained
   bool streaming = false;
+  bool deferred = false;  // a deferrable unary call waiting for complete()
   uint64_t call_id = 0;
   bool finished = false;
 };
@@ -84,6 +85,7 @@ struct GrpcServer::Impl {
   struct Route {
     bool streaming = false;
     UnaryFn unary;
+    DeferrableUnaryFn deferrable;
     StreamOpenFn open;
     StreamCloseFn close;
   };
@@ -91,11 +93,13 @@ struct GrpcServer::Impl {
     int fd;
     uint32_t sid;
     std::string route;
+    bool deferred = false;  // a deferrable unary call, not a stream
   };
   struct Outgoing {
     std::string route;  // broadcast to every stream of this route ("" = one call)
     uint64_t call_id;
     std::string msg;
+    std::optional<Reply> reply;  // the answer of a deferred unary call
   };
 
   std::unordered_map<std::string, Route> routes;
@@ -202,7 +206,7 @@ struct GrpcServer::Impl {
   void finish_stream(Conn& c, uint32_t sid) {
     auto it = c.streams.find(sid);
     if (it == c.streams.end()) return;
-    if (it->second.streaming) end_call(it->second.call_id);
+    if (it->second.streaming || it->second.deferred) end_call(it->second.call_id);
     c.streams.erase(it);
   }
 
@@ -278,11 +282,39 @@ struct GrpcServer::Impl {
       pump(c, s);
       return;
     }
-    try {
-      rep = r->second.unary(req);
-    } catch (const std::exception& e) {
-      rep = Reply{kUnknown, e.what(), ""};
+    if (r->second.deferrable) {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        call_id = next_call++;
+        calls[call_id] = CallRef{c.fd, s.id, s.path, true};
+      }
+      s.deferred = true;
+      s.call_id = call_id;
+      std::optional<Reply> now;
+      try {
+        now = r->second.deferrable(call_id, req);
+      } catch (const std::exception& e) {
+        now = Reply{kUnknown, e.what(), ""};
+      }
+      if (!now) return;  // complete(call_id, ...) answers it
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        calls.erase(call_id);
+      }
+      s.deferred = false;
+      rep = std::move(*now);
+    } else {
+      try {
+        rep = r->second.unary(req);
+      } catch (const std::exception& e) {
+        rep = Reply{kUnknown, e.what(), ""};
+      }
     }
+    answer(c, s, rep);
+  }
+
+  // a unary call's response: headers, the message and OK trailers, or trailers only
+  void answer(Conn& c, Stream& s, const Reply& rep) {
     if (rep.status != kOk) return trailers_only(c, s, rep.status, rep.message);
     send_headers(c, s.id, response_headers(), false);
     queue_message(c, s, rep.body);
@@ -630,6 +662,25 @@ struct GrpcServer::Impl {
       todo.swap(outbox);
     }
     for (auto& o : todo) {
+      if (o.reply) {  // a deferred unary call's answer
+        CallRef ref{};
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          auto it = calls.find(o.call_id);
+          if (it == calls.end()) continue;  // reset or its connection ended meanwhile
+          ref = it->second;
+          calls.erase(it);
+        }
+        auto ci = conns.find(ref.fd);
+        if (ci == conns.end()) continue;
+        Conn& c = *ci->second;
+        auto si = c.streams.find(ref.sid);
+        if (si == c.streams.end() || !si->second.deferred) continue;
+        si->second.deferred = false;
+        answer(c, si->second, *o.reply);
+        if (pump(c, si->second) || si->second.finished) finish_stream(c, ref.sid);
+        continue;
+      }
       targets.clear();
       {
         std::lock_guard<std::mutex> lk(mu);
@@ -638,7 +689,7 @@ struct GrpcServer::Impl {
           if (it != calls.end()) targets.emplace_back(it->first, it->second);
         } else {
           for (auto& [id, ref] : calls)
-            if (ref.route == o.route) targets.emplace_back(id, ref);
+            if (!ref.deferred && ref.route == o.route) targets.emplace_back(id, ref);
         }
       }
       for (auto& [id, ref] : targets) {
@@ -646,7 +697,7 @@ struct GrpcServer::Impl {
         if (ci == conns.end()) continue;
         Conn& c = *ci->second;
         auto si = c.streams.find(ref.sid);
-        if (si == c.streams.end() || si->second.trailers_queued) continue;
+        if (si == c.streams.end() || si->second.trailers_queued || si->second.deferred) continue;
         queue_message(c, si->second, o.msg);
         if (pump(c, si->second)) finish_stream(c, ref.sid);
       }
@@ -666,6 +717,14 @@ struct GrpcServer::Impl {
           s.trailers = trailer_block(kOk, "", false);
           s.trailers_queued = true;
           if (pump(*c, s)) done.push_back(sid);
+        } else if (s.deferred && !s.finished) {  // a deferred answer that will not come
+          s.deferred = false;
+          trailers_only(*c, s, kUnavailable, "server stopping");
+          done.push_back(sid);
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            calls.erase(s.call_id);
+          }
         }
       }
       for (uint32_t sid : done) finish_stream(*c, sid);
@@ -756,6 +815,12 @@ void GrpcServer::add_server_stream(const std::string& path, StreamOpenFn open, S
   impl_->routes[path] = std::move(r);
 }
 
+void GrpcServer::add_unary_deferrable(const std::string& path, DeferrableUnaryFn fn) {
+  Impl::Route r;
+  r.deferrable = std::move(fn);
+  impl_->routes[path] = std::move(r);
+}
+
 std::string GrpcServer::start(const std::string& unix_path) {
   if (running_.load()) return "already running";
   Impl& I = *impl_;
@@ -823,7 +888,7 @@ size_t GrpcServer::broadcast(const std::string& path, const std::string& msg) {
   {
     std::lock_guard<std::mutex> lk(I.mu);
     if (!running_.load()) return 0;
-    for (auto& [id, ref] : I.calls) n += ref.route == path;
+    for (auto& [id, ref] : I.calls) n += !ref.deferred && ref.route == path;
     if (!n) return 0;
     I.outbox.push_back(Impl::Outgoing{path, 0, msg});
   }
@@ -842,10 +907,21 @@ bool GrpcServer::send(uint64_t call_id, const std::string& msg) {
   return true;
 }
 
+bool GrpcServer::complete(uint64_t call_id, Reply reply) {
+  Impl& I = *impl_;
+  {
+    std::lock_guard<std::mutex> lk(I.mu);
+    if (!running_.load() || !I.calls.count(call_id)) return false;
+    I.outbox.push_back(Impl::Outgoing{"", call_id, "", std::move(reply)});
+  }
+  I.wake();
+  return true;
+}
+
 size_t GrpcServer::open_streams(const std::string& path) const {
   std::lock_guard<std::mutex> lk(impl_->mu);
   size_t n = 0;
-  for (auto& [id, ref] : impl_->calls) n += path.empty() || ref.route == path;
+  for (auto& [id, ref] : impl_->calls) n += !ref.deferred && (path.empty() || ref.route == path);
   return n;
 }
 

@@ -6,8 +6,12 @@
 //
 // Reference fixtures are optional: missing => those cases are skipped.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
+#include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <thread>
@@ -278,6 +282,7 @@ std::string request(uint32_t sid, const std::string& path, const std::string& ms
 }
 struct Result {
   int grpc_status = -1;
+  std::string grpc_message;
   std::vector<std::string> messages;
 };
 // reads frames until END_STREAM on `sid`
@@ -301,8 +306,10 @@ bool read_call(int fd, uint32_t sid, Result* r, mi355x::rpc::HpackDecoder* dec, 
       if (type == 1) {
         mi355x::rpc::HeaderList hl;
         if (!dec->decode(reinterpret_cast<const uint8_t*>(p.data()), p.size(), &hl)) return false;
-        for (auto& [k, v] : hl)
+        for (auto& [k, v] : hl) {
           if (k == "grpc-status") r->grpc_status = std::atoi(v.c_str());
+          if (k == "grpc-message") r->grpc_message = v;
+        }
       } else if (type == 0) {
         data += p;
         while (data.size() >= 5) {
@@ -403,6 +410,106 @@ static void test_grpc_server() {
   h2t::Result r7;
   CHECK(h2t::read_call(fd, 9, &r7, &dec) && r7.grpc_status == 0);
   CHECK(svc.drain_events().size() == 4);  // options, 2x Allocate, ListAndWatch (unknown methods are not service calls)
+  ::close(fd);
+  ::unlink(sock.c_str());
+  ::rmdir(dir);
+}
+
+// PreStartContainer with a gate: the answer comes from another thread later;
+// calls on the same connection are answered meanwhile; a stopping server
+// answers a check still running UNAVAILABLE and drops its late answer.
+static void test_grpc_deferred_prestart() {
+  using namespace mi355x::rpc;
+  char tmpl[] = "/tmp/mi355x-rpc-XXXXXX";
+  const char* dir = ::mkdtemp(tmpl);
+  if (!dir) {
+    ++g_skip;
+    return;
+  }
+  const std::string sock = std::string(dir) + "/dp.sock";
+  GrpcServer srv;
+  DevicePluginService svc;
+  svc.attach(srv);
+  svc.set_options(std::string("\x08\x01", 2));  // pre_start_required
+  std::vector<std::thread> gates;
+  std::mutex held_mu;
+  std::vector<std::function<void(Reply)>> held;  // checks that finish only when the test says
+  svc.set_prestart_gate([&](std::vector<std::string> ids, std::function<void(Reply)> done) {
+    if (ids.size() == 1 && ids[0] == "hold") {
+      std::lock_guard<std::mutex> lk(held_mu);
+      held.push_back(std::move(done));
+      return;
+    }
+    gates.emplace_back([ids, done = std::move(done)] {
+      std::this_thread::sleep_for(std::chrono::milliseconds(200));
+      done(ids[0] == "bad" ? Reply{kFailedPrecondition, "bad GPU", ""} : Reply{});
+    });
+  });
+  CHECK(srv.start(sock).empty());
+  const int fd = h2t::connect_unix(sock);
+  CHECK(fd >= 0);
+  if (fd < 0) return;
+  HpackDecoder dec;
+  auto req = [](const std::string& id) {
+    std::string r;
+    pb::put_bytes(&r, 1, id);
+    return r;
+  };
+  auto send = [&](uint32_t sid, const char* method, const std::string& msg) {
+    const std::string q = h2t::request(sid, DevicePluginService::path(method), msg);
+    return ::write(fd, q.data(), q.size()) == static_cast<ssize_t>(q.size());
+  };
+  // a check in flight, and GetDevicePluginOptions on the next stream answered first
+  CHECK(send(1, "PreStartContainer", req("a")) && send(3, "GetDevicePluginOptions", ""));
+  std::vector<uint32_t> order;  // streams in the order they ended
+  std::map<uint32_t, int> status;
+  {
+    std::string buf;
+    char tmp[4096];
+    while (order.size() < 2) {
+      while (buf.size() >= 9) {
+        const auto* f = reinterpret_cast<const uint8_t*>(buf.data());
+        const size_t len = (size_t(f[0]) << 16) | (size_t(f[1]) << 8) | f[2];
+        if (buf.size() < 9 + len) break;
+        const uint32_t sid = ((f[5] & 0x7f) << 24) | (f[6] << 16) | (f[7] << 8) | f[8];
+        if (f[3] == 1) {  // HEADERS: every block decoded in order
+          HeaderList hl;
+          CHECK(dec.decode(f + 9, len, &hl));
+          for (auto& [k, v] : hl)
+            if (k == "grpc-status") status[sid] = std::atoi(v.c_str());
+        }
+        if ((f[3] == 0 || f[3] == 1) && (f[4] & 1)) order.push_back(sid);
+        buf.erase(0, 9 + len);
+      }
+      if (order.size() >= 2) break;
+      const ssize_t n = ::read(fd, tmp, sizeof(tmp));
+      if (n <= 0) break;
+      buf.append(tmp, static_cast<size_t>(n));
+    }
+  }
+  CHECK(order == (std::vector<uint32_t>{3, 1}) && status[3] == 0 && status[1] == 0);
+  CHECK(send(5, "PreStartContainer", req("bad")));
+  h2t::Result b;
+  CHECK(h2t::read_call(fd, 5, &b, &dec) && b.grpc_status == kFailedPrecondition && b.grpc_message == "bad GPU");
+  // a check that outlives the server: UNAVAILABLE at stop; its late answer goes nowhere
+  CHECK(send(7, "PreStartContainer", req("hold")));
+  for (int i = 0; i < 200; ++i) {
+    {
+      std::lock_guard<std::mutex> lk(held_mu);
+      if (!held.empty()) break;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  svc.detach();
+  srv.stop(0.5);
+  h2t::Result h;
+  CHECK(h2t::read_call(fd, 7, &h, &dec) && h.grpc_status == kUnavailable);
+  {
+    std::lock_guard<std::mutex> lk(held_mu);
+    CHECK(held.size() == 1);
+    for (auto& d : held) d(Reply{});  // after detach: dropped, nothing touches the stopped server
+  }
+  for (auto& t : gates) t.join();
   ::close(fd);
   ::unlink(sock.c_str());
   ::rmdir(dir);
@@ -895,6 +1002,7 @@ int main(int argc, char** argv) {
   test_degraded_links(ref);
   test_hpack();
   test_grpc_server();
+  test_grpc_deferred_prestart();
   test_fuzz_rpc(ref);
   test_registration_generations();
   test_registration_watchdog();

@@ -50,6 +50,7 @@ class Admission:
     allocate_ms: float
     total_ms: float
     preferred_used: bool
+    prestart_ms: float = 0.0   # PreStartContainer, when the plugin's options require it
 
 
 class NativeRpcError(grpc.RpcError):
@@ -247,11 +248,19 @@ class FakeKubelet:
         aresp = await self._call(st, "Allocate", areq, pb.AllocateResponse)
         t2 = time.perf_counter()
         st.allocated.update(chosen)
-        return Admission(resource, chosen, aresp, pref_ms, (t2 - t1) * 1e3, (t2 - t0) * 1e3, used)
+        pre_ms = 0.0
+        if st.options.pre_start_required:
+            # kubelet's devicemanager before the container is created (its timeout: 30 s);
+            # an error fails the container start
+            await self._call(st, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=chosen),
+                             pb.PreStartContainerResponse, timeout=30.0)
+            pre_ms = (time.perf_counter() - t2) * 1e3
+        t3 = time.perf_counter()
+        return Admission(resource, chosen, aresp, pref_ms, (t2 - t1) * 1e3, (t3 - t0) * 1e3, used, pre_ms)
 
-    async def _call(self, st: ResourceState, method: str, req, resp_type):
+    async def _call(self, st: ResourceState, method: str, req, resp_type, timeout: float = 10.0):
         if self.rpc_client == "aio":
-            return await getattr(st.stub, method)(req, timeout=10)
+            return await getattr(st.stub, method)(req, timeout=timeout)
         if st.native is None:
             from ..ops.native import core
             st.native = core().GrpcClient()
@@ -261,9 +270,9 @@ class FakeKubelet:
                 raise NativeRpcError(-1, err)
         path, data = f"/{pb.PACKAGE}.DevicePlugin/{method}", req.SerializeToString()
         if self.rpc_client == "native-thread":
-            status, msg, body = await asyncio.to_thread(st.native.unary, path, data, 10.0)
+            status, msg, body = await asyncio.to_thread(st.native.unary, path, data, timeout)
         else:
-            status, msg, body = st.native.unary(path, data, 10.0)
+            status, msg, body = st.native.unary(path, data, timeout)
         if status != 0:
             if status < 0:
                 st.native.close()

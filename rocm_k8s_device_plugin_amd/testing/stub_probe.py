@@ -7,7 +7,8 @@ per ROCr ordinal comes from the JSON file named by $MI355X_STUB_PROBE_CONTROL
 ``{"0": "ok", "3": "fail", "5": "hang", "6": "stale", "7": "garbage"}``
 (missing ordinals are "ok"; "serve": "broken" makes --serve fail to start,
 "serve": "slow_start" delays its hello by "serve_start_s" seconds;
-"server_fail" fails only inside --serve: a stale server runtime).
+"server_fail" fails only inside --serve: a stale server runtime; "slow" answers ok
+after "slow_s" seconds, in --serve).
 Exercises the real LivenessProber code path: process spawn, server protocol,
 deadline kill, fallback to per-device isolation, output parsing, nonce check,
 hysteresis. Each start appends a line to $MI355X_STUB_PROBE_LOG if set.
@@ -130,6 +131,9 @@ def serve():
                 mode = "fail"
             if mode == "hang":
                 time.sleep(3600)
+            if mode == "slow":   # a verdict that takes "slow_s" seconds, then ok
+                time.sleep(float(ctl.get("slow_s", 1.0)))
+                mode = "ok"
             if mode == "garbage":
                 print("segfault-ish noise", flush=True)
                 return 139

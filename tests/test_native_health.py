@@ -424,6 +424,117 @@ def test_daemon_liveness_verdicts_reach_listandwatch(tmp_path):
     asyncio.run(asyncio.wait_for(go(), 90))
 
 
+def test_prestart_liveness_gate(tmp_path):
+    """-prestart_liveness: the options ask kubelet for PreStartContainer, which
+    probes the container's GPUs through the probe server right before the start
+    and fails it (FAILED_PRECONDITION, naming the device) on a definite fault.
+    The check runs off the RPC thread: a slow one holds back no other call."""
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import NativeRpcError
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text("{}")
+    kdir = str(tmp_path / "dp")
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = {o: d for d, o in eng.ordinals().items()}
+    eng.close()
+    bad = subprocess.run([EXE, "-dry_run", "-sysfs_root", str(fi.sysfs), "-prestart_liveness"],
+                         capture_output=True, text=True, timeout=30)
+    assert bad.returncode == 1 and "prestart_liveness needs -liveness" in bad.stderr
+
+    async def go():
+        k = FakeKubelet(kdir, rpc_client="native")
+        await k.start()
+        p = _daemon(kdir, fi, "-pulse", "3600", "-liveness", "-liveness_probe", STUB, "-prestart_liveness",
+                    "-liveness_timeout", "5", "-exporter_socket", "", env={"MI355X_STUB_PROBE_CONTROL": str(ctl)})
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            assert st.options.pre_start_required and st.options.get_preferred_allocation_available
+            adm = await k.admit("amd.com/gpu", 2)          # kubelet's sequence, the check included
+            assert adm.prestart_ms > 0 and len(adm.device_ids) == 2
+            k.release("amd.com/gpu", adm.device_ids)
+
+            async def prestart(ids):
+                return await k._call(st, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=ids),
+                                     pb.PreStartContainerResponse, timeout=30.0)
+            ctl.write_text(json.dumps({"3": "fail"}))         # the GPU broke after the last sweep
+            with pytest.raises(NativeRpcError) as e:
+                await prestart([dev[2], dev[3]])
+            assert e.value.status == 9 and dev[3] in e.value.message and dev[2] not in e.value.message
+            assert "MFMA liveness check failed" in e.value.message
+            await prestart([dev[2]])
+            # a slow check (1.5 s) on one connection; Allocate on another is answered meanwhile
+            ctl.write_text(json.dumps({"4": "slow", "slow_s": 1.5}))
+            slow = asyncio.create_task(asyncio.to_thread(
+                lambda: _unary_fresh(kdir, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=[dev[4]]))))
+            await asyncio.sleep(0.3)
+            t0 = time.monotonic()
+            areq = pb.AllocateRequest()
+            areq.container_requests.add(devices_ids=[dev[6]])
+            await asyncio.to_thread(lambda: _unary_fresh(kdir, "Allocate", areq))
+            assert time.monotonic() - t0 < 1.0
+            status, msg, took = await slow
+            assert status == 0 and took >= 1.2, (status, msg, took)
+        finally:
+            rc, err = await asyncio.to_thread(_stop, p)
+            await k.stop()
+        assert rc == 0, err[-3000:]
+        assert "PreStartContainer: MFMA liveness check failed (" + dev[3] in err
+
+    asyncio.run(asyncio.wait_for(go(), 90))
+
+
+def _unary_fresh(kdir, method, req):
+    """One call on a connection of its own: (status, message, seconds)."""
+    c = core().GrpcClient()
+    assert c.connect(os.path.join(kdir, "amd.com_gpu"), 5.0) == ""
+    try:
+        t0 = time.monotonic()
+        status, msg, _ = c.unary(f"/v1beta1.DevicePlugin/{method}", req.SerializeToString(), 30.0)
+        return status, msg, time.monotonic() - t0
+    finally:
+        c.close()
+
+
+def test_prestart_pending_at_shutdown_is_answered(tmp_path):
+    """SIGTERM while a PreStartContainer check is running: the check is cut
+    short, which is no fault (OK), or the server stops first (UNAVAILABLE);
+    either way the call is answered at once, not after the 30 s check, and the
+    daemon exits promptly."""
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text("{}")
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+    kub = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    p = _daemon(kdir, fi, "-pulse", "3600", "-liveness", "-liveness_probe", STUB, "-prestart_liveness",
+                "-liveness_timeout", "20", "-exporter_socket", "", "-grpc_watchdog", "0",
+                env={"MI355X_STUB_PROBE_CONTROL": str(ctl)})
+    try:
+        deadline = time.monotonic() + 30
+        while not os.path.exists(os.path.join(kdir, "amd.com_gpu")) and time.monotonic() < deadline:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+        d0 = {o: d for d, o in eng.ordinals().items()}[0]
+        eng.close()
+        ctl.write_text(json.dumps({"0": "slow", "slow_s": 30}))
+        import concurrent.futures
+        with concurrent.futures.ThreadPoolExecutor(1) as ex:
+            fut = ex.submit(_unary_fresh, kdir, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=[d0]))
+            time.sleep(0.5)
+            t0 = time.monotonic()
+            rc, err = _stop(p)
+            status, msg, took = fut.result(timeout=20)
+        assert rc == 0 and time.monotonic() - t0 < 10, err[-2000:]
+        assert status in (0, 14) and took < 10, (status, msg, took)
+    finally:
+        if p.poll() is None:
+            p.kill()
+        kub.close()
+
+
 def test_daemon_hung_exporter_blocks_neither_registration_nor_shutdown(tmp_path):
     """An exporter that accepts and never answers (10 s deadline per call): a
     kubelet restart is re-registered within a second, RPCs are answered at
