@@ -106,6 +106,10 @@ def make_parser():
                     help="with --health-pulse on the native daemon: -liveness_mode (one kept-queue probe server, or "
                          "a fresh probe process per device per sweep); extra.health_loop reports the host memory "
                          "of the daemon and its probe processes over the run")
+    ap.add_argument("--health-prestart", type=int, default=0,
+                    help="with --health-pulse on the native daemon: -prestart_liveness (kubelet's PreStartContainer "
+                         "probes the pod's GPUs through the probe server before the container starts; its time is "
+                         "part of the latency and reported as extra.prestart_rpc_p50_ms) (1 = on)")
     ap.add_argument("--advertise", type=int, default=0,
                     help="advertise M devices and request --gpus N of them per pod (default M = N: the headline, "
                          "'GPUs advertised at N'). With M > N the timed admissions start from a fragmented "

@@ -40,6 +40,7 @@ class StepRecords:
     latency_ms: List[float] = field(default_factory=list)
     rpc_ms: List[float] = field(default_factory=list)          # GetPreferredAllocation + Allocate round trips
     allocate_rpc_ms: List[float] = field(default_factory=list)
+    prestart_rpc_ms: List[float] = field(default_factory=list)  # PreStartContainer (-prestart_liveness), in rpc_ms
     ready_ms: List[float] = field(default_factory=list)        # latency - rpc
     kernel_us: List[float] = field(default_factory=list)
     prespawn_ms: List[float] = field(default_factory=list)     # after the RPCs, before the container's spawn
@@ -127,7 +128,7 @@ class Admissions:
         # the container's /dev: the DeviceSpecs, per allocated GPU (card + render node)
         spec_paths = {ds.host_path for ds in car.devices}
         groups = [[p for p in pl.minor_to_paths[m] if p in spec_paths] for m in minors]
-        return adm, (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids), mounts, groups)
+        return adm, (t0, ordl, adm.total_ms, adm.allocate_ms, list(adm.device_ids), mounts, groups, adm.prestart_ms)
 
     def _container(self, runtime, mode, dev_view, ordl, mounts, groups):
         """This rank's container (if it has one): (ok, t_ready, kernel us, error, phases), lingering kfd procs."""
@@ -181,7 +182,7 @@ class Admissions:
             adm, payload = self._admit(pl)
         else:
             payload = None
-        t0, ordl, tot, amsl, ids, mounts, groups = d.bcast(payload)
+        t0, ordl, tot, amsl, ids, mounts, groups, pre_ms = d.bcast(payload)
         mine, lingering = self._container(runtime, mode, dev_view, ordl, mounts, groups)
         into = rec if record is True else (record or None)
         if record is True:   # the containers are up: does the bench / plugin process hold the GPU?
@@ -233,6 +234,7 @@ class Admissions:
         rec.latency_ms.append(lat)
         rec.rpc_ms.append(tot)
         rec.allocate_rpc_ms.append(amsl)
+        rec.prestart_rpc_ms.append(pre_ms)
         rec.ready_ms.append(lat - tot)
         rec.kernel_us.append(max(m[2] for m in allr))
         rec.exec_ms.append((tm - sp) / 1e6)
@@ -250,6 +252,9 @@ class Admissions:
         return {
             "plugin_rpc_p50_ms": round(pct(rec.rpc_ms, .5), 4), "plugin_rpc_p99_ms": round(pct(rec.rpc_ms, .99), 4),
             "allocate_rpc_p50_ms": round(pct(rec.allocate_rpc_ms, .5), 4),
+            # kubelet's PreStartContainer when the plugin requires it (-prestart_liveness: a probe of the GPUs)
+            "prestart_rpc_p50_ms": (round(pct(rec.prestart_rpc_ms, .5), 4)
+                                    if any(x > 0 for x in rec.prestart_rpc_ms) else None),
             "container_start_to_ready_p50_ms": round(pct(rec.ready_ms, .5), 3),
             "latency_p99_ms": round(pct(rec.latency_ms, .99), 3),
             "latency_mean_ms": round(statistics.mean(rec.latency_ms), 3) if rec.latency_ms else None,

@@ -47,7 +47,9 @@ class BenchNode:
         if hp > 0 and self.plugin_kind == "native-daemon":
             self.health_flags = ("-pulse", str(max(1, int(round(hp)))),
                                  *(() if args.fixture else ("-liveness", "-liveness_mode", args.health_liveness_mode,
-                                                            "-smi_ecc", "-smi_events", "-smi_xgmi")))
+                                                            "-smi_ecc", "-smi_events", "-smi_xgmi",
+                                                            *(("-prestart_liveness",) if args.health_prestart
+                                                              else ()))))
         # the daemon and the oracle plugin serve on the same C++ server, off the bench's event loop
         self.kclient = args.kubelet_client or "native"
 

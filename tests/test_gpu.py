@@ -400,6 +400,71 @@ def test_native_daemon_corrupted_tile_reaches_listandwatch(inv, ordinals, tmp_pa
     assert not [pid for pid in children if os.path.exists(f"/proc/{pid}")], children
 
 
+def test_native_daemon_prestart_gate(ordinals, tmp_path):
+    """-prestart_liveness on MI355X: kubelet's PreStartContainer probes the
+    pod's GPU through the daemon's kept-queue probe server right before the
+    container starts. A healthy GPU passes in about a millisecond; a flipped
+    output bit fails the start with FAILED_PRECONDITION naming the device."""
+    import signal
+    import time
+    from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet, NativeRpcError
+
+    exe = os.environ.get("MI355X_NATIVE_DAEMON_EXE") or os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    probe = os.path.join(str(PKG_DIR), "bin", "mi355x-liveness-probe")
+    dev_id, _ = sorted(ordinals.items(), key=lambda kv: kv[1])[0]
+    fault = tmp_path / "corrupt"
+    fault.write_text("")
+    kdir = str(tmp_path / "dp")
+    out = {}
+
+    async def go():
+        k = FakeKubelet(kdir, rpc_client="native")
+        await k.start()
+        env = dict(os.environ, MI355X_PROBE_CORRUPT_FILE=str(fault))
+        proc = await asyncio.create_subprocess_exec(
+            exe, "-kubelet_dir", kdir, "-exporter_socket", "", "-pulse", "3600", "-liveness", "-liveness_probe",
+            probe, "-liveness_timeout", "30", "-prestart_liveness", stdout=asyncio.subprocess.DEVNULL,
+            stderr=asyncio.subprocess.PIPE, env=env)
+        try:
+            st = await k.wait_for_resource("amd.com/gpu", 1, timeout=60)
+            assert st.options.pre_start_required and st.devices.get(dev_id) == "Healthy"
+            adm = await k.admit("amd.com/gpu", 1, must_include=[dev_id])
+            assert adm.prestart_ms > 0
+            k.release("amd.com/gpu", adm.device_ids)
+            req = pb.PreStartContainerRequest(devices_ids=[dev_id])
+            lat = []
+            for _ in range(20):
+                t0 = time.perf_counter()
+                await k._call(st, "PreStartContainer", req, pb.PreStartContainerResponse, timeout=30.0)
+                lat.append((time.perf_counter() - t0) * 1e3)
+            lat.sort()
+            out["prestart_ms_p50"], out["prestart_ms_max"] = lat[len(lat) // 2], lat[-1]
+            assert out["prestart_ms_p50"] < 50, lat
+            fault.write_text("17")
+            with pytest.raises(NativeRpcError) as e:
+                await k._call(st, "PreStartContainer", req, pb.PreStartContainerResponse, timeout=30.0)
+            assert e.value.status == 9 and dev_id in e.value.message and "differ" in e.value.message, e.value.message
+            fault.write_text("")
+            await k._call(st, "PreStartContainer", req, pb.PreStartContainerResponse, timeout=30.0)
+        finally:
+            if proc.returncode is None:
+                proc.send_signal(signal.SIGTERM)
+            _, err = await asyncio.wait_for(proc.communicate(), 30)
+            print(err.decode(errors="replace")[-3000:])
+            await k.stop()
+        err = err.decode(errors="replace")
+        assert proc.returncode == 0, err[-3000:]
+        assert "ERROR: AddressSanitizer" not in err and "runtime error:" not in err and "ThreadSanitizer" not in err
+
+    asyncio.run(asyncio.wait_for(go(), 240))
+    print(f"prestart gate on {dev_id}: p50 {out['prestart_ms_p50']:.2f} ms, max {out['prestart_ms_max']:.2f} ms")
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/prestart_gate_box.json", "w") as f:
+        json.dump({"device": dev_id, **out}, f)
+
+
 def _foreign_queue_pids(gpu_id, exclude=()):
     """kfd proc entries (host PIDs) other than `exclude` with a user queue on kfd gpu_id."""
     root = "/sys/class/kfd/kfd/proc"

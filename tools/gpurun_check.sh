@@ -8,6 +8,7 @@
 #   torchrun1 the driver's torchrun launch at N = 1       -> gpurun_out/bench_torchrun1.json
 #   bench100  100 timed admissions                        -> gpurun_out/bench100.json
 #   health  bench with the health DaemonSet loop (-pulse 2, liveness, amd-smi) -> gpurun_out/bench_health.json
+#   healthpre  the same with -prestart_liveness                     -> gpurun_out/bench_health_prestart.json
 #   prof    rocprofv3 kernel stats of a short bench       -> gpurun_out/prof_bench/
 #   profprobe  rocprofv3 kernel stats of one HIP container entrypoint -> gpurun_out/prof_probe/
 #   hipvariants  tools/hip_setup_variants.py (own vs null stream)     -> gpurun_out/hip_setup_variants.json
@@ -71,6 +72,13 @@ for s in "$@"; do
         --json-out gpurun_out/bench_health.json > gpurun_out/bench_health.log 2>&1 \
         || { tail -20 gpurun_out/bench_health.log; exit 1; }
       python3 -c "import json; d=json.load(open('gpurun_out/bench_health.json')); print(d['value'], d['extra']['health_loop'])" ;;
+    healthpre)
+      # the health DaemonSet configuration plus -prestart_liveness (kubelet's PreStartContainer probes the pod's GPU)
+      step healthpre
+      timeout -k 10 400 python3 bench.py --steps 30 --health-pulse 2 --health-prestart 1 --runtime-compare 0 \
+        --json-out gpurun_out/bench_health_prestart.json > gpurun_out/bench_health_prestart.log 2>&1 \
+        || { tail -20 gpurun_out/bench_health_prestart.log; exit 1; }
+      python3 -c "import json; d=json.load(open('gpurun_out/bench_health_prestart.json')); e=d['extra']; print(d['value'], e['plugin_rpc_p50_ms'], e['prestart_rpc_p50_ms'], e['health_loop'])" ;;
     prof)
       step prof
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o bench \
