@@ -139,6 +139,21 @@ std::optional<Reply> DevicePluginService::prestart(uint64_t call_id, const std::
   RpcEvent ev;
   ev.rpc = "PreStartContainer";
   ev.t0_ns = mono_ns();
+  std::shared_ptr<const PreStartGate> gate;
+  std::shared_ptr<Sink> sink;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (native_) gate = gate_;
+    sink = sink_;
+  }
+  auto now = [&](Reply r) {
+    ev.dur_ns = mono_ns() - ev.t0_ns;
+    ev.status = r.status;
+    ev.message = r.message;
+    record(std::move(ev));
+    return r;
+  };
+  if (!gate || !sink) return now(Reply{kOk, "", ""});  // the reference's no-op: the request is not even read
   std::vector<std::string> ids;
   const bool ok = pb::scan(
       req.data(), req.size(),
@@ -147,23 +162,9 @@ std::optional<Reply> DevicePluginService::prestart(uint64_t call_id, const std::
         return true;
       },
       nullptr);
-  std::shared_ptr<const PreStartGate> gate;
-  std::shared_ptr<Sink> sink;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (native_) gate = gate_;
-    sink = sink_;
-  }
-  ev.ids = ids;
-  auto now = [&](Reply r) {
-    ev.dur_ns = mono_ns() - ev.t0_ns;
-    ev.status = r.status;
-    ev.message = r.message;
-    record(std::move(ev));
-    return r;
-  };
   if (!ok) return now(Reply{kInternal, "malformed PreStartContainerRequest", ""});
-  if (!gate || !sink || ids.empty()) return now(Reply{kOk, "", ""});
+  ev.ids = ids;
+  if (ids.empty()) return now(Reply{kOk, "", ""});
   (*gate)(std::move(ids), [this, sink, call_id, ev](Reply r) mutable {
     std::lock_guard<std::mutex> lk(sink->mu);
     if (!sink->srv) return;  // detached: the call was answered UNAVAILABLE at stop (this service may be gone)
