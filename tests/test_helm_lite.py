@@ -77,6 +77,8 @@ def test_chart_health_defaults_follow_the_measured_choice():
 
     c = dp({"dp": {"liveness": {"enabled": True}}})
     assert "-liveness_mode=persistent" in c["args"] and c["resources"] == {"requests": {"memory": "3072Mi"}}
+    assert "-prestart_liveness=true" in c["args"]
+    assert "-prestart_liveness=false" in dp({"dp": {"liveness": {"enabled": True, "prestart": False}}})["args"]
     assert dp({"dp": {"liveness": {"enabled": True, "mode": "spawn"}}})["args"].count("-liveness_mode=spawn") == 1
     assert dp({"dp": {"liveness": {"enabled": True}, "resources": {"limits": {"memory": "4Gi"}}}})["resources"] == \
         {"limits": {"memory": "4Gi"}}
@@ -89,3 +91,4 @@ def test_chart_health_defaults_follow_the_measured_choice():
     with open(os.path.join(repo, "k8s-ds-amdgpu-dp-health.yaml")) as f:
         man = yaml.safe_load(f)["spec"]["template"]["spec"]["containers"][0]
     assert "-liveness_mode=persistent" in man["args"] and man["resources"]["requests"]["memory"] == "3Gi"
+    assert "-prestart_liveness=true" in man["args"]
