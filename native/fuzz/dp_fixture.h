@@ -5,8 +5,11 @@
 // the ListAndWatch list, on a Unix socket in the scratch directory.
 #pragma once
 
+#include <atomic>
+#include <functional>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fuzz_common.h"
@@ -85,6 +88,13 @@ inline DpServer& dp_server() {
     d->service->set_allocator(alloc);
     d->service->set_allocate_template(t);
     d->service->set_device_list(list);
+    // PreStartContainer through a gate, as -prestart_liveness runs it: every other
+    // check answers at once on the I/O thread, the rest from a thread of their own
+    d->service->set_prestart_gate([](std::vector<std::string>, std::function<void(rpc::Reply)> done) {
+      static std::atomic<uint64_t> n{0};
+      if (n++ % 2 == 0) return done(rpc::Reply{});
+      std::thread([done = std::move(done)] { done(rpc::Reply{}); }).detach();
+    });
     d->service->attach(*d->server);
     d->sock = scratch_dir() + "/amd.com_gpu";
     if (const std::string e = d->server->start(d->sock); !e.empty()) fail("server start", e);

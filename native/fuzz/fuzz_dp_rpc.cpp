@@ -101,8 +101,13 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (r.status != rpc::kUnimplemented) fail("unknown method not UNIMPLEMENTED");
     return 0;
   }
-  if (sel >= 2) {
-    if (r.status != 0) fail("Options / PreStart failed", r.message);
+  if (sel == 3) {  // PreStartContainer through the gate: OK unless the request does not parse
+    const bool wellformed = rpc::pb::scan(body.data(), body.size(), nullptr, nullptr);
+    if (wellformed ? r.status != 0 : r.status != rpc::kInternal) fail("PreStart answer", r.message);
+    return 0;
+  }
+  if (sel == 2) {
+    if (r.status != 0) fail("Options failed", r.message);
     return 0;
   }
   std::vector<Container> req;
