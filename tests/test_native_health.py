@@ -484,6 +484,46 @@ def test_prestart_liveness_gate(tmp_path):
     asyncio.run(asyncio.wait_for(go(), 90))
 
 
+def test_prestart_gate_on_cpx_partitions(tmp_path):
+    """CPX: each partition is its own ROCr agent. A container given three
+    partitions of one GPU is checked on exactly those three agents; a fault on
+    one of them names that partition only."""
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    fi = make_mi355x_node(tmp_path / "n", compute_partition="cpx")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text("{}")
+    log = tmp_path / "starts.log"
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    ords = eng.ordinals()
+    eng.close()
+    inv = discover(str(fi.sysfs))
+    gpu0 = sorted((d for d in inv.devices if d.bdf == fi.bdfs[0]), key=lambda d: ords[d.id])
+    picked = [d.id for d in gpu0[:3]]
+    kub = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    p = _daemon(kdir, fi, "-pulse", "3600", "-liveness", "-liveness_probe", STUB, "-prestart_liveness",
+                "-liveness_timeout", "5", "-exporter_socket", "", "-grpc_watchdog", "0",
+                env={"MI355X_STUB_PROBE_CONTROL": str(ctl)})
+    try:
+        deadline = time.monotonic() + 30
+        while not os.path.exists(os.path.join(kdir, "amd.com_gpu")) and time.monotonic() < deadline:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        req = pb.PreStartContainerRequest(devices_ids=picked)
+        assert _unary_fresh(kdir, "PreStartContainer", req)[0] == 0
+        ctl.write_text(json.dumps({str(ords[picked[1]]): "fail"}))
+        status, msg, _ = _unary_fresh(kdir, "PreStartContainer", req)
+        assert status == 9 and picked[1] in msg and picked[0] not in msg and picked[2] not in msg, msg
+        # a container on other partitions of the same GPU is not held back
+        other = pb.PreStartContainerRequest(devices_ids=[d.id for d in gpu0[3:5]])
+        assert _unary_fresh(kdir, "PreStartContainer", other)[0] == 0
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+    assert rc == 0, err[-2000:]
+
+
 def _unary_fresh(kdir, method, req):
     """One call on a connection of its own: (status, message, seconds)."""
     c = core().GrpcClient()
