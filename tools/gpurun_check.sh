@@ -17,6 +17,7 @@
 #   asansoak  the same soak against the ASan/UBSan daemon in asan_bin/ -> gpurun_out/soak_asan.json
 #   tsansoak  2 min (SOAK_SECONDS) soak of the ThreadSanitizer daemon, every health source on, HIP containers -> gpurun_out/soak_tsan.json
 #   soak    4 min native daemon soak, every health source on, a HIP container every second -> gpurun_out/soak_native.json
+#   soakpre the soak with -prestart_liveness (a GPU check per admission)  -> gpurun_out/soak_prestart.json
 #   cov     pytest -m gpu against the gcov build in cov_bin/ -> gpurun_out/gcov (merged by tools/native_coverage.py)
 #
 #   gpurun --timeout 900 -- bash tools/gpurun_check.sh smoke tests bench
@@ -103,6 +104,14 @@ for s in "$@"; do
         --out gpurun_out/soak_native.json > gpurun_out/soak_native.log 2>&1 \
         || { tail -20 gpurun_out/soak_native.log; exit 1; }
       tail -c 1500 gpurun_out/soak_native.json ;;
+    soakpre)
+      # the same soak with -prestart_liveness: every admission's PreStartContainer probes its GPU
+      step soakpre
+      timeout -k 10 420 python3 tools/soak_native.py --seconds 240 --report 30 --container-interval 1 \
+        --extra "-liveness -prestart_liveness -liveness_chip_sweep_every 10 -perf_check_every 60 -smi_ecc -smi_events -smi_xgmi" \
+        --out gpurun_out/soak_prestart.json > gpurun_out/soak_prestart.log 2>&1 \
+        || { tail -20 gpurun_out/soak_prestart.log; exit 1; }
+      tail -c 1500 gpurun_out/soak_prestart.json ;;
     asan)
       # the GPU tests that drive the native daemons, against their ASan/UBSan builds (host code only;
       # asan_bin/ holds build/native-address-undefined/pkg/bin/*, copied before the call)
