@@ -170,6 +170,10 @@ int Daemon::init() {
       serve_.node = nv;
     }
   }
+  if (f_.prestart_liveness && f_.liveness_mode == "spawn")
+    MI_LOG(kWarning, "-prestart_liveness with -liveness_mode=spawn: every container start waits for a fresh probe "
+                     "process (GPU runtime start-up) and then for its kfd teardown; -liveness_mode=persistent "
+                     "answers from the kept queue in about a millisecond");
   if (f_.prestart_liveness)  // runs on the RPC thread: the probe goes to a gate thread
     serve_.prestart = [this](std::vector<std::string> ids, std::function<void(rpc::Reply)> done) {
       std::shared_ptr<health::Engine> engine;
