@@ -196,10 +196,22 @@ def _fmt(v) -> str:
     return str(v)
 
 
+def _go_numbers(v):
+    """Helm's values are JSON numbers (float64); Go's YAML encoder writes an
+    integral one without a fraction (3, not 3.0)."""
+    if isinstance(v, dict):
+        return {k: _go_numbers(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_go_numbers(x) for x in v]
+    if isinstance(v, float) and v.is_integer() and abs(v) < 1e15:
+        return int(v)
+    return v
+
+
 def _to_yaml(v) -> str:
     if v in ({}, [], None):
         return "{}" if v == {} or v is None else "[]"
-    return yaml.safe_dump(v, default_flow_style=False, sort_keys=True).rstrip("\n")
+    return yaml.safe_dump(_go_numbers(v), default_flow_style=False, sort_keys=True).rstrip("\n")
 
 
 def _indent(n, s) -> str:

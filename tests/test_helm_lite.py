@@ -92,3 +92,44 @@ def test_chart_health_defaults_follow_the_measured_choice():
         man = yaml.safe_load(f)["spec"]["template"]["spec"]["containers"][0]
     assert "-liveness_mode=persistent" in man["args"] and man["resources"]["requests"]["memory"] == "3Gi"
     assert "-prestart_liveness=true" in man["args"]
+
+
+def test_chart_device_count_and_config_file(tmp_path):
+    """dp.deviceCount -> AMD_GPU_DEVICE_COUNT; dp.config -> a ConfigMap mounted at
+    /etc/amdgpu/config.yaml with CONFIG_FILE_PATH (the upstream docs' recipe,
+    docs/user-guide/configuration.md), read by the daemon as rendered."""
+    import os
+    import subprocess
+
+    import yaml
+
+    from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+    from rocm_k8s_device_plugin_amd.testing.fixtures import make_mi355x_node
+    from rocm_k8s_device_plugin_amd.testing.helm_lite import rendered_objects
+    chart = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "helm", "amd-gpu")
+    objs = rendered_objects(chart, {"dp": {"deviceCount": 2, "config": {"gpu": {"device_count": 3}}}})
+    cm = [o for o in objs if o.get("kind") == "ConfigMap"]
+    ds = [o for o in objs if o.get("kind") == "DaemonSet" and "labeller" not in o["metadata"]["name"]][0]
+    pod = ds["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert env == {"AMD_GPU_DEVICE_COUNT": "2", "CONFIG_FILE_PATH": "/etc/amdgpu/config.yaml"}
+    assert {"name": "config", "mountPath": "/etc/amdgpu", "readOnly": True} in c["volumeMounts"]
+    assert len(cm) == 1 and {"name": "config", "configMap": {"name": cm[0]["metadata"]["name"]}} in pod["volumes"]
+    assert yaml.safe_load(cm[0]["data"]["config.yaml"]) == {"gpu": {"device_count": 3}}
+    # defaults render neither (as upstream)
+    plain = [o for o in rendered_objects(chart, {}) if o.get("kind") == "DaemonSet"][0]
+    assert "env" not in plain["spec"]["template"]["spec"]["containers"][0]
+    assert not [o for o in rendered_objects(chart, {}) if o.get("kind") == "ConfigMap"]
+    # the daemon reads what the chart mounts: the env beats the file, the file alone limits too
+    fi = make_mi355x_node(tmp_path / "n")
+    (tmp_path / "config.yaml").write_text(cm[0]["data"]["config.yaml"])
+    exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    for extra, want in (({"AMD_GPU_DEVICE_COUNT": env["AMD_GPU_DEVICE_COUNT"]}, 2), ({}, 3)):
+        e = {k: v for k, v in os.environ.items() if k != "AMD_GPU_DEVICE_COUNT"}
+        e.update(extra, CONFIG_FILE_PATH=str(tmp_path / "config.yaml"))
+        p = subprocess.run([exe, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                            "-exporter_socket="], capture_output=True, text=True, timeout=30, env=e)
+        assert p.returncode == 0, p.stderr[-500:]
+        import json
+        assert len(json.loads(p.stdout)["resources"]["amd.com/gpu"]["devices"]) == want
