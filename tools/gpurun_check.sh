@@ -135,13 +135,14 @@ for s in "$@"; do
         > gpurun_out/gputests_tsan.log 2>&1 || { tail -40 gpurun_out/gputests_tsan.log; exit 1; }
       tail -3 gpurun_out/gputests_tsan.log ;;
     tsansoak)
-      # 2 minutes of the soak against the ThreadSanitizer daemon: admissions back to back, a HIP
-      # container every 2 s, liveness + chip sweep + throughput check + the three amd-smi sources
+      # 2 minutes of the soak against the ThreadSanitizer daemon: admissions back to back (each with its
+      # PreStartContainer GPU check), a HIP container every 2 s, liveness + chip sweep + throughput check +
+      # the three amd-smi sources
       step tsansoak
       w=$(tsan_launchers)
       TSAN_OPTIONS="$TSAN_ENV" timeout -k 10 $(( ${SOAK_SECONDS:-120} + 180 )) python3 tools/soak_native.py --seconds "${SOAK_SECONDS:-120}" \
         --report 20 --container-interval 2 --exe "$w/mi355x-device-plugin" \
-        --extra "-liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
+        --extra "-liveness -prestart_liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_tsan.json > gpurun_out/soak_tsan.log 2>&1 || { tail -c 3000 gpurun_out/soak_tsan.json; exit 1; }
       tail -c 800 gpurun_out/soak_tsan.json ;;
     asansoak)
@@ -149,7 +150,7 @@ for s in "$@"; do
       step asansoak
       UBSAN_OPTIONS="print_stacktrace=1" timeout -k 10 $(( ${SOAK_SECONDS:-120} + 180 )) python3 tools/soak_native.py --seconds "${SOAK_SECONDS:-120}" \
         --report 20 --container-interval 2 --exe "$PWD/asan_bin/mi355x-device-plugin" \
-        --extra "-liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
+        --extra "-liveness -prestart_liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_asan.json > gpurun_out/soak_asan.log 2>&1 || { tail -c 3000 gpurun_out/soak_asan.json; exit 1; }
       tail -c 800 gpurun_out/soak_asan.json ;;
     cov)
