@@ -591,7 +591,18 @@ std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::str
   for (const auto& [id, o] : sel) uniq.push_back(o);
   std::sort(uniq.begin(), uniq.end());
   uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-  const auto by_ord = prober_->probe(uniq, {}, "probe");
+  // GPUs with other processes' queues (the probe server's own excluded), as a sweep
+  // sees them: a dispatch still queued behind their work there is pending, not a
+  // fault to confirm with a fresh process (which the container would then wait for)
+  std::set<int64_t> gids;
+  for (const auto& [id, o] : sel) gids.insert(gpu_id(id));
+  gids.erase(0);
+  std::map<int64_t, std::pair<int, int>> load;
+  const bool known = kfd_load(prober_->own_kfd_entries(gids), &load);
+  std::set<int> busy;
+  for (const auto& [id, o] : sel)
+    if (!known || load.count(gpu_id(id))) busy.insert(o);
+  const auto by_ord = prober_->probe(uniq, busy, "probe");
   std::map<std::string, ProbeOutcome> raw;
   for (const auto& [id, o] : sel)
     if (auto it = by_ord.find(o); it != by_ord.end()) raw[id] = it->second;

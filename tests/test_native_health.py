@@ -524,6 +524,45 @@ def test_prestart_gate_on_cpx_partitions(tmp_path):
     assert rc == 0, err[-2000:]
 
 
+def test_prestart_gate_pending_behind_a_tenant_is_no_fault(tmp_path):
+    """A dispatch still queued behind another process' kernels (its queues are on
+    that GPU) is pending: the start goes ahead at once, with no fresh probe
+    process the container would then wait for. On an idle GPU the same silence
+    is confirmed by a fresh process and fails the start."""
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text("{}")
+    log = tmp_path / "starts.log"
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = {o: d for d, o in eng.ordinals().items()}
+    eng.close()
+    kub = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    p = _daemon(kdir, fi, "-pulse", "3600", "-liveness", "-liveness_probe", STUB, "-prestart_liveness",
+                "-liveness_timeout", "5", "-exporter_socket", "", "-grpc_watchdog", "0",
+                env={"MI355X_STUB_PROBE_CONTROL": str(ctl), "MI355X_STUB_PROBE_LOG": str(log)})
+    try:
+        deadline = time.monotonic() + 30
+        while not os.path.exists(os.path.join(kdir, "amd.com_gpu")) and time.monotonic() < deadline:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        _busy_gpu(fi, inv, dev[3])
+        ctl.write_text(json.dumps({"3": "pending", "5": "pending"}))
+        status, msg, took = _unary_fresh(kdir, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=[dev[3]]))
+        assert status == 0 and took < 2.0, (status, msg, took)
+        assert "3" not in log.read_text().split()                # no fresh process on the busy GPU
+        status, msg, _ = _unary_fresh(kdir, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=[dev[5]]))
+        assert status == 9 and dev[5] in msg, (status, msg)
+        assert "5" in log.read_text().split()                    # confirmed by a fresh process
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+    assert rc == 0, err[-2000:]
+
+
 def _unary_fresh(kdir, method, req):
     """One call on a connection of its own: (status, message, seconds)."""
     c = core().GrpcClient()
