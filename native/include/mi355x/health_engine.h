@@ -172,7 +172,8 @@ class Engine {
   bool sweep();
   // A liveness probe of `ids` now, outside the sweep cadence (a container about
   // to start on them: PreStartContainer). Waits for a sweep in flight; changes no
-  // verdict. id -> outcome; devices without a ROCr ordinal are absent.
+  // verdict. id -> outcome; devices without a ROCr ordinal, and devices on GPUs
+  // the probe server steps off (crowded with tenant processes), are absent.
   std::map<std::string, ProbeOutcome> probe_now(const std::vector<std::string>& ids);
   std::map<std::string, Verdict> snapshot() const;
   uint64_t version() const;

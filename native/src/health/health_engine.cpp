@@ -584,8 +584,8 @@ std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::str
   trace::Span span("liveness.prestart", "health", {{"devices", std::to_string(ids.size())}});
   std::map<std::string, int> sel;
   const auto& ords = ordinals();
-  for (const auto& id : ids)
-    if (auto it = ords.find(id); it != ords.end()) sel[id] = it->second;
+  for (const auto& id : ids)  // the probe server stays off crowded GPUs here too (update_crowded)
+    if (auto it = ords.find(id); it != ords.end() && !crowded_.count(id)) sel[id] = it->second;
   if (sel.empty()) return {};
   std::vector<int> uniq;
   for (const auto& [id, o] : sel) uniq.push_back(o);

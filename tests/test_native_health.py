@@ -563,6 +563,45 @@ def test_prestart_gate_pending_behind_a_tenant_is_no_fault(tmp_path):
     assert rc == 0, err[-2000:]
 
 
+def test_prestart_gate_leaves_crowded_gpus_alone(tmp_path):
+    """A GPU crowded with tenant processes has no probe-server queue (the sweep
+    steps off it); a container start there is not checked either, rather than
+    restarting the server onto that GPU."""
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text(json.dumps({"3": "fail"}))
+    log = tmp_path / "starts.log"
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = {o: d for d, o in eng.ordinals().items()}
+    eng.close()
+    for pid in range(800, 807):
+        _busy_gpu(fi, inv, dev[3], pid=str(pid))
+    kub = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    p = _daemon(kdir, fi, "-pulse", "3600", "-liveness", "-liveness_probe", STUB, "-prestart_liveness",
+                "-liveness_timeout", "5", "-exporter_socket", "", "-grpc_watchdog", "0",
+                env={"MI355X_STUB_PROBE_CONTROL": str(ctl), "MI355X_STUB_PROBE_LOG": str(log)})
+    try:
+        deadline = time.monotonic() + 30
+        while not os.path.exists(os.path.join(kdir, "amd.com_gpu")) and time.monotonic() < deadline:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        starts = log.read_text().split().count("serve+keep")
+        status, msg, _ = _unary_fresh(kdir, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=[dev[3]]))
+        assert status == 0, msg
+        status, msg, _ = _unary_fresh(kdir, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=[dev[2]]))
+        assert status == 0, msg
+        words = log.read_text().split()
+        assert words.count("serve+keep") == starts == 1 and "visible=0,1,2,4,5,6,7" in words
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+    assert rc == 0, err[-2000:]
+
+
 def _unary_fresh(kdir, method, req):
     """One call on a connection of its own: (status, message, seconds)."""
     c = core().GrpcClient()
