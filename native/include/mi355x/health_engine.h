@@ -171,7 +171,7 @@ class Engine {
   // One sweep; true when any device's health changed. Blocking.
   bool sweep();
   // A liveness probe of `ids` now, outside the sweep cadence (a container about
-  // to start on them: PreStartContainer). Waits for a sweep in flight; changes no
+  // to start on them: PreStartContainer). Waits for a sweep's liveness pass; changes no
   // verdict. id -> outcome; devices without a ROCr ordinal, and devices on GPUs
   // the probe server steps off (crowded with tenant processes), are absent.
   std::map<std::string, ProbeOutcome> probe_now(const std::vector<std::string>& ids);
@@ -274,7 +274,7 @@ class Engine {
   std::string xgmi_error_;
 
   mutable std::mutex mu_;  // snapshot_ / version_ / degraded_ / fabric_version_ / links_down_
-  std::mutex op_mu_;       // sweep() and probe_now(): one user of the prober at a time
+  std::mutex op_mu_;       // the liveness pass of sweep() and probe_now(): one user of the prober at a time
   std::set<std::pair<std::string, std::string>> degraded_;
   std::map<std::string, int> links_down_;
   uint64_t fabric_version_ = 0;

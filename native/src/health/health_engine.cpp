@@ -610,7 +610,6 @@ std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::str
 }
 
 bool Engine::sweep() {
-  std::lock_guard<std::mutex> op(op_mu_);
   trace::Span span("health.sweep", "health", {{"devices", std::to_string(devices_.size())}});
   const double t0 = mono_s();
   Reasons reasons;
@@ -622,7 +621,12 @@ bool Engine::sweep() {
       if (auto it = hmap.find(d.bdf); it != hmap.end() && !it->second)
         reasons[d.id].push_back("exporter reports " + d.bdf + " unhealthy");
   }
-  if (cfg_.liveness && prober_) liveness_pass(&reasons);
+  if (cfg_.liveness && prober_) {
+    // the prober, the ordinal map and the crowd state are shared with probe_now(); a
+    // PreStartContainer check waits for this pass only, not for the exporter or amd-smi
+    std::lock_guard<std::mutex> op(op_mu_);
+    liveness_pass(&reasons);
+  }
   if (cfg_.smi_ecc && smi_available()) ecc_pass(&reasons);
   if (cfg_.smi_events) events_pass(&reasons);
   if (cfg_.smi_xgmi) fabric_check();

@@ -602,6 +602,42 @@ def test_prestart_gate_leaves_crowded_gpus_alone(tmp_path):
     assert rc == 0, err[-2000:]
 
 
+def test_prestart_gate_does_not_wait_for_a_hung_exporter(tmp_path):
+    """A sweep stuck in the metrics exporter (10 s deadline) holds the engine's
+    prober only for its liveness pass: a PreStartContainer check meanwhile is
+    answered at once."""
+    from rocm_k8s_device_plugin_amd.proto import deviceplugin as pb
+    fi = make_mi355x_node(tmp_path / "n")
+    ctl = tmp_path / "ctl.json"
+    ctl.write_text("{}")
+    kdir = str(tmp_path / "dp")
+    os.makedirs(kdir)
+    eng = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = {o: d for d, o in eng.ordinals().items()}
+    eng.close()
+    exp = gp.GoServer(str(tmp_path / "exp.sock"), {}, gp.GoServerConfig(never_answer=True))
+    kub = gp.GoServer(os.path.join(kdir, "kubelet.sock"), {"/v1beta1.Registration/Register": lambda m: (0, "", b"")})
+    p = _daemon(kdir, fi, "-pulse", "1", "-liveness", "-liveness_probe", STUB, "-prestart_liveness",
+                "-liveness_timeout", "5", "-exporter_socket", str(tmp_path / "exp.sock"), "-grpc_watchdog", "0",
+                env={"MI355X_STUB_PROBE_CONTROL": str(ctl)})
+    try:
+        deadline = time.monotonic() + 40       # the first sweep waits out the exporter's 10 s
+        while not os.path.exists(os.path.join(kdir, "amd.com_gpu")) and time.monotonic() < deadline:
+            time.sleep(0.05)
+        n = len(exp.calls)
+        while len(exp.calls) == n and time.monotonic() < deadline:   # the next sweep is now in the exporter
+            time.sleep(0.05)
+        assert len(exp.calls) > n, "no second exporter call"
+        time.sleep(0.5)
+        status, msg, took = _unary_fresh(kdir, "PreStartContainer", pb.PreStartContainerRequest(devices_ids=[dev[1]]))
+        assert status == 0 and took < 3.0, (status, msg, took)
+    finally:
+        rc, err = _stop(p)
+        kub.close()
+        exp.close()
+    assert rc == 0, err[-2000:]
+
+
 def _unary_fresh(kdir, method, req):
     """One call on a connection of its own: (status, message, seconds)."""
     c = core().GrpcClient()
