@@ -1,7 +1,11 @@
 // The YAML subset configuration files use (see yaml.h).
 #include "yaml.h"
 
+#include <cctype>
 #include <cstdint>
+#include <cstring>
+#include <map>
+#include <optional>
 #include <vector>
 
 namespace mi355x::yaml {
@@ -130,6 +134,8 @@ class Parser {
   // nesting bound (block and flow collections): a hostile or broken file
   // must not exhaust the stack (the JSON reader has the same bound)
   static constexpr int kMaxDepth = 128;
+  // nodes aliases may copy in one document: a "billion laughs" of nested aliases is refused
+  static constexpr size_t kMaxAliasNodes = size_t{1} << 20;
   struct Nest {
     explicit Nest(int* d) : d_(d) { ++*d_; }
     ~Nest() { --*d_; }
@@ -151,14 +157,24 @@ class Parser {
       Line& l = lines_[*i];
       std::string rest = l.text.size() > 1 ? l.text.substr(2) : "";
       while (!rest.empty() && rest[0] == ' ') rest.erase(0, 1);
+      // `- &a` then a block, `- &a |`, `- &a - x`: the anchor (and tag) name the entry;
+      // `- &a k: v` anchors the key (mapping() reads it), inline values keep theirs for flow()
+      std::string anchor, tag;
+      if (!props(&rest, l.no, true, &anchor, &tag)) return std::nullopt;
+      auto keep = [&](json::Value v) {
+        if (!tagged(tag, &v, l.no)) return false;
+        if (!anchor.empty()) anchors_[anchor] = v;
+        arr.arr.push_back(std::move(v));
+        return true;
+      };
       if (rest.empty()) {  // the item is the nested block below
         ++*i;
         if (*i < lines_.size() && lines_[*i].indent > indent) {
           auto v = block(i, lines_[*i].indent);
           if (!v) return std::nullopt;
-          arr.arr.push_back(std::move(*v));
+          if (!keep(std::move(*v))) return std::nullopt;
         } else {
-          arr.arr.push_back(json::Value{});
+          if (!keep(json::Value{})) return std::nullopt;
         }
         continue;
       }
@@ -169,7 +185,7 @@ class Parser {
         l.text = rest;
         auto v = sequence(i, item_indent);
         if (!v) return std::nullopt;
-        arr.arr.push_back(std::move(*v));
+        if (!keep(std::move(*v))) return std::nullopt;
         continue;
       }
       if (key_colon(rest) != std::string::npos && rest[0] != '{' && rest[0] != '[') {
@@ -178,24 +194,72 @@ class Parser {
         l.text = rest;
         auto v = mapping(i, item_indent);
         if (!v) return std::nullopt;
-        arr.arr.push_back(std::move(*v));
+        if (!keep(std::move(*v))) return std::nullopt;
       } else if (rest[0] == '|' || rest[0] == '>') {
         ++*i;
         auto v = block_scalar(rest, l.no, indent, i);
         if (!v) return std::nullopt;
-        arr.arr.push_back(std::move(*v));
+        if (!keep(std::move(*v))) return std::nullopt;
       } else {
         ++*i;
         auto v = scalar_or_flow(continued(rest, l.no, indent, i), l.no);
         if (!v) return std::nullopt;
-        arr.arr.push_back(std::move(*v));
+        if (!keep(std::move(*v))) return std::nullopt;
       }
     }
     return arr;
   }
 
+  // Node properties (an anchor, a tag, both in either order) at the start of `*t` when
+  // what follows them is a block node: nothing (the block on the next lines), a block
+  // scalar or, for a sequence entry, a nested "- item". They are taken off `*t` into
+  // *anchor / *tag; properties of an inline value stay for flow().
+  bool props(std::string* t, int no, bool entry, std::string* anchor, std::string* tag) {
+    std::string r = *t, a, g;
+    for (int k = 0; k < 2 && !r.empty() && (r[0] == '&' || r[0] == '!'); ++k) {
+      if (r[0] == '&') {
+        if (!a.empty()) return true;
+        const auto name = take_anchor(&r, no);
+        if (!name) return false;
+        a = *name;
+      } else {
+        if (!g.empty()) return true;
+        size_t e = 0;
+        while (e < r.size() && !space(r[e])) ++e;
+        g = r.substr(0, e);
+        while (e < r.size() && space(r[e])) ++e;
+        r.erase(0, e);
+      }
+    }
+    if (a.empty() && g.empty()) return true;
+    if (r.empty() || r[0] == '|' || r[0] == '>' || (entry && is_seq_item(r))) {
+      *t = r;
+      *anchor = a;
+      *tag = g;
+    }
+    return true;
+  }
+
+  // a standard tag on a block node: the node must be of its kind
+  bool tagged(const std::string& tag, json::Value* v, int no) {
+    if (tag.empty()) return true;
+    const auto k = v->kind;
+    if (tag == "!!str" && (k == json::Value::String || k == json::Value::Null)) {
+      if (k == json::Value::Null) *v = json::Value::string("");  // `key: !!str` is ""
+      return true;
+    }
+    if ((tag == "!!map" && k == json::Value::Object) || (tag == "!!seq" && k == json::Value::Array) ||
+        (tag == "!!null" && k == json::Value::Null))
+      return true;
+    if (tag != "!!str" && tag != "!!map" && tag != "!!seq" && tag != "!!null")
+      return fail(no, "unsupported tag " + tag + " on a block node"), false;
+    return fail(no, "tag " + tag + " on a block node of another kind"), false;
+  }
+
   std::optional<json::Value> mapping(size_t* i, int indent) {
     json::Value obj = json::Value::object();
+    std::vector<json::Value> merges;  // the values of `<<` keys
+    const size_t start = *i;
     while (*i < lines_.size() && lines_[*i].indent == indent && !is_seq_item(lines_[*i].text)) {
       const Line l = lines_[*i];
       const size_t c = key_colon(l.text);
@@ -205,39 +269,70 @@ class Parser {
       }
       std::string key = l.text.substr(0, c);
       while (!key.empty() && (key.back() == ' ' || key.back() == '\t')) key.pop_back();
-      if (!key.empty() && (key[0] == '"' || key[0] == '\'')) {  // a quoted key: escapes and '' resolved
+      const auto key_anchor = take_anchor(&key, l.no);  // `&a k: v` anchors the key (as PyYAML reads it)
+      if (!key_anchor) return std::nullopt;
+      const bool quoted = !key.empty() && (key[0] == '"' || key[0] == '\'');
+      if (quoted || (!key.empty() && key[0] == '*')) {  // a quoted key (escapes and '' resolved) or an alias
         auto k = scalar_or_flow(key, l.no);
-        if (!k || k->kind != json::Value::String) return fail(l.no, "bad quoted key"), std::nullopt;
+        if (!k) return std::nullopt;
+        if (k->kind != json::Value::String) return fail(l.no, "a key that is not a string"), std::nullopt;
         key = k->s;
       }
+      if (!key_anchor->empty()) anchors_[*key_anchor] = json::Value::string(key);
       std::string val = c + 1 < l.text.size() ? l.text.substr(c + 1) : "";
       while (!val.empty() && val[0] == ' ') val.erase(0, 1);
+      // an anchor / tag before a block value (`key: &a` then the block, `key: !!str |`);
+      // inline values keep theirs for flow()
+      std::string anchor, tag;
+      if (!props(&val, l.no, false, &anchor, &tag)) return std::nullopt;
       ++*i;
+      std::optional<json::Value> v;
       if (!val.empty() && (val[0] == '|' || val[0] == '>')) {  // block scalar
-        auto v = block_scalar(val, l.no, indent, i);
-        if (!v) return std::nullopt;
+        v = block_scalar(val, l.no, indent, i);
+      } else if (val.empty()) {
+        if (*i < lines_.size() && lines_[*i].indent > indent)
+          v = block(i, lines_[*i].indent);
+        else if (*i < lines_.size() && lines_[*i].indent == indent && is_seq_item(lines_[*i].text))
+          v = sequence(i, indent);  // "key:\n- item" at the key's indentation
+        else
+          v = json::Value{};
+      } else {
+        v = scalar_or_flow(continued(val, l.no, indent, i), l.no);
+      }
+      if (!v || !tagged(tag, &*v, l.no)) return std::nullopt;
+      if (!anchor.empty()) anchors_[anchor] = *v;
+      if (key == "<<" && !quoted)
+        merges.push_back(std::move(*v));
+      else
         obj.set(key, std::move(*v));
-        continue;
-      }
-      if (val.empty()) {
-        if (*i < lines_.size() && lines_[*i].indent > indent) {
-          auto v = block(i, lines_[*i].indent);
-          if (!v) return std::nullopt;
-          obj.set(key, std::move(*v));
-        } else if (*i < lines_.size() && lines_[*i].indent == indent && is_seq_item(lines_[*i].text)) {
-          auto v = sequence(i, indent);  // "key:\n- item" at the key's indentation
-          if (!v) return std::nullopt;
-          obj.set(key, std::move(*v));
-        } else {
-          obj.set(key, json::Value{});
-        }
-        continue;
-      }
-      auto v = scalar_or_flow(continued(val, l.no, indent, i), l.no);
-      if (!v) return std::nullopt;
-      obj.set(key, std::move(*v));
     }
+    if (!merges.empty() && !merge(&obj, merges, lines_[start].no)) return std::nullopt;
     return obj;
+  }
+
+  // `<<: *base` / `<<: [*a, *b]`, the merge key PyYAML's SafeLoader reads: the merged
+  // mappings' entries come first (of a list's, the earlier mapping wins), then the
+  // mapping's own entries, which override them
+  bool merge(json::Value* obj, const std::vector<json::Value>& merges, int no) {
+    json::Value out = json::Value::object();
+    for (const auto& m : merges) {
+      std::vector<const json::Value*> from;
+      if (m.kind == json::Value::Object) {
+        from.push_back(&m);
+      } else if (m.kind == json::Value::Array) {
+        for (auto it = m.arr.rbegin(); it != m.arr.rend(); ++it) {
+          if (it->kind != json::Value::Object) return fail(no, "expected a mapping for merging"), false;
+          from.push_back(&*it);
+        }
+      } else {
+        return fail(no, "expected a mapping or list of mappings for merging"), false;
+      }
+      for (const json::Value* f : from)
+        for (const auto& kv : f->obj) out.set(kv.first, kv.second);
+    }
+    for (auto& kv : obj->obj) out.set(kv.first, std::move(kv.second));
+    *obj = std::move(out);
+    return true;
   }
 
   // A value that goes on over the following lines indented deeper than its
@@ -362,6 +457,44 @@ class Parser {
       return std::nullopt;
     }
     return v;
+  }
+
+  // the name of the anchor `&name` / alias `*name` at s[*p] (*p past it and the blanks after):
+  // letters, digits, - and _, as PyYAML scans it; "" when there is none or something other
+  // than a blank or ':' (in flow also , ] } ?) follows it
+  static std::string anchor_name(const std::string& s, size_t* p, bool in_flow) {
+    size_t e = *p + 1;
+    while (e < s.size() && (std::isalnum(static_cast<unsigned char>(s[e])) || s[e] == '-' || s[e] == '_')) ++e;
+    if (e < s.size() && !space(s[e]) && s[e] != ':' && !(in_flow && std::strchr(",]}?", s[e]) != nullptr))
+      return "";
+    std::string name = s.substr(*p + 1, e - *p - 1);
+    *p = e;
+    while (*p < s.size() && (s[*p] == ' ' || s[*p] == '\t')) ++*p;
+    return name;
+  }
+
+  // the nodes in `v`, counted up to just past the alias budget
+  static size_t nodes(const json::Value& v) {
+    size_t n = 1;
+    for (const auto& e : v.arr) {
+      n += nodes(e);
+      if (n > kMaxAliasNodes) return n;
+    }
+    for (const auto& kv : v.obj) {
+      n += nodes(kv.second);
+      if (n > kMaxAliasNodes) return n;
+    }
+    return n;
+  }
+
+  // a block node's anchor at the start of `t`: its name ("" = none), `t` left with the rest
+  std::optional<std::string> take_anchor(std::string* t, int no) {
+    if (t->empty() || (*t)[0] != '&') return std::string();
+    size_t p = 0;
+    std::string name = anchor_name(*t, &p, false);
+    if (name.empty()) return fail(no, "expected an anchor name of letters, digits, - or _"), std::nullopt;
+    t->erase(0, p);
+    return name;
   }
 
   static json::Value plain(const std::string& t) {
@@ -493,30 +626,56 @@ class Parser {
     while (*p < s.size() && space(s[*p])) ++*p;
     if (*p >= s.size()) return json::Value{};
     const char c = s[*p];
+    if (c == '&') {  // an anchor: the node after it, remembered for its aliases
+      const std::string name = anchor_name(s, p, in_flow);
+      if (name.empty()) return fail(no, "expected an anchor name of letters, digits, - or _"), std::nullopt;
+      auto v = flow(s, p, no, in_flow);
+      if (!v) return std::nullopt;
+      anchors_[name] = *v;
+      return v;
+    }
+    if (c == '*') {  // an alias: a copy of the anchored node
+      const std::string name = anchor_name(s, p, in_flow);
+      if (name.empty()) return fail(no, "expected an alias name of letters, digits, - or _"), std::nullopt;
+      auto it = anchors_.find(name);
+      if (it == anchors_.end()) return fail(no, "found undefined alias '" + name + "'"), std::nullopt;
+      aliased_ += nodes(it->second);
+      if (aliased_ > kMaxAliasNodes) return fail(no, "aliases expand to too large a document"), std::nullopt;
+      return it->second;
+    }
     if (c == '!') {  // a standard tag: !!str !!null !!bool !!int !!float !!map !!seq
       size_t e = *p;
       while (e < s.size() && !space(s[e])) ++e;
       const std::string tag = s.substr(*p, e - *p);
       *p = e;
       while (*p < s.size() && (s[*p] == ' ' || s[*p] == '\t')) ++*p;
+      std::string anchor;  // `!!str &a x`: the anchor after the tag
+      if (*p < s.size() && s[*p] == '&') {
+        anchor = anchor_name(s, p, in_flow);
+        if (anchor.empty()) return fail(no, "expected an anchor name of letters, digits, - or _"), std::nullopt;
+      }
+      auto keep = [&](json::Value v) {
+        if (!anchor.empty()) anchors_[anchor] = v;
+        return v;
+      };
       const bool quoted = *p < s.size() && (s[*p] == '"' || s[*p] == '\'');
       if (tag == "!!str" && !quoted) {
         bool colon = false;
         std::string text = plain_text(s, p, in_flow, &colon);
         if (colon) return fail(no, "mapping values are not allowed here"), std::nullopt;
-        return json::Value::string(text);
+        return keep(json::Value::string(text));
       }
       auto v = flow(s, p, no, in_flow);
       if (!v) return std::nullopt;
-      if (tag == "!!null") return json::Value{};
+      if (tag == "!!null") return keep(json::Value{});
       if (tag == "!!bool" && v->kind == json::Value::String) {
         json::Value b = plain(v->s);
         if (b.kind != json::Value::Bool) return fail(no, "!!bool on a non-boolean"), std::nullopt;
-        return b;
+        return keep(b);
       }
       if (tag == "!!str" || tag == "!!bool" || tag == "!!int" || tag == "!!float" || tag == "!!map" ||
           tag == "!!seq")
-        return v;  // numbers stay text, as plain ones do
+        return keep(*v);  // numbers stay text, as plain ones do
       return fail(no, "unsupported tag " + tag), std::nullopt;
     }
     if (c == '"') {
@@ -605,13 +764,16 @@ class Parser {
     }
     if (c == '{') {
       json::Value obj = json::Value::object();
+      std::vector<json::Value> merges;  // the values of `<<` keys
+      auto done = [&]() -> std::optional<json::Value> {
+        ++*p;
+        if (!merges.empty() && !merge(&obj, merges, no)) return std::nullopt;
+        return obj;
+      };
       ++*p;
       while (true) {
         while (*p < s.size() && space(s[*p])) ++*p;
-        if (*p < s.size() && s[*p] == '}') {
-          ++*p;
-          return obj;
-        }
+        if (*p < s.size() && s[*p] == '}') return done();
         const bool quoted_key = s[*p] == '"' || s[*p] == '\'';
         auto k = flow(s, p, no, true);
         if (!k) return std::nullopt;
@@ -620,19 +782,22 @@ class Parser {
         ++*p;
         auto v = flow(s, p, no, true);
         if (!v) return std::nullopt;
-        obj.set(flow_key(*k, quoted_key), std::move(*v));
+        if (!quoted_key && k->kind == json::Value::String && k->s == "<<")
+          merges.push_back(std::move(*v));
+        else
+          obj.set(flow_key(*k, quoted_key), std::move(*v));
         while (*p < s.size() && space(s[*p])) ++*p;
         if (*p < s.size() && s[*p] == ',') {
           ++*p;
           continue;
         }
-        if (*p < s.size() && s[*p] == '}') {
-          ++*p;
-          return obj;
-        }
+        if (*p < s.size() && s[*p] == '}') return done();
         return fail(no, "expected , or } in a flow mapping"), std::nullopt;
       }
     }
+    // indicators no plain scalar starts with (in flow , ] } end an empty node instead)
+    if (std::strchr("%@`|>", c) != nullptr || (!in_flow && std::strchr(",]}", c) != nullptr))
+      return fail(no, std::string("found character '") + c + "' that cannot start any token"), std::nullopt;
     bool colon = false;
     std::string text = plain_text(s, p, in_flow, &colon);
     if (colon) return fail(no, "mapping values are not allowed here"), std::nullopt;
@@ -641,6 +806,8 @@ class Parser {
 
   std::string* err_;
   int depth_ = 0;
+  std::map<std::string, json::Value> anchors_;  // &name -> the node (aliases copy it)
+  size_t aliased_ = 0;                            // nodes copied by aliases so far
   std::vector<std::string> raw_;
   std::vector<Line> lines_;
 };

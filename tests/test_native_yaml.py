@@ -65,6 +65,17 @@ def test_native_reader_equals_pyyaml(doc, flow, style, width, unicode):
     "a: |+\n  x\n\n\nb: c\n", "a: >\n  one\n\n\n  two\n", "a: \"one\n\n\n  two\"\n",
     # single-pair mappings inside flow sequences
     "a: [b: c]\n", "a: [b: c, d, \"e\": [f: g], h:]\n", "[x: 1, y]\n", "a: {b:, c: [d:]}\n", "a: [http://x:80/y, z]\n",
+    # anchors and aliases: on scalars, block and flow collections, keys, after/before a tag
+    "a: &x v\nb: *x\n", "a: &x\n  b: v\nc: *x\n", "l1: &id001\n- x\nl2: *id001\n", "f: [&id001 [x, y], *id001]\n",
+    "- &x [v]\n- *x\n", "- &s\n  - v\n- *s\n", "- &s |\n  text\n- *s\n", "a: &x >-\n  f\n  g\nb: *x\n",
+    "a: !!str &x v\nb: *x\n", "a: &x !!str v\nb: *x\n", "a: !!map &m\n  k: v\nb: *m\n", "- &s !!seq\n  - a\n- *s\n",
+    "- &a k: v\n- *a\n", "&k key: v\nother: *k\n", "a: &x k\n*x : v\n", "a: &x k\n*x: v\n", "a: {&q k: *q}\n",
+    "a: &x\nb: *x\n", "a: &x-1_y z\nb: *x-1_y\n",
+    # merge keys: one mapping, a list (the earlier mapping wins), own keys override, in flow
+    "base: &b {x: p, y: q}\nd:\n  <<: *b\n  y: r\n", "a: &a {x: p}\nb: &b {x: q, y: r}\nc:\n  <<: [*a, *b]\n  z: s\n",
+    "a: &a {x: p}\nc: {<<: *a, q: t}\n", "x: &a\n  <<: {p: q}\n  r: s\ny: *a\n", "- <<: {a: b}\n  c: d\n", "\"<<\": v\n",
+    # tags on block values
+    "a: !!str |\n  x\n", "a: !!map\n  b: c\n", "a: !!seq\n- b\n", "a: !!str\n", "a: !!null\n", "- !!map\n  a: b\n",
 ])
 def test_hand_written_documents(text):
     assert native(text) == _stringify(yaml.safe_load(text))
@@ -86,10 +97,47 @@ def _stringify(v):
                                   # a mapping indicator inside a plain scalar (an indentation mistake)
                                   "a: b\n  c: d\n", "a: b c: d\n", "a: v:\n", "- b\n  c: d\n",
                                   # a plain scalar cannot go on past a comment line
-                                  "a: b\n  # c\n  d\n"])
+                                  "a: b\n  # c\n  d\n",
+                                  # aliases to nothing, bad anchor names, merges of non-mappings
+                                  "a: *nope\n", "a: &x.y z\n", "a: &\n", "a: *\n", "a: &a v\nc:\n  <<: *a\n",
+                                  "a: &a [v]\nc:\n  <<: *a\n", "- &s - v\n  - w\n- *s\n",
+                                  # indicators that cannot start a plain scalar; tags on the wrong kind
+                                  "a: , v\n", "a: %x\n", "a: @x\n", "a: `x\n", "a: [|]\n", "a: ]\n", "- ,\n",
+                                  "a: [a, %b]\n", "a: !!str\n  b: c\n", "- !!seq\n- x\n"])
 def test_malformed_documents_are_refused(text):
     """Documents PyYAML refuses are refused here too, with an error."""
     with pytest.raises(yaml.YAMLError):
         yaml.safe_load(text)
     out, err = core().yaml_to_json(text)
     assert out is None and err, (text, out)
+
+
+def test_anchor_redefinition_rebinds():
+    """A later anchor of the same name rebinds it for the aliases after it (YAML 1.2 3.2.2.2,
+    as go-yaml reads it); PyYAML refuses the document instead."""
+    assert native("a: &x v\na2: &x w\nb: *x\n") == {"a": "v", "a2": "w", "b": "w"}
+
+
+_SHARED = st.one_of(st.lists(_SCALAR, min_size=1, max_size=3), st.dictionaries(_KEY, _SCALAR, min_size=1, max_size=3))
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(doc=st.dictionaries(_KEY, _VALUE, max_size=4), shared=_SHARED, keys=st.lists(_KEY, min_size=2, max_size=4),
+       flow=st.sampled_from([False, True, None]), nested=st.booleans())
+def test_shared_nodes_equal_pyyaml(doc, shared, keys, flow, nested):
+    """An object referenced more than once is written once with an anchor (&id001) and
+    then as aliases (*id001); the native reader must expand them as PyYAML does."""
+    doc = dict(doc)
+    for n, k in enumerate(keys):
+        doc[k] = [shared, n] if nested and n % 2 else shared
+    text = yaml.safe_dump(doc, default_flow_style=flow, sort_keys=False)
+    assert native(text) == _stringify(yaml.safe_load(text)), text
+
+
+def test_alias_expansion_is_bounded():
+    """Ten aliases of ten aliases of ... (a "billion laughs") are refused, not expanded."""
+    lines = ["a0: &a0 [x, x, x, x, x, x, x, x, x, x]"]
+    lines += [f"a{i}: &a{i} [" + ", ".join([f"*a{i - 1}"] * 10) + "]" for i in range(1, 12)]
+    out, err = core().yaml_to_json("\n".join(lines) + "\n")
+    assert out is None and "too large" in err
+    assert len(native("\n".join(lines[:4]) + "\n")["a3"]) == 10  # small expansions stay fine

@@ -158,7 +158,9 @@ def make_seeds(work: Path, env: Dict[str, str]) -> Dict[str, Path]:
     config = (b"# plugin config\npulse: 10\nliveness: true\nresource_naming_strategy: mixed\n"
               b"allocator_search: auto\nexporter_socket: ''\nmessage: |\n  literal\n  block\nfolded: >\n"
               b"  a\n  b\nlist: [1, 2, \"three\"]\nnested:\n  - a: 1\n    b: [x, y]\n")
-    seeds["yaml"] += [kubeconfig, config, json.dumps(node).encode()]
+    anchors = (b"base: &b {x: p, y: q}\nl: &l\n- a\n- *b\nd:\n  <<: [*b, {z: r}]\n  y: s\n"
+               b"e: !!str &t |\n  text\nf: [&q k, *q, {&k2 m: *t}]\n&key g: *l\n")
+    seeds["yaml"] += [kubeconfig, config, json.dumps(node).encode(), anchors]
 
     seeds["sysfs"] += [b"", bytes([0, 0, 5, 0]) + b"bad\n\n", bytes([7, 0, 0xFF, 0xFF]),
                        bytes([40, 0, 12, 0]) + b"node_to 999\n"]
