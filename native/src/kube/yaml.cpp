@@ -63,33 +63,60 @@ class Parser {
  public:
   Parser(const std::string& text, std::string* err) : err_(err) {
     int no = 0;
-    size_t pos = 0;
+    size_t pos = text.compare(0, 3, "\xEF\xBB\xBF") == 0 ? 3 : 0;  // a UTF-8 byte order mark
     while (pos <= text.size()) {
       size_t nl = text.find('\n', pos);
       if (nl == std::string::npos) nl = text.size();
       raw_.push_back(text.substr(pos, nl - pos));
       pos = nl + 1;
     }
-    for (const auto& r : raw_) {
+    // One document: directives (%YAML, %TAG) and a `---` may come before it, `...` may end
+    // it; a second document is refused. `--- content` starts the document on that line.
+    bool started = false, ended = false, directives = false;
+    for (auto& r : raw_) {
       ++no;
+      const bool marker = r.compare(0, 3, "---") == 0 && (r.size() == 3 || r[3] == ' ' || r[3] == '\t' || r[3] == '\r');
+      const bool end = r.compare(0, 3, "...") == 0 && (r.size() == 3 || r[3] == ' ' || r[3] == '\t' || r[3] == '\r');
+      if (!started && !marker && r.compare(0, 1, "%") == 0) {
+        directives = true;
+        r.clear();
+        continue;
+      }
+      if (marker || end) {
+        if ((marker && (started || ended)) || (end && ended)) {
+          fail(no, "expected a single document in the stream");
+          return;
+        }
+        started = true;
+        ended = end;
+        r.replace(0, 3, "   ");
+      }
       std::string t = rtrim(r);
       size_t ind = 0;
       while (ind < t.size() && t[ind] == ' ') ++ind;
       std::string body = rtrim(strip_comments(t.substr(ind)));
-      if (body.empty() || body == "---" || body == "...") continue;
+      if (body.empty()) continue;
+      if (ended) {
+        fail(no, "expected a single document in the stream");
+        return;
+      }
+      if (directives && !started) {
+        fail(no, "directives without a document start (---)");
+        return;
+      }
+      started = true;
       lines_.push_back({static_cast<int>(ind), body, no});
     }
+    if (directives && !started) fail(1, "directives without a document start (---)");
   }
 
   std::optional<json::Value> document() {
+    if (!err_->empty()) return std::nullopt;
     if (lines_.empty()) return json::Value::object();
     const char c0 = lines_[0].text[0];
     if (c0 == '[' || c0 == '{') {  // a flow collection as the document, possibly over several lines
       std::string all;
-      for (const auto& r : raw_) {
-        const std::string t = rtrim(r);
-        if (t != "---" && t != "...") all += t + "\n";
-      }
+      for (const auto& r : raw_) all += rtrim(r) + "\n";  // (markers and directives blanked above)
       auto v = scalar_or_flow(strip_comments(all), lines_[0].no);
       if (!err_->empty()) return std::nullopt;
       return v;
@@ -147,6 +174,14 @@ class Parser {
     if (*i >= lines_.size()) return json::Value{};
     if (depth_ > kMaxDepth) return fail(lines_[*i].no, "nested too deeply"), std::nullopt;
     if (is_seq_item(lines_[*i].text)) return sequence(i, indent);
+    if (key_colon(lines_[*i].text) == std::string::npos) {
+      // a scalar or flow collection on the lines below its key (`key:` then `  value`)
+      const Line l = lines_[*i];
+      ++*i;
+      auto v = scalar_or_flow(continued(l.text, l.no, indent - 1, i), l.no);
+      if (v && *i < lines_.size() && lines_[*i].indent >= indent) fail(lines_[*i].no, "unexpected content");
+      return v;
+    }
     return mapping(i, indent);
   }
 
@@ -509,7 +544,7 @@ class Parser {
       v.kind = json::Value::Bool;
       return v;
     }
-    if (t == "null" || t == "~" || t.empty()) return json::Value{};
+    if (t == "null" || t == "Null" || t == "NULL" || t == "~" || t.empty()) return json::Value{};
     return json::Value::string(t);
   }
 
@@ -795,6 +830,10 @@ class Parser {
         return fail(no, "expected , or } in a flow mapping"), std::nullopt;
       }
     }
+    if (c == '-' && (*p + 1 == s.size() || space(s[*p + 1])))
+      return fail(no, "sequence entries are not allowed here"), std::nullopt;
+    if (c == '?' && (*p + 1 == s.size() || space(s[*p + 1])))
+      return fail(no, "complex keys (? key) are not supported"), std::nullopt;
     // indicators no plain scalar starts with (in flow , ] } end an empty node instead)
     if (std::strchr("%@`|>", c) != nullptr || (!in_flow && std::strchr(",]}", c) != nullptr))
       return fail(no, std::string("found character '") + c + "' that cannot start any token"), std::nullopt;

@@ -74,6 +74,11 @@ def test_native_reader_equals_pyyaml(doc, flow, style, width, unicode):
     # merge keys: one mapping, a list (the earlier mapping wins), own keys override, in flow
     "base: &b {x: p, y: q}\nd:\n  <<: *b\n  y: r\n", "a: &a {x: p}\nb: &b {x: q, y: r}\nc:\n  <<: [*a, *b]\n  z: s\n",
     "a: &a {x: p}\nc: {<<: *a, q: t}\n", "x: &a\n  <<: {p: q}\n  r: s\ny: *a\n", "- <<: {a: b}\n  c: d\n", "\"<<\": v\n",
+    # one document with its markers and directives, a byte order mark, CRLF, Null / NULL,
+    # scalars and flow collections on the lines below their key
+    "---\ngpu:\n  device_count: 2\n", "--- # c\na: b\n", "a: b\n...\n", "%YAML 1.1\n---\na: b\n",
+    "\ufeffa: b\n", "a: b\r\nc: d\r\n", "--- {a: b}\n", "--- [x,\n  y]\n", "---\n- x\n", "a: Null\nb: NULL\n",
+    "a:    \n  b\n", "a:\n  b\n  c\nd: e\n", "a:\n  \"q\"\n", "a:\n  [x, y]\n", "- \n  {b: c}\n",
     # tags on block values
     "a: !!str |\n  x\n", "a: !!map\n  b: c\n", "a: !!seq\n- b\n", "a: !!str\n", "a: !!null\n", "- !!map\n  a: b\n",
 ])
@@ -103,11 +108,22 @@ def _stringify(v):
                                   "a: &a [v]\nc:\n  <<: *a\n", "- &s - v\n  - w\n- *s\n",
                                   # indicators that cannot start a plain scalar; tags on the wrong kind
                                   "a: , v\n", "a: %x\n", "a: @x\n", "a: `x\n", "a: [|]\n", "a: ]\n", "- ,\n",
-                                  "a: [a, %b]\n", "a: !!str\n  b: c\n", "- !!seq\n- x\n"])
+                                  "a: [a, %b]\n", "a: !!str\n  b: c\n", "- !!seq\n- x\n",
+                                  # a second document, directives without ---, a stray "- "
+                                  "a: b\n---\nc: d\n", "a: b\n...\nc: d\n", "%YAML 1.1\na: b\n", "a: - b\n",
+                                  "a: -\n", "a:\n  b\n   c: d\n"])
 def test_malformed_documents_are_refused(text):
     """Documents PyYAML refuses are refused here too, with an error."""
     with pytest.raises(yaml.YAMLError):
         yaml.safe_load(text)
+    out, err = core().yaml_to_json(text)
+    assert out is None and err, (text, out)
+
+
+@pytest.mark.parametrize("text", ["? a\n: b\n", "a: !!binary |\n  eA==\n"])
+def test_unsupported_documents_are_refused(text):
+    """What PyYAML reads but no config here needs (complex keys, bytes) is refused, not misread."""
+    yaml.safe_load(text)
     out, err = core().yaml_to_json(text)
     assert out is None and err, (text, out)
 
