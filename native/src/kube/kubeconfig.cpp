@@ -61,14 +61,22 @@ std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* 
     *error = "kubeconfig " + path + ": " + (perr.empty() ? "not a mapping" : perr);
     return std::nullopt;
   }
+  // a name that is set must be found (as client-go validates it); an unset one takes the first entry
   const std::string ctx_name = doc->str("current-context");
   const json::Value* ctx = named(doc->get("contexts"), ctx_name, "context");
-  if (!ctx) ctx = named(doc->get("contexts"), "", "context");
+  if (!ctx && !ctx_name.empty()) {
+    *error = "kubeconfig " + path + ": context \"" + ctx_name + "\" not found";
+    return std::nullopt;
+  }
   const std::string cluster_name = ctx ? ctx->str("cluster") : "", user_name = ctx ? ctx->str("user") : "";
   const json::Value* cluster = named(doc->get("clusters"), cluster_name, "cluster");
-  if (!cluster) cluster = named(doc->get("clusters"), "", "cluster");
   const json::Value* user = named(doc->get("users"), user_name, "user");
-  if (!user) user = named(doc->get("users"), "", "user");
+  if ((!cluster && !cluster_name.empty()) || (!user && !user_name.empty())) {
+    *error = "kubeconfig " + path + ": " + (!cluster && !cluster_name.empty() ? "cluster \"" + cluster_name
+                                                                                : "user \"" + user_name) +
+             "\" of context \"" + ctx_name + "\" not found";
+    return std::nullopt;
+  }
   if (!cluster || cluster->str("server").empty()) {
     *error = "kubeconfig " + path + ": no cluster server for context \"" + ctx_name + "\"";
     return std::nullopt;
@@ -98,6 +106,15 @@ std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* 
     kc.http.key_file = rel(user->str("client-key"));
     if (!data(user, "client-certificate-data", &kc.http.cert_pem)) return std::nullopt;
     if (!data(user, "client-key-data", &kc.http.key_pem)) return std::nullopt;
+  }
+  if (user && kc.token.empty() && kc.token_file.empty() && kc.http.cert_file.empty() && kc.http.cert_pem.empty()) {
+    // credentials this labeller cannot produce: refused rather than sent unauthenticated
+    for (const char* plugin : {"exec", "auth-provider", "username"})
+      if (user->get(plugin)) {
+        *error = "kubeconfig " + path + ": user \"" + user_name + "\" authenticates with " + plugin +
+                 ", which the labeller does not support; give it a token, tokenFile or client certificate";
+        return std::nullopt;
+      }
   }
   if (!kc.token_file.empty()) {
     auto t = read_trimmed(kc.token_file);

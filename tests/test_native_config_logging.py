@@ -350,10 +350,32 @@ users:
         srv.stop()
 
 
+_KC = """clusters:
+- name: c
+  cluster: {{server: "http://127.0.0.1:9"}}
+contexts:
+- name: x
+  context: {{cluster: {cluster}, user: {user}}}
+current-context: {ctx}
+users:
+- name: u
+  user: {{{cred}}}
+"""
+
+
 def test_kubeconfig_errors_are_reported(tmp_path):
     for text, want in (("clusters: [", "kubeconfig"), ("users: []\n", "no cluster server"),
                        ("clusters:\n- name: a\n  cluster:\n    server: http://x\n    certificate-authority-data: '%%%'\n",
-                        "base64")):
+                        "base64"),
+                       # a dangling current-context / cluster / user name is not replaced by the first entry
+                       (_KC.format(ctx="y", cluster="c", user="u", cred="token: t"), 'context "y" not found'),
+                       (_KC.format(ctx="x", cluster="c2", user="u", cred="token: t"), 'cluster "c2" of context "x"'),
+                       (_KC.format(ctx="x", cluster="c", user="u2", cred="token: t"), 'user "u2" of context "x"'),
+                       # credential plugins are refused, not skipped into unauthenticated requests
+                       (_KC.format(ctx="x", cluster="c", user="u", cred="exec: {command: aws}"), "authenticates with exec"),
+                       (_KC.format(ctx="x", cluster="c", user="u", cred="auth-provider: {name: gcp}"),
+                        "authenticates with auth-provider"),
+                       (_KC.format(ctx="x", cluster="c", user="u", cred="username: admin"), "authenticates with username")):
         kc = tmp_path / "kc"
         kc.write_text(text)
         p = subprocess.run([LBL, "-node_name", "n", "-kubeconfig", str(kc)], capture_output=True, text=True,
