@@ -442,15 +442,18 @@ clk::time_point after_s(double s) {
 }
 
 // The apiserver client as controller-runtime's GetConfigOrDie sets it up:
-// -kubeconfig, else in-cluster unless $KUBECONFIG is set, else $KUBECONFIG /
-// $HOME/.kube/config; in-cluster: the service account's token and CA.
+// -kubeconfig, else in-cluster unless $KUBECONFIG is set, else $KUBECONFIG (the
+// list's files merged) / $HOME/.kube/config; in-cluster: the service account's token and CA.
 bool configure_kube(const Flags& f, Kube* kube) {
   std::string err;
   const char* svc_host = std::getenv("KUBERNETES_SERVICE_HOST");
   const bool in_cluster = (svc_host && *svc_host) || !f.apiserver.empty();
-  const std::string kc_path = !f.kubeconfig.empty() ? f.kubeconfig : kube::default_kubeconfig_path(in_cluster);
-  if (!kc_path.empty()) {
-    auto kc = kube::load_kubeconfig(kc_path, &err);
+  const std::vector<std::string> kc_paths =
+      !f.kubeconfig.empty() ? std::vector<std::string>{f.kubeconfig} : kube::default_kubeconfig_paths(in_cluster);
+  if (!kc_paths.empty()) {
+    auto kc = kube::load_kubeconfig_files(kc_paths, &err);
+    std::string kc_path;
+    for (const auto& p : kc_paths) kc_path += (kc_path.empty() ? "" : ":") + p;
     if (!kc) {
       MI_LOG(kError, "unable to set up kubernetes client: %s", err.c_str());
       return false;

@@ -47,20 +47,70 @@ const json::Value* named(const json::Value* list, const std::string& name, const
   return name.empty() ? first : nullptr;
 }
 
+// the file paths an entry names, made absolute against the file's directory (as
+// clientcmd resolves them before it merges files)
+void resolve_paths(json::Value* doc, const std::string& base) {
+  static const std::pair<const char*, std::vector<const char*>> kFields[] = {
+      {"clusters", {"certificate-authority"}},
+      {"users", {"client-certificate", "client-key", "tokenFile"}}};
+  for (const auto& [list, fields] : kFields) {
+    json::Value* l = doc->get(list);
+    if (!l || l->kind != json::Value::Array) continue;
+    for (auto& e : l->arr) {
+      json::Value* body = e.get(std::string(list) == "clusters" ? "cluster" : "user");
+      if (!body || body->kind != json::Value::Object) continue;
+      for (const char* f : fields) {
+        json::Value* v = body->get(f);
+        if (v && v->kind == json::Value::String && !v->s.empty() && v->s[0] != '/') v->s = base + "/" + v->s;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* error) {
-  auto text = read_file(path);
-  if (!text) {
-    *error = "kubeconfig " + path + ": unreadable";
-    return std::nullopt;
+  return load_kubeconfig_files({path}, error);
+}
+
+std::optional<KubeConfig> load_kubeconfig_files(const std::vector<std::string>& paths, std::string* error) {
+  // clientcmd's merge of a $KUBECONFIG list: the first file that sets current-context
+  // wins it, and a cluster / context / user comes from the first file that names it
+  json::Value merged = json::Value::object();
+  std::string path;  // for messages: the files, ':'-joined
+  for (const auto& p : paths) {
+    path += (path.empty() ? "" : ":") + p;
+    auto text = read_file(p);
+    if (!text) {
+      *error = "kubeconfig " + p + ": unreadable";
+      return std::nullopt;
+    }
+    std::string perr;
+    auto doc = yaml::parse(*text, &perr);
+    if (!doc || doc->kind != json::Value::Object) {
+      *error = "kubeconfig " + p + ": " + (perr.empty() ? "not a mapping" : perr);
+      return std::nullopt;
+    }
+    resolve_paths(&*doc, p.find('/') == std::string::npos ? "." : p.substr(0, p.rfind('/')));
+    if (merged.str("current-context").empty() && !doc->str("current-context").empty())
+      merged.set("current-context", json::Value::string(doc->str("current-context")));
+    for (const char* list : {"clusters", "contexts", "users"}) {
+      const json::Value* l = doc->get(list);
+      if (!l || l->kind != json::Value::Array) continue;
+      json::Value* into = merged.get(list);
+      if (!into) {
+        json::Value arr;
+        arr.kind = json::Value::Array;
+        into = &merged.set(list, std::move(arr));
+      }
+      for (const auto& e : l->arr) {
+        bool seen = false;
+        for (const auto& have : into->arr) seen = seen || have.str("name") == e.str("name");
+        if (!seen) into->arr.push_back(e);
+      }
+    }
   }
-  std::string perr;
-  auto doc = yaml::parse(*text, &perr);
-  if (!doc || doc->kind != json::Value::Object) {
-    *error = "kubeconfig " + path + ": " + (perr.empty() ? "not a mapping" : perr);
-    return std::nullopt;
-  }
+  const json::Value* doc = &merged;
   // a name that is set must be found (as client-go validates it); an unset one takes the first entry
   const std::string ctx_name = doc->str("current-context");
   const json::Value* ctx = named(doc->get("contexts"), ctx_name, "context");
@@ -81,8 +131,6 @@ std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* 
     *error = "kubeconfig " + path + ": no cluster server for context \"" + ctx_name + "\"";
     return std::nullopt;
   }
-  const std::string base = path.find('/') == std::string::npos ? "." : path.substr(0, path.rfind('/'));
-  auto rel = [&](const std::string& p) { return p.empty() || p[0] == '/' ? p : base + "/" + p; };
   auto data = [&](const json::Value* v, const char* key, std::string* out) {
     const std::string enc = v ? v->str(key) : "";
     if (enc.empty()) return true;
@@ -95,15 +143,15 @@ std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* 
   std::string server = cluster->str("server");
   while (!server.empty() && server.back() == '/') server.pop_back();
   kc.http.server = server;
-  kc.http.ca_file = rel(cluster->str("certificate-authority"));
+  kc.http.ca_file = cluster->str("certificate-authority");
   if (!data(cluster, "certificate-authority-data", &kc.http.ca_pem)) return std::nullopt;
   if (const json::Value* ins = cluster->get("insecure-skip-tls-verify"))
     kc.http.insecure = ins->kind == json::Value::Bool ? ins->b : ins->s == "true";
   if (user) {
     kc.token = user->str("token");
-    if (kc.token.empty()) kc.token_file = rel(user->str("tokenFile"));
-    kc.http.cert_file = rel(user->str("client-certificate"));
-    kc.http.key_file = rel(user->str("client-key"));
+    if (kc.token.empty()) kc.token_file = user->str("tokenFile");
+    kc.http.cert_file = user->str("client-certificate");
+    kc.http.key_file = user->str("client-key");
     if (!data(user, "client-certificate-data", &kc.http.cert_pem)) return std::nullopt;
     if (!data(user, "client-key-data", &kc.http.key_pem)) return std::nullopt;
   }
@@ -126,24 +174,28 @@ std::optional<KubeConfig> load_kubeconfig(const std::string& path, std::string* 
   return kc;
 }
 
-std::string default_kubeconfig_path(bool in_cluster_available) {
+std::vector<std::string> default_kubeconfig_paths(bool in_cluster_available) {
   const char* env = std::getenv("KUBECONFIG");
   if (!env || !*env) {
-    if (in_cluster_available) return "";
+    if (in_cluster_available) return {};
     const char* home = std::getenv("HOME");
     const std::string p = std::string(home && *home ? home : "") + "/.kube/config";
-    return home && *home && path_exists(p) ? p : "";
+    if (home && *home && path_exists(p)) return {p};
+    return {};
   }
-  std::string list = env;
+  std::vector<std::string> out;
+  const std::string list = env;
   size_t pos = 0;
   while (pos <= list.size()) {
     size_t c = list.find(':', pos);
     if (c == std::string::npos) c = list.size();
     const std::string p = list.substr(pos, c - pos);
-    if (!p.empty() && path_exists(p)) return p;
+    bool dup = false;
+    for (const auto& q : out) dup = dup || q == p;
+    if (!p.empty() && !dup && path_exists(p)) out.push_back(p);  // missing entries are skipped
     pos = c + 1;
   }
-  return "";
+  return out;
 }
 
 }  // namespace mi355x::kube

@@ -280,7 +280,7 @@ def test_kubeconfig_flow_yaml_static_token_and_env_order(tmp_path):
                       "users: [{name: a, user: {token: t0}}]\n")
         assert _label_once(kc, fi).returncode == 0
         assert srv.labels("worker")["amd.com/gpu.mode"] == "container"
-        # no flag, no in-cluster env: $KUBECONFIG (first existing entry of the list)
+        # no flag, no in-cluster env: $KUBECONFIG (missing entries of the list skipped)
         srv.set_labels("worker", {})
         p = _label_once(None, fi, env=_env(KUBECONFIG=f"{tmp_path}/missing:{kc}"))
         assert p.returncode == 0, p.stderr and srv.labels("worker")["amd.com/gpu.mode"] == "container"
@@ -361,6 +361,37 @@ users:
 - name: u
   user: {{{cred}}}
 """
+
+
+def test_kubeconfig_list_is_merged_like_clientcmd(tmp_path):
+    """$KUBECONFIG=a:b: current-context from the first file that sets it, each named
+    entry from the first file naming it, relative paths against that entry's file."""
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="t0").start()
+    try:
+        srv.add_node("worker")
+        (tmp_path / "a").mkdir()
+        (tmp_path / "b").mkdir()
+        (tmp_path / "a" / "tok").write_text("t0\n")
+        ka, kb = tmp_path / "a" / "config", tmp_path / "b" / "config"
+        ka.write_text("current-context: x\ncontexts: [{name: x, context: {cluster: c, user: u}}]\n"
+                      "users: [{name: u, user: {tokenFile: tok}}]\n")
+        kb.write_text(f"current-context: other\nclusters: [{{name: c, cluster: {{server: '{srv.url}'}}}}]\n"
+                      "contexts: [{name: other, context: {cluster: c, user: v}}]\n"
+                      "users: [{name: u, user: {token: nope}}, {name: v, user: {token: nope}}]\n")
+        p = _label_once(None, fi, env=_env(KUBECONFIG=f"{ka}:{tmp_path}/missing:{kb}"))
+        assert p.returncode == 0, p.stderr
+        assert srv.labels("worker")["amd.com/gpu.mode"] == "container"
+        # the other order: b's context and user win, whose token the apiserver refuses
+        srv.set_labels("worker", {})
+        proc = subprocess.Popen([LBL, "-node_name", "worker", "-once", "-mode", "-sysfs_root", str(fi.sysfs)],
+                                stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                                env=_env(KUBECONFIG=f"{kb}:{ka}"))
+        time.sleep(0.8)
+        rc, err = _term(proc)
+        assert "HTTP 401" in err and "amd.com/gpu.mode" not in srv.labels("worker")
+    finally:
+        srv.stop()
 
 
 def test_kubeconfig_errors_are_reported(tmp_path):
