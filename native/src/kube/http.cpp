@@ -189,11 +189,12 @@ std::string Conn::open(const Config& cfg) {
   }
   ssl_ = SSL_new(ctx_);
   if (!ssl_) return ssl_error();
-  if (is_ip(host_)) {
-    X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl_), host_.c_str());
+  const std::string& name = cfg.tls_server_name.empty() ? host_ : cfg.tls_server_name;
+  if (is_ip(name)) {
+    X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl_), name.c_str());
   } else {
-    SSL_set_tlsext_host_name(ssl_, host_.c_str());
-    SSL_set1_host(ssl_, host_.c_str());
+    SSL_set_tlsext_host_name(ssl_, name.c_str());
+    SSL_set1_host(ssl_, name.c_str());
   }
   SSL_set_fd(ssl_, fd_);
   if (SSL_connect(ssl_) != 1) {

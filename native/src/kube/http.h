@@ -20,6 +20,7 @@ struct Config {
   // client certificate auth (kubeconfig users[].user): files or PEM in memory
   std::string cert_file, key_file, cert_pem, key_pem;
   bool insecure = false;
+  std::string tls_server_name;  // kubeconfig tls-server-name: SNI and the name the certificate must carry
   double timeout_s = 15.0;
 };
 

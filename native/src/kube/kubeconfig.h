@@ -5,7 +5,7 @@
 // $HOME/.kube/config.
 //
 // The file is YAML (or JSON). Only what a client needs is read: the current
-// context's cluster (server, certificate-authority[-data],
+// context's cluster (server, certificate-authority[-data], tls-server-name,
 // insecure-skip-tls-verify) and user (token, tokenFile,
 // client-certificate[-data], client-key[-data]); relative paths resolve
 // against the file's directory, as clientcmd does.

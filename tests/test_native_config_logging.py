@@ -394,6 +394,39 @@ def test_kubeconfig_list_is_merged_like_clientcmd(tmp_path):
         srv.stop()
 
 
+def test_kubeconfig_tls_server_name(tmp_path):
+    """tls-server-name replaces the server's host for SNI and the certificate check:
+    the server's certificate names kubernetes.default.svc and 127.0.0.1."""
+    d = tmp_path / "pki"
+    d.mkdir()
+    _tls_material(d)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="t0", tls=(str(d / "srv.crt"), str(d / "srv.key"))).start()
+    try:
+        srv.add_node("worker")
+        kc = tmp_path / "kc"
+        for name, ok in (("kubernetes.default.svc", True), ("other.example", False), ("", True)):
+            line = f"    tls-server-name: {name}\n" if name else ""
+            kc.write_text(f"clusters:\n- name: c\n  cluster:\n    server: {srv.url}\n    certificate-authority: pki/ca.crt\n"
+                          f"{line}contexts: [{{name: x, context: {{cluster: c, user: u}}}}]\ncurrent-context: x\n"
+                          "users: [{name: u, user: {token: t0}}]\n")
+            srv.set_labels("worker", {})
+            if ok:
+                p = _label_once(kc, fi)
+                assert p.returncode == 0, (name, p.stderr)
+                assert srv.labels("worker")["amd.com/gpu.mode"] == "container"
+                continue
+            proc = subprocess.Popen([LBL, "-node_name", "worker", "-once", "-mode", "-sysfs_root", str(fi.sysfs),
+                                     "-kubeconfig", str(kc)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                    text=True, env=_env())
+            time.sleep(1.0)
+            rc, err = _term(proc)
+            assert "certificate verify failed" in err, err
+            assert "amd.com/gpu.mode" not in srv.labels("worker")
+    finally:
+        srv.stop()
+
+
 def test_kubeconfig_errors_are_reported(tmp_path):
     for text, want in (("clusters: [", "kubeconfig"), ("users: []\n", "no cluster server"),
                        ("clusters:\n- name: a\n  cluster:\n    server: http://x\n    certificate-authority-data: '%%%'\n",
