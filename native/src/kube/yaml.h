@@ -3,9 +3,11 @@
 // too), plain and quoted scalars over several lines with YAML's line folding
 // and escaped line breaks, literal / folded block scalars with chomping and
 // indentation indicators, the standard !!str / !!null / !!bool / !!int /
-// !!float tags, and comments, into a JSON value. Plain scalars other than
-// booleans and null stay text. JSON documents are read as JSON. Anchors,
-// custom tags, complex (`?`) keys and multi-document streams are refused (no
+// !!float tags, anchors / aliases / merge keys (aliases copy the anchored
+// node, at most 2^20 nodes per document), one document with its --- / ...
+// markers and % directives, and comments, into a JSON value. Plain scalars
+// other than booleans and null stay text. JSON documents are read as JSON.
+// Custom tags, complex (`?`) keys and a second document are refused (no
 // kubeconfig or plugin config uses them). Checked against PyYAML on generated
 // documents (tests/test_native_yaml.py).
 #pragma once
