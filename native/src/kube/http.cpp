@@ -23,7 +23,11 @@ namespace mi355x::http {
 
 namespace {
 
-bool parse_url(const std::string& url, bool* tls, std::string* host, int* port) {
+// scheme://host[:port][/prefix]: *authority gets "host[:port]" as written (the Host
+// header, as Go's net/http sends it), *prefix the path without its trailing '/'
+// (requests go below it, e.g. an apiserver behind a proxy at /k8s/clusters/c-1)
+bool parse_url(const std::string& url, bool* tls, std::string* host, int* port, std::string* authority = nullptr,
+               std::string* prefix = nullptr) {
   std::string rest;
   if (url.rfind("https://", 0) == 0) {
     *tls = true;
@@ -34,8 +38,16 @@ bool parse_url(const std::string& url, bool* tls, std::string* host, int* port) 
   } else {
     return false;
   }
-  const size_t slash = rest.find('/');
-  if (slash != std::string::npos) rest = rest.substr(0, slash);
+  const size_t slash = rest.find_first_of("/?#");
+  std::string path;
+  if (slash != std::string::npos) {
+    path = rest.substr(slash);
+    rest = rest.substr(0, slash);
+  }
+  if (path.find_first_of("?#") != std::string::npos) return false;  // a query or fragment is no API root
+  while (!path.empty() && path.back() == '/') path.pop_back();
+  if (authority) *authority = rest;
+  if (prefix) *prefix = path;
   *port = *tls ? 443 : 80;
   if (!rest.empty() && rest[0] == '[') {  // [v6]:port
     const size_t close = rest.find(']');
@@ -92,7 +104,7 @@ std::string Conn::open(const Config& cfg) {
   close();
   bool tls = false;
   int port = 0;
-  if (!parse_url(cfg.server, &tls, &host_, &port)) return "bad server URL " + cfg.server;
+  if (!parse_url(cfg.server, &tls, &host_, &port, &authority_, &prefix_)) return "bad server URL " + cfg.server;
   addrinfo hints{};
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -329,8 +341,8 @@ std::string start(Conn* c, const Config& cfg, const std::string& method, const s
                   int timeout_ms, int wake_fd) {
   std::string err = c->open(cfg);
   if (!err.empty()) return err;
-  const std::string host = c->host().find(':') != std::string::npos ? "[" + c->host() + "]" : c->host();  // IPv6
-  std::string req = method + " " + path + " HTTP/1.1\r\nHost: " + host + "\r\nConnection: close\r\n";
+  std::string req = method + " " + c->prefix() + path + " HTTP/1.1\r\nHost: " + c->authority() +
+                    "\r\nConnection: close\r\n";
   for (const auto& [k, v] : headers) req += k + ": " + v + "\r\n";
   if (!body.empty() || method == "PATCH" || method == "PUT" || method == "POST")
     req += "Content-Length: " + std::to_string(body.size()) + "\r\n";

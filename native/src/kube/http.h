@@ -45,12 +45,14 @@ class Conn {
   long read_some(char* buf, size_t n, int timeout_ms, int wake_fd = -1);
   void close();
   const std::string& host() const { return host_; }
+  const std::string& authority() const { return authority_; }  // host[:port] as the server URL writes it
+  const std::string& prefix() const { return prefix_; }        // the server URL's path, below which requests go
 
  private:
   int fd_ = -1;
   SSL_CTX* ctx_ = nullptr;
   SSL* ssl_ = nullptr;
-  std::string host_;
+  std::string host_, authority_, prefix_;
 };
 
 // A response body read incrementally (Content-Length, chunked, or to EOF).

@@ -30,11 +30,15 @@ def merge_patch(target, patch):
 
 class FakeApiServer:
     def __init__(self, token: Optional[str] = "test-token", tls: Optional[Tuple[str, str]] = None,
-                 client_ca: Optional[str] = None, host: str = "127.0.0.1"):
+                 client_ca: Optional[str] = None, host: str = "127.0.0.1", prefix: str = ""):
         """tls: (cert chain PEM, key PEM) to serve HTTPS; client_ca: also require
         a client certificate signed by this CA (kubeconfig client-certificate auth);
-        host: the listen address ("::1" for an IPv6 cluster)."""
+        host: the listen address ("::1" for an IPv6 cluster); prefix: the API is
+        served below this path only (an apiserver behind a proxy, e.g.
+        /k8s/clusters/c-1), which ``url`` includes."""
         self.host = host
+        self.prefix = prefix.rstrip("/")
+        self.host_headers: List[str] = []
         self.token = token
         self.nodes: Dict[str, dict] = {}
         self.requests: List[Tuple[str, str, Optional[dict]]] = []
@@ -120,6 +124,12 @@ class FakeApiServer:
                 return None
 
             def _handle(self, method):
+                with srv._lock:
+                    srv.host_headers.append(self.headers.get("Host", ""))
+                if srv.prefix:
+                    if not self.path.startswith(srv.prefix + "/"):
+                        return self._send(404, {"kind": "Status", "message": f"{self.path} is outside {srv.prefix}"})
+                    self.path = self.path[len(srv.prefix):]
                 url = urllib.parse.urlparse(self.path)
                 q = urllib.parse.parse_qs(url.query)
                 if method == "GET" and url.path.rstrip("/") == "/api/v1/nodes" and q.get("watch") == ["1"]:
@@ -193,7 +203,7 @@ class FakeApiServer:
     @property
     def url(self) -> str:
         host = f"[{self.host}]" if ":" in self.host else self.host
-        return f"{self.scheme}://{host}:{self.port}"
+        return f"{self.scheme}://{host}:{self.port}{self.prefix}"
 
     def _store(self, name: str, node: dict, event: str) -> None:
         """(lock held) bump the resourceVersion, store, notify watchers."""

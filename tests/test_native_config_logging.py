@@ -427,6 +427,37 @@ def test_kubeconfig_tls_server_name(tmp_path):
         srv.stop()
 
 
+@pytest.mark.parametrize("trailing", ["", "/"])
+def test_server_url_path_prefix_and_host_header(tmp_path, trailing):
+    """A server URL with a path (an apiserver behind a proxy at /k8s/clusters/<id>, as
+    client-go takes it) prefixes every request, watches included; the Host header
+    carries the URL's host:port, as Go's net/http sends it."""
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="t0", prefix="/k8s/clusters/c-1").start()
+    try:
+        srv.add_node("worker")
+        kc = tmp_path / "kc"
+        kc.write_text(f"clusters: [{{name: c, cluster: {{server: '{srv.url}{trailing}'}}}}]\n"
+                      "contexts: [{name: x, context: {cluster: c, user: u}}]\ncurrent-context: x\n"
+                      "users: [{name: u, user: {token: t0}}]\n")
+        p = _label_once(kc, fi)
+        assert p.returncode == 0, p.stderr
+        assert srv.labels("worker")["amd.com/gpu.mode"] == "container"
+        assert srv.requests and all(r[1].startswith("/api/v1/nodes") for r in srv.requests), srv.requests
+        assert set(srv.host_headers) == {f"127.0.0.1:{srv.port}"}, srv.host_headers
+        # the watch goes below the prefix too
+        proc = subprocess.Popen([LBL, "-node_name", "worker", "-mode", "-sysfs_root", str(fi.sysfs),
+                                 "-kubeconfig", str(kc)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                text=True, env=_env())
+        deadline = time.monotonic() + 10
+        while srv.watch_starts == 0 and time.monotonic() < deadline:
+            time.sleep(0.05)
+        rc, err = _term(proc)
+        assert srv.watch_starts >= 1, err
+    finally:
+        srv.stop()
+
+
 def test_kubeconfig_errors_are_reported(tmp_path):
     for text, want in (("clusters: [", "kubeconfig"), ("users: []\n", "no cluster server"),
                        ("clusters:\n- name: a\n  cluster:\n    server: http://x\n    certificate-authority-data: '%%%'\n",
