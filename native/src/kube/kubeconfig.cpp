@@ -156,6 +156,11 @@ std::optional<KubeConfig> load_kubeconfig_files(const std::vector<std::string>& 
     if (!data(user, "client-certificate-data", &kc.http.cert_pem)) return std::nullopt;
     if (!data(user, "client-key-data", &kc.http.key_pem)) return std::nullopt;
   }
+  if (kc.http.insecure && (!kc.http.ca_file.empty() || !kc.http.ca_pem.empty())) {
+    // as client-go's transport refuses it (vendor/k8s.io/client-go/transport/transport.go:81-83)
+    *error = "kubeconfig " + path + ": specifying a root certificates file with the insecure flag is not allowed";
+    return std::nullopt;
+  }
   if (user && kc.token.empty() && kc.token_file.empty() && kc.http.cert_file.empty() && kc.http.cert_pem.empty()) {
     // credentials this labeller cannot produce: refused rather than sent unauthenticated
     for (const char* plugin : {"exec", "auth-provider", "username"})

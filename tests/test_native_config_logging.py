@@ -470,7 +470,11 @@ def test_kubeconfig_errors_are_reported(tmp_path):
                        (_KC.format(ctx="x", cluster="c", user="u", cred="exec: {command: aws}"), "authenticates with exec"),
                        (_KC.format(ctx="x", cluster="c", user="u", cred="auth-provider: {name: gcp}"),
                         "authenticates with auth-provider"),
-                       (_KC.format(ctx="x", cluster="c", user="u", cred="username: admin"), "authenticates with username")):
+                       (_KC.format(ctx="x", cluster="c", user="u", cred="username: admin"), "authenticates with username"),
+                       # a CA and insecure-skip-tls-verify together, as client-go's transport refuses them
+                       (_KC.format(ctx="x", cluster="c", user="u", cred="token: t").replace(
+                           'server: "http://127.0.0.1:9"', 'server: "https://127.0.0.1:9", certificate-authority-data: QUJD, '
+                           'insecure-skip-tls-verify: true'), "root certificates file with the insecure flag")):
         kc = tmp_path / "kc"
         kc.write_text(text)
         p = subprocess.run([LBL, "-node_name", "n", "-kubeconfig", str(kc)], capture_output=True, text=True,
