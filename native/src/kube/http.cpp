@@ -14,7 +14,10 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <cctype>
 #include <cerrno>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -81,7 +84,160 @@ std::string lower(std::string s) {
   return s;
 }
 
+// TCP connection to host:port within tmo_ms (every resolved address tried); "" or an error
+std::string connect_tcp(const std::string& host, int port, int tmo_ms, int* out) {
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  addrinfo* res = nullptr;
+  const int gai = getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res);
+  if (gai != 0) return std::string("resolve ") + host + ": " + gai_strerror(gai);
+  std::string err = "no address for " + host;
+  for (addrinfo* a = res; a; a = a->ai_next) {
+    const int fd = ::socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, a->ai_protocol);
+    if (fd < 0) continue;
+    int rc = ::connect(fd, a->ai_addr, a->ai_addrlen);
+    if (rc != 0 && errno == EINPROGRESS) {
+      pollfd p{fd, POLLOUT, 0};
+      rc = ::poll(&p, 1, tmo_ms) == 1 ? 0 : -1;
+      int so = 0;
+      socklen_t sl = sizeof(so);
+      if (rc == 0 && (getsockopt(fd, SOL_SOCKET, SO_ERROR, &so, &sl) != 0 || so != 0)) {
+        errno = so ? so : errno;
+        rc = -1;
+      } else if (rc != 0) {
+        errno = ETIMEDOUT;
+      }
+    }
+    if (rc == 0) {
+      ::fcntl(fd, F_SETFL, ::fcntl(fd, F_GETFL) & ~O_NONBLOCK);
+      const int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+      *out = fd;
+      freeaddrinfo(res);
+      return "";
+    }
+    err = "connect " + host + ":" + std::to_string(port) + ": " + std::strerror(errno);
+    ::close(fd);
+  }
+  freeaddrinfo(res);
+  return err;
+}
+
+std::string b64(const std::string& in) {
+  static const char* tbl = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string out;
+  size_t i = 0;
+  for (; i + 2 < in.size(); i += 3) {
+    const uint32_t v = (uint8_t(in[i]) << 16) | (uint8_t(in[i + 1]) << 8) | uint8_t(in[i + 2]);
+    for (int k = 18; k >= 0; k -= 6) out.push_back(tbl[(v >> k) & 63]);
+  }
+  if (i < in.size()) {
+    const uint32_t v = (uint8_t(in[i]) << 16) | (i + 1 < in.size() ? uint8_t(in[i + 1]) << 8 : 0);
+    out.push_back(tbl[(v >> 18) & 63]);
+    out.push_back(tbl[(v >> 12) & 63]);
+    out.push_back(i + 1 < in.size() ? tbl[(v >> 6) & 63] : '=');
+    out.push_back('=');
+  }
+  return out;
+}
+
+std::string pct_decode(const std::string& s) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && std::isxdigit(static_cast<unsigned char>(s[i + 1])) &&
+        std::isxdigit(static_cast<unsigned char>(s[i + 2]))) {
+      out.push_back(static_cast<char>(std::stoi(s.substr(i + 1, 2), nullptr, 16)));
+      i += 2;
+    } else {
+      out.push_back(s[i]);
+    }
+  }
+  return out;
+}
+
+bool ip_in_cidr(const std::string& ip, const std::string& cidr) {
+  const size_t slash = cidr.find('/');
+  if (slash == std::string::npos) return false;
+  const std::string net = cidr.substr(0, slash);
+  char* end = nullptr;
+  const long bits = std::strtol(cidr.c_str() + slash + 1, &end, 10);
+  if (*end) return false;
+  unsigned char a[16] = {}, b[16] = {};
+  int len = 0;
+  if (inet_pton(AF_INET, ip.c_str(), a) == 1 && inet_pton(AF_INET, net.c_str(), b) == 1) len = 4;
+  else if (inet_pton(AF_INET6, ip.c_str(), a) == 1 && inet_pton(AF_INET6, net.c_str(), b) == 1) len = 16;
+  if (!len || bits < 0 || bits > len * 8) return false;
+  for (long k = 0; k < bits; ++k)
+    if (((a[k / 8] ^ b[k / 8]) >> (7 - k % 8)) & 1) return false;
+  return true;
+}
+
 }  // namespace
+
+bool no_proxy_match(const std::string& no_proxy, const std::string& host_in, int port) {
+  const std::string host = lower(host_in);
+  size_t pos = 0;
+  while (pos <= no_proxy.size()) {
+    size_t c = no_proxy.find(',', pos);
+    if (c == std::string::npos) c = no_proxy.size();
+    std::string e = lower(no_proxy.substr(pos, c - pos));
+    pos = c + 1;
+    while (!e.empty() && std::isspace(static_cast<unsigned char>(e.front()))) e.erase(0, 1);
+    while (!e.empty() && std::isspace(static_cast<unsigned char>(e.back()))) e.pop_back();
+    if (e.empty()) continue;
+    if (e == "*") return true;
+    if (e.find('/') != std::string::npos) {  // a CIDR block
+      if (is_ip(host) && ip_in_cidr(host, e)) return true;
+      continue;
+    }
+    std::string h = e, p;  // host[:port], [v6]:port
+    if (!e.empty() && e[0] == '[') {
+      const size_t close = e.find(']');
+      if (close == std::string::npos) continue;
+      h = e.substr(1, close - 1);
+      if (close + 1 < e.size() && e[close + 1] == ':') p = e.substr(close + 2);
+    } else if (std::count(e.begin(), e.end(), ':') == 1) {
+      h = e.substr(0, e.find(':'));
+      p = e.substr(e.find(':') + 1);
+    }
+    if (h.empty()) continue;
+    if (!p.empty() && p != std::to_string(port)) continue;
+    if (is_ip(h)) {
+      unsigned char x[16] = {}, y[16] = {};
+      const int af = h.find(':') != std::string::npos ? AF_INET6 : AF_INET;
+      if (inet_pton(af, h.c_str(), x) == 1 && inet_pton(af, host.c_str(), y) == 1 &&
+          std::memcmp(x, y, af == AF_INET ? 4 : 16) == 0)
+        return true;
+      continue;
+    }
+    if (h.rfind("*.", 0) == 0) h.erase(0, 1);
+    const bool exact_too = h[0] != '.';  // "foo.com" matches foo.com and its subdomains, ".foo.com" only these
+    if (exact_too) h = "." + h;
+    if ((host.size() > h.size() && host.compare(host.size() - h.size(), h.size(), h) == 0) ||
+        (exact_too && host == h.substr(1)))
+      return true;
+  }
+  return false;
+}
+
+std::string env_proxy(bool tls, const std::string& host, int port) {
+  auto env = [](const char* a, const char* b) {
+    const char* v = std::getenv(a);
+    if (!v || !*v) v = std::getenv(b);
+    return std::string(v ? v : "");
+  };
+  const std::string proxy = tls ? env("HTTPS_PROXY", "https_proxy") : env("HTTP_PROXY", "http_proxy");
+  if (proxy.empty()) return "";
+  // never for the local host (Go's httpproxy), nor what NO_PROXY names
+  in6_addr a6{};
+  in_addr a4{};
+  if (lower(host) == "localhost" || (inet_pton(AF_INET, host.c_str(), &a4) == 1 && (ntohl(a4.s_addr) >> 24) == 127) ||
+      (inet_pton(AF_INET6, host.c_str(), &a6) == 1 && IN6_IS_ADDR_LOOPBACK(&a6)))
+    return "";
+  if (no_proxy_match(env("NO_PROXY", "no_proxy"), host, port)) return "";
+  return proxy.find("://") == std::string::npos ? "http://" + proxy : proxy;
+}
 
 Conn::~Conn() { close(); }
 
@@ -105,42 +261,51 @@ std::string Conn::open(const Config& cfg) {
   bool tls = false;
   int port = 0;
   if (!parse_url(cfg.server, &tls, &host_, &port, &authority_, &prefix_)) return "bad server URL " + cfg.server;
-  addrinfo hints{};
-  hints.ai_family = AF_UNSPEC;
-  hints.ai_socktype = SOCK_STREAM;
-  addrinfo* res = nullptr;
-  const int gai = getaddrinfo(host_.c_str(), std::to_string(port).c_str(), &hints, &res);
-  if (gai != 0) return std::string("resolve ") + host_ + ": " + gai_strerror(gai);
-  std::string err = "no address for " + host_;
   const int tmo_ms = static_cast<int>(cfg.timeout_s * 1000);
-  for (addrinfo* a = res; a; a = a->ai_next) {
-    const int fd = ::socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, a->ai_protocol);
-    if (fd < 0) continue;
-    int rc = ::connect(fd, a->ai_addr, a->ai_addrlen);
-    if (rc != 0 && errno == EINPROGRESS) {
-      pollfd p{fd, POLLOUT, 0};
-      rc = ::poll(&p, 1, tmo_ms) == 1 ? 0 : -1;
-      int so = 0;
-      socklen_t sl = sizeof(so);
-      if (rc == 0 && (getsockopt(fd, SOL_SOCKET, SO_ERROR, &so, &sl) != 0 || so != 0)) {
-        errno = so ? so : errno;
-        rc = -1;
-      } else if (rc != 0) {
-        errno = ETIMEDOUT;
+  absolute_form_ = false;
+  proxy_auth_.clear();
+  const std::string proxy = !cfg.proxy_url.empty() ? cfg.proxy_url : cfg.proxy_from_env ? env_proxy(tls, host_, port) : "";
+  if (proxy.empty()) {
+    std::string err = connect_tcp(host_, port, tmo_ms, &fd_);
+    if (!err.empty()) return err;
+  } else {
+    // an HTTP proxy (kubeconfig proxy-url, else $HTTPS_PROXY / $HTTP_PROXY as Go reads them):
+    // CONNECT for an https server, absolute-form requests for an http one
+    bool ptls = false;
+    int pport = 0;
+    std::string phost, pauth_url;
+    std::string purl = proxy;
+    const size_t at = purl.find('@'), scheme = purl.find("://");
+    if (at != std::string::npos && scheme != std::string::npos && at > scheme) {
+      pauth_url = pct_decode(purl.substr(scheme + 3, at - scheme - 3));
+      purl.erase(scheme + 3, at - scheme - 2);
+    }
+    if (purl.rfind("http://", 0) != 0) return "proxy " + purl + ": only http:// proxies are supported";
+    if (!parse_url(purl, &ptls, &phost, &pport)) return "bad proxy URL " + purl;
+    if (!pauth_url.empty()) proxy_auth_ = "Basic " + b64(pauth_url);
+    std::string err = connect_tcp(phost, pport, tmo_ms, &fd_);
+    if (!err.empty()) return "proxy " + err;
+    if (!tls) {
+      absolute_form_ = true;
+    } else {
+      const std::string target = (host_.find(':') != std::string::npos ? "[" + host_ + "]" : host_) + ":" +
+                                 std::to_string(port);
+      std::string req = "CONNECT " + target + " HTTP/1.1\r\nHost: " + target + "\r\n";
+      if (!proxy_auth_.empty()) req += "Proxy-Authorization: " + proxy_auth_ + "\r\n";
+      req += "\r\n";
+      if (!write_all(req)) return "proxy CONNECT: send failed";
+      std::string head;  // byte by byte: what follows the head is the server's TLS
+      while (head.size() < 8192 && head.find("\r\n\r\n") == std::string::npos) {
+        char ch;
+        const long n = read_some(&ch, 1, tmo_ms);
+        if (n <= 0) return "proxy CONNECT: no answer";
+        head.push_back(ch);
       }
+      const size_t sp = head.find(' ');
+      if (head.rfind("HTTP/1.", 0) != 0 || sp == std::string::npos || std::atoi(head.c_str() + sp + 1) != 200)
+        return "proxy CONNECT " + target + ": " + head.substr(0, head.find("\r\n"));
     }
-    if (rc == 0) {
-      ::fcntl(fd, F_SETFL, ::fcntl(fd, F_GETFL) & ~O_NONBLOCK);
-      const int one = 1;
-      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-      fd_ = fd;
-      break;
-    }
-    err = "connect " + host_ + ":" + std::to_string(port) + ": " + std::strerror(errno);
-    ::close(fd);
   }
-  freeaddrinfo(res);
-  if (fd_ < 0) return err;
   // a blocking read never outlives the request deadline (TLS records can arrive in pieces)
   timeval tv{static_cast<time_t>(cfg.timeout_s), static_cast<suseconds_t>((cfg.timeout_s - static_cast<long>(cfg.timeout_s)) * 1e6)};
   setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
@@ -341,8 +506,9 @@ std::string start(Conn* c, const Config& cfg, const std::string& method, const s
                   int timeout_ms, int wake_fd) {
   std::string err = c->open(cfg);
   if (!err.empty()) return err;
-  std::string req = method + " " + c->prefix() + path + " HTTP/1.1\r\nHost: " + c->authority() +
-                    "\r\nConnection: close\r\n";
+  const std::string target = (c->absolute_form() ? "http://" + c->authority() : "") + c->prefix() + path;
+  std::string req = method + " " + target + " HTTP/1.1\r\nHost: " + c->authority() + "\r\nConnection: close\r\n";
+  if (c->absolute_form() && !c->proxy_auth().empty()) req += "Proxy-Authorization: " + c->proxy_auth() + "\r\n";
   for (const auto& [k, v] : headers) req += k + ": " + v + "\r\n";
   if (!body.empty() || method == "PATCH" || method == "PUT" || method == "POST")
     req += "Content-Length: " + std::to_string(body.size()) + "\r\n";

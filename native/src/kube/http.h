@@ -21,6 +21,10 @@ struct Config {
   std::string cert_file, key_file, cert_pem, key_pem;
   bool insecure = false;
   std::string tls_server_name;  // kubeconfig tls-server-name: SNI and the name the certificate must carry
+  // an HTTP proxy (kubeconfig proxy-url); else, with proxy_from_env, $HTTPS_PROXY / $HTTP_PROXY
+  // and $NO_PROXY as Go's net/http reads them (never for localhost / loopback)
+  std::string proxy_url;
+  bool proxy_from_env = true;
   double timeout_s = 15.0;
 };
 
@@ -47,13 +51,22 @@ class Conn {
   const std::string& host() const { return host_; }
   const std::string& authority() const { return authority_; }  // host[:port] as the server URL writes it
   const std::string& prefix() const { return prefix_; }        // the server URL's path, below which requests go
+  bool absolute_form() const { return absolute_form_; }        // through an HTTP proxy to an http:// server
+  const std::string& proxy_auth() const { return proxy_auth_; }
 
  private:
   int fd_ = -1;
   SSL_CTX* ctx_ = nullptr;
   SSL* ssl_ = nullptr;
-  std::string host_, authority_, prefix_;
+  std::string host_, authority_, prefix_, proxy_auth_;
+  bool absolute_form_ = false;
 };
+
+// $NO_PROXY matching as Go's httpproxy does it: "*", IPs, CIDR blocks, host[:port],
+// "foo.com" (itself and its subdomains), ".foo.com" / "*.foo.com" (subdomains only)
+bool no_proxy_match(const std::string& no_proxy, const std::string& host, int port);
+// the proxy URL the environment gives for a request to host:port ("" = direct)
+std::string env_proxy(bool tls, const std::string& host, int port);
 
 // A response body read incrementally (Content-Length, chunked, or to EOF).
 class Body {

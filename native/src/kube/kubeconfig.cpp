@@ -146,6 +146,7 @@ std::optional<KubeConfig> load_kubeconfig_files(const std::vector<std::string>& 
   kc.http.ca_file = cluster->str("certificate-authority");
   if (!data(cluster, "certificate-authority-data", &kc.http.ca_pem)) return std::nullopt;
   kc.http.tls_server_name = cluster->str("tls-server-name");
+  kc.http.proxy_url = cluster->str("proxy-url");
   if (const json::Value* ins = cluster->get("insecure-skip-tls-verify"))
     kc.http.insecure = ins->kind == json::Value::Bool ? ins->b : ins->s == "true";
   if (user) {

@@ -21,6 +21,9 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#ifdef MI355X_TEST_HTTP
+#include "../src/kube/http.h"
+#endif
 #include "../src/kube/labels.h"
 #include "../src/rpc/hpack.h"
 #include "flags.h"
@@ -928,6 +931,39 @@ static void test_driver_version_value() {
     CHECK(driver_version_value(same) == same);
 }
 
+#ifdef MI355X_TEST_HTTP
+// $NO_PROXY / $HTTPS_PROXY as Go's golang.org/x/net/http/httpproxy reads them
+static void test_proxy_environment() {
+  using http::no_proxy_match;
+  CHECK(no_proxy_match("*", "anything.example", 443));
+  CHECK(no_proxy_match("foo.com", "foo.com", 443) && no_proxy_match("foo.com", "bar.foo.com", 443));
+  CHECK(!no_proxy_match("foo.com", "barfoo.com", 443));
+  CHECK(!no_proxy_match(".foo.com", "foo.com", 443) && no_proxy_match(".foo.com", "bar.foo.com", 443));
+  CHECK(!no_proxy_match("*.foo.com", "foo.com", 443) && no_proxy_match("*.foo.com", "a.b.foo.com", 443));
+  CHECK(no_proxy_match("10.0.0.0/8", "10.1.2.3", 443) && !no_proxy_match("10.0.0.0/8", "11.0.0.1", 443));
+  CHECK(!no_proxy_match("10.0.0.0/8", "ten.example", 443));
+  CHECK(no_proxy_match("fd00::/8", "fd12::1", 443) && !no_proxy_match("fd00::/8", "fe80::1", 443));
+  CHECK(no_proxy_match("192.168.1.1", "192.168.1.1", 6443) && !no_proxy_match("192.168.1.1", "192.168.1.2", 6443));
+  CHECK(no_proxy_match("2001:db8::1", "2001:db8:0::1", 443));
+  CHECK(no_proxy_match("[2001:db8::2]:443", "2001:db8::2", 443) && !no_proxy_match("[2001:db8::2]:443", "2001:db8::2", 80));
+  CHECK(no_proxy_match("foo.com:8443", "foo.com", 8443) && !no_proxy_match("foo.com:8443", "foo.com", 443));
+  CHECK(no_proxy_match(" bar.com , FOO.com ", "api.foo.COM", 443));
+  CHECK(!no_proxy_match("", "foo.com", 443) && !no_proxy_match(",,", "foo.com", 443));
+  ::setenv("HTTPS_PROXY", "proxy.example:3128", 1);
+  ::setenv("NO_PROXY", ".svc,10.96.0.0/12", 1);
+  ::setenv("HTTP_PROXY", "", 1);
+  ::setenv("http_proxy", "http://lower.example:8080", 1);
+  CHECK(http::env_proxy(true, "api.example", 6443) == "http://proxy.example:3128");
+  CHECK(http::env_proxy(true, "kubernetes.default.svc", 443).empty());
+  CHECK(http::env_proxy(true, "10.96.0.1", 443).empty() && http::env_proxy(true, "10.112.0.1", 443) != "");
+  CHECK(http::env_proxy(true, "localhost", 443).empty() && http::env_proxy(true, "127.0.0.1", 443).empty() &&
+        http::env_proxy(true, "::1", 443).empty());
+  CHECK(http::env_proxy(false, "api.example", 80) == "http://lower.example:8080");  // an empty HTTP_PROXY falls back
+  for (const char* v : {"HTTPS_PROXY", "NO_PROXY", "HTTP_PROXY", "http_proxy"}) ::unsetenv(v);
+  CHECK(http::env_proxy(true, "api.example", 6443).empty());
+}
+#endif
+
 static void test_metrics_registry() {
   metrics::Registry r;
   r.inc("mi355x_x_total", {{"b", "2"}, {"a", "1"}}, 1.0, "things");
@@ -1012,6 +1048,9 @@ int main(int argc, char** argv) {
   test_metrics_registry();
   test_driver_version_value();
   test_cdi_json_strings();
+#ifdef MI355X_TEST_HTTP
+  test_proxy_environment();
+#endif
   {
     char dir[] = "/tmp/mi355x-test-core-XXXXXX";
     if (::mkdtemp(dir)) {

@@ -14,7 +14,9 @@ client-certificate auth, CA from a file or inline data, block or flow YAML.
 import base64
 import os
 import signal
+import socket
 import subprocess
+import threading
 import time
 
 import pytest
@@ -36,7 +38,8 @@ def _built():
 
 def _env(**kw):
     env = {k: v for k, v in os.environ.items()
-           if k not in ("KUBERNETES_SERVICE_HOST", "KUBERNETES_SERVICE_PORT", "KUBECONFIG", "DS_NODE_NAME")}
+           if k not in ("KUBERNETES_SERVICE_HOST", "KUBERNETES_SERVICE_PORT", "KUBECONFIG", "DS_NODE_NAME")
+           and k.lower() not in ("https_proxy", "http_proxy", "no_proxy")}
     env.update(kw)
     return env
 
@@ -455,6 +458,129 @@ def test_server_url_path_prefix_and_host_header(tmp_path, trailing):
         rc, err = _term(proc)
         assert srv.watch_starts >= 1, err
     finally:
+        srv.stop()
+
+
+class _Proxy:
+    """An HTTP proxy that sends every connection to 127.0.0.1:<upstream>: CONNECT
+    tunnels (https servers) and absolute-form requests rewritten to origin form."""
+
+    def __init__(self, upstream: int):
+        self.upstream = upstream
+        self.lines, self.auth = [], []
+        self.sock = socket.socket()
+        self.sock.bind(("127.0.0.1", 0))
+        self.sock.listen(16)
+        self.port = self.sock.getsockname()[1]
+        threading.Thread(target=self._accept, daemon=True).start()
+
+    def _accept(self):
+        while True:
+            try:
+                c, _ = self.sock.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._serve, args=(c,), daemon=True).start()
+
+    @staticmethod
+    def _pipe(a, b):
+        try:
+            while (d := a.recv(65536)):
+                b.sendall(d)
+        except OSError:
+            pass
+        finally:
+            for x in (a, b):
+                try:
+                    x.shutdown(socket.SHUT_RDWR)
+                except OSError:
+                    pass
+
+    def _serve(self, c):
+        head = b""
+        while b"\r\n\r\n" not in head:
+            d = c.recv(1)
+            if not d:
+                return c.close()
+            head += d
+        lines = head.decode().split("\r\n")
+        self.lines.append(lines[0])
+        self.auth += [ln.split(":", 1)[1].strip() for ln in lines if ln.lower().startswith("proxy-authorization:")]
+        up = socket.create_connection(("127.0.0.1", self.upstream))
+        method, target, ver = lines[0].split(" ")
+        if method == "CONNECT":
+            c.sendall(b"HTTP/1.1 200 Connection established\r\n\r\n")
+        else:  # http://host:port/path -> /path, the other header lines as they came
+            path = "/" + target.split("://", 1)[1].split("/", 1)[1]
+            up.sendall((" ".join((method, path, ver)) + "\r\n" + "\r\n".join(
+                ln for ln in lines[1:] if not ln.lower().startswith("proxy-authorization:"))).encode())
+        threading.Thread(target=self._pipe, args=(up, c), daemon=True).start()
+        self._pipe(c, up)
+
+    def close(self):
+        self.sock.close()
+
+
+def test_apiserver_through_an_http_proxy(tmp_path):
+    """$HTTPS_PROXY (with credentials) tunnels an https apiserver through CONNECT by
+    name, $NO_PROXY bypasses it, $HTTP_PROXY carries an http one in absolute form and
+    a kubeconfig proxy-url applies without any environment, as client-go does."""
+    d = tmp_path / "pki"
+    d.mkdir()
+    _tls_material(d)
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="t0", tls=(str(d / "srv.crt"), str(d / "srv.key"))).start()
+    proxy = _Proxy(srv.port)
+    try:
+        srv.add_node("worker")
+        kc = tmp_path / "kc"
+
+        def write(server, extra=""):
+            kc.write_text(f"clusters:\n- name: c\n  cluster:\n    server: {server}\n    certificate-authority: pki/ca.crt\n"
+                          f"{extra}contexts: [{{name: x, context: {{cluster: c, user: u}}}}]\ncurrent-context: x\n"
+                          "users: [{name: u, user: {token: t0}}]\n")
+
+        # the certificate names kubernetes.default.svc, which only the proxy can reach
+        write(f"https://kubernetes.default.svc:{srv.port}")
+        p = _label_once(kc, fi, env=_env(HTTPS_PROXY=f"http://robot:p%40ss@127.0.0.1:{proxy.port}"))
+        assert p.returncode == 0, p.stderr
+        assert srv.labels("worker")["amd.com/gpu.mode"] == "container"
+        assert proxy.lines and set(proxy.lines) == {f"CONNECT kubernetes.default.svc:{srv.port} HTTP/1.1"}
+        assert set(proxy.auth) == {"Basic " + base64.b64encode(b"robot:p@ss").decode()}
+        # NO_PROXY: straight to kubernetes.default.svc, which does not resolve here
+        n = len(proxy.lines)
+        srv.set_labels("worker", {})
+        proc = subprocess.Popen([LBL, "-node_name", "worker", "-once", "-mode", "-sysfs_root", str(fi.sysfs),
+                                 "-kubeconfig", str(kc)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                                env=_env(HTTPS_PROXY=f"127.0.0.1:{proxy.port}", NO_PROXY="10.0.0.0/8, .svc"))
+        time.sleep(1.0)
+        rc, err = _term(proc)
+        assert "resolve kubernetes.default.svc" in err and len(proxy.lines) == n
+        assert "amd.com/gpu.mode" not in srv.labels("worker")
+        # proxy-url in the kubeconfig, no environment
+        write(f"https://kubernetes.default.svc:{srv.port}", f"    proxy-url: http://127.0.0.1:{proxy.port}\n")
+        p = _label_once(kc, fi)
+        assert p.returncode == 0, p.stderr
+        assert srv.labels("worker")["amd.com/gpu.mode"] == "container" and len(proxy.lines) > n
+    finally:
+        proxy.close()
+        srv.stop()
+    # an http apiserver through $HTTP_PROXY: absolute-form requests
+    srv = FakeApiServer(token="t0").start()
+    proxy = _Proxy(srv.port)
+    try:
+        srv.add_node("worker")
+        kc.write_text(f"clusters: [{{name: c, cluster: {{server: 'http://apiserver.test:{srv.port}'}}}}]\n"
+                      "contexts: [{name: x, context: {cluster: c, user: u}}]\ncurrent-context: x\n"
+                      "users: [{name: u, user: {token: t0}}]\n")
+        p = _label_once(kc, fi, env=_env(HTTP_PROXY=f"http://127.0.0.1:{proxy.port}"))
+        assert p.returncode == 0, p.stderr
+        assert srv.labels("worker")["amd.com/gpu.mode"] == "container"
+        assert proxy.lines and all(ln.split(" ")[1].startswith(f"http://apiserver.test:{srv.port}/api/v1/nodes")
+                                   for ln in proxy.lines), proxy.lines
+        assert set(srv.host_headers) == {f"apiserver.test:{srv.port}"}
+    finally:
+        proxy.close()
         srv.stop()
 
 
