@@ -2,6 +2,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <unordered_map>
 
 namespace mi355x::json {
 
@@ -112,11 +113,13 @@ struct Parser {
           unsigned cp = 0;
           if (!hex4(&cp)) return false;
           if (cp >= 0xD800 && cp < 0xDC00 && i + 1 < t.size() && t[i] == '\\' && t[i + 1] == 'u') {
+            const size_t next = i;
             i += 2;
             unsigned lo = 0;
-            if (!hex4(&lo)) return false;
-            if (lo >= 0xDC00 && lo < 0xE000) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            if (hex4(&lo) && lo >= 0xDC00 && lo < 0xE000) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            else i = next;  // not a low surrogate: that escape is read on its own
           }
+          if (cp >= 0xD800 && cp < 0xE000) cp = 0xFFFD;  // a lone surrogate, as Go's encoding/json reads it
           utf8(out, cp);
           break;
         }
@@ -187,6 +190,19 @@ struct Parser {
             break;
           }
           return fail("expected ',' or '}'");
+        }
+        if (v->obj.size() > 1) {
+          // a repeated key: the last value wins, at the first one's place (Go's encoding/json
+          // and Python's json keep the last)
+          std::unordered_map<std::string, size_t> at;
+          std::vector<std::pair<std::string, Value>> kept;
+          kept.reserve(v->obj.size());
+          for (auto& kv : v->obj) {
+            auto [it, fresh] = at.emplace(kv.first, kept.size());
+            if (fresh) kept.push_back(std::move(kv));
+            else kept[it->second].second = std::move(kv.second);
+          }
+          v->obj = std::move(kept);
         }
       }
     } else if (c == '[') {

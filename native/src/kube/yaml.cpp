@@ -597,6 +597,21 @@ class Parser {
         }
         if (cp > 0x10FFFF) return false;
         *p += n;
+        if (cp >= 0xD800 && cp < 0xDC00 && *p + 6 < s.size() && s[*p + 1] == '\\' && s[*p + 2] == 'u') {
+          uint32_t lo = 0;  // a UTF-16 pair written as two escapes
+          for (size_t k = 3; k <= 6; ++k) {
+            const char h = s[*p + k];
+            const int d = h >= '0' && h <= '9' ? h - '0' : h >= 'a' && h <= 'f' ? h - 'a' + 10
+                          : h >= 'A' && h <= 'F' ? h - 'A' + 10 : -1;
+            lo = d < 0 ? 0 : lo * 16 + static_cast<uint32_t>(d);
+            if (d < 0) break;
+          }
+          if (lo >= 0xDC00 && lo < 0xE000) {
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            *p += 6;
+          }
+        }
+        if (cp >= 0xD800 && cp < 0xE000) cp = 0xFFFD;  // a lone surrogate: no valid UTF-8 for it
         utf8(out, cp);
         return true;
       }

@@ -128,6 +128,25 @@ def test_unsupported_documents_are_refused(text):
     assert out is None and err, (text, out)
 
 
+@pytest.mark.parametrize("text, want", [
+    # JSON: a repeated key keeps the last value (Python's json and Go's encoding/json agree)
+    ('{"a": 1, "b": 2, "a": 3}', {"a": "3", "b": "2"}),
+    # UTF-16 escapes: a pair is one code point, a lone surrogate U+FFFD (Go's encoding/json),
+    # and an escape after a lone high surrogate is read on its own
+    ('{"a": "\\ud83d\\ude00"}', {"a": "\U0001F600"}), ('{"a": "\\ud800"}', {"a": "\ufffd"}),
+    ('{"a": "\\ud800\\u0041"}', {"a": "\ufffdA"}), ('{"a": "x\\udc00"}', {"a": "x\ufffd"}),
+    # the same in YAML double-quoted scalars
+    ('a: "\\ud83d\\ude00"\n', {"a": "\U0001F600"}), ('a: "\\ud800 x"\n', {"a": "\ufffd x"}),
+])
+def test_repeated_keys_and_surrogate_escapes(text, want):
+    """Output is always valid UTF-8 and a repeated key reads as the readers the labeller
+    replaces read it."""
+    out, err = core().yaml_to_json(text)
+    assert out is not None, err
+    got = json.loads(out)
+    assert {k: str(v) if isinstance(v, int) else v for k, v in got.items()} == want
+
+
 def test_anchor_redefinition_rebinds():
     """A later anchor of the same name rebinds it for the aliases after it (YAML 1.2 3.2.2.2,
     as go-yaml reads it); PyYAML refuses the document instead."""
