@@ -2,9 +2,28 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string_view>
 #include <unordered_map>
+#include <unordered_set>
 
 namespace mi355x::json {
+namespace {
+
+// true when a key occurs twice (small objects, the common case, without allocating)
+bool repeated_key(const std::vector<std::pair<std::string, Value>>& obj) {
+  if (obj.size() <= 16) {
+    for (size_t a = 0; a < obj.size(); ++a)
+      for (size_t b = a + 1; b < obj.size(); ++b)
+        if (obj[a].first == obj[b].first) return true;
+    return false;
+  }
+  std::unordered_set<std::string_view> seen;
+  for (const auto& kv : obj)
+    if (!seen.insert(kv.first).second) return true;
+  return false;
+}
+
+}  // namespace
 
 const Value* Value::get(const std::string& key) const {
   if (kind != Object) return nullptr;
@@ -191,7 +210,7 @@ struct Parser {
           }
           return fail("expected ',' or '}'");
         }
-        if (v->obj.size() > 1) {
+        if (v->obj.size() > 1 && repeated_key(v->obj)) {
           // a repeated key: the last value wins, at the first one's place (Go's encoding/json
           // and Python's json keep the last)
           std::unordered_map<std::string, size_t> at;
