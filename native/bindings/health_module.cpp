@@ -63,6 +63,7 @@ class PyHealthEngine {
     s("xgmi_file", &c.xgmi_file);
     s("probe_exe", &c.prober.exe);
     d("probe_timeout_s", &c.prober.timeout_s);
+    d("busy_deadline_s", &c.prober.busy_deadline_s);
     i("probe_iters", &c.prober.iters);
     i("probe_max_parallel", &c.prober.max_parallel);
     b("persistent", &c.prober.persistent);
@@ -96,9 +97,13 @@ class PyHealthEngine {
     d["chip_sweeps"] = eng_->chip_sweeps();
     d["perf_checks"] = eng_->perf_checks();
     if (auto* p = eng_->prober()) {
-      d["server_starts"] = p->server_starts;
-      d["server_restarts"] = p->server_restarts;
-      d["fallbacks"] = p->fallbacks;
+      d["server_starts"] = p->server_starts.load();
+      d["server_restarts"] = p->server_restarts.load();
+      d["fallbacks"] = p->fallbacks.load();
+      d["prober_sweeps"] = p->sweeps.load();
+      d["checks"] = p->checks.load();
+      d["check_fresh"] = p->check_fresh.load();
+      d["check_inconclusive"] = p->check_inconclusive.load();
       d["server_running"] = p->server_running();
     }
     return d;
@@ -125,6 +130,25 @@ class PyHealthEngine {
     else eng_->exporter_source = [h] { return *h; };
   }
   std::map<std::string, int> ordinals() { return eng_->ordinals(); }
+  // PreStartContainer's check (Engine::probe_now): device id -> outcome dict
+  py::dict check(const std::vector<std::string>& ids, double budget_s) {
+    std::map<std::string, health::ProbeOutcome> res;
+    {
+      py::gil_scoped_release nogil;
+      res = eng_->probe_now(ids, budget_s);
+    }
+    py::dict out;
+    for (const auto& [id, o] : res) {
+      py::dict d;
+      d["ok"] = o.ok;
+      d["pending"] = o.pending;
+      d["interrupted"] = o.interrupted;
+      d["reason"] = o.reason;
+      d["latency_ms"] = o.latency_ms;
+      out[py::str(id)] = d;
+    }
+    return out;
+  }
   void close() {
     py::gil_scoped_release nogil;
     eng_->close();
@@ -144,6 +168,8 @@ void bind_health(py::module_& m) {
       .def("snapshot", &PyHealthEngine::snapshot, "device id -> (healthy, reasons)")
       .def("stats", &PyHealthEngine::stats)
       .def("ordinals", &PyHealthEngine::ordinals)
+      .def("check", &PyHealthEngine::check, py::arg("ids"), py::arg("budget_s") = 5.0,
+           "PreStartContainer's check of these devices now (beside any sweep)")
       .def("set_activity", &PyHealthEngine::set_activity, py::arg("activity"),
            "bdf -> GFX activity % used instead of amd-smi (None = amd-smi)")
       .def("set_exporter", &PyHealthEngine::set_exporter, py::arg("health"),

@@ -35,6 +35,7 @@
 // thread; snapshot() may be called from any thread.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -60,6 +61,7 @@ struct ProbeOutcome {
   bool ok = false;
   bool pending = false;    // the dispatch is still queued (kept slot) or missed its deadline on a busy GPU
   bool interrupted = false;  // shutdown cut the probe short: no verdict either way
+  bool queue_lost = false;   // a dispatch timed out on a queue the server cannot free (no kept queues)
   std::string reason;
   double latency_ms = 0;
   int kfd_node_id = -1;    // identity of the agent that answered (-1 / "" = not reported)
@@ -74,6 +76,10 @@ struct ProberConfig {
   std::vector<std::string> argv_prefix;  // e.g. {"python3"} for a scripted stand-in
   std::string exe;                       // mi355x-liveness-probe
   double timeout_s = 10.0;
+  // a probe on a GPU other processes have queues on: that long, not timeout_s.
+  // A dispatch queued behind a tenant's kernel is inconclusive whenever it
+  // ends, and with kept queues its verdict is collected by the next request.
+  double busy_deadline_s = 0.05;
   int iters = 4;
   int max_parallel = 8;
   bool persistent = true;                // one --serve child, else a process per device per sweep
@@ -85,6 +91,16 @@ struct ProberConfig {
 };
 
 // The probe processes (LivenessProber in health/liveness.py).
+//
+// Two kinds of callers share one kept-queue probe server:
+//   the health sweep  probe() / probe_ordinal() / set_visible() / close(): one
+//                     caller at a time (Engine::sweep); it alone starts,
+//                     restarts and stops the server and runs the fallback to
+//                     per-device processes.
+//   PreStartContainer check(): any thread, at the same time as a sweep. Every
+//                     request is tagged and the server answers tagged requests
+//                     concurrently, so a check waits for its own GPUs only,
+//                     never behind a sweep's wait on another GPU.
 class LivenessProber {
  public:
   explicit LivenessProber(ProberConfig cfg);
@@ -93,11 +109,20 @@ class LivenessProber {
   LivenessProber& operator=(const LivenessProber&) = delete;
 
   // host ROCr ordinal -> outcome. `busy`: ordinals whose GPU runs other
-  // processes' queues (a pending dispatch there is not re-probed).
+  // processes' queues (a pending dispatch there is not re-probed, and with
+  // kept queues they get busy_deadline_s).
   std::map<int, ProbeOutcome> probe(const std::vector<int>& ordinals, const std::set<int>& busy = {},
                                     const std::string& kind = "probe");
   // one device in a fresh process (ROCR_VISIBLE_DEVICES=<ordinal>)
   ProbeOutcome probe_ordinal(int ordinal, const std::string& kind = "probe");
+  // A PreStartContainer check within `budget_s`: the running server first
+  // (busy GPUs: busy_deadline_s; idle ones: 40% of the budget), then a
+  // fresh process for each idle GPU the server failed or could not answer
+  // for, while at least a second of the budget is left. Busy GPUs and
+  // whatever the budget leaves unsettled come back pending. Never starts,
+  // restarts or stops the server; a failure a fresh process does not confirm
+  // asks the next sweep to restart it. Leaves the sweep's backoff and counters alone.
+  std::map<int, ProbeOutcome> check(const std::vector<int>& ordinals, const std::set<int>& busy, double budget_s);
   // restrict the server to these host ordinals (nullopt = all); a change restarts it
   void set_visible(std::optional<std::vector<int>> ordinals);
   void close();
@@ -107,19 +132,33 @@ class LivenessProber {
   // a readable fd ends every wait at once (shutdown)
   void set_abort_fd(int fd) { abort_fd_ = fd; }
 
-  int server_starts = 0, server_restarts = 0, fallbacks = 0, sweeps = 0;
+  // sweep path counters (check() keeps its own)
+  std::atomic<int> server_starts{0}, server_restarts{0}, fallbacks{0}, sweeps{0};
+  std::atomic<int> checks{0}, check_fresh{0}, check_inconclusive{0};
   const ProberConfig& config() const { return cfg_; }
+  enum class Got { kLine, kTimeout, kEof, kAbort };
 
  private:
   struct Server;
-  std::map<int, ProbeOutcome> probe_server(const std::vector<int>& uniq, const std::string& kind, std::string* err);
-  std::map<int, ProbeOutcome> spawn_all(const std::vector<int>& ords, const std::string& kind);
+  std::shared_ptr<Server> ensure_server(const std::vector<int>& uniq, std::string* err);
+  Got transact(const std::shared_ptr<Server>& s, const std::string& body, double deadline, std::string* reply);
+  // one tagged request to `s`; host ordinal -> outcome, or *err
+  std::map<int, ProbeOutcome> request(const std::shared_ptr<Server>& s, const std::vector<int>& uniq,
+                                      const std::string& kind, const std::map<int, double>& deadlines,
+                                      double wait_until, std::string* err);
+  std::map<int, ProbeOutcome> probe_server(const std::vector<int>& uniq, const std::set<int>& busy,
+                                           const std::string& kind, std::string* err);
+  std::map<int, ProbeOutcome> spawn_all(const std::vector<int>& ords, const std::string& kind, double timeout_s);
+  double inner_timeout() const;
   ProberConfig cfg_;
-  std::unique_ptr<Server> server_;
+  mutable std::mutex mu_;            // server_, visible_, backoff_, issued_, restart_wanted_
+  std::shared_ptr<Server> server_;
   int backoff_ = 0;
-  std::map<int, uint32_t> pending_nonce_;
-  std::optional<std::vector<int>> visible_, server_visible_;
-  std::set<std::string> own_kfd_;
+  bool restart_wanted_ = false;
+  // ordinal -> nonces of probe dispatches that may still answer late (kept slot)
+  std::map<int, std::vector<uint32_t>> issued_;
+  std::optional<std::vector<int>> visible_;
+  std::atomic<uint64_t> next_id_{1};
   int abort_fd_ = -1;
 };
 
@@ -170,18 +209,21 @@ class Engine {
 
   // One sweep; true when any device's health changed. Blocking.
   bool sweep();
-  // A liveness probe of `ids` now, outside the sweep cadence (a container about
-  // to start on them: PreStartContainer). Waits for a sweep's liveness pass; changes no
-  // verdict. id -> outcome; devices without a ROCr ordinal, and devices on GPUs
-  // the probe server steps off (crowded with tenant processes), are absent.
-  std::map<std::string, ProbeOutcome> probe_now(const std::vector<std::string>& ids);
+  // A liveness check of `ids` now, outside the sweep cadence (a container about
+  // to start on them: PreStartContainer), within `budget_s`
+  // (LivenessProber::check). Runs beside a sweep, never waiting for it; changes
+  // no verdict. id -> outcome; devices without a ROCr ordinal, and devices on
+  // GPUs the probe server steps off (crowded with tenant processes), are
+  // absent; a reply from another agent than the device's is left to the sweep
+  // (pending).
+  std::map<std::string, ProbeOutcome> probe_now(const std::vector<std::string>& ids, double budget_s = 5.0);
   std::map<std::string, Verdict> snapshot() const;
   uint64_t version() const;
   void set_abort_fd(int fd);
   void close();
 
   // device id -> host ROCr ordinal (positional over accessible kfd GPU nodes)
-  const std::map<std::string, int>& ordinals();
+  std::map<std::string, int> ordinals();
   // sources a test (or another collector) can replace
   std::function<std::map<std::string, int>()> activity_source;       // bdf -> GFX activity %, -1 unknown
   std::function<std::map<std::string, bool>()> exporter_source;      // bdf -> healthy
@@ -274,7 +316,8 @@ class Engine {
   std::string xgmi_error_;
 
   mutable std::mutex mu_;  // snapshot_ / version_ / degraded_ / fabric_version_ / links_down_
-  std::mutex op_mu_;       // the liveness pass of sweep() and probe_now(): one user of the prober at a time
+  std::mutex op_mu_;       // the liveness pass of sweep(): one sweep at a time on the prober's sweep path
+  mutable std::mutex state_mu_;  // ordinals_ and crowded_, read by probe_now() beside a sweep
   std::set<std::pair<std::string, std::string>> degraded_;
   std::map<std::string, int> links_down_;
   uint64_t fabric_version_ = 0;

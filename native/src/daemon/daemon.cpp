@@ -77,54 +77,73 @@ void Daemon::shutdown() {
     }
   }
   workers_.join_all();  // every wait ends at the stop pipe
-  gate_threads_.join_all();
+  gate_pool_.join_all();
+  std::shared_ptr<health::Engine> gate;
   {
     std::lock_guard<std::mutex> lk(gate_mu_);
-    gate_engine_.reset();
+    gate.swap(gate_engine_);
   }
+  gate.reset();  // outside gate_mu_: the last reference closes the probe server
   if (health_) health_->close();
   reg_.stop_all();
 }
 
-void GateThreads::run(std::function<void()> fn) {
+bool GatePool::submit(std::function<void()> fn) {
   std::lock_guard<std::mutex> lk(mu_);
-  for (auto it = ts_.begin(); it != ts_.end();) {
-    if (it->second->load()) {
-      it->first.join();
-      it = ts_.erase(it);
-    } else {
-      ++it;
-    }
-  }
-  auto done = std::make_shared<std::atomic<bool>>(false);
-  ts_.emplace_back(std::thread([fn = std::move(fn), done] {
-                     fn();
-                     done->store(true);
-                   }),
-                   done);
+  if (stop_ || q_.size() >= max_queued_) return false;
+  q_.push_back(std::move(fn));
+  if (ts_.size() < workers_) ts_.emplace_back([this] { loop(); });  // started on demand
+  cv_.notify_one();
+  return true;
 }
 
-void GateThreads::join_all() {
-  std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> ts;
+void GatePool::loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  while (true) {
+    cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+    if (q_.empty()) return;  // stopping, nothing left
+    auto fn = std::move(q_.front());
+    q_.pop_front();
+    lk.unlock();
+    fn();
+    lk.lock();
+  }
+}
+
+void GatePool::join_all() {
+  std::vector<std::thread> ts;
   {
     std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
     ts.swap(ts_);
   }
+  cv_.notify_all();
   for (auto& t : ts)
-    if (t.first.joinable()) t.first.join();
+    if (t.joinable()) t.join();
 }
 
-rpc::Reply prestart_verdict(health::Engine* engine, const std::vector<std::string>& ids) {
+size_t GatePool::threads() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return ts_.size();
+}
+
+rpc::Reply prestart_verdict(health::Engine* engine, const std::vector<std::string>& ids, double budget_s,
+                            std::chrono::steady_clock::time_point arrival) {
   if (!engine) return rpc::Reply{};
   const auto t0 = std::chrono::steady_clock::now();
-  std::string bad;
-  for (const auto& [id, o] : engine->probe_now(ids))
+  const double queued = std::chrono::duration<double>(t0 - arrival).count();
+  std::string bad, unsure;
+  for (const auto& [id, o] : engine->probe_now(ids, std::max(0.0, budget_s - queued))) {
     if (!o.ok && !o.pending && !o.interrupted) bad += (bad.empty() ? "" : "; ") + id + ": " + o.reason;
-  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    else if (o.pending) unsure += (unsure.empty() ? "" : "; ") + id + ": " + o.reason;
+  }
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - arrival).count();
   auto& m = metrics::global();
-  m.inc("mi355x_dp_prestart_checks_total", {{"result", bad.empty() ? "ok" : "failed"}}, 1.0,
-        "PreStartContainer liveness checks (-prestart_liveness)");
-  m.observe_ms("mi355x_dp_prestart_check_seconds", ms, {}, "PreStartContainer liveness check latency");
+  const char* result = !bad.empty() ? "failed" : !unsure.empty() ? "inconclusive" : "ok";
+  m.inc("mi355x_dp_prestart_checks_total", {{"result", result}}, 1.0,
+        "PreStartContainer liveness checks (-prestart_liveness): ok, failed, inconclusive (busy GPU or budget spent)");
+  m.observe_ms("mi355x_dp_prestart_check_seconds", ms, {}, "PreStartContainer liveness check latency (queue wait included)");
+  if (!unsure.empty()) MI_VLOG(2, "PreStartContainer: inconclusive, the start goes ahead (%s)", unsure.c_str());
   if (bad.empty()) return rpc::Reply{};
   MI_LOG(kError, "PreStartContainer: MFMA liveness check failed (%s)", bad.c_str());
   return rpc::Reply{rpc::kFailedPrecondition, "MFMA liveness check failed before the container start: " + bad, ""};
@@ -145,9 +164,21 @@ std::string Daemon::write_cdi(const std::set<std::string>& stale) {
 }
 
 void Daemon::rebuild_health() {
+  std::shared_ptr<health::Engine> old;
+  {
+    std::lock_guard<std::mutex> lk(gate_mu_);
+    old.swap(gate_engine_);  // no new check starts on the old engine
+  }
   health_->rebuild(driver_, container_devices_, topo_, reg_.all());
-  std::lock_guard<std::mutex> lk(gate_mu_);
-  gate_engine_ = health_->engine();
+  {
+    std::lock_guard<std::mutex> lk(gate_mu_);
+    gate_engine_ = health_->engine();
+  }
+  // The old engine's probe server is stopped here (its teardown waits for the
+  // GPU process), outside gate_mu_, so the RPC thread's PreStartContainer
+  // hand-off never waits for it. A check or sweep still holding the engine
+  // keeps it until it lets go.
+  if (old && old.use_count() == 1) old->close();
 }
 
 int Daemon::init() {
@@ -174,16 +205,24 @@ int Daemon::init() {
     MI_LOG(kWarning, "-prestart_liveness with -liveness_mode=spawn: every container start waits for a fresh probe "
                      "process (GPU runtime start-up) and then for its kfd teardown; -liveness_mode=persistent "
                      "answers from the kept queue in about a millisecond");
-  if (f_.prestart_liveness)  // runs on the RPC thread: the probe goes to a gate thread
+  if (f_.prestart_liveness)  // runs on the RPC thread: the check goes to a gate worker
     serve_.prestart = [this](std::vector<std::string> ids, std::function<void(rpc::Reply)> done) {
+      const auto arrival = std::chrono::steady_clock::now();
       std::shared_ptr<health::Engine> engine;
       {
         std::lock_guard<std::mutex> lk(gate_mu_);
         engine = gate_engine_;
       }
-      gate_threads_.run([engine, ids = std::move(ids), done = std::move(done)] {
-        done(prestart_verdict(engine.get(), ids));
-      });
+      auto shared_done = std::make_shared<std::function<void(rpc::Reply)>>(std::move(done));
+      const double budget = f_.prestart_budget;
+      if (!gate_pool_.submit([engine, ids = std::move(ids), shared_done, budget, arrival] {
+            (*shared_done)(prestart_verdict(engine.get(), ids, budget, arrival));
+          })) {
+        metrics::global().inc("mi355x_dp_prestart_checks_total", {{"result", "overflow"}}, 1.0,
+                              "PreStartContainer liveness checks (-prestart_liveness): ok, failed, inconclusive (busy GPU or budget spent)");
+        MI_LOG(kWarning, "PreStartContainer: %zu checks already queued; this start goes ahead unchecked", size_t{64});
+        (*shared_done)(rpc::Reply{});
+      }
     };
   // explicit -driver_type: exit 1 when it cannot start (main.go:94-105); else
   // container -> VF -> PF, and with none the manager still starts and idles (main.go:106-119)

@@ -24,6 +24,9 @@
 #include <signal.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -54,23 +57,37 @@ struct Completion {
   SweepResult sweep;
 };
 
-// -prestart_liveness: PreStartContainer's answer from a probe of the
-// container's devices now (blocking; a gate thread). FAILED_PRECONDITION names
-// each device with a definite fault; a pending or interrupted probe, or a
-// device the probe server cannot reach, does not hold the container back.
-rpc::Reply prestart_verdict(health::Engine* engine, const std::vector<std::string>& ids);
+// -prestart_liveness: PreStartContainer's answer from a check of the
+// container's devices now (blocking; a gate worker), within what is left of
+// `budget_s` since `arrival`. FAILED_PRECONDITION names each device with a
+// definite fault; a pending or interrupted probe, a device the probe server
+// cannot reach, and a check whose budget ran out do not hold the container
+// back (counted in mi355x_dp_prestart_checks_total{result="inconclusive"}).
+rpc::Reply prestart_verdict(health::Engine* engine, const std::vector<std::string>& ids, double budget_s,
+                            std::chrono::steady_clock::time_point arrival);
 
-// The threads PreStartContainer checks run on (one per check, off the RPC
-// thread): finished ones are joined when the next starts, the rest at shutdown.
-class GateThreads {
+// The workers PreStartContainer checks run on, off the RPC thread: a fixed
+// pool and a bounded queue. A check that finds the queue full is answered at
+// once (`overflow`); one that waited past its budget in the queue runs with
+// nothing left and is answered inconclusive.
+class GatePool {
  public:
-  ~GateThreads() { join_all(); }
-  void run(std::function<void()> fn);
+  explicit GatePool(size_t workers = 8, size_t max_queued = 64) : workers_(workers), max_queued_(max_queued) {}
+  ~GatePool() { join_all(); }
+  // false (and `fn` not run) when the queue is full
+  bool submit(std::function<void()> fn);
+  // runs what is queued, then stops the workers
   void join_all();
+  size_t threads() const;
 
  private:
-  std::mutex mu_;
-  std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> ts_;
+  void loop();
+  const size_t workers_, max_queued_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> ts_;
+  bool stop_ = false;
 };
 
 // Register{version=1, endpoint=2, resource_name=3, options=4} on kubelet.sock (blocking; worker thread)
@@ -126,7 +143,7 @@ class Daemon {
   // -prestart_liveness: the engine the gate probes with (read on RPC threads)
   std::mutex gate_mu_;
   std::shared_ptr<health::Engine> gate_engine_;
-  GateThreads gate_threads_;
+  GatePool gate_pool_;
   // kubelet
   std::string kubelet_sock_;
   DirWatcher watch_;

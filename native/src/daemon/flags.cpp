@@ -16,7 +16,7 @@ std::string usage(const std::string& argv0) {
          "[-allocator_extended_search] [-grpc_watchdog S] [-reregister S] [-register_timeout S] [-config FILE] "
          "[-metrics_port N] [-topology_watch S] "
          "[-device_list_strategy device-specs|cdi-cri|cdi-annotations[,...]] [-cdi_spec_dir DIR] "
-         "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-prestart_liveness] [-liveness_timeout S] "
+         "[-liveness [-liveness_mode persistent|spawn] [-liveness_keep_queues] [-prestart_liveness [-prestart_budget S]] [-liveness_timeout S] [-liveness_busy_deadline S] "
          "[-liveness_fail_threshold N] [-liveness_busy_grace S] [-liveness_unknown_busy_grace S] "
          "[-liveness_corroborate] [-liveness_crowded_procs N] [-liveness_probe PATH] [-liveness_chip_sweep_every N] "
          "[-perf_check_every N [-perf_mib N] [-perf_action report|unhealthy] [-perf_min_hbm_read_gbps X] "
@@ -49,6 +49,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, 
       {"perf_mib", &f->perf_mib}};
   std::map<std::string, double*> floats = {
       {"liveness_timeout", &f->liveness_timeout}, {"liveness_busy_grace", &f->liveness_busy_grace},
+      {"prestart_budget", &f->prestart_budget}, {"liveness_busy_deadline", &f->liveness_busy_deadline},
       {"liveness_unknown_busy_grace", &f->liveness_unknown_busy_grace}, {"grpc_watchdog", &f->grpc_watchdog_s},
       {"register_timeout", &f->register_timeout_s}, {"topology_watch", &f->topology_watch_s},
       {"reregister", &f->reregister_s},
@@ -139,6 +140,9 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* help, 
   if (f->liveness && f->pulse == 0) return *err = "-liveness needs -pulse > 0 (the probe runs once per pulse)", false;
   if (f->prestart_liveness && !f->liveness)
     return *err = "prestart_liveness needs -liveness (the check runs in the probe server)", false;
+  if (!(f->prestart_budget > 0 && f->prestart_budget < 30))
+    return *err = "prestart_budget must be in (0, 30) seconds (kubelet's PreStartContainer deadline is 30 s)", false;
+  if (!(f->liveness_busy_deadline > 0)) return *err = "liveness_busy_deadline must be > 0", false;
   if (f->perf_action != "report" && f->perf_action != "unhealthy")
     return *err = "invalid perf_action provided: " + f->perf_action + ", supported values are report or unhealthy",
            false;

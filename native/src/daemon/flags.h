@@ -34,7 +34,13 @@ struct Flags {
   // PreStartContainer probes the container's GPUs (through the probe server) and
   // fails the start on a definite fault; needs -liveness
   bool prestart_liveness = false;
+  // the check's whole budget, kubelet's 30 s PreStartContainer deadline in
+  // mind (v1beta1/constants.go:44): what it cannot settle in time is let through
+  double prestart_budget = 5.0;
   double liveness_timeout = 10.0;
+  // probe deadline on a GPU other processes have queues on (kept queues): a
+  // dispatch queued behind a tenant's kernel is inconclusive however long it waits
+  double liveness_busy_deadline = 0.05;
   int liveness_iters = 4;
   int liveness_fail_threshold = 2;
   int liveness_recover_threshold = 1;

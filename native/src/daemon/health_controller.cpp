@@ -27,6 +27,7 @@ health::Config engine_config(const Flags& f) {
   hc.liveness = f.liveness;
   hc.prober.exe = !f.liveness_probe.empty() ? f.liveness_probe : path_join(self_dir(), "mi355x-liveness-probe");
   hc.prober.timeout_s = f.liveness_timeout;
+  hc.prober.busy_deadline_s = f.liveness_busy_deadline;
   hc.prober.iters = f.liveness_iters;
   hc.prober.persistent = f.liveness_mode == "persistent";
   hc.prober.keep_queues = f.liveness_keep_queues;

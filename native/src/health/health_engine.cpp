@@ -147,7 +147,8 @@ const GpuDevice* Engine::dev(const std::string& id) const {
   return it == by_id_.end() ? nullptr : &devices_[it->second];
 }
 
-const std::map<std::string, int>& Engine::ordinals() {
+std::map<std::string, int> Engine::ordinals() {
+  std::lock_guard<std::mutex> lk(state_mu_);
   if (!ordinals_) ordinals_ = hip_ordinals(devices_, topo_, cfg_.dev_root);
   return *ordinals_;
 }
@@ -283,7 +284,10 @@ std::map<std::string, ProbeOutcome> Engine::verify_identity(const std::map<std::
   for (const auto& [id, o] : ordinals())
     if (!ords.count(id)) merged[id] = o;
   for (const auto& [id, o] : new_ords) merged[id] = o;
-  ordinals_ = merged;
+  {
+    std::lock_guard<std::mutex> lk(state_mu_);
+    ordinals_ = merged;
+  }
   identity_remaps_++;
   metrics::global().inc("mi355x_dp_probe_identity_mismatch_total", {}, 1.0,
                         "sweeps whose probe replies came from other devices than the positional ordinal map");
@@ -329,6 +333,7 @@ bool Engine::update_busy_state(const std::map<std::string, int>& ords, std::set<
 // off them until they stay uncrowded for crowded_release_sweeps sweeps.
 std::set<std::string> Engine::update_crowded(const std::map<std::string, int>& ords) {
   std::set<std::string> crowded;
+  std::lock_guard<std::mutex> lk(state_mu_);
   if (cfg_.crowded_procs <= 0) {
     crowded_.clear();
     return crowded;
@@ -577,23 +582,23 @@ bool Engine::publish(Reasons reasons) {
   return changed;
 }
 
-// One sweep: every source adds its reasons; a device with none is Healthy.
-std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::string>& ids) {
-  std::lock_guard<std::mutex> op(op_mu_);
+// PreStartContainer's check: beside any sweep, never behind it.
+std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::string>& ids, double budget_s) {
   if (!cfg_.liveness || !prober_) return {};
   trace::Span span("liveness.prestart", "health", {{"devices", std::to_string(ids.size())}});
   std::map<std::string, int> sel;
-  const auto& ords = ordinals();
-  for (const auto& id : ids)  // the probe server stays off crowded GPUs here too (update_crowded)
-    if (auto it = ords.find(id); it != ords.end() && !crowded_.count(id)) sel[id] = it->second;
+  {
+    const auto ords = ordinals();
+    std::lock_guard<std::mutex> lk(state_mu_);
+    for (const auto& id : ids)  // the probe server stays off crowded GPUs here too (update_crowded)
+      if (auto it = ords.find(id); it != ords.end() && !crowded_.count(id)) sel[id] = it->second;
+  }
   if (sel.empty()) return {};
   std::vector<int> uniq;
   for (const auto& [id, o] : sel) uniq.push_back(o);
-  std::sort(uniq.begin(), uniq.end());
-  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
   // GPUs with other processes' queues (the probe server's own excluded), as a sweep
-  // sees them: a dispatch still queued behind their work there is pending, not a
-  // fault to confirm with a fresh process (which the container would then wait for)
+  // sees them: a dispatch queued behind their work there is inconclusive, gets the
+  // short deadline and no fresh-process confirmation (which the container would wait for)
   std::set<int64_t> gids;
   for (const auto& [id, o] : sel) gids.insert(gpu_id(id));
   gids.erase(0);
@@ -602,13 +607,24 @@ std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::str
   std::set<int> busy;
   for (const auto& [id, o] : sel)
     if (!known || load.count(gpu_id(id))) busy.insert(o);
-  const auto by_ord = prober_->probe(uniq, busy, "probe");
-  std::map<std::string, ProbeOutcome> raw;
-  for (const auto& [id, o] : sel)
-    if (auto it = by_ord.find(o); it != by_ord.end()) raw[id] = it->second;
-  return verify_identity(sel, raw);
+  const auto by_ord = prober_->check(uniq, busy, budget_s);
+  std::map<std::string, ProbeOutcome> out;
+  for (const auto& [id, o] : sel) {
+    auto it = by_ord.find(o);
+    if (it == by_ord.end()) continue;
+    ProbeOutcome r = it->second;
+    if (const GpuDevice* d = dev(id); d && !r.interrupted && !identity_matches(*d, r)) {
+      // the ordinal map is stale (the sweep re-keys it): no verdict on this device from another agent's reply
+      r.ok = false;
+      r.pending = true;
+      r.reason = "probe reply from agent " + r.pci_bus_id + ", not this device: left to the next sweep";
+    }
+    out[id] = r;
+  }
+  return out;
 }
 
+// One sweep: every source adds its reasons; a device with none is Healthy.
 bool Engine::sweep() {
   trace::Span span("health.sweep", "health", {{"devices", std::to_string(devices_.size())}});
   const double t0 = mono_s();
@@ -622,8 +638,8 @@ bool Engine::sweep() {
         reasons[d.id].push_back("exporter reports " + d.bdf + " unhealthy");
   }
   if (cfg_.liveness && prober_) {
-    // the prober, the ordinal map and the crowd state are shared with probe_now(); a
-    // PreStartContainer check waits for this pass only, not for the exporter or amd-smi
+    // probe_now() runs beside this pass: it reads the ordinal map and the crowd
+    // state under state_mu_ and sends its own tagged request to the probe server
     std::lock_guard<std::mutex> op(op_mu_);
     liveness_pass(&reasons);
   }

@@ -160,7 +160,7 @@ struct DeviceWork {
     }
     if (keep) {
       Resident* s = resident_slot(ordinal);
-      std::unique_lock<std::mutex> lk(s->mu);
+      std::unique_lock<std::timed_mutex> lk(s->mu);
       if (!s->ready && !s->pending && !s->blocker) {
         mi355x_probe_result scratch;
         std::memset(&scratch, 0, sizeof(scratch));
@@ -240,7 +240,7 @@ struct DeviceWork {
 
   const Agent& ag;
   Resident* slot = nullptr;
-  std::unique_lock<std::mutex> slot_lk;
+  std::unique_lock<std::timed_mutex> slot_lk;
   hsa_code_object_reader_t reader{};
   hsa_executable_t exe{};
   hsa_queue_t* queue = nullptr;

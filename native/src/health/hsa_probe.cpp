@@ -468,7 +468,7 @@ std::vector<std::pair<int, std::unique_ptr<Resident>>> g_resident;
 void release_residents() {
   std::lock_guard<std::mutex> lk(g_resident_mu);
   for (auto& e : g_resident) {
-    std::lock_guard<std::mutex> lk2(e.second->mu);
+    std::lock_guard<std::timed_mutex> lk2(e.second->mu);
     if (e.second->ready && !e.second->pending && !e.second->blocker) e.second->r.release();
     if (e.second->blocker && e.second->blocker->s.handle &&
         H().hsa_signal_load_scacquire(e.second->blocker->s) >= 1)
@@ -535,7 +535,18 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
 
   if (keep) {
     Resident* slot = resident_slot(ordinal);
-    std::lock_guard<std::mutex> lk(slot->mu);
+    // another request's probe, chip sweep or throughput check holds this
+    // device's kept queue (concurrent --serve requests): wait for it no longer
+    // than this probe's own deadline, then answer pending without a dispatch
+    std::unique_lock<std::timed_mutex> lk(slot->mu, std::defer_lock);
+    if (!lk.try_lock_for(std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0))) {
+      const double s_out = std::max(1e-3, std::chrono::duration<double>(clk::now() - t0).count());
+      std::snprintf(out->error, sizeof(out->error),
+                    "another request on this device's queue still running after %.2fs (not dispatched)", s_out);
+      out->pending_s = s_out;
+      out->hip_error = -1;
+      return finish();
+    }
     if (!slot->ready) {
       if (!setup_resources(ag, slot->r, slot->k, out)) {
         slot->r.release();

@@ -97,7 +97,7 @@ struct KernelInfo {
 
 // Kept ("resident") per-device resources for mi355x_hsa_probe_keep(1).
 struct Resident {
-  std::mutex mu;  // one probe at a time per device
+  std::timed_mutex mu;  // one probe at a time per device (a waiter gives up at its deadline)
   bool ready = false;
   ProbeResources r;
   KernelInfo k;

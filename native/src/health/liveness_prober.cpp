@@ -17,7 +17,11 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
 
 #include "../kube/json.h"
 #include "mi355x/dp_service.h"
@@ -166,7 +170,7 @@ bool drain(Child* c) {
   }
 }
 
-enum class Got { kLine, kTimeout, kEof, kAbort };
+using Got = LivenessProber::Got;
 
 // next '\n'-terminated line of c's stdout within `deadline`
 Got read_line(Child* c, double deadline, int abort_fd, std::string* line) {
@@ -240,34 +244,97 @@ std::string join_ints(const std::vector<int>& v, const char* sep) {
 }  // namespace
 
 // =============================================================== LivenessProber
+// The running --serve child. Replies are routed by request id: whichever
+// caller is waiting reads the pipe for everyone (reading), files each line
+// under its id and wakes the others. The pipe fds live as long as the object,
+// so a reader never polls a descriptor another thread closed.
 struct LivenessProber::Server {
   Child c;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool reading = false;  // a caller is reading c.out (c.buf and c.eof are its own meanwhile)
+  bool dead = false;     // EOF, write failure or shut down
+  bool aborted = false;  // the abort fd became readable (shutdown)
+  bool reaped = false;
+  bool concurrent = false;  // the hello line: tagged requests are answered as they complete
+  std::map<uint64_t, std::string> replies;
+  std::set<uint64_t> waiting;
+  std::deque<uint64_t> order;  // waiting ids in send order (a reply without an id answers the oldest)
+  std::optional<std::vector<int>> visible;
+  std::set<std::string> own_kfd;
+
+  ~Server() {
+    stop();
+    if (c.in >= 0) ::close(c.in);
+    if (c.out >= 0) ::close(c.out);
+  }
   bool alive() {
-    if (c.pid <= 0) return false;
+    std::lock_guard<std::mutex> lk(mu);
+    if (dead || c.pid <= 0) return false;
     int st = 0;
-    const pid_t r = ::waitpid(c.pid, &st, WNOHANG);
-    if (r == c.pid) {
-      c.pid = -1;
+    if (::waitpid(c.pid, &st, WNOHANG) == c.pid) {
+      reaped = true;
+      dead = true;
+      cv.notify_all();
       return false;
     }
     return true;
+  }
+  // "quit", SIGKILL to its session, reaped; the waiters see EOF
+  void stop() {
+    pid_t pid;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!dead && c.in >= 0) write_all(c.in, "quit\n");
+      dead = true;
+      pid = reaped ? -1 : c.pid;
+      reaped = true;
+      cv.notify_all();
+    }
+    if (pid > 0) {
+      ::kill(-pid, SIGKILL);
+      ::kill(pid, SIGKILL);
+      int st = 0;
+      while (::waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+      }
+    }
+  }
+  // a reply line -> the waiting caller it answers (under mu)
+  void file(const std::string& line) {
+    uint64_t id = 0;
+    bool tagged = false;
+    if (line.compare(0, 6, "{\"id\":") == 0) {
+      char* end = nullptr;
+      id = std::strtoull(line.c_str() + 6, &end, 10);
+      tagged = end != line.c_str() + 6;
+    }
+    if (!tagged) {
+      if (order.empty()) return;
+      id = order.front();
+    }
+    if (waiting.count(id)) replies[id] = line;
   }
 };
 
 LivenessProber::LivenessProber(ProberConfig cfg) : cfg_(std::move(cfg)) {}
 LivenessProber::~LivenessProber() { close(); }
 
-bool LivenessProber::server_running() const { return server_ && server_->c.pid > 0; }
+bool LivenessProber::server_running() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return server_ && server_->c.pid > 0 && !server_->dead;
+}
+
+double LivenessProber::inner_timeout() const { return cfg_.timeout_s - std::min(0.5, 0.25 * cfg_.timeout_s); }
 
 void LivenessProber::close() {
-  pending_nonce_.clear();  // a new server starts without outstanding dispatches
-  if (server_) {
-    if (server_->c.in >= 0) write_all(server_->c.in, "quit\n");
-    kill_child(&server_->c);
-    server_.reset();
+  std::shared_ptr<Server> old;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    old.swap(server_);
+    issued_.clear();  // a new server starts without outstanding dispatches
+    restart_wanted_ = false;
   }
-  server_visible_.reset();
-  own_kfd_.clear();
+  if (old) old->stop();  // outside mu_: the GPU process' teardown can take a while
 }
 
 void LivenessProber::set_visible(std::optional<std::vector<int>> ordinals) {
@@ -275,39 +342,47 @@ void LivenessProber::set_visible(std::optional<std::vector<int>> ordinals) {
     std::sort(ordinals->begin(), ordinals->end());
     ordinals->erase(std::unique(ordinals->begin(), ordinals->end()), ordinals->end());
   }
+  std::lock_guard<std::mutex> lk(mu_);
   visible_ = std::move(ordinals);
 }
 
 std::set<std::string> LivenessProber::own_kfd_entries(const std::set<int64_t>& gpu_ids) {
-  if (!server_ || !server_->alive()) return {};
-  if (own_kfd_.size() > 1) {  // another GPU process started with the server: keep what still exists
+  std::shared_ptr<Server> s;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    s = server_;
+  }
+  if (!s || !s->alive()) return {};
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (s->own_kfd.size() > 1) {  // another GPU process started with the server: keep what still exists
     std::set<std::string> still;
     for (const auto& e : list_dir(cfg_.kfd_proc_dir))
-      if (own_kfd_.count(e)) still.insert(e);
-    own_kfd_ = still;
+      if (s->own_kfd.count(e)) still.insert(e);
+    s->own_kfd = still;
   }
-  if (own_kfd_.size() == 1) return own_kfd_;
-  if (own_kfd_.size() > 1 && cfg_.keep_queues && !gpu_ids.empty()) {
+  if (s->own_kfd.size() == 1) return s->own_kfd;
+  if (s->own_kfd.size() > 1 && cfg_.keep_queues && !gpu_ids.empty()) {
     // the kept-queue server holds a queue on every GPU it probed; a pod's process only on the pod's
     std::vector<std::string> match;
-    for (const auto& e : own_kfd_) {
+    for (const auto& e : s->own_kfd) {
       std::set<int64_t> have;
       const std::string qdir = path_join(path_join(cfg_.kfd_proc_dir, e), "queues");
       for (const auto& q : list_dir(qdir))
         if (auto g = read_trimmed(path_join(path_join(qdir, q), "gpuid"))) have.insert(parse_i64(*g, 0));
       if (std::includes(have.begin(), have.end(), gpu_ids.begin(), gpu_ids.end())) match.push_back(e);
     }
-    if (match.size() == 1) own_kfd_ = {match[0]};
-    if (own_kfd_.size() == 1) return own_kfd_;
+    if (match.size() == 1) s->own_kfd = {match[0]};
+    if (s->own_kfd.size() == 1) return s->own_kfd;
   }
   return {};
 }
 
 ProbeOutcome LivenessProber::probe_ordinal(int ordinal, const std::string& kind) {
-  return spawn_all({ordinal}, kind)[ordinal];
+  return spawn_all({ordinal}, kind, cfg_.timeout_s)[ordinal];
 }
 
-std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& ords, const std::string& kind) {
+std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& ords, const std::string& kind,
+                                                      double timeout_s) {
   std::map<int, ProbeOutcome> out;
   const size_t par = static_cast<size_t>(std::max(1, cfg_.max_parallel));
   for (size_t start = 0; start < ords.size(); start += par) {
@@ -326,7 +401,7 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
       j.ordinal = ords[i];
       j.nonce = make_nonce(j.ordinal);
       char tmo[32];
-      std::snprintf(tmo, sizeof(tmo), "%.2f", std::max(0.5, cfg_.timeout_s - 0.5));
+      std::snprintf(tmo, sizeof(tmo), "%.2f", std::max(0.5, timeout_s - 0.5));
       std::vector<std::string> argv = cfg_.argv_prefix;
       for (const std::string& a : {cfg_.exe, std::string("--devices"), std::string("0"), std::string("--iters"),
                                    std::to_string(cfg_.iters), std::string("--nonce"), std::to_string(j.nonce),
@@ -347,7 +422,7 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
       }
       jobs.push_back(std::move(j));
     }
-    const double deadline = mono_s() + cfg_.timeout_s;
+    const double deadline = mono_s() + timeout_s;
     bool aborted = false;
     while (true) {
       std::vector<pollfd> pf;
@@ -381,7 +456,7 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
         kill_child(&j.c);
         ProbeOutcome o;
         char why[64];
-        std::snprintf(why, sizeof(why), "deadline exceeded (%.1fs)", cfg_.timeout_s);
+        std::snprintf(why, sizeof(why), "deadline exceeded (%.1fs)", timeout_s);
         o.reason = aborted ? "probe interrupted (shutdown)" : why;
         o.latency_ms = ms;
         o.pending = kind == "probe" && !aborted;  // inconclusive on a busy GPU
@@ -423,72 +498,146 @@ std::map<int, ProbeOutcome> LivenessProber::spawn_all(const std::vector<int>& or
   return out;
 }
 
-std::map<int, ProbeOutcome> LivenessProber::probe_server(const std::vector<int>& uniq, const std::string& kind,
-                                                         std::string* err) {
-  trace::Span span("liveness.request", "health", {{"ordinals", std::to_string(uniq.size())}, {"kind", kind}});
-  const double t0 = mono_s();
-  std::optional<std::vector<int>> visible = visible_;
-  if (visible) {
-    std::set<int> u(visible->begin(), visible->end());
-    bool grow = false;
-    for (int o : uniq) grow |= u.insert(o).second;
-    if (grow) visible = std::vector<int>(u.begin(), u.end());
-  }
-  if (server_ && server_->alive() && visible != server_visible_) close();  // the GPUs it may touch changed
-  if (!server_ || !server_->alive()) {
-    if (server_) close();
-    std::vector<std::string> argv = cfg_.argv_prefix;
-    argv.push_back(cfg_.exe);
-    argv.push_back("--serve");
-    if (cfg_.keep_queues) argv.push_back("--keep");
-    std::set<std::string> before;
-    for (const auto& e : list_dir(cfg_.kfd_proc_dir)) before.insert(e);
-    auto srv = std::make_unique<Server>();
-    if (!spawn_child(argv, child_env(cfg_, visible ? join_ints(*visible, ",") : ""), true, &srv->c, err)) return {};
-    std::string hello;
-    const Got g = read_line(&srv->c, mono_s() + cfg_.timeout_s, abort_fd_, &hello);
-    auto doc = g == Got::kLine ? json::parse(hello) : std::nullopt;
-    if (!doc || !jbool(&*doc, "serve") || !jbool(&*doc, "ok")) {
-      kill_child(&srv->c);
-      // shutdown interrupted the start: "interrupted", so probe() reports interrupted
-      // outcomes instead of falling back to fresh GPU processes while the daemon stops
-      *err = g == Got::kAbort     ? "interrupted"
-             : g == Got::kTimeout ? "probe server did not start within the deadline"
-                                  : "probe server failed to start: " + hello.substr(0, 200);
-      return {};
+// The server for the sweep's next request: started (or restarted, when the
+// GPUs it may touch changed or a check asked for it) here and only here.
+std::shared_ptr<LivenessProber::Server> LivenessProber::ensure_server(const std::vector<int>& uniq,
+                                                                      std::string* err) {
+  std::optional<std::vector<int>> visible;
+  std::shared_ptr<Server> stale;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    visible = visible_;
+    if (visible) {
+      std::set<int> u(visible->begin(), visible->end());
+      bool grow = false;
+      for (int o : uniq) grow |= u.insert(o).second;
+      if (grow) visible = std::vector<int>(u.begin(), u.end());
     }
-    server_ = std::move(srv);
-    server_visible_ = visible;
-    own_kfd_.clear();
-    for (const auto& e : list_dir(cfg_.kfd_proc_dir))
-      if (!before.count(e)) own_kfd_.insert(e);
-    server_starts++;
+    if (server_ && !restart_wanted_ && server_->visible == visible && server_->alive()) return server_;
+    if (restart_wanted_ && server_) {
+      server_restarts++;
+      MI_LOG(kWarning, "probe server failed a device that a fresh process found healthy (PreStartContainer check); "
+                       "restarting it");
+    }
+    restart_wanted_ = false;
+    stale.swap(server_);
+    issued_.clear();
   }
+  if (stale) stale->stop();
+  std::vector<std::string> argv = cfg_.argv_prefix;
+  argv.push_back(cfg_.exe);
+  argv.push_back("--serve");
+  if (cfg_.keep_queues) argv.push_back("--keep");
+  std::set<std::string> before;
+  for (const auto& e : list_dir(cfg_.kfd_proc_dir)) before.insert(e);
+  auto srv = std::make_shared<Server>();
+  if (!spawn_child(argv, child_env(cfg_, visible ? join_ints(*visible, ",") : ""), true, &srv->c, err)) return nullptr;
+  std::string hello;
+  const Got g = read_line(&srv->c, mono_s() + cfg_.timeout_s, abort_fd_, &hello);
+  auto doc = g == Got::kLine ? json::parse(hello) : std::nullopt;
+  if (!doc || !jbool(&*doc, "serve") || !jbool(&*doc, "ok")) {
+    srv->stop();
+    // shutdown interrupted the start: "interrupted", so probe() reports interrupted
+    // outcomes instead of falling back to fresh GPU processes while the daemon stops
+    *err = g == Got::kAbort     ? "interrupted"
+           : g == Got::kTimeout ? "probe server did not start within the deadline"
+                                : "probe server failed to start: " + hello.substr(0, 200);
+    return nullptr;
+  }
+  srv->concurrent = jbool(&*doc, "concurrent");
+  srv->visible = visible;
+  for (const auto& e : list_dir(cfg_.kfd_proc_dir))
+    if (!before.count(e)) srv->own_kfd.insert(e);
+  std::lock_guard<std::mutex> lk(mu_);
+  server_ = srv;
+  issued_.clear();
+  server_starts++;
+  return srv;
+}
+
+// Sends "@<id> <body>" and waits for the reply with that id until `deadline`.
+LivenessProber::Got LivenessProber::transact(const std::shared_ptr<Server>& s, const std::string& body,
+                                             double deadline, std::string* reply) {
+  const uint64_t id = next_id_++;
+  std::unique_lock<std::mutex> lk(s->mu);
+  if (s->dead) return Got::kEof;
+  if (!write_all(s->c.in, "@" + std::to_string(id) + " " + body + "\n")) {
+    s->dead = true;
+    s->cv.notify_all();
+    return Got::kEof;
+  }
+  s->waiting.insert(id);
+  s->order.push_back(id);
+  Got result;
+  while (true) {
+    if (auto it = s->replies.find(id); it != s->replies.end()) {
+      *reply = std::move(it->second);
+      s->replies.erase(it);
+      result = Got::kLine;
+      break;
+    }
+    if (s->aborted) {
+      result = Got::kAbort;
+      break;
+    }
+    if (s->dead) {
+      result = Got::kEof;
+      break;
+    }
+    if (mono_s() >= deadline) {
+      result = Got::kTimeout;
+      break;
+    }
+    if (!s->reading) {
+      s->reading = true;
+      lk.unlock();
+      std::string line;
+      const Got g = read_line(&s->c, deadline, abort_fd_, &line);
+      lk.lock();
+      s->reading = false;
+      if (g == Got::kLine) s->file(line);
+      else if (g == Got::kEof) s->dead = true;
+      else if (g == Got::kAbort) s->aborted = true;
+      s->cv.notify_all();
+      continue;
+    }
+    const double left = deadline - mono_s();
+    s->cv.wait_for(lk, std::chrono::duration<double>(std::max(0.0, left)));
+  }
+  s->waiting.erase(id);  // a reply that comes later is dropped
+  s->order.erase(std::remove(s->order.begin(), s->order.end(), id), s->order.end());
+  return result;
+}
+
+std::map<int, ProbeOutcome> LivenessProber::request(const std::shared_ptr<Server>& s, const std::vector<int>& uniq,
+                                                    const std::string& kind, const std::map<int, double>& deadlines,
+                                                    double wait_until, std::string* err) {
+  const double t0 = mono_s();
   // the server numbers the GPUs it sees: with a visibility list, their positions
   std::map<int, int> local, host;
   for (int o : uniq) {
     int l = o;
-    if (server_visible_) l = static_cast<int>(std::find(server_visible_->begin(), server_visible_->end(), o) -
-                                              server_visible_->begin());
+    if (s->visible) l = static_cast<int>(std::find(s->visible->begin(), s->visible->end(), o) - s->visible->begin());
     local[o] = l;
     host[l] = o;
   }
   std::map<int, uint32_t> nonces;
   for (int o : uniq) nonces[o] = make_nonce(o);
-  const double inner = cfg_.timeout_s - std::min(0.5, 0.25 * cfg_.timeout_s);
+  double top = 0;
+  for (const auto& [o, d] : deadlines) top = std::max(top, d);
   char head[96];
   if (kind == "perf")
-    std::snprintf(head, sizeof(head), "perf %d %.2f %d", cfg_.perf_iters, inner, cfg_.perf_mib);
+    std::snprintf(head, sizeof(head), "perf %d %.3f %d", cfg_.perf_iters, top, cfg_.perf_mib);
   else
-    std::snprintf(head, sizeof(head), "%s %d %.2f", kind.c_str(), cfg_.iters, inner);
+    std::snprintf(head, sizeof(head), "%s %d %.3f", kind.c_str(), cfg_.iters, top);
   std::string line = head;
-  for (int o : uniq) line += " " + std::to_string(local[o]) + ":" + std::to_string(nonces[o]);
-  if (!write_all(server_->c.in, line + "\n")) {
-    *err = "probe server gone (write failed)";
-    return {};
+  for (int o : uniq) {
+    char tok[64];
+    std::snprintf(tok, sizeof(tok), " %d:%u:%.3f", local[o], nonces[o], deadlines.at(o));
+    line += tok;
   }
   std::string reply;
-  const Got g = read_line(&server_->c, mono_s() + cfg_.timeout_s, abort_fd_, &reply);
+  const Got g = transact(s, line, wait_until, &reply);
   if (g != Got::kLine) {
     *err = g == Got::kTimeout ? "probe server missed its deadline"
            : g == Got::kAbort ? "interrupted"
@@ -509,6 +658,7 @@ std::map<int, ProbeOutcome> LivenessProber::probe_server(const std::vector<int>&
       if (host.count(l)) by_ord[host[l]] = &d;
     }
   std::map<int, ProbeOutcome> out;
+  std::lock_guard<std::mutex> lk(mu_);  // issued_
   for (int o : uniq) {
     auto it = by_ord.find(o);
     if (it == by_ord.end()) {
@@ -519,37 +669,62 @@ std::map<int, ProbeOutcome> LivenessProber::probe_server(const std::vector<int>&
       continue;
     }
     const json::Value* d = it->second;
+    const bool timed_out = jnum(d, "hip_error", 0) == -1 || jnum(d, "hsa_error", 0) == -1;
     if (kind != "probe") {  // sweeps run on their own queue: the kept slot is untouched
       out[o] = judge(jbool(d, "ok"), d, nonces[o], ms);
+      out[o].queue_lost = timed_out && !cfg_.keep_queues;
       continue;
     }
-    // a late verdict answers the dispatch (and nonce) of the probe that left it pending
+    // a late verdict answers the dispatch (and nonce) of an earlier request that left it pending
+    auto& mine = issued_[o];
     const bool late = jbool(d, "late");
     uint32_t expect = nonces[o];
     if (late) {
-      auto pn = pending_nonce_.find(o);
-      if (pn != pending_nonce_.end()) {
-        expect = pn->second;
-        pending_nonce_.erase(pn);
+      const json::Value* n = d->get("nonce");
+      const uint32_t got = n && n->kind == json::Value::Number
+                               ? static_cast<uint32_t>(std::strtoull(n->s.c_str(), nullptr, 10)) : 0;
+      if (auto f = std::find(mine.begin(), mine.end(), got); f != mine.end()) {
+        expect = got;
+        mine.erase(f);
       }
     }
     ProbeOutcome r = judge(jbool(d, "ok"), d, expect, ms);
+    r.queue_lost = timed_out && !cfg_.keep_queues;
     if (!r.ok && jnum(d, "pending_s", 0) > 0) {
       r.pending = true;
-      pending_nonce_.emplace(o, nonces[o]);
+      mine.push_back(nonces[o]);  // may be the dispatch still queued on the kept slot
+      if (mine.size() > 8) mine.erase(mine.begin());
     } else if (!r.ok && jnum(d, "hip_error", 0) == -1 && !cfg_.keep_queues) {
       r.pending = true;  // timed out without a kept slot: no late verdict will follow
     } else if (!late) {
-      pending_nonce_.erase(o);
+      mine.clear();  // the slot had nothing outstanding
     }
     out[o] = r;
   }
-  if (!cfg_.keep_queues)
-    for (const auto& [o, d] : by_ord)
-      if (jnum(d, "hip_error", 0) == -1 || jnum(d, "hsa_error", 0) == -1) {
-        close();  // a timed-out dispatch's queue can never be freed by the server: restart it
-        break;
-      }
+  return out;
+}
+
+std::map<int, ProbeOutcome> LivenessProber::probe_server(const std::vector<int>& uniq, const std::set<int>& busy,
+                                                         const std::string& kind, std::string* err) {
+  trace::Span span("liveness.request", "health", {{"ordinals", std::to_string(uniq.size())}, {"kind", kind}});
+  std::shared_ptr<Server> srv = ensure_server(uniq, err);
+  if (!srv) return {};
+  const double inner = inner_timeout();
+  std::map<int, double> deadlines;
+  for (int o : uniq)  // a dispatch queued behind a tenant's kernel stays on the kept queue for the next request
+    deadlines[o] = kind == "probe" && cfg_.keep_queues && busy.count(o) ? std::min(inner, cfg_.busy_deadline_s) : inner;
+  double top = 0;
+  for (const auto& [o, d] : deadlines) top = std::max(top, d);
+  // the reply is due at the longest device deadline; the margin covers the
+  // server's own bookkeeping (the full timeout when every device gets it)
+  const double wait = mono_s() + std::min(cfg_.timeout_s, top + (cfg_.timeout_s - inner));
+  auto out = request(srv, uniq, kind, deadlines, wait, err);
+  if (!err->empty()) return {};
+  for (const auto& [o, r] : out)
+    if (r.queue_lost) {
+      close();  // a timed-out dispatch's queue can never be freed by the server: restart it
+      break;
+    }
   return out;
 }
 
@@ -559,18 +734,22 @@ std::map<int, ProbeOutcome> LivenessProber::probe(const std::vector<int>& ordina
   std::sort(uniq.begin(), uniq.end());
   uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
   if (uniq.empty()) return {};
-  const bool use_server = cfg_.persistent && backoff_ == 0;
-  backoff_ = std::max(0, backoff_ - 1);
+  bool use_server;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    use_server = cfg_.persistent && backoff_ == 0;
+    backoff_ = std::max(0, backoff_ - 1);
+  }
   if (use_server) {
     std::string err;
-    auto res = probe_server(uniq, kind, &err);
+    auto res = probe_server(uniq, busy, kind, &err);
     if (err.empty()) {
       std::vector<int> failed;
       for (int o : uniq)
         if (!res[o].ok && !(res[o].pending && busy.count(o))) failed.push_back(o);
       if (!failed.empty()) {
         // the server's runtime lives across sweeps: a failure only counts if a fresh process confirms it
-        auto fresh = spawn_all(failed, kind);
+        auto fresh = spawn_all(failed, kind, cfg_.timeout_s);
         bool stale = false;
         std::vector<int> healed;
         for (int o : failed) {
@@ -605,12 +784,111 @@ std::map<int, ProbeOutcome> LivenessProber::probe(const std::vector<int>& ordina
     // a wedged device stalls the whole server: drop it and isolate per device
     MI_LOG(kWarning, "probe server failed (%s); re-probing each device in its own process", err.c_str());
     fallbacks++;
-    backoff_ = 4;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      backoff_ = 4;
+    }
     close();
   }
-  auto res = spawn_all(uniq, kind);
+  auto res = spawn_all(uniq, kind, cfg_.timeout_s);
   sweeps++;
   return res;
+}
+
+std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordinals, const std::set<int>& busy,
+                                                  double budget_s) {
+  trace::Span span("liveness.check", "health", {{"ordinals", std::to_string(ordinals.size())}});
+  const double t0 = mono_s(), end = t0 + budget_s;
+  std::vector<int> uniq(ordinals);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  checks++;
+  std::map<int, ProbeOutcome> out;
+  if (uniq.empty()) return out;
+  auto inconclusive = [&](int o, const std::string& why) {
+    ProbeOutcome r;
+    r.pending = true;
+    r.reason = why;
+    r.latency_ms = (mono_s() - t0) * 1e3;
+    out[o] = r;
+    check_inconclusive++;
+  };
+  std::shared_ptr<Server> srv;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (cfg_.persistent && backoff_ == 0 && server_ && !restart_wanted_) {
+      bool covers = true;
+      if (server_->visible)
+        for (int o : uniq)
+          covers = covers && std::count(server_->visible->begin(), server_->visible->end(), o);
+      if (covers) srv = server_;
+    }
+  }
+  std::map<int, ProbeOutcome> got;
+  if (srv && srv->alive()) {
+    // idle GPUs: 40% of the budget on the kept queue leaves the rest for a
+    // fresh process' confirmation (runtime start-up included)
+    const double inner = inner_timeout();
+    const double idle_dl = std::min(inner, std::max(0.2, 0.4 * budget_s));
+    std::map<int, double> deadlines;
+    double top = 0;
+    for (int o : uniq) top = std::max(top, deadlines[o] = busy.count(o) ? std::min(inner, cfg_.busy_deadline_s) : idle_dl);
+    std::string err;
+    got = request(srv, uniq, "probe", deadlines, std::min(end, mono_s() + top + 0.25), &err);
+    if (!err.empty()) {
+      if (err == "interrupted") {
+        for (int o : uniq) {
+          out[o].reason = "probe interrupted (shutdown)";
+          out[o].interrupted = true;
+        }
+        return out;
+      }
+      MI_LOG(kWarning, "PreStartContainer check: probe server: %s", err.c_str());
+      got.clear();
+    }
+    for (const auto& [o, r] : got)
+      if (r.queue_lost) {
+        std::lock_guard<std::mutex> lk(mu_);
+        restart_wanted_ = true;  // its timed-out queue cannot be freed: the next sweep restarts it
+      }
+  }
+  std::vector<int> confirm;
+  for (int o : uniq) {
+    auto it = got.find(o);
+    if (it != got.end() && it->second.ok) {
+      out[o] = it->second;
+    } else if (busy.count(o)) {
+      // queued behind (or, without a server answer, would queue behind) another process' kernels
+      inconclusive(o, it != got.end() ? it->second.reason : "no probe server answer on a busy GPU");
+    } else {
+      confirm.push_back(o);
+    }
+  }
+  if (confirm.empty()) return out;
+  const double left = end - mono_s();
+  if (left < 1.0) {  // a fresh GPU process needs its runtime start-up: not within what is left
+    for (int o : confirm)
+      inconclusive(o, "check budget spent" + (got.count(o) ? " (server: " + got[o].reason + ")" : std::string()));
+    return out;
+  }
+  check_fresh += static_cast<int>(confirm.size());
+  auto fresh = spawn_all(confirm, "probe", std::min(cfg_.timeout_s, left));
+  for (int o : confirm) {
+    ProbeOutcome f = fresh[o];
+    const bool server_failed = got.count(o) && !got[o].ok;
+    if (f.ok) {
+      if (server_failed) {
+        std::lock_guard<std::mutex> lk(mu_);
+        restart_wanted_ = true;  // a stale server runtime: the next sweep restarts it
+      }
+    } else if (!f.interrupted) {
+      if (f.pending)  // a fresh process on a GPU no other process uses got nothing back either
+        f.pending = false;
+      if (server_failed) f.reason += " (server: " + got[o].reason + ")";
+    }
+    out[o] = f;
+  }
+  return out;
 }
 
 }  // namespace mi355x::health

@@ -25,6 +25,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -213,8 +216,8 @@ void refresh_fault_injection() {
 
 // Probe (or identify) a set of ordinals, one host thread per GPU so an 8-GPU
 // request pays one device setup, not eight. Returns true when all are live.
-bool run_batch(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, int iters, double timeout_s,
-               bool identify, int n, std::vector<mi355x_probe_result>& results) {
+bool run_batch(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, int iters,
+               const std::vector<double>& timeouts, bool identify, int n, std::vector<mi355x_probe_result>& results) {
   results.assign(ords.size(), mi355x_probe_result{});
   std::vector<int> rcs(ords.size(), 1);
   auto run_one = [&](size_t i) {
@@ -223,7 +226,7 @@ bool run_batch(const std::vector<int>& ords, const std::vector<uint32_t>& nonces
       std::snprintf(results[i].error, sizeof(results[i].error), "no such GPU (count=%d)", n);
       return;
     }
-    rcs[i] = identify ? identify_dev(ords[i], &results[i]) : probe(ords[i], nonces[i], iters, timeout_s, &results[i]);
+    rcs[i] = identify ? identify_dev(ords[i], &results[i]) : probe(ords[i], nonces[i], iters, timeouts[i], &results[i]);
     if (identify && rcs[i] == 0) results[i].ok = 1;
   };
   if (ords.size() > 1) {
@@ -302,8 +305,8 @@ std::string sweep_json(const mi355x_sweep_result& r) {
 }
 
 // --sweep: the full-chip sweep on each selected GPU (parallel host threads).
-bool run_sweeps(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, int iters, double timeout_s,
-                int n, std::string& json) {
+bool run_sweeps(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, int iters,
+                const std::vector<double>& timeouts, int n, std::string& json) {
   std::vector<mi355x_sweep_result> res(ords.size());
   std::vector<int> rcs(ords.size(), 1);
   auto one = [&](size_t i) {
@@ -313,7 +316,7 @@ bool run_sweeps(const std::vector<int>& ords, const std::vector<uint32_t>& nonce
       std::snprintf(res[i].error, sizeof(res[i].error), "no such GPU (count=%d)", n);
       return;
     }
-    rcs[i] = chip_sweep(ords[i], nonces[i], iters, timeout_s, &res[i]);
+    rcs[i] = chip_sweep(ords[i], nonces[i], iters, timeouts[i], &res[i]);
   };
   std::vector<std::thread> ths;
   for (size_t i = 0; i < ords.size(); ++i) ths.emplace_back(one, i);
@@ -357,7 +360,7 @@ std::string perf_json(const mi355x_perf_result& r) {
 // --perf: the throughput check on each selected GPU (parallel host threads;
 // every GPU has its own HBM and matrix cores).
 bool run_perf(const std::vector<int>& ords, const std::vector<uint32_t>& nonces, uint64_t bytes, int iters,
-              double timeout_s, int n, std::string& json) {
+              const std::vector<double>& timeouts, int n, std::string& json) {
   std::vector<mi355x_perf_result> res(ords.size());
   std::vector<int> rcs(ords.size(), 1);
   auto one = [&](size_t i) {
@@ -367,7 +370,7 @@ bool run_perf(const std::vector<int>& ords, const std::vector<uint32_t>& nonces,
       std::snprintf(res[i].error, sizeof(res[i].error), "no such GPU (count=%d)", n);
       return;
     }
-    rcs[i] = perf_check(ords[i], nonces[i], bytes, iters, timeout_s, &res[i]);
+    rcs[i] = perf_check(ords[i], nonces[i], bytes, iters, timeouts[i], &res[i]);
   };
   std::vector<std::thread> ths;
   for (size_t i = 0; i < ords.size(); ++i) ths.emplace_back(one, i);
@@ -394,8 +397,18 @@ std::string devices_json(const std::vector<mi355x_probe_result>& results) {
 
 // --serve: a long-lived prober for the plugin's health loop. The runtime is
 // initialised once; every request line
-//     probe <iters> <timeout_s> <ordinal>:<nonce> [<ordinal>:<nonce> ...]
-// is answered with one JSON line {"ok":..,"t_ready_ns":..,"devices":[..]}.
+//     [@<id> ]probe <iters> <timeout_s> <ordinal>:<nonce>[:<deadline_s>] ...
+//     [@<id> ]sweep <iters> <timeout_s> <ordinal>:<nonce>[:<deadline_s>] ...
+//     [@<id> ]perf <mfma_iters> <timeout_s> <mib> <ordinal>:<nonce>[:<deadline_s>] ...
+// is answered with one JSON line {"id":..,"ok":..,"t_ready_ns":..,"devices":[..]}
+// ("id" only for a tagged request). A device's own deadline replaces the
+// request's timeout for that device: the plugin gives GPUs that run other
+// processes' kernels a short one, since a dispatch queued behind them is
+// inconclusive anyway and its verdict is collected by the next request.
+// Tagged requests are answered on worker threads, in completion order (the
+// HSA build): a PreStartContainer check of one GPU never waits behind a
+// health sweep still waiting for another GPU. Requests on the same device
+// serialise on its kept queue (each waits no longer than its own deadline).
 // "quit" or EOF on stdin ends the server, and so does the parent's death
 // (PR_SET_PDEATHSIG). Spawning a fresh probe process per pulse would create
 // and tear down a kfd process each time, and a GPU process that starts while
@@ -404,72 +417,160 @@ std::string devices_json(const std::vector<mi355x_probe_result>& results) {
 // With --keep the per-device queue, executable and buffers also stay: a probe
 // is then one AQL packet, with no queue creation (an HWS runlist update that
 // preempts every queue on that GPU, ~5 ms, profiles/archive/measurements_r1_r3.md §3f) per pulse.
+#ifdef MI355X_PROBE_HSA
+constexpr bool kConcurrentServe = true;
+#else
+constexpr bool kConcurrentServe = false;  // the HIP build answers in order
+#endif
+constexpr int kMaxServeWorkers = 64;  // beyond this a tagged request is answered inline
+
+struct ServeRequest {
+  bool tagged = false;
+  unsigned long long id = 0;
+  std::string kind;  // probe | sweep | perf
+  int iters = 0;
+  double timeout_s = 0;
+  unsigned long long perf_mib = 0;
+  std::vector<int> ords;
+  std::vector<uint32_t> nonces;
+  std::vector<double> timeouts;  // per device
+};
+
+bool parse_request(const std::string& line, ServeRequest* r) {
+  const char* p = line.c_str();
+  if (*p == '@') {
+    char* end = nullptr;
+    r->id = std::strtoull(p + 1, &end, 10);
+    if (end == p + 1 || *end != ' ') return false;
+    r->tagged = true;
+    p = end + 1;
+  }
+  int consumed = 0;
+  bool parsed = false;
+  if (std::strncmp(p, "perf ", 5) == 0) {
+    r->kind = "perf";
+    parsed = std::sscanf(p, "perf %d %lf %llu %n", &r->iters, &r->timeout_s, &r->perf_mib, &consumed) >= 3;
+  } else if (std::strncmp(p, "sweep ", 6) == 0) {
+    r->kind = "sweep";
+    parsed = std::sscanf(p, "sweep %d %lf %n", &r->iters, &r->timeout_s, &consumed) >= 2;
+  } else if (std::strncmp(p, "probe ", 6) == 0) {
+    r->kind = "probe";
+    parsed = std::sscanf(p, "probe %d %lf %n", &r->iters, &r->timeout_s, &consumed) >= 2;
+  }
+  if (!parsed || consumed == 0) return false;
+  p += consumed;
+  while (*p) {
+    char* end = nullptr;
+    const long o = std::strtol(p, &end, 10);
+    if (end == p || *end != ':') break;
+    p = end + 1;
+    const unsigned long nc = std::strtoul(p, &end, 0);
+    if (end == p) break;
+    p = end;
+    double dl = r->timeout_s;
+    if (*p == ':') {
+      const double v = std::strtod(p + 1, &end);
+      if (end == p + 1) break;
+      if (v > 0) dl = v;
+      p = end;
+    }
+    r->ords.push_back(static_cast<int>(o));
+    r->nonces.push_back(static_cast<uint32_t>(nc));
+    r->timeouts.push_back(dl);
+    while (*p == ' ') ++p;
+  }
+  return true;
+}
+
+std::mutex g_out_mu;
+
+void emit_line(const std::string& s) {
+  std::lock_guard<std::mutex> lk(g_out_mu);
+  std::fputs(s.c_str(), stdout);
+  std::fputc('\n', stdout);
+  std::fflush(stdout);
+}
+
+std::string id_field(const ServeRequest& r) {
+  return r.tagged ? "\"id\":" + std::to_string(r.id) + "," : std::string();
+}
+
+// One request, start to reply line; then the runtime's deferred frees.
+void answer(const ServeRequest& r, int n) {
+  refresh_fault_injection();
+  defer_teardown();
+  std::string body;
+  bool ok;
+  if (r.kind == "sweep") {
+    ok = run_sweeps(r.ords, r.nonces, r.iters, r.timeouts, n, body);
+  } else if (r.kind == "perf") {
+    ok = run_perf(r.ords, r.nonces, static_cast<uint64_t>(r.perf_mib) << 20, r.iters, r.timeouts, n, body);
+  } else {
+    std::vector<mi355x_probe_result> results;
+    ok = run_batch(r.ords, r.nonces, r.iters, r.timeouts, false, n, results);
+    body = devices_json(results);
+  }
+  char head[256];
+  std::snprintf(head, sizeof(head), "{%s\"ok\":%s,\"hip_device_count\":%d,\"sweep\":%s,\"perf\":%s,\"t_ready_ns\":%llu,",
+                id_field(r).c_str(), ok ? "true" : "false", n, r.kind == "sweep" ? "true" : "false",
+                r.kind == "perf" ? "true" : "false", static_cast<unsigned long long>(mono_ns()));
+  emit_line(std::string(head) + "\"devices\":" + body + "}");
+  teardown();  // queues/executables go, the runtime (and the kfd process) stays
+}
+
 int serve(int n, uint64_t t_start, uint64_t t_runtime) {
   prctl(PR_SET_PDEATHSIG, SIGKILL);
   if (getppid() == 1) return 0;  // parent already gone
-  std::printf("{\"serve\":true,\"ok\":%s,\"hip_device_count\":%d,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu}\n",
-              n >= 0 ? "true" : "false", n < 0 ? 0 : n, static_cast<unsigned long long>(t_start),
-              static_cast<unsigned long long>(t_runtime));
-  std::fflush(stdout);
+  char hello[320];
+  std::snprintf(hello, sizeof(hello),
+                "{\"serve\":true,\"ok\":%s,\"hip_device_count\":%d,\"concurrent\":%s,\"deadlines\":true,"
+                "\"t_start_ns\":%llu,\"t_runtime_ns\":%llu}",
+                n >= 0 ? "true" : "false", n < 0 ? 0 : n, kConcurrentServe ? "true" : "false",
+                static_cast<unsigned long long>(t_start), static_cast<unsigned long long>(t_runtime));
+  emit_line(hello);
   if (n < 0) return 2;
+  std::mutex wmu;
+  std::condition_variable wcv;
+  int running = 0;
   std::string line;
-  char buf[4096];
+  char buf[8192];
   while (std::fgets(buf, sizeof(buf), stdin)) {
     line = buf;
     while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
     if (line.empty()) continue;
     if (line == "quit") break;
-    int iters = 0;
-    double timeout_s = 0;
-    int consumed = 0;
-    unsigned long long perf_mib = 0;
-    const bool sweep_req = line.compare(0, 6, "sweep ") == 0;
-    const bool perf_req = line.compare(0, 5, "perf ") == 0;
-    bool parsed;
-    if (perf_req) {  // perf <mfma_iters> <timeout_s> <mib> <ordinal>:<nonce> ...
-      parsed = std::sscanf(line.c_str(), "perf %d %lf %llu %n", &iters, &timeout_s, &perf_mib, &consumed) >= 3;
-    } else {
-      parsed = std::sscanf(line.c_str(), sweep_req ? "sweep %d %lf %n" : "probe %d %lf %n", &iters, &timeout_s,
-                           &consumed) >= 2;
-    }
-    if (!parsed || consumed == 0) {
-      std::printf("{\"ok\":false,\"error\":\"bad request\",\"devices\":[]}\n");
-      std::fflush(stdout);
+    ServeRequest r;
+    if (!parse_request(line, &r)) {
+      emit_line("{" + id_field(r) + "\"ok\":false,\"error\":\"bad request\",\"devices\":[]}");
       continue;
     }
-    std::vector<int> ords;
-    std::vector<uint32_t> nonces;
-    const char* p = line.c_str() + consumed;
-    while (*p) {
-      char* end = nullptr;
-      const long o = std::strtol(p, &end, 10);
-      if (end == p || *end != ':') break;
-      p = end + 1;
-      const unsigned long nc = std::strtoul(p, &end, 0);
-      if (end == p) break;
-      ords.push_back(static_cast<int>(o));
-      nonces.push_back(static_cast<uint32_t>(nc));
-      p = end;
-      while (*p == ' ') ++p;
+    bool async = false;
+    if (r.tagged && kConcurrentServe) {
+      std::lock_guard<std::mutex> lk(wmu);
+      if (running < kMaxServeWorkers) {
+        running++;
+        async = true;
+      }
     }
-    std::vector<mi355x_probe_result> results;
-    refresh_fault_injection();
-    defer_teardown();
-    std::string body;
-    bool ok;
-    if (sweep_req) {
-      ok = run_sweeps(ords, nonces, iters, timeout_s, n, body);
-    } else if (perf_req) {
-      ok = run_perf(ords, nonces, static_cast<uint64_t>(perf_mib) << 20, iters, timeout_s, n, body);
-    } else {
-      ok = run_batch(ords, nonces, iters, timeout_s, false, n, results);
-      body = devices_json(results);
+    if (!async) {
+      answer(r, n);
+      continue;
     }
-    std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"sweep\":%s,\"perf\":%s,\"t_ready_ns\":%llu,\"devices\":%s}\n",
-                ok ? "true" : "false", n, sweep_req ? "true" : "false", perf_req ? "true" : "false",
-                static_cast<unsigned long long>(mono_ns()), body.c_str());
-    std::fflush(stdout);
-    teardown();  // queues/executables go, the runtime (and the kfd process) stays
+    std::thread([r = std::move(r), n, &wmu, &wcv, &running] {
+      answer(r, n);
+      std::lock_guard<std::mutex> lk(wmu);
+      running--;
+      wcv.notify_all();
+    }).detach();
+  }
+  {
+    // every worker's waits are bounded by its deadlines; one stuck inside the
+    // runtime past that keeps the runtime up: exit without shutting it down
+    std::unique_lock<std::mutex> lk(wmu);
+    if (!wcv.wait_for(lk, std::chrono::seconds(60), [&] { return running == 0; })) {
+      std::fflush(stdout);
+      std::_Exit(0);
+    }
   }
   runtime_shutdown();
   return 0;
@@ -604,9 +705,10 @@ int main(int argc, char** argv) {
   if (peer_mode) return run_peer(ords, nonce, peer_bytes, peer_reps, timeout_s, n);
   std::vector<uint32_t> nonces;
   for (size_t i = 0; i < ords.size(); ++i) nonces.push_back(nonce + static_cast<uint32_t>(i));
+  const std::vector<double> timeouts(ords.size(), timeout_s);
   if (perf_mode) {
     std::string body;
-    const bool ok = run_perf(ords, nonces, perf_mib << 20, perf_iters, timeout_s, n, body);
+    const bool ok = run_perf(ords, nonces, perf_mib << 20, perf_iters, timeouts, n, body);
     std::printf("{\"ok\":%s,\"perf\":true,\"hip_device_count\":%d,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
                 "\"t_ready_ns\":%llu,\"devices\":%s}\n",
                 ok ? "true" : "false", n, static_cast<unsigned long long>(t_start),
@@ -616,7 +718,7 @@ int main(int argc, char** argv) {
   }
   if (sweep_mode) {
     std::string body;
-    const bool ok = run_sweeps(ords, nonces, iters, timeout_s, n, body);
+    const bool ok = run_sweeps(ords, nonces, iters, timeouts, n, body);
     std::printf("{\"ok\":%s,\"sweep\":true,\"hip_device_count\":%d,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"
                 "\"t_ready_ns\":%llu,\"devices\":%s}\n",
                 ok ? "true" : "false", n, static_cast<unsigned long long>(t_start),
@@ -629,7 +731,7 @@ int main(int argc, char** argv) {
   // (container runtime, health loop) only waits for the JSON line.
   refresh_fault_injection();
   defer_teardown();
-  const bool all_ok = run_batch(ords, nonces, iters, timeout_s, identify, n, results);
+  const bool all_ok = run_batch(ords, nonces, iters, timeouts, identify, n, results);
   const uint64_t t_ready = mono_ns();
   const double cpu_ready = cpu_ms();
   std::printf("{\"ok\":%s,\"hip_device_count\":%d,\"identify\":%s,\"t_start_ns\":%llu,\"t_runtime_ns\":%llu,"

@@ -18,13 +18,22 @@ struct Line {
   int no;
 };
 
-// "# comment" to the end of each line, outside quoted scalars (which may span lines)
+// "# comment" to the end of each line, outside quoted scalars (which may span
+// lines). A quote opens a quoted scalar only where a node may start: at the
+// start of a line, after a block indicator followed by a blank ("key: ",
+// "- ", "? "), after an anchor or tag, and in flow context after '[', '{', ','
+// or a value ':'. Anywhere else (a plain scalar such as the key `:'` or
+// `a'b`) it is an ordinary character.
 std::string strip_comments(const std::string& s) {
   std::string out;
   char q = 0;
+  int flow = 0;
+  bool at_start = true;  // the next non-blank character begins a node
+  auto blank = [](char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; };
   for (size_t k = 0; k < s.size(); ++k) {
     const char ch = s[k];
     const char prev = k ? s[k - 1] : '\n';
+    const char next = k + 1 < s.size() ? s[k + 1] : '\n';
     if (q) {
       if (q == '"' && ch == '\\' && k + 1 < s.size()) {
         out += ch;
@@ -38,18 +47,58 @@ std::string strip_comments(const std::string& s) {
           continue;
         }
         q = 0;
+        at_start = false;
       }
       out += ch;
-    } else if ((ch == '"' || ch == '\'') && (prev == ' ' || prev == '\n' || prev == ':' || prev == '[' ||
-                                             prev == '{' || prev == ',' || prev == '\t')) {
-      q = ch;
-      out += ch;
-    } else if (ch == '#' && (prev == ' ' || prev == '\t' || prev == '\n')) {
+      continue;
+    }
+    if (ch == '#' && (prev == ' ' || prev == '\t' || prev == '\n')) {
       while (k < s.size() && s[k] != '\n') ++k;
       if (k < s.size()) out += '\n';
-    } else {
-      out += ch;
+      at_start = true;
+      continue;
     }
+    out += ch;
+    if (ch == '\n') {
+      at_start = true;
+      continue;
+    }
+    if (ch == ' ' || ch == '\t' || ch == '\r') continue;
+    if (at_start) {
+      if (ch == '"' || ch == '\'') {
+        q = ch;
+        continue;
+      }
+      if (ch == '[' || ch == '{') {
+        flow++;
+        continue;
+      }
+      if ((ch == '-' || ch == '?') && blank(next)) continue;
+      if (ch == '&' || ch == '!') {  // an anchor or tag: the node itself follows it
+        while (k + 1 < s.size() && !blank(s[k + 1])) out += s[++k];
+        continue;
+      }
+    }
+    if (flow > 0) {
+      if (ch == ',') {
+        at_start = true;
+        continue;
+      }
+      if (ch == ']' || ch == '}') {
+        flow--;
+        at_start = false;
+        continue;
+      }
+      if (ch == ':' && (blank(next) || prev == '"' || prev == '\'')) {  // after a JSON-like key: adjacent value
+        at_start = true;
+        continue;
+      }
+    }
+    if (ch == ':' && blank(next)) {
+      at_start = true;
+      continue;
+    }
+    at_start = false;
   }
   return out;
 }

@@ -126,24 +126,33 @@ bool parse_flag(const std::string& name, const std::string& value, bool has_valu
   };
   if (name == "logtostderr") return as_bool(&o->logtostderr), true;
   if (name == "alsologtostderr") return as_bool(&o->alsologtostderr), true;
-  if (name == "v") {  // glog's Level: strconv.ParseInt(value, 10, 32)
+  if (name == "v") {  // glog's Level.Set: strconv.Atoi (64-bit), stored as int32 (glog_flags.go:115-130)
     int64_t v = 0;
-    if (goflag::parse_int(value, 10, 32, &v))
-      o->v = static_cast<int>(v);
+    if (goflag::parse_int(value, 10, 64, &v))
+      o->v = static_cast<int32_t>(static_cast<uint32_t>(static_cast<uint64_t>(v)));
     else
       *err = "invalid value \"" + value + "\" for flag -v";
     return true;
   }
-  if (name == "stderrthreshold") {  // glog's severity.Set: a name in any case, else ParseInt(value, 10, 32)
+  if (name == "stderrthreshold") {
+    // glog's severityFlag.Set (glog_flags.go:341-356): a severity name in any
+    // case, else strconv.Atoi; the number becomes a logsink.Severity (int8) and
+    // must be INFO..FATAL
     std::string u;
     for (char c : value) u.push_back(static_cast<char>(std::toupper(static_cast<unsigned char>(c))));
-    int64_t sev = -1;
-    bool ok = false;
-    for (int i = 0; i < 4 && !ok; ++i)
-      if (u == kSevName[i]) sev = i, ok = true;
-    if (!ok) ok = goflag::parse_int(value, 10, 32, &sev);
-    if (!ok) *err = "invalid value \"" + value + "\" for flag -stderrthreshold";
-    else o->stderrthreshold = static_cast<int>(sev);
+    for (int i = 0; i < 4; ++i)
+      if (u == kSevName[i]) return o->stderrthreshold = i, true;
+    int64_t v = 0;
+    if (!goflag::parse_int(value, 10, 64, &v)) {
+      *err = "invalid value \"" + value + "\" for flag -stderrthreshold";
+      return true;
+    }
+    const int sev = static_cast<int8_t>(static_cast<uint8_t>(static_cast<uint64_t>(v)));
+    if (sev < 0 || sev > 3)
+      *err = "invalid value \"" + value + "\" for flag -stderrthreshold: Severity " + std::to_string(v) +
+             " out of range (min 0, max 3).";
+    else
+      o->stderrthreshold = sev;
     return true;
   }
   if (name == "log_dir") return o->log_dir = value, true;

@@ -886,10 +886,12 @@ static void test_flags_go_semantics() {
   for (const char* badv : {"-pulse=08", "-pulse=1__0", "-pulse=_1", "-pulse=1_", "-pulse=0x", "-pulse=1.5",
                            "-pulse= 3", "-pulse=99999999999", "-pulse=9223372036854775808"})
     CHECK(!parse({badv}, &syn, &err) && syn && err.find("invalid value") == 0);
-  // glog's -v: strconv.ParseInt(s, 10, 32), so leading zeros are decimal and prefixes are refused
+  // glog's -v: strconv.Atoi (64-bit) stored as an int32 (Level.Set, glog_flags.go:115-130), so
+  // leading zeros are decimal, prefixes are refused, and 2^32 + 3 is level 3
   CHECK(parse({"-v=05"}, &syn, &err, &f) && f.log.v == 5);
   CHECK(!parse({"-v=0x5"}, &syn, &err) && syn);
-  CHECK(!parse({"-v=4294967296"}, &syn, &err) && syn);
+  CHECK(parse({"-v=4294967299"}, &syn, &err, &f) && f.log.v == 3);
+  CHECK(!parse({"-v=9223372036854775808"}, &syn, &err) && syn);
   // strconv.ParseFloat
   CHECK(parse({"-liveness_timeout=2.5e1"}, &syn, &err, &f) && f.liveness_timeout == 25.0);
   CHECK(!parse({"-liveness_timeout= 2"}, &syn, &err) && syn);

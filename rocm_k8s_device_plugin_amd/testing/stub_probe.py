@@ -8,7 +8,11 @@ per ROCr ordinal comes from the JSON file named by $MI355X_STUB_PROBE_CONTROL
 (missing ordinals are "ok"; "serve": "broken" makes --serve fail to start,
 "serve": "slow_start" delays its hello by "serve_start_s" seconds;
 "server_fail" fails only inside --serve: a stale server runtime; "slow" answers ok
-after "slow_s" seconds, in --serve).
+after "slow_s" seconds, in --serve; "pending" keeps the dispatch queued and, like
+the real server, answers only when the device's deadline has passed).
+--serve speaks the real server's protocol: "@<id>"-tagged requests answered
+concurrently with their id, per-device deadlines ("<ordinal>:<nonce>:<s>"),
+requests on one device serialised on its slot.
 Exercises the real LivenessProber code path: process spawn, server protocol,
 deadline kill, fallback to per-device isolation, output parsing, nonce check,
 hysteresis. Each start appends a line to $MI355X_STUB_PROBE_LOG if set.
@@ -92,7 +96,23 @@ def _kfd_entry():
     return entry
 
 
+def _parse(line):
+    """One request line: (id or None, kind, timeout_s, [(ordinal, nonce, deadline_s)])."""
+    parts = line.split()
+    rid = None
+    if parts and parts[0].startswith("@"):
+        rid, parts = int(parts[0][1:]), parts[1:]
+    kind = parts[0]
+    timeout = float(parts[2])
+    devs = []
+    for tok in parts[4:] if kind == "perf" else parts[3:]:
+        f = tok.split(":")
+        devs.append((f[0], int(f[1], 0), float(f[2]) if len(f) > 2 and float(f[2]) > 0 else timeout))
+    return rid, kind, timeout, devs
+
+
 def serve():
+    import threading
     ctl = _control()
     if ctl.get("serve") == "broken":
         print(json.dumps({"serve": True, "ok": False, "hip_device_count": 0}), flush=True)
@@ -101,61 +121,102 @@ def serve():
         time.sleep(float(ctl.get("serve_start_s", 30)))
     _kfd_entry()
     t = time.monotonic_ns()
-    print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "t_start_ns": t, "t_runtime_ns": t}),
-          flush=True)
+    # like the real server: tagged requests are answered concurrently, as they complete
+    print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "concurrent": True, "deadlines": True,
+                      "t_start_ns": t, "t_runtime_ns": t}), flush=True)
     slots = {}   # ordinal -> nonce of the kept slot's outstanding dispatch (like --keep)
+    locks = {}   # ordinal -> its kept slot's lock (requests on one device serialise, as on the real server)
+    out_mu, state_mu = threading.Lock(), threading.Lock()
     # like ROCr: with ROCR_VISIBLE_DEVICES the server numbers only those GPUs
     vis = [x for x in os.environ.get("ROCR_VISIBLE_DEVICES", "").split(",") if x]
     starts_log = os.environ.get("MI355X_STUB_PROBE_LOG")
     if starts_log and vis:
         with open(starts_log, "a") as f:
             f.write("visible=" + ",".join(vis) + "\n")
+
+    def one(kind, o, n, deadline, ctl):
+        hosto = vis[int(o)] if vis and int(o) < len(vis) else o
+        if kind == "perf":
+            pmode = ctl.get("perf", {}).get(hosto, "ok")
+            if pmode == "hang":   # a check that never finishes (the daemon stops meanwhile)
+                time.sleep(3600)
+            return _perf_device(int(o), pmode, n, host_ordinal=int(hosto))
+        mode = ctl.get(hosto, "ok")
+        if mode == "server_fail":
+            mode = "fail"
+        if mode == "hang":
+            time.sleep(3600)
+        if mode == "slow":   # a verdict that takes "slow_s" seconds, then ok
+            time.sleep(float(ctl.get("slow_s", 1.0)))
+            mode = "ok"
+        if mode == "garbage":
+            print("segfault-ish noise", flush=True)
+            os._exit(139)
+        if mode == "timeout":   # server without kept queues: the dispatch did not complete
+            time.sleep(deadline)
+            d = _device(int(o), "fail", n, host_ordinal=int(hosto))
+            d.update(hip_error=-1, mismatches=0, error=f"dispatch did not complete within {deadline:.1f}s")
+            return d
+        if mode == "pending" and kind != "sweep":
+            # kept-queue server: the dispatch stays queued behind other work; the
+            # server waits out this device's whole deadline first, as
+            # hsa_probe.cpp's wait_and_verify does
+            with state_mu:
+                slots.setdefault(o, n)
+            if starts_log:   # a test can tell when a request is waiting on this device
+                with open(starts_log, "a") as f:
+                    f.write(f"pending:{hosto}\n")
+            time.sleep(deadline)
+            d = _device(int(o), "fail", n, host_ordinal=int(hosto))
+            d.update(hip_error=-1, mismatches=0, pending_s=max(deadline, 1e-3),
+                     error=f"dispatch pending for {deadline:.1f}s (not completed)")
+            return d
+        with state_mu:
+            late = slots.pop(o, None) if kind != "sweep" else None
+        if late is not None:   # the outstanding dispatch completed: its late verdict
+            d = _device(int(o), mode, late, host_ordinal=int(hosto))
+            d["late"] = 1
+            return d
+        return _device(int(o), "ok" if mode == "pending" else mode, n, host_ordinal=int(hosto))
+
+    def answer(rid, kind, devs_in):
+        ctl = _control()
+        res = [None] * len(devs_in)
+
+        def dev(i, o, n, dl):
+            with state_mu:
+                lk = locks.setdefault(o, threading.Lock())
+            if not lk.acquire(timeout=dl):   # another request holds this device's slot past our deadline
+                d = _device(int(o), "fail", n)
+                d.update(hip_error=-1, mismatches=0, pending_s=dl, error="another request on this device's queue")
+                res[i] = d
+                return
+            try:
+                res[i] = one(kind, o, n, dl, ctl)
+            finally:
+                lk.release()
+        ths = [threading.Thread(target=dev, args=(i, *x), daemon=True) for i, x in enumerate(devs_in)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        doc = {"ok": all(d["ok"] for d in res), "hip_device_count": 8, "sweep": kind == "sweep",
+               "t_ready_ns": time.monotonic_ns(), "devices": res}
+        if rid is not None:
+            doc = {"id": rid, **doc}
+        with out_mu:
+            sys.stdout.write(json.dumps(doc) + "\n")
+            sys.stdout.flush()
+
     for line in sys.stdin:
         parts = line.split()
         if not parts or parts[0] == "quit":
             break
-        kind = parts[0]
-        ctl = _control()
-        devs = []
-        for tok in parts[4:] if kind == "perf" else parts[3:]:
-            o, n = tok.split(":")
-            hosto = vis[int(o)] if vis and int(o) < len(vis) else o
-            if kind == "perf":
-                pmode = ctl.get("perf", {}).get(hosto, "ok")
-                if pmode == "hang":   # a check that never finishes (the daemon stops meanwhile)
-                    time.sleep(3600)
-                devs.append(_perf_device(int(o), pmode, int(n, 0), host_ordinal=int(hosto)))
-                continue
-            mode = ctl.get(hosto, "ok")
-            if mode == "server_fail":
-                mode = "fail"
-            if mode == "hang":
-                time.sleep(3600)
-            if mode == "slow":   # a verdict that takes "slow_s" seconds, then ok
-                time.sleep(float(ctl.get("slow_s", 1.0)))
-                mode = "ok"
-            if mode == "garbage":
-                print("segfault-ish noise", flush=True)
-                return 139
-            if mode == "timeout":   # server without kept queues: the dispatch did not complete
-                d = _device(int(o), "fail", int(n, 0), host_ordinal=int(hosto))
-                d.update(hip_error=-1, mismatches=0, error="dispatch did not complete within 1.0s")
-                devs.append(d)
-                continue
-            if mode == "pending" and kind != "sweep":   # kept-queue server: dispatch still queued behind other work
-                slots.setdefault(o, int(n, 0))
-                d = _device(int(o), "fail", int(n, 0), host_ordinal=int(hosto))
-                d.update(hip_error=-1, mismatches=0, pending_s=1.0, error="dispatch pending for 1.0s (not completed)")
-                devs.append(d)
-                continue
-            if kind != "sweep" and o in slots:   # the outstanding dispatch completed: its late verdict
-                d = _device(int(o), mode, slots.pop(o), host_ordinal=int(hosto))
-                d["late"] = 1
-                devs.append(d)
-                continue
-            devs.append(_device(int(o), "ok" if mode == "pending" else mode, int(n, 0), host_ordinal=int(hosto)))
-        print(json.dumps({"ok": all(d["ok"] for d in devs), "hip_device_count": 8, "sweep": kind == "sweep",
-                          "t_ready_ns": time.monotonic_ns(), "devices": devs}), flush=True)
+        rid, kind, _, devs = _parse(line)
+        if rid is None:
+            answer(rid, kind, devs)
+        else:
+            threading.Thread(target=answer, args=(rid, kind, devs), daemon=True).start()
     return 0
 
 
@@ -176,8 +237,12 @@ def main(argv):
         d = _perf_device(0, _control().get("perf", {}).get(ordinal, "ok"), nonce, host_ordinal=int(ordinal))
         print(json.dumps({"ok": d["ok"], "perf": True, "hip_device_count": 1, "devices": [d]}))
         return 0 if d["ok"] else 1
-    mode = _control().get(ordinal, "ok")
+    ctl = _control()
+    mode = ctl.get(ordinal, "ok")
     if mode == "server_fail":
+        mode = "ok"
+    if mode == "slow":
+        time.sleep(float(ctl.get("slow_s", 1.0)))
         mode = "ok"
     if mode in ("pending", "timeout"):   # a fresh process waits too, then gives up
         mode = "fail"

@@ -11,6 +11,23 @@ if str(REPO) not in sys.path:
 
 REF_TESTDATA = Path("/root/reference/testdata")
 
+# Hypothesis: the suite's verdict must not depend on the draw. "ci" (the
+# default) derandomizes and ignores the local example database, so every run
+# of the suite tries the same examples; "explore" (HYPOTHESIS_PROFILE=explore)
+# draws fresh ones, many more of them (tools/yaml_differential.py records such
+# a run). A failure found while exploring goes into the parametrised cases.
+try:
+    from hypothesis import HealthCheck, settings as _hyp_settings
+
+    _hyp_settings.register_profile("ci", derandomize=True, database=None, max_examples=300, deadline=None,
+                                   print_blob=True, suppress_health_check=[HealthCheck.too_slow])
+    _hyp_settings.register_profile("explore", derandomize=False, max_examples=int(os.environ.get(
+        "MI355X_HYPOTHESIS_EXAMPLES", "10000")), deadline=None, print_blob=True,
+        suppress_health_check=[HealthCheck.too_slow])
+    _hyp_settings.load_profile(os.environ.get("HYPOTHESIS_PROFILE", "ci"))
+except ImportError:  # hypothesis is optional for the non-property tests
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")

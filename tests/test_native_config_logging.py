@@ -135,8 +135,9 @@ def test_stderrthreshold_names_numbers_and_backtrace_at(tmp_path):
     with open(src) as f:
         line = next(i + 1 for i, s in enumerate(f) if '"Found %zu AMDGPUs"' in s)
     base = [DP, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-exporter_socket="]
+    # a number is a logsink.Severity (int8): 256 wraps to INFO, 259 to FATAL (glog_flags.go:341-356)
     for thr, info_on_stderr in (("warning", False), ("0", True), ("INFO", True), ("Error", False), ("2", False),
-                                ("-1", True), ("7", False)):
+                                ("+1", False), ("256", True), ("259", False)):
         logs = tmp_path / f"logs-{thr}"
         p = subprocess.run(base + ["-logtostderr=false", f"-log_dir={logs}", f"-stderrthreshold={thr}"],
                            capture_output=True, text=True, timeout=30)
@@ -145,6 +146,15 @@ def test_stderrthreshold_names_numbers_and_backtrace_at(tmp_path):
         assert "Found 8 AMDGPUs" in (logs / "k8s-device-plugin.INFO").read_text()
     bad = subprocess.run(base + ["-stderrthreshold=loud"], capture_output=True, text=True, timeout=30)
     assert bad.returncode == 2 and 'invalid value "loud" for flag -stderrthreshold' in bad.stderr
+    # numbers outside INFO..FATAL are refused, as golang/glog refuses them
+    for thr in ("-1", "7", "4", "255"):
+        bad = subprocess.run(base + [f"-stderrthreshold={thr}"], capture_output=True, text=True, timeout=30)
+        assert bad.returncode == 2 and f"Severity {thr} out of range (min 0, max 3)." in bad.stderr, (thr, bad.stderr)
+    # -v is strconv.Atoi (64-bit) stored as an int32: 2^32+2 is level 2
+    p = subprocess.run(base + ["-v", str(2 ** 32 + 2)], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 0, p.stderr
+    p = subprocess.run(base + ["-v", str(2 ** 63)], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 2 and "for flag -v" in p.stderr
     # the stack follows exactly the record logged at resources.cpp:<line>, nowhere else
     p = subprocess.run(base + [f"-log_backtrace_at=resources.cpp:{line}"], capture_output=True, text=True,
                        timeout=30)

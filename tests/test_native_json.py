@@ -28,7 +28,7 @@ def roundtrip(text):
     return out
 
 
-@settings(max_examples=400, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(deadline=None, suppress_health_check=[HealthCheck.too_slow])  # examples: the profile (conftest.py)
 @given(v=_VALUE, indent=st.sampled_from([None, 0, 2]), ascii_=st.booleans())
 def test_roundtrip_equals_python(v, indent, ascii_):
     text = json.dumps(v, indent=indent, ensure_ascii=ascii_)
