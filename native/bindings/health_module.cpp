@@ -72,8 +72,17 @@ class PyHealthEngine {
     if (auto v = get("argv_prefix"); !v.is_none()) c.prober.argv_prefix = v.cast<std::vector<std::string>>();
     if (auto v = get("extra_env"); !v.is_none())
       for (auto& [k, val] : v.cast<std::map<std::string, std::string>>()) c.prober.extra_env.emplace_back(k, val);
+    if (auto v = get("kfd_exclude"); !v.is_none())
+      for (const auto& pid : v.cast<std::vector<std::string>>()) c.kfd_exclude.insert(pid);
     const KfdTopology topo = KfdTopology::load_sysfs(sysfs_root);
     DiscoveryResult res = discover_gpus(sysfs_root, topo);
+    if (auto v = get("device_ids"); !v.is_none()) {  // judge only these (as the daemon's -device_ids)
+      const auto keep = v.cast<std::set<std::string>>();
+      std::vector<GpuDevice> sel;
+      for (auto& d : res.devices)
+        if (keep.count(d.id)) sel.push_back(std::move(d));
+      res.devices = std::move(sel);
+    }
     eng_ = std::make_unique<health::Engine>(std::move(res.devices), topo, c);
   }
 
@@ -105,7 +114,10 @@ class PyHealthEngine {
       d["check_fresh"] = p->check_fresh.load();
       d["check_inconclusive"] = p->check_inconclusive.load();
       d["server_running"] = p->server_running();
+      d["server_pid"] = p->server_pid();
     }
+    d["xgmi_readings"] = eng_->xgmi_readings();
+    d["xgmi_error"] = eng_->xgmi_error();
     return d;
   }
   std::vector<std::pair<std::string, std::string>> degraded_links() const { return eng_->degraded_links(); }
@@ -130,6 +142,13 @@ class PyHealthEngine {
     else eng_->exporter_source = [h] { return *h; };
   }
   std::map<std::string, int> ordinals() { return eng_->ordinals(); }
+  // kfd gpu_id -> (other processes with queues, their queues) as the last sweep saw it
+  std::map<int64_t, std::pair<int, int>> gpu_load() const { return eng_->gpu_load(); }
+  // the running probe server's kfd proc entries covering these kfd gpu ids
+  std::set<std::string> own_kfd_entries(const std::set<int64_t>& gpu_ids) {
+    auto* p = eng_->prober();
+    return p ? p->own_kfd_entries(gpu_ids) : std::set<std::string>{};
+  }
   // PreStartContainer's check (Engine::probe_now): device id -> outcome dict
   py::dict check(const std::vector<std::string>& ids, double budget_s) {
     std::map<std::string, health::ProbeOutcome> res;
@@ -168,6 +187,8 @@ void bind_health(py::module_& m) {
       .def("snapshot", &PyHealthEngine::snapshot, "device id -> (healthy, reasons)")
       .def("stats", &PyHealthEngine::stats)
       .def("ordinals", &PyHealthEngine::ordinals)
+      .def("gpu_load", &PyHealthEngine::gpu_load)
+      .def("own_kfd_entries", &PyHealthEngine::own_kfd_entries, py::arg("gpu_ids"))
       .def("check", &PyHealthEngine::check, py::arg("ids"), py::arg("budget_s") = 5.0,
            "PreStartContainer's check of these devices now (beside any sweep)")
       .def("set_activity", &PyHealthEngine::set_activity, py::arg("activity"),

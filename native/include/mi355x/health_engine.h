@@ -127,6 +127,7 @@ class LivenessProber {
   void set_visible(std::optional<std::vector<int>> ordinals);
   void close();
   bool server_running() const;
+  int server_pid() const;  // -1 when none is running
   // the running server's kfd proc entry names (empty while ambiguous / unknown)
   std::set<std::string> own_kfd_entries(const std::set<int64_t>& gpu_ids);
   // a readable fd ends every wait at once (shutdown)
@@ -193,6 +194,9 @@ struct Config {
   double perf_min_xcd_clock_ratio = 0.6;
   bool smi_xgmi = false;
   std::string xgmi_file;  // JSON snapshot (smi_xgmi_links' shape) read instead of amd-smi: fault injection
+  // kfd proc entries (PIDs) never counted as tenants, besides the probe
+  // server's own: e.g. a process embedding the engine that holds GPU queues itself
+  std::set<std::string> kfd_exclude;
 };
 
 struct Verdict {
@@ -248,6 +252,8 @@ class Engine {
   // why a correct throughput reply counts as degraded ([] if it does not)
   std::vector<std::string> perf_problems(const ProbeOutcome& o) const;
   bool busy_state_known() const { return busy_known_; }
+  // kfd gpu_id -> (other processes with queues, their queues) as the last sweep saw it
+  std::map<int64_t, std::pair<int, int>> gpu_load() const { return load_; }
   double last_sweep_ms() const { return last_sweep_ms_; }
 
  private:
@@ -261,8 +267,8 @@ class Engine {
   using Reasons = std::map<std::string, std::vector<std::string>>;  // device -> why it is Unhealthy
   // the phases of sweep()
   void liveness_pass(Reasons* reasons);
-  void ecc_pass(Reasons* reasons);
-  void events_pass(Reasons* reasons);
+  bool ecc_pass(Reasons* reasons);     // false: no amd-smi snapshot this sweep
+  bool events_pass(Reasons* reasons);  // false: no event subscription
   bool publish(Reasons reasons);
   // liveness_pass's steps
   std::map<std::string, int> judged_ordinals(const Reasons& reasons);
@@ -285,7 +291,7 @@ class Engine {
                                                       const std::map<std::string, ProbeOutcome>& outcomes);
   bool identity_matches(const GpuDevice& d, const ProbeOutcome& o) const;
   const GpuDevice* dev(const std::string& id) const;
-  void fabric_check();
+  bool fabric_check();  // false: no xGMI link reading this sweep
   void perf_check(const std::map<std::string, int>& ords);
   SmiXgmiSnapshot read_xgmi();
 

@@ -207,7 +207,7 @@ bool Engine::kfd_load(const std::set<std::string>& exclude, std::map<int64_t, st
   if (::access(root.c_str(), R_OK | X_OK) != 0) return false;
   std::map<int64_t, std::pair<int, int>> load;
   for (const auto& pid : list_dir(root)) {
-    if (exclude.count(pid)) continue;
+    if (exclude.count(pid) || cfg_.kfd_exclude.count(pid)) continue;
     const std::string qdir = path_join(path_join(root, pid), "queues");
     if (!is_dir(qdir)) continue;  // exited meanwhile
     if (::access(qdir.c_str(), R_OK | X_OK) != 0) return false;
@@ -507,10 +507,10 @@ void Engine::liveness_pass(Reasons* reasons) {
 }
 
 // amd-smi: a rise of a device's uncorrectable ECC count since the last sweep
-void Engine::ecc_pass(Reasons* reasons) {
+bool Engine::ecc_pass(Reasons* reasons) {
   if (!smi_held_) smi_held_ = smi_hold();
   const SmiSnapshot snap = smi_snapshot();
-  if (!snap.ok) return;
+  if (!snap.ok) return false;
   std::map<std::string, const SmiGpu*> by_bdf;
   for (const auto& g : snap.gpus)
     if (g.ecc_ok) by_bdf[g.bdf] = &g;
@@ -524,11 +524,12 @@ void Engine::ecc_pass(Reasons* reasons) {
                                  std::to_string(cur));
     ecc_[d.id] = cur;
   }
+  return true;
 }
 
 // amd-smi events: counted and logged; a GPU between gpu_pre_reset and
 // gpu_post_reset is Unhealthy
-void Engine::events_pass(Reasons* reasons) {
+bool Engine::events_pass(Reasons* reasons) {
   if (!events_started_) {
     events_started_ = true;
     events_ = std::make_unique<SmiEventWatcher>();
@@ -555,6 +556,7 @@ void Engine::events_pass(Reasons* reasons) {
   for (const auto& d : devices_)
     if (resetting_.count(d.bdf))
       (*reasons)[d.id].push_back("GPU reset in progress (amd-smi gpu_pre_reset, no post_reset yet)");
+  return events_ && events_->running();
 }
 
 // reasons -> the published snapshot; true when any device's health changed
@@ -625,14 +627,24 @@ std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::str
 }
 
 // One sweep: every source adds its reasons; a device with none is Healthy.
+// one reading of a health source: /metrics shows which sources run and answer
+static void source_reading(const char* source, bool ok) {
+  metrics::global().inc("mi355x_dp_health_source_readings_total", {{"source", source}, {"result", ok ? "ok" : "error"}},
+                        1.0, "readings of each health source per sweep: ok, or error (source unavailable)");
+}
+
 bool Engine::sweep() {
   trace::Span span("health.sweep", "health", {{"devices", std::to_string(devices_.size())}});
   const double t0 = mono_s();
   Reasons reasons;
   for (const auto& d : devices_) reasons[d.id];
-  for (const auto& [id, r] : kfd_verdicts()) reasons[id].push_back(r);
+  const auto kv = kfd_verdicts();
+  source_reading("kfd", !(kv.size() == devices_.size() && !devices_.empty() &&
+                          kv.begin()->second == "kfd topology unavailable"));
+  for (const auto& [id, r] : kv) reasons[id].push_back(r);
   if (!cfg_.exporter_socket.empty() || exporter_source) {
     const auto hmap = exporter_health();
+    source_reading("exporter", !hmap.empty());
     for (const auto& d : devices_)
       if (auto it = hmap.find(d.bdf); it != hmap.end() && !it->second)
         reasons[d.id].push_back("exporter reports " + d.bdf + " unhealthy");
@@ -641,11 +653,16 @@ bool Engine::sweep() {
     // probe_now() runs beside this pass: it reads the ordinal map and the crowd
     // state under state_mu_ and sends its own tagged request to the probe server
     std::lock_guard<std::mutex> op(op_mu_);
+    const uint64_t fb = static_cast<uint64_t>(prober_->fallbacks.load());
     liveness_pass(&reasons);
+    source_reading("liveness", static_cast<uint64_t>(prober_->fallbacks.load()) == fb);
   }
-  if (cfg_.smi_ecc && smi_available()) ecc_pass(&reasons);
-  if (cfg_.smi_events) events_pass(&reasons);
-  if (cfg_.smi_xgmi) fabric_check();
+  if (cfg_.smi_ecc) {
+    const bool ok = smi_available() && ecc_pass(&reasons);
+    source_reading("smi_ecc", ok);
+  }
+  if (cfg_.smi_events) source_reading("smi_events", events_pass(&reasons));
+  if (cfg_.smi_xgmi) source_reading("smi_xgmi", fabric_check());
   const bool changed = publish(std::move(reasons));
   sweeps_++;
   last_sweep_ms_ = (mono_s() - t0) * 1e3;
@@ -713,12 +730,12 @@ SmiXgmiSnapshot Engine::read_xgmi() {
   return smi_xgmi_links();
 }
 
-void Engine::fabric_check() {
+bool Engine::fabric_check() {
   const SmiXgmiSnapshot snap = read_xgmi();
   if (!snap.ok) {
     if (snap.error != xgmi_error_) MI_LOG(kWarning, "xGMI link state unavailable: %s", snap.error.c_str());
     xgmi_error_ = snap.error;
-    return;
+    return false;
   }
   xgmi_error_.clear();
   xgmi_readings_++;
@@ -767,7 +784,7 @@ void Engine::fabric_check() {
   for (const auto& [b, n] : down) total += n;
   std::lock_guard<std::mutex> lk(mu_);
   links_down_ = down;
-  if (degraded == degraded_) return;
+  if (degraded == degraded_) return true;
   for (const auto& p : degraded)
     if (!degraded_.count(p))
       MI_LOG(kWarning, "xGMI link between GPUs %s and %s is down: multi-GPU placement avoids the pair",
@@ -778,6 +795,7 @@ void Engine::fabric_check() {
   degraded_ = std::move(degraded);
   fabric_version_++;
   metrics::global().set("mi355x_dp_xgmi_links_down", total, {}, "xGMI links down vs the first reading");
+  return true;
 }
 
 std::vector<std::pair<std::string, std::string>> Engine::degraded_links() const {

@@ -547,6 +547,9 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
       out->hip_error = -1;
       return finish();
     }
+    // the deadline counts from the request, the wait for the slot included
+    const double left_s =
+        std::max(1e-3, (timeout_s > 0 ? timeout_s : 5.0) - std::chrono::duration<double>(clk::now() - t0).count());
     if (!slot->ready) {
       if (!setup_resources(ag, slot->r, slot->k, out)) {
         slot->r.release();
@@ -571,7 +574,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
     if (slot->pending) {
       // the previous probe's dispatch is still outstanding: wait for it (it
       // carries its own nonce), never stack a second one behind it
-      if (!wait_and_verify(ag, slot->r, slot->pending_nonce, slot->pending_iters, timeout_s, out)) {
+      if (!wait_and_verify(ag, slot->r, slot->pending_nonce, slot->pending_iters, left_s, out)) {
         const double s_out = std::max(1e-3, std::chrono::duration<double>(clk::now() - slot->pending_since).count());
         std::snprintf(out->error, sizeof(out->error), "dispatch pending for %.1fs (not completed)", s_out);
         out->pending_s = s_out;
@@ -581,7 +584,7 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
       out->late = 1;  // verdict of the dispatch submitted by an earlier probe
     } else {
       submit_dispatch(slot->r, slot->k, nonce, out->iters, out);
-      if (!wait_and_verify(ag, slot->r, nonce, out->iters, timeout_s, out)) {
+      if (!wait_and_verify(ag, slot->r, nonce, out->iters, left_s, out)) {
         slot->pending = true;
         slot->pending_nonce = nonce;
         slot->pending_iters = out->iters;

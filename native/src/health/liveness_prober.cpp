@@ -324,6 +324,11 @@ bool LivenessProber::server_running() const {
   return server_ && server_->c.pid > 0 && !server_->dead;
 }
 
+int LivenessProber::server_pid() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return server_ && !server_->dead ? static_cast<int>(server_->c.pid) : -1;
+}
+
 double LivenessProber::inner_timeout() const { return cfg_.timeout_s - std::min(0.5, 0.25 * cfg_.timeout_s); }
 
 void LivenessProber::close() {
@@ -857,8 +862,9 @@ std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordina
     auto it = got.find(o);
     if (it != got.end() && it->second.ok) {
       out[o] = it->second;
-    } else if (busy.count(o)) {
-      // queued behind (or, without a server answer, would queue behind) another process' kernels
+    } else if (busy.count(o) && (it == got.end() || it->second.pending)) {
+      // queued behind (or, without a server answer, would queue behind) another process' kernels;
+      // a definite failure there (a wrong tile, an error) is confirmed like anywhere else
       inconclusive(o, it != got.end() ? it->second.reason : "no probe server answer on a busy GPU");
     } else {
       confirm.push_back(o);
@@ -882,8 +888,10 @@ std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordina
         restart_wanted_ = true;  // a stale server runtime: the next sweep restarts it
       }
     } else if (!f.interrupted) {
-      if (f.pending)  // a fresh process on a GPU no other process uses got nothing back either
-        f.pending = false;
+      // a fresh process that got nothing back: on a GPU no other process uses
+      // that is a fault; on a busy one it may wait behind the tenant's kernels
+      if (f.pending && !busy.count(o)) f.pending = false;
+      if (f.pending) check_inconclusive++;
       if (server_failed) f.reason += " (server: " + got[o].reason + ")";
     }
     out[o] = f;

@@ -166,12 +166,24 @@ void gen_product_name(Ctx& c, Labels* out) {
   create_labels("product-name", counts, out);
 }
 
+// A GPU whose kfd node this process may not read (a device cgroup denies it)
+// is still counted in vram / simd-count / cu-count from what discovery
+// recovered from PCI sysfs: its own mem_info_vram_total, and the SIMD shape of
+// a readable GPU of the same part and partition mode. The counts then agree
+// with device-id. The reference's labeller runs privileged and reads every
+// node (k8s-ds-amdgpu-labeller.yaml:66-67); unprivileged it would drop such
+// GPUs from these counts (cmd/k8s-node-labeller/main.go:237-277).
+bool recovered(const GpuDevice& g) { return g.identity == "sysfs"; }
+
 void gen_vram(Ctx& c, Labels* out) {
   std::map<std::string, int> counts;
   for (const auto& g : c.gpus) {
     const KfdNode* n = c.kfd_node(g);
-    if (!n || n->mem_banks.empty()) continue;
-    const uint64_t mib = n->mem_banks[0].size_in_bytes / (1024 * 1024);
+    uint64_t size = 0;
+    if (n && !n->mem_banks.empty()) size = n->mem_banks[0].size_in_bytes;
+    else if (!n && recovered(g) && g.vram_bytes > 0) size = g.vram_bytes;
+    else continue;
+    const uint64_t mib = size / (1024 * 1024);
     // Go math.Round: half away from zero
     counts[std::to_string(static_cast<long long>(std::floor(static_cast<double>(mib) / 1024.0 + 0.5))) + "G"]++;
   }
@@ -182,8 +194,8 @@ void gen_simd_count(Ctx& c, Labels* out) {
   std::map<std::string, int> counts;
   for (const auto& g : c.gpus) {
     const KfdNode* n = c.kfd_node(g);
-    if (!n || !n->props.count("simd_count")) continue;
-    counts[std::to_string(n->simd_count())]++;
+    if (n && n->props.count("simd_count")) counts[std::to_string(n->simd_count())]++;
+    else if (!n && recovered(g) && g.simd_count > 0) counts[std::to_string(g.simd_count)]++;
   }
   create_labels("simd-count", counts, out);
 }
@@ -192,8 +204,8 @@ void gen_cu_count(Ctx& c, Labels* out) {
   std::map<std::string, int> counts;
   for (const auto& g : c.gpus) {
     const KfdNode* n = c.kfd_node(g);
-    if (!n || n->simd_per_cu() == 0) continue;
-    counts[std::to_string(n->simd_count() / n->simd_per_cu())]++;
+    if (n && n->simd_per_cu() != 0) counts[std::to_string(n->simd_count() / n->simd_per_cu())]++;
+    else if (!n && recovered(g) && g.cu_count() > 0) counts[std::to_string(g.cu_count())]++;
   }
   create_labels("cu-count", counts, out);
 }

@@ -915,6 +915,26 @@ class Parser {
   std::vector<Line> lines_;
 };
 
+// A JSON document is also YAML 1.1, where a number with an exponent needs a
+// '.' and a signed exponent to resolve as a float (PyYAML's float resolver;
+// `1e3` and `1.5e3` are text there). Such numbers are kept as their text, as
+// a plain YAML scalar would be.
+bool yaml11_numeric(const std::string& t) {
+  const size_t e = t.find_first_of("eE");
+  if (e == std::string::npos) return true;
+  return t.find('.') != std::string::npos && e + 1 < t.size() && (t[e + 1] == '+' || t[e + 1] == '-');
+}
+
+void retype_json_numbers(json::Value* v) {
+  if (v->kind == json::Value::Number && !yaml11_numeric(v->s)) {
+    *v = json::Value::string(v->s);
+  } else if (v->kind == json::Value::Array) {
+    for (auto& x : v->arr) retype_json_numbers(&x);
+  } else if (v->kind == json::Value::Object) {
+    for (auto& kv : v->obj) retype_json_numbers(&kv.second);
+  }
+}
+
 }  // namespace
 
 std::optional<json::Value> parse(const std::string& text, std::string* error) {
@@ -923,7 +943,10 @@ std::optional<json::Value> parse(const std::string& text, std::string* error) {
   if (first != std::string::npos && (text[first] == '{' || text[first] == '[')) {
     // JSON (a JSON kubeconfig); else a YAML flow collection, whose error is
     // reported only when the text is not JSON either
-    if (auto v = json::parse(text, &err)) return v;
+    if (auto v = json::parse(text, &err)) {
+      retype_json_numbers(&*v);
+      return v;
+    }
     std::string yerr;
     Parser p(text, &yerr);
     if (auto v = p.document()) return v;

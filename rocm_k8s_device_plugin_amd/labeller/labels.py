@@ -9,6 +9,13 @@ value transformation and the removal sets are kept identical:
 * ``firmware`` labels are beta-only (main.go:132-155);
 * ``vram`` is round(size_in_bytes / MiB / 1024) + "G" from kfd mem_banks/0
   (main.go:236-272);
+* a GPU whose kfd node this process may not read (a device cgroup denies it)
+  is still counted in ``vram``, ``simd-count`` and ``cu-count`` from what
+  discovery recovered from PCI sysfs (its own mem_info_vram_total; the SIMD
+  shape of a readable GPU of the same part and partition mode), so those
+  counts agree with ``device-id``. The reference's labeller runs privileged
+  and reads every node (k8s-ds-amdgpu-labeller.yaml:66-67); unprivileged it
+  would drop such GPUs from these counts (main.go:237-277);
 * ``product-name`` replaces spaces by ``_`` and drops parentheses (main.go:213-233);
 * VF mode: gim driver versions, ``vf-passthrough`` mode on both prefixes and
   raw VF device ids; PF mode: only ``amd.com/gpu.mode=pf-passthrough`` and
@@ -256,16 +263,22 @@ def _product_name(ctx: LabelContext) -> Dict[str, str]:
     return create_labels("product-name", counts)
 
 
+def _recovered(g) -> bool:
+    """Identity recovered from PCI sysfs: kfd denied this GPU's node."""
+    return getattr(g, "identity", "") == "sysfs"
+
+
 def _vram(ctx: LabelContext) -> Dict[str, str]:
     counts: Dict[str, int] = {}
     for g in ctx.gpus:
         node = ctx.kfd_node(g)
-        if node is None:
+        if node is not None and node.mem_bank_sizes:
+            size = node.mem_bank_sizes[0]
+        elif node is None and _recovered(g) and g.vram_bytes > 0:
+            size = g.vram_bytes
+        else:
             continue
-        banks = node.mem_bank_sizes
-        if not banks:
-            continue
-        mib = banks[0] // (1024 * 1024)
+        mib = size // (1024 * 1024)
         # Go's math.Round: half away from zero
         s = int(math.floor(mib / 1024 + 0.5))
         k = f"{s}G"
@@ -277,9 +290,12 @@ def _simd_count(ctx: LabelContext) -> Dict[str, str]:
     counts: Dict[str, int] = {}
     for g in ctx.gpus:
         node = ctx.kfd_node(g)
-        if node is None or "simd_count" not in node.props:
+        if node is not None and "simd_count" in node.props:
+            k = str(node.simd_count)
+        elif node is None and _recovered(g) and g.simd_count > 0:
+            k = str(g.simd_count)
+        else:
             continue
-        k = str(node.simd_count)
         counts[k] = counts.get(k, 0) + 1
     return create_labels("simd-count", counts)
 
@@ -288,9 +304,12 @@ def _cu_count(ctx: LabelContext) -> Dict[str, str]:
     counts: Dict[str, int] = {}
     for g in ctx.gpus:
         node = ctx.kfd_node(g)
-        if node is None or node.simd_per_cu == 0:
+        if node is not None and node.simd_per_cu != 0:
+            k = str(node.simd_count // node.simd_per_cu)
+        elif node is None and _recovered(g) and g.simd_per_cu > 0 and g.simd_count > 0:
+            k = str(g.simd_count // g.simd_per_cu)
+        else:
             continue
-        k = str(node.simd_count // node.simd_per_cu)
         counts[k] = counts.get(k, 0) + 1
     return create_labels("cu-count", counts)
 

@@ -179,3 +179,49 @@ def test_partitions_for_mode_matches_models():
                 assert n.xcc_count_for_device_id(did) == m.xcds, m.name
             for mode in m.compute_partitions:
                 assert n.partitions_for_mode(mode, m.xcds) == m.partitions_per_gpu(mode)
+
+
+def test_labels_count_denied_gpus_like_device_id(tmp_path):
+    """The gpurun box's shape (7 of 8 kfd nodes EPERM): vram / cu-count /
+    simd-count count every GPU, like device-id and product-name, from what
+    discovery recovered from PCI sysfs; native labeller and Python oracle agree,
+    and the counts match the raw sysfs (8 pci:amdgpu functions, 1 readable kfd
+    GPU node). The reference labeller runs privileged and reads every node
+    (k8s-ds-amdgpu-labeller.yaml:66-67), so a privileged run gives these counts."""
+    import json
+    import subprocess
+    from rocm_k8s_device_plugin_amd.labeller import labels as L
+    from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+    fi = make_mi355x_node(tmp_path, xcp_layout="kernel", probe_order=PROBE_ORDER)
+    allowed = fi.bdfs[5]
+    deny_kfd_nodes(fi, [n for d, n in fi.node_ids.items() if d != allowed])
+    pci = [b for b in os.listdir(fi.sysfs / "module/amdgpu/drivers/pci:amdgpu") if b.count(":") == 2]
+    nodes = fi.sysfs / "class/kfd/kfd/topology/nodes"
+    readable = []
+    for n in os.listdir(nodes):
+        try:   # deny_kfd_nodes makes the read fail, as EPERM does on the box
+            props = (nodes / n / "properties").read_text()
+        except OSError:
+            continue
+        if "cpu_cores_count 0" in props and "simd_count" in props:
+            readable.append(n)
+    assert len(pci) == 8 and len(readable) == 1
+    kinds = ["device-id", "product-name", "vram", "cu-count", "simd-count"]
+    exe = os.path.join(str(PKG_DIR), "bin", "mi355x-node-labeller")
+    p = subprocess.run([exe, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev),
+                        *[f"-{k}" for k in kinds]], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    assert got == L.generate_labels({k: True for k in kinds}, "container", sysfs_root=str(fi.sysfs),
+                                    dev_root=str(fi.dev))
+    assert got["amd.com/gpu.device-id.75a3"] == str(len(pci))
+    assert got["amd.com/gpu.vram.288G"] == got["amd.com/gpu.cu-count.256"] == got["amd.com/gpu.simd-count.1024"] \
+        == str(len(pci))
+    # a GPU with nothing readable or recovered (no readable sibling of its part) stays uncounted
+    deny_kfd_nodes(fi, [fi.node_ids[allowed]])
+    p = subprocess.run([exe, "-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-cu-count",
+                        "-vram"], capture_output=True, text=True, timeout=60)
+    got = json.loads(p.stdout)
+    assert not any(k.startswith("amd.com/gpu.cu-count") for k in got), got
+    assert got["amd.com/gpu.vram.288G"] == "8"                   # each GPU's own mem_info_vram_total
+

@@ -420,6 +420,27 @@ def test_real_node_labels_equal_the_python_labeller():
     want = L.generate_labels({k: True for k in KINDS}, "")
     assert got == want
     assert got["amd.com/gpu.family"] == "AI" and got["amd.com/gpu.gfx-target"] == "gfx950"
+    # counts against the raw sysfs, not only the twin: every amdgpu PCI function is
+    # counted in device-id, and in vram / cu-count / simd-count too (kfd-denied
+    # GPUs from PCI sysfs); the readable kfd GPU nodes are a subset
+    pci = [b for b in os.listdir("/sys/module/amdgpu/drivers/pci:amdgpu") if b.count(":") == 2]
+    readable = []
+    for n in os.listdir("/sys/class/kfd/kfd/topology/nodes"):
+        try:
+            with open(f"/sys/class/kfd/kfd/topology/nodes/{n}/properties") as f:
+                props = dict(ln.split() for ln in f if len(ln.split()) == 2)
+        except OSError:
+            continue
+        if props.get("cpu_cores_count") == "0" and int(props.get("gfx_target_version", "0")) > 0:
+            readable.append(n)
+    spx = got.get("amd.com/gpu.compute-memory-partition", "").startswith("spx")
+    if spx:
+        dev_key = next(k for k in got if k.startswith("amd.com/gpu.device-id."))
+        assert int(got[dev_key]) == len(pci), (got[dev_key], pci)
+        for kind in ("vram", "cu-count", "simd-count"):
+            counts = [int(v) for k, v in got.items() if k.startswith(f"amd.com/gpu.{kind}.")]
+            assert sum(counts) == len(pci), (kind, counts, len(pci))
+    assert 1 <= len(readable) <= len(pci), (readable, pci)
     # the Python CLI's cost for the same pass, for the footprint comparison
     t1 = time.monotonic()
     py = subprocess.run([sys.executable, "-m", "rocm_k8s_device_plugin_amd.cli.node_labeller", "-dry_run",
@@ -428,7 +449,8 @@ def test_real_node_labels_equal_the_python_labeller():
     assert py.returncode == 0 and json.loads(py.stdout) == got
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/native_labeller_box.json", "w") as f:
-        json.dump({"labels": got, "native_dry_run_wall_ms": round(wall_ms, 1),
+        json.dump({"labels": got, "pci_amdgpu_functions": len(pci), "readable_kfd_gpu_nodes": len(readable),
+                   "native_dry_run_wall_ms": round(wall_ms, 1),
                    "python_cli_dry_run_wall_ms": round(py_ms, 1)}, f, indent=1)
 
 

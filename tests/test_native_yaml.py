@@ -53,6 +53,9 @@ def test_native_reader_equals_pyyaml(doc, flow, style, width, unicode):
     "gpu:\n  device_count: 4\n",
     # block scalars with chomping indicators, comments, blank lines, nested sequences
     "a: |+\n  keep\n\n\nb: >\n  folded\n  line\n\n  para\nc: |-\n  strip\n# comment\nd:\n- - x\n  - y\n- z\n",
+    # a JSON document read as YAML 1.1: an exponent needs a '.' and a sign to be a float (the
+    # explore profile's find, profiles/r6/yaml_differential_10k.json)
+    "[[0E0]]\n", "[1e3, 1.5e3]\n", "{\"a\": 0E0, \"b\": [1E2, 3.25e2]}\n",
     # quotes inside plain scalars are ordinary characters: keys `:'` / `:"`, `a'b`, a quote after a
     # flow indicator in block context (`:'` was read as an open quoted scalar)
     ":': ' #'\n", ":\": ' #'\n", ":': \" #\"\n", "a:': b # c\n", "a'b: c # d\n", "a: b'c # d\n",
@@ -150,6 +153,13 @@ def test_repeated_keys_and_surrogate_escapes(text, want):
     assert out is not None, err
     got = json.loads(out)
     assert {k: str(v) if isinstance(v, int) else v for k, v in got.items()} == want
+
+
+@pytest.mark.parametrize("text", ["[1e3, 1.5e3, 1.5e+3, -2.0E-1, 7, -0.5]\n", "{\"a\": 0E0, \"b\": [1E+2, 3.25e-2]}\n"])
+def test_json_numbers_resolve_as_yaml11(text):
+    """A JSON document's numbers as PyYAML's YAML 1.1 resolvers read them: floats
+    need a '.' and a signed exponent, the rest stays text."""
+    assert native(text) == yaml.safe_load(text)
 
 
 def test_anchor_redefinition_rebinds():

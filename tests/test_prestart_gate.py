@@ -109,6 +109,25 @@ def test_check_beside_a_sweep_waiting_on_another_gpu(tmp_path):
         eng.close()
 
 
+def test_definite_failure_on_a_busy_gpu_still_fails_the_check(tmp_path):
+    """Only a pending dispatch on a busy GPU is inconclusive: a wrong tile there
+    is confirmed by a fresh process and fails the check like anywhere else
+    (the GPU test suite's own process keeps queues on the GPU it probes)."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    ctl, eng = _engine(fi, tmp_path, {})
+    dev = {o: d for d, o in eng.ordinals().items()}
+    try:
+        eng.sweep()
+        _busy_gpu(fi, inv, dev[4])
+        ctl.write_text(json.dumps({"4": "fail"}))
+        r = eng.check([dev[4]], 5.0)[dev[4]]
+        assert not r["ok"] and not r["pending"] and "differ" in r["reason"], r
+        assert eng.stats()["check_fresh"] == 1
+    finally:
+        eng.close()
+
+
 def test_sweep_gives_busy_gpus_the_short_deadline(tmp_path):
     """Sweep side: a pending dispatch on a busy GPU costs the sweep the busy
     deadline (0.3 s here), not the 5 s probe deadline; the verdict is

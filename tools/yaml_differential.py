@@ -40,9 +40,17 @@ def main() -> int:
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True)
     took = time.monotonic() - t0
     out = p.stdout + p.stderr
-    passing = re.findall(r"(\d+) passing examples", out)
+    # per property: "- N passing, M failing, and K invalid test cases" (--hypothesis-show-statistics)
+    stats, name = {}, None
+    for ln in out.splitlines():
+        m = re.match(r"^(tests/\S+::\S+):$", ln.strip())
+        if m:
+            name = m.group(1)
+        cnt = re.search(r"(\d+) passing, (\d+) failing", ln)
+        if cnt and name:
+            stats[name] = {"passing": int(cnt.group(1)), "failing": int(cnt.group(2))}
     res = {"examples_per_property": a.examples, "seed": seed, "returncode": p.returncode, "seconds": round(took, 1),
-           "passing_examples_reported": [int(x) for x in passing], "summary": out.strip().splitlines()[-1:],
+           "generate_phase": stats, "summary": out.strip().splitlines()[-1:],
            "command": " ".join(cmd[2:])}
     if p.returncode != 0:
         res["failure_tail"] = out[-4000:]
