@@ -77,7 +77,8 @@ class PyHealthEngine {
     const KfdTopology topo = KfdTopology::load_sysfs(sysfs_root);
     DiscoveryResult res = discover_gpus(sysfs_root, topo);
     if (auto v = get("device_ids"); !v.is_none()) {  // judge only these (as the daemon's -device_ids)
-      const auto keep = v.cast<std::set<std::string>>();
+      const auto ids = v.cast<std::vector<std::string>>();
+      const std::set<std::string> keep(ids.begin(), ids.end());
       std::vector<GpuDevice> sel;
       for (auto& d : res.devices)
         if (keep.count(d.id)) sel.push_back(std::move(d));

@@ -16,7 +16,11 @@
 
 namespace mi355x::versions {
 
-std::string git_describe();                     // "dev" when the build was not stamped
+// the build's describe, or a newer one from <bin>/../VERSION when that file
+// names this build's own source digest (_build.py keeps it current); "dev"
+// when the build was not stamped
+std::string git_describe();
+std::string source_digest();                    // first 12 hex of the native sources' content hash, or ""
 std::string rocm(const std::string& rocm_path = "");  // <ROCM_PATH or /opt/rocm>/.info/version
 std::string amdgpu(const std::string& sysfs_root);    // module version, "in-tree", or ""
 std::string libdrm_amdgpu();                    // path of the libdrm_amdgpu the process would load, or ""
@@ -25,7 +29,7 @@ std::string amd_smi();                          // amdsmi_get_lib_version(), or 
 // "rocm: 7.2.0, amdgpu: in-tree, libdrm_amdgpu: /usr/lib/..., amd-smi: 26.2.1, numa_source: sysfs"
 std::string library_line(const std::string& sysfs_root);
 
-// The banner: `title`, "<argv0> version <describe>", the library line.
+// The banner: `title`, "<argv0> version <describe> (native sources <digest>)", the library line.
 std::vector<std::string> banner(const std::string& title, const std::string& argv0, const std::string& sysfs_root);
 
 }  // namespace mi355x::versions

@@ -423,14 +423,9 @@ bool wait_and_verify(const Agent& ag, ProbeResources& r, uint32_t nonce, int ite
                      mi355x_probe_result* out) {
   using clk = std::chrono::steady_clock;
   const auto t_wait = clk::now();
-  const auto deadline = t_wait + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
-  hsa_signal_value_t v = 1;
-  while ((v = H().hsa_signal_wait_scacquire(r.sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
-                                        HSA_WAIT_STATE_BLOCKED)) >= 1) {
-    if (clk::now() > deadline) break;
-  }
+  const bool done = wait_signal(r.sig, timeout_s);
   out->phase_us[3] = std::chrono::duration<double, std::micro>(clk::now() - t_wait).count();
-  if (v >= 1) {
+  if (!done) {
     std::snprintf(out->error, sizeof(out->error), "dispatch did not complete within %.1fs", timeout_s);
     out->hip_error = -1;
     return false;
@@ -618,15 +613,20 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
 
 namespace mi355x::hsa_rt {
 
-// Bounded wait for a DMA completion signal (value 1 -> 0).
+// Bounded wait for a completion signal (value 1 -> 0): true when it completed.
+// Each blocking wait is capped at 20 ms and at what is left of the deadline,
+// in the system timestamp's unit (hsa_signal_wait's timeout_hint; 100 MHz on
+// MI355X, so a fixed 20e6 hint meant up to 200 ms past a 50 ms deadline).
 bool wait_signal(hsa_signal_t sig, double timeout_s) {
   using clk = std::chrono::steady_clock;
   const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
-  while (H().hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 20 * 1000 * 1000ull,
-                                       HSA_WAIT_STATE_BLOCKED) >= 1) {
-    if (clk::now() > deadline) return false;
+  const double ticks_per_s = g_rt.ts_freq ? static_cast<double>(g_rt.ts_freq) : 1e9;
+  while (true) {
+    const double left = std::chrono::duration<double>(deadline - clk::now()).count();
+    if (left <= 0) return H().hsa_signal_load_scacquire(sig) < 1;
+    const uint64_t hint = static_cast<uint64_t>(std::max(1.0, std::min(0.02, left) * ticks_per_s));
+    if (H().hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_BLOCKED) < 1) return true;
   }
-  return true;
 }
 
 void bus_id(const Agent& ag, char* out, size_t n) {

@@ -3,6 +3,7 @@
 #include <dlfcn.h>
 #include <link.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -12,6 +13,9 @@
 
 #ifndef MI355X_GIT_DESCRIBE
 #define MI355X_GIT_DESCRIBE "dev"
+#endif
+#ifndef MI355X_SOURCE_DIGEST
+#define MI355X_SOURCE_DIGEST ""
 #endif
 
 namespace mi355x::versions {
@@ -45,7 +49,37 @@ struct SmiVersion {
 
 }  // namespace
 
-std::string git_describe() { return MI355X_GIT_DESCRIBE; }
+std::string source_digest() { return MI355X_SOURCE_DIGEST; }
+
+// <dir of this executable>/../VERSION: "describe=<x>" and "digest=<y>" lines
+// that _build.py rewrites whenever HEAD's describe changes while the native
+// sources (and so these binaries) stay the same. Used only when its digest is
+// this build's own: a commit then names itself without relinking anything.
+std::string stamped_describe() {
+  const std::string own = source_digest();
+  if (own.empty()) return "";
+  char buf[4096];
+  const ssize_t n = ::readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+  if (n <= 0) return "";
+  buf[n] = 0;
+  std::string dir = buf;
+  dir = dir.substr(0, dir.rfind('/'));
+  std::ifstream f(dir.substr(0, dir.rfind('/')) + "/VERSION");
+  std::string line, describe, digest;
+  while (std::getline(f, line)) {
+    if (line.rfind("describe=", 0) == 0) describe = line.substr(9);
+    if (line.rfind("digest=", 0) == 0) digest = line.substr(7);
+  }
+  return digest == own ? describe : "";
+}
+
+std::string git_describe() {
+  static const std::string d = [] {
+    const std::string s = stamped_describe();
+    return s.empty() ? std::string(MI355X_GIT_DESCRIBE) : s;
+  }();
+  return d;
+}
 
 std::string rocm(const std::string& path) { return read_trimmed((path.empty() ? rocm_path() : path) + "/.info/version"); }
 
@@ -94,7 +128,9 @@ std::string library_line(const std::string& sysfs_root) {
 }
 
 std::vector<std::string> banner(const std::string& title, const std::string& argv0, const std::string& sysfs_root) {
-  return {title, argv0 + " version " + git_describe(), library_line(sysfs_root)};
+  const std::string dg = source_digest();
+  return {title, argv0 + " version " + git_describe() + (dg.empty() ? "" : " (native sources " + dg + ")"),
+          library_line(sysfs_root)};
 }
 
 }  // namespace mi355x::versions

@@ -60,15 +60,44 @@ def _source_digest() -> str:
     return h.hexdigest()
 
 
-def _up_to_date(targets) -> bool:
+def _up_to_date(targets, hip: bool = False) -> bool:
     # Compare the sources' content hash with the one recorded after the last
     # successful build, not mtimes: a copy of the tree (the gpurun snapshot, a
     # container image layer) changes mtimes without changing what was built.
+    # A host-only build (hip=False) stamps the same digest without building the
+    # GPU targets: it does not count as up to date for a HIP build.
     if not all(t.exists() for t in targets):
         return False
     if not STAMP.exists():
         return False
-    return f"digest={_source_digest()}" in STAMP.read_text().split()
+    words = STAMP.read_text().split()
+    if hip and "hip=True" not in words:
+        return False
+    return f"digest={_source_digest()}" in words
+
+
+VERSION_FILE = PKG_DIR / "VERSION"
+
+
+def stamp_version(digest: str | None = None) -> None:
+    """<package>/VERSION: this tree's `git describe` next to the native
+    sources' digest. The binaries' banner reads it when the digest is their
+    own (native/src/util/versions.cpp), so a commit that changes no native
+    source still names itself, without relinking binaries a running suite may
+    be executing. Rewritten only when its content changes."""
+    digest = (digest or _source_digest())[:12]
+    describe = git_describe()
+    if not describe:
+        return
+    text = f"describe={describe}\ndigest={digest}\n"
+    try:
+        if VERSION_FILE.exists() and VERSION_FILE.read_text() == text:
+            return
+        tmp = VERSION_FILE.with_suffix(".tmp")
+        tmp.write_text(text)
+        tmp.replace(VERSION_FILE)
+    except OSError:
+        pass
 
 
 def git_describe() -> str:
@@ -127,6 +156,8 @@ def _build_tree(bdir: Path, hip: bool, sanitize: str, coverage: bool, build_dir,
     describe = git_describe()
     if describe:
         cfg.append(f"-DMI355X_GIT_DESCRIBE={describe}")
+    digest12 = _source_digest()[:12]
+    cfg.append(f"-DMI355X_SOURCE_DIGEST={digest12}")
     if variant:
         # sanitizer / coverage builds keep the package outputs untouched
         cfg.append(f"-DMI355X_PKG_DIR={bdir / 'pkg'}")
@@ -143,7 +174,9 @@ def _build_tree(bdir: Path, hip: bool, sanitize: str, coverage: bool, build_dir,
         restamp = bool(describe) and f"MI355X_GIT_DESCRIBE:STRING={describe}\n" not in cache and (
             bool(os.environ.get("GIT_DESCRIBE")) or not STAMP.exists()
             or f"digest={_source_digest()}" not in STAMP.read_text().split())
-        if want not in cache or restamp:
+        # the digest changes only with the sources, when the binaries are rebuilt anyway
+        stale_digest = f"MI355X_SOURCE_DIGEST:STRING={digest12}\n" not in cache
+        if want not in cache or restamp or stale_digest:
             subprocess.run(cfg, check=True, stdout=out)
     j = jobs or min(8, os.cpu_count() or 4)
     res = subprocess.run(["cmake", "--build", str(bdir), "-j", str(j)], stdout=subprocess.PIPE,
@@ -154,6 +187,7 @@ def _build_tree(bdir: Path, hip: bool, sanitize: str, coverage: bool, build_dir,
     if not variant and build_dir is None:
         STAMP.parent.mkdir(parents=True, exist_ok=True)
         STAMP.write_text(f"hip={hip}\ndigest={_source_digest()}\n")
+        stamp_version()
     if not quiet:
         sys.stdout.write(res.stdout)
 
@@ -171,12 +205,12 @@ def ensure_built(hip: bool | None = None) -> None:
     if hip in _checked:
         return
     targets = [NATIVE_SO] + ([HIP_SO, PROBE_EXE, PROBE_EXE_HIP, MOUNTEMU_EXE, HIP_DEVEMU_EXE, HSACO] if hip else [])
-    if not _up_to_date(targets):
+    if not _up_to_date(targets, hip):
         BUILD_DIR.mkdir(parents=True, exist_ok=True)
         with open(BUILD_DIR.parent / ".build.lock", "w") as lk:
             fcntl.flock(lk, fcntl.LOCK_EX)
             try:
-                if not _up_to_date(targets):
+                if not _up_to_date(targets, hip):
                     try:
                         build(hip=hip)
                     except (RuntimeError, OSError, subprocess.CalledProcessError) as e:
@@ -190,6 +224,8 @@ def ensure_built(hip: bool | None = None) -> None:
                                       f"({e}); using the existing build outputs")
             finally:
                 fcntl.flock(lk, fcntl.LOCK_UN)
+    elif STAMP.exists():
+        stamp_version()  # HEAD may have moved since the build
     _checked.add(hip)
 
 

@@ -48,13 +48,21 @@ def _probe_exe():
     return os.path.join(str(PKG_DIR), "bin", "mi355x-liveness-probe")
 
 
+def _present_kfd_entries():
+    """kfd proc entries now. They are named by host PID, which a container's PID
+    namespace (the gpurun box) does not show as os.getpid(): this pytest
+    process, which may hold HIP queues from earlier GPU tests, is among them."""
+    root = "/sys/class/kfd/kfd/proc"
+    return sorted(os.listdir(root)) if os.path.isdir(root) else []
+
+
 def _engine(ordinals, **opts):
-    """The engine on the accessible GPUs. This pytest process may hold HIP
-    queues from earlier GPU tests: it is never counted as a tenant, as a
+    """The engine on the accessible GPUs. The processes already on the GPU
+    (this pytest process among them) are never counted as tenants, as a
     process embedding the engine would not be (Config::kfd_exclude)."""
     from rocm_k8s_device_plugin_amd.ops.native import core
     o = dict(dev_root="/dev", liveness=True, probe_exe=_probe_exe(), probe_timeout_s=60.0,
-             device_ids=sorted(ordinals), kfd_exclude=[str(os.getpid())])
+             device_ids=sorted(ordinals), kfd_exclude=_present_kfd_entries())
     o.update(opts)
     return core().HealthEngine("/sys", o)
 
@@ -92,7 +100,7 @@ def test_native_kept_queue_server_is_not_a_tenant(inv, ordinals):
     from rocm_k8s_device_plugin_amd.topology import kfd_busy_gpu_ids
     dev_id = min(ordinals, key=ordinals.get)
     gid = inv.topology.node(inv.by_id[dev_id].node_id).gpu_id
-    before = kfd_busy_gpu_ids("/sys", exclude={str(os.getpid())})   # other tenants of the shared host
+    initial = set(_present_kfd_entries())          # this test process among them
     eng = _engine({dev_id: ordinals[dev_id]})
     try:
         eng.sweep()
@@ -105,18 +113,22 @@ def test_native_kept_queue_server_is_not_a_tenant(inv, ordinals):
             own = eng.own_kfd_entries({gid})
         if not own:
             pytest.skip("another GPU process started with the probe server and is still running")
-        assert own == {str(eng.stats()["server_pid"])}, (own, eng.stats())
+        # kfd names its proc entries by host PID, which differs from the server's PID
+        # inside a container's PID namespace (as on the gpurun box): one entry, with our queue
+        assert len(own) == 1 and eng.stats()["server_pid"] > 0, (own, eng.stats())
         qdir = os.path.join("/sys/class/kfd/kfd/proc", next(iter(own)), "queues")
         gids = {int(open(os.path.join(qdir, q, "gpuid")).read()) for q in os.listdir(qdir)}
         assert gid in gids                                       # the server's kept queue ...
+        assert gid in kfd_busy_gpu_ids("/sys", exclude=initial)   # ... makes the GPU look busy to a naive reader
         eng.sweep()
         assert eng.stats()["busy_state_known"]
-        assert (gid in eng.gpu_load()) == (gid in before)        # ... is not counted as a tenant
+        # ... but not to the engine (other processes of the shared host may come and go: same view)
+        assert (gid in eng.gpu_load()) == (gid in kfd_busy_gpu_ids("/sys", exclude=initial | own))
     finally:
         eng.close()
 
 
-def test_native_probe_server_killed_is_replaced(ordinals):
+def test_native_probe_server_killed_is_replaced(inv, ordinals):
     """SIGKILL of the real probe server between sweeps (OOM killer, operator):
     the next sweep starts a new one, the device stays Healthy."""
     eng = _engine(ordinals)
@@ -130,12 +142,20 @@ def test_native_probe_server_killed_is_replaced(ordinals):
         st = eng.stats()
         assert st["server_starts"] == 2 and st["server_pid"] not in (-1, pid), st
         assert all(ok for ok, _ in eng.snapshot().values()), eng.snapshot()
-        # a check right after a kill: no server until the sweep restarts it -> a fresh process
+        # a check after a kill: no server until the sweep restarts it -> a fresh process.
+        # Until the dead server's kfd process is torn down its queue still counts as
+        # another process' (the GPU is busy): such a check is inconclusive, not failed.
+        gids = {inv.topology.node(inv.by_id[d].node_id).gpu_id for d in ordinals}
+        own = eng.own_kfd_entries(gids)
         os.kill(st["server_pid"], signal.SIGKILL)
-        time.sleep(0.5)
+        res = eng.check(sorted(ordinals), 10.0)
+        assert all(r["ok"] or r["pending"] for r in res.values()), res
+        deadline = time.monotonic() + 30
+        while own & set(_present_kfd_entries()) and time.monotonic() < deadline:
+            time.sleep(0.1)
         res = eng.check(sorted(ordinals), 10.0)
         assert all(r["ok"] for r in res.values()), res
-        assert eng.stats()["check_fresh"] == len(ordinals)
+        assert eng.stats()["check_fresh"] >= len(ordinals)
     finally:
         eng.close()
 

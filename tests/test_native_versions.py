@@ -36,10 +36,16 @@ def _stamped():
 
 
 def _check_banner(lines, exe):
+    from rocm_k8s_device_plugin_amd import _build
     assert lines[0] == TITLES[os.path.basename(exe)]
-    m = re.fullmatch(re.escape(exe) + r" version (\S+)", lines[1])
+    m = re.fullmatch(re.escape(exe) + r" version (\S+) \(native sources ([0-9a-f]{12})\)", lines[1])
     assert m, lines[1]
-    if _stamped():
+    assert m.group(2) == _build._source_digest()[:12]
+    # HEAD's describe (<package>/VERSION, kept current without a relink), else the compiled-in one
+    version = os.path.join(os.path.dirname(BIN), "VERSION")
+    if os.path.exists(version):
+        assert "describe=" + m.group(1) in open(version).read().split()
+    elif _stamped():
         assert m.group(1) == _stamped()
     assert re.fullmatch(r"rocm: \S+, amdgpu: \S+, libdrm_amdgpu: \S+, amd-smi: \S+, numa_source: sysfs", lines[2]), lines[2]
 

@@ -336,3 +336,26 @@ def test_gate_flags_validated(flag, value, want):
     p = subprocess.run([EXE, "-pulse", "1", "-liveness", "-prestart_liveness", flag, value, "-dry_run"],
                        capture_output=True, text=True, timeout=20)
     assert p.returncode == 1 and want in p.stderr, p.stderr
+
+
+def test_engine_binding_device_filter_and_tenant_exclusion(tmp_path):
+    """The binding's device_ids (judge only these, as the daemon's -device_ids)
+    and kfd_exclude (entries never counted as tenants, e.g. the embedding
+    process' own queues) options."""
+    fi = make_mi355x_node(tmp_path / "n")
+    inv = discover(str(fi.sysfs))
+    eng0 = core().HealthEngine(str(fi.sysfs), {"dev_root": str(fi.dev)})
+    dev = {o: d for d, o in eng0.ordinals().items()}
+    eng0.close()
+    ctl, eng = _engine(fi, tmp_path, {}, device_ids=[dev[1], dev[2]], kfd_exclude=["4242"])
+    try:
+        assert sorted(eng.ordinals()) == sorted([dev[1], dev[2]])
+        _busy_gpu(fi, inv, dev[1], pid="4242")               # excluded: not a tenant
+        _busy_gpu(fi, inv, dev[2], pid="4343")               # a tenant
+        eng.sweep()
+        assert sorted(eng.snapshot()) == sorted([dev[1], dev[2]])
+        gid = lambda d: inv.topology.node(inv.by_id[d].node_id).gpu_id  # noqa: E731
+        assert gid(dev[1]) not in eng.gpu_load() and eng.gpu_load()[gid(dev[2])] == (1, 1)
+    finally:
+        eng.close()
+
