@@ -617,9 +617,12 @@ namespace mi355x::hsa_rt {
 // Each blocking wait is capped at 20 ms and at what is left of the deadline,
 // in the system timestamp's unit (hsa_signal_wait's timeout_hint; 100 MHz on
 // MI355X, so a fixed 20e6 hint meant up to 200 ms past a 50 ms deadline).
+// The first wait lasts at least 1 ms: no dispatch completes faster than its
+// launch, so a shorter deadline would only abandon work that is about to finish.
 bool wait_signal(hsa_signal_t sig, double timeout_s) {
   using clk = std::chrono::steady_clock;
-  const auto deadline = clk::now() + std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 5.0);
+  const auto t0 = clk::now();
+  const auto deadline = t0 + std::chrono::duration<double>(std::max(1e-3, timeout_s > 0 ? timeout_s : 5.0));
   const double ticks_per_s = g_rt.ts_freq ? static_cast<double>(g_rt.ts_freq) : 1e9;
   while (true) {
     const double left = std::chrono::duration<double>(deadline - clk::now()).count();
