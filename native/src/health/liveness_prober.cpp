@@ -320,13 +320,25 @@ LivenessProber::LivenessProber(ProberConfig cfg) : cfg_(std::move(cfg)) {}
 LivenessProber::~LivenessProber() { close(); }
 
 bool LivenessProber::server_running() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return server_ && server_->c.pid > 0 && !server_->dead;
+  std::shared_ptr<Server> s;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    s = server_;
+  }
+  if (!s) return false;
+  std::lock_guard<std::mutex> lk(s->mu);
+  return s->c.pid > 0 && !s->dead;
 }
 
 int LivenessProber::server_pid() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return server_ && !server_->dead ? static_cast<int>(server_->c.pid) : -1;
+  std::shared_ptr<Server> s;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    s = server_;
+  }
+  if (!s) return -1;
+  std::lock_guard<std::mutex> lk(s->mu);
+  return s->dead ? -1 : static_cast<int>(s->c.pid);
 }
 
 double LivenessProber::inner_timeout() const { return cfg_.timeout_s - std::min(0.5, 0.25 * cfg_.timeout_s); }
@@ -606,8 +618,14 @@ LivenessProber::Got LivenessProber::transact(const std::shared_ptr<Server>& s, c
       s->cv.notify_all();
       continue;
     }
-    const double left = deadline - mono_s();
-    s->cv.wait_for(lk, std::chrono::duration<double>(std::max(0.0, left)));
+    // a bounded wait on the system clock: libstdc++ implements it with
+    // pthread_cond_timedwait (steady-clock waits use pthread_cond_clockwait,
+    // which GCC 11's ThreadSanitizer does not intercept); the loop re-checks
+    // the steady deadline, so a clock step costs at most one 50 ms slice
+    const double left = std::min(0.05, std::max(0.0, deadline - mono_s()));
+    s->cv.wait_until(lk, std::chrono::system_clock::now() +
+                             std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                 std::chrono::duration<double>(left)));
   }
   s->waiting.erase(id);  // a reply that comes later is dropped
   s->order.erase(std::remove(s->order.begin(), s->order.end(), id), s->order.end());
