@@ -115,14 +115,19 @@ class LivenessProber {
                                     const std::string& kind = "probe");
   // one device in a fresh process (ROCR_VISIBLE_DEVICES=<ordinal>)
   ProbeOutcome probe_ordinal(int ordinal, const std::string& kind = "probe");
-  // A PreStartContainer check within `budget_s`: the running server first
-  // (busy GPUs: busy_deadline_s; idle ones: 40% of the budget), then a
-  // fresh process for each idle GPU the server failed or could not answer
-  // for, while at least a second of the budget is left. Busy GPUs and
-  // whatever the budget leaves unsettled come back pending. Never starts,
+  // A PreStartContainer check within `budget_s`, on the running server:
+  //   1. every GPU with busy_deadline_s (an idle GPU answers in microseconds);
+  //   2. only if some did not pass: `busy_of()` (ordinals other processes
+  //      use, a kfd process-list scan). A pending dispatch on a busy GPU is
+  //      inconclusive; on an idle one the same dispatch gets until 40% of the
+  //      budget;
+  //   3. a fresh process for each GPU the server failed or could not answer
+  //      for (a pending one only where idle), while at least 1 s is left.
+  // Whatever the budget leaves unsettled comes back pending. Never starts,
   // restarts or stops the server; a failure a fresh process does not confirm
   // asks the next sweep to restart it. Leaves the sweep's backoff and counters alone.
-  std::map<int, ProbeOutcome> check(const std::vector<int>& ordinals, const std::set<int>& busy, double budget_s);
+  std::map<int, ProbeOutcome> check(const std::vector<int>& ordinals, const std::function<std::set<int>()>& busy_of,
+                                    double budget_s);
   // restrict the server to these host ordinals (nullopt = all); a change restarts it
   void set_visible(std::optional<std::vector<int>> ordinals);
   void close();

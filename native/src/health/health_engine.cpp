@@ -599,17 +599,21 @@ std::map<std::string, ProbeOutcome> Engine::probe_now(const std::vector<std::str
   std::vector<int> uniq;
   for (const auto& [id, o] : sel) uniq.push_back(o);
   // GPUs with other processes' queues (the probe server's own excluded), as a sweep
-  // sees them: a dispatch queued behind their work there is inconclusive, gets the
-  // short deadline and no fresh-process confirmation (which the container would wait for)
-  std::set<int64_t> gids;
-  for (const auto& [id, o] : sel) gids.insert(gpu_id(id));
-  gids.erase(0);
-  std::map<int64_t, std::pair<int, int>> load;
-  const bool known = kfd_load(prober_->own_kfd_entries(gids), &load);
-  std::set<int> busy;
-  for (const auto& [id, o] : sel)
-    if (!known || load.count(gpu_id(id))) busy.insert(o);
-  const auto by_ord = prober_->check(uniq, busy, budget_s);
+  // sees them: a dispatch queued behind their work there is inconclusive and gets
+  // no fresh-process confirmation (which the container would wait for). Read only
+  // when a probe did not pass at once.
+  auto busy_of = [this, &sel] {
+    std::set<int64_t> gids;
+    for (const auto& [id, o] : sel) gids.insert(gpu_id(id));
+    gids.erase(0);
+    std::map<int64_t, std::pair<int, int>> load;
+    const bool known = kfd_load(prober_->own_kfd_entries(gids), &load);
+    std::set<int> busy;
+    for (const auto& [id, o] : sel)
+      if (!known || load.count(gpu_id(id))) busy.insert(o);
+    return busy;
+  };
+  const auto by_ord = prober_->check(uniq, busy_of, budget_s);
   std::map<std::string, ProbeOutcome> out;
   for (const auto& [id, o] : sel) {
     auto it = by_ord.find(o);

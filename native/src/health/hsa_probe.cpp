@@ -614,21 +614,30 @@ extern "C" int mi355x_hsa_probe_device(int ordinal, uint32_t nonce, int iters, d
 namespace mi355x::hsa_rt {
 
 // Bounded wait for a completion signal (value 1 -> 0): true when it completed.
-// Each blocking wait is capped at 20 ms and at what is left of the deadline,
-// in the system timestamp's unit (hsa_signal_wait's timeout_hint; 100 MHz on
-// MI355X, so a fixed 20e6 hint meant up to 200 ms past a 50 ms deadline).
+// hsa_signal_wait's BLOCKED wait (interrupt-driven: returns as soon as the
+// dispatch completes) overshoots its timeout hint by up to ~20 ms on MI355X
+// (a 50 ms deadline came back after 69 ms p50, tools/probe_deadline_tenant.py),
+// so it is used only while more than kBlockedMargin is left, with the hint
+// cut to leave that margin; the rest of the deadline is polled every 200 us.
 // The first wait lasts at least 1 ms: no dispatch completes faster than its
 // launch, so a shorter deadline would only abandon work that is about to finish.
 bool wait_signal(hsa_signal_t sig, double timeout_s) {
   using clk = std::chrono::steady_clock;
+  constexpr double kBlockedMargin = 0.025;
   const auto t0 = clk::now();
   const auto deadline = t0 + std::chrono::duration<double>(std::max(1e-3, timeout_s > 0 ? timeout_s : 5.0));
   const double ticks_per_s = g_rt.ts_freq ? static_cast<double>(g_rt.ts_freq) : 1e9;
   while (true) {
     const double left = std::chrono::duration<double>(deadline - clk::now()).count();
     if (left <= 0) return H().hsa_signal_load_scacquire(sig) < 1;
-    const uint64_t hint = static_cast<uint64_t>(std::max(1.0, std::min(0.02, left) * ticks_per_s));
-    if (H().hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_BLOCKED) < 1) return true;
+    if (left > kBlockedMargin + 1e-3) {
+      const double hint_s = std::min(0.02, left - kBlockedMargin);
+      const uint64_t hint = static_cast<uint64_t>(std::max(1.0, hint_s * ticks_per_s));
+      if (H().hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_BLOCKED) < 1) return true;
+      continue;
+    }
+    if (H().hsa_signal_load_scacquire(sig) < 1) return true;
+    std::this_thread::sleep_for(std::chrono::duration<double>(std::min(left, 2e-4)));
   }
 }
 

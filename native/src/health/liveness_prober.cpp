@@ -818,8 +818,8 @@ std::map<int, ProbeOutcome> LivenessProber::probe(const std::vector<int>& ordina
   return res;
 }
 
-std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordinals, const std::set<int>& busy,
-                                                  double budget_s) {
+std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordinals,
+                                                  const std::function<std::set<int>()>& busy_of, double budget_s) {
   trace::Span span("liveness.check", "health", {{"ordinals", std::to_string(ordinals.size())}});
   const double t0 = mono_s(), end = t0 + budget_s;
   std::vector<int> uniq(ordinals);
@@ -836,6 +836,13 @@ std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordina
     out[o] = r;
     check_inconclusive++;
   };
+  // which GPUs other processes use: read (a kfd process-list scan) only when a
+  // probe did not pass at once, i.e. never on the common path
+  std::optional<std::set<int>> busy_memo;
+  auto busy = [&]() -> const std::set<int>& {
+    if (!busy_memo) busy_memo = busy_of ? busy_of() : std::set<int>{};
+    return *busy_memo;
+  };
   std::shared_ptr<Server> srv;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -847,46 +854,71 @@ std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordina
       if (covers) srv = server_;
     }
   }
-  std::map<int, ProbeOutcome> got;
-  if (srv && srv->alive()) {
-    // idle GPUs: 40% of the budget on the kept queue leaves the rest for a
-    // fresh process' confirmation (runtime start-up included)
-    const double inner = inner_timeout();
-    const double idle_dl = std::min(inner, std::max(0.2, 0.4 * budget_s));
-    std::map<int, double> deadlines;
-    double top = 0;
-    for (int o : uniq) top = std::max(top, deadlines[o] = busy.count(o) ? std::min(inner, cfg_.busy_deadline_s) : idle_dl);
+  bool interrupted = false;
+  auto ask = [&](const std::vector<int>& ords, double deadline) {
+    std::map<int, double> dl;
+    for (int o : ords) dl[o] = deadline;
     std::string err;
-    got = request(srv, uniq, "probe", deadlines, std::min(end, mono_s() + top + 0.25), &err);
+    auto got = request(srv, ords, "probe", dl, std::min(end, mono_s() + deadline + 0.25), &err);
     if (!err.empty()) {
-      if (err == "interrupted") {
-        for (int o : uniq) {
-          out[o].reason = "probe interrupted (shutdown)";
-          out[o].interrupted = true;
-        }
-        return out;
-      }
-      MI_LOG(kWarning, "PreStartContainer check: probe server: %s", err.c_str());
-      got.clear();
+      interrupted = err == "interrupted";
+      if (!interrupted) MI_LOG(kWarning, "PreStartContainer check: probe server: %s", err.c_str());
+      return std::map<int, ProbeOutcome>{};
     }
     for (const auto& [o, r] : got)
       if (r.queue_lost) {
         std::lock_guard<std::mutex> lk(mu_);
         restart_wanted_ = true;  // its timed-out queue cannot be freed: the next sweep restarts it
       }
-  }
+    return got;
+  };
+  std::map<int, ProbeOutcome> got;  // the server's last verdict per ordinal
   std::vector<int> confirm;
-  for (int o : uniq) {
-    auto it = got.find(o);
-    if (it != got.end() && it->second.ok) {
-      out[o] = it->second;
-    } else if (busy.count(o) && (it == got.end() || it->second.pending)) {
-      // queued behind (or, without a server answer, would queue behind) another process' kernels;
-      // a definite failure there (a wrong tile, an error) is confirmed like anywhere else
-      inconclusive(o, it != got.end() ? it->second.reason : "no probe server answer on a busy GPU");
-    } else {
-      confirm.push_back(o);
+  if (srv && srv->alive()) {
+    const double inner = inner_timeout();
+    // 1: every GPU with the busy deadline. An idle GPU answers in microseconds;
+    // a dispatch queued behind a tenant's kernel stays on the kept queue.
+    got = ask(uniq, std::min(inner, cfg_.busy_deadline_s));
+    std::vector<int> idle_pending;
+    for (int o : uniq) {
+      if (interrupted) break;
+      auto it = got.find(o);
+      if (it != got.end() && it->second.ok) {
+        out[o] = it->second;
+      } else if (it != got.end() && !it->second.pending) {
+        confirm.push_back(o);  // a definite failure (a wrong tile, an error): busy or not
+      } else if (busy().count(o)) {
+        inconclusive(o, it != got.end() ? it->second.reason : "no probe server answer on a busy GPU");
+      } else if (it != got.end()) {
+        idle_pending.push_back(o);
+      } else {
+        confirm.push_back(o);
+      }
     }
+    // 2: pending where no other process runs: wait for that same dispatch up
+    // to 40% of the budget in all (the rest is for a fresh process' confirmation)
+    const double idle_dl = std::min(inner, std::max(0.2, 0.4 * budget_s)) - (mono_s() - t0);
+    if (!interrupted && !idle_pending.empty()) {
+      auto again = ask(idle_pending, std::max(0.01, idle_dl));
+      for (int o : idle_pending) {
+        if (auto it = again.find(o); it != again.end()) got[o] = it->second;
+        if (got.count(o) && got[o].ok) out[o] = got[o];
+        else confirm.push_back(o);
+      }
+    }
+  } else {
+    for (int o : uniq) {
+      if (busy().count(o)) inconclusive(o, "no probe server answer on a busy GPU");
+      else confirm.push_back(o);
+    }
+  }
+  if (interrupted) {
+    for (int o : uniq) {
+      out[o] = ProbeOutcome{};
+      out[o].reason = "probe interrupted (shutdown)";
+      out[o].interrupted = true;
+    }
+    return out;
   }
   if (confirm.empty()) return out;
   const double left = end - mono_s();
@@ -908,7 +940,7 @@ std::map<int, ProbeOutcome> LivenessProber::check(const std::vector<int>& ordina
     } else if (!f.interrupted) {
       // a fresh process that got nothing back: on a GPU no other process uses
       // that is a fault; on a busy one it may wait behind the tenant's kernels
-      if (f.pending && !busy.count(o)) f.pending = false;
+      if (f.pending && !busy().count(o)) f.pending = false;
       if (f.pending) check_inconclusive++;
       if (server_failed) f.reason += " (server: " + got[o].reason + ")";
     }

@@ -123,7 +123,9 @@ async def main(a) -> int:
                                                 stdout=asyncio.subprocess.DEVNULL, stderr=errf)
     rows = []
     try:
-        st = await k.wait_for_resource("amd.com/gpu", 1, timeout=30)
+        # the first health sweep (with -perf_check_every: a throughput check) runs before
+        # registration; a sanitizer build takes a while longer
+        st = await k.wait_for_resource("amd.com/gpu", 1, timeout=120)
         n = len(st.devices)
         t_end = time.monotonic() + a.seconds
         next_report = time.monotonic() + a.report
