@@ -27,6 +27,7 @@
 #include <cstring>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -529,9 +530,36 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
                 static_cast<unsigned long long>(t_start), static_cast<unsigned long long>(t_runtime));
   emit_line(hello);
   if (n < 0) return 2;
-  std::mutex wmu;
-  std::condition_variable wcv;
-  int running = 0;
+  // Tagged requests go to a pool of worker threads that stay for the server's
+  // life (a thread per request cost its creation on every probe); the pool
+  // grows while every worker is busy -- a request stuck on a wedged device
+  // holds its worker, not the others -- up to kMaxServeWorkers, beyond which
+  // a request is answered inline.
+  struct Pool {
+    std::mutex mu;
+    std::condition_variable cv, done;
+    std::deque<ServeRequest> q;
+    int workers = 0, idle = 0, busy = 0;
+    bool stop = false;
+  } pool;
+  std::vector<std::thread> threads;
+  auto worker = [&pool, n] {
+    std::unique_lock<std::mutex> lk(pool.mu);
+    while (true) {
+      pool.idle++;
+      pool.cv.wait(lk, [&] { return pool.stop || !pool.q.empty(); });
+      pool.idle--;
+      if (pool.q.empty()) return;  // stopping
+      ServeRequest r = std::move(pool.q.front());
+      pool.q.pop_front();
+      pool.busy++;
+      lk.unlock();
+      answer(r, n);
+      lk.lock();
+      pool.busy--;
+      pool.done.notify_all();
+    }
+  };
   std::string line;
   char buf[8192];
   while (std::fgets(buf, sizeof(buf), stdin)) {
@@ -544,34 +572,35 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
       emit_line("{" + id_field(r) + "\"ok\":false,\"error\":\"bad request\",\"devices\":[]}");
       continue;
     }
-    bool async = false;
+    bool queued = false;
     if (r.tagged && kConcurrentServe) {
-      std::lock_guard<std::mutex> lk(wmu);
-      if (running < kMaxServeWorkers) {
-        running++;
-        async = true;
+      std::lock_guard<std::mutex> lk(pool.mu);
+      if (pool.idle > static_cast<int>(pool.q.size()) || pool.workers < kMaxServeWorkers) {
+        if (pool.idle <= static_cast<int>(pool.q.size())) {
+          pool.workers++;
+          threads.emplace_back(worker);
+        }
+        pool.q.push_back(std::move(r));
+        pool.cv.notify_one();
+        queued = true;
       }
     }
-    if (!async) {
-      answer(r, n);
-      continue;
-    }
-    std::thread([r = std::move(r), n, &wmu, &wcv, &running] {
-      answer(r, n);
-      std::lock_guard<std::mutex> lk(wmu);
-      running--;
-      wcv.notify_all();
-    }).detach();
+    if (!queued) answer(r, n);
   }
   {
     // every worker's waits are bounded by its deadlines; one stuck inside the
     // runtime past that keeps the runtime up: exit without shutting it down
-    std::unique_lock<std::mutex> lk(wmu);
-    if (!wcv.wait_for(lk, std::chrono::seconds(60), [&] { return running == 0; })) {
+    std::unique_lock<std::mutex> lk(pool.mu);
+    const bool drained =
+        pool.done.wait_for(lk, std::chrono::seconds(60), [&] { return pool.q.empty() && pool.busy == 0; });
+    if (!drained) {
       std::fflush(stdout);
       std::_Exit(0);
     }
+    pool.stop = true;
+    pool.cv.notify_all();
   }
+  for (auto& t : threads) t.join();
   runtime_shutdown();
   return 0;
 }
