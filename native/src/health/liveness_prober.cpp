@@ -561,6 +561,8 @@ std::shared_ptr<LivenessProber::Server> LivenessProber::ensure_server(const std:
                                 : "probe server failed to start: " + hello.substr(0, 200);
     return nullptr;
   }
+  // informational: a server built on the HIP runtime answers tagged requests in
+  // order, so a check there waits its turn (within its own budget)
   srv->concurrent = jbool(&*doc, "concurrent");
   srv->visible = visible;
   for (const auto& e : list_dir(cfg_.kfd_proc_dir))

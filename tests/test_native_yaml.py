@@ -8,6 +8,14 @@ must return what ``yaml.safe_load`` returns. Plain scalars that are not
 booleans or null stay strings in the native reader (configs read them as
 text), so the generated documents hold no numbers: PyYAML quotes any string
 that would resolve to one.
+
+A second generator writes documents the way people write configs by hand
+(per-level indentation, sequences at their key's column, comments after
+values and on their own lines, blank lines, document markers, short flow
+leaves); every one PyYAML accepts must read the same natively.
+
+The suite runs these properties derandomized (the "ci" Hypothesis profile,
+tests/conftest.py); tools/yaml_differential.py explores fresh draws.
 """
 import json
 
@@ -191,3 +199,98 @@ def test_alias_expansion_is_bounded():
     out, err = core().yaml_to_json("\n".join(lines) + "\n")
     assert out is None and "too large" in err
     assert len(native("\n".join(lines[:4]) + "\n")["a3"]) == 10  # small expansions stay fine
+
+
+# ---- hand-written surface syntax -------------------------------------------------
+# safe_dump writes one canonical layout. Config files and kubeconfigs written
+# by hand vary indentation per level, put "- " entries at the key's own column,
+# comment after values and on lines of their own, leave blank lines, mark the
+# document, and use flow collections for short leaves. The native reader must
+# read those as PyYAML does (a generated text PyYAML refuses is skipped).
+# plain scalars PyYAML also reads as text (no 0b1 / 0x1 / 1_0 / 017 / 1:30 numbers:
+# the native reader keeps every plain scalar as text, see the module docstring)
+def _reads_as_text(t):
+    try:
+        return isinstance(yaml.safe_load(t), str)
+    except (yaml.YAMLError, ValueError):  # PyYAML itself fails on "0x_" / "0b_"
+        return False
+
+
+_PLAIN = st.text(alphabet=st.sampled_from(list("abcxyz_-./0123456789")), min_size=1, max_size=8).filter(
+    lambda t: t[0] not in "-." and _reads_as_text(t))
+_LEAF = st.one_of(_PLAIN, st.sampled_from(["true", "false", "null", "~", "''", '""']),
+                  st.tuples(st.sampled_from(["'", '"']), _TEXT.filter(lambda t: "\\" not in t and "\n" not in t
+                                                                     and "\t" not in t)))
+_TREE = st.recursive(_LEAF, lambda c: st.one_of(st.lists(c, min_size=1, max_size=3),
+                                               st.dictionaries(_PLAIN, c, min_size=1, max_size=3)), max_leaves=10)
+
+
+def _leaf_text(v):
+    if isinstance(v, tuple):
+        q, t = v
+        return q + (t.replace("'", "''") if q == "'" else t.replace('"', '\\"')) + q
+    return v
+
+
+def _flow(v):
+    if isinstance(v, list):
+        return "[" + ", ".join(_flow(x) for x in v) + "]"
+    if isinstance(v, dict):
+        return "{" + ", ".join(f"{k}: {_flow(x)}" for k, x in v.items()) + "}"
+    return _leaf_text(v)
+
+
+@st.composite
+def _hand_written(draw):
+    tree = draw(st.dictionaries(_PLAIN, _TREE, min_size=1, max_size=4))
+    lines = []
+    if draw(st.booleans()):
+        lines.append("---" + (" # start" if draw(st.booleans()) else ""))
+
+    def comment():
+        c = draw(st.sampled_from(["", "", " # note", "  # a: b", " #- x", " # 'q"]))
+        return c
+
+    def emit(v, indent):
+        if isinstance(v, dict):
+            for k, x in v.items():
+                if draw(st.integers(0, 5)) == 0:
+                    lines.append(" " * draw(st.integers(0, indent + 2)) + "# " + draw(_PLAIN))
+                if draw(st.integers(0, 6)) == 0:
+                    lines.append("")
+                if isinstance(x, (dict, list)) and x and draw(st.integers(0, 3)):
+                    lines.append(" " * indent + f"{k}:" + comment())
+                    step = draw(st.integers(1, 4))
+                    # a block sequence may sit at its key's own column
+                    emit(x, indent if isinstance(x, list) and draw(st.booleans()) else indent + step)
+                else:
+                    lines.append(" " * indent + f"{k}: {_flow(x)}" + comment())
+        else:
+            for x in v:
+                if isinstance(x, dict) and x and draw(st.booleans()):
+                    items = list(x.items())
+                    k0, x0 = items[0]
+                    lines.append(" " * indent + f"- {k0}: {_flow(x0)}" + comment())
+                    for k, y in items[1:]:
+                        lines.append(" " * (indent + 2) + f"{k}: {_flow(y)}" + comment())
+                elif isinstance(x, (dict, list)) and x and draw(st.booleans()):
+                    lines.append(" " * indent + "-" + comment())
+                    emit(x, indent + draw(st.integers(1, 3)))
+                else:
+                    lines.append(" " * indent + f"- {_flow(x)}" + comment())
+
+    emit(tree, 0)
+    if draw(st.booleans()):
+        lines.append("..." if draw(st.booleans()) else "# end")
+    return "\n".join(lines) + "\n"
+
+
+@settings(deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.filter_too_much])
+@given(text=_hand_written())
+def test_hand_written_layouts_equal_pyyaml(text):
+    from hypothesis import assume
+    try:
+        want = yaml.safe_load(text)
+    except yaml.YAMLError:
+        assume(False)
+    assert native(text) == _stringify(want), text

@@ -34,7 +34,8 @@ TESTS = ["tests/test_native_daemon.py", "tests/test_native_health.py", "tests/te
          "tests/test_native_config_logging.py", "tests/test_native_stress.py", "tests/test_go_interop.py",
          "tests/test_native_cdi.py", "tests/test_native_reload.py", "tests/test_native_views.py",
          "tests/test_native_metrics.py", "tests/test_native_dryrun.py", "tests/test_native_perf.py",
-         "tests/test_native_fabric.py"]
+         "tests/test_native_fabric.py", "tests/test_prestart_gate.py", "tests/test_kfd_denied.py",
+         "tests/test_provenance.py"]
 
 _LINES = re.compile(r"Lines executed:\s*([\d.]+)% of (\d+)")
 

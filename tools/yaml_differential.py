@@ -22,6 +22,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PROPERTIES = ["tests/test_native_yaml.py::test_native_reader_equals_pyyaml",
+              "tests/test_native_yaml.py::test_hand_written_layouts_equal_pyyaml",
               "tests/test_native_yaml.py::test_shared_nodes_equal_pyyaml",
               "tests/test_native_json.py"]
 
