@@ -79,6 +79,9 @@ def test_chart_health_defaults_follow_the_measured_choice():
     assert "-liveness_mode=persistent" in c["args"] and c["resources"] == {"requests": {"memory": "3072Mi"}}
     assert "-prestart_liveness=true" in c["args"]
     assert "-prestart_liveness=false" in dp({"dp": {"liveness": {"enabled": True, "prestart": False}}})["args"]
+    assert "-prestart_budget=5" in c["args"] and "-liveness_busy_deadline=0.05" in c["args"]
+    tuned = dp({"dp": {"liveness": {"enabled": True, "prestartBudget": 8, "busyDeadline": 0.02}}})["args"]
+    assert "-prestart_budget=8" in tuned and "-liveness_busy_deadline=0.02" in tuned
     assert dp({"dp": {"liveness": {"enabled": True, "mode": "spawn"}}})["args"].count("-liveness_mode=spawn") == 1
     assert dp({"dp": {"liveness": {"enabled": True}, "resources": {"limits": {"memory": "4Gi"}}}})["resources"] == \
         {"limits": {"memory": "4Gi"}}
