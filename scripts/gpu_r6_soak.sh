@@ -11,9 +11,9 @@ step() { local name=$1 limit=$2; shift 2; timeout -k 10 "$limit" "$@" > "gpurun_
 [ -n "$SKIP_DEADLINE" ] || step probe_deadline_tenant 200 python -u tools/probe_deadline_tenant.py --out gpurun_out/probe_deadline_tenant.json
 [ -n "$SKIP_TENANT" ] || step prestart_tenant_after 300 python -u tools/prestart_tenant.py --out gpurun_out/prestart_tenant_after.json
 [ -n "$SKIP_SUITE" ] || step r6_gpu_suite 480 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread -p no:cacheprovider
-[ -n "$SKIP_SOAK" ] || step soak_prestart_r6 400 python -u tools/soak_native.py --seconds ${SOAK_SECONDS:-240} --report 30 \
+[ -n "$SKIP_SOAK" ] || step soak_prestart_r6 $(( ${SOAK_SECONDS:-240} + 180 )) python -u tools/soak_native.py --seconds ${SOAK_SECONDS:-240} --report 30 \
   --container-interval 1 --extra "$FLAGS" --out gpurun_out/soak_prestart_r6.json
-[ -n "$SKIP_TSAN" ] || TSAN_OPTIONS="halt_on_error=1" step soak_prestart_tsan_r6 400 python -u tools/soak_native.py \
+[ -n "$SKIP_TSAN" ] || TSAN_OPTIONS="halt_on_error=1" step soak_prestart_tsan_r6 $(( ${TSAN_SECONDS:-180} + 240 )) python -u tools/soak_native.py \
   --seconds ${TSAN_SECONDS:-180} --report 30 --container-interval 1 --exe tsan_bin/mi355x-device-plugin --extra "$FLAGS" \
   --out gpurun_out/soak_prestart_tsan_r6.json
 echo done
