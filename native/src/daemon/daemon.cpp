@@ -220,7 +220,8 @@ int Daemon::init() {
           })) {
         metrics::global().inc("mi355x_dp_prestart_checks_total", {{"result", "overflow"}}, 1.0,
                               "PreStartContainer liveness checks (-prestart_liveness): ok, failed, inconclusive (busy GPU or budget spent)");
-        MI_LOG(kWarning, "PreStartContainer: %zu checks already queued; this start goes ahead unchecked", size_t{64});
+        MI_LOG(kWarning, "PreStartContainer: %zu checks already queued; this start goes ahead unchecked",
+               gate_pool_.max_queued());
         (*shared_done)(rpc::Reply{});
       }
     };

@@ -79,6 +79,7 @@ class GatePool {
   // runs what is queued, then stops the workers
   void join_all();
   size_t threads() const;
+  size_t max_queued() const { return max_queued_; }
 
  private:
   void loop();
