@@ -329,6 +329,33 @@ def test_daemon_gate_workers_are_bounded(tmp_path):
     assert rc == 0, err[-3000:]
 
 
+def test_daemon_gate_queue_overflow_lets_starts_through(tmp_path):
+    """100 PreStartContainer calls at once on GPUs that never answer: 8 run
+    (and fail within the budget), up to 64 wait in the queue and come out
+    inconclusive once their budget is spent there, and the rest find the queue
+    full and are let through at once (`overflow`). Every call is answered,
+    none later than the budget plus its queue wait allows."""
+    n = _Node(tmp_path, {}, "-pulse", "3600", "-liveness_timeout", "20", "-prestart_budget", "2")
+    try:
+        n.ctl.write_text(json.dumps({str(o): "hang" for o in range(8)}))
+        with concurrent.futures.ThreadPoolExecutor(100) as ex:
+            res = list(ex.map(lambda i: _prestart(n.kdir, [n.dev[i % 8]]), range(100)))
+        m = n.metrics()
+        got = {r: m.get(f'mi355x_dp_prestart_checks_total{{result="{r}"}}', 0)
+               for r in ("ok", "failed", "inconclusive", "overflow")}
+        assert sum(got.values()) == 100, got
+        assert got["overflow"] >= 1 and got["ok"] == 0, got
+        assert 1 <= got["failed"] <= 8, got
+        failed = [r for r in res if r[0] != 0]
+        assert len(failed) == got["failed"] and all(s == 9 for s, _, _ in failed), failed
+        assert max(t for _, _, t in res) < 2 * 2 + 5, sorted(t for _, _, t in res)[-5:]
+        quick = sorted(t for _, _, t in res)[:int(got["overflow"])]
+        assert max(quick) < 1.0, quick   # the overflow answers did not wait for a worker
+    finally:
+        rc, err = n.close()
+    assert rc == 0, err[-3000:]
+
+
 @pytest.mark.parametrize("flag,value,want", [("-prestart_budget", "0", "prestart_budget must be in (0, 30)"),
                                              ("-prestart_budget", "30", "prestart_budget must be in (0, 30)"),
                                              ("-liveness_busy_deadline", "0", "liveness_busy_deadline must be > 0")])
