@@ -7,9 +7,11 @@ per ROCr ordinal comes from the JSON file named by $MI355X_STUB_PROBE_CONTROL
 ``{"0": "ok", "3": "fail", "5": "hang", "6": "stale", "7": "garbage"}``
 (missing ordinals are "ok"; "serve": "broken" makes --serve fail to start,
 "serve": "slow_start" delays its hello by "serve_start_s" seconds;
-"server_fail" fails only inside --serve: a stale server runtime; "slow" answers ok
-after "slow_s" seconds, in --serve; "pending" keeps the dispatch queued and, like
-the real server, answers only when the device's deadline has passed).
+"server_fail" fails only inside --serve: a stale server runtime; "slow" is a
+dispatch that completes "slow_s" seconds after it was submitted: in --serve a
+request whose deadline comes first is answered pending and a later one collects
+the late verdict; "pending" keeps the dispatch queued and, like the real server,
+answers only when the device's deadline has passed).
 --serve speaks the real server's protocol: "@<id>"-tagged requests answered
 concurrently with their id, per-device deadlines ("<ordinal>:<nonce>:<s>"),
 requests on one device serialised on its slot.
@@ -125,6 +127,7 @@ def serve():
     print(json.dumps({"serve": True, "ok": True, "hip_device_count": 8, "concurrent": True, "deadlines": True,
                       "t_start_ns": t, "t_runtime_ns": t}), flush=True)
     slots = {}   # ordinal -> nonce of the kept slot's outstanding dispatch (like --keep)
+    slow = {}    # ordinal -> (submitted at, nonce) of a "slow" device's outstanding dispatch
     locks = {}   # ordinal -> its kept slot's lock (requests on one device serialise, as on the real server)
     out_mu, state_mu = threading.Lock(), threading.Lock()
     # like ROCr: with ROCR_VISIBLE_DEVICES the server numbers only those GPUs
@@ -146,9 +149,26 @@ def serve():
             mode = "fail"
         if mode == "hang":
             time.sleep(3600)
-        if mode == "slow":   # a verdict that takes "slow_s" seconds, then ok
-            time.sleep(float(ctl.get("slow_s", 1.0)))
-            mode = "ok"
+        if mode == "slow":
+            # a dispatch that completes "slow_s" seconds after it was submitted:
+            # a request whose deadline comes first is answered pending (the
+            # dispatch stays queued), and a later one collects its late verdict
+            with state_mu:
+                since, first = slow.setdefault(o, (time.monotonic(), n))
+            left = since + float(ctl.get("slow_s", 1.0)) - time.monotonic()
+            if left > deadline:
+                time.sleep(deadline)
+                d = _device(int(o), "fail", n, host_ordinal=int(hosto))
+                d.update(hip_error=-1, mismatches=0, pending_s=max(time.monotonic() - since, 1e-3),
+                         error=f"dispatch pending for {time.monotonic() - since:.1f}s (not completed)")
+                return d
+            time.sleep(max(0.0, left))
+            with state_mu:
+                slow.pop(o, None)
+            d = _device(int(o), "ok", first, host_ordinal=int(hosto))
+            if first != n:
+                d["late"] = 1
+            return d
         if mode == "garbage":
             print("segfault-ish noise", flush=True)
             os._exit(139)
