@@ -519,6 +519,41 @@ void answer(const ServeRequest& r, int n) {
   teardown();  // queues/executables go, the runtime (and the kfd process) stays
 }
 
+// Tagged requests go to a pool of worker threads that stay for the server's
+// life (a thread per request cost its creation on every probe); the pool
+// grows while every worker is busy -- a request stuck on a wedged device
+// holds its worker, not the others -- up to kMaxServeWorkers, beyond which
+// a request is answered inline.
+struct ServePool {
+  std::mutex mu;
+  std::condition_variable cv, done;
+  std::deque<ServeRequest> q;
+  int workers = 0, idle = 0, busy = 0;
+  bool stop = false;
+};
+
+void serve_worker(ServePool* pool, int n) {
+  while (true) {
+    ServeRequest r;
+    {
+      std::unique_lock<std::mutex> lk(pool->mu);
+      pool->idle++;
+      pool->cv.wait(lk, [pool] { return pool->stop || !pool->q.empty(); });
+      pool->idle--;
+      if (pool->q.empty()) return;  // stopping
+      r = std::move(pool->q.front());
+      pool->q.pop_front();
+      pool->busy++;
+    }
+    answer(r, n);  // no lock held: a request may take its whole deadline
+    {
+      std::lock_guard<std::mutex> lk(pool->mu);
+      pool->busy--;
+    }
+    pool->done.notify_all();
+  }
+}
+
 int serve(int n, uint64_t t_start, uint64_t t_runtime) {
   prctl(PR_SET_PDEATHSIG, SIGKILL);
   if (getppid() == 1) return 0;  // parent already gone
@@ -530,36 +565,8 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
                 static_cast<unsigned long long>(t_start), static_cast<unsigned long long>(t_runtime));
   emit_line(hello);
   if (n < 0) return 2;
-  // Tagged requests go to a pool of worker threads that stay for the server's
-  // life (a thread per request cost its creation on every probe); the pool
-  // grows while every worker is busy -- a request stuck on a wedged device
-  // holds its worker, not the others -- up to kMaxServeWorkers, beyond which
-  // a request is answered inline.
-  struct Pool {
-    std::mutex mu;
-    std::condition_variable cv, done;
-    std::deque<ServeRequest> q;
-    int workers = 0, idle = 0, busy = 0;
-    bool stop = false;
-  } pool;
+  ServePool pool;
   std::vector<std::thread> threads;
-  auto worker = [&pool, n] {
-    std::unique_lock<std::mutex> lk(pool.mu);
-    while (true) {
-      pool.idle++;
-      pool.cv.wait(lk, [&] { return pool.stop || !pool.q.empty(); });
-      pool.idle--;
-      if (pool.q.empty()) return;  // stopping
-      ServeRequest r = std::move(pool.q.front());
-      pool.q.pop_front();
-      pool.busy++;
-      lk.unlock();
-      answer(r, n);
-      lk.lock();
-      pool.busy--;
-      pool.done.notify_all();
-    }
-  };
   std::string line;
   char buf[8192];
   while (std::fgets(buf, sizeof(buf), stdin)) {
@@ -578,7 +585,7 @@ int serve(int n, uint64_t t_start, uint64_t t_runtime) {
       if (pool.idle > static_cast<int>(pool.q.size()) || pool.workers < kMaxServeWorkers) {
         if (pool.idle <= static_cast<int>(pool.q.size())) {
           pool.workers++;
-          threads.emplace_back(worker);
+          threads.emplace_back(serve_worker, &pool, n);
         }
         pool.q.push_back(std::move(r));
         pool.cv.notify_one();
