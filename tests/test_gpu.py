@@ -1125,6 +1125,67 @@ def test_rocprof_kept_queue_server_one_dispatch_per_sweep(tmp_path):
     shutil.copy(traces[0], "gpurun_out/rocprof_kept_server_kernel_trace.csv")
 
 
+def test_probe_server_answers_a_burst_of_tagged_requests():
+    """The kept-queue server's worker pool (probe_main.cpp serve_worker): 48 tagged probes written at once, with an
+    untagged chip sweep among them, each answered once with its own id and nonce; the pool stays bounded; `quit`
+    drains it and the server exits 0."""
+    import select
+    import time
+    from rocm_k8s_device_plugin_amd.ops.native import probe_executable
+    p = subprocess.Popen([str(probe_executable("hsa")), "--serve", "--keep"], stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, cwd="/tmp")
+    buf = b""
+
+    def lines_until(pred, timeout):
+        nonlocal buf
+        got, end = [], time.monotonic() + timeout
+        while not pred(got):
+            left = end - time.monotonic()
+            assert left > 0, f"timed out with {len(got)} replies"
+            if "\n" not in buf.decode(errors="replace"):
+                r, _, _ = select.select([p.stdout], [], [], left)
+                if not r:
+                    continue
+                chunk = os.read(p.stdout.fileno(), 1 << 16)
+                assert chunk, "probe server closed its stdout"
+                buf += chunk
+                continue
+            line, buf = buf.split(b"\n", 1)
+            if line.startswith(b"{"):
+                got.append(json.loads(line))
+        return got
+
+    try:
+        hello = lines_until(lambda g: len(g) >= 1, 120)[0]
+        assert hello["serve"] and hello["ok"] and hello["concurrent"], hello
+        p.stdin.write(b"probe 4 5.0 0:1\n")  # sets the kept queue up
+        p.stdin.flush()
+        first = lines_until(lambda g: len(g) >= 1, 60)[0]
+        assert first["ok"], first
+        n = 48
+        reqs = [f"@{i} probe 4 5.0 0:{2000 + i}:5.0\n" for i in range(1, n + 1)]
+        reqs.insert(n // 2, "sweep 4 5.0 0:77\n")
+        p.stdin.write("".join(reqs).encode())
+        p.stdin.flush()
+        got = lines_until(lambda g: len(g) >= n + 1, 120)
+        with open(f"/proc/{p.pid}/status") as f:
+            threads = int(next(l for l in f if l.startswith("Threads:")).split()[1])
+        tagged = {d["id"]: d for d in got if "id" in d}
+        assert sorted(tagged) == list(range(1, n + 1)), sorted(tagged)
+        for i, d in tagged.items():
+            assert d["ok"] and d["devices"][0]["nonce"] == 2000 + i, d
+        sweep = [d for d in got if "id" not in d]
+        assert len(sweep) == 1 and sweep[0]["sweep"] and sweep[0]["ok"], sweep
+        assert threads <= 64 + 16, threads  # kMaxServeWorkers plus the runtime's own threads
+        p.stdin.write(b"quit\n")
+        p.stdin.flush()
+        assert p.wait(timeout=60) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait(timeout=30)
+
+
 def test_real_box_matches_mi355x_model(inv):
     """The registry's MI355X numbers against the real part; consistent partitions."""
     from rocm_k8s_device_plugin_amd.models import MI355X, check_inventory, model_for
