@@ -1,6 +1,6 @@
 // Prometheus metrics for the native daemon: counters, gauges and latency
 // histograms with labels, rendered in the text exposition format (0.0.4), and a
-// small HTTP/1.0 endpoint for GET /metrics and /healthz.
+// small HTTP/1.0 endpoint for GET /metrics, /healthz and /readyz.
 //
 // Same names, labels, buckets and text layout as the Python registry
 // (rocm_k8s_device_plugin_amd/utils/metrics.py), so dashboards and the alert
@@ -11,6 +11,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -52,14 +53,23 @@ class Registry {
 
 Registry& global();
 
-// GET /metrics (render), /healthz ("ok"), anything else 404; one thread,
-// connections answered one at a time with a 5 s read deadline.
+// GET /metrics (render), /healthz and /readyz ("ok", or 503 with the reason
+// a check gives), anything else 404; one thread, connections answered one at a
+// time with a 5 s read deadline.
 class HttpEndpoint {
  public:
+  // "" = healthy / ready; anything else is the 503 body. Called on the
+  // endpoint's thread, so a check reads only atomics. Unset: always "ok".
+  using Check = std::function<std::string()>;
   explicit HttpEndpoint(Registry& reg = global()) : reg_(reg) {}
   ~HttpEndpoint() { stop(); }
   HttpEndpoint(const HttpEndpoint&) = delete;
   HttpEndpoint& operator=(const HttpEndpoint&) = delete;
+  // set before start()
+  void set_checks(Check healthz, Check readyz) {
+    healthz_ = std::move(healthz);
+    readyz_ = std::move(readyz);
+  }
   // "" on success; port 0 picks a free port (see port())
   std::string start(const std::string& host, int port);
   void stop();
@@ -73,6 +83,7 @@ class HttpEndpoint {
   int stop_[2] = {-1, -1};
   std::thread thread_;
   std::atomic<uint64_t> requests_{0};
+  Check healthz_, readyz_;
 };
 
 }  // namespace mi355x::metrics

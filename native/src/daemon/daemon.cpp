@@ -546,8 +546,38 @@ int Daemon::poll_timeout_ms(Clock::time_point now) const {
   return static_cast<int>(std::max(0LL, wait_ms));
 }
 
+void Daemon::note_tick() {
+  int n = 0, registered = 0;
+  for (const auto& r : reg_.all()) {
+    n++;
+    registered += r.server && r.reg.registered();
+  }
+  resources_n_.store(n);
+  registered_n_.store(registered);
+  loop_tick_ns_.store(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count());
+}
+
+std::string Daemon::healthz() const {
+  const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+  const double age = (now - loop_tick_ns_.load()) * 1e-9;
+  if (age <= kLoopStallS) return "";
+  char b[128];
+  std::snprintf(b, sizeof(b), "control loop stalled: last ran %.0f s ago", age);
+  return b;
+}
+
+std::string Daemon::readyz() const {
+  const int n = resources_n_.load(), registered = registered_n_.load();
+  if (n == 0) return "no GPU resources to advertise";
+  if (registered < n)
+    return "registered with kubelet: " + std::to_string(registered) + " of " + std::to_string(n) + " resources";
+  return "";
+}
+
 int Daemon::run(int sig_fd, const volatile sig_atomic_t* stop) {
   metrics::HttpEndpoint metrics_http;
+  note_tick();
+  metrics_http.set_checks([this] { return healthz(); }, [this] { return readyz(); });
   if (f_.metrics_port > 0) {
     const std::string merr = metrics_http.start("0.0.0.0", f_.metrics_port);
     if (!merr.empty()) {
@@ -590,6 +620,7 @@ int Daemon::run(int sig_fd, const volatile sig_atomic_t* stop) {
     }
     topology_tick();
     pulse_tick();
+    note_tick();
   }
   if (*stop) MI_LOG(kInfo, "Received signal, shutting down.");
   shutdown();

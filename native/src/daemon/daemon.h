@@ -128,6 +128,12 @@ class Daemon {
   void pulse_tick();
   int poll_timeout_ms(Clock::time_point now) const;
   void shutdown();
+  // /healthz: the control loop ran within kLoopStallS; /readyz: every resource
+  // is registered with kubelet. Both read only the atomics note_tick() sets, on
+  // the metrics endpoint's thread.
+  void note_tick();
+  std::string healthz() const;
+  std::string readyz() const;
 
   Flags f_;
   int dev_limit_ = -1;
@@ -167,6 +173,10 @@ class Daemon {
   std::chrono::milliseconds topo_period_{0};
   TopologyWatch topo_state_;
   Clock::time_point next_topo_{};
+  // probe endpoints
+  static constexpr double kLoopStallS = 60;  // the loop wakes at least every 5 s (kubelet.sock stat)
+  std::atomic<int64_t> loop_tick_ns_{0};
+  std::atomic<int> resources_n_{0}, registered_n_{0};
 };
 
 }  // namespace mi355x::daemon

@@ -264,8 +264,14 @@ void HttpEndpoint::loop() {
       path = req.substr(sp + 1, e == std::string::npos ? std::string::npos : e - sp - 1);
     }
     std::string body, status;
+    auto probe = [&](const Check& check) {
+      const std::string why = check ? check() : std::string();
+      if (why.empty()) body = "ok\n", status = "200 OK";
+      else body = why + "\n", status = "503 Service Unavailable";
+    };
     if (path.rfind("/metrics", 0) == 0) body = reg_.render(), status = "200 OK";
-    else if (path.rfind("/healthz", 0) == 0) body = "ok\n", status = "200 OK";
+    else if (path.rfind("/healthz", 0) == 0) probe(healthz_);
+    else if (path.rfind("/readyz", 0) == 0) probe(readyz_);
     else body = "not found\n", status = "404 Not Found";
     requests_++;
     std::string resp = "HTTP/1.0 " + status + "\r\nContent-Type: text/plain; version=0.0.4\r\nContent-Length: " +

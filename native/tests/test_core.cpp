@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include <netinet/in.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -991,6 +992,54 @@ static void test_metrics_registry() {
   CHECK(r.render().empty() && r.value("mi355x_g") == 0.0 && r.count("mi355x_h_seconds", {{"rpc", "Allocate"}}) == 0);
 }
 
+// one GET over loopback: the status line
+static std::string http_status(int port, const char* path) {
+  const int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return "";
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  std::string got;
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0) {
+    const std::string req = std::string("GET ") + path + " HTTP/1.0\r\n\r\n";
+    if (::write(fd, req.data(), req.size()) == static_cast<ssize_t>(req.size())) {
+      char b[512];
+      ssize_t n;
+      while ((n = ::read(fd, b, sizeof(b))) > 0) got.append(b, static_cast<size_t>(n));
+    }
+  }
+  ::close(fd);
+  return got;
+}
+
+static void test_http_endpoint_checks() {
+  // /healthz and /readyz answer 200 "ok" or 503 with the check's reason; the
+  // checks run on the endpoint's thread at every request
+  metrics::Registry reg;
+  metrics::HttpEndpoint ep(reg);
+  std::atomic<bool> live{true}, ready{false};
+  ep.set_checks([&] { return live ? std::string() : std::string("control loop stalled"); },
+                [&] { return ready ? std::string() : std::string("registered with kubelet: 0 of 1 resources"); });
+  CHECK(ep.start("127.0.0.1", 0).empty());
+  const int port = ep.port();
+  CHECK(http_status(port, "/healthz").rfind("HTTP/1.0 200 OK\r\n", 0) == 0);
+  std::string r = http_status(port, "/readyz");
+  CHECK(r.rfind("HTTP/1.0 503 Service Unavailable\r\n", 0) == 0);
+  CHECK(r.find("\r\n\r\nregistered with kubelet: 0 of 1 resources\n") != std::string::npos);
+  ready = true;
+  live = false;
+  CHECK(http_status(port, "/readyz").find("\r\n\r\nok\n") != std::string::npos);
+  CHECK(http_status(port, "/healthz").rfind("HTTP/1.0 503 ", 0) == 0);
+  CHECK(http_status(port, "/other").rfind("HTTP/1.0 404 ", 0) == 0);
+  ep.stop();
+  // no checks set: both always ok
+  metrics::HttpEndpoint plain(reg);
+  CHECK(plain.start("127.0.0.1", 0).empty());
+  CHECK(http_status(plain.port(), "/readyz").find("\r\n\r\nok\n") != std::string::npos);
+  plain.stop();
+}
+
 static void test_health_controller_generations(const std::string& tmp) {
   // passthrough sweeps on worker threads against a reload on the control thread
   // (run under TSan in CI: the job shares nothing with the controller)
@@ -1048,6 +1097,7 @@ int main(int argc, char** argv) {
   test_topology_watch();
   test_flags_go_semantics();
   test_metrics_registry();
+  test_http_endpoint_checks();
   test_driver_version_value();
   test_cdi_json_strings();
 #ifdef MI355X_TEST_HTTP

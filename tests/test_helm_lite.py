@@ -136,3 +136,30 @@ def test_chart_device_count_and_config_file(tmp_path):
         assert p.returncode == 0, p.stderr[-500:]
         import json
         assert len(json.loads(p.stdout)["resources"]["amd.com/gpu"]["devices"]) == want
+
+
+def test_chart_metrics_port_adds_probes():
+    """dp.metricsPort: the daemon serves /metrics, /healthz and /readyz on it, and the DaemonSet's container gets a
+    named port with a liveness probe on /healthz and a readiness probe on /readyz; without a port there are none
+    (as upstream, which has no probes)."""
+    import os
+
+    from rocm_k8s_device_plugin_amd.testing.helm_lite import rendered_objects
+    chart = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "helm", "amd-gpu")
+
+    def dp(values):
+        ds = [o for o in rendered_objects(chart, values)
+              if o.get("kind") == "DaemonSet" and "labeller" not in o["metadata"]["name"]]
+        return ds[0]["spec"]["template"]["spec"]["containers"][0]
+
+    c = dp({"dp": {"metricsPort": 9400}})
+    assert "-metrics_port=9400" in c["args"]
+    assert c["ports"] == [{"name": "metrics", "containerPort": 9400}]
+    assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": "metrics"}
+    assert c["readinessProbe"]["httpGet"] == {"path": "/readyz", "port": "metrics"}
+    # kubelet restarts the daemon after failureThreshold x periodSeconds of failed checks: well past the
+    # daemon's own 60 s stall limit
+    lp = c["livenessProbe"]
+    assert lp["failureThreshold"] * lp["periodSeconds"] >= 60
+    plain = dp({})
+    assert not {"ports", "livenessProbe", "readinessProbe"} & set(plain)

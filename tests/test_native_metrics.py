@@ -232,3 +232,47 @@ def test_metrics_endpoint_survives_awkward_clients(tmp_path):
     finally:
         rc, err = _stop(p)
     assert rc == 0, err[-3000:]
+
+
+def test_daemon_readyz_follows_kubelet_registration(tmp_path):
+    """/readyz is 503 (with the count) until every resource is registered with kubelet, then 200; /healthz is 200
+    while the control loop runs (it turns 503 only when the loop has not run for 60 s: unit-tested in
+    native/tests/test_core.cpp test_http_endpoint_checks). The chart points its probes at them."""
+    import time
+    fi = make_mi355x_node(tmp_path / "n")
+    kdir = tmp_path / "dp"
+    kdir.mkdir()
+    port = _free_port()
+    p = _daemon(str(kdir), fi, "-exporter_socket", "", "-metrics_port", str(port))
+
+    def until(path, want, timeout=20):
+        deadline, got = time.monotonic() + timeout, None
+        while time.monotonic() < deadline:
+            try:
+                got = _get(port, path)
+                if got[0] == want:
+                    return got
+            except OSError:
+                pass
+            time.sleep(0.05)
+        raise AssertionError(f"{path}: {got}")
+
+    async def go():
+        k = FakeKubelet(str(kdir))
+        try:
+            assert await asyncio.to_thread(until, "/healthz", 200) == (200, "ok\n")
+            before = await asyncio.to_thread(until, "/readyz", 503)
+            await k.start()
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=20)
+            after = await asyncio.to_thread(until, "/readyz", 200)
+            return before, after
+        finally:
+            await k.stop()
+
+    try:
+        before, after = asyncio.run(asyncio.wait_for(go(), 60))
+    finally:
+        rc, err = _stop(p)
+    assert before == (503, "registered with kubelet: 0 of 1 resources\n"), before
+    assert after == (200, "ok\n")
+    assert rc == 0, err[-3000:]
