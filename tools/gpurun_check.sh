@@ -107,7 +107,7 @@ for s in "$@"; do
     soakpre)
       # the same soak with -prestart_liveness: every admission's PreStartContainer probes its GPU
       step soakpre
-      timeout -k 10 420 python3 tools/soak_native.py --seconds 240 --report 30 --container-interval 1 \
+      timeout -k 10 420 python3 tools/soak_native.py --seconds 240 --report 30 --container-interval 1 --metrics-port 9437 \
         --extra "-liveness -prestart_liveness -liveness_chip_sweep_every 10 -perf_check_every 60 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_prestart.json > gpurun_out/soak_prestart.log 2>&1 \
         || { tail -20 gpurun_out/soak_prestart.log; exit 1; }

@@ -106,6 +106,25 @@ async def run_container(adm, minor_to_ord: dict, cont: dict) -> None:
     await asyncio.to_thread(wait_kfd_released, res.kfd_lingering, 1.0)
 
 
+def probe_endpoints(port: int) -> dict:
+    """/healthz and /readyz as kubelet's probes read them: status code and time to the answer."""
+    import urllib.error
+    import urllib.request
+    out = {}
+    for path in ("/healthz", "/readyz"):
+        t0 = time.monotonic()
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=10) as r:
+                code = r.status
+        except urllib.error.HTTPError as e:
+            code = e.code
+        except OSError:
+            code = 0
+        out[path.strip("/")] = code
+        out[path.strip("/") + "_ms"] = round((time.monotonic() - t0) * 1e3, 2)
+    return out
+
+
 async def main(a) -> int:
     global CONTAINER_RUNTIME
     CONTAINER_RUNTIME = a.container_runtime
@@ -166,6 +185,8 @@ async def main(a) -> int:
                                          "ready_ms_p50": pct(cont["ready_ms"], 0.5),
                                          "ready_ms_p99": pct(cont["ready_ms"], 0.99),
                                          "device_unhealthy_after": cont["unhealthy_seen"]}
+                if a.metrics_port:
+                    row["probes"] = await asyncio.to_thread(probe_endpoints, a.metrics_port)
                 rows.append(row)
                 print(json.dumps(row), flush=True)
                 lat = []
@@ -195,6 +216,9 @@ async def main(a) -> int:
         reports, first_report = sanitizer_reports(errf)
         errf.close()
     doc["exit_code"] = proc.returncode
+    # kubelet's liveness / readiness probes (the chart's, with a metrics port) at every report
+    doc["probe_failures"] = sum(1 for r in doc["reports"] if "probes" in r
+                                and (r["probes"]["healthz"] != 200 or r["probes"]["readyz"] != 200))
     doc["sanitizer_reports"] = reports
     # stopping the daemon must not flip a device (a check cut short by the shutdown is no verdict)
     tail_text = err.decode(errors="replace")
@@ -208,7 +232,7 @@ async def main(a) -> int:
             json.dump(doc, f, indent=1)
     print(json.dumps({k_: doc[k_] for k_ in ("admissions", "errors", "exit_code")}))
     bad_containers = doc["containers"] and (doc["containers"]["failed"] or doc["containers"]["device_unhealthy_after"])
-    ok = doc["errors"] == 0 and doc["exit_code"] == 0 and not bad_containers and not reports
+    ok = doc["errors"] == 0 and doc["exit_code"] == 0 and not bad_containers and not reports and not doc["probe_failures"]
     return 0 if ok and not doc["transitions_after_shutdown"] else 1
 
 
