@@ -568,7 +568,8 @@ std::string Daemon::healthz() const {
 
 std::string Daemon::readyz() const {
   const int n = resources_n_.load(), registered = registered_n_.load();
-  if (n == 0) return "no GPU resources to advertise";
+  // a node without GPUs idles as the reference's manager does; it is ready, so a
+  // DaemonSet rolling update (maxUnavailable) is not held up by CPU-only nodes
   if (registered < n)
     return "registered with kubelet: " + std::to_string(registered) + " of " + std::to_string(n) + " resources";
   return "";

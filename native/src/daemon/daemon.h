@@ -129,7 +129,7 @@ class Daemon {
   int poll_timeout_ms(Clock::time_point now) const;
   void shutdown();
   // /healthz: the control loop ran within kLoopStallS; /readyz: every resource
-  // is registered with kubelet. Both read only the atomics note_tick() sets, on
+  // is registered with kubelet (a node without GPUs has none and is ready). Both read only the atomics note_tick() sets, on
   // the metrics endpoint's thread.
   void note_tick();
   std::string healthz() const;

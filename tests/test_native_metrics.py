@@ -276,3 +276,32 @@ def test_daemon_readyz_follows_kubelet_registration(tmp_path):
     assert before == (503, "registered with kubelet: 0 of 1 resources\n"), before
     assert after == (200, "ok\n")
     assert rc == 0, err[-3000:]
+
+
+def test_daemon_without_gpus_is_ready(tmp_path):
+    """A node without GPUs: the daemon idles (as the reference's manager does) and /readyz is 200, so a DaemonSet
+    rolling update is not held up by CPU-only nodes (maxUnavailable counts not-ready pods)."""
+    import time
+    (tmp_path / "sys").mkdir()
+    (tmp_path / "dev").mkdir()
+    kdir = tmp_path / "dp"
+    kdir.mkdir()
+    port = _free_port()
+    from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
+    import subprocess
+    exe = os.path.join(str(PKG_DIR), "bin", "mi355x-device-plugin")
+    p = subprocess.Popen([exe, "-kubelet_dir", str(kdir), "-sysfs_root", str(tmp_path / "sys"), "-dev_root",
+                          str(tmp_path / "dev"), "-exporter_socket", "", "-metrics_port", str(port)],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        got, deadline = None, time.monotonic() + 20
+        while time.monotonic() < deadline:
+            try:
+                got = (_get(port, "/healthz"), _get(port, "/readyz"))
+                break
+            except OSError:
+                time.sleep(0.05)
+    finally:
+        rc, err = _stop(p)
+    assert got == ((200, "ok\n"), (200, "ok\n")), got
+    assert rc == 0, err[-3000:]
