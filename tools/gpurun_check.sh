@@ -141,7 +141,7 @@ for s in "$@"; do
       step tsansoak
       w=$(tsan_launchers)
       TSAN_OPTIONS="$TSAN_ENV" timeout -k 10 $(( ${SOAK_SECONDS:-120} + 180 )) python3 tools/soak_native.py --seconds "${SOAK_SECONDS:-120}" \
-        --report 20 --container-interval 2 --exe "$w/mi355x-device-plugin" \
+        --report 20 --container-interval 2 --metrics-port 9438 --exe "$w/mi355x-device-plugin" \
         --extra "-liveness -prestart_liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_tsan.json > gpurun_out/soak_tsan.log 2>&1 || { tail -c 3000 gpurun_out/soak_tsan.json; exit 1; }
       tail -c 800 gpurun_out/soak_tsan.json ;;
@@ -149,7 +149,7 @@ for s in "$@"; do
       # the same 2-minute soak against the ASan/UBSan daemon (asan_bin/)
       step asansoak
       UBSAN_OPTIONS="print_stacktrace=1" timeout -k 10 $(( ${SOAK_SECONDS:-120} + 180 )) python3 tools/soak_native.py --seconds "${SOAK_SECONDS:-120}" \
-        --report 20 --container-interval 2 --exe "$PWD/asan_bin/mi355x-device-plugin" \
+        --report 20 --container-interval 2 --metrics-port 9439 --exe "$PWD/asan_bin/mi355x-device-plugin" \
         --extra "-liveness -prestart_liveness -liveness_probe $PWD/rocm_k8s_device_plugin_amd/bin/mi355x-liveness-probe -liveness_chip_sweep_every 5 -perf_check_every 20 -smi_ecc -smi_events -smi_xgmi" \
         --out gpurun_out/soak_asan.json > gpurun_out/soak_asan.log 2>&1 || { tail -c 3000 gpurun_out/soak_asan.json; exit 1; }
       tail -c 800 gpurun_out/soak_asan.json ;;
