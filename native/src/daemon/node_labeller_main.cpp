@@ -38,6 +38,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <chrono>
 #include <cmath>
@@ -62,6 +63,7 @@
 #include "mi355x/drm_query.h"
 #include "mi355x/gpu_discovery.h"
 #include "mi355x/kfd_topology.h"
+#include "mi355x/metrics.h"
 #include "mi355x/pci_scan.h"
 #include "mi355x/smi_query.h"
 #include "mi355x/sysfs.h"
@@ -92,6 +94,7 @@ struct Flags {
   std::string ca_file;
   double watch_backoff_max_s = 30.0;
   int watch_timeout_s = 300;
+  int metrics_port = 0;  // /metrics, /healthz, /readyz (0 = off; the reference serves none)
   glog::Options log;
 };
 
@@ -103,7 +106,7 @@ void print_usage(FILE* out, const char* argv0, const std::string& sysfs_root) {
   for (const auto& line : versions::banner(kTitle, argv0, sysfs_root)) std::fprintf(out, "%s\n", line.c_str());
   std::fprintf(out, "usage: %s [-<label kind> ...] [-driver_type container|vf-passthrough|pf-passthrough] "
                "[-node_name NAME] [-kubeconfig PATH] [-resync S] [-once] [-watch=false] [-topology_watch S] "
-               "[-dry_run] [-sysfs_root DIR] [-dev_root DIR] [-v N] [-logtostderr] [-alsologtostderr] "
+               "[-dry_run] [-metrics_port N] [-sysfs_root DIR] [-dev_root DIR] [-v N] [-logtostderr] [-alsologtostderr] "
                "[-stderrthreshold SEV] [-log_dir DIR] [-vmodule P=N] [-log_backtrace_at FILE:N]\nlabel kinds:",
                argv0);
   for (const auto& k : kKinds) std::fprintf(out, " -%s", k.c_str());
@@ -120,7 +123,7 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* syntax
   static const std::set<std::string> kBool = {"watch", "dry_run", "once"};
   static const std::set<std::string> kValued = {"driver_type", "node_name", "kubeconfig", "resync", "topology_watch",
                                                 "watch_backoff_max", "watch_timeout", "sysfs_root", "dev_root",
-                                                "sa_dir", "apiserver", "token_file", "ca_file"};
+                                                "sa_dir", "apiserver", "token_file", "ca_file", "metrics_port"};
   *syntax = false;
   auto bad = [&](std::string msg) {
     *err = std::move(msg);
@@ -186,6 +189,11 @@ bool parse_flags(int argc, char** argv, Flags* f, std::string* err, bool* syntax
       int v = 0;
       if (!goflag::parse_int_flag(value, &v)) return bad("invalid value \"" + value + "\" for flag -watch_timeout");
       f->watch_timeout_s = std::max(1, v);
+    } else if (name == "metrics_port") {
+      int v = 0;
+      if (!goflag::parse_int_flag(value, &v) || v < 0 || v > 65535)
+        return bad("invalid value \"" + value + "\" for flag -metrics_port");
+      f->metrics_port = v;
     } else if (name == "sysfs_root") {
       f->sysfs_root = value;
     } else if (name == "dev_root") {
@@ -612,6 +620,29 @@ class NodeWatch {
   std::string rv_;
 };
 
+// -metrics_port: /healthz is 200 while the controller loop runs (it wakes at
+// least every kLoopWakeS; one reconcile against a hung apiserver can take
+// ~180 s of 15 s call timeouts, so a loop that has not run for kLoopStallS is
+// stuck past every timeout) and /readyz while the last reconcile succeeded.
+// The checks run on the endpoint's thread and read only these atomics.
+constexpr double kLoopWakeS = 15, kLoopStallS = 300;
+std::atomic<int64_t> g_loop_tick_ns{0};
+std::atomic<bool> g_reconciled{false};
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now().time_since_epoch()).count();
+}
+
+std::string labeller_healthz() {
+  const double age = (now_ns() - g_loop_tick_ns.load()) * 1e-9;
+  if (age <= kLoopStallS) return "";
+  char b[128];
+  std::snprintf(b, sizeof(b), "controller loop stalled: last ran %.0f s ago", age);
+  return b;
+}
+
+std::string labeller_readyz() { return g_reconciled.load() ? "" : "node labels not reconciled yet (see the log)"; }
+
 // The controller loop: reconcile at start, every -resync s, on watch events
 // and on a partition switch (a kfd fingerprint that held one -topology_watch
 // interval: a switch passes through half states).
@@ -620,6 +651,17 @@ int run(const Flags& f, Labeller& lab, Kube& kube) {
   // then only when the Node object is (re-)created; no periodic re-assert
   const bool created_only = f.resync_s <= 0;
   const double resync_s = created_only ? 3600.0 * 24 * 365 : f.resync_s;
+  g_loop_tick_ns = now_ns();
+  metrics::HttpEndpoint endpoint;
+  if (f.metrics_port > 0) {
+    endpoint.set_checks(labeller_healthz, labeller_readyz);
+    if (const std::string e = endpoint.start("0.0.0.0", f.metrics_port); !e.empty()) {
+      MI_LOG(kError, "cannot serve /metrics: %s", e.c_str());
+      return 1;
+    }
+    MI_LOG(kInfo, "serving /metrics, /healthz, /readyz on :%d", endpoint.port());
+  }
+  auto& m = metrics::global();
   NodeWatch watch(f, &kube, &lab, created_only, g_sig_pipe[0]);
   bool kick = true;
   auto next_resync = clk::now();
@@ -629,22 +671,30 @@ int run(const Flags& f, Labeller& lab, Kube& kube) {
   while (!g_stop) {
     if (kick || clk::now() >= next_resync) {
       kick = false;
+      const int patches = lab.st.patches;
       const bool ok = lab.reconcile();
+      g_reconciled = ok;
+      m.inc("mi355x_labeller_reconciles_total", {{"result", ok ? "ok" : "error"}}, 1.0,
+            "node label reconciles: ok (labels match, or patched) or error");
+      if (lab.st.patches > patches)
+        m.inc("mi355x_labeller_patches_total", {}, 1.0, "node label patches (or GET + update) the apiserver accepted");
       next_resync = after_s(ok ? resync_s : 5.0);
     }
+    g_loop_tick_ns = now_ns();
     if (topo_watch && clk::now() >= next_topo) {
       next_topo = after_s(f.topology_watch_s);
       const std::string cur = topology_signature(f.sysfs_root);
       if (cur != topo_last && cur == topo_seen) {
         topo_last = cur;
         ++lab.st.topology_changes;
+        m.inc("mi355x_labeller_topology_changes_total", {}, 1.0, "GPU partition switches that triggered a relabel");
         MI_LOG(kInfo, "GPU topology changed (partition switch?): relabelling node %s", f.node_name.c_str());
         kick = true;
       }
       topo_seen = cur;
       if (kick) continue;
     }
-    int wait_ms = ms_until(next_resync);
+    int wait_ms = std::min(ms_until(next_resync), static_cast<int>(kLoopWakeS * 1000));
     if (topo_watch) wait_ms = std::min(wait_ms, ms_until(next_topo));
     const NodeWatch::Event ev = watch.wait(wait_ms);
     if (ev == NodeWatch::kStop) break;

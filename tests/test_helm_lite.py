@@ -163,3 +163,25 @@ def test_chart_metrics_port_adds_probes():
     assert lp["failureThreshold"] * lp["periodSeconds"] >= 60
     plain = dp({})
     assert not {"ports", "livenessProbe", "readinessProbe"} & set(plain)
+
+
+def test_chart_labeller_metrics_port_adds_probes():
+    """lbl.metricsPort: the labeller gets -metrics_port, a named port and probes on /healthz and /readyz."""
+    import os
+
+    from rocm_k8s_device_plugin_amd.testing.helm_lite import rendered_objects
+    chart = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "helm", "amd-gpu")
+
+    def lbl(values):
+        ds = [o for o in rendered_objects(chart, dict(values, labeller={"enabled": True}))
+              if o.get("kind") == "DaemonSet" and "labeller" in o["metadata"]["name"]]
+        return ds[0]["spec"]["template"]["spec"]["containers"][0]
+
+    c = lbl({"lbl": {"metricsPort": 9401}})
+    assert "-metrics_port=9401" in c["args"]
+    assert c["ports"] == [{"name": "metrics", "containerPort": 9401}]
+    assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": "metrics"}
+    assert c["readinessProbe"]["httpGet"] == {"path": "/readyz", "port": "metrics"}
+    plain = lbl({})
+    assert not {"ports", "livenessProbe", "readinessProbe"} & set(plain)
+    assert not any(a.startswith("-metrics_port") for a in plain["args"])

@@ -653,3 +653,56 @@ users:
         if p is not None and p.poll() is None:
             p.kill()
         srv.stop()
+
+
+def test_metrics_port_health_and_readiness(tmp_path):
+    """-metrics_port (an addition; the reference's labeller serves nothing): /readyz is 503 while the node cannot
+    be labelled (it does not exist yet) and 200 once a reconcile succeeded; /healthz is 200 while the controller
+    loop runs; /metrics counts the reconciles by result and the patches."""
+    import socket
+    import urllib.error
+    import urllib.request
+
+    def get(port, path):
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+                return r.status, r.read().decode()
+        except urllib.error.HTTPError as e:
+            return e.code, e.read().decode()
+        except OSError:
+            return 0, ""
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    p = None
+    try:
+        log = tmp_path / "labeller.log"
+        p, _ = _start(fi, srv, tmp_path, "-resync", "0.5", "-watch=false", "-topology_watch", "0",
+                      "-metrics_port", str(port), stderr=open(log, "w"))
+        assert _wait(lambda: get(port, "/healthz")[0] == 200)
+        assert _wait(lambda: len(srv.requests) >= 1)                 # a reconcile ran: 404, no node yet
+        assert get(port, "/readyz") == (503, "node labels not reconciled yet (see the log)\n")
+        srv.add_node("node-n")
+        assert _wait(lambda: get(port, "/readyz")[0] == 200)
+        assert srv.labels("node-n").get("amd.com/gpu.vram") == "288G"
+        status, text = get(port, "/metrics")
+        assert status == 200
+        series = {ln.rsplit(" ", 1)[0]: float(ln.rsplit(" ", 1)[1]) for ln in text.splitlines()
+                  if ln and not ln.startswith("#")}
+        assert series['mi355x_labeller_reconciles_total{result="error"}'] >= 1
+        assert series['mi355x_labeller_reconciles_total{result="ok"}'] >= 1
+        assert series["mi355x_labeller_patches_total"] == 1
+        rc, _ = _stop(p)
+        assert rc == 0, open(log).read()[-2000:]
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        srv.stop()
+
+
+def test_metrics_port_flag_syntax(tmp_path):
+    p = subprocess.run([EXE, "-metrics_port", "x"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 2 and 'invalid value "x" for flag -metrics_port' in p.stderr
