@@ -123,8 +123,9 @@ def containers(objs):
                 yield o["metadata"]["name"], c
 
 
-def run_container(c, tmp_path, fi):
-    """Run container spec `c` from its image's replayed root; (returncode, stdout, stderr, kind)."""
+def container_argv(c, tmp_path):
+    """Container spec `c` as it starts from its image's replayed root: (argv with the image's executable, cwd,
+    env, image kind)."""
     images = image_map()
     assert c["image"] in images, f"{c['image']} is not an image this build makes ({sorted(images)})"
     df = images[c["image"]]
@@ -139,15 +140,20 @@ def run_container(c, tmp_path, fi):
     if argv[0].startswith("/"):
         exe = root + argv[0]
     assert os.access(exe, os.X_OK), f"{df}: {argv[0]} does not exist in the image (from {cwd})"
-    labeller = "labeller" in df
-    extra = (["-dry_run", "-node_name", "node-0", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)]
-             if labeller else
-             ["-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-kubelet_dir", str(tmp_path / "dp"),
-              "-exporter_socket", "", "-cdi_spec_dir", str(tmp_path / "cdi"), "-liveness_timeout", "5"])
     env = {k: v for k, v in os.environ.items() if not k.startswith("MI355X_")}
     env.update({k: (root + v if v.startswith("/opt/mi355x") else v) for k, v in st["env"].items()})
-    p = subprocess.run([exe] + argv[1:] + extra, cwd=cwd, env=env, capture_output=True, text=True, timeout=120)
-    return p.returncode, p.stdout, p.stderr, "labeller" if labeller else "device-plugin"
+    return [exe] + argv[1:], cwd, env, "labeller" if "labeller" in df else "device-plugin"
+
+
+def run_container(c, tmp_path, fi):
+    """Run container spec `c` from its image's replayed root; (returncode, stdout, stderr, kind)."""
+    argv, cwd, env, kind = container_argv(c, tmp_path)
+    extra = (["-dry_run", "-node_name", "node-0", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev)]
+             if kind == "labeller" else
+             ["-dry_run", "-sysfs_root", str(fi.sysfs), "-dev_root", str(fi.dev), "-kubelet_dir", str(tmp_path / "dp"),
+              "-exporter_socket", "", "-cdi_spec_dir", str(tmp_path / "cdi"), "-liveness_timeout", "5"])
+    p = subprocess.run(argv + extra, cwd=cwd, env=env, capture_output=True, text=True, timeout=120)
+    return p.returncode, p.stdout, p.stderr, kind
 
 
 def check_ok(c, tmp_path, fi):
@@ -219,6 +225,90 @@ def test_chart_containers_run_from_their_image(name, tmp_path, node):
         if name == "cdi-metrics" and "resources" in doc:
             assert doc["device_list_strategy"] == ["device-specs", "cdi-cri"]
             assert (tmp_path / "cdi").is_dir() and os.listdir(tmp_path / "cdi")
+
+
+def test_chart_probes_reach_the_running_binaries(tmp_path, node):
+    """With dp.metricsPort / lbl.metricsPort, the rendered containers run from their images (not a dry run) and
+    the paths and ports of the rendered liveness and readiness probes answer 200 once the daemon is registered
+    with kubelet and the labeller has labelled its node: the probes point at what the binaries serve."""
+    import asyncio
+    import socket
+    import time
+    import urllib.error
+    import urllib.request
+
+    from rocm_k8s_device_plugin_amd.testing.fake_apiserver import FakeApiServer
+    from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
+
+    def free_port():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            return s.getsockname()[1]
+
+    def status(port, path):
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+                return r.status
+        except urllib.error.HTTPError as e:
+            return e.code
+        except OSError:
+            return 0
+
+    def probes_ok(c):
+        port = next(p["containerPort"] for p in c["ports"] if p["name"] == c["livenessProbe"]["httpGet"]["port"])
+        paths = [c[k]["httpGet"]["path"] for k in ("livenessProbe", "readinessProbe")]
+        deadline = time.monotonic() + 30
+        while time.monotonic() < deadline:
+            if all(status(port, path) == 200 for path in paths):
+                return True
+            time.sleep(0.1)
+        return {path: status(port, path) for path in paths}
+
+    cs = dict((kind, c) for kind, c in (
+        ("labeller" if "labeller" in o["metadata"]["name"] else "dp", o["spec"]["template"]["spec"]["containers"][0])
+        for o in rendered_objects(CHART, {"dp": {"metricsPort": free_port()}, "labeller": {"enabled": True},
+                                          "lbl": {"metricsPort": free_port()}})
+        if o.get("kind") == "DaemonSet"))
+    # the device plugin: a kubelet to register with
+    kdir = tmp_path / "dp"
+    kdir.mkdir()
+    argv, cwd, env, kind = container_argv(cs["dp"], tmp_path / "dp-image")
+    assert kind == "device-plugin"
+
+    async def dp():
+        k = FakeKubelet(str(kdir))
+        await k.start()
+        p = subprocess.Popen(argv + ["-sysfs_root", str(node.sysfs), "-dev_root", str(node.dev), "-kubelet_dir",
+                                     str(kdir), "-exporter_socket", ""], cwd=cwd, env=env,
+                             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        try:
+            await k.wait_for_resource("amd.com/gpu", 8, timeout=30)
+            return await asyncio.to_thread(probes_ok, cs["dp"])
+        finally:
+            p.terminate()
+            p.communicate(timeout=20)
+            await k.stop()
+
+    assert asyncio.run(asyncio.wait_for(dp(), 90)) is True
+    # the labeller: an apiserver with its node
+    srv = FakeApiServer(token="tok").start()
+    tok = tmp_path / "token"
+    tok.write_text("tok\n")
+    argv, cwd, env, kind = container_argv(cs["labeller"], tmp_path / "lbl-image")
+    assert kind == "labeller"
+    p = None
+    try:
+        srv.add_node("node-0")
+        p = subprocess.Popen(argv + ["-node_name", "node-0", "-apiserver", srv.url, "-token_file", str(tok),
+                                     "-sysfs_root", str(node.sysfs), "-dev_root", str(node.dev)],
+                             cwd=cwd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        assert probes_ok(cs["labeller"]) is True
+        assert srv.labels("node-0")
+    finally:
+        if p is not None:
+            p.terminate()
+            p.communicate(timeout=20)
+        srv.stop()
 
 
 def test_a_wrong_flag_or_command_fails(tmp_path, node):
