@@ -706,3 +706,23 @@ def test_metrics_port_health_and_readiness(tmp_path):
 def test_metrics_port_flag_syntax(tmp_path):
     p = subprocess.run([EXE, "-metrics_port", "x"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 2 and 'invalid value "x" for flag -metrics_port' in p.stderr
+
+
+def test_metrics_port_in_use_is_an_error(tmp_path):
+    """A -metrics_port that cannot be bound is a start-up error (exit 1), as in the device plugin."""
+    import socket
+    fi = make_mi355x_node(tmp_path / "n")
+    srv = FakeApiServer(token="tok").start()
+    try:
+        srv.add_node("node-n")
+        with socket.socket() as s:
+            s.bind(("0.0.0.0", 0))
+            s.listen(1)
+            p, _ = _start(fi, srv, tmp_path, "-metrics_port", str(s.getsockname()[1]))
+            rc = p.wait(30)
+            err = p.stderr.read()
+        assert rc == 1 and "cannot serve /metrics" in err, err[-2000:]
+    finally:
+        if p.poll() is None:
+            p.kill()
+        srv.stop()
