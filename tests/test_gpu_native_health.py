@@ -200,8 +200,9 @@ def test_native_xgmi_link_state(inv, ordinals):
 def test_native_daemon_admission_with_smi_sources(inv, ordinals, tmp_path):
     """The health DaemonSet's configuration through the daemon: -liveness with
     amd-smi ECC, events and xGMI link state. Every source reads ok each pulse
-    (/metrics), ListAndWatch shows the GPUs Healthy, and a container given the
-    allocated DeviceSpecs runs its MFMA probe on exactly that GPU."""
+    (/metrics), ListAndWatch shows the GPUs Healthy, a container given the
+    allocated DeviceSpecs runs its MFMA probe on exactly that GPU, and /healthz
+    and /readyz answer 200."""
     from rocm_k8s_device_plugin_amd.container_runtime import render_minors_from_specs, start_container
     from rocm_k8s_device_plugin_amd.ops.native import PKG_DIR
     from rocm_k8s_device_plugin_amd.testing.fake_kubelet import FakeKubelet
@@ -251,6 +252,10 @@ def test_native_daemon_admission_with_smi_sources(inv, ordinals, tmp_path):
             m = await asyncio.to_thread(metrics)
             assert m['mi355x_dp_prestart_checks_total{result="ok"}'] >= 1
             assert m.get("mi355x_dp_xgmi_links_down", 0.0) == 0.0
+            # what the chart's probes read (dp.metricsPort): the loop runs, the resource is registered
+            for path in ("/healthz", "/readyz"):
+                with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+                    assert (r.status, r.read()) == (200, b"ok\n"), path
         finally:
             if proc.returncode is None:
                 proc.send_signal(signal.SIGTERM)
