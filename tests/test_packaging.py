@@ -38,6 +38,12 @@ def test_device_plugin_manifests():
     assert "-pulse=2" in c["args"] and "-liveness=true" in c["args"] and "-smi_xgmi=true" in c["args"]
     assert c["resources"]["requests"]["memory"] == "3Gi"
     assert "/dev" in {m["mountPath"] for m in c["volumeMounts"]}
+    # the health DaemonSet restarts a wedged daemon and gates rollouts on registration
+    assert "-metrics_port=9400" in c["args"] and c["ports"] == [{"name": "metrics", "containerPort": 9400}]
+    assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": "metrics"}
+    assert c["readinessProbe"]["httpGet"] == {"path": "/readyz", "port": "metrics"}
+    plain = _ds(_docs("k8s-ds-amdgpu-dp.yaml")[0])["containers"][0]
+    assert "livenessProbe" not in plain                # the plain manifest stays as upstream
 
 
 def test_labeller_manifest():
