@@ -161,8 +161,11 @@ def test_chart_metrics_port_adds_probes():
     # daemon's own 60 s stall limit
     lp = c["livenessProbe"]
     assert lp["failureThreshold"] * lp["periodSeconds"] >= 60
+    # the endpoint is served once the daemon is in its loop (after the first sweep): start-up has its own probe
+    sp = c["startupProbe"]
+    assert sp["httpGet"] == lp["httpGet"] and sp["failureThreshold"] * sp["periodSeconds"] >= 300
     plain = dp({})
-    assert not {"ports", "livenessProbe", "readinessProbe"} & set(plain)
+    assert not {"ports", "startupProbe", "livenessProbe", "readinessProbe"} & set(plain)
 
 
 def test_chart_labeller_metrics_port_adds_probes():
@@ -183,5 +186,5 @@ def test_chart_labeller_metrics_port_adds_probes():
     assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": "metrics"}
     assert c["readinessProbe"]["httpGet"] == {"path": "/readyz", "port": "metrics"}
     plain = lbl({})
-    assert not {"ports", "livenessProbe", "readinessProbe"} & set(plain)
+    assert not {"ports", "startupProbe", "livenessProbe", "readinessProbe"} & set(plain)
     assert not any(a.startswith("-metrics_port") for a in plain["args"])

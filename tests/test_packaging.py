@@ -42,6 +42,7 @@ def test_device_plugin_manifests():
     assert "-metrics_port=9400" in c["args"] and c["ports"] == [{"name": "metrics", "containerPort": 9400}]
     assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": "metrics"}
     assert c["readinessProbe"]["httpGet"] == {"path": "/readyz", "port": "metrics"}
+    assert c["startupProbe"]["httpGet"] == c["livenessProbe"]["httpGet"]
     plain = _ds(_docs("k8s-ds-amdgpu-dp.yaml")[0])["containers"][0]
     assert "livenessProbe" not in plain                # the plain manifest stays as upstream
 
